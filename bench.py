@@ -1,0 +1,157 @@
+#!/usr/bin/env python
+"""Flagship benchmark: DeepFM training throughput (samples/s, whole node) + eval AUC.
+
+Config (BASELINE.json config #4, "Criteo-1TB-shape"): F = 39 fields (13 dense + 26
+categorical with the Criteo-Terabyte per-field cardinalities, V = 882.8M feature ids),
+embedding K = 8, deep layers 128,64,32 with keep-prob 0.5 dropout (the notebooks' model,
+NBPS:82), Adam lr 5e-4 x world size (HVD:149), l2 1e-4 on fm_w/fm_v, bf16 MLP operands with
+fp32 accumulation and fp32 tables / optimizer state.  The 882.8M-row table is replicated at
+N=1 and row-sharded across ranks (all-to-all) at N>1; updates are "lazy" (touched rows only,
+SURVEY Q8 — a TF1-dense sweep of 882.8M rows per step is what the reference would do).
+
+Data: synthetic Criteo-shaped batches (Zipf ids, teacher labels), generated on the GPU and
+kept HBM-resident (the reference's ``cache()`` analogue); random-init weights.  Weak scaling:
+the per-GPU batch is fixed as N grows.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--batch_size B] [--preset criteo_1tb]
+  python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+if REPO not in sys.path:
+    sys.path.insert(0, REPO)
+
+METRIC = ("samples/sec (whole node) + eval AUC, Criteo-1TB-shape DeepFM at 1/2/4/8 MI355X")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--batch_size", type=int, default=16384, help="per-GPU batch")
+    ap.add_argument("--preset", default="criteo_1tb")
+    ap.add_argument("--embedding_size", type=int, default=8)
+    ap.add_argument("--deep_layers", default="128,64,32")
+    ap.add_argument("--dropout", default="0.5,0.5,0.5")
+    ap.add_argument("--optimizer", default="Adam")
+    ap.add_argument("--sparse_update", default="lazy")
+    ap.add_argument("--embedding_mode", default="auto")
+    ap.add_argument("--pool", type=int, default=16, help="resident synthetic batches per rank")
+    ap.add_argument("--eval_batches", type=int, default=8)
+    ap.add_argument("--no_graph", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    import hipfm
+    from hipfm.data.synthetic import make_synth
+    from hipfm.models.deepfm import NativeDeepFM
+    from hipfm.ops import kernels as KN
+    from hipfm.ops.metrics import auc_from_hist
+    from hipfm.parallel.dist import Comm, init_distributed
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    comm = None
+    if world > 1:
+        init_distributed("nccl")
+        mode = "sharded" if args.embedding_mode == "auto" else args.embedding_mode
+        comm = Comm(sharded=(mode == "sharded"))
+
+    synth = make_synth(args.preset, seed=2024)
+    F = synth.F
+    B = args.batch_size
+    layers = [int(x) for x in args.deep_layers.split(",")]
+    keep = [float(x) for x in args.dropout.split(",")]
+    model = NativeDeepFM(synth.feature_size, F, args.embedding_size, layers, keep, l2_reg=1e-4,
+                         learning_rate=5e-4, optimizer=args.optimizer,
+                         sparse_update=args.sparse_update, seed=1234, batch_size=B, device=dev,
+                         comm=comm)
+    pool = [synth.batch(B, step=rank * 100000 + i, device=dev, id_dtype=torch.int32)
+            for i in range(args.pool)]
+    use_graph = not args.no_graph
+    torch.cuda.synchronize()
+
+    def run(nsteps, start):
+        for s in range(nsteps):
+            ids, vals, labels = pool[(start + s) % len(pool)]
+            model.train_step(ids, vals, labels, use_graph=use_graph)
+
+    run(args.warmup, 0)
+    torch.cuda.synchronize()
+    if comm is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run(args.steps, args.warmup)
+    torch.cuda.synchronize()
+    if comm is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    loss = model.loss_value(B)
+    ms = elapsed * 1000.0 / max(1, args.steps)
+    if comm is not None:
+        t = torch.tensor([ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        ms = float(t.item())
+
+    # eval AUC on held-out batches (distributed: every rank evaluates its shard, hist all-reduced)
+    hist = torch.zeros(2, 201, dtype=torch.int64, device=dev)
+    for i in range(args.eval_batches):
+        ids, vals, labels = synth.batch(B, step=10_000_000 + rank * 1000 + i, device=dev,
+                                        id_dtype=torch.int32)
+        model.eval_batch(ids, vals, labels, hist)
+    if comm is not None:
+        dist.all_reduce(hist)
+    auc = auc_from_hist(hist.cpu())
+
+    value = world * B / (ms / 1000.0)
+    if rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": round(value, 1),
+            "unit": "samples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic (Criteo-shaped Zipf ids + teacher labels, HBM-resident), random-init weights",
+            "config": {
+                "model": f"DeepFM Criteo-1TB-shape (F={F}, V={synth.feature_size}, K={args.embedding_size}, "
+                         f"deep {args.deep_layers}, keep {args.dropout})",
+                "global_batch": world * B,
+                "per_gpu_batch": B,
+                "seq_len": None,
+                "fields": F,
+                "parallelism": f"dp{world}" + ("" if world == 1 else
+                                                f"+{'row-sharded' if comm.sharded else 'replicated'}-embedding"),
+                "optimizer": f"{args.optimizer} ({args.sparse_update})",
+                "hip_graph": use_graph,
+            },
+            "eval_auc": round(auc, 5),
+            "train_loss": round(loss, 5),
+        }
+        print(json.dumps(out), flush=True)
+    if comm is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,80 @@
+// Shared definitions for the hipfm gfx950 (MI355X / CDNA4) kernels.
+//
+// Every kernel library entry point is a C ABI function (HFM_API) taking raw device
+// pointers + a hipStream_t and returning a hipError_t as int.  Python binds them with
+// ctypes after `import torch` (so the HIP runtime torch already loaded is reused: both
+// carry SONAME libamdhip64.so.7) and launches on torch's current stream, which makes the
+// whole train step capturable into a HIP graph.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+#define HFM_API extern "C" __attribute__((visibility("default")))
+
+#define HFM_LAUNCH_CHECK() return (int)hipGetLastError()
+
+// ---- counter-based RNG (mirrors hipfm/utils/rng.py bit-for-bit) ----
+__device__ __forceinline__ uint32_t fmix32(uint32_t h) {
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= h >> 13;
+  h *= 0xC2B2AE35u;
+  h ^= h >> 16;
+  return h;
+}
+__device__ __forceinline__ uint32_t dropout_salt(uint32_t seed, uint32_t step, uint32_t layer) {
+  return fmix32(seed ^ fmix32(step + layer * 0x632BE5ABu));
+}
+__device__ __forceinline__ bool dropout_keep(uint32_t flat, uint32_t salt, uint32_t thr) {
+  return fmix32((flat * 0x9E3779B1u) ^ salt) < thr;
+}
+
+__device__ __forceinline__ float bf2f(bf16 x) { return (float)x; }
+__device__ __forceinline__ bf16 f2bf(float x) { return (bf16)x; }
+
+// Optimizer ids shared by the sparse/dense optimizer kernels (hipfm/ops/optim.py).
+enum HfmOpt { OPT_ADAM = 0, OPT_ADAGRAD = 1, OPT_MOMENTUM = 2, OPT_FTRL = 3, OPT_GD = 4 };
+
+struct OptHyper {
+  float lr;        // base learning rate (already x world size)
+  float l2;        // l2_reg added as l2*w to sparse-table grads (0 for dense MLP params)
+  float b1, b2, eps;
+  float momentum;  // Momentum
+};
+
+// TF1 Adam learning-rate correction with the beta powers of step t (1-based).
+__device__ __forceinline__ float adam_lr_t(const OptHyper& h, int64_t t) {
+  float b1p = powf(h.b1, (float)t), b2p = powf(h.b2, (float)t);
+  return h.lr * sqrtf(1.f - b2p) / (1.f - b1p);
+}
+
+// One optimizer update of a single element; s0/s1 are the optimizer slots.
+template <int OPT>
+__device__ __forceinline__ void opt_update(float& p, float g, float& s0, float& s1,
+                                           const OptHyper& h, float lr_t) {
+  if (OPT == OPT_ADAM) {
+    s0 = s0 * h.b1 + (1.f - h.b1) * g;
+    s1 = s1 * h.b2 + (1.f - h.b2) * g * g;
+    p -= lr_t * s0 / (sqrtf(s1) + h.eps);
+  } else if (OPT == OPT_ADAGRAD) {
+    s0 += g * g;
+    p -= h.lr * g * rsqrtf(s0);
+  } else if (OPT == OPT_MOMENTUM) {
+    s0 = s0 * h.momentum + g;
+    p -= h.lr * s0;
+  } else if (OPT == OPT_FTRL) {  // lr_power=-0.5, l1=l2=0 (tf.train.FtrlOptimizer defaults)
+    float a0 = s0, an = a0 + g * g;
+    float sa = sqrtf(an);
+    float sigma = (sa - sqrtf(a0)) / h.lr;
+    s1 = s1 + g - sigma * p;
+    s0 = an;
+    p = -s1 / (sa / h.lr);
+  } else {  // GD
+    p -= h.lr * g;
+  }
+}

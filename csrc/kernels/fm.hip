@@ -1,0 +1,146 @@
+// K1 fm_fused_fwd and K2 fm_fused_bwd.
+//
+// Reference ops replaced (2-hvd-gpu/DeepFM-hvd-tfrecord-vectorized-map.py):
+//   embedding_lookup(FM_W) * x, reduce_sum          HVD:169-171   -> y_w
+//   embedding_lookup(FM_V) * x                      HVD:173-176   -> E
+//   0.5*sum((sum E)^2 - sum E^2)                    HVD:177-179   -> y_v
+//   reshape(E, [-1, F*K])                           HVD:195       -> MLP input (bf16, + transpose)
+// and their gradients, in two kernels instead of ~15 TF ops.
+//
+// Layout: K/4 lanes per sample, each lane owns a float4 slice of the K-wide embedding row,
+// so a wave gathers 64/(K/4) samples' rows with 16-B loads; the row index for each field is
+// wave-coherent per sample.  E is written row-major [B, KP] (KP = F*K padded to 32, the GEMM
+// K dimension) and transposed [KP, B] (the B operand of the layer-1 weight-gradient GEMM,
+// see mlp.hip), so no GEMM ever needs an LDS transpose.
+#include "common.h"
+
+template <int K>
+__global__ void __launch_bounds__(256) fm_fwd_kernel(
+    const int* __restrict__ idx, const float* __restrict__ vals, const float* __restrict__ tv,
+    const float* __restrict__ tw, const float* __restrict__ bias, int B, int F, int KP,
+    float* __restrict__ y_fm, float* __restrict__ S, bf16* __restrict__ E, bf16* __restrict__ Et) {
+  constexpr int LPS = K / 4;  // lanes per sample
+  const int gt = blockIdx.x * blockDim.x + threadIdx.x;
+  const int b = gt / LPS;
+  const int sub = gt % LPS;
+  if (b >= B) return;
+  f32x4 s = {0.f, 0.f, 0.f, 0.f}, q = {0.f, 0.f, 0.f, 0.f};
+  float yw = 0.f;
+  const int* ib = idx + (size_t)b * F;
+  const float* xb = vals + (size_t)b * F;
+  bf16* eb = E + (size_t)b * KP + sub * 4;
+#pragma unroll 4
+  for (int f = 0; f < F; ++f) {
+    const int id = ib[f];
+    const float x = xb[f];
+    const f32x4 v = *reinterpret_cast<const f32x4*>(tv + (size_t)id * K + sub * 4);
+    const f32x4 e = v * x;
+    s += e;
+    q += e * e;
+    if ((f % LPS) == sub) yw += tw[id] * x;
+    bf16x4 eh = {f2bf(e[0]), f2bf(e[1]), f2bf(e[2]), f2bf(e[3])};
+    *reinterpret_cast<bf16x4*>(eb + f * K) = eh;
+    if (Et) {
+      const size_t c = (size_t)(f * K + sub * 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) Et[(c + j) * B + b] = eh[j];
+    }
+  }
+  float yv = 0.f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) yv += s[j] * s[j] - q[j];
+#pragma unroll
+  for (int o = 1; o < LPS; o <<= 1) {
+    yv += __shfl_xor(yv, o, 64);
+    yw += __shfl_xor(yw, o, 64);
+  }
+  if (S) *reinterpret_cast<f32x4*>(S + (size_t)b * K + sub * 4) = s;
+  if (sub == 0) y_fm[b] = bias[0] + yw + 0.5f * yv;
+}
+
+// Gradient rows in SORTED order (i = position in the id-sorted slot list):
+//   dE[b,f,:] = dX0[b, f*K:(f+1)*K] + dy_b * (S_b - E_bf)        (E_bf = V[row]*x)
+//   G[i].v    = x * dE[b,f,:]     (d fm_v row)     G[i].w = dy_b * x   (d fm_w)
+// The caller reduces G by key (hipcub ReduceByKey) -> one deterministic row-gradient per
+// unique id, with no atomics.
+template <int K>
+struct alignas(16) GradRow {
+  float v[K];
+  float w;
+  float pad[3];
+};
+
+template <int K>
+__global__ void __launch_bounds__(256) fm_bwd_sorted_kernel(
+    const int* __restrict__ perm, const int* __restrict__ idx, const float* __restrict__ vals,
+    const float* __restrict__ tv, const float* __restrict__ dlogit, const float* __restrict__ dX0,
+    const float* __restrict__ S, int n, int F, int KP, GradRow<K>* __restrict__ G) {
+  constexpr int LPS = K / 4;
+  const int gt = blockIdx.x * blockDim.x + threadIdx.x;
+  const int i = gt / LPS;
+  const int sub = gt % LPS;
+  if (i >= n) return;
+  const int p = perm[i];
+  const int b = p / F, f = p - b * F;
+  const int row = idx[p];
+  const float x = vals[p];
+  const float dy = dlogit[b];
+  const f32x4 v = *reinterpret_cast<const f32x4*>(tv + (size_t)row * K + sub * 4);
+  const f32x4 s = *reinterpret_cast<const f32x4*>(S + (size_t)b * K + sub * 4);
+  const f32x4 dx = *reinterpret_cast<const f32x4*>(dX0 + (size_t)b * KP + f * K + sub * 4);
+  const f32x4 de = dx + dy * (s - v * x);
+  *reinterpret_cast<f32x4*>(&G[i].v[sub * 4]) = de * x;
+  if (sub == 0) *reinterpret_cast<f32x4*>(&G[i].w) = f32x4{dy * x, 0.f, 0.f, 0.f};
+}
+
+template <int K>
+static int launch_fm_fwd(const int* idx, const float* vals, const float* tv, const float* tw,
+                         const float* bias, int B, int F, int KP, float* y_fm, float* S, bf16* E,
+                         bf16* Et, hipStream_t st) {
+  constexpr int LPS = K / 4;
+  const long threads = (long)B * LPS;
+  const int grid = (int)((threads + 255) / 256);
+  hipLaunchKernelGGL(fm_fwd_kernel<K>, dim3(grid), dim3(256), 0, st, idx, vals, tv, tw, bias, B,
+                     F, KP, y_fm, S, E, Et);
+  HFM_LAUNCH_CHECK();
+}
+
+template <int K>
+static int launch_fm_bwd(const int* perm, const int* idx, const float* vals, const float* tv,
+                         const float* dlogit, const float* dX0, const float* S, int n, int F,
+                         int KP, void* G, hipStream_t st) {
+  constexpr int LPS = K / 4;
+  const long threads = (long)n * LPS;
+  const int grid = (int)((threads + 255) / 256);
+  hipLaunchKernelGGL(fm_bwd_sorted_kernel<K>, dim3(grid), dim3(256), 0, st, perm, idx, vals, tv,
+                     dlogit, dX0, S, n, F, KP, (GradRow<K>*)G);
+  HFM_LAUNCH_CHECK();
+}
+
+#define HFM_K_DISPATCH(K, CALL) \
+  switch (K) {                  \
+    case 4: return CALL(4);     \
+    case 8: return CALL(8);     \
+    case 16: return CALL(16);   \
+    case 32: return CALL(32);   \
+    case 64: return CALL(64);   \
+    default: return (int)hipErrorInvalidValue; \
+  }
+
+HFM_API int hfm_fm_fwd(const int* idx, const float* vals, const float* tv, const float* tw,
+                       const float* bias, int B, int F, int K, int KP, float* y_fm, float* S,
+                       void* E, void* Et, hipStream_t st) {
+#define CALL(KK) launch_fm_fwd<KK>(idx, vals, tv, tw, bias, B, F, KP, y_fm, S, (bf16*)E, (bf16*)Et, st)
+  HFM_K_DISPATCH(K, CALL)
+#undef CALL
+}
+
+HFM_API int hfm_fm_bwd_sorted(const int* perm, const int* idx, const float* vals, const float* tv,
+                              const float* dlogit, const float* dX0, const float* S, int n, int F,
+                              int K, int KP, void* G, hipStream_t st) {
+#define CALL(KK) launch_fm_bwd<KK>(perm, idx, vals, tv, dlogit, dX0, S, n, F, KP, G, st)
+  HFM_K_DISPATCH(K, CALL)
+#undef CALL
+}
+
+HFM_API int hfm_grad_row_bytes(int K) { return K * 4 + 16; }

@@ -1,0 +1,316 @@
+// K6 mlp_fwd / K6-bwd mlp_bwd / K7 head_loss.
+//
+// Every deep-tower GEMM is expressed as an "NT" product  C[M,N] = A[M,Kd] . B[N,Kd]^T  with
+// BOTH operands contiguous along the reduction dimension, because every producer in the step
+// writes its output twice — row-major and transposed (fm.hip writes E and E^T, the forward
+// epilogue writes H and H^T, the backward epilogues write dZ and dZ^T, the dense optimizer
+// keeps W and W^T in bf16).  The gfx950 MFMA fragments for v_mfma_f32_16x16x32_bf16
+// (lane l: A[l&15][8(l>>4)+j], B[8(l>>4)+j][l&15], j=0..7) are then single 16-B global loads
+// straight into VGPRs — no LDS staging and no LDS transposes:
+//   forward  H_i   = relu(X_i W_i^T + b_i) (.) dropout      A = X_i  [M,K_i]  B = W_i   [N_i,K_i]
+//   dgrad    dZ_{i-1} = (dZ_i W_i) (.) mask(H_{i-1})/keep    A = dZ_i [M,N_i]  B = W_i^T [K_i,N_i]
+//   wgrad    dW_i  = dZ_i^T X_i  (split over the batch)      A = dZ_i^T [N_i,M] B = X_i^T [K_i,M]
+// Tiles: one wave owns a 32x32 output block (2x2 MFMA 16x16x32 tiles, 4 f32x4 accumulators);
+// a workgroup is WM x WN waves.  Dropout masks are regenerated from a counter hash
+// (utils/rng.py) in the forward epilogue; the backward recovers the mask from H>0, so no mask
+// tensor is ever stored.  The whole deep tower is ~1 MFLOP/sample: these kernels are sized for
+// occupancy and HBM traffic, not for MFMA peak.
+#include "common.h"
+
+enum EpiMode {
+  EPI_F32 = 0,        // C f32 [M,N] (split-K: slab blockIdx.z at C + z*M*N)
+  EPI_FWD = 1,        // +bias, relu, dropout -> H bf16 [M,N] and H^T bf16 [N,M]
+  EPI_DGRAD = 2,      // mask by Hprev>0, *scale -> dZ bf16 [M,N] and dZ^T [N,M]
+  EPI_FWD_EVAL = 3,   // +bias, relu (no dropout), H only
+};
+
+struct EpiArgs {
+  const float* bias;       // [N]
+  const bf16* hprev;       // EPI_DGRAD: activation whose >0 pattern masks the gradient [M,N]
+  float scale;             // EPI_DGRAD: 1/keep of that activation's dropout
+  uint32_t seed, layer, keep_thr;
+  int drop;                // apply dropout
+  const int64_t* step;     // device step counter (dropout salt)
+  void* out;               // f32 C or bf16 H/dZ
+  bf16* out_t;             // transposed copy (nullable)
+};
+
+template <int WM, int WN, int EPI>
+__global__ void __launch_bounds__(WM * WN * 64) gemm_nt_kernel(
+    const bf16* __restrict__ A, int lda, const bf16* __restrict__ Bm, int ldb, int M, int N,
+    int kchunk, EpiArgs ep) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wm = wave / WN, wn = wave % WN;
+  const int row0 = blockIdx.x * (WM * 32) + wm * 32;
+  const int col0 = blockIdx.y * (WN * 32) + wn * 32;
+  const int k0 = blockIdx.z * kchunk;
+  const int r = lane & 15, kq = (lane >> 4) * 8;
+
+  const bf16* a0 = A + (size_t)(row0 + r) * lda + k0 + kq;
+  const bf16* a1 = a0 + (size_t)16 * lda;
+  const bf16* b0 = Bm + (size_t)(col0 + r) * ldb + k0 + kq;
+  const bf16* b1 = b0 + (size_t)16 * ldb;
+
+  f32x4 c00 = {0, 0, 0, 0}, c01 = c00, c10 = c00, c11 = c00;
+
+  for (int k = 0; k < kchunk; k += 32) {
+    const bf16x8 fa0 = *reinterpret_cast<const bf16x8*>(a0 + k);
+    const bf16x8 fa1 = *reinterpret_cast<const bf16x8*>(a1 + k);
+    const bf16x8 fb0 = *reinterpret_cast<const bf16x8*>(b0 + k);
+    const bf16x8 fb1 = *reinterpret_cast<const bf16x8*>(b1 + k);
+    c00 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa0, fb0, c00, 0, 0, 0);
+    c01 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa0, fb1, c01, 0, 0, 0);
+    c10 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa1, fb0, c10, 0, 0, 0);
+    c11 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa1, fb1, c11, 0, 0, 0);
+  }
+
+  // C/D map: col = lane&15, row = (lane>>4)*4 + j
+  const int cr = (lane >> 4) * 4, cc = lane & 15;
+  uint32_t salt = 0;
+  if (EPI == EPI_FWD && ep.drop) salt = dropout_salt(ep.seed, (uint32_t)(*ep.step), ep.layer);
+  f32x4 accs[2][2] = {{c00, c01}, {c10, c11}};
+#pragma unroll
+  for (int ti = 0; ti < 2; ++ti) {
+#pragma unroll
+    for (int tj = 0; tj < 2; ++tj) {
+      const int col = col0 + tj * 16 + cc;
+      const int rowb = row0 + ti * 16 + cr;
+      const f32x4 acc = accs[ti][tj];
+      if (EPI == EPI_F32) {
+        float* C = reinterpret_cast<float*>(ep.out) + (size_t)blockIdx.z * M * N;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) C[(size_t)(rowb + j) * N + col] = acc[j];
+      } else {
+        bf16x4 tv;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int row = rowb + j;
+          float v = acc[j];
+          if (EPI == EPI_FWD || EPI == EPI_FWD_EVAL) {
+            v = fmaxf(v + ep.bias[col], 0.f);
+            if (EPI == EPI_FWD && ep.drop)
+              v = dropout_keep((uint32_t)(row * N + col), salt, ep.keep_thr) ? v * ep.scale : 0.f;
+          } else {  // EPI_DGRAD
+            v = (bf2f(ep.hprev[(size_t)row * N + col]) > 0.f) ? v * ep.scale : 0.f;
+          }
+          const bf16 hv = f2bf(v);
+          reinterpret_cast<bf16*>(ep.out)[(size_t)row * N + col] = hv;
+          tv[j] = hv;
+        }
+        if (ep.out_t) *reinterpret_cast<bf16x4*>(ep.out_t + (size_t)col * M + rowb) = tv;
+      }
+    }
+  }
+}
+
+template <int WM, int WN, int EPI>
+static int launch_gemm(const bf16* A, int lda, const bf16* B, int ldb, int M, int N, int Kd,
+                       int splitk, const EpiArgs& ep, hipStream_t st) {
+  if (M % (WM * 32) || N % (WN * 32) || Kd % (32 * splitk)) return (int)hipErrorInvalidValue;
+  dim3 grid(M / (WM * 32), N / (WN * 32), splitk);
+  hipLaunchKernelGGL((gemm_nt_kernel<WM, WN, EPI>), grid, dim3(WM * WN * 64), 0, st, A, lda, B, ldb,
+                     M, N, Kd / splitk, ep);
+  HFM_LAUNCH_CHECK();
+}
+
+// tile: 0 = 64x64 (2x2 waves), 1 = 128x32 (4x1), 2 = 32x128 (1x4), 3 = 32x32 (1x1), 4 = 32x64 (1x2)
+template <int EPI>
+static int gemm_tile(int tile, const bf16* A, int lda, const bf16* B, int ldb, int M, int N, int Kd,
+                     int splitk, const EpiArgs& ep, hipStream_t st) {
+  switch (tile) {
+    case 0: return launch_gemm<2, 2, EPI>(A, lda, B, ldb, M, N, Kd, splitk, ep, st);
+    case 1: return launch_gemm<4, 1, EPI>(A, lda, B, ldb, M, N, Kd, splitk, ep, st);
+    case 2: return launch_gemm<1, 4, EPI>(A, lda, B, ldb, M, N, Kd, splitk, ep, st);
+    case 3: return launch_gemm<1, 1, EPI>(A, lda, B, ldb, M, N, Kd, splitk, ep, st);
+    case 4: return launch_gemm<1, 2, EPI>(A, lda, B, ldb, M, N, Kd, splitk, ep, st);
+    default: return (int)hipErrorInvalidValue;
+  }
+}
+
+HFM_API int hfm_gemm_nt(int epi, int tile, const void* A, int lda, const void* B, int ldb, int M,
+                        int N, int Kd, int splitk, const EpiArgs* ep, hipStream_t st) {
+  const bf16* a = (const bf16*)A;
+  const bf16* b = (const bf16*)B;
+  switch (epi) {
+    case EPI_F32: return gemm_tile<EPI_F32>(tile, a, lda, b, ldb, M, N, Kd, splitk, *ep, st);
+    case EPI_FWD: return gemm_tile<EPI_FWD>(tile, a, lda, b, ldb, M, N, Kd, 1, *ep, st);
+    case EPI_DGRAD: return gemm_tile<EPI_DGRAD>(tile, a, lda, b, ldb, M, N, Kd, 1, *ep, st);
+    case EPI_FWD_EVAL: return gemm_tile<EPI_FWD_EVAL>(tile, a, lda, b, ldb, M, N, Kd, 1, *ep, st);
+    default: return (int)hipErrorInvalidValue;
+  }
+}
+
+HFM_API int hfm_epi_args_bytes() { return (int)sizeof(EpiArgs); }
+
+// ------------------------------------------------------------------ K7 head
+// Per sample: y_d = h_L . w_out + b_out;  y = y_fm + y_d;  p = sigmoid(y);
+//   loss_b = BCE(y, label) (or (p-label)^2);  dlogit = dL/dy * gscale  (gscale = 1/global batch)
+//   dZ_L = dlogit * w_out (.) (h_L > 0) / keep_L     (bf16, + transpose)
+// Block partials (deterministic LDS tree): [ sum dlogit*h_L (L) | sum dlogit | sum loss ].
+struct HeadArgs {
+  const bf16* h;        // [M, L] last hidden activation (post dropout)
+  const float* w_out;   // [L] (inside the flat param buffer)
+  const float* b_out;   // [1]
+  const float* y_fm;    // [M]
+  const float* labels;  // [M] (nullable in predict mode)
+  int M, L, nvalid;     // nvalid: rows < nvalid contribute to loss/grad (padding rows excluded)
+  int square_loss;
+  int train;            // 0: predict/eval (probabilities + loss only)
+  float gscale;         // 1 / global batch
+  float scale_l;        // 1/keep of the last hidden layer's dropout
+  float* prob;          // [M]
+  float* logit;         // [M] (nullable)
+  float* dlogit;        // [M]
+  bf16* dz;             // [M, L]
+  bf16* dz_t;           // [L, M]
+  float* partial;       // [gridDim.x, L + 2]
+};
+
+template <int L>
+__global__ void __launch_bounds__(256) head_kernel(HeadArgs a) {
+  __shared__ float red[256];
+  const int b = blockIdx.x * 256 + threadIdx.x;
+  float hv[L];
+  float dl = 0.f, lossb = 0.f;
+  const bool valid = b < a.nvalid;
+  if (b < a.M) {
+    const bf16* hr = a.h + (size_t)b * L;
+#pragma unroll
+    for (int j = 0; j < L; j += 8) {
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(hr + j);
+#pragma unroll
+      for (int t = 0; t < 8; ++t) hv[j + t] = bf2f(v[t]);
+    }
+    float yd = a.b_out[0];
+#pragma unroll
+    for (int j = 0; j < L; ++j) yd += hv[j] * a.w_out[j];
+    const float y = a.y_fm[b] + yd;
+    const float p = 1.f / (1.f + __expf(-y));
+    a.prob[b] = p;
+    if (a.logit) a.logit[b] = y;
+    if (a.labels && valid) {
+      const float lab = a.labels[b];
+      if (a.square_loss) {
+        lossb = (p - lab) * (p - lab);
+        dl = 2.f * (p - lab) * p * (1.f - p) * a.gscale;
+      } else {
+        lossb = fmaxf(y, 0.f) - y * lab + log1pf(__expf(-fabsf(y)));
+        dl = (p - lab) * a.gscale;
+      }
+    }
+    if (a.train) {
+      a.dlogit[b] = dl;
+      bf16* dzr = a.dz + (size_t)b * L;
+#pragma unroll
+      for (int j = 0; j < L; ++j) {
+        const float g = hv[j] > 0.f ? dl * a.w_out[j] * a.scale_l : 0.f;
+        const bf16 gh = f2bf(g);
+        dzr[j] = gh;
+        a.dz_t[(size_t)j * a.M + b] = gh;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < L; ++j) hv[j] = 0.f;
+  }
+  // deterministic block reductions: L + 2 sums
+  float* part = a.partial + (size_t)blockIdx.x * (L + 2);
+  for (int q = 0; q < L + 2; ++q) {
+    float v;
+    if (q < L) v = a.train ? dl * hv[q] : 0.f;
+    else if (q == L) v = dl;
+    else v = lossb;
+    red[threadIdx.x] = v;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+      if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) part[q] = red[0];
+    __syncthreads();
+  }
+}
+
+HFM_API int hfm_head(const HeadArgs* a, hipStream_t st) {
+  const int grid = (a->M + 255) / 256;
+  switch (a->L) {
+    case 32: hipLaunchKernelGGL(head_kernel<32>, dim3(grid), dim3(256), 0, st, *a); break;
+    case 64: hipLaunchKernelGGL(head_kernel<64>, dim3(grid), dim3(256), 0, st, *a); break;
+    case 96: hipLaunchKernelGGL(head_kernel<96>, dim3(grid), dim3(256), 0, st, *a); break;
+    case 128: hipLaunchKernelGGL(head_kernel<128>, dim3(grid), dim3(256), 0, st, *a); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+  HFM_LAUNCH_CHECK();
+}
+HFM_API int hfm_head_args_bytes() { return (int)sizeof(HeadArgs); }
+
+// ------------------------------------------------------------------ gradient finalize
+// Sums split-K wgrad slabs and head partials into the flat dense-gradient buffer (one job
+// table, one launch), and computes bias gradients as row sums of the transposed dZ^T.
+struct SlabJob {
+  float* dst;
+  const float* src;
+  long n;          // elements
+  int nslab;
+  long stride;     // elements between slabs
+  long src_ld;     // source row stride (elements; == n if contiguous)
+  int cols;        // dst/src columns per row (to map linear index -> src offset with src_ld)
+  float scale;
+};
+
+__global__ void slab_reduce_kernel(const SlabJob* __restrict__ jobs, int njobs) {
+  const SlabJob j = jobs[blockIdx.y];
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < j.n; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / j.cols, c = i % j.cols;
+    const long so = r * j.src_ld + c;
+    float s = 0.f;
+    for (int z = 0; z < j.nslab; ++z) s += j.src[so + (long)z * j.stride];
+    j.dst[i] = s * j.scale;
+  }
+}
+
+HFM_API int hfm_slab_reduce(const void* jobs, int njobs, int max_n, hipStream_t st) {
+  int gx = (max_n + 255) / 256;
+  if (gx > 1024) gx = 1024;
+  if (gx < 1) gx = 1;
+  hipLaunchKernelGGL(slab_reduce_kernel, dim3(gx, njobs), dim3(256), 0, st, (const SlabJob*)jobs, njobs);
+  HFM_LAUNCH_CHECK();
+}
+HFM_API int hfm_slab_job_bytes() { return (int)sizeof(SlabJob); }
+
+struct RowSumJob {
+  float* dst;       // [rows]
+  const bf16* src;  // [rows, ld]
+  int rows, n;      // sum the first n entries of each row
+  long ld;
+};
+
+__global__ void __launch_bounds__(256) rowsum_kernel(const RowSumJob* __restrict__ jobs, int njobs) {
+  __shared__ float red[256];
+  // blockIdx.x enumerates (job, row) pairs
+  int rem = blockIdx.x, ji = 0;
+  while (ji < njobs && rem >= jobs[ji].rows) { rem -= jobs[ji].rows; ++ji; }
+  if (ji >= njobs) return;
+  const RowSumJob j = jobs[ji];
+  const bf16* s = j.src + (size_t)rem * j.ld;
+  float acc = 0.f;
+  for (int i = threadIdx.x * 8; i < j.n; i += 256 * 8) {
+    const bf16x8 v = *reinterpret_cast<const bf16x8*>(s + i);
+#pragma unroll
+    for (int t = 0; t < 8; ++t) acc += bf2f(v[t]);
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) j.dst[rem] = red[0];
+}
+
+HFM_API int hfm_rowsum(const void* jobs, int njobs, int total_rows, hipStream_t st) {
+  if (total_rows <= 0) return 0;
+  hipLaunchKernelGGL(rowsum_kernel, dim3(total_rows), dim3(256), 0, st, (const RowSumJob*)jobs, njobs);
+  HFM_LAUNCH_CHECK();
+}
+HFM_API int hfm_rowsum_job_bytes() { return (int)sizeof(RowSumJob); }

@@ -1,0 +1,299 @@
+// K4 sparse_optim and K5 dense_optim.
+//
+// Embedding tables (fm_v [R,K], fm_w [R]) — two modes:
+//  * lazy      : update only the unique rows of this step (one fused row-wise kernel; the
+//                l2*w term of the whole-table l2_loss is applied to those rows only).
+//  * tf1_dense : reference semantics.  TF1 aggregates the gather's IndexedSlices with the
+//                dense gradient of l2_loss(fm_v) (= l2*fm_v) into IndexedSlices covering every
+//                row, so Adam/Adagrad/... move EVERY row EVERY step.  Implemented as a scatter of
+//                the unique row-gradients into a persistent zero-invariant gradient buffer,
+//                then one streaming sweep that applies g = l2*w + G and re-zeroes G.
+// Dense MLP parameters live in one flat fp32 buffer (one all-reduce bucket); the dense
+// optimizer also refreshes the bf16 W and W^T copies the MFMA GEMMs read (mlp.hip).
+//
+// The optimizer step t is read from device memory (t = *step + 1), so one captured HIP graph
+// replays correctly for every step.
+#include "common.h"
+
+template <int K>
+struct alignas(16) GradRowO {
+  float v[K];
+  float w;
+  float pad[3];
+};
+
+template <int OPT>
+__device__ __forceinline__ float lr_t_of(const OptHyper& h, const int64_t* step) {
+  return OPT == OPT_ADAM ? adam_lr_t(h, *step + 1) : h.lr;
+}
+
+// ------------------------------------------------------------------ lazy row update
+template <int K, int OPT>
+__global__ void __launch_bounds__(256) sparse_rows_kernel(
+    const int* __restrict__ ukeys, const GradRowO<K>* __restrict__ UG, const int* __restrict__ num,
+    int row_div, float* __restrict__ tv, float* __restrict__ tw, float* __restrict__ s0v,
+    float* __restrict__ s1v, float* __restrict__ s0w, float* __restrict__ s1w, OptHyper h,
+    const int64_t* __restrict__ step) {
+  constexpr int LPS = K / 4;
+  const int gt = blockIdx.x * blockDim.x + threadIdx.x;
+  const int u = gt / LPS, sub = gt % LPS;
+  if (u >= *num) return;
+  const float lr_t = lr_t_of<OPT>(h, step);
+  const size_t row = (size_t)(ukeys[u] / row_div);
+  const size_t o = row * K + sub * 4;
+  f32x4 p = *reinterpret_cast<f32x4*>(tv + o);
+  f32x4 g = *reinterpret_cast<const f32x4*>(&UG[u].v[sub * 4]);
+  f32x4 a = {0, 0, 0, 0}, c = {0, 0, 0, 0};
+  if (OPT != OPT_GD) a = *reinterpret_cast<f32x4*>(s0v + o);
+  if (OPT == OPT_ADAM || OPT == OPT_FTRL) c = *reinterpret_cast<f32x4*>(s1v + o);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    float gj = g[j] + h.l2 * p[j];
+    float pj = p[j], aj = a[j], cj = c[j];
+    opt_update<OPT>(pj, gj, aj, cj, h, lr_t);
+    p[j] = pj; a[j] = aj; c[j] = cj;
+  }
+  *reinterpret_cast<f32x4*>(tv + o) = p;
+  if (OPT != OPT_GD) *reinterpret_cast<f32x4*>(s0v + o) = a;
+  if (OPT == OPT_ADAM || OPT == OPT_FTRL) *reinterpret_cast<f32x4*>(s1v + o) = c;
+  if (sub == 0) {
+    float pw = tw[row];
+    float gw = UG[u].w + h.l2 * pw;
+    float aw = (OPT != OPT_GD) ? s0w[row] : 0.f;
+    float cw = (OPT == OPT_ADAM || OPT == OPT_FTRL) ? s1w[row] : 0.f;
+    opt_update<OPT>(pw, gw, aw, cw, h, lr_t);
+    tw[row] = pw;
+    if (OPT != OPT_GD) s0w[row] = aw;
+    if (OPT == OPT_ADAM || OPT == OPT_FTRL) s1w[row] = cw;
+  }
+}
+
+// ------------------------------------------------------------------ tf1_dense
+template <int K>
+__global__ void scatter_rows_kernel(const int* __restrict__ ukeys, const GradRowO<K>* __restrict__ UG,
+                                    const int* __restrict__ num, int row_div, float* __restrict__ Gv,
+                                    float* __restrict__ Gw) {
+  constexpr int LPS = K / 4;
+  const int gt = blockIdx.x * blockDim.x + threadIdx.x;
+  const int u = gt / LPS, sub = gt % LPS;
+  if (u >= *num) return;
+  const size_t row = (size_t)(ukeys[u] / row_div);
+  *reinterpret_cast<f32x4*>(Gv + row * K + sub * 4) =
+      *reinterpret_cast<const f32x4*>(&UG[u].v[sub * 4]);
+  if (sub == 0) Gw[row] = UG[u].w;
+}
+
+template <int K, int OPT>
+__global__ void __launch_bounds__(256) dense_sweep_kernel(
+    long R, float* __restrict__ tv, float* __restrict__ tw, float* __restrict__ Gv,
+    float* __restrict__ Gw, float* __restrict__ s0v, float* __restrict__ s1v,
+    float* __restrict__ s0w, float* __restrict__ s1w, OptHyper h, const int64_t* __restrict__ step) {
+  constexpr int LPS = K / 4;
+  const float lr_t = lr_t_of<OPT>(h, step);
+  const long total = R * LPS;
+  for (long gt = blockIdx.x * (long)blockDim.x + threadIdx.x; gt < total;
+       gt += (long)gridDim.x * blockDim.x) {
+    const long row = gt / LPS;
+    const int sub = (int)(gt % LPS);
+    const size_t o = (size_t)row * K + sub * 4;
+    f32x4 p = *reinterpret_cast<f32x4*>(tv + o);
+    f32x4 g = *reinterpret_cast<f32x4*>(Gv + o);
+    f32x4 a = {0, 0, 0, 0}, c = {0, 0, 0, 0};
+    if (OPT != OPT_GD) a = *reinterpret_cast<f32x4*>(s0v + o);
+    if (OPT == OPT_ADAM || OPT == OPT_FTRL) c = *reinterpret_cast<f32x4*>(s1v + o);
+    const bool touched = (g[0] != 0.f) | (g[1] != 0.f) | (g[2] != 0.f) | (g[3] != 0.f);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float gj = g[j] + h.l2 * p[j];
+      float pj = p[j], aj = a[j], cj = c[j];
+      opt_update<OPT>(pj, gj, aj, cj, h, lr_t);
+      p[j] = pj; a[j] = aj; c[j] = cj;
+    }
+    *reinterpret_cast<f32x4*>(tv + o) = p;
+    if (OPT != OPT_GD) *reinterpret_cast<f32x4*>(s0v + o) = a;
+    if (OPT == OPT_ADAM || OPT == OPT_FTRL) *reinterpret_cast<f32x4*>(s1v + o) = c;
+    if (touched) *reinterpret_cast<f32x4*>(Gv + o) = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (sub == 0) {
+      float pw = tw[row];
+      float g0 = Gw[row];
+      float gw = g0 + h.l2 * pw;
+      float aw = (OPT != OPT_GD) ? s0w[row] : 0.f;
+      float cw = (OPT == OPT_ADAM || OPT == OPT_FTRL) ? s1w[row] : 0.f;
+      opt_update<OPT>(pw, gw, aw, cw, h, lr_t);
+      tw[row] = pw;
+      if (OPT != OPT_GD) s0w[row] = aw;
+      if (OPT == OPT_ADAM || OPT == OPT_FTRL) s1w[row] = cw;
+      if (g0 != 0.f) Gw[row] = 0.f;
+    }
+  }
+}
+
+// ------------------------------------------------------------------ dense flat params
+struct ShadowSeg {   // a weight matrix [rows, cols] inside the flat buffer with bf16 copies
+  long off;          // element offset in the flat buffer
+  int rows, cols;
+  bf16* w16;         // [rows, cols]
+  bf16* wt16;        // [cols, rows]
+};
+
+template <int OPT>
+__global__ void __launch_bounds__(256) dense_opt_kernel(
+    float* __restrict__ p, const float* __restrict__ g, float* __restrict__ s0, float* __restrict__ s1,
+    long n, OptHyper h, const int64_t* __restrict__ step, const ShadowSeg* __restrict__ segs, int nseg) {
+  const float lr_t = lr_t_of<OPT>(h, step);
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    float pi = p[i];
+    float a = (OPT != OPT_GD) ? s0[i] : 0.f;
+    float c = (OPT == OPT_ADAM || OPT == OPT_FTRL) ? s1[i] : 0.f;
+    opt_update<OPT>(pi, g[i], a, c, h, lr_t);
+    p[i] = pi;
+    if (OPT != OPT_GD) s0[i] = a;
+    if (OPT == OPT_ADAM || OPT == OPT_FTRL) s1[i] = c;
+    for (int s = 0; s < nseg; ++s) {
+      const long rel = i - segs[s].off;
+      const long sz = (long)segs[s].rows * segs[s].cols;
+      if (rel >= 0 && rel < sz) {
+        const int r = (int)(rel / segs[s].cols), cc = (int)(rel % segs[s].cols);
+        segs[s].w16[rel] = f2bf(pi);
+        segs[s].wt16[(long)cc * segs[s].rows + r] = f2bf(pi);
+      }
+    }
+  }
+}
+
+// refresh bf16 shadows without an update (after init / checkpoint load)
+__global__ void shadow_refresh_kernel(const float* __restrict__ p, long n,
+                                      const ShadowSeg* __restrict__ segs, int nseg) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    for (int s = 0; s < nseg; ++s) {
+      const long rel = i - segs[s].off;
+      const long sz = (long)segs[s].rows * segs[s].cols;
+      if (rel >= 0 && rel < sz) {
+        const int r = (int)(rel / segs[s].cols), cc = (int)(rel % segs[s].cols);
+        segs[s].w16[rel] = f2bf(p[i]);
+        segs[s].wt16[(long)cc * segs[s].rows + r] = f2bf(p[i]);
+      }
+    }
+  }
+}
+
+__global__ void step_inc_kernel(int64_t* step) { *step += 1; }
+
+// ------------------------------------------------------------------ dispatch
+#define HFM_OPT_DISPATCH(OPT, CALL)   \
+  switch (OPT) {                      \
+    case OPT_ADAM: CALL(OPT_ADAM); break;         \
+    case OPT_ADAGRAD: CALL(OPT_ADAGRAD); break;   \
+    case OPT_MOMENTUM: CALL(OPT_MOMENTUM); break; \
+    case OPT_FTRL: CALL(OPT_FTRL); break;         \
+    case OPT_GD: CALL(OPT_GD); break;             \
+    default: return (int)hipErrorInvalidValue;    \
+  }
+
+template <int K>
+static int sparse_rows_k(int opt, const int* ukeys, const void* UG, const int* num, int max_n,
+                         int row_div, float* tv, float* tw, float* s0v, float* s1v, float* s0w,
+                         float* s1w, OptHyper h, const int64_t* step, hipStream_t st) {
+  constexpr int LPS = K / 4;
+  const long th = (long)max_n * LPS;
+  const int grid = (int)((th + 255) / 256);
+  if (grid == 0) return 0;
+#define CALL(O)                                                                                   \
+  hipLaunchKernelGGL((sparse_rows_kernel<K, O>), dim3(grid), dim3(256), 0, st, ukeys,             \
+                     (const GradRowO<K>*)UG, num, row_div, tv, tw, s0v, s1v, s0w, s1w, h, step)
+  HFM_OPT_DISPATCH(opt, CALL)
+#undef CALL
+  HFM_LAUNCH_CHECK();
+}
+
+template <int K>
+static int scatter_k(const int* ukeys, const void* UG, const int* num, int max_n, int row_div,
+                     float* Gv, float* Gw, hipStream_t st) {
+  constexpr int LPS = K / 4;
+  const long th = (long)max_n * LPS;
+  const int grid = (int)((th + 255) / 256);
+  if (grid == 0) return 0;
+  hipLaunchKernelGGL(scatter_rows_kernel<K>, dim3(grid), dim3(256), 0, st, ukeys,
+                     (const GradRowO<K>*)UG, num, row_div, Gv, Gw);
+  HFM_LAUNCH_CHECK();
+}
+
+template <int K>
+static int sweep_k(int opt, long R, float* tv, float* tw, float* Gv, float* Gw, float* s0v,
+                   float* s1v, float* s0w, float* s1w, OptHyper h, const int64_t* step,
+                   hipStream_t st) {
+  constexpr int LPS = K / 4;
+  const long th = R * LPS;
+  long g = (th + 255) / 256;
+  const int grid = (int)(g < 8192 ? g : 8192);
+  if (grid == 0) return 0;
+#define CALL(O)                                                                              \
+  hipLaunchKernelGGL((dense_sweep_kernel<K, O>), dim3(grid), dim3(256), 0, st, R, tv, tw, Gv, \
+                     Gw, s0v, s1v, s0w, s1w, h, step)
+  HFM_OPT_DISPATCH(opt, CALL)
+#undef CALL
+  HFM_LAUNCH_CHECK();
+}
+
+#define HFM_K_DISPATCH(K, CALL) \
+  switch (K) {                  \
+    case 4: return CALL(4);     \
+    case 8: return CALL(8);     \
+    case 16: return CALL(16);   \
+    case 32: return CALL(32);   \
+    case 64: return CALL(64);   \
+    default: return (int)hipErrorInvalidValue; \
+  }
+
+HFM_API int hfm_sparse_rows_update(int K, int opt, const int* ukeys, const void* UG, const int* num,
+                                   int max_n, int row_div, float* tv, float* tw, float* s0v,
+                                   float* s1v, float* s0w, float* s1w, const OptHyper* h,
+                                   const int64_t* step, hipStream_t st) {
+#define CALL(KK) sparse_rows_k<KK>(opt, ukeys, UG, num, max_n, row_div, tv, tw, s0v, s1v, s0w, s1w, *h, step, st)
+  HFM_K_DISPATCH(K, CALL)
+#undef CALL
+}
+
+HFM_API int hfm_scatter_rows(int K, const int* ukeys, const void* UG, const int* num, int max_n,
+                             int row_div, float* Gv, float* Gw, hipStream_t st) {
+#define CALL(KK) scatter_k<KK>(ukeys, UG, num, max_n, row_div, Gv, Gw, st)
+  HFM_K_DISPATCH(K, CALL)
+#undef CALL
+}
+
+HFM_API int hfm_dense_sweep(int K, int opt, long R, float* tv, float* tw, float* Gv, float* Gw,
+                            float* s0v, float* s1v, float* s0w, float* s1w, const OptHyper* h,
+                            const int64_t* step, hipStream_t st) {
+#define CALL(KK) sweep_k<KK>(opt, R, tv, tw, Gv, Gw, s0v, s1v, s0w, s1w, *h, step, st)
+  HFM_K_DISPATCH(K, CALL)
+#undef CALL
+}
+
+HFM_API int hfm_dense_opt(int opt, float* p, const float* g, float* s0, float* s1, long n,
+                          const OptHyper* h, const int64_t* step, const void* segs, int nseg,
+                          hipStream_t st) {
+  long gg = (n + 255) / 256;
+  const int grid = (int)(gg < 4096 ? gg : 4096);
+#define CALL(O)                                                                                  \
+  hipLaunchKernelGGL((dense_opt_kernel<O>), dim3(grid), dim3(256), 0, st, p, g, s0, s1, n, *h, step, \
+                     (const ShadowSeg*)segs, nseg)
+  HFM_OPT_DISPATCH(opt, CALL)
+#undef CALL
+  HFM_LAUNCH_CHECK();
+}
+
+HFM_API int hfm_shadow_refresh(const float* p, long n, const void* segs, int nseg, hipStream_t st) {
+  long gg = (n + 255) / 256;
+  const int grid = (int)(gg < 4096 ? gg : 4096);
+  hipLaunchKernelGGL(shadow_refresh_kernel, dim3(grid), dim3(256), 0, st, p, n,
+                     (const ShadowSeg*)segs, nseg);
+  HFM_LAUNCH_CHECK();
+}
+
+HFM_API int hfm_step_inc(int64_t* step, hipStream_t st) {
+  hipLaunchKernelGGL(step_inc_kernel, dim3(1), dim3(1), 0, st, step);
+  HFM_LAUNCH_CHECK();
+}
+
+HFM_API int hfm_shadow_seg_bytes() { return (int)sizeof(ShadowSeg); }
+HFM_API int hfm_opt_hyper_bytes() { return (int)sizeof(OptHyper); }

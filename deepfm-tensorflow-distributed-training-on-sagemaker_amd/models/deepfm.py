@@ -1,0 +1,536 @@
+"""NativeDeepFM: the MI355X executor of one DeepFM training / inference step.
+
+No autograd and no per-op dispatch: the step is a fixed sequence of hand-written gfx950
+kernels over pre-allocated HBM buffers (so it can be captured once into a HIP graph and
+replayed), with the backward written out explicitly:
+
+  K1 fm_fwd        gather fm_w/fm_v rows, y_w, y_v, S = sum_f E, E and E^T (bf16)     fm.hip
+  K6 gemm(FWD)     per deep layer: relu(X W^T + b) * dropout -> H, H^T            mlp.hip
+  K7 head          y_d, y, sigmoid, BCE, dlogit, dZ_L, partial sums               mlp.hip
+  K6 gemm(F32)     per layer: wgrad slabs (split over the batch)                  mlp.hip
+  K6 gemm(DGRAD)   per layer: dZ_{i-1} = (dZ_i W_i) masked by H_{i-1} > 0         mlp.hip
+  finalize         slab sums + bias row-sums -> flat dense gradient               mlp.hip
+  [dense all-reduce over RCCL, async, overlapped with the sparse backward]
+  K3 sort          radix sort of the batch ids (hipCUB)                           sparse.hip
+  K2 fm_bwd        per-slot embedding row gradients in sorted order               fm.hip
+  K3 reduce        reduce-by-key -> one gradient row per unique id                sparse.hip
+  [sparse exchange: allgather (replicated table) or all-to-all (row-sharded)]
+  K4 sparse optim  lazy row update, or tf1_dense scatter + full-table sweep        optim.hip
+  K5 dense optim   flat Adam/... over MLP params + fm_bias, refreshes bf16 W, W^T   optim.hip
+
+Numerics contract (tests/test_gpu_kernels.py): fp32 tables and optimizer state, bf16 MLP
+operands with fp32 accumulation, matching models/reference.py (the TF1 transcription).
+Reference parity cites: model_fn HVD:141-287, optimizer HVD:252-263, LR scaling HVD:149.
+"""
+from __future__ import annotations
+
+import math
+from collections import OrderedDict
+from dataclasses import dataclass
+from typing import Dict, List, Optional
+
+import torch
+
+from ..ops import kernels as KN
+from ..ops._lib import EpiArgs, HeadArgs, RowSumJob, ShadowSeg, SlabJob
+from ..utils.rng import keep_threshold
+from .reference import glorot_std, init_params, pad32
+
+
+def _align(n: int, a: int = 64) -> int:
+    return (n + a - 1) // a * a
+
+
+def _pick_tile(M: int, N: int) -> int:
+    if M % 64 == 0 and N % 64 == 0:
+        return 0
+    if N == 32 and M % 128 == 0:
+        return 1
+    if M == 32 and N % 128 == 0:
+        return 2
+    if M == 32 and N % 64 == 0:
+        return 4
+    return 3
+
+
+def _pick_splitk(M: int, N: int, Kd: int, tile: int, target_blocks: int = 512) -> int:
+    bm, bn = KN.TILES[tile]
+    tiles = (M // bm) * (N // bn)
+    ksteps = Kd // 32
+    want = max(1, min(ksteps, target_blocks // max(1, tiles)))
+    for s in range(want, 0, -1):
+        if ksteps % s == 0:
+            return s
+    return 1
+
+
+@dataclass
+class DenseSeg:
+    name: str
+    off: int
+    shape: tuple        # native layout shape
+    tf_shape: tuple     # TF checkpoint shape
+
+
+class NativeDeepFM:
+    """DeepFM on one GPU (one rank).  ``comm`` (parallel.dist.Comm) adds data parallelism."""
+
+    def __init__(self, feature_size: int, field_size: int, embedding_size: int = 32,
+                 deep_layers=(256, 128, 64), keep_probs=(0.5, 0.5, 0.5), l2_reg: float = 1e-4,
+                 learning_rate: float = 5e-4, optimizer: str = "Adam", loss_type: str = "log_loss",
+                 sparse_update: str = "tf1_dense", seed: int = 1234, batch_size: int = 1024,
+                 device="cuda", comm=None, init: bool = True, batch_norm: bool = False):
+        if batch_norm:
+            raise NotImplementedError("batch_norm on the native path is not implemented yet; "
+                                      "use --device cpu (golden path) for batch_norm runs")
+        self.V, self.F, self.K = int(feature_size), int(field_size), int(embedding_size)
+        if self.K not in (4, 8, 16, 32, 64):
+            raise ValueError("embedding_size must be one of 4, 8, 16, 32, 64 on the native path")
+        self.layers = [int(x) for x in deep_layers]
+        self.keep = [float(x) for x in keep_probs]
+        self.l2 = float(l2_reg)
+        self.comm = comm
+        self.world = comm.world_size if comm is not None else 1
+        self.rank = comm.rank if comm is not None else 0
+        self.lr = float(learning_rate) * self.world          # HVD:149
+        self.optimizer = optimizer
+        self.opt_id = KN.OPT_IDS[optimizer]
+        self.loss_type = loss_type
+        self.sparse_update = sparse_update
+        self.seed = int(seed)
+        self.device = torch.device(device)
+        self.sharded = comm is not None and comm.sharded
+        # local rows of the embedding tables (row-sharded: id -> rank id % N, row id // N)
+        self.R = (self.V + self.world - 1) // self.world if self.sharded else self.V
+        self.row_div = self.world if self.sharded else 1
+        self.end_bit = max(1, int(math.ceil(math.log2(max(2, self.V)))))
+
+        # ---- dense parameter layout (flat fp32 buffer = one all-reduce bucket) ----
+        F, K = self.F, self.K
+        self.d0 = F * K
+        self.K0p = pad32(self.d0)
+        self.Np = [pad32(L) for L in self.layers]
+        self.Kp = [self.K0p] + self.Np[:-1]
+        segs: List[DenseSeg] = []
+        off = 0
+
+        def add(name, shape, tf_shape):
+            nonlocal off
+            segs.append(DenseSeg(name, off, shape, tf_shape))
+            off = _align(off + int(torch.Size(shape).numel()))
+        add("fm_bias", (1,), (1,))
+        din = self.d0
+        for i, L in enumerate(self.layers):
+            add(f"Deep-part/mlp{i}/weights", (self.Np[i], self.Kp[i]), (din, L))
+            add(f"Deep-part/mlp{i}/biases", (self.Np[i],), (L,))
+            din = L
+        add("Deep-part/deep_out/weights", (self.Np[-1],), (din, 1))
+        add("Deep-part/deep_out/biases", (1,), (1,))
+        self.dense_segs: "OrderedDict[str, DenseSeg]" = OrderedDict((s.name, s) for s in segs)
+        self.P = off
+
+        dev = self.device
+        f32 = dict(dtype=torch.float32, device=dev)
+        self.tv = torch.zeros(self.R, K, **f32)
+        self.tw = torch.zeros(self.R, **f32)
+        self.p = torch.zeros(self.P, **f32)
+        self.g = torch.zeros(self.P, **f32)
+        self.step = torch.zeros(1, dtype=torch.int64, device=dev)
+        self._alloc_slots()
+        if self.sparse_update == "tf1_dense":
+            self.Gv = torch.zeros(self.R, K, **f32)
+            self.Gw = torch.zeros(self.R, **f32)
+        self.W16, self.WT16 = [], []
+        shadow = []
+        for i in range(len(self.layers)):
+            s = self.dense_segs[f"Deep-part/mlp{i}/weights"]
+            w16 = torch.zeros(self.Np[i], self.Kp[i], dtype=torch.bfloat16, device=dev)
+            wt16 = torch.zeros(self.Kp[i], self.Np[i], dtype=torch.bfloat16, device=dev)
+            self.W16.append(w16)
+            self.WT16.append(wt16)
+            shadow.append(ShadowSeg(s.off, self.Np[i], self.Kp[i], w16.data_ptr(), wt16.data_ptr()))
+        self._shadow_dev = KN.struct_array_to_device(shadow, dev)
+        self._nshadow = len(shadow)
+        self.h_sparse = KN.hyper(self.lr, self.l2)
+        self.h_dense = KN.hyper(self.lr, 0.0)
+        self._bufs_M = 0
+        self.batch_size = int(batch_size)
+        if init:
+            if self.V * self.K <= (1 << 24):
+                # small tables: the exact golden initialization (CPU generator, bit-reproducible)
+                self.load_tf_params(init_params(self.V, F, K, self.layers, False, self.seed))
+            else:
+                # huge tables (Criteo-1TB shape): same distributions, generated in place on the
+                # GPU per rank (no host staging, no full-table temporary)
+                self.load_tf_params(init_params(self.V, F, K, self.layers, False, self.seed,
+                                                tables=False))
+                self.init_tables_inplace()
+        self._alloc_step_buffers(self._padM(self.batch_size))
+
+    # ------------------------------------------------------------------ allocation
+    def init_tables_inplace(self):
+        g = torch.Generator(device=self.device)
+        g.manual_seed(self.seed * 7919 + self.rank)
+        with torch.no_grad():
+            for t, shape in ((self.tw, (self.V,)), (self.tv, (self.V, self.K))):
+                std = glorot_std(shape)
+                torch.nn.init.trunc_normal_(t, 0.0, std, -2 * std, 2 * std, generator=g)
+
+    def _alloc_slots(self):
+        f32 = dict(dtype=torch.float32, device=self.device)
+        R, K, P = self.R, self.K, self.P
+        z = lambda *s: torch.zeros(*s, **f32)
+        e = torch.empty(0, **f32)
+        o = self.optimizer
+        if o == "Adam":
+            self.sv = [z(R, K), z(R, K), z(R), z(R)]
+            self.sd = [z(P), z(P)]
+        elif o == "Adagrad":
+            self.sv = [torch.full((R, K), 1e-8, **f32), e, torch.full((R,), 1e-8, **f32), e]
+            self.sd = [torch.full((P,), 1e-8, **f32), e]
+        elif o == "Momentum":
+            self.sv = [z(R, K), e, z(R), e]
+            self.sd = [z(P), e]
+        elif o == "ftrl":
+            self.sv = [torch.full((R, K), 0.1, **f32), z(R, K), torch.full((R,), 0.1, **f32), z(R)]
+            self.sd = [torch.full((P,), 0.1, **f32), z(P)]
+        else:  # GD
+            self.sv = [e, e, e, e]
+            self.sd = [e, e]
+
+    @staticmethod
+    def _padM(B: int) -> int:
+        return max(128, (B + 127) // 128 * 128)
+
+    def _alloc_step_buffers(self, M: int):
+        """Per-step activations/gradients for a (padded) batch of M rows."""
+        if M <= self._bufs_M:
+            return
+        dev = self.device
+        F, K, K0p = self.F, self.K, self.K0p
+        bf = dict(dtype=torch.bfloat16, device=dev)
+        f32 = dict(dtype=torch.float32, device=dev)
+        i32 = dict(dtype=torch.int32, device=dev)
+        self.M = M
+        self.idx = torch.zeros(M * F, **i32)
+        self.vals = torch.zeros(M * F, **f32)
+        self.labels = torch.zeros(M, **f32)
+        self.y_fm = torch.zeros(M, **f32)
+        self.S = torch.zeros(M, K, **f32)
+        self.E = torch.zeros(M, K0p, **bf)
+        self.Et = torch.zeros(K0p, M, **bf)
+        self.H = [torch.zeros(M, n, **bf) for n in self.Np]
+        self.Ht = [torch.zeros(n, M, **bf) for n in self.Np]
+        self.dZ = [torch.zeros(M, n, **bf) for n in self.Np]
+        self.dZt = [torch.zeros(n, M, **bf) for n in self.Np]
+        self.dX0 = torch.zeros(M, K0p, **f32)
+        self.prob = torch.zeros(M, **f32)
+        self.dlogit = torch.zeros(M, **f32)
+        self.nhead = (M + 255) // 256
+        self.partial = torch.zeros(self.nhead, self.Np[-1] + 2, **f32)
+        self.loss_sum = torch.zeros(1, **f32)
+        # wgrad split-K configuration + slabs
+        self.wg_cfg = []
+        for i in range(len(self.layers)):
+            Mg, Ng, Kd = self.Np[i], self.Kp[i], M
+            t = _pick_tile(Mg, Ng)
+            s = _pick_splitk(Mg, Ng, Kd, t)
+            self.wg_cfg.append((t, s))
+        self.slabs = [torch.zeros(s, self.Np[i], self.Kp[i], **f32) for i, (t, s) in enumerate(self.wg_cfg)]
+        # sparse path
+        n = M * F
+        gr = KN.grad_row_floats(K)
+        self.sorted_keys = torch.zeros(n, **i32)
+        self.perm = torch.zeros(n, **i32)
+        self.iota_tmp = torch.zeros(n, **i32)
+        self.G = torch.zeros(n, gr, **f32)
+        self.UG = torch.zeros(n, gr, **f32)
+        self.ukeys = torch.zeros(n, **i32)
+        self.num_u = torch.zeros(1, **i32)
+        tb = max(KN.sort_temp_bytes(n, self.end_bit), KN.rbk_temp_bytes(K, n), KN.scan_temp_bytes(n))
+        self.temp = torch.zeros(tb + 256, dtype=torch.uint8, device=dev)
+        self._build_finalize_jobs()
+        self._bufs_M = M
+        self._graph = None
+
+    def _build_finalize_jobs(self):
+        jobs = []
+        maxn = 1
+        for i in range(len(self.layers)):
+            s = self.dense_segs[f"Deep-part/mlp{i}/weights"]
+            n = self.Np[i] * self.Kp[i]
+            nsl = self.wg_cfg[i][1]
+            jobs.append(SlabJob(self.g.data_ptr() + 4 * s.off, self.slabs[i].data_ptr(), n, nsl, n,
+                                self.Kp[i], self.Kp[i], 1.0))
+            maxn = max(maxn, n)
+        Lp = self.Np[-1]
+        pw = self.partial.data_ptr()
+        so = self.dense_segs["Deep-part/deep_out/weights"].off
+        sb = self.dense_segs["Deep-part/deep_out/biases"].off
+        sf = self.dense_segs["fm_bias"].off
+        g0 = self.g.data_ptr()
+        jobs.append(SlabJob(g0 + 4 * so, pw, Lp, self.nhead, Lp + 2, Lp, Lp, 1.0))
+        jobs.append(SlabJob(g0 + 4 * sb, pw + 4 * Lp, 1, self.nhead, Lp + 2, 1, 1, 1.0))
+        jobs.append(SlabJob(g0 + 4 * sf, pw + 4 * Lp, 1, self.nhead, Lp + 2, 1, 1, 1.0))
+        jobs.append(SlabJob(self.loss_sum.data_ptr(), pw + 4 * (Lp + 1), 1, self.nhead, Lp + 2, 1, 1, 1.0))
+        self._slab_jobs = KN.struct_array_to_device(jobs, self.device)
+        self._nslab_jobs = len(jobs)
+        self._slab_maxn = maxn
+        rj = []
+        for i in range(len(self.layers)):
+            sbias = self.dense_segs[f"Deep-part/mlp{i}/biases"].off
+            rj.append(RowSumJob(g0 + 4 * sbias, self.dZt[i].data_ptr(), self.Np[i], self.M, self.M))
+        self._row_jobs = KN.struct_array_to_device(rj, self.device)
+        self._nrow_jobs = len(rj)
+        self._row_total = sum(self.Np)
+
+    # ------------------------------------------------------------------ parameters
+    def load_tf_params(self, params: Dict[str, torch.Tensor]):
+        """Load TF-named / TF-layout parameters (reference §2.7.4) into the native buffers."""
+        with torch.no_grad():
+            fw, fv = params.get("fm_w"), params.get("fm_v")
+            if fw is None:
+                pass
+            elif self.sharded:
+                r, N = self.rank, self.world
+                self.tw.zero_()
+                self.tv.zero_()
+                loc_w = fw[r::N].to(self.device, torch.float32)
+                loc_v = fv[r::N].to(self.device, torch.float32)
+                self.tw[: loc_w.shape[0]].copy_(loc_w)
+                self.tv[: loc_v.shape[0]].copy_(loc_v)
+            else:
+                self.tw.copy_(fw.to(self.device, torch.float32))
+                self.tv.copy_(fv.to(self.device, torch.float32))
+            self.p.zero_()
+            for name, s in self.dense_segs.items():
+                if name not in params:
+                    continue
+                self._dense_view(self.p, s).copy_(self._tf_to_native(name, params[name]).to(self.device))
+        self.refresh_shadows()
+
+    def _dense_view(self, flat: torch.Tensor, s: DenseSeg) -> torch.Tensor:
+        n = int(torch.Size(s.shape).numel())
+        return flat[s.off: s.off + n].view(s.shape)
+
+    def _tf_to_native(self, name: str, t: torch.Tensor) -> torch.Tensor:
+        s = self.dense_segs[name]
+        t = t.detach().float().cpu()
+        out = torch.zeros(s.shape, dtype=torch.float32)
+        if name.endswith("/weights") and "deep_out" not in name:
+            din, L = t.shape
+            out[:L, :din] = t.t()
+        elif "deep_out/weights" in name:
+            out[: t.shape[0]] = t.reshape(-1)
+        else:
+            out[: t.numel()] = t.reshape(-1)
+        return out
+
+    def _native_to_tf(self, name: str, flat: torch.Tensor) -> torch.Tensor:
+        s = self.dense_segs[name]
+        v = self._dense_view(flat, s).detach().float().cpu()
+        if name.endswith("/weights") and "deep_out" not in name:
+            din, L = s.tf_shape
+            return v[:L, :din].t().contiguous()
+        n = int(torch.Size(s.tf_shape).numel())
+        return v.reshape(-1)[:n].reshape(s.tf_shape).clone()
+
+    def dense_tf_params(self, flat: Optional[torch.Tensor] = None) -> "OrderedDict[str, torch.Tensor]":
+        flat = self.p if flat is None else flat
+        return OrderedDict((n, self._native_to_tf(n, flat)) for n in self.dense_segs)
+
+    def refresh_shadows(self):
+        KN.shadow_refresh(self.p, self.P, self._shadow_dev, self._nshadow)
+
+    # ------------------------------------------------------------------ batch staging
+    def stage_batch(self, ids: torch.Tensor, vals: torch.Tensor, labels: Optional[torch.Tensor]):
+        """Copy a batch into the static input buffers (device->device when already resident)."""
+        B = ids.shape[0]
+        M = self._padM(B)
+        if M > self._bufs_M:
+            self._alloc_step_buffers(M)
+        n = B * self.F
+        self.idx[:n].copy_(ids.reshape(-1), non_blocking=True)
+        self.vals[:n].copy_(vals.reshape(-1), non_blocking=True)
+        if n < self.idx.numel():
+            self.idx[n:].zero_()
+            self.vals[n:].zero_()
+        if labels is not None:
+            self.labels[:B].copy_(labels.reshape(-1), non_blocking=True)
+        return B
+
+    # ------------------------------------------------------------------ forward pieces
+    def _forward(self, B: int, train: bool):
+        M, F, K = self.M, self.F, self.K
+        idx = self.idx
+        tv, tw = self.tv, self.tw
+        if self.sharded:
+            idx, tv, tw = self.comm.sharded_forward_gather(self, B)
+        fm_bias = self.p[self.dense_segs["fm_bias"].off:]
+        KN.fm_fwd(idx, self.vals, tv, tw, fm_bias, M, F, K, self.K0p, self.y_fm, self.S, self.E,
+                  self.Et if train else None)
+        X = self.E
+        for i in range(len(self.layers)):
+            s = self.dense_segs[f"Deep-part/mlp{i}/biases"]
+            keep = self.keep[i]
+            drop = train and keep < 1.0
+            ep = EpiArgs()
+            ep.bias = self.p.data_ptr() + 4 * s.off
+            ep.scale = (1.0 / keep) if drop else 1.0
+            ep.seed = self.seed & 0xFFFFFFFF
+            ep.layer = i
+            ep.keep_thr = min(keep_threshold(keep), 0xFFFFFFFF)
+            ep.drop = 1 if drop else 0
+            ep.step = self.step.data_ptr()
+            ep.out = self.H[i].data_ptr()
+            ep.out_t = self.Ht[i].data_ptr() if train else 0
+            N = self.Np[i]
+            KN.gemm_nt(KN.EPI_FWD if train else KN.EPI_FWD_EVAL, _pick_tile(M, N), X, self.Kp[i],
+                       self.W16[i], self.Kp[i], M, N, self.Kp[i], 1, ep)
+            X = self.H[i]
+        return idx, tv
+
+    def _head(self, B: int, train: bool, with_labels: bool = True):
+        a = HeadArgs()
+        a.h = self.H[-1].data_ptr()
+        a.w_out = self.p.data_ptr() + 4 * self.dense_segs["Deep-part/deep_out/weights"].off
+        a.b_out = self.p.data_ptr() + 4 * self.dense_segs["Deep-part/deep_out/biases"].off
+        a.y_fm = self.y_fm.data_ptr()
+        a.labels = self.labels.data_ptr() if with_labels else 0
+        a.M, a.L, a.nvalid = self.M, self.Np[-1], B
+        a.square_loss = 1 if self.loss_type == "square_loss" else 0
+        a.train = 1 if train else 0
+        a.gscale = 1.0 / (B * self.world)
+        keep = self.keep[-1]
+        a.scale_l = (1.0 / keep) if keep < 1.0 else 1.0
+        a.prob = self.prob.data_ptr()
+        a.logit = 0
+        a.dlogit = self.dlogit.data_ptr()
+        a.dz = self.dZ[-1].data_ptr()
+        a.dz_t = self.dZt[-1].data_ptr()
+        a.partial = self.partial.data_ptr()
+        KN.head(a)
+
+    # ------------------------------------------------------------------ backward pieces
+    def _mlp_backward(self):
+        M = self.M
+        for i in reversed(range(len(self.layers))):
+            Xt = self.Et if i == 0 else self.Ht[i - 1]
+            t, s = self.wg_cfg[i]
+            ep = EpiArgs()
+            ep.out = self.slabs[i].data_ptr()
+            KN.gemm_nt(KN.EPI_F32, t, self.dZt[i], M, Xt, M, self.Np[i], self.Kp[i], M, s, ep)
+            ep = EpiArgs()
+            if i > 0:
+                keep = self.keep[i - 1]
+                ep.hprev = self.H[i - 1].data_ptr()
+                ep.scale = (1.0 / keep) if keep < 1.0 else 1.0
+                ep.out = self.dZ[i - 1].data_ptr()
+                ep.out_t = self.dZt[i - 1].data_ptr()
+                N = self.Np[i - 1]
+                KN.gemm_nt(KN.EPI_DGRAD, _pick_tile(M, N), self.dZ[i], self.Np[i], self.WT16[i],
+                           self.Np[i], M, N, self.Np[i], 1, ep)
+            else:
+                ep.out = self.dX0.data_ptr()
+                KN.gemm_nt(KN.EPI_F32, _pick_tile(M, self.K0p), self.dZ[0], self.Np[0],
+                           self.WT16[0], self.Np[0], M, self.K0p, self.Np[0], 1, ep)
+        KN.slab_reduce(self._slab_jobs, self._nslab_jobs, self._slab_maxn)
+        KN.rowsum(self._row_jobs, self._nrow_jobs, self._row_total)
+
+    def _sparse_backward(self, B: int, idx, tv):
+        """Sorted per-slot gradients -> unique-row gradients (ukeys, UG, num_u)."""
+        n = B * self.F
+        if self.sharded:
+            return self.comm.sharded_backward(self, B, idx, tv)
+        KN.sort_ids(self.idx, self.sorted_keys, self.iota_tmp, self.perm, n, self.end_bit, self.temp)
+        KN.fm_bwd_sorted(self.perm, idx, self.vals, tv, self.dlogit, self.dX0, self.S, n, self.F,
+                         self.K, self.K0p, self.G)
+        KN.reduce_by_key(self.K, self.sorted_keys, self.G, self.ukeys, self.UG, self.num_u, n, self.temp)
+        if self.comm is not None and self.world > 1:
+            return self.comm.replicated_exchange(self, n)
+        return self.ukeys, self.UG, self.num_u, n
+
+    def _sparse_update(self, ukeys, UG, num, max_n):
+        if self.sparse_update == "lazy":
+            KN.sparse_rows_update(self.K, self.opt_id, ukeys, UG, num, max_n, self.row_div, self.tv,
+                                  self.tw, self.sv, self.h_sparse, self.step)
+        else:
+            KN.scatter_rows(self.K, ukeys, UG, num, max_n, self.row_div, self.Gv, self.Gw)
+            KN.dense_sweep(self.K, self.opt_id, self.R, self.tv, self.tw, self.Gv, self.Gw, self.sv,
+                           self.h_sparse, self.step)
+
+    # ------------------------------------------------------------------ public step API
+    def train_step_enqueue(self, B: int):
+        """Enqueue one full training step on the current stream (no host sync)."""
+        idx, tv = self._forward(B, train=True)
+        self._head(B, train=True)
+        self._mlp_backward()
+        work = None
+        if self.comm is not None and self.world > 1:
+            work = self.comm.allreduce_dense_async(self.g)
+        ukeys, UG, num, max_n = self._sparse_backward(B, idx, tv)
+        self._sparse_update(ukeys, UG, num, max_n)
+        if work is not None:
+            self.comm.wait(work)
+        KN.dense_opt(self.opt_id, self.p, self.g, self.sd[0], self.sd[1], self.P, self.h_dense,
+                     self.step, self._shadow_dev, self._nshadow)
+        KN.step_inc(self.step)
+
+    def train_step(self, ids, vals, labels, use_graph: bool = False):
+        B = self.stage_batch(ids, vals, labels)
+        if use_graph and (self.comm is None or self.comm.graph_safe):
+            self._replay_graph(B)
+        else:
+            self.train_step_enqueue(B)
+        return B
+
+    def _replay_graph(self, B: int):
+        if self._graph is None or self._graph_B != B:
+            # The first step of a batch shape runs eagerly (it is a real step: it also warms up
+            # hipCUB/RCCL lazy init), then the step is captured (capture records, it does not
+            # execute) and every later step is one graph replay.
+            self.train_step_enqueue(B)
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self.train_step_enqueue(B)
+            self._graph, self._graph_B = g, B
+            return
+        self._graph.replay()
+
+    def loss_value(self, B: int, include_l2: bool = False) -> float:
+        """Mean data loss of the last step (+ l2 terms over the whole tables if asked)."""
+        v = float(self.loss_sum.item()) / B
+        if include_l2:
+            v += self.l2_value()
+        return v
+
+    def l2_value(self) -> float:
+        s = KN.sumsq(self.tv) + KN.sumsq(self.tw)
+        if self.comm is not None and self.sharded and self.world > 1:
+            s = self.comm.allreduce_scalar(s)
+        return float(self.l2 * 0.5 * s)
+
+    def predict_enqueue(self, B: int, with_labels: bool = False):
+        self._forward(B, train=False)
+        self._head(B, train=False, with_labels=with_labels)
+
+    def predict(self, ids, vals) -> torch.Tensor:
+        B = self.stage_batch(ids, vals, None)
+        self.predict_enqueue(B, with_labels=False)
+        return self.prob[:B].clone()
+
+    def eval_batch(self, ids, vals, labels, hist: torch.Tensor):
+        """Forward + accumulate the 200-threshold AUC histogram and the loss sum."""
+        B = self.stage_batch(ids, vals, labels)
+        self.predict_enqueue(B, with_labels=True)
+        KN.auc_hist(self.prob, self.labels, B, hist)
+        return B
+
+    # ------------------------------------------------------------------ state export
+    def global_step(self) -> int:
+        return int(self.step.item())
+
+    def sparse_tables_tf(self):
+        """fm_w / fm_v of THIS rank (full tables when replicated; local rows when sharded)."""
+        return self.tw, self.tv

@@ -1,0 +1,142 @@
+"""ctypes binding of ``_lib/libhipfm_kernels.so`` (the gfx950 HIP kernels, csrc/kernels).
+
+The library is loaded AFTER ``import torch`` so its ``libamdhip64.so.7`` dependency resolves to
+the HIP runtime torch already loaded (same SONAME) — device pointers and ``hipStream_t``
+handles from torch are then valid in our kernels, and launches on torch's current stream are
+captured by ``torch.cuda.CUDAGraph`` like any torch op.
+
+There is no silent fallback: on a GPU run, a missing library raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+import torch
+
+from .build import KERNELS_SO
+
+_lock = threading.Lock()
+_lib = None
+
+c_int, c_long, c_float, c_void_p, c_uint32 = C.c_int, C.c_long, C.c_float, C.c_void_p, C.c_uint32
+c_size_t = C.c_size_t
+
+
+class OptHyper(C.Structure):
+    _fields_ = [("lr", c_float), ("l2", c_float), ("b1", c_float), ("b2", c_float),
+                ("eps", c_float), ("momentum", c_float)]
+
+
+class EpiArgs(C.Structure):
+    _fields_ = [("bias", c_void_p), ("hprev", c_void_p), ("scale", c_float), ("seed", c_uint32),
+                ("layer", c_uint32), ("keep_thr", c_uint32), ("drop", c_int), ("step", c_void_p),
+                ("out", c_void_p), ("out_t", c_void_p)]
+
+
+class HeadArgs(C.Structure):
+    _fields_ = [("h", c_void_p), ("w_out", c_void_p), ("b_out", c_void_p), ("y_fm", c_void_p),
+                ("labels", c_void_p), ("M", c_int), ("L", c_int), ("nvalid", c_int),
+                ("square_loss", c_int), ("train", c_int), ("gscale", c_float), ("scale_l", c_float),
+                ("prob", c_void_p), ("logit", c_void_p), ("dlogit", c_void_p), ("dz", c_void_p),
+                ("dz_t", c_void_p), ("partial", c_void_p)]
+
+
+class SlabJob(C.Structure):
+    _fields_ = [("dst", c_void_p), ("src", c_void_p), ("n", c_long), ("nslab", c_int),
+                ("stride", c_long), ("src_ld", c_long), ("cols", c_int), ("scale", c_float)]
+
+
+class RowSumJob(C.Structure):
+    _fields_ = [("dst", c_void_p), ("src", c_void_p), ("rows", c_int), ("n", c_int), ("ld", c_long)]
+
+
+class ShadowSeg(C.Structure):
+    _fields_ = [("off", c_long), ("rows", c_int), ("cols", c_int), ("w16", c_void_p),
+                ("wt16", c_void_p)]
+
+
+_SIGS = {
+    "hfm_fm_fwd": [c_void_p] * 5 + [c_int] * 4 + [c_void_p] * 4 + [c_void_p],
+    "hfm_fm_bwd_sorted": [c_void_p] * 7 + [c_int] * 4 + [c_void_p, c_void_p],
+    "hfm_grad_row_bytes": [c_int],
+    "hfm_sort_pairs_temp_bytes": [c_int, c_int, C.POINTER(c_size_t)],
+    "hfm_sort_ids": [c_void_p] * 4 + [c_int, c_int, c_void_p, c_size_t, c_void_p],
+    "hfm_reduce_by_key_temp_bytes": [c_int, c_int, C.POINTER(c_size_t)],
+    "hfm_reduce_by_key": [c_int] + [c_void_p] * 5 + [c_int, c_void_p, c_size_t, c_void_p],
+    "hfm_scan_temp_bytes": [c_int, C.POINTER(c_size_t)],
+    "hfm_unique_inverse": [c_void_p, c_void_p, c_int] + [c_void_p] * 6 + [c_size_t, c_void_p],
+    "hfm_owner_keys": [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p],
+    "hfm_gather_i32": [c_void_p, c_void_p, c_int, c_void_p, c_void_p],
+    "hfm_sparse_rows_update": [c_int, c_int] + [c_void_p] * 3 + [c_int, c_int] + [c_void_p] * 6
+                              + [C.POINTER(OptHyper), c_void_p, c_void_p],
+    "hfm_scatter_rows": [c_int] + [c_void_p] * 3 + [c_int, c_int, c_void_p, c_void_p, c_void_p],
+    "hfm_dense_sweep": [c_int, c_int, c_long] + [c_void_p] * 8 + [C.POINTER(OptHyper), c_void_p, c_void_p],
+    "hfm_dense_opt": [c_int] + [c_void_p] * 4 + [c_long, C.POINTER(OptHyper), c_void_p, c_void_p, c_int, c_void_p],
+    "hfm_shadow_refresh": [c_void_p, c_long, c_void_p, c_int, c_void_p],
+    "hfm_step_inc": [c_void_p, c_void_p],
+    "hfm_shadow_seg_bytes": [],
+    "hfm_opt_hyper_bytes": [],
+    "hfm_gemm_nt": [c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int,
+                    C.POINTER(EpiArgs), c_void_p],
+    "hfm_epi_args_bytes": [],
+    "hfm_head": [C.POINTER(HeadArgs), c_void_p],
+    "hfm_head_args_bytes": [],
+    "hfm_slab_reduce": [c_void_p, c_int, c_int, c_void_p],
+    "hfm_slab_job_bytes": [],
+    "hfm_rowsum": [c_void_p, c_int, c_int, c_void_p],
+    "hfm_rowsum_job_bytes": [],
+    "hfm_auc_hist": [c_void_p, c_void_p, c_int, c_void_p, c_void_p],
+    "hfm_sumsq_partials": [c_void_p, c_long, c_void_p, c_int, c_void_p],
+}
+
+
+def lib_path() -> str:
+    return os.environ.get("HIPFM_KERNELS_SO", KERNELS_SO)
+
+
+def available() -> bool:
+    return os.path.exists(lib_path())
+
+
+def get_lib():
+    """Load (once) and return the kernel library; raises if it was not built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        p = lib_path()
+        if not os.path.exists(p):
+            raise RuntimeError(f"hipfm kernel library not found at {p}; build it with "
+                               "`python -m hipfm.ops.build` (or __graft_entry__.build())")
+        lib = C.CDLL(p, mode=C.RTLD_GLOBAL)
+        for name, args in _SIGS.items():
+            fn = getattr(lib, name)
+            fn.argtypes = args
+            fn.restype = c_int
+        # ABI checks: ctypes struct layouts must match the C structs
+        for cname, pys in (("hfm_epi_args_bytes", EpiArgs), ("hfm_head_args_bytes", HeadArgs),
+                           ("hfm_slab_job_bytes", SlabJob), ("hfm_rowsum_job_bytes", RowSumJob),
+                           ("hfm_shadow_seg_bytes", ShadowSeg), ("hfm_opt_hyper_bytes", OptHyper)):
+            n = getattr(lib, cname)()
+            if n != C.sizeof(pys):
+                raise RuntimeError(f"ABI mismatch {pys.__name__}: C {n} vs ctypes {C.sizeof(pys)}")
+        _lib = lib
+        return _lib
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        raise RuntimeError(f"hipfm kernel call {what} failed with hipError {rc}")
+
+
+def stream_handle(stream=None) -> int:
+    s = torch.cuda.current_stream() if stream is None else stream
+    return s.cuda_stream
+
+
+def ptr(t) -> int:
+    return 0 if t is None else t.data_ptr()

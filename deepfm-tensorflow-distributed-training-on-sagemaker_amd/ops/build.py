@@ -1,0 +1,107 @@
+"""In-tree build of the native libraries (no JIT cache, no pip install).
+
+* ``_lib/libhipfm_kernels.so`` — every ``csrc/kernels/*.hip`` compiled by ``hipcc
+  --offload-arch=gfx950`` (cross-compiles without a GPU), C ABI, bound with ctypes.
+* ``_lib/libhipfm_io.so``      — ``csrc/io/*.cpp`` (TFRecord framing + CRC32C, tf.train.Example
+  decoder, libsvm parser, threaded batch loader), host-only C++17.
+
+Objects are rebuilt only when a source or header is newer than the object.
+Usage: ``python -m hipfm.ops.build [--force]``.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import glob
+import os
+import shutil
+import subprocess
+import sys
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REPO = os.path.dirname(PKG_DIR)
+CSRC = os.path.join(REPO, "csrc")
+LIB_DIR = os.path.join(PKG_DIR, "_lib")
+BUILD_DIR = os.path.join(REPO, "build", "obj")
+ARCH = os.environ.get("HIPFM_ARCH", "gfx950")
+
+KERNELS_SO = os.path.join(LIB_DIR, "libhipfm_kernels.so")
+IO_SO = os.path.join(LIB_DIR, "libhipfm_io.so")
+
+
+def _hipcc() -> str:
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if c and os.path.exists(c):
+            return c
+    raise RuntimeError("hipcc not found (ROCm required to build hipfm kernels)")
+
+
+def _newer(src_files, target) -> bool:
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(s) > t for s in src_files)
+
+
+def _run(cmd):
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("build failed:\n" + " ".join(cmd) + "\n" + r.stdout)
+    return r.stdout
+
+
+def build_kernels(force: bool = False, jobs: int = 8, verbose: bool = False) -> str:
+    srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
+    hdrs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.h")))
+    os.makedirs(BUILD_DIR, exist_ok=True)
+    os.makedirs(LIB_DIR, exist_ok=True)
+    hipcc = _hipcc()
+    objs = []
+    todo = []
+    for s in srcs:
+        o = os.path.join(BUILD_DIR, os.path.basename(s) + ".o")
+        objs.append(o)
+        if force or _newer([s] + hdrs, o):
+            todo.append((s, o))
+
+    def comp(so):
+        s, o = so
+        cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17",
+               "-fvisibility=hidden", "-Wno-unused-result", "-c", s, "-o", o]
+        out = _run(cmd)
+        if verbose and out.strip():
+            print(out)
+        return o
+
+    if todo:
+        with cf.ThreadPoolExecutor(max_workers=max(1, min(jobs, len(todo)))) as ex:
+            list(ex.map(comp, todo))
+    if force or todo or _newer(objs, KERNELS_SO):
+        tmp = KERNELS_SO + ".tmp"
+        _run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs)
+        os.replace(tmp, KERNELS_SO)
+    return KERNELS_SO
+
+
+def build_io(force: bool = False, verbose: bool = False) -> str:
+    srcs = sorted(glob.glob(os.path.join(CSRC, "io", "*.cpp")))
+    hdrs = sorted(glob.glob(os.path.join(CSRC, "io", "*.h")))
+    if not srcs:
+        return ""
+    os.makedirs(LIB_DIR, exist_ok=True)
+    if force or _newer(srcs + hdrs, IO_SO):
+        cxx = os.environ.get("CXX", "g++")
+        tmp = IO_SO + ".tmp"
+        out = _run([cxx, "-O3", "-std=c++17", "-fPIC", "-shared", "-msse4.2", "-pthread",
+                    "-fvisibility=hidden", "-o", tmp] + srcs)
+        if verbose and out.strip():
+            print(out)
+        os.replace(tmp, IO_SO)
+    return IO_SO
+
+
+def build_all(force: bool = False, verbose: bool = False):
+    return build_kernels(force, verbose=verbose), build_io(force, verbose=verbose)
+
+
+if __name__ == "__main__":
+    print(build_all(force="--force" in sys.argv, verbose=True))

@@ -1,0 +1,152 @@
+"""Thin typed wrappers over the kernel library (one function per C entry point).
+
+All wrappers launch on torch's current HIP stream and never synchronize, so sequences of
+them can be captured into a HIP graph (``torch.cuda.CUDAGraph``).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import List, Optional, Sequence
+
+import torch
+
+from . import _lib
+from ._lib import (EpiArgs, HeadArgs, OptHyper, RowSumJob, ShadowSeg, SlabJob, check, ptr,
+                   stream_handle)
+
+EPI_F32, EPI_FWD, EPI_DGRAD, EPI_FWD_EVAL = 0, 1, 2, 3
+OPT_IDS = {"Adam": 0, "Adagrad": 1, "Momentum": 2, "ftrl": 3, "GD": 4}
+
+# tile ids of hfm_gemm_nt: (rows per block, cols per block)
+TILES = {0: (64, 64), 1: (128, 32), 2: (32, 128), 3: (32, 32), 4: (32, 64)}
+
+
+def L():
+    return _lib.get_lib()
+
+
+def fm_fwd(idx, vals, tv, tw, bias, B, F, K, KP, y_fm, S, E, Et):
+    check(L().hfm_fm_fwd(ptr(idx), ptr(vals), ptr(tv), ptr(tw), ptr(bias), B, F, K, KP, ptr(y_fm),
+                         ptr(S), ptr(E), ptr(Et), stream_handle()), "fm_fwd")
+
+
+def fm_bwd_sorted(perm, idx, vals, tv, dlogit, dX0, S, n, F, K, KP, G):
+    check(L().hfm_fm_bwd_sorted(ptr(perm), ptr(idx), ptr(vals), ptr(tv), ptr(dlogit), ptr(dX0),
+                                ptr(S), n, F, K, KP, ptr(G), stream_handle()), "fm_bwd_sorted")
+
+
+def grad_row_floats(K: int) -> int:
+    return K + 4
+
+
+def sort_temp_bytes(n: int, end_bit: int) -> int:
+    b = C.c_size_t(0)
+    check(L().hfm_sort_pairs_temp_bytes(n, end_bit, C.byref(b)), "sort_temp")
+    return b.value
+
+
+def rbk_temp_bytes(K: int, n: int) -> int:
+    b = C.c_size_t(0)
+    check(L().hfm_reduce_by_key_temp_bytes(K, n, C.byref(b)), "rbk_temp")
+    return b.value
+
+
+def scan_temp_bytes(n: int) -> int:
+    b = C.c_size_t(0)
+    check(L().hfm_scan_temp_bytes(n, C.byref(b)), "scan_temp")
+    return b.value
+
+
+def sort_ids(keys_in, keys_out, vals_tmp, perm_out, n, end_bit, temp):
+    check(L().hfm_sort_ids(ptr(keys_in), ptr(keys_out), ptr(vals_tmp), ptr(perm_out), n, end_bit,
+                           ptr(temp), temp.numel(), stream_handle()), "sort_ids")
+
+
+def reduce_by_key(K, sorted_keys, G, ukeys, UG, num, n, temp):
+    check(L().hfm_reduce_by_key(K, ptr(sorted_keys), ptr(G), ptr(ukeys), ptr(UG), ptr(num), n,
+                                ptr(temp), temp.numel(), stream_handle()), "reduce_by_key")
+
+
+def unique_inverse(sorted_keys, perm, n, flags_tmp, seg_tmp, uniq, inverse, num, temp):
+    check(L().hfm_unique_inverse(ptr(sorted_keys), ptr(perm), n, ptr(flags_tmp), ptr(seg_tmp),
+                                 ptr(uniq), ptr(inverse), ptr(num), ptr(temp), temp.numel(),
+                                 stream_handle()), "unique_inverse")
+
+
+def gather_i32(src, perm, n, out):
+    check(L().hfm_gather_i32(ptr(src), ptr(perm), n, ptr(out), stream_handle()), "gather_i32")
+
+
+def hyper(lr: float, l2: float, b1=0.9, b2=0.999, eps=1e-8, momentum=0.95) -> OptHyper:
+    return OptHyper(lr, l2, b1, b2, eps, momentum)
+
+
+def sparse_rows_update(K, opt, ukeys, UG, num, max_n, row_div, tv, tw, slots, h: OptHyper, step):
+    s0v, s1v, s0w, s1w = slots
+    check(L().hfm_sparse_rows_update(K, opt, ptr(ukeys), ptr(UG), ptr(num), max_n, row_div, ptr(tv),
+                                     ptr(tw), ptr(s0v), ptr(s1v), ptr(s0w), ptr(s1w), C.byref(h),
+                                     ptr(step), stream_handle()), "sparse_rows_update")
+
+
+def scatter_rows(K, ukeys, UG, num, max_n, row_div, Gv, Gw):
+    check(L().hfm_scatter_rows(K, ptr(ukeys), ptr(UG), ptr(num), max_n, row_div, ptr(Gv), ptr(Gw),
+                               stream_handle()), "scatter_rows")
+
+
+def dense_sweep(K, opt, R, tv, tw, Gv, Gw, slots, h: OptHyper, step):
+    s0v, s1v, s0w, s1w = slots
+    check(L().hfm_dense_sweep(K, opt, R, ptr(tv), ptr(tw), ptr(Gv), ptr(Gw), ptr(s0v), ptr(s1v),
+                              ptr(s0w), ptr(s1w), C.byref(h), ptr(step), stream_handle()),
+          "dense_sweep")
+
+
+def dense_opt(opt, p, g, s0, s1, n, h: OptHyper, step, segs_dev, nseg):
+    check(L().hfm_dense_opt(opt, ptr(p), ptr(g), ptr(s0), ptr(s1), n, C.byref(h), ptr(step),
+                            ptr(segs_dev), nseg, stream_handle()), "dense_opt")
+
+
+def shadow_refresh(p, n, segs_dev, nseg):
+    check(L().hfm_shadow_refresh(ptr(p), n, ptr(segs_dev), nseg, stream_handle()), "shadow_refresh")
+
+
+def step_inc(step):
+    check(L().hfm_step_inc(ptr(step), stream_handle()), "step_inc")
+
+
+def gemm_nt(epi, tile, A, lda, B, ldb, M, N, Kd, splitk, ep: EpiArgs):
+    check(L().hfm_gemm_nt(epi, tile, ptr(A), lda, ptr(B), ldb, M, N, Kd, splitk, C.byref(ep),
+                          stream_handle()), f"gemm_nt(epi={epi},tile={tile},M={M},N={N},K={Kd})")
+
+
+def head(a: HeadArgs):
+    check(L().hfm_head(C.byref(a), stream_handle()), "head")
+
+
+def slab_reduce(jobs_dev, njobs, max_n):
+    check(L().hfm_slab_reduce(ptr(jobs_dev), njobs, max_n, stream_handle()), "slab_reduce")
+
+
+def rowsum(jobs_dev, njobs, total_rows):
+    check(L().hfm_rowsum(ptr(jobs_dev), njobs, total_rows, stream_handle()), "rowsum")
+
+
+def auc_hist(pred, label, n, hist):
+    check(L().hfm_auc_hist(ptr(pred), ptr(label), n, ptr(hist), stream_handle()), "auc_hist")
+
+
+def sumsq(x: torch.Tensor, nblocks: int = 512) -> torch.Tensor:
+    out = torch.empty(nblocks, dtype=torch.float64, device=x.device)
+    check(L().hfm_sumsq_partials(ptr(x), x.numel(), ptr(out), nblocks, stream_handle()), "sumsq")
+    return out.sum()
+
+
+def struct_array_to_device(structs: Sequence[C.Structure], device) -> torch.Tensor:
+    """Pack ctypes structs into a device byte tensor (job tables, shadow segment lists)."""
+    if not structs:
+        return torch.zeros(16, dtype=torch.uint8, device=device)
+    sz = C.sizeof(structs[0])
+    buf = (C.c_uint8 * (sz * len(structs)))()
+    for i, s in enumerate(structs):
+        C.memmove(C.addressof(buf) + i * sz, C.addressof(s), sz)
+    host = torch.frombuffer(bytearray(buf), dtype=torch.uint8)
+    return host.to(device)
