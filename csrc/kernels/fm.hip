@@ -19,17 +19,31 @@ __global__ void __launch_bounds__(256) fm_fwd_kernel(
     const int* __restrict__ idx, const float* __restrict__ vals, const float* __restrict__ tv,
     const float* __restrict__ tw, const float* __restrict__ bias, int B, int F, int KP,
     float* __restrict__ y_fm, float* __restrict__ S, bf16* __restrict__ E, bf16* __restrict__ Et) {
-  constexpr int LPS = K / 4;  // lanes per sample
-  const int gt = blockIdx.x * blockDim.x + threadIdx.x;
-  const int b = gt / LPS;
-  const int sub = gt % LPS;
+  constexpr int LPS = K / 4;       // lanes per sample
+  constexpr int SB = 256 / LPS;    // samples per workgroup
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  int* lidx = reinterpret_cast<int*>(smem);
+  float* lval = reinterpret_cast<float*>(smem) + SB * F;
+  // stage the workgroup's [SB, F] ids / values with coalesced loads, so every row gather of
+  // the field loop below is independent of a preceding global load
+  const int s0 = blockIdx.x * SB;
+  const int cnt = min(SB, B - s0) * F;
+  const size_t base = (size_t)s0 * F;
+  for (int t = threadIdx.x; t < cnt; t += 256) {
+    lidx[t] = idx[base + t];
+    lval[t] = vals[base + t];
+  }
+  __syncthreads();
+  const int ls = threadIdx.x / LPS;
+  const int sub = threadIdx.x % LPS;
+  const int b = s0 + ls;
   if (b >= B) return;
   f32x4 s = {0.f, 0.f, 0.f, 0.f}, q = {0.f, 0.f, 0.f, 0.f};
   float yw = 0.f;
-  const int* ib = idx + (size_t)b * F;
-  const float* xb = vals + (size_t)b * F;
+  const int* ib = lidx + ls * F;
+  const float* xb = lval + ls * F;
   bf16* eb = E + (size_t)b * KP + sub * 4;
-#pragma unroll 4
+#pragma unroll 8
   for (int f = 0; f < F; ++f) {
     const int id = ib[f];
     const float x = xb[f];
@@ -98,9 +112,10 @@ static int launch_fm_fwd(const int* idx, const float* vals, const float* tv, con
                          const float* bias, int B, int F, int KP, float* y_fm, float* S, bf16* E,
                          bf16* Et, hipStream_t st) {
   constexpr int LPS = K / 4;
-  const long threads = (long)B * LPS;
-  const int grid = (int)((threads + 255) / 256);
-  hipLaunchKernelGGL(fm_fwd_kernel<K>, dim3(grid), dim3(256), 0, st, idx, vals, tv, tw, bias, B,
+  constexpr int SB = 256 / LPS;
+  const int grid = (B + SB - 1) / SB;
+  const size_t lds = (size_t)SB * F * 8;
+  hipLaunchKernelGGL(fm_fwd_kernel<K>, dim3(grid), dim3(256), lds, st, idx, vals, tv, tw, bias, B,
                      F, KP, y_fm, S, E, Et);
   HFM_LAUNCH_CHECK();
 }

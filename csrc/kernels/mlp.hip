@@ -113,7 +113,8 @@ static int launch_gemm(const bf16* A, int lda, const bf16* B, int ldb, int M, in
   HFM_LAUNCH_CHECK();
 }
 
-// tile: 0 = 64x64 (2x2 waves), 1 = 128x32 (4x1), 2 = 32x128 (1x4), 3 = 32x32 (1x1), 4 = 32x64 (1x2)
+// tile: 0 = 64x64 (2x2 waves), 1 = 128x32 (4x1), 2 = 32x128 (1x4), 3 = 32x32 (1x1), 4 = 32x64 (1x2),
+//       5 = 32x160 (1x5), 6 = 32x320 (1x10), 7 = 32x256 (1x8)
 template <int EPI>
 static int gemm_tile(int tile, const bf16* A, int lda, const bf16* B, int ldb, int M, int N, int Kd,
                      int splitk, const EpiArgs& ep, hipStream_t st) {
@@ -123,6 +124,9 @@ static int gemm_tile(int tile, const bf16* A, int lda, const bf16* B, int ldb, i
     case 2: return launch_gemm<1, 4, EPI>(A, lda, B, ldb, M, N, Kd, splitk, ep, st);
     case 3: return launch_gemm<1, 1, EPI>(A, lda, B, ldb, M, N, Kd, splitk, ep, st);
     case 4: return launch_gemm<1, 2, EPI>(A, lda, B, ldb, M, N, Kd, splitk, ep, st);
+    case 5: return launch_gemm<1, 5, EPI>(A, lda, B, ldb, M, N, Kd, splitk, ep, st);
+    case 6: return launch_gemm<1, 10, EPI>(A, lda, B, ldb, M, N, Kd, splitk, ep, st);
+    case 7: return launch_gemm<1, 8, EPI>(A, lda, B, ldb, M, N, Kd, splitk, ep, st);
     default: return (int)hipErrorInvalidValue;
   }
 }
@@ -166,28 +170,41 @@ struct HeadArgs {
   float* partial;       // [gridDim.x, L + 2]
 };
 
+// 4 lanes per sample (each owns L/4 hidden columns): 64 samples per 256-thread workgroup, so a
+// 16K batch is 256 workgroups (one per CU) instead of 64.
 template <int L>
 __global__ void __launch_bounds__(256) head_kernel(HeadArgs a) {
-  __shared__ float red[256];
-  const int b = blockIdx.x * 256 + threadIdx.x;
-  float hv[L];
+  constexpr int Q = L / 4;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int b = blockIdx.x * 64 + (tid >> 2), q = tid & 3;
+  float hv[Q];
   float dl = 0.f, lossb = 0.f;
+  const bool inb = b < a.M;
   const bool valid = b < a.nvalid;
-  if (b < a.M) {
-    const bf16* hr = a.h + (size_t)b * L;
+  float yd = 0.f;
+  if (inb) {
+    const bf16* hr = a.h + (size_t)b * L + q * Q;
 #pragma unroll
-    for (int j = 0; j < L; j += 8) {
+    for (int j = 0; j < Q; j += 8) {
       const bf16x8 v = *reinterpret_cast<const bf16x8*>(hr + j);
 #pragma unroll
       for (int t = 0; t < 8; ++t) hv[j + t] = bf2f(v[t]);
     }
-    float yd = a.b_out[0];
 #pragma unroll
-    for (int j = 0; j < L; ++j) yd += hv[j] * a.w_out[j];
-    const float y = a.y_fm[b] + yd;
+    for (int j = 0; j < Q; ++j) yd += hv[j] * a.w_out[q * Q + j];
+  } else {
+#pragma unroll
+    for (int j = 0; j < Q; ++j) hv[j] = 0.f;
+  }
+  yd += __shfl_xor(yd, 1, 64);
+  yd += __shfl_xor(yd, 2, 64);
+  if (inb) {
+    const float y = a.y_fm[b] + yd + a.b_out[0];
     const float p = 1.f / (1.f + __expf(-y));
-    a.prob[b] = p;
-    if (a.logit) a.logit[b] = y;
+    if (q == 0) {
+      a.prob[b] = p;
+      if (a.logit) a.logit[b] = y;
+    }
     if (a.labels && valid) {
       const float lab = a.labels[b];
       if (a.square_loss) {
@@ -199,45 +216,56 @@ __global__ void __launch_bounds__(256) head_kernel(HeadArgs a) {
       }
     }
     if (a.train) {
-      a.dlogit[b] = dl;
-      bf16* dzr = a.dz + (size_t)b * L;
+      if (q == 0) a.dlogit[b] = dl;
+      bf16* dzr = a.dz + (size_t)b * L + q * Q;
 #pragma unroll
-      for (int j = 0; j < L; ++j) {
-        const float g = hv[j] > 0.f ? dl * a.w_out[j] * a.scale_l : 0.f;
-        const bf16 gh = f2bf(g);
-        dzr[j] = gh;
-        a.dz_t[(size_t)j * a.M + b] = gh;
+      for (int j = 0; j < Q; j += 8) {
+        bf16x8 pk;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+          const int col = q * Q + j + t;
+          const float g = hv[j + t] > 0.f ? dl * a.w_out[col] * a.scale_l : 0.f;
+          pk[t] = f2bf(g);
+          a.dz_t[(size_t)col * a.M + b] = pk[t];
+        }
+        *reinterpret_cast<bf16x8*>(dzr + j) = pk;
       }
     }
-  } else {
+  }
+  // block partials [sum dl*h (L) | sum dl | sum loss]: butterflies over the 16 lanes of a wave
+  // that share q, then the 4 waves in order through LDS (deterministic).
+  __shared__ float wsum[4][L + 2];
 #pragma unroll
-    for (int j = 0; j < L; ++j) hv[j] = 0.f;
+  for (int j = 0; j < Q; ++j) {
+    float v = a.train ? dl * hv[j] : 0.f;
+    v += __shfl_xor(v, 4, 64);
+    v += __shfl_xor(v, 8, 64);
+    v += __shfl_xor(v, 16, 64);
+    v += __shfl_xor(v, 32, 64);
+    if (lane < 4) wsum[wv][lane * Q + j] = v;   // lane == q here
   }
-  // deterministic block reductions: L + 2 sums
+  float v0 = (q == 0) ? dl : 0.f, v1 = (q == 0) ? lossb : 0.f;
+#pragma unroll
+  for (int o = 4; o < 64; o <<= 1) {
+    v0 += __shfl_xor(v0, o, 64);
+    v1 += __shfl_xor(v1, o, 64);
+  }
+  if (lane == 0) {
+    wsum[wv][L] = v0;
+    wsum[wv][L + 1] = v1;
+  }
+  __syncthreads();
   float* part = a.partial + (size_t)blockIdx.x * (L + 2);
-  for (int q = 0; q < L + 2; ++q) {
-    float v;
-    if (q < L) v = a.train ? dl * hv[q] : 0.f;
-    else if (q == L) v = dl;
-    else v = lossb;
-    red[threadIdx.x] = v;
-    __syncthreads();
-    for (int s = 128; s > 0; s >>= 1) {
-      if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
-      __syncthreads();
-    }
-    if (threadIdx.x == 0) part[q] = red[0];
-    __syncthreads();
-  }
+  for (int c = tid; c < L + 2; c += blockDim.x)
+    part[c] = ((wsum[0][c] + wsum[1][c]) + wsum[2][c]) + wsum[3][c];
 }
 
 HFM_API int hfm_head(const HeadArgs* a, hipStream_t st) {
-  const int grid = (a->M + 255) / 256;
+  const int grid = (a->M + 63) / 64;
   switch (a->L) {
-    case 32: hipLaunchKernelGGL(head_kernel<32>, dim3(grid), dim3(256), 0, st, *a); break;
-    case 64: hipLaunchKernelGGL(head_kernel<64>, dim3(grid), dim3(256), 0, st, *a); break;
-    case 96: hipLaunchKernelGGL(head_kernel<96>, dim3(grid), dim3(256), 0, st, *a); break;
-    case 128: hipLaunchKernelGGL(head_kernel<128>, dim3(grid), dim3(256), 0, st, *a); break;
+#define HL(LL) case LL: hipLaunchKernelGGL(head_kernel<LL>, dim3(grid), dim3(256), 0, st, *a); break;
+    HL(32) HL(64) HL(96) HL(128) HL(160) HL(192) HL(224) HL(256)
+#undef HL
     default: return (int)hipErrorInvalidValue;
   }
   HFM_LAUNCH_CHECK();
@@ -258,20 +286,39 @@ struct SlabJob {
   float scale;
 };
 
-__global__ void slab_reduce_kernel(const SlabJob* __restrict__ jobs, int njobs) {
-  const SlabJob j = jobs[blockIdx.y];
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < j.n; i += (long)gridDim.x * blockDim.x) {
-    const long r = i / j.cols, c = i % j.cols;
-    const long so = r * j.src_ld + c;
+// blockIdx.y = job.  A workgroup owns 32 consecutive output elements; its 8 slab-lanes per
+// element each sum a strided subset of the slabs, then the 8 partials are added in a fixed
+// order through LDS (deterministic).  Parallel over both outputs and slabs, so a job with 41K
+// outputs x 32 slabs (layer-1 wgrad) and one with 32 outputs x 256 slabs (head partials) are
+// both short.
+__global__ void __launch_bounds__(256) slab_reduce_kernel(const SlabJob* __restrict__ jobs, int njobs) {
+  __shared__ float red[8][33];
+  const SlabJob& jr = jobs[blockIdx.y];
+  const int n = (int)jr.n, nslab = jr.nslab, stride = (int)jr.stride, cols = jr.cols, ld = (int)jr.src_ld;
+  const float* src = jr.src;
+  const int e = threadIdx.x & 31, zl = threadIdx.x >> 5;
+  for (int i0 = blockIdx.x * 32; i0 < n; i0 += gridDim.x * 32) {
+    const int i = i0 + e;
     float s = 0.f;
-    for (int z = 0; z < j.nslab; ++z) s += j.src[so + (long)z * j.stride];
-    j.dst[i] = s * j.scale;
+    if (i < n) {
+      const int r = i / cols, c = i - r * cols;
+      const float* sp = src + r * ld + c;
+      for (int z = zl; z < nslab; z += 8) s += sp[z * stride];
+    }
+    red[zl][e] = s;
+    __syncthreads();
+    if (zl == 0 && i < n) {
+      float t = ((red[0][e] + red[1][e]) + (red[2][e] + red[3][e])) +
+                ((red[4][e] + red[5][e]) + (red[6][e] + red[7][e]));
+      jr.dst[i] = t * jr.scale;
+    }
+    __syncthreads();
   }
 }
 
 HFM_API int hfm_slab_reduce(const void* jobs, int njobs, int max_n, hipStream_t st) {
-  int gx = (max_n + 255) / 256;
-  if (gx > 1024) gx = 1024;
+  int gx = (max_n + 31) / 32;
+  if (gx > 2048) gx = 2048;
   if (gx < 1) gx = 1;
   hipLaunchKernelGGL(slab_reduce_kernel, dim3(gx, njobs), dim3(256), 0, st, (const SlabJob*)jobs, njobs);
   HFM_LAUNCH_CHECK();

@@ -32,7 +32,7 @@ from typing import Dict, List, Optional
 import torch
 
 from ..ops import kernels as KN
-from ..ops._lib import EpiArgs, HeadArgs, RowSumJob, ShadowSeg, SlabJob
+from ..ops._lib import EpiArgs, HeadArgs, RowSumJob, SegApplyArgs, ShadowSeg, SlabJob
 from ..utils.rng import keep_threshold
 from .reference import glorot_std, init_params, pad32
 
@@ -41,7 +41,21 @@ def _align(n: int, a: int = 64) -> int:
     return (n + a - 1) // a * a
 
 
-def _pick_tile(M: int, N: int) -> int:
+def _pick_tile(M: int, N: int, row_major_stream: bool = True) -> int:
+    """Tile for an NT GEMM.  Activation GEMMs (M = batch) take the widest column tile that
+    covers N in one workgroup row, so the big A operand (E, H, dZ) is streamed exactly once."""
+    if row_major_stream and M % 32 == 0:
+        for t, w in ((3, 32), (4, 64), (2, 128), (5, 160), (7, 256), (6, 320)):
+            if N == w:
+                return t
+        if N % 320 == 0:
+            return 6
+        if N % 256 == 0:
+            return 7
+        if N % 160 == 0:
+            return 5
+        if N % 128 == 0:
+            return 2
     if M % 64 == 0 and N % 64 == 0:
         return 0
     if N == 32 and M % 128 == 0:
@@ -53,11 +67,14 @@ def _pick_tile(M: int, N: int) -> int:
     return 3
 
 
-def _pick_splitk(M: int, N: int, Kd: int, tile: int, target_blocks: int = 512) -> int:
+def _pick_splitk(M: int, N: int, Kd: int, tile: int, target_blocks: int = 512,
+                 max_split: int = 32) -> int:
+    """Split the batch reduction of a weight-gradient GEMM: enough workgroups to fill the
+    256 CUs, but few enough slabs that the finalize pass stays a short, coalesced read."""
     bm, bn = KN.TILES[tile]
     tiles = (M // bm) * (N // bn)
     ksteps = Kd // 32
-    want = max(1, min(ksteps, target_blocks // max(1, tiles)))
+    want = max(1, min(ksteps, max_split, target_blocks // max(1, tiles)))
     for s in range(want, 0, -1):
         if ksteps % s == 0:
             return s
@@ -79,7 +96,8 @@ class NativeDeepFM:
                  deep_layers=(256, 128, 64), keep_probs=(0.5, 0.5, 0.5), l2_reg: float = 1e-4,
                  learning_rate: float = 5e-4, optimizer: str = "Adam", loss_type: str = "log_loss",
                  sparse_update: str = "tf1_dense", seed: int = 1234, batch_size: int = 1024,
-                 device="cuda", comm=None, init: bool = True, batch_norm: bool = False):
+                 device="cuda", comm=None, init: bool = True, batch_norm: bool = False,
+                 adam_epsilon: float = 1e-8, adagrad_init: float = 1e-8):
         if batch_norm:
             raise NotImplementedError("batch_norm on the native path is not implemented yet; "
                                       "use --device cpu (golden path) for batch_norm runs")
@@ -94,6 +112,7 @@ class NativeDeepFM:
         self.rank = comm.rank if comm is not None else 0
         self.lr = float(learning_rate) * self.world          # HVD:149
         self.optimizer = optimizer
+        self.adagrad_init = float(adagrad_init)
         self.opt_id = KN.OPT_IDS[optimizer]
         self.loss_type = loss_type
         self.sparse_update = sparse_update
@@ -151,8 +170,8 @@ class NativeDeepFM:
             shadow.append(ShadowSeg(s.off, self.Np[i], self.Kp[i], w16.data_ptr(), wt16.data_ptr()))
         self._shadow_dev = KN.struct_array_to_device(shadow, dev)
         self._nshadow = len(shadow)
-        self.h_sparse = KN.hyper(self.lr, self.l2)
-        self.h_dense = KN.hyper(self.lr, 0.0)
+        self.h_sparse = KN.hyper(self.lr, self.l2, eps=adam_epsilon)
+        self.h_dense = KN.hyper(self.lr, 0.0, eps=adam_epsilon)
         self._bufs_M = 0
         self.batch_size = int(batch_size)
         if init:
@@ -186,8 +205,9 @@ class NativeDeepFM:
             self.sv = [z(R, K), z(R, K), z(R), z(R)]
             self.sd = [z(P), z(P)]
         elif o == "Adagrad":
-            self.sv = [torch.full((R, K), 1e-8, **f32), e, torch.full((R,), 1e-8, **f32), e]
-            self.sd = [torch.full((P,), 1e-8, **f32), e]
+            a0 = self.adagrad_init
+            self.sv = [torch.full((R, K), a0, **f32), e, torch.full((R,), a0, **f32), e]
+            self.sd = [torch.full((P,), a0, **f32), e]
         elif o == "Momentum":
             self.sv = [z(R, K), e, z(R), e]
             self.sd = [z(P), e]
@@ -226,14 +246,14 @@ class NativeDeepFM:
         self.dX0 = torch.zeros(M, K0p, **f32)
         self.prob = torch.zeros(M, **f32)
         self.dlogit = torch.zeros(M, **f32)
-        self.nhead = (M + 255) // 256
+        self.nhead = (M + 63) // 64      # head kernel: 64 samples per workgroup
         self.partial = torch.zeros(self.nhead, self.Np[-1] + 2, **f32)
         self.loss_sum = torch.zeros(1, **f32)
         # wgrad split-K configuration + slabs
         self.wg_cfg = []
         for i in range(len(self.layers)):
             Mg, Ng, Kd = self.Np[i], self.Kp[i], M
-            t = _pick_tile(Mg, Ng)
+            t = _pick_tile(Mg, Ng, row_major_stream=False)
             s = _pick_splitk(Mg, Ng, Kd, t)
             self.wg_cfg.append((t, s))
         self.slabs = [torch.zeros(s, self.Np[i], self.Kp[i], **f32) for i, (t, s) in enumerate(self.wg_cfg)]
@@ -242,12 +262,15 @@ class NativeDeepFM:
         gr = KN.grad_row_floats(K)
         self.sorted_keys = torch.zeros(n, **i32)
         self.perm = torch.zeros(n, **i32)
-        self.iota_tmp = torch.zeros(n, **i32)
-        self.G = torch.zeros(n, gr, **f32)
+        self.G = torch.zeros(n, gr, **f32)          # per-unique partial sums (fused backward)
         self.UG = torch.zeros(n, gr, **f32)
+        self.cont = torch.zeros(KN.seg_tiles(K, n) + 1, gr, **f32)
         self.ukeys = torch.zeros(n, **i32)
         self.num_u = torch.zeros(1, **i32)
-        tb = max(KN.sort_temp_bytes(n, self.end_bit), KN.rbk_temp_bytes(K, n), KN.scan_temp_bytes(n))
+        self.seg_flags = torch.zeros(n, **i32)
+        self.sid_incl = torch.zeros(n, **i32)
+        self.seg_start = torch.zeros(n + 1, **i32)
+        tb = max(KN.radix_temp_bytes(n), KN.rbk_temp_bytes(K, n), KN.scan_temp_bytes(n))
         self.temp = torch.zeros(tb + 256, dtype=torch.uint8, device=dev)
         self._build_finalize_jobs()
         self._bufs_M = M
@@ -437,18 +460,60 @@ class NativeDeepFM:
         KN.slab_reduce(self._slab_jobs, self._nslab_jobs, self._slab_maxn)
         KN.rowsum(self._row_jobs, self._nrow_jobs, self._row_total)
 
+    def seg_args(self, n: int, compact: bool, vsrc=None, vsrc_compact: bool = False) -> SegApplyArgs:
+        A = SegApplyArgs()
+        A.sorted_keys = self.sorted_keys.data_ptr()
+        A.ukeys = self.ukeys.data_ptr()
+        A.seg_start = self.seg_start.data_ptr()
+        A.num = self.num_u.data_ptr()
+        A.n = n
+        A.ntiles = KN.seg_tiles(self.K, n)
+        A.compact = 1 if compact else 0
+        A.row_div = self.row_div
+        A.vsrc_compact = 1 if vsrc_compact else 0
+        A.vsrc = 0 if vsrc is None else vsrc.data_ptr()
+        A.partial = self.G.data_ptr()
+        A.cont = self.cont.data_ptr()
+        A.UG = self.UG.data_ptr()
+        A.tv, A.tw = self.tv.data_ptr(), self.tw.data_ptr()
+        A.s0v, A.s1v, A.s0w, A.s1w = (t.data_ptr() if t.numel() else 0 for t in self.sv)
+        if self.sparse_update == "tf1_dense":
+            A.Gv, A.Gw = self.Gv.data_ptr(), self.Gw.data_ptr()
+        A.h = self.h_sparse
+        A.step = self.step.data_ptr()
+        return A
+
     def _sparse_backward(self, B: int, idx, tv):
-        """Sorted per-slot gradients -> unique-row gradients (ukeys, UG, num_u)."""
+        """Embedding backward.  Single rank: the row update is fused into the reduction
+        (returns None).  Multi-rank: returns compact unique-row gradients for the exchange."""
         n = B * self.F
         if self.sharded:
             return self.comm.sharded_backward(self, B, idx, tv)
-        KN.sort_ids(self.idx, self.sorted_keys, self.iota_tmp, self.perm, n, self.end_bit, self.temp)
-        KN.fm_bwd_sorted(self.perm, idx, self.vals, tv, self.dlogit, self.dX0, self.S, n, self.F,
-                         self.K, self.K0p, self.G)
-        KN.reduce_by_key(self.K, self.sorted_keys, self.G, self.ukeys, self.UG, self.num_u, n, self.temp)
-        if self.comm is not None and self.world > 1:
-            return self.comm.replicated_exchange(self, n)
-        return self.ukeys, self.UG, self.num_u, n
+        KN.sort_ids(self.idx, self.sorted_keys, None, self.perm, n, self.end_bit, self.temp)
+        if self.comm is None or self.world == 1:
+            self._segment_reduce(n, compact=False)
+            A = self.seg_args(n, compact=False)
+            if self.sparse_update == "lazy":
+                KN.seg_apply(self.K, KN.SEG_LAZY, self.opt_id, A, n)
+            else:
+                KN.seg_apply(self.K, KN.SEG_SCATTER, 0, A, n)
+                KN.dense_sweep(self.K, self.opt_id, self.R, self.tv, self.tw, self.Gv, self.Gw,
+                               self.sv, self.h_sparse, self.step)
+            return None
+        self._segment_reduce(n, compact=True)
+        KN.seg_apply(self.K, KN.SEG_WRITE_UG, 0, self.seg_args(n, compact=True), n)
+        return self.comm.replicated_exchange(self, n)
+
+    def _segment_reduce(self, n: int, compact: bool):
+        """Per-slot gradients + per-tile run sums (K2+K3).  compact: partials indexed by the
+        unique index (needs the segment structure), else by head position."""
+        sid = None
+        if compact:
+            KN.segments(self.sorted_keys, n, self.seg_flags, self.sid_incl, self.ukeys,
+                        self.seg_start, self.num_u, self.temp)
+            sid = self.sid_incl
+        KN.fm_bwd_seg(self.K, self.sorted_keys, self.perm, sid, self.vals, self.dlogit, self.dX0,
+                      self.S, n, self.F, self.K0p, self.G, self.cont)
 
     def _sparse_update(self, ukeys, UG, num, max_n):
         if self.sparse_update == "lazy":
@@ -468,13 +533,30 @@ class NativeDeepFM:
         work = None
         if self.comm is not None and self.world > 1:
             work = self.comm.allreduce_dense_async(self.g)
-        ukeys, UG, num, max_n = self._sparse_backward(B, idx, tv)
-        self._sparse_update(ukeys, UG, num, max_n)
+        out = self._sparse_backward(B, idx, tv)
+        if out is not None:
+            self._sparse_update(*out)
         if work is not None:
             self.comm.wait(work)
         KN.dense_opt(self.opt_id, self.p, self.g, self.sd[0], self.sd[1], self.P, self.h_dense,
                      self.step, self._shadow_dev, self._nshadow)
         KN.step_inc(self.step)
+
+    def compute_grads(self, ids, vals, labels):
+        """Forward + backward WITHOUT any update (tests / debugging): returns the flat dense
+        gradient and the compact unique-row embedding gradients (ukeys, UG, U)."""
+        if self.sharded:
+            raise NotImplementedError("compute_grads is single-rank / replicated only")
+        B = self.stage_batch(ids, vals, labels)
+        idx, tv = self._forward(B, train=True)
+        self._head(B, train=True)
+        self._mlp_backward()
+        n = B * self.F
+        KN.sort_ids(self.idx, self.sorted_keys, None, self.perm, n, self.end_bit, self.temp)
+        self._segment_reduce(n, compact=True)
+        KN.seg_apply(self.K, KN.SEG_WRITE_UG, 0, self.seg_args(n, compact=True), n)
+        U = int(self.num_u.item())
+        return self.g.clone(), self.ukeys[:U].clone(), self.UG[:U].clone()
 
     def train_step(self, ids, vals, labels, use_graph: bool = False):
         B = self.stage_batch(ids, vals, labels)

@@ -128,7 +128,10 @@ class GoldenDeepFM:
                  batch_norm_decay: float = 0.9, l2_reg: float = 1e-4, learning_rate: float = 5e-4,
                  optimizer: str = "Adam", loss_type: str = "log_loss",
                  sparse_update: str = "tf1_dense", seed: int = 1234, world_size: int = 1,
-                 device="cpu", params: Optional[Dict[str, torch.Tensor]] = None):
+                 device="cpu", params: Optional[Dict[str, torch.Tensor]] = None,
+                 adam_epsilon: float = 1e-8, adagrad_init: float = 1e-8):
+        self.adam_eps = float(adam_epsilon)      # TF AdamOptimizer epsilon (HVD:253)
+        self.adagrad_init = float(adagrad_init)  # initial_accumulator_value (HVD:255)
         self.V, self.F, self.K = int(feature_size), int(field_size), int(embedding_size)
         self.layers = [int(x) for x in deep_layers]
         self.keep = [float(x) for x in keep_probs]
@@ -161,7 +164,7 @@ class GoldenDeepFM:
                 self.slots[f"{name}/Adam"] = torch.zeros_like(p)
                 self.slots[f"{name}/Adam_1"] = torch.zeros_like(p)
             elif self.optimizer == "Adagrad":
-                self.slots[f"{name}/Adagrad"] = torch.full_like(p, 1e-8)  # HVD:255
+                self.slots[f"{name}/Adagrad"] = torch.full_like(p, self.adagrad_init)  # HVD:255
             elif self.optimizer == "Momentum":
                 self.slots[f"{name}/Momentum"] = torch.zeros_like(p)
             elif self.optimizer == "ftrl":
@@ -250,7 +253,7 @@ class GoldenDeepFM:
         lr = self.lr
         opt = self.optimizer
         if opt == "Adam":
-            b1, b2, eps = 0.9, 0.999, 1e-8
+            b1, b2, eps = 0.9, 0.999, self.adam_eps
             b1p, b2p = self.slots["beta1_power"], self.slots["beta2_power"]
             lr_t = lr * torch.sqrt(1 - b2p) / (1 - b1p)
         for name, g in grads.items():

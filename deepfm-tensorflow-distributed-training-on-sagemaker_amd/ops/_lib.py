@@ -57,6 +57,16 @@ class ShadowSeg(C.Structure):
                 ("wt16", c_void_p)]
 
 
+class SegApplyArgs(C.Structure):
+    _fields_ = [("sorted_keys", c_void_p), ("ukeys", c_void_p), ("seg_start", c_void_p),
+                ("num", c_void_p), ("n", c_int), ("ntiles", c_int), ("compact", c_int),
+                ("row_div", c_int), ("vsrc_compact", c_int), ("vsrc", c_void_p),
+                ("partial", c_void_p), ("cont", c_void_p), ("UG", c_void_p), ("tv", c_void_p),
+                ("tw", c_void_p), ("s0v", c_void_p), ("s1v", c_void_p), ("s0w", c_void_p),
+                ("s1w", c_void_p), ("Gv", c_void_p), ("Gw", c_void_p), ("h", OptHyper),
+                ("step", c_void_p)]
+
+
 _SIGS = {
     "hfm_fm_fwd": [c_void_p] * 5 + [c_int] * 4 + [c_void_p] * 4 + [c_void_p],
     "hfm_fm_bwd_sorted": [c_void_p] * 7 + [c_int] * 4 + [c_void_p, c_void_p],
@@ -89,6 +99,13 @@ _SIGS = {
     "hfm_rowsum_job_bytes": [],
     "hfm_auc_hist": [c_void_p, c_void_p, c_int, c_void_p, c_void_p],
     "hfm_sumsq_partials": [c_void_p, c_long, c_void_p, c_int, c_void_p],
+    "hfm_seg_tiles": [c_int, c_int],
+    "hfm_radix_sort_temp_bytes": [c_int, C.POINTER(c_size_t)],
+    "hfm_radix_sort_ids": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_size_t, c_void_p],
+    "hfm_segments": [c_void_p, c_int] + [c_void_p] * 5 + [c_void_p, c_size_t, c_void_p],
+    "hfm_fm_bwd_seg": [c_int] + [c_void_p] * 7 + [c_int, c_int, c_int, c_void_p, c_void_p, c_void_p],
+    "hfm_seg_apply": [c_int, c_int, c_int, C.POINTER(SegApplyArgs), c_int, c_void_p],
+    "hfm_seg_apply_args_bytes": [],
 }
 
 
@@ -120,7 +137,8 @@ def get_lib():
         # ABI checks: ctypes struct layouts must match the C structs
         for cname, pys in (("hfm_epi_args_bytes", EpiArgs), ("hfm_head_args_bytes", HeadArgs),
                            ("hfm_slab_job_bytes", SlabJob), ("hfm_rowsum_job_bytes", RowSumJob),
-                           ("hfm_shadow_seg_bytes", ShadowSeg), ("hfm_opt_hyper_bytes", OptHyper)):
+                           ("hfm_shadow_seg_bytes", ShadowSeg), ("hfm_opt_hyper_bytes", OptHyper),
+                           ("hfm_seg_apply_args_bytes", SegApplyArgs)):
             n = getattr(lib, cname)()
             if n != C.sizeof(pys):
                 raise RuntimeError(f"ABI mismatch {pys.__name__}: C {n} vs ctypes {C.sizeof(pys)}")

@@ -11,14 +11,15 @@ from typing import List, Optional, Sequence
 import torch
 
 from . import _lib
-from ._lib import (EpiArgs, HeadArgs, OptHyper, RowSumJob, ShadowSeg, SlabJob, check, ptr,
-                   stream_handle)
+from ._lib import (EpiArgs, HeadArgs, OptHyper, RowSumJob, SegApplyArgs, ShadowSeg, SlabJob, check,
+                   ptr, stream_handle)
 
 EPI_F32, EPI_FWD, EPI_DGRAD, EPI_FWD_EVAL = 0, 1, 2, 3
 OPT_IDS = {"Adam": 0, "Adagrad": 1, "Momentum": 2, "ftrl": 3, "GD": 4}
 
 # tile ids of hfm_gemm_nt: (rows per block, cols per block)
-TILES = {0: (64, 64), 1: (128, 32), 2: (32, 128), 3: (32, 32), 4: (32, 64)}
+TILES = {0: (64, 64), 1: (128, 32), 2: (32, 128), 3: (32, 32), 4: (32, 64), 5: (32, 160),
+         6: (32, 320), 7: (32, 256)}
 
 
 def L():
@@ -57,9 +58,23 @@ def scan_temp_bytes(n: int) -> int:
     return b.value
 
 
-def sort_ids(keys_in, keys_out, vals_tmp, perm_out, n, end_bit, temp):
+def radix_temp_bytes(n: int) -> int:
+    b = C.c_size_t(0)
+    check(L().hfm_radix_sort_temp_bytes(n, C.byref(b)), "radix_temp")
+    return b.value
+
+
+def cub_sort_ids(keys_in, keys_out, vals_tmp, perm_out, n, end_bit, temp):
+    """hipCUB SortPairs (reference implementation for tests / A-B timing)."""
     check(L().hfm_sort_ids(ptr(keys_in), ptr(keys_out), ptr(vals_tmp), ptr(perm_out), n, end_bit,
-                           ptr(temp), temp.numel(), stream_handle()), "sort_ids")
+                           ptr(temp), temp.numel(), stream_handle()), "cub_sort_ids")
+
+
+def sort_ids(keys_in, keys_out, vals_tmp, perm_out, n, end_bit, temp):
+    """Stable sort of slot ids -> (sorted keys, slot permutation): csrc/kernels/radix_sort.hip.
+    ``temp`` must hold max(radix_temp_bytes(n), ...) bytes; ``vals_tmp`` is unused."""
+    check(L().hfm_radix_sort_ids(ptr(keys_in), ptr(keys_out), ptr(perm_out), n, end_bit, ptr(temp),
+                                 temp.numel(), stream_handle()), "radix_sort_ids")
 
 
 def reduce_by_key(K, sorted_keys, G, ukeys, UG, num, n, temp):
@@ -75,6 +90,31 @@ def unique_inverse(sorted_keys, perm, n, flags_tmp, seg_tmp, uniq, inverse, num,
 
 def gather_i32(src, perm, n, out):
     check(L().hfm_gather_i32(ptr(src), ptr(perm), n, ptr(out), stream_handle()), "gather_i32")
+
+
+def seg_tiles(K: int, n: int) -> int:
+    return L().hfm_seg_tiles(K, n)
+
+
+def segments(sorted_keys, n, flags_tmp, sid_incl, ukeys, seg_start, num, temp):
+    """Segment structure of a sorted id list: ukeys[U], seg_start[U+1], num=[U] (device)."""
+    check(L().hfm_segments(ptr(sorted_keys), n, ptr(flags_tmp), ptr(sid_incl), ptr(ukeys),
+                           ptr(seg_start), ptr(num), ptr(temp), temp.numel(), stream_handle()),
+          "segments")
+
+
+def fm_bwd_seg(K, sorted_keys, perm, sid_incl, vals, dlogit, dX0, S, n, F, KP, partial, cont):
+    """Per-slot gradients + in-tile run sums.  sid_incl=None -> position-indexed partials."""
+    check(L().hfm_fm_bwd_seg(K, ptr(sorted_keys), ptr(perm), ptr(sid_incl), ptr(vals), ptr(dlogit),
+                             ptr(dX0), ptr(S), n, F, KP, ptr(partial), ptr(cont), stream_handle()),
+          "fm_bwd_seg")
+
+
+SEG_LAZY, SEG_SCATTER, SEG_WRITE_UG = 0, 1, 2
+
+
+def seg_apply(K, mode, opt, args: SegApplyArgs, max_groups):
+    check(L().hfm_seg_apply(K, mode, opt, C.byref(args), max_groups, stream_handle()), "seg_apply")
 
 
 def hyper(lr: float, l2: float, b1=0.9, b2=0.999, eps=1e-8, momentum=0.95) -> OptHyper:

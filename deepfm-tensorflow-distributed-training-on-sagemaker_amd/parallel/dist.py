@@ -111,7 +111,7 @@ class Comm:
             st["seg"] = torch.zeros(m.M * m.F, **i32)
             st["uniq"] = torch.zeros(m.M * m.F, **i32)
             st["M"] = m.M
-        KN.sort_ids(m.idx, m.sorted_keys, m.iota_tmp, m.perm, n, m.end_bit, m.temp)
+        KN.sort_ids(m.idx, m.sorted_keys, None, m.perm, n, m.end_bit, m.temp)
         KN.unique_inverse(m.sorted_keys, m.perm, n, st["flags"], st["seg"], st["uniq"], st["inv"],
                           m.num_u, m.temp)
         U = int(m.num_u.item())                                   # host sync (routing sizes)
@@ -142,8 +142,8 @@ class Comm:
         n = B * m.F
         K = m.K
         gr = KN.grad_row_floats(K)
-        KN.fm_bwd_sorted(m.perm, idx, m.vals, tv, m.dlogit, m.dX0, m.S, n, m.F, K, m.K0p, m.G)
-        KN.reduce_by_key(K, m.sorted_keys, m.G, m.ukeys, m.UG, m.num_u, n, m.temp)
+        m._segment_reduce(n, compact=True)
+        KN.seg_apply(K, KN.SEG_WRITE_UG, 0, m.seg_args(n, compact=True, vsrc=tv, vsrc_compact=True), n)
         U = st["U"]
         send = m.UG[:U].index_select(0, st["order"])
         recv = torch.empty(len(st["recv_ids"]), gr, dtype=torch.float32, device=m.device)
@@ -161,9 +161,9 @@ class Comm:
         sk = torch.empty(R, **i32)
         perm = torch.empty(R, **i32)
         tmp = torch.empty(R, **i32)
-        tb = max(KN.sort_temp_bytes(R, m.end_bit), KN.rbk_temp_bytes(m.K, R))
+        tb = max(KN.radix_temp_bytes(R), KN.rbk_temp_bytes(m.K, R))
         temp = torch.empty(tb + 256, dtype=torch.uint8, device=dev)
-        KN.sort_ids(keys, sk, tmp, perm, R, m.end_bit, temp)
+        KN.sort_ids(keys, sk, None, perm, R, m.end_bit, temp)
         rows_sorted = rows.index_select(0, perm.long())
         uk = torch.empty(R, **i32)
         ug = torch.empty_like(rows_sorted)

@@ -1,0 +1,55 @@
+"""Summarise a rocprofv3 --kernel-trace --stats run into markdown (for profiles/).
+
+usage: python tools/prof_summary.py <prof_dir> <out.md> [title]
+Writes the top kernels by total time and one steady-state training step's kernel timeline
+(the step between two consecutive ``step_inc_kernel`` dispatches).
+"""
+import csv
+import glob
+import os
+import sys
+
+
+def main():
+    d, out = sys.argv[1], sys.argv[2]
+    title = sys.argv[3] if len(sys.argv) > 3 else os.path.basename(d.rstrip("/"))
+    stats = glob.glob(os.path.join(d, "**", "*kernel_stats.csv"), recursive=True)
+    trace = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)
+    lines = [f"# {title}", ""]
+    bench = os.path.join(d, "bench.log")
+    if os.path.exists(bench):
+        js = [l for l in open(bench) if l.startswith("{")]
+        if js:
+            lines += ["bench line (under the profiler):", "", "```", js[-1].strip(), "```", ""]
+    if stats:
+        rows = list(csv.DictReader(open(stats[0])))
+        rows.sort(key=lambda r: -float(r["TotalDurationNs"]))
+        lines += ["## Top kernels (whole run, incl. warm-up / data generation / eval)", "",
+                  "| total us | calls | avg us | % | kernel |", "|---:|---:|---:|---:|---|"]
+        for r in rows[:25]:
+            lines.append(f"| {float(r['TotalDurationNs'])/1e3:.1f} | {r['Calls']} | "
+                         f"{float(r['AverageNs'])/1e3:.2f} | {float(r['Percentage']):.1f} | "
+                         f"`{r['Name'][:90]}` |")
+        lines.append("")
+    if trace:
+        rows = list(csv.DictReader(open(trace[0])))
+        rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+        idx = [i for i, r in enumerate(rows) if r["Kernel_Name"].startswith("step_inc")]
+        if len(idx) >= 3:
+            a, b = idx[len(idx) // 2 - 1], idx[len(idx) // 2]
+            t0 = int(rows[a]["End_Timestamp"])
+            lines += ["## One steady-state training step (graph replay)", "",
+                      "| start us | dur us | kernel |", "|---:|---:|---|"]
+            tot = 0
+            for r in rows[a + 1: b + 1]:
+                s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+                tot += e - s
+                lines.append(f"| {(s - t0)/1e3:.2f} | {(e - s)/1e3:.2f} | `{r['Kernel_Name'][:80]}` |")
+            span = (int(rows[b]["End_Timestamp"]) - t0) / 1e3
+            lines += ["", f"step span {span:.1f} us, sum of kernel durations {tot/1e3:.1f} us", ""]
+    open(out, "w").write("\n".join(lines) + "\n")
+    print(out)
+
+
+if __name__ == "__main__":
+    main()
