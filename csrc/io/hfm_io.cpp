@@ -1,0 +1,645 @@
+// hipfm host I/O runtime.
+//
+// Replaces the TensorFlow C++ input stack the reference relies on:
+//   TFRecordDataset (record framing + CRC)           PS:108, HVD:93          -> TfRecordReader
+//   tf.parse_example with FixedLenFeature schema     PS:79-92, HVD:76-89     -> decode_example
+//   PipeModeDataset (SageMaker FIFO stream)           PS:111, HVD:105         -> same reader on a FIFO
+//   shard / batch(drop_remainder) / prefetch          PS:113-128, HVD:95-128  -> Loader
+// plus the libsvm text format (CONV:15-23, DOC p.42) and a fast TFRecord writer.
+//
+// Loader: W worker threads own files w, w+W, ... (file-level parallelism, each rank reads only
+// its own files — SURVEY Q1), decode records straight into SoA chunks (label f32, ids i64[F],
+// values f32[F]) and hand them over through bounded per-worker queues.  The consumer takes
+// chunks round-robin over the workers (a deterministic interleave, like tf.data's
+// interleave(deterministic=True)), so the batch sequence is reproducible for any thread
+// timing.  Record-level sharding (dataset.shard(n, i), the reference's semantics) uses one
+// sequential worker and keeps records with index % n == i.
+//
+// C ABI, bound with ctypes from hipfm/data/native_io.py.
+#include <nmmintrin.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <atomic>
+#include <condition_variable>
+#include <deque>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#define HFMIO_API extern "C" __attribute__((visibility("default")))
+
+// ------------------------------------------------------------------------------ errors
+static thread_local std::string g_err;
+static void set_err(const std::string& s) { g_err = s; }
+HFMIO_API const char* hfmio_last_error() { return g_err.c_str(); }
+
+// ------------------------------------------------------------------------------ CRC32C
+static uint32_t crc_table[256];
+static bool crc_init = [] {
+  for (uint32_t i = 0; i < 256; ++i) {
+    uint32_t c = i;
+    for (int k = 0; k < 8; ++k) c = (c & 1) ? (c >> 1) ^ 0x82F63B78u : c >> 1;
+    crc_table[i] = c;
+  }
+  return true;
+}();
+
+static bool have_sse42() {
+  static int v = -1;
+  if (v < 0) v = __builtin_cpu_supports("sse4.2") ? 1 : 0;
+  return v == 1;
+}
+
+__attribute__((target("sse4.2"))) static uint32_t crc32c_hw(const uint8_t* p, size_t n, uint32_t crc) {
+  uint64_t c = crc ^ 0xFFFFFFFFu;
+  while (n >= 8) {
+    uint64_t v;
+    memcpy(&v, p, 8);
+    c = _mm_crc32_u64(c, v);
+    p += 8;
+    n -= 8;
+  }
+  uint32_t c32 = (uint32_t)c;
+  while (n--) c32 = _mm_crc32_u8(c32, *p++);
+  return c32 ^ 0xFFFFFFFFu;
+}
+
+static uint32_t crc32c_sw(const uint8_t* p, size_t n, uint32_t crc) {
+  uint32_t c = crc ^ 0xFFFFFFFFu;
+  while (n--) c = crc_table[(c ^ *p++) & 0xFF] ^ (c >> 8);
+  return c ^ 0xFFFFFFFFu;
+}
+
+HFMIO_API uint32_t hfmio_crc32c(const uint8_t* p, size_t n) {
+  return have_sse42() ? crc32c_hw(p, n, 0) : crc32c_sw(p, n, 0);
+}
+static inline uint32_t masked(uint32_t c) { return ((c >> 15) | (c << 17)) + 0xA282EAD8u; }
+HFMIO_API uint32_t hfmio_masked_crc32c(const uint8_t* p, size_t n) { return masked(hfmio_crc32c(p, n)); }
+
+// ------------------------------------------------------------------------------ readers
+class ByteReader {  // buffered sequential reader: files and FIFOs alike (no seeks)
+ public:
+  explicit ByteReader(const std::string& path) : path_(path) {
+    f_ = fopen(path.c_str(), "rb");
+    if (f_) setvbuf(f_, nullptr, _IOFBF, 1 << 22);
+  }
+  ~ByteReader() {
+    if (f_) fclose(f_);
+  }
+  bool ok() const { return f_ != nullptr; }
+  size_t read(void* dst, size_t n) { return fread(dst, 1, n, f_); }
+  // line read for libsvm; returns false at EOF
+  bool getline(std::string& out) {
+    out.clear();
+    int c;
+    while ((c = fgetc(f_)) != EOF) {
+      if (c == '\n') return true;
+      out.push_back((char)c);
+    }
+    return !out.empty();
+  }
+  const std::string& path() const { return path_; }
+
+ private:
+  std::string path_;
+  FILE* f_ = nullptr;
+};
+
+// returns 1 = record, 0 = clean EOF, -1 = error
+static int next_tfrecord(ByteReader& r, std::vector<uint8_t>& buf, bool verify) {
+  uint8_t hdr[12];
+  size_t got = r.read(hdr, 12);
+  if (got == 0) return 0;
+  if (got < 12) {
+    set_err("truncated TFRecord header in " + r.path());
+    return -1;
+  }
+  uint64_t len;
+  memcpy(&len, hdr, 8);
+  uint32_t hcrc;
+  memcpy(&hcrc, hdr + 8, 4);
+  if (verify && hcrc != masked(hfmio_crc32c(hdr, 8))) {
+    set_err("TFRecord length CRC mismatch in " + r.path());
+    return -1;
+  }
+  if (len > (1ull << 31)) {
+    set_err("TFRecord too large in " + r.path());
+    return -1;
+  }
+  buf.resize(len + 4);
+  if (r.read(buf.data(), len + 4) != len + 4) {
+    set_err("truncated TFRecord payload in " + r.path());
+    return -1;
+  }
+  if (verify) {
+    uint32_t dcrc;
+    memcpy(&dcrc, buf.data() + len, 4);
+    if (dcrc != masked(hfmio_crc32c(buf.data(), len))) {
+      set_err("TFRecord data CRC mismatch in " + r.path());
+      return -1;
+    }
+  }
+  buf.resize(len);
+  return 1;
+}
+
+// ------------------------------------------------------------------------------ Example decode
+static inline bool rd_varint(const uint8_t*& p, const uint8_t* e, uint64_t& v) {
+  v = 0;
+  int s = 0;
+  while (p < e) {
+    uint8_t c = *p++;
+    v |= (uint64_t)(c & 0x7F) << s;
+    if (!(c & 0x80)) return true;
+    s += 7;
+    if (s > 63) return false;
+  }
+  return false;
+}
+
+static bool skip_field(const uint8_t*& p, const uint8_t* e, int wt) {
+  uint64_t v;
+  switch (wt) {
+    case 0: return rd_varint(p, e, v);
+    case 1: p += 8; return p <= e;
+    case 2: if (!rd_varint(p, e, v)) return false; p += v; return p <= e;
+    case 5: p += 4; return p <= e;
+    default: return false;
+  }
+}
+
+// decode FloatList / Int64List payload (packed or not) into dst; returns count or -1
+static long decode_list(const uint8_t* p, const uint8_t* e, bool is_float, float* fdst,
+                        int64_t* idst, long cap) {
+  long n = 0;
+  while (p < e) {
+    uint64_t key;
+    if (!rd_varint(p, e, key)) return -1;
+    int f = (int)(key >> 3), wt = (int)(key & 7);
+    if (f != 1) {
+      if (!skip_field(p, e, wt)) return -1;
+      continue;
+    }
+    if (is_float) {
+      if (wt == 2) {
+        uint64_t ln;
+        if (!rd_varint(p, e, ln) || p + ln > e) return -1;
+        long k = (long)(ln / 4);
+        if (n + k > cap) return -2;
+        memcpy(fdst + n, p, k * 4);
+        n += k;
+        p += ln;
+      } else if (wt == 5) {
+        if (n + 1 > cap) return -2;
+        memcpy(fdst + n, p, 4);
+        n++;
+        p += 4;
+      } else return -1;
+    } else {
+      if (wt == 2) {
+        uint64_t ln;
+        if (!rd_varint(p, e, ln) || p + ln > e) return -1;
+        const uint8_t* q = p;
+        const uint8_t* qe = p + ln;
+        while (q < qe) {
+          uint64_t v;
+          if (!rd_varint(q, qe, v)) return -1;
+          if (n + 1 > cap) return -2;
+          idst[n++] = (int64_t)v;
+        }
+        p = qe;
+      } else if (wt == 0) {
+        uint64_t v;
+        if (!rd_varint(p, e, v)) return -1;
+        if (n + 1 > cap) return -2;
+        idst[n++] = (int64_t)v;
+      } else return -1;
+    }
+  }
+  return n;
+}
+
+// Fixed-schema decode of one serialized tf.train.Example (label f32[1], ids i64[F], values f32[F]).
+static bool decode_example(const uint8_t* p, size_t len, int F, float* label, int64_t* ids,
+                           float* vals) {
+  const uint8_t* e = p + len;
+  int have = 0;
+  while (p < e) {
+    uint64_t key;
+    if (!rd_varint(p, e, key)) return false;
+    if ((key >> 3) != 1 || (key & 7) != 2) {
+      if (!skip_field(p, e, key & 7)) return false;
+      continue;
+    }
+    uint64_t ln;
+    if (!rd_varint(p, e, ln) || p + ln > e) return false;
+    const uint8_t* fp = p;           // Features
+    const uint8_t* fe = p + ln;
+    p = fe;
+    while (fp < fe) {
+      uint64_t k2;
+      if (!rd_varint(fp, fe, k2)) return false;
+      if ((k2 >> 3) != 1 || (k2 & 7) != 2) {
+        if (!skip_field(fp, fe, k2 & 7)) return false;
+        continue;
+      }
+      uint64_t l2;
+      if (!rd_varint(fp, fe, l2) || fp + l2 > fe) return false;
+      const uint8_t* mp = fp;        // map entry {key=1, value=2}
+      const uint8_t* me = fp + l2;
+      fp = me;
+      const char* name = nullptr;
+      size_t nlen = 0;
+      const uint8_t* vp = nullptr;
+      const uint8_t* ve = nullptr;
+      while (mp < me) {
+        uint64_t k3;
+        if (!rd_varint(mp, me, k3)) return false;
+        uint64_t l3;
+        if ((k3 & 7) != 2) {
+          if (!skip_field(mp, me, k3 & 7)) return false;
+          continue;
+        }
+        if (!rd_varint(mp, me, l3) || mp + l3 > me) return false;
+        if ((k3 >> 3) == 1) {
+          name = (const char*)mp;
+          nlen = l3;
+        } else if ((k3 >> 3) == 2) {
+          vp = mp;
+          ve = mp + l3;
+        }
+        mp += l3;
+      }
+      if (!name || !vp) continue;
+      // Feature { oneof bytes=1 float=2 int64=3 }
+      const uint8_t* q = vp;
+      uint64_t k4, l4;
+      if (!rd_varint(q, ve, k4) || (k4 & 7) != 2 || !rd_varint(q, ve, l4) || q + l4 > ve) return false;
+      const int kind = (int)(k4 >> 3);
+      if (nlen == 5 && !memcmp(name, "label", 5) && kind == 2) {
+        if (decode_list(q, q + l4, true, label, nullptr, 1) != 1) return false;
+        have |= 1;
+      } else if (nlen == 3 && !memcmp(name, "ids", 3) && kind == 3) {
+        if (decode_list(q, q + l4, false, nullptr, ids, F) != F) return false;
+        have |= 2;
+      } else if (nlen == 6 && !memcmp(name, "values", 6) && kind == 2) {
+        if (decode_list(q, q + l4, true, vals, nullptr, F) != F) return false;
+        have |= 4;
+      }
+    }
+  }
+  return have == 7;
+}
+
+HFMIO_API int hfmio_decode_example(const uint8_t* p, size_t len, int F, float* label, int64_t* ids,
+                                   float* vals) {
+  return decode_example(p, len, F, label, ids, vals) ? 0 : -1;
+}
+
+// ------------------------------------------------------------------------------ libsvm
+static bool parse_libsvm(const std::string& line, int F, float* label, int64_t* ids, float* vals) {
+  const char* s = line.c_str();
+  char* end;
+  *label = strtof(s, &end);
+  if (end == s) return false;
+  s = end;
+  int n = 0;
+  while (*s) {
+    while (*s == ' ' || *s == '\t' || *s == '\r') ++s;
+    if (!*s) break;
+    long long id = strtoll(s, &end, 10);
+    if (end == s || *end != ':') return false;
+    s = end + 1;
+    float v = strtof(s, &end);
+    if (end == s) return false;
+    s = end;
+    if (n >= F) return false;
+    ids[n] = id;
+    vals[n] = v;
+    ++n;
+  }
+  return n == F;
+}
+
+// ------------------------------------------------------------------------------ loader
+struct Chunk {
+  int n = 0;
+  std::vector<float> label;
+  std::vector<int64_t> ids;
+  std::vector<float> vals;
+};
+
+struct WorkerQueue {
+  std::mutex m;
+  std::condition_variable cv_put, cv_get;
+  std::deque<std::unique_ptr<Chunk>> q;
+  bool done = false;
+  bool failed = false;
+  std::string err;
+};
+
+struct Loader {
+  std::vector<std::string> paths;
+  int format = 0, F = 0, B = 0, drop_remainder = 1, verify = 1;
+  int shard_n = 1, shard_i = 0;   // record-level shard (1 = off)
+  int depth = 4;
+  int chunk = 1024;
+  std::vector<std::unique_ptr<WorkerQueue>> queues;
+  std::vector<std::thread> threads;
+  std::atomic<bool> stop{false};
+  // consumer state
+  int turn = 0;
+  std::unique_ptr<Chunk> cur;
+  int cur_off = 0;
+  std::string err;
+
+  void worker(int w, int W) {
+    WorkerQueue& Q = *queues[w];
+    auto push = [&](std::unique_ptr<Chunk> c) {
+      std::unique_lock<std::mutex> lk(Q.m);
+      Q.cv_put.wait(lk, [&] { return (int)Q.q.size() < depth || stop.load(); });
+      if (stop.load()) return false;
+      Q.q.push_back(std::move(c));
+      Q.cv_get.notify_one();
+      return true;
+    };
+    auto fail = [&](const std::string& e) {
+      std::lock_guard<std::mutex> lk(Q.m);
+      Q.failed = true;
+      Q.err = e;
+      Q.done = true;
+      Q.cv_get.notify_all();
+    };
+    auto fresh = [&] {
+      auto c = std::make_unique<Chunk>();
+      c->label.resize(chunk);
+      c->ids.resize((size_t)chunk * F);
+      c->vals.resize((size_t)chunk * F);
+      return c;
+    };
+    std::unique_ptr<Chunk> c = fresh();
+    std::vector<uint8_t> buf;
+    std::string line;
+    long long rec = 0;   // record index in this worker's stream (record sharding uses W == 1)
+    for (size_t fi = w; fi < paths.size() && !stop.load(); fi += W) {
+      ByteReader r(paths[fi]);
+      if (!r.ok()) {
+        fail("cannot open " + paths[fi]);
+        return;
+      }
+      while (!stop.load()) {
+        float* lab = c->label.data() + c->n;
+        int64_t* ids = c->ids.data() + (size_t)c->n * F;
+        float* vals = c->vals.data() + (size_t)c->n * F;
+        bool okrec;
+        if (format == 0) {
+          int rc = next_tfrecord(r, buf, verify);
+          if (rc == 0) break;
+          if (rc < 0) {
+            fail(g_err);
+            return;
+          }
+          if (shard_n > 1 && (rec++ % shard_n) != shard_i) continue;
+          okrec = decode_example(buf.data(), buf.size(), F, lab, ids, vals);
+          if (!okrec) {
+            fail("Example does not match the fixed schema (label, ids[F], values[F]) in " + paths[fi]);
+            return;
+          }
+        } else {
+          if (!r.getline(line)) break;
+          if (line.find_first_not_of(" \t\r") == std::string::npos) continue;
+          if (shard_n > 1 && (rec++ % shard_n) != shard_i) continue;
+          if (!parse_libsvm(line, F, lab, ids, vals)) {
+            fail("bad libsvm line (expected label + " + std::to_string(F) + " id:val) in " + paths[fi]);
+            return;
+          }
+        }
+        if (++c->n == chunk) {
+          if (!push(std::move(c))) return;
+          c = fresh();
+        }
+      }
+    }
+    if (c->n > 0) push(std::move(c));
+    std::lock_guard<std::mutex> lk(Q.m);
+    Q.done = true;
+    Q.cv_get.notify_all();
+  }
+
+  // next chunk in deterministic round-robin order; nullptr at end
+  std::unique_ptr<Chunk> take() {
+    const int W = (int)queues.size();
+    int idle = 0;
+    while (idle < W) {
+      WorkerQueue& Q = *queues[turn];
+      std::unique_lock<std::mutex> lk(Q.m);
+      Q.cv_get.wait(lk, [&] { return !Q.q.empty() || Q.done; });
+      if (Q.failed) {
+        err = Q.err;
+        return nullptr;
+      }
+      if (!Q.q.empty()) {
+        auto c = std::move(Q.q.front());
+        Q.q.pop_front();
+        Q.cv_put.notify_one();
+        turn = (turn + 1) % W;
+        return c;
+      }
+      // this worker is exhausted; skip it for good
+      ++idle;
+      turn = (turn + 1) % W;
+    }
+    return nullptr;
+  }
+
+  // returns rows written (B, or < B for the final partial batch), 0 at end, -1 error
+  int next(float* lab, int64_t* ids, float* vals) {
+    int got = 0;
+    while (got < B) {
+      if (!cur || cur_off >= cur->n) {
+        cur = take();
+        cur_off = 0;
+        if (!cur) {
+          if (!err.empty()) return -1;
+          break;
+        }
+      }
+      int k = std::min(B - got, cur->n - cur_off);
+      memcpy(lab + got, cur->label.data() + cur_off, k * 4);
+      memcpy(ids + (size_t)got * F, cur->ids.data() + (size_t)cur_off * F, (size_t)k * F * 8);
+      memcpy(vals + (size_t)got * F, cur->vals.data() + (size_t)cur_off * F, (size_t)k * F * 4);
+      got += k;
+      cur_off += k;
+    }
+    if (got < B && drop_remainder) return 0;
+    return got;
+  }
+
+  void shutdown() {
+    stop.store(true);
+    for (auto& q : queues) {
+      std::lock_guard<std::mutex> lk(q->m);
+      q->cv_put.notify_all();
+      q->cv_get.notify_all();
+    }
+    for (auto& t : threads)
+      if (t.joinable()) t.join();
+  }
+};
+
+HFMIO_API void* hfmio_loader_create(const char** paths, int npaths, int format, int F, int batch,
+                                    int drop_remainder, int num_threads, int shard_n, int shard_i,
+                                    int verify_crc, int queue_depth) {
+  auto* L = new Loader();
+  for (int i = 0; i < npaths; ++i) L->paths.emplace_back(paths[i]);
+  L->format = format;
+  L->F = F;
+  L->B = batch;
+  L->drop_remainder = drop_remainder;
+  L->verify = verify_crc;
+  L->shard_n = shard_n < 1 ? 1 : shard_n;
+  L->shard_i = shard_i;
+  L->depth = queue_depth < 1 ? 4 : queue_depth;
+  int W = num_threads < 1 ? 1 : num_threads;
+  if (L->shard_n > 1) W = 1;                 // record-level shard needs the sequential stream
+  if (W > npaths) W = npaths < 1 ? 1 : npaths;
+  for (int w = 0; w < W; ++w) L->queues.emplace_back(new WorkerQueue());
+  for (int w = 0; w < W; ++w) L->threads.emplace_back(&Loader::worker, L, w, W);
+  return L;
+}
+
+HFMIO_API int hfmio_loader_next(void* h, float* labels, int64_t* ids, float* vals) {
+  auto* L = (Loader*)h;
+  int r = L->next(labels, ids, vals);
+  if (r < 0) set_err(L->err);
+  return r;
+}
+
+HFMIO_API void hfmio_loader_destroy(void* h) {
+  auto* L = (Loader*)h;
+  L->shutdown();
+  delete L;
+}
+
+// ------------------------------------------------------------------------------ writers
+static void put_varint(std::string& s, uint64_t v) {
+  while (v >= 0x80) {
+    s.push_back((char)((v & 0x7F) | 0x80));
+    v >>= 7;
+  }
+  s.push_back((char)v);
+}
+static void put_ld(std::string& s, int field, const std::string& payload) {
+  put_varint(s, ((uint64_t)field << 3) | 2);
+  put_varint(s, payload.size());
+  s += payload;
+}
+
+static std::string encode_example(float label, const int64_t* ids, const float* vals, int F) {
+  std::string fl;
+  put_ld(fl, 1, std::string((const char*)&label, 4));
+  std::string flab;
+  put_ld(flab, 2, fl);
+  std::string packed_ids;
+  for (int i = 0; i < F; ++i) put_varint(packed_ids, (uint64_t)ids[i]);
+  std::string il;
+  put_ld(il, 1, packed_ids);
+  std::string fids;
+  put_ld(fids, 3, il);
+  std::string vl;
+  put_ld(vl, 1, std::string((const char*)vals, (size_t)F * 4));
+  std::string fvals;
+  put_ld(fvals, 2, vl);
+  std::string entries;
+  auto entry = [&](const char* k, const std::string& v) {
+    std::string e;
+    put_ld(e, 1, std::string(k));
+    put_ld(e, 2, v);
+    put_ld(entries, 1, e);
+  };
+  entry("label", flab);
+  entry("ids", fids);
+  entry("values", fvals);
+  std::string ex;
+  put_ld(ex, 1, entries);
+  return ex;
+}
+
+static bool write_record(FILE* f, const std::string& d) {
+  uint64_t len = d.size();
+  uint32_t hc = masked(hfmio_crc32c((const uint8_t*)&len, 8));
+  uint32_t dc = masked(hfmio_crc32c((const uint8_t*)d.data(), d.size()));
+  return fwrite(&len, 8, 1, f) == 1 && fwrite(&hc, 4, 1, f) == 1 &&
+         fwrite(d.data(), 1, d.size(), f) == d.size() && fwrite(&dc, 4, 1, f) == 1;
+}
+
+HFMIO_API int hfmio_write_examples(const char* path, const float* labels, const int64_t* ids,
+                                   const float* vals, long n, int F, int append) {
+  FILE* f = fopen(path, append ? "ab" : "wb");
+  if (!f) {
+    set_err(std::string("cannot open ") + path);
+    return -1;
+  }
+  for (long i = 0; i < n; ++i)
+    if (!write_record(f, encode_example(labels[i], ids + (size_t)i * F, vals + (size_t)i * F, F))) {
+      fclose(f);
+      set_err("write failed");
+      return -1;
+    }
+  fclose(f);
+  return 0;
+}
+
+// native libsvm -> TFRecord converter (C36); returns records written or -1
+HFMIO_API long hfmio_libsvm_to_tfrecord(const char* src, const char* dst, int F) {
+  ByteReader r(src);
+  if (!r.ok()) {
+    set_err(std::string("cannot open ") + src);
+    return -1;
+  }
+  FILE* f = fopen(dst, "wb");
+  if (!f) {
+    set_err(std::string("cannot open ") + dst);
+    return -1;
+  }
+  std::string line;
+  std::vector<int64_t> ids(F);
+  std::vector<float> vals(F);
+  long n = 0;
+  while (r.getline(line)) {
+    if (line.find_first_not_of(" \t\r") == std::string::npos) continue;
+    float lab;
+    if (!parse_libsvm(line, F, &lab, ids.data(), vals.data())) {
+      set_err("bad libsvm line " + std::to_string(n + 1));
+      fclose(f);
+      return -1;
+    }
+    write_record(f, encode_example(lab, ids.data(), vals.data(), F));
+    ++n;
+  }
+  fclose(f);
+  return n;
+}
+
+HFMIO_API long hfmio_count_records(const char* path, int format, int verify) {
+  ByteReader r(path);
+  if (!r.ok()) {
+    set_err(std::string("cannot open ") + path);
+    return -1;
+  }
+  long n = 0;
+  if (format == 0) {
+    std::vector<uint8_t> buf;
+    int rc;
+    while ((rc = next_tfrecord(r, buf, verify)) == 1) ++n;
+    return rc < 0 ? -1 : n;
+  }
+  std::string line;
+  while (r.getline(line))
+    if (line.find_first_not_of(" \t\r") != std::string::npos) ++n;
+  return n;
+}

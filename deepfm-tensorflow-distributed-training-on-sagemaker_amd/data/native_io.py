@@ -1,0 +1,150 @@
+"""ctypes binding of ``_lib/libhipfm_io.so`` (csrc/io/hfm_io.cpp): the native TFRecord /
+Example / libsvm reader, threaded deterministic batch loader, CRC32C and writers."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+from typing import Iterator, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from ..ops.build import IO_SO, build_io
+
+_lib = None
+_lock = threading.Lock()
+
+FMT_TFRECORD, FMT_LIBSVM = 0, 1
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(IO_SO):
+                build_io()
+            L = C.CDLL(IO_SO)
+            vp, ci, cl = C.c_void_p, C.c_int, C.c_long
+            L.hfmio_last_error.restype = C.c_char_p
+            L.hfmio_crc32c.argtypes = [vp, C.c_size_t]
+            L.hfmio_crc32c.restype = C.c_uint32
+            L.hfmio_masked_crc32c.argtypes = [vp, C.c_size_t]
+            L.hfmio_masked_crc32c.restype = C.c_uint32
+            L.hfmio_decode_example.argtypes = [vp, C.c_size_t, ci, vp, vp, vp]
+            L.hfmio_decode_example.restype = ci
+            L.hfmio_loader_create.argtypes = [C.POINTER(C.c_char_p), ci, ci, ci, ci, ci, ci, ci, ci,
+                                              ci, ci]
+            L.hfmio_loader_create.restype = vp
+            L.hfmio_loader_next.argtypes = [vp, vp, vp, vp]
+            L.hfmio_loader_next.restype = ci
+            L.hfmio_loader_destroy.argtypes = [vp]
+            L.hfmio_write_examples.argtypes = [C.c_char_p, vp, vp, vp, cl, ci, ci]
+            L.hfmio_write_examples.restype = ci
+            L.hfmio_libsvm_to_tfrecord.argtypes = [C.c_char_p, C.c_char_p, ci]
+            L.hfmio_libsvm_to_tfrecord.restype = cl
+            L.hfmio_count_records.argtypes = [C.c_char_p, ci, ci]
+            L.hfmio_count_records.restype = cl
+            _lib = L
+    return _lib
+
+
+def _err() -> str:
+    return lib().hfmio_last_error().decode(errors="replace")
+
+
+def crc32c(data: bytes) -> int:
+    return lib().hfmio_crc32c(data, len(data))
+
+
+def masked_crc32c(data: bytes) -> int:
+    return lib().hfmio_masked_crc32c(data, len(data))
+
+
+def decode_example(data: bytes, F: int):
+    lab = np.zeros(1, np.float32)
+    ids = np.zeros(F, np.int64)
+    vals = np.zeros(F, np.float32)
+    rc = lib().hfmio_decode_example(data, len(data), F, lab.ctypes.data, ids.ctypes.data,
+                                    vals.ctypes.data)
+    if rc != 0:
+        raise ValueError("Example does not match the fixed schema")
+    return float(lab[0]), ids, vals
+
+
+def write_examples(path: str, labels: np.ndarray, ids: np.ndarray, vals: np.ndarray,
+                   append: bool = False) -> None:
+    labels = np.ascontiguousarray(labels, np.float32)
+    ids = np.ascontiguousarray(ids, np.int64)
+    vals = np.ascontiguousarray(vals, np.float32)
+    n, F = ids.shape
+    if lib().hfmio_write_examples(path.encode(), labels.ctypes.data, ids.ctypes.data,
+                                  vals.ctypes.data, n, F, 1 if append else 0) != 0:
+        raise IOError(_err())
+
+
+def libsvm_to_tfrecord(src: str, dst: str, field_size: int) -> int:
+    n = lib().hfmio_libsvm_to_tfrecord(src.encode(), dst.encode(), field_size)
+    if n < 0:
+        raise IOError(_err())
+    return n
+
+
+def count_records(path: str, fmt: int = FMT_TFRECORD, verify: bool = True) -> int:
+    n = lib().hfmio_count_records(path.encode(), fmt, 1 if verify else 0)
+    if n < 0:
+        raise IOError(_err())
+    return n
+
+
+class NativeLoader:
+    """Iterator of (labels f32[B], ids i64[B,F], vals f32[B,F]) numpy batches.
+
+    ``record_shard=(n, i)`` reproduces ``dataset.shard(n, i)`` on the concatenated record
+    stream (reference semantics); without it the files are read in parallel by ``threads``
+    workers with a deterministic round-robin interleave of 1024-record chunks."""
+
+    def __init__(self, paths: Sequence[str], field_size: int, batch_size: int,
+                 fmt: int = FMT_TFRECORD, drop_remainder: bool = True, threads: int = 4,
+                 record_shard: Tuple[int, int] = (1, 0), verify_crc: bool = True,
+                 queue_depth: int = 4):
+        self.paths = [str(p) for p in paths]
+        self.F, self.B = int(field_size), int(batch_size)
+        arr = (C.c_char_p * max(1, len(self.paths)))(*[p.encode() for p in self.paths])
+        self._h = lib().hfmio_loader_create(arr, len(self.paths), fmt, self.F, self.B,
+                                            1 if drop_remainder else 0, threads, record_shard[0],
+                                            record_shard[1], 1 if verify_crc else 0, queue_depth)
+        self._done = False
+
+    def next_into(self, labels: np.ndarray, ids: np.ndarray, vals: np.ndarray) -> int:
+        """Fill caller buffers (e.g. pinned host memory); returns rows (0 at end)."""
+        if self._done:
+            return 0
+        r = lib().hfmio_loader_next(self._h, labels.ctypes.data, ids.ctypes.data, vals.ctypes.data)
+        if r < 0:
+            raise IOError(_err())
+        if r == 0:
+            self._done = True
+        return r
+
+    def __iter__(self) -> Iterator[Tuple[np.ndarray, np.ndarray, np.ndarray]]:
+        while True:
+            lab = np.empty(self.B, np.float32)
+            ids = np.empty((self.B, self.F), np.int64)
+            vals = np.empty((self.B, self.F), np.float32)
+            r = self.next_into(lab, ids, vals)
+            if r == 0:
+                return
+            yield lab[:r], ids[:r], vals[:r]
+
+    def close(self):
+        if self._h:
+            lib().hfmio_loader_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

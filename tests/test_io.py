@@ -1,0 +1,173 @@
+"""I/O tests: TFRecord framing + CRC, Example codec, libsvm, native loader,
+shard policy coverage (disjoint + complete: fixes quirk Q1)."""
+import os
+import random
+import struct
+
+import numpy as np
+import pytest
+import torch
+
+import hipfm
+from hipfm.data import native_io as nio
+from hipfm.data import tfrecord as tr
+from hipfm.data.pipeline import InputPipeline, discover_files, plan_shard, shard_spec
+
+
+def _rows(n, F, seed=0):
+    rng = np.random.default_rng(seed)
+    ids = rng.integers(0, 1 << 40, size=(n, F), dtype=np.int64)
+    vals = rng.random((n, F), dtype=np.float32)
+    lab = (rng.random(n) < 0.3).astype(np.float32)
+    return lab, ids, vals
+
+
+def test_crc32c_known_vectors():
+    # RFC 3720 test vector: 32 bytes of zeros -> 0x8a9136aa
+    assert tr.crc32c(b"\x00" * 32) == 0x8A9136AA
+    assert nio.crc32c(b"\x00" * 32) == 0x8A9136AA
+    assert tr.crc32c(b"123456789") == 0xE3069283
+    data = bytes(range(256)) * 7
+    assert nio.crc32c(data) == tr.crc32c(data)
+    assert nio.masked_crc32c(data) == tr.masked_crc32c(data)
+
+
+def test_example_roundtrip_python_and_native():
+    F = 39
+    lab, ids, vals = _rows(3, F)
+    for i in range(3):
+        b = tr.encode_example(lab[i], ids[i].tolist(), vals[i].tolist())
+        l2, i2, v2 = tr.parse_deepfm_example(b, F)
+        assert l2 == lab[i] and i2 == ids[i].tolist()
+        assert np.allclose(v2, vals[i])
+        l3, i3, v3 = nio.decode_example(b, F)
+        assert l3 == lab[i] and np.array_equal(i3, ids[i]) and np.array_equal(v3, vals[i])
+    with pytest.raises(ValueError):
+        nio.decode_example(tr.encode_example(1.0, [1, 2], [1.0, 2.0]), F)
+
+
+def test_example_decoder_accepts_unpacked_and_reordered_fields():
+    # hand-built Example with unpacked int64/float lists and the features in another order
+    def ld(f, p):
+        return tr._key(f, 2) + tr._varint(len(p)) + p
+    ids_list = b"".join(tr._key(1, 0) + tr._varint(v) for v in (5, 7))
+    vals_list = b"".join(tr._key(1, 5) + struct.pack("<f", v) for v in (0.5, 2.0))
+    lab_list = tr._key(1, 5) + struct.pack("<f", 1.0)
+    feats = [("values", ld(2, vals_list)), ("label", ld(2, lab_list)), ("ids", ld(3, ids_list))]
+    entries = b"".join(ld(1, ld(1, k.encode()) + ld(2, v)) for k, v in feats)
+    ex = ld(1, entries)
+    lab, ids, vals = nio.decode_example(ex, 2)
+    assert lab == 1.0 and ids.tolist() == [5, 7] and vals.tolist() == [0.5, 2.0]
+    assert tr.parse_deepfm_example(ex, 2) == (1.0, [5, 7], [0.5, 2.0])
+
+
+def test_tfrecord_file_roundtrip_and_crc_detection(tmp_path):
+    F = 5
+    lab, ids, vals = _rows(100, F, 1)
+    p = str(tmp_path / "tr-0.tfrecords")
+    nio.write_examples(p, lab, ids, vals)
+    # python reader verifies every CRC of the native writer's output
+    recs = list(tr.read_records(p))
+    assert len(recs) == 100
+    assert tr.parse_deepfm_example(recs[7], F)[1] == ids[7].tolist()
+    assert nio.count_records(p) == 100
+    # corrupt one payload byte -> CRC error from both readers
+    raw = bytearray(open(p, "rb").read())
+    raw[40] ^= 0xFF
+    q = str(tmp_path / "bad.tfrecords")
+    open(q, "wb").write(raw)
+    with pytest.raises(IOError):
+        list(tr.read_records(q))
+    with pytest.raises(IOError):
+        list(nio.NativeLoader([q], F, 10))
+
+
+def test_libsvm_parse_and_convert(tmp_path):
+    src = tmp_path / "train.libsvm"
+    src.write_text("1 1:0.5 2:0.03519 3:1\n0 4:1 5:0.25 9:2\n\n")
+    assert tr.parse_libsvm_line("1 1:0.5 2:0.03519 3:1") == (1.0, [1, 2, 3], [0.5, 0.03519, 1.0])
+    n = nio.libsvm_to_tfrecord(str(src), str(tmp_path / "a.tfrecords"), 3)
+    assert n == 2
+    n2 = tr.libsvm_to_tfrecord(str(src), str(tmp_path / "b.tfrecords"), 3)
+    assert n2 == 2
+    assert open(tmp_path / "a.tfrecords", "rb").read() == open(tmp_path / "b.tfrecords", "rb").read()
+    batches = list(nio.NativeLoader([str(src)], 3, 2, fmt=nio.FMT_LIBSVM))
+    assert len(batches) == 1
+    lab, ids, vals = batches[0]
+    assert lab.tolist() == [1.0, 0.0] and ids[1].tolist() == [4, 5, 9]
+
+
+@pytest.mark.parametrize("threads", [1, 3])
+def test_native_loader_batches_deterministic(tmp_path, threads):
+    F = 4
+    files = []
+    allrows = []
+    for k in range(5):
+        lab, ids, vals = _rows(700 + 13 * k, F, k)
+        p = str(tmp_path / f"tr-{k}.tfrecords")
+        nio.write_examples(p, lab, ids, vals)
+        files.append(p)
+        allrows.append(ids)
+    b1 = [x[1].copy() for x in nio.NativeLoader(files, F, 256, threads=threads)]
+    b2 = [x[1].copy() for x in nio.NativeLoader(files, F, 256, threads=threads)]
+    assert len(b1) == len(b2) and all(np.array_equal(a, b) for a, b in zip(b1, b2))
+    total = sum(len(r) for r in allrows)
+    assert len(b1) == total // 256                       # drop_remainder=True
+    got = np.concatenate(b1)
+    want = np.concatenate(allrows)
+    assert set(map(tuple, got.tolist())) <= set(map(tuple, want.tolist()))
+    # no drop: every record exactly once
+    full = np.concatenate([x[1] for x in nio.NativeLoader(files, F, 256, drop_remainder=False,
+                                                          threads=threads)])
+    assert sorted(map(tuple, full.tolist())) == sorted(map(tuple, want.tolist()))
+
+
+def test_record_shard_matches_reference_semantics(tmp_path):
+    F = 3
+    lab, ids, vals = _rows(50, F, 9)
+    p = str(tmp_path / "tr.tfrecords")
+    nio.write_examples(p, lab, ids, vals)
+    for n in (2, 3):
+        for i in range(n):
+            got = np.concatenate([x[1] for x in nio.NativeLoader([p], F, 1, record_shard=(n, i))])
+            assert np.array_equal(got, ids[i::n])
+
+
+def test_shard_plan_disjoint_and_complete():
+    files = [f"f{i}" for i in range(11)]
+    for n in (1, 2, 3, 8):
+        seen = []
+        for i in range(n):
+            plan = plan_shard(files, n, i, "file", seed=3, epoch=2)
+            assert plan.record_shard == (1, 0) or n == 1
+            seen += plan.files
+        assert sorted(seen) == sorted(files)            # disjoint + complete
+    # fewer files than ranks -> record-level shard of the identical order
+    p0 = plan_shard(files[:2], 4, 1, "file", seed=3)
+    assert p0.record_shard == (4, 1) and sorted(p0.files) == files[:2]
+
+
+def test_shard_spec_matrix():
+    assert shard_spec(8, 5, 1, 4, 2, enable_s3_shard=False) == (8, 5)
+    assert shard_spec(8, 5, 1, 4, 2, enable_s3_shard=True) == (4, 1)
+    assert shard_spec(8, 5, 1, 4, 2, pipe_mode=True, enable_data_multi_path=True) == (2, 1)
+    assert shard_spec(8, 5, 1, 4, 2, pipe_mode=True, enable_data_multi_path=True,
+                      enable_s3_shard=True) == (1, 0)
+    assert shard_spec(8, 5, 1, 4, 2, pipe_mode=True, enable_s3_shard=True) == (4, 1)
+
+
+def test_discover_and_pipeline_cache(tmp_path):
+    F = 3
+    d = tmp_path / "data" / "sub"
+    d.mkdir(parents=True)
+    for k in range(3):
+        lab, ids, vals = _rows(100, F, k)
+        nio.write_examples(str(d / f"tr-{k}.tfrecords"), lab, ids, vals)
+    nio.write_examples(str(d / "va-0.tfrecords"), *_rows(10, F, 7))
+    tr_files = discover_files(str(tmp_path / "data"), "tr")
+    assert len(tr_files) == 3 and len(discover_files(str(tmp_path / "data"), "va")) == 1
+    pipe = InputPipeline(tr_files, F, 64, num_epochs=2, cache=True, seed=1)
+    e0 = [b[0] for b in pipe.iter_epoch(0)]
+    e1 = [b[0] for b in pipe.iter_epoch(1)]
+    assert len(e0) == 300 // 64 and all(torch.equal(a, b) for a, b in zip(e0, e1))
+    assert pipe.local_records() == 300
