@@ -77,6 +77,9 @@ static uint32_t crc32c_sw(const uint8_t* p, size_t n, uint32_t crc) {
 HFMIO_API uint32_t hfmio_crc32c(const uint8_t* p, size_t n) {
   return have_sse42() ? crc32c_hw(p, n, 0) : crc32c_sw(p, n, 0);
 }
+HFMIO_API uint32_t hfmio_crc32c_extend(uint32_t crc, const uint8_t* p, size_t n) {
+  return have_sse42() ? crc32c_hw(p, n, crc) : crc32c_sw(p, n, crc);
+}
 static inline uint32_t masked(uint32_t c) { return ((c >> 15) | (c << 17)) + 0xA282EAD8u; }
 HFMIO_API uint32_t hfmio_masked_crc32c(const uint8_t* p, size_t n) { return masked(hfmio_crc32c(p, n)); }
 

@@ -1,0 +1,178 @@
+"""Entrypoint with the reference's flags and task dispatch (reference L5, PS:341-467, HVD:289-431).
+
+  python -m hipfm --task_type train --training_data_dir D --val_data_dir V --model_dir M \
+      --feature_size 117581 --field_size 39 --batch_size 1024 --deep_layers 128,64,32 ...
+  python -m hipfm.launch --nproc_per_node 8 -m hipfm --task_type train ...     (data parallel)
+
+task_type (PS:61):
+  train   per epoch: train one epoch, then evaluate (HVD:390-394 file mode) — all ranks evaluate
+          their shard (Q10); pipe mode: one pass over num_epochs FIFO epochs (HVD:396-405);
+          then export the servable (train|export, PS:450-467)
+  eval    evaluate va* files (PS:443-444)
+  infer   predict te* files from val_data_dir -> "<val_data_dir>/pred.txt" ("%f\\n" per row,
+          PS:445-449); ``--pred_path`` overrides (Q9)
+  export  export the servable only
+"""
+from __future__ import annotations
+
+import json
+import os
+import shutil
+import sys
+from typing import List, Optional, Sequence
+
+import torch
+import torch.distributed as dist
+
+from .config import RunConfig, parse_flags
+from .data.pipeline import InputPipeline, discover_files, shard_spec
+from .estimator import Estimator
+
+
+def _channels() -> List[str]:
+    raw = os.environ.get("SM_CHANNELS")
+    if not raw:
+        return []
+    try:
+        return list(json.loads(raw))
+    except ValueError:
+        return [c for c in raw.split(",") if c]
+
+
+def _init_dist(cfg: RunConfig):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1 and not dist.is_initialized():
+        from .parallel.dist import init_distributed
+        dev = cfg.device
+        backend = "gloo" if dev == "cpu" or (dev == "auto" and not torch.cuda.is_available()) else "nccl"
+        if backend == "nccl":
+            torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+        init_distributed(backend)
+
+
+def build_pipelines(cfg: RunConfig, est: Estimator):
+    rank, world = est.rank, est.world
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    fmt = cfg.data_format
+    shard = shard_spec(world, rank, local_rank, cfg.worker_per_host, len(cfg.hosts),
+                       cfg.enable_s3_shard, bool(cfg.pipe_mode), cfg.enable_data_multi_path)
+    dev = est.device if (est.native and cfg.cache_data) else None
+    id_dtype = torch.int64
+    common = dict(fmt=fmt, seed=cfg.seed, threads=max(1, min(8, cfg.num_threads)), device=dev,
+                  id_dtype=id_dtype)
+    if cfg.pipe_mode:
+        ch = _channels()
+        tr_ch = cfg.training_channel_name or (ch[1 + local_rank] if len(ch) > 1 + local_rank else "training")
+        ev_ch = cfg.evaluation_channel_name or (ch[0] if ch else "evaluation")
+        tr = lambda epochs: InputPipeline([], cfg.field_size, cfg.batch_size, epochs, shard=shard,
+                                          pipe_channel=tr_ch, **common)
+        va = lambda: InputPipeline([], cfg.field_size, cfg.batch_size, 1, shard=(world, rank),
+                                   pipe_channel=ev_ch, **common)
+        te = va
+        return tr, va, te
+    ext = "tfrecord" if fmt == "tfrecord" else "libsvm"
+    tr_files = discover_files(cfg.training_data_dir, "tr", ext)
+    va_files = discover_files(cfg.val_data_dir, "va", ext)
+    te_files = discover_files(cfg.val_data_dir, "te", ext)
+    est.log.info(f"tr_files: {tr_files}")
+    est.log.info(f"va_files: {va_files}")
+    est.log.info(f"te_files: {te_files}")
+    cache_tr = InputPipeline(tr_files, cfg.field_size, cfg.batch_size, 1, shard=shard,
+                             cache=cfg.cache_data, **common)
+
+    def tr(epochs):
+        return cache_tr
+    va = lambda: InputPipeline(va_files, cfg.field_size, cfg.batch_size, 1, shard=(world, rank),
+                               shuffle_files=False, **{**common, "device": None})
+    te = lambda: InputPipeline(te_files, cfg.field_size, cfg.batch_size, 1, shard=(1, 0),
+                               shuffle_files=False, drop_remainder=False, **{**common, "device": None})
+    return tr, va, te
+
+
+def run(cfg: RunConfig) -> dict:
+    _init_dist(cfg)
+    rank = dist.get_rank() if dist.is_initialized() else 0
+    if rank == 0:
+        print(sys.argv, flush=True)
+        print(cfg.dump(), flush=True)
+    if cfg.clear_existing_model and cfg.ckpt_dir and rank == 0:     # HVD:334-340
+        try:
+            shutil.rmtree(cfg.ckpt_dir)
+            print(f"existing model cleaned at {cfg.ckpt_dir}")
+        except Exception as e:  # noqa: BLE001
+            print(e, "at clear_existing_model")
+    if dist.is_initialized():
+        dist.barrier()
+    est = Estimator(cfg)
+    tr, va, te = build_pipelines(cfg, est)
+    result = {}
+    if cfg.task_type == "train":
+        max_steps = cfg.max_steps or None
+        if cfg.pipe_mode:
+            pipe = tr(cfg.num_epochs)
+            est.train(pipe, max_steps, eval_fn=lambda: est.evaluate(va()))
+            est.save()
+            result = est.evaluate(va())
+        else:
+            pipe = tr(1)
+            for epoch in range(cfg.num_epochs):
+                pipe.num_epochs = 1
+                est.train(pipe.iter_epoch(epoch) if not hasattr(pipe, "local_records") else
+                          _EpochView(pipe, epoch), max_steps, eval_fn=lambda: est.evaluate(va()))
+                result = est.evaluate(va())
+                if max_steps is not None and est.global_step >= max_steps:
+                    break
+            est.save()
+    elif cfg.task_type == "eval":
+        result = est.evaluate(va())
+    elif cfg.task_type == "infer":
+        path = cfg.pred_path or os.path.join(cfg.val_data_dir, "pred.txt")
+        if est.rank == 0:
+            n = 0
+            with open(path, "w") as fo:
+                for prob in est.predict(te()):
+                    for p in prob.tolist():
+                        fo.write("%f\n" % p)
+                        n += 1
+            result = {"pred_path": path, "rows": n}
+            est.log.info(f"wrote {n} predictions to {path}")
+    if cfg.task_type in ("export", "train") and cfg.servable_model_dir:
+        path = est.export(cfg.servable_model_dir)
+        result["export_dir"] = path
+    est.log.close()
+    return result
+
+
+class _EpochView:
+    """One epoch of an InputPipeline that still exposes local_records (equal-steps logic)."""
+
+    def __init__(self, pipe: InputPipeline, epoch: int):
+        self.pipe, self.epoch = pipe, epoch
+        self.B = pipe.B
+
+    def local_records(self):
+        return self.pipe.local_records(self.epoch)
+
+    @property
+    def max_batches(self):
+        return self.pipe.max_batches
+
+    @max_batches.setter
+    def max_batches(self, v):
+        self.pipe.max_batches = v
+
+    def __iter__(self):
+        return self.pipe.iter_epoch(self.epoch)
+
+
+def main(argv: Optional[Sequence[str]] = None) -> dict:
+    cfg = parse_flags(argv)
+    res = run(cfg)
+    if dist.is_initialized():
+        dist.barrier()
+        dist.destroy_process_group()
+    return res
+
+
+if __name__ == "__main__":
+    main()

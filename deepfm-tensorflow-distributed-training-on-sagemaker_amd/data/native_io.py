@@ -30,6 +30,8 @@ def lib():
             L.hfmio_last_error.restype = C.c_char_p
             L.hfmio_crc32c.argtypes = [vp, C.c_size_t]
             L.hfmio_crc32c.restype = C.c_uint32
+            L.hfmio_crc32c_extend.argtypes = [C.c_uint32, vp, C.c_size_t]
+            L.hfmio_crc32c_extend.restype = C.c_uint32
             L.hfmio_masked_crc32c.argtypes = [vp, C.c_size_t]
             L.hfmio_masked_crc32c.restype = C.c_uint32
             L.hfmio_decode_example.argtypes = [vp, C.c_size_t, ci, vp, vp, vp]
@@ -56,6 +58,15 @@ def _err() -> str:
 
 def crc32c(data: bytes) -> int:
     return lib().hfmio_crc32c(data, len(data))
+
+
+def crc32c_extend(crc: int, data: bytes) -> int:
+    """crc32c(a + b) == crc32c_extend(crc32c(a), b)"""
+    return lib().hfmio_crc32c_extend(crc, data, len(data))
+
+
+def mask_crc(c: int) -> int:
+    return (((c >> 15) | (c << 17)) + 0xA282EAD8) & 0xFFFFFFFF
 
 
 def masked_crc32c(data: bytes) -> int:

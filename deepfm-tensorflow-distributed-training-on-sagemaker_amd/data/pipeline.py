@@ -41,7 +41,10 @@ def discover_files(data_dir: str, prefix: str, fmt: str = "tfrecord") -> List[st
         return []
     pat = f"{prefix}*.tfrecords" if fmt == "tfrecord" else f"{prefix}*"
     files = glob.glob(os.path.join(data_dir, "**", pat), recursive=True)
-    return sorted(f for f in files if os.path.isfile(f) and not f.endswith(".txt.pred"))
+    files = [f for f in files if os.path.isfile(f)]
+    if fmt != "tfrecord":   # libsvm text: anything named like the split except TFRecords
+        files = [f for f in files if not f.endswith(".tfrecords")]
+    return sorted(files)
 
 
 def shard_spec(world: int, rank: int, local_rank: int = 0, worker_per_host: int = 1,

@@ -1,0 +1,383 @@
+"""Estimator-style training API (reference L4: tf.estimator.Estimator + train_and_evaluate).
+
+Reference call sites:
+  Estimator(model_fn, model_dir, params, config)                     PS:435, HVD:365-368
+  train_and_evaluate(TrainSpec, EvalSpec(throttle_secs, start_delay))   PS:439-442
+  for epoch: train(input_fn(num_epochs=1), hooks=[bcast]); rank0 evaluate   HVD:390-394
+  evaluate -> {auc, loss, global_step};  predict(predict_keys="prob")       PS:443-449
+  export_savedmodel(servable_model_dir, raw receiver)                        PS:451-467
+Differences by design (MI355X):
+  * one persistent training loop; the epoch boundary is a counter (Q11) and the model state
+    never leaves the GPU between epochs (no per-epoch re-broadcast);
+  * every rank evaluates its shard and the AUC histograms / loss sums are all-reduced (Q10) —
+    no idle ranks while rank 0 evaluates;
+  * checkpoints: every rank saves its own state, atomic publish, auto-resume (§5.4);
+  * equal steps per rank are enforced up front (Horovod "uneven data" shutdown, DOC p.22-23).
+Backends: ``cuda`` -> NativeDeepFM (HIP kernels; fails loudly without its library),
+``cpu`` -> GoldenDeepFM (reference-semantics PyTorch; data parallel over gloo).
+"""
+from __future__ import annotations
+
+import math
+import os
+import shutil
+import time
+from dataclasses import dataclass
+from typing import Callable, Dict, Iterable, Iterator, List, Optional
+
+import torch
+import torch.distributed as dist
+
+from .ckpt.export import export_servable
+from .ckpt.native import CheckpointManager, reshard_rows
+from .config import RunConfig
+from .ops.metrics import auc_from_hist, hist_torch
+from .utils.logging import MetricsLogger, StepTimer
+
+
+def _dist_on() -> bool:
+    return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+
+
+def resolve_device(cfg: RunConfig):
+    if cfg.device == "cpu":
+        return torch.device("cpu")
+    if cfg.device in ("cuda", "gpu") or (cfg.device == "auto" and torch.cuda.is_available()):
+        if not torch.cuda.is_available():
+            raise RuntimeError("--device cuda requested but no GPU is visible")
+        return torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
+    return torch.device("cpu")
+
+
+@dataclass
+class TrainSpec:
+    input_fn: Callable[[], Iterable]
+    max_steps: Optional[int] = None
+    hooks: tuple = ()
+
+
+@dataclass
+class EvalSpec:
+    input_fn: Callable[[], Iterable]
+    steps: Optional[int] = None
+    start_delay_secs: float = 0.0     # reference: 1000 (PS:441)
+    throttle_secs: float = 0.0        # reference: 1200 (PS:441)
+
+
+class Estimator:
+    def __init__(self, cfg: RunConfig, device=None):
+        cfg.validate()
+        self.cfg = cfg
+        self.device = torch.device(device) if device is not None else resolve_device(cfg)
+        self.native = self.device.type == "cuda"
+        self.rank = dist.get_rank() if _dist_on() else 0
+        self.world = dist.get_world_size() if _dist_on() else 1
+        torch.manual_seed(cfg.seed)
+        self.comm = None
+        if self.native:
+            from .models.deepfm import NativeDeepFM
+            if self.world > 1:
+                from .parallel.dist import Comm
+                mode = cfg.embedding_mode
+                if mode == "auto":
+                    mode = "sharded" if cfg.feature_size * cfg.embedding_size > (1 << 27) else "replicated"
+                self.comm = Comm(sharded=(mode == "sharded"))
+            self.model = NativeDeepFM(cfg.feature_size, cfg.field_size, cfg.embedding_size, cfg.layers,
+                                      cfg.keep_probs, l2_reg=cfg.l2_reg, learning_rate=cfg.learning_rate,
+                                      optimizer=cfg.optimizer, loss_type=cfg.loss_type,
+                                      sparse_update=cfg.sparse_update, seed=cfg.seed,
+                                      batch_size=cfg.batch_size, device=self.device, comm=self.comm,
+                                      batch_norm=cfg.batch_norm)
+        else:
+            from .models.reference import GoldenDeepFM
+            self.model = GoldenDeepFM(cfg.feature_size, cfg.field_size, cfg.embedding_size, cfg.layers,
+                                      cfg.keep_probs, batch_norm=cfg.batch_norm,
+                                      batch_norm_decay=cfg.batch_norm_decay, l2_reg=cfg.l2_reg,
+                                      learning_rate=cfg.learning_rate, optimizer=cfg.optimizer,
+                                      loss_type=cfg.loss_type, sparse_update=cfg.sparse_update,
+                                      seed=cfg.seed, world_size=self.world)
+        barrier = (lambda: dist.barrier()) if _dist_on() else None
+        self.ckpt = CheckpointManager(cfg.ckpt_dir, cfg.keep_checkpoint_max, self.rank, self.world,
+                                      barrier) if cfg.ckpt_dir else None
+        mpath = cfg.metrics_file or (os.path.join(cfg.ckpt_dir, "metrics.jsonl") if cfg.ckpt_dir else None)
+        self.log = MetricsLogger(mpath, self.rank)
+        self.timer = StepTimer()
+        self._last_save_t = time.time()
+        self._last_eval_t = 0.0
+        self.restored_from = self.restore_latest()
+
+    # ------------------------------------------------------------------ state
+    @property
+    def global_step(self) -> int:
+        return self.model.global_step() if self.native else int(self.model.global_step)
+
+    def _state(self):
+        return self.model.state_dict_local()
+
+    def _meta(self):
+        if self.native:
+            return self.model.ckpt_meta()
+        return {"format": "hipfm-golden", "V": self.cfg.feature_size, "F": self.cfg.field_size,
+                "K": self.cfg.embedding_size, "layers": self.cfg.layers, "optimizer": self.cfg.optimizer,
+                "world": self.world, "sharding": "replicated"}
+
+    def save(self) -> Optional[str]:
+        if self.ckpt is None:
+            return None
+        if self.native:
+            torch.cuda.synchronize(self.device)
+        path = self.ckpt.save(self.global_step, self._state(), self._meta())
+        self._last_save_t = time.time()
+        self.log.info(f"Saving checkpoints for {self.global_step} into {path}.")
+        return path
+
+    def restore_latest(self) -> Optional[str]:
+        if self.ckpt is None:
+            return None
+        path = self.ckpt.latest()
+        if path is None:
+            return None
+        man = self.ckpt.load_manifest(path)
+        meta = man["meta"]
+        fmt_ok = meta.get("format") == self._meta().get("format")
+        if not fmt_ok:
+            raise RuntimeError(f"checkpoint {path} was written by {meta.get('format')}; this job "
+                               f"runs {self._meta().get('format')} (convert via TF bundle export)")
+        if man["world"] == self.world and meta.get("sharding") == self._meta().get("sharding"):
+            st = self.ckpt.load_rank(path, self.rank)
+        else:
+            st = self._reshard_load(path, man)
+        self.model.load_state_dict_local(st)
+        self.log.info(f"Restoring parameters from {path} (global_step {self.global_step})")
+        return path
+
+    def _reshard_load(self, path: str, man: dict) -> Dict[str, torch.Tensor]:
+        """Resume on a different world size / sharding: replicated rows are sliced, mod-sharded
+        rows are regrouped (owner = id % N)."""
+        old_world = man["world"]
+        old_sh = man["meta"].get("sharding", "replicated")
+        base = self.ckpt.load_rank(path, 0)
+        if not self.native:
+            return base
+        out = dict(base)
+        m = self.model
+        table_keys = [k for k in base if k.startswith("fm_")]
+        for k in table_keys:
+            row_shape = tuple(base[k].shape[1:])
+            if old_sh == "replicated":
+                full = base[k]
+            else:
+                full = None
+            if m.sharded:
+                if full is not None:
+                    loc = full[m.rank::m.world]
+                    t = torch.zeros((m.R,) + row_shape)
+                    t[: loc.shape[0]] = loc
+                    out[k] = t
+                else:
+                    out[k] = reshard_rows(path, k, old_world, m.world, m.rank, m.R, row_shape)
+            else:
+                if full is not None:
+                    out[k] = full
+                else:
+                    out[k] = reshard_rows(path, k, old_world, 1, 0, m.R, row_shape)
+        return out
+
+    # ------------------------------------------------------------------ DP helpers (golden)
+    def _golden_grad_sync(self, grads, touched):
+        if self.world == 1:
+            return grads, touched
+        out = {}
+        for k, g in grads.items():
+            t = g.contiguous().clone()
+            dist.all_reduce(t)
+            out[k] = t / self.world
+        mask = torch.zeros(self.cfg.feature_size, dtype=torch.int32)
+        mask[touched] = 1
+        dist.all_reduce(mask, op=dist.ReduceOp.MAX)
+        return out, torch.nonzero(mask).reshape(-1)
+
+    def _enforce_equal_steps(self, pipeline):
+        """Every rank runs the same number of steps per epoch (min over ranks)."""
+        if self.world == 1 or not hasattr(pipeline, "local_records"):
+            return
+        n = pipeline.local_records() // pipeline.B
+        t = torch.tensor([n], dtype=torch.int64, device=self.device if self.native else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        pipeline.max_batches = int(t.item())
+
+    # ------------------------------------------------------------------ train
+    def train(self, batches: Iterable, max_steps: Optional[int] = None,
+              eval_fn: Optional[Callable[[], dict]] = None) -> int:
+        cfg = self.cfg
+        if hasattr(batches, "local_records"):
+            self._enforce_equal_steps(batches)
+        t_log = time.time()
+        n_log = 0
+        start_step = self.global_step
+        use_graph = cfg.graph and self.native
+        t_wait = time.time()
+        for ids, vals, labels in batches:
+            self.timer.add("data_wait", time.time() - t_wait)
+            if max_steps is not None and self.global_step >= max_steps:
+                break
+            t0 = time.time()
+            B = ids.shape[0]
+            if self.native:
+                self.model.train_step(ids.to(self.device, non_blocking=True),
+                                      vals.to(self.device, non_blocking=True),
+                                      labels.to(self.device, non_blocking=True), use_graph=use_graph)
+                if cfg.debug_sync:
+                    torch.cuda.synchronize(self.device)
+                    self._nan_check()
+            else:
+                self.model.train_step(ids, vals, labels, grad_sync=self._golden_grad_sync)
+            self.timer.add("step_enqueue", time.time() - t0)
+            n_log += B
+            step = self.global_step
+            if cfg.log_steps and step % cfg.log_steps == 0:
+                if self.native:
+                    torch.cuda.synchronize(self.device)
+                dt = max(1e-9, time.time() - t_log)
+                loss = self.model.loss_value(B) if self.native else self.model.last_loss
+                sps = n_log / dt
+                self.log.info(f"loss = {loss:.6f}, step = {step} ({dt:.3f} sec)")
+                self.log.info(f"global_step/sec: {cfg.log_steps / dt:.4g}")
+                self.log.log("train", step=step, loss=loss, samples_per_sec_rank=sps,
+                             samples_per_sec_job=sps * self.world, **self.timer.summary(),
+                             comm_bytes=getattr(self.comm, "bytes_sent", 0))
+                t_log, n_log = time.time(), 0
+            if self.ckpt is not None and (
+                    (cfg.save_checkpoints_steps and step % cfg.save_checkpoints_steps == 0) or
+                    (not cfg.save_checkpoints_steps and cfg.save_checkpoints_secs and
+                     time.time() - self._last_save_t >= cfg.save_checkpoints_secs)):
+                self.save()
+            if eval_fn is not None and cfg.eval_every_steps and step % cfg.eval_every_steps == 0:
+                eval_fn()
+            t_wait = time.time()
+        if self.native:
+            torch.cuda.synchronize(self.device)
+        return self.global_step - start_step
+
+    def _nan_check(self):
+        for name, t in (("fm_v", self.model.tv), ("dense", self.model.p)):
+            if not torch.isfinite(t).all():
+                raise FloatingPointError(f"non-finite values in {name} at step {self.global_step}")
+
+    # ------------------------------------------------------------------ evaluate / predict
+    def evaluate(self, batches: Iterable, steps: Optional[int] = None) -> dict:
+        dev = self.device if self.native else torch.device("cpu")
+        hist = torch.zeros(2, 201, dtype=torch.int64, device=dev)
+        loss_sum = torch.zeros(1, dtype=torch.float64, device=dev)
+        n = torch.zeros(1, dtype=torch.float64, device=dev)
+        k = 0
+        for ids, vals, labels in batches:
+            if steps is not None and k >= steps:
+                break
+            B = ids.shape[0]
+            if self.native:
+                self.model.eval_batch(ids.to(dev), vals.to(dev), labels.to(dev), hist)
+                loss_sum += self.model.eval_loss_sum.double()
+            else:
+                with torch.no_grad():
+                    y = self.model.forward(ids, vals, train=False)
+                    p = torch.sigmoid(y)
+                    hist += hist_torch(p, labels)
+                    _, data = self.model.loss(y, labels)
+                    loss_sum += float(data) * B
+            n += B
+            k += 1
+        if _dist_on():
+            dist.all_reduce(hist)
+            dist.all_reduce(loss_sum)
+            dist.all_reduce(n)
+        nn = max(1.0, float(n.item()))
+        data_loss = float(loss_sum.item()) / nn
+        l2 = self.model.l2_value() if self.native else float(
+            self.cfg.l2_reg * 0.5 * ((self.model.params["fm_w"] ** 2).sum() + (self.model.params["fm_v"] ** 2).sum()))
+        res = {"auc": auc_from_hist(hist.cpu()), "loss": data_loss + l2, "logloss": data_loss,
+               "global_step": self.global_step, "examples": int(nn)}
+        self._last_eval_t = time.time()
+        self.log.info("Saving dict for global step %d: auc = %.6f, global_step = %d, loss = %.6f"
+                      % (res["global_step"], res["auc"], res["global_step"], res["loss"]))
+        self.log.log("eval", **res)
+        return res
+
+    def predict(self, batches: Iterable) -> Iterator[torch.Tensor]:
+        for ids, vals, _ in batches:
+            if self.native:
+                yield self.model.predict(ids.to(self.device), vals.to(self.device)).cpu()
+            else:
+                yield self.model.predict(ids, vals)
+
+    # ------------------------------------------------------------------ export
+    def tf_variables(self):
+        if self.native and self.model.sharded:
+            raise NotImplementedError("TF-layout export of a row-sharded table: gather first "
+                                      "(Estimator.export gathers when the table fits)")
+        return self.model.tf_variables()
+
+    def model_config(self) -> dict:
+        c = self.cfg
+        return {"feature_size": c.feature_size, "field_size": c.field_size,
+                "embedding_size": c.embedding_size, "deep_layers": c.layers,
+                "dropout_keep": c.keep_probs, "batch_norm": c.batch_norm, "loss_type": c.loss_type}
+
+    def _gathered_tf_variables(self):
+        """TF view with FULL tables for a row-sharded model: all-gather the shards (rank 0)."""
+        m = self.model
+        if not (self.native and m.sharded):
+            return m.tf_variables()
+        N = m.world
+
+        def gather_rows(local):
+            parts = [torch.empty_like(local) for _ in range(N)]
+            dist.all_gather(parts, local.contiguous())
+            full = torch.empty((m.R * N,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+            for r in range(N):
+                full[r::N] = parts[r]
+            return full[: m.V].cpu()
+        tw, tv = gather_rows(m.tw), gather_rows(m.tv)
+        sv = [gather_rows(s) if s.numel() else s for s in m.sv]
+        return m.tf_variables(tables=(tw, tv, sv))
+
+    def export(self, servable_dir: str) -> Optional[str]:
+        if not servable_dir:
+            return None
+        variables = self._gathered_tf_variables() if self.native else self.model.tf_variables()
+        path = None
+        if self.rank == 0:
+            path = export_servable(variables, self.model_config(), servable_dir)
+            self.log.info(f"SavedModel written to: {path}")
+        if _dist_on():
+            dist.barrier()
+        return path
+
+    def export_tf_checkpoint(self, model_dir: str) -> Optional[str]:
+        """TF1 tensor_bundle ``model.ckpt-<step>`` + ``checkpoint`` state file (§2.7.4)."""
+        from .ckpt.tf_bundle import write_bundle, write_checkpoint_state
+        variables = self._gathered_tf_variables() if self.native else self.model.tf_variables()
+        if self.rank != 0:
+            return None
+        name = f"model.ckpt-{self.global_step}"
+        write_bundle(os.path.join(model_dir, name), variables)
+        write_checkpoint_state(model_dir, name, [name])
+        return os.path.join(model_dir, name)
+
+
+def train_and_evaluate(est: Estimator, train_spec: TrainSpec, eval_spec: EvalSpec) -> dict:
+    """tf.estimator.train_and_evaluate (PS:439-442): train; evaluate after checkpoints once
+    start_delay_secs has passed, at most every throttle_secs; final evaluation at the end."""
+    t0 = time.time()
+    last = {"t": 0.0}
+
+    def maybe_eval():
+        now = time.time()
+        if now - t0 >= eval_spec.start_delay_secs and now - last["t"] >= eval_spec.throttle_secs:
+            last["t"] = now
+            return est.evaluate(eval_spec.input_fn(), eval_spec.steps)
+        return None
+
+    est.train(train_spec.input_fn(), train_spec.max_steps, eval_fn=maybe_eval)
+    est.save()
+    return est.evaluate(eval_spec.input_fn(), eval_spec.steps)

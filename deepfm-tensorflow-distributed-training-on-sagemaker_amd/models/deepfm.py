@@ -607,6 +607,7 @@ class NativeDeepFM:
         B = self.stage_batch(ids, vals, labels)
         self.predict_enqueue(B, with_labels=True)
         KN.auc_hist(self.prob, self.labels, B, hist)
+        self.eval_loss_sum = self.partial[:, -1].sum()     # sum of per-sample data loss (device)
         return B
 
     # ------------------------------------------------------------------ state export
@@ -616,3 +617,92 @@ class NativeDeepFM:
     def sparse_tables_tf(self):
         """fm_w / fm_v of THIS rank (full tables when replicated; local rows when sharded)."""
         return self.tw, self.tv
+
+    # ------------------------------------------------------------------ checkpoint protocol
+    SLOT_NAMES = {"Adam": ("Adam", "Adam_1"), "Adagrad": ("Adagrad", None),
+                  "Momentum": ("Momentum", None), "ftrl": ("Ftrl", "Ftrl_1"), "GD": (None, None)}
+
+    def state_dict_local(self) -> "OrderedDict[str, torch.Tensor]":
+        """This rank's state in native layout (row-sharded tables: local rows only)."""
+        d = OrderedDict(fm_v=self.tv, fm_w=self.tw, dense=self.p, global_step=self.step)
+        for i, t in enumerate(self.sv):
+            if t.numel():
+                d[f"fm_slot{i}"] = t
+        for i, t in enumerate(self.sd):
+            if t.numel():
+                d[f"dense_slot{i}"] = t
+        return d
+
+    def ckpt_meta(self) -> dict:
+        return {"format": "hipfm-native", "V": self.V, "F": self.F, "K": self.K,
+                "layers": self.layers, "keep": self.keep, "optimizer": self.optimizer,
+                "world": self.world, "rank": self.rank, "R": self.R,
+                "sharding": "mod" if self.sharded else "replicated", "P": self.P,
+                "dense_segs": [[s.name, s.off, list(s.shape), list(s.tf_shape)]
+                               for s in self.dense_segs.values()]}
+
+    def load_state_dict_local(self, d: Dict[str, torch.Tensor]):
+        cur = self.state_dict_local()
+        with torch.no_grad():
+            for k, v in d.items():
+                if k in cur:
+                    if cur[k].shape != v.shape:
+                        raise ValueError(f"checkpoint tensor {k}: shape {tuple(v.shape)} != "
+                                         f"model {tuple(cur[k].shape)}")
+                    cur[k].copy_(v.to(cur[k].device, cur[k].dtype))
+        self.refresh_shadows()
+        self._graph = None
+
+    def tf_variables(self, tables=None) -> "OrderedDict[str, torch.Tensor]":
+        """TF1 checkpoint view: reference variable names, [in,out] weights,
+        optimizer slots ``<var>/Adam`` ..., ``beta{1,2}_power``, ``global_step``.
+        ``tables=(fm_w, fm_v, slots...)`` overrides the local tables (gathered full tables)."""
+        out = OrderedDict()
+        dense = self.dense_tf_params()
+        tw, tv = (self.tw, self.tv) if tables is None else tables[:2]
+        sv = self.sv if tables is None else tables[2]
+        out["fm_bias"] = dense["fm_bias"]
+        out["fm_w"], out["fm_v"] = tw, tv
+        for k, v in dense.items():
+            if k != "fm_bias":
+                out[k] = v
+        s0n, s1n = self.SLOT_NAMES[self.optimizer]
+        for slot_i, sname in ((0, s0n), (1, s1n)):
+            if sname is None:
+                continue
+            if self.sd[slot_i].numel():
+                for k, v in self.dense_tf_params(self.sd[slot_i]).items():
+                    out[f"{k}/{sname}"] = v
+            vt, wt = sv[slot_i], sv[2 + slot_i]
+            if vt.numel():
+                out[f"fm_v/{sname}"] = vt
+                out[f"fm_w/{sname}"] = wt
+        t = self.global_step()
+        out["global_step"] = torch.tensor(t, dtype=torch.int64)
+        if self.optimizer == "Adam":
+            out["beta1_power"] = torch.tensor(0.9 ** (t + 1), dtype=torch.float32)
+            out["beta2_power"] = torch.tensor(0.999 ** (t + 1), dtype=torch.float32)
+        return out
+
+    def load_tf_variables(self, tv: Dict[str, torch.Tensor]):
+        """Inverse of ``tf_variables`` for replicated tables (params + slots + step)."""
+        self.load_tf_params({k: torch.as_tensor(v) for k, v in tv.items()
+                             if k in ("fm_w", "fm_v") or k in self.dense_segs})
+        s0n, s1n = self.SLOT_NAMES[self.optimizer]
+        with torch.no_grad():
+            for slot_i, sname in ((0, s0n), (1, s1n)):
+                if sname is None:
+                    continue
+                if self.sd[slot_i].numel():
+                    for name, s in self.dense_segs.items():
+                        key = f"{name}/{sname}"
+                        if key in tv:
+                            self._dense_view(self.sd[slot_i], s).copy_(
+                                self._tf_to_native(name, torch.as_tensor(tv[key])).to(self.device))
+                for tname, dst in (("fm_v", self.sv[slot_i]), ("fm_w", self.sv[2 + slot_i])):
+                    key = f"{tname}/{sname}"
+                    if key in tv and dst.numel() and not self.sharded:
+                        dst.copy_(torch.as_tensor(tv[key]).to(dst))
+            if "global_step" in tv:
+                self.step.fill_(int(torch.as_tensor(tv["global_step"])))
+        self._graph = None

@@ -241,13 +241,40 @@ class GoldenDeepFM:
         grads = torch.autograd.grad(total, [P[n] for n in names])
         return total.detach(), data.detach(), dict(zip(names, grads))
 
-    def train_step(self, ids, vals, labels) -> float:
-        total, _, grads = self.compute_grads(ids, vals, labels)
+    def train_step(self, ids, vals, labels, grad_sync=None) -> float:
+        """One step.  ``grad_sync(grads, touched) -> (grads, touched)`` lets a data-parallel
+        caller average gradients across ranks (Horovod DistributedOptimizer semantics) and
+        union the touched rows before the identical update on every rank."""
+        total, data, grads = self.compute_grads(ids, vals, labels)
         touched = torch.unique(ids.reshape(-1).long())
+        if grad_sync is not None:
+            grads, touched = grad_sync(grads, touched)
         with torch.no_grad():
             self._apply(grads, touched)
         self.global_step += 1
+        self.last_loss = float(data)
         return float(total)
+
+    # ------------------------------------------------------------------ state
+    def state_dict_local(self) -> "OrderedDict[str, torch.Tensor]":
+        """TF-named variables + optimizer slots + global_step (SURVEY §2.7.4 names)."""
+        d = OrderedDict((k, v) for k, v in self.params.items())
+        d.update((k, v) for k, v in self.slots.items())
+        d["global_step"] = torch.tensor(self.global_step, dtype=torch.int64)
+        return d
+
+    def load_state_dict_local(self, d: Dict[str, torch.Tensor]):
+        with torch.no_grad():
+            for k, v in d.items():
+                if k == "global_step":
+                    self.global_step = int(v)
+                elif k in self.params:
+                    self.params[k].copy_(v.to(self.params[k]))
+                elif k in self.slots:
+                    self.slots[k].copy_(v.to(self.slots[k]))
+
+    def tf_variables(self) -> "OrderedDict[str, torch.Tensor]":
+        return self.state_dict_local()
 
     def _apply(self, grads: Dict[str, torch.Tensor], touched: torch.Tensor):
         lr = self.lr
