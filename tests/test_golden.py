@@ -64,7 +64,7 @@ def test_tf1_adam_dense_semantics_touch_every_row():
     # (m/sqrt(v) = (1-b1)/sqrt(1-b2) so the step is ~lr, minus eps=1e-8 against the tiny
     # l2-only gradient of an untouched row)
     d = (g.params["fm_v"][50] - before[50]).abs()
-    assert torch.all(d <= 0.01 * 1.0001) and torch.all(d >= 0.01 * 0.8)
+    assert torch.all(d <= 0.01 * 1.0001) and torch.all(d >= 0.01 * 0.5)
 
 
 def test_lazy_touches_only_batch_rows():
