@@ -30,6 +30,7 @@ import torch
 import torch.distributed as dist
 
 from ..ops import kernels as KN
+from .embedding import Router
 
 
 def init_distributed(backend: Optional[str] = None, timeout_s: int = 600):
@@ -62,7 +63,16 @@ class Comm:
         self.sharded = bool(sharded) and self.world_size > 1
         # steps with host-synchronous routing (variable all-to-all splits) cannot be graphed
         self.graph_safe = self.world_size == 1
-        self.bytes_sent = 0
+        self.router = Router(self.world_size, self.rank, group)
+        self._bytes = 0
+
+    @property
+    def bytes_sent(self) -> int:
+        return self._bytes + self.router.bytes_sent
+
+    @bytes_sent.setter
+    def bytes_sent(self, v: int):
+        self._bytes = v - self.router.bytes_sent
 
     # ------------------------------------------------------------------ dense
     def allreduce_dense_async(self, g: torch.Tensor):
@@ -115,24 +125,15 @@ class Comm:
         KN.unique_inverse(m.sorted_keys, m.perm, n, st["flags"], st["seg"], st["uniq"], st["inv"],
                           m.num_u, m.temp)
         U = int(m.num_u.item())                                   # host sync (routing sizes)
-        uniq = st["uniq"][:U].long()
-        owner = uniq % N
-        order = torch.argsort(owner, stable=True)
-        send_ids = uniq[order].to(torch.int32)
-        send_counts = torch.bincount(owner, minlength=N).to(torch.int64)
-        recv_counts = self._a2a_counts(send_counts)
-        sc, rc = send_counts.tolist(), recv_counts.tolist()
-        recv_ids = torch.empty(sum(rc), **i32)
-        self._a2a(recv_ids, send_ids, rc, sc)
-        rows = torch.empty(recv_ids.numel(), K + 1, dtype=torch.float32, device=dev)
-        loc = (recv_ids // N).long()
-        rows[:, :K] = m.tv.index_select(0, loc)
-        rows[:, K] = m.tw.index_select(0, loc)
-        got = torch.empty(U, K + 1, dtype=torch.float32, device=dev)
-        self._a2a(got, rows, sc, rc)
-        rows_u = torch.empty_like(got)
-        rows_u[order] = got
-        st.update(U=U, order=order, sc=sc, rc=rc, recv_ids=recv_ids)
+        plan = self.router.route(st["uniq"][:U])
+
+        def serve(loc):
+            rows = torch.empty(loc.numel(), K + 1, dtype=torch.float32, device=dev)
+            rows[:, :K] = m.tv.index_select(0, loc)
+            rows[:, K] = m.tw.index_select(0, loc)
+            return rows
+        rows_u = self.router.fetch_rows(plan, serve)
+        st.update(U=U, plan=plan)
         st["tv_rows"] = rows_u[:, :K].contiguous()
         st["tw_rows"] = rows_u[:, K].contiguous()
         return st["inv"], st["tv_rows"], st["tw_rows"]
@@ -144,11 +145,8 @@ class Comm:
         gr = KN.grad_row_floats(K)
         m._segment_reduce(n, compact=True)
         KN.seg_apply(K, KN.SEG_WRITE_UG, 0, m.seg_args(n, compact=True, vsrc=tv, vsrc_compact=True), n)
-        U = st["U"]
-        send = m.UG[:U].index_select(0, st["order"])
-        recv = torch.empty(len(st["recv_ids"]), gr, dtype=torch.float32, device=m.device)
-        self._a2a(recv, send, st["rc"], st["sc"])
-        return self._owner_reduce(m, st["recv_ids"], recv)
+        ids, recv = self.router.push_grads(st["plan"], m.UG[: st["U"]])
+        return self._owner_reduce(m, ids, recv)
 
     def _owner_reduce(self, m, keys: torch.Tensor, rows: torch.Tensor):
         """Deduplicate received (global id, grad row) pairs on the owner (sort + reduce)."""

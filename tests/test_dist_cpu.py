@@ -1,0 +1,136 @@
+"""Multi-process data parallelism on CPU with gloo: the row-sharded
+all-to-all algorithm and the replicated (Horovod-parity) gradient averaging both reproduce a
+single-process run on the global batch; distributed evaluation sums AUC histograms."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import hipfm
+
+V, F, K, LAYERS = 600, 6, 4, [8]
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _batches(steps, B):
+    g = torch.Generator().manual_seed(5)
+    out = []
+    for _ in range(steps):
+        ids = torch.randint(0, V, (B, F), generator=g)
+        ids[:, 0] = 3                                         # a hot id shared by every row
+        out.append((ids, torch.rand(B, F, generator=g), (torch.rand(B, generator=g) < 0.4).float()))
+    return out
+
+
+def _worker(rank, world, port, mode, opt, update, q):
+    try:
+        _worker_body(rank, world, port, mode, opt, update, q)
+    except BaseException:
+        import traceback
+        q.put({"error": traceback.format_exc()})
+        raise
+
+
+def _worker_body(rank, world, port, mode, opt, update, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from hipfm.models.reference import GoldenDeepFM, init_params
+    from hipfm.parallel.embedding import make_sharded_golden
+    params = init_params(V, F, K, LAYERS, False, seed=9)
+    kw = dict(keep_probs=[1.0], optimizer=opt, sparse_update=update, learning_rate=0.01, params=params)
+    B = 32
+    data = _batches(4, B * world)
+    if mode == "sharded":
+        m = make_sharded_golden(V, F, K, LAYERS, world=world, rank=rank, **kw)
+        for ids, vals, lab in data:
+            sl = slice(rank * B, (rank + 1) * B)
+            m.train_step(ids[sl], vals[sl], lab[sl])
+        fv, fw = m.full_table("fm_v"), m.full_table("fm_w")
+        dense = {k: v for k, v in m.params.items() if k.startswith("Deep") or k == "fm_bias"}
+    else:
+        from hipfm.config import parse_flags
+        m = GoldenDeepFM(V, F, K, LAYERS, world_size=world, **kw)
+
+        def sync(grads, touched):
+            out = {}
+            for k, g in grads.items():
+                t = g.contiguous().clone()
+                dist.all_reduce(t)
+                out[k] = t / world
+            mask = torch.zeros(V, dtype=torch.int32)
+            mask[touched] = 1
+            dist.all_reduce(mask, op=dist.ReduceOp.MAX)
+            return out, torch.nonzero(mask).reshape(-1)
+        for ids, vals, lab in data:
+            sl = slice(rank * B, (rank + 1) * B)
+            m.train_step(ids[sl], vals[sl], lab[sl], grad_sync=sync)
+        fv, fw = m.params["fm_v"], m.params["fm_w"]
+        dense = {k: v for k, v in m.params.items() if k.startswith("Deep") or k == "fm_bias"}
+    if rank == 0:
+        q.put({"fm_v": fv.clone(), "fm_w": fw.clone(), **{k: v.clone() for k, v in dense.items()}})
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode,opt,update", [("sharded", "Adam", "tf1_dense"), ("sharded", "Adam", "lazy"),
+                                             ("sharded", "Adagrad", "lazy"), ("replicated", "Adam", "tf1_dense"),
+                                             ("replicated", "ftrl", "lazy")])
+def test_dp_matches_single_process_global_batch(mode, opt, update):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, mode, opt, update, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=240)
+    assert "error" not in got, got.get("error")
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    from hipfm.models.reference import GoldenDeepFM, init_params
+    params = init_params(V, F, K, LAYERS, False, seed=9)
+    ref = GoldenDeepFM(V, F, K, LAYERS, [1.0], optimizer=opt, sparse_update=update, learning_rate=0.01,
+                       world_size=world, params=params)
+    for ids, vals, lab in _batches(4, 32 * world):
+        ref.train_step(ids, vals, lab)
+    for k, v in got.items():
+        assert torch.allclose(v, ref.params[k], atol=2e-6, rtol=1e-5), (k, (v - ref.params[k]).abs().max())
+
+
+def _eval_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from hipfm.ops.metrics import auc_from_hist, hist_torch
+    g = torch.Generator().manual_seed(1)
+    p = torch.rand(4000, generator=g)
+    y = (torch.rand(4000, generator=g) < p).float()
+    h = hist_torch(p[rank::world], y[rank::world])
+    dist.all_reduce(h)
+    if rank == 0:
+        q.put((auc_from_hist(h), auc_from_hist(hist_torch(p, y))))
+    dist.destroy_process_group()
+
+
+def test_distributed_eval_histogram_allreduce():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_eval_worker, args=(r, 3, port, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    a, b = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+    assert a == b
