@@ -119,6 +119,8 @@ class NativeDeepFM:
         self.seed = int(seed)
         self.device = torch.device(device)
         self.sharded = comm is not None and comm.sharded
+        # multi-rank code path (also forced on a 1-rank group by tests: comm.force_exchange)
+        self.exchange = comm is not None and (self.world > 1 or getattr(comm, "force_exchange", False))
         # local rows of the embedding tables (row-sharded: id -> rank id % N, row id // N)
         self.R = (self.V + self.world - 1) // self.world if self.sharded else self.V
         self.row_div = self.world if self.sharded else 1
@@ -490,7 +492,7 @@ class NativeDeepFM:
         if self.sharded:
             return self.comm.sharded_backward(self, B, idx, tv)
         KN.sort_ids(self.idx, self.sorted_keys, None, self.perm, n, self.end_bit, self.temp)
-        if self.comm is None or self.world == 1:
+        if not self.exchange:
             self._segment_reduce(n, compact=False)
             A = self.seg_args(n, compact=False)
             if self.sparse_update == "lazy":
@@ -531,7 +533,7 @@ class NativeDeepFM:
         self._head(B, train=True)
         self._mlp_backward()
         work = None
-        if self.comm is not None and self.world > 1:
+        if self.exchange:
             work = self.comm.allreduce_dense_async(self.g)
         out = self._sparse_backward(B, idx, tv)
         if out is not None:

@@ -56,13 +56,15 @@ def world_info():
 class Comm:
     """Collective engine used by NativeDeepFM for one process group."""
 
-    def __init__(self, sharded: bool = True, group=None):
+    def __init__(self, sharded: bool = True, group=None, force_exchange: bool = False):
         self.group = group
         self.rank = dist.get_rank(group)
         self.world_size = dist.get_world_size(group)
-        self.sharded = bool(sharded) and self.world_size > 1
+        # force_exchange: run the multi-rank code path even on a 1-rank group (tests on 1 GPU)
+        self.force_exchange = bool(force_exchange)
+        self.sharded = bool(sharded) and (self.world_size > 1 or self.force_exchange)
         # steps with host-synchronous routing (variable all-to-all splits) cannot be graphed
-        self.graph_safe = self.world_size == 1
+        self.graph_safe = self.world_size == 1 and not self.force_exchange
         self.router = Router(self.world_size, self.rank, group)
         self._bytes = 0
 

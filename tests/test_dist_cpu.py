@@ -134,3 +134,32 @@ def test_distributed_eval_histogram_allreduce():
     for p in procs:
         p.join(timeout=60)
     assert a == b
+
+
+def test_launcher_cli_two_ranks_gloo(tmp_path):
+    """python -m hipfm.launch --nproc_per_node 2 -m hipfm ... on CPU/gloo: both ranks train on
+    disjoint file shards, evaluate their shard (histograms all-reduced) and save one checkpoint."""
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    d = tmp_path / "data"
+    subprocess.check_call([sys.executable, os.path.join(repo, "tools", "gen_synthetic_criteo.py"),
+                           "--out", str(d), "--preset", "total:8000", "--train_rows", "2048",
+                           "--val_rows", "512", "--files", "4"], cwd=repo)
+    md = tmp_path / "model"
+    env = dict(os.environ, PYTHONPATH=repo)
+    r = subprocess.run([sys.executable, "-m", "hipfm.launch", "--nproc_per_node", "2",
+                        "--master_port", str(_port()), "-m", "hipfm", "--task_type", "train",
+                        "--training_data_dir", str(d), "--val_data_dir", str(d), "--model_dir", str(md),
+                        "--feature_size", "8000", "--field_size", "39", "--embedding_size", "4",
+                        "--batch_size", "64", "--deep_layers", "16", "--dropout", "1.0",
+                        "--num_epochs", "1", "--device", "cpu", "--log_steps", "4"],
+                       cwd=repo, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "auc = " in r.stdout
+    import json as _json
+    idx = _json.load(open(md / "hipfm_checkpoint.json"))
+    # 2048 rows / 2 ranks / 64 per batch = 16 steps (same on both ranks: equal-steps rule)
+    assert idx["latest"] == "ckpt-16"
+    man = _json.load(open(md / "ckpt-16" / "manifest.json"))
+    assert man["world"] == 2 and os.path.exists(md / "ckpt-16" / "rank1.bin")

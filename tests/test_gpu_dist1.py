@@ -1,0 +1,57 @@
+"""The multi-rank executor code paths on ONE GPU: a 1-rank RCCL group with ``force_exchange``
+runs the full row-sharded (sort -> unique -> all-to-all ids/rows -> fused backward -> all-to-all
+grads -> owner dedup -> row update) and replicated (all-gather of unique rows) paths, which must
+reproduce the single-rank fused path.  Real 2..8-GPU runs happen in the driver's scaling bench."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+
+pytestmark = pytest.mark.gpu
+if not torch.cuda.is_available():
+    pytest.skip("needs a GPU", allow_module_level=True)
+
+import hipfm  # noqa: E402
+from hipfm.data.synthetic import make_synth  # noqa: E402
+from hipfm.models.deepfm import NativeDeepFM  # noqa: E402
+from hipfm.models.reference import init_params  # noqa: E402
+from hipfm.parallel.dist import Comm  # noqa: E402
+
+
+@pytest.fixture(scope="module")
+def group():
+    if not dist.is_initialized():
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+        s.close()
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1",
+                          LOCAL_RANK="0")
+        torch.cuda.set_device(0)
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    yield
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("sharded,update", [(True, "lazy"), (True, "tf1_dense"), (False, "lazy")])
+def test_exchange_paths_match_local(group, sharded, update):
+    synth = make_synth("total:6000", seed=21)
+    F, K, layers, keep = synth.F, 8, [64, 32], [0.8, 0.8]
+    V = synth.feature_size
+    params = init_params(V, F, K, layers, False, seed=2)
+    kw = dict(sparse_update=update, batch_size=512, device="cuda", init=False)
+    a = NativeDeepFM(V, F, K, layers, keep, **kw)
+    b = NativeDeepFM(V, F, K, layers, keep, comm=Comm(sharded=sharded, force_exchange=True), **kw)
+    a.load_tf_params(params)
+    b.load_tf_params(params)
+    assert b.exchange and b.sharded == sharded
+    for s in range(4):
+        ids, vals, labels = synth.batch(512, step=s, device="cuda", id_dtype=torch.int32)
+        a.train_step(ids, vals, labels)
+        b.train_step(ids, vals, labels, use_graph=True)    # graph refused -> eager exchange
+    torch.cuda.synchronize()
+    assert torch.allclose(a.tv, b.tv, atol=1e-6) and torch.allclose(a.tw, b.tw, atol=1e-6)
+    assert torch.allclose(a.p, b.p, atol=1e-6)
+    assert b.comm.bytes_sent > 0
