@@ -82,6 +82,8 @@ def main():
             for i in range(args.pool)]
     use_graph = not args.no_graph
     torch.cuda.synchronize()
+    if use_graph and (comm is None or comm.graph_safe):
+        model.precapture(pool)        # one HIP graph per resident batch, captured before timing
 
     def run(nsteps, start):
         for s in range(nsteps):

@@ -138,3 +138,201 @@ HFM_API int hfm_radix_sort_ids(const int* keys_in, int* keys_out, int* perm_out,
   }
   HFM_LAUNCH_CHECK();
 }
+
+// =============================================================================================
+// Onesweep variant: ONE global-histogram kernel for all digit passes + ONE kernel per pass that
+// ranks its tile, finds its per-digit offset with a decoupled look-back over the earlier tiles,
+// and scatters.  4 passes (30-bit ids) = 1 memset + 5 launches instead of 16.
+//
+// Inter-workgroup protocol (guide §6 Guideline 16, "R2: the data IS the flag"): each tile
+// publishes, per digit, one 32-bit word {2-bit state | 30-bit count} with a relaxed agent-scope
+// atomic store — state 1 = this tile's own count (aggregate), 2 = inclusive prefix through this
+// tile.  A tile resolves its exclusive prefix by polling earlier tiles' words (relaxed agent
+// loads) back to the first inclusive one.  Tiles are handed out by an atomic ticket, so a tile
+// only ever waits on tiles already owned by running workgroups (no dispatch-order assumption).
+// Spins are bounded; a timeout sets an error word instead of hanging the GPU.
+// The status words and tickets are zeroed by a hipMemsetAsync node before every sort.
+namespace {
+constexpr int OS_ITEMS = 8;
+constexpr int OS_TILE = RS_THREADS * OS_ITEMS;      // 2048 keys per tile
+constexpr unsigned OS_AGG = 1u << 30, OS_INC = 2u << 30, OS_VAL = (1u << 30) - 1;
+constexpr int OS_MAX_PASSES = 4;
+}  // namespace
+
+__global__ void __launch_bounds__(RS_THREADS) os_hist_kernel(const int* __restrict__ keys, int n,
+                                                            int passes, unsigned* __restrict__ ghist) {
+  __shared__ unsigned h[OS_MAX_PASSES][RS_RADIX];
+  for (int p = 0; p < passes; ++p) h[p][threadIdx.x] = 0;
+  __syncthreads();
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const int k = keys[i];
+    for (int p = 0; p < passes; ++p) atomicAdd(&h[p][(k >> (p * RS_BITS)) & (RS_RADIX - 1)], 1u);
+  }
+  __syncthreads();
+  for (int p = 0; p < passes; ++p)
+    if (h[p][threadIdx.x]) atomicAdd(&ghist[p * RS_RADIX + threadIdx.x], h[p][threadIdx.x]);
+}
+
+__global__ void __launch_bounds__(RS_THREADS) os_pass_kernel(
+    const int* __restrict__ keys_in, const int* __restrict__ vals_in, int* __restrict__ keys_out,
+    int* __restrict__ vals_out, int n, int shift, const unsigned* __restrict__ ghist_p,
+    unsigned* __restrict__ status, unsigned* __restrict__ ticket, unsigned* __restrict__ err) {
+  __shared__ int cnt[RS_RADIX];
+  __shared__ int wcnt[4][RS_RADIX];
+  __shared__ int base[RS_RADIX];
+  __shared__ unsigned tile_s;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  if (tid == 0) tile_s = atomicAdd(ticket, 1u);
+  cnt[tid] = 0;
+  wcnt[0][tid] = wcnt[1][tid] = wcnt[2][tid] = wcnt[3][tid] = 0;
+  __syncthreads();
+  const int tile = (int)tile_s;
+  const int b0 = tile * OS_TILE;
+  int kr[OS_ITEMS], vr[OS_ITEMS], dr[OS_ITEMS];
+#pragma unroll
+  for (int k = 0; k < OS_ITEMS; ++k) {
+    const int i = b0 + k * RS_THREADS + tid;
+    kr[k] = i < n ? keys_in[i] : 0;
+    vr[k] = i < n ? (vals_in ? vals_in[i] : i) : 0;
+    dr[k] = (kr[k] >> shift) & (RS_RADIX - 1);
+  }
+  // tile histogram (LDS atomics) -> publish the aggregate as early as possible
+  __shared__ int th[RS_RADIX];
+  th[tid] = 0;
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < OS_ITEMS; ++k)
+    if (b0 + k * RS_THREADS + tid < n) atomicAdd(&th[dr[k]], 1);
+  __syncthreads();
+  const unsigned mine = (unsigned)th[tid];
+  unsigned* st = status + (size_t)tile * RS_RADIX;
+  __hip_atomic_store(&st[tid], (tile == 0 ? OS_INC : OS_AGG) | mine, __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+  // global digit base: exclusive scan of this pass's global histogram (in LDS)
+  base[tid] = (int)ghist_p[tid];
+  __syncthreads();
+  for (int off = 1; off < RS_RADIX; off <<= 1) {
+    const int v = tid >= off ? base[tid - off] : 0;
+    __syncthreads();
+    base[tid] += v;
+    __syncthreads();
+  }
+  int excl_digit = base[tid] - (int)ghist_p[tid];
+  // decoupled look-back over earlier tiles for digit tid, 16 predecessors per round (the 16
+  // status loads are independent and issued together; a round costs ~one L2 round trip)
+  unsigned prefix = 0;
+  if (tile > 0) {
+    constexpr int W = 16;
+    int j = tile - 1;
+    unsigned spins = 0;
+    while (j >= 0) {
+      unsigned w[W];
+#pragma unroll
+      for (int q = 0; q < W; ++q)
+        w[q] = (j - q >= 0) ? __hip_atomic_load(&status[(size_t)(j - q) * RS_RADIX + tid],
+                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                            : OS_INC;
+      // usable prefix of the window: stop at the first not-yet-published word
+      unsigned acc = 0;
+      int q = 0;
+      bool done = false;
+      for (; q < W; ++q) {
+        const unsigned state = w[q] & ~OS_VAL;
+        if (state == 0) break;
+        if (j - q < 0) { done = true; break; }
+        acc += w[q] & OS_VAL;
+        if (state == OS_INC) { done = true; break; }
+      }
+      prefix += acc;
+      if (done) break;
+      if (q == 0) {
+        if (++spins > (1u << 22)) { atomicExch(err, 1u); break; }
+        __builtin_amdgcn_s_sleep(1);
+        continue;
+      }
+      j -= q;   // consumed q aggregates; continue below them
+    }
+    __hip_atomic_store(&st[tid], OS_INC | (prefix + mine), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  base[tid] = excl_digit + (int)prefix;
+  __syncthreads();
+  const unsigned long long lt = (1ull << lane) - 1ull;
+#pragma unroll
+  for (int k = 0; k < OS_ITEMS; ++k) {
+    const int i = b0 + k * RS_THREADS + tid;
+    const bool valid = i < n;
+    const int d = dr[k];
+    unsigned long long peers = __ballot(valid);
+#pragma unroll
+    for (int bit = 0; bit < RS_BITS; ++bit) {
+      const bool bset = (d >> bit) & 1;
+      const unsigned long long bal = __ballot(bset);
+      peers &= bset ? bal : ~bal;
+    }
+    const int rk = __popcll(peers & lt);
+    if (valid && rk == 0) wcnt[wv][d] = __popcll(peers);
+    __syncthreads();
+    if (valid) {
+      int r = cnt[d] + rk;
+      for (int w = 0; w < wv; ++w) r += wcnt[w][d];
+      const int dst = base[d] + r;
+      keys_out[dst] = kr[k];
+      vals_out[dst] = vr[k];
+    }
+    __syncthreads();
+    cnt[tid] += wcnt[0][tid] + wcnt[1][tid] + wcnt[2][tid] + wcnt[3][tid];
+    wcnt[0][tid] = wcnt[1][tid] = wcnt[2][tid] = wcnt[3][tid] = 0;
+    __syncthreads();
+  }
+}
+
+static inline int os_tiles(int n) { return (n + OS_TILE - 1) / OS_TILE; }
+
+// workspace: [zeroed block: ghist P*256 | tickets P | err 1 | pad][status P*tiles*256][ping k][ping v]
+HFM_API int hfm_onesweep_temp_bytes(int n, size_t* bytes) {
+  const size_t tiles = os_tiles(n);
+  *bytes = 8192 + (size_t)OS_MAX_PASSES * tiles * RS_RADIX * 4 + (size_t)n * 8 + 1024;
+  return 0;
+}
+
+HFM_API int hfm_onesweep_sort_ids(const int* keys_in, int* keys_out, int* perm_out, int n, int end_bit,
+                                  void* temp, size_t temp_bytes, hipStream_t st) {
+  if (n <= 0) return 0;
+  const int tiles = os_tiles(n);
+  const int passes = (end_bit + RS_BITS - 1) / RS_BITS;
+  if (passes > OS_MAX_PASSES) return (int)hipErrorInvalidValue;
+  size_t need;
+  hfm_onesweep_temp_bytes(n, &need);
+  if (temp_bytes < need) return (int)hipErrorInvalidValue;
+  char* t = (char*)temp;
+  unsigned* ghist = (unsigned*)t;                          // P*256
+  unsigned* tickets = ghist + OS_MAX_PASSES * RS_RADIX;    // P
+  unsigned* err = tickets + OS_MAX_PASSES;                 // 1
+  unsigned* status = (unsigned*)(t + 8192);
+  const size_t status_words = (size_t)passes * tiles * RS_RADIX;
+  int* pk = (int*)(((uintptr_t)(status + (size_t)OS_MAX_PASSES * tiles * RS_RADIX) + 255) & ~(uintptr_t)255);
+  int* pv = pk + n;
+  // one memset node zeroes histogram, tickets, error word and this sort's status words
+  hipError_t e = hipMemsetAsync(t, 0, 8192 + status_words * 4, st);
+  if (e != hipSuccess) return (int)e;
+  int hg = (n + RS_THREADS - 1) / RS_THREADS;
+  if (hg > 1024) hg = 1024;
+  hipLaunchKernelGGL(os_hist_kernel, dim3(hg), dim3(RS_THREADS), 0, st, keys_in, n, passes, ghist);
+  const int* ki = keys_in;
+  const int* vi = nullptr;
+  for (int p = 0; p < passes; ++p) {
+    const bool to_out = ((passes - 1 - p) % 2) == 0;
+    int* ko = to_out ? keys_out : pk;
+    int* vo = to_out ? perm_out : pv;
+    hipLaunchKernelGGL(os_pass_kernel, dim3(tiles), dim3(RS_THREADS), 0, st, ki, vi, ko, vo, n,
+                       p * RS_BITS, ghist + p * RS_RADIX, status + (size_t)p * tiles * RS_RADIX,
+                       tickets + p, err);
+    ki = ko;
+    vi = vo;
+  }
+  HFM_LAUNCH_CHECK();
+}
+
+// error word of the last onesweep sort in `temp` (1 = a look-back spin timed out)
+HFM_API int hfm_onesweep_error_offset() { return (OS_MAX_PASSES * RS_RADIX + OS_MAX_PASSES) * 4; }

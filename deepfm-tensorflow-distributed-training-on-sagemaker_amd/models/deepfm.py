@@ -276,6 +276,9 @@ class NativeDeepFM:
         self.temp = torch.zeros(tb + 256, dtype=torch.uint8, device=dev)
         self._build_finalize_jobs()
         self._bufs_M = M
+        self._own_in = (self.idx, self.vals, self.labels)
+        self._graphs = {}
+        self.max_graphs = 256
         self._graph = None
 
     def _build_finalize_jobs(self):
@@ -370,6 +373,7 @@ class NativeDeepFM:
     # ------------------------------------------------------------------ batch staging
     def stage_batch(self, ids: torch.Tensor, vals: torch.Tensor, labels: Optional[torch.Tensor]):
         """Copy a batch into the static input buffers (device->device when already resident)."""
+        self.idx, self.vals, self.labels = self._own_in
         B = ids.shape[0]
         M = self._padM(B)
         if M > self._bufs_M:
@@ -561,26 +565,62 @@ class NativeDeepFM:
         return self.g.clone(), self.ukeys[:U].clone(), self.UG[:U].clone()
 
     def train_step(self, ids, vals, labels, use_graph: bool = False):
-        B = self.stage_batch(ids, vals, labels)
+        """One training step.  A device-resident int32 batch whose size equals the allocated
+        batch is bound in place (no staging copy); with ``use_graph`` each such resident batch
+        gets its own captured HIP graph (the HBM-cached epoch replays graphs back to back)."""
+        direct = (ids.is_cuda and ids.dtype == torch.int32 and vals.dtype == torch.float32 and
+                  ids.is_contiguous() and vals.is_contiguous() and labels.is_contiguous() and
+                  ids.shape[0] == self.M and ids.numel() == self.M * self.F)
+        if direct:
+            B = ids.shape[0]
+            self.idx, self.vals, self.labels = ids.reshape(-1), vals.reshape(-1), labels.reshape(-1)
+            key = (ids.data_ptr(), vals.data_ptr(), labels.data_ptr(), B)
+        else:
+            self.idx, self.vals, self.labels = self._own_in
+            B = self.stage_batch(ids, vals, labels)
+            key = ("staged", B)
         if use_graph and (self.comm is None or self.comm.graph_safe):
-            self._replay_graph(B)
+            self._replay_graph(key, B)
         else:
             self.train_step_enqueue(B)
         return B
 
-    def _replay_graph(self, B: int):
-        if self._graph is None or self._graph_B != B:
-            # The first step of a batch shape runs eagerly (it is a real step: it also warms up
-            # hipCUB/RCCL lazy init), then the step is captured (capture records, it does not
-            # execute) and every later step is one graph replay.
-            self.train_step_enqueue(B)
-            torch.cuda.synchronize()
+    def _replay_graph(self, key, B: int):
+        g = self._graphs.get(key)
+        if g is None:
+            # The very first step runs eagerly (it is a real step and warms up lazy library
+            # state), then it is captured (capture records, it does not execute); every later
+            # step of the same input binding is one graph replay.
+            if not self._graphs:
+                self.train_step_enqueue(B)
+                torch.cuda.synchronize()
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    self.train_step_enqueue(B)
+                self._graphs[key] = g
+                return
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
                 self.train_step_enqueue(B)
-            self._graph, self._graph_B = g, B
-            return
-        self._graph.replay()
+            if len(self._graphs) >= self.max_graphs:
+                self._graphs.pop(next(iter(self._graphs)))
+            self._graphs[key] = g
+        g.replay()
+
+    def precapture(self, batches):
+        """Capture the graphs of resident batches up front (keeps capture out of timed loops)."""
+        for ids, vals, labels in batches:
+            if not self._graphs:
+                self.train_step(ids, vals, labels, use_graph=True)   # eager first step + capture
+                continue
+            self.idx, self.vals, self.labels = ids.reshape(-1), vals.reshape(-1), labels.reshape(-1)
+            key = (ids.data_ptr(), vals.data_ptr(), labels.data_ptr(), ids.shape[0])
+            if key not in self._graphs:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    self.train_step_enqueue(ids.shape[0])
+                self._graphs[key] = g
+        torch.cuda.synchronize()
 
     def loss_value(self, B: int, include_l2: bool = False) -> float:
         """Mean data loss of the last step (+ l2 terms over the whole tables if asked)."""
@@ -653,7 +693,7 @@ class NativeDeepFM:
                                          f"model {tuple(cur[k].shape)}")
                     cur[k].copy_(v.to(cur[k].device, cur[k].dtype))
         self.refresh_shadows()
-        self._graph = None
+        self._graphs = {}
 
     def tf_variables(self, tables=None) -> "OrderedDict[str, torch.Tensor]":
         """TF1 checkpoint view: reference variable names, [in,out] weights,
@@ -707,4 +747,4 @@ class NativeDeepFM:
                         dst.copy_(torch.as_tensor(tv[key]).to(dst))
             if "global_step" in tv:
                 self.step.fill_(int(torch.as_tensor(tv["global_step"])))
-        self._graph = None
+        self._graphs = {}

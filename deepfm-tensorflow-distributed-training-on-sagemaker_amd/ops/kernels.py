@@ -59,9 +59,12 @@ def scan_temp_bytes(n: int) -> int:
 
 
 def radix_temp_bytes(n: int) -> int:
+    """Workspace bytes for ``sort_ids`` (covers both sort implementations)."""
     b = C.c_size_t(0)
     check(L().hfm_radix_sort_temp_bytes(n, C.byref(b)), "radix_temp")
-    return b.value
+    b2 = C.c_size_t(0)
+    check(L().hfm_onesweep_temp_bytes(n, C.byref(b2)), "onesweep_temp")
+    return max(b.value, b2.value)
 
 
 def cub_sort_ids(keys_in, keys_out, vals_tmp, perm_out, n, end_bit, temp):
@@ -70,11 +73,34 @@ def cub_sort_ids(keys_in, keys_out, vals_tmp, perm_out, n, end_bit, temp):
                            ptr(temp), temp.numel(), stream_handle()), "cub_sort_ids")
 
 
-def sort_ids(keys_in, keys_out, vals_tmp, perm_out, n, end_bit, temp):
-    """Stable sort of slot ids -> (sorted keys, slot permutation): csrc/kernels/radix_sort.hip.
-    ``temp`` must hold max(radix_temp_bytes(n), ...) bytes; ``vals_tmp`` is unused."""
+def lsd_sort_ids(keys_in, keys_out, perm_out, n, end_bit, temp):
+    """Classic 3-kernel-per-pass LSD radix sort (A/B reference for the onesweep sort)."""
     check(L().hfm_radix_sort_ids(ptr(keys_in), ptr(keys_out), ptr(perm_out), n, end_bit, ptr(temp),
                                  temp.numel(), stream_handle()), "radix_sort_ids")
+
+
+def onesweep_sort_ids(keys_in, keys_out, perm_out, n, end_bit, temp):
+    """Onesweep radix sort (global histogram + one decoupled-look-back pass per 8 bits)."""
+    check(L().hfm_onesweep_sort_ids(ptr(keys_in), ptr(keys_out), ptr(perm_out), n, end_bit,
+                                    ptr(temp), temp.numel(), stream_handle()), "onesweep_sort_ids")
+
+
+SORT_IMPL = "lsd"   # A/B measured in tools/bench_sort.py; the faster one is the default
+
+
+def sort_ids(keys_in, keys_out, vals_tmp, perm_out, n, end_bit, temp):
+    """Stable sort of slot ids -> (sorted keys, slot permutation) (csrc/kernels/radix_sort.hip).
+    ``temp`` must hold radix_temp_bytes(n) bytes; ``vals_tmp`` is unused."""
+    if SORT_IMPL == "onesweep":
+        onesweep_sort_ids(keys_in, keys_out, perm_out, n, end_bit, temp)
+    else:
+        lsd_sort_ids(keys_in, keys_out, perm_out, n, end_bit, temp)
+
+
+def sort_error(temp) -> int:
+    """1 if the last onesweep sort in ``temp`` timed out in its look-back (device read: syncs)."""
+    off = L().hfm_onesweep_error_offset()
+    return int(temp[off: off + 4].view(torch.int32).item())
 
 
 def reduce_by_key(K, sorted_keys, G, ukeys, UG, num, n, temp):

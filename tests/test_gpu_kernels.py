@@ -142,11 +142,18 @@ def test_radix_sort_stable(n, bits):
     sk = torch.zeros_like(keys)
     perm = torch.zeros_like(keys)
     temp = torch.zeros(KN.radix_temp_bytes(n), dtype=torch.uint8, device=DEV)
-    KN.sort_ids(keys, sk, None, perm, n, bits, temp)
-    torch.cuda.synchronize()
     ref_k, ref_p = torch.sort(keys.long(), stable=True)
-    assert torch.equal(sk.long(), ref_k)
-    assert torch.equal(perm.long(), ref_p)
+    for fn in (lambda: KN.onesweep_sort_ids(keys, sk, perm, n, bits, temp),
+               lambda: KN.lsd_sort_ids(keys, sk, perm, n, bits, temp),
+               lambda: KN.sort_ids(keys, sk, None, perm, n, bits, temp)):
+        sk.zero_()
+        perm.zero_()
+        fn()
+        torch.cuda.synchronize()
+        assert torch.equal(sk.long(), ref_k)
+        assert torch.equal(perm.long(), ref_p)
+        if fn.__code__.co_names[-1] == "onesweep_sort_ids":
+            assert KN.sort_error(temp) == 0
 
 
 def test_auc_hist_matches_torch():

@@ -29,10 +29,11 @@ def main():
             tmp = torch.empty_like(keys)
             temp = torch.empty(max(KN.sort_temp_bytes(n, bits), KN.radix_temp_bytes(n)) + 256,
                                dtype=torch.uint8, device=dev)
-            t0 = timeit(lambda: KN.sort_ids(keys, sk, tmp, perm, n, bits, temp))
+            t0 = timeit(lambda: KN.onesweep_sort_ids(keys, sk, perm, n, bits, temp))
+            tl = timeit(lambda: KN.lsd_sort_ids(keys, sk, perm, n, bits, temp))
             t1 = timeit(lambda: KN.cub_sort_ids(keys, sk, tmp, perm, n, bits, temp))
             t2 = timeit(lambda: torch.sort(keys, stable=True))
-            print(f"n={n:8d} bits={bits}: hipfm radix {t0:8.1f} us  hipcub SortPairs {t1:8.1f} us   "
+            print(f"n={n:8d} bits={bits}: onesweep {t0:8.1f} us  lsd {tl:8.1f} us  hipcub SortPairs {t1:8.1f} us   "
                   f"torch.sort {t2:8.1f} us", flush=True)
 
 
