@@ -53,15 +53,40 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_nt_kernel(
 
   f32x4 c00 = {0, 0, 0, 0}, c01 = c00, c10 = c00, c11 = c00;
 
-  for (int k = 0; k < kchunk; k += 32) {
-    const bf16x8 fa0 = *reinterpret_cast<const bf16x8*>(a0 + k);
-    const bf16x8 fa1 = *reinterpret_cast<const bf16x8*>(a1 + k);
-    const bf16x8 fb0 = *reinterpret_cast<const bf16x8*>(b0 + k);
-    const bf16x8 fb1 = *reinterpret_cast<const bf16x8*>(b1 + k);
-    c00 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa0, fb0, c00, 0, 0, 0);
-    c01 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa0, fb1, c01, 0, 0, 0);
-    c10 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa1, fb0, c10, 0, 0, 0);
-    c11 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa1, fb1, c11, 0, 0, 0);
+  // Register ring of PF k-steps: the fragments of step k+PF are requested while step k is
+  // multiplied, so PF x 4 KB of loads per wave are in flight.  These GEMMs are short in
+  // MFMA work (4 MFMAs per 4 fragment loads) and latency-bound without it: one wave per
+  // SIMD, 10 k-steps, each waiting a full memory round trip (measured 14 us -> see profiles/).
+  constexpr int PF = 4;
+  const int nsteps = kchunk / 32;
+  bf16x8 ra0[PF], ra1[PF], rb0[PF], rb1[PF];
+#pragma unroll
+  for (int j = 0; j < PF; ++j) {
+    if (j < nsteps) {
+      ra0[j] = *reinterpret_cast<const bf16x8*>(a0 + j * 32);
+      ra1[j] = *reinterpret_cast<const bf16x8*>(a1 + j * 32);
+      rb0[j] = *reinterpret_cast<const bf16x8*>(b0 + j * 32);
+      rb1[j] = *reinterpret_cast<const bf16x8*>(b1 + j * 32);
+    }
+  }
+  for (int kb = 0; kb < nsteps; kb += PF) {
+#pragma unroll
+    for (int j = 0; j < PF; ++j) {
+      const int ks = kb + j;
+      if (ks < nsteps) {
+        c00 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ra0[j], rb0[j], c00, 0, 0, 0);
+        c01 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ra0[j], rb1[j], c01, 0, 0, 0);
+        c10 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ra1[j], rb0[j], c10, 0, 0, 0);
+        c11 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ra1[j], rb1[j], c11, 0, 0, 0);
+        const int kn = (ks + PF) * 32;
+        if (ks + PF < nsteps) {
+          ra0[j] = *reinterpret_cast<const bf16x8*>(a0 + kn);
+          ra1[j] = *reinterpret_cast<const bf16x8*>(a1 + kn);
+          rb0[j] = *reinterpret_cast<const bf16x8*>(b0 + kn);
+          rb1[j] = *reinterpret_cast<const bf16x8*>(b1 + kn);
+        }
+      }
+    }
   }
 
   // C/D map: col = lane&15, row = (lane>>4)*4 + j
@@ -90,8 +115,8 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_nt_kernel(
             v = fmaxf(v + ep.bias[col], 0.f);
             if (EPI == EPI_FWD && ep.drop)
               v = dropout_keep((uint32_t)(row * N + col), salt, ep.keep_thr) ? v * ep.scale : 0.f;
-          } else {  // EPI_DGRAD
-            v = (bf2f(ep.hprev[(size_t)row * N + col]) > 0.f) ? v * ep.scale : 0.f;
+          } else {  // EPI_DGRAD (hprev == nullptr: plain bf16 store, e.g. dX0 of layer 1)
+            v = (!ep.hprev || bf2f(ep.hprev[(size_t)row * N + col]) > 0.f) ? v * ep.scale : 0.f;
           }
           const bf16 hv = f2bf(v);
           reinterpret_cast<bf16*>(ep.out)[(size_t)row * N + col] = hv;

@@ -21,53 +21,79 @@ constexpr int RS_ITEMS = 8;
 constexpr int RS_TILE = RS_THREADS * RS_ITEMS;
 }  // namespace
 
+// LSD passes use digits of DB = ceil(end_bit / passes) bits with passes = ceil(end_bit / 11):
+// 30-bit ids (882.8M-row table) sort in 3 passes of 10 bits, 21-bit ids in 2 passes of 11 bits.
+template <int DB>
 __global__ void __launch_bounds__(RS_THREADS) rs_upsweep_kernel(const int* __restrict__ keys, int n,
                                                                int shift, int nblocks,
                                                                int* __restrict__ hist) {
-  __shared__ int h[RS_RADIX];
-  h[threadIdx.x] = 0;
+  constexpr int RADIX = 1 << DB;
+  __shared__ int h[RADIX];
+  for (int d = threadIdx.x; d < RADIX; d += RS_THREADS) h[d] = 0;
   __syncthreads();
   const int b0 = blockIdx.x * RS_TILE;
 #pragma unroll
   for (int k = 0; k < RS_ITEMS; ++k) {
     const int i = b0 + k * RS_THREADS + threadIdx.x;
-    if (i < n) atomicAdd(&h[(keys[i] >> shift) & (RS_RADIX - 1)], 1);
+    if (i < n) atomicAdd(&h[(keys[i] >> shift) & (RADIX - 1)], 1);
   }
   __syncthreads();
-  hist[threadIdx.x * nblocks + blockIdx.x] = h[threadIdx.x];
+  for (int d = threadIdx.x; d < RADIX; d += RS_THREADS) hist[d * nblocks + blockIdx.x] = h[d];
 }
 
+// Downsweep: stable in-tile ranking, then the tile is reordered by digit in LDS and written
+// out in LDS order, so consecutive threads store consecutive addresses of one digit's run
+// (coalesced) instead of 2 scattered 4-B stores per key.
+template <int DB>
 __global__ void __launch_bounds__(RS_THREADS) rs_downsweep_kernel(
     const int* __restrict__ keys_in, const int* __restrict__ vals_in, int* __restrict__ keys_out,
     int* __restrict__ vals_out, int n, int shift, int nblocks, const int* __restrict__ offs) {
-  __shared__ int cnt[RS_RADIX];
-  __shared__ int wcnt[4][RS_RADIX];
-  __shared__ int base[RS_RADIX];
+  constexpr int RADIX = 1 << DB;
+  static_assert(RADIX == RS_THREADS, "one thread per digit");
+  __shared__ int cnt[RADIX];
+  __shared__ int wcnt[4][RADIX];
+  __shared__ int gbase[RADIX];   // global offset of this tile's run of digit d
+  __shared__ int lbase[RADIX];   // local (in-tile) exclusive offset of digit d
+  __shared__ int lk[RS_TILE];
+  __shared__ int lv[RS_TILE];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   cnt[tid] = 0;
   wcnt[0][tid] = wcnt[1][tid] = wcnt[2][tid] = wcnt[3][tid] = 0;
-  base[tid] = offs[tid * nblocks + blockIdx.x];
+  gbase[tid] = offs[tid * nblocks + blockIdx.x];
+  lbase[tid] = 0;
   __syncthreads();
   const unsigned long long lt = (1ull << lane) - 1ull;
   const int b0 = blockIdx.x * RS_TILE;
-  // issue every load of the tile up front (no load latency inside the ranking loop)
+  const int nloc = min(RS_TILE, n - b0);
   int kr[RS_ITEMS], vr[RS_ITEMS];
 #pragma unroll
   for (int k = 0; k < RS_ITEMS; ++k) {
     const int i = b0 + k * RS_THREADS + tid;
     kr[k] = i < n ? keys_in[i] : 0;
     vr[k] = i < n ? (vals_in ? vals_in[i] : i) : 0;
+    if (i < n) atomicAdd(&lbase[(kr[k] >> shift) & (RADIX - 1)], 1);
   }
+  __syncthreads();
+  {  // exclusive scan of the tile histogram (Hillis-Steele over 256 digits)
+    const int own = lbase[tid];
+    for (int off = 1; off < RADIX; off <<= 1) {
+      const int v = tid >= off ? lbase[tid - off] : 0;
+      __syncthreads();
+      lbase[tid] += v;
+      __syncthreads();
+    }
+    lbase[tid] -= own;
+    __syncthreads();
+  }
+  int lpos[RS_ITEMS];
 #pragma unroll
   for (int k = 0; k < RS_ITEMS; ++k) {
     const int i = b0 + k * RS_THREADS + tid;
     const bool valid = i < n;
-    const int key = kr[k];
-    const int val = vr[k];
-    const int d = (key >> shift) & (RS_RADIX - 1);
+    const int d = (kr[k] >> shift) & (RADIX - 1);
     unsigned long long peers = __ballot(valid);
 #pragma unroll
-    for (int bit = 0; bit < RS_BITS; ++bit) {
+    for (int bit = 0; bit < DB; ++bit) {
       const bool bset = (d >> bit) & 1;
       const unsigned long long bal = __ballot(bset);
       peers &= bset ? bal : ~bal;
@@ -78,27 +104,62 @@ __global__ void __launch_bounds__(RS_THREADS) rs_downsweep_kernel(
     if (valid) {
       int r = cnt[d] + rk;
       for (int w = 0; w < wv; ++w) r += wcnt[w][d];
-      const int dst = base[d] + r;
-      keys_out[dst] = key;
-      vals_out[dst] = val;
+      lpos[k] = lbase[d] + r;
     }
     __syncthreads();
     cnt[tid] += wcnt[0][tid] + wcnt[1][tid] + wcnt[2][tid] + wcnt[3][tid];
     wcnt[0][tid] = wcnt[1][tid] = wcnt[2][tid] = wcnt[3][tid] = 0;
     __syncthreads();
   }
+#pragma unroll
+  for (int k = 0; k < RS_ITEMS; ++k) {
+    if (b0 + k * RS_THREADS + tid < n) {
+      lk[lpos[k]] = kr[k];
+      lv[lpos[k]] = vr[k];
+    }
+  }
+  __syncthreads();
+  for (int j = tid; j < nloc; j += RS_THREADS) {
+    const int key = lk[j];
+    const int d = (key >> shift) & (RADIX - 1);
+    const int dst = gbase[d] + (j - lbase[d]);
+    keys_out[dst] = key;
+    vals_out[dst] = lv[j];
+  }
 }
 
 static inline int rs_blocks(int n) { return (n + RS_TILE - 1) / RS_TILE; }
+static inline int rs_digit_bits(int end_bit, int* passes) {
+  // 8-bit digits measured fastest on MI355X (tools/bench_sort.py): wider digits cost more in
+  // the per-tile ranking than the saved pass
+  int p = (end_bit + 7) / 8;
+  if (p < 1) p = 1;
+  *passes = p;
+  return 8;
+}
 
 // workspace: [hist, offs: RADIX*nblocks ints each][ping keys n][ping vals n][scan temp]
 HFM_API int hfm_radix_sort_temp_bytes(int n, size_t* bytes) {
   const int nb = rs_blocks(n);
+  const size_t R = 2048;  // largest digit (11 bits)
   size_t scan_tb = 0;
   hipError_t e = hipcub::DeviceScan::ExclusiveSum(nullptr, scan_tb, (const int*)nullptr, (int*)nullptr,
-                                                  RS_RADIX * nb);
-  *bytes = (size_t)RS_RADIX * nb * 8 + (size_t)n * 8 + scan_tb + 1024;
+                                                  (int)(R * nb));
+  *bytes = R * nb * 8 + (size_t)n * 8 + scan_tb + 2048;
   return (int)e;
+}
+
+template <int DB>
+static int lsd_pass(const int* ki, const int* vi, int* ko, int* vo, int n, int shift, int nb,
+                    int* hist, int* offs, void* t, size_t scan_tb, hipStream_t st) {
+  constexpr int RADIX = 1 << DB;
+  hipLaunchKernelGGL(rs_upsweep_kernel<DB>, dim3(nb), dim3(RS_THREADS), 0, st, ki, n, shift, nb, hist);
+  size_t tb = scan_tb;
+  hipError_t e = hipcub::DeviceScan::ExclusiveSum(t, tb, hist, offs, RADIX * nb, st);
+  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(rs_downsweep_kernel<DB>, dim3(nb), dim3(RS_THREADS), 0, st, ki, vi, ko, vo, n,
+                     shift, nb, offs);
+  return 0;
 }
 
 // Sort keys (< 2^end_bit) ascending; perm_out[i] = input position of the i-th smallest (stable).
@@ -106,11 +167,12 @@ HFM_API int hfm_radix_sort_ids(const int* keys_in, int* keys_out, int* perm_out,
                                void* temp, size_t temp_bytes, hipStream_t st) {
   if (n <= 0) return 0;
   const int nb = rs_blocks(n);
-  const int passes = (end_bit + RS_BITS - 1) / RS_BITS;
+  int passes;
+  const int db = rs_digit_bits(end_bit, &passes);
   char* t = (char*)temp;
   int* hist = (int*)t;
-  int* offs = hist + (size_t)RS_RADIX * nb;
-  t += (size_t)RS_RADIX * nb * 8;
+  int* offs = hist + (size_t)2048 * nb;
+  t += (size_t)2048 * nb * 8;
   t = (char*)(((uintptr_t)t + 255) & ~(uintptr_t)255);
   int* pk = (int*)t;
   int* pv = pk + n;
@@ -121,18 +183,14 @@ HFM_API int hfm_radix_sort_ids(const int* keys_in, int* keys_out, int* perm_out,
   const int* ki = keys_in;
   const int* vi = nullptr;
   for (int p = 0; p < passes; ++p) {
-    const bool last = (p == passes - 1);
     const bool to_out = ((passes - 1 - p) % 2) == 0;
     int* ko = to_out ? keys_out : pk;
     int* vo = to_out ? perm_out : pv;
-    (void)last;
-    const int shift = p * RS_BITS;
-    hipLaunchKernelGGL(rs_upsweep_kernel, dim3(nb), dim3(RS_THREADS), 0, st, ki, n, shift, nb, hist);
-    size_t tb = scan_tb;
-    hipError_t e = hipcub::DeviceScan::ExclusiveSum(t, tb, hist, offs, RS_RADIX * nb, st);
-    if (e != hipSuccess) return (int)e;
-    hipLaunchKernelGGL(rs_downsweep_kernel, dim3(nb), dim3(RS_THREADS), 0, st, ki, vi, ko, vo, n,
-                       shift, nb, offs);
+    const int shift = p * db;
+    int rc;
+    (void)db;
+    rc = lsd_pass<8>(ki, vi, ko, vo, n, shift, nb, hist, offs, t, scan_tb, st);
+    if (rc) return rc;
     ki = ko;
     vi = vo;
   }

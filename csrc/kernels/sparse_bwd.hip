@@ -3,6 +3,7 @@
 //
 // Per slot (b, f) with id r and value x:
 //     d fm_v[r] += x*(dX0[b, f*K:(f+1)*K] + dy_b*(S_b - x*V[r]))  =  a_slot - V[r]*c_slot
+// (dX0, the layer-1 input gradient, arrives in bf16 like every other MLP activation)
 //     d fm_w[r] += dy_b*x
 // with a_slot = x*(dX0 + dy_b*S_b) and c_slot = x^2*dy_b.  V[r] is the SAME row for every slot
 // of an id, so it is factored out of the sum: the per-slot pass never touches the embedding
@@ -57,7 +58,7 @@ __global__ void seg_info_kernel(const int* __restrict__ sk, const int* __restric
 template <int K>
 __global__ void __launch_bounds__(256) fm_bwd_seg_kernel(
     const int* __restrict__ sorted_keys, const int* __restrict__ perm, const int* __restrict__ sid_incl,
-    const float* __restrict__ vals, const float* __restrict__ dlogit, const float* __restrict__ dX0,
+    const float* __restrict__ vals, const float* __restrict__ dlogit, const bf16* __restrict__ dX0,
     const float* __restrict__ S, int n, int F, int KP, float* __restrict__ partial,
     float* __restrict__ cont) {
   using T = TileCfg<K>;
@@ -75,7 +76,8 @@ __global__ void __launch_bounds__(256) fm_bwd_seg_kernel(
       const float x = vals[q];
       const float dy = dlogit[b];
       const f32x4 s = *reinterpret_cast<const f32x4*>(S + (size_t)b * K + sub * 4);
-      const f32x4 dx = *reinterpret_cast<const f32x4*>(dX0 + (size_t)b * KP + f * K + sub * 4);
+      const bf16x4 dxh = *reinterpret_cast<const bf16x4*>(dX0 + (size_t)b * KP + f * K + sub * 4);
+      const f32x4 dx = {bf2f(dxh[0]), bf2f(dxh[1]), bf2f(dxh[2]), bf2f(dxh[3])};
       const f32x4 a = (dx + dy * s) * x;
 #pragma unroll
       for (int j = 0; j < 4; ++j) g[p][sub * 4 + j] = a[j];
@@ -259,7 +261,7 @@ HFM_API int hfm_segments(const int* sorted_keys, int n, int* flags_tmp, int* sid
 
 template <int K>
 static int bwd_seg_k(const int* sk, const int* perm, const int* sid_incl, const float* vals,
-                     const float* dlogit, const float* dX0, const float* S, int n, int F, int KP,
+                     const float* dlogit, const bf16* dX0, const float* S, int n, int F, int KP,
                      float* partial, float* cont, hipStream_t st) {
   using T = TileCfg<K>;
   const int tiles = (n + T::TP - 1) / T::TP;
@@ -306,8 +308,9 @@ static int apply_k(int mode, int opt, const SegApplyArgs& A, int max_groups, hip
 
 // sid_incl == nullptr -> position-indexed partials
 HFM_API int hfm_fm_bwd_seg(int K, const int* sk, const int* perm, const int* sid_incl,
-                           const float* vals, const float* dlogit, const float* dX0, const float* S,
+                           const float* vals, const float* dlogit, const void* dX0v, const float* S,
                            int n, int F, int KP, float* partial, float* cont, hipStream_t st) {
+  const bf16* dX0 = (const bf16*)dX0v;   // dX0 is bf16 [B, KP] (layer-1 dgrad output)
 #define CALL(KK) bwd_seg_k<KK>(sk, perm, sid_incl, vals, dlogit, dX0, S, n, F, KP, partial, cont, st)
   HFM_K_DISPATCH(K, CALL)
 #undef CALL

@@ -103,6 +103,7 @@ _DEFS = [
     ("graph", _str2bool, True, "capture the train step in a HIP graph when possible"),
     ("max_steps", int, 0, "stop after this many steps (0 = run num_epochs)"),
     ("debug_sync", _str2bool, False, "synchronize + NaN/Inf check after each step (debug mode)"),
+    ("watchdog_secs", float, 1800.0, "abort a rank whose training step stalls this long (0 = off)"),
 ]
 
 
@@ -162,6 +163,7 @@ class RunConfig:
     graph: bool = True
     max_steps: int = 0
     debug_sync: bool = False
+    watchdog_secs: float = 1800.0
     hosts: List[str] = dataclasses.field(default_factory=_env_hosts)
 
     # ---- derived views (reference C09: CSV parsing with list(map(...)), PS:153-163) ----

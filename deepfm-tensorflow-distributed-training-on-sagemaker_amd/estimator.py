@@ -32,7 +32,9 @@ from .ckpt.export import export_servable
 from .ckpt.native import CheckpointManager, reshard_rows
 from .config import RunConfig
 from .ops.metrics import auc_from_hist, hist_torch
+from .utils.fault import Watchdog, maybe_inject_fault
 from .utils.logging import MetricsLogger, StepTimer
+from .utils.profiling import StepWindow
 
 
 def _dist_on() -> bool:
@@ -216,6 +218,8 @@ class Estimator:
         n_log = 0
         start_step = self.global_step
         use_graph = cfg.graph and self.native
+        wd = Watchdog(cfg.watchdog_secs, self.rank).start()
+        window = StepWindow()
         t_wait = time.time()
         for ids, vals, labels in batches:
             self.timer.add("data_wait", time.time() - t_wait)
@@ -235,6 +239,9 @@ class Estimator:
             self.timer.add("step_enqueue", time.time() - t0)
             n_log += B
             step = self.global_step
+            wd.beat(step)
+            window.step(step)
+            maybe_inject_fault(step, self.rank)
             if cfg.log_steps and step % cfg.log_steps == 0:
                 if self.native:
                     torch.cuda.synchronize(self.device)
@@ -257,6 +264,7 @@ class Estimator:
             t_wait = time.time()
         if self.native:
             torch.cuda.synchronize(self.device)
+        wd.stop()
         return self.global_step - start_step
 
     def _nan_check(self):

@@ -245,7 +245,7 @@ class NativeDeepFM:
         self.Ht = [torch.zeros(n, M, **bf) for n in self.Np]
         self.dZ = [torch.zeros(M, n, **bf) for n in self.Np]
         self.dZt = [torch.zeros(n, M, **bf) for n in self.Np]
-        self.dX0 = torch.zeros(M, K0p, **f32)
+        self.dX0 = torch.zeros(M, K0p, **bf)            # layer-1 input gradient (bf16)
         self.prob = torch.zeros(M, **f32)
         self.dlogit = torch.zeros(M, **f32)
         self.nhead = (M + 63) // 64      # head kernel: 64 samples per workgroup
@@ -460,8 +460,9 @@ class NativeDeepFM:
                 KN.gemm_nt(KN.EPI_DGRAD, _pick_tile(M, N), self.dZ[i], self.Np[i], self.WT16[i],
                            self.Np[i], M, N, self.Np[i], 1, ep)
             else:
-                ep.out = self.dX0.data_ptr()
-                KN.gemm_nt(KN.EPI_F32, _pick_tile(M, self.K0p), self.dZ[0], self.Np[0],
+                ep.out = self.dX0.data_ptr()          # hprev = 0: unmasked bf16 store
+                ep.scale = 1.0
+                KN.gemm_nt(KN.EPI_DGRAD, _pick_tile(M, self.K0p), self.dZ[0], self.Np[0],
                            self.WT16[0], self.Np[0], M, self.K0p, self.Np[0], 1, ep)
         KN.slab_reduce(self._slab_jobs, self._nslab_jobs, self._slab_maxn)
         KN.rowsum(self._row_jobs, self._nrow_jobs, self._row_total)
