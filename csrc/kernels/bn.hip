@@ -1,0 +1,210 @@
+// K6b batch norm in the deep tower: the reference's
+// ``batch_norm_layer`` (1-ps-cpu/DeepFM-dist-ps-for-multipleCPU-multiInstance.py:288-292,
+// tf.contrib.layers.batch_norm, center+scale, eps 1e-3, updates_collections=None) applied
+// AFTER the ReLU and BEFORE dropout (PS:213-218), batch statistics per rank (no sync-BN, as
+// with Horovod).
+//
+// Per BN layer the step is
+//   fwd:  R = relu(X W^T + b)                 (gemm_nt EPI_FWD_EVAL, bf16 R)
+//         part[tile] = (sum R, sum R^2)        bn_partial<0>   (deterministic per-64-row tiles)
+//         mean, var, scale, shift, moving      bn_finalize<0>  (double reduction, fixed order)
+//         H = (R*scale + shift)*keep/keep_p    bn_apply<0>     (-> H and H^T, LDS transpose)
+//   bwd:  dY = dH (.) keep/keep_p              (dH fp32 from gemm EPI_F32 or the head)
+//         part[tile] = (sum dY, sum dY*xhat)   bn_partial<1>
+//         dbeta, dgamma, c1, c2                bn_finalize<2>  (grads land in the flat buffer)
+//         dZ = (R>0) gamma*rstd*(dY - c1 - xhat*c2)   bn_apply<1>  (-> dZ and dZ^T)
+// Dropout masks are regenerated from the counter hash with the same flat index as the GEMM
+// epilogue (row * Npad + col).  Padding rows (>= nvalid) are excluded from every statistic
+// and get a zero gradient.
+#include "common.h"
+
+struct BnArgs {
+  int M, N, nvalid;
+  const bf16* r;          // [M,N] relu output (pre-BN)
+  const float* dh;        // [M,N] gradient w.r.t. the layer output (post BN + dropout)
+  const float* gamma;     // [N]
+  const float* beta;      // [N]
+  float* mm;              // moving mean [N]
+  float* mv;              // moving variance [N]
+  float* save;            // [6,N]: mean, rstd, scale, shift, c1, c2
+  float* part;            // [M/64, 2N]
+  float* dgamma;          // [N] (flat gradient buffer)
+  float* dbeta;           // [N]
+  float eps, decay;
+  uint32_t seed, layer, keep_thr;
+  int drop;
+  float inv_keep;
+  const int64_t* step;
+  bf16* out;              // fwd: H [M,N]   bwd: dZ [M,N]
+  bf16* out_t;            // fwd: H^T       bwd: dZ^T   (nullable)
+};
+
+__device__ __forceinline__ float drop_factor(const BnArgs& a, uint32_t salt, int row, int col) {
+  if (!a.drop) return 1.f;
+  return dropout_keep((uint32_t)(row * a.N + col), salt, a.keep_thr) ? a.inv_keep : 0.f;
+}
+
+// grid (M/64, N/32), 256 threads: 32 columns x 8 row-groups of 8 rows.
+template <int BWD>
+__global__ void __launch_bounds__(256) bn_partial_kernel(BnArgs a) {
+  __shared__ float red[2][8][32];
+  const int c = threadIdx.x & 31, rg = threadIdx.x >> 5;
+  const int col = blockIdx.y * 32 + c;
+  const int r0 = blockIdx.x * 64 + rg * 8;
+  const float* sv = a.save;
+  float mean = 0.f, rstd = 0.f;
+  uint32_t salt = 0;
+  if (BWD) {
+    mean = sv[col];
+    rstd = sv[a.N + col];
+    if (a.drop) salt = dropout_salt(a.seed, (uint32_t)(*a.step), a.layer);
+  }
+  float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int row = r0 + j;
+    if (row < a.nvalid) {
+      const size_t o = (size_t)row * a.N + col;
+      const float x = bf2f(a.r[o]);
+      if (BWD) {
+        const float dy = a.dh[o] * drop_factor(a, salt, row, col);
+        s0 += dy;
+        s1 += dy * (x - mean) * rstd;
+      } else {
+        s0 += x;
+        s1 += x * x;
+      }
+    }
+  }
+  red[0][rg][c] = s0;
+  red[1][rg][c] = s1;
+  __syncthreads();
+  if (rg < 2) {
+    const float* v = red[rg][0] + c;
+    const float t = ((v[0] + v[32]) + (v[64] + v[96])) + ((v[128] + v[160]) + (v[192] + v[224]));
+    a.part[(size_t)blockIdx.x * 2 * a.N + rg * a.N + col] = t;
+  }
+}
+
+// MODE 0: train forward (batch stats + moving-average update), 1: eval (moving stats),
+// 2: backward (dbeta/dgamma + c1/c2).  grid N/32, 256 threads: 32 columns x 8 row-lanes.
+template <int MODE>
+__global__ void __launch_bounds__(256) bn_finalize_kernel(BnArgs a, int nrow) {
+  __shared__ double red[2][8][32];
+  const int c = threadIdx.x & 31, rl = threadIdx.x >> 5;
+  const int col = blockIdx.x * 32 + c;
+  const int N = a.N;
+  double s0 = 0.0, s1 = 0.0;
+  if (MODE != 1) {
+    for (int r = rl; r < nrow; r += 8) {
+      s0 += (double)a.part[(size_t)r * 2 * N + col];
+      s1 += (double)a.part[(size_t)r * 2 * N + N + col];
+    }
+  }
+  red[0][rl][c] = s0;
+  red[1][rl][c] = s1;
+  __syncthreads();
+  if (rl != 0) return;
+  s0 = ((red[0][0][c] + red[0][1][c]) + (red[0][2][c] + red[0][3][c])) +
+       ((red[0][4][c] + red[0][5][c]) + (red[0][6][c] + red[0][7][c]));
+  s1 = ((red[1][0][c] + red[1][1][c]) + (red[1][2][c] + red[1][3][c])) +
+       ((red[1][4][c] + red[1][5][c]) + (red[1][6][c] + red[1][7][c]));
+  float* sv = a.save;
+  const double n = (double)a.nvalid;
+  if (MODE == 2) {
+    a.dbeta[col] = (float)s0;
+    a.dgamma[col] = (float)s1;
+    sv[4 * N + col] = (float)(s0 / n);
+    sv[5 * N + col] = (float)(s1 / n);
+    return;
+  }
+  float mean, var;
+  if (MODE == 0) {
+    const double m = s0 / n;
+    double v = s1 / n - m * m;
+    if (v < 0.0) v = 0.0;
+    mean = (float)m;
+    var = (float)v;
+    const float d = a.decay;
+    const float unb = (float)(v * (n / (n > 1.0 ? n - 1.0 : 1.0)));   // fused BN reports Bessel var
+    a.mm[col] = a.mm[col] * d + mean * (1.f - d);
+    a.mv[col] = a.mv[col] * d + unb * (1.f - d);
+  } else {
+    mean = a.mm[col];
+    var = a.mv[col];
+  }
+  const float rstd = 1.f / sqrtf(var + a.eps);
+  const float scale = a.gamma[col] * rstd;
+  sv[col] = mean;
+  sv[N + col] = rstd;
+  sv[2 * N + col] = scale;
+  sv[3 * N + col] = a.beta[col] - mean * scale;
+}
+
+// grid (M/64, N/32), 256 threads; tile 64 rows x 32 cols, 8 contiguous columns per thread,
+// transposed copy through LDS (each thread then writes 8 consecutive rows of one column).
+template <int BWD>
+__global__ void __launch_bounds__(256) bn_apply_kernel(BnArgs a) {
+  __shared__ bf16 tile[32][64 + 8];
+  const int t = threadIdx.x;
+  const int lr = t >> 2, cq = (t & 3) * 8;
+  const int row = blockIdx.x * 64 + lr;
+  const int cb = blockIdx.y * 32 + cq;
+  const int N = a.N;
+  const float* sv = a.save;
+  uint32_t salt = 0;
+  if (a.drop) salt = dropout_salt(a.seed, (uint32_t)(*a.step), a.layer);
+  const size_t o = (size_t)row * N + cb;
+  const bf16x8 xr = *reinterpret_cast<const bf16x8*>(a.r + o);
+  bf16x8 ov;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int col = cb + j;
+    const float x = bf2f(xr[j]);
+    float v;
+    if (BWD) {
+      if (row < a.nvalid && x > 0.f) {
+        const float dy = a.dh[o + j] * drop_factor(a, salt, row, col);
+        const float xhat = (x - sv[col]) * sv[N + col];
+        v = sv[2 * N + col] * (dy - sv[4 * N + col] - xhat * sv[5 * N + col]);
+      } else {
+        v = 0.f;
+      }
+    } else {
+      v = (x * sv[2 * N + col] + sv[3 * N + col]) * drop_factor(a, salt, row, col);
+    }
+    ov[j] = f2bf(v);
+    tile[cq + j][lr] = ov[j];
+  }
+  *reinterpret_cast<bf16x8*>(a.out + o) = ov;
+  if (!a.out_t) return;
+  __syncthreads();
+  const int tc = t >> 3, tr = (t & 7) * 8;
+  bf16x8 w;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) w[j] = tile[tc][tr + j];
+  *reinterpret_cast<bf16x8*>(a.out_t + (size_t)(blockIdx.y * 32 + tc) * a.M + blockIdx.x * 64 + tr) = w;
+}
+
+static bool bn_shape_ok(const BnArgs& a) { return a.M % 64 == 0 && a.N % 32 == 0 && a.M > 0 && a.N > 0; }
+
+// phase: 0 fwd partial, 1 fwd finalize (train), 2 eval finalize, 3 fwd apply,
+//        4 bwd partial, 5 bwd finalize, 6 bwd apply
+HFM_API int hfm_bn(int phase, const BnArgs* ap, hipStream_t st) {
+  const BnArgs a = *ap;
+  if (!bn_shape_ok(a)) return (int)hipErrorInvalidValue;
+  const dim3 tiles(a.M / 64, a.N / 32);
+  const int nrow = a.M / 64;
+  switch (phase) {
+    case 0: hipLaunchKernelGGL(bn_partial_kernel<0>, tiles, dim3(256), 0, st, a); break;
+    case 1: hipLaunchKernelGGL(bn_finalize_kernel<0>, dim3(a.N / 32), dim3(256), 0, st, a, nrow); break;
+    case 2: hipLaunchKernelGGL(bn_finalize_kernel<1>, dim3(a.N / 32), dim3(256), 0, st, a, nrow); break;
+    case 3: hipLaunchKernelGGL(bn_apply_kernel<0>, tiles, dim3(256), 0, st, a); break;
+    case 4: hipLaunchKernelGGL(bn_partial_kernel<1>, tiles, dim3(256), 0, st, a); break;
+    case 5: hipLaunchKernelGGL(bn_finalize_kernel<2>, dim3(a.N / 32), dim3(256), 0, st, a, nrow); break;
+    case 6: hipLaunchKernelGGL(bn_apply_kernel<1>, tiles, dim3(256), 0, st, a); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+  HFM_LAUNCH_CHECK();
+}
+HFM_API int hfm_bn_args_bytes() { return (int)sizeof(BnArgs); }

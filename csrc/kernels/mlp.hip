@@ -193,6 +193,8 @@ struct HeadArgs {
   bf16* dz;             // [M, L]
   bf16* dz_t;           // [L, M]
   float* partial;       // [gridDim.x, L + 2]
+  float* dh;            // batch-norm towers: raw dL/dh_L = dlogit * w_out, f32 [M, L] (the BN
+                        // backward applies dropout/ReLU itself); dz/dz_t are then unused
 };
 
 // 4 lanes per sample (each owns L/4 hidden columns): 64 samples per 256-thread workgroup, so a
@@ -240,7 +242,12 @@ __global__ void __launch_bounds__(256) head_kernel(HeadArgs a) {
         dl = (p - lab) * a.gscale;
       }
     }
-    if (a.train) {
+    if (a.train && a.dh) {
+      if (q == 0) a.dlogit[b] = dl;
+      float* dhr = a.dh + (size_t)b * L + q * Q;
+#pragma unroll
+      for (int j = 0; j < Q; ++j) dhr[j] = dl * a.w_out[q * Q + j];
+    } else if (a.train) {
       if (q == 0) a.dlogit[b] = dl;
       bf16* dzr = a.dz + (size_t)b * L + q * Q;
 #pragma unroll

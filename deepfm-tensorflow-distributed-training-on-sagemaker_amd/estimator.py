@@ -89,7 +89,7 @@ class Estimator:
                                       optimizer=cfg.optimizer, loss_type=cfg.loss_type,
                                       sparse_update=cfg.sparse_update, seed=cfg.seed,
                                       batch_size=cfg.batch_size, device=self.device, comm=self.comm,
-                                      batch_norm=cfg.batch_norm)
+                                      batch_norm=cfg.batch_norm, batch_norm_decay=cfg.batch_norm_decay)
         else:
             from .models.reference import GoldenDeepFM
             self.model = GoldenDeepFM(cfg.feature_size, cfg.field_size, cfg.embedding_size, cfg.layers,
@@ -107,6 +107,8 @@ class Estimator:
         self._last_save_t = time.time()
         self._last_eval_t = 0.0
         self.restored_from = self.restore_latest()
+        if self.world > 1:
+            self.broadcast_state()
 
     # ------------------------------------------------------------------ state
     @property
@@ -152,6 +154,21 @@ class Estimator:
         self.model.load_state_dict_local(st)
         self.log.info(f"Restoring parameters from {path} (global_step {self.global_step})")
         return path
+
+    def broadcast_state(self):
+        """Rank 0's replicated state to every rank (reference C23: BroadcastGlobalVariablesHook(0)
+        on every train() call, HVD:371-372,392).  Done once per job here: the state never leaves
+        device memory between epochs, so there is nothing to re-synchronize per epoch.  The
+        golden (CPU) path broadcasts a golden model's global_step separately."""
+        if not _dist_on():
+            return
+        for t in self.model.replicated_state():
+            if t.dtype == torch.float32 or t.dtype == torch.int64:
+                dist.broadcast(t, src=0)
+        if not self.native:
+            gs = torch.tensor([int(self.model.global_step)], dtype=torch.int64)
+            dist.broadcast(gs, src=0)
+            self.model.global_step = int(gs.item())
 
     def _reshard_load(self, path: str, man: dict) -> Dict[str, torch.Tensor]:
         """Resume on a different world size / sharding: replicated rows are sliced, mod-sharded

@@ -9,7 +9,7 @@ The reference's Horovod job is started by SageMaker with ``mpirun`` and
 Every child gets torchrun-style ``RANK / LOCAL_RANK / WORLD_SIZE / LOCAL_WORLD_SIZE /
 MASTER_ADDR / MASTER_PORT`` and initialises RCCL through ``torch.distributed`` (TCPStore
 rendezvous, no MPI).  Multi-host: ``--nnodes/--node_rank`` or SageMaker's ``SM_HOSTS`` /
-``SM_CURRENT_HOST`` / ``SM_NUM_GPUS``.  If any rank fails, the others are terminated (Horovod's
+``SM_CURRENT_HOST`` / ``SM_NUM_GPUS``, or a parameter-server ``TF_CONFIG``.  If any rank fails, the others are terminated (Horovod's
 "one rank died -> job shut down" behaviour, DOC p.22) and the failing exit code is returned.
 """
 from __future__ import annotations
@@ -34,6 +34,32 @@ def _sagemaker_defaults():
     cur = os.environ.get("SM_CURRENT_HOST", hosts[0])
     return {"nnodes": len(hosts), "node_rank": hosts.index(cur) if cur in hosts else 0,
             "master_addr": hosts[0], "nproc": int(os.environ.get("SM_NUM_GPUS", "0") or 0)}
+
+
+def _tf_config_defaults():
+    """Map a parameter-server ``TF_CONFIG`` (reference C26, PS:414-428: cluster
+    {chief|master, worker, ps}, task {type, index}) onto this launcher's node layout: every
+    chief/master/worker host becomes a training node (synchronous data parallel over RCCL);
+    ``ps`` and ``evaluator`` tasks have no role here (the embedding table lives in GPU HBM)
+    and exit 0, so a PS-style launch configuration still starts the right processes."""
+    raw = os.environ.get("TF_CONFIG")
+    if not raw:
+        return None
+    try:
+        tc = json.loads(raw)
+    except ValueError:
+        return None
+    cluster, task = tc.get("cluster", {}), tc.get("task", {})
+    nodes = []
+    for role in ("chief", "master", "worker"):
+        nodes += [(role, i, h) for i, h in enumerate(cluster.get(role, []))]
+    if not nodes:
+        return None
+    ttype, tidx = task.get("type", "worker"), int(task.get("index", 0))
+    if ttype in ("ps", "evaluator"):
+        return {"idle_role": ttype}
+    rank = next((k for k, (r, i, _) in enumerate(nodes) if r == ttype and i == tidx), 0)
+    return {"nnodes": len(nodes), "node_rank": rank, "master_addr": nodes[0][2].split(":")[0]}
 
 
 def main(argv=None) -> int:
@@ -62,7 +88,11 @@ def main(argv=None) -> int:
         a.module, a.args = target[1], target[2:]
     elif target:
         a.script, a.args = target[0], target[1:]
-    sm = _sagemaker_defaults() or {}
+    sm = _sagemaker_defaults() or _tf_config_defaults() or {}
+    if "idle_role" in sm:
+        print(f"[hipfm.launch] TF_CONFIG task type {sm['idle_role']!r} has no role in hipfm "
+              "(no parameter servers: the table is sharded over GPU HBM); exiting", flush=True)
+        return 0
     nnodes = a.nnodes or sm.get("nnodes", 1)
     node_rank = a.node_rank if a.node_rank >= 0 else sm.get("node_rank", 0)
     master = a.master_addr or sm.get("master_addr", "127.0.0.1")

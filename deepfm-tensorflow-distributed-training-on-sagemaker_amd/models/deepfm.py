@@ -32,7 +32,7 @@ from typing import Dict, List, Optional
 import torch
 
 from ..ops import kernels as KN
-from ..ops._lib import EpiArgs, HeadArgs, RowSumJob, SegApplyArgs, ShadowSeg, SlabJob
+from ..ops._lib import BnArgs, EpiArgs, HeadArgs, RowSumJob, SegApplyArgs, ShadowSeg, SlabJob
 from ..utils.rng import keep_threshold
 from .reference import glorot_std, init_params, pad32
 
@@ -97,10 +97,11 @@ class NativeDeepFM:
                  learning_rate: float = 5e-4, optimizer: str = "Adam", loss_type: str = "log_loss",
                  sparse_update: str = "tf1_dense", seed: int = 1234, batch_size: int = 1024,
                  device="cuda", comm=None, init: bool = True, batch_norm: bool = False,
-                 adam_epsilon: float = 1e-8, adagrad_init: float = 1e-8):
-        if batch_norm:
-            raise NotImplementedError("batch_norm on the native path is not implemented yet; "
-                                      "use --device cpu (golden path) for batch_norm runs")
+                 batch_norm_decay: float = 0.9, adam_epsilon: float = 1e-8,
+                 adagrad_init: float = 1e-8):
+        self.batch_norm = bool(batch_norm)
+        self.bn_decay = float(batch_norm_decay)
+        self.bn_eps = 1e-3          # tf.contrib.layers.batch_norm default epsilon (PS:289)
         self.V, self.F, self.K = int(feature_size), int(field_size), int(embedding_size)
         if self.K not in (4, 8, 16, 32, 64):
             raise ValueError("embedding_size must be one of 4, 8, 16, 32, 64 on the native path")
@@ -144,6 +145,9 @@ class NativeDeepFM:
         for i, L in enumerate(self.layers):
             add(f"Deep-part/mlp{i}/weights", (self.Np[i], self.Kp[i]), (din, L))
             add(f"Deep-part/mlp{i}/biases", (self.Np[i],), (L,))
+            if self.batch_norm:     # trainable BN params live in the flat (all-reduced) buffer
+                add(f"Deep-part/bn_{i}/beta", (self.Np[i],), (L,))
+                add(f"Deep-part/bn_{i}/gamma", (self.Np[i],), (L,))
             din = L
         add("Deep-part/deep_out/weights", (self.Np[-1],), (din, 1))
         add("Deep-part/deep_out/biases", (1,), (1,))
@@ -157,6 +161,18 @@ class NativeDeepFM:
         self.p = torch.zeros(self.P, **f32)
         self.g = torch.zeros(self.P, **f32)
         self.step = torch.zeros(1, dtype=torch.int64, device=dev)
+        # BN moving statistics: non-trainable, outside the optimizer/all-reduce buffer
+        # (rank-local, like the reference's per-worker batch_norm updates)
+        self.bn_moving = torch.zeros(2 * sum(self.Np) if self.batch_norm else 0, **f32)
+        self.bn_mm, self.bn_mv = [], []
+        if self.batch_norm:
+            o = 0
+            for n in self.Np:
+                self.bn_mm.append(self.bn_moving[o:o + n])
+                self.bn_mv.append(self.bn_moving[o + n:o + 2 * n])
+                o += 2 * n
+            for t in self.bn_mv:
+                t.fill_(1.0)
         self._alloc_slots()
         if self.sparse_update == "tf1_dense":
             self.Gv = torch.zeros(self.R, K, **f32)
@@ -179,19 +195,20 @@ class NativeDeepFM:
         if init:
             if self.V * self.K <= (1 << 24):
                 # small tables: the exact golden initialization (CPU generator, bit-reproducible)
-                self.load_tf_params(init_params(self.V, F, K, self.layers, False, self.seed))
+                self.load_tf_params(init_params(self.V, F, K, self.layers, self.batch_norm,
+                                                self.seed))
             else:
                 # huge tables (Criteo-1TB shape): same distributions, generated in place on the
                 # GPU per rank (no host staging, no full-table temporary)
-                self.load_tf_params(init_params(self.V, F, K, self.layers, False, self.seed,
-                                                tables=False))
+                self.load_tf_params(init_params(self.V, F, K, self.layers, self.batch_norm,
+                                                self.seed, tables=False))
                 self.init_tables_inplace()
         self._alloc_step_buffers(self._padM(self.batch_size))
 
     # ------------------------------------------------------------------ allocation
     def init_tables_inplace(self):
         g = torch.Generator(device=self.device)
-        g.manual_seed(self.seed * 7919 + self.rank)
+        g.manual_seed(self.seed * 7919 + (self.rank if self.sharded else 0))
         with torch.no_grad():
             for t, shape in ((self.tw, (self.V,)), (self.tv, (self.V, self.K))):
                 std = glorot_std(shape)
@@ -246,6 +263,11 @@ class NativeDeepFM:
         self.dZ = [torch.zeros(M, n, **bf) for n in self.Np]
         self.dZt = [torch.zeros(n, M, **bf) for n in self.Np]
         self.dX0 = torch.zeros(M, K0p, **bf)            # layer-1 input gradient (bf16)
+        if self.batch_norm:
+            self.Rb = [torch.zeros(M, n, **bf) for n in self.Np]          # relu output (pre-BN)
+            self.dH = [torch.zeros(M, n, **f32) for n in self.Np]         # dL/d(layer output)
+            self.bn_save = [torch.zeros(6, n, **f32) for n in self.Np]
+            self.bn_part = torch.zeros(M // 64, 2 * max(self.Np), **f32)
         self.prob = torch.zeros(M, **f32)
         self.dlogit = torch.zeros(M, **f32)
         self.nhead = (M + 63) // 64      # head kernel: 64 samples per workgroup
@@ -335,6 +357,12 @@ class NativeDeepFM:
                 if name not in params:
                     continue
                 self._dense_view(self.p, s).copy_(self._tf_to_native(name, params[name]).to(self.device))
+            for i in range(len(self.bn_mm)):
+                for key, dst in ((f"Deep-part/bn_{i}/moving_mean", self.bn_mm[i]),
+                                 (f"Deep-part/bn_{i}/moving_variance", self.bn_mv[i])):
+                    if key in params:
+                        t = params[key].detach().reshape(-1).to(self.device, torch.float32)
+                        dst[: t.numel()].copy_(t)
         self.refresh_shadows()
 
     def _dense_view(self, flat: torch.Tensor, s: DenseSeg) -> torch.Tensor:
@@ -414,10 +442,62 @@ class NativeDeepFM:
             ep.out = self.H[i].data_ptr()
             ep.out_t = self.Ht[i].data_ptr() if train else 0
             N = self.Np[i]
-            KN.gemm_nt(KN.EPI_FWD if train else KN.EPI_FWD_EVAL, _pick_tile(M, N), X, self.Kp[i],
-                       self.W16[i], self.Kp[i], M, N, self.Kp[i], 1, ep)
+            if self.batch_norm:
+                ep.out, ep.out_t = self.Rb[i].data_ptr(), 0
+                KN.gemm_nt(KN.EPI_FWD_EVAL, _pick_tile(M, N), X, self.Kp[i], self.W16[i],
+                           self.Kp[i], M, N, self.Kp[i], 1, ep)
+                self._bn_forward(i, B, train)
+            else:
+                KN.gemm_nt(KN.EPI_FWD if train else KN.EPI_FWD_EVAL, _pick_tile(M, N), X,
+                           self.Kp[i], self.W16[i], self.Kp[i], M, N, self.Kp[i], 1, ep)
             X = self.H[i]
         return idx, tv
+
+    def _bn_args(self, i: int, B: int, drop: bool) -> BnArgs:
+        a = BnArgs()
+        a.M, a.N, a.nvalid = self.M, self.Np[i], B
+        a.r = self.Rb[i].data_ptr()
+        a.dh = self.dH[i].data_ptr()
+        pb = self.p.data_ptr()
+        gb = self.g.data_ptr()
+        sb = self.dense_segs[f"Deep-part/bn_{i}/beta"].off
+        sg = self.dense_segs[f"Deep-part/bn_{i}/gamma"].off
+        a.beta, a.gamma = pb + 4 * sb, pb + 4 * sg
+        a.dbeta, a.dgamma = gb + 4 * sb, gb + 4 * sg
+        a.mm, a.mv = self.bn_mm[i].data_ptr(), self.bn_mv[i].data_ptr()
+        a.save = self.bn_save[i].data_ptr()
+        a.part = self.bn_part.data_ptr()
+        a.eps, a.decay = self.bn_eps, self.bn_decay
+        keep = self.keep[i]
+        a.seed = self.seed & 0xFFFFFFFF
+        a.layer = i
+        a.keep_thr = min(keep_threshold(keep), 0xFFFFFFFF)
+        a.drop = 1 if (drop and keep < 1.0) else 0
+        a.inv_keep = (1.0 / keep) if a.drop else 1.0
+        a.step = self.step.data_ptr()
+        return a
+
+    def _bn_forward(self, i: int, B: int, train: bool):
+        """relu output R -> batch norm (batch stats + moving update, or moving stats) ->
+        dropout -> H (and H^T when training)."""
+        a = self._bn_args(i, B, drop=train)
+        if train:
+            KN.bn(KN.BN_FWD_PARTIAL, a)
+            KN.bn(KN.BN_FWD_FINALIZE, a)
+        else:
+            KN.bn(KN.BN_EVAL_FINALIZE, a)
+        a.out = self.H[i].data_ptr()
+        a.out_t = self.Ht[i].data_ptr() if train else 0
+        KN.bn(KN.BN_FWD_APPLY, a)
+
+    def _bn_backward(self, i: int, B: int):
+        """dH_i (f32) -> dZ_i, dZ_i^T (bf16) through dropout, batch norm and relu; writes the
+        beta/gamma gradients into the flat gradient buffer."""
+        a = self._bn_args(i, B, drop=True)
+        KN.bn(KN.BN_BWD_PARTIAL, a)
+        KN.bn(KN.BN_BWD_FINALIZE, a)
+        a.out, a.out_t = self.dZ[i].data_ptr(), self.dZt[i].data_ptr()
+        KN.bn(KN.BN_BWD_APPLY, a)
 
     def _head(self, B: int, train: bool, with_labels: bool = True):
         a = HeadArgs()
@@ -438,19 +518,27 @@ class NativeDeepFM:
         a.dz = self.dZ[-1].data_ptr()
         a.dz_t = self.dZt[-1].data_ptr()
         a.partial = self.partial.data_ptr()
+        a.dh = self.dH[-1].data_ptr() if (self.batch_norm and train) else 0
         KN.head(a)
 
     # ------------------------------------------------------------------ backward pieces
-    def _mlp_backward(self):
+    def _mlp_backward(self, B: int):
         M = self.M
         for i in reversed(range(len(self.layers))):
+            if self.batch_norm:
+                self._bn_backward(i, B)
             Xt = self.Et if i == 0 else self.Ht[i - 1]
             t, s = self.wg_cfg[i]
             ep = EpiArgs()
             ep.out = self.slabs[i].data_ptr()
             KN.gemm_nt(KN.EPI_F32, t, self.dZt[i], M, Xt, M, self.Np[i], self.Kp[i], M, s, ep)
             ep = EpiArgs()
-            if i > 0:
+            if i > 0 and self.batch_norm:
+                ep.out = self.dH[i - 1].data_ptr()    # f32 dL/dH_{i-1}; BN backward masks it
+                N = self.Np[i - 1]
+                KN.gemm_nt(KN.EPI_F32, _pick_tile(M, N), self.dZ[i], self.Np[i], self.WT16[i],
+                           self.Np[i], M, N, self.Np[i], 1, ep)
+            elif i > 0:
                 keep = self.keep[i - 1]
                 ep.hprev = self.H[i - 1].data_ptr()
                 ep.scale = (1.0 / keep) if keep < 1.0 else 1.0
@@ -536,7 +624,7 @@ class NativeDeepFM:
         """Enqueue one full training step on the current stream (no host sync)."""
         idx, tv = self._forward(B, train=True)
         self._head(B, train=True)
-        self._mlp_backward()
+        self._mlp_backward(B)
         work = None
         if self.exchange:
             work = self.comm.allreduce_dense_async(self.g)
@@ -557,7 +645,7 @@ class NativeDeepFM:
         B = self.stage_batch(ids, vals, labels)
         idx, tv = self._forward(B, train=True)
         self._head(B, train=True)
-        self._mlp_backward()
+        self._mlp_backward(B)
         n = B * self.F
         KN.sort_ids(self.idx, self.sorted_keys, None, self.perm, n, self.end_bit, self.temp)
         self._segment_reduce(n, compact=True)
@@ -674,12 +762,25 @@ class NativeDeepFM:
         for i, t in enumerate(self.sd):
             if t.numel():
                 d[f"dense_slot{i}"] = t
+        if self.batch_norm:
+            d["bn_moving"] = self.bn_moving
         return d
+
+    def replicated_state(self) -> List[torch.Tensor]:
+        """Tensors every rank must hold identically (broadcast from rank 0 at start, like the
+        reference's BroadcastGlobalVariablesHook(0), HVD:372): dense params + slots + step, and
+        the tables/slots when the table is replicated rather than row-sharded."""
+        out = [self.p, self.step] + [t for t in self.sd if t.numel()]
+        if self.batch_norm:
+            out.append(self.bn_moving)
+        if not self.sharded:
+            out += [self.tv, self.tw] + [t for t in self.sv if t.numel()]
+        return out
 
     def ckpt_meta(self) -> dict:
         return {"format": "hipfm-native", "V": self.V, "F": self.F, "K": self.K,
                 "layers": self.layers, "keep": self.keep, "optimizer": self.optimizer,
-                "world": self.world, "rank": self.rank, "R": self.R,
+                "world": self.world, "rank": self.rank, "R": self.R, "batch_norm": self.batch_norm,
                 "sharding": "mod" if self.sharded else "replicated", "P": self.P,
                 "dense_segs": [[s.name, s.off, list(s.shape), list(s.tf_shape)]
                                for s in self.dense_segs.values()]}
@@ -709,6 +810,9 @@ class NativeDeepFM:
         for k, v in dense.items():
             if k != "fm_bias":
                 out[k] = v
+        for i, L in enumerate(self.layers[: len(self.bn_mm)]):
+            out[f"Deep-part/bn_{i}/moving_mean"] = self.bn_mm[i][:L].detach().cpu().clone()
+            out[f"Deep-part/bn_{i}/moving_variance"] = self.bn_mv[i][:L].detach().cpu().clone()
         s0n, s1n = self.SLOT_NAMES[self.optimizer]
         for slot_i, sname in ((0, s0n), (1, s1n)):
             if sname is None:
@@ -730,7 +834,7 @@ class NativeDeepFM:
     def load_tf_variables(self, tv: Dict[str, torch.Tensor]):
         """Inverse of ``tf_variables`` for replicated tables (params + slots + step)."""
         self.load_tf_params({k: torch.as_tensor(v) for k, v in tv.items()
-                             if k in ("fm_w", "fm_v") or k in self.dense_segs})
+                             if k in ("fm_w", "fm_v") or k in self.dense_segs or "moving_" in k})
         s0n, s1n = self.SLOT_NAMES[self.optimizer]
         with torch.no_grad():
             for slot_i, sname in ((0, s0n), (1, s1n)):

@@ -276,6 +276,10 @@ class GoldenDeepFM:
     def tf_variables(self) -> "OrderedDict[str, torch.Tensor]":
         return self.state_dict_local()
 
+    def replicated_state(self) -> List[torch.Tensor]:
+        """Tensors broadcast from rank 0 at start (BroadcastGlobalVariablesHook(0), HVD:372)."""
+        return list(self.params.values()) + list(self.slots.values())
+
     def _apply(self, grads: Dict[str, torch.Tensor], touched: torch.Tensor):
         lr = self.lr
         opt = self.optimizer

@@ -40,7 +40,16 @@ class HeadArgs(C.Structure):
                 ("labels", c_void_p), ("M", c_int), ("L", c_int), ("nvalid", c_int),
                 ("square_loss", c_int), ("train", c_int), ("gscale", c_float), ("scale_l", c_float),
                 ("prob", c_void_p), ("logit", c_void_p), ("dlogit", c_void_p), ("dz", c_void_p),
-                ("dz_t", c_void_p), ("partial", c_void_p)]
+                ("dz_t", c_void_p), ("partial", c_void_p), ("dh", c_void_p)]
+
+
+class BnArgs(C.Structure):
+    _fields_ = [("M", c_int), ("N", c_int), ("nvalid", c_int), ("r", c_void_p), ("dh", c_void_p),
+                ("gamma", c_void_p), ("beta", c_void_p), ("mm", c_void_p), ("mv", c_void_p),
+                ("save", c_void_p), ("part", c_void_p), ("dgamma", c_void_p), ("dbeta", c_void_p),
+                ("eps", c_float), ("decay", c_float), ("seed", c_uint32), ("layer", c_uint32),
+                ("keep_thr", c_uint32), ("drop", c_int), ("inv_keep", c_float), ("step", c_void_p),
+                ("out", c_void_p), ("out_t", c_void_p)]
 
 
 class SlabJob(C.Structure):
@@ -109,6 +118,8 @@ _SIGS = {
     "hfm_fm_bwd_seg": [c_int] + [c_void_p] * 7 + [c_int, c_int, c_int, c_void_p, c_void_p, c_void_p],
     "hfm_seg_apply": [c_int, c_int, c_int, C.POINTER(SegApplyArgs), c_int, c_void_p],
     "hfm_seg_apply_args_bytes": [],
+    "hfm_bn": [c_int, C.POINTER(BnArgs), c_void_p],
+    "hfm_bn_args_bytes": [],
 }
 
 
@@ -141,7 +152,7 @@ def get_lib():
         for cname, pys in (("hfm_epi_args_bytes", EpiArgs), ("hfm_head_args_bytes", HeadArgs),
                            ("hfm_slab_job_bytes", SlabJob), ("hfm_rowsum_job_bytes", RowSumJob),
                            ("hfm_shadow_seg_bytes", ShadowSeg), ("hfm_opt_hyper_bytes", OptHyper),
-                           ("hfm_seg_apply_args_bytes", SegApplyArgs)):
+                           ("hfm_seg_apply_args_bytes", SegApplyArgs), ("hfm_bn_args_bytes", BnArgs)):
             n = getattr(lib, cname)()
             if n != C.sizeof(pys):
                 raise RuntimeError(f"ABI mismatch {pys.__name__}: C {n} vs ctypes {C.sizeof(pys)}")

@@ -11,7 +11,7 @@ from typing import List, Optional, Sequence
 import torch
 
 from . import _lib
-from ._lib import (EpiArgs, HeadArgs, OptHyper, RowSumJob, SegApplyArgs, ShadowSeg, SlabJob, check,
+from ._lib import (BnArgs, EpiArgs, HeadArgs, OptHyper, RowSumJob, SegApplyArgs, ShadowSeg, SlabJob, check,
                    ptr, stream_handle)
 
 EPI_F32, EPI_FWD, EPI_DGRAD, EPI_FWD_EVAL = 0, 1, 2, 3
@@ -186,6 +186,17 @@ def gemm_nt(epi, tile, A, lda, B, ldb, M, N, Kd, splitk, ep: EpiArgs):
 
 def head(a: HeadArgs):
     check(L().hfm_head(C.byref(a), stream_handle()), "head")
+
+
+BN_FWD_PARTIAL, BN_FWD_FINALIZE, BN_EVAL_FINALIZE, BN_FWD_APPLY = 0, 1, 2, 3
+BN_BWD_PARTIAL, BN_BWD_FINALIZE, BN_BWD_APPLY = 4, 5, 6
+
+
+def bn(phase: int, a: BnArgs):
+    """Batch-norm phase (csrc/kernels/bn.hip); M % 64 == 0 and N % 32 == 0 are required."""
+    if a.M % 64 or a.N % 32:
+        raise ValueError(f"bn: M={a.M} must be a multiple of 64 and N={a.N} of 32")
+    check(L().hfm_bn(phase, C.byref(a), stream_handle()), f"bn[{phase}]")
 
 
 def slab_reduce(jobs_dev, njobs, max_n):

@@ -163,3 +163,17 @@ def test_launcher_cli_two_ranks_gloo(tmp_path):
     assert idx["latest"] == "ckpt-16"
     man = _json.load(open(md / "ckpt-16" / "manifest.json"))
     assert man["world"] == 2 and os.path.exists(md / "ckpt-16" / "rank1.bin")
+
+
+def test_launcher_tf_config_mapping(monkeypatch):
+    """PS-style TF_CONFIG (reference PS:414-428) -> node layout; ps/evaluator tasks idle."""
+    import json
+    from hipfm import launch
+    cluster = {"chief": ["algo-1:2222"], "worker": ["algo-2:2222", "algo-3:2222"],
+               "ps": ["algo-1:2223", "algo-2:2223", "algo-3:2223"]}
+    monkeypatch.delenv("SM_HOSTS", raising=False)
+    monkeypatch.setenv("TF_CONFIG", json.dumps({"cluster": cluster, "task": {"type": "worker", "index": 1}}))
+    d = launch._tf_config_defaults()
+    assert d == {"nnodes": 3, "node_rank": 2, "master_addr": "algo-1"}
+    monkeypatch.setenv("TF_CONFIG", json.dumps({"cluster": cluster, "task": {"type": "ps", "index": 0}}))
+    assert launch.main(["--nproc_per_node", "1", "-m", "hipfm"]) == 0
