@@ -5,7 +5,7 @@
 // with Horovod).
 //
 // Per BN layer the step is
-//   fwd:  R = relu(X W^T + b)                 (gemm_nt EPI_FWD_EVAL, bf16 R)
+//   fwd:  R = relu(X W^T + b)                 (gemm_nt EPI_RELU_F32, f32 R)
 //         part[tile] = (sum R, sum R^2)        bn_partial<0>   (deterministic per-64-row tiles)
 //         mean, var, scale, shift, moving      bn_finalize<0>  (double reduction, fixed order)
 //         H = (R*scale + shift)*keep/keep_p    bn_apply<0>     (-> H and H^T, LDS transpose)
@@ -20,7 +20,7 @@
 
 struct BnArgs {
   int M, N, nvalid;
-  const bf16* r;          // [M,N] relu output (pre-BN)
+  const float* r;         // [M,N] relu output (pre-BN), f32
   const float* dh;        // [M,N] gradient w.r.t. the layer output (post BN + dropout)
   const float* gamma;     // [N]
   const float* beta;      // [N]
@@ -65,7 +65,7 @@ __global__ void __launch_bounds__(256) bn_partial_kernel(BnArgs a) {
     const int row = r0 + j;
     if (row < a.nvalid) {
       const size_t o = (size_t)row * a.N + col;
-      const float x = bf2f(a.r[o]);
+      const float x = a.r[o];
       if (BWD) {
         const float dy = a.dh[o] * drop_factor(a, salt, row, col);
         s0 += dy;
@@ -155,12 +155,13 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(BnArgs a) {
   uint32_t salt = 0;
   if (a.drop) salt = dropout_salt(a.seed, (uint32_t)(*a.step), a.layer);
   const size_t o = (size_t)row * N + cb;
-  const bf16x8 xr = *reinterpret_cast<const bf16x8*>(a.r + o);
+  const f32x4 xr0 = *reinterpret_cast<const f32x4*>(a.r + o);
+  const f32x4 xr1 = *reinterpret_cast<const f32x4*>(a.r + o + 4);
   bf16x8 ov;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const int col = cb + j;
-    const float x = bf2f(xr[j]);
+    const float x = j < 4 ? xr0[j] : xr1[j - 4];
     float v;
     if (BWD) {
       if (row < a.nvalid && x > 0.f) {

@@ -22,6 +22,8 @@ enum EpiMode {
   EPI_FWD = 1,        // +bias, relu, dropout -> H bf16 [M,N] and H^T bf16 [N,M]
   EPI_DGRAD = 2,      // mask by Hprev>0, *scale -> dZ bf16 [M,N] and dZ^T [N,M]
   EPI_FWD_EVAL = 3,   // +bias, relu (no dropout), H only
+  EPI_RELU_F32 = 4,   // +bias, relu -> f32 [M,N] (batch-norm input: BN divides by the batch
+                      // std, which would amplify bf16 rounding of R by mean/std)
 };
 
 struct EpiArgs {
@@ -105,6 +107,11 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_nt_kernel(
         float* C = reinterpret_cast<float*>(ep.out) + (size_t)blockIdx.z * M * N;
 #pragma unroll
         for (int j = 0; j < 4; ++j) C[(size_t)(rowb + j) * N + col] = acc[j];
+      } else if (EPI == EPI_RELU_F32) {
+        float* C = reinterpret_cast<float*>(ep.out);
+        const float bc = ep.bias[col];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) C[(size_t)(rowb + j) * N + col] = fmaxf(acc[j] + bc, 0.f);
       } else {
         bf16x4 tv;
 #pragma unroll
@@ -165,6 +172,7 @@ HFM_API int hfm_gemm_nt(int epi, int tile, const void* A, int lda, const void* B
     case EPI_FWD: return gemm_tile<EPI_FWD>(tile, a, lda, b, ldb, M, N, Kd, 1, *ep, st);
     case EPI_DGRAD: return gemm_tile<EPI_DGRAD>(tile, a, lda, b, ldb, M, N, Kd, 1, *ep, st);
     case EPI_FWD_EVAL: return gemm_tile<EPI_FWD_EVAL>(tile, a, lda, b, ldb, M, N, Kd, 1, *ep, st);
+    case EPI_RELU_F32: return gemm_tile<EPI_RELU_F32>(tile, a, lda, b, ldb, M, N, Kd, 1, *ep, st);
     default: return (int)hipErrorInvalidValue;
   }
 }

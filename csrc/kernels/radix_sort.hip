@@ -200,7 +200,9 @@ HFM_API int hfm_radix_sort_ids(const int* keys_in, int* keys_out, int* perm_out,
 // =============================================================================================
 // Onesweep variant: ONE global-histogram kernel for all digit passes + ONE kernel per pass that
 // ranks its tile, finds its per-digit offset with a decoupled look-back over the earlier tiles,
-// and scatters.  4 passes (30-bit ids) = 1 memset + 5 launches instead of 16.
+// and scatters.  4 passes (30-bit ids) = 1 memset + 5 launches instead of 16: inside a HIP graph
+// every kernel boundary costs a few us (L2 release/acquire across the 8 XCDs, measured with
+// tools/bench_launch.py), so launch count matters as much as bandwidth at this size.
 //
 // Inter-workgroup protocol (guide §6 Guideline 16, "R2: the data IS the flag"): each tile
 // publishes, per digit, one 32-bit word {2-bit state | 30-bit count} with a relaxed agent-scope
@@ -211,16 +213,17 @@ HFM_API int hfm_radix_sort_ids(const int* keys_in, int* keys_out, int* perm_out,
 // Spins are bounded; a timeout sets an error word instead of hanging the GPU.
 // The status words and tickets are zeroed by a hipMemsetAsync node before every sort.
 namespace {
-constexpr int OS_ITEMS = 8;
-constexpr int OS_TILE = RS_THREADS * OS_ITEMS;      // 2048 keys per tile
+constexpr int OS_ITEMS = 16;
+constexpr int OS_TILE = RS_THREADS * OS_ITEMS;      // 4096 keys per tile (156 tiles at n = 640K)
 constexpr unsigned OS_AGG = 1u << 30, OS_INC = 2u << 30, OS_VAL = (1u << 30) - 1;
 constexpr int OS_MAX_PASSES = 4;
+constexpr int OS_HIST_BLOCKS = 128;
 }  // namespace
 
 __global__ void __launch_bounds__(RS_THREADS) os_hist_kernel(const int* __restrict__ keys, int n,
                                                             int passes, unsigned* __restrict__ ghist) {
   __shared__ unsigned h[OS_MAX_PASSES][RS_RADIX];
-  for (int p = 0; p < passes; ++p) h[p][threadIdx.x] = 0;
+  for (int p = 0; p < OS_MAX_PASSES; ++p) h[p][threadIdx.x] = 0;
   __syncthreads();
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     const int k = keys[i];
@@ -231,56 +234,96 @@ __global__ void __launch_bounds__(RS_THREADS) os_hist_kernel(const int* __restri
     if (h[p][threadIdx.x]) atomicAdd(&ghist[p * RS_RADIX + threadIdx.x], h[p][threadIdx.x]);
 }
 
+// Exclusive scan of one value per thread (256 threads) -> returns the exclusive prefix and
+// leaves the block total in *total.  Wave-level shuffles + one LDS exchange of 4 wave sums.
+__device__ __forceinline__ int block_excl_scan256(int v, int* wsum, int* total) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  int x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) wsum[wv] = x;
+  __syncthreads();
+  int pre = 0;
+  for (int w = 0; w < wv; ++w) pre += wsum[w];
+  *total = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+  return pre + x - v;
+}
+
+// One onesweep pass.  Ranking is wave-private: wave w owns the contiguous quarter
+// [w*64*IT, (w+1)*64*IT) of the tile and walks it 64 keys at a time, keeping running per-digit
+// counts in its own LDS row (no block barrier inside the loop; a lane's rank among same-digit
+// lanes comes from 8 ballots).  One barrier then turns the 4 wave rows into wave-exclusive
+// offsets and the tile histogram, which is published for the look-back before the tile's
+// global base is resolved.  Keys are reordered in LDS so the global stores are runs of one
+// digit.
+template <int IT>
 __global__ void __launch_bounds__(RS_THREADS) os_pass_kernel(
     const int* __restrict__ keys_in, const int* __restrict__ vals_in, int* __restrict__ keys_out,
     int* __restrict__ vals_out, int n, int shift, const unsigned* __restrict__ ghist_p,
     unsigned* __restrict__ status, unsigned* __restrict__ ticket, unsigned* __restrict__ err) {
-  __shared__ int cnt[RS_RADIX];
-  __shared__ int wcnt[4][RS_RADIX];
-  __shared__ int base[RS_RADIX];
+  constexpr int TILE = RS_THREADS * IT;
+  __shared__ int whist[4][RS_RADIX];
+  __shared__ int lbase[RS_RADIX];
+  __shared__ int gbase[RS_RADIX];
+  __shared__ int wsum[4];
+  __shared__ int lk[TILE];
+  __shared__ int lv[TILE];
   __shared__ unsigned tile_s;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   if (tid == 0) tile_s = atomicAdd(ticket, 1u);
-  cnt[tid] = 0;
-  wcnt[0][tid] = wcnt[1][tid] = wcnt[2][tid] = wcnt[3][tid] = 0;
+  whist[0][tid] = whist[1][tid] = whist[2][tid] = whist[3][tid] = 0;
   __syncthreads();
   const int tile = (int)tile_s;
-  const int b0 = tile * OS_TILE;
-  int kr[OS_ITEMS], vr[OS_ITEMS], dr[OS_ITEMS];
+  const int b0 = tile * TILE;
+  const int w0 = b0 + wv * 64 * IT;
+  int kr[IT], vr[IT], rr[IT];
 #pragma unroll
-  for (int k = 0; k < OS_ITEMS; ++k) {
-    const int i = b0 + k * RS_THREADS + tid;
-    kr[k] = i < n ? keys_in[i] : 0;
+  for (int k = 0; k < IT; ++k) {
+    const int i = w0 + k * 64 + lane;
+    kr[k] = i < n ? keys_in[i] : -1;
     vr[k] = i < n ? (vals_in ? vals_in[i] : i) : 0;
-    dr[k] = (kr[k] >> shift) & (RS_RADIX - 1);
   }
-  // tile histogram (LDS atomics) -> publish the aggregate as early as possible
-  __shared__ int th[RS_RADIX];
-  th[tid] = 0;
-  __syncthreads();
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  int* wh = whist[wv];
 #pragma unroll
-  for (int k = 0; k < OS_ITEMS; ++k)
-    if (b0 + k * RS_THREADS + tid < n) atomicAdd(&th[dr[k]], 1);
-  __syncthreads();
-  const unsigned mine = (unsigned)th[tid];
-  unsigned* st = status + (size_t)tile * RS_RADIX;
-  __hip_atomic_store(&st[tid], (tile == 0 ? OS_INC : OS_AGG) | mine, __ATOMIC_RELAXED,
-                     __HIP_MEMORY_SCOPE_AGENT);
-  // global digit base: exclusive scan of this pass's global histogram (in LDS)
-  base[tid] = (int)ghist_p[tid];
-  __syncthreads();
-  for (int off = 1; off < RS_RADIX; off <<= 1) {
-    const int v = tid >= off ? base[tid - off] : 0;
-    __syncthreads();
-    base[tid] += v;
-    __syncthreads();
+  for (int k = 0; k < IT; ++k) {
+    const bool valid = kr[k] >= 0;
+    const int d = (kr[k] >> shift) & (RS_RADIX - 1);
+    unsigned long long peers = __ballot(valid);
+#pragma unroll
+    for (int bit = 0; bit < RS_BITS; ++bit) {
+      const bool bset = (d >> bit) & 1;
+      const unsigned long long bal = __ballot(bset);
+      peers &= bset ? bal : ~bal;
+    }
+    const int rk = __popcll(peers & lt);
+    const int old = wh[d];                 // LDS ops of one wave execute in order: every lane
+    rr[k] = old + rk;                      // reads before the leader's update below lands
+    if (valid && rk == 0) wh[d] = old + __popcll(peers);
   }
-  int excl_digit = base[tid] - (int)ghist_p[tid];
-  // decoupled look-back over earlier tiles for digit tid, 16 predecessors per round (the 16
-  // status loads are independent and issued together; a round costs ~one L2 round trip)
+  __syncthreads();
+  // per digit (thread tid): wave-exclusive offsets + tile count
+  const int c0 = whist[0][tid], c1 = whist[1][tid], c2 = whist[2][tid], c3 = whist[3][tid];
+  const int mine = c0 + c1 + c2 + c3;
+  unsigned* st = status + (size_t)tile * RS_RADIX;
+  __hip_atomic_store(&st[tid], (tile == 0 ? OS_INC : OS_AGG) | (unsigned)mine, __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+  whist[0][tid] = 0;
+  whist[1][tid] = c0;
+  whist[2][tid] = c0 + c1;
+  whist[3][tid] = c0 + c1 + c2;
+  int tot;
+  lbase[tid] = block_excl_scan256(mine, wsum, &tot);
+  __syncthreads();
+  const int g = (int)ghist_p[tid];
+  const int gex = block_excl_scan256(g, wsum + 0, &tot);
+  // decoupled look-back for digit tid: 32 predecessor words per round
   unsigned prefix = 0;
   if (tile > 0) {
-    constexpr int W = 16;
+    constexpr int W = 32;
     int j = tile - 1;
     unsigned spins = 0;
     while (j >= 0) {
@@ -290,7 +333,6 @@ __global__ void __launch_bounds__(RS_THREADS) os_pass_kernel(
         w[q] = (j - q >= 0) ? __hip_atomic_load(&status[(size_t)(j - q) * RS_RADIX + tid],
                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                             : OS_INC;
-      // usable prefix of the window: stop at the first not-yet-published word
       unsigned acc = 0;
       int q = 0;
       bool done = false;
@@ -308,40 +350,31 @@ __global__ void __launch_bounds__(RS_THREADS) os_pass_kernel(
         __builtin_amdgcn_s_sleep(1);
         continue;
       }
-      j -= q;   // consumed q aggregates; continue below them
+      j -= q;
     }
-    __hip_atomic_store(&st[tid], OS_INC | (prefix + mine), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&st[tid], OS_INC | (prefix + (unsigned)mine), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  }
+  gbase[tid] = gex + (int)prefix;
+  __syncthreads();
+  // reorder the tile by digit in LDS, then store runs of one digit
+#pragma unroll
+  for (int k = 0; k < IT; ++k) {
+    if (kr[k] >= 0) {
+      const int d = (kr[k] >> shift) & (RS_RADIX - 1);
+      const int lp = lbase[d] + wh[d] + rr[k];
+      lk[lp] = kr[k];
+      lv[lp] = vr[k];
+    }
   }
   __syncthreads();
-  base[tid] = excl_digit + (int)prefix;
-  __syncthreads();
-  const unsigned long long lt = (1ull << lane) - 1ull;
-#pragma unroll
-  for (int k = 0; k < OS_ITEMS; ++k) {
-    const int i = b0 + k * RS_THREADS + tid;
-    const bool valid = i < n;
-    const int d = dr[k];
-    unsigned long long peers = __ballot(valid);
-#pragma unroll
-    for (int bit = 0; bit < RS_BITS; ++bit) {
-      const bool bset = (d >> bit) & 1;
-      const unsigned long long bal = __ballot(bset);
-      peers &= bset ? bal : ~bal;
-    }
-    const int rk = __popcll(peers & lt);
-    if (valid && rk == 0) wcnt[wv][d] = __popcll(peers);
-    __syncthreads();
-    if (valid) {
-      int r = cnt[d] + rk;
-      for (int w = 0; w < wv; ++w) r += wcnt[w][d];
-      const int dst = base[d] + r;
-      keys_out[dst] = kr[k];
-      vals_out[dst] = vr[k];
-    }
-    __syncthreads();
-    cnt[tid] += wcnt[0][tid] + wcnt[1][tid] + wcnt[2][tid] + wcnt[3][tid];
-    wcnt[0][tid] = wcnt[1][tid] = wcnt[2][tid] = wcnt[3][tid] = 0;
-    __syncthreads();
+  const int nloc = min(TILE, n - b0);
+  for (int j = tid; j < nloc; j += RS_THREADS) {
+    const int key = lk[j];
+    const int d = (key >> shift) & (RS_RADIX - 1);
+    const int dst = gbase[d] + (j - lbase[d]);
+    keys_out[dst] = key;
+    vals_out[dst] = lv[j];
   }
 }
 
@@ -375,7 +408,7 @@ HFM_API int hfm_onesweep_sort_ids(const int* keys_in, int* keys_out, int* perm_o
   hipError_t e = hipMemsetAsync(t, 0, 8192 + status_words * 4, st);
   if (e != hipSuccess) return (int)e;
   int hg = (n + RS_THREADS - 1) / RS_THREADS;
-  if (hg > 1024) hg = 1024;
+  if (hg > OS_HIST_BLOCKS) hg = OS_HIST_BLOCKS;
   hipLaunchKernelGGL(os_hist_kernel, dim3(hg), dim3(RS_THREADS), 0, st, keys_in, n, passes, ghist);
   const int* ki = keys_in;
   const int* vi = nullptr;
@@ -383,7 +416,7 @@ HFM_API int hfm_onesweep_sort_ids(const int* keys_in, int* keys_out, int* perm_o
     const bool to_out = ((passes - 1 - p) % 2) == 0;
     int* ko = to_out ? keys_out : pk;
     int* vo = to_out ? perm_out : pv;
-    hipLaunchKernelGGL(os_pass_kernel, dim3(tiles), dim3(RS_THREADS), 0, st, ki, vi, ko, vo, n,
+    hipLaunchKernelGGL(os_pass_kernel<OS_ITEMS>, dim3(tiles), dim3(RS_THREADS), 0, st, ki, vi, ko, vo, n,
                        p * RS_BITS, ghist + p * RS_RADIX, status + (size_t)p * tiles * RS_RADIX,
                        tickets + p, err);
     ki = ko;

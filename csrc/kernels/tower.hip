@@ -1,0 +1,335 @@
+// Fused deep tower (SURVEY §2.5 rows 7, 9-12, 15-16 "small-N specialization fuses the whole
+// tower, with activations kept in LDS"): for a block of 32 samples ONE workgroup runs
+//
+//   forward   H_i = dropout(relu(H_{i-1} W_i^T + b_i))      i = 0..nl-1   (H_{-1} = E, global)
+//   head      y = y_fm + H_last . w_out + b_out, p, loss, dlogit, dZ_last
+//   dgrad     dZ_{i-1} = (dZ_i W_i) (.) [H_{i-1} > 0] / keep   (row-local: needs only this block)
+//             dX0      =  dZ_0 W_0
+//
+// with every H_i and dZ_i tile resident in LDS (bf16, rows padded by 8 elements), weights read
+// from L2 as MFMA B fragments, and only what later kernels need written to HBM: H_i^T and
+// dZ_i^T (operands of the batch-reduction wgrad GEMMs), dX0 (FM backward), prob / dlogit and
+// per-block head partials.  This replaces 3 forward GEMMs + head + 3 dgrad GEMMs (7 launches;
+// each kernel boundary in a HIP graph costs a few us on MI355X, see tools/bench_launch.py) by
+// one.  The weight gradients (reductions over the whole batch) run afterwards as ONE grouped
+// launch (wgrad_group_kernel) whose unit of work is a single wave owning a 32x32 tile of one
+// layer's split-K slab.
+//
+// MFMA: v_mfma_f32_16x16x32_bf16, one wave = 32x32 outputs (2x2 tiles); A fragment lane l:
+// A[l&15][8(l>>4)+j], B fragment B[8(l>>4)+j][l&15]; C: col = l&15, row = (l>>4)*4 + j.
+// Dropout masks: counter hash, flat index (global row) * Npad + col, identical to mlp.hip.
+#include "common.h"
+
+constexpr int TW_MAXL = 8;
+constexpr int TW_ROWS = 32;
+
+struct TowerArgs {
+  int M, nvalid, nl, K0p;
+  int Np[TW_MAXL];
+  const bf16* E;                  // [M, K0p]
+  const bf16* W[TW_MAXL];         // [Np_i, Kp_i]
+  const bf16* WT[TW_MAXL];        // [Kp_i, Np_i]
+  const float* bias[TW_MAXL];
+  uint32_t keep_thr[TW_MAXL];
+  float inv_keep[TW_MAXL];
+  int drop[TW_MAXL];
+  uint32_t seed;
+  int train;                      // 1: forward + head + dgrad chain; 0: forward + head (eval)
+  int square_loss;
+  float gscale;                   // 1 / global batch
+  const int64_t* step;
+  const float* w_out;             // [Np_last]
+  const float* b_out;             // [1]
+  const float* y_fm;              // [M]
+  const float* labels;            // [M] or null
+  bf16* Ht[TW_MAXL];              // [Np_i, M]   (train)
+  bf16* dZt[TW_MAXL];             // [Np_i, M]   (train)
+  bf16* dX0;                      // [M, K0p]    (train)
+  float* prob;                    // [M]
+  float* dlogit;                  // [M]         (train)
+  float* partial;                 // [M/32, Np_last + 2]
+  int h_off[TW_MAXL];             // LDS element offsets of the H tiles
+  int dz_off[2];                  // LDS element offsets of the two dZ tiles
+  int lds_bytes;
+};
+
+// One wave: c[2][2] += A[32 x 32*nk] . B[32 x 32*nk]^T, both K-contiguous (row strides lda/ldb
+// in elements).  Register ring of PF k-steps so PF fragment sets are in flight.
+template <int PF>
+__device__ __forceinline__ void mma32(const bf16* __restrict__ A, int lda, const bf16* __restrict__ B,
+                                      int ldb, int nk, int lane, f32x4& c00, f32x4& c01, f32x4& c10,
+                                      f32x4& c11) {
+  const int r = lane & 15, kq = (lane >> 4) * 8;
+  const bf16* a0 = A + r * lda + kq;
+  const bf16* a1 = a0 + 16 * lda;
+  const bf16* b0 = B + r * ldb + kq;
+  const bf16* b1 = b0 + 16 * ldb;
+  bf16x8 ra0[PF], ra1[PF], rb0[PF], rb1[PF];
+#pragma unroll
+  for (int j = 0; j < PF; ++j) {
+    if (j < nk) {
+      ra0[j] = *reinterpret_cast<const bf16x8*>(a0 + j * 32);
+      ra1[j] = *reinterpret_cast<const bf16x8*>(a1 + j * 32);
+      rb0[j] = *reinterpret_cast<const bf16x8*>(b0 + j * 32);
+      rb1[j] = *reinterpret_cast<const bf16x8*>(b1 + j * 32);
+    }
+  }
+  for (int kb = 0; kb < nk; kb += PF) {
+#pragma unroll
+    for (int j = 0; j < PF; ++j) {
+      const int ks = kb + j;
+      if (ks < nk) {
+        c00 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ra0[j], rb0[j], c00, 0, 0, 0);
+        c01 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ra0[j], rb1[j], c01, 0, 0, 0);
+        c10 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ra1[j], rb0[j], c10, 0, 0, 0);
+        c11 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ra1[j], rb1[j], c11, 0, 0, 0);
+        const int kn = (ks + PF) * 32;
+        if (ks + PF < nk) {
+          ra0[j] = *reinterpret_cast<const bf16x8*>(a0 + kn);
+          ra1[j] = *reinterpret_cast<const bf16x8*>(a1 + kn);
+          rb0[j] = *reinterpret_cast<const bf16x8*>(b0 + kn);
+          rb1[j] = *reinterpret_cast<const bf16x8*>(b1 + kn);
+        }
+      }
+    }
+  }
+}
+
+// Copy a [32 x N] bf16 LDS tile (row stride ld) to its transpose in global memory:
+// out[c * M + row0 + r]; each thread moves 8 consecutive rows of one column (16-B stores).
+__device__ __forceinline__ void store_tile_t(const bf16* t, int ld, int N, bf16* out, int M, int row0) {
+  for (int e = threadIdx.x; e < N * 4; e += blockDim.x) {
+    const int c = e >> 2, r8 = (e & 3) * 8;
+    bf16x8 v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = t[(r8 + j) * ld + c];
+    *reinterpret_cast<bf16x8*>(out + (size_t)c * M + row0 + r8) = v;
+  }
+}
+
+__global__ void __launch_bounds__(256) tower_kernel(TowerArgs a) {
+  extern __shared__ __align__(16) unsigned char tw_lds_raw[];
+  bf16* lds = reinterpret_cast<bf16*>(tw_lds_raw);
+  __shared__ float s_dl[TW_ROWS];
+  __shared__ float s_loss[TW_ROWS];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int row0 = blockIdx.x * TW_ROWS;
+  const int cr = (lane >> 4) * 4, cc = lane & 15;
+  const uint32_t step = (uint32_t)(*a.step);
+  const int nl = a.nl;
+
+  // ------------------------------------------------------------------ forward
+  for (int i = 0; i < nl; ++i) {
+    const int N = a.Np[i];
+    const int Kp = i == 0 ? a.K0p : a.Np[i - 1];
+    const int ldh = N + 8;
+    bf16* Hl = lds + a.h_off[i];
+    const bool drop = a.train && a.drop[i];
+    const uint32_t salt = drop ? dropout_salt(a.seed, step, (uint32_t)i) : 0u;
+    const float sc = a.inv_keep[i];
+    for (int ct = wave; ct < N / 32; ct += 4) {
+      f32x4 c00 = {0, 0, 0, 0}, c01 = c00, c10 = c00, c11 = c00;
+      const bf16* Bw = a.W[i] + (size_t)ct * 32 * Kp;
+      if (i == 0)
+        mma32<4>(a.E + (size_t)row0 * a.K0p, a.K0p, Bw, Kp, Kp / 32, lane, c00, c01, c10, c11);
+      else
+        mma32<2>(lds + a.h_off[i - 1], Kp + 8, Bw, Kp, Kp / 32, lane, c00, c01, c10, c11);
+      f32x4 acc[2][2] = {{c00, c01}, {c10, c11}};
+#pragma unroll
+      for (int ti = 0; ti < 2; ++ti) {
+#pragma unroll
+        for (int tj = 0; tj < 2; ++tj) {
+          const int col = ct * 32 + tj * 16 + cc;
+          const float bc = a.bias[i][col];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int row = ti * 16 + cr + j;
+            float v = fmaxf(acc[ti][tj][j] + bc, 0.f);
+            if (drop)
+              v = dropout_keep((uint32_t)((row0 + row) * N + col), salt, a.keep_thr[i]) ? v * sc : 0.f;
+            Hl[row * ldh + col] = f2bf(v);
+          }
+        }
+      }
+    }
+    __syncthreads();
+    if (a.train) store_tile_t(Hl, ldh, N, a.Ht[i], a.M, row0);
+  }
+
+  // ------------------------------------------------------------------ head
+  const int L = a.Np[nl - 1];
+  {
+    const bf16* H = lds + a.h_off[nl - 1];
+    const int ldh = L + 8;
+    const int row = tid >> 3, q = tid & 7, Q = L / 8;
+    const int grow = row0 + row;
+    float yd = 0.f;
+    for (int j = 0; j < Q; ++j) yd += bf2f(H[row * ldh + q * Q + j]) * a.w_out[q * Q + j];
+    yd += __shfl_xor(yd, 1, 64);
+    yd += __shfl_xor(yd, 2, 64);
+    yd += __shfl_xor(yd, 4, 64);
+    const float y = a.y_fm[grow] + yd + a.b_out[0];
+    const float p = 1.f / (1.f + __expf(-y));
+    float dl = 0.f, lossb = 0.f;
+    if (a.labels && grow < a.nvalid) {
+      const float lab = a.labels[grow];
+      if (a.square_loss) {
+        lossb = (p - lab) * (p - lab);
+        dl = 2.f * (p - lab) * p * (1.f - p) * a.gscale;
+      } else {
+        lossb = fmaxf(y, 0.f) - y * lab + log1pf(__expf(-fabsf(y)));
+        dl = (p - lab) * a.gscale;
+      }
+    }
+    if (q == 0) {
+      a.prob[grow] = p;
+      s_dl[row] = dl;
+      s_loss[row] = lossb;
+      if (a.train) a.dlogit[grow] = dl;
+    }
+    if (a.train) {
+      bf16* Z = lds + a.dz_off[0];
+      const int ldz = L + 8;
+      const float sl = a.inv_keep[nl - 1];
+      for (int j = 0; j < Q; ++j) {
+        const int col = q * Q + j;
+        const float g = bf2f(H[row * ldh + col]) > 0.f ? dl * a.w_out[col] * sl : 0.f;
+        Z[row * ldz + col] = f2bf(g);
+      }
+    }
+    __syncthreads();
+    // block partials [sum_rows dl*h (L) | sum dl | sum loss], fixed summation order
+    float* part = a.partial + (size_t)blockIdx.x * (L + 2);
+    for (int c = tid; c < L + 2; c += blockDim.x) {
+      float s = 0.f;
+      if (c < L) {
+        if (a.train)
+          for (int r = 0; r < TW_ROWS; ++r) s += s_dl[r] * bf2f(H[r * ldh + c]);
+      } else if (c == L) {
+        for (int r = 0; r < TW_ROWS; ++r) s += s_dl[r];
+      } else {
+        for (int r = 0; r < TW_ROWS; ++r) s += s_loss[r];
+      }
+      part[c] = s;
+    }
+  }
+  if (!a.train) return;
+  store_tile_t(lds + a.dz_off[0], L + 8, L, a.dZt[nl - 1], a.M, row0);
+
+  // ------------------------------------------------------------------ dgrad chain
+  int cur = 0;
+  for (int i = nl - 1; i >= 1; --i) {
+    const int Nout = a.Np[i - 1], Kin = a.Np[i];
+    const bf16* Az = lds + a.dz_off[cur];
+    bf16* Zo = lds + a.dz_off[cur ^ 1];
+    const bf16* Hp = lds + a.h_off[i - 1];
+    const int ldh = Nout + 8, ldz_in = Kin + 8, ldz_out = Nout + 8;
+    const float sc = a.inv_keep[i - 1];
+    for (int ct = wave; ct < Nout / 32; ct += 4) {
+      f32x4 c00 = {0, 0, 0, 0}, c01 = c00, c10 = c00, c11 = c00;
+      mma32<2>(Az, ldz_in, a.WT[i] + (size_t)ct * 32 * Kin, Kin, Kin / 32, lane, c00, c01, c10, c11);
+      f32x4 acc[2][2] = {{c00, c01}, {c10, c11}};
+#pragma unroll
+      for (int ti = 0; ti < 2; ++ti) {
+#pragma unroll
+        for (int tj = 0; tj < 2; ++tj) {
+          const int col = ct * 32 + tj * 16 + cc;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int row = ti * 16 + cr + j;
+            const float v = bf2f(Hp[row * ldh + col]) > 0.f ? acc[ti][tj][j] * sc : 0.f;
+            Zo[row * ldz_out + col] = f2bf(v);
+          }
+        }
+      }
+    }
+    __syncthreads();
+    store_tile_t(Zo, ldz_out, Nout, a.dZt[i - 1], a.M, row0);
+    cur ^= 1;
+  }
+  {
+    const int N0 = a.Np[0];
+    const bf16* Az = lds + a.dz_off[cur];
+    for (int ct = wave; ct < a.K0p / 32; ct += 4) {
+      f32x4 c00 = {0, 0, 0, 0}, c01 = c00, c10 = c00, c11 = c00;
+      mma32<2>(Az, N0 + 8, a.WT[0] + (size_t)ct * 32 * N0, N0, N0 / 32, lane, c00, c01, c10, c11);
+      f32x4 acc[2][2] = {{c00, c01}, {c10, c11}};
+#pragma unroll
+      for (int ti = 0; ti < 2; ++ti) {
+#pragma unroll
+        for (int tj = 0; tj < 2; ++tj) {
+          const int col = ct * 32 + tj * 16 + cc;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int row = row0 + ti * 16 + cr + j;
+            a.dX0[(size_t)row * a.K0p + col] = f2bf(acc[ti][tj][j]);
+          }
+        }
+      }
+    }
+  }
+}
+
+HFM_API int hfm_tower(const TowerArgs* ap, hipStream_t st) {
+  const TowerArgs& a = *ap;
+  if (a.M % TW_ROWS || a.nl < 1 || a.nl > TW_MAXL || a.K0p % 32) return (int)hipErrorInvalidValue;
+  for (int i = 0; i < a.nl; ++i)
+    if (a.Np[i] % 32 || a.Np[i] <= 0) return (int)hipErrorInvalidValue;
+  if (a.Np[a.nl - 1] % 8) return (int)hipErrorInvalidValue;
+  if (a.lds_bytes > 160 * 1024 - 1024) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(tower_kernel, dim3(a.M / TW_ROWS), dim3(256), a.lds_bytes, st, a);
+  HFM_LAUNCH_CHECK();
+}
+HFM_API int hfm_tower_args_bytes() { return (int)sizeof(TowerArgs); }
+
+// ---------------------------------------------------------------------------------------------
+// Grouped weight-gradient GEMMs: dW_i = dZ_i^T X_i for every layer in ONE launch.  A wave task
+// is (job, split z, tile_m, tile_n) with tile_n fastest, so the 4 waves of a workgroup usually
+// share the same dZ^T rows.  Output: f32 slab z of job j at out + z * M * N.
+struct WgJob {
+  const bf16* A;   // [M, K] = dZ_i^T  (M = Np_i, K = batch)
+  const bf16* B;   // [N, K] = X_i^T   (N = Kp_i)
+  float* out;      // [splitk, M, N]
+  int lda, ldb;
+  int M, N;
+  int tiles_m, tiles_n, splitk, kchunk;
+  int task0;       // first global wave-task of this job
+  int pad;
+};
+
+__global__ void __launch_bounds__(256) wgrad_group_kernel(const WgJob* __restrict__ jobs, int njobs,
+                                                          int ntasks) {
+  const int lane = threadIdx.x & 63;
+  const int task = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (task >= ntasks) return;
+  int j = 0;
+  while (j + 1 < njobs && task >= jobs[j + 1].task0) ++j;
+  const WgJob jb = jobs[j];
+  int t = task - jb.task0;
+  const int tn = t % jb.tiles_n;
+  t /= jb.tiles_n;
+  const int tm = t % jb.tiles_m;
+  const int z = t / jb.tiles_m;
+  const int row0 = tm * 32, col0 = tn * 32, k0 = z * jb.kchunk;
+  f32x4 c00 = {0, 0, 0, 0}, c01 = c00, c10 = c00, c11 = c00;
+  mma32<4>(jb.A + (size_t)row0 * jb.lda + k0, jb.lda, jb.B + (size_t)col0 * jb.ldb + k0, jb.ldb,
+           jb.kchunk / 32, lane, c00, c01, c10, c11);
+  float* C = jb.out + (size_t)z * jb.M * jb.N;
+  const int cr = (lane >> 4) * 4, cc = lane & 15;
+  f32x4 acc[2][2] = {{c00, c01}, {c10, c11}};
+#pragma unroll
+  for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+    for (int tj = 0; tj < 2; ++tj)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        C[(size_t)(row0 + ti * 16 + cr + q) * jb.N + col0 + tj * 16 + cc] = acc[ti][tj][q];
+}
+
+HFM_API int hfm_wgrad_group(const void* jobs_dev, int njobs, int ntasks, hipStream_t st) {
+  if (ntasks <= 0) return 0;
+  hipLaunchKernelGGL(wgrad_group_kernel, dim3((ntasks + 3) / 4), dim3(256), 0, st,
+                     (const WgJob*)jobs_dev, njobs, ntasks);
+  HFM_LAUNCH_CHECK();
+}
+HFM_API int hfm_wg_job_bytes() { return (int)sizeof(WgJob); }

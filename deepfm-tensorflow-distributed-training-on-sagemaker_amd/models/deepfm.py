@@ -25,6 +25,7 @@ Reference parity cites: model_fn HVD:141-287, optimizer HVD:252-263, LR scaling 
 from __future__ import annotations
 
 import math
+import os
 from collections import OrderedDict
 from dataclasses import dataclass
 from typing import Dict, List, Optional
@@ -32,7 +33,7 @@ from typing import Dict, List, Optional
 import torch
 
 from ..ops import kernels as KN
-from ..ops._lib import BnArgs, EpiArgs, HeadArgs, RowSumJob, SegApplyArgs, ShadowSeg, SlabJob
+from ..ops._lib import TW_MAXL, BnArgs, EpiArgs, HeadArgs, TowerArgs, WgJob, RowSumJob, SegApplyArgs, ShadowSeg, SlabJob
 from ..utils.rng import keep_threshold
 from .reference import glorot_std, init_params, pad32
 
@@ -98,7 +99,7 @@ class NativeDeepFM:
                  sparse_update: str = "tf1_dense", seed: int = 1234, batch_size: int = 1024,
                  device="cuda", comm=None, init: bool = True, batch_norm: bool = False,
                  batch_norm_decay: float = 0.9, adam_epsilon: float = 1e-8,
-                 adagrad_init: float = 1e-8):
+                 adagrad_init: float = 1e-8, fused: Optional[bool] = None):
         self.batch_norm = bool(batch_norm)
         self.bn_decay = float(batch_norm_decay)
         self.bn_eps = 1e-3          # tf.contrib.layers.batch_norm default epsilon (PS:289)
@@ -192,6 +193,13 @@ class NativeDeepFM:
         self.h_dense = KN.hyper(self.lr, 0.0, eps=adam_epsilon)
         self._bufs_M = 0
         self.batch_size = int(batch_size)
+        # fused deep tower (csrc/kernels/tower.hip): whole forward + head + dgrad chain in one
+        # launch per 32-sample block; batch norm (needs batch-wide statistics between the
+        # GEMMs) and towers whose activations do not fit in LDS use the per-layer kernels
+        can_fuse = (not self.batch_norm and len(self.layers) <= TW_MAXL and
+                    self._tower_lds_bytes() <= 150 * 1024)
+        want = os.environ.get("HIPFM_FUSED_TOWER", "1") != "0" if fused is None else bool(fused)
+        self.fused = can_fuse and want
         if init:
             if self.V * self.K <= (1 << 24):
                 # small tables: the exact golden initialization (CPU generator, bit-reproducible)
@@ -237,6 +245,10 @@ class NativeDeepFM:
             self.sv = [e, e, e, e]
             self.sd = [e, e]
 
+    def _tower_lds_bytes(self) -> int:
+        h = sum(32 * (n + 8) * 2 for n in self.Np)
+        return h + 2 * 32 * (max(self.Np) + 8) * 2
+
     @staticmethod
     def _padM(B: int) -> int:
         return max(128, (B + 127) // 128 * 128)
@@ -264,19 +276,26 @@ class NativeDeepFM:
         self.dZt = [torch.zeros(n, M, **bf) for n in self.Np]
         self.dX0 = torch.zeros(M, K0p, **bf)            # layer-1 input gradient (bf16)
         if self.batch_norm:
-            self.Rb = [torch.zeros(M, n, **bf) for n in self.Np]          # relu output (pre-BN)
+            self.Rb = [torch.zeros(M, n, **f32) for n in self.Np]         # relu output (pre-BN)
             self.dH = [torch.zeros(M, n, **f32) for n in self.Np]         # dL/d(layer output)
             self.bn_save = [torch.zeros(6, n, **f32) for n in self.Np]
             self.bn_part = torch.zeros(M // 64, 2 * max(self.Np), **f32)
         self.prob = torch.zeros(M, **f32)
         self.dlogit = torch.zeros(M, **f32)
-        self.nhead = (M + 63) // 64      # head kernel: 64 samples per workgroup
+        # head partial rows: one per 64-sample head workgroup, or per 32-sample tower block
+        self.nhead = M // 32 if self.fused else (M + 63) // 64
         self.partial = torch.zeros(self.nhead, self.Np[-1] + 2, **f32)
         self.loss_sum = torch.zeros(1, **f32)
         # wgrad split-K configuration + slabs
         self.wg_cfg = []
         for i in range(len(self.layers)):
             Mg, Ng, Kd = self.Np[i], self.Kp[i], M
+            if self.fused:
+                s = int(os.environ.get("HIPFM_WG_SPLIT", "32"))
+                while s > 1 and (M % (32 * s) or M // s < 128):
+                    s //= 2
+                self.wg_cfg.append((None, s))
+                continue
             t = _pick_tile(Mg, Ng, row_major_stream=False)
             s = _pick_splitk(Mg, Ng, Kd, t)
             self.wg_cfg.append((t, s))
@@ -297,6 +316,8 @@ class NativeDeepFM:
         tb = max(KN.radix_temp_bytes(n), KN.rbk_temp_bytes(K, n), KN.scan_temp_bytes(n))
         self.temp = torch.zeros(tb + 256, dtype=torch.uint8, device=dev)
         self._build_finalize_jobs()
+        if self.fused:
+            self._build_wgrad_jobs()
         self._bufs_M = M
         self._own_in = (self.idx, self.vals, self.labels)
         self._graphs = {}
@@ -333,6 +354,78 @@ class NativeDeepFM:
         self._row_jobs = KN.struct_array_to_device(rj, self.device)
         self._nrow_jobs = len(rj)
         self._row_total = sum(self.Np)
+
+    def _build_wgrad_jobs(self):
+        jobs, task0 = [], 0
+        M = self.M
+        for i in range(len(self.layers)):
+            s = self.wg_cfg[i][1]
+            Xt = self.Et if i == 0 else self.Ht[i - 1]
+            j = WgJob()
+            j.A, j.B, j.out = self.dZt[i].data_ptr(), Xt.data_ptr(), self.slabs[i].data_ptr()
+            j.lda = j.ldb = M
+            j.M, j.N = self.Np[i], self.Kp[i]
+            j.tiles_m, j.tiles_n = self.Np[i] // 32, self.Kp[i] // 32
+            j.splitk, j.kchunk = s, M // s
+            j.task0 = task0
+            task0 += j.tiles_m * j.tiles_n * s
+            jobs.append(j)
+        self._wg_jobs = KN.struct_array_to_device(jobs, self.device)
+        self._nwg_jobs = len(jobs)
+        self._wg_tasks = task0
+
+    def _tower_args(self, B: int, train: bool, with_labels: bool = True) -> TowerArgs:
+        a = TowerArgs()
+        nl = len(self.layers)
+        a.M, a.nvalid, a.nl, a.K0p = self.M, B, nl, self.K0p
+        pb = self.p.data_ptr()
+        off = 0
+        for i in range(nl):
+            a.Np[i] = self.Np[i]
+            a.W[i] = self.W16[i].data_ptr()
+            a.WT[i] = self.WT16[i].data_ptr()
+            a.bias[i] = pb + 4 * self.dense_segs[f"Deep-part/mlp{i}/biases"].off
+            keep = self.keep[i]
+            a.keep_thr[i] = min(keep_threshold(keep), 0xFFFFFFFF)
+            a.inv_keep[i] = (1.0 / keep) if keep < 1.0 else 1.0
+            a.drop[i] = 1 if keep < 1.0 else 0
+            a.Ht[i] = self.Ht[i].data_ptr()
+            a.dZt[i] = self.dZt[i].data_ptr()
+            a.h_off[i] = off
+            off += 32 * (self.Np[i] + 8)
+        a.dz_off[0] = off
+        a.dz_off[1] = off + 32 * (max(self.Np) + 8)
+        a.lds_bytes = self._tower_lds_bytes()
+        a.E = self.E.data_ptr()
+        a.seed = self.seed & 0xFFFFFFFF
+        a.train = 1 if train else 0
+        a.square_loss = 1 if self.loss_type == "square_loss" else 0
+        a.gscale = 1.0 / (B * self.world)
+        a.step = self.step.data_ptr()
+        a.w_out = pb + 4 * self.dense_segs["Deep-part/deep_out/weights"].off
+        a.b_out = pb + 4 * self.dense_segs["Deep-part/deep_out/biases"].off
+        a.y_fm = self.y_fm.data_ptr()
+        a.labels = self.labels.data_ptr() if with_labels else 0
+        a.dX0 = self.dX0.data_ptr()
+        a.prob = self.prob.data_ptr()
+        a.dlogit = self.dlogit.data_ptr()
+        a.partial = self.partial.data_ptr()
+        return a
+
+    def _dense_fwd_bwd(self, B: int):
+        """Forward, loss head and the whole deep-tower backward (dense grads into self.g, dX0
+        for the FM backward).  Returns the (idx, table) pair the sparse backward uses."""
+        if self.fused:
+            idx, tv = self._fm_forward(B, train=True)
+            KN.tower(self._tower_args(B, train=True))
+            KN.wgrad_group(self._wg_jobs, self._nwg_jobs, self._wg_tasks)
+            KN.slab_reduce(self._slab_jobs, self._nslab_jobs, self._slab_maxn)
+            KN.rowsum(self._row_jobs, self._nrow_jobs, self._row_total)
+            return idx, tv
+        idx, tv = self._forward(B, train=True)
+        self._head(B, train=True)
+        self._mlp_backward(B)
+        return idx, tv
 
     # ------------------------------------------------------------------ parameters
     def load_tf_params(self, params: Dict[str, torch.Tensor]):
@@ -417,7 +510,7 @@ class NativeDeepFM:
         return B
 
     # ------------------------------------------------------------------ forward pieces
-    def _forward(self, B: int, train: bool):
+    def _fm_forward(self, B: int, train: bool):
         M, F, K = self.M, self.F, self.K
         idx = self.idx
         tv, tw = self.tv, self.tw
@@ -426,6 +519,11 @@ class NativeDeepFM:
         fm_bias = self.p[self.dense_segs["fm_bias"].off:]
         KN.fm_fwd(idx, self.vals, tv, tw, fm_bias, M, F, K, self.K0p, self.y_fm, self.S, self.E,
                   self.Et if train else None)
+        return idx, tv
+
+    def _forward(self, B: int, train: bool):
+        M = self.M
+        idx, tv = self._fm_forward(B, train)
         X = self.E
         for i in range(len(self.layers)):
             s = self.dense_segs[f"Deep-part/mlp{i}/biases"]
@@ -444,7 +542,7 @@ class NativeDeepFM:
             N = self.Np[i]
             if self.batch_norm:
                 ep.out, ep.out_t = self.Rb[i].data_ptr(), 0
-                KN.gemm_nt(KN.EPI_FWD_EVAL, _pick_tile(M, N), X, self.Kp[i], self.W16[i],
+                KN.gemm_nt(KN.EPI_RELU_F32, _pick_tile(M, N), X, self.Kp[i], self.W16[i],
                            self.Kp[i], M, N, self.Kp[i], 1, ep)
                 self._bn_forward(i, B, train)
             else:
@@ -622,9 +720,7 @@ class NativeDeepFM:
     # ------------------------------------------------------------------ public step API
     def train_step_enqueue(self, B: int):
         """Enqueue one full training step on the current stream (no host sync)."""
-        idx, tv = self._forward(B, train=True)
-        self._head(B, train=True)
-        self._mlp_backward(B)
+        idx, tv = self._dense_fwd_bwd(B)
         work = None
         if self.exchange:
             work = self.comm.allreduce_dense_async(self.g)
@@ -643,9 +739,7 @@ class NativeDeepFM:
         if self.sharded:
             raise NotImplementedError("compute_grads is single-rank / replicated only")
         B = self.stage_batch(ids, vals, labels)
-        idx, tv = self._forward(B, train=True)
-        self._head(B, train=True)
-        self._mlp_backward(B)
+        self._dense_fwd_bwd(B)
         n = B * self.F
         KN.sort_ids(self.idx, self.sorted_keys, None, self.perm, n, self.end_bit, self.temp)
         self._segment_reduce(n, compact=True)
@@ -725,6 +819,10 @@ class NativeDeepFM:
         return float(self.l2 * 0.5 * s)
 
     def predict_enqueue(self, B: int, with_labels: bool = False):
+        if self.fused:
+            self._fm_forward(B, train=False)
+            KN.tower(self._tower_args(B, train=False, with_labels=with_labels))
+            return
         self._forward(B, train=False)
         self._head(B, train=False, with_labels=with_labels)
 

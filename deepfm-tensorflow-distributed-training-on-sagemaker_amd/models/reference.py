@@ -64,6 +64,11 @@ def xavier_uniform_(t: torch.Tensor, gen: Optional[torch.Generator] = None) -> t
     return t
 
 
+def _bf16_round(t: torch.Tensor) -> torch.Tensor:
+    """Round to bf16 and back (autograd: the gradient is rounded to bf16 on the way back)."""
+    return t.to(torch.bfloat16).to(torch.float32)
+
+
 def param_shapes(V: int, F: int, K: int, layers: List[int], batch_norm: bool) -> "OrderedDict[str, tuple]":
     shapes = OrderedDict()
     shapes["fm_bias"] = (1,)
@@ -129,7 +134,10 @@ class GoldenDeepFM:
                  optimizer: str = "Adam", loss_type: str = "log_loss",
                  sparse_update: str = "tf1_dense", seed: int = 1234, world_size: int = 1,
                  device="cpu", params: Optional[Dict[str, torch.Tensor]] = None,
-                 adam_epsilon: float = 1e-8, adagrad_init: float = 1e-8):
+                 adam_epsilon: float = 1e-8, adagrad_init: float = 1e-8, mlp_bf16: bool = False):
+        # mlp_bf16: round the deep-tower GEMM operands to bf16 like the native MFMA path does
+        # (tests use it to separate kernel bugs from bf16 rounding amplified by batch norm)
+        self.mlp_bf16 = bool(mlp_bf16)
         self.adam_eps = float(adam_epsilon)      # TF AdamOptimizer epsilon (HVD:253)
         self.adagrad_init = float(adagrad_init)  # initial_accumulator_value (HVD:255)
         self.V, self.F, self.K = int(feature_size), int(field_size), int(embedding_size)
@@ -189,7 +197,10 @@ class GoldenDeepFM:
         y_v = 0.5 * (S * S - (E * E).sum(1)).sum(1)
         h = E.reshape(B, self.F * self.K)
         for i, L in enumerate(self.layers):
-            h = torch.relu(h @ P[f"Deep-part/mlp{i}/weights"] + P[f"Deep-part/mlp{i}/biases"])
+            w = P[f"Deep-part/mlp{i}/weights"]
+            if self.mlp_bf16:
+                h, w = _bf16_round(h), _bf16_round(w)
+            h = torch.relu(h @ w + P[f"Deep-part/mlp{i}/biases"])
             if self.batch_norm:
                 h = self._bn(h, i, P, train)
             if train and self.keep[i] < 1.0:

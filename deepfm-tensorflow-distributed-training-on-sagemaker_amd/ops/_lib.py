@@ -76,6 +76,28 @@ class SegApplyArgs(C.Structure):
                 ("step", c_void_p)]
 
 
+TW_MAXL = 8
+
+
+class TowerArgs(C.Structure):
+    _fields_ = [("M", c_int), ("nvalid", c_int), ("nl", c_int), ("K0p", c_int),
+                ("Np", c_int * TW_MAXL), ("E", c_void_p), ("W", c_void_p * TW_MAXL),
+                ("WT", c_void_p * TW_MAXL), ("bias", c_void_p * TW_MAXL),
+                ("keep_thr", c_uint32 * TW_MAXL), ("inv_keep", c_float * TW_MAXL),
+                ("drop", c_int * TW_MAXL), ("seed", c_uint32), ("train", c_int),
+                ("square_loss", c_int), ("gscale", c_float), ("step", c_void_p),
+                ("w_out", c_void_p), ("b_out", c_void_p), ("y_fm", c_void_p), ("labels", c_void_p),
+                ("Ht", c_void_p * TW_MAXL), ("dZt", c_void_p * TW_MAXL), ("dX0", c_void_p),
+                ("prob", c_void_p), ("dlogit", c_void_p), ("partial", c_void_p),
+                ("h_off", c_int * TW_MAXL), ("dz_off", c_int * 2), ("lds_bytes", c_int)]
+
+
+class WgJob(C.Structure):
+    _fields_ = [("A", c_void_p), ("B", c_void_p), ("out", c_void_p), ("lda", c_int), ("ldb", c_int),
+                ("M", c_int), ("N", c_int), ("tiles_m", c_int), ("tiles_n", c_int),
+                ("splitk", c_int), ("kchunk", c_int), ("task0", c_int), ("pad", c_int)]
+
+
 _SIGS = {
     "hfm_fm_fwd": [c_void_p] * 5 + [c_int] * 4 + [c_void_p] * 4 + [c_void_p],
     "hfm_fm_bwd_sorted": [c_void_p] * 7 + [c_int] * 4 + [c_void_p, c_void_p],
@@ -119,6 +141,10 @@ _SIGS = {
     "hfm_seg_apply": [c_int, c_int, c_int, C.POINTER(SegApplyArgs), c_int, c_void_p],
     "hfm_seg_apply_args_bytes": [],
     "hfm_bn": [c_int, C.POINTER(BnArgs), c_void_p],
+    "hfm_tower": [C.POINTER(TowerArgs), c_void_p],
+    "hfm_tower_args_bytes": [],
+    "hfm_wgrad_group": [c_void_p, c_int, c_int, c_void_p],
+    "hfm_wg_job_bytes": [],
     "hfm_bn_args_bytes": [],
 }
 
@@ -152,7 +178,8 @@ def get_lib():
         for cname, pys in (("hfm_epi_args_bytes", EpiArgs), ("hfm_head_args_bytes", HeadArgs),
                            ("hfm_slab_job_bytes", SlabJob), ("hfm_rowsum_job_bytes", RowSumJob),
                            ("hfm_shadow_seg_bytes", ShadowSeg), ("hfm_opt_hyper_bytes", OptHyper),
-                           ("hfm_seg_apply_args_bytes", SegApplyArgs), ("hfm_bn_args_bytes", BnArgs)):
+                           ("hfm_seg_apply_args_bytes", SegApplyArgs), ("hfm_bn_args_bytes", BnArgs),
+                           ("hfm_tower_args_bytes", TowerArgs), ("hfm_wg_job_bytes", WgJob)):
             n = getattr(lib, cname)()
             if n != C.sizeof(pys):
                 raise RuntimeError(f"ABI mismatch {pys.__name__}: C {n} vs ctypes {C.sizeof(pys)}")

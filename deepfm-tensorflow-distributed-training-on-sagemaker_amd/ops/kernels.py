@@ -11,10 +11,10 @@ from typing import List, Optional, Sequence
 import torch
 
 from . import _lib
-from ._lib import (BnArgs, EpiArgs, HeadArgs, OptHyper, RowSumJob, SegApplyArgs, ShadowSeg, SlabJob, check,
+from ._lib import (BnArgs, EpiArgs, HeadArgs, TowerArgs, WgJob, OptHyper, RowSumJob, SegApplyArgs, ShadowSeg, SlabJob, check,
                    ptr, stream_handle)
 
-EPI_F32, EPI_FWD, EPI_DGRAD, EPI_FWD_EVAL = 0, 1, 2, 3
+EPI_F32, EPI_FWD, EPI_DGRAD, EPI_FWD_EVAL, EPI_RELU_F32 = 0, 1, 2, 3, 4
 OPT_IDS = {"Adam": 0, "Adagrad": 1, "Momentum": 2, "ftrl": 3, "GD": 4}
 
 # tile ids of hfm_gemm_nt: (rows per block, cols per block)
@@ -186,6 +186,16 @@ def gemm_nt(epi, tile, A, lda, B, ldb, M, N, Kd, splitk, ep: EpiArgs):
 
 def head(a: HeadArgs):
     check(L().hfm_head(C.byref(a), stream_handle()), "head")
+
+
+def tower(a: TowerArgs):
+    """Fused deep tower: forward + head (+ dgrad chain when a.train) (csrc/kernels/tower.hip)."""
+    check(L().hfm_tower(C.byref(a), stream_handle()), "tower")
+
+
+def wgrad_group(jobs_dev, njobs: int, ntasks: int):
+    """All layers' split-K weight-gradient GEMMs in one launch (wave-granular tasks)."""
+    check(L().hfm_wgrad_group(ptr(jobs_dev), njobs, ntasks, stream_handle()), "wgrad_group")
 
 
 BN_FWD_PARTIAL, BN_FWD_FINALIZE, BN_EVAL_FINALIZE, BN_FWD_APPLY = 0, 1, 2, 3

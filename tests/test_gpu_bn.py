@@ -44,20 +44,27 @@ def test_bn_gradients_match_golden(B):
     nat = NativeDeepFM(V, F, K, layers, keep, batch_size=B, device=DEV, init=False, batch_norm=True)
     nat.load_tf_params(params)
     gold = GoldenDeepFM(V, F, K, layers, keep, params=params, batch_norm=True)
+    # the same model with bf16-rounded GEMM operands: BN divides by small batch stds, which
+    # amplifies bf16 rounding (measured: up to ~9% of max|grad| vs fp32 on small-var columns),
+    # so the tight check is against bf16-emulating autograd and the fp32 check is looser
+    gold16 = GoldenDeepFM(V, F, K, layers, keep, params=params, batch_norm=True, mlp_bf16=True)
     ids, vals, labels = synth.batch(B, step=0)
     _, data, gg = gold.compute_grads(ids, vals, labels)
+    _, _, gg16 = gold16.compute_grads(ids, vals, labels)
     g, uk, UG = nat.compute_grads(ids.to(DEV, torch.int32), vals.to(DEV), labels.to(DEV))
     torch.cuda.synchronize()
     assert abs(nat.loss_value(B) - float(data)) < 2e-3
     dense = nat.dense_tf_params(g)
     for k, v in dense.items():
-        ref = gg[k]
-        scale = ref.abs().max().item() + 1e-12
-        assert (v - ref).abs().max().item() <= 0.08 * scale + 1e-6, (k, (v - ref).abs().max(), scale)
+        for ref, tol in ((gg16[k], 0.03), (gg[k], 0.15)):
+            scale = ref.abs().max().item() + 1e-12
+            err = (v - ref).abs().max().item()
+            assert err <= tol * scale + 1e-6, (k, tol, err, scale)
     uk = uk.long().cpu()
-    gv = gg["fm_v"][uk] - 1e-4 * params["fm_v"][uk]
-    sv = gv.abs().max().item()
-    assert (UG.cpu()[:, :K] - gv).abs().max().item() <= 0.05 * sv
+    for ref, tol in ((gg16, 0.03), (gg, 0.1)):
+        gv = ref["fm_v"][uk] - 1e-4 * params["fm_v"][uk]
+        sv = gv.abs().max().item()
+        assert (UG.cpu()[:, :K] - gv).abs().max().item() <= tol * sv, tol
     # moving statistics after one update (golden updated them inside compute_grads)
     tv = nat.tf_variables()
     for i in range(len(layers)):
@@ -76,7 +83,8 @@ def test_bn_train_eval_match_golden():
     nat = NativeDeepFM(V, F, K, layers, keep, sparse_update="lazy", batch_size=256, device=DEV,
                        init=False, learning_rate=lr, **kw)
     nat.load_tf_params(params)
-    gold = GoldenDeepFM(V, F, K, layers, keep, sparse_update="lazy", params=params, learning_rate=lr, **kw)
+    gold = GoldenDeepFM(V, F, K, layers, keep, sparse_update="lazy", params=params, learning_rate=lr,
+                        mlp_bf16=True, **kw)
     steps = 3
     for s in range(steps):
         ids, vals, labels = synth.batch(256, step=s)

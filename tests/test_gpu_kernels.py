@@ -269,3 +269,36 @@ def test_graph_replay_equals_eager():
         b.train_step(ids, vals, labels, use_graph=True)
     torch.cuda.synchronize()
     assert torch.equal(a.tv, b.tv) and torch.equal(a.p, b.p)   # bitwise: deterministic kernels
+
+
+@pytest.mark.parametrize("layers,K", [([64, 32], 8), ([256, 128, 64], 16)])
+def test_fused_tower_matches_per_layer_kernels(layers, K):
+    """tower.hip (one launch: fwd + head + dgrad chain, grouped wgrad) vs the per-layer GEMMs."""
+    synth = make_synth("total:4000", seed=13)
+    F = synth.F
+    V = synth.feature_size
+    keep = [0.5] * len(layers)
+    params = init_params(V, F, K, layers, False, seed=8)
+    a = NativeDeepFM(V, F, K, layers, keep, batch_size=500, device=DEV, init=False, fused=True)
+    b = NativeDeepFM(V, F, K, layers, keep, batch_size=500, device=DEV, init=False, fused=False)
+    assert a.fused and not b.fused
+    a.load_tf_params(params)
+    b.load_tf_params(params)
+    ids, vals, labels = synth.batch(500, step=0)
+    args = (ids.to(DEV, torch.int32), vals.to(DEV), labels.to(DEV))
+    ga, uka, UGa = a.compute_grads(*args)
+    gb, ukb, UGb = b.compute_grads(*args)
+    torch.cuda.synchronize()
+    # same MFMA k-order; only the head's dot-product summation order differs (ulp-level), which
+    # can flip single bf16 roundings downstream
+    assert abs(a.loss_value(500) - b.loss_value(500)) < 1e-5
+    assert torch.allclose(a.prob[:500], b.prob[:500], atol=2e-6, rtol=0)
+    dxa, dxb = a.dX0[:500].float(), b.dX0[:500].float()
+    assert (dxa - dxb).abs().max().item() <= 1e-2 * dxb.abs().max().item()
+    scale = gb.abs().max().item()
+    assert (ga - gb).abs().max().item() <= 1e-2 * scale + 1e-7
+    assert torch.equal(uka, ukb)
+    assert (UGa - UGb).abs().max().item() <= 1e-2 * UGb.abs().max().item()
+    pa = a.predict(*args[:2])
+    pb = b.predict(*args[:2])
+    assert torch.allclose(pa, pb, atol=2e-6, rtol=0)

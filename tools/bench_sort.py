@@ -1,4 +1,5 @@
-"""Microbenchmark: id sort (hipCUB radix SortPairs) vs torch.sort at DeepFM batch sizes."""
+"""Microbenchmark: id sorts at DeepFM batch sizes, timed as HIP-graph replays (the way the train
+step runs them; eager timing would mostly measure host launch cost)."""
 import sys
 import time
 
@@ -9,19 +10,32 @@ import hipfm  # noqa: E402
 from hipfm.ops import kernels as KN  # noqa: E402
 
 
-def timeit(fn, reps=20):
+def timeit(fn, reps=20, inner=10):
     fn()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g):
+            for _ in range(inner):
+                fn()
+    torch.cuda.current_stream().wait_stream(s)
+    g.replay()
     torch.cuda.synchronize()
     t = time.perf_counter()
     for _ in range(reps):
-        fn()
+        g.replay()
     torch.cuda.synchronize()
-    return (time.perf_counter() - t) / reps * 1e6
+    return (time.perf_counter() - t) / (reps * inner) * 1e6
 
 
 def main():
     dev = torch.device("cuda", 0)
-    for n in (39 * 1024, 39 * 16384, 39 * 32768, 39 * 65536):
+    sizes = (39 * 1024, 39 * 16384, 39 * 32768, 39 * 65536)
+    if "--only" in sys.argv:
+        sizes = (int(sys.argv[sys.argv.index("--only") + 1]),)
+    for n in sizes:
         for bits in (21, 30):
             keys = torch.randint(0, 1 << bits, (n,), dtype=torch.int32, device=dev)
             sk = torch.empty_like(keys)
@@ -33,6 +47,10 @@ def main():
             tl = timeit(lambda: KN.lsd_sort_ids(keys, sk, perm, n, bits, temp))
             t1 = timeit(lambda: KN.cub_sort_ids(keys, sk, tmp, perm, n, bits, temp))
             t2 = timeit(lambda: torch.sort(keys, stable=True))
+            KN.onesweep_sort_ids(keys, sk, perm, n, bits, temp)
+            ref_k, ref_p = torch.sort(keys.long(), stable=True)
+            ok = torch.equal(sk.long(), ref_k) and torch.equal(perm.long(), ref_p)
+            assert KN.sort_error(temp) == 0 and ok, "onesweep sort mismatch"
             print(f"n={n:8d} bits={bits}: onesweep {t0:8.1f} us  lsd {tl:8.1f} us  hipcub SortPairs {t1:8.1f} us   "
                   f"torch.sort {t2:8.1f} us", flush=True)
 
