@@ -164,13 +164,19 @@ static inline bool rd_varint(const uint8_t*& p, const uint8_t* e, uint64_t& v) {
   return false;
 }
 
+// true if [p, p + n) lies inside [p, e)  (length compare: no out-of-range pointer arithmetic,
+// found by the UBSan self-test, csrc/io/io_selftest.cpp)
+static inline bool fits(const uint8_t* p, const uint8_t* e, uint64_t n) {
+  return n <= (uint64_t)(e - p);
+}
+
 static bool skip_field(const uint8_t*& p, const uint8_t* e, int wt) {
   uint64_t v;
   switch (wt) {
     case 0: return rd_varint(p, e, v);
-    case 1: p += 8; return p <= e;
-    case 2: if (!rd_varint(p, e, v)) return false; p += v; return p <= e;
-    case 5: p += 4; return p <= e;
+    case 1: if (!fits(p, e, 8)) return false; p += 8; return true;
+    case 2: if (!rd_varint(p, e, v) || !fits(p, e, v)) return false; p += v; return true;
+    case 5: if (!fits(p, e, 4)) return false; p += 4; return true;
     default: return false;
   }
 }
@@ -190,13 +196,14 @@ static long decode_list(const uint8_t* p, const uint8_t* e, bool is_float, float
     if (is_float) {
       if (wt == 2) {
         uint64_t ln;
-        if (!rd_varint(p, e, ln) || p + ln > e) return -1;
+        if (!rd_varint(p, e, ln) || !fits(p, e, ln)) return -1;
         long k = (long)(ln / 4);
         if (n + k > cap) return -2;
         memcpy(fdst + n, p, k * 4);
         n += k;
         p += ln;
       } else if (wt == 5) {
+        if (!fits(p, e, 4)) return -1;
         if (n + 1 > cap) return -2;
         memcpy(fdst + n, p, 4);
         n++;
@@ -205,7 +212,7 @@ static long decode_list(const uint8_t* p, const uint8_t* e, bool is_float, float
     } else {
       if (wt == 2) {
         uint64_t ln;
-        if (!rd_varint(p, e, ln) || p + ln > e) return -1;
+        if (!rd_varint(p, e, ln) || !fits(p, e, ln)) return -1;
         const uint8_t* q = p;
         const uint8_t* qe = p + ln;
         while (q < qe) {
@@ -239,7 +246,7 @@ static bool decode_example(const uint8_t* p, size_t len, int F, float* label, in
       continue;
     }
     uint64_t ln;
-    if (!rd_varint(p, e, ln) || p + ln > e) return false;
+    if (!rd_varint(p, e, ln) || !fits(p, e, ln)) return false;
     const uint8_t* fp = p;           // Features
     const uint8_t* fe = p + ln;
     p = fe;
@@ -251,7 +258,7 @@ static bool decode_example(const uint8_t* p, size_t len, int F, float* label, in
         continue;
       }
       uint64_t l2;
-      if (!rd_varint(fp, fe, l2) || fp + l2 > fe) return false;
+      if (!rd_varint(fp, fe, l2) || !fits(fp, fe, l2)) return false;
       const uint8_t* mp = fp;        // map entry {key=1, value=2}
       const uint8_t* me = fp + l2;
       fp = me;
@@ -267,7 +274,7 @@ static bool decode_example(const uint8_t* p, size_t len, int F, float* label, in
           if (!skip_field(mp, me, k3 & 7)) return false;
           continue;
         }
-        if (!rd_varint(mp, me, l3) || mp + l3 > me) return false;
+        if (!rd_varint(mp, me, l3) || !fits(mp, me, l3)) return false;
         if ((k3 >> 3) == 1) {
           name = (const char*)mp;
           nlen = l3;
@@ -281,7 +288,7 @@ static bool decode_example(const uint8_t* p, size_t len, int F, float* label, in
       // Feature { oneof bytes=1 float=2 int64=3 }
       const uint8_t* q = vp;
       uint64_t k4, l4;
-      if (!rd_varint(q, ve, k4) || (k4 & 7) != 2 || !rd_varint(q, ve, l4) || q + l4 > ve) return false;
+      if (!rd_varint(q, ve, k4) || (k4 & 7) != 2 || !rd_varint(q, ve, l4) || !fits(q, ve, l4)) return false;
       const int kind = (int)(k4 >> 3);
       if (nlen == 5 && !memcmp(name, "label", 5) && kind == 2) {
         if (decode_list(q, q + l4, true, label, nullptr, 1) != 1) return false;

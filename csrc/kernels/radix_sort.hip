@@ -12,6 +12,7 @@
 // k*256 + w*64 + l), so (k, w, l) order == input order and the scatter is stable.
 #include <hipcub/hipcub.hpp>
 #include "common.h"
+#include <stdlib.h>
 
 namespace {
 constexpr int RS_BITS = 8;
@@ -263,7 +264,8 @@ template <int IT>
 __global__ void __launch_bounds__(RS_THREADS) os_pass_kernel(
     const int* __restrict__ keys_in, const int* __restrict__ vals_in, int* __restrict__ keys_out,
     int* __restrict__ vals_out, int n, int shift, const unsigned* __restrict__ ghist_p,
-    unsigned* __restrict__ status, unsigned* __restrict__ ticket, unsigned* __restrict__ err) {
+    unsigned* __restrict__ status, unsigned* __restrict__ ticket, unsigned* __restrict__ err,
+    int debug_nolb) {
   constexpr int TILE = RS_THREADS * IT;
   __shared__ int whist[4][RS_RADIX];
   __shared__ int lbase[RS_RADIX];
@@ -320,41 +322,42 @@ __global__ void __launch_bounds__(RS_THREADS) os_pass_kernel(
   __syncthreads();
   const int g = (int)ghist_p[tid];
   const int gex = block_excl_scan256(g, wsum + 0, &tot);
-  // decoupled look-back for digit tid: 32 predecessor words per round
+  // decoupled look-back for digit tid.  Every tile publishes its aggregate right after ranking,
+  // so predecessors' words are read in batches of W independent loads (one memory round trip
+  // per batch) and only a still-unpublished word is re-polled; the walk stops at the first
+  // inclusive prefix.
   unsigned prefix = 0;
-  if (tile > 0) {
-    constexpr int W = 32;
+  if (tile > 0 && !debug_nolb) {
+    constexpr int W = 64;
     int j = tile - 1;
-    unsigned spins = 0;
-    while (j >= 0) {
+    bool done = false;
+    while (!done && j >= 0) {
       unsigned w[W];
 #pragma unroll
       for (int q = 0; q < W; ++q)
         w[q] = (j - q >= 0) ? __hip_atomic_load(&status[(size_t)(j - q) * RS_RADIX + tid],
                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                            : OS_INC;
-      unsigned acc = 0;
-      int q = 0;
-      bool done = false;
-      for (; q < W; ++q) {
-        const unsigned state = w[q] & ~OS_VAL;
-        if (state == 0) break;
-        if (j - q < 0) { done = true; break; }
-        acc += w[q] & OS_VAL;
-        if (state == OS_INC) { done = true; break; }
+                            : 0u;
+#pragma unroll
+      for (int q = 0; q < W; ++q) {
+        if (done || j - q < 0) continue;
+        unsigned v = w[q];
+        unsigned spins = 0;
+        while ((v & ~OS_VAL) == 0u) {
+          if (++spins > (1u << 22)) { atomicExch(err, 1u); v = OS_INC; break; }
+          __builtin_amdgcn_s_sleep(1);
+          v = __hip_atomic_load(&status[(size_t)(j - q) * RS_RADIX + tid], __ATOMIC_RELAXED,
+                                __HIP_MEMORY_SCOPE_AGENT);
+        }
+        prefix += v & OS_VAL;
+        if ((v & ~OS_VAL) == OS_INC) done = true;
       }
-      prefix += acc;
-      if (done) break;
-      if (q == 0) {
-        if (++spins > (1u << 22)) { atomicExch(err, 1u); break; }
-        __builtin_amdgcn_s_sleep(1);
-        continue;
-      }
-      j -= q;
+      j -= W;
     }
+  }
+  if (tile > 0)
     __hip_atomic_store(&st[tid], OS_INC | (prefix + (unsigned)mine), __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
-  }
   gbase[tid] = gex + (int)prefix;
   __syncthreads();
   // reorder the tile by digit in LDS, then store runs of one digit
@@ -405,6 +408,8 @@ HFM_API int hfm_onesweep_sort_ids(const int* keys_in, int* keys_out, int* perm_o
   int* pk = (int*)(((uintptr_t)(status + (size_t)OS_MAX_PASSES * tiles * RS_RADIX) + 255) & ~(uintptr_t)255);
   int* pv = pk + n;
   // one memset node zeroes histogram, tickets, error word and this sort's status words
+  // HIPFM_OS_DEBUG_NOLB=1: skip the look-back (WRONG order; only to time its share)
+  static const int debug_nolb = getenv("HIPFM_OS_DEBUG_NOLB") ? atoi(getenv("HIPFM_OS_DEBUG_NOLB")) : 0;
   hipError_t e = hipMemsetAsync(t, 0, 8192 + status_words * 4, st);
   if (e != hipSuccess) return (int)e;
   int hg = (n + RS_THREADS - 1) / RS_THREADS;
@@ -418,7 +423,7 @@ HFM_API int hfm_onesweep_sort_ids(const int* keys_in, int* keys_out, int* perm_o
     int* vo = to_out ? perm_out : pv;
     hipLaunchKernelGGL(os_pass_kernel<OS_ITEMS>, dim3(tiles), dim3(RS_THREADS), 0, st, ki, vi, ko, vo, n,
                        p * RS_BITS, ghist + p * RS_RADIX, status + (size_t)p * tiles * RS_RADIX,
-                       tickets + p, err);
+                       tickets + p, err, debug_nolb);
     ki = ko;
     vi = vo;
   }

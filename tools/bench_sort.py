@@ -1,5 +1,6 @@
 """Microbenchmark: id sorts at DeepFM batch sizes, timed as HIP-graph replays (the way the train
 step runs them; eager timing would mostly measure host launch cost)."""
+import os
 import sys
 import time
 
@@ -50,7 +51,8 @@ def main():
             KN.onesweep_sort_ids(keys, sk, perm, n, bits, temp)
             ref_k, ref_p = torch.sort(keys.long(), stable=True)
             ok = torch.equal(sk.long(), ref_k) and torch.equal(perm.long(), ref_p)
-            assert KN.sort_error(temp) == 0 and ok, "onesweep sort mismatch"
+            if not os.environ.get("HIPFM_OS_DEBUG_NOLB"):
+                assert KN.sort_error(temp) == 0 and ok, "onesweep sort mismatch"
             print(f"n={n:8d} bits={bits}: onesweep {t0:8.1f} us  lsd {tl:8.1f} us  hipcub SortPairs {t1:8.1f} us   "
                   f"torch.sort {t2:8.1f} us", flush=True)
 
