@@ -72,6 +72,83 @@ __global__ void __launch_bounds__(256) fm_fwd_kernel(
   if (sub == 0) y_fm[b] = bias[0] + yw + 0.5f * yv;
 }
 
+// fm_fwd2: one thread per (sample, field) pair for the gathers — a workgroup owns SB = 256/K
+// samples (32 at K = 8, i.e. 512 workgroups for a 16K batch instead of 128 with one lane group
+// per sample looping over the fields), so the random row reads of the whole batch are in flight
+// at once.  The scaled rows e = V[id]*x go to an LDS tile [SB][F*K+1] (fp32); the per-sample
+// sums S, sum e^2 and y_w are then reduced in fixed field order (deterministic), and E^T is
+// written from the tile with 32-sample contiguous runs.
+template <int K>
+__global__ void __launch_bounds__(256) fm_fwd2_kernel(
+    const int* __restrict__ idx, const float* __restrict__ vals, const float* __restrict__ tv,
+    const float* __restrict__ tw, const float* __restrict__ bias, int B, int F, int KP,
+    float* __restrict__ y_fm, float* __restrict__ S, bf16* __restrict__ E, bf16* __restrict__ Et) {
+  constexpr int SB = 256 / K;
+  constexpr int V4 = K / 4;
+  extern __shared__ __attribute__((aligned(16))) float fsm[];
+  const int RS = F * K + 1;            // padded tile row (bank spread for the E^T pass)
+  float* et = fsm;                     // [SB][RS]
+  float* wx = fsm + SB * RS;           // [SB][F]
+  const int s0 = blockIdx.x * SB;
+  const int nsb = min(SB, B - s0);
+  const int npair = nsb * F;
+  const size_t base = (size_t)s0 * F;
+#pragma unroll 4
+  for (int p = threadIdx.x; p < npair; p += 256) {
+    const int id = idx[base + p];
+    const float x = vals[base + p];
+    const f32x4* row = reinterpret_cast<const f32x4*>(tv + (size_t)id * K);
+    f32x4 v[V4];
+#pragma unroll
+    for (int j = 0; j < V4; ++j) v[j] = row[j];
+    const float w = tw[id];
+    const int sl = p / F, f = p - sl * F;
+    wx[sl * F + f] = w * x;
+    float* dst = et + sl * RS + f * K;
+    bf16* eo = E + (size_t)(s0 + sl) * KP + f * K;
+#pragma unroll
+    for (int j = 0; j < V4; ++j) {
+      const f32x4 e = v[j] * x;
+      dst[4 * j + 0] = e[0];
+      dst[4 * j + 1] = e[1];
+      dst[4 * j + 2] = e[2];
+      dst[4 * j + 3] = e[3];
+      bf16x4 eh = {f2bf(e[0]), f2bf(e[1]), f2bf(e[2]), f2bf(e[3])};
+      *reinterpret_cast<bf16x4*>(eo + 4 * j) = eh;
+    }
+  }
+  __syncthreads();
+  {  // per (sample, k): S, sum e^2, y_w, y_v — fixed order over fields
+    const int sl = threadIdx.x / K, k = threadIdx.x % K;
+    float sum = 0.f, sq = 0.f, yw = 0.f;
+    if (sl < nsb) {
+      const float* er = et + sl * RS + k;
+      for (int f = 0; f < F; ++f) {
+        const float e = er[f * K];
+        sum += e;
+        sq += e * e;
+      }
+      for (int f = k; f < F; f += K) yw += wx[sl * F + f];
+      if (S) S[(size_t)(s0 + sl) * K + k] = sum;
+    }
+    float yv = sum * sum - sq;
+#pragma unroll
+    for (int o = 1; o < K; o <<= 1) {
+      yv += __shfl_xor(yv, o, 64);
+      yw += __shfl_xor(yw, o, 64);
+    }
+    if (sl < nsb && k == 0) y_fm[s0 + sl] = bias[0] + yw + 0.5f * yv;
+  }
+  if (Et) {
+    const int sl = threadIdx.x % SB;
+    if (sl < nsb) {
+      const int FK = F * K;
+      for (int c = threadIdx.x / SB; c < FK; c += 256 / SB)
+        Et[(size_t)c * B + s0 + sl] = f2bf(et[sl * RS + c]);
+    }
+  }
+}
+
 // Gradient rows in SORTED order (i = position in the id-sorted slot list):
 //   dE[b,f,:] = dX0[b, f*K:(f+1)*K] + dy_b * (S_b - E_bf)        (E_bf = V[row]*x)
 //   G[i].v    = x * dE[b,f,:]     (d fm_v row)     G[i].w = dy_b * x   (d fm_w)
@@ -111,10 +188,19 @@ template <int K>
 static int launch_fm_fwd(const int* idx, const float* vals, const float* tv, const float* tw,
                          const float* bias, int B, int F, int KP, float* y_fm, float* S, bf16* E,
                          bf16* Et, hipStream_t st) {
+  constexpr int SB = 256 / K;
+  const size_t lds2 = ((size_t)SB * (F * K + 1) + (size_t)SB * F) * 4;
+  if (lds2 <= 120 * 1024) {
+    const int grid = (B + SB - 1) / SB;
+    hipLaunchKernelGGL(fm_fwd2_kernel<K>, dim3(grid), dim3(256), lds2, st, idx, vals, tv, tw, bias,
+                       B, F, KP, y_fm, S, E, Et);
+    HFM_LAUNCH_CHECK();
+  }
+  // very wide inputs (F*K > ~30K): lane-group-per-sample variant, small LDS footprint
   constexpr int LPS = K / 4;
-  constexpr int SB = 256 / LPS;
-  const int grid = (B + SB - 1) / SB;
-  const size_t lds = (size_t)SB * F * 8;
+  constexpr int SB1 = 256 / LPS;
+  const int grid = (B + SB1 - 1) / SB1;
+  const size_t lds = (size_t)SB1 * F * 8;
   hipLaunchKernelGGL(fm_fwd_kernel<K>, dim3(grid), dim3(256), lds, st, idx, vals, tv, tw, bias, B,
                      F, KP, y_fm, S, E, Et);
   HFM_LAUNCH_CHECK();

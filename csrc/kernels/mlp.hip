@@ -324,6 +324,8 @@ struct SlabJob {
   long src_ld;     // source row stride (elements; == n if contiguous)
   int cols;        // dst/src columns per row (to map linear index -> src offset with src_ld)
   float scale;
+  int lanes;       // finalize_kernel: slab-lanes per output (2 or 8); 256/lanes outputs per block
+  int chunk0;      // finalize_kernel: first block of this job
 };
 
 // blockIdx.y = job.  A workgroup owns 32 consecutive output elements; its 8 slab-lanes per
@@ -356,6 +358,59 @@ __global__ void __launch_bounds__(256) slab_reduce_kernel(const SlabJob* __restr
   }
 }
 
+// One launch for the whole gradient finalize: blocks [0, nslab_blocks) reduce split-K slabs and
+// head partials (job j owns blocks [chunk0_j, chunk0_j + ceil(n_j / (256 / lanes_j)))), the
+// remaining blocks compute bias gradients as row sums of dZ^T (one block per row).  Every
+// reduction has a fixed order (deterministic).
+struct RowSumJob;
+__device__ void rowsum_block(const RowSumJob* jobs, int njobs, int b);
+
+__global__ void __launch_bounds__(256) finalize_kernel(const SlabJob* __restrict__ sj, int nsj,
+                                                       int nslab_blocks, const RowSumJob* rj,
+                                                       int nrj) {
+  const int b = blockIdx.x;
+  if (b >= nslab_blocks) {
+    rowsum_block(rj, nrj, b - nslab_blocks);
+    return;
+  }
+  int j = 0;
+  while (j + 1 < nsj && b >= sj[j + 1].chunk0) ++j;
+  const SlabJob& jr = sj[j];
+  const int lanes = jr.lanes, per = 256 / lanes;
+  const int e = threadIdx.x % per, zl = threadIdx.x / per;
+  const int i = (b - jr.chunk0) * per + e;
+  const int n = (int)jr.n, nslab = jr.nslab, stride = (int)jr.stride;
+  float s = 0.f;
+  if (i < n) {
+    const int r = i / jr.cols, c = i - r * jr.cols;
+    const float* sp = jr.src + (size_t)r * jr.src_ld + c;
+#pragma unroll 8
+    for (int z = zl; z < nslab; z += lanes) s += sp[(size_t)z * stride];
+  }
+  if (lanes == 1) {
+    if (i < n) jr.dst[i] = s * jr.scale;
+    return;
+  }
+  // lanes > 1: per in {32, 128}; combine the lanes in order through LDS
+  __shared__ float red2[256];
+  red2[threadIdx.x] = s;
+  __syncthreads();
+  if (zl == 0 && i < n) {
+    float t = 0.f;
+    for (int l = 0; l < lanes; ++l) t += red2[l * per + e];
+    jr.dst[i] = t * jr.scale;
+  }
+}
+
+HFM_API int hfm_finalize(const void* slab_jobs, int nsj, int nslab_blocks, const void* row_jobs,
+                         int nrj, int total_rows, hipStream_t st) {
+  const int grid = nslab_blocks + total_rows;
+  if (grid <= 0) return 0;
+  hipLaunchKernelGGL(finalize_kernel, dim3(grid), dim3(256), 0, st, (const SlabJob*)slab_jobs, nsj,
+                     nslab_blocks, (const RowSumJob*)row_jobs, nrj);
+  HFM_LAUNCH_CHECK();
+}
+
 HFM_API int hfm_slab_reduce(const void* jobs, int njobs, int max_n, hipStream_t st) {
   int gx = (max_n + 31) / 32;
   if (gx > 2048) gx = 2048;
@@ -372,10 +427,10 @@ struct RowSumJob {
   long ld;
 };
 
-__global__ void __launch_bounds__(256) rowsum_kernel(const RowSumJob* __restrict__ jobs, int njobs) {
+__device__ void rowsum_block(const RowSumJob* jobs, int njobs, int b) {
   __shared__ float red[256];
-  // blockIdx.x enumerates (job, row) pairs
-  int rem = blockIdx.x, ji = 0;
+  // b enumerates (job, row) pairs
+  int rem = b, ji = 0;
   while (ji < njobs && rem >= jobs[ji].rows) { rem -= jobs[ji].rows; ++ji; }
   if (ji >= njobs) return;
   const RowSumJob j = jobs[ji];
@@ -393,6 +448,10 @@ __global__ void __launch_bounds__(256) rowsum_kernel(const RowSumJob* __restrict
     __syncthreads();
   }
   if (threadIdx.x == 0) j.dst[rem] = red[0];
+}
+
+__global__ void __launch_bounds__(256) rowsum_kernel(const RowSumJob* __restrict__ jobs, int njobs) {
+  rowsum_block(jobs, njobs, blockIdx.x);
 }
 
 HFM_API int hfm_rowsum(const void* jobs, int njobs, int total_rows, hipStream_t st) {

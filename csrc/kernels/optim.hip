@@ -139,7 +139,8 @@ struct ShadowSeg {   // a weight matrix [rows, cols] inside the flat buffer with
 template <int OPT>
 __global__ void __launch_bounds__(256) dense_opt_kernel(
     float* __restrict__ p, const float* __restrict__ g, float* __restrict__ s0, float* __restrict__ s1,
-    long n, OptHyper h, const int64_t* __restrict__ step, const ShadowSeg* __restrict__ segs, int nseg) {
+    long n, OptHyper h, int64_t* __restrict__ step, const ShadowSeg* __restrict__ segs, int nseg,
+    unsigned* __restrict__ done_ctr) {
   const float lr_t = lr_t_of<OPT>(h, step);
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
     float pi = p[i];
@@ -156,6 +157,18 @@ __global__ void __launch_bounds__(256) dense_opt_kernel(
         const int r = (int)(rel / segs[s].cols), cc = (int)(rel % segs[s].cols);
         segs[s].w16[rel] = f2bf(pi);
         segs[s].wt16[(long)cc * segs[s].rows + r] = f2bf(pi);
+      }
+    }
+  }
+  // the step counter advances once every block has read it (last block to finish does it):
+  // replaces a separate 1-thread step_inc launch at the end of every training step
+  if (done_ctr) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const unsigned prev = atomicAdd(done_ctr, 1u);
+      if (prev == gridDim.x - 1) {
+        *step += 1;
+        *done_ctr = 0u;
       }
     }
   }
@@ -270,13 +283,13 @@ HFM_API int hfm_dense_sweep(int K, int opt, long R, float* tv, float* tw, float*
 }
 
 HFM_API int hfm_dense_opt(int opt, float* p, const float* g, float* s0, float* s1, long n,
-                          const OptHyper* h, const int64_t* step, const void* segs, int nseg,
-                          hipStream_t st) {
+                          const OptHyper* h, int64_t* step, const void* segs, int nseg,
+                          unsigned* done_ctr, hipStream_t st) {
   long gg = (n + 255) / 256;
   const int grid = (int)(gg < 4096 ? gg : 4096);
 #define CALL(O)                                                                                  \
   hipLaunchKernelGGL((dense_opt_kernel<O>), dim3(grid), dim3(256), 0, st, p, g, s0, s1, n, *h, step, \
-                     (const ShadowSeg*)segs, nseg)
+                     (const ShadowSeg*)segs, nseg, done_ctr)
   HFM_OPT_DISPATCH(opt, CALL)
 #undef CALL
   HFM_LAUNCH_CHECK();

@@ -235,6 +235,11 @@ __global__ void __launch_bounds__(RS_THREADS) os_hist_kernel(const int* __restri
     if (h[p][threadIdx.x]) atomicAdd(&ghist[p * RS_RADIX + threadIdx.x], h[p][threadIdx.x]);
 }
 
+__global__ void __launch_bounds__(256) os_zero_kernel(unsigned* __restrict__ p, long n) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256L)
+    __hip_atomic_store(&p[i], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // Exclusive scan of one value per thread (256 threads) -> returns the exclusive prefix and
 // leaves the block total in *total.  Wave-level shuffles + one LDS exchange of 4 wave sums.
 __device__ __forceinline__ int block_excl_scan256(int v, int* wsum, int* total) {
@@ -320,7 +325,9 @@ __global__ void __launch_bounds__(RS_THREADS) os_pass_kernel(
   int tot;
   lbase[tid] = block_excl_scan256(mine, wsum, &tot);
   __syncthreads();
-  const int g = (int)ghist_p[tid];
+  // ghist was built with device atomics by os_hist_kernel: read it coherently (agent scope,
+  // bypassing a possibly stale L2 line left by an earlier sort's plain read on this XCD)
+  const int g = (int)__hip_atomic_load(&ghist_p[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int gex = block_excl_scan256(g, wsum + 0, &tot);
   // decoupled look-back for digit tid.  Every tile publishes its aggregate right after ranking,
   // so predecessors' words are read in batches of W independent loads (one memory round trip
@@ -407,11 +414,17 @@ HFM_API int hfm_onesweep_sort_ids(const int* keys_in, int* keys_out, int* perm_o
   const size_t status_words = (size_t)passes * tiles * RS_RADIX;
   int* pk = (int*)(((uintptr_t)(status + (size_t)OS_MAX_PASSES * tiles * RS_RADIX) + 255) & ~(uintptr_t)255);
   int* pv = pk + n;
-  // one memset node zeroes histogram, tickets, error word and this sort's status words
+  // one zeroing kernel clears histogram, tickets, error word and this sort's status words (a
+  // kernel, not a memset node: inside a HIP graph a memset node may be executed by a DMA
+  // engine, outside the L2 coherence path the look-back relies on)
   // HIPFM_OS_DEBUG_NOLB=1: skip the look-back (WRONG order; only to time its share)
   static const int debug_nolb = getenv("HIPFM_OS_DEBUG_NOLB") ? atoi(getenv("HIPFM_OS_DEBUG_NOLB")) : 0;
-  hipError_t e = hipMemsetAsync(t, 0, 8192 + status_words * 4, st);
-  if (e != hipSuccess) return (int)e;
+  {
+    const size_t words = (8192 + status_words * 4) / 4;
+    int zg = (int)((words + 1023) / 1024);
+    if (zg > 1024) zg = 1024;
+    hipLaunchKernelGGL(os_zero_kernel, dim3(zg), dim3(256), 0, st, (unsigned*)t, (long)words);
+  }
   int hg = (n + RS_THREADS - 1) / RS_THREADS;
   if (hg > OS_HIST_BLOCKS) hg = OS_HIST_BLOCKS;
   hipLaunchKernelGGL(os_hist_kernel, dim3(hg), dim3(RS_THREADS), 0, st, keys_in, n, passes, ghist);

@@ -165,6 +165,8 @@ class Estimator:
         for t in self.model.replicated_state():
             if t.dtype == torch.float32 or t.dtype == torch.int64:
                 dist.broadcast(t, src=0)
+        if self.native:
+            self.model._host_step = None      # step counter came from rank 0
         if not self.native:
             gs = torch.tensor([int(self.model.global_step)], dtype=torch.int64)
             dist.broadcast(gs, src=0)

@@ -38,6 +38,11 @@ from ..utils.rng import keep_threshold
 from .reference import glorot_std, init_params, pad32
 
 
+# A/B switches (debug / perf comparison)
+_SEPARATE_STEP_INC = os.environ.get("HIPFM_STEP_INC", "0") == "1"
+_OLD_FINALIZE = os.environ.get("HIPFM_OLD_FINALIZE", "0") == "1"
+
+
 def _align(n: int, a: int = 64) -> int:
     return (n + a - 1) // a * a
 
@@ -162,6 +167,8 @@ class NativeDeepFM:
         self.p = torch.zeros(self.P, **f32)
         self.g = torch.zeros(self.P, **f32)
         self.step = torch.zeros(1, dtype=torch.int64, device=dev)
+        self._done_ctr = torch.zeros(1, dtype=torch.int32, device=dev)   # dense_opt block counter
+        self._host_step = 0
         # BN moving statistics: non-trainable, outside the optimizer/all-reduce buffer
         # (rank-local, like the reference's per-worker batch_norm updates)
         self.bn_moving = torch.zeros(2 * sum(self.Np) if self.batch_norm else 0, **f32)
@@ -344,6 +351,12 @@ class NativeDeepFM:
         jobs.append(SlabJob(g0 + 4 * sb, pw + 4 * Lp, 1, self.nhead, Lp + 2, 1, 1, 1.0))
         jobs.append(SlabJob(g0 + 4 * sf, pw + 4 * Lp, 1, self.nhead, Lp + 2, 1, 1, 1.0))
         jobs.append(SlabJob(self.loss_sum.data_ptr(), pw + 4 * (Lp + 1), 1, self.nhead, Lp + 2, 1, 1, 1.0))
+        nb = 0
+        for j in jobs:                       # finalize_kernel block mapping
+            j.lanes = 8 if j.nslab >= 64 else 2
+            j.chunk0 = nb
+            nb += (j.n + 256 // j.lanes - 1) // (256 // j.lanes)
+        self._slab_blocks = nb
         self._slab_jobs = KN.struct_array_to_device(jobs, self.device)
         self._nslab_jobs = len(jobs)
         self._slab_maxn = maxn
@@ -419,8 +432,7 @@ class NativeDeepFM:
             idx, tv = self._fm_forward(B, train=True)
             KN.tower(self._tower_args(B, train=True))
             KN.wgrad_group(self._wg_jobs, self._nwg_jobs, self._wg_tasks)
-            KN.slab_reduce(self._slab_jobs, self._nslab_jobs, self._slab_maxn)
-            KN.rowsum(self._row_jobs, self._nrow_jobs, self._row_total)
+            self._finalize_grads()
             return idx, tv
         idx, tv = self._forward(B, train=True)
         self._head(B, train=True)
@@ -650,8 +662,15 @@ class NativeDeepFM:
                 ep.scale = 1.0
                 KN.gemm_nt(KN.EPI_DGRAD, _pick_tile(M, self.K0p), self.dZ[0], self.Np[0],
                            self.WT16[0], self.Np[0], M, self.K0p, self.Np[0], 1, ep)
-        KN.slab_reduce(self._slab_jobs, self._nslab_jobs, self._slab_maxn)
-        KN.rowsum(self._row_jobs, self._nrow_jobs, self._row_total)
+        self._finalize_grads()
+
+    def _finalize_grads(self):
+        if _OLD_FINALIZE:
+            KN.slab_reduce(self._slab_jobs, self._nslab_jobs, self._slab_maxn)
+            KN.rowsum(self._row_jobs, self._nrow_jobs, self._row_total)
+            return
+        KN.finalize(self._slab_jobs, self._nslab_jobs, self._slab_blocks, self._row_jobs,
+                    self._nrow_jobs, self._row_total)
 
     def seg_args(self, n: int, compact: bool, vsrc=None, vsrc_compact: bool = False) -> SegApplyArgs:
         A = SegApplyArgs()
@@ -729,9 +748,13 @@ class NativeDeepFM:
             self._sparse_update(*out)
         if work is not None:
             self.comm.wait(work)
-        KN.dense_opt(self.opt_id, self.p, self.g, self.sd[0], self.sd[1], self.P, self.h_dense,
-                     self.step, self._shadow_dev, self._nshadow)
-        KN.step_inc(self.step)
+        if _SEPARATE_STEP_INC:
+            KN.dense_opt(self.opt_id, self.p, self.g, self.sd[0], self.sd[1], self.P, self.h_dense,
+                         self.step, self._shadow_dev, self._nshadow)
+            KN.step_inc(self.step)
+        else:
+            KN.dense_opt(self.opt_id, self.p, self.g, self.sd[0], self.sd[1], self.P, self.h_dense,
+                         self.step, self._shadow_dev, self._nshadow, done_ctr=self._done_ctr)
 
     def compute_grads(self, ids, vals, labels):
         """Forward + backward WITHOUT any update (tests / debugging): returns the flat dense
@@ -766,6 +789,8 @@ class NativeDeepFM:
             self._replay_graph(key, B)
         else:
             self.train_step_enqueue(B)
+        if self._host_step is not None:
+            self._host_step += 1
         return B
 
     def _replay_graph(self, key, B: int):
@@ -841,7 +866,11 @@ class NativeDeepFM:
 
     # ------------------------------------------------------------------ state export
     def global_step(self) -> int:
-        return int(self.step.item())
+        """Host mirror of the device step counter: read once (sync), then advanced by
+        train_step, so the training loop never blocks on the GPU just to know the step."""
+        if self._host_step is None:
+            self._host_step = int(self.step.item())
+        return self._host_step
 
     def sparse_tables_tf(self):
         """fm_w / fm_v of THIS rank (full tables when replicated; local rows when sharded)."""
@@ -884,6 +913,7 @@ class NativeDeepFM:
                                for s in self.dense_segs.values()]}
 
     def load_state_dict_local(self, d: Dict[str, torch.Tensor]):
+        self._host_step = None
         cur = self.state_dict_local()
         with torch.no_grad():
             for k, v in d.items():
@@ -950,4 +980,5 @@ class NativeDeepFM:
                         dst.copy_(torch.as_tensor(tv[key]).to(dst))
             if "global_step" in tv:
                 self.step.fill_(int(torch.as_tensor(tv["global_step"])))
+                self._host_step = None
         self._graphs = {}

@@ -54,7 +54,8 @@ class BnArgs(C.Structure):
 
 class SlabJob(C.Structure):
     _fields_ = [("dst", c_void_p), ("src", c_void_p), ("n", c_long), ("nslab", c_int),
-                ("stride", c_long), ("src_ld", c_long), ("cols", c_int), ("scale", c_float)]
+                ("stride", c_long), ("src_ld", c_long), ("cols", c_int), ("scale", c_float),
+                ("lanes", c_int), ("chunk0", c_int)]
 
 
 class RowSumJob(C.Structure):
@@ -114,7 +115,9 @@ _SIGS = {
                               + [C.POINTER(OptHyper), c_void_p, c_void_p],
     "hfm_scatter_rows": [c_int] + [c_void_p] * 3 + [c_int, c_int, c_void_p, c_void_p, c_void_p],
     "hfm_dense_sweep": [c_int, c_int, c_long] + [c_void_p] * 8 + [C.POINTER(OptHyper), c_void_p, c_void_p],
-    "hfm_dense_opt": [c_int] + [c_void_p] * 4 + [c_long, C.POINTER(OptHyper), c_void_p, c_void_p, c_int, c_void_p],
+    "hfm_dense_opt": [c_int] + [c_void_p] * 4 + [c_long, C.POINTER(OptHyper), c_void_p, c_void_p, c_int,
+                                                 c_void_p, c_void_p],
+    "hfm_finalize": [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p],
     "hfm_shadow_refresh": [c_void_p, c_long, c_void_p, c_int, c_void_p],
     "hfm_step_inc": [c_void_p, c_void_p],
     "hfm_shadow_seg_bytes": [],

@@ -6,6 +6,7 @@ them can be captured into a HIP graph (``torch.cuda.CUDAGraph``).
 from __future__ import annotations
 
 import ctypes as C
+import os
 from typing import List, Optional, Sequence
 
 import torch
@@ -85,7 +86,8 @@ def onesweep_sort_ids(keys_in, keys_out, perm_out, n, end_bit, temp):
                                     ptr(temp), temp.numel(), stream_handle()), "onesweep_sort_ids")
 
 
-SORT_IMPL = "lsd"   # A/B measured in tools/bench_sort.py; the faster one is the default
+SORT_IMPL = os.environ.get("HIPFM_SORT_IMPL", "onesweep")
+# A/B in tools/bench_sort.py (graph-timed): onesweep 56 us vs LSD 101 us at n = 640K, 30 bits
 
 
 def sort_ids(keys_in, keys_out, vals_tmp, perm_out, n, end_bit, temp):
@@ -166,9 +168,18 @@ def dense_sweep(K, opt, R, tv, tw, Gv, Gw, slots, h: OptHyper, step):
           "dense_sweep")
 
 
-def dense_opt(opt, p, g, s0, s1, n, h: OptHyper, step, segs_dev, nseg):
+def dense_opt(opt, p, g, s0, s1, n, h: OptHyper, step, segs_dev, nseg, done_ctr=None):
+    """Fused dense optimizer + bf16 shadow refresh; with ``done_ctr`` (an int32 device word,
+    zero-initialised) the last block also advances ``step`` (no separate step_inc launch)."""
     check(L().hfm_dense_opt(opt, ptr(p), ptr(g), ptr(s0), ptr(s1), n, C.byref(h), ptr(step),
-                            ptr(segs_dev), nseg, stream_handle()), "dense_opt")
+                            ptr(segs_dev), nseg, ptr(done_ctr) if done_ctr is not None else None,
+                            stream_handle()), "dense_opt")
+
+
+def finalize(slab_jobs_dev, nsj, nslab_blocks, row_jobs_dev, nrj, total_rows):
+    """Split-K / head-partial reductions and bias row sums in one launch (mlp.hip)."""
+    check(L().hfm_finalize(ptr(slab_jobs_dev), nsj, nslab_blocks, ptr(row_jobs_dev), nrj, total_rows,
+                           stream_handle()), "finalize")
 
 
 def shadow_refresh(p, n, segs_dev, nseg):

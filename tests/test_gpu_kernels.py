@@ -302,3 +302,35 @@ def test_fused_tower_matches_per_layer_kernels(layers, K):
     pa = a.predict(*args[:2])
     pb = b.predict(*args[:2])
     assert torch.allclose(pa, pb, atol=2e-6, rtol=0)
+
+
+@pytest.mark.parametrize("impl", ["lsd", "onesweep"])
+def test_sort_graph_replay_with_new_inputs(impl):
+    """A captured sort replayed on NEW keys written into the same buffers (how the train step's
+    per-batch graphs use it): results must match torch.sort every time."""
+    dev = torch.device(DEV)
+    for n, bits in ((19968, 16), (39 * 4096, 30)):
+        keys = torch.zeros(n, dtype=torch.int32, device=dev)
+        sk = torch.empty_like(keys)
+        perm = torch.empty_like(keys)
+        temp = torch.empty(KN.radix_temp_bytes(n) + 256, dtype=torch.uint8, device=dev)
+        fn = KN.onesweep_sort_ids if impl == "onesweep" else KN.lsd_sort_ids
+        keys.copy_(torch.randint(0, 1 << bits, (n,), dtype=torch.int32, device=dev))
+        fn(keys, sk, perm, n, bits, temp)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            fn(keys, sk, perm, n, bits, temp)
+        gen = torch.Generator(device=dev).manual_seed(n)
+        for it in range(6):
+            if it % 2:   # heavily duplicated (Zipf-like) keys
+                k = (torch.rand(n, generator=gen, device=dev) ** 6 * (1 << bits)).to(torch.int32)
+            else:
+                k = torch.randint(0, 1 << bits, (n,), generator=gen, dtype=torch.int32, device=dev)
+            keys.copy_(k)
+            g.replay()
+            torch.cuda.synchronize()
+            if impl == "onesweep":
+                assert KN.sort_error(temp) == 0
+            rk, rp = torch.sort(keys.long(), stable=True)
+            assert torch.equal(sk.long(), rk) and torch.equal(perm.long(), rp), (n, bits, it)
