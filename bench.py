@@ -77,7 +77,7 @@ def main():
     model = NativeDeepFM(synth.feature_size, F, args.embedding_size, layers, keep, l2_reg=1e-4,
                          learning_rate=5e-4, optimizer=args.optimizer,
                          sparse_update=args.sparse_update, seed=1234, batch_size=B, device=dev,
-                         comm=comm)
+                         comm=comm, field_ranges=synth.field_ranges())
     pool = [synth.batch(B, step=rank * 100000 + i, device=dev, id_dtype=torch.int32)
             for i in range(args.pool)]
     use_graph = not args.no_graph

@@ -85,6 +85,11 @@ class CriteoSynth:
     def feature_size(self) -> int:
         return self.V
 
+    def field_ranges(self) -> List[Tuple[int, int]]:
+        """Per-field id ranges [lo, hi): dense field j -> {j}, categorical c -> its vocabulary."""
+        dense = [(j, j + 1) for j in range(self.n_dense)]
+        return dense + [(o, o + v) for o, v in zip(self.offsets, self.cat_vocab)]
+
     def _teacher_w(self, ids: torch.Tensor) -> torch.Tensor:
         h = (ids.long() * 0x9E3779B1 + self.seed) & M32
         h = h ^ (h >> 16)

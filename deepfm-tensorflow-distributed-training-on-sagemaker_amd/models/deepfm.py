@@ -28,7 +28,7 @@ import math
 import os
 from collections import OrderedDict
 from dataclasses import dataclass
-from typing import Dict, List, Optional
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
 
@@ -41,6 +41,32 @@ from .reference import glorot_std, init_params, pad32
 # A/B switches (debug / perf comparison)
 _SEPARATE_STEP_INC = os.environ.get("HIPFM_STEP_INC", "0") == "1"
 _OLD_FINALIZE = os.environ.get("HIPFM_OLD_FINALIZE", "0") == "1"
+_SORT_MODE = os.environ.get("HIPFM_SORT", "auto")                # auto | global
+_SORT_SIDE_STREAM = os.environ.get("HIPFM_SORT_SIDE_STREAM", "1") == "1"
+
+
+def check_field_ranges(ranges, F: int, V: int) -> List[Tuple[int, int]]:
+    """Validate per-field id ranges [lo, hi): one per field, non-empty, disjoint and increasing
+    in field order, inside [0, V).  Returns them as a list of int pairs."""
+    out = [(int(lo), int(hi)) for lo, hi in ranges]
+    if len(out) != F:
+        raise ValueError(f"field_ranges: expected {F} ranges, got {len(out)}")
+    prev = 0
+    for f, (lo, hi) in enumerate(out):
+        if lo < prev or hi <= lo or hi > V:
+            raise ValueError(f"field_ranges: field {f} range [{lo}, {hi}) is not disjoint/increasing "
+                             f"inside [0, {V})")
+        prev = hi
+    return out
+
+
+def field_ranges_from_sizes(sizes: Sequence[int]) -> List[Tuple[int, int]]:
+    """Consecutive per-field vocabularies starting at id 0 (the usual CTR id layout)."""
+    out, lo = [], 0
+    for n in sizes:
+        out.append((lo, lo + int(n)))
+        lo += int(n)
+    return out
 
 
 def _align(n: int, a: int = 64) -> int:
@@ -104,7 +130,8 @@ class NativeDeepFM:
                  sparse_update: str = "tf1_dense", seed: int = 1234, batch_size: int = 1024,
                  device="cuda", comm=None, init: bool = True, batch_norm: bool = False,
                  batch_norm_decay: float = 0.9, adam_epsilon: float = 1e-8,
-                 adagrad_init: float = 1e-8, fused: Optional[bool] = None):
+                 adagrad_init: float = 1e-8, fused: Optional[bool] = None,
+                 field_ranges: Optional[Sequence[Tuple[int, int]]] = None):
         self.batch_norm = bool(batch_norm)
         self.bn_decay = float(batch_norm_decay)
         self.bn_eps = 1e-3          # tf.contrib.layers.batch_norm default epsilon (PS:289)
@@ -132,6 +159,11 @@ class NativeDeepFM:
         self.R = (self.V + self.world - 1) // self.world if self.sharded else self.V
         self.row_div = self.world if self.sharded else 1
         self.end_bit = max(1, int(math.ceil(math.log2(max(2, self.V)))))
+        # per-field id ranges [lo, hi) (disjoint, increasing): enable the one-launch per-field
+        # LDS sort of the slot ids (csrc/kernels/field_sort.hip) instead of the global sort
+        self.field_ranges = None
+        if field_ranges is not None:
+            self.field_ranges = check_field_ranges(field_ranges, self.F, self.V)
 
         # ---- dense parameter layout (flat fp32 buffer = one all-reduce bucket) ----
         F, K = self.F, self.K
@@ -199,6 +231,7 @@ class NativeDeepFM:
         self.h_sparse = KN.hyper(self.lr, self.l2, eps=adam_epsilon)
         self.h_dense = KN.hyper(self.lr, 0.0, eps=adam_epsilon)
         self._bufs_M = 0
+        self._side = None
         self.batch_size = int(batch_size)
         # fused deep tower (csrc/kernels/tower.hip): whole forward + head + dgrad chain in one
         # launch per 32-sample block; batch norm (needs batch-wide statistics between the
@@ -320,6 +353,12 @@ class NativeDeepFM:
         self.seg_flags = torch.zeros(n, **i32)
         self.sid_incl = torch.zeros(n, **i32)
         self.seg_start = torch.zeros(n + 1, **i32)
+        self.fs_err = torch.zeros(1, **i32)
+        self._fs_ranges = None
+        if self.field_ranges is not None:
+            fr = [(lo, hi, int(math.ceil(math.log2(hi - lo))) if hi - lo > 1 else 0)
+                  for lo, hi in self.field_ranges]
+            self._fs_ranges = torch.tensor(fr, dtype=torch.int32).reshape(-1).to(dev)
         tb = max(KN.radix_temp_bytes(n), KN.rbk_temp_bytes(K, n), KN.scan_temp_bytes(n))
         self.temp = torch.zeros(tb + 256, dtype=torch.uint8, device=dev)
         self._build_finalize_jobs()
@@ -695,13 +734,33 @@ class NativeDeepFM:
         A.step = self.step.data_ptr()
         return A
 
-    def _sparse_backward(self, B: int, idx, tv):
+    def uses_field_sort(self, B: int) -> bool:
+        return (self._fs_ranges is not None and _SORT_MODE != "global" and
+                B <= KN.field_sort_max_rows())
+
+    def _sort_slots(self, B: int):
+        """Stable sort of the B*F slot ids -> (sorted_keys, perm): one per-field LDS launch when
+        the field id ranges are known, else the global radix sort."""
+        n = B * self.F
+        if self.uses_field_sort(B):
+            KN.field_sort(self.idx, B, self.F, self._fs_ranges, self.sorted_keys, self.perm, self.fs_err)
+        else:
+            KN.sort_ids(self.idx, self.sorted_keys, None, self.perm, n, self.end_bit, self.temp)
+
+    def check_errors(self):
+        """Raise on device-side input errors flagged by earlier steps (host sync)."""
+        if self._fs_ranges is not None and int(self.fs_err.item()) != 0:
+            raise RuntimeError("an id lies outside its field's declared range (field_ranges): "
+                               "the per-field sort is invalid for this data")
+
+    def _sparse_backward(self, B: int, idx, tv, presorted: bool = False):
         """Embedding backward.  Single rank: the row update is fused into the reduction
         (returns None).  Multi-rank: returns compact unique-row gradients for the exchange."""
         n = B * self.F
         if self.sharded:
             return self.comm.sharded_backward(self, B, idx, tv)
-        KN.sort_ids(self.idx, self.sorted_keys, None, self.perm, n, self.end_bit, self.temp)
+        if not presorted:
+            self._sort_slots(B)
         if not self.exchange:
             self._segment_reduce(n, compact=False)
             A = self.seg_args(n, compact=False)
@@ -738,12 +797,25 @@ class NativeDeepFM:
 
     # ------------------------------------------------------------------ public step API
     def train_step_enqueue(self, B: int):
-        """Enqueue one full training step on the current stream (no host sync)."""
+        """Enqueue one full training step on the current stream (no host sync).  The slot-id
+        sort depends only on the batch, so it runs on a side stream concurrently with the
+        forward / tower backward (a parallel branch of the captured graph)."""
+        presorted = False
+        if not self.sharded and _SORT_SIDE_STREAM:
+            main = torch.cuda.current_stream(self.device)
+            if self._side is None:
+                self._side = torch.cuda.Stream(self.device)
+            self._side.wait_stream(main)
+            with torch.cuda.stream(self._side):
+                self._sort_slots(B)
+            presorted = True
         idx, tv = self._dense_fwd_bwd(B)
+        if presorted:
+            main.wait_stream(self._side)
         work = None
         if self.exchange:
             work = self.comm.allreduce_dense_async(self.g)
-        out = self._sparse_backward(B, idx, tv)
+        out = self._sparse_backward(B, idx, tv, presorted=presorted)
         if out is not None:
             self._sparse_update(*out)
         if work is not None:
@@ -764,7 +836,7 @@ class NativeDeepFM:
         B = self.stage_batch(ids, vals, labels)
         self._dense_fwd_bwd(B)
         n = B * self.F
-        KN.sort_ids(self.idx, self.sorted_keys, None, self.perm, n, self.end_bit, self.temp)
+        self._sort_slots(B)
         self._segment_reduce(n, compact=True)
         KN.seg_apply(self.K, KN.SEG_WRITE_UG, 0, self.seg_args(n, compact=True), n)
         U = int(self.num_u.item())
@@ -833,6 +905,7 @@ class NativeDeepFM:
     def loss_value(self, B: int, include_l2: bool = False) -> float:
         """Mean data loss of the last step (+ l2 terms over the whole tables if asked)."""
         v = float(self.loss_sum.item()) / B
+        self.check_errors()
         if include_l2:
             v += self.l2_value()
         return v

@@ -99,6 +99,19 @@ def sort_ids(keys_in, keys_out, vals_tmp, perm_out, n, end_bit, temp):
         lsd_sort_ids(keys_in, keys_out, perm_out, n, end_bit, temp)
 
 
+def field_sort_max_rows() -> int:
+    """Largest batch the one-workgroup-per-field LDS sort handles (csrc/kernels/field_sort.hip)."""
+    return int(L().hfm_field_sort_max_rows())
+
+
+def field_sort(ids, B, F, franges_dev, keys_out, perm_out, err):
+    """Per-field LDS sort of the B*F slot ids (field ranges disjoint and increasing): output is
+    identical to ``sort_ids`` on the same slots.  ``franges_dev``: int32 [F, 3] {lo, hi, bits};
+    ``err``: int32 [1], set non-zero when an id lies outside its field's range."""
+    check(L().hfm_field_sort(ptr(ids), B, F, ptr(franges_dev), ptr(keys_out), ptr(perm_out), ptr(err),
+                             stream_handle()), "field_sort")
+
+
 def sort_error(temp) -> int:
     """1 if the last onesweep sort in ``temp`` timed out in its look-back (device read: syncs)."""
     off = L().hfm_onesweep_error_offset()

@@ -334,3 +334,67 @@ def test_sort_graph_replay_with_new_inputs(impl):
                 assert KN.sort_error(temp) == 0
             rk, rp = torch.sort(keys.long(), stable=True)
             assert torch.equal(sk.long(), rk) and torch.equal(perm.long(), rp), (n, bits, it)
+
+
+def _franges_dev(ranges):
+    import math
+    fr = [(lo, hi, int(math.ceil(math.log2(hi - lo))) if hi - lo > 1 else 0) for lo, hi in ranges]
+    return torch.tensor(fr, dtype=torch.int32).reshape(-1).to(DEV)
+
+
+@pytest.mark.parametrize("preset,B", [("criteo_1tb", 16384), ("criteo_kaggle", 1000), ("reference", 4096)])
+def test_field_sort_equals_global_sort(preset, B):
+    """The per-field LDS sort (field_sort.hip) returns exactly the stable global sort of the
+    B*F slot ids, in eager mode and as a graph replayed on new batches."""
+    synth = make_synth(preset)
+    F = synth.F
+    fr = _franges_dev(synth.field_ranges())
+    ids = torch.zeros(B * F, dtype=torch.int32, device=DEV)
+    sk = torch.full_like(ids, -7)
+    perm = torch.full_like(ids, -7)
+    err = torch.zeros(1, dtype=torch.int32, device=DEV)
+    ids.copy_(synth.batch(B, 0, device=DEV, id_dtype=torch.int32)[0].reshape(-1))
+    KN.field_sort(ids, B, F, fr, sk, perm, err)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        KN.field_sort(ids, B, F, fr, sk, perm, err)
+    for it in range(3):
+        if it:
+            ids.copy_(synth.batch(B, it, device=DEV, id_dtype=torch.int32)[0].reshape(-1))
+            g.replay()
+        torch.cuda.synchronize()
+        rk, rp = torch.sort(ids.long(), stable=True)
+        assert int(err.item()) == 0
+        assert torch.equal(sk.long(), rk) and torch.equal(perm.long(), rp), (preset, B, it)
+
+
+def test_field_sort_flags_out_of_range_ids():
+    synth = make_synth("criteo_kaggle")
+    F, B = synth.F, 512
+    fr = _franges_dev(synth.field_ranges())
+    ids = synth.batch(B, 0, device=DEV, id_dtype=torch.int32)[0].contiguous()
+    ids[7, 20] = synth.field_ranges()[21][0]          # an id of field 21 in field 20
+    sk, perm = torch.empty(B * F, dtype=torch.int32, device=DEV), torch.empty(B * F, dtype=torch.int32, device=DEV)
+    err = torch.zeros(1, dtype=torch.int32, device=DEV)
+    KN.field_sort(ids.reshape(-1), B, F, fr, sk, perm, err)
+    assert int(err.item()) != 0
+
+
+def test_train_step_field_sort_bitwise_equals_global_sort():
+    """Whole graph-replayed train steps (field sort on a side stream) give bitwise the same
+    parameters as the global-sort path."""
+    synth = make_synth("criteo_kaggle")
+    F, K, layers, keep, B = synth.F, 8, [64, 32], [0.5, 0.5], 1024
+    kw = dict(sparse_update="lazy", batch_size=B, device=DEV, seed=3)
+    a = NativeDeepFM(synth.feature_size, F, K, layers, keep, field_ranges=synth.field_ranges(), **kw)
+    b = NativeDeepFM(synth.feature_size, F, K, layers, keep, **kw)
+    assert a.uses_field_sort(B) and not b.uses_field_sort(B)
+    batches = [synth.batch(B, i, device=DEV, id_dtype=torch.int32) for i in range(3)]
+    for step in range(5):
+        ids, vals, lab = batches[step % 3]
+        a.train_step(ids, vals, lab, use_graph=True)
+        b.train_step(ids, vals, lab, use_graph=False)
+    torch.cuda.synchronize()
+    assert torch.equal(a.tv, b.tv) and torch.equal(a.tw, b.tw) and torch.equal(a.p, b.p)
+    a.check_errors()
