@@ -18,7 +18,8 @@ template <int K>
 __global__ void __launch_bounds__(256) fm_fwd_kernel(
     const int* __restrict__ idx, const float* __restrict__ vals, const float* __restrict__ tv,
     const float* __restrict__ tw, const float* __restrict__ bias, int B, int F, int KP,
-    float* __restrict__ y_fm, float* __restrict__ S, bf16* __restrict__ E, bf16* __restrict__ Et) {
+    float* __restrict__ y_fm, float* __restrict__ S, bf16* __restrict__ E, bf16* __restrict__ Et,
+    long ldv, long ldw) {
   constexpr int LPS = K / 4;       // lanes per sample
   constexpr int SB = 256 / LPS;    // samples per workgroup
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -47,11 +48,11 @@ __global__ void __launch_bounds__(256) fm_fwd_kernel(
   for (int f = 0; f < F; ++f) {
     const int id = ib[f];
     const float x = xb[f];
-    const f32x4 v = *reinterpret_cast<const f32x4*>(tv + (size_t)id * K + sub * 4);
+    const f32x4 v = *reinterpret_cast<const f32x4*>(tv + (size_t)id * ldv + sub * 4);
     const f32x4 e = v * x;
     s += e;
     q += e * e;
-    if ((f % LPS) == sub) yw += tw[id] * x;
+    if ((f % LPS) == sub) yw += tw[(size_t)id * ldw] * x;
     bf16x4 eh = {f2bf(e[0]), f2bf(e[1]), f2bf(e[2]), f2bf(e[3])};
     *reinterpret_cast<bf16x4*>(eb + f * K) = eh;
     if (Et) {
@@ -82,7 +83,8 @@ template <int K>
 __global__ void __launch_bounds__(256) fm_fwd2_kernel(
     const int* __restrict__ idx, const float* __restrict__ vals, const float* __restrict__ tv,
     const float* __restrict__ tw, const float* __restrict__ bias, int B, int F, int KP,
-    float* __restrict__ y_fm, float* __restrict__ S, bf16* __restrict__ E, bf16* __restrict__ Et) {
+    float* __restrict__ y_fm, float* __restrict__ S, bf16* __restrict__ E, bf16* __restrict__ Et,
+    long ldv, long ldw) {
   constexpr int SB = 256 / K;
   constexpr int V4 = K / 4;
   extern __shared__ __attribute__((aligned(16))) float fsm[];
@@ -97,11 +99,11 @@ __global__ void __launch_bounds__(256) fm_fwd2_kernel(
   for (int p = threadIdx.x; p < npair; p += 256) {
     const int id = idx[base + p];
     const float x = vals[base + p];
-    const f32x4* row = reinterpret_cast<const f32x4*>(tv + (size_t)id * K);
+    const f32x4* row = reinterpret_cast<const f32x4*>(tv + (size_t)id * ldv);
     f32x4 v[V4];
 #pragma unroll
     for (int j = 0; j < V4; ++j) v[j] = row[j];
-    const float w = tw[id];
+    const float w = tw[(size_t)id * ldw];
     const int sl = p / F, f = p - sl * F;
     wx[sl * F + f] = w * x;
     float* dst = et + sl * RS + f * K;
@@ -187,13 +189,13 @@ __global__ void __launch_bounds__(256) fm_bwd_sorted_kernel(
 template <int K>
 static int launch_fm_fwd(const int* idx, const float* vals, const float* tv, const float* tw,
                          const float* bias, int B, int F, int KP, float* y_fm, float* S, bf16* E,
-                         bf16* Et, hipStream_t st) {
+                         bf16* Et, long ldv, long ldw, hipStream_t st) {
   constexpr int SB = 256 / K;
   const size_t lds2 = ((size_t)SB * (F * K + 1) + (size_t)SB * F) * 4;
   if (lds2 <= 120 * 1024) {
     const int grid = (B + SB - 1) / SB;
     hipLaunchKernelGGL(fm_fwd2_kernel<K>, dim3(grid), dim3(256), lds2, st, idx, vals, tv, tw, bias,
-                       B, F, KP, y_fm, S, E, Et);
+                       B, F, KP, y_fm, S, E, Et, ldv, ldw);
     HFM_LAUNCH_CHECK();
   }
   // very wide inputs (F*K > ~30K): lane-group-per-sample variant, small LDS footprint
@@ -202,7 +204,7 @@ static int launch_fm_fwd(const int* idx, const float* vals, const float* tv, con
   const int grid = (B + SB1 - 1) / SB1;
   const size_t lds = (size_t)SB1 * F * 8;
   hipLaunchKernelGGL(fm_fwd_kernel<K>, dim3(grid), dim3(256), lds, st, idx, vals, tv, tw, bias, B,
-                     F, KP, y_fm, S, E, Et);
+                     F, KP, y_fm, S, E, Et, ldv, ldw);
   HFM_LAUNCH_CHECK();
 }
 
@@ -230,8 +232,10 @@ static int launch_fm_bwd(const int* perm, const int* idx, const float* vals, con
 
 HFM_API int hfm_fm_fwd(const int* idx, const float* vals, const float* tv, const float* tw,
                        const float* bias, int B, int F, int K, int KP, float* y_fm, float* S,
-                       void* E, void* Et, hipStream_t st) {
-#define CALL(KK) launch_fm_fwd<KK>(idx, vals, tv, tw, bias, B, F, KP, y_fm, S, (bf16*)E, (bf16*)Et, st)
+                       void* E, void* Et, long ldv, long ldw, hipStream_t st) {
+  // ldv / ldw: floats between consecutive rows of the v table and entries of the w table
+  // (K and 1 for plain tables; the record stride for the interleaved row-record layout)
+#define CALL(KK) launch_fm_fwd<KK>(idx, vals, tv, tw, bias, B, F, KP, y_fm, S, (bf16*)E, (bf16*)Et, ldv, ldw, st)
   HFM_K_DISPATCH(K, CALL)
 #undef CALL
 }

@@ -33,14 +33,15 @@ __global__ void __launch_bounds__(256) sparse_rows_kernel(
     const int* __restrict__ ukeys, const GradRowO<K>* __restrict__ UG, const int* __restrict__ num,
     int row_div, float* __restrict__ tv, float* __restrict__ tw, float* __restrict__ s0v,
     float* __restrict__ s1v, float* __restrict__ s0w, float* __restrict__ s1w, OptHyper h,
-    const int64_t* __restrict__ step) {
+    const int64_t* __restrict__ step, long ldv, long ldw) {
   constexpr int LPS = K / 4;
   const int gt = blockIdx.x * blockDim.x + threadIdx.x;
   const int u = gt / LPS, sub = gt % LPS;
   if (u >= *num) return;
   const float lr_t = lr_t_of<OPT>(h, step);
   const size_t row = (size_t)(ukeys[u] / row_div);
-  const size_t o = row * K + sub * 4;
+  const size_t o = row * ldv + sub * 4;
+  const size_t ow = row * ldw;
   f32x4 p = *reinterpret_cast<f32x4*>(tv + o);
   f32x4 g = *reinterpret_cast<const f32x4*>(&UG[u].v[sub * 4]);
   f32x4 a = {0, 0, 0, 0}, c = {0, 0, 0, 0};
@@ -57,14 +58,14 @@ __global__ void __launch_bounds__(256) sparse_rows_kernel(
   if (OPT != OPT_GD) *reinterpret_cast<f32x4*>(s0v + o) = a;
   if (OPT == OPT_ADAM || OPT == OPT_FTRL) *reinterpret_cast<f32x4*>(s1v + o) = c;
   if (sub == 0) {
-    float pw = tw[row];
+    float pw = tw[ow];
     float gw = UG[u].w + h.l2 * pw;
-    float aw = (OPT != OPT_GD) ? s0w[row] : 0.f;
-    float cw = (OPT == OPT_ADAM || OPT == OPT_FTRL) ? s1w[row] : 0.f;
+    float aw = (OPT != OPT_GD) ? s0w[ow] : 0.f;
+    float cw = (OPT == OPT_ADAM || OPT == OPT_FTRL) ? s1w[ow] : 0.f;
     opt_update<OPT>(pw, gw, aw, cw, h, lr_t);
-    tw[row] = pw;
-    if (OPT != OPT_GD) s0w[row] = aw;
-    if (OPT == OPT_ADAM || OPT == OPT_FTRL) s1w[row] = cw;
+    tw[ow] = pw;
+    if (OPT != OPT_GD) s0w[ow] = aw;
+    if (OPT == OPT_ADAM || OPT == OPT_FTRL) s1w[ow] = cw;
   }
 }
 
@@ -87,7 +88,8 @@ template <int K, int OPT>
 __global__ void __launch_bounds__(256) dense_sweep_kernel(
     long R, float* __restrict__ tv, float* __restrict__ tw, float* __restrict__ Gv,
     float* __restrict__ Gw, float* __restrict__ s0v, float* __restrict__ s1v,
-    float* __restrict__ s0w, float* __restrict__ s1w, OptHyper h, const int64_t* __restrict__ step) {
+    float* __restrict__ s0w, float* __restrict__ s1w, OptHyper h, const int64_t* __restrict__ step,
+    long ldv, long ldw) {
   constexpr int LPS = K / 4;
   const float lr_t = lr_t_of<OPT>(h, step);
   const long total = R * LPS;
@@ -95,9 +97,11 @@ __global__ void __launch_bounds__(256) dense_sweep_kernel(
        gt += (long)gridDim.x * blockDim.x) {
     const long row = gt / LPS;
     const int sub = (int)(gt % LPS);
-    const size_t o = (size_t)row * K + sub * 4;
+    const size_t o = (size_t)row * ldv + sub * 4;     // table / slot rows (record stride)
+    const size_t og = (size_t)row * K + sub * 4;      // gradient buffer rows (dense [R, K])
+    const size_t ow = (size_t)row * ldw;
     f32x4 p = *reinterpret_cast<f32x4*>(tv + o);
-    f32x4 g = *reinterpret_cast<f32x4*>(Gv + o);
+    f32x4 g = *reinterpret_cast<f32x4*>(Gv + og);
     f32x4 a = {0, 0, 0, 0}, c = {0, 0, 0, 0};
     if (OPT != OPT_GD) a = *reinterpret_cast<f32x4*>(s0v + o);
     if (OPT == OPT_ADAM || OPT == OPT_FTRL) c = *reinterpret_cast<f32x4*>(s1v + o);
@@ -112,17 +116,17 @@ __global__ void __launch_bounds__(256) dense_sweep_kernel(
     *reinterpret_cast<f32x4*>(tv + o) = p;
     if (OPT != OPT_GD) *reinterpret_cast<f32x4*>(s0v + o) = a;
     if (OPT == OPT_ADAM || OPT == OPT_FTRL) *reinterpret_cast<f32x4*>(s1v + o) = c;
-    if (touched) *reinterpret_cast<f32x4*>(Gv + o) = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (touched) *reinterpret_cast<f32x4*>(Gv + og) = f32x4{0.f, 0.f, 0.f, 0.f};
     if (sub == 0) {
-      float pw = tw[row];
+      float pw = tw[ow];
       float g0 = Gw[row];
       float gw = g0 + h.l2 * pw;
-      float aw = (OPT != OPT_GD) ? s0w[row] : 0.f;
-      float cw = (OPT == OPT_ADAM || OPT == OPT_FTRL) ? s1w[row] : 0.f;
+      float aw = (OPT != OPT_GD) ? s0w[ow] : 0.f;
+      float cw = (OPT == OPT_ADAM || OPT == OPT_FTRL) ? s1w[ow] : 0.f;
       opt_update<OPT>(pw, gw, aw, cw, h, lr_t);
-      tw[row] = pw;
-      if (OPT != OPT_GD) s0w[row] = aw;
-      if (OPT == OPT_ADAM || OPT == OPT_FTRL) s1w[row] = cw;
+      tw[ow] = pw;
+      if (OPT != OPT_GD) s0w[ow] = aw;
+      if (OPT == OPT_ADAM || OPT == OPT_FTRL) s1w[ow] = cw;
       if (g0 != 0.f) Gw[row] = 0.f;
     }
   }
@@ -206,14 +210,15 @@ __global__ void step_inc_kernel(int64_t* step) { *step += 1; }
 template <int K>
 static int sparse_rows_k(int opt, const int* ukeys, const void* UG, const int* num, int max_n,
                          int row_div, float* tv, float* tw, float* s0v, float* s1v, float* s0w,
-                         float* s1w, OptHyper h, const int64_t* step, hipStream_t st) {
+                         float* s1w, OptHyper h, const int64_t* step, long ldv, long ldw,
+                         hipStream_t st) {
   constexpr int LPS = K / 4;
   const long th = (long)max_n * LPS;
   const int grid = (int)((th + 255) / 256);
   if (grid == 0) return 0;
 #define CALL(O)                                                                                   \
   hipLaunchKernelGGL((sparse_rows_kernel<K, O>), dim3(grid), dim3(256), 0, st, ukeys,             \
-                     (const GradRowO<K>*)UG, num, row_div, tv, tw, s0v, s1v, s0w, s1w, h, step)
+                     (const GradRowO<K>*)UG, num, row_div, tv, tw, s0v, s1v, s0w, s1w, h, step, ldv, ldw)
   HFM_OPT_DISPATCH(opt, CALL)
 #undef CALL
   HFM_LAUNCH_CHECK();
@@ -234,7 +239,7 @@ static int scatter_k(const int* ukeys, const void* UG, const int* num, int max_n
 template <int K>
 static int sweep_k(int opt, long R, float* tv, float* tw, float* Gv, float* Gw, float* s0v,
                    float* s1v, float* s0w, float* s1w, OptHyper h, const int64_t* step,
-                   hipStream_t st) {
+                   long ldv, long ldw, hipStream_t st) {
   constexpr int LPS = K / 4;
   const long th = R * LPS;
   long g = (th + 255) / 256;
@@ -242,7 +247,7 @@ static int sweep_k(int opt, long R, float* tv, float* tw, float* Gv, float* Gw, 
   if (grid == 0) return 0;
 #define CALL(O)                                                                              \
   hipLaunchKernelGGL((dense_sweep_kernel<K, O>), dim3(grid), dim3(256), 0, st, R, tv, tw, Gv, \
-                     Gw, s0v, s1v, s0w, s1w, h, step)
+                     Gw, s0v, s1v, s0w, s1w, h, step, ldv, ldw)
   HFM_OPT_DISPATCH(opt, CALL)
 #undef CALL
   HFM_LAUNCH_CHECK();
@@ -261,8 +266,8 @@ static int sweep_k(int opt, long R, float* tv, float* tw, float* Gv, float* Gw, 
 HFM_API int hfm_sparse_rows_update(int K, int opt, const int* ukeys, const void* UG, const int* num,
                                    int max_n, int row_div, float* tv, float* tw, float* s0v,
                                    float* s1v, float* s0w, float* s1w, const OptHyper* h,
-                                   const int64_t* step, hipStream_t st) {
-#define CALL(KK) sparse_rows_k<KK>(opt, ukeys, UG, num, max_n, row_div, tv, tw, s0v, s1v, s0w, s1w, *h, step, st)
+                                   const int64_t* step, long ldv, long ldw, hipStream_t st) {
+#define CALL(KK) sparse_rows_k<KK>(opt, ukeys, UG, num, max_n, row_div, tv, tw, s0v, s1v, s0w, s1w, *h, step, ldv, ldw, st)
   HFM_K_DISPATCH(K, CALL)
 #undef CALL
 }
@@ -276,8 +281,8 @@ HFM_API int hfm_scatter_rows(int K, const int* ukeys, const void* UG, const int*
 
 HFM_API int hfm_dense_sweep(int K, int opt, long R, float* tv, float* tw, float* Gv, float* Gw,
                             float* s0v, float* s1v, float* s0w, float* s1w, const OptHyper* h,
-                            const int64_t* step, hipStream_t st) {
-#define CALL(KK) sweep_k<KK>(opt, R, tv, tw, Gv, Gw, s0v, s1v, s0w, s1w, *h, step, st)
+                            const int64_t* step, long ldv, long ldw, hipStream_t st) {
+#define CALL(KK) sweep_k<KK>(opt, R, tv, tw, Gv, Gw, s0v, s1v, s0w, s1w, *h, step, ldv, ldw, st)
   HFM_K_DISPATCH(K, CALL)
 #undef CALL
 }

@@ -97,8 +97,8 @@ __global__ void __launch_bounds__(256) fm_bwd_seg_kernel(
     // the whole tile is one id (dense-field / Zipf-hot ids): all 256 threads reduce it —
     // 8 lanes per column sum strided slices, then the 8 partials are added in a fixed order
     __shared__ float red[8][T::C];
-    const int c = threadIdx.x % 32, zl = threadIdx.x / 32;
-    if (c < T::C) {
+    const int zl = threadIdx.x / 32;
+    for (int c = threadIdx.x % 32; c < T::C; c += 32) {   // K >= 32: C > 32 columns
       float a0 = 0.f, a1 = 0.f;
       for (int q = zl; q < T::TP; q += 16) {
         a0 += g[q][c];
@@ -160,6 +160,7 @@ struct SegApplyArgs {
   float *Gv, *Gw;
   OptHyper h;
   const int64_t* step;
+  long ldv, ldw;           // table row strides (record layout: both = record floats)
 };
 
 template <int K, int MODE, int OPT>
@@ -200,7 +201,7 @@ __global__ void __launch_bounds__(256) seg_apply_kernel(SegApplyArgs A) {
     }
   }
   const size_t row = (size_t)(key / A.row_div);
-  const float* vrow = A.vsrc ? (A.vsrc + (size_t)(A.vsrc_compact ? u : row) * K) : (A.tv + row * K);
+  const float* vrow = A.vsrc ? (A.vsrc + (size_t)(A.vsrc_compact ? u : row) * K) : (A.tv + row * A.ldv);
   const f32x4 v = *reinterpret_cast<const f32x4*>(vrow + sub * 4);
   const f32x4 gv = a - v * c;
   if (MODE == 2) {
@@ -212,7 +213,8 @@ __global__ void __launch_bounds__(256) seg_apply_kernel(SegApplyArgs A) {
   } else {
     constexpr int O = OPT;
     const float lr_t = (O == OPT_ADAM) ? adam_lr_t(A.h, *A.step + 1) : A.h.lr;
-    const size_t o = row * K + sub * 4;
+    const size_t o = row * A.ldv + sub * 4;
+    const size_t ow = row * A.ldw;
     f32x4 p = A.vsrc ? *reinterpret_cast<f32x4*>(A.tv + o) : v;   // same row already loaded
     f32x4 s0 = {0, 0, 0, 0}, s1 = {0, 0, 0, 0};
     if (O != OPT_GD) s0 = *reinterpret_cast<f32x4*>(A.s0v + o);
@@ -228,14 +230,14 @@ __global__ void __launch_bounds__(256) seg_apply_kernel(SegApplyArgs A) {
     if (O != OPT_GD) *reinterpret_cast<f32x4*>(A.s0v + o) = s0;
     if (O == OPT_ADAM || O == OPT_FTRL) *reinterpret_cast<f32x4*>(A.s1v + o) = s1;
     if (sub == 0) {
-      float pw = A.tw[row];
+      float pw = A.tw[ow];
       float gw = w + A.h.l2 * pw;
-      float aw = (O != OPT_GD) ? A.s0w[row] : 0.f;
-      float cw = (O == OPT_ADAM || O == OPT_FTRL) ? A.s1w[row] : 0.f;
+      float aw = (O != OPT_GD) ? A.s0w[ow] : 0.f;
+      float cw = (O == OPT_ADAM || O == OPT_FTRL) ? A.s1w[ow] : 0.f;
       opt_update<O>(pw, gw, aw, cw, A.h, lr_t);
-      A.tw[row] = pw;
-      if (O != OPT_GD) A.s0w[row] = aw;
-      if (O == OPT_ADAM || O == OPT_FTRL) A.s1w[row] = cw;
+      A.tw[ow] = pw;
+      if (O != OPT_GD) A.s0w[ow] = aw;
+      if (O == OPT_ADAM || O == OPT_FTRL) A.s1w[ow] = cw;
     }
   }
 }

@@ -1,0 +1,308 @@
+// Fused embedding backward + row optimizer over the sorted slots (single rank / tf1_dense
+// scatter): K2 (per-slot FM + MLP-input gradient), K3 (sum per unique id) and K4 (lazy row
+// optimizer, or the tf1_dense gradient scatter) in one tile kernel plus one small carry kernel.
+// SURVEY §2.5 rows 17-20, §7.4 item 1; the reference's update is TF1 Adam._apply_sparse on the
+// IndexedSlices of embedding_lookup (HVD:170-176, HVD:252-263).
+//
+// Per slot (b, f) with id r and value x (see sparse_bwd.hip for the derivation):
+//     a = x*(dX0[b, f] + dy_b*S_b),  g_w = dy_b*x,  c = x^2*dy_b;   d fm_v[r] = sum(a) - V[r]*sum(c)
+//
+// Tile kernel (one workgroup per TP consecutive sorted slots):
+//   1. per-slot [a | g_w | c] rows into LDS;
+//   2. segmented sums without serial walks over long runs: the tile is cut into CH-slot chunks;
+//      one thread per (chunk, column) sums each run piece inside its chunk (in place at the
+//      run's head) and the chunk's leading piece (slots before its first head);
+//   3. every run head adds the leading pieces of the following chunks up to the chunk holding
+//      the next head.  A run that closes inside the tile is applied right here (optimizer on the
+//      row, or scatter); the one run that continues into the next tile leaves its partial in
+//      ctail[tile].  The tile's own leading piece (continuation of an earlier run) goes to
+//      lead[tile], with a flag when the tile has no head at all.
+// Carry kernel: each open run = ctail[t] + lead[t+1] + ... up to the first tile with a head
+// (tile order), then applied.  Every sum has a fixed order: bitwise reproducible, atomic-free.
+// Long runs (Criteo's integer fields: one id in every row) cost one lead read per tile they span.
+#include "common.h"
+
+template <int K>
+struct SfCfg {
+  static constexpr int TP = (K <= 16) ? 512 : (K == 32 ? 256 : 128);  // slots per tile
+  static constexpr int LPS = K / 4;                                    // lanes per slot (f32x4 each)
+  static constexpr int PPP = 256 / LPS;                                // slots per pass
+  static constexpr int PASSES = TP / PPP;
+  static constexpr int C = K + 2;  // columns: a[K], g_w, c
+  static constexpr int CH = 16;    // chunk length of the segmented sums
+  static constexpr int NCH = TP / CH;
+  static constexpr int RS = K + 4;  // ctail / lead row stride (16-B aligned)
+};
+
+struct SfArgs {
+  const int* sorted_keys;
+  const int* perm;  // slot position b*F + f of each sorted slot
+  const float* vals;
+  const float* dlogit;
+  const bf16* dX0;  // [B, KP] bf16
+  const float* S;   // [B, K]
+  int n, F, KP, row_div;
+  float* ctail;  // [tiles][RS]
+  float* lead;   // [tiles][RS]
+  int* tinfo;    // [tiles][2]: {headless, open-run key or -1}
+  float *tv, *tw, *s0v, *s1v, *s0w, *s1w;
+  float *Gv, *Gw;
+  OptHyper h;
+  const int64_t* step;
+  long ldv, ldw;  // table row strides (record layout: both = record floats)
+};
+
+// MODE 0: lazy optimizer OPT on the row; 1: tf1_dense scatter of the row gradient
+template <int K, int MODE, int OPT>
+__device__ __forceinline__ void sf_apply_row(const SfArgs& A, int key, int sub, f32x4 a, float w, float c,
+                                             float lr_t) {
+  const size_t row = (size_t)(key / A.row_div);
+  const size_t o = row * A.ldv + sub * 4;
+  const size_t ow = row * A.ldw;
+  f32x4 p = *reinterpret_cast<const f32x4*>(A.tv + o);
+  const f32x4 gv = a - p * c;
+  if (MODE == 1) {
+    *reinterpret_cast<f32x4*>(A.Gv + row * K + sub * 4) = gv;
+    if (sub == 0) A.Gw[row] = w;
+    return;
+  }
+  f32x4 s0 = {0, 0, 0, 0}, s1 = {0, 0, 0, 0};
+  if (OPT != OPT_GD) s0 = *reinterpret_cast<const f32x4*>(A.s0v + o);
+  if (OPT == OPT_ADAM || OPT == OPT_FTRL) s1 = *reinterpret_cast<const f32x4*>(A.s1v + o);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    float gj = gv[j] + A.h.l2 * p[j];
+    float pj = p[j], aj = s0[j], cj = s1[j];
+    opt_update<OPT>(pj, gj, aj, cj, A.h, lr_t);
+    p[j] = pj;
+    s0[j] = aj;
+    s1[j] = cj;
+  }
+  *reinterpret_cast<f32x4*>(A.tv + o) = p;
+  if (OPT != OPT_GD) *reinterpret_cast<f32x4*>(A.s0v + o) = s0;
+  if (OPT == OPT_ADAM || OPT == OPT_FTRL) *reinterpret_cast<f32x4*>(A.s1v + o) = s1;
+  if (sub == 0) {
+    float pw = A.tw[ow];
+    float gw = w + A.h.l2 * pw;
+    float aw = (OPT != OPT_GD) ? A.s0w[ow] : 0.f;
+    float cw = (OPT == OPT_ADAM || OPT == OPT_FTRL) ? A.s1w[ow] : 0.f;
+    opt_update<OPT>(pw, gw, aw, cw, A.h, lr_t);
+    A.tw[ow] = pw;
+    if (OPT != OPT_GD) A.s0w[ow] = aw;
+    if (OPT == OPT_ADAM || OPT == OPT_FTRL) A.s1w[ow] = cw;
+  }
+}
+
+template <int OPT>
+__device__ __forceinline__ float sf_lr_t(const SfArgs& A) {
+  return OPT == OPT_ADAM ? adam_lr_t(A.h, *A.step + 1) : A.h.lr;
+}
+
+template <int K, int MODE, int OPT>
+__global__ void __launch_bounds__(256) sf_tile_kernel(SfArgs A) {
+  using T = SfCfg<K>;
+  constexpr int CH = T::CH;
+  __shared__ float g[T::TP][T::C];
+  __shared__ int skl[T::TP];
+  __shared__ float lead[T::NCH][T::C];
+  __shared__ int fh[T::NCH];  // offset of the first head in the chunk (CH: none)
+  __shared__ int hl[T::TP];   // head positions, ascending
+  __shared__ int wcount[4];
+  __shared__ int open_key_s;
+  const int tile = blockIdx.x, b0 = tile * T::TP;
+  const int nloc = min(T::TP, A.n - b0);
+  const int nch = (nloc + CH - 1) / CH;
+  const int tid = threadIdx.x, sub = tid % T::LPS, lane = tid & 63, wv = tid >> 6;
+  const int prev_key = b0 > 0 ? A.sorted_keys[b0 - 1] : -1;
+  const int next_key = (b0 + nloc < A.n) ? A.sorted_keys[b0 + nloc] : -1;
+  if (tid == 0) open_key_s = -1;
+  // 1. per-slot contributions
+#pragma unroll
+  for (int ps = 0; ps < T::PASSES; ++ps) {
+    const int p = ps * T::PPP + tid / T::LPS;
+    if (p < nloc) {
+      const int i = b0 + p;
+      const int q = A.perm[i];
+      const int b = q / A.F, f = q - b * A.F;
+      const float x = A.vals[q];
+      const float dy = A.dlogit[b];
+      const f32x4 s = *reinterpret_cast<const f32x4*>(A.S + (size_t)b * K + sub * 4);
+      const bf16x4 dxh = *reinterpret_cast<const bf16x4*>(A.dX0 + (size_t)b * A.KP + f * K + sub * 4);
+      const f32x4 dx = {bf2f(dxh[0]), bf2f(dxh[1]), bf2f(dxh[2]), bf2f(dxh[3])};
+      const f32x4 av = (dx + dy * s) * x;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) g[p][sub * 4 + j] = av[j];
+      if (sub == 0) {
+        g[p][K] = dy * x;
+        g[p][K + 1] = dy * x * x;
+        skl[p] = A.sorted_keys[i];
+      }
+    }
+  }
+  __syncthreads();
+  // head flags -> compacted head list (ascending) and per-chunk first head
+  int nh = 0;
+  for (int r = 0; r < T::TP; r += 256) {
+    const int p = r + tid;
+    bool head = false;
+    if (p < nloc) head = (p == 0) ? (skl[0] != prev_key) : (skl[p] != skl[p - 1]);
+    const unsigned long long bal = __ballot(head);
+    if (lane == 0) wcount[wv] = __popcll(bal);
+    __syncthreads();
+    int off = nh;
+    for (int w = 0; w < wv; ++w) off += wcount[w];
+    if (head) hl[off + __popcll(bal & ((1ull << lane) - 1ull))] = p;
+    nh += wcount[0] + wcount[1] + wcount[2] + wcount[3];
+    __syncthreads();
+  }
+  if (tid < T::NCH) {
+    int f = CH;
+    for (int q = 0; q < CH; ++q) {
+      const int p = tid * CH + q;
+      if (p >= nloc) break;
+      if ((p == 0) ? (skl[0] != prev_key) : (skl[p] != skl[p - 1])) {
+        f = q;
+        break;
+      }
+    }
+    fh[tid] = f;
+  }
+  // 2. chunk-local run pieces: in place at the head, leading piece into lead[j]
+  for (int t = tid; t < T::NCH * T::C; t += 256) {
+    const int j = t / T::C, c = t - j * T::C;
+    const int p0 = j * CH, p1 = min(p0 + CH, nloc);
+    float s = 0.f;
+    int h = -1;
+    for (int p = p0; p < p1; ++p) {
+      const bool head = (p == 0) ? (skl[0] != prev_key) : (skl[p] != skl[p - 1]);
+      if (head) {
+        if (h < 0) lead[j][c] = s;
+        else g[h][c] = s;
+        s = 0.f;
+        h = p;
+      }
+      s += g[p][c];
+    }
+    if (h < 0) lead[j][c] = s;
+    else g[h][c] = s;
+  }
+  __syncthreads();
+  // tile leading piece (continuation of an earlier tile's run) + headless flag
+  if (tid < T::C) {
+    float s = 0.f;
+    bool any = false;
+    for (int j = 0; j < nch; ++j) {
+      s += lead[j][tid];
+      if (fh[j] < CH) {
+        any = true;
+        break;
+      }
+    }
+    A.lead[(size_t)tile * T::RS + tid] = s;
+    if (tid == 0) A.tinfo[tile * 2] = any ? 0 : 1;
+  }
+  // 3. finish every run headed in this tile
+  const float lr_t = sf_lr_t<OPT>(A);
+  for (int u = tid / T::LPS; u < nh; u += T::PPP) {
+    const int hp = hl[u];
+    const int key = skl[hp];
+    const int j = hp / CH;
+    f32x4 a = {g[hp][sub * 4], g[hp][sub * 4 + 1], g[hp][sub * 4 + 2], g[hp][sub * 4 + 3]};
+    float w = g[hp][K], c = g[hp][K + 1];
+    bool closed = (u + 1 < nh) && (hl[u + 1] / CH == j);
+    if (!closed) {
+      for (int jj = j + 1; jj < nch; ++jj) {
+        a += f32x4{lead[jj][sub * 4], lead[jj][sub * 4 + 1], lead[jj][sub * 4 + 2], lead[jj][sub * 4 + 3]};
+        w += lead[jj][K];
+        c += lead[jj][K + 1];
+        if (fh[jj] < CH) {
+          closed = true;
+          break;
+        }
+      }
+      if (!closed) closed = (next_key != key);
+    }
+    if (closed) {
+      sf_apply_row<K, MODE, OPT>(A, key, sub, a, w, c, lr_t);
+    } else {
+      float* ct = A.ctail + (size_t)tile * T::RS;
+      *reinterpret_cast<f32x4*>(ct + sub * 4) = a;
+      if (sub == 0) {
+        ct[K] = w;
+        ct[K + 1] = c;
+        open_key_s = key;
+      }
+    }
+  }
+  __syncthreads();
+  if (tid == 0) A.tinfo[tile * 2 + 1] = open_key_s;
+}
+
+template <int K, int MODE, int OPT>
+__global__ void __launch_bounds__(256) sf_carry_kernel(SfArgs A, int ntiles) {
+  using T = SfCfg<K>;
+  const int gt = blockIdx.x * blockDim.x + threadIdx.x;
+  const int t = gt / T::LPS, sub = gt % T::LPS;
+  if (t >= ntiles) return;
+  const int key = A.tinfo[t * 2 + 1];
+  if (key < 0) return;
+  const float* ct = A.ctail + (size_t)t * T::RS;
+  f32x4 a = *reinterpret_cast<const f32x4*>(ct + sub * 4);
+  float w = ct[K], c = ct[K + 1];
+  for (int t2 = t + 1; t2 < ntiles; ++t2) {
+    const float* ld = A.lead + (size_t)t2 * T::RS;
+    a += *reinterpret_cast<const f32x4*>(ld + sub * 4);
+    w += ld[K];
+    c += ld[K + 1];
+    if (!A.tinfo[t2 * 2]) break;
+  }
+  sf_apply_row<K, MODE, OPT>(A, key, sub, a, w, c, sf_lr_t<OPT>(A));
+}
+
+HFM_API int hfm_sparse_fused_tiles(int K, int n) {
+  const int tp = (K <= 16) ? 512 : (K == 32 ? 256 : 128);
+  return (n + tp - 1) / tp;
+}
+
+template <int K, int MODE, int OPT>
+static void sf_launch(const SfArgs& A, hipStream_t st) {
+  using T = SfCfg<K>;
+  const int tiles = (A.n + T::TP - 1) / T::TP;
+  hipLaunchKernelGGL((sf_tile_kernel<K, MODE, OPT>), dim3(tiles), dim3(256), 0, st, A);
+  const int cg = (tiles * T::LPS + 255) / 256;
+  hipLaunchKernelGGL((sf_carry_kernel<K, MODE, OPT>), dim3(cg), dim3(256), 0, st, A, tiles);
+}
+
+template <int K>
+static int sf_dispatch(int mode, int opt, const SfArgs& A, hipStream_t st) {
+  if (mode == 1) {
+    sf_launch<K, 1, 0>(A, st);
+    return 0;
+  }
+  switch (opt) {
+    case OPT_ADAM: sf_launch<K, 0, OPT_ADAM>(A, st); break;
+    case OPT_ADAGRAD: sf_launch<K, 0, OPT_ADAGRAD>(A, st); break;
+    case OPT_MOMENTUM: sf_launch<K, 0, OPT_MOMENTUM>(A, st); break;
+    case OPT_FTRL: sf_launch<K, 0, OPT_FTRL>(A, st); break;
+    case OPT_GD: sf_launch<K, 0, OPT_GD>(A, st); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+  return 0;
+}
+
+// mode 0: lazy optimizer `opt` on every unique row; 1: tf1_dense scatter into (Gv, Gw)
+HFM_API int hfm_sparse_fused(int K, int mode, int opt, const SfArgs* A, hipStream_t st) {
+  if (A->n <= 0) return 0;
+  int rc;
+  switch (K) {
+    case 4: rc = sf_dispatch<4>(mode, opt, *A, st); break;
+    case 8: rc = sf_dispatch<8>(mode, opt, *A, st); break;
+    case 16: rc = sf_dispatch<16>(mode, opt, *A, st); break;
+    case 32: rc = sf_dispatch<32>(mode, opt, *A, st); break;
+    case 64: rc = sf_dispatch<64>(mode, opt, *A, st); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+  if (rc) return rc;
+  HFM_LAUNCH_CHECK();
+}
+HFM_API int hfm_sparse_fused_args_bytes() { return (int)sizeof(SfArgs); }

@@ -36,7 +36,15 @@ _DT_INV = {v: k for k, v in _DT.items()}
 
 
 def _tensor_bytes_iter(t: torch.Tensor, chunk: int = 1 << 28):
-    t = t.detach().contiguous().view(-1)
+    t = t.detach()
+    if not t.is_contiguous() and t.dim() >= 1 and t.shape[0] > 0:
+        # strided views (row-record table layout): stream row blocks, never a full-table copy
+        row_bytes = max(1, t[0].numel() * t.element_size())
+        rows = max(1, chunk // row_bytes)
+        for i in range(0, t.shape[0], rows):
+            yield from _tensor_bytes_iter(t[i: i + rows].contiguous(), chunk)
+        return
+    t = t.contiguous().view(-1)
     es = t.element_size()
     step = max(1, chunk // es)
     for i in range(0, t.numel(), step):

@@ -33,7 +33,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import torch
 
 from ..ops import kernels as KN
-from ..ops._lib import TW_MAXL, BnArgs, EpiArgs, HeadArgs, TowerArgs, WgJob, RowSumJob, SegApplyArgs, ShadowSeg, SlabJob
+from ..ops._lib import TW_MAXL, BnArgs, EpiArgs, HeadArgs, TowerArgs, WgJob, RowSumJob, SegApplyArgs, SfArgs, ShadowSeg, SlabJob
 from ..utils.rng import keep_threshold
 from .reference import glorot_std, init_params, pad32
 
@@ -43,6 +43,7 @@ _SEPARATE_STEP_INC = os.environ.get("HIPFM_STEP_INC", "0") == "1"
 _OLD_FINALIZE = os.environ.get("HIPFM_OLD_FINALIZE", "0") == "1"
 _SORT_MODE = os.environ.get("HIPFM_SORT", "auto")                # auto | global
 _SORT_SIDE_STREAM = os.environ.get("HIPFM_SORT_SIDE_STREAM", "1") == "1"
+_SPARSE_IMPL = os.environ.get("HIPFM_SPARSE", "fused")             # fused | seg
 
 
 def check_field_ranges(ranges, F: int, V: int) -> List[Tuple[int, int]]:
@@ -67,6 +68,20 @@ def field_ranges_from_sizes(sizes: Sequence[int]) -> List[Tuple[int, int]]:
         out.append((lo, lo + int(n)))
         lo += int(n)
     return out
+
+
+_OPT_SLOTS = {"Adam": 2, "ftrl": 2, "Adagrad": 1, "Momentum": 1, "GD": 0}
+_TABLE_LAYOUT = os.environ.get("HIPFM_TABLE_LAYOUT", "record")     # record | split
+
+
+def table_record_floats(K: int, optimizer: str) -> int:
+    """Floats per embedding-row record in the interleaved table layout:
+        [ v (K) | w, w_slot0, w_slot1, pad | v_slot0 (K) | v_slot1 (K) ]  rounded up to 64 B
+    (<= 16 floats) or to whole 128-B lines.  A lazy row update then reads and writes one record
+    (K = 8 with Adam: exactly one 128-B line) instead of one row in each of six tables, and the
+    forward gather finds v and w in the same 64-B sector."""
+    x = K + 4 + _OPT_SLOTS[optimizer] * K
+    return (x + 15) // 16 * 16 if x <= 16 else (x + 31) // 32 * 32
 
 
 def _align(n: int, a: int = 64) -> int:
@@ -194,8 +209,19 @@ class NativeDeepFM:
 
         dev = self.device
         f32 = dict(dtype=torch.float32, device=dev)
-        self.tv = torch.zeros(self.R, K, **f32)
-        self.tw = torch.zeros(self.R, **f32)
+        # embedding tables: fm_v [R, K], fm_w [R] and their optimizer slots are strided views of
+        # one [R, RS] record buffer (table_record_floats); HIPFM_TABLE_LAYOUT=split keeps six
+        # separate contiguous tables (A/B)
+        self.record = _TABLE_LAYOUT == "record"
+        if self.record:
+            self.rec_stride = table_record_floats(K, optimizer)
+            self.rec = torch.zeros(self.R, self.rec_stride, **f32)
+            self.tv = self.rec[:, :K]
+            self.tw = self.rec[:, K]
+        else:
+            self.rec = None
+            self.tv = torch.zeros(self.R, K, **f32)
+            self.tw = torch.zeros(self.R, **f32)
         self.p = torch.zeros(self.P, **f32)
         self.g = torch.zeros(self.P, **f32)
         self.step = torch.zeros(1, dtype=torch.int64, device=dev)
@@ -265,25 +291,24 @@ class NativeDeepFM:
     def _alloc_slots(self):
         f32 = dict(dtype=torch.float32, device=self.device)
         R, K, P = self.R, self.K, self.P
-        z = lambda *s: torch.zeros(*s, **f32)
         e = torch.empty(0, **f32)
         o = self.optimizer
-        if o == "Adam":
-            self.sv = [z(R, K), z(R, K), z(R), z(R)]
-            self.sd = [z(P), z(P)]
-        elif o == "Adagrad":
-            a0 = self.adagrad_init
-            self.sv = [torch.full((R, K), a0, **f32), e, torch.full((R,), a0, **f32), e]
-            self.sd = [torch.full((P,), a0, **f32), e]
-        elif o == "Momentum":
-            self.sv = [z(R, K), e, z(R), e]
-            self.sd = [z(P), e]
-        elif o == "ftrl":
-            self.sv = [torch.full((R, K), 0.1, **f32), z(R, K), torch.full((R,), 0.1, **f32), z(R)]
-            self.sd = [torch.full((P,), 0.1, **f32), z(P)]
-        else:  # GD
-            self.sv = [e, e, e, e]
-            self.sd = [e, e]
+        ns = _OPT_SLOTS[o]
+        init = {"Adagrad": self.adagrad_init, "ftrl": 0.1}.get(o, 0.0)   # slot-0 initial value
+        if self.record:
+            rec = self.rec
+            s0v, s1v = rec[:, K + 4: 2 * K + 4], rec[:, 2 * K + 4: 3 * K + 4]
+            s0w, s1w = rec[:, K + 1], rec[:, K + 2]
+        else:
+            s0v, s1v = torch.zeros(R, K, **f32), torch.zeros(R, K, **f32)
+            s0w, s1w = torch.zeros(R, **f32), torch.zeros(R, **f32)
+        self.sv = [s0v if ns >= 1 else e, s1v if ns >= 2 else e,
+                   s0w if ns >= 1 else e, s1w if ns >= 2 else e]
+        self.sd = [torch.zeros(P, **f32) if ns >= 1 else e, torch.zeros(P, **f32) if ns >= 2 else e]
+        if init:
+            with torch.no_grad():
+                for t in (self.sv[0], self.sv[2], self.sd[0]):
+                    t.fill_(init)
 
     def _tower_lds_bytes(self) -> int:
         h = sum(32 * (n + 8) * 2 for n in self.Np)
@@ -353,6 +378,10 @@ class NativeDeepFM:
         self.seg_flags = torch.zeros(n, **i32)
         self.sid_incl = torch.zeros(n, **i32)
         self.seg_start = torch.zeros(n + 1, **i32)
+        nt = KN.sparse_fused_tiles(K, n)
+        self.sf_ctail = torch.zeros(nt, K + 4, **f32)
+        self.sf_lead = torch.zeros(nt, K + 4, **f32)
+        self.sf_tinfo = torch.zeros(nt, 2, **i32)
         self.fs_err = torch.zeros(1, **i32)
         self._fs_ranges = None
         if self.field_ranges is not None:
@@ -732,6 +761,7 @@ class NativeDeepFM:
             A.Gv, A.Gw = self.Gv.data_ptr(), self.Gw.data_ptr()
         A.h = self.h_sparse
         A.step = self.step.data_ptr()
+        A.ldv, A.ldw = KN._ld(self.tv, self.tw)
         return A
 
     def uses_field_sort(self, B: int) -> bool:
@@ -753,6 +783,22 @@ class NativeDeepFM:
             raise RuntimeError("an id lies outside its field's declared range (field_ranges): "
                                "the per-field sort is invalid for this data")
 
+    def sf_args(self, n: int) -> SfArgs:
+        A = SfArgs()
+        A.sorted_keys, A.perm = self.sorted_keys.data_ptr(), self.perm.data_ptr()
+        A.vals, A.dlogit = self.vals.data_ptr(), self.dlogit.data_ptr()
+        A.dX0, A.S = self.dX0.data_ptr(), self.S.data_ptr()
+        A.n, A.F, A.KP, A.row_div = n, self.F, self.K0p, self.row_div
+        A.ctail, A.lead, A.tinfo = self.sf_ctail.data_ptr(), self.sf_lead.data_ptr(), self.sf_tinfo.data_ptr()
+        A.tv, A.tw = self.tv.data_ptr(), self.tw.data_ptr()
+        A.s0v, A.s1v, A.s0w, A.s1w = (t.data_ptr() if t.numel() else 0 for t in self.sv)
+        if self.sparse_update == "tf1_dense":
+            A.Gv, A.Gw = self.Gv.data_ptr(), self.Gw.data_ptr()
+        A.h = self.h_sparse
+        A.step = self.step.data_ptr()
+        A.ldv, A.ldw = KN._ld(self.tv, self.tw)
+        return A
+
     def _sparse_backward(self, B: int, idx, tv, presorted: bool = False):
         """Embedding backward.  Single rank: the row update is fused into the reduction
         (returns None).  Multi-rank: returns compact unique-row gradients for the exchange."""
@@ -761,6 +807,13 @@ class NativeDeepFM:
             return self.comm.sharded_backward(self, B, idx, tv)
         if not presorted:
             self._sort_slots(B)
+        if not self.exchange and _SPARSE_IMPL == "fused":
+            KN.sparse_fused(self.K, KN.SF_LAZY if self.sparse_update == "lazy" else KN.SF_SCATTER,
+                            self.opt_id, self.sf_args(n))
+            if self.sparse_update != "lazy":
+                KN.dense_sweep(self.K, self.opt_id, self.R, self.tv, self.tw, self.Gv, self.Gw,
+                               self.sv, self.h_sparse, self.step)
+            return None
         if not self.exchange:
             self._segment_reduce(n, compact=False)
             A = self.seg_args(n, compact=False)
@@ -974,7 +1027,10 @@ class NativeDeepFM:
         if self.batch_norm:
             out.append(self.bn_moving)
         if not self.sharded:
-            out += [self.tv, self.tw] + [t for t in self.sv if t.numel()]
+            if self.record:
+                out.append(self.rec)          # collectives need contiguous tensors
+            else:
+                out += [self.tv, self.tw] + [t for t in self.sv if t.numel()]
         return out
 
     def ckpt_meta(self) -> dict:

@@ -74,7 +74,16 @@ class SegApplyArgs(C.Structure):
                 ("partial", c_void_p), ("cont", c_void_p), ("UG", c_void_p), ("tv", c_void_p),
                 ("tw", c_void_p), ("s0v", c_void_p), ("s1v", c_void_p), ("s0w", c_void_p),
                 ("s1w", c_void_p), ("Gv", c_void_p), ("Gw", c_void_p), ("h", OptHyper),
-                ("step", c_void_p)]
+                ("step", c_void_p), ("ldv", c_long), ("ldw", c_long)]
+
+
+class SfArgs(C.Structure):
+    _fields_ = [("sorted_keys", c_void_p), ("perm", c_void_p), ("vals", c_void_p), ("dlogit", c_void_p),
+                ("dX0", c_void_p), ("S", c_void_p), ("n", c_int), ("F", c_int), ("KP", c_int),
+                ("row_div", c_int), ("ctail", c_void_p), ("lead", c_void_p), ("tinfo", c_void_p),
+                ("tv", c_void_p), ("tw", c_void_p), ("s0v", c_void_p), ("s1v", c_void_p),
+                ("s0w", c_void_p), ("s1w", c_void_p), ("Gv", c_void_p), ("Gw", c_void_p),
+                ("h", OptHyper), ("step", c_void_p), ("ldv", c_long), ("ldw", c_long)]
 
 
 TW_MAXL = 8
@@ -100,7 +109,7 @@ class WgJob(C.Structure):
 
 
 _SIGS = {
-    "hfm_fm_fwd": [c_void_p] * 5 + [c_int] * 4 + [c_void_p] * 4 + [c_void_p],
+    "hfm_fm_fwd": [c_void_p] * 5 + [c_int] * 4 + [c_void_p] * 4 + [c_long, c_long, c_void_p],
     "hfm_fm_bwd_sorted": [c_void_p] * 7 + [c_int] * 4 + [c_void_p, c_void_p],
     "hfm_grad_row_bytes": [c_int],
     "hfm_sort_pairs_temp_bytes": [c_int, c_int, C.POINTER(c_size_t)],
@@ -112,9 +121,10 @@ _SIGS = {
     "hfm_owner_keys": [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p],
     "hfm_gather_i32": [c_void_p, c_void_p, c_int, c_void_p, c_void_p],
     "hfm_sparse_rows_update": [c_int, c_int] + [c_void_p] * 3 + [c_int, c_int] + [c_void_p] * 6
-                              + [C.POINTER(OptHyper), c_void_p, c_void_p],
+                              + [C.POINTER(OptHyper), c_void_p, c_long, c_long, c_void_p],
     "hfm_scatter_rows": [c_int] + [c_void_p] * 3 + [c_int, c_int, c_void_p, c_void_p, c_void_p],
-    "hfm_dense_sweep": [c_int, c_int, c_long] + [c_void_p] * 8 + [C.POINTER(OptHyper), c_void_p, c_void_p],
+    "hfm_dense_sweep": [c_int, c_int, c_long] + [c_void_p] * 8 + [C.POINTER(OptHyper), c_void_p, c_long,
+                                                                  c_long, c_void_p],
     "hfm_dense_opt": [c_int] + [c_void_p] * 4 + [c_long, C.POINTER(OptHyper), c_void_p, c_void_p, c_int,
                                                  c_void_p, c_void_p],
     "hfm_finalize": [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p],
@@ -139,6 +149,9 @@ _SIGS = {
     "hfm_onesweep_sort_ids": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_size_t, c_void_p],
     "hfm_onesweep_error_offset": [],
     "hfm_field_sort_max_rows": [],
+    "hfm_sparse_fused_tiles": [c_int, c_int],
+    "hfm_sparse_fused": [c_int, c_int, c_int, c_void_p, c_void_p],
+    "hfm_sparse_fused_args_bytes": [],
     "hfm_field_sort": [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "hfm_radix_sort_ids": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_size_t, c_void_p],
     "hfm_segments": [c_void_p, c_int] + [c_void_p] * 5 + [c_void_p, c_size_t, c_void_p],
@@ -184,7 +197,8 @@ def get_lib():
                            ("hfm_slab_job_bytes", SlabJob), ("hfm_rowsum_job_bytes", RowSumJob),
                            ("hfm_shadow_seg_bytes", ShadowSeg), ("hfm_opt_hyper_bytes", OptHyper),
                            ("hfm_seg_apply_args_bytes", SegApplyArgs), ("hfm_bn_args_bytes", BnArgs),
-                           ("hfm_tower_args_bytes", TowerArgs), ("hfm_wg_job_bytes", WgJob)):
+                           ("hfm_tower_args_bytes", TowerArgs), ("hfm_wg_job_bytes", WgJob),
+                           ("hfm_sparse_fused_args_bytes", SfArgs)):
             n = getattr(lib, cname)()
             if n != C.sizeof(pys):
                 raise RuntimeError(f"ABI mismatch {pys.__name__}: C {n} vs ctypes {C.sizeof(pys)}")

@@ -12,7 +12,7 @@ from typing import List, Optional, Sequence
 import torch
 
 from . import _lib
-from ._lib import (BnArgs, EpiArgs, HeadArgs, TowerArgs, WgJob, OptHyper, RowSumJob, SegApplyArgs, ShadowSeg, SlabJob, check,
+from ._lib import (BnArgs, EpiArgs, HeadArgs, TowerArgs, WgJob, OptHyper, RowSumJob, SegApplyArgs, SfArgs, ShadowSeg, SlabJob, check,
                    ptr, stream_handle)
 
 EPI_F32, EPI_FWD, EPI_DGRAD, EPI_FWD_EVAL, EPI_RELU_F32 = 0, 1, 2, 3, 4
@@ -27,9 +27,17 @@ def L():
     return _lib.get_lib()
 
 
+def _ld(tv, tw):
+    """Row strides (in floats) of a v table [R, K] and a w table [R] (plain or record views)."""
+    ldv = tv.stride(0) if tv.dim() == 2 else tv.shape[-1]
+    ldw = tw.stride(0) if tw.dim() == 1 else 1
+    return ldv, ldw
+
+
 def fm_fwd(idx, vals, tv, tw, bias, B, F, K, KP, y_fm, S, E, Et):
+    assert tv.stride(-1) == 1
     check(L().hfm_fm_fwd(ptr(idx), ptr(vals), ptr(tv), ptr(tw), ptr(bias), B, F, K, KP, ptr(y_fm),
-                         ptr(S), ptr(E), ptr(Et), stream_handle()), "fm_fwd")
+                         ptr(S), ptr(E), ptr(Et), *_ld(tv, tw), stream_handle()), "fm_fwd")
 
 
 def fm_bwd_sorted(perm, idx, vals, tv, dlogit, dX0, S, n, F, K, KP, G):
@@ -154,6 +162,19 @@ def fm_bwd_seg(K, sorted_keys, perm, sid_incl, vals, dlogit, dX0, S, n, F, KP, p
 SEG_LAZY, SEG_SCATTER, SEG_WRITE_UG = 0, 1, 2
 
 
+SF_LAZY, SF_SCATTER = 0, 1
+
+
+def sparse_fused_tiles(K: int, n: int) -> int:
+    return int(L().hfm_sparse_fused_tiles(K, n))
+
+
+def sparse_fused(K, mode, opt, args: SfArgs):
+    """Fused embedding backward + row optimizer (lazy) or tf1_dense scatter over sorted slots
+    (csrc/kernels/sparse_fused.hip): one tile kernel + one carry kernel."""
+    check(L().hfm_sparse_fused(K, mode, opt, C.byref(args), stream_handle()), "sparse_fused")
+
+
 def seg_apply(K, mode, opt, args: SegApplyArgs, max_groups):
     check(L().hfm_seg_apply(K, mode, opt, C.byref(args), max_groups, stream_handle()), "seg_apply")
 
@@ -166,7 +187,7 @@ def sparse_rows_update(K, opt, ukeys, UG, num, max_n, row_div, tv, tw, slots, h:
     s0v, s1v, s0w, s1w = slots
     check(L().hfm_sparse_rows_update(K, opt, ptr(ukeys), ptr(UG), ptr(num), max_n, row_div, ptr(tv),
                                      ptr(tw), ptr(s0v), ptr(s1v), ptr(s0w), ptr(s1w), C.byref(h),
-                                     ptr(step), stream_handle()), "sparse_rows_update")
+                                     ptr(step), *_ld(tv, tw), stream_handle()), "sparse_rows_update")
 
 
 def scatter_rows(K, ukeys, UG, num, max_n, row_div, Gv, Gw):
@@ -177,7 +198,7 @@ def scatter_rows(K, ukeys, UG, num, max_n, row_div, Gv, Gw):
 def dense_sweep(K, opt, R, tv, tw, Gv, Gw, slots, h: OptHyper, step):
     s0v, s1v, s0w, s1w = slots
     check(L().hfm_dense_sweep(K, opt, R, ptr(tv), ptr(tw), ptr(Gv), ptr(Gw), ptr(s0v), ptr(s1v),
-                              ptr(s0w), ptr(s1w), C.byref(h), ptr(step), stream_handle()),
+                              ptr(s0w), ptr(s1w), C.byref(h), ptr(step), *_ld(tv, tw), stream_handle()),
           "dense_sweep")
 
 
@@ -246,6 +267,12 @@ def auc_hist(pred, label, n, hist):
 
 
 def sumsq(x: torch.Tensor, nblocks: int = 512) -> torch.Tensor:
+    if not x.is_contiguous():       # strided table views (record layout): row blocks
+        tot = torch.zeros((), dtype=torch.float64, device=x.device)
+        step = 1 << 22
+        for i in range(0, x.shape[0], step):
+            tot += sumsq(x[i: i + step].contiguous(), nblocks)
+        return tot
     out = torch.empty(nblocks, dtype=torch.float64, device=x.device)
     check(L().hfm_sumsq_partials(ptr(x), x.numel(), ptr(out), nblocks, stream_handle()), "sumsq")
     return out.sum()

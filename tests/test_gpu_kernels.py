@@ -398,3 +398,37 @@ def test_train_step_field_sort_bitwise_equals_global_sort():
     torch.cuda.synchronize()
     assert torch.equal(a.tv, b.tv) and torch.equal(a.tw, b.tw) and torch.equal(a.p, b.p)
     a.check_errors()
+
+
+@pytest.mark.parametrize("opt,mode,K", [("Adam", "lazy", 8), ("Adagrad", "lazy", 16), ("ftrl", "tf1_dense", 4),
+                                        ("Adam", "tf1_dense", 32), ("Momentum", "lazy", 64)])
+def test_sparse_fused_matches_segment_kernels(opt, mode, K):
+    """sparse_fused.hip (tile kernel + carry kernel, chunked segmented sums, optimizer applied in
+    place) vs the two-kernel fm_bwd_seg + seg_apply path: same updates up to fp32 summation
+    order.  Criteo-shaped ids: 13 integer fields are one id in every row (runs spanning many
+    tiles), small categorical vocabularies give long runs, large ones mostly singletons."""
+    import hipfm.models.deepfm as dm
+    synth = make_synth("criteo_kaggle")
+    F, layers, keep, B = synth.F, [64, 32], [0.5, 0.5], 2000
+    kw = dict(optimizer=opt, sparse_update=mode, batch_size=B, device=DEV, seed=5,
+              field_ranges=synth.field_ranges())
+    a = NativeDeepFM(synth.feature_size, F, K, layers, keep, **kw)
+    b = NativeDeepFM(synth.feature_size, F, K, layers, keep, **kw)
+    batches = [synth.batch(B, i, device=DEV, id_dtype=torch.int32) for i in range(3)]
+    old = dm._SPARSE_IMPL
+    try:
+        for step in range(3):
+            ids, vals, lab = batches[step]
+            dm._SPARSE_IMPL = "fused"
+            a.train_step(ids, vals, lab)
+            dm._SPARSE_IMPL = "seg"
+            b.train_step(ids, vals, lab)
+        torch.cuda.synchronize()
+    finally:
+        dm._SPARSE_IMPL = old
+    for x, y in ((a.tv, b.tv), (a.tw, b.tw), (a.p, b.p)):
+        d = (x - y).abs().max().item()
+        assert d <= 1e-5 * max(1.0, y.abs().max().item()), d
+    for sa, sb in zip(a.sv, b.sv):
+        if sa.numel():
+            assert (sa - sb).abs().max().item() <= 1e-5 * max(1e-6, sb.abs().max().item()) + 1e-12
