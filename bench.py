@@ -47,6 +47,8 @@ def main():
     ap.add_argument("--pool", type=int, default=16, help="resident synthetic batches per rank")
     ap.add_argument("--eval_batches", type=int, default=8)
     ap.add_argument("--no_graph", action="store_true")
+    ap.add_argument("--force_exchange", action="store_true",
+                    help="run the multi-GPU (row-sharded exchange) step on a 1-rank group")
     args = ap.parse_args()
 
     import torch
@@ -63,13 +65,20 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    synth = make_synth(args.preset, seed=2024)
     comm = None
-    if world > 1:
+    if world > 1 or args.force_exchange:
         init_distributed("nccl")
         mode = "sharded" if args.embedding_mode == "auto" else args.embedding_mode
-        comm = Comm(sharded=(mode == "sharded"))
+        cap = None
+        if mode == "sharded":
+            # per-peer capacity of the fixed-size all-to-alls, measured on sample batches of this
+            # rank's id distribution (x1.25 + 256 slack; overflow raises, never drops rows)
+            from hipfm.parallel.sharded import estimate_capacity
+            cap = estimate_capacity((synth.batch(args.batch_size, step=rank * 100000 + i, device=dev,
+                                                 id_dtype=torch.int32)[0] for i in range(4)), world)
+        comm = Comm(sharded=(mode == "sharded"), force_exchange=args.force_exchange, capacity=cap)
 
-    synth = make_synth(args.preset, seed=2024)
     F = synth.F
     B = args.batch_size
     layers = [int(x) for x in args.deep_layers.split(",")]

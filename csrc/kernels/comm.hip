@@ -1,0 +1,58 @@
+// Native collective engine over RCCL (Horovod core + NCCL -> RCCL over xGMI).
+//
+// The data-parallel step issues its collectives straight into RCCL on the HIP streams the
+// kernels run on, so the whole multi-GPU step (exchanges included) is one capturable sequence
+// with no host synchronisation:
+//   * all_reduce   : the flat dense-gradient bucket (Horovod DistributedOptimizer, HVD:262),
+//                    issued on a side stream and overlapped with the sparse backward;
+//   * all_to_all   : fixed-capacity id / row / gradient exchanges of the row-sharded embedding
+//                    (every peer block has the same byte size, so no split sizes ever travel
+//                    through the host; xGMI is a full mesh, so all 7 peer links run at once).
+// The communicator is bootstrapped from a unique id that rank 0 creates and the launcher's
+// process group broadcasts (the reference's hvd.init / mpirun rendezvous, HVD:295).
+// librccl.so.1 is the RCCL PyTorch already loaded (same SONAME), so one RCCL runs per process.
+#include <rccl/rccl.h>
+#include <string.h>
+#include "common.h"
+
+static int nccl_rc(ncclResult_t r) { return r == ncclSuccess ? 0 : 1000 + (int)r; }
+
+HFM_API int hfm_comm_id_bytes() { return (int)sizeof(ncclUniqueId); }
+
+HFM_API int hfm_comm_unique_id(void* out) {
+  ncclUniqueId id;
+  const ncclResult_t r = ncclGetUniqueId(&id);
+  if (r != ncclSuccess) return nccl_rc(r);
+  memcpy(out, &id, sizeof(id));
+  return 0;
+}
+
+// The calling thread's current HIP device is the communicator's device.
+HFM_API int hfm_comm_init(void** comm, int nranks, int rank, const void* id_bytes) {
+  ncclUniqueId id;
+  memcpy(&id, id_bytes, sizeof(id));
+  ncclComm_t c = nullptr;
+  const ncclResult_t r = ncclCommInitRank(&c, nranks, id, rank);
+  if (r != ncclSuccess) return nccl_rc(r);
+  *comm = (void*)c;
+  return 0;
+}
+
+HFM_API int hfm_comm_destroy(void* comm) {
+  if (!comm) return 0;
+  return nccl_rc(ncclCommDestroy((ncclComm_t)comm));
+}
+
+HFM_API int hfm_comm_allreduce_f32(void* comm, float* buf, size_t n, hipStream_t st) {
+  if (n == 0) return 0;
+  return nccl_rc(ncclAllReduce(buf, buf, n, ncclFloat32, ncclSum, (ncclComm_t)comm, st));
+}
+
+// send/recv: nranks blocks of `bytes_per_peer` bytes each (block p goes to / comes from rank p)
+HFM_API int hfm_comm_alltoall(void* comm, const void* send, void* recv, size_t bytes_per_peer,
+                              hipStream_t st) {
+  if (bytes_per_peer == 0) return 0;
+  if (bytes_per_peer % 4 == 0)
+    return nccl_rc(ncclAllToAll(send, recv, bytes_per_peer / 4, ncclInt32, (ncclComm_t)comm, st));
+  return nccl_rc(ncclAllToAll(send, recv, bytes_per_peer, ncclInt8, (ncclComm_t)comm, st));
+}

@@ -1,0 +1,314 @@
+// Row-sharded embedding exchange with FIXED per-peer capacity (SURVEY P1/P4, §2.6 row-sharded
+// mode; the reference's parameter servers pull rows and push gradients over gRPC, PS:414-442).
+//
+// owner(id) = id % N, local row = id / N.  Every exchange moves N blocks of exactly C entries
+// (unused entries carry id -1), so all-to-alls need no host-side split sizes and the whole step
+// is one capturable stream sequence without a host synchronisation:
+//
+//   requester                                        owner
+//   sorted uniques -> sh_scatter: send_ids[o][c]  -- a2a -->  recv_ids[p][c]
+//   (upos[u] = o*C + c)                                       sh_serve: rows[p][c] = {v, w}
+//   rows_in[o][c]                                 <-- a2a --
+//   sh_slot_rows: slot -> rows_in row; fm_fwd / tower / sparse_fused (MODE 2: gradient rows
+//   g_u written at send_g[upos[u]], V taken from rows_in)
+//   send_g[o][c]                                  -- a2a -->  recv_g[p][c]
+//                                                             sh_owner_tag: tag[row][p] = (step, c)
+//                                                             sh_owner_apply: the lowest requesting
+//                                                             rank sums the rows of all requesters
+//                                                             in rank order, applies the optimizer
+//
+// The tag table [R_local][N] (64-bit {step+1, c}) replaces a sort of the received ids: a row
+// requested by several ranks is found by direct addressing, and the sum runs in rank order, so
+// results are bitwise reproducible.  A bucket larger than C sets err bit 2 (the host raises).
+#include "common.h"
+
+namespace {
+constexpr int SH_THREADS = 256;
+constexpr int SH_ITEMS = 16;
+constexpr int SH_TILE = SH_THREADS * SH_ITEMS;
+constexpr int SH_MAXN = 64;  // ranks
+}  // namespace
+
+__global__ void __launch_bounds__(SH_THREADS) sh_count_kernel(const int* __restrict__ ukeys,
+                                                             const int* __restrict__ num_u, int N,
+                                                             int* __restrict__ cnt) {
+  __shared__ int h[SH_MAXN];
+  if (threadIdx.x < N) h[threadIdx.x] = 0;
+  __syncthreads();
+  const int U = *num_u;
+  const int b0 = blockIdx.x * SH_TILE;
+#pragma unroll 4
+  for (int k = 0; k < SH_ITEMS; ++k) {
+    const int u = b0 + k * SH_THREADS + threadIdx.x;
+    if (u < U) atomicAdd(&h[ukeys[u] % N], 1);
+  }
+  __syncthreads();
+  if (threadIdx.x < N) cnt[blockIdx.x * N + threadIdx.x] = h[threadIdx.x];
+}
+
+// Stable bucketing of the (id-sorted) unique list by owner: send_ids[o*C + c] and upos[u].
+__global__ void __launch_bounds__(SH_THREADS) sh_scatter_kernel(
+    const int* __restrict__ ukeys, const int* __restrict__ num_u, int N, int nbits, int C,
+    const int* __restrict__ cnt, int nb, int* __restrict__ send_ids, int* __restrict__ upos,
+    int* __restrict__ send_cnt, unsigned* __restrict__ err) {
+  __shared__ int off[SH_MAXN];
+  __shared__ int wc[4][SH_MAXN];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int U = *num_u;
+  if (tid < N) {
+    int s = 0, tot = 0;
+    for (int b = 0; b < nb; ++b) {
+      const int c = cnt[b * N + tid];
+      if (b < (int)blockIdx.x) s += c;
+      tot += c;
+    }
+    off[tid] = s;
+    if (blockIdx.x == 0) {
+      send_cnt[tid] = tot;
+      if (tot > C) atomicOr(err, 2u);
+    }
+  }
+  if (tid < SH_MAXN) wc[0][tid] = wc[1][tid] = wc[2][tid] = wc[3][tid] = 0;
+  __syncthreads();
+  const int w0 = blockIdx.x * SH_TILE + wv * 64 * SH_ITEMS;
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  int own[SH_ITEMS], rnk[SH_ITEMS];
+#pragma unroll
+  for (int k = 0; k < SH_ITEMS; ++k) {
+    const int u = w0 + k * 64 + lane;
+    const bool valid = u < U;
+    const int o = valid ? ukeys[u] % N : 0;
+    unsigned long long peers = __ballot(valid);
+    for (int bit = 0; bit < nbits; ++bit) {
+      const bool bset = (o >> bit) & 1;
+      const unsigned long long bal = __ballot(bset);
+      peers &= bset ? bal : ~bal;
+    }
+    const int rk = __popcll(peers & lt);
+    const int old = wc[wv][o];  // in-order LDS ops of one wave: all lanes read before the update
+    own[k] = o;
+    rnk[k] = old + rk;
+    if (valid && rk == 0) wc[wv][o] = old + __popcll(peers);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < SH_ITEMS; ++k) {
+    const int u = w0 + k * 64 + lane;
+    if (u >= U) continue;
+    const int o = own[k];
+    int pos = off[o] + rnk[k];
+    for (int w = 0; w < wv; ++w) pos += wc[w][o];
+    if (pos < C) {
+      send_ids[o * C + pos] = ukeys[u];
+      upos[u] = o * C + pos;
+    } else {
+      upos[u] = -1;
+      atomicOr(err, 2u);
+    }
+  }
+}
+
+// fm_fwd row index of every slot: the received row of its unique id
+__global__ void sh_slot_rows_kernel(const int* __restrict__ perm, const int* __restrict__ sid_incl,
+                                    const int* __restrict__ upos, int n, int* __restrict__ idx) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int r = upos[sid_incl[i] - 1];
+  idx[perm[i]] = r < 0 ? 0 : r;
+}
+
+// Owner: rows[e] = {v[K], w, 0, 0, 0} of each requested id (zeros for padding entries)
+template <int K>
+__global__ void sh_serve_kernel(const int* __restrict__ recv_ids, int total, int N,
+                                const float* __restrict__ tv, const float* __restrict__ tw, long ldv,
+                                long ldw, float* __restrict__ rows) {
+  constexpr int LPS = K / 4, RW = K + 4;
+  const int gt = blockIdx.x * blockDim.x + threadIdx.x;
+  const int e = gt / LPS, sub = gt % LPS;
+  if (e >= total) return;
+  const int id = recv_ids[e];
+  f32x4 v = {0.f, 0.f, 0.f, 0.f};
+  float w = 0.f;
+  if (id >= 0) {
+    const size_t row = (size_t)(id / N);
+    v = *reinterpret_cast<const f32x4*>(tv + row * ldv + sub * 4);
+    if (sub == 0) w = tw[row * ldw];
+  }
+  float* o = rows + (size_t)e * RW;
+  *reinterpret_cast<f32x4*>(o + sub * 4) = v;
+  if (sub == 0) *reinterpret_cast<f32x4*>(o + K) = f32x4{w, 0.f, 0.f, 0.f};
+}
+
+__global__ void sh_owner_tag_kernel(const int* __restrict__ recv_ids, int total, int N, int C,
+                                    const int64_t* __restrict__ step,
+                                    unsigned long long* __restrict__ tags) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= total) return;
+  const int id = recv_ids[e];
+  if (id < 0) return;
+  const unsigned long long tag = (unsigned long long)(*step + 1) << 32;
+  tags[(size_t)(id / N) * N + e / C] = tag | (unsigned)(e % C);
+}
+
+// MODE 0: lazy optimizer OPT on the owner's row; 1: tf1_dense scatter into (Gv, Gw)
+template <int K, int MODE, int OPT>
+__global__ void sh_owner_apply_kernel(const int* __restrict__ recv_ids, int total, int N, int C,
+                                      const float* __restrict__ recv_g,
+                                      const unsigned long long* __restrict__ tags, float* tv, float* tw,
+                                      float* s0v, float* s1v, float* s0w, float* s1w, long ldv, long ldw,
+                                      float* Gv, float* Gw, OptHyper h, const int64_t* __restrict__ step) {
+  constexpr int LPS = K / 4, RW = K + 4;
+  const int gt = blockIdx.x * blockDim.x + threadIdx.x;
+  const int e = gt / LPS, sub = gt % LPS;
+  if (e >= total) return;
+  const int id = recv_ids[e];
+  if (id < 0) return;
+  const int p = e / C;
+  const size_t row = (size_t)(id / N);
+  const unsigned cur = (unsigned)(*step + 1);
+  const unsigned long long* tr = tags + row * N;
+  for (int q = 0; q < p; ++q)
+    if ((unsigned)(tr[q] >> 32) == cur) return;  // a lower rank also requested it: it leads
+  f32x4 g = {0.f, 0.f, 0.f, 0.f};
+  float gw = 0.f;
+  for (int q = p; q < N; ++q) {
+    const unsigned long long t = tr[q];
+    if ((unsigned)(t >> 32) != cur) continue;
+    const float* src = recv_g + ((size_t)q * C + (unsigned)t) * RW;
+    g += *reinterpret_cast<const f32x4*>(src + sub * 4);
+    gw += src[K];
+  }
+  if (MODE == 1) {
+    *reinterpret_cast<f32x4*>(Gv + row * K + sub * 4) = g;
+    if (sub == 0) Gw[row] = gw;
+    return;
+  }
+  const float lr_t = OPT == OPT_ADAM ? adam_lr_t(h, *step + 1) : h.lr;
+  const size_t o = row * ldv + sub * 4, ow = row * ldw;
+  f32x4 pv = *reinterpret_cast<const f32x4*>(tv + o);
+  f32x4 a = {0, 0, 0, 0}, c = {0, 0, 0, 0};
+  if (OPT != OPT_GD) a = *reinterpret_cast<const f32x4*>(s0v + o);
+  if (OPT == OPT_ADAM || OPT == OPT_FTRL) c = *reinterpret_cast<const f32x4*>(s1v + o);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    float gj = g[j] + h.l2 * pv[j];
+    float pj = pv[j], aj = a[j], cj = c[j];
+    opt_update<OPT>(pj, gj, aj, cj, h, lr_t);
+    pv[j] = pj;
+    a[j] = aj;
+    c[j] = cj;
+  }
+  *reinterpret_cast<f32x4*>(tv + o) = pv;
+  if (OPT != OPT_GD) *reinterpret_cast<f32x4*>(s0v + o) = a;
+  if (OPT == OPT_ADAM || OPT == OPT_FTRL) *reinterpret_cast<f32x4*>(s1v + o) = c;
+  if (sub == 0) {
+    float pw = tw[ow];
+    float g1 = gw + h.l2 * pw;
+    float aw = (OPT != OPT_GD) ? s0w[ow] : 0.f;
+    float cw = (OPT == OPT_ADAM || OPT == OPT_FTRL) ? s1w[ow] : 0.f;
+    opt_update<OPT>(pw, g1, aw, cw, h, lr_t);
+    tw[ow] = pw;
+    if (OPT != OPT_GD) s0w[ow] = aw;
+    if (OPT == OPT_ADAM || OPT == OPT_FTRL) s1w[ow] = cw;
+  }
+}
+
+// ------------------------------------------------------------------------------------ host API
+HFM_API int hfm_sh_count_blocks(int nmax) { return (nmax + SH_TILE - 1) / SH_TILE; }
+
+// ukeys/num_u: this rank's unique ids (sorted); nmax: host upper bound of U (= slots per step)
+HFM_API int hfm_sh_bucket(const int* ukeys, const int* num_u, int nmax, int N, int C, int* cnt_tmp,
+                          int* send_ids, int* upos, int* send_cnt, unsigned* err, hipStream_t st) {
+  if (N < 1 || N > SH_MAXN) return (int)hipErrorInvalidValue;
+  const int nb = hfm_sh_count_blocks(nmax);
+  int nbits = 0;
+  while ((1 << nbits) < N) ++nbits;
+  hipError_t e = hipMemsetAsync(send_ids, 0xFF, (size_t)N * C * sizeof(int), st);
+  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(sh_count_kernel, dim3(nb), dim3(SH_THREADS), 0, st, ukeys, num_u, N, cnt_tmp);
+  hipLaunchKernelGGL(sh_scatter_kernel, dim3(nb), dim3(SH_THREADS), 0, st, ukeys, num_u, N, nbits, C,
+                     cnt_tmp, nb, send_ids, upos, send_cnt, err);
+  HFM_LAUNCH_CHECK();
+}
+
+HFM_API int hfm_sh_slot_rows(const int* perm, const int* sid_incl, const int* upos, int n, int* idx,
+                             hipStream_t st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(sh_slot_rows_kernel, dim3((n + 255) / 256), dim3(256), 0, st, perm, sid_incl, upos,
+                     n, idx);
+  HFM_LAUNCH_CHECK();
+}
+
+#define HFM_K_DISPATCH(K, CALL) \
+  switch (K) {                  \
+    case 4: CALL(4); break;     \
+    case 8: CALL(8); break;     \
+    case 16: CALL(16); break;   \
+    case 32: CALL(32); break;   \
+    case 64: CALL(64); break;   \
+    default: return (int)hipErrorInvalidValue; \
+  }
+
+HFM_API int hfm_sh_serve(int K, const int* recv_ids, int total, int N, const float* tv, const float* tw,
+                         long ldv, long ldw, float* rows, hipStream_t st) {
+  const long th = (long)total * (K / 4);
+  const int grid = (int)((th + 255) / 256);
+  if (grid == 0) return 0;
+#define CALL(KK) hipLaunchKernelGGL(sh_serve_kernel<KK>, dim3(grid), dim3(256), 0, st, recv_ids, total, N, \
+                                    tv, tw, ldv, ldw, rows)
+  HFM_K_DISPATCH(K, CALL)
+#undef CALL
+  HFM_LAUNCH_CHECK();
+}
+
+struct ShApplyArgs {
+  const int* recv_ids;
+  int total, N, C, mode;
+  const float* recv_g;
+  unsigned long long* tags;
+  float *tv, *tw, *s0v, *s1v, *s0w, *s1w;
+  long ldv, ldw;
+  float *Gv, *Gw;
+  OptHyper h;
+  const int64_t* step;
+};
+
+template <int K>
+static int sh_apply_k(int opt, const ShApplyArgs& A, hipStream_t st) {
+  const long th = (long)A.total * (K / 4);
+  const int grid = (int)((th + 255) / 256);
+  hipLaunchKernelGGL(sh_owner_tag_kernel, dim3((A.total + 255) / 256), dim3(256), 0, st, A.recv_ids,
+                     A.total, A.N, A.C, A.step, A.tags);
+#define L_(M, O)                                                                                      \
+  hipLaunchKernelGGL((sh_owner_apply_kernel<K, M, O>), dim3(grid), dim3(256), 0, st, A.recv_ids, A.total, \
+                     A.N, A.C, A.recv_g, A.tags, A.tv, A.tw, A.s0v, A.s1v, A.s0w, A.s1w, A.ldv, A.ldw,  \
+                     A.Gv, A.Gw, A.h, A.step)
+  if (A.mode == 1) {
+    L_(1, 0);
+    return 0;
+  }
+  switch (opt) {
+    case OPT_ADAM: L_(0, OPT_ADAM); break;
+    case OPT_ADAGRAD: L_(0, OPT_ADAGRAD); break;
+    case OPT_MOMENTUM: L_(0, OPT_MOMENTUM); break;
+    case OPT_FTRL: L_(0, OPT_FTRL); break;
+    case OPT_GD: L_(0, OPT_GD); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+#undef L_
+  return 0;
+}
+
+// owner side of the backward: tag every received gradient row, then the lead requester of each
+// row sums all requesters' rows in rank order and applies the optimizer (mode 0) or scatters
+// into the tf1_dense gradient buffer (mode 1)
+HFM_API int hfm_sh_owner_apply(int K, int opt, const ShApplyArgs* A, hipStream_t st) {
+  if (A->total <= 0) return 0;
+  int rc = 0;
+#define CALL(KK) rc = sh_apply_k<KK>(opt, *A, st)
+  HFM_K_DISPATCH(K, CALL)
+#undef CALL
+  if (rc) return rc;
+  HFM_LAUNCH_CHECK();
+}
+HFM_API int hfm_sh_apply_args_bytes() { return (int)sizeof(ShApplyArgs); }

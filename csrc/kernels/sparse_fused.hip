@@ -44,18 +44,33 @@ struct SfArgs {
   int n, F, KP, row_div;
   float* ctail;  // [tiles][RS]
   float* lead;   // [tiles][RS]
-  int* tinfo;    // [tiles][2]: {headless, open-run key or -1}
+  int* tinfo;    // [tiles][4]: {headless, open-run key or -1, open-run head position, pad}
   float *tv, *tw, *s0v, *s1v, *s0w, *s1w;
   float *Gv, *Gw;
   OptHyper h;
   const int64_t* step;
   long ldv, ldw;  // table row strides (record layout: both = record floats)
+  // MODE 2 (row-sharded exchange): gradient row of unique u -> gout[upos[u]] ({g_v, g_w, 0, 0, 0}),
+  // V from the received rows (tv = rows_in, ldv = K + 4); u = sid[head position] - 1
+  const int* sid;
+  const int* upos;
+  float* gout;
 };
 
-// MODE 0: lazy optimizer OPT on the row; 1: tf1_dense scatter of the row gradient
+// MODE 0: lazy optimizer OPT on the row; 1: tf1_dense scatter of the row gradient;
+// 2: compact gradient row for the owner exchange
 template <int K, int MODE, int OPT>
-__device__ __forceinline__ void sf_apply_row(const SfArgs& A, int key, int sub, f32x4 a, float w, float c,
-                                             float lr_t) {
+__device__ __forceinline__ void sf_apply_row(const SfArgs& A, int key, int hpos, int sub, f32x4 a, float w,
+                                             float c, float lr_t) {
+  if (MODE == 2) {
+    const int r = A.upos[A.sid[hpos] - 1];
+    if (r < 0) return;  // capacity overflow (flagged by the bucketing kernel)
+    const f32x4 pv = *reinterpret_cast<const f32x4*>(A.tv + (size_t)r * A.ldv + sub * 4);
+    float* go = A.gout + (size_t)r * (K + 4);
+    *reinterpret_cast<f32x4*>(go + sub * 4) = a - pv * c;
+    if (sub == 0) *reinterpret_cast<f32x4*>(go + K) = f32x4{w, 0.f, 0.f, 0.f};
+    return;
+  }
   const size_t row = (size_t)(key / A.row_div);
   const size_t o = row * A.ldv + sub * 4;
   const size_t ow = row * A.ldw;
@@ -108,14 +123,14 @@ __global__ void __launch_bounds__(256) sf_tile_kernel(SfArgs A) {
   __shared__ int fh[T::NCH];  // offset of the first head in the chunk (CH: none)
   __shared__ int hl[T::TP];   // head positions, ascending
   __shared__ int wcount[4];
-  __shared__ int open_key_s;
+  __shared__ int open_key_s, open_pos_s;
   const int tile = blockIdx.x, b0 = tile * T::TP;
   const int nloc = min(T::TP, A.n - b0);
   const int nch = (nloc + CH - 1) / CH;
   const int tid = threadIdx.x, sub = tid % T::LPS, lane = tid & 63, wv = tid >> 6;
   const int prev_key = b0 > 0 ? A.sorted_keys[b0 - 1] : -1;
   const int next_key = (b0 + nloc < A.n) ? A.sorted_keys[b0 + nloc] : -1;
-  if (tid == 0) open_key_s = -1;
+  if (tid == 0) open_key_s = open_pos_s = -1;
   // 1. per-slot contributions
 #pragma unroll
   for (int ps = 0; ps < T::PASSES; ++ps) {
@@ -199,7 +214,7 @@ __global__ void __launch_bounds__(256) sf_tile_kernel(SfArgs A) {
       }
     }
     A.lead[(size_t)tile * T::RS + tid] = s;
-    if (tid == 0) A.tinfo[tile * 2] = any ? 0 : 1;
+    if (tid == 0) A.tinfo[tile * 4] = any ? 0 : 1;
   }
   // 3. finish every run headed in this tile
   const float lr_t = sf_lr_t<OPT>(A);
@@ -223,7 +238,7 @@ __global__ void __launch_bounds__(256) sf_tile_kernel(SfArgs A) {
       if (!closed) closed = (next_key != key);
     }
     if (closed) {
-      sf_apply_row<K, MODE, OPT>(A, key, sub, a, w, c, lr_t);
+      sf_apply_row<K, MODE, OPT>(A, key, b0 + hp, sub, a, w, c, lr_t);
     } else {
       float* ct = A.ctail + (size_t)tile * T::RS;
       *reinterpret_cast<f32x4*>(ct + sub * 4) = a;
@@ -231,11 +246,15 @@ __global__ void __launch_bounds__(256) sf_tile_kernel(SfArgs A) {
         ct[K] = w;
         ct[K + 1] = c;
         open_key_s = key;
+        open_pos_s = b0 + hp;
       }
     }
   }
   __syncthreads();
-  if (tid == 0) A.tinfo[tile * 2 + 1] = open_key_s;
+  if (tid == 0) {
+    A.tinfo[tile * 4 + 1] = open_key_s;
+    A.tinfo[tile * 4 + 2] = open_pos_s;
+  }
 }
 
 template <int K, int MODE, int OPT>
@@ -244,8 +263,9 @@ __global__ void __launch_bounds__(256) sf_carry_kernel(SfArgs A, int ntiles) {
   const int gt = blockIdx.x * blockDim.x + threadIdx.x;
   const int t = gt / T::LPS, sub = gt % T::LPS;
   if (t >= ntiles) return;
-  const int key = A.tinfo[t * 2 + 1];
+  const int key = A.tinfo[t * 4 + 1];
   if (key < 0) return;
+  const int hpos = A.tinfo[t * 4 + 2];
   const float* ct = A.ctail + (size_t)t * T::RS;
   f32x4 a = *reinterpret_cast<const f32x4*>(ct + sub * 4);
   float w = ct[K], c = ct[K + 1];
@@ -254,9 +274,9 @@ __global__ void __launch_bounds__(256) sf_carry_kernel(SfArgs A, int ntiles) {
     a += *reinterpret_cast<const f32x4*>(ld + sub * 4);
     w += ld[K];
     c += ld[K + 1];
-    if (!A.tinfo[t2 * 2]) break;
+    if (!A.tinfo[t2 * 4]) break;
   }
-  sf_apply_row<K, MODE, OPT>(A, key, sub, a, w, c, sf_lr_t<OPT>(A));
+  sf_apply_row<K, MODE, OPT>(A, key, hpos, sub, a, w, c, sf_lr_t<OPT>(A));
 }
 
 HFM_API int hfm_sparse_fused_tiles(int K, int n) {
@@ -275,8 +295,9 @@ static void sf_launch(const SfArgs& A, hipStream_t st) {
 
 template <int K>
 static int sf_dispatch(int mode, int opt, const SfArgs& A, hipStream_t st) {
-  if (mode == 1) {
-    sf_launch<K, 1, 0>(A, st);
+  if (mode == 1 || mode == 2) {
+    if (mode == 1) sf_launch<K, 1, 0>(A, st);
+    else sf_launch<K, 2, 0>(A, st);
     return 0;
   }
   switch (opt) {
@@ -290,7 +311,8 @@ static int sf_dispatch(int mode, int opt, const SfArgs& A, hipStream_t st) {
   return 0;
 }
 
-// mode 0: lazy optimizer `opt` on every unique row; 1: tf1_dense scatter into (Gv, Gw)
+// mode 0: lazy optimizer `opt` on every unique row; 1: tf1_dense scatter into (Gv, Gw);
+// 2: gradient rows for the row-sharded owner exchange (gout[upos[u]])
 HFM_API int hfm_sparse_fused(int K, int mode, int opt, const SfArgs* A, hipStream_t st) {
   if (A->n <= 0) return 0;
   int rc;

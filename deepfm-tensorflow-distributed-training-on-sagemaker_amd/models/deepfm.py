@@ -258,6 +258,8 @@ class NativeDeepFM:
         self.h_dense = KN.hyper(self.lr, 0.0, eps=adam_epsilon)
         self._bufs_M = 0
         self._side = None
+        self._comm_stream = None
+        self.shx = None
         self.batch_size = int(batch_size)
         # fused deep tower (csrc/kernels/tower.hip): whole forward + head + dgrad chain in one
         # launch per 32-sample block; batch norm (needs batch-wide statistics between the
@@ -381,7 +383,7 @@ class NativeDeepFM:
         nt = KN.sparse_fused_tiles(K, n)
         self.sf_ctail = torch.zeros(nt, K + 4, **f32)
         self.sf_lead = torch.zeros(nt, K + 4, **f32)
-        self.sf_tinfo = torch.zeros(nt, 2, **i32)
+        self.sf_tinfo = torch.zeros(nt, 4, **i32)
         self.fs_err = torch.zeros(1, **i32)
         self._fs_ranges = None
         if self.field_ranges is not None:
@@ -394,6 +396,12 @@ class NativeDeepFM:
         if self.fused:
             self._build_wgrad_jobs()
         self._bufs_M = M
+        self.shx = None
+        if self.sharded and getattr(self.comm, "engine", None) is not None:
+            from ..parallel.sharded import FixedCapacityExchange
+            old = getattr(self, "_shx_tags", None)
+            self.shx = FixedCapacityExchange(self, self.comm.engine, self.comm.capacity, tags=old)
+            self._shx_tags = self.shx.tags
         self._own_in = (self.idx, self.vals, self.labels)
         self._graphs = {}
         self.max_graphs = 256
@@ -594,7 +602,9 @@ class NativeDeepFM:
         M, F, K = self.M, self.F, self.K
         idx = self.idx
         tv, tw = self.tv, self.tw
-        if self.sharded:
+        if self.shx is not None:
+            idx, tv, tw = self.shx.forward(B)
+        elif self.sharded:
             idx, tv, tw = self.comm.sharded_forward_gather(self, B)
         fm_bias = self.p[self.dense_segs["fm_bias"].off:]
         KN.fm_fwd(idx, self.vals, tv, tw, fm_bias, M, F, K, self.K0p, self.y_fm, self.S, self.E,
@@ -782,6 +792,9 @@ class NativeDeepFM:
         if self._fs_ranges is not None and int(self.fs_err.item()) != 0:
             raise RuntimeError("an id lies outside its field's declared range (field_ranges): "
                                "the per-field sort is invalid for this data")
+        if self.shx is not None and self.shx.error() != 0:
+            raise RuntimeError(f"row-sharded exchange: a rank sent more than capacity={self.shx.C} "
+                               "unique ids to one owner (raise the capacity)")
 
     def sf_args(self, n: int) -> SfArgs:
         A = SfArgs()
@@ -803,6 +816,9 @@ class NativeDeepFM:
         """Embedding backward.  Single rank: the row update is fused into the reduction
         (returns None).  Multi-rank: returns compact unique-row gradients for the exchange."""
         n = B * self.F
+        if self.shx is not None:
+            self.shx.backward(B)
+            return None
         if self.sharded:
             return self.comm.sharded_backward(self, B, idx, tv)
         if not presorted:
@@ -866,11 +882,22 @@ class NativeDeepFM:
         if presorted:
             main.wait_stream(self._side)
         work = None
-        if self.exchange:
+        eng = getattr(self.comm, "engine_dense", None) if self.exchange else None
+        if eng is not None:
+            # dense bucket all-reduce on a side stream, overlapped with the sparse exchange
+            main = torch.cuda.current_stream(self.device)
+            if self._comm_stream is None:
+                self._comm_stream = torch.cuda.Stream(self.device)
+            self._comm_stream.wait_stream(main)
+            with torch.cuda.stream(self._comm_stream):
+                eng.allreduce_(self.g)
+        elif self.exchange:
             work = self.comm.allreduce_dense_async(self.g)
         out = self._sparse_backward(B, idx, tv, presorted=presorted)
         if out is not None:
             self._sparse_update(*out)
+        if eng is not None:
+            main.wait_stream(self._comm_stream)
         if work is not None:
             self.comm.wait(work)
         if _SEPARATE_STEP_INC:

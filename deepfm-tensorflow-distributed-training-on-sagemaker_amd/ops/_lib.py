@@ -83,7 +83,16 @@ class SfArgs(C.Structure):
                 ("row_div", c_int), ("ctail", c_void_p), ("lead", c_void_p), ("tinfo", c_void_p),
                 ("tv", c_void_p), ("tw", c_void_p), ("s0v", c_void_p), ("s1v", c_void_p),
                 ("s0w", c_void_p), ("s1w", c_void_p), ("Gv", c_void_p), ("Gw", c_void_p),
-                ("h", OptHyper), ("step", c_void_p), ("ldv", c_long), ("ldw", c_long)]
+                ("h", OptHyper), ("step", c_void_p), ("ldv", c_long), ("ldw", c_long),
+                ("sid", c_void_p), ("upos", c_void_p), ("gout", c_void_p)]
+
+
+class ShApplyArgs(C.Structure):
+    _fields_ = [("recv_ids", c_void_p), ("total", c_int), ("N", c_int), ("C", c_int), ("mode", c_int),
+                ("recv_g", c_void_p), ("tags", c_void_p), ("tv", c_void_p), ("tw", c_void_p),
+                ("s0v", c_void_p), ("s1v", c_void_p), ("s0w", c_void_p), ("s1w", c_void_p),
+                ("ldv", c_long), ("ldw", c_long), ("Gv", c_void_p), ("Gw", c_void_p), ("h", OptHyper),
+                ("step", c_void_p)]
 
 
 TW_MAXL = 8
@@ -149,6 +158,18 @@ _SIGS = {
     "hfm_onesweep_sort_ids": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_size_t, c_void_p],
     "hfm_onesweep_error_offset": [],
     "hfm_field_sort_max_rows": [],
+    "hfm_comm_id_bytes": [],
+    "hfm_comm_unique_id": [c_void_p],
+    "hfm_comm_init": [C.POINTER(c_void_p), c_int, c_int, c_void_p],
+    "hfm_comm_destroy": [c_void_p],
+    "hfm_comm_allreduce_f32": [c_void_p, c_void_p, c_size_t, c_void_p],
+    "hfm_comm_alltoall": [c_void_p, c_void_p, c_void_p, c_size_t, c_void_p],
+    "hfm_sh_count_blocks": [c_int],
+    "hfm_sh_bucket": [c_void_p, c_void_p, c_int, c_int, c_int] + [c_void_p] * 5 + [c_void_p],
+    "hfm_sh_slot_rows": [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p],
+    "hfm_sh_serve": [c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_long, c_long, c_void_p, c_void_p],
+    "hfm_sh_owner_apply": [c_int, c_int, c_void_p, c_void_p],
+    "hfm_sh_apply_args_bytes": [],
     "hfm_sparse_fused_tiles": [c_int, c_int],
     "hfm_sparse_fused": [c_int, c_int, c_int, c_void_p, c_void_p],
     "hfm_sparse_fused_args_bytes": [],
@@ -198,7 +219,8 @@ def get_lib():
                            ("hfm_shadow_seg_bytes", ShadowSeg), ("hfm_opt_hyper_bytes", OptHyper),
                            ("hfm_seg_apply_args_bytes", SegApplyArgs), ("hfm_bn_args_bytes", BnArgs),
                            ("hfm_tower_args_bytes", TowerArgs), ("hfm_wg_job_bytes", WgJob),
-                           ("hfm_sparse_fused_args_bytes", SfArgs)):
+                           ("hfm_sparse_fused_args_bytes", SfArgs),
+                           ("hfm_sh_apply_args_bytes", ShApplyArgs)):
             n = getattr(lib, cname)()
             if n != C.sizeof(pys):
                 raise RuntimeError(f"ABI mismatch {pys.__name__}: C {n} vs ctypes {C.sizeof(pys)}")

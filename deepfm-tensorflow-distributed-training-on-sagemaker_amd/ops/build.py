@@ -77,7 +77,9 @@ def build_kernels(force: bool = False, jobs: int = 8, verbose: bool = False) -> 
             list(ex.map(comp, todo))
     if force or todo or _newer(objs, KERNELS_SO):
         tmp = KERNELS_SO + ".tmp"
-        _run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs)
+        # librccl.so.1 resolves to the RCCL PyTorch already loaded (same SONAME) at run time
+        _run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs +
+             ["-L/opt/rocm/lib", "-lrccl"])
         os.replace(tmp, KERNELS_SO)
     return KERNELS_SO
 

@@ -12,7 +12,7 @@ from typing import List, Optional, Sequence
 import torch
 
 from . import _lib
-from ._lib import (BnArgs, EpiArgs, HeadArgs, TowerArgs, WgJob, OptHyper, RowSumJob, SegApplyArgs, SfArgs, ShadowSeg, SlabJob, check,
+from ._lib import (BnArgs, EpiArgs, HeadArgs, TowerArgs, WgJob, OptHyper, RowSumJob, SegApplyArgs, SfArgs, ShApplyArgs, ShadowSeg, SlabJob, check,
                    ptr, stream_handle)
 
 EPI_F32, EPI_FWD, EPI_DGRAD, EPI_FWD_EVAL, EPI_RELU_F32 = 0, 1, 2, 3, 4
@@ -162,7 +162,7 @@ def fm_bwd_seg(K, sorted_keys, perm, sid_incl, vals, dlogit, dX0, S, n, F, KP, p
 SEG_LAZY, SEG_SCATTER, SEG_WRITE_UG = 0, 1, 2
 
 
-SF_LAZY, SF_SCATTER = 0, 1
+SF_LAZY, SF_SCATTER, SF_EXCHANGE = 0, 1, 2
 
 
 def sparse_fused_tiles(K: int, n: int) -> int:
@@ -288,3 +288,56 @@ def struct_array_to_device(structs: Sequence[C.Structure], device) -> torch.Tens
         C.memmove(C.addressof(buf) + i * sz, C.addressof(s), sz)
     host = torch.frombuffer(bytearray(buf), dtype=torch.uint8)
     return host.to(device)
+
+
+# ------------------------------------------------------------------ RCCL engine (comm.hip)
+def comm_unique_id() -> bytes:
+    n = int(L().hfm_comm_id_bytes())
+    buf = (C.c_char * n)()
+    check(L().hfm_comm_unique_id(buf), "comm_unique_id")
+    return bytes(buf)
+
+
+def comm_init(nranks: int, rank: int, uid: bytes) -> int:
+    h = C.c_void_p()
+    buf = (C.c_char * len(uid)).from_buffer_copy(uid)
+    check(L().hfm_comm_init(C.byref(h), nranks, rank, buf), "comm_init")
+    return int(h.value)
+
+
+def comm_destroy(h: int):
+    check(L().hfm_comm_destroy(h), "comm_destroy")
+
+
+def comm_allreduce_(h: int, t: torch.Tensor):
+    assert t.dtype == torch.float32 and t.is_contiguous()
+    check(L().hfm_comm_allreduce_f32(h, ptr(t), t.numel(), stream_handle()), "comm_allreduce")
+
+
+def comm_alltoall(h: int, send: torch.Tensor, recv: torch.Tensor, bytes_per_peer: int):
+    assert send.is_contiguous() and recv.is_contiguous()
+    check(L().hfm_comm_alltoall(h, ptr(send), ptr(recv), bytes_per_peer, stream_handle()), "comm_alltoall")
+
+
+# ------------------------------------------------------------------ row-sharded exchange (shard.hip)
+def sh_count_blocks(nmax: int) -> int:
+    return int(L().hfm_sh_count_blocks(nmax))
+
+
+def sh_bucket(ukeys, num_u, nmax, N, Cap, cnt_tmp, send_ids, upos, send_cnt, err):
+    check(L().hfm_sh_bucket(ptr(ukeys), ptr(num_u), nmax, N, Cap, ptr(cnt_tmp), ptr(send_ids), ptr(upos),
+                            ptr(send_cnt), ptr(err), stream_handle()), "sh_bucket")
+
+
+def sh_slot_rows(perm, sid_incl, upos, n, idx):
+    check(L().hfm_sh_slot_rows(ptr(perm), ptr(sid_incl), ptr(upos), n, ptr(idx), stream_handle()),
+          "sh_slot_rows")
+
+
+def sh_serve(K, recv_ids, total, N, tv, tw, rows):
+    check(L().hfm_sh_serve(K, ptr(recv_ids), total, N, ptr(tv), ptr(tw), *_ld(tv, tw), ptr(rows),
+                           stream_handle()), "sh_serve")
+
+
+def sh_owner_apply(K, opt, args: ShApplyArgs):
+    check(L().hfm_sh_owner_apply(K, opt, C.byref(args), stream_handle()), "sh_owner_apply")

@@ -39,6 +39,8 @@ def init_distributed(backend: Optional[str] = None, timeout_s: int = 600):
         return
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29500")
+    os.environ.setdefault("RANK", "0")               # single-process runs (tests, --force_exchange)
+    os.environ.setdefault("WORLD_SIZE", "1")
     if backend is None:
         backend = "nccl" if torch.cuda.is_available() else "gloo"
     kw = dict(backend=backend, timeout=datetime.timedelta(seconds=timeout_s))
@@ -56,21 +58,36 @@ def world_info():
 class Comm:
     """Collective engine used by NativeDeepFM for one process group."""
 
-    def __init__(self, sharded: bool = True, group=None, force_exchange: bool = False):
+    def __init__(self, sharded: bool = True, group=None, force_exchange: bool = False,
+                 native: Optional[bool] = None, capacity: Optional[int] = None):
         self.group = group
         self.rank = dist.get_rank(group)
         self.world_size = dist.get_world_size(group)
         # force_exchange: run the multi-rank code path even on a 1-rank group (tests on 1 GPU)
         self.force_exchange = bool(force_exchange)
         self.sharded = bool(sharded) and (self.world_size > 1 or self.force_exchange)
-        # steps with host-synchronous routing (variable all-to-all splits) cannot be graphed
-        self.graph_safe = self.world_size == 1 and not self.force_exchange
         self.router = Router(self.world_size, self.rank, group)
         self._bytes = 0
+        # native RCCL engine (csrc/kernels/comm.hip): fixed-capacity all-to-alls + dense
+        # all-reduce issued on our streams -> no host sync, graph-capturable step.  Two
+        # communicators: the dense all-reduce runs on a side stream concurrently with the
+        # sparse exchange, and one communicator must not carry concurrent operations.
+        if native is None:
+            native = (dist.get_backend(group) == "nccl" and self.sharded and
+                      os.environ.get("HIPFM_SHARD_EXCHANGE", "fixed") == "fixed")
+        self.engine = self.engine_dense = None
+        self.capacity = capacity
+        if native:
+            from .sharded import RcclEngine
+            self.engine = RcclEngine(group)
+            self.engine_dense = RcclEngine(group)
+        # steps with host-synchronous routing (variable all-to-all splits) cannot be graphed
+        self.graph_safe = (self.world_size == 1 and not self.force_exchange) or self.engine is not None
 
     @property
     def bytes_sent(self) -> int:
-        return self._bytes + self.router.bytes_sent
+        eng = sum(e.bytes_sent for e in (self.engine, self.engine_dense) if e is not None)
+        return self._bytes + self.router.bytes_sent + eng
 
     @bytes_sent.setter
     def bytes_sent(self, v: int):
