@@ -1,27 +1,33 @@
-// Field-partitioned slot-id sort: ONE launch, one workgroup per field, sorted entirely in LDS
-// (SURVEY §2.5 row 19, K3 — the "Unique + UnsortedSegmentSum" of TF1's sparse apply needs the
-// B*F slot ids grouped by id, deterministically).
+// Field-partitioned slot-id sort (SURVEY §2.5 row 19, K3 — the "Unique + UnsortedSegmentSum"
+// of TF1's sparse apply needs the B*F slot ids grouped by id, deterministically).
 //
 // CTR data gives every field its own id range (Criteo: 13 integer fields + 26 categorical
 // vocabularies; the reference's libsvm ids, PS:74, and the per-field hashing behind
 // feature_size).  When the ranges [lo_f, hi_f) are disjoint and increasing in f, the globally
-// sorted slot list is the concatenation of F per-field sorted lists, each of only B keys of
-// ceil(log2(hi_f - lo_f)) bits.  So instead of 4 global LSD passes over n = B*F keys (6 launches,
-// each pass a decoupled look-back across the whole chip), each field is sorted by one 1024-thread
-// workgroup holding its B <= 16384 (key, row) pairs in 128 KB of LDS:
+// sorted slot list is the concatenation of F per-field sorted lists of B keys of
+// bits_f = ceil(log2(hi_f - lo_f)) bits each.  Instead of 4 global LSD passes over n = B*F keys
+// (6 launches, each pass a decoupled look-back across the chip), two launches sort everything:
 //
-//   * single-id fields (Criteo's integer fields: one id each) are written out directly;
-//   * other fields run ceil(bits / 8) stable LSD passes of 8-bit digits in LDS.  Item k of lane l
-//     of wave w is element w*64*IT + k*64 + l, so (w, k, l) order is input order.  A lane's rank
-//     among same-digit lanes of its wave comes from 8 ballots; running per-digit counts live in the
-//     wave's own LDS row (no block barrier inside the ranking loop); one barrier then turns the 16
-//     wave rows into wave-exclusive digit offsets.  Rows beyond B carry the all-ones sentinel
-//     (every digit 255) and, being last in input order, stay last.
+//   fs_transpose: ids [B, F] -> field-major [F, B] (coalesced reads for every field's workgroups)
+//   fs_sort:      field f is split into P_f = 2^pb_f MSD partitions by the top pb_f key bits
+//                 (pb_f = min(bits_f, max_pb), chosen by the host); one 1024-thread workgroup per
+//                 (field, partition):
+//       1. reads all B keys of the field, counts the keys of lower partitions (= its output
+//          offset) and stably compacts its own keys into LDS (ballot ranks, wave order);
+//       2. sorts its m keys by the remaining bits_f - pb bits with stable LSD passes of 8-bit
+//          digits in LDS: a lane's rank among same-digit lanes of its wave from 8 ballots, running
+//          per-digit counts in the wave's own LDS row, one barrier to turn the 16 wave rows into
+//          wave-exclusive offsets.  The m keys are striped over all 16 waves (csz = m/16 rounded
+//          up to 64), so a partition of 1K keys costs each wave one 64-key step per pass;
+//       3. writes its run at the partition offset.
+// Ballot ranking is VALU-bound (~10 instructions per key bit), so spreading a field over 16
+// CUs instead of one is what makes the sort fast when it is on the critical path (the multi-GPU
+// step, max_pb = 4: 405 workgroups at the Criteo-1TB shape); when it runs on a side stream
+// concurrently with the forward (single GPU), max_pb = 0 keeps it on 39 CUs so the tower keeps
+// the rest of the chip.  Single-id fields (Criteo's integer fields) need no ranking at all.
 //
-// The output is bit-identical to the stable global sort (ties keep slot order b*F+f, i.e. row
-// order within a field), so every downstream kernel and test is unchanged.  An id outside its
-// field's declared range sets *err (the host raises on it): the concatenation would then not be
-// globally sorted.
+// Output is bit-identical to the stable global sort (ties keep row order b, i.e. slot order
+// b*F+f).  An id outside its field's declared range sets *err (the host raises on it).
 #include "common.h"
 
 namespace {
@@ -29,30 +35,56 @@ constexpr int FS_THREADS = 1024;
 constexpr int FS_WAVES = FS_THREADS / 64;
 constexpr int FS_IT = 16;
 constexpr int FS_MAXB = FS_THREADS * FS_IT;  // rows per field
-constexpr int FS_LDS = (2 * FS_MAXB + FS_WAVES * 256 + 256 + 16) * 4;
+constexpr int FS_PBMAX = 4;                   // up to 16 partitions per field
+constexpr int FS_LDS = (2 * FS_MAXB + FS_WAVES * 256 + 256 + 64) * 4;
 }  // namespace
 
-// fr: per field {lo, hi, bits}
-__global__ void __launch_bounds__(FS_THREADS) field_sort_kernel(const int* __restrict__ ids, int B, int F,
-                                                               const int* __restrict__ fr,
-                                                               int* __restrict__ sorted_keys,
-                                                               int* __restrict__ perm,
-                                                               unsigned* __restrict__ err) {
+__global__ void __launch_bounds__(256) fs_transpose_kernel(const int* __restrict__ ids, int B, int F,
+                                                          int* __restrict__ idsT) {
+  __shared__ int t[64][65];
+  const int b0 = blockIdx.x * 64;
+  const int nb = min(64, B - b0);
+  for (int f0 = 0; f0 < F; f0 += 64) {
+    const int nf = min(64, F - f0);
+    for (int e = threadIdx.x; e < nb * nf; e += 256) {
+      const int b = e / nf, f = e - b * nf;
+      t[f][b] = ids[(size_t)(b0 + b) * F + f0 + f];
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < nb * nf; e += 256) {
+      const int f = e / nb, b = e - f * nb;
+      idsT[(size_t)(f0 + f) * B + b0 + b] = t[f][b];
+    }
+    __syncthreads();
+  }
+}
+
+// fr: per field {lo, hi, bits, pb}; work: per workgroup {field, partition}
+__global__ void __launch_bounds__(FS_THREADS) fs_sort_kernel(const int* __restrict__ idsT, int B, int F,
+                                                            const int* __restrict__ fr,
+                                                            const int* __restrict__ work,
+                                                            int* __restrict__ sorted_keys,
+                                                            int* __restrict__ perm,
+                                                            unsigned* __restrict__ err) {
   extern __shared__ __align__(16) unsigned char fs_lds_raw[];
   unsigned* lk = reinterpret_cast<unsigned*>(fs_lds_raw);  // [FS_MAXB]
   unsigned* lv = lk + FS_MAXB;                              // [FS_MAXB]
   unsigned* wc = lv + FS_MAXB;                              // [FS_WAVES][256]
   unsigned* dbase = wc + FS_WAVES * 256;                    // [256]
-  unsigned* wsum = dbase + 256;                             // [4]
-  const int f = blockIdx.x;
-  const int lo = fr[3 * f], hi = fr[3 * f + 1], bits = fr[3 * f + 2];
+  unsigned* wsum = dbase + 256;                             // [16]
+  unsigned* wlow = wsum + 16;                               // [16]
+  const int f = work[2 * blockIdx.x], part = work[2 * blockIdx.x + 1];
+  const int lo = fr[4 * f], hi = fr[4 * f + 1], bits = fr[4 * f + 2], pb = fr[4 * f + 3];
+  const int rb = bits - pb;  // bits sorted inside the partition
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const unsigned long long lt = (1ull << lane) - 1ull;
   int* sko = sorted_keys + (size_t)f * B;
   int* pko = perm + (size_t)f * B;
+  const int* src = idsT + (size_t)f * B;
   bool bad = false;
   if (bits == 0) {
     for (int b = tid; b < B; b += FS_THREADS) {
-      const int id = ids[(size_t)b * F + f];
+      const int id = src[b];
       bad |= id != lo;
       sko[b] = id;
       pko[b] = b * F + f;
@@ -60,29 +92,85 @@ __global__ void __launch_bounds__(FS_THREADS) field_sort_kernel(const int* __res
     if (__any(bad) && lane == 0) atomicOr(err, 1u);
     return;
   }
+  // ---- 1. partition: count lower partitions, stably compact this partition's keys
   const int base = wv * 64 * FS_IT;
-  unsigned key[FS_IT], val[FS_IT];
+  unsigned key[FS_IT];
+  unsigned mine_bits = 0;
+  unsigned my_cnt = 0, low_cnt = 0;
 #pragma unroll
   for (int k = 0; k < FS_IT; ++k) {
     const int p = base + k * 64 + lane;
-    val[k] = (unsigned)p;
-    key[k] = 0xFFFFFFFFu;
+    key[k] = 0u;
+    int kp = 1 << 30;
     if (p < B) {
-      const int id = ids[(size_t)p * F + f];
+      const int id = src[p];
       bad |= (id < lo) | (id >= hi);
       key[k] = (unsigned)(id - lo) & ((1u << bits) - 1u);
+      kp = (int)(key[k] >> rb);
     }
+    const unsigned long long bm = __ballot(kp == part);
+    const unsigned long long bl = __ballot(kp < part);
+    if (kp == part) mine_bits |= 1u << k;
+    my_cnt += (unsigned)__popcll(bm);
+    low_cnt += (unsigned)__popcll(bl);
   }
   if (__any(bad) && lane == 0) atomicOr(err, 1u);
-  const unsigned long long lt = (1ull << lane) - 1ull;
+  if (lane == 0) {
+    wsum[wv] = my_cnt;
+    wlow[wv] = low_cnt;
+  }
+  __syncthreads();
+  unsigned woff = 0, m = 0, out_base = 0;
+  for (int w = 0; w < FS_WAVES; ++w) {
+    const unsigned c = wsum[w];
+    if (w < wv) woff += c;
+    m += c;
+    out_base += wlow[w];
+  }
+  {
+    unsigned run = woff;
+#pragma unroll
+    for (int k = 0; k < FS_IT; ++k) {
+      const bool mine = (mine_bits >> k) & 1u;
+      const unsigned long long bm = __ballot(mine);
+      if (mine) {
+        const unsigned q = run + (unsigned)__popcll(bm & lt);
+        lk[q] = key[k] & ((1u << rb) - 1u);
+        lv[q] = (unsigned)(base + k * 64 + lane);
+      }
+      run += (unsigned)__popcll(bm);
+    }
+  }
+  __syncthreads();
+  // ---- 2. LSD passes over the rb low bits; the m keys striped over all waves
+  const int csz = (((int)m + FS_WAVES * 64 - 1) / (FS_WAVES * 64)) * 64;  // keys per wave (x64)
+  const int its = csz / 64;
+  const int wb = wv * csz;
+  unsigned val[FS_IT];
+  {
+    const unsigned* lkp = lk + wb + lane;
+    const unsigned* lvp = lv + wb + lane;
+#pragma unroll
+    for (int k = 0; k < FS_IT; ++k) {
+      const bool in = k < its && wb + k * 64 + lane < (int)m;
+      key[k] = in ? lkp[k * 64] : 0xFFFFFFFFu;
+      val[k] = in ? lvp[k * 64] : 0u;
+    }
+  }
   unsigned* wh = wc + wv * 256;
-  const int passes = (bits + 7) >> 3;
+#ifdef FS_DEBUG_MAX_PASSES  // timing harness only (tools/fsbench): cap the LSD passes
+  const int passes = min((rb + 7) >> 3, FS_DEBUG_MAX_PASSES);
+#else
+  const int passes = (rb + 7) >> 3;
+#endif
   for (int pass = 0; pass < passes; ++pass) {
     const int shift = pass * 8;
+    __syncthreads();  // everyone's previous reloads are done before the LDS arrays are rewritten
 #pragma unroll
     for (int d = lane; d < 256; d += 64) wh[d] = 0u;
 #pragma unroll
     for (int k = 0; k < FS_IT; ++k) {
+      if (k >= its) break;  // wave-uniform
       const unsigned d = (key[k] >> shift) & 255u;
       unsigned long long peers = ~0ull;
 #pragma unroll
@@ -93,12 +181,12 @@ __global__ void __launch_bounds__(FS_THREADS) field_sort_kernel(const int* __res
       }
       const unsigned rk = (unsigned)__popcll(peers & lt);
       const unsigned old = wh[d];  // a wave's LDS ops execute in order: every lane reads before
-      val[k] |= (old + rk) << 16;  // the leader's update below lands.  rank < 1024, row < 2^16
-      if (rk == 0) wh[d] = old + (unsigned)__popcll(peers);
+      val[k] |= (old + rk) << 16;  // the update below lands (all peers store the same value).
+      wh[d] = old + (unsigned)__popcll(peers);  // rank < 1024, row < 2^16
     }
     __syncthreads();
     unsigned tot = 0, x = 0;
-    if (tid < 256) {  // digit tid: wave-exclusive offsets, tile total
+    if (tid < 256) {  // digit tid: wave-exclusive offsets, total
 #pragma unroll
       for (int w = 0; w < FS_WAVES; ++w) {
         const unsigned c = wc[w * 256 + tid];
@@ -122,6 +210,7 @@ __global__ void __launch_bounds__(FS_THREADS) field_sort_kernel(const int* __res
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < FS_IT; ++k) {
+      if (k >= its) break;
       const unsigned d = (key[k] >> shift) & 255u;
       const unsigned p = dbase[d] + wh[d] + (val[k] >> 16);
       lk[p] = key[k];
@@ -129,36 +218,42 @@ __global__ void __launch_bounds__(FS_THREADS) field_sort_kernel(const int* __res
     }
     __syncthreads();
     {
-      // one base address per array + immediate offsets (lv sits 64 KB in: beyond the DS offset
-      // field, so per-item addresses would otherwise be hoisted into 16 registers and spilled)
-      const unsigned* lkp = lk + base + lane;
-      const unsigned* lvp = lv + base + lane;
+      const unsigned* lkp = lk + wb + lane;
+      const unsigned* lvp = lv + wb + lane;
 #pragma unroll
       for (int k = 0; k < FS_IT; ++k) {
+        if (k >= its) break;
         key[k] = lkp[k * 64];
         val[k] = lvp[k * 64];
       }
     }
   }
+  // ---- 3. write the partition's run (sentinels sort last, so [0, m) are the real keys)
+  const int kbase = lo + (part << rb);
 #pragma unroll
   for (int k = 0; k < FS_IT; ++k) {
-    const int p = base + k * 64 + lane;
-    if (p < B) {
-      sko[p] = lo + (int)key[k];
-      pko[p] = (int)val[k] * F + f;
+    if (k >= its) break;
+    const int q = wb + k * 64 + lane;
+    if (q < (int)m) {
+      sko[out_base + q] = kbase + (int)key[k];
+      pko[out_base + q] = (int)(val[k] & 0xFFFFu) * F + f;
     }
   }
 }
 
 HFM_API int hfm_field_sort_max_rows() { return FS_MAXB; }
 
-// ids: [B, F] int32 (row-major slots); fr_dev: [F][3] {lo, hi, bits} on the device; outputs are
-// the n = B*F sorted keys and their slot positions (field f occupies [f*B, (f+1)*B)).
-HFM_API int hfm_field_sort(const int* ids, int B, int F, const int* fr_dev, int* sorted_keys, int* perm,
-                           unsigned* err, hipStream_t st) {
+HFM_API int hfm_field_sort_max_pb() { return FS_PBMAX; }
+
+// ids: [B, F] int32 (row-major slots); fr_dev: [F][4] {lo, hi, bits, pb}; work_dev: [nwork][2]
+// {field, partition}; idsT: [F, B] scratch.  Outputs: the n = B*F sorted keys and their slot
+// positions (field f occupies [f*B, (f+1)*B)).
+HFM_API int hfm_field_sort(const int* ids, int B, int F, const int* fr_dev, const int* work_dev, int nwork,
+                           int* idsT, int* sorted_keys, int* perm, unsigned* err, hipStream_t st) {
   if (B <= 0 || F <= 0) return 0;
   if (B > FS_MAXB) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(field_sort_kernel, dim3(F), dim3(FS_THREADS), FS_LDS, st, ids, B, F, fr_dev,
-                     sorted_keys, perm, err);
+  hipLaunchKernelGGL(fs_transpose_kernel, dim3((B + 63) / 64), dim3(256), 0, st, ids, B, F, idsT);
+  hipLaunchKernelGGL(fs_sort_kernel, dim3(nwork), dim3(FS_THREADS), FS_LDS, st, idsT, B, F, fr_dev,
+                     work_dev, sorted_keys, perm, err);
   HFM_LAUNCH_CHECK();
 }

@@ -384,12 +384,12 @@ class NativeDeepFM:
         self.sf_ctail = torch.zeros(nt, K + 4, **f32)
         self.sf_lead = torch.zeros(nt, K + 4, **f32)
         self.sf_tinfo = torch.zeros(nt, 4, **i32)
-        self.fs_err = torch.zeros(1, **i32)
-        self._fs_ranges = None
+        self._fsort = None
         if self.field_ranges is not None:
-            fr = [(lo, hi, int(math.ceil(math.log2(hi - lo))) if hi - lo > 1 else 0)
-                  for lo, hi in self.field_ranges]
-            self._fs_ranges = torch.tensor(fr, dtype=torch.int32).reshape(-1).to(dev)
+            # on the single-GPU step the sort overlaps the forward on a side stream: one workgroup
+            # per field; on the sharded step it gates the row exchange: 16-way MSD split per field
+            self._fsort = KN.FieldSort(self.field_ranges, min(M, KN.field_sort_max_rows()), dev,
+                                       max_pb=4 if self.sharded else 0)
         tb = max(KN.radix_temp_bytes(n), KN.rbk_temp_bytes(K, n), KN.scan_temp_bytes(n))
         self.temp = torch.zeros(tb + 256, dtype=torch.uint8, device=dev)
         self._build_finalize_jobs()
@@ -775,21 +775,20 @@ class NativeDeepFM:
         return A
 
     def uses_field_sort(self, B: int) -> bool:
-        return (self._fs_ranges is not None and _SORT_MODE != "global" and
-                B <= KN.field_sort_max_rows())
+        return (self._fsort is not None and _SORT_MODE != "global" and B <= self._fsort.max_rows)
 
     def _sort_slots(self, B: int):
         """Stable sort of the B*F slot ids -> (sorted_keys, perm): one per-field LDS launch when
         the field id ranges are known, else the global radix sort."""
         n = B * self.F
         if self.uses_field_sort(B):
-            KN.field_sort(self.idx, B, self.F, self._fs_ranges, self.sorted_keys, self.perm, self.fs_err)
+            self._fsort(self.idx, B, self.sorted_keys, self.perm)
         else:
             KN.sort_ids(self.idx, self.sorted_keys, None, self.perm, n, self.end_bit, self.temp)
 
     def check_errors(self):
         """Raise on device-side input errors flagged by earlier steps (host sync)."""
-        if self._fs_ranges is not None and int(self.fs_err.item()) != 0:
+        if self._fsort is not None and int(self._fsort.err.item()) != 0:
             raise RuntimeError("an id lies outside its field's declared range (field_ranges): "
                                "the per-field sort is invalid for this data")
         if self.shx is not None and self.shx.error() != 0:

@@ -173,7 +173,8 @@ _SIGS = {
     "hfm_sparse_fused_tiles": [c_int, c_int],
     "hfm_sparse_fused": [c_int, c_int, c_int, c_void_p, c_void_p],
     "hfm_sparse_fused_args_bytes": [],
-    "hfm_field_sort": [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
+    "hfm_field_sort_max_pb": [],
+    "hfm_field_sort": [c_void_p, c_int, c_int, c_void_p, c_void_p, c_int] + [c_void_p] * 4 + [c_void_p],
     "hfm_radix_sort_ids": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_size_t, c_void_p],
     "hfm_segments": [c_void_p, c_int] + [c_void_p] * 5 + [c_void_p, c_size_t, c_void_p],
     "hfm_fm_bwd_seg": [c_int] + [c_void_p] * 7 + [c_int, c_int, c_int, c_void_p, c_void_p, c_void_p],

@@ -112,12 +112,35 @@ def field_sort_max_rows() -> int:
     return int(L().hfm_field_sort_max_rows())
 
 
-def field_sort(ids, B, F, franges_dev, keys_out, perm_out, err):
-    """Per-field LDS sort of the B*F slot ids (field ranges disjoint and increasing): output is
-    identical to ``sort_ids`` on the same slots.  ``franges_dev``: int32 [F, 3] {lo, hi, bits};
-    ``err``: int32 [1], set non-zero when an id lies outside its field's range."""
-    check(L().hfm_field_sort(ptr(ids), B, F, ptr(franges_dev), ptr(keys_out), ptr(perm_out), ptr(err),
-                             stream_handle()), "field_sort")
+class FieldSort:
+    """Per-field MSD-partitioned LDS sort of the B*F slot ids (csrc/kernels/field_sort.hip) for
+    disjoint, increasing per-field id ranges [lo, hi): output identical to ``sort_ids`` on the
+    same slots.  ``err`` (int32 [1]) turns non-zero when an id lies outside its field's range."""
+
+    def __init__(self, ranges, max_rows: int, device, max_pb: int = 0):
+        """``max_pb``: each field is split into up to 2^max_pb workgroups (MSD partitions): 4 when
+        the sort is on the critical path, 0 (one workgroup per field) when it overlaps other work."""
+        import math
+        max_pb = min(int(max_pb), int(L().hfm_field_sort_max_pb()))
+        fr, work = [], []
+        for f, (lo, hi) in enumerate(ranges):
+            bits = int(math.ceil(math.log2(hi - lo))) if hi - lo > 1 else 0
+            pb = min(bits, max_pb)
+            fr.append((int(lo), int(hi), bits, pb))
+            work += [(f, p) for p in range(1 << pb)]
+        self.F = len(fr)
+        self.fr = torch.tensor(fr, dtype=torch.int32).reshape(-1).to(device)
+        self.work = torch.tensor(work, dtype=torch.int32).reshape(-1).to(device)
+        self.nwork = len(work)
+        self.idsT = torch.zeros(self.F * max(1, max_rows), dtype=torch.int32, device=device)
+        self.err = torch.zeros(1, dtype=torch.int32, device=device)
+        self.max_rows = max_rows
+
+    def __call__(self, ids, B: int, keys_out, perm_out):
+        assert B <= self.max_rows and ids.numel() >= B * self.F
+        check(L().hfm_field_sort(ptr(ids), B, self.F, ptr(self.fr), ptr(self.work), self.nwork,
+                                 ptr(self.idsT), ptr(keys_out), ptr(perm_out), ptr(self.err),
+                                 stream_handle()), "field_sort")
 
 
 def sort_error(temp) -> int:

@@ -336,29 +336,25 @@ def test_sort_graph_replay_with_new_inputs(impl):
             assert torch.equal(sk.long(), rk) and torch.equal(perm.long(), rp), (n, bits, it)
 
 
-def _franges_dev(ranges):
-    import math
-    fr = [(lo, hi, int(math.ceil(math.log2(hi - lo))) if hi - lo > 1 else 0) for lo, hi in ranges]
-    return torch.tensor(fr, dtype=torch.int32).reshape(-1).to(DEV)
-
-
-@pytest.mark.parametrize("preset,B", [("criteo_1tb", 16384), ("criteo_kaggle", 1000), ("reference", 4096)])
-def test_field_sort_equals_global_sort(preset, B):
+@pytest.mark.parametrize("preset,B,max_pb", [("criteo_1tb", 16384, 4), ("criteo_1tb", 16384, 0),
+                                             ("criteo_kaggle", 1000, 4), ("reference", 4096, 2),
+                                             ("criteo_1tb", 333, 4)])
+def test_field_sort_equals_global_sort(preset, B, max_pb):
     """The per-field LDS sort (field_sort.hip) returns exactly the stable global sort of the
     B*F slot ids, in eager mode and as a graph replayed on new batches."""
     synth = make_synth(preset)
     F = synth.F
-    fr = _franges_dev(synth.field_ranges())
+    fs = KN.FieldSort(synth.field_ranges(), B, DEV, max_pb=max_pb)
+    err = fs.err
     ids = torch.zeros(B * F, dtype=torch.int32, device=DEV)
     sk = torch.full_like(ids, -7)
     perm = torch.full_like(ids, -7)
-    err = torch.zeros(1, dtype=torch.int32, device=DEV)
     ids.copy_(synth.batch(B, 0, device=DEV, id_dtype=torch.int32)[0].reshape(-1))
-    KN.field_sort(ids, B, F, fr, sk, perm, err)
+    fs(ids, B, sk, perm)
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g):
-        KN.field_sort(ids, B, F, fr, sk, perm, err)
+        fs(ids, B, sk, perm)
     for it in range(3):
         if it:
             ids.copy_(synth.batch(B, it, device=DEV, id_dtype=torch.int32)[0].reshape(-1))
@@ -372,13 +368,12 @@ def test_field_sort_equals_global_sort(preset, B):
 def test_field_sort_flags_out_of_range_ids():
     synth = make_synth("criteo_kaggle")
     F, B = synth.F, 512
-    fr = _franges_dev(synth.field_ranges())
+    fs = KN.FieldSort(synth.field_ranges(), B, DEV, max_pb=4)
     ids = synth.batch(B, 0, device=DEV, id_dtype=torch.int32)[0].contiguous()
     ids[7, 20] = synth.field_ranges()[21][0]          # an id of field 21 in field 20
     sk, perm = torch.empty(B * F, dtype=torch.int32, device=DEV), torch.empty(B * F, dtype=torch.int32, device=DEV)
-    err = torch.zeros(1, dtype=torch.int32, device=DEV)
-    KN.field_sort(ids.reshape(-1), B, F, fr, sk, perm, err)
-    assert int(err.item()) != 0
+    fs(ids.reshape(-1), B, sk, perm)
+    assert int(fs.err.item()) != 0
 
 
 def test_train_step_field_sort_bitwise_equals_global_sort():

@@ -37,19 +37,17 @@ def field_main(dev):
     from hipfm.data.synthetic import make_synth
     synth = make_synth("criteo_1tb")
     F = synth.F
-    fr = [(lo, hi, int(math.ceil(math.log2(hi - lo))) if hi - lo > 1 else 0) for lo, hi in synth.field_ranges()]
-    frd = torch.tensor(fr, dtype=torch.int32).reshape(-1).to(dev)
-    for B in (4096, 8192, 16384):
+    for B in (1024, 4096, 8192, 16384):
+        fs = KN.FieldSort(synth.field_ranges(), B, dev, max_pb=int(os.environ.get("HIPFM_FS_MAX_PB", "4")))
         n = B * F
         ids = synth.batch(B, 0, device=dev, id_dtype=torch.int32)[0].reshape(-1).contiguous()
         sk, perm = torch.empty_like(ids), torch.empty_like(ids)
-        err = torch.zeros(1, dtype=torch.int32, device=dev)
         temp = torch.empty(KN.radix_temp_bytes(n) + 256, dtype=torch.uint8, device=dev)
-        tf = timeit(lambda: KN.field_sort(ids, B, F, frd, sk, perm, err))
+        tf = timeit(lambda: fs(ids, B, sk, perm))
         t0 = timeit(lambda: KN.onesweep_sort_ids(ids, sk, perm, n, 30, temp))
-        KN.field_sort(ids, B, F, frd, sk, perm, err)
+        fs(ids, B, sk, perm)
         rk, rp = torch.sort(ids.long(), stable=True)
-        ok = torch.equal(sk.long(), rk) and torch.equal(perm.long(), rp) and int(err.item()) == 0
+        ok = torch.equal(sk.long(), rk) and torch.equal(perm.long(), rp) and int(fs.err.item()) == 0
         print(f"criteo_1tb B={B:6d} n={n:8d}: field_sort {tf:7.1f} us  onesweep {t0:7.1f} us  exact={ok}",
               flush=True)
 
