@@ -97,7 +97,8 @@ def main():
     def run(nsteps, start):
         for s in range(nsteps):
             ids, vals, labels = pool[(start + s) % len(pool)]
-            model.train_step(ids, vals, labels, use_graph=use_graph)
+            nxt = pool[(start + s + 1) % len(pool)][0]     # next batch: its id routing is prefetched
+            model.train_step(ids, vals, labels, use_graph=use_graph, next_ids=nxt)
 
     run(args.warmup, 0)
     torch.cuda.synchronize()
@@ -159,8 +160,12 @@ def main():
             "train_loss": round(loss, 5),
         }
         print(json.dumps(out), flush=True)
+    model.check_errors()
     if comm is not None:
         dist.barrier()
+        torch.cuda.synchronize()
+        # (native RCCL communicators are left to process exit: ncclCommDestroy after graph
+        # capture blocks on ROCm 7)
         dist.destroy_process_group()
 
 

@@ -56,3 +56,15 @@ HFM_API int hfm_comm_alltoall(void* comm, const void* send, void* recv, size_t b
     return nccl_rc(ncclAllToAll(send, recv, bytes_per_peer / 4, ncclInt32, (ncclComm_t)comm, st));
   return nccl_rc(ncclAllToAll(send, recv, bytes_per_peer, ncclInt8, (ncclComm_t)comm, st));
 }
+
+// recv: nranks blocks of `bytes_per_rank` (block p = rank p's send buffer).  Used for the id
+// routing of the NEXT batch on a side stream: captured collectives (all-reduce / all-gather) are
+// safe on forked capture streams, where RCCL's peer-to-peer all-to-all is not (ROCm 7 / RCCL 2.26
+// segfaults at graph instantiation), so there the routing trades N x bytes for capturability.
+HFM_API int hfm_comm_allgather(void* comm, const void* send, void* recv, size_t bytes_per_rank,
+                               hipStream_t st) {
+  if (bytes_per_rank == 0) return 0;
+  if (bytes_per_rank % 4 == 0)
+    return nccl_rc(ncclAllGather(send, recv, bytes_per_rank / 4, ncclInt32, (ncclComm_t)comm, st));
+  return nccl_rc(ncclAllGather(send, recv, bytes_per_rank, ncclInt8, (ncclComm_t)comm, st));
+}

@@ -44,6 +44,7 @@ _OLD_FINALIZE = os.environ.get("HIPFM_OLD_FINALIZE", "0") == "1"
 _SORT_MODE = os.environ.get("HIPFM_SORT", "auto")                # auto | global
 _SORT_SIDE_STREAM = os.environ.get("HIPFM_SORT_SIDE_STREAM", "1") == "1"
 _SPARSE_IMPL = os.environ.get("HIPFM_SPARSE", "fused")             # fused | seg
+_SHARD_PIPELINE = os.environ.get("HIPFM_SHARD_PIPELINE", "1") == "1"
 
 
 def check_field_ranges(ranges, F: int, V: int) -> List[Tuple[int, int]]:
@@ -260,6 +261,7 @@ class NativeDeepFM:
         self._side = None
         self._comm_stream = None
         self.shx = None
+        self._shx_plan = None
         self.batch_size = int(batch_size)
         # fused deep tower (csrc/kernels/tower.hip): whole forward + head + dgrad chain in one
         # launch per 32-sample block; batch norm (needs batch-wide statistics between the
@@ -400,7 +402,10 @@ class NativeDeepFM:
         if self.sharded and getattr(self.comm, "engine", None) is not None:
             from ..parallel.sharded import FixedCapacityExchange
             old = getattr(self, "_shx_tags", None)
-            self.shx = FixedCapacityExchange(self, self.comm.engine, self.comm.capacity, tags=old)
+            self.shx = FixedCapacityExchange(self, self.comm.engine, self.comm.capacity, tags=old,
+                                             engine_route=getattr(self.comm, "engine_route", None))
+            if self.shx.eng_route is None and not hasattr(self.comm, "route_engine"):
+                self.shx.eng_route = self.comm.engine
             self._shx_tags = self.shx.tags
         self._own_in = (self.idx, self.vals, self.labels)
         self._graphs = {}
@@ -603,7 +608,7 @@ class NativeDeepFM:
         idx = self.idx
         tv, tw = self.tv, self.tw
         if self.shx is not None:
-            idx, tv, tw = self.shx.forward(B)
+            idx, tv, tw = self.shx.fetch(self._shx_plan)
         elif self.sharded:
             idx, tv, tw = self.comm.sharded_forward_gather(self, B)
         fm_bias = self.p[self.dense_segs["fm_bias"].off:]
@@ -816,7 +821,7 @@ class NativeDeepFM:
         (returns None).  Multi-rank: returns compact unique-row gradients for the exchange."""
         n = B * self.F
         if self.shx is not None:
-            self.shx.backward(B)
+            self.shx.backward(self._shx_plan, B)
             return None
         if self.sharded:
             return self.comm.sharded_backward(self, B, idx, tv)
@@ -869,6 +874,8 @@ class NativeDeepFM:
         sort depends only on the batch, so it runs on a side stream concurrently with the
         forward / tower backward (a parallel branch of the captured graph)."""
         presorted = False
+        if self.shx is not None:
+            self._shx_start(B)
         if not self.sharded and _SORT_SIDE_STREAM:
             main = torch.cuda.current_stream(self.device)
             if self._side is None:
@@ -899,6 +906,8 @@ class NativeDeepFM:
             main.wait_stream(self._comm_stream)
         if work is not None:
             self.comm.wait(work)
+        if self.shx is not None:
+            self.shx.end(self._shx_plan)
         if _SEPARATE_STEP_INC:
             KN.dense_opt(self.opt_id, self.p, self.g, self.sd[0], self.sd[1], self.P, self.h_dense,
                          self.step, self._shadow_dev, self._nshadow)
@@ -906,6 +915,13 @@ class NativeDeepFM:
         else:
             KN.dense_opt(self.opt_id, self.p, self.g, self.sd[0], self.sd[1], self.P, self.h_dense,
                          self.step, self._shadow_dev, self._nshadow, done_ctr=self._done_ctr)
+
+    def _shx_start(self, B: int):
+        """Row-sharded step start: routing plan (inline unless prefetched by the previous step)
+        and the fork of the next batch's routing."""
+        if self._shx_plan is None:
+            self._shx_plan = self.shx.plan(self.idx, B, None, resident=False)
+        self.shx.begin(self._shx_plan, B)
 
     def compute_grads(self, ids, vals, labels):
         """Forward + backward WITHOUT any update (tests / debugging): returns the flat dense
@@ -921,10 +937,12 @@ class NativeDeepFM:
         U = int(self.num_u.item())
         return self.g.clone(), self.ukeys[:U].clone(), self.UG[:U].clone()
 
-    def train_step(self, ids, vals, labels, use_graph: bool = False):
+    def train_step(self, ids, vals, labels, use_graph: bool = False, next_ids=None):
         """One training step.  A device-resident int32 batch whose size equals the allocated
         batch is bound in place (no staging copy); with ``use_graph`` each such resident batch
-        gets its own captured HIP graph (the HBM-cached epoch replays graphs back to back)."""
+        gets its own captured HIP graph (the HBM-cached epoch replays graphs back to back).
+        ``next_ids`` (resident ids of the NEXT step's batch): on the row-sharded multi-GPU step
+        its routing is prefetched on a side stream during this step."""
         direct = (ids.is_cuda and ids.dtype == torch.int32 and vals.dtype == torch.float32 and
                   ids.is_contiguous() and vals.is_contiguous() and labels.is_contiguous() and
                   ids.shape[0] == self.M and ids.numel() == self.M * self.F)
@@ -936,10 +954,23 @@ class NativeDeepFM:
             self.idx, self.vals, self.labels = self._own_in
             B = self.stage_batch(ids, vals, labels)
             key = ("staged", B)
+        self._shx_plan = None
+        if self.shx is not None:
+            nxt = None
+            if (direct and next_ids is not None and _SHARD_PIPELINE and next_ids.is_cuda and
+                    next_ids.dtype == torch.int32 and next_ids.is_contiguous() and
+                    next_ids.shape[0] == B and next_ids.numel() == B * self.F):
+                nxt = next_ids.reshape(-1)
+            self._shx_plan = self.shx.plan(self.idx, B, nxt, resident=direct)
+            self.shx._next_ids = nxt
+            key = key + self._shx_plan
         if use_graph and (self.comm is None or self.comm.graph_safe):
             self._replay_graph(key, B)
         else:
             self.train_step_enqueue(B)
+        if self.shx is not None:
+            self.shx.commit(self._shx_plan, self.idx, B, resident=direct)
+            self._shx_plan = None
         if self._host_step is not None:
             self._host_step += 1
         return B
@@ -967,18 +998,13 @@ class NativeDeepFM:
         g.replay()
 
     def precapture(self, batches):
-        """Capture the graphs of resident batches up front (keeps capture out of timed loops)."""
-        for ids, vals, labels in batches:
-            if not self._graphs:
-                self.train_step(ids, vals, labels, use_graph=True)   # eager first step + capture
-                continue
-            self.idx, self.vals, self.labels = ids.reshape(-1), vals.reshape(-1), labels.reshape(-1)
-            key = (ids.data_ptr(), vals.data_ptr(), labels.data_ptr(), ids.shape[0])
-            if key not in self._graphs:
-                g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g):
-                    self.train_step_enqueue(ids.shape[0])
-                self._graphs[key] = g
+        """One pass over the resident batches with graph capture (the first step eager, every new
+        binding captured then replayed), so timed loops only replay graphs.  Consecutive batches
+        are chained: the row-sharded step prefetches the next batch's routing.  These are real
+        training steps (use them as warm-up)."""
+        P = len(batches)
+        for i, (ids, vals, labels) in enumerate(batches):
+            self.train_step(ids, vals, labels, use_graph=True, next_ids=batches[(i + 1) % P][0])
         torch.cuda.synchronize()
 
     def loss_value(self, B: int, include_l2: bool = False) -> float:
@@ -996,6 +1022,16 @@ class NativeDeepFM:
         return float(self.l2 * 0.5 * s)
 
     def predict_enqueue(self, B: int, with_labels: bool = False):
+        if self.shx is not None:           # row-sharded: route this batch inline, then fetch
+            self._shx_plan = self.shx.plan(self.idx, B, None, resident=False)
+            self.shx.begin(self._shx_plan, B)
+            self._predict_body(B, with_labels)
+            self.shx.commit(self._shx_plan, self.idx, B, resident=False)
+            self._shx_plan = None
+            return
+        self._predict_body(B, with_labels)
+
+    def _predict_body(self, B: int, with_labels: bool):
         if self.fused:
             self._fm_forward(B, train=False)
             KN.tower(self._tower_args(B, train=False, with_labels=with_labels))

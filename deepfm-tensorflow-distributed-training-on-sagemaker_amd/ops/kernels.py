@@ -342,6 +342,11 @@ def comm_alltoall(h: int, send: torch.Tensor, recv: torch.Tensor, bytes_per_peer
     check(L().hfm_comm_alltoall(h, ptr(send), ptr(recv), bytes_per_peer, stream_handle()), "comm_alltoall")
 
 
+def comm_allgather(h: int, send: torch.Tensor, recv: torch.Tensor, bytes_per_rank: int):
+    assert send.is_contiguous() and recv.is_contiguous()
+    check(L().hfm_comm_allgather(h, ptr(send), ptr(recv), bytes_per_rank, stream_handle()), "comm_allgather")
+
+
 # ------------------------------------------------------------------ row-sharded exchange (shard.hip)
 def sh_count_blocks(nmax: int) -> int:
     return int(L().hfm_sh_count_blocks(nmax))

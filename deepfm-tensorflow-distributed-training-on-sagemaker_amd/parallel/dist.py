@@ -75,18 +75,29 @@ class Comm:
         if native is None:
             native = (dist.get_backend(group) == "nccl" and self.sharded and
                       os.environ.get("HIPFM_SHARD_EXCHANGE", "fixed") == "fixed")
-        self.engine = self.engine_dense = None
+        self.engine = self.engine_dense = self.engine_route = None
+        if capacity is not None and self.world_size > 1:
+            # every rank must use the SAME per-peer block size in the fixed-capacity all-to-alls:
+            # take the max of the per-rank estimates (each rank measured its own batches)
+            cdev = (torch.device("cuda", torch.cuda.current_device())
+                    if dist.get_backend(group) == "nccl" else torch.device("cpu"))
+            t = torch.tensor([int(capacity)], dtype=torch.int64, device=cdev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+            capacity = int(t.item())
         self.capacity = capacity
         if native:
             from .sharded import RcclEngine
-            self.engine = RcclEngine(group)
-            self.engine_dense = RcclEngine(group)
+            self.engine = RcclEngine(group)          # row / gradient exchange (main stream)
+            self.engine_dense = RcclEngine(group)    # dense all-reduce (side stream)
+            # the next batch's id routing (side stream) gets its own communicator on first use:
+            # an idle RCCL communicator next to graph-captured ones faults replays (ROCm 7)
         # steps with host-synchronous routing (variable all-to-all splits) cannot be graphed
         self.graph_safe = (self.world_size == 1 and not self.force_exchange) or self.engine is not None
 
     @property
     def bytes_sent(self) -> int:
-        eng = sum(e.bytes_sent for e in (self.engine, self.engine_dense) if e is not None)
+        eng = sum(e.bytes_sent for e in (self.engine, self.engine_dense, self.engine_route)
+                  if e is not None)
         return self._bytes + self.router.bytes_sent + eng
 
     @bytes_sent.setter
@@ -111,6 +122,21 @@ class Comm:
 
     def barrier(self):
         dist.barrier(group=self.group)
+
+    def route_engine(self):
+        """Communicator for the prefetched routing; created collectively on first use (every
+        rank reaches its first prefetching step together), never inside a graph capture."""
+        if self.engine_route is None and self.engine is not None:
+            from .sharded import RcclEngine
+            self.engine_route = RcclEngine(self.group)
+        return self.engine_route
+
+    def close(self):
+        """Destroy the native RCCL communicators (before the process group goes away).  Not for
+        communicators captured into HIP graphs: ncclCommDestroy then blocks (ROCm 7)."""
+        for e in (self.engine, self.engine_dense, self.engine_route):
+            if e is not None:
+                e.close()
 
     # ------------------------------------------------------------------ helpers
     def _a2a_counts(self, send_counts: torch.Tensor) -> List[int]:

@@ -57,6 +57,10 @@ class RcclEngine:
         self.bytes_sent += bytes_per_peer * self.world
         KN.comm_alltoall(self.handle, send, recv, bytes_per_peer)
 
+    def allgather(self, send: torch.Tensor, recv: torch.Tensor, bytes_per_rank: int):
+        self.bytes_sent += bytes_per_rank * self.world
+        KN.comm_allgather(self.handle, send, recv, bytes_per_rank)
+
     def allreduce_(self, t: torch.Tensor):
         self.bytes_sent += t.numel() * 4
         KN.comm_allreduce_(self.handle, t)
@@ -67,11 +71,44 @@ class RcclEngine:
             self.handle = 0
 
 
-class FixedCapacityExchange:
-    """Buffers + step pieces of the row-sharded exchange for one NativeDeepFM (one rank)."""
+class _RouteSet:
+    """Routing state of one batch: sorted slots, unique ids, owner buckets, received requests.
+    Depends only on the batch ids (not on the table), so the next batch's set can be built while
+    the current batch trains."""
 
-    def __init__(self, m, engine, capacity: Optional[int] = None, tags: Optional[torch.Tensor] = None):
+    def __init__(self, m, n: int, N: int, C: int, temp_bytes: int):
+        dev = m.device
+        i32 = dict(dtype=torch.int32, device=dev)
+        self.sorted_keys = torch.zeros(n, **i32)
+        self.perm = torch.zeros(n, **i32)
+        self.seg_flags = torch.zeros(n, **i32)
+        self.sid_incl = torch.zeros(n, **i32)
+        self.ukeys = torch.zeros(n, **i32)
+        self.seg_start = torch.zeros(n + 1, **i32)
+        self.num_u = torch.zeros(1, **i32)
+        self.temp = torch.zeros(temp_bytes, dtype=torch.uint8, device=dev)
+        self.upos = torch.zeros(n, **i32)
+        self.cnt_tmp = torch.zeros(KN.sh_count_blocks(n) * N, **i32)
+        self.send_ids = torch.full((N * C,), -1, **i32)
+        self.recv_ids = torch.full((N * C,), -1, **i32)
+        self.send_cnt = torch.zeros(N, **i32)
+        self.gathered = None     # [N, N*C] all-gathered requests (side-stream routing)
+        self.slot_row = torch.zeros(n, **i32)
+        self.key = None          # host: (ids data_ptr, B) routed into this set
+
+
+class FixedCapacityExchange:
+    """Buffers + step pieces of the row-sharded exchange for one NativeDeepFM (one rank).
+
+    Two routing sets alternate: with ``next`` known (resident / prefetched batches), the routing
+    of batch i+1 (sort, dedup, owner buckets, id all-to-all, slot->row map) runs on a side stream
+    during step i — the sparse-input-dist pipelining of production DLRM trainers — so the
+    critical path of a step keeps only the row fetch, the compute and the gradient exchange."""
+
+    def __init__(self, m, engine, capacity: Optional[int] = None, tags: Optional[torch.Tensor] = None,
+                 engine_route=None):
         self.m, self.eng = m, engine
+        self.eng_route = engine_route     # created on the first prefetching step (plan())
         self.N, self.rank = engine.world, engine.rank
         dev = m.device
         K, n = m.K, m.M * m.F
@@ -79,51 +116,110 @@ class FixedCapacityExchange:
         self.C = (self.C + 63) // 64 * 64
         self.RW = K + 4                      # exchanged row: {v[K], w, 0, 0, 0} / {g_v, g_w, 0, 0, 0}
         T = self.N * self.C
-        i32 = dict(dtype=torch.int32, device=dev)
         f32 = dict(dtype=torch.float32, device=dev)
-        self.send_ids = torch.full((T,), -1, **i32)
-        self.recv_ids = torch.full((T,), -1, **i32)
-        self.upos = torch.zeros(n, **i32)
-        self.cnt_tmp = torch.zeros(KN.sh_count_blocks(n) * self.N, **i32)
-        self.send_cnt = torch.zeros(self.N, **i32)
-        self.err = torch.zeros(1, **i32)
-        self.slot_row = torch.zeros(n, **i32)
+        self.sets = [_RouteSet(m, n, self.N, self.C, m.temp.numel()) for _ in range(2)]
+        for rs in self.sets:
+            rs.gathered = torch.zeros(self.N * self.N * self.C, dtype=torch.int32, device=dev)
+        self.cur = 0
+        self.err = torch.zeros(1, dtype=torch.int32, device=dev)
         self.rows_out = torch.zeros(T, self.RW, **f32)
         self.rows_in = torch.zeros(T, self.RW, **f32)
         self.send_g = torch.zeros(T, self.RW, **f32)
         self.recv_g = torch.zeros(T, self.RW, **f32)
         # owner-side request tags: [local rows][N] of {step + 1, slot} (64-bit)
         self.tags = tags if tags is not None else torch.zeros(m.R * self.N, dtype=torch.int64, device=dev)
+        self._side = None
 
-    # ------------------------------------------------------------------ forward
-    def forward(self, B: int):
-        """Sort + dedup the slot ids, fetch the unique rows from their owners.  Returns the
-        per-slot row index and the (tv, tw) views of the received rows for fm_fwd."""
+    # ------------------------------------------------------------------ host-side plan
+    def plan(self, ids: torch.Tensor, B: int, nxt: Optional[torch.Tensor], resident: bool = True):
+        """Routing decisions for one step (part of the graph key): (set index, route the current
+        batch inline?, next ids or None).  Only resident batches (fixed device buffers) can have
+        been prefetched: staged buffers change content under the same address."""
+        c = self.cur
+        key = (ids.data_ptr(), B)
+        inline = (not resident) or self.sets[c].key != key
+        if nxt is not None and self.eng_route is None:
+            get = getattr(self.m.comm, "route_engine", None)
+            self.eng_route = get() if get is not None else self.eng
+        return (c, inline, None if nxt is None else (nxt.data_ptr(), nxt.numel() // self.m.F))
+
+    def commit(self, plan, ids: torch.Tensor, B: int, resident: bool = True):
+        """Consecutive steps always use alternate routing sets (prefetched or not): a step's
+        routing kernels never overwrite buffers the previous step's backward still reads, even
+        when graph replays run back to back."""
+        c, _, nk = plan
+        self.sets[c].key = (ids.data_ptr(), B) if resident else None
+        if nk is not None:
+            self.sets[1 - c].key = nk
+        self.cur = 1 - c
+
+    # ------------------------------------------------------------------ pieces
+    def route(self, rs: _RouteSet, ids: torch.Tensor, B: int, eng, gather: bool = False):
+        """Sort + dedup the slot ids, bucket the unique ids by owner, send the requests.
+        ``gather``: requests travel by all-gather (every rank's [N, C] block; this rank keeps
+        column ``rank``) instead of all-to-all — RCCL's all-to-all cannot be captured on a forked
+        side stream (segfault at graph instantiation on ROCm 7), its collectives can."""
         m = self.m
         n = B * m.F
-        m._sort_slots(B)
-        KN.segments(m.sorted_keys, n, m.seg_flags, m.sid_incl, m.ukeys, m.seg_start, m.num_u, m.temp)
-        KN.sh_bucket(m.ukeys, m.num_u, n, self.N, self.C, self.cnt_tmp, self.send_ids, self.upos,
-                     self.send_cnt, self.err)
-        self.eng.alltoall(self.send_ids, self.recv_ids, self.C * 4)
-        KN.sh_serve(m.K, self.recv_ids, self.N * self.C, self.N, m.tv, m.tw, self.rows_out)
-        self.eng.alltoall(self.rows_out, self.rows_in, self.C * self.RW * 4)
-        KN.sh_slot_rows(m.perm, m.sid_incl, self.upos, n, self.slot_row)
-        return self.slot_row, self.rows_in[:, : m.K], self.rows_in[:, m.K]
+        if m.uses_field_sort(B):
+            m._fsort(ids, B, rs.sorted_keys, rs.perm)
+        else:
+            KN.sort_ids(ids, rs.sorted_keys, None, rs.perm, n, m.end_bit, rs.temp)
+        KN.segments(rs.sorted_keys, n, rs.seg_flags, rs.sid_incl, rs.ukeys, rs.seg_start, rs.num_u, rs.temp)
+        KN.sh_bucket(rs.ukeys, rs.num_u, n, self.N, self.C, rs.cnt_tmp, rs.send_ids, rs.upos,
+                     rs.send_cnt, self.err)
+        if gather:
+            if rs.gathered is None:
+                rs.gathered = torch.zeros(self.N * self.N * self.C, dtype=torch.int32, device=m.device)
+            eng.allgather(rs.send_ids, rs.gathered, self.N * self.C * 4)
+            rs.recv_ids.view(self.N, self.C).copy_(
+                rs.gathered.view(self.N, self.N, self.C)[:, self.rank, :])
+        else:
+            eng.alltoall(rs.send_ids, rs.recv_ids, self.C * 4)
+        KN.sh_slot_rows(rs.perm, rs.sid_incl, rs.upos, n, rs.slot_row)
 
-    # ------------------------------------------------------------------ backward
-    def backward(self, B: int):
+    def begin(self, plan, B: int):
+        """Start of a step: route the current batch if it was not prefetched, then fork the
+        routing of the next batch onto a side stream."""
+        m = self.m
+        c, inline, nk = plan
+        if inline:
+            self.route(self.sets[c], m.idx, B, self.eng)
+        if nk is not None:
+            main = torch.cuda.current_stream(m.device)
+            if self._side is None:
+                self._side = torch.cuda.Stream(m.device)
+            self._side.wait_stream(main)
+            nxt_ids = self._next_ids
+            with torch.cuda.stream(self._side):
+                self.route(self.sets[1 - c], nxt_ids, nk[1], self.eng_route, gather=True)
+
+    def end(self, plan):
+        if plan[2] is not None:
+            torch.cuda.current_stream(self.m.device).wait_stream(self._side)
+
+    def fetch(self, plan):
+        """Owners serve the requested rows (after the previous step's updates), rows come back."""
+        m = self.m
+        rs = self.sets[plan[0]]
+        KN.sh_serve(m.K, rs.recv_ids, self.N * self.C, self.N, m.tv, m.tw, self.rows_out)
+        self.eng.alltoall(self.rows_out, self.rows_in, self.C * self.RW * 4)
+        return rs.slot_row, self.rows_in[:, : m.K], self.rows_in[:, m.K]
+
+    def backward(self, plan, B: int):
         """Per-unique gradient rows -> owners -> rank-ordered sum + row update on the owner."""
         m = self.m
+        rs = self.sets[plan[0]]
         n = B * m.F
         A = m.sf_args(n)
+        A.sorted_keys, A.perm = rs.sorted_keys.data_ptr(), rs.perm.data_ptr()
         A.tv, A.tw = self.rows_in.data_ptr(), self.rows_in.data_ptr() + 4 * m.K
         A.ldv = A.ldw = self.RW
-        A.sid, A.upos, A.gout = m.sid_incl.data_ptr(), self.upos.data_ptr(), self.send_g.data_ptr()
+        A.sid, A.upos, A.gout = rs.sid_incl.data_ptr(), rs.upos.data_ptr(), self.send_g.data_ptr()
         KN.sparse_fused(m.K, KN.SF_EXCHANGE, m.opt_id, A)
         self.eng.alltoall(self.send_g, self.recv_g, self.C * self.RW * 4)
         S = ShApplyArgs()
-        S.recv_ids, S.total, S.N, S.C = self.recv_ids.data_ptr(), self.N * self.C, self.N, self.C
+        S.recv_ids, S.total, S.N, S.C = rs.recv_ids.data_ptr(), self.N * self.C, self.N, self.C
         S.mode = 0 if m.sparse_update == "lazy" else 1
         S.recv_g, S.tags = self.recv_g.data_ptr(), self.tags.data_ptr()
         S.tv, S.tw = m.tv.data_ptr(), m.tw.data_ptr()

@@ -177,3 +177,31 @@ def test_launcher_tf_config_mapping(monkeypatch):
     assert d == {"nnodes": 3, "node_rank": 2, "master_addr": "algo-1"}
     monkeypatch.setenv("TF_CONFIG", json.dumps({"cluster": cluster, "task": {"type": "ps", "index": 0}}))
     assert launch.main(["--nproc_per_node", "1", "-m", "hipfm"]) == 0
+
+
+def _cap_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from hipfm.parallel.dist import Comm
+    # every rank measured a different per-peer capacity on its own batches
+    c = Comm(sharded=True, capacity=64 * (rank + 1))
+    q.put((rank, c.capacity))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_fixed_capacity_agreed_across_ranks():
+    """The fixed-capacity all-to-all blocks must have one size on every rank: Comm takes the max
+    of the per-rank capacity estimates (bench.py measures each rank's own batches)."""
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_cap_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(v == 64 * world for v in got.values()), got

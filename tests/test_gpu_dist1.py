@@ -35,8 +35,9 @@ def group():
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("sharded,update", [(True, "lazy"), (True, "tf1_dense"), (False, "lazy")])
-def test_exchange_paths_match_local(group, sharded, update):
+@pytest.mark.parametrize("sharded,update,prefetch", [(True, "lazy", False), (True, "tf1_dense", False),
+                                                     (False, "lazy", False), (True, "lazy", True)])
+def test_exchange_paths_match_local(group, sharded, update, prefetch):
     synth = make_synth("total:6000", seed=21)
     F, K, layers, keep = synth.F, 8, [64, 32], [0.8, 0.8]
     V = synth.feature_size
@@ -47,10 +48,13 @@ def test_exchange_paths_match_local(group, sharded, update):
     a.load_tf_params(params)
     b.load_tf_params(params)
     assert b.exchange and b.sharded == sharded
-    for s in range(4):
-        ids, vals, labels = synth.batch(512, step=s, device="cuda", id_dtype=torch.int32)
+    data = [synth.batch(512, step=s % 3, device="cuda", id_dtype=torch.int32) for s in range(6)]
+    for s in range(6):
+        ids, vals, labels = data[s]
         a.train_step(ids, vals, labels)
-        b.train_step(ids, vals, labels, use_graph=True)    # graph refused -> eager exchange
+        nxt = data[s + 1][0] if (prefetch and s + 1 < 6) else None
+        # native RCCL engine: captured into graphs (next batch's routing on a side stream)
+        b.train_step(ids, vals, labels, use_graph=True, next_ids=nxt)
     torch.cuda.synchronize()
     assert torch.allclose(a.tv, b.tv, atol=1e-6) and torch.allclose(a.tw, b.tw, atol=1e-6)
     assert torch.allclose(a.p, b.p, atol=1e-6)

@@ -64,6 +64,16 @@ class MeshEngine:
             dst[p].copy_(sp.view(-1).view(torch.uint8).view(N, bytes_per_peer)[r])
         self._finish(s)
 
+    def allgather(self, send, recv, bytes_per_rank):
+        self.bytes_sent += bytes_per_rank * self.world
+        s = self._publish(send)
+        dst = recv.view(-1).view(torch.uint8).view(self.world, bytes_per_rank)
+        for p in range(self.world):
+            sp, evp = self.hub.slots[p]
+            s.wait_event(evp)
+            dst[p].copy_(sp.view(-1).view(torch.uint8))
+        self._finish(s)
+
     def allreduce_(self, t):
         s = self._publish(t)
         acc = torch.zeros_like(t)
@@ -82,6 +92,7 @@ class MeshComm:
         self.force_exchange = False
         self.engine = MeshEngine(hub, rank)
         self.engine_dense = MeshEngine(hub, rank)
+        self.engine_route = MeshEngine(hub, rank)
         self.capacity = capacity
         self.graph_safe = False
 
@@ -90,7 +101,7 @@ class MeshComm:
         return self.engine.bytes_sent
 
 
-def _run_ranks(models, batches):
+def _run_ranks(models, batches, prefetch=False):
     errs = []
 
     def body(r):
@@ -98,8 +109,10 @@ def _run_ranks(models, batches):
             torch.cuda.set_device(0)
             s = torch.cuda.Stream()
             with torch.cuda.stream(s):
-                for ids, vals, lab in batches[r]:
-                    models[r].train_step(ids, vals, lab)
+                bl = batches[r]
+                for i, (ids, vals, lab) in enumerate(bl):
+                    nxt = bl[i + 1][0] if (prefetch and i + 1 < len(bl)) else None
+                    models[r].train_step(ids, vals, lab, next_ids=nxt)
             s.synchronize()
         except BaseException as e:          # surface failures instead of hanging the barrier
             errs.append(e)
@@ -114,9 +127,9 @@ def _run_ranks(models, batches):
         raise errs[0]
 
 
-@pytest.mark.parametrize("N,opt,update", [(2, "Adam", "lazy"), (3, "Adagrad", "lazy"),
-                                          (4, "Adam", "tf1_dense")])
-def test_sharded_exchange_matches_global_batch(N, opt, update):
+@pytest.mark.parametrize("N,opt,update,prefetch", [(2, "Adam", "lazy", False), (3, "Adagrad", "lazy", True),
+                                                   (4, "Adam", "tf1_dense", False), (4, "Adam", "lazy", True)])
+def test_sharded_exchange_matches_global_batch(N, opt, update, prefetch):
     synth = make_synth("criteo_kaggle", seed=4)
     F, K, layers, keep, B = synth.F, 8, [64, 32], [1.0, 1.0], 512
     V = synth.feature_size
@@ -140,7 +153,7 @@ def test_sharded_exchange_matches_global_batch(N, opt, update):
         models.append(m)
     batches = [[(ids[r * B:(r + 1) * B].contiguous(), vals[r * B:(r + 1) * B].contiguous(),
                  lab[r * B:(r + 1) * B].contiguous()) for ids, vals, lab in data] for r in range(N)]
-    _run_ranks(models, batches)
+    _run_ranks(models, batches, prefetch)
     torch.cuda.synchronize()
     for m in models:
         m.check_errors()
