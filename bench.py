@@ -44,6 +44,8 @@ def main():
     ap.add_argument("--optimizer", default="Adam")
     ap.add_argument("--sparse_update", default="lazy")
     ap.add_argument("--embedding_mode", default="auto")
+    ap.add_argument("--mlp_dtype", default="bf16", choices=["bf16", "fp8"],
+                    help="deep-tower forward GEMM operands (fp8 = OCP e4m3 MFMA, config #5)")
     ap.add_argument("--pool", type=int, default=16, help="resident synthetic batches per rank")
     ap.add_argument("--eval_batches", type=int, default=8)
     ap.add_argument("--no_graph", action="store_true")
@@ -86,7 +88,7 @@ def main():
     model = NativeDeepFM(synth.feature_size, F, args.embedding_size, layers, keep, l2_reg=1e-4,
                          learning_rate=5e-4, optimizer=args.optimizer,
                          sparse_update=args.sparse_update, seed=1234, batch_size=B, device=dev,
-                         comm=comm, field_ranges=synth.field_ranges())
+                         comm=comm, field_ranges=synth.field_ranges(), mlp_dtype=args.mlp_dtype)
     pool = [synth.batch(B, step=rank * 100000 + i, device=dev, id_dtype=torch.int32)
             for i in range(args.pool)]
     use_graph = not args.no_graph
@@ -142,7 +144,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16",
+            "dtype": args.mlp_dtype,
             "data": "synthetic (Criteo-shaped Zipf ids + teacher labels, HBM-resident), random-init weights",
             "config": {
                 "model": f"DeepFM Criteo-1TB-shape (F={F}, V={synth.feature_size}, K={args.embedding_size}, "
@@ -155,6 +157,7 @@ def main():
                                                 f"+{'row-sharded' if comm.sharded else 'replicated'}-embedding"),
                 "optimizer": f"{args.optimizer} ({args.sparse_update})",
                 "hip_graph": use_graph,
+                "mlp_dtype": args.mlp_dtype + (" fwd GEMMs, bf16 backward" if args.mlp_dtype == "fp8" else ""),
             },
             "eval_auc": round(auc, 5),
             "train_loss": round(loss, 5),

@@ -37,6 +37,28 @@ __device__ __forceinline__ bool dropout_keep(uint32_t flat, uint32_t salt, uint3
 __device__ __forceinline__ float bf2f(bf16 x) { return (float)x; }
 __device__ __forceinline__ bf16 f2bf(float x) { return (bf16)x; }
 
+// ---- OCP fp8 e4m3 (gfx950 v_cvt_pk_fp8_f32 is OCP e4m3fn, max 448; NOT MI300's fnuz) ----
+constexpr float FP8_MAX = 448.f;
+// 4 floats -> 4 e4m3 bytes (little-endian: a in byte 0), round-to-nearest-even, saturating
+__device__ __forceinline__ uint32_t pack4_fp8(float a, float b, float c, float d) {
+  a = __builtin_amdgcn_fmed3f(a, FP8_MAX, -FP8_MAX);
+  b = __builtin_amdgcn_fmed3f(b, FP8_MAX, -FP8_MAX);
+  c = __builtin_amdgcn_fmed3f(c, FP8_MAX, -FP8_MAX);
+  d = __builtin_amdgcn_fmed3f(d, FP8_MAX, -FP8_MAX);
+  int w = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+  w = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, w, true);
+  return (uint32_t)w;
+}
+// Power-of-two quantization scale s for a row / tensor of absolute max `amax`: amax * s lands
+// in (224, 448], and s and its inverse are exact (dequantization adds no rounding).
+__device__ __forceinline__ float fp8_pow2_scale(float amax) {
+  if (!(amax > 1e-30f) || !(amax < 3.0e38f)) return 1.f;
+  int e;
+  frexpf(FP8_MAX / amax, &e);
+  e = e > 100 ? 100 : e;
+  return ldexpf(1.f, e - 1);
+}
+
 // Optimizer ids shared by the sparse/dense optimizer kernels (hipfm/ops/optim.py).
 enum HfmOpt { OPT_ADAM = 0, OPT_ADAGRAD = 1, OPT_MOMENTUM = 2, OPT_FTRL = 3, OPT_GD = 4 };
 

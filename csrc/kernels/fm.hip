@@ -84,13 +84,14 @@ __global__ void __launch_bounds__(256) fm_fwd2_kernel(
     const int* __restrict__ idx, const float* __restrict__ vals, const float* __restrict__ tv,
     const float* __restrict__ tw, const float* __restrict__ bias, int B, int F, int KP,
     float* __restrict__ y_fm, float* __restrict__ S, bf16* __restrict__ E, bf16* __restrict__ Et,
-    long ldv, long ldw) {
+    uint8_t* __restrict__ E8, float* __restrict__ sE, long ldv, long ldw) {
   constexpr int SB = 256 / K;
   constexpr int V4 = K / 4;
   extern __shared__ __attribute__((aligned(16))) float fsm[];
   const int RS = F * K + 1;            // padded tile row (bank spread for the E^T pass)
   float* et = fsm;                     // [SB][RS]
   float* wx = fsm + SB * RS;           // [SB][F]
+  float* qs = wx + SB * F;             // [SB] fp8 row scales (E8 mode)
   const int s0 = blockIdx.x * SB;
   const int nsb = min(SB, B - s0);
   const int npair = nsb * F;
@@ -107,7 +108,6 @@ __global__ void __launch_bounds__(256) fm_fwd2_kernel(
     const int sl = p / F, f = p - sl * F;
     wx[sl * F + f] = w * x;
     float* dst = et + sl * RS + f * K;
-    bf16* eo = E + (size_t)(s0 + sl) * KP + f * K;
 #pragma unroll
     for (int j = 0; j < V4; ++j) {
       const f32x4 e = v[j] * x;
@@ -115,20 +115,23 @@ __global__ void __launch_bounds__(256) fm_fwd2_kernel(
       dst[4 * j + 1] = e[1];
       dst[4 * j + 2] = e[2];
       dst[4 * j + 3] = e[3];
-      bf16x4 eh = {f2bf(e[0]), f2bf(e[1]), f2bf(e[2]), f2bf(e[3])};
-      *reinterpret_cast<bf16x4*>(eo + 4 * j) = eh;
+      if (E) {
+        bf16x4 eh = {f2bf(e[0]), f2bf(e[1]), f2bf(e[2]), f2bf(e[3])};
+        *reinterpret_cast<bf16x4*>(E + (size_t)(s0 + sl) * KP + f * K + 4 * j) = eh;
+      }
     }
   }
   __syncthreads();
   {  // per (sample, k): S, sum e^2, y_w, y_v — fixed order over fields
     const int sl = threadIdx.x / K, k = threadIdx.x % K;
-    float sum = 0.f, sq = 0.f, yw = 0.f;
+    float sum = 0.f, sq = 0.f, yw = 0.f, am = 0.f;
     if (sl < nsb) {
       const float* er = et + sl * RS + k;
       for (int f = 0; f < F; ++f) {
         const float e = er[f * K];
         sum += e;
         sq += e * e;
+        am = fmaxf(am, fabsf(e));
       }
       for (int f = k; f < F; f += K) yw += wx[sl * F + f];
       if (S) S[(size_t)(s0 + sl) * K + k] = sum;
@@ -138,8 +141,27 @@ __global__ void __launch_bounds__(256) fm_fwd2_kernel(
     for (int o = 1; o < K; o <<= 1) {
       yv += __shfl_xor(yv, o, 64);
       yw += __shfl_xor(yw, o, 64);
+      am = fmaxf(am, __shfl_xor(am, o, 64));
     }
-    if (sl < nsb && k == 0) y_fm[s0 + sl] = bias[0] + yw + 0.5f * yv;
+    if (sl < nsb && k == 0) {
+      y_fm[s0 + sl] = bias[0] + yw + 0.5f * yv;
+      if (E8) {
+        const float q = fp8_pow2_scale(am);
+        qs[sl] = q;
+        sE[s0 + sl] = 1.f / q;
+      }
+    }
+  }
+  if (E8) {  // fp8 MLP input: per-sample power-of-two scale (current scaling, no amax history)
+    __syncthreads();
+    const int FK4 = F * K / 4;
+    for (int e = threadIdx.x; e < nsb * FK4; e += 256) {
+      const int sl = e / FK4, c4 = e - sl * FK4;
+      const float* src = et + sl * RS + 4 * c4;
+      const float q = qs[sl];
+      *reinterpret_cast<uint32_t*>(E8 + (size_t)(s0 + sl) * KP + 4 * c4) =
+          pack4_fp8(src[0] * q, src[1] * q, src[2] * q, src[3] * q);
+    }
   }
   if (Et) {
     const int sl = threadIdx.x % SB;
@@ -189,15 +211,16 @@ __global__ void __launch_bounds__(256) fm_bwd_sorted_kernel(
 template <int K>
 static int launch_fm_fwd(const int* idx, const float* vals, const float* tv, const float* tw,
                          const float* bias, int B, int F, int KP, float* y_fm, float* S, bf16* E,
-                         bf16* Et, long ldv, long ldw, hipStream_t st) {
+                         bf16* Et, uint8_t* E8, float* sE, long ldv, long ldw, hipStream_t st) {
   constexpr int SB = 256 / K;
-  const size_t lds2 = ((size_t)SB * (F * K + 1) + (size_t)SB * F) * 4;
+  const size_t lds2 = ((size_t)SB * (F * K + 1) + (size_t)SB * F + SB) * 4;
   if (lds2 <= 120 * 1024) {
     const int grid = (B + SB - 1) / SB;
     hipLaunchKernelGGL(fm_fwd2_kernel<K>, dim3(grid), dim3(256), lds2, st, idx, vals, tv, tw, bias,
-                       B, F, KP, y_fm, S, E, Et, ldv, ldw);
+                       B, F, KP, y_fm, S, E, Et, E8, sE, ldv, ldw);
     HFM_LAUNCH_CHECK();
   }
+  if (E8 || !E) return (int)hipErrorInvalidValue;  // fp8 output: only the row-tile variant
   // very wide inputs (F*K > ~30K): lane-group-per-sample variant, small LDS footprint
   constexpr int LPS = K / 4;
   constexpr int SB1 = 256 / LPS;
@@ -232,10 +255,12 @@ static int launch_fm_bwd(const int* perm, const int* idx, const float* vals, con
 
 HFM_API int hfm_fm_fwd(const int* idx, const float* vals, const float* tv, const float* tw,
                        const float* bias, int B, int F, int K, int KP, float* y_fm, float* S,
-                       void* E, void* Et, long ldv, long ldw, hipStream_t st) {
+                       void* E, void* Et, void* E8, float* sE, long ldv, long ldw, hipStream_t st) {
   // ldv / ldw: floats between consecutive rows of the v table and entries of the w table
-  // (K and 1 for plain tables; the record stride for the interleaved row-record layout)
-#define CALL(KK) launch_fm_fwd<KK>(idx, vals, tv, tw, bias, B, F, KP, y_fm, S, (bf16*)E, (bf16*)Et, ldv, ldw, st)
+  // (K and 1 for plain tables; the record stride for the interleaved row-record layout).
+  // E8 / sE (optional): the MLP input as OCP fp8 e4m3 rows with per-row dequant factors
+  // (mlp_dtype = fp8); E may then be null.
+#define CALL(KK) launch_fm_fwd<KK>(idx, vals, tv, tw, bias, B, F, KP, y_fm, S, (bf16*)E, (bf16*)Et, (uint8_t*)E8, sE, ldv, ldw, st)
   HFM_K_DISPATCH(K, CALL)
 #undef CALL
 }

@@ -51,6 +51,15 @@ struct TowerArgs {
   int h_off[TW_MAXL];             // LDS element offsets of the H tiles
   int dz_off[2];                  // LDS element offsets of the two dZ tiles
   int lds_bytes;
+  // fp8 forward (mlp_dtype = fp8): every forward GEMM on v_mfma_f32_16x16x32_fp8_fp8 with OCP
+  // e4m3 operands — E8 rows (fm_fwd) / H rows (quantized from the LDS tile) with per-row
+  // power-of-two scales, W8 with per-output-channel scales — dequantized in the fp32 epilogue.
+  // The backward (dgrad chain, wgrad) stays bf16.
+  int fp8;
+  const uint8_t* E8;              // [M, K0p]
+  const float* sE;                // [M]     row dequant factors of E8
+  const uint8_t* W8[TW_MAXL];     // [Np_i, Kp_i]
+  const float* sW[TW_MAXL];       // [Np_i]  channel dequant factors of W8
 };
 
 // One wave: c[2][2] += A[32 x 32*nk] . B[32 x 32*nk]^T, both K-contiguous (row strides lda/ldb
@@ -95,6 +104,78 @@ __device__ __forceinline__ void mma32(const bf16* __restrict__ A, int lda, const
   }
 }
 
+// fp8 variant of mma32 (16x16x32 fp8 MFMA; same fragment map as bf16 with 8 one-byte elements
+// per lane): A and B are e4m3 rows in global memory (row strides in bytes).
+template <int PF>
+__device__ __forceinline__ void mma32_f8(const uint8_t* __restrict__ A, int lda, const uint8_t* __restrict__ B,
+                                         int ldb, int nk, int lane, f32x4& c00, f32x4& c01, f32x4& c10,
+                                         f32x4& c11) {
+  const int r = lane & 15, kq = (lane >> 4) * 8;
+  const uint8_t* a0 = A + r * lda + kq;
+  const uint8_t* a1 = a0 + 16 * lda;
+  const uint8_t* b0 = B + r * ldb + kq;
+  const uint8_t* b1 = b0 + 16 * ldb;
+  long ra0[PF], ra1[PF], rb0[PF], rb1[PF];
+#pragma unroll
+  for (int j = 0; j < PF; ++j) {
+    if (j < nk) {
+      ra0[j] = *reinterpret_cast<const long*>(a0 + j * 32);
+      ra1[j] = *reinterpret_cast<const long*>(a1 + j * 32);
+      rb0[j] = *reinterpret_cast<const long*>(b0 + j * 32);
+      rb1[j] = *reinterpret_cast<const long*>(b1 + j * 32);
+    }
+  }
+  for (int kb = 0; kb < nk; kb += PF) {
+#pragma unroll
+    for (int j = 0; j < PF; ++j) {
+      const int ks = kb + j;
+      if (ks < nk) {
+        c00 = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(ra0[j], rb0[j], c00, 0, 0, 0);
+        c01 = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(ra0[j], rb1[j], c01, 0, 0, 0);
+        c10 = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(ra1[j], rb0[j], c10, 0, 0, 0);
+        c11 = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(ra1[j], rb1[j], c11, 0, 0, 0);
+        const int kn = (ks + PF) * 32;
+        if (ks + PF < nk) {
+          ra0[j] = *reinterpret_cast<const long*>(a0 + kn);
+          ra1[j] = *reinterpret_cast<const long*>(a1 + kn);
+          rb0[j] = *reinterpret_cast<const long*>(b0 + kn);
+          rb1[j] = *reinterpret_cast<const long*>(b1 + kn);
+        }
+      }
+    }
+  }
+}
+
+// 8 bf16 LDS elements * q -> one fp8 A fragment (8 e4m3 bytes)
+__device__ __forceinline__ long lds_to_fp8x8(const bf16* p, float q) {
+  const bf16x8 v = *reinterpret_cast<const bf16x8*>(p);
+  const uint32_t lo = pack4_fp8(bf2f(v[0]) * q, bf2f(v[1]) * q, bf2f(v[2]) * q, bf2f(v[3]) * q);
+  const uint32_t hi = pack4_fp8(bf2f(v[4]) * q, bf2f(v[5]) * q, bf2f(v[6]) * q, bf2f(v[7]) * q);
+  return (long)(((unsigned long)hi << 32) | lo);
+}
+
+// fp8 GEMM with the A operand quantized on the fly from a bf16 LDS tile (row r scaled by q[r])
+__device__ __forceinline__ void mma32_f8_lds(const bf16* A, int lda, const float* q,
+                                             const uint8_t* __restrict__ B, int ldb, int nk, int lane,
+                                             f32x4& c00, f32x4& c01, f32x4& c10, f32x4& c11) {
+  const int r = lane & 15, kq = (lane >> 4) * 8;
+  const bf16* a0 = A + r * lda + kq;
+  const bf16* a1 = a0 + 16 * lda;
+  const float q0 = q[r], q1 = q[r + 16];
+  const uint8_t* b0 = B + r * ldb + kq;
+  const uint8_t* b1 = b0 + 16 * ldb;
+  for (int ks = 0; ks < nk; ++ks) {
+    const long ra0 = lds_to_fp8x8(a0 + ks * 32, q0);
+    const long ra1 = lds_to_fp8x8(a1 + ks * 32, q1);
+    const long rb0 = *reinterpret_cast<const long*>(b0 + ks * 32);
+    const long rb1 = *reinterpret_cast<const long*>(b1 + ks * 32);
+    c00 = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(ra0, rb0, c00, 0, 0, 0);
+    c01 = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(ra0, rb1, c01, 0, 0, 0);
+    c10 = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(ra1, rb0, c10, 0, 0, 0);
+    c11 = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(ra1, rb1, c11, 0, 0, 0);
+  }
+}
+
 // Copy a [32 x N] bf16 LDS tile (row stride ld) to its transpose in global memory:
 // out[c * M + row0 + r]; each thread moves 8 consecutive rows of one column (16-B stores).
 __device__ __forceinline__ void store_tile_t(const bf16* t, int ld, int N, bf16* out, int M, int row0) {
@@ -107,11 +188,14 @@ __device__ __forceinline__ void store_tile_t(const bf16* t, int ld, int N, bf16*
   }
 }
 
+template <bool FP8>
 __global__ void __launch_bounds__(256) tower_kernel(TowerArgs a) {
   extern __shared__ __align__(16) unsigned char tw_lds_raw[];
   bf16* lds = reinterpret_cast<bf16*>(tw_lds_raw);
   __shared__ float s_dl[TW_ROWS];
   __shared__ float s_loss[TW_ROWS];
+  __shared__ float s_q[TW_ROWS];   // fp8: quantization scales of the current H rows
+  __shared__ float s_dq[TW_ROWS];  //      and their inverses
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int row0 = blockIdx.x * TW_ROWS;
   const int cr = (lane >> 4) * 4, cc = lane & 15;
@@ -129,11 +213,19 @@ __global__ void __launch_bounds__(256) tower_kernel(TowerArgs a) {
     const float sc = a.inv_keep[i];
     for (int ct = wave; ct < N / 32; ct += 4) {
       f32x4 c00 = {0, 0, 0, 0}, c01 = c00, c10 = c00, c11 = c00;
-      const bf16* Bw = a.W[i] + (size_t)ct * 32 * Kp;
-      if (i == 0)
-        mma32<4>(a.E + (size_t)row0 * a.K0p, a.K0p, Bw, Kp, Kp / 32, lane, c00, c01, c10, c11);
-      else
-        mma32<2>(lds + a.h_off[i - 1], Kp + 8, Bw, Kp, Kp / 32, lane, c00, c01, c10, c11);
+      if (FP8) {
+        const uint8_t* Bw8 = a.W8[i] + (size_t)ct * 32 * Kp;
+        if (i == 0)
+          mma32_f8<4>(a.E8 + (size_t)row0 * a.K0p, a.K0p, Bw8, Kp, Kp / 32, lane, c00, c01, c10, c11);
+        else
+          mma32_f8_lds(lds + a.h_off[i - 1], Kp + 8, s_q, Bw8, Kp, Kp / 32, lane, c00, c01, c10, c11);
+      } else {
+        const bf16* Bw = a.W[i] + (size_t)ct * 32 * Kp;
+        if (i == 0)
+          mma32<4>(a.E + (size_t)row0 * a.K0p, a.K0p, Bw, Kp, Kp / 32, lane, c00, c01, c10, c11);
+        else
+          mma32<2>(lds + a.h_off[i - 1], Kp + 8, Bw, Kp, Kp / 32, lane, c00, c01, c10, c11);
+      }
       f32x4 acc[2][2] = {{c00, c01}, {c10, c11}};
 #pragma unroll
       for (int ti = 0; ti < 2; ++ti) {
@@ -141,10 +233,12 @@ __global__ void __launch_bounds__(256) tower_kernel(TowerArgs a) {
         for (int tj = 0; tj < 2; ++tj) {
           const int col = ct * 32 + tj * 16 + cc;
           const float bc = a.bias[i][col];
+          const float dqc = FP8 ? a.sW[i][col] : 1.f;
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             const int row = ti * 16 + cr + j;
-            float v = fmaxf(acc[ti][tj][j] + bc, 0.f);
+            const float dq = FP8 ? dqc * (i == 0 ? a.sE[row0 + row] : s_dq[row]) : 1.f;
+            float v = fmaxf(acc[ti][tj][j] * dq + bc, 0.f);
             if (drop)
               v = dropout_keep((uint32_t)((row0 + row) * N + col), salt, a.keep_thr[i]) ? v * sc : 0.f;
             Hl[row * ldh + col] = f2bf(v);
@@ -154,6 +248,20 @@ __global__ void __launch_bounds__(256) tower_kernel(TowerArgs a) {
     }
     __syncthreads();
     if (a.train) store_tile_t(Hl, ldh, N, a.Ht[i], a.M, row0);
+    if (FP8 && i + 1 < nl) {  // per-row scales of H_i, the next layer's fp8 A operand
+      const int r = tid >> 3, q8 = tid & 7;
+      float m = 0.f;
+      for (int c = q8; c < N; c += 8) m = fmaxf(m, fabsf(bf2f(Hl[r * ldh + c])));
+      m = fmaxf(m, __shfl_xor(m, 1, 64));
+      m = fmaxf(m, __shfl_xor(m, 2, 64));
+      m = fmaxf(m, __shfl_xor(m, 4, 64));
+      if (q8 == 0) {
+        const float q = fp8_pow2_scale(m);
+        s_q[r] = q;
+        s_dq[r] = 1.f / q;
+      }
+      __syncthreads();
+    }
   }
 
   // ------------------------------------------------------------------ head
@@ -277,9 +385,58 @@ HFM_API int hfm_tower(const TowerArgs* ap, hipStream_t st) {
     if (a.Np[i] % 32 || a.Np[i] <= 0) return (int)hipErrorInvalidValue;
   if (a.Np[a.nl - 1] % 8) return (int)hipErrorInvalidValue;
   if (a.lds_bytes > 160 * 1024 - 1024) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(tower_kernel, dim3(a.M / TW_ROWS), dim3(256), a.lds_bytes, st, a);
+  if (a.fp8) {
+    if (!a.E8 || !a.sE) return (int)hipErrorInvalidValue;
+    for (int i = 0; i < a.nl; ++i)
+      if (!a.W8[i] || !a.sW[i]) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(tower_kernel<true>, dim3(a.M / TW_ROWS), dim3(256), a.lds_bytes, st, a);
+  } else {
+    hipLaunchKernelGGL(tower_kernel<false>, dim3(a.M / TW_ROWS), dim3(256), a.lds_bytes, st, a);
+  }
   HFM_LAUNCH_CHECK();
 }
+
+// ---------------------------------------------------------------------------------------------
+// fp8 weight shadows: W8[r, :] = e4m3(W[r, :] * q_r), sW[r] = 1 / q_r with a power-of-two q_r
+// from the row's absolute max (per output channel), from the fp32 master weights.  One wave per
+// row of every layer, one launch (run after each dense optimizer update and after loads).
+struct W8Job {
+  const float* src;  // [rows, cols] fp32 (the flat parameter buffer segment)
+  uint8_t* dst;      // [rows, cols]
+  float* sdq;        // [rows]
+  int rows, cols;
+  int row0;          // first global row of this job
+  int pad;
+};
+
+__global__ void __launch_bounds__(256) w8_quant_kernel(const W8Job* __restrict__ jobs, int njobs, int total) {
+  const int grow = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (grow >= total) return;
+  int j = 0;
+  while (j + 1 < njobs && grow >= jobs[j + 1].row0) ++j;
+  const W8Job jb = jobs[j];
+  const int r = grow - jb.row0;
+  const float* src = jb.src + (size_t)r * jb.cols;
+  float m = 0.f;
+  for (int c = lane; c < jb.cols; c += 64) m = fmaxf(m, fabsf(src[c]));
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  const float q = fp8_pow2_scale(m);
+  uint8_t* dst = jb.dst + (size_t)r * jb.cols;
+  for (int c4 = lane; c4 < jb.cols / 4; c4 += 64) {
+    const float* s4 = src + 4 * c4;
+    *reinterpret_cast<uint32_t*>(dst + 4 * c4) = pack4_fp8(s4[0] * q, s4[1] * q, s4[2] * q, s4[3] * q);
+  }
+  if (lane == 0) jb.sdq[r] = 1.f / q;
+}
+
+HFM_API int hfm_w8_quant(const void* jobs_dev, int njobs, int total_rows, hipStream_t st) {
+  if (total_rows <= 0) return 0;
+  hipLaunchKernelGGL(w8_quant_kernel, dim3((total_rows + 3) / 4), dim3(256), 0, st,
+                     (const W8Job*)jobs_dev, njobs, total_rows);
+  HFM_LAUNCH_CHECK();
+}
+HFM_API int hfm_w8_job_bytes() { return (int)sizeof(W8Job); }
 HFM_API int hfm_tower_args_bytes() { return (int)sizeof(TowerArgs); }
 
 // ---------------------------------------------------------------------------------------------

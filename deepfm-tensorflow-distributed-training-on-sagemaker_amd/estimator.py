@@ -89,7 +89,8 @@ class Estimator:
                                       optimizer=cfg.optimizer, loss_type=cfg.loss_type,
                                       sparse_update=cfg.sparse_update, seed=cfg.seed,
                                       batch_size=cfg.batch_size, device=self.device, comm=self.comm,
-                                      batch_norm=cfg.batch_norm, batch_norm_decay=cfg.batch_norm_decay)
+                                      batch_norm=cfg.batch_norm, batch_norm_decay=cfg.batch_norm_decay,
+                                      mlp_dtype=cfg.mlp_dtype)
         else:
             from .models.reference import GoldenDeepFM
             self.model = GoldenDeepFM(cfg.feature_size, cfg.field_size, cfg.embedding_size, cfg.layers,
@@ -167,6 +168,7 @@ class Estimator:
                 dist.broadcast(t, src=0)
         if self.native:
             self.model._host_step = None      # step counter came from rank 0
+            self.model.refresh_shadows()      # bf16 / fp8 weight copies of the broadcast params
         if not self.native:
             gs = torch.tensor([int(self.model.global_step)], dtype=torch.int64)
             dist.broadcast(gs, src=0)

@@ -33,7 +33,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import torch
 
 from ..ops import kernels as KN
-from ..ops._lib import TW_MAXL, BnArgs, EpiArgs, HeadArgs, TowerArgs, WgJob, RowSumJob, SegApplyArgs, SfArgs, ShadowSeg, SlabJob
+from ..ops._lib import TW_MAXL, BnArgs, EpiArgs, HeadArgs, TowerArgs, W8Job, WgJob, RowSumJob, SegApplyArgs, SfArgs, ShadowSeg, SlabJob
 from ..utils.rng import keep_threshold
 from .reference import glorot_std, init_params, pad32
 
@@ -147,9 +147,14 @@ class NativeDeepFM:
                  device="cuda", comm=None, init: bool = True, batch_norm: bool = False,
                  batch_norm_decay: float = 0.9, adam_epsilon: float = 1e-8,
                  adagrad_init: float = 1e-8, fused: Optional[bool] = None,
-                 field_ranges: Optional[Sequence[Tuple[int, int]]] = None):
+                 field_ranges: Optional[Sequence[Tuple[int, int]]] = None, mlp_dtype: str = "bf16"):
         self.batch_norm = bool(batch_norm)
         self.bn_decay = float(batch_norm_decay)
+        if mlp_dtype not in ("bf16", "fp8"):
+            raise ValueError(f"mlp_dtype must be bf16 or fp8, got {mlp_dtype!r}")
+        # fp8: the deep tower's forward GEMMs take OCP e4m3 operands (per-row / per-channel
+        # power-of-two scales, fp32 accumulation); backward and master weights stay bf16 / fp32
+        self.fp8 = mlp_dtype == "fp8"
         self.bn_eps = 1e-3          # tf.contrib.layers.batch_norm default epsilon (PS:289)
         self.V, self.F, self.K = int(feature_size), int(field_size), int(embedding_size)
         if self.K not in (4, 8, 16, 32, 64):
@@ -255,6 +260,20 @@ class NativeDeepFM:
             shadow.append(ShadowSeg(s.off, self.Np[i], self.Kp[i], w16.data_ptr(), wt16.data_ptr()))
         self._shadow_dev = KN.struct_array_to_device(shadow, dev)
         self._nshadow = len(shadow)
+        self.W8, self.sW = [], []
+        if self.fp8:
+            jobs, row0 = [], 0
+            for i in range(len(self.layers)):
+                s = self.dense_segs[f"Deep-part/mlp{i}/weights"]
+                w8 = torch.zeros(self.Np[i], self.Kp[i], dtype=torch.uint8, device=dev)
+                sw = torch.ones(self.Np[i], dtype=torch.float32, device=dev)
+                self.W8.append(w8)
+                self.sW.append(sw)
+                jobs.append(W8Job(self.p.data_ptr() + 4 * s.off, w8.data_ptr(), sw.data_ptr(),
+                                  self.Np[i], self.Kp[i], row0, 0))
+                row0 += self.Np[i]
+            self._w8_jobs = KN.struct_array_to_device(jobs, dev)
+            self._w8_rows = row0
         self.h_sparse = KN.hyper(self.lr, self.l2, eps=adam_epsilon)
         self.h_dense = KN.hyper(self.lr, 0.0, eps=adam_epsilon)
         self._bufs_M = 0
@@ -270,6 +289,9 @@ class NativeDeepFM:
                     self._tower_lds_bytes() <= 150 * 1024)
         want = os.environ.get("HIPFM_FUSED_TOWER", "1") != "0" if fused is None else bool(fused)
         self.fused = can_fuse and want
+        if self.fp8 and not self.fused:
+            raise ValueError("mlp_dtype=fp8 runs on the fused tower kernel (no batch norm, "
+                             "activations within LDS)")
         if init:
             if self.V * self.K <= (1 << 24):
                 # small tables: the exact golden initialization (CPU generator, bit-reproducible)
@@ -339,6 +361,9 @@ class NativeDeepFM:
         self.S = torch.zeros(M, K, **f32)
         self.E = torch.zeros(M, K0p, **bf)
         self.Et = torch.zeros(K0p, M, **bf)
+        if self.fp8:
+            self.E8 = torch.zeros(M, K0p, dtype=torch.uint8, device=dev)
+            self.sE = torch.ones(M, **f32)
         self.H = [torch.zeros(M, n, **bf) for n in self.Np]
         self.Ht = [torch.zeros(n, M, **bf) for n in self.Np]
         self.dZ = [torch.zeros(M, n, **bf) for n in self.Np]
@@ -491,6 +516,11 @@ class NativeDeepFM:
         a.dz_off[1] = off + 32 * (max(self.Np) + 8)
         a.lds_bytes = self._tower_lds_bytes()
         a.E = self.E.data_ptr()
+        if self.fp8:
+            a.fp8 = 1
+            a.E8, a.sE = self.E8.data_ptr(), self.sE.data_ptr()
+            for i in range(nl):
+                a.W8[i], a.sW[i] = self.W8[i].data_ptr(), self.sW[i].data_ptr()
         a.seed = self.seed & 0xFFFFFFFF
         a.train = 1 if train else 0
         a.square_loss = 1 if self.loss_type == "square_loss" else 0
@@ -583,6 +613,8 @@ class NativeDeepFM:
 
     def refresh_shadows(self):
         KN.shadow_refresh(self.p, self.P, self._shadow_dev, self._nshadow)
+        if self.fp8:
+            KN.w8_quant(self._w8_jobs, len(self.layers), self._w8_rows)
 
     # ------------------------------------------------------------------ batch staging
     def stage_batch(self, ids: torch.Tensor, vals: torch.Tensor, labels: Optional[torch.Tensor]):
@@ -612,8 +644,12 @@ class NativeDeepFM:
         elif self.sharded:
             idx, tv, tw = self.comm.sharded_forward_gather(self, B)
         fm_bias = self.p[self.dense_segs["fm_bias"].off:]
-        KN.fm_fwd(idx, self.vals, tv, tw, fm_bias, M, F, K, self.K0p, self.y_fm, self.S, self.E,
-                  self.Et if train else None)
+        if self.fp8:
+            KN.fm_fwd(idx, self.vals, tv, tw, fm_bias, M, F, K, self.K0p, self.y_fm, self.S, None,
+                      self.Et if train else None, E8=self.E8, sE=self.sE)
+        else:
+            KN.fm_fwd(idx, self.vals, tv, tw, fm_bias, M, F, K, self.K0p, self.y_fm, self.S, self.E,
+                      self.Et if train else None)
         return idx, tv
 
     def _forward(self, B: int, train: bool):
@@ -915,6 +951,8 @@ class NativeDeepFM:
         else:
             KN.dense_opt(self.opt_id, self.p, self.g, self.sd[0], self.sd[1], self.P, self.h_dense,
                          self.step, self._shadow_dev, self._nshadow, done_ctr=self._done_ctr)
+        if self.fp8:
+            KN.w8_quant(self._w8_jobs, len(self.layers), self._w8_rows)
 
     def _shx_start(self, B: int):
         """Row-sharded step start: routing plan (inline unless prefetched by the previous step)

@@ -108,7 +108,14 @@ class TowerArgs(C.Structure):
                 ("w_out", c_void_p), ("b_out", c_void_p), ("y_fm", c_void_p), ("labels", c_void_p),
                 ("Ht", c_void_p * TW_MAXL), ("dZt", c_void_p * TW_MAXL), ("dX0", c_void_p),
                 ("prob", c_void_p), ("dlogit", c_void_p), ("partial", c_void_p),
-                ("h_off", c_int * TW_MAXL), ("dz_off", c_int * 2), ("lds_bytes", c_int)]
+                ("h_off", c_int * TW_MAXL), ("dz_off", c_int * 2), ("lds_bytes", c_int),
+                ("fp8", c_int), ("E8", c_void_p), ("sE", c_void_p), ("W8", c_void_p * TW_MAXL),
+                ("sW", c_void_p * TW_MAXL)]
+
+
+class W8Job(C.Structure):
+    _fields_ = [("src", c_void_p), ("dst", c_void_p), ("sdq", c_void_p), ("rows", c_int),
+                ("cols", c_int), ("row0", c_int), ("pad", c_int)]
 
 
 class WgJob(C.Structure):
@@ -118,7 +125,7 @@ class WgJob(C.Structure):
 
 
 _SIGS = {
-    "hfm_fm_fwd": [c_void_p] * 5 + [c_int] * 4 + [c_void_p] * 4 + [c_long, c_long, c_void_p],
+    "hfm_fm_fwd": [c_void_p] * 5 + [c_int] * 4 + [c_void_p] * 6 + [c_long, c_long, c_void_p],
     "hfm_fm_bwd_sorted": [c_void_p] * 7 + [c_int] * 4 + [c_void_p, c_void_p],
     "hfm_grad_row_bytes": [c_int],
     "hfm_sort_pairs_temp_bytes": [c_int, c_int, C.POINTER(c_size_t)],
@@ -186,6 +193,8 @@ _SIGS = {
     "hfm_tower_args_bytes": [],
     "hfm_wgrad_group": [c_void_p, c_int, c_int, c_void_p],
     "hfm_wg_job_bytes": [],
+    "hfm_w8_quant": [c_void_p, c_int, c_int, c_void_p],
+    "hfm_w8_job_bytes": [],
     "hfm_bn_args_bytes": [],
 }
 
@@ -221,6 +230,7 @@ def get_lib():
                            ("hfm_shadow_seg_bytes", ShadowSeg), ("hfm_opt_hyper_bytes", OptHyper),
                            ("hfm_seg_apply_args_bytes", SegApplyArgs), ("hfm_bn_args_bytes", BnArgs),
                            ("hfm_tower_args_bytes", TowerArgs), ("hfm_wg_job_bytes", WgJob),
+                           ("hfm_w8_job_bytes", W8Job),
                            ("hfm_sparse_fused_args_bytes", SfArgs),
                            ("hfm_sh_apply_args_bytes", ShApplyArgs)):
             n = getattr(lib, cname)()

@@ -12,7 +12,7 @@ from typing import List, Optional, Sequence
 import torch
 
 from . import _lib
-from ._lib import (BnArgs, EpiArgs, HeadArgs, TowerArgs, WgJob, OptHyper, RowSumJob, SegApplyArgs, SfArgs, ShApplyArgs, ShadowSeg, SlabJob, check,
+from ._lib import (BnArgs, EpiArgs, HeadArgs, TowerArgs, W8Job, WgJob, OptHyper, RowSumJob, SegApplyArgs, SfArgs, ShApplyArgs, ShadowSeg, SlabJob, check,
                    ptr, stream_handle)
 
 EPI_F32, EPI_FWD, EPI_DGRAD, EPI_FWD_EVAL, EPI_RELU_F32 = 0, 1, 2, 3, 4
@@ -34,10 +34,15 @@ def _ld(tv, tw):
     return ldv, ldw
 
 
-def fm_fwd(idx, vals, tv, tw, bias, B, F, K, KP, y_fm, S, E, Et):
+def fm_fwd(idx, vals, tv, tw, bias, B, F, K, KP, y_fm, S, E, Et, E8=None, sE=None):
+    """FM forward (y_fm, S) + the MLP input: E (bf16 [B, KP]) and/or E8 (OCP fp8 e4m3 rows,
+    per-row dequant factors sE) for the fp8 tower; Et (bf16 [KP, B]) for the weight gradient."""
     assert tv.stride(-1) == 1
+    if E8 is not None:
+        assert E8.dtype == torch.uint8 and E8.is_contiguous() and sE is not None
     check(L().hfm_fm_fwd(ptr(idx), ptr(vals), ptr(tv), ptr(tw), ptr(bias), B, F, K, KP, ptr(y_fm),
-                         ptr(S), ptr(E), ptr(Et), *_ld(tv, tw), stream_handle()), "fm_fwd")
+                         ptr(S), ptr(E), ptr(Et), ptr(E8), ptr(sE), *_ld(tv, tw), stream_handle()),
+          "fm_fwd")
 
 
 def fm_bwd_sorted(perm, idx, vals, tv, dlogit, dX0, S, n, F, K, KP, G):
@@ -259,6 +264,11 @@ def head(a: HeadArgs):
 def tower(a: TowerArgs):
     """Fused deep tower: forward + head (+ dgrad chain when a.train) (csrc/kernels/tower.hip)."""
     check(L().hfm_tower(C.byref(a), stream_handle()), "tower")
+
+
+def w8_quant(jobs_dev, njobs: int, total_rows: int):
+    """fp8 e4m3 weight shadows with per-output-channel power-of-two scales (tower.hip)."""
+    check(L().hfm_w8_quant(ptr(jobs_dev), njobs, total_rows, stream_handle()), "w8_quant")
 
 
 def wgrad_group(jobs_dev, njobs: int, ntasks: int):
