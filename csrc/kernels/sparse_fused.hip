@@ -257,26 +257,65 @@ __global__ void __launch_bounds__(256) sf_tile_kernel(SfArgs A) {
   }
 }
 
+// One wave per tile: the tile's open run (if any) = ctail[t] + lead[t+1] + ... + lead[t_end],
+// t_end = the first following tile that holds a head.  The 64 lanes read 64 following tiles'
+// leads at once and the run total is a fixed butterfly over lanes (then window order), so long
+// runs (Criteo's 13 integer fields span every tile) cost one parallel read per 64 tiles instead
+// of a serial chain of dependent loads.  Fixed order: still bitwise reproducible.
 template <int K, int MODE, int OPT>
 __global__ void __launch_bounds__(256) sf_carry_kernel(SfArgs A, int ntiles) {
   using T = SfCfg<K>;
-  const int gt = blockIdx.x * blockDim.x + threadIdx.x;
-  const int t = gt / T::LPS, sub = gt % T::LPS;
+  constexpr int NV = T::RS / 4;  // f32x4 per lead row: a[K], w, c, pad, pad
+  const int t = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (t >= ntiles) return;
   const int key = A.tinfo[t * 4 + 1];
-  if (key < 0) return;
+  if (key < 0) return;  // wave-uniform
   const int hpos = A.tinfo[t * 4 + 2];
-  const float* ct = A.ctail + (size_t)t * T::RS;
-  f32x4 a = *reinterpret_cast<const f32x4*>(ct + sub * 4);
-  float w = ct[K], c = ct[K + 1];
-  for (int t2 = t + 1; t2 < ntiles; ++t2) {
-    const float* ld = A.lead + (size_t)t2 * T::RS;
-    a += *reinterpret_cast<const f32x4*>(ld + sub * 4);
-    w += ld[K];
-    c += ld[K + 1];
-    if (!A.tinfo[t2 * 4]) break;
+  f32x4 tot[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) tot[v] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int base = t + 1; base < ntiles; base += 64) {
+    const int t2 = base + lane;
+    const bool valid = t2 < ntiles;
+    const bool has_head = valid && !A.tinfo[t2 * 4];
+    const unsigned long long stop = __ballot(has_head);
+    const int last = stop ? __ffsll((long long)stop) - 1 : 63;  // last lane whose lead is included
+    f32x4 p[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      p[v] = (valid && lane <= last)
+                 ? *reinterpret_cast<const f32x4*>(A.lead + (size_t)t2 * T::RS + 4 * v)
+                 : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) {
+        p[v][0] += __shfl_xor(p[v][0], o, 64);
+        p[v][1] += __shfl_xor(p[v][1], o, 64);
+        p[v][2] += __shfl_xor(p[v][2], o, 64);
+        p[v][3] += __shfl_xor(p[v][3], o, 64);
+      }
+      tot[v] += p[v];
+    }
+    if (stop) break;
   }
-  sf_apply_row<K, MODE, OPT>(A, key, hpos, sub, a, w, c, sf_lr_t<OPT>(A));
+  const int sub = lane;
+  if (sub >= T::LPS) return;
+  const float* ct = A.ctail + (size_t)t * T::RS;
+  f32x4 av = *reinterpret_cast<const f32x4*>(ct + sub * 4);
+  float w = ct[K], c = ct[K + 1];
+  f32x4 ad = {0.f, 0.f, 0.f, 0.f};
+  float wd = 0.f, cd = 0.f;
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    if (v == sub) ad = tot[v];
+    if (v == K / 4) {
+      wd = tot[v][0];
+      cd = tot[v][1];
+    }
+  }
+  av += ad;
+  w += wd;
+  c += cd;
+  sf_apply_row<K, MODE, OPT>(A, key, hpos, sub, av, w, c, sf_lr_t<OPT>(A));
 }
 
 HFM_API int hfm_sparse_fused_tiles(int K, int n) {
@@ -289,8 +328,7 @@ static void sf_launch(const SfArgs& A, hipStream_t st) {
   using T = SfCfg<K>;
   const int tiles = (A.n + T::TP - 1) / T::TP;
   hipLaunchKernelGGL((sf_tile_kernel<K, MODE, OPT>), dim3(tiles), dim3(256), 0, st, A);
-  const int cg = (tiles * T::LPS + 255) / 256;
-  hipLaunchKernelGGL((sf_carry_kernel<K, MODE, OPT>), dim3(cg), dim3(256), 0, st, A, tiles);
+  hipLaunchKernelGGL((sf_carry_kernel<K, MODE, OPT>), dim3((tiles + 3) / 4), dim3(256), 0, st, A, tiles);
 }
 
 template <int K>

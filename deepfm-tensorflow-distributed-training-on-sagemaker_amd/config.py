@@ -91,7 +91,6 @@ _DEFS = [
     ("sparse_update", str, "tf1_dense", "tf1_dense (reference non-lazy semantics: every row moves "
      "every step, full-table L2) | lazy (touched rows only)"),
     ("mlp_dtype", str, "bf16", "bf16 | fp8 (deep-part GEMM input precision; accumulation is fp32)"),
-    ("table_dtype", str, "fp32", "fp32 | bf16 (embedding storage; optimizer state stays fp32)"),
     ("save_checkpoints_steps", int, 0, "checkpoint every N steps (0: use save_checkpoints_secs)"),
     ("save_checkpoints_secs", int, 600, "checkpoint every N seconds (TF Estimator default 600)"),
     ("keep_checkpoint_max", int, 5, "checkpoints to keep (TF default 5)"),
@@ -151,7 +150,6 @@ class RunConfig:
     embedding_mode: str = "auto"
     sparse_update: str = "tf1_dense"
     mlp_dtype: str = "bf16"
-    table_dtype: str = "fp32"
     save_checkpoints_steps: int = 0
     save_checkpoints_secs: int = 600
     keep_checkpoint_max: int = 5
@@ -201,6 +199,8 @@ class RunConfig:
             raise ValueError(f"unknown loss_type {self.loss_type!r}")
         if self.sparse_update not in ("tf1_dense", "lazy"):
             raise ValueError(f"unknown sparse_update {self.sparse_update!r}")
+        if self.mlp_dtype not in ("bf16", "fp8"):
+            raise ValueError(f"unknown mlp_dtype {self.mlp_dtype!r} (bf16 | fp8)")
         if self.embedding_mode not in ("auto", "replicated", "sharded"):
             raise ValueError(f"unknown embedding_mode {self.embedding_mode!r}")
         kp = self.keep_probs
