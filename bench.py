@@ -30,6 +30,116 @@ if REPO not in sys.path:
 
 METRIC = ("samples/sec (whole node) + eval AUC, Criteo-1TB-shape DeepFM at 1/2/4/8 MI355X")
 
+# Multi-GPU execution ladder (bench supervisor, below): the fastest path first, then paths with
+# fewer moving parts.  Every rung is the same full training step (same model, optimizer, data).
+LADDER = [
+    ("graph+prefetch", {}),                                  # HIP graphs, next-batch routing prefetch
+    ("eager+prefetch", {"HIPFM_BENCH_NO_GRAPH": "1"}),       # same collectives, launched eagerly
+    ("eager", {"HIPFM_BENCH_NO_GRAPH": "1", "HIPFM_SHARD_PIPELINE": "0"}),
+]
+
+
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def supervise(argv) -> int:
+    """Multi-rank supervisor (one per torchrun worker; never touches the GPU).
+
+    Runs the benchmark in a child process per rung of LADDER.  If any rank's child fails (non-zero
+    exit) or stops making progress (no progress-file update for HIPFM_BENCH_HANG_S seconds), every
+    rank kills its child and the job moves to the next rung on a fresh rendezvous port, so one
+    misbehaving execution mode costs a retry instead of the whole measurement.  Ranks coordinate
+    through torchrun's agent store (keys ``hipfm_bench/*``).  Returns the exit code."""
+    import signal
+    import subprocess
+    import tempfile
+    import time
+
+    import torch.distributed as dist
+
+    rank = int(os.environ["RANK"])
+    world = int(os.environ["WORLD_SIZE"])
+    store = dist.TCPStore(os.environ.get("MASTER_ADDR", "127.0.0.1"), int(os.environ["MASTER_PORT"]),
+                          world, is_master=False, timeout=__import__("datetime").timedelta(seconds=600))
+    hang_s = float(os.environ.get("HIPFM_BENCH_HANG_S", "240"))
+    ladder = LADDER[int(os.environ.get("HIPFM_BENCH_FIRST_RUNG", "0")):]
+    for k, (name, extra) in enumerate(ladder):
+        if rank == 0:
+            store.set(f"hipfm_bench/port{k}", str(_free_port()))
+        port = store.get(f"hipfm_bench/port{k}").decode()
+        prog = os.path.join(tempfile.gettempdir(), f"hipfm_bench_progress_{os.getpid()}_{k}")
+        result = os.path.join(tempfile.gettempdir(), f"hipfm_bench_result_{os.getpid()}_{k}.json")
+        env = dict(os.environ, HIPFM_BENCH_CHILD="1", HIPFM_BENCH_RUNG=name, MASTER_PORT=port,
+                   TORCHELASTIC_USE_AGENT_STORE="False", HIPFM_BENCH_PROGRESS=prog,
+                   HIPFM_BENCH_RESULT=result, **extra)
+        child = subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env,
+                                 start_new_session=True)
+        failed = False
+        last = time.time()
+        while True:
+            rc = child.poll()
+            if rc is not None:
+                failed = rc != 0
+                break
+            if store.check([f"hipfm_bench/fail{k}"]):
+                failed = True
+                break
+            try:
+                last = max(last, os.path.getmtime(prog))
+            except OSError:
+                pass
+            if time.time() - last > hang_s:
+                print(f"[bench rank {rank}] rung {name}: no progress for {hang_s:.0f}s", flush=True)
+                failed = True
+                break
+            time.sleep(0.5)
+        if child.poll() is None:
+            os.killpg(child.pid, signal.SIGKILL)
+            child.wait()
+        if not failed:
+            # the rung counts only when every rank's child succeeded
+            store.set(f"hipfm_bench/ok{k}_{rank}", "1")
+            oks = [f"hipfm_bench/ok{k}_{r}" for r in range(world)]
+            while not store.check(oks) and not store.check([f"hipfm_bench/fail{k}"]):
+                time.sleep(0.2)
+            if store.check(oks):
+                if rank == 0 and os.path.exists(result):
+                    print(open(result).read().strip(), flush=True)
+                return 0
+            failed = True
+        store.set(f"hipfm_bench/fail{k}", "1")
+        print(f"[bench rank {rank}] rung {name} failed (rc={child.returncode}); "
+              f"{'retrying with ' + ladder[k + 1][0] if k + 1 < len(ladder) else 'no rung left'}",
+              flush=True)
+        # every rank's child of this rung is gone before the next rung starts
+        store.set(f"hipfm_bench/down{k}_{rank}", "1")
+        store.wait([f"hipfm_bench/down{k}_{r}" for r in range(world)])
+    return 1
+
+
+def _emit(line: str):
+    """The result line: printed directly, or (under the supervisor) handed over in a file and
+    printed by rank 0's supervisor once every rank finished this execution rung."""
+    p = os.environ.get("HIPFM_BENCH_RESULT")
+    if p:
+        with open(p, "w") as f:
+            f.write(line + "\n")
+    else:
+        print(line, flush=True)
+
+
+def _progress():
+    p = os.environ.get("HIPFM_BENCH_PROGRESS")
+    if p:
+        with open(p, "w") as f:
+            f.write("x")
+
 
 def main():
     ap = argparse.ArgumentParser()
@@ -52,7 +162,13 @@ def main():
     ap.add_argument("--force_exchange", action="store_true",
                     help="run the multi-GPU (row-sharded exchange) step on a 1-rank group")
     args = ap.parse_args()
+    if os.environ.get("HIPFM_BENCH_NO_GRAPH") == "1":
+        args.no_graph = True
+    fake = os.environ.get("HIPFM_BENCH_FAKE")          # supervisor tests (CPU): fake rank work
+    if fake:
+        return _fake_child(args, fake)
 
+    _progress()
     import torch
     import torch.distributed as dist
     import hipfm
@@ -71,6 +187,7 @@ def main():
     comm = None
     if world > 1 or args.force_exchange:
         init_distributed("nccl")
+        _progress()
         mode = "sharded" if args.embedding_mode == "auto" else args.embedding_mode
         cap = None
         if mode == "sharded":
@@ -89,21 +206,27 @@ def main():
                          learning_rate=5e-4, optimizer=args.optimizer,
                          sparse_update=args.sparse_update, seed=1234, batch_size=B, device=dev,
                          comm=comm, field_ranges=synth.field_ranges(), mlp_dtype=args.mlp_dtype)
+    _progress()
     pool = [synth.batch(B, step=rank * 100000 + i, device=dev, id_dtype=torch.int32)
             for i in range(args.pool)]
     use_graph = not args.no_graph
     torch.cuda.synchronize()
+    _progress()
     if use_graph and (comm is None or comm.graph_safe):
-        model.precapture(pool)        # one HIP graph per resident batch, captured before timing
+        model.precapture(pool, progress=_progress)        # one HIP graph per resident batch, captured before timing
 
     def run(nsteps, start):
         for s in range(nsteps):
+            if s % 16 == 0:
+                _progress()
             ids, vals, labels = pool[(start + s) % len(pool)]
             nxt = pool[(start + s + 1) % len(pool)][0]     # next batch: its id routing is prefetched
             model.train_step(ids, vals, labels, use_graph=use_graph, next_ids=nxt)
 
+    _progress()
     run(args.warmup, 0)
     torch.cuda.synchronize()
+    _progress()
     if comm is not None:
         dist.barrier()
     torch.cuda.synchronize()
@@ -157,12 +280,13 @@ def main():
                                                 f"+{'row-sharded' if comm.sharded else 'replicated'}-embedding"),
                 "optimizer": f"{args.optimizer} ({args.sparse_update})",
                 "hip_graph": use_graph,
+                "exec": os.environ.get("HIPFM_BENCH_RUNG", "graph+prefetch" if use_graph else "eager"),
                 "mlp_dtype": args.mlp_dtype + (" fwd GEMMs, bf16 backward" if args.mlp_dtype == "fp8" else ""),
             },
             "eval_auc": round(auc, 5),
             "train_loss": round(loss, 5),
         }
-        print(json.dumps(out), flush=True)
+        _emit(json.dumps(out))
     model.check_errors()
     if comm is not None:
         dist.barrier()
@@ -172,5 +296,29 @@ def main():
         dist.destroy_process_group()
 
 
+def _fake_child(args, spec):
+    """CPU stand-in for a bench child (tests of the supervisor): ``spec`` = '<rung>:<rank>:<fail|hang>'
+    entries separated by commas make that rank fail / hang in that rung; others print a line."""
+    import time
+    rank = int(os.environ.get("RANK", "0"))
+    rung = os.environ.get("HIPFM_BENCH_RUNG", "")
+    for item in spec.split(","):
+        r_name, r_rank, what = item.split(":")
+        if r_name == rung and int(r_rank) == rank:
+            if what == "fail":
+                sys.exit(3)
+            while True:             # hang without progress
+                time.sleep(1)
+    _progress()
+    if rank == 0:
+        _emit(json.dumps({"metric": METRIC, "value": 1.0, "n_gpus": int(os.environ.get("WORLD_SIZE", "1")),
+                          "config": {"exec": rung}}))
+    return 0
+
+
 if __name__ == "__main__":
-    main()
+    sup = os.environ.get("HIPFM_BENCH_SUPERVISE", "1")      # 0: off; force: also at 1 rank (tests)
+    if (os.environ.get("HIPFM_BENCH_CHILD") != "1" and sup != "0" and "TORCHELASTIC_RUN_ID" in os.environ
+            and (int(os.environ.get("WORLD_SIZE", "1")) > 1 or sup == "force")):
+        sys.exit(supervise(sys.argv[1:]))
+    sys.exit(main() or 0)

@@ -1035,7 +1035,7 @@ class NativeDeepFM:
             self._graphs[key] = g
         g.replay()
 
-    def precapture(self, batches):
+    def precapture(self, batches, progress=None):
         """One pass over the resident batches with graph capture (the first step eager, every new
         binding captured then replayed), so timed loops only replay graphs.  Consecutive batches
         are chained: the row-sharded step prefetches the next batch's routing.  These are real
@@ -1043,6 +1043,8 @@ class NativeDeepFM:
         P = len(batches)
         for i, (ids, vals, labels) in enumerate(batches):
             self.train_step(ids, vals, labels, use_graph=True, next_ids=batches[(i + 1) % P][0])
+            if progress is not None:
+                progress()
         torch.cuda.synchronize()
 
     def loss_value(self, B: int, include_l2: bool = False) -> float:
