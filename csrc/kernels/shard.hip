@@ -7,12 +7,12 @@
 //
 //   requester                                        owner
 //   sorted uniques -> sh_scatter: send_ids[o][c]  -- a2a -->  recv_ids[p][c]
-//   (upos[u] = o*C + c)                                       sh_serve: rows[p][c] = {v, w}
+//   (upos[u] = o*C + c)                                       sh_serve: rows[p][c] = {v, w},
+//                                                             tag[row][p] = (step, c)
 //   rows_in[o][c]                                 <-- a2a --
 //   sh_slot_rows: slot -> rows_in row; fm_fwd / tower / sparse_fused (MODE 2: gradient rows
 //   g_u written at send_g[upos[u]], V taken from rows_in)
 //   send_g[o][c]                                  -- a2a -->  recv_g[p][c]
-//                                                             sh_owner_tag: tag[row][p] = (step, c)
 //                                                             sh_owner_apply: the lowest requesting
 //                                                             rank sums the rows of all requesters
 //                                                             in rank order, applies the optimizer
@@ -118,10 +118,14 @@ __global__ void sh_slot_rows_kernel(const int* __restrict__ perm, const int* __r
 }
 
 // Owner: rows[e] = {v[K], w, 0, 0, 0} of each requested id (zeros for padding entries)
+// Training steps (tags != null) also stamp the owner-side request tags here, at the start of the
+// step: the requests of the backward exchange are this step's requests, so the owner update at
+// the end of the step needs no separate tagging launch on the critical path.
 template <int K>
-__global__ void sh_serve_kernel(const int* __restrict__ recv_ids, int total, int N,
+__global__ void sh_serve_kernel(const int* __restrict__ recv_ids, int total, int N, int C,
                                 const float* __restrict__ tv, const float* __restrict__ tw, long ldv,
-                                long ldw, float* __restrict__ rows) {
+                                long ldw, float* __restrict__ rows, const int64_t* __restrict__ step,
+                                unsigned long long* __restrict__ tags) {
   constexpr int LPS = K / 4, RW = K + 4;
   const int gt = blockIdx.x * blockDim.x + threadIdx.x;
   const int e = gt / LPS, sub = gt % LPS;
@@ -132,7 +136,10 @@ __global__ void sh_serve_kernel(const int* __restrict__ recv_ids, int total, int
   if (id >= 0) {
     const size_t row = (size_t)(id / N);
     v = *reinterpret_cast<const f32x4*>(tv + row * ldv + sub * 4);
-    if (sub == 0) w = tw[row * ldw];
+    if (sub == 0) {
+      w = tw[row * ldw];
+      if (tags) tags[row * N + e / C] = ((unsigned long long)(*step + 1) << 32) | (unsigned)(e % C);
+    }
   }
   float* o = rows + (size_t)e * RW;
   *reinterpret_cast<f32x4*>(o + sub * 4) = v;
@@ -249,13 +256,14 @@ HFM_API int hfm_sh_slot_rows(const int* perm, const int* sid_incl, const int* up
     default: return (int)hipErrorInvalidValue; \
   }
 
-HFM_API int hfm_sh_serve(int K, const int* recv_ids, int total, int N, const float* tv, const float* tw,
-                         long ldv, long ldw, float* rows, hipStream_t st) {
+HFM_API int hfm_sh_serve(int K, const int* recv_ids, int total, int N, int C, const float* tv, const float* tw,
+                         long ldv, long ldw, float* rows, const int64_t* step, void* tags, hipStream_t st) {
   const long th = (long)total * (K / 4);
   const int grid = (int)((th + 255) / 256);
   if (grid == 0) return 0;
+  if (tags && (!step || C <= 0)) return (int)hipErrorInvalidValue;
 #define CALL(KK) hipLaunchKernelGGL(sh_serve_kernel<KK>, dim3(grid), dim3(256), 0, st, recv_ids, total, N, \
-                                    tv, tw, ldv, ldw, rows)
+                                    C, tv, tw, ldv, ldw, rows, step, (unsigned long long*)tags)
   HFM_K_DISPATCH(K, CALL)
 #undef CALL
   HFM_LAUNCH_CHECK();
@@ -277,13 +285,14 @@ template <int K>
 static int sh_apply_k(int opt, const ShApplyArgs& A, hipStream_t st) {
   const long th = (long)A.total * (K / 4);
   const int grid = (int)((th + 255) / 256);
-  hipLaunchKernelGGL(sh_owner_tag_kernel, dim3((A.total + 255) / 256), dim3(256), 0, st, A.recv_ids,
-                     A.total, A.N, A.C, A.step, A.tags);
+  if (A.mode & 2)  // tags not stamped by this step's serve (eval-style fetch): stamp them here
+    hipLaunchKernelGGL(sh_owner_tag_kernel, dim3((A.total + 255) / 256), dim3(256), 0, st, A.recv_ids,
+                       A.total, A.N, A.C, A.step, A.tags);
 #define L_(M, O)                                                                                      \
   hipLaunchKernelGGL((sh_owner_apply_kernel<K, M, O>), dim3(grid), dim3(256), 0, st, A.recv_ids, A.total, \
                      A.N, A.C, A.recv_g, A.tags, A.tv, A.tw, A.s0v, A.s1v, A.s0w, A.s1w, A.ldv, A.ldw,  \
                      A.Gv, A.Gw, A.h, A.step)
-  if (A.mode == 1) {
+  if ((A.mode & 1) == 1) {
     L_(1, 0);
     return 0;
   }

@@ -640,7 +640,7 @@ class NativeDeepFM:
         idx = self.idx
         tv, tw = self.tv, self.tw
         if self.shx is not None:
-            idx, tv, tw = self.shx.fetch(self._shx_plan)
+            idx, tv, tw = self.shx.fetch(self._shx_plan, train)
         elif self.sharded:
             idx, tv, tw = self.comm.sharded_forward_gather(self, B)
         fm_bias = self.p[self.dense_segs["fm_bias"].off:]

@@ -175,7 +175,8 @@ _SIGS = {
     "hfm_sh_count_blocks": [c_int],
     "hfm_sh_bucket": [c_void_p, c_void_p, c_int, c_int, c_int] + [c_void_p] * 5 + [c_void_p],
     "hfm_sh_slot_rows": [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p],
-    "hfm_sh_serve": [c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_long, c_long, c_void_p, c_void_p],
+    "hfm_sh_serve": [c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_long, c_long, c_void_p,
+                     c_void_p, c_void_p, c_void_p],
     "hfm_sh_owner_apply": [c_int, c_int, c_void_p, c_void_p],
     "hfm_sh_apply_args_bytes": [],
     "hfm_sparse_fused_tiles": [c_int, c_int],

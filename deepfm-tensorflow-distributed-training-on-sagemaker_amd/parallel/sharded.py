@@ -198,11 +198,17 @@ class FixedCapacityExchange:
         if plan[2] is not None:
             torch.cuda.current_stream(self.m.device).wait_stream(self._side)
 
-    def fetch(self, plan):
-        """Owners serve the requested rows (after the previous step's updates), rows come back."""
+    def fetch(self, plan, train: bool = True):
+        """Owners serve the requested rows (after the previous step's updates), rows come back.
+        Training steps stamp the owner-side request tags here (read by the update at the end of
+        the step); eval / predict fetches leave them alone."""
         m = self.m
         rs = self.sets[plan[0]]
-        KN.sh_serve(m.K, rs.recv_ids, self.N * self.C, self.N, m.tv, m.tw, self.rows_out)
+        if train:
+            KN.sh_serve(m.K, rs.recv_ids, self.N * self.C, self.N, m.tv, m.tw, self.rows_out,
+                        C=self.C, step=m.step, tags=self.tags)
+        else:
+            KN.sh_serve(m.K, rs.recv_ids, self.N * self.C, self.N, m.tv, m.tw, self.rows_out)
         self.eng.alltoall(self.rows_out, self.rows_in, self.C * self.RW * 4)
         return rs.slot_row, self.rows_in[:, : m.K], self.rows_in[:, m.K]
 
@@ -220,7 +226,7 @@ class FixedCapacityExchange:
         self.eng.alltoall(self.send_g, self.recv_g, self.C * self.RW * 4)
         S = ShApplyArgs()
         S.recv_ids, S.total, S.N, S.C = rs.recv_ids.data_ptr(), self.N * self.C, self.N, self.C
-        S.mode = 0 if m.sparse_update == "lazy" else 1
+        S.mode = 0 if m.sparse_update == "lazy" else 1      # tags were stamped by fetch()
         S.recv_g, S.tags = self.recv_g.data_ptr(), self.tags.data_ptr()
         S.tv, S.tw = m.tv.data_ptr(), m.tw.data_ptr()
         S.s0v, S.s1v, S.s0w, S.s1w = (t.data_ptr() if t.numel() else 0 for t in m.sv)
