@@ -45,6 +45,7 @@ _SORT_MODE = os.environ.get("HIPFM_SORT", "auto")                # auto | global
 _SORT_SIDE_STREAM = os.environ.get("HIPFM_SORT_SIDE_STREAM", "1") == "1"
 _SPARSE_IMPL = os.environ.get("HIPFM_SPARSE", "fused")             # fused | seg
 _SHARD_PIPELINE = os.environ.get("HIPFM_SHARD_PIPELINE", "1") == "1"
+_DENSE_SIDE_STREAM = os.environ.get("HIPFM_DENSE_SIDE_STREAM", "auto")   # auto | 1 | 0
 
 
 def check_field_ranges(ranges, F: int, V: int) -> List[Tuple[int, int]]:
@@ -536,14 +537,16 @@ class NativeDeepFM:
         a.partial = self.partial.data_ptr()
         return a
 
-    def _dense_fwd_bwd(self, B: int):
+    def _dense_fwd_bwd(self, B: int, defer_wgrad: bool = False):
         """Forward, loss head and the whole deep-tower backward (dense grads into self.g, dX0
-        for the FM backward).  Returns the (idx, table) pair the sparse backward uses."""
+        for the FM backward).  Returns the (idx, table) pair the sparse backward uses.
+        ``defer_wgrad``: stop after the fused tower (the caller runs wgrad + finalize)."""
         if self.fused:
             idx, tv = self._fm_forward(B, train=True)
             KN.tower(self._tower_args(B, train=True))
-            KN.wgrad_group(self._wg_jobs, self._nwg_jobs, self._wg_tasks)
-            self._finalize_grads()
+            if not defer_wgrad:
+                KN.wgrad_group(self._wg_jobs, self._nwg_jobs, self._wg_tasks)
+                self._finalize_grads()
             return idx, tv
         idx, tv = self._forward(B, train=True)
         self._head(B, train=True)
@@ -920,25 +923,38 @@ class NativeDeepFM:
             with torch.cuda.stream(self._side):
                 self._sort_slots(B)
             presorted = True
-        idx, tv = self._dense_fwd_bwd(B)
+        # fused tower: the weight gradients (wgrad + finalize, then the dense all-reduce) only
+        # feed the dense optimizer, so on the multi-rank step they run on their own stream
+        # concurrently with the sparse exchange (which needs only dX0 / dlogit / S from the
+        # tower): 0.210 -> 0.199 ms.  On one GPU the concurrent wgrad slows the sparse backward
+        # more than it saves (0.156 -> 0.161 ms), so there it stays in line.
+        split = self.fused and (_DENSE_SIDE_STREAM == "1" or
+                                (_DENSE_SIDE_STREAM == "auto" and self.exchange))
+        idx, tv = self._dense_fwd_bwd(B, defer_wgrad=split)
+        main = torch.cuda.current_stream(self.device)
         if presorted:
             main.wait_stream(self._side)
         work = None
         eng = getattr(self.comm, "engine_dense", None) if self.exchange else None
-        if eng is not None:
-            # dense bucket all-reduce on a side stream, overlapped with the sparse exchange
-            main = torch.cuda.current_stream(self.device)
+        if split or eng is not None:
+            # dense gradient branch (+ bucket all-reduce) overlapped with the sparse exchange
             if self._comm_stream is None:
                 self._comm_stream = torch.cuda.Stream(self.device)
             self._comm_stream.wait_stream(main)
             with torch.cuda.stream(self._comm_stream):
-                eng.allreduce_(self.g)
+                if split:
+                    KN.wgrad_group(self._wg_jobs, self._nwg_jobs, self._wg_tasks)
+                    self._finalize_grads()
+                if eng is not None:
+                    eng.allreduce_(self.g)
+                elif self.exchange:
+                    work = self.comm.allreduce_dense_async(self.g)
         elif self.exchange:
             work = self.comm.allreduce_dense_async(self.g)
         out = self._sparse_backward(B, idx, tv, presorted=presorted)
         if out is not None:
             self._sparse_update(*out)
-        if eng is not None:
+        if split or eng is not None:
             main.wait_stream(self._comm_stream)
         if work is not None:
             self.comm.wait(work)
