@@ -104,6 +104,10 @@ class Estimator:
                                       barrier) if cfg.ckpt_dir else None
         mpath = cfg.metrics_file or (os.path.join(cfg.ckpt_dir, "metrics.jsonl") if cfg.ckpt_dir else None)
         self.log = MetricsLogger(mpath, self.rank)
+        # TensorBoard scalars like the reference Estimator's default summary hooks (rank 0):
+        # <model_dir>/events.out.tfevents.* (loss, global_step/sec) and <model_dir>/eval/ (auc, loss)
+        self._tb = self._tb_eval = None
+        self._tb_on = bool(cfg.ckpt_dir) and self.rank == 0 and getattr(cfg, "tensorboard", True)
         self.timer = StepTimer()
         self._last_save_t = time.time()
         self._last_eval_t = 0.0
@@ -274,6 +278,8 @@ class Estimator:
                 self.log.log("train", step=step, loss=loss, samples_per_sec_rank=sps,
                              samples_per_sec_job=sps * self.world, **self.timer.summary(),
                              comm_bytes=getattr(self.comm, "bytes_sent", 0))
+                self._summary("train", step, {"loss": loss, "global_step/sec": cfg.log_steps / dt,
+                                              "examples/sec": sps * self.world})
                 t_log, n_log = time.time(), 0
             if self.ckpt is not None and (
                     (cfg.save_checkpoints_steps and step % cfg.save_checkpoints_steps == 0) or
@@ -330,7 +336,22 @@ class Estimator:
         self.log.info("Saving dict for global step %d: auc = %.6f, global_step = %d, loss = %.6f"
                       % (res["global_step"], res["auc"], res["global_step"], res["loss"]))
         self.log.log("eval", **res)
+        self._summary("eval", res["global_step"], {"auc": res["auc"], "loss": res["loss"]})
         return res
+
+    def _summary(self, kind: str, step: int, values: dict):
+        """Scalar summaries for TensorBoard (reference: Estimator default hooks)."""
+        if not self._tb_on:
+            return
+        from .utils.tfevents import EventFileWriter
+        if kind == "train":
+            if self._tb is None:
+                self._tb = EventFileWriter(self.cfg.ckpt_dir)
+            self._tb.scalars(step, values)
+        else:
+            if self._tb_eval is None:
+                self._tb_eval = EventFileWriter(os.path.join(self.cfg.ckpt_dir, "eval"))
+            self._tb_eval.scalars(step, values)
 
     def predict(self, batches: Iterable) -> Iterator[torch.Tensor]:
         for ids, vals, _ in batches:

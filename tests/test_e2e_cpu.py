@@ -42,6 +42,15 @@ def test_train_eval_infer_export_resume(dataset, tmp_path):
     assert res["auc"] > 0.68, res             # teacher labels are learnable
     idx = json.load(open(os.path.join(md, "hipfm_checkpoint.json")))
     assert idx["latest"] == f"ckpt-{res['global_step']}"
+    # TensorBoard scalars like the Estimator's default hooks: train loss in model_dir, eval in eval/
+    from hipfm.utils.tfevents import read_events
+    import glob
+    ev_train = [e for f in glob.glob(os.path.join(md, "events.out.tfevents.*")) for e in read_events(f)]
+    ev_eval = [e for f in glob.glob(os.path.join(md, "eval", "events.out.tfevents.*")) for e in read_events(f)]
+    assert ev_train and ev_train[0].get("file_version") == "brain.Event:2"
+    assert any("loss" in e["scalars"] for e in ev_train)
+    aucs = [e["scalars"]["auc"] for e in ev_eval if "auc" in e["scalars"]]
+    assert aucs and abs(aucs[-1] - res["auc"]) < 1e-6
     # eval restores the latest checkpoint and reproduces the final metrics exactly
     ev = main(_flags(dataset, md, ["--task_type", "eval"]))
     assert ev["global_step"] == res["global_step"] and abs(ev["auc"] - res["auc"]) < 1e-9
