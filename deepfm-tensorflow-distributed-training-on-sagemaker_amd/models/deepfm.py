@@ -46,6 +46,7 @@ _SORT_SIDE_STREAM = os.environ.get("HIPFM_SORT_SIDE_STREAM", "1") == "1"
 _SPARSE_IMPL = os.environ.get("HIPFM_SPARSE", "fused")             # fused | seg
 _SHARD_PIPELINE = os.environ.get("HIPFM_SHARD_PIPELINE", "1") == "1"
 _DENSE_SIDE_STREAM = os.environ.get("HIPFM_DENSE_SIDE_STREAM", "auto")   # auto | 1 | 0
+_TOWER_STAGE = os.environ.get("HIPFM_TOWER_STAGE", "auto")       # auto | 1 | 0
 
 
 def check_field_ranges(ranges, F: int, V: int) -> List[Tuple[int, int]]:
@@ -338,8 +339,21 @@ class NativeDeepFM:
                     t.fill_(init)
 
     def _tower_lds_bytes(self) -> int:
+        """H tiles + two dZ tiles + the [32][K0p + 8] input / dX0 staging tile (bf16)."""
         h = sum(32 * (n + 8) * 2 for n in self.Np)
-        return h + 2 * 32 * (max(self.Np) + 8) * 2
+        return h + 2 * 32 * (max(self.Np) + 8) * 2 + (32 * (self.K0p + 8) * 2 if self._stage_x else 0)
+
+    @property
+    def _stage_x(self) -> bool:
+        """Stage the tower's 32 input rows (and its dX0 tile) in LDS: -3.5 us in layer 0 and -1 us
+        in the dX0 phase per workgroup (tools/tower_phases.py), but +21 KB of LDS per workgroup,
+        and next to the side-stream field sort (148 KB per workgroup on 39 CUs) the 512 tower
+        workgroups then no longer fit in one residency round (start spread 0.5 -> 26 us, step
+        0.156 -> 0.174 ms).  On the row-sharded step (different side-stream work) it measured
+        0.207 -> 0.202 ms, so: on for the sharded step, off on one GPU (HIPFM_TOWER_STAGE=0/1
+        overrides)."""
+        on = self.sharded if _TOWER_STAGE == "auto" else _TOWER_STAGE == "1"
+        return on and self.K0p <= 512
 
     @staticmethod
     def _padM(B: int) -> int:
@@ -515,6 +529,7 @@ class NativeDeepFM:
             off += 32 * (self.Np[i] + 8)
         a.dz_off[0] = off
         a.dz_off[1] = off + 32 * (max(self.Np) + 8)
+        a.x_off = off + 2 * 32 * (max(self.Np) + 8) if self._stage_x else -1
         a.lds_bytes = self._tower_lds_bytes()
         a.E = self.E.data_ptr()
         if self.fp8:

@@ -108,9 +108,9 @@ class TowerArgs(C.Structure):
                 ("w_out", c_void_p), ("b_out", c_void_p), ("y_fm", c_void_p), ("labels", c_void_p),
                 ("Ht", c_void_p * TW_MAXL), ("dZt", c_void_p * TW_MAXL), ("dX0", c_void_p),
                 ("prob", c_void_p), ("dlogit", c_void_p), ("partial", c_void_p),
-                ("h_off", c_int * TW_MAXL), ("dz_off", c_int * 2), ("lds_bytes", c_int),
+                ("h_off", c_int * TW_MAXL), ("dz_off", c_int * 2), ("x_off", c_int), ("lds_bytes", c_int),
                 ("fp8", c_int), ("E8", c_void_p), ("sE", c_void_p), ("W8", c_void_p * TW_MAXL),
-                ("sW", c_void_p * TW_MAXL)]
+                ("sW", c_void_p * TW_MAXL), ("tstamp", c_void_p)]
 
 
 class W8Job(C.Structure):

@@ -427,3 +427,27 @@ def test_sparse_fused_matches_segment_kernels(opt, mode, K):
     for sa, sb in zip(a.sv, b.sv):
         if sa.numel():
             assert (sa - sb).abs().max().item() <= 1e-5 * max(1e-6, sb.abs().max().item()) + 1e-12
+
+
+@pytest.mark.parametrize("mlp_dtype", ["bf16", "fp8"])
+def test_tower_lds_staged_input_bitwise_equal(monkeypatch, mlp_dtype):
+    """The tower's LDS-staged input / dX0 tiles (on by default on the sharded step) change only
+    where the operands come from: parameters after graph-replayed steps are bitwise equal."""
+    import hipfm.models.deepfm as D
+    synth = make_synth("criteo_kaggle", seed=11)
+    F, K, layers, keep, B = synth.F, 8, [128, 64, 32], [0.5] * 3, 1024
+    params = init_params(synth.feature_size, F, K, layers, False, seed=4)
+    out = []
+    for stage in ("1", "0"):
+        monkeypatch.setattr(D, "_TOWER_STAGE", stage)
+        m = NativeDeepFM(synth.feature_size, F, K, layers, keep, batch_size=B, device=DEV, init=False,
+                         sparse_update="lazy", mlp_dtype=mlp_dtype)
+        assert m._stage_x == (stage == "1")
+        m.load_tf_params(params)
+        for s in range(4):
+            ids, vals, lab = synth.batch(B, step=s, device=DEV, id_dtype=torch.int32)
+            m.train_step(ids, vals, lab, use_graph=True)
+        torch.cuda.synchronize()
+        out.append((m.p.clone(), m.tv.clone(), m.dX0.clone()))
+    assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
+    assert torch.equal(out[0][2], out[1][2])
