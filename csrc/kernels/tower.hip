@@ -22,6 +22,11 @@
 
 constexpr int TW_MAXL = 8;
 constexpr int TW_ROWS = 32;
+// k-steps of A/B fragments in flight per wave: PF0 for layer 0, PF1 for the other GEMMs.  The
+// deep variant (5, 4: layer 0 in two latency rounds instead of three, the rest in one) needs 168
+// VGPRs, i.e. 2 waves per SIMD: it loses on one GPU, where the side-stream field sort holds 39
+// CUs and the 512 tower workgroups then need a second residency round (0.157 -> 0.177 ms), and
+// is within run-to-run noise on the row-sharded step.  TowerArgs.deep picks the variant.
 
 struct TowerArgs {
   int M, nvalid, nl, K0p;
@@ -62,6 +67,7 @@ struct TowerArgs {
   const uint8_t* W8[TW_MAXL];     // [Np_i, Kp_i]
   const float* sW[TW_MAXL];       // [Np_i]  channel dequant factors of W8
   unsigned long long* tstamp;     // optional phase timestamps [grid][16] (tools/tower_phases.py)
+  int deep;                       // 1: deep-prefetch variant (see TW prefetch note)
 };
 
 #define TW_STAMP(k)                                                        \
@@ -193,7 +199,7 @@ __device__ __forceinline__ void store_tile_t(const bf16* t, int ld, int N, bf16*
   }
 }
 
-template <bool FP8>
+template <bool FP8, int TW_PF0, int TW_PF1>
 __global__ void __launch_bounds__(256) tower_kernel(TowerArgs a) {
   extern __shared__ __align__(16) unsigned char tw_lds_raw[];
   bf16* lds = reinterpret_cast<bf16*>(tw_lds_raw);
@@ -266,9 +272,9 @@ __global__ void __launch_bounds__(256) tower_kernel(TowerArgs a) {
         if (i == 0 && stage)
           mma32<4>(Xl, ldx, Bw, Kp, Kp / 32, lane, c00, c01, c10, c11);
         else if (i == 0)
-          mma32<4>(a.E + (size_t)row0 * a.K0p, a.K0p, Bw, Kp, Kp / 32, lane, c00, c01, c10, c11);
+          mma32<TW_PF0>(a.E + (size_t)row0 * a.K0p, a.K0p, Bw, Kp, Kp / 32, lane, c00, c01, c10, c11);
         else
-          mma32<2>(lds + a.h_off[i - 1], Kp + 8, Bw, Kp, Kp / 32, lane, c00, c01, c10, c11);
+          mma32<TW_PF1>(lds + a.h_off[i - 1], Kp + 8, Bw, Kp, Kp / 32, lane, c00, c01, c10, c11);
       }
       f32x4 acc[2][2] = {{c00, c01}, {c10, c11}};
 #pragma unroll
@@ -381,7 +387,7 @@ __global__ void __launch_bounds__(256) tower_kernel(TowerArgs a) {
     const float sc = a.inv_keep[i - 1];
     for (int ct = wave; ct < Nout / 32; ct += 4) {
       f32x4 c00 = {0, 0, 0, 0}, c01 = c00, c10 = c00, c11 = c00;
-      mma32<2>(Az, ldz_in, a.WT[i] + (size_t)ct * 32 * Kin, Kin, Kin / 32, lane, c00, c01, c10, c11);
+      mma32<TW_PF1>(Az, ldz_in, a.WT[i] + (size_t)ct * 32 * Kin, Kin, Kin / 32, lane, c00, c01, c10, c11);
       f32x4 acc[2][2] = {{c00, c01}, {c10, c11}};
 #pragma unroll
       for (int ti = 0; ti < 2; ++ti) {
@@ -407,7 +413,7 @@ __global__ void __launch_bounds__(256) tower_kernel(TowerArgs a) {
     const bf16* Az = lds + a.dz_off[cur];
     for (int ct = wave; ct < a.K0p / 32; ct += 4) {
       f32x4 c00 = {0, 0, 0, 0}, c01 = c00, c10 = c00, c11 = c00;
-      mma32<2>(Az, N0 + 8, a.WT[0] + (size_t)ct * 32 * N0, N0, N0 / 32, lane, c00, c01, c10, c11);
+      mma32<TW_PF1>(Az, N0 + 8, a.WT[0] + (size_t)ct * 32 * N0, N0, N0 / 32, lane, c00, c01, c10, c11);
       f32x4 acc[2][2] = {{c00, c01}, {c10, c11}};
 #pragma unroll
       for (int ti = 0; ti < 2; ++ti) {
@@ -447,9 +453,14 @@ HFM_API int hfm_tower(const TowerArgs* ap, hipStream_t st) {
     if (!a.E8 || !a.sE) return (int)hipErrorInvalidValue;
     for (int i = 0; i < a.nl; ++i)
       if (!a.W8[i] || !a.sW[i]) return (int)hipErrorInvalidValue;
-    hipLaunchKernelGGL(tower_kernel<true>, dim3(a.M / TW_ROWS), dim3(256), a.lds_bytes, st, a);
+    if (a.deep)
+      hipLaunchKernelGGL((tower_kernel<true, 5, 4>), dim3(a.M / TW_ROWS), dim3(256), a.lds_bytes, st, a);
+    else
+      hipLaunchKernelGGL((tower_kernel<true, 4, 2>), dim3(a.M / TW_ROWS), dim3(256), a.lds_bytes, st, a);
+  } else if (a.deep) {
+    hipLaunchKernelGGL((tower_kernel<false, 5, 4>), dim3(a.M / TW_ROWS), dim3(256), a.lds_bytes, st, a);
   } else {
-    hipLaunchKernelGGL(tower_kernel<false>, dim3(a.M / TW_ROWS), dim3(256), a.lds_bytes, st, a);
+    hipLaunchKernelGGL((tower_kernel<false, 4, 2>), dim3(a.M / TW_ROWS), dim3(256), a.lds_bytes, st, a);
   }
   HFM_LAUNCH_CHECK();
 }

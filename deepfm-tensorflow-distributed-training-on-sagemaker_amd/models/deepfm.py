@@ -46,7 +46,8 @@ _SORT_SIDE_STREAM = os.environ.get("HIPFM_SORT_SIDE_STREAM", "1") == "1"
 _SPARSE_IMPL = os.environ.get("HIPFM_SPARSE", "fused")             # fused | seg
 _SHARD_PIPELINE = os.environ.get("HIPFM_SHARD_PIPELINE", "1") == "1"
 _DENSE_SIDE_STREAM = os.environ.get("HIPFM_DENSE_SIDE_STREAM", "auto")   # auto | 1 | 0
-_TOWER_STAGE = os.environ.get("HIPFM_TOWER_STAGE", "auto")       # auto | 1 | 0
+_TOWER_STAGE = os.environ.get("HIPFM_TOWER_STAGE", "0")          # auto (sharded step) | 1 | 0
+_TOWER_DEEP = os.environ.get("HIPFM_TOWER_DEEP", "0")            # auto (sharded step) | 1 | 0
 
 
 def check_field_ranges(ranges, F: int, V: int) -> List[Tuple[int, int]]:
@@ -349,9 +350,8 @@ class NativeDeepFM:
         in the dX0 phase per workgroup (tools/tower_phases.py), but +21 KB of LDS per workgroup,
         and next to the side-stream field sort (148 KB per workgroup on 39 CUs) the 512 tower
         workgroups then no longer fit in one residency round (start spread 0.5 -> 26 us, step
-        0.156 -> 0.174 ms).  On the row-sharded step (different side-stream work) it measured
-        0.207 -> 0.202 ms, so: on for the sharded step, off on one GPU (HIPFM_TOWER_STAGE=0/1
-        overrides)."""
+        0.156 -> 0.174 ms).  On the row-sharded step a same-box A/B showed no difference beyond
+        run-to-run noise (0.198-0.202 ms), so it is off by default (HIPFM_TOWER_STAGE=1 / auto)."""
         on = self.sharded if _TOWER_STAGE == "auto" else _TOWER_STAGE == "1"
         return on and self.K0p <= 512
 
@@ -530,6 +530,9 @@ class NativeDeepFM:
         a.dz_off[0] = off
         a.dz_off[1] = off + 32 * (max(self.Np) + 8)
         a.x_off = off + 2 * 32 * (max(self.Np) + 8) if self._stage_x else -1
+        # deep-prefetch tower variant (more VGPRs, fewer latency rounds): slower on one GPU next
+        # to the side-stream sort, no measurable change on the sharded step (off by default)
+        a.deep = 1 if (_TOWER_DEEP == "1" or (_TOWER_DEEP == "auto" and self.sharded)) else 0
         a.lds_bytes = self._tower_lds_bytes()
         a.E = self.E.data_ptr()
         if self.fp8:

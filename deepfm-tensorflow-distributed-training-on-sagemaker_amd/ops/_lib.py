@@ -110,7 +110,7 @@ class TowerArgs(C.Structure):
                 ("prob", c_void_p), ("dlogit", c_void_p), ("partial", c_void_p),
                 ("h_off", c_int * TW_MAXL), ("dz_off", c_int * 2), ("x_off", c_int), ("lds_bytes", c_int),
                 ("fp8", c_int), ("E8", c_void_p), ("sE", c_void_p), ("W8", c_void_p * TW_MAXL),
-                ("sW", c_void_p * TW_MAXL), ("tstamp", c_void_p)]
+                ("sW", c_void_p * TW_MAXL), ("tstamp", c_void_p), ("deep", c_int)]
 
 
 class W8Job(C.Structure):

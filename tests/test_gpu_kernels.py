@@ -431,8 +431,9 @@ def test_sparse_fused_matches_segment_kernels(opt, mode, K):
 
 @pytest.mark.parametrize("mlp_dtype", ["bf16", "fp8"])
 def test_tower_lds_staged_input_bitwise_equal(monkeypatch, mlp_dtype):
-    """The tower's LDS-staged input / dX0 tiles (on by default on the sharded step) change only
-    where the operands come from: parameters after graph-replayed steps are bitwise equal."""
+    """The tower's LDS-staged input / dX0 tiles and its deep-prefetch variant (both on by default
+    on the sharded step) change only where / when operands are loaded: parameters after
+    graph-replayed steps are bitwise equal."""
     import hipfm.models.deepfm as D
     synth = make_synth("criteo_kaggle", seed=11)
     F, K, layers, keep, B = synth.F, 8, [128, 64, 32], [0.5] * 3, 1024
@@ -440,6 +441,7 @@ def test_tower_lds_staged_input_bitwise_equal(monkeypatch, mlp_dtype):
     out = []
     for stage in ("1", "0"):
         monkeypatch.setattr(D, "_TOWER_STAGE", stage)
+        monkeypatch.setattr(D, "_TOWER_DEEP", stage)        # deep-prefetch variant with it
         m = NativeDeepFM(synth.feature_size, F, K, layers, keep, batch_size=B, device=DEV, init=False,
                          sparse_update="lazy", mlp_dtype=mlp_dtype)
         assert m._stage_x == (stage == "1")
