@@ -59,3 +59,25 @@ def test_exchange_paths_match_local(group, sharded, update, prefetch):
     assert torch.allclose(a.tv, b.tv, atol=1e-6) and torch.allclose(a.tw, b.tw, atol=1e-6)
     assert torch.allclose(a.p, b.p, atol=1e-6)
     assert b.comm.bytes_sent > 0
+
+
+def test_exchange_staged_batches_graph_replay(group):
+    """Loader-style batches (int64 ids, staged into the model's own input buffers every step) on
+    the row-sharded exchange with HIP graphs: routing is inline every step (staged content changes
+    under the same addresses) and the two routing sets alternate; must equal the local path."""
+    synth = make_synth("total:6000", seed=23)
+    F, K, layers, keep = synth.F, 8, [64, 32], [0.8, 0.8]
+    V = synth.feature_size
+    params = init_params(V, F, K, layers, False, seed=5)
+    kw = dict(sparse_update="lazy", batch_size=512, device="cuda", init=False)
+    a = NativeDeepFM(V, F, K, layers, keep, **kw)
+    b = NativeDeepFM(V, F, K, layers, keep, comm=Comm(sharded=True, force_exchange=True), **kw)
+    a.load_tf_params(params)
+    b.load_tf_params(params)
+    for s in range(5):
+        ids, vals, labels = synth.batch(512, step=s)               # CPU, int64: staged path
+        a.train_step(ids, vals, labels)
+        b.train_step(ids, vals, labels, use_graph=True)
+    torch.cuda.synchronize()
+    assert len(b._graphs) == 2                                     # ("staged", B) x 2 routing sets
+    assert torch.allclose(a.tv, b.tv, atol=1e-6) and torch.allclose(a.p, b.p, atol=1e-6)
