@@ -68,6 +68,15 @@ struct TowerArgs {
   const float* sW[TW_MAXL];       // [Np_i]  channel dequant factors of W8
   unsigned long long* tstamp;     // optional phase timestamps [grid][16] (tools/tower_phases.py)
   int deep;                       // 1: deep-prefetch variant (see TW prefetch note)
+  // Slot-order FM gradient records for the fused sparse backward (optional): for every slot
+  // (b, f) G[b*F + f] = {x*(dX0[b,f,:] + dy_b*S_b) (K floats), dy_b*x, dy_b*x^2, 0, 0}.  The
+  // sparse tile kernel then reads ONE 16-B-aligned record per slot (in id order) instead of
+  // four scattered per-sample arrays.  dX0 is rounded to bf16 first, exactly as when the tile
+  // kernel read the bf16 dX0, so the numbers are unchanged.
+  float* G;                       // [M*F][K+4] or null
+  const float* S;                 // [M, K]
+  const float* vals;              // [M, F]
+  int F, K;
 };
 
 #define TW_STAMP(k)                                                        \
@@ -422,10 +431,27 @@ __global__ void __launch_bounds__(256) tower_kernel(TowerArgs a) {
           const int col = ct * 32 + tj * 16 + cc;
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
+            const int rl = ti * 16 + cr + j;
+            const bf16 dxh = f2bf(acc[ti][tj][j]);
+            if (a.G) {
+              const int f = col / a.K, k = col - f * a.K;
+              if (f < a.F) {
+                const size_t b = (size_t)(row0 + rl);
+                const float dy = s_dl[rl];
+                const float x = a.vals[b * a.F + f];
+                float* gr = a.G + (b * a.F + f) * (size_t)(a.K + 4);
+                gr[k] = (bf2f(dxh) + dy * a.S[b * a.K + k]) * x;
+                if (k == 0) {
+                  gr[a.K] = dy * x;
+                  gr[a.K + 1] = dy * x * x;
+                }
+              }
+            }
+            if (!a.dX0) continue;
             if (stage)
-              Xl[(ti * 16 + cr + j) * ldx + col] = f2bf(acc[ti][tj][j]);
+              Xl[rl * ldx + col] = dxh;
             else
-              a.dX0[(size_t)(row0 + ti * 16 + cr + j) * a.K0p + col] = f2bf(acc[ti][tj][j]);
+              a.dX0[(size_t)(row0 + rl) * a.K0p + col] = dxh;
           }
         }
       }
@@ -433,7 +459,7 @@ __global__ void __launch_bounds__(256) tower_kernel(TowerArgs a) {
     // dX0 tile (staged in the input tile's LDS, free since layer 0) -> global in 16-B rows
     __syncthreads();
     const int cpr = a.K0p / 8;
-    for (int e = tid; stage && e < TW_ROWS * cpr; e += 256) {
+    for (int e = tid; stage && a.dX0 && e < TW_ROWS * cpr; e += 256) {
       const int r = e / cpr, c = e - r * cpr;
       *reinterpret_cast<f32x4*>(a.dX0 + (size_t)(row0 + r) * a.K0p + c * 8) =
           *reinterpret_cast<const f32x4*>(Xl + r * ldx + c * 8);

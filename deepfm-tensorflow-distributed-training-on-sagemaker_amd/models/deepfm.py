@@ -48,6 +48,9 @@ _SHARD_PIPELINE = os.environ.get("HIPFM_SHARD_PIPELINE", "1") == "1"
 _DENSE_SIDE_STREAM = os.environ.get("HIPFM_DENSE_SIDE_STREAM", "auto")   # auto | 1 | 0
 _TOWER_STAGE = os.environ.get("HIPFM_TOWER_STAGE", "0")          # auto (sharded step) | 1 | 0
 _TOWER_DEEP = os.environ.get("HIPFM_TOWER_DEEP", "0")            # auto (sharded step) | 1 | 0
+# slot-order gradient records from the tower (TowerArgs.G): measured slower (tower +12 us for the
+# scattered record writes, sparse tile -0.7 us: its cost is not the per-sample gathers), so off
+_GSLOT = os.environ.get("HIPFM_GSLOT", "0") == "1"
 
 
 def check_field_ranges(ranges, F: int, V: int) -> List[Tuple[int, int]]:
@@ -384,6 +387,9 @@ class NativeDeepFM:
         self.dZ = [torch.zeros(M, n, **bf) for n in self.Np]
         self.dZt = [torch.zeros(n, M, **bf) for n in self.Np]
         self.dX0 = torch.zeros(M, K0p, **bf)            # layer-1 input gradient (bf16)
+        # slot-order FM gradient records written by the fused tower for the fused sparse
+        # backward (csrc/kernels/tower.hip, TowerArgs.G): [M*F][K+4]
+        self.Gslot = torch.zeros(M * F, K + 4, **f32) if (self.fused and _GSLOT) else None
         if self.batch_norm:
             self.Rb = [torch.zeros(M, n, **f32) for n in self.Np]         # relu output (pre-BN)
             self.dH = [torch.zeros(M, n, **f32) for n in self.Np]         # dL/d(layer output)
@@ -508,7 +514,15 @@ class NativeDeepFM:
         self._nwg_jobs = len(jobs)
         self._wg_tasks = task0
 
-    def _tower_args(self, B: int, train: bool, with_labels: bool = True) -> TowerArgs:
+    def _gslot_mode(self) -> bool:
+        """The fused tower writes slot-order gradient records (and no dX0) when the sparse
+        backward is the fused tile kernel: single rank with HIPFM_SPARSE=fused, or the
+        row-sharded exchange."""
+        return _GSLOT and self.fused and self.Gslot is not None and (
+            self.shx is not None or (not self.exchange and _SPARSE_IMPL == "fused"))
+
+    def _tower_args(self, B: int, train: bool, with_labels: bool = True,
+                    gslot: bool = False) -> TowerArgs:
         a = TowerArgs()
         nl = len(self.layers)
         a.M, a.nvalid, a.nl, a.K0p = self.M, B, nl, self.K0p
@@ -549,19 +563,22 @@ class NativeDeepFM:
         a.b_out = pb + 4 * self.dense_segs["Deep-part/deep_out/biases"].off
         a.y_fm = self.y_fm.data_ptr()
         a.labels = self.labels.data_ptr() if with_labels else 0
-        a.dX0 = self.dX0.data_ptr()
+        a.dX0 = 0 if gslot else self.dX0.data_ptr()
+        if gslot:
+            a.G, a.S, a.vals = self.Gslot.data_ptr(), self.S.data_ptr(), self.vals.data_ptr()
+            a.F, a.K = self.F, self.K
         a.prob = self.prob.data_ptr()
         a.dlogit = self.dlogit.data_ptr()
         a.partial = self.partial.data_ptr()
         return a
 
-    def _dense_fwd_bwd(self, B: int, defer_wgrad: bool = False):
+    def _dense_fwd_bwd(self, B: int, defer_wgrad: bool = False, gslot: bool = False):
         """Forward, loss head and the whole deep-tower backward (dense grads into self.g, dX0
         for the FM backward).  Returns the (idx, table) pair the sparse backward uses.
         ``defer_wgrad``: stop after the fused tower (the caller runs wgrad + finalize)."""
         if self.fused:
             idx, tv = self._fm_forward(B, train=True)
-            KN.tower(self._tower_args(B, train=True))
+            KN.tower(self._tower_args(B, train=True, gslot=gslot))
             if not defer_wgrad:
                 KN.wgrad_group(self._wg_jobs, self._nwg_jobs, self._wg_tasks)
                 self._finalize_grads()
@@ -871,6 +888,7 @@ class NativeDeepFM:
         A.h = self.h_sparse
         A.step = self.step.data_ptr()
         A.ldv, A.ldw = KN._ld(self.tv, self.tw)
+        A.G = self.Gslot.data_ptr() if getattr(self, "_gslot_step", False) else 0
         return A
 
     def _sparse_backward(self, B: int, idx, tv, presorted: bool = False):
@@ -948,7 +966,9 @@ class NativeDeepFM:
         # more than it saves (0.156 -> 0.161 ms), so there it stays in line.
         split = self.fused and (_DENSE_SIDE_STREAM == "1" or
                                 (_DENSE_SIDE_STREAM == "auto" and self.exchange))
-        idx, tv = self._dense_fwd_bwd(B, defer_wgrad=split)
+        gslot = self._gslot_mode()
+        self._gslot_step = gslot
+        idx, tv = self._dense_fwd_bwd(B, defer_wgrad=split, gslot=gslot)
         main = torch.cuda.current_stream(self.device)
         if presorted:
             main.wait_stream(self._side)

@@ -453,3 +453,26 @@ def test_tower_lds_staged_input_bitwise_equal(monkeypatch, mlp_dtype):
         out.append((m.p.clone(), m.tv.clone(), m.dX0.clone()))
     assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
     assert torch.equal(out[0][2], out[1][2])
+
+
+def test_tower_slot_records_match_dx0_gathers(monkeypatch):
+    """Optional slot-order gradient records (HIPFM_GSLOT): the fused sparse backward fed from
+    the tower's records gives bitwise the same update as the per-sample gathers of dX0/S/x/dy."""
+    import hipfm.models.deepfm as D
+    synth = make_synth("criteo_kaggle", seed=3)
+    F, K, layers, B = synth.F, 8, [128, 64, 32], 1024
+    params = init_params(synth.feature_size, F, K, layers, False, seed=1)
+    out = []
+    for on in (True, False):
+        monkeypatch.setattr(D, "_GSLOT", on)
+        m = NativeDeepFM(synth.feature_size, F, K, layers, [0.5] * 3, batch_size=B, device=DEV, init=False,
+                         sparse_update="lazy", field_ranges=synth.field_ranges())
+        m.load_tf_params(params)
+        for s in range(3):
+            ids, vals, lab = synth.batch(B, step=s, device=DEV, id_dtype=torch.int32)
+            m.train_step(ids, vals, lab, use_graph=True)
+        torch.cuda.synchronize()
+        assert m._gslot_step == on
+        out.append((m.tv.clone(), m.tw.clone(), m.p.clone()))
+    for x, y in zip(*out):
+        assert torch.equal(x, y)
