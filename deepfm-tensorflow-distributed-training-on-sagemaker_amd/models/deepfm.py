@@ -434,10 +434,13 @@ class NativeDeepFM:
         self.sf_tinfo = torch.zeros(nt, 4, **i32)
         self._fsort = None
         if self.field_ranges is not None:
-            # on the single-GPU step the sort overlaps the forward on a side stream: one workgroup
-            # per field; on the sharded step it gates the row exchange: 16-way MSD split per field
+            # the sort runs on a side stream next to the step in both cases, and every sort
+            # workgroup holds 148 KB of LDS: one workgroup per field on one GPU (0.160 ms/step vs
+            # 0.162 / 0.169 / 0.179 with 2 / 4 / 16 per field); 4 per field for the next batch's
+            # routing on the sharded step (0.198 ms vs 0.206 with 16; HIPFM_FSORT_PB overrides)
+            pb = os.environ.get("HIPFM_FSORT_PB")
             self._fsort = KN.FieldSort(self.field_ranges, min(M, KN.field_sort_max_rows()), dev,
-                                       max_pb=4 if self.sharded else 0)
+                                       max_pb=int(pb) if pb is not None else (2 if self.sharded else 0))
         tb = max(KN.radix_temp_bytes(n), KN.rbk_temp_bytes(K, n), KN.scan_temp_bytes(n))
         self.temp = torch.zeros(tb + 256, dtype=torch.uint8, device=dev)
         self._build_finalize_jobs()
