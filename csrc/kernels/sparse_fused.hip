@@ -57,6 +57,8 @@ struct SfArgs {
   float* gout;
   const float* G;  // optional slot-order gradient records from the tower ([n][K+4]); replaces
                    // the vals / dlogit / S / dX0 gathers
+  int step_off;    // 1: *step is this step's index - 1 (the dense optimizer advances it later);
+                   // 0: the dense optimizer already ran and advanced it (single-GPU early mode)
 };
 
 // MODE 0: lazy optimizer OPT on the row; 1: tf1_dense scatter of the row gradient;
@@ -112,7 +114,7 @@ __device__ __forceinline__ void sf_apply_row(const SfArgs& A, int key, int hpos,
 
 template <int OPT>
 __device__ __forceinline__ float sf_lr_t(const SfArgs& A) {
-  return OPT == OPT_ADAM ? adam_lr_t(A.h, *A.step + 1) : A.h.lr;
+  return OPT == OPT_ADAM ? adam_lr_t(A.h, *A.step + A.step_off) : A.h.lr;
 }
 
 template <int K, int MODE, int OPT>

@@ -44,6 +44,7 @@ _OLD_FINALIZE = os.environ.get("HIPFM_OLD_FINALIZE", "0") == "1"
 _SORT_MODE = os.environ.get("HIPFM_SORT", "auto")                # auto | global
 _SORT_SIDE_STREAM = os.environ.get("HIPFM_SORT_SIDE_STREAM", "1") == "1"
 _SORT_FORK = os.environ.get("HIPFM_SORT_FORK", "after_fm")         # start | after_fm
+_DENSE_EARLY = os.environ.get("HIPFM_DENSE_EARLY", "1") == "1"
 _SPARSE_IMPL = os.environ.get("HIPFM_SPARSE", "fused")             # fused | seg
 _SHARD_PIPELINE = os.environ.get("HIPFM_SHARD_PIPELINE", "1") == "1"
 _DENSE_SIDE_STREAM = os.environ.get("HIPFM_DENSE_SIDE_STREAM", "auto")   # auto | 1 | 0
@@ -288,6 +289,7 @@ class NativeDeepFM:
         self._comm_stream = None
         self.shx = None
         self._shx_plan = None
+        self._dense_early = False
         self.batch_size = int(batch_size)
         # fused deep tower (csrc/kernels/tower.hip): whole forward + head + dgrad chain in one
         # launch per 32-sample block; batch norm (needs batch-wide statistics between the
@@ -897,6 +899,7 @@ class NativeDeepFM:
         A.step = self.step.data_ptr()
         A.ldv, A.ldw = KN._ld(self.tv, self.tw)
         A.G = self.Gslot.data_ptr() if getattr(self, "_gslot_step", False) else 0
+        A.step_off = 0 if self._dense_early else 1
         return A
 
     def _sparse_backward(self, B: int, idx, tv, presorted: bool = False):
@@ -988,6 +991,13 @@ class NativeDeepFM:
         self._gslot_step = gslot
         idx, tv = self._dense_fwd_bwd(B, defer_wgrad=split, gslot=gslot, after_fm=after_fm)
         main = torch.cuda.current_stream(self.device)
+        # single GPU, lazy rows: the dense optimizer needs only the finished dense gradient, so it
+        # runs BEFORE the join with the side-stream sort, inside the gap the join costs anyway;
+        # it advances the step counter, and the sparse kernels are told so (SfArgs.step_off)
+        self._dense_early = (presorted and not self.exchange and _DENSE_EARLY and
+                             self.sparse_update == "lazy" and _SPARSE_IMPL == "fused")
+        if self._dense_early:
+            self._dense_opt()
         if presorted:
             main.wait_stream(self._side)
         work = None
@@ -1016,6 +1026,11 @@ class NativeDeepFM:
             self.comm.wait(work)
         if self.shx is not None:
             self.shx.end(self._shx_plan)
+        if not self._dense_early:
+            self._dense_opt()
+
+    def _dense_opt(self):
+        """Dense optimizer over the flat buffer (+ bf16 / fp8 weight shadows); advances the step."""
         if _SEPARATE_STEP_INC:
             KN.dense_opt(self.opt_id, self.p, self.g, self.sd[0], self.sd[1], self.P, self.h_dense,
                          self.step, self._shadow_dev, self._nshadow)
