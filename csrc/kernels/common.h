@@ -100,3 +100,47 @@ __device__ __forceinline__ void opt_update(float& p, float g, float& s0, float& 
     p -= h.lr * g;
   }
 }
+
+// A weight matrix [rows, cols] inside the flat dense buffer with bf16 copies (MFMA operands).
+struct ShadowSeg {
+  long off;          // element offset in the flat buffer
+  int rows, cols;
+  bf16* w16;         // [rows, cols]
+  bf16* wt16;        // [cols, rows]
+};
+
+// Dense optimizer applied by the thread that produces an element's final gradient (the
+// single-GPU finalize + dense_opt fusion, mlp.hip): no second pass over the flat buffer.
+struct FinOpt {
+  float* p;
+  float* g;          // flat gradient buffer; a finalize output outside [g, g + n) is no parameter
+  float* s0;
+  float* s1;
+  long n;
+  OptHyper h;
+  int64_t* step;     // read by every block; the last block to finish advances it
+  const ShadowSeg* segs;
+  int nseg;
+  unsigned* done_ctr;
+};
+
+template <int OPT>
+__device__ __forceinline__ void fin_opt_apply(const FinOpt& o, float lr_t, const float* dst, float gv) {
+  const long i = dst - o.g;
+  if (i < 0 || i >= o.n) return;
+  float pi = o.p[i];
+  float a = (OPT != OPT_GD) ? o.s0[i] : 0.f;
+  float c = (OPT == OPT_ADAM || OPT == OPT_FTRL) ? o.s1[i] : 0.f;
+  opt_update<OPT>(pi, gv, a, c, o.h, lr_t);
+  o.p[i] = pi;
+  if (OPT != OPT_GD) o.s0[i] = a;
+  if (OPT == OPT_ADAM || OPT == OPT_FTRL) o.s1[i] = c;
+  for (int s = 0; s < o.nseg; ++s) {
+    const long rel = i - o.segs[s].off;
+    if (rel >= 0 && rel < (long)o.segs[s].rows * o.segs[s].cols) {
+      const int r = (int)(rel / o.segs[s].cols), cc = (int)(rel % o.segs[s].cols);
+      o.segs[s].w16[rel] = f2bf(pi);
+      o.segs[s].wt16[(long)cc * o.segs[s].rows + r] = f2bf(pi);
+    }
+  }
+}

@@ -84,7 +84,8 @@ __global__ void __launch_bounds__(256) fm_fwd2_kernel(
     const int* __restrict__ idx, const float* __restrict__ vals, const float* __restrict__ tv,
     const float* __restrict__ tw, const float* __restrict__ bias, int B, int F, int KP,
     float* __restrict__ y_fm, float* __restrict__ S, bf16* __restrict__ E, bf16* __restrict__ Et,
-    uint8_t* __restrict__ E8, float* __restrict__ sE, long ldv, long ldw) {
+    uint8_t* __restrict__ E8, float* __restrict__ sE, long ldv, long ldw, int* __restrict__ idsT,
+    int Bt) {
   constexpr int SB = 256 / K;
   constexpr int V4 = K / 4;
   extern __shared__ __attribute__((aligned(16))) float fsm[];
@@ -92,6 +93,7 @@ __global__ void __launch_bounds__(256) fm_fwd2_kernel(
   float* et = fsm;                     // [SB][RS]
   float* wx = fsm + SB * RS;           // [SB][F]
   float* qs = wx + SB * F;             // [SB] fp8 row scales (E8 mode)
+  int* il = reinterpret_cast<int*>(qs + SB);  // [SB][F] the tile's ids (idsT mode)
   const int s0 = blockIdx.x * SB;
   const int nsb = min(SB, B - s0);
   const int npair = nsb * F;
@@ -107,6 +109,7 @@ __global__ void __launch_bounds__(256) fm_fwd2_kernel(
     const float w = tw[(size_t)id * ldw];
     const int sl = p / F, f = p - sl * F;
     wx[sl * F + f] = w * x;
+    if (idsT) il[p] = id;
     float* dst = et + sl * RS + f * K;
 #pragma unroll
     for (int j = 0; j < V4; ++j) {
@@ -122,6 +125,15 @@ __global__ void __launch_bounds__(256) fm_fwd2_kernel(
     }
   }
   __syncthreads();
+  if (idsT) {
+    // field-major copy of the ids for the per-field sort (field_sort.hip), which then needs no
+    // transpose launch of its own: one field's SB consecutive samples per coalesced segment
+    // (LDS reads at stride F, odd for Criteo's 39: conflict-free)
+    for (int e = threadIdx.x; e < F * SB; e += 256) {
+      const int f = e / SB, sl = e - f * SB;
+      if (sl < nsb && s0 + sl < Bt) idsT[(size_t)f * Bt + s0 + sl] = il[sl * F + f];
+    }
+  }
   {  // per (sample, k): S, sum e^2, y_w, y_v — fixed order over fields
     const int sl = threadIdx.x / K, k = threadIdx.x % K;
     float sum = 0.f, sq = 0.f, yw = 0.f, am = 0.f;
@@ -211,16 +223,18 @@ __global__ void __launch_bounds__(256) fm_bwd_sorted_kernel(
 template <int K>
 static int launch_fm_fwd(const int* idx, const float* vals, const float* tv, const float* tw,
                          const float* bias, int B, int F, int KP, float* y_fm, float* S, bf16* E,
-                         bf16* Et, uint8_t* E8, float* sE, long ldv, long ldw, hipStream_t st) {
+                         bf16* Et, uint8_t* E8, float* sE, long ldv, long ldw, int* idsT, int Bt,
+                         hipStream_t st) {
   constexpr int SB = 256 / K;
-  const size_t lds2 = ((size_t)SB * (F * K + 1) + (size_t)SB * F + SB) * 4;
+  const size_t lds2 = ((size_t)SB * (F * K + 1) + (size_t)SB * F * (idsT ? 2 : 1) + SB) * 4;
   if (lds2 <= 120 * 1024) {
     const int grid = (B + SB - 1) / SB;
     hipLaunchKernelGGL(fm_fwd2_kernel<K>, dim3(grid), dim3(256), lds2, st, idx, vals, tv, tw, bias,
-                       B, F, KP, y_fm, S, E, Et, E8, sE, ldv, ldw);
+                       B, F, KP, y_fm, S, E, Et, E8, sE, ldv, ldw, idsT, Bt);
     HFM_LAUNCH_CHECK();
   }
-  if (E8 || !E) return (int)hipErrorInvalidValue;  // fp8 output: only the row-tile variant
+  // fp8 output and the field-major id copy: only the row-tile variant
+  if (E8 || !E || idsT) return (int)hipErrorInvalidValue;  // fp8 output: only the row-tile variant
   // very wide inputs (F*K > ~30K): lane-group-per-sample variant, small LDS footprint
   constexpr int LPS = K / 4;
   constexpr int SB1 = 256 / LPS;
@@ -255,12 +269,15 @@ static int launch_fm_bwd(const int* perm, const int* idx, const float* vals, con
 
 HFM_API int hfm_fm_fwd(const int* idx, const float* vals, const float* tv, const float* tw,
                        const float* bias, int B, int F, int K, int KP, float* y_fm, float* S,
-                       void* E, void* Et, void* E8, float* sE, long ldv, long ldw, hipStream_t st) {
+                       void* E, void* Et, void* E8, float* sE, long ldv, long ldw, int* idsT,
+                       int Bt, hipStream_t st) {
   // ldv / ldw: floats between consecutive rows of the v table and entries of the w table
   // (K and 1 for plain tables; the record stride for the interleaved row-record layout).
   // E8 / sE (optional): the MLP input as OCP fp8 e4m3 rows with per-row dequant factors
   // (mlp_dtype = fp8); E may then be null.
-#define CALL(KK) launch_fm_fwd<KK>(idx, vals, tv, tw, bias, B, F, KP, y_fm, S, (bf16*)E, (bf16*)Et, (uint8_t*)E8, sE, ldv, ldw, st)
+  // idsT (optional): also write the first Bt samples' ids field-major ([F, Bt]) for
+  // hfm_field_sort_pre.
+#define CALL(KK) launch_fm_fwd<KK>(idx, vals, tv, tw, bias, B, F, KP, y_fm, S, (bf16*)E, (bf16*)Et, (uint8_t*)E8, sE, ldv, ldw, idsT, Bt, st)
   HFM_K_DISPATCH(K, CALL)
 #undef CALL
 }

@@ -363,14 +363,20 @@ __global__ void __launch_bounds__(256) slab_reduce_kernel(const SlabJob* __restr
 // remaining blocks compute bias gradients as row sums of dZ^T (one block per row).  Every
 // reduction has a fixed order (deterministic).
 struct RowSumJob;
-__device__ void rowsum_block(const RowSumJob* jobs, int njobs, int b);
+template <int OPT = -1>
+__device__ void rowsum_block(const RowSumJob* jobs, int njobs, int b, const FinOpt* o = nullptr,
+                             float lr_t = 0.f);
 
-__global__ void __launch_bounds__(256) finalize_kernel(const SlabJob* __restrict__ sj, int nsj,
-                                                       int nslab_blocks, const RowSumJob* rj,
-                                                       int nrj) {
+// OPT >= 0 (single GPU, dense optimizer fused): the thread that writes an element's final
+// gradient also applies the optimizer to it (fin_opt_apply), and the last block to finish
+// advances the step counter -- the separate dense_opt launch and its kernel boundary go away.
+template <int OPT>
+__device__ __forceinline__ void finalize_block(const SlabJob* __restrict__ sj, int nsj,
+                                               int nslab_blocks, const RowSumJob* rj, int nrj,
+                                               const FinOpt& o, float lr_t) {
   const int b = blockIdx.x;
   if (b >= nslab_blocks) {
-    rowsum_block(rj, nrj, b - nslab_blocks);
+    rowsum_block<OPT>(rj, nrj, b - nslab_blocks, &o, lr_t);
     return;
   }
   int j = 0;
@@ -388,7 +394,10 @@ __global__ void __launch_bounds__(256) finalize_kernel(const SlabJob* __restrict
     for (int z = zl; z < nslab; z += lanes) s += sp[(size_t)z * stride];
   }
   if (lanes == 1) {
-    if (i < n) jr.dst[i] = s * jr.scale;
+    if (i < n) {
+      jr.dst[i] = s * jr.scale;
+      if (OPT >= 0) fin_opt_apply<OPT>(o, lr_t, jr.dst + i, s * jr.scale);
+    }
     return;
   }
   // lanes > 1: per in {32, 128}; combine the lanes in order through LDS
@@ -399,6 +408,29 @@ __global__ void __launch_bounds__(256) finalize_kernel(const SlabJob* __restrict
     float t = 0.f;
     for (int l = 0; l < lanes; ++l) t += red2[l * per + e];
     jr.dst[i] = t * jr.scale;
+    if (OPT >= 0) fin_opt_apply<OPT>(o, lr_t, jr.dst + i, t * jr.scale);
+  }
+}
+
+__global__ void __launch_bounds__(256) finalize_kernel(const SlabJob* __restrict__ sj, int nsj,
+                                                       int nslab_blocks, const RowSumJob* rj,
+                                                       int nrj) {
+  finalize_block<-1>(sj, nsj, nslab_blocks, rj, nrj, FinOpt{}, 0.f);
+}
+
+template <int OPT>
+__global__ void __launch_bounds__(256) finalize_opt_kernel(const SlabJob* __restrict__ sj, int nsj,
+                                                           int nslab_blocks, const RowSumJob* rj,
+                                                           int nrj, FinOpt o) {
+  const float lr_t = OPT == OPT_ADAM ? adam_lr_t(o.h, *o.step + 1) : o.h.lr;
+  finalize_block<OPT>(sj, nsj, nslab_blocks, rj, nrj, o, lr_t);
+  __syncthreads();
+  if (threadIdx.x == 0) {  // every block has read *step (lr_t) before it arrives here
+    const unsigned prev = atomicAdd(o.done_ctr, 1u);
+    if (prev == gridDim.x - 1) {
+      *o.step += 1;
+      *o.done_ctr = 0u;
+    }
   }
 }
 
@@ -408,6 +440,27 @@ HFM_API int hfm_finalize(const void* slab_jobs, int nsj, int nslab_blocks, const
   if (grid <= 0) return 0;
   hipLaunchKernelGGL(finalize_kernel, dim3(grid), dim3(256), 0, st, (const SlabJob*)slab_jobs, nsj,
                      nslab_blocks, (const RowSumJob*)row_jobs, nrj);
+  HFM_LAUNCH_CHECK();
+}
+
+HFM_API int hfm_finalize_opt(int opt, const void* slab_jobs, int nsj, int nslab_blocks,
+                             const void* row_jobs, int nrj, int total_rows, float* p, float* g,
+                             float* s0, float* s1, long n, const OptHyper* h, int64_t* step,
+                             const void* segs, int nseg, unsigned* done_ctr, hipStream_t st) {
+  const int grid = nslab_blocks + total_rows;
+  if (grid <= 0 || !done_ctr) return (int)hipErrorInvalidValue;
+  const FinOpt o{p, g, s0, s1, n, *h, step, (const ShadowSeg*)segs, nseg, done_ctr};
+  switch (opt) {
+#define CASE(O)                                                                                 \
+  case O:                                                                                       \
+    hipLaunchKernelGGL(finalize_opt_kernel<O>, dim3(grid), dim3(256), 0, st,                    \
+                       (const SlabJob*)slab_jobs, nsj, nslab_blocks, (const RowSumJob*)row_jobs, \
+                       nrj, o);                                                                 \
+    break;
+    CASE(OPT_ADAM) CASE(OPT_ADAGRAD) CASE(OPT_MOMENTUM) CASE(OPT_FTRL) CASE(OPT_GD)
+#undef CASE
+    default: return (int)hipErrorInvalidValue;
+  }
   HFM_LAUNCH_CHECK();
 }
 
@@ -427,7 +480,8 @@ struct RowSumJob {
   long ld;
 };
 
-__device__ void rowsum_block(const RowSumJob* jobs, int njobs, int b) {
+template <int OPT>
+__device__ void rowsum_block(const RowSumJob* jobs, int njobs, int b, const FinOpt* o, float lr_t) {
   __shared__ float red[256];
   // b enumerates (job, row) pairs
   int rem = b, ji = 0;
@@ -447,7 +501,10 @@ __device__ void rowsum_block(const RowSumJob* jobs, int njobs, int b) {
     if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
     __syncthreads();
   }
-  if (threadIdx.x == 0) j.dst[rem] = red[0];
+  if (threadIdx.x == 0) {
+    j.dst[rem] = red[0];
+    if (OPT >= 0) fin_opt_apply<OPT>(*o, lr_t, j.dst + rem, red[0]);
+  }
 }
 
 __global__ void __launch_bounds__(256) rowsum_kernel(const RowSumJob* __restrict__ jobs, int njobs) {

@@ -133,12 +133,7 @@ __global__ void __launch_bounds__(256) dense_sweep_kernel(
 }
 
 // ------------------------------------------------------------------ dense flat params
-struct ShadowSeg {   // a weight matrix [rows, cols] inside the flat buffer with bf16 copies
-  long off;          // element offset in the flat buffer
-  int rows, cols;
-  bf16* w16;         // [rows, cols]
-  bf16* wt16;        // [cols, rows]
-};
+// ShadowSeg: common.h
 
 template <int OPT>
 __global__ void __launch_bounds__(256) dense_opt_kernel(

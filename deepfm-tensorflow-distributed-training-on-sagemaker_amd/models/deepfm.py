@@ -43,8 +43,10 @@ _SEPARATE_STEP_INC = os.environ.get("HIPFM_STEP_INC", "0") == "1"
 _OLD_FINALIZE = os.environ.get("HIPFM_OLD_FINALIZE", "0") == "1"
 _SORT_MODE = os.environ.get("HIPFM_SORT", "auto")                # auto | global
 _SORT_SIDE_STREAM = os.environ.get("HIPFM_SORT_SIDE_STREAM", "1") == "1"
-_SORT_FORK = os.environ.get("HIPFM_SORT_FORK", "after_fm")         # start | after_fm
+_SORT_FORK = os.environ.get("HIPFM_SORT_FORK", "after_fm")   # start | after_fm | after_tower
 _DENSE_EARLY = os.environ.get("HIPFM_DENSE_EARLY", "1") == "1"
+_FWD_IDST = os.environ.get("HIPFM_FWD_IDST", "1") == "1"         # fm_fwd writes ids field-major
+_FUSE_FIN_OPT = os.environ.get("HIPFM_FUSE_FIN_OPT", "1") == "1"  # dense optimizer in finalize
 _SPARSE_IMPL = os.environ.get("HIPFM_SPARSE", "fused")             # fused | seg
 _SHARD_PIPELINE = os.environ.get("HIPFM_SHARD_PIPELINE", "1") == "1"
 _DENSE_SIDE_STREAM = os.environ.get("HIPFM_DENSE_SIDE_STREAM", "auto")   # auto | 1 | 0
@@ -290,6 +292,8 @@ class NativeDeepFM:
         self.shx = None
         self._shx_plan = None
         self._dense_early = False
+        self._fuse_opt = False     # dense optimizer fused into the finalize launch (this step)
+        self._idsT_B = 0
         self.batch_size = int(batch_size)
         # fused deep tower (csrc/kernels/tower.hip): whole forward + head + dgrad chain in one
         # launch per 32-sample block; batch norm (needs batch-wide statistics between the
@@ -500,6 +504,14 @@ class NativeDeepFM:
         self._row_jobs = KN.struct_array_to_device(rj, self.device)
         self._nrow_jobs = len(rj)
         self._row_total = sum(self.Np)
+        # the dense optimizer can ride on the finalize launch only if finalize writes the final
+        # gradient of EVERY flat parameter (not so with batch norm: bn.hip writes beta / gamma)
+        cov = torch.zeros(self.P, dtype=torch.bool)
+        for d, n in [(j.dst, j.n) for j in jobs] + [(r.dst, r.rows) for r in rj]:
+            o = (d - g0) // 4
+            if 0 <= o < self.P:
+                cov[o:o + n] = True
+        self._fin_covers_all = bool(cov.all()) and not self.batch_norm
 
     def _build_wgrad_jobs(self):
         jobs, task0 = [], 0
@@ -578,15 +590,19 @@ class NativeDeepFM:
         a.partial = self.partial.data_ptr()
         return a
 
-    def _dense_fwd_bwd(self, B: int, defer_wgrad: bool = False, gslot: bool = False, after_fm=None):
+    def _dense_fwd_bwd(self, B: int, defer_wgrad: bool = False, gslot: bool = False, after_fm=None,
+                       after_tower=None):
         """Forward, loss head and the whole deep-tower backward (dense grads into self.g, dX0
         for the FM backward).  Returns the (idx, table) pair the sparse backward uses.
-        ``defer_wgrad``: stop after the fused tower (the caller runs wgrad + finalize)."""
+        ``defer_wgrad``: stop after the fused tower (the caller runs wgrad + finalize).
+        ``after_fm`` / ``after_tower``: hooks called once the FM forward / the tower is enqueued."""
         if self.fused:
             idx, tv = self._fm_forward(B, train=True)
             if after_fm is not None:
                 after_fm()
             KN.tower(self._tower_args(B, train=True, gslot=gslot))
+            if after_tower is not None:
+                after_tower()
             if not defer_wgrad:
                 KN.wgrad_group(self._wg_jobs, self._nwg_jobs, self._wg_tasks)
                 self._finalize_grads()
@@ -594,6 +610,8 @@ class NativeDeepFM:
         idx, tv = self._forward(B, train=True)
         if after_fm is not None:
             after_fm()
+        if after_tower is not None:
+            after_tower()
         self._head(B, train=True)
         self._mlp_backward(B)
         return idx, tv
@@ -692,12 +710,15 @@ class NativeDeepFM:
         elif self.sharded:
             idx, tv, tw = self.comm.sharded_forward_gather(self, B)
         fm_bias = self.p[self.dense_segs["fm_bias"].off:]
+        # the side-stream field sort forked after this launch reads the ids field-major from it
+        ib = self._idsT_B if train else 0
+        ext = dict(idsT=self._fsort.idsT, Bt=ib) if ib else {}
         if self.fp8:
             KN.fm_fwd(idx, self.vals, tv, tw, fm_bias, M, F, K, self.K0p, self.y_fm, self.S, None,
-                      self.Et if train else None, E8=self.E8, sE=self.sE)
+                      self.Et if train else None, E8=self.E8, sE=self.sE, **ext)
         else:
             KN.fm_fwd(idx, self.vals, tv, tw, fm_bias, M, F, K, self.K0p, self.y_fm, self.S, self.E,
-                      self.Et if train else None)
+                      self.Et if train else None, **ext)
         return idx, tv
 
     def _forward(self, B: int, train: bool):
@@ -836,6 +857,12 @@ class NativeDeepFM:
             KN.slab_reduce(self._slab_jobs, self._nslab_jobs, self._slab_maxn)
             KN.rowsum(self._row_jobs, self._nrow_jobs, self._row_total)
             return
+        if self._fuse_opt:
+            KN.finalize_opt(self.opt_id, self._slab_jobs, self._nslab_jobs, self._slab_blocks,
+                            self._row_jobs, self._nrow_jobs, self._row_total, self.p, self.g,
+                            self.sd[0], self.sd[1], self.P, self.h_dense, self.step,
+                            self._shadow_dev, self._nshadow, self._done_ctr)
+            return
         KN.finalize(self._slab_jobs, self._nslab_jobs, self._slab_blocks, self._row_jobs,
                     self._nrow_jobs, self._row_total)
 
@@ -962,21 +989,40 @@ class NativeDeepFM:
         presorted = False
         if self.shx is not None:
             self._shx_start(B)
-        after_fm = None
+        after_fm = after_tower = None
         if not self.sharded and _SORT_SIDE_STREAM:
             main = torch.cuda.current_stream(self.device)
             if self._side is None:
                 self._side = torch.cuda.Stream(self.device)
 
+            # fm_fwd writes the ids field-major as it reads them, so the forked sort skips its
+            # transpose launch (the sort branch is the step's critical path)
+            pre = (_SORT_FORK != "start" and _FWD_IDST and self.uses_field_sort(B) and
+                   KN.fm_fwd_writes_idsT(self.F, self.K))
+            self._idsT_B = B if pre else 0
+            fork = []
+
+            def mark():
+                fork.append(main.record_event())
+
             def fork_sort():
-                self._side.wait_stream(main)
+                if fork:
+                    self._side.wait_event(fork[0])
+                else:
+                    self._side.wait_stream(main)
                 with torch.cuda.stream(self._side):
-                    self._sort_slots(B)
+                    if pre:
+                        self._fsort.sort_pre(B, self.sorted_keys, self.perm)
+                    else:
+                        self._sort_slots(B)
             # graph branches launch in capture order: forking after fm_fwd is enqueued lets the
             # step's first kernel start at once instead of after the sort's launches
-            # (same-box A/B: 0.160 -> 0.154 ms/step, bitwise-identical results)
+            # (same-box A/B: 0.160 -> 0.154 ms/step, bitwise-identical results); after_tower
+            # keeps the fork point after fm_fwd but enqueues the sort after the tower
             if _SORT_FORK == "after_fm":
                 after_fm = fork_sort
+            elif _SORT_FORK == "after_tower":
+                after_fm, after_tower = mark, fork_sort
             else:
                 fork_sort()
             presorted = True
@@ -989,14 +1035,25 @@ class NativeDeepFM:
                                 (_DENSE_SIDE_STREAM == "auto" and self.exchange))
         gslot = self._gslot_mode()
         self._gslot_step = gslot
-        idx, tv = self._dense_fwd_bwd(B, defer_wgrad=split, gslot=gslot, after_fm=after_fm)
-        main = torch.cuda.current_stream(self.device)
         # single GPU, lazy rows: the dense optimizer needs only the finished dense gradient, so it
         # runs BEFORE the join with the side-stream sort, inside the gap the join costs anyway;
-        # it advances the step counter, and the sparse kernels are told so (SfArgs.step_off)
-        self._dense_early = (presorted and not self.exchange and _DENSE_EARLY and
+        # it advances the step counter, and the sparse kernels are told so (SfArgs.step_off).
+        # With the fused tower it rides on the finalize launch itself (one kernel boundary less)
+        self._dense_early = (presorted and not self.exchange and not split and _DENSE_EARLY and
                              self.sparse_update == "lazy" and _SPARSE_IMPL == "fused")
-        if self._dense_early:
+        self._fuse_opt = (self._dense_early and self.fused and _FUSE_FIN_OPT and
+                          not _OLD_FINALIZE and self._fin_covers_all)
+        try:
+            idx, tv = self._dense_fwd_bwd(B, defer_wgrad=split, gslot=gslot, after_fm=after_fm,
+                                          after_tower=after_tower)
+        finally:
+            self._idsT_B = 0
+            fused_opt, self._fuse_opt = self._fuse_opt, False
+        main = torch.cuda.current_stream(self.device)
+        if fused_opt:
+            if self.fp8:
+                KN.w8_quant(self._w8_jobs, len(self.layers), self._w8_rows)
+        elif self._dense_early:
             self._dense_opt()
         if presorted:
             main.wait_stream(self._side)

@@ -127,7 +127,8 @@ class WgJob(C.Structure):
 
 
 _SIGS = {
-    "hfm_fm_fwd": [c_void_p] * 5 + [c_int] * 4 + [c_void_p] * 6 + [c_long, c_long, c_void_p],
+    "hfm_fm_fwd": [c_void_p] * 5 + [c_int] * 4 + [c_void_p] * 6 + [c_long, c_long, c_void_p, c_int,
+                                                                      c_void_p],
     "hfm_fm_bwd_sorted": [c_void_p] * 7 + [c_int] * 4 + [c_void_p, c_void_p],
     "hfm_grad_row_bytes": [c_int],
     "hfm_sort_pairs_temp_bytes": [c_int, c_int, C.POINTER(c_size_t)],
@@ -146,6 +147,8 @@ _SIGS = {
     "hfm_dense_opt": [c_int] + [c_void_p] * 4 + [c_long, C.POINTER(OptHyper), c_void_p, c_void_p, c_int,
                                                  c_void_p, c_void_p],
     "hfm_finalize": [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p],
+    "hfm_finalize_opt": [c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_int] + [c_void_p] * 4
+                        + [c_long, C.POINTER(OptHyper), c_void_p, c_void_p, c_int, c_void_p, c_void_p],
     "hfm_shadow_refresh": [c_void_p, c_long, c_void_p, c_int, c_void_p],
     "hfm_step_inc": [c_void_p, c_void_p],
     "hfm_shadow_seg_bytes": [],
@@ -186,6 +189,7 @@ _SIGS = {
     "hfm_sparse_fused_args_bytes": [],
     "hfm_field_sort_max_pb": [],
     "hfm_field_sort": [c_void_p, c_int, c_int, c_void_p, c_void_p, c_int] + [c_void_p] * 4 + [c_void_p],
+    "hfm_field_sort_pre": [c_void_p, c_int, c_int, c_void_p, c_void_p, c_int] + [c_void_p] * 3 + [c_void_p],
     "hfm_radix_sort_ids": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_size_t, c_void_p],
     "hfm_segments": [c_void_p, c_int] + [c_void_p] * 5 + [c_void_p, c_size_t, c_void_p],
     "hfm_fm_bwd_seg": [c_int] + [c_void_p] * 7 + [c_int, c_int, c_int, c_void_p, c_void_p, c_void_p],

@@ -34,15 +34,28 @@ def _ld(tv, tw):
     return ldv, ldw
 
 
-def fm_fwd(idx, vals, tv, tw, bias, B, F, K, KP, y_fm, S, E, Et, E8=None, sE=None):
+def fm_fwd(idx, vals, tv, tw, bias, B, F, K, KP, y_fm, S, E, Et, E8=None, sE=None, idsT=None,
+           Bt=0):
     """FM forward (y_fm, S) + the MLP input: E (bf16 [B, KP]) and/or E8 (OCP fp8 e4m3 rows,
-    per-row dequant factors sE) for the fp8 tower; Et (bf16 [KP, B]) for the weight gradient."""
+    per-row dequant factors sE) for the fp8 tower; Et (bf16 [KP, B]) for the weight gradient.
+    ``idsT`` (int32 [F * Bt], optional): the first Bt samples' ids written field-major for
+    ``FieldSort.sort_pre`` (row-tile variant only, see ``fm_fwd_writes_idsT``)."""
     assert tv.stride(-1) == 1
     if E8 is not None:
         assert E8.dtype == torch.uint8 and E8.is_contiguous() and sE is not None
+    if idsT is not None:
+        assert fm_fwd_writes_idsT(F, K) and 0 < Bt <= B and idsT.numel() >= F * Bt
     check(L().hfm_fm_fwd(ptr(idx), ptr(vals), ptr(tv), ptr(tw), ptr(bias), B, F, K, KP, ptr(y_fm),
-                         ptr(S), ptr(E), ptr(Et), ptr(E8), ptr(sE), *_ld(tv, tw), stream_handle()),
+                         ptr(S), ptr(E), ptr(Et), ptr(E8), ptr(sE), *_ld(tv, tw), ptr(idsT), int(Bt),
+                         stream_handle()),
           "fm_fwd")
+
+
+def fm_fwd_writes_idsT(F: int, K: int) -> bool:
+    """Whether fm_fwd takes the row-tile variant (csrc/kernels/fm.hip launch_fm_fwd), the one
+    that can also write the field-major id copy."""
+    sb = 256 // K
+    return (sb * (F * K + 1) + 2 * sb * F + sb) * 4 <= 120 * 1024
 
 
 def fm_bwd_sorted(perm, idx, vals, tv, dlogit, dX0, S, n, F, K, KP, G):
@@ -147,6 +160,13 @@ class FieldSort:
                                  ptr(self.idsT), ptr(keys_out), ptr(perm_out), ptr(self.err),
                                  stream_handle()), "field_sort")
 
+    def sort_pre(self, B: int, keys_out, perm_out):
+        """The sort alone, from ``self.idsT`` already filled field-major ([F, B]) by fm_fwd."""
+        assert B <= self.max_rows
+        check(L().hfm_field_sort_pre(ptr(self.idsT), B, self.F, ptr(self.fr), ptr(self.work),
+                                     self.nwork, ptr(keys_out), ptr(perm_out), ptr(self.err),
+                                     stream_handle()), "field_sort_pre")
+
 
 def sort_error(temp) -> int:
     """1 if the last onesweep sort in ``temp`` timed out in its look-back (device read: syncs)."""
@@ -242,6 +262,16 @@ def finalize(slab_jobs_dev, nsj, nslab_blocks, row_jobs_dev, nrj, total_rows):
     """Split-K / head-partial reductions and bias row sums in one launch (mlp.hip)."""
     check(L().hfm_finalize(ptr(slab_jobs_dev), nsj, nslab_blocks, ptr(row_jobs_dev), nrj, total_rows,
                            stream_handle()), "finalize")
+
+
+def finalize_opt(opt, slab_jobs_dev, nsj, nslab_blocks, row_jobs_dev, nrj, total_rows, p, g, s0, s1,
+                 n, h: OptHyper, step, segs_dev, nseg, done_ctr):
+    """``finalize`` with the dense optimizer fused in (mlp.hip finalize_opt_kernel): every
+    element's update is applied by the thread that produces its final gradient, the last block
+    advances ``step``.  Only valid when the finalize outputs cover all n parameters."""
+    check(L().hfm_finalize_opt(opt, ptr(slab_jobs_dev), nsj, nslab_blocks, ptr(row_jobs_dev), nrj,
+                               total_rows, ptr(p), ptr(g), ptr(s0), ptr(s1), n, C.byref(h), ptr(step),
+                               ptr(segs_dev), nseg, ptr(done_ctr), stream_handle()), "finalize_opt")
 
 
 def shadow_refresh(p, n, segs_dev, nseg):

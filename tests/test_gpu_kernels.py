@@ -476,3 +476,33 @@ def test_tower_slot_records_match_dx0_gathers(monkeypatch):
         out.append((m.tv.clone(), m.tw.clone(), m.p.clone()))
     for x, y in zip(*out):
         assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("preset,B,M", [("criteo_1tb", 16384, 16384), ("criteo_kaggle", 1000, 1024)])
+def test_fm_fwd_idsT_feeds_field_sort(preset, B, M):
+    """fm_fwd's field-major id copy (idsT, first B of M padded rows) + FieldSort.sort_pre give
+    exactly the transpose + sort launch pair of FieldSort.__call__ (and the stable global sort)."""
+    synth = make_synth(preset)
+    F, K = synth.F, 8
+    assert KN.fm_fwd_writes_idsT(F, K)
+    fs = KN.FieldSort(synth.field_ranges(), B, DEV, max_pb=0)
+    ids = torch.zeros(M, F, dtype=torch.int32, device=DEV)
+    ids[:B] = synth.batch(B, 0, device=DEV, id_dtype=torch.int32)[0]
+    V = int(ids.max().item()) + 1
+    vals = torch.rand(M, F, device=DEV)
+    # stride-0 tables (ldv = ldw = 0): every id reads row 0, so 882M-row ids need no table
+    tv, tw = torch.randn(1, K, device=DEV).expand(V, K), torch.randn(1, device=DEV).expand(V)
+    KP = ((F * K + 31) // 32) * 32
+    y, S = torch.zeros(M, device=DEV), torch.zeros(M, K, device=DEV)
+    E = torch.zeros(M, KP, dtype=torch.bfloat16, device=DEV)
+    fs.idsT.fill_(-1)
+    KN.fm_fwd(ids, vals, tv, tw, torch.zeros(1, device=DEV), M, F, K, KP, y, S, E, None,
+              idsT=fs.idsT, Bt=B)
+    torch.cuda.synchronize()
+    assert torch.equal(fs.idsT[:F * B].view(F, B), ids[:B].t())
+    sk, perm = torch.empty(B * F, dtype=torch.int32, device=DEV), torch.empty(B * F, dtype=torch.int32, device=DEV)
+    fs.sort_pre(B, sk, perm)
+    torch.cuda.synchronize()
+    rk, rp = torch.sort(ids[:B].reshape(-1).long(), stable=True)
+    assert int(fs.err.item()) == 0
+    assert torch.equal(sk.long(), rk) and torch.equal(perm.long(), rp)
