@@ -75,29 +75,32 @@ __device__ __forceinline__ float adam_lr_t(const OptHyper& h, int64_t t) {
   return h.lr * sqrtf(1.f - b2p) / (1.f - b1p);
 }
 
-// One optimizer update of a single element; s0/s1 are the optimizer slots.
+// One optimizer update of a single element; s0/s1 are the optimizer slots.  Every
+// multiply-add is an explicit fmaf and no product feeds a plain add/sub, so the rounding does not
+// depend on which FMAs the compiler would form in the inlining context: the dense optimizer fused
+// into the gradient finalize (fin_opt_apply) and the dense_opt sweep stay bitwise equal.
 template <int OPT>
 __device__ __forceinline__ void opt_update(float& p, float g, float& s0, float& s1,
                                            const OptHyper& h, float lr_t) {
   if (OPT == OPT_ADAM) {
-    s0 = s0 * h.b1 + (1.f - h.b1) * g;
-    s1 = s1 * h.b2 + (1.f - h.b2) * g * g;
+    s0 = fmaf(s0, h.b1, (1.f - h.b1) * g);
+    s1 = fmaf(s1, h.b2, (1.f - h.b2) * g * g);
     p -= lr_t * s0 / (sqrtf(s1) + h.eps);
   } else if (OPT == OPT_ADAGRAD) {
-    s0 += g * g;
-    p -= h.lr * g * rsqrtf(s0);
+    s0 = fmaf(g, g, s0);
+    p = fmaf(-h.lr * g, rsqrtf(s0), p);
   } else if (OPT == OPT_MOMENTUM) {
-    s0 = s0 * h.momentum + g;
-    p -= h.lr * s0;
+    s0 = fmaf(s0, h.momentum, g);
+    p = fmaf(-h.lr, s0, p);
   } else if (OPT == OPT_FTRL) {  // lr_power=-0.5, l1=l2=0 (tf.train.FtrlOptimizer defaults)
-    float a0 = s0, an = a0 + g * g;
+    float a0 = s0, an = fmaf(g, g, a0);
     float sa = sqrtf(an);
     float sigma = (sa - sqrtf(a0)) / h.lr;
-    s1 = s1 + g - sigma * p;
+    s1 = fmaf(-sigma, p, s1 + g);
     s0 = an;
     p = -s1 / (sa / h.lr);
   } else {  // GD
-    p -= h.lr * g;
+    p = fmaf(-h.lr, g, p);
   }
 }
 
@@ -128,6 +131,10 @@ template <int OPT>
 __device__ __forceinline__ void fin_opt_apply(const FinOpt& o, float lr_t, const float* dst, float gv) {
   const long i = dst - o.g;
   if (i < 0 || i >= o.n) return;
+  // gv arrives as an SSA product (slab sum * scale): pin it to a rounded fp32 register so the
+  // update cannot contract that multiply into its own adds -- dense_opt reads g from memory, and
+  // the fused path must stay bitwise equal to it (tests/test_gpu_kernels.py)
+  asm volatile("" : "+v"(gv));
   float pi = o.p[i];
   float a = (OPT != OPT_GD) ? o.s0[i] : 0.f;
   float c = (OPT == OPT_ADAM || OPT == OPT_FTRL) ? o.s1[i] : 0.f;

@@ -505,13 +505,19 @@ class NativeDeepFM:
         self._nrow_jobs = len(rj)
         self._row_total = sum(self.Np)
         # the dense optimizer can ride on the finalize launch only if finalize writes the final
-        # gradient of EVERY flat parameter (not so with batch norm: bn.hip writes beta / gamma)
+        # gradient of EVERY flat parameter (not so with batch norm: bn.hip writes beta / gamma).
+        # Only the segments count: the 64-element alignment gaps between them hold no parameter
+        # (their p / g / slots stay 0, which every optimizer maps to 0 -- dense_opt's sweep over
+        # them is a no-op).
         cov = torch.zeros(self.P, dtype=torch.bool)
         for d, n in [(j.dst, j.n) for j in jobs] + [(r.dst, r.rows) for r in rj]:
             o = (d - g0) // 4
             if 0 <= o < self.P:
                 cov[o:o + n] = True
-        self._fin_covers_all = bool(cov.all()) and not self.batch_norm
+        need = torch.zeros(self.P, dtype=torch.bool)
+        for s in self.dense_segs.values():
+            need[s.off:s.off + int(torch.Size(s.shape).numel())] = True
+        self._fin_covers_all = bool(cov[need].all()) and not self.batch_norm
 
     def _build_wgrad_jobs(self):
         jobs, task0 = [], 0
@@ -1050,6 +1056,7 @@ class NativeDeepFM:
             self._idsT_B = 0
             fused_opt, self._fuse_opt = self._fuse_opt, False
         main = torch.cuda.current_stream(self.device)
+        self._fin_opt_step = fused_opt          # observable by tests: which dense-optimizer path ran
         if fused_opt:
             if self.fp8:
                 KN.w8_quant(self._w8_jobs, len(self.layers), self._w8_rows)

@@ -506,3 +506,37 @@ def test_fm_fwd_idsT_feeds_field_sort(preset, B, M):
     rk, rp = torch.sort(ids[:B].reshape(-1).long(), stable=True)
     assert int(fs.err.item()) == 0
     assert torch.equal(sk.long(), rk) and torch.equal(perm.long(), rp)
+
+
+@pytest.mark.parametrize("opt,mlp_dtype", [("Adam", "bf16"), ("ftrl", "bf16"), ("Adam", "fp8")])
+def test_finalize_fused_dense_opt_bitwise_equal(monkeypatch, opt, mlp_dtype):
+    """The 1-GPU lazy step runs the dense optimizer inside the finalize launch (mlp.hip
+    finalize_opt_kernel); parameters, optimizer slots and the bf16 shadows after graph-replayed
+    steps are bitwise those of the separate dense_opt launch, early or after the sparse join."""
+    import hipfm.models.deepfm as D
+    synth = make_synth("criteo_kaggle", seed=5)
+    F, K, layers, B = synth.F, 8, [128, 64, 32], 1024
+    params = init_params(synth.feature_size, F, K, layers, False, seed=2)
+    out = []
+    for fuse, early in ((True, True), (False, True), (False, False)):
+        monkeypatch.setattr(D, "_FUSE_FIN_OPT", fuse)
+        monkeypatch.setattr(D, "_DENSE_EARLY", early)
+        m = NativeDeepFM(synth.feature_size, F, K, layers, [0.5] * 3, batch_size=B, device=DEV,
+                         init=False, optimizer=opt, sparse_update="lazy", mlp_dtype=mlp_dtype,
+                         field_ranges=synth.field_ranges())
+        m.load_tf_params(params)
+        for s in range(4):
+            ids, vals, lab = synth.batch(B, step=s, device=DEV, id_dtype=torch.int32)
+            m.train_step(ids, vals, lab, use_graph=True)
+        torch.cuda.synchronize()
+        assert m._fin_opt_step == fuse
+        out.append([m.p.clone(), m.tv.clone(), m.tw.clone(), m.sd[0].clone(), m.sd[1].clone(),
+                    m.step.clone()] + [w.clone() for w in m.W16])
+    names = ["p", "tv", "tw", "s0", "s1", "step"] + [f"W16[{i}]" for i in range(len(layers))]
+    for k, ref in enumerate(out[1:]):
+        for nm, x, y in zip(names, out[0], ref):
+            if not torch.equal(x, y):
+                bad = (x != y).nonzero().flatten()[:8].tolist()
+                d = (x.float() - y.float()).abs().max().item()
+                segs = {s.name: s.off for s in m.dense_segs.values()}
+                pytest.fail(f"variant {k + 1}: {nm} differs, max {d:.3e} at {bad}; segs {segs}")

@@ -2,7 +2,8 @@
 
 usage: python tools/prof_summary.py <prof_dir> <out.md> [title]
 Writes the top kernels by total time and one steady-state training step's kernel timeline
-(the step between two consecutive end-of-step kernels: dense_opt, formerly step_inc).
+(one period between two consecutive dense-optimizer kernels: dense_opt, or finalize_opt when
+the optimizer rides on the gradient finalize; formerly step_inc).
 """
 import csv
 import glob
@@ -34,7 +35,7 @@ def main():
     if trace:
         rows = list(csv.DictReader(open(trace[0])))
         rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-        idx = [i for i, r in enumerate(rows) if r["Kernel_Name"].startswith(("step_inc", "void dense_opt_kernel"))]
+        idx = [i for i, r in enumerate(rows) if r["Kernel_Name"].startswith(("step_inc", "void dense_opt_kernel", "void finalize_opt_kernel"))]
         if len(idx) >= 3:
             a, b = idx[len(idx) // 2 - 1], idx[len(idx) // 2]
             t0 = int(rows[a]["End_Timestamp"])
