@@ -181,6 +181,9 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world and rank == 0:
+        print(f"[bench] --gpus {args.gpus} but WORLD_SIZE={world}: measuring {world} rank(s)",
+              file=sys.stderr, flush=True)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     synth = make_synth(args.preset, seed=2024)
@@ -316,7 +319,33 @@ def _fake_child(args, spec):
     return 0
 
 
+def _requested_gpus(argv) -> int:
+    """--gpus N from argv without importing torch (the launching parent never touches the GPU)."""
+    ap = argparse.ArgumentParser(add_help=False)
+    ap.add_argument("--gpus", type=int, default=1)
+    ns, _ = ap.parse_known_args(argv)
+    return ns.gpus
+
+
+def self_launch(argv, n: int) -> int:
+    """``python bench.py --gpus N`` (N > 1) outside a launcher: start one rank per GPU of this
+    node (the reference's mpirun -np N / processes_per_host, NBHVD:87-92, HVD:295) through
+    torch.distributed.run on 127.0.0.1, as a CHILD process -- this process has not initialised the
+    GPU and only relays the exit code.  Each rank then runs the supervised bench below."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)]
+    cmd += list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
 if __name__ == "__main__":
+    if "WORLD_SIZE" not in os.environ and os.environ.get("HIPFM_BENCH_CHILD") != "1":
+        n_req = _requested_gpus(sys.argv[1:])
+        if n_req > 1:
+            sys.exit(self_launch(sys.argv[1:], n_req))
     sup = os.environ.get("HIPFM_BENCH_SUPERVISE", "1")      # 0: off; force: also at 1 rank (tests)
     if (os.environ.get("HIPFM_BENCH_CHILD") != "1" and sup != "0" and "TORCHELASTIC_RUN_ID" in os.environ
             and (int(os.environ.get("WORLD_SIZE", "1")) > 1 or sup == "force")):

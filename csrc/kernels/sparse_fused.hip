@@ -55,8 +55,6 @@ struct SfArgs {
   const int* sid;
   const int* upos;
   float* gout;
-  const float* G;  // optional slot-order gradient records from the tower ([n][K+4]); replaces
-                   // the vals / dlogit / S / dX0 gathers
   int step_off;    // 1: *step is this step's index - 1 (the dense optimizer advances it later);
                    // 0: the dense optimizer already ran and advanced it (single-GPU early mode)
 };
@@ -142,31 +140,19 @@ __global__ void __launch_bounds__(256) sf_tile_kernel(SfArgs A) {
     if (p < nloc) {
       const int i = b0 + p;
       const int q = A.perm[i];
-      if (A.G) {
-        const float* gr = A.G + (size_t)q * (K + 4);
-        const f32x4 av = *reinterpret_cast<const f32x4*>(gr + sub * 4);
+      const int b = q / A.F, f = q - b * A.F;
+      const float x = A.vals[q];
+      const float dy = A.dlogit[b];
+      const f32x4 s = *reinterpret_cast<const f32x4*>(A.S + (size_t)b * K + sub * 4);
+      const bf16x4 dxh = *reinterpret_cast<const bf16x4*>(A.dX0 + (size_t)b * A.KP + f * K + sub * 4);
+      const f32x4 dx = {bf2f(dxh[0]), bf2f(dxh[1]), bf2f(dxh[2]), bf2f(dxh[3])};
+      const f32x4 av = (dx + dy * s) * x;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) g[p][sub * 4 + j] = av[j];
-        if (sub == 0) {
-          g[p][K] = gr[K];
-          g[p][K + 1] = gr[K + 1];
-          skl[p] = A.sorted_keys[i];
-        }
-      } else {
-        const int b = q / A.F, f = q - b * A.F;
-        const float x = A.vals[q];
-        const float dy = A.dlogit[b];
-        const f32x4 s = *reinterpret_cast<const f32x4*>(A.S + (size_t)b * K + sub * 4);
-        const bf16x4 dxh = *reinterpret_cast<const bf16x4*>(A.dX0 + (size_t)b * A.KP + f * K + sub * 4);
-        const f32x4 dx = {bf2f(dxh[0]), bf2f(dxh[1]), bf2f(dxh[2]), bf2f(dxh[3])};
-        const f32x4 av = (dx + dy * s) * x;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) g[p][sub * 4 + j] = av[j];
-        if (sub == 0) {
-          g[p][K] = dy * x;
-          g[p][K + 1] = dy * x * x;
-          skl[p] = A.sorted_keys[i];
-        }
+      for (int j = 0; j < 4; ++j) g[p][sub * 4 + j] = av[j];
+      if (sub == 0) {
+        g[p][K] = dy * x;
+        g[p][K + 1] = dy * x * x;
+        skl[p] = A.sorted_keys[i];
       }
     }
   }

@@ -22,11 +22,8 @@
 
 constexpr int TW_MAXL = 8;
 constexpr int TW_ROWS = 32;
-// k-steps of A/B fragments in flight per wave: PF0 for layer 0, PF1 for the other GEMMs.  The
-// deep variant (5, 4: layer 0 in two latency rounds instead of three, the rest in one) needs 168
-// VGPRs, i.e. 2 waves per SIMD: it loses on one GPU, where the side-stream field sort holds 39
-// CUs and the 512 tower workgroups then need a second residency round (0.157 -> 0.177 ms), and
-// is within run-to-run noise on the row-sharded step.  TowerArgs.deep picks the variant.
+// k-steps of A/B fragments in flight per wave: PF0 = 4 for layer 0, PF1 = 2 for the other GEMMs
+// (deeper rings need > 128 VGPRs, i.e. fewer resident waves, and measured slower).
 
 struct TowerArgs {
   int M, nvalid, nl, K0p;
@@ -55,7 +52,6 @@ struct TowerArgs {
   float* partial;                 // [M/32, Np_last + 2]
   int h_off[TW_MAXL];             // LDS element offsets of the H tiles
   int dz_off[2];                  // LDS element offsets of the two dZ tiles
-  int x_off;                      // LDS element offset of the [32][K0p + 8] input / dX0 tile
   int lds_bytes;
   // fp8 forward (mlp_dtype = fp8): every forward GEMM on v_mfma_f32_16x16x32_fp8_fp8 with OCP
   // e4m3 operands — E8 rows (fm_fwd) / H rows (quantized from the LDS tile) with per-row
@@ -66,21 +62,7 @@ struct TowerArgs {
   const float* sE;                // [M]     row dequant factors of E8
   const uint8_t* W8[TW_MAXL];     // [Np_i, Kp_i]
   const float* sW[TW_MAXL];       // [Np_i]  channel dequant factors of W8
-  unsigned long long* tstamp;     // optional phase timestamps [grid][16] (tools/tower_phases.py)
-  int deep;                       // 1: deep-prefetch variant (see TW prefetch note)
-  // Slot-order FM gradient records for the fused sparse backward (optional): for every slot
-  // (b, f) G[b*F + f] = {x*(dX0[b,f,:] + dy_b*S_b) (K floats), dy_b*x, dy_b*x^2, 0, 0}.  The
-  // sparse tile kernel then reads ONE 16-B-aligned record per slot (in id order) instead of
-  // four scattered per-sample arrays.  dX0 is rounded to bf16 first, exactly as when the tile
-  // kernel read the bf16 dX0, so the numbers are unchanged.
-  float* G;                       // [M*F][K+4] or null
-  const float* S;                 // [M, K]
-  const float* vals;              // [M, F]
-  int F, K;
 };
-
-#define TW_STAMP(k)                                                        \
-  if (a.tstamp && threadIdx.x == 0) a.tstamp[blockIdx.x * 16 + (k)] = wall_clock64();
 
 // One wave: c[2][2] += A[32 x 32*nk] . B[32 x 32*nk]^T, both K-contiguous (row strides lda/ldb
 // in elements).  Register ring of PF k-steps so PF fragment sets are in flight.
@@ -223,41 +205,6 @@ __global__ void __launch_bounds__(256) tower_kernel(TowerArgs a) {
   const int nl = a.nl;
 
   // ------------------------------------------------------------------ forward
-  TW_STAMP(0);
-  // The block's 32 input rows (E, or E8 with --mlp_dtype fp8) go to LDS once, with every
-  // 16-byte load of the tile in flight together: the 4 waves then take their layer-0 A
-  // fragments from LDS instead of each re-reading the rows from L2 in k-step batches.
-  const bool stage = a.x_off >= 0;                // wide inputs (K0p > 512) stay in L2 instead
-  bf16* Xl = lds + (stage ? a.x_off : 0);
-  const int ldx = a.K0p + 8;                      // bf16 elements (fp8: bytes, 2 * ldx)
-  if (stage) {
-    const int cpr = FP8 ? a.K0p / 16 : a.K0p / 8;  // 16-B chunks per row
-    const unsigned char* src = FP8 ? reinterpret_cast<const unsigned char*>(a.E8)
-                                   : reinterpret_cast<const unsigned char*>(a.E);
-    const size_t rowb = FP8 ? (size_t)a.K0p : (size_t)a.K0p * 2;
-    unsigned char* dst = reinterpret_cast<unsigned char*>(Xl);
-    const int total = TW_ROWS * cpr;
-    for (int e0 = tid; e0 < total; e0 += 256 * 8) {
-      f32x4 v[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const int e = e0 + k * 256;
-        if (e < total) {
-          const int r = e / cpr, c = e - r * cpr;
-          v[k] = *reinterpret_cast<const f32x4*>(src + (size_t)(row0 + r) * rowb + c * 16);
-        }
-      }
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const int e = e0 + k * 256;
-        if (e < total) {
-          const int r = e / cpr, c = e - r * cpr;
-          *reinterpret_cast<f32x4*>(dst + (size_t)r * ldx * 2 + c * 16) = v[k];
-        }
-      }
-    }
-    __syncthreads();
-  }
   for (int i = 0; i < nl; ++i) {
     const int N = a.Np[i];
     const int Kp = i == 0 ? a.K0p : a.Np[i - 1];
@@ -270,17 +217,13 @@ __global__ void __launch_bounds__(256) tower_kernel(TowerArgs a) {
       f32x4 c00 = {0, 0, 0, 0}, c01 = c00, c10 = c00, c11 = c00;
       if (FP8) {
         const uint8_t* Bw8 = a.W8[i] + (size_t)ct * 32 * Kp;
-        if (i == 0 && stage)
-          mma32_f8<4>(reinterpret_cast<const uint8_t*>(Xl), 2 * ldx, Bw8, Kp, Kp / 32, lane, c00, c01, c10, c11);
-        else if (i == 0)
+        if (i == 0)
           mma32_f8<4>(a.E8 + (size_t)row0 * a.K0p, a.K0p, Bw8, Kp, Kp / 32, lane, c00, c01, c10, c11);
         else
           mma32_f8_lds(lds + a.h_off[i - 1], Kp + 8, s_q, Bw8, Kp, Kp / 32, lane, c00, c01, c10, c11);
       } else {
         const bf16* Bw = a.W[i] + (size_t)ct * 32 * Kp;
-        if (i == 0 && stage)
-          mma32<4>(Xl, ldx, Bw, Kp, Kp / 32, lane, c00, c01, c10, c11);
-        else if (i == 0)
+        if (i == 0)
           mma32<TW_PF0>(a.E + (size_t)row0 * a.K0p, a.K0p, Bw, Kp, Kp / 32, lane, c00, c01, c10, c11);
         else
           mma32<TW_PF1>(lds + a.h_off[i - 1], Kp + 8, Bw, Kp, Kp / 32, lane, c00, c01, c10, c11);
@@ -321,7 +264,6 @@ __global__ void __launch_bounds__(256) tower_kernel(TowerArgs a) {
       }
       __syncthreads();
     }
-    TW_STAMP(1 + i);
   }
 
   // ------------------------------------------------------------------ head
@@ -381,7 +323,6 @@ __global__ void __launch_bounds__(256) tower_kernel(TowerArgs a) {
       part[c] = s;
     }
   }
-  TW_STAMP(9);
   if (!a.train) return;
   store_tile_t(lds + a.dz_off[0], L + 8, L, a.dZt[nl - 1], a.M, row0);
 
@@ -415,7 +356,6 @@ __global__ void __launch_bounds__(256) tower_kernel(TowerArgs a) {
     __syncthreads();
     store_tile_t(Zo, ldz_out, Nout, a.dZt[i - 1], a.M, row0);
     cur ^= 1;
-    TW_STAMP(10 + (nl - 1 - i));
   }
   {
     const int N0 = a.Np[0];
@@ -432,40 +372,12 @@ __global__ void __launch_bounds__(256) tower_kernel(TowerArgs a) {
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             const int rl = ti * 16 + cr + j;
-            const bf16 dxh = f2bf(acc[ti][tj][j]);
-            if (a.G) {
-              const int f = col / a.K, k = col - f * a.K;
-              if (f < a.F) {
-                const size_t b = (size_t)(row0 + rl);
-                const float dy = s_dl[rl];
-                const float x = a.vals[b * a.F + f];
-                float* gr = a.G + (b * a.F + f) * (size_t)(a.K + 4);
-                gr[k] = (bf2f(dxh) + dy * a.S[b * a.K + k]) * x;
-                if (k == 0) {
-                  gr[a.K] = dy * x;
-                  gr[a.K + 1] = dy * x * x;
-                }
-              }
-            }
-            if (!a.dX0) continue;
-            if (stage)
-              Xl[rl * ldx + col] = dxh;
-            else
-              a.dX0[(size_t)(row0 + rl) * a.K0p + col] = dxh;
+            a.dX0[(size_t)(row0 + rl) * a.K0p + col] = f2bf(acc[ti][tj][j]);
           }
         }
       }
     }
-    // dX0 tile (staged in the input tile's LDS, free since layer 0) -> global in 16-B rows
-    __syncthreads();
-    const int cpr = a.K0p / 8;
-    for (int e = tid; stage && a.dX0 && e < TW_ROWS * cpr; e += 256) {
-      const int r = e / cpr, c = e - r * cpr;
-      *reinterpret_cast<f32x4*>(a.dX0 + (size_t)(row0 + r) * a.K0p + c * 8) =
-          *reinterpret_cast<const f32x4*>(Xl + r * ldx + c * 8);
-    }
   }
-  TW_STAMP(15);
 }
 
 HFM_API int hfm_tower(const TowerArgs* ap, hipStream_t st) {
@@ -479,12 +391,7 @@ HFM_API int hfm_tower(const TowerArgs* ap, hipStream_t st) {
     if (!a.E8 || !a.sE) return (int)hipErrorInvalidValue;
     for (int i = 0; i < a.nl; ++i)
       if (!a.W8[i] || !a.sW[i]) return (int)hipErrorInvalidValue;
-    if (a.deep)
-      hipLaunchKernelGGL((tower_kernel<true, 5, 4>), dim3(a.M / TW_ROWS), dim3(256), a.lds_bytes, st, a);
-    else
-      hipLaunchKernelGGL((tower_kernel<true, 4, 2>), dim3(a.M / TW_ROWS), dim3(256), a.lds_bytes, st, a);
-  } else if (a.deep) {
-    hipLaunchKernelGGL((tower_kernel<false, 5, 4>), dim3(a.M / TW_ROWS), dim3(256), a.lds_bytes, st, a);
+    hipLaunchKernelGGL((tower_kernel<true, 4, 2>), dim3(a.M / TW_ROWS), dim3(256), a.lds_bytes, st, a);
   } else {
     hipLaunchKernelGGL((tower_kernel<false, 4, 2>), dim3(a.M / TW_ROWS), dim3(256), a.lds_bytes, st, a);
   }

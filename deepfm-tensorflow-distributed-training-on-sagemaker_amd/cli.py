@@ -66,8 +66,14 @@ def build_pipelines(cfg: RunConfig, est: Estimator):
         ev_ch = cfg.evaluation_channel_name or (ch[0] if ch else "evaluation")
         tr = lambda epochs: InputPipeline([], cfg.field_size, cfg.batch_size, epochs, shard=shard,
                                           pipe_channel=tr_ch, **common)
-        va = lambda: InputPipeline([], cfg.field_size, cfg.batch_size, 1, shard=(world, rank),
-                                   pipe_channel=ev_ch, **common)
+
+        # one FIFO has one reader: rank 0 evaluates the whole evaluation channel (HVD:403-405);
+        # the other ranks contribute empty histograms to the all-reduced AUC
+        def va():
+            if rank != 0:
+                return []
+            return InputPipeline([], cfg.field_size, cfg.batch_size, 1, shard=(1, 0),
+                                 pipe_channel=ev_ch, **{**common, "device": None})
         te = va
         return tr, va, te
     ext = "tfrecord" if fmt == "tfrecord" else "libsvm"

@@ -24,6 +24,7 @@ from __future__ import annotations
 import glob
 import os
 import random
+import threading
 from dataclasses import dataclass
 from typing import Iterator, List, Optional, Sequence, Tuple
 
@@ -33,6 +34,8 @@ import torch
 from .native_io import FMT_LIBSVM, FMT_TFRECORD, NativeLoader, count_records
 
 PIPE_ROOT = "/opt/ml/input/data"
+_pipe_lock = threading.Lock()
+_pipe_opened = {}        # channel -> number of epoch streams opened so far (this process)
 
 
 def discover_files(data_dir: str, prefix: str, fmt: str = "tfrecord") -> List[str]:
@@ -78,9 +81,25 @@ def plan_shard(files: Sequence[str], n: int, i: int, policy: str = "file", seed:
     return ShardPlan(files, (n, i))
 
 
+def pipe_root() -> str:
+    return os.environ.get("HIPFM_PIPE_ROOT", PIPE_ROOT)
+
+
 def pipe_channel_path(channel: str, epoch: int) -> str:
     """SageMaker Pipe-mode FIFO of a channel for an epoch (PipeModeDataset, PS:111)."""
-    return os.path.join(PIPE_ROOT, f"{channel}_{epoch}")
+    return os.path.join(pipe_root(), f"{channel}_{epoch}")
+
+
+def next_pipe_stream(channel: str) -> str:
+    """The next unread epoch stream of a Pipe-mode channel.  Pipe mode hands out every epoch of
+    a channel exactly once, as ``<channel>_0``, ``<channel>_1``, ... (a FIFO can be read only
+    once), so each reader that opens the channel -- a training epoch, every evaluation pass --
+    takes the next index instead of re-opening a drained stream (reference HVD:396: re-entering
+    PipeModeDataset on the same FIFO breaks)."""
+    with _pipe_lock:
+        k = _pipe_opened.get(channel, 0)
+        _pipe_opened[channel] = k + 1
+    return pipe_channel_path(channel, k)
 
 
 class InputPipeline:
@@ -109,13 +128,21 @@ class InputPipeline:
         self._cached: Optional[List[Tuple[torch.Tensor, ...]]] = None
         self.max_batches: Optional[int] = None   # equal-steps enforcement across ranks
 
+    @property
+    def countable(self) -> bool:
+        """Files can be counted ahead of training; a Pipe-mode stream can only be read once."""
+        return self.pipe_channel is None
+
     def epoch_plan(self, epoch: int) -> ShardPlan:
         if self.pipe_channel is not None:
-            return ShardPlan([pipe_channel_path(self.pipe_channel, epoch)], self.shard)
+            return ShardPlan([next_pipe_stream(self.pipe_channel)], self.shard)
         return plan_shard(self.files, self.shard[0], self.shard[1], self.policy, self.seed, epoch,
                           self.shuffle_files)
 
     def local_records(self, epoch: int = 0) -> int:
+        if not self.countable:
+            raise RuntimeError("a Pipe-mode channel is a stream: its records cannot be counted "
+                               "before training (equal steps are agreed per step instead)")
         plan = self.epoch_plan(epoch)
         total = sum(count_records(f, self.fmt) for f in plan.files)
         n, i = plan.record_shard

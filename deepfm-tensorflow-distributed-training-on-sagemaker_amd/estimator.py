@@ -75,6 +75,11 @@ class Estimator:
         self.rank = dist.get_rank() if _dist_on() else 0
         self.world = dist.get_world_size() if _dist_on() else 1
         torch.manual_seed(cfg.seed)
+        # host-side control messages (per-step "still have data" votes of stream inputs) travel
+        # over a gloo group, so they never wait on the GPU stream the way an RCCL op would
+        self._ctl = None
+        if self.world > 1 and dist.get_backend() != "gloo":
+            self._ctl = dist.new_group(backend="gloo")
         self.comm = None
         if self.native:
             from .models.deepfm import NativeDeepFM
@@ -225,13 +230,33 @@ class Estimator:
         return out, torch.nonzero(mask).reshape(-1)
 
     def _enforce_equal_steps(self, pipeline):
-        """Every rank runs the same number of steps per epoch (min over ranks)."""
+        """Every rank runs the same number of steps per epoch (min over ranks).  Files are
+        counted up front; streams (Pipe mode) cannot be, see ``_agreed_batches``."""
         if self.world == 1 or not hasattr(pipeline, "local_records"):
+            return
+        if not getattr(pipeline, "countable", True):
             return
         n = pipeline.local_records() // pipeline.B
         t = torch.tensor([n], dtype=torch.int64, device=self.device if self.native else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MIN)
         pipeline.max_batches = int(t.item())
+
+    def _agreed_batches(self, batches: Iterable) -> Iterator:
+        """Equal steps on uncountable (stream) inputs: before each step every rank votes whether
+        it still has a batch, and all ranks stop at the first rank's end of stream (the
+        reference's equal-data rule against Horovod's uneven-data shutdown, DOC p.22-23, applied
+        without reading any stream twice).  Costs one tiny gloo all-reduce per step."""
+        it = iter(batches)
+        while True:
+            b = next(it, None)
+            flag = torch.tensor([0 if b is None else 1], dtype=torch.int32)
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self._ctl)
+            if int(flag.item()) == 0:
+                close = getattr(it, "close", None)
+                if close is not None:
+                    close()
+                return
+            yield b
 
     # ------------------------------------------------------------------ train
     def train(self, batches: Iterable, max_steps: Optional[int] = None,
@@ -239,6 +264,8 @@ class Estimator:
         cfg = self.cfg
         if hasattr(batches, "local_records"):
             self._enforce_equal_steps(batches)
+        if self.world > 1 and not getattr(batches, "countable", True):
+            batches = self._agreed_batches(batches)
         t_log = time.time()
         n_log = 0
         start_step = self.global_step

@@ -38,23 +38,15 @@ from ..utils.rng import keep_threshold
 from .reference import glorot_std, init_params, pad32
 
 
-# A/B switches (debug / perf comparison)
-_SEPARATE_STEP_INC = os.environ.get("HIPFM_STEP_INC", "0") == "1"
-_OLD_FINALIZE = os.environ.get("HIPFM_OLD_FINALIZE", "0") == "1"
+# Execution-mode switches (each one is a supported, tested mode; rejected experiments are gone)
 _SORT_MODE = os.environ.get("HIPFM_SORT", "auto")                # auto | global
 _SORT_SIDE_STREAM = os.environ.get("HIPFM_SORT_SIDE_STREAM", "1") == "1"
-_SORT_FORK = os.environ.get("HIPFM_SORT_FORK", "after_fm")   # start | after_fm | after_tower
 _DENSE_EARLY = os.environ.get("HIPFM_DENSE_EARLY", "1") == "1"
 _FWD_IDST = os.environ.get("HIPFM_FWD_IDST", "1") == "1"         # fm_fwd writes ids field-major
 _FUSE_FIN_OPT = os.environ.get("HIPFM_FUSE_FIN_OPT", "1") == "1"  # dense optimizer in finalize
 _SPARSE_IMPL = os.environ.get("HIPFM_SPARSE", "fused")             # fused | seg
 _SHARD_PIPELINE = os.environ.get("HIPFM_SHARD_PIPELINE", "1") == "1"
 _DENSE_SIDE_STREAM = os.environ.get("HIPFM_DENSE_SIDE_STREAM", "auto")   # auto | 1 | 0
-_TOWER_STAGE = os.environ.get("HIPFM_TOWER_STAGE", "0")          # auto (sharded step) | 1 | 0
-_TOWER_DEEP = os.environ.get("HIPFM_TOWER_DEEP", "0")            # auto (sharded step) | 1 | 0
-# slot-order gradient records from the tower (TowerArgs.G): measured slower (tower +12 us for the
-# scattered record writes, sparse tile -0.7 us: its cost is not the per-sample gathers), so off
-_GSLOT = os.environ.get("HIPFM_GSLOT", "0") == "1"
 
 
 def check_field_ranges(ranges, F: int, V: int) -> List[Tuple[int, int]]:
@@ -350,20 +342,9 @@ class NativeDeepFM:
                     t.fill_(init)
 
     def _tower_lds_bytes(self) -> int:
-        """H tiles + two dZ tiles + the [32][K0p + 8] input / dX0 staging tile (bf16)."""
+        """H tiles + two dZ tiles (bf16, rows padded by 8 elements)."""
         h = sum(32 * (n + 8) * 2 for n in self.Np)
-        return h + 2 * 32 * (max(self.Np) + 8) * 2 + (32 * (self.K0p + 8) * 2 if self._stage_x else 0)
-
-    @property
-    def _stage_x(self) -> bool:
-        """Stage the tower's 32 input rows (and its dX0 tile) in LDS: -3.5 us in layer 0 and -1 us
-        in the dX0 phase per workgroup (tools/tower_phases.py), but +21 KB of LDS per workgroup,
-        and next to the side-stream field sort (148 KB per workgroup on 39 CUs) the 512 tower
-        workgroups then no longer fit in one residency round (start spread 0.5 -> 26 us, step
-        0.156 -> 0.174 ms).  On the row-sharded step a same-box A/B showed no difference beyond
-        run-to-run noise (0.198-0.202 ms), so it is off by default (HIPFM_TOWER_STAGE=1 / auto)."""
-        on = self.sharded if _TOWER_STAGE == "auto" else _TOWER_STAGE == "1"
-        return on and self.K0p <= 512
+        return h + 2 * 32 * (max(self.Np) + 8) * 2
 
     @staticmethod
     def _padM(B: int) -> int:
@@ -394,9 +375,6 @@ class NativeDeepFM:
         self.dZ = [torch.zeros(M, n, **bf) for n in self.Np]
         self.dZt = [torch.zeros(n, M, **bf) for n in self.Np]
         self.dX0 = torch.zeros(M, K0p, **bf)            # layer-1 input gradient (bf16)
-        # slot-order FM gradient records written by the fused tower for the fused sparse
-        # backward (csrc/kernels/tower.hip, TowerArgs.G): [M*F][K+4]
-        self.Gslot = torch.zeros(M * F, K + 4, **f32) if (self.fused and _GSLOT) else None
         if self.batch_norm:
             self.Rb = [torch.zeros(M, n, **f32) for n in self.Np]         # relu output (pre-BN)
             self.dH = [torch.zeros(M, n, **f32) for n in self.Np]         # dL/d(layer output)
@@ -538,15 +516,7 @@ class NativeDeepFM:
         self._nwg_jobs = len(jobs)
         self._wg_tasks = task0
 
-    def _gslot_mode(self) -> bool:
-        """The fused tower writes slot-order gradient records (and no dX0) when the sparse
-        backward is the fused tile kernel: single rank with HIPFM_SPARSE=fused, or the
-        row-sharded exchange."""
-        return _GSLOT and self.fused and self.Gslot is not None and (
-            self.shx is not None or (not self.exchange and _SPARSE_IMPL == "fused"))
-
-    def _tower_args(self, B: int, train: bool, with_labels: bool = True,
-                    gslot: bool = False) -> TowerArgs:
+    def _tower_args(self, B: int, train: bool, with_labels: bool = True) -> TowerArgs:
         a = TowerArgs()
         nl = len(self.layers)
         a.M, a.nvalid, a.nl, a.K0p = self.M, B, nl, self.K0p
@@ -567,10 +537,6 @@ class NativeDeepFM:
             off += 32 * (self.Np[i] + 8)
         a.dz_off[0] = off
         a.dz_off[1] = off + 32 * (max(self.Np) + 8)
-        a.x_off = off + 2 * 32 * (max(self.Np) + 8) if self._stage_x else -1
-        # deep-prefetch tower variant (more VGPRs, fewer latency rounds): slower on one GPU next
-        # to the side-stream sort, no measurable change on the sharded step (off by default)
-        a.deep = 1 if (_TOWER_DEEP == "1" or (_TOWER_DEEP == "auto" and self.sharded)) else 0
         a.lds_bytes = self._tower_lds_bytes()
         a.E = self.E.data_ptr()
         if self.fp8:
@@ -587,28 +553,22 @@ class NativeDeepFM:
         a.b_out = pb + 4 * self.dense_segs["Deep-part/deep_out/biases"].off
         a.y_fm = self.y_fm.data_ptr()
         a.labels = self.labels.data_ptr() if with_labels else 0
-        a.dX0 = 0 if gslot else self.dX0.data_ptr()
-        if gslot:
-            a.G, a.S, a.vals = self.Gslot.data_ptr(), self.S.data_ptr(), self.vals.data_ptr()
-            a.F, a.K = self.F, self.K
+        a.dX0 = self.dX0.data_ptr()
         a.prob = self.prob.data_ptr()
         a.dlogit = self.dlogit.data_ptr()
         a.partial = self.partial.data_ptr()
         return a
 
-    def _dense_fwd_bwd(self, B: int, defer_wgrad: bool = False, gslot: bool = False, after_fm=None,
-                       after_tower=None):
+    def _dense_fwd_bwd(self, B: int, defer_wgrad: bool = False, after_fm=None):
         """Forward, loss head and the whole deep-tower backward (dense grads into self.g, dX0
         for the FM backward).  Returns the (idx, table) pair the sparse backward uses.
         ``defer_wgrad``: stop after the fused tower (the caller runs wgrad + finalize).
-        ``after_fm`` / ``after_tower``: hooks called once the FM forward / the tower is enqueued."""
+        ``after_fm``: hook called once the FM forward is enqueued."""
         if self.fused:
             idx, tv = self._fm_forward(B, train=True)
             if after_fm is not None:
                 after_fm()
-            KN.tower(self._tower_args(B, train=True, gslot=gslot))
-            if after_tower is not None:
-                after_tower()
+            KN.tower(self._tower_args(B, train=True))
             if not defer_wgrad:
                 KN.wgrad_group(self._wg_jobs, self._nwg_jobs, self._wg_tasks)
                 self._finalize_grads()
@@ -616,8 +576,6 @@ class NativeDeepFM:
         idx, tv = self._forward(B, train=True)
         if after_fm is not None:
             after_fm()
-        if after_tower is not None:
-            after_tower()
         self._head(B, train=True)
         self._mlp_backward(B)
         return idx, tv
@@ -859,10 +817,6 @@ class NativeDeepFM:
         self._finalize_grads()
 
     def _finalize_grads(self):
-        if _OLD_FINALIZE:
-            KN.slab_reduce(self._slab_jobs, self._nslab_jobs, self._slab_maxn)
-            KN.rowsum(self._row_jobs, self._nrow_jobs, self._row_total)
-            return
         if self._fuse_opt:
             KN.finalize_opt(self.opt_id, self._slab_jobs, self._nslab_jobs, self._slab_blocks,
                             self._row_jobs, self._nrow_jobs, self._row_total, self.p, self.g,
@@ -931,7 +885,6 @@ class NativeDeepFM:
         A.h = self.h_sparse
         A.step = self.step.data_ptr()
         A.ldv, A.ldw = KN._ld(self.tv, self.tw)
-        A.G = self.Gslot.data_ptr() if getattr(self, "_gslot_step", False) else 0
         A.step_off = 0 if self._dense_early else 1
         return A
 
@@ -995,7 +948,7 @@ class NativeDeepFM:
         presorted = False
         if self.shx is not None:
             self._shx_start(B)
-        after_fm = after_tower = None
+        after_fm = None
         if not self.sharded and _SORT_SIDE_STREAM:
             main = torch.cuda.current_stream(self.device)
             if self._side is None:
@@ -1003,19 +956,11 @@ class NativeDeepFM:
 
             # fm_fwd writes the ids field-major as it reads them, so the forked sort skips its
             # transpose launch (the sort branch is the step's critical path)
-            pre = (_SORT_FORK != "start" and _FWD_IDST and self.uses_field_sort(B) and
-                   KN.fm_fwd_writes_idsT(self.F, self.K))
+            pre = (_FWD_IDST and self.uses_field_sort(B) and KN.fm_fwd_writes_idsT(self.F, self.K))
             self._idsT_B = B if pre else 0
-            fork = []
-
-            def mark():
-                fork.append(main.record_event())
 
             def fork_sort():
-                if fork:
-                    self._side.wait_event(fork[0])
-                else:
-                    self._side.wait_stream(main)
+                self._side.wait_stream(main)
                 with torch.cuda.stream(self._side):
                     if pre:
                         self._fsort.sort_pre(B, self.sorted_keys, self.perm)
@@ -1023,14 +968,8 @@ class NativeDeepFM:
                         self._sort_slots(B)
             # graph branches launch in capture order: forking after fm_fwd is enqueued lets the
             # step's first kernel start at once instead of after the sort's launches
-            # (same-box A/B: 0.160 -> 0.154 ms/step, bitwise-identical results); after_tower
-            # keeps the fork point after fm_fwd but enqueues the sort after the tower
-            if _SORT_FORK == "after_fm":
-                after_fm = fork_sort
-            elif _SORT_FORK == "after_tower":
-                after_fm, after_tower = mark, fork_sort
-            else:
-                fork_sort()
+            # (same-box A/B: 0.160 -> 0.154 ms/step, bitwise-identical results)
+            after_fm = fork_sort
             presorted = True
         # fused tower: the weight gradients (wgrad + finalize, then the dense all-reduce) only
         # feed the dense optimizer, so on the multi-rank step they run on their own stream
@@ -1039,19 +978,15 @@ class NativeDeepFM:
         # more than it saves (0.156 -> 0.161 ms), so there it stays in line.
         split = self.fused and (_DENSE_SIDE_STREAM == "1" or
                                 (_DENSE_SIDE_STREAM == "auto" and self.exchange))
-        gslot = self._gslot_mode()
-        self._gslot_step = gslot
         # single GPU, lazy rows: the dense optimizer needs only the finished dense gradient, so it
         # runs BEFORE the join with the side-stream sort, inside the gap the join costs anyway;
         # it advances the step counter, and the sparse kernels are told so (SfArgs.step_off).
         # With the fused tower it rides on the finalize launch itself (one kernel boundary less)
         self._dense_early = (presorted and not self.exchange and not split and _DENSE_EARLY and
                              self.sparse_update == "lazy" and _SPARSE_IMPL == "fused")
-        self._fuse_opt = (self._dense_early and self.fused and _FUSE_FIN_OPT and
-                          not _OLD_FINALIZE and self._fin_covers_all)
+        self._fuse_opt = (self._dense_early and self.fused and _FUSE_FIN_OPT and self._fin_covers_all)
         try:
-            idx, tv = self._dense_fwd_bwd(B, defer_wgrad=split, gslot=gslot, after_fm=after_fm,
-                                          after_tower=after_tower)
+            idx, tv = self._dense_fwd_bwd(B, defer_wgrad=split, after_fm=after_fm)
         finally:
             self._idsT_B = 0
             fused_opt, self._fuse_opt = self._fuse_opt, False
@@ -1095,13 +1030,8 @@ class NativeDeepFM:
 
     def _dense_opt(self):
         """Dense optimizer over the flat buffer (+ bf16 / fp8 weight shadows); advances the step."""
-        if _SEPARATE_STEP_INC:
-            KN.dense_opt(self.opt_id, self.p, self.g, self.sd[0], self.sd[1], self.P, self.h_dense,
-                         self.step, self._shadow_dev, self._nshadow)
-            KN.step_inc(self.step)
-        else:
-            KN.dense_opt(self.opt_id, self.p, self.g, self.sd[0], self.sd[1], self.P, self.h_dense,
-                         self.step, self._shadow_dev, self._nshadow, done_ctr=self._done_ctr)
+        KN.dense_opt(self.opt_id, self.p, self.g, self.sd[0], self.sd[1], self.P, self.h_dense,
+                     self.step, self._shadow_dev, self._nshadow, done_ctr=self._done_ctr)
         if self.fp8:
             KN.w8_quant(self._w8_jobs, len(self.layers), self._w8_rows)
 

@@ -84,8 +84,7 @@ class SfArgs(C.Structure):
                 ("tv", c_void_p), ("tw", c_void_p), ("s0v", c_void_p), ("s1v", c_void_p),
                 ("s0w", c_void_p), ("s1w", c_void_p), ("Gv", c_void_p), ("Gw", c_void_p),
                 ("h", OptHyper), ("step", c_void_p), ("ldv", c_long), ("ldw", c_long),
-                ("sid", c_void_p), ("upos", c_void_p), ("gout", c_void_p), ("G", c_void_p),
-                ("step_off", c_int)]
+                ("sid", c_void_p), ("upos", c_void_p), ("gout", c_void_p), ("step_off", c_int)]
 
 
 class ShApplyArgs(C.Structure):
@@ -109,10 +108,9 @@ class TowerArgs(C.Structure):
                 ("w_out", c_void_p), ("b_out", c_void_p), ("y_fm", c_void_p), ("labels", c_void_p),
                 ("Ht", c_void_p * TW_MAXL), ("dZt", c_void_p * TW_MAXL), ("dX0", c_void_p),
                 ("prob", c_void_p), ("dlogit", c_void_p), ("partial", c_void_p),
-                ("h_off", c_int * TW_MAXL), ("dz_off", c_int * 2), ("x_off", c_int), ("lds_bytes", c_int),
+                ("h_off", c_int * TW_MAXL), ("dz_off", c_int * 2), ("lds_bytes", c_int),
                 ("fp8", c_int), ("E8", c_void_p), ("sE", c_void_p), ("W8", c_void_p * TW_MAXL),
-                ("sW", c_void_p * TW_MAXL), ("tstamp", c_void_p), ("deep", c_int),
-                ("G", c_void_p), ("S", c_void_p), ("vals", c_void_p), ("F", c_int), ("K", c_int)]
+                ("sW", c_void_p * TW_MAXL)]
 
 
 class W8Job(C.Structure):

@@ -41,6 +41,20 @@ def test_supervisor_falls_back_and_prints_one_line(fake, rung):
     assert len(lines) == 1 and lines[0]["config"]["exec"] == rung and lines[0]["n_gpus"] == 2
 
 
+@pytest.mark.parametrize("n", [2, 3])
+def test_plain_bench_gpus_n_spawns_n_ranks(n):
+    """The driver's SCALE shape without a launcher: ``python bench.py --gpus N`` starts N ranks
+    itself (torchrun-style env, 127.0.0.1) and prints exactly one line with n_gpus == N."""
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "TORCHELASTIC_RUN_ID", "MASTER_PORT")}
+    env.update(HIPFM_BENCH_FAKE="none:0:fail", HIPFM_BENCH_HANG_S="20")
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", str(n), "--steps", "3"],
+                       env=env, capture_output=True, text=True, timeout=180, cwd=REPO)
+    lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert len(lines) == 1 and lines[0]["n_gpus"] == n
+
+
 def test_supervisor_fails_when_every_rung_fails():
     rc, lines = _run("graph+prefetch:0:fail,eager+prefetch:0:fail,eager:1:fail")
     assert rc != 0 and not lines

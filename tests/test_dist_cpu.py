@@ -77,7 +77,9 @@ def _worker_body(rank, world, port, mode, opt, update, q):
         fv, fw = m.params["fm_v"], m.params["fm_w"]
         dense = {k: v for k, v in m.params.items() if k.startswith("Deep") or k == "fm_bias"}
     if rank == 0:
-        q.put({"fm_v": fv.clone(), "fm_w": fw.clone(), **{k: v.clone() for k, v in dense.items()}})
+        # numpy copies: a torch tensor in a Queue travels as a shared-memory fd that dies with
+        # this process, so the parent could read it only while the worker is still alive
+        q.put({k: v.detach().numpy().copy() for k, v in {"fm_v": fv, "fm_w": fw, **dense}.items()})
     dist.barrier()
     dist.destroy_process_group()
 
@@ -106,6 +108,7 @@ def test_dp_matches_single_process_global_batch(mode, opt, update):
     for ids, vals, lab in _batches(4, 32 * world):
         ref.train_step(ids, vals, lab)
     for k, v in got.items():
+        v = torch.from_numpy(v)
         assert torch.allclose(v, ref.params[k], atol=2e-6, rtol=1e-5), (k, (v - ref.params[k]).abs().max())
 
 
