@@ -159,6 +159,8 @@ def main():
     ap.add_argument("--pool", type=int, default=16, help="resident synthetic batches per rank")
     ap.add_argument("--eval_batches", type=int, default=8)
     ap.add_argument("--no_graph", action="store_true")
+    ap.add_argument("--graph_steps", type=int, default=int(os.environ.get("HIPFM_GRAPH_STEPS", "16")),
+                    help="consecutive training steps captured per HIP graph (divides --pool)")
     ap.add_argument("--force_exchange", action="store_true",
                     help="run the multi-GPU (row-sharded exchange) step on a 1-rank group")
     args = ap.parse_args()
@@ -213,28 +215,56 @@ def main():
     pool = [synth.batch(B, step=rank * 100000 + i, device=dev, id_dtype=torch.int32)
             for i in range(args.pool)]
     use_graph = not args.no_graph
+    P = len(pool)
+    G = max(1, min(args.graph_steps, P))
+    while P % G:
+        G -= 1
     torch.cuda.synchronize()
     _progress()
-    if use_graph and (comm is None or comm.graph_safe):
-        model.precapture(pool, progress=_progress)        # one HIP graph per resident batch, captured before timing
 
-    def run(nsteps, start):
-        for s in range(nsteps):
-            if s % 16 == 0:
+    def chunks(lo, hi):
+        """Global step positions [lo, hi) cut into runs of consecutive pool batches: cuts at
+        multiples of G (so a run never wraps the pool) and at the warm-up / timed boundary, so
+        the timed runs are exactly runs already captured before timing."""
+        t = lo
+        while t < hi:
+            e = min(hi, (t // G + 1) * G)
+            if t < args.warmup < e:
+                e = args.warmup
+            yield t, e
+            t = e
+
+    def run(lo, hi):
+        for k, (t, e) in enumerate(chunks(lo, hi)):
+            if k % 8 == 0:
                 _progress()
-            ids, vals, labels = pool[(start + s) % len(pool)]
-            nxt = pool[(start + s + 1) % len(pool)][0]     # next batch: its id routing is prefetched
-            model.train_step(ids, vals, labels, use_graph=use_graph, next_ids=nxt)
+            i = t % P
+            nxt = pool[e % P][0]                      # next batch: its sort / routing is prefetched
+            if use_graph and G > 1:
+                model.train_steps(pool[i:i + (e - t)], next_ids=nxt)
+            else:
+                for j in range(e - t):
+                    ids, vals, labels = pool[i + j]
+                    model.train_step(ids, vals, labels, use_graph=use_graph,
+                                     next_ids=pool[(i + j + 1) % P][0])
 
+    if use_graph and (comm is None or comm.graph_safe):
+        # every graph the warm-up and timed runs replay is captured here first (real steps)
+        run(0, args.warmup + args.steps)
+        if (args.warmup + args.steps) % 2:
+            # the sorted-slot / routing sets alternate step by step: an even number of steps
+            # before the warm-up keeps every run's set parity equal to its parity at capture
+            model.train_step(*pool[0], use_graph=use_graph, next_ids=pool[1 % P][0])
+        torch.cuda.synchronize()
     _progress()
-    run(args.warmup, 0)
+    run(0, args.warmup)
     torch.cuda.synchronize()
     _progress()
     if comm is not None:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    run(args.steps, args.warmup)
+    run(args.warmup, args.warmup + args.steps)
     torch.cuda.synchronize()
     if comm is not None:
         dist.barrier()
@@ -283,6 +313,7 @@ def main():
                                                 f"+{'row-sharded' if comm.sharded else 'replicated'}-embedding"),
                 "optimizer": f"{args.optimizer} ({args.sparse_update})",
                 "hip_graph": use_graph,
+                "graph_steps": G if use_graph else 0,
                 "exec": os.environ.get("HIPFM_BENCH_RUNG", "graph+prefetch" if use_graph else "eager"),
                 "mlp_dtype": args.mlp_dtype + (" fwd GEMMs, bf16 backward" if args.mlp_dtype == "fp8" else ""),
             },

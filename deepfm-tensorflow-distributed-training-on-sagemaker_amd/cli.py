@@ -121,10 +121,19 @@ def run(cfg: RunConfig) -> dict:
             result = est.evaluate(va())
         else:
             pipe = tr(1)
-            for epoch in range(cfg.num_epochs):
+            # resume from the checkpoint's data position: its epoch, minus the batches of that
+            # epoch already trained on
+            first, skip = est.epoch, est.epoch_batch
+            if first >= cfg.num_epochs:
+                # the checkpoint's run completed its epochs: this job trains num_epochs more on
+                # top of it (the reference re-runs its epoch loop on restored weights, HVD:390-392)
+                first, skip = 0, 0
+            for epoch in range(first, cfg.num_epochs):
                 pipe.num_epochs = 1
-                est.train(pipe.iter_epoch(epoch) if not hasattr(pipe, "local_records") else
-                          _EpochView(pipe, epoch), max_steps, eval_fn=lambda: est.evaluate(va()))
+                est.epoch, est.epoch_batch = epoch, (skip if epoch == first else 0)
+                est.train(_EpochView(pipe, epoch, est.epoch_batch), max_steps,
+                          eval_fn=lambda: est.evaluate(va()))
+                est.epoch, est.epoch_batch = epoch + 1, 0
                 result = est.evaluate(va())
                 if max_steps is not None and est.global_step >= max_steps:
                     break
@@ -150,14 +159,19 @@ def run(cfg: RunConfig) -> dict:
 
 
 class _EpochView:
-    """One epoch of an InputPipeline that still exposes local_records (equal-steps logic)."""
+    """One epoch of an InputPipeline (from batch ``skip`` on) that still exposes local_records
+    (equal-steps logic)."""
 
-    def __init__(self, pipe: InputPipeline, epoch: int):
-        self.pipe, self.epoch = pipe, epoch
+    def __init__(self, pipe: InputPipeline, epoch: int, skip: int = 0):
+        self.pipe, self.epoch, self.skip = pipe, epoch, int(skip)
         self.B = pipe.B
 
+    @property
+    def countable(self):
+        return self.pipe.countable
+
     def local_records(self):
-        return self.pipe.local_records(self.epoch)
+        return self.pipe.local_records(self.epoch)     # the whole epoch: max_batches counts skips
 
     @property
     def max_batches(self):
@@ -168,7 +182,7 @@ class _EpochView:
         self.pipe.max_batches = v
 
     def __iter__(self):
-        return self.pipe.iter_epoch(self.epoch)
+        return self.pipe.iter_epoch(self.epoch, skip=self.skip)
 
 
 def main(argv: Optional[Sequence[str]] = None) -> dict:

@@ -157,19 +157,26 @@ class InputPipeline:
             t = tuple(x.to(self.device, non_blocking=True) for x in t)
         return t
 
-    def iter_epoch(self, epoch: int) -> Iterator[Tuple[torch.Tensor, torch.Tensor, torch.Tensor]]:
+    def iter_epoch(self, epoch: int, skip: int = 0) -> Iterator[Tuple[torch.Tensor, torch.Tensor, torch.Tensor]]:
+        """Batches of one epoch; ``skip`` drops the first batches (resume mid-epoch: they are
+        read past, never decoded to tensors or trained on).  ``max_batches`` counts the skipped
+        ones too (it is the epoch's length)."""
         if self.cache and self._cached is not None:
-            yield from self._cached[: self.max_batches] if self.max_batches else self._cached
+            end = self.max_batches if self.max_batches else len(self._cached)
+            yield from self._cached[skip:end]
             return
         plan = self.epoch_plan(epoch)
         loader = NativeLoader(plan.files, self.F, self.B, self.fmt, self.drop_remainder,
                               self.threads, plan.record_shard)
-        store = [] if self.cache else None
+        store = [] if (self.cache and skip == 0) else None
         k = 0
         try:
             for lab, ids, vals in loader:
                 if self.max_batches is not None and k >= self.max_batches:
                     break
+                if k < skip:
+                    k += 1
+                    continue
                 t = self._to_tensors(lab, ids, vals)
                 if store is not None:
                     store.append(t)

@@ -114,6 +114,11 @@ class Estimator:
         self._tb = self._tb_eval = None
         self._tb_on = bool(cfg.ckpt_dir) and self.rank == 0 and getattr(cfg, "tensorboard", True)
         self.timer = StepTimer()
+        # data-iterator position: epoch index and batches of that epoch already
+        # trained on.  Saved with every checkpoint and restored with it, so a resumed job skips
+        # what it already trained on instead of replaying the epoch.
+        self.epoch = 0
+        self.epoch_batch = 0
         self._last_save_t = time.time()
         self._last_eval_t = 0.0
         self.restored_from = self.restore_latest()
@@ -130,10 +135,13 @@ class Estimator:
 
     def _meta(self):
         if self.native:
-            return self.model.ckpt_meta()
-        return {"format": "hipfm-golden", "V": self.cfg.feature_size, "F": self.cfg.field_size,
-                "K": self.cfg.embedding_size, "layers": self.cfg.layers, "optimizer": self.cfg.optimizer,
-                "world": self.world, "sharding": "replicated"}
+            meta = dict(self.model.ckpt_meta())
+        else:
+            meta = {"format": "hipfm-golden", "V": self.cfg.feature_size, "F": self.cfg.field_size,
+                    "K": self.cfg.embedding_size, "layers": self.cfg.layers,
+                    "optimizer": self.cfg.optimizer, "world": self.world, "sharding": "replicated"}
+        meta["data_pos"] = {"epoch": self.epoch, "batch": self.epoch_batch}
+        return meta
 
     def save(self) -> Optional[str]:
         if self.ckpt is None:
@@ -162,7 +170,12 @@ class Estimator:
         else:
             st = self._reshard_load(path, man)
         self.model.load_state_dict_local(st)
-        self.log.info(f"Restoring parameters from {path} (global_step {self.global_step})")
+        pos = meta.get("data_pos") or {}
+        if man["world"] == self.world:
+            # the data position is per rank-shard: it carries over only to the same world size
+            self.epoch, self.epoch_batch = int(pos.get("epoch", 0)), int(pos.get("batch", 0))
+        self.log.info(f"Restoring parameters from {path} (global_step {self.global_step}, "
+                      f"epoch {self.epoch} batch {self.epoch_batch})")
         return path
 
     def broadcast_state(self):
@@ -289,6 +302,7 @@ class Estimator:
             else:
                 self.model.train_step(ids, vals, labels, grad_sync=self._golden_grad_sync)
             self.timer.add("step_enqueue", time.time() - t0)
+            self.epoch_batch += 1
             n_log += B
             step = self.global_step
             wd.beat(step)

@@ -280,6 +280,8 @@ class NativeDeepFM:
         self.h_dense = KN.hyper(self.lr, 0.0, eps=adam_epsilon)
         self._bufs_M = 0
         self._side = None
+        self._side_next = None
+        self._next_sort_ids = None
         self._comm_stream = None
         self.shx = None
         self._shx_plan = None
@@ -418,6 +420,15 @@ class NativeDeepFM:
         self.sf_lead = torch.zeros(nt, K + 4, **f32)
         self.sf_tinfo = torch.zeros(nt, 4, **i32)
         self._fsort = None
+        self._fsort_next = None
+        # sorted-slot sets: set c holds the sort of the batch this step trains, set 1 - c receives
+        # the sort of the NEXT batch, computed on a side stream during this step (single GPU,
+        # next batch declared by the caller); the two sets alternate step by step
+        self._ss = [(self.sorted_keys, self.perm),
+                    (torch.zeros(n, **i32), torch.zeros(n, **i32))]
+        self._ss_key = [None, None]
+        self._ss_cur = 0
+        self._sort_plan = None
         if self.field_ranges is not None:
             # the sort runs on a side stream next to the step in both cases, and every sort
             # workgroup holds 148 KB of LDS: one workgroup per field on one GPU (0.160 ms/step vs
@@ -426,6 +437,9 @@ class NativeDeepFM:
             pb = os.environ.get("HIPFM_FSORT_PB")
             self._fsort = KN.FieldSort(self.field_ranges, min(M, KN.field_sort_max_rows()), dev,
                                        max_pb=int(pb) if pb is not None else (2 if self.sharded else 0))
+            if not self.sharded:
+                self._fsort_next = KN.FieldSort(self.field_ranges, min(M, KN.field_sort_max_rows()),
+                                                dev, max_pb=int(pb) if pb is not None else 0)
         tb = max(KN.radix_temp_bytes(n), KN.rbk_temp_bytes(K, n), KN.scan_temp_bytes(n))
         self.temp = torch.zeros(tb + 256, dtype=torch.uint8, device=dev)
         self._build_finalize_jobs()
@@ -864,7 +878,7 @@ class NativeDeepFM:
 
     def check_errors(self):
         """Raise on device-side input errors flagged by earlier steps (host sync)."""
-        if self._fsort is not None and int(self._fsort.err.item()) != 0:
+        if any(fs is not None and int(fs.err.item()) != 0 for fs in (self._fsort, self._fsort_next)):
             raise RuntimeError("an id lies outside its field's declared range (field_ranges): "
                                "the per-field sort is invalid for this data")
         if self.shx is not None and self.shx.error() != 0:
@@ -949,8 +963,28 @@ class NativeDeepFM:
         if self.shx is not None:
             self._shx_start(B)
         after_fm = None
-        if not self.sharded and _SORT_SIDE_STREAM:
-            main = torch.cuda.current_stream(self.device)
+        plan = self._sort_plan
+        self.sorted_keys, self.perm = self._ss[plan[0] if plan is not None else self._ss_cur]
+        prefetch = plan is not None and plan[2] is not None
+        inline = plan is None or plan[1]
+        main = torch.cuda.current_stream(self.device)
+        if prefetch:
+            # the next batch's sort: a ROOT branch of the step's graph (no dependency on this
+            # step's kernels), enqueued after fm_fwd so the first kernel is launched first; it
+            # overlaps the whole step and is joined only at its end
+            if self._side_next is None:
+                self._side_next = torch.cuda.Stream(self.device)
+            self._side_next.wait_stream(main)
+            nk_ids, nk_B = self._next_sort_ids, plan[2][1]
+            nxt_keys, nxt_perm = self._ss[1 - plan[0]]
+
+            def sort_next():
+                with torch.cuda.stream(self._side_next):
+                    self._fsort_next(nk_ids, nk_B, nxt_keys, nxt_perm)
+            after_fm = sort_next
+        if not inline:
+            presorted = True            # sorted during the previous step
+        elif not self.sharded and _SORT_SIDE_STREAM:
             if self._side is None:
                 self._side = torch.cuda.Stream(self.device)
 
@@ -969,7 +1003,14 @@ class NativeDeepFM:
             # graph branches launch in capture order: forking after fm_fwd is enqueued lets the
             # step's first kernel start at once instead of after the sort's launches
             # (same-box A/B: 0.160 -> 0.154 ms/step, bitwise-identical results)
-            after_fm = fork_sort
+            if after_fm is None:
+                after_fm = fork_sort
+            else:
+                first = after_fm
+
+                def after_fm():
+                    fork_sort()
+                    first()
             presorted = True
         # fused tower: the weight gradients (wgrad + finalize, then the dense all-reduce) only
         # feed the dense optimizer, so on the multi-rank step they run on their own stream
@@ -997,7 +1038,7 @@ class NativeDeepFM:
                 KN.w8_quant(self._w8_jobs, len(self.layers), self._w8_rows)
         elif self._dense_early:
             self._dense_opt()
-        if presorted:
+        if presorted and inline:
             main.wait_stream(self._side)
         work = None
         eng = getattr(self.comm, "engine_dense", None) if self.exchange else None
@@ -1027,6 +1068,8 @@ class NativeDeepFM:
             self.shx.end(self._shx_plan)
         if not self._dense_early:
             self._dense_opt()
+        if prefetch:
+            main.wait_stream(self._side_next)
 
     def _dense_opt(self):
         """Dense optimizer over the flat buffer (+ bf16 / fp8 weight shadows); advances the step."""
@@ -1056,15 +1099,16 @@ class NativeDeepFM:
         U = int(self.num_u.item())
         return self.g.clone(), self.ukeys[:U].clone(), self.UG[:U].clone()
 
-    def train_step(self, ids, vals, labels, use_graph: bool = False, next_ids=None):
-        """One training step.  A device-resident int32 batch whose size equals the allocated
-        batch is bound in place (no staging copy); with ``use_graph`` each such resident batch
-        gets its own captured HIP graph (the HBM-cached epoch replays graphs back to back).
-        ``next_ids`` (resident ids of the NEXT step's batch): on the row-sharded multi-GPU step
-        its routing is prefetched on a side stream during this step."""
-        direct = (ids.is_cuda and ids.dtype == torch.int32 and vals.dtype == torch.float32 and
-                  ids.is_contiguous() and vals.is_contiguous() and labels.is_contiguous() and
-                  ids.shape[0] == self.M and ids.numel() == self.M * self.F)
+    def _resident(self, ids, vals, labels) -> bool:
+        return (ids.is_cuda and ids.dtype == torch.int32 and vals.dtype == torch.float32 and
+                ids.is_contiguous() and vals.is_contiguous() and labels.is_contiguous() and
+                ids.shape[0] == self.M and ids.numel() == self.M * self.F)
+
+    def _bind_step(self, ids, vals, labels, next_ids=None):
+        """Bind one step's batch (in place when resident, else a staging copy) and decide its
+        host-side plans (sort / routing: inline or prefetched, next batch or none).  Returns
+        (B, direct, key) -- ``key`` identifies the step's captured graph."""
+        direct = self._resident(ids, vals, labels)
         if direct:
             B = ids.shape[0]
             self.idx, self.vals, self.labels = ids.reshape(-1), vals.reshape(-1), labels.reshape(-1)
@@ -1073,26 +1117,122 @@ class NativeDeepFM:
             self.idx, self.vals, self.labels = self._own_in
             B = self.stage_batch(ids, vals, labels)
             key = ("staged", B)
+        nxt_ok = (direct and next_ids is not None and next_ids.is_cuda and
+                  next_ids.dtype == torch.int32 and next_ids.is_contiguous() and
+                  next_ids.shape[0] == B and next_ids.numel() == B * self.F)
         self._shx_plan = None
+        self._sort_plan = None
+        if (not self.sharded and _SORT_SIDE_STREAM and self._fsort_next is not None and
+                self.uses_field_sort(B)):
+            # the sort of a batch the caller declared as next (resident, unchanged until its step)
+            # was computed during the previous step: reuse it when that batch is this one
+            c = self._ss_cur
+            inline = not (direct and self._ss_key[c] == (ids.data_ptr(), B))
+            nk = None
+            if nxt_ok:
+                nk = (next_ids.data_ptr(), B)
+                self._next_sort_ids = next_ids.reshape(-1)
+            self._sort_plan = (c, inline, nk)
+            key = key + ("sort",) + self._sort_plan
         if self.shx is not None:
-            nxt = None
-            if (direct and next_ids is not None and _SHARD_PIPELINE and next_ids.is_cuda and
-                    next_ids.dtype == torch.int32 and next_ids.is_contiguous() and
-                    next_ids.shape[0] == B and next_ids.numel() == B * self.F):
-                nxt = next_ids.reshape(-1)
+            nxt = next_ids.reshape(-1) if (nxt_ok and _SHARD_PIPELINE) else None
             self._shx_plan = self.shx.plan(self.idx, B, nxt, resident=direct)
             self.shx._next_ids = nxt
             key = key + self._shx_plan
+        return B, direct, key
+
+    def _commit_step(self, B: int, direct: bool):
+        if self.shx is not None:
+            self.shx.commit(self._shx_plan, self.idx, B, resident=direct)
+            self._shx_plan = None
+        if self._sort_plan is not None:
+            c, _, nk = self._sort_plan
+            self._ss_key[c] = None          # consumed: reused only through a next-batch declaration
+            self._ss_key[1 - c] = nk
+            self._ss_cur = 1 - c
+            self._sort_plan = None
+        if self._host_step is not None:
+            self._host_step += 1
+
+    def _plan_state(self):
+        sh = None if self.shx is None else (self.shx.cur, [rs.key for rs in self.shx.sets])
+        return self._ss_cur, list(self._ss_key), sh
+
+    def _set_plan_state(self, st):
+        self._ss_cur, self._ss_key = st[0], list(st[1])
+        if st[2] is not None:
+            self.shx.cur = st[2][0]
+            for rs, k in zip(self.shx.sets, st[2][1]):
+                rs.key = k
+
+    def train_step(self, ids, vals, labels, use_graph: bool = False, next_ids=None):
+        """One training step.  A device-resident int32 batch whose size equals the allocated
+        batch is bound in place (no staging copy); with ``use_graph`` each such resident batch
+        gets its own captured HIP graph (the HBM-cached epoch replays graphs back to back).
+        ``next_ids`` (resident ids of the NEXT step's batch, unchanged until that step): its
+        slot sort (one GPU) or its routing (row-sharded multi-GPU step) is computed on a side
+        stream during this step."""
+        B, direct, key = self._bind_step(ids, vals, labels, next_ids)
         if use_graph and (self.comm is None or self.comm.graph_safe):
             self._replay_graph(key, B)
         else:
             self.train_step_enqueue(B)
-        if self.shx is not None:
-            self.shx.commit(self._shx_plan, self.idx, B, resident=direct)
-            self._shx_plan = None
-        if self._host_step is not None:
-            self._host_step += 1
+        self._commit_step(B, direct)
         return B
+
+    def train_steps(self, batches, next_ids=None) -> int:
+        """Consecutive training steps over resident batches as ONE captured HIP graph (a whole
+        launch-bound inner loop per replay: the per-replay launch and branch-join cost is paid
+        once per run of steps instead of once per step).  Every step is complete -- forward,
+        backward, sparse and dense optimizer -- and identical to ``train_step`` (bitwise, tested).
+        Batch i declares batch i+1 as its next batch (prefetched sort / routing); ``next_ids``
+        is the batch after the last one.  Returns the number of steps."""
+        batches = list(batches)
+        if not batches:
+            return 0
+        if not all(self._resident(*b) for b in batches) or not (self.comm is None or self.comm.graph_safe):
+            for i, (ids, vals, labels) in enumerate(batches):
+                nxt = batches[i + 1][0] if i + 1 < len(batches) else next_ids
+                self.train_step(ids, vals, labels, use_graph=True, next_ids=nxt)
+            return len(batches)
+        st0 = self._plan_state()
+        h0 = self._host_step
+        keys, Bs = [], []
+        for i, (ids, vals, labels) in enumerate(batches):       # plans only: the graph key
+            nxt = batches[i + 1][0] if i + 1 < len(batches) else next_ids
+            B, direct, k = self._bind_step(ids, vals, labels, nxt)
+            keys.append(k)
+            Bs.append(B)
+            self._commit_step(B, direct)
+        key = ("run",) + tuple(keys)
+        g = self._graphs.get(key)
+        if g is None:
+            self._set_plan_state(st0)
+            self._host_step = h0
+            eager_first = not self._graphs and not getattr(self, "_warm", False)
+            if eager_first:
+                self._warm = True
+                # the very first step of the model runs eagerly (warms up lazy library state)
+                ids, vals, labels = batches[0]
+                self.train_step(ids, vals, labels, use_graph=False,
+                                next_ids=batches[1][0] if len(batches) > 1 else next_ids)
+                torch.cuda.synchronize()
+                rest = batches[1:]
+                if not rest:
+                    return 1
+                return 1 + self.train_steps(rest, next_ids)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                for i, (ids, vals, labels) in enumerate(batches):
+                    nxt = batches[i + 1][0] if i + 1 < len(batches) else next_ids
+                    B, direct, _ = self._bind_step(ids, vals, labels, nxt)
+                    self.train_step_enqueue(B)
+                    self._commit_step(B, direct)
+            if len(self._graphs) >= self.max_graphs:
+                self._graphs.pop(next(iter(self._graphs)))
+            self._graphs[key] = g
+        g.replay()
+        return len(batches)
 
     def _replay_graph(self, key, B: int):
         g = self._graphs.get(key)

@@ -146,11 +146,13 @@ class FixedCapacityExchange:
     def commit(self, plan, ids: torch.Tensor, B: int, resident: bool = True):
         """Consecutive steps always use alternate routing sets (prefetched or not): a step's
         routing kernels never overwrite buffers the previous step's backward still reads, even
-        when graph replays run back to back."""
+        when graph replays run back to back.  A routing set is reused ONLY for the batch the
+        caller declared as next (``next_ids``): a set is never matched again by address alone,
+        since a freshly allocated batch can get the address of an earlier one back from the
+        caching allocator."""
         c, _, nk = plan
-        self.sets[c].key = (ids.data_ptr(), B) if resident else None
-        if nk is not None:
-            self.sets[1 - c].key = nk
+        self.sets[c].key = None
+        self.sets[1 - c].key = nk
         self.cur = 1 - c
 
     # ------------------------------------------------------------------ pieces

@@ -27,7 +27,7 @@ def test_kill_and_resume_reproduces(tmp_path):
                            "--val_rows", "256", "--files", "1"], cwd=REPO)
     base = ["--training_data_dir", str(d), "--val_data_dir", str(d), "--feature_size", "5000",
             "--field_size", "39", "--embedding_size", "4", "--batch_size", "64", "--deep_layers", "16",
-            "--dropout", "1.0", "--num_epochs", "1", "--device", "cpu", "--save_checkpoints_steps", "8",
+            "--dropout", "0.5", "--num_epochs", "1", "--device", "cpu", "--save_checkpoints_steps", "8",
             "--log_steps", "100"]
     ref = _run(base + ["--model_dir", str(tmp_path / "ref")])
     assert ref.returncode == 0, ref.stderr[-2000:]
@@ -38,11 +38,17 @@ def test_kill_and_resume_reproduces(tmp_path):
     res = _run(base + ["--model_dir", str(tmp_path / "crash")])
     assert res.returncode == 0, res.stderr[-2000:]
     assert "Restoring parameters" in res.stdout
-    a = CheckpointManager(str(tmp_path / "ref")).load_rank(CheckpointManager(str(tmp_path / "ref")).latest(), 0)
+    ra = CheckpointManager(str(tmp_path / "ref"))
+    a = ra.load_rank(ra.latest(), 0)
     b = m.load_rank(m.latest(), 0)
-    assert int(a["global_step"]) == 32 and int(b["global_step"]) >= 32
-    # the resumed run replays epoch 0 from its start (data position is the epoch boundary), so
-    # it ends with more steps; the first 16 steps are bitwise identical by construction
+    # the checkpoint restores the data position (epoch 0, batch 16): the resumed run trains only
+    # batches 16..31 and ends bitwise equal to the uninterrupted run (params, slots, step)
+    assert int(a["global_step"]) == 32 and int(b["global_step"]) == 32
+    assert "epoch 0 batch 16" in res.stdout
+    assert set(a) == set(b)
+    for k in a:
+        assert torch.equal(a[k], b[k]), k
+    assert ra.load_manifest(ra.latest())["meta"]["data_pos"] == {"epoch": 1, "batch": 0}
 
 
 def test_watchdog_fires_on_stall():

@@ -491,3 +491,76 @@ def test_finalize_fused_dense_opt_bitwise_equal(monkeypatch, opt, mlp_dtype):
                 d = (x.float() - y.float()).abs().max().item()
                 segs = {s.name: s.off for s in m.dense_segs.values()}
                 pytest.fail(f"variant {k + 1}: {nm} differs, max {d:.3e} at {bad}; segs {segs}")
+
+
+@pytest.mark.parametrize("use_graph", [False, True])
+def test_prefetched_next_batch_sort_bitwise_equal(use_graph):
+    """The next batch's slot sort computed on a side stream during the current step (next_ids)
+    gives bitwise the parameters of the step that sorts its own batch."""
+    synth = make_synth("criteo_kaggle", seed=21)
+    F, K, layers, keep, B = synth.F, 8, [128, 64, 32], [0.5] * 3, 1024
+    params = init_params(synth.feature_size, F, K, layers, False, seed=2)
+    pool = [synth.batch(B, step=s, device=DEV, id_dtype=torch.int32) for s in range(3)]
+    out = []
+    for pre in (True, False):
+        m = NativeDeepFM(synth.feature_size, F, K, layers, keep, batch_size=B, device=DEV, init=False,
+                         sparse_update="lazy", field_ranges=synth.field_ranges())
+        m.load_tf_params(params)
+        for s in range(7):
+            ids, vals, lab = pool[s % 3]
+            m.train_step(ids, vals, lab, use_graph=use_graph, next_ids=pool[(s + 1) % 3][0] if pre else None)
+        torch.cuda.synchronize()
+        m.check_errors()
+        out.append((m.tv.clone(), m.tw.clone(), m.p.clone()))
+    for x, y in zip(*out):
+        assert torch.equal(x, y)
+
+
+def test_fresh_batch_allocations_never_reuse_stale_sorts():
+    """A caller that allocates every batch anew (the caching allocator hands old addresses back)
+    and declares no next batch gets exactly the staged-copy results (results cached
+    under a reused address must never be trusted)."""
+    synth = make_synth("criteo_kaggle", seed=22)
+    F, K, layers, keep, B = synth.F, 8, [64, 32], [1.0, 1.0], 1024
+    params = init_params(synth.feature_size, F, K, layers, False, seed=3)
+    out = []
+    for fresh in (True, False):
+        m = NativeDeepFM(synth.feature_size, F, K, layers, keep, batch_size=B, device=DEV, init=False,
+                         sparse_update="lazy", field_ranges=synth.field_ranges())
+        m.load_tf_params(params)
+        for s in range(6):
+            ids, vals, lab = synth.batch(B, step=s)
+            if fresh:
+                m.train_step(ids.to(DEV, torch.int32), vals.to(DEV), lab.to(DEV), use_graph=True)
+            else:
+                m.train_step(ids.to(DEV), vals.to(DEV), lab.to(DEV))     # int64 -> staged copy
+        torch.cuda.synchronize()
+        out.append((m.tv.clone(), m.p.clone()))
+    assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
+
+
+@pytest.mark.parametrize("G", [2, 4])
+def test_multi_step_graph_bitwise_equals_single_steps(G):
+    """train_steps (G consecutive steps captured as ONE graph, next-batch sorts prefetched inside
+    it) leaves bitwise the state of the same steps run one by one."""
+    synth = make_synth("criteo_kaggle", seed=23)
+    F, K, layers, keep, B = synth.F, 8, [128, 64, 32], [0.5] * 3, 1024
+    params = init_params(synth.feature_size, F, K, layers, False, seed=5)
+    pool = [synth.batch(B, step=s, device=DEV, id_dtype=torch.int32) for s in range(4)]
+    out = []
+    for multi in (True, False):
+        m = NativeDeepFM(synth.feature_size, F, K, layers, keep, batch_size=B, device=DEV, init=False,
+                         sparse_update="lazy", field_ranges=synth.field_ranges())
+        m.load_tf_params(params)
+        for rep in range(3):
+            if multi:
+                for i in range(0, 4, G):
+                    m.train_steps(pool[i:i + G], next_ids=pool[(i + G) % 4][0])
+            else:
+                for i in range(4):
+                    m.train_step(*pool[i], use_graph=True, next_ids=pool[(i + 1) % 4][0])
+        torch.cuda.synchronize()
+        assert m.global_step() == 12 and int(m.step.item()) == 12
+        out.append((m.tv.clone(), m.tw.clone(), m.p.clone(), m.sv[0].clone()))
+    for x, y in zip(*out):
+        assert torch.equal(x, y)
