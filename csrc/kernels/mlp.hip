@@ -490,6 +490,7 @@ __device__ void rowsum_block(const RowSumJob* jobs, int njobs, int b, const FinO
   const RowSumJob j = jobs[ji];
   const bf16* s = j.src + (size_t)rem * j.ld;
   float acc = 0.f;
+#pragma unroll 8
   for (int i = threadIdx.x * 8; i < j.n; i += 256 * 8) {
     const bf16x8 v = *reinterpret_cast<const bf16x8*>(s + i);
 #pragma unroll

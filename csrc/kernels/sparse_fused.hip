@@ -1,6 +1,6 @@
 // Fused embedding backward + row optimizer over the sorted slots (single rank / tf1_dense
 // scatter): K2 (per-slot FM + MLP-input gradient), K3 (sum per unique id) and K4 (lazy row
-// optimizer, or the tf1_dense gradient scatter) in one tile kernel plus one small carry kernel.
+// optimizer, or the tf1_dense gradient scatter) in ONE launch.
 // SURVEY §2.5 rows 17-20, §7.4 item 1; the reference's update is TF1 Adam._apply_sparse on the
 // IndexedSlices of embedding_lookup (HVD:170-176, HVD:252-263).
 //
@@ -17,10 +17,14 @@
 //      row, or scatter); the one run that continues into the next tile leaves its partial in
 //      ctail[tile].  The tile's own leading piece (continuation of an earlier run) goes to
 //      lead[tile], with a flag when the tile has no head at all.
-// Carry kernel: each open run = ctail[t] + lead[t+1] + ... up to the first tile with a head
-// (tile order), then applied.  Every sum has a fixed order: bitwise reproducible, atomic-free.
-// Long runs (Criteo's integer fields: one id in every row) cost one lead read per tile they span.
-#include "common.h"
+//   4. the tile publishes (lead, ctail, run info) and, if its leading piece closes a run that
+//      started in an earlier tile (first slot not a head, and the run ends in this tile), one
+//      wave looks back over the predecessors, 64 tiles per round: the run total
+//      = own lead + leads of the headless tiles in between + ctail of the origin tile, applied
+//      right there (sync.h hand-off; predecessors have lower ids, so the wait always ends).
+// Every sum has a fixed order: bitwise reproducible, atomic-free.  Long runs (Criteo's integer
+// fields: one id in every row) cost one parallel lead read per 64 tiles they span.
+#include "sync.h"
 
 template <int K>
 struct SfCfg {
@@ -55,7 +59,9 @@ struct SfArgs {
   const int* sid;
   const int* upos;
   float* gout;
-  int step_off;    // 1: *step is this step's index - 1 (the dense optimizer advances it later);
+  int step_off;
+  unsigned* flags;  // [tiles] publication flags: the step's 1-based index (*step + step_off)
+  unsigned* sync;   // {pad, pad, error bits, pad}    // 1: *step is this step's index - 1 (the dense optimizer advances it later);
                    // 0: the dense optimizer already ran and advanced it (single-GPU early mode)
 };
 
@@ -115,6 +121,81 @@ __device__ __forceinline__ float sf_lr_t(const SfArgs& A) {
   return OPT == OPT_ADAM ? adam_lr_t(A.h, *A.step + A.step_off) : A.h.lr;
 }
 
+// One wave: the run that started in an earlier tile and closes in tile `tile` (see step 4).
+template <int K, int MODE, int OPT>
+__device__ __forceinline__ void sf_lookback(const SfArgs& A, int tile, unsigned tag, const float* own,
+                                            float lr_t) {
+  using T = SfCfg<K>;
+  constexpr int NV = T::RS / 4;  // f32x4 per lead row: a[K], w, c, pad, pad
+  const int lane = threadIdx.x & 63;
+  f32x4 tot[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) tot[v][j] = (4 * v + j < T::C) ? own[4 * v + j] : 0.f;
+  for (int t0 = tile - 1; t0 >= 0; t0 -= 64) {
+    const int t2 = t0 - lane;  // lane 0 = the nearest predecessor
+    const bool valid = t2 >= 0;
+    unsigned spins = 0;
+    while (!__all(!valid || hx_load(A.flags + t2) == tag)) {
+      if (++spins >= HFM_SPIN_LIMIT) {
+        if (lane == 0) atomicOr(A.sync + 2, 1u);
+        return;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    asm volatile("" ::: "memory");  // every handed-off word below is read write-through (sc1)
+    const bool has_head = valid && !hx_ldi(A.tinfo + t2 * 4);
+    const unsigned long long stop = __ballot(has_head);
+    const int first = stop ? __ffsll((long long)stop) - 1 : 64;  // the run's origin tile (lane)
+    f32x4 p[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      p[v] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (valid && lane < first) {
+        const float* lp = A.lead + (size_t)t2 * T::RS + 4 * v;
+        p[v] = f32x4{hx_ldf(lp), hx_ldf(lp + 1), hx_ldf(lp + 2), hx_ldf(lp + 3)};
+      }
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) {
+        p[v][0] += __shfl_xor(p[v][0], o, 64);
+        p[v][1] += __shfl_xor(p[v][1], o, 64);
+        p[v][2] += __shfl_xor(p[v][2], o, 64);
+        p[v][3] += __shfl_xor(p[v][3], o, 64);
+      }
+      tot[v] += p[v];
+    }
+    if (!stop) continue;
+    const int org = t0 - first;
+    const int key = hx_ldi(A.tinfo + org * 4 + 1), hpos = hx_ldi(A.tinfo + org * 4 + 2);
+    if (key < 0) {  // an origin tile always leaves its last run open: inconsistent publication
+      if (lane == 0) atomicOr(A.sync + 2, 2u);
+      return;
+    }
+    const int sub = lane;
+    if (sub >= T::LPS) return;
+    const float* ct = A.ctail + (size_t)org * T::RS;
+    f32x4 av = {hx_ldf(ct + sub * 4), hx_ldf(ct + sub * 4 + 1), hx_ldf(ct + sub * 4 + 2), hx_ldf(ct + sub * 4 + 3)};
+    float w = hx_ldf(ct + K), c = hx_ldf(ct + K + 1);
+    f32x4 ad = {0.f, 0.f, 0.f, 0.f};
+    float wd = 0.f, cd = 0.f;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      if (v == sub) ad = tot[v];
+      if (v == K / 4) {
+        wd = tot[v][0];
+        cd = tot[v][1];
+      }
+    }
+    av += ad;
+    w += wd;
+    c += cd;
+    sf_apply_row<K, MODE, OPT>(A, key, hpos, sub, av, w, c, lr_t);
+    return;
+  }
+  if (lane == 0) atomicOr(A.sync + 2, 4u);  // no origin before tile 0: impossible
+}
+
 template <int K, int MODE, int OPT>
 __global__ void __launch_bounds__(256) sf_tile_kernel(SfArgs A) {
   using T = SfCfg<K>;
@@ -126,6 +207,10 @@ __global__ void __launch_bounds__(256) sf_tile_kernel(SfArgs A) {
   __shared__ int hl[T::TP];   // head positions, ascending
   __shared__ int wcount[4];
   __shared__ int open_key_s, open_pos_s;
+  __shared__ float own_lead[T::C];
+  // publication tag of this step: its 1-based index (unique per training step; the host zeroes
+  // the flags whenever the step counter is rewritten)
+  const unsigned tag = (unsigned)(*A.step + A.step_off);
   const int tile = blockIdx.x, b0 = tile * T::TP;
   const int nloc = min(T::TP, A.n - b0);
   const int nch = (nloc + CH - 1) / CH;
@@ -215,8 +300,9 @@ __global__ void __launch_bounds__(256) sf_tile_kernel(SfArgs A) {
         break;
       }
     }
-    A.lead[(size_t)tile * T::RS + tid] = s;
-    if (tid == 0) A.tinfo[tile * 4] = any ? 0 : 1;
+    hx_stf(A.lead + (size_t)tile * T::RS + tid, s);      // handed off: write-through stores
+    own_lead[tid] = s;
+    if (tid == 0) hx_sti(A.tinfo + tile * 4, any ? 0 : 1);
   }
   // 3. finish every run headed in this tile
   const float lr_t = sf_lr_t<OPT>(A);
@@ -243,10 +329,11 @@ __global__ void __launch_bounds__(256) sf_tile_kernel(SfArgs A) {
       sf_apply_row<K, MODE, OPT>(A, key, b0 + hp, sub, a, w, c, lr_t);
     } else {
       float* ct = A.ctail + (size_t)tile * T::RS;
-      *reinterpret_cast<f32x4*>(ct + sub * 4) = a;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) hx_stf(ct + sub * 4 + j, a[j]);
       if (sub == 0) {
-        ct[K] = w;
-        ct[K + 1] = c;
+        hx_stf(ct + K, w);
+        hx_stf(ct + K + 1, c);
         open_key_s = key;
         open_pos_s = b0 + hp;
       }
@@ -254,70 +341,17 @@ __global__ void __launch_bounds__(256) sf_tile_kernel(SfArgs A) {
   }
   __syncthreads();
   if (tid == 0) {
-    A.tinfo[tile * 4 + 1] = open_key_s;
-    A.tinfo[tile * 4 + 2] = open_pos_s;
+    hx_sti(A.tinfo + tile * 4 + 1, open_key_s);
+    hx_sti(A.tinfo + tile * 4 + 2, open_pos_s);
   }
-}
-
-// One wave per tile: the tile's open run (if any) = ctail[t] + lead[t+1] + ... + lead[t_end],
-// t_end = the first following tile that holds a head.  The 64 lanes read 64 following tiles'
-// leads at once and the run total is a fixed butterfly over lanes (then window order), so long
-// runs (Criteo's 13 integer fields span every tile) cost one parallel read per 64 tiles instead
-// of a serial chain of dependent loads.  Fixed order: still bitwise reproducible.
-template <int K, int MODE, int OPT>
-__global__ void __launch_bounds__(256) sf_carry_kernel(SfArgs A, int ntiles) {
-  using T = SfCfg<K>;
-  constexpr int NV = T::RS / 4;  // f32x4 per lead row: a[K], w, c, pad, pad
-  const int t = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-  if (t >= ntiles) return;
-  const int key = A.tinfo[t * 4 + 1];
-  if (key < 0) return;  // wave-uniform
-  const int hpos = A.tinfo[t * 4 + 2];
-  f32x4 tot[NV];
-#pragma unroll
-  for (int v = 0; v < NV; ++v) tot[v] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int base = t + 1; base < ntiles; base += 64) {
-    const int t2 = base + lane;
-    const bool valid = t2 < ntiles;
-    const bool has_head = valid && !A.tinfo[t2 * 4];
-    const unsigned long long stop = __ballot(has_head);
-    const int last = stop ? __ffsll((long long)stop) - 1 : 63;  // last lane whose lead is included
-    f32x4 p[NV];
-#pragma unroll
-    for (int v = 0; v < NV; ++v) {
-      p[v] = (valid && lane <= last)
-                 ? *reinterpret_cast<const f32x4*>(A.lead + (size_t)t2 * T::RS + 4 * v)
-                 : f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int o = 32; o >= 1; o >>= 1) {
-        p[v][0] += __shfl_xor(p[v][0], o, 64);
-        p[v][1] += __shfl_xor(p[v][1], o, 64);
-        p[v][2] += __shfl_xor(p[v][2], o, 64);
-        p[v][3] += __shfl_xor(p[v][3], o, 64);
-      }
-      tot[v] += p[v];
-    }
-    if (stop) break;
-  }
-  const int sub = lane;
-  if (sub >= T::LPS) return;
-  const float* ct = A.ctail + (size_t)t * T::RS;
-  f32x4 av = *reinterpret_cast<const f32x4*>(ct + sub * 4);
-  float w = ct[K], c = ct[K + 1];
-  f32x4 ad = {0.f, 0.f, 0.f, 0.f};
-  float wd = 0.f, cd = 0.f;
-#pragma unroll
-  for (int v = 0; v < NV; ++v) {
-    if (v == sub) ad = tot[v];
-    if (v == K / 4) {
-      wd = tot[v][0];
-      cd = tot[v][1];
-    }
-  }
-  av += ad;
-  w += wd;
-  c += cd;
-  sf_apply_row<K, MODE, OPT>(A, key, hpos, sub, av, w, c, sf_lr_t<OPT>(A));
+  // 4. publish this tile, then close the run that continues into it (if any)
+  hx_drain();
+  __syncthreads();
+  if (tid == 0) hx_flag(A.flags + tile, tag);
+  // the leading piece continues an earlier run; it ends inside this tile (at the first head) or,
+  // for a headless tile, at the tile's end when the next tile starts a new id (or there is none)
+  const bool closes = nloc > 0 && skl[0] == prev_key && (nh > 0 || next_key != skl[nloc - 1]);
+  if (closes && wv == 0) sf_lookback<K, MODE, OPT>(A, tile, tag, own_lead, lr_t);
 }
 
 HFM_API int hfm_sparse_fused_tiles(int K, int n) {
@@ -330,7 +364,6 @@ static void sf_launch(const SfArgs& A, hipStream_t st) {
   using T = SfCfg<K>;
   const int tiles = (A.n + T::TP - 1) / T::TP;
   hipLaunchKernelGGL((sf_tile_kernel<K, MODE, OPT>), dim3(tiles), dim3(256), 0, st, A);
-  hipLaunchKernelGGL((sf_carry_kernel<K, MODE, OPT>), dim3((tiles + 3) / 4), dim3(256), 0, st, A, tiles);
 }
 
 template <int K>
@@ -355,6 +388,7 @@ static int sf_dispatch(int mode, int opt, const SfArgs& A, hipStream_t st) {
 // 2: gradient rows for the row-sharded owner exchange (gout[upos[u]])
 HFM_API int hfm_sparse_fused(int K, int mode, int opt, const SfArgs* A, hipStream_t st) {
   if (A->n <= 0) return 0;
+  if (!A->flags || !A->sync) return (int)hipErrorInvalidValue;
   int rc;
   switch (K) {
     case 4: rc = sf_dispatch<4>(mode, opt, *A, st); break;

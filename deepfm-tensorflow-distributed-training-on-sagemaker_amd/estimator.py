@@ -190,6 +190,7 @@ class Estimator:
                 dist.broadcast(t, src=0)
         if self.native:
             self.model._host_step = None      # step counter came from rank 0
+            self.model._reset_sync()          # hand-off flags are tagged with the step index
             self.model.refresh_shadows()      # bf16 / fp8 weight copies of the broadcast params
         if not self.native:
             gs = torch.tensor([int(self.model.global_step)], dtype=torch.int64)

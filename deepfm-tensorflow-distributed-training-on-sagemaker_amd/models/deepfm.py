@@ -419,6 +419,11 @@ class NativeDeepFM:
         self.sf_ctail = torch.zeros(nt, K + 4, **f32)
         self.sf_lead = torch.zeros(nt, K + 4, **f32)
         self.sf_tinfo = torch.zeros(nt, 4, **i32)
+        # in-launch hand-off words of the sparse tile kernel (csrc/kernels/sync.h): per-tile
+        # publication flags (tagged with the step index) and error bits; zeroed whenever the
+        # step counter is rewritten (_reset_sync)
+        self.sf_flags = torch.zeros(nt, **i32)
+        self.sf_sync = torch.zeros(4, **i32)
         self._fsort = None
         self._fsort_next = None
         # sorted-slot sets: set c holds the sort of the batch this step trains, set 1 - c receives
@@ -482,7 +487,9 @@ class NativeDeepFM:
         jobs.append(SlabJob(self.loss_sum.data_ptr(), pw + 4 * (Lp + 1), 1, self.nhead, Lp + 2, 1, 1, 1.0))
         nb = 0
         for j in jobs:                       # finalize_kernel block mapping
-            j.lanes = 8 if j.nslab >= 64 else 2
+            # slab-lanes per output: each thread sums <= 8 slabs, all its loads in flight at once
+            # (the 512 head-partial rows of the 1-block jobs were 64 dependent-load rounds)
+            j.lanes = 64 if j.nslab >= 256 else (8 if j.nslab >= 64 else 4)
             j.chunk0 = nb
             nb += (j.n + 256 // j.lanes - 1) // (256 // j.lanes)
         self._slab_blocks = nb
@@ -654,6 +661,12 @@ class NativeDeepFM:
     def dense_tf_params(self, flat: Optional[torch.Tensor] = None) -> "OrderedDict[str, torch.Tensor]":
         flat = self.p if flat is None else flat
         return OrderedDict((n, self._native_to_tf(n, flat)) for n in self.dense_segs)
+
+    def _reset_sync(self):
+        """In-launch hand-off flags carry the step index as their tag: a step counter moved
+        backwards (checkpoint restore) must not meet flags of its future."""
+        if hasattr(self, "sf_flags"):
+            self.sf_flags.zero_()
 
     def refresh_shadows(self):
         KN.shadow_refresh(self.p, self.P, self._shadow_dev, self._nshadow)
@@ -881,6 +894,10 @@ class NativeDeepFM:
         if any(fs is not None and int(fs.err.item()) != 0 for fs in (self._fsort, self._fsort_next)):
             raise RuntimeError("an id lies outside its field's declared range (field_ranges): "
                                "the per-field sort is invalid for this data")
+        e = int(self.sf_sync[2].item())
+        if e != 0:
+            raise RuntimeError(f"sparse backward hand-off failed (error bits {e:#x}): a look-back "
+                               "timed out or read an inconsistent tile publication")
         if self.shx is not None and self.shx.error() != 0:
             raise RuntimeError(f"row-sharded exchange: a rank sent more than capacity={self.shx.C} "
                                "unique ids to one owner (raise the capacity)")
@@ -900,6 +917,7 @@ class NativeDeepFM:
         A.step = self.step.data_ptr()
         A.ldv, A.ldw = KN._ld(self.tv, self.tw)
         A.step_off = 0 if self._dense_early else 1
+        A.flags, A.sync = self.sf_flags.data_ptr(), self.sf_sync.data_ptr()
         return A
 
     def _sparse_backward(self, B: int, idx, tv, presorted: bool = False):
@@ -1375,6 +1393,7 @@ class NativeDeepFM:
                                          f"model {tuple(cur[k].shape)}")
                     cur[k].copy_(v.to(cur[k].device, cur[k].dtype))
         self.refresh_shadows()
+        self._reset_sync()
         self._graphs = {}
 
     def tf_variables(self, tables=None) -> "OrderedDict[str, torch.Tensor]":
@@ -1433,4 +1452,5 @@ class NativeDeepFM:
             if "global_step" in tv:
                 self.step.fill_(int(torch.as_tensor(tv["global_step"])))
                 self._host_step = None
+                self._reset_sync()
         self._graphs = {}

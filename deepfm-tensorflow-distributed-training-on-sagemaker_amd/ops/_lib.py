@@ -84,7 +84,8 @@ class SfArgs(C.Structure):
                 ("tv", c_void_p), ("tw", c_void_p), ("s0v", c_void_p), ("s1v", c_void_p),
                 ("s0w", c_void_p), ("s1w", c_void_p), ("Gv", c_void_p), ("Gw", c_void_p),
                 ("h", OptHyper), ("step", c_void_p), ("ldv", c_long), ("ldw", c_long),
-                ("sid", c_void_p), ("upos", c_void_p), ("gout", c_void_p), ("step_off", c_int)]
+                ("sid", c_void_p), ("upos", c_void_p), ("gout", c_void_p), ("step_off", c_int),
+                ("flags", c_void_p), ("sync", c_void_p)]
 
 
 class ShApplyArgs(C.Structure):
