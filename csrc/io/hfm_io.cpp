@@ -466,8 +466,10 @@ struct Loader {
     return nullptr;
   }
 
-  // returns rows written (B, or < B for the final partial batch), 0 at end, -1 error
-  int next(float* lab, int64_t* ids, float* vals) {
+  // returns rows written (B, or < B for the final partial batch), 0 at end, -1 error.
+  // ids32 != null: ids are narrowed to int32 (the device id type) while copying, straight into
+  // the caller's (pinned) buffer; an id outside [0, 2^31) is an error.
+  int next(float* lab, int64_t* ids, float* vals, int32_t* ids32 = nullptr) {
     int got = 0;
     while (got < B) {
       if (!cur || cur_off >= cur->n) {
@@ -480,7 +482,23 @@ struct Loader {
       }
       int k = std::min(B - got, cur->n - cur_off);
       memcpy(lab + got, cur->label.data() + cur_off, k * 4);
-      memcpy(ids + (size_t)got * F, cur->ids.data() + (size_t)cur_off * F, (size_t)k * F * 8);
+      if (ids32) {
+        const int64_t* src = cur->ids.data() + (size_t)cur_off * F;
+        int32_t* dst = ids32 + (size_t)got * F;
+        const size_t m = (size_t)k * F;
+        int64_t bad = 0;
+        for (size_t i = 0; i < m; ++i) {
+          const int64_t v = src[i];
+          bad |= v >> 31;  // non-zero for negatives and ids >= 2^31
+          dst[i] = (int32_t)v;
+        }
+        if (bad) {
+          err = "feature id outside [0, 2^31) for the int32 device path";
+          return -1;
+        }
+      } else {
+        memcpy(ids + (size_t)got * F, cur->ids.data() + (size_t)cur_off * F, (size_t)k * F * 8);
+      }
       memcpy(vals + (size_t)got * F, cur->vals.data() + (size_t)cur_off * F, (size_t)k * F * 4);
       got += k;
       cur_off += k;
@@ -525,6 +543,13 @@ HFMIO_API void* hfmio_loader_create(const char** paths, int npaths, int format, 
 HFMIO_API int hfmio_loader_next(void* h, float* labels, int64_t* ids, float* vals) {
   auto* L = (Loader*)h;
   int r = L->next(labels, ids, vals);
+  if (r < 0) set_err(L->err);
+  return r;
+}
+
+HFMIO_API int hfmio_loader_next32(void* h, float* labels, int32_t* ids, float* vals) {
+  auto* L = (Loader*)h;
+  int r = L->next(labels, nullptr, vals, ids);
   if (r < 0) set_err(L->err);
   return r;
 }

@@ -56,10 +56,12 @@ def build_pipelines(cfg: RunConfig, est: Estimator):
     fmt = cfg.data_format
     shard = shard_spec(world, rank, local_rank, cfg.worker_per_host, len(cfg.hosts),
                        cfg.enable_s3_shard, bool(cfg.pipe_mode), cfg.enable_data_multi_path)
-    dev = est.device if (est.native and cfg.cache_data) else None
-    id_dtype = torch.int64
-    common = dict(fmt=fmt, seed=cfg.seed, threads=max(1, min(8, cfg.num_threads)), device=dev,
-                  id_dtype=id_dtype)
+    # native path: batches go to the GPU through pinned buffers + a copy stream, ids as int32 (the
+    # device id type: no staging cast per step), and the first epoch stays HBM-resident (cache())
+    dev = est.device if est.native else None
+    id_dtype = torch.int32 if est.native else torch.int64
+    common = dict(fmt=fmt, seed=cfg.seed, threads=max(1, min(os.cpu_count() or 1, cfg.num_threads)),
+                  device=dev, id_dtype=id_dtype)
     if cfg.pipe_mode:
         ch = _channels()
         tr_ch = cfg.training_channel_name or (ch[1 + local_rank] if len(ch) > 1 + local_rank else "training")
@@ -89,14 +91,17 @@ def build_pipelines(cfg: RunConfig, est: Estimator):
     def tr(epochs):
         return cache_tr
     va = lambda: InputPipeline(va_files, cfg.field_size, cfg.batch_size, 1, shard=(world, rank),
-                               shuffle_files=False, **{**common, "device": None})
+                               shuffle_files=False, **common)
     te = lambda: InputPipeline(te_files, cfg.field_size, cfg.batch_size, 1, shard=(1, 0),
-                               shuffle_files=False, drop_remainder=False, **{**common, "device": None})
+                               shuffle_files=False, drop_remainder=False, **common)
     return tr, va, te
 
 
 def run(cfg: RunConfig) -> dict:
     _init_dist(cfg)
+    # CPU threading (reference C25: intra/inter-op threads = num_cpus, PS:405-432): torch's CPU
+    # pool for the golden path and host-side tensor work; loader threads use the same budget
+    torch.set_num_threads(max(1, cfg.num_threads))
     rank = dist.get_rank() if dist.is_initialized() else 0
     if rank == 0:
         print(sys.argv, flush=True)
@@ -114,7 +119,32 @@ def run(cfg: RunConfig) -> dict:
     result = {}
     if cfg.task_type == "train":
         max_steps = cfg.max_steps or None
-        if cfg.pipe_mode:
+        if cfg.schedule == "ps" and not cfg.pipe_mode:
+            # PS recipe: train_and_evaluate(TrainSpec(all epochs), EvalSpec(start delay, throttle))
+            from .estimator import EvalSpec, TrainSpec, train_and_evaluate
+            pipe = tr(1)
+            first, skip = est.epoch, est.epoch_batch
+            if first >= cfg.num_epochs:
+                first, skip = 0, 0
+
+            def all_epochs():
+                for epoch in range(first, cfg.num_epochs):
+                    est.epoch, est.epoch_batch = epoch, (skip if epoch == first else 0)
+                    view = _EpochView(pipe, epoch, est.epoch_batch)
+                    est._enforce_equal_steps(view)
+                    yield from view
+                    est.adopt_field_ranges(pipe)
+                est.epoch, est.epoch_batch = cfg.num_epochs, 0
+
+            class _Run:                  # the whole run as one batch source (cache flag visible)
+                countable = True
+
+                def __iter__(self):
+                    return all_epochs()
+            _Run.pipe = pipe
+            result = train_and_evaluate(est, TrainSpec(_Run, max_steps),
+                                        EvalSpec(va, None, cfg.eval_start_delay_secs, cfg.eval_throttle_secs))
+        elif cfg.pipe_mode:
             pipe = tr(cfg.num_epochs)
             est.train(pipe, max_steps, eval_fn=lambda: est.evaluate(va()))
             est.save()
@@ -134,6 +164,7 @@ def run(cfg: RunConfig) -> dict:
                 est.train(_EpochView(pipe, epoch, est.epoch_batch), max_steps,
                           eval_fn=lambda: est.evaluate(va()))
                 est.epoch, est.epoch_batch = epoch + 1, 0
+                est.adopt_field_ranges(pipe)
                 result = est.evaluate(va())
                 if max_steps is not None and est.global_step >= max_steps:
                     break

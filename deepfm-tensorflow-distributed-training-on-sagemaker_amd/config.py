@@ -95,6 +95,16 @@ _DEFS = [
     ("save_checkpoints_secs", int, 600, "checkpoint every N seconds (TF Estimator default 600)"),
     ("keep_checkpoint_max", int, 5, "checkpoints to keep (TF default 5)"),
     ("eval_every_steps", int, 0, "evaluate every N steps during train (0: per epoch, rank-parallel)"),
+    ("schedule", str, "hvd", "hvd: per-epoch train + evaluate (HVD:390-394) | ps: train_and_evaluate with "
+     "throttled evaluation (PS:439-442)"),
+    ("eval_start_delay_secs", float, 1000.0, "ps schedule: no evaluation before this (EvalSpec default "
+     "of the reference, PS:441)"),
+    ("eval_throttle_secs", float, 1200.0, "ps schedule: at most one evaluation per this many seconds "
+     "(PS:441)"),
+    ("time_check_steps", int, 20, "steps between the (rank-agreed) checks of time-based triggers"),
+    ("graph_steps", int, 8, "consecutive steps over the HBM-cached epoch captured per HIP graph"),
+    ("field_sizes", str, "", "csv per-field vocabulary sizes (fields own consecutive id ranges): "
+     "enables the per-field slot sort; empty: derived from the first cached epoch when possible"),
     ("pred_path", str, "", "predictions output file (default <val_data_dir>/pred.txt, Q9)"),
     ("export_tf_bundle", _str2bool, True, "also write a TF1 tensor_bundle checkpoint on export"),
     ("metrics_file", str, "", "JSONL metrics output (default <model_dir>/metrics.jsonl)"),
@@ -154,6 +164,12 @@ class RunConfig:
     save_checkpoints_secs: int = 600
     keep_checkpoint_max: int = 5
     eval_every_steps: int = 0
+    schedule: str = "hvd"
+    eval_start_delay_secs: float = 1000.0
+    eval_throttle_secs: float = 1200.0
+    time_check_steps: int = 20
+    graph_steps: int = 8
+    field_sizes: str = ""
     pred_path: str = ""
     export_tf_bundle: bool = True
     metrics_file: str = ""
@@ -201,6 +217,12 @@ class RunConfig:
             raise ValueError(f"unknown sparse_update {self.sparse_update!r}")
         if self.mlp_dtype not in ("bf16", "fp8"):
             raise ValueError(f"unknown mlp_dtype {self.mlp_dtype!r} (bf16 | fp8)")
+        if self.schedule not in ("hvd", "ps"):
+            raise ValueError(f"unknown schedule {self.schedule!r} (hvd | ps)")
+        if self.field_sizes:
+            fs = [int(x) for x in self.field_sizes.split(",") if x.strip()]
+            if len(fs) != self.field_size or sum(fs) > self.feature_size or min(fs) < 1:
+                raise ValueError("field_sizes: one positive size per field, summing to <= feature_size")
         if self.embedding_mode not in ("auto", "replicated", "sharded"):
             raise ValueError(f"unknown embedding_mode {self.embedding_mode!r}")
         kp = self.keep_probs

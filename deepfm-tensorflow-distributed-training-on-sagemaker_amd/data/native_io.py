@@ -41,6 +41,8 @@ def lib():
             L.hfmio_loader_create.restype = vp
             L.hfmio_loader_next.argtypes = [vp, vp, vp, vp]
             L.hfmio_loader_next.restype = ci
+            L.hfmio_loader_next32.argtypes = [vp, vp, vp, vp]
+            L.hfmio_loader_next32.restype = ci
             L.hfmio_loader_destroy.argtypes = [vp]
             L.hfmio_write_examples.argtypes = [C.c_char_p, vp, vp, vp, cl, ci, ci]
             L.hfmio_write_examples.restype = ci
@@ -109,6 +111,14 @@ def count_records(path: str, fmt: int = FMT_TFRECORD, verify: bool = True) -> in
     return n
 
 
+def _addr(a) -> int:
+    return a.ctypes.data if isinstance(a, np.ndarray) else a.data_ptr()
+
+
+def _dtype_of(a) -> int:
+    return a.dtype.itemsize if isinstance(a, np.ndarray) else a.element_size()
+
+
 class NativeLoader:
     """Iterator of (labels f32[B], ids i64[B,F], vals f32[B,F]) numpy batches.
 
@@ -128,11 +138,13 @@ class NativeLoader:
                                             record_shard[1], 1 if verify_crc else 0, queue_depth)
         self._done = False
 
-    def next_into(self, labels: np.ndarray, ids: np.ndarray, vals: np.ndarray) -> int:
-        """Fill caller buffers (e.g. pinned host memory); returns rows (0 at end)."""
+    def next_into(self, labels, ids, vals) -> int:
+        """Fill caller buffers (numpy arrays or pinned CPU torch tensors); ``ids`` int64, or int32
+        (narrowed in the loader thread, checked to fit); returns rows (0 at end)."""
         if self._done:
             return 0
-        r = lib().hfmio_loader_next(self._h, labels.ctypes.data, ids.ctypes.data, vals.ctypes.data)
+        fn = lib().hfmio_loader_next32 if _dtype_of(ids) == 4 else lib().hfmio_loader_next
+        r = fn(self._h, _addr(labels), _addr(ids), _addr(vals))
         if r < 0:
             raise IOError(_err())
         if r == 0:

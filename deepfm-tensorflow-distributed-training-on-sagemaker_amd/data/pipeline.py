@@ -102,6 +102,70 @@ def next_pipe_stream(channel: str) -> str:
     return pipe_channel_path(channel, k)
 
 
+class _DeviceFeeder:
+    """Loader batches -> device batches: the C++ loader threads decode straight into a ring of
+    pinned host buffers (ids narrowed to the device id type there), and each buffer goes to the
+    GPU with an async copy on a dedicated copy stream.  The compute stream waits on the copy's
+    event, never the host; a pinned buffer is refilled only after its previous copy finished
+    (3-deep ring: decode of batch i+2, copy of i+1 and compute of i overlap)."""
+
+    def __init__(self, loader, F: int, B: int, device, id_dtype, depth: int = 3):
+        self.loader, self.F, self.B, self.device, self.id_dtype = loader, F, B, device, id_dtype
+        self.copy = torch.cuda.Stream(device)
+        pin = dict(pin_memory=True)
+        self.ring = [(torch.empty(B, dtype=torch.float32, **pin),
+                      torch.empty(B, F, dtype=id_dtype, **pin),
+                      torch.empty(B, F, dtype=torch.float32, **pin)) for _ in range(depth)]
+        self.done = [None] * depth
+        self.h2d_s = 0.0         # host time spent issuing copies (the copies themselves are async)
+
+    def __iter__(self):
+        import time
+        k = 0
+        compute = torch.cuda.current_stream(self.device)
+        while True:
+            slot = k % len(self.ring)
+            if self.done[slot] is not None:
+                self.done[slot].synchronize()          # this pinned buffer's last copy is over
+            lab, ids, vals = self.ring[slot]
+            r = self.loader.next_into(lab, ids, vals)
+            if r == 0:
+                return
+            t0 = time.perf_counter()
+            d_ids = torch.empty(r, self.F, dtype=self.id_dtype, device=self.device)
+            d_vals = torch.empty(r, self.F, dtype=torch.float32, device=self.device)
+            d_lab = torch.empty(r, dtype=torch.float32, device=self.device)
+            self.copy.wait_stream(compute)             # the new buffers are free on the copy stream
+            with torch.cuda.stream(self.copy):
+                d_ids.copy_(ids[:r], non_blocking=True)
+                d_vals.copy_(vals[:r], non_blocking=True)
+                d_lab.copy_(lab[:r], non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(self.copy)
+            self.done[slot] = ev
+            compute.wait_event(ev)
+            self.h2d_s += time.perf_counter() - t0
+            k += 1
+            yield d_ids, d_vals, d_lab
+
+
+def derive_field_ranges(fmin: torch.Tensor, fmax: torch.Tensor, V: int):
+    """Per-field id ranges from the per-field min / max ids seen in the data: [lo_f, hi_f) with
+    lo_0 = 0, hi_f = lo_{f+1} = min_{f+1}, hi_last = V (gaps between fields are covered, so any id
+    a field can take between its neighbours' ranges stays valid).  None unless the observed
+    intervals are disjoint and increasing in field order (then the per-field sort cannot apply)."""
+    mn, mx = [int(x) for x in fmin.tolist()], [int(x) for x in fmax.tolist()]
+    F = len(mn)
+    for f in range(F - 1):
+        if not mx[f] < mn[f + 1]:
+            return None
+    if mn[0] < 0 or mx[-1] >= V:
+        return None
+    lo = [0] + mn[1:]
+    hi = mn[1:] + [V]
+    return list(zip(lo, hi))
+
+
 class InputPipeline:
     """Epoch-aware batch source (the reference's ``input_fn``, PS:76-133 / HVD:74-133)."""
 
@@ -127,6 +191,9 @@ class InputPipeline:
         self.id_dtype = id_dtype
         self._cached: Optional[List[Tuple[torch.Tensor, ...]]] = None
         self.max_batches: Optional[int] = None   # equal-steps enforcement across ranks
+        self.from_cache = False                  # the epoch being iterated replays the cache
+        self.h2d_s = 0.0                          # host time issuing H2D copies (last epoch)
+        self._fmin = self._fmax = None           # per-field id min / max over the cached epoch
 
     @property
     def countable(self) -> bool:
@@ -154,7 +221,7 @@ class InputPipeline:
         t = (torch.from_numpy(np.array(ids)).to(self.id_dtype), torch.from_numpy(np.array(vals)),
              torch.from_numpy(np.array(lab)))
         if self.device is not None:
-            t = tuple(x.to(self.device, non_blocking=True) for x in t)
+            t = tuple(x.to(self.device) for x in t)
         return t
 
     def iter_epoch(self, epoch: int, skip: int = 0) -> Iterator[Tuple[torch.Tensor, torch.Tensor, torch.Tensor]]:
@@ -163,29 +230,51 @@ class InputPipeline:
         ones too (it is the epoch's length)."""
         if self.cache and self._cached is not None:
             end = self.max_batches if self.max_batches else len(self._cached)
+            self.from_cache = True
             yield from self._cached[skip:end]
             return
+        self.from_cache = False
         plan = self.epoch_plan(epoch)
         loader = NativeLoader(plan.files, self.F, self.B, self.fmt, self.drop_remainder,
                               self.threads, plan.record_shard)
         store = [] if (self.cache and skip == 0) else None
+        on_gpu = self.device is not None and torch.device(self.device).type == "cuda"
+        src = (_DeviceFeeder(loader, self.F, self.B, torch.device(self.device), self.id_dtype)
+               if on_gpu else None)
         k = 0
         try:
-            for lab, ids, vals in loader:
+            for item in (src if src is not None else loader):
                 if self.max_batches is not None and k >= self.max_batches:
                     break
                 if k < skip:
                     k += 1
                     continue
-                t = self._to_tensors(lab, ids, vals)
+                t = item if src is not None else self._to_tensors(*item)
                 if store is not None:
                     store.append(t)
+                    ids = t[0]
+                    mn, mx = ids.amin(0), ids.amax(0)
+                    self._fmin = mn if self._fmin is None else torch.minimum(self._fmin, mn)
+                    self._fmax = mx if self._fmax is None else torch.maximum(self._fmax, mx)
                 k += 1
                 yield t
         finally:
             loader.close()
+            if src is not None:
+                self.h2d_s = src.h2d_s
         if store is not None:
             self._cached = store
+
+    def field_ranges(self, V: int):
+        """Per-field id ranges derived from the cached epoch (None before it is cached, or when
+        the fields' ids are not disjoint and increasing)."""
+        if self._fmin is None:
+            return None
+        return derive_field_ranges(self._fmin.cpu(), self._fmax.cpu(), V)
+
+    @property
+    def cached_batches(self) -> int:
+        return 0 if self._cached is None else len(self._cached)
 
     def __iter__(self):
         for e in range(self.num_epochs):

@@ -35,6 +35,7 @@ from .ops.metrics import auc_from_hist, hist_torch
 from .utils.fault import Watchdog, maybe_inject_fault
 from .utils.logging import MetricsLogger, StepTimer
 from .utils.profiling import StepWindow
+from .utils.profiling import range as prof_range
 
 
 def _dist_on() -> bool:
@@ -82,7 +83,10 @@ class Estimator:
             self._ctl = dist.new_group(backend="gloo")
         self.comm = None
         if self.native:
-            from .models.deepfm import NativeDeepFM
+            from .models.deepfm import NativeDeepFM, field_ranges_from_sizes
+            ranges = None
+            if cfg.field_sizes:
+                ranges = field_ranges_from_sizes([int(x) for x in cfg.field_sizes.split(",") if x.strip()])
             if self.world > 1:
                 from .parallel.dist import Comm
                 mode = cfg.embedding_mode
@@ -95,7 +99,7 @@ class Estimator:
                                       sparse_update=cfg.sparse_update, seed=cfg.seed,
                                       batch_size=cfg.batch_size, device=self.device, comm=self.comm,
                                       batch_norm=cfg.batch_norm, batch_norm_decay=cfg.batch_norm_decay,
-                                      mlp_dtype=cfg.mlp_dtype)
+                                      mlp_dtype=cfg.mlp_dtype, field_ranges=ranges)
         else:
             from .models.reference import GoldenDeepFM
             self.model = GoldenDeepFM(cfg.feature_size, cfg.field_size, cfg.embedding_size, cfg.layers,
@@ -146,9 +150,12 @@ class Estimator:
     def save(self) -> Optional[str]:
         if self.ckpt is None:
             return None
+        t0 = time.perf_counter()
         if self.native:
             torch.cuda.synchronize(self.device)
-        path = self.ckpt.save(self.global_step, self._state(), self._meta())
+        with prof_range("checkpoint"):
+            path = self.ckpt.save(self.global_step, self._state(), self._meta())
+        self.timer.add("ckpt", time.perf_counter() - t0)
         self._last_save_t = time.time()
         self.log.info(f"Saving checkpoints for {self.global_step} into {path}.")
         return path
@@ -273,68 +280,143 @@ class Estimator:
             yield b
 
     # ------------------------------------------------------------------ train
+    def _agreed_due(self, due: bool) -> bool:
+        """A time-based decision (checkpoint every N secs, throttled eval) taken identically on
+        every rank: rank 0's clock decides and the bit travels over the host control group, so
+        no rank enters a collective save / evaluation alone."""
+        if self.world == 1:
+            return due
+        t = torch.tensor([1 if due else 0], dtype=torch.int32)
+        dist.broadcast(t, src=0, group=self._ctl)
+        return bool(t.item())
+
+    def _next(self, it):
+        t0 = time.perf_counter()
+        with prof_range("data_wait"):
+            b = next(it, None)
+        self.timer.add("data_wait", time.perf_counter() - t0)
+        return b
+
     def train(self, batches: Iterable, max_steps: Optional[int] = None,
-              eval_fn: Optional[Callable[[], dict]] = None) -> int:
+              eval_fn: Optional[Callable[[], dict]] = None,
+              eval_due: Optional[Callable[[], bool]] = None) -> int:
+        """Train over ``batches`` (device or host tensors).  The native path keeps one batch of
+        look-ahead: a resident next batch has its slot sort / routing computed during the current
+        step; batches replayed from the HBM cache run as captured graphs, ``graph_steps`` of them
+        per graph; one-off streamed batches are staged into the static input buffers and replay
+        one graph.  Host timers (data wait, H2D, step enqueue, checkpoint, eval) go to the metrics
+        log; roctx ranges mark the same phases.  ``eval_due`` (PS schedule): polled at the agreed
+        decision steps, evaluates when it returns True."""
         cfg = self.cfg
         if hasattr(batches, "local_records"):
             self._enforce_equal_steps(batches)
+        src = batches
         if self.world > 1 and not getattr(batches, "countable", True):
             batches = self._agreed_batches(batches)
         t_log = time.time()
         n_log = 0
         start_step = self.global_step
         use_graph = cfg.graph and self.native
+        gsteps = max(1, int(getattr(cfg, "graph_steps", 1)))
+        check_every = max(1, int(getattr(cfg, "time_check_steps", 20)))
         wd = Watchdog(cfg.watchdog_secs, self.rank).start()
         window = StepWindow()
-        t_wait = time.time()
-        for ids, vals, labels in batches:
-            self.timer.add("data_wait", time.time() - t_wait)
+        it = iter(batches)
+        cur = self._next(it)
+        while cur is not None:
             if max_steps is not None and self.global_step >= max_steps:
                 break
-            t0 = time.time()
-            B = ids.shape[0]
+            from_cache = bool(getattr(src, "from_cache", False)) or bool(
+                getattr(getattr(src, "pipe", None), "from_cache", False))
+            run = [cur]
+            nxt = self._next(it)
+            if self.native and use_graph and from_cache and gsteps > 1:
+                lim = gsteps if max_steps is None else min(gsteps, max_steps - self.global_step)
+                while len(run) < lim and nxt is not None:
+                    run.append(nxt)
+                    nxt = self._next(it)
+            t0 = time.perf_counter()
+            B = int(run[0][0].shape[0])
             if self.native:
-                self.model.train_step(ids.to(self.device, non_blocking=True),
-                                      vals.to(self.device, non_blocking=True),
-                                      labels.to(self.device, non_blocking=True), use_graph=use_graph)
+                if not run[0][0].is_cuda:
+                    t1 = time.perf_counter()
+                    with prof_range("h2d"):
+                        run = [tuple(x.to(self.device, non_blocking=True) for x in b) for b in run]
+                    self.timer.add("h2d", time.perf_counter() - t1)
+                nxt_ids = nxt[0] if (nxt is not None and nxt[0].is_cuda) else None
+                with prof_range("step"):
+                    if len(run) > 1:
+                        self.model.train_steps(run, next_ids=nxt_ids)
+                    else:
+                        ids, vals, labels = run[0]
+                        # replayed cache batches: bound in place (one graph per batch); one-off
+                        # streamed batches: staged into the static buffers (one shared graph)
+                        self.model.train_step(ids, vals, labels, use_graph=use_graph,
+                                              next_ids=nxt_ids if from_cache else None,
+                                              stage=not from_cache)
                 if cfg.debug_sync:
                     torch.cuda.synchronize(self.device)
                     self._nan_check()
             else:
-                self.model.train_step(ids, vals, labels, grad_sync=self._golden_grad_sync)
-            self.timer.add("step_enqueue", time.time() - t0)
-            self.epoch_batch += 1
-            n_log += B
+                for ids, vals, labels in run:
+                    self.model.train_step(ids, vals, labels, grad_sync=self._golden_grad_sync)
+            self.timer.add("step_enqueue", time.perf_counter() - t0)
+            prev = self.global_step - len(run)
+            self.epoch_batch += len(run)
+            n_log += B * len(run)
             step = self.global_step
             wd.beat(step)
             window.step(step)
             maybe_inject_fault(step, self.rank)
-            if cfg.log_steps and step % cfg.log_steps == 0:
+            crossed = lambda every: bool(every) and step // every > prev // every  # noqa: E731
+            if crossed(cfg.log_steps):
                 if self.native:
                     torch.cuda.synchronize(self.device)
                 dt = max(1e-9, time.time() - t_log)
                 loss = self.model.loss_value(B) if self.native else self.model.last_loss
                 sps = n_log / dt
                 self.log.info(f"loss = {loss:.6f}, step = {step} ({dt:.3f} sec)")
-                self.log.info(f"global_step/sec: {cfg.log_steps / dt:.4g}")
+                self.log.info(f"global_step/sec: {n_log / B / dt:.4g}")
                 self.log.log("train", step=step, loss=loss, samples_per_sec_rank=sps,
                              samples_per_sec_job=sps * self.world, **self.timer.summary(),
                              comm_bytes=getattr(self.comm, "bytes_sent", 0))
-                self._summary("train", step, {"loss": loss, "global_step/sec": cfg.log_steps / dt,
+                self._summary("train", step, {"loss": loss, "global_step/sec": n_log / B / dt,
                                               "examples/sec": sps * self.world})
                 t_log, n_log = time.time(), 0
-            if self.ckpt is not None and (
-                    (cfg.save_checkpoints_steps and step % cfg.save_checkpoints_steps == 0) or
-                    (not cfg.save_checkpoints_steps and cfg.save_checkpoints_secs and
-                     time.time() - self._last_save_t >= cfg.save_checkpoints_secs)):
-                self.save()
-            if eval_fn is not None and cfg.eval_every_steps and step % cfg.eval_every_steps == 0:
+            if self.ckpt is not None:
+                due = crossed(cfg.save_checkpoints_steps)
+                if not cfg.save_checkpoints_steps and cfg.save_checkpoints_secs and crossed(check_every):
+                    due = self._agreed_due(time.time() - self._last_save_t >= cfg.save_checkpoints_secs)
+                if due:
+                    self.save()
+            if eval_fn is not None and crossed(cfg.eval_every_steps):
                 eval_fn()
-            t_wait = time.time()
+            elif eval_due is not None and crossed(check_every) and self._agreed_due(eval_due()):
+                eval_fn_ps = getattr(eval_due, "run", None)
+                if eval_fn_ps is not None:
+                    eval_fn_ps()
+            cur = nxt
         if self.native:
             torch.cuda.synchronize(self.device)
         wd.stop()
         return self.global_step - start_step
+
+    def adopt_field_ranges(self, pipeline) -> bool:
+        """After the first epoch was cached: per-field id ranges derived from it switch the slot
+        sort to the per-field LDS sort (when the fields' ids are disjoint and increasing; with
+        --field_sizes they are known from the start).  Returns True if the model took them."""
+        if not self.native or self.model.field_ranges is not None or self.model.sharded:
+            return False
+        r = pipeline.field_ranges(self.cfg.feature_size) if hasattr(pipeline, "field_ranges") else None
+        if self.world > 1:   # every rank must take the same decision (and the same ranges)
+            objs = [r]
+            dist.broadcast_object_list(objs, src=0, group=self._ctl)
+            r = objs[0]
+        if r is None:
+            return False
+        self.model.set_field_ranges(r)
+        self.log.info("per-field id ranges derived from the cached epoch: per-field slot sort on")
+        return True
 
     def _nan_check(self):
         for name, t in (("fm_v", self.model.tv), ("dense", self.model.p)):
@@ -343,6 +425,13 @@ class Estimator:
 
     # ------------------------------------------------------------------ evaluate / predict
     def evaluate(self, batches: Iterable, steps: Optional[int] = None) -> dict:
+        t0 = time.perf_counter()
+        with prof_range("eval"):
+            res = self._evaluate(batches, steps)
+        self.timer.add("eval", time.perf_counter() - t0)
+        return res
+
+    def _evaluate(self, batches: Iterable, steps: Optional[int] = None) -> dict:
         dev = self.device if self.native else torch.device("cpu")
         hist = torch.zeros(2, 201, dtype=torch.int64, device=dev)
         loss_sum = torch.zeros(1, dtype=torch.float64, device=dev)
@@ -458,18 +547,23 @@ class Estimator:
 
 
 def train_and_evaluate(est: Estimator, train_spec: TrainSpec, eval_spec: EvalSpec) -> dict:
-    """tf.estimator.train_and_evaluate (PS:439-442): train; evaluate after checkpoints once
-    start_delay_secs has passed, at most every throttle_secs; final evaluation at the end."""
+    """tf.estimator.train_and_evaluate (PS:439-442): train; once ``start_delay_secs`` have passed,
+    evaluate at most every ``throttle_secs`` -- each time on a freshly saved checkpoint, like
+    TF's evaluator that evaluates the latest checkpoint -- and a final evaluation at the end.
+    Time decisions are rank 0's and broadcast, so all ranks evaluate together."""
     t0 = time.time()
-    last = {"t": 0.0}
+    last = {"t": None}
 
-    def maybe_eval():
+    def due() -> bool:
         now = time.time()
-        if now - t0 >= eval_spec.start_delay_secs and now - last["t"] >= eval_spec.throttle_secs:
-            last["t"] = now
-            return est.evaluate(eval_spec.input_fn(), eval_spec.steps)
-        return None
+        return (now - t0 >= eval_spec.start_delay_secs and
+                (last["t"] is None or now - last["t"] >= eval_spec.throttle_secs))
 
-    est.train(train_spec.input_fn(), train_spec.max_steps, eval_fn=maybe_eval)
+    def run():
+        last["t"] = time.time()
+        est.save()
+        est.evaluate(eval_spec.input_fn(), eval_spec.steps)
+    due.run = run
+    est.train(train_spec.input_fn(), train_spec.max_steps, eval_due=due)
     est.save()
     return est.evaluate(eval_spec.input_fn(), eval_spec.steps)

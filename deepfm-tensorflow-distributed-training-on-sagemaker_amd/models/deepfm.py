@@ -434,17 +434,7 @@ class NativeDeepFM:
         self._ss_key = [None, None]
         self._ss_cur = 0
         self._sort_plan = None
-        if self.field_ranges is not None:
-            # the sort runs on a side stream next to the step in both cases, and every sort
-            # workgroup holds 148 KB of LDS: one workgroup per field on one GPU (0.160 ms/step vs
-            # 0.162 / 0.169 / 0.179 with 2 / 4 / 16 per field); 4 per field for the next batch's
-            # routing on the sharded step (0.198 ms vs 0.206 with 16; HIPFM_FSORT_PB overrides)
-            pb = os.environ.get("HIPFM_FSORT_PB")
-            self._fsort = KN.FieldSort(self.field_ranges, min(M, KN.field_sort_max_rows()), dev,
-                                       max_pb=int(pb) if pb is not None else (2 if self.sharded else 0))
-            if not self.sharded:
-                self._fsort_next = KN.FieldSort(self.field_ranges, min(M, KN.field_sort_max_rows()),
-                                                dev, max_pb=int(pb) if pb is not None else 0)
+        self._make_field_sorts()
         tb = max(KN.radix_temp_bytes(n), KN.rbk_temp_bytes(K, n), KN.scan_temp_bytes(n))
         self.temp = torch.zeros(tb + 256, dtype=torch.uint8, device=dev)
         self._build_finalize_jobs()
@@ -464,6 +454,30 @@ class NativeDeepFM:
         self._graphs = {}
         self.max_graphs = 256
         self._graph = None
+
+    def _make_field_sorts(self):
+        self._fsort = self._fsort_next = None
+        if self.field_ranges is None:
+            return
+        M, dev = self.M, self.device
+        # the sort runs on a side stream next to the step in both cases, and every sort
+        # workgroup holds 148 KB of LDS: one workgroup per field on one GPU (0.160 ms/step vs
+        # 0.162 / 0.169 / 0.179 with 2 / 4 / 16 per field); 4 per field for the next batch's
+        # routing on the sharded step (0.198 ms vs 0.206 with 16; HIPFM_FSORT_PB overrides)
+        pb = os.environ.get("HIPFM_FSORT_PB")
+        self._fsort = KN.FieldSort(self.field_ranges, min(M, KN.field_sort_max_rows()), dev,
+                                   max_pb=int(pb) if pb is not None else (2 if self.sharded else 0))
+        if not self.sharded:
+            self._fsort_next = KN.FieldSort(self.field_ranges, min(M, KN.field_sort_max_rows()),
+                                            dev, max_pb=int(pb) if pb is not None else 0)
+
+    def set_field_ranges(self, ranges):
+        """Per-field id ranges found after construction (e.g. derived while caching the first
+        epoch): switches the slot sort to the one-launch per-field LDS sort."""
+        self.field_ranges = None if ranges is None else check_field_ranges(ranges, self.F, self.V)
+        self._make_field_sorts()
+        self._ss_key = [None, None]
+        self._graphs = {}
 
     def _build_finalize_jobs(self):
         jobs = []
@@ -1122,11 +1136,12 @@ class NativeDeepFM:
                 ids.is_contiguous() and vals.is_contiguous() and labels.is_contiguous() and
                 ids.shape[0] == self.M and ids.numel() == self.M * self.F)
 
-    def _bind_step(self, ids, vals, labels, next_ids=None):
-        """Bind one step's batch (in place when resident, else a staging copy) and decide its
-        host-side plans (sort / routing: inline or prefetched, next batch or none).  Returns
-        (B, direct, key) -- ``key`` identifies the step's captured graph."""
-        direct = self._resident(ids, vals, labels)
+    def _bind_step(self, ids, vals, labels, next_ids=None, stage: bool = False):
+        """Bind one step's batch (in place when resident, else -- or with ``stage`` -- a copy into
+        the static input buffers) and decide its host-side plans (sort / routing: inline or
+        prefetched, next batch or none).  Returns (B, direct, key) -- ``key`` identifies the
+        step's captured graph (staged steps of one batch size share one graph)."""
+        direct = (not stage) and self._resident(ids, vals, labels)
         if direct:
             B = ids.shape[0]
             self.idx, self.vals, self.labels = ids.reshape(-1), vals.reshape(-1), labels.reshape(-1)
@@ -1183,14 +1198,16 @@ class NativeDeepFM:
             for rs, k in zip(self.shx.sets, st[2][1]):
                 rs.key = k
 
-    def train_step(self, ids, vals, labels, use_graph: bool = False, next_ids=None):
+    def train_step(self, ids, vals, labels, use_graph: bool = False, next_ids=None,
+                   stage: bool = False):
         """One training step.  A device-resident int32 batch whose size equals the allocated
         batch is bound in place (no staging copy); with ``use_graph`` each such resident batch
         gets its own captured HIP graph (the HBM-cached epoch replays graphs back to back).
         ``next_ids`` (resident ids of the NEXT step's batch, unchanged until that step): its
         slot sort (one GPU) or its routing (row-sharded multi-GPU step) is computed on a side
-        stream during this step."""
-        B, direct, key = self._bind_step(ids, vals, labels, next_ids)
+        stream during this step.  ``stage``: copy the batch into the static input buffers even if
+        it is resident (a stream of one-off batches then replays ONE graph)."""
+        B, direct, key = self._bind_step(ids, vals, labels, next_ids, stage)
         if use_graph and (self.comm is None or self.comm.graph_safe):
             self._replay_graph(key, B)
         else:
