@@ -8,7 +8,7 @@
 //   requester                                        owner
 //   sorted uniques -> sh_scatter: send_ids[o][c]  -- a2a -->  recv_ids[p][c]
 //   (upos[u] = o*C + c)                                       sh_serve: rows[p][c] = {v, w},
-//                                                             tag[row][p] = (step, c)
+//                                                             request table: row -> c per p
 //   rows_in[o][c]                                 <-- a2a --
 //   sh_slot_rows: slot -> rows_in row; fm_fwd / tower / sparse_fused (MODE 2: gradient rows
 //   g_u written at send_g[upos[u]], V taken from rows_in)
@@ -17,10 +17,63 @@
 //                                                             rank sums the rows of all requesters
 //                                                             in rank order, applies the optimizer
 //
-// The tag table [R_local][N] (64-bit {step+1, c}) replaces a sort of the received ids: a row
-// requested by several ranks is found by direct addressing, and the sum runs in rank order, so
-// results are bitwise reproducible.  A bucket larger than C sets err bit 2 (the host raises).
+// The request table replaces a sort of the received ids: an open-addressing hash table of the
+// rows requested this step (>= 2x the N*C request slots, so at most half full; keys and the per-
+// requester positions carry the step stamp {step+1} in their high word, so nothing is cleared
+// between steps).  A row requested by several ranks is found in O(1), and its lead requester
+// sums the rows of all requesters in rank order: bitwise reproducible.  Its size follows the
+// exchange (N*C), not the table: tens of MB per rank instead of the 8*R*N bytes a direct-
+// addressed [R_local][N] tag array costs (7 GB per rank at the Criteo-1TB shape).
+// A bucket larger than C sets err bit 2 (the host raises).
 #include "common.h"
+
+// hash table of the owner's requested rows: key[slot] = {stamp, row}, pos[slot][p] = {stamp, c}
+struct ShTable {
+  unsigned long long* key;  // [slots]
+  unsigned long long* pos;  // [slots][N]
+  unsigned mask;            // slots - 1 (power of two)
+  int pad;
+};
+
+__device__ __forceinline__ unsigned sh_hash(unsigned row) {
+  unsigned h = row * 0x9E3779B1u;
+  return h ^ (h >> 15);
+}
+
+// insert `row` (requested by rank p at position c) for the step `stamp`; returns nothing: the
+// position is recorded in the row's slot.  Stale slots (older stamps) count as empty.
+__device__ __forceinline__ void sh_insert(const ShTable& T, int N, unsigned row, int p, unsigned c,
+                                          unsigned stamp) {
+  const unsigned long long want = ((unsigned long long)stamp << 32) | row;
+  unsigned s = sh_hash(row) & T.mask;
+  for (unsigned probe = 0; probe <= T.mask; ++probe, s = (s + 1) & T.mask) {
+    unsigned long long cur = T.key[s];
+    if (cur != want) {
+      if ((unsigned)(cur >> 32) == stamp) continue;  // taken by another row this step
+      const unsigned long long prev = atomicCAS(T.key + s, cur, want);
+      if (prev != cur && prev != want) {  // lost the slot to another row: re-examine it
+        if ((unsigned)(prev >> 32) == stamp) continue;
+        --probe;
+        s = (s - 1) & T.mask;
+        continue;
+      }
+    }
+    T.pos[(size_t)s * N + p] = ((unsigned long long)stamp << 32) | c;
+    return;
+  }
+}
+
+__device__ __forceinline__ const unsigned long long* sh_find(const ShTable& T, int N, unsigned row,
+                                                             unsigned stamp) {
+  const unsigned long long want = ((unsigned long long)stamp << 32) | row;
+  unsigned s = sh_hash(row) & T.mask;
+  for (unsigned probe = 0; probe <= T.mask; ++probe, s = (s + 1) & T.mask) {
+    const unsigned long long cur = T.key[s];
+    if (cur == want) return T.pos + (size_t)s * N;
+    if ((unsigned)(cur >> 32) != stamp) return nullptr;  // an empty slot ends the probe chain
+  }
+  return nullptr;
+}
 
 namespace {
 constexpr int SH_THREADS = 256;
@@ -125,7 +178,7 @@ template <int K>
 __global__ void sh_serve_kernel(const int* __restrict__ recv_ids, int total, int N, int C,
                                 const float* __restrict__ tv, const float* __restrict__ tw, long ldv,
                                 long ldw, float* __restrict__ rows, const int64_t* __restrict__ step,
-                                unsigned long long* __restrict__ tags) {
+                                ShTable T) {
   constexpr int LPS = K / 4, RW = K + 4;
   const int gt = blockIdx.x * blockDim.x + threadIdx.x;
   const int e = gt / LPS, sub = gt % LPS;
@@ -138,7 +191,7 @@ __global__ void sh_serve_kernel(const int* __restrict__ recv_ids, int total, int
     v = *reinterpret_cast<const f32x4*>(tv + row * ldv + sub * 4);
     if (sub == 0) {
       w = tw[row * ldw];
-      if (tags) tags[row * N + e / C] = ((unsigned long long)(*step + 1) << 32) | (unsigned)(e % C);
+      if (T.key) sh_insert(T, N, (unsigned)row, e / C, (unsigned)(e % C), (unsigned)(*step + 1));
     }
   }
   float* o = rows + (size_t)e * RW;
@@ -147,21 +200,18 @@ __global__ void sh_serve_kernel(const int* __restrict__ recv_ids, int total, int
 }
 
 __global__ void sh_owner_tag_kernel(const int* __restrict__ recv_ids, int total, int N, int C,
-                                    const int64_t* __restrict__ step,
-                                    unsigned long long* __restrict__ tags) {
+                                    const int64_t* __restrict__ step, ShTable T) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= total) return;
   const int id = recv_ids[e];
   if (id < 0) return;
-  const unsigned long long tag = (unsigned long long)(*step + 1) << 32;
-  tags[(size_t)(id / N) * N + e / C] = tag | (unsigned)(e % C);
+  sh_insert(T, N, (unsigned)(id / N), e / C, (unsigned)(e % C), (unsigned)(*step + 1));
 }
 
 // MODE 0: lazy optimizer OPT on the owner's row; 1: tf1_dense scatter into (Gv, Gw)
 template <int K, int MODE, int OPT>
 __global__ void sh_owner_apply_kernel(const int* __restrict__ recv_ids, int total, int N, int C,
-                                      const float* __restrict__ recv_g,
-                                      const unsigned long long* __restrict__ tags, float* tv, float* tw,
+                                      const float* __restrict__ recv_g, ShTable T, float* tv, float* tw,
                                       float* s0v, float* s1v, float* s0w, float* s1w, long ldv, long ldw,
                                       float* Gv, float* Gw, OptHyper h, const int64_t* __restrict__ step) {
   constexpr int LPS = K / 4, RW = K + 4;
@@ -173,7 +223,8 @@ __global__ void sh_owner_apply_kernel(const int* __restrict__ recv_ids, int tota
   const int p = e / C;
   const size_t row = (size_t)(id / N);
   const unsigned cur = (unsigned)(*step + 1);
-  const unsigned long long* tr = tags + row * N;
+  const unsigned long long* tr = sh_find(T, N, (unsigned)row, cur);
+  if (!tr) return;  // cannot happen: every received row was inserted by this step's serve / tag
   for (int q = 0; q < p; ++q)
     if ((unsigned)(tr[q] >> 32) == cur) return;  // a lower rank also requested it: it leads
   f32x4 g = {0.f, 0.f, 0.f, 0.f};
@@ -256,14 +307,18 @@ HFM_API int hfm_sh_slot_rows(const int* perm, const int* sid_incl, const int* up
     default: return (int)hipErrorInvalidValue; \
   }
 
+// table = {key, pos, mask} of the request table, or key == null (eval-style fetch: no insert)
 HFM_API int hfm_sh_serve(int K, const int* recv_ids, int total, int N, int C, const float* tv, const float* tw,
-                         long ldv, long ldw, float* rows, const int64_t* step, void* tags, hipStream_t st) {
+                         long ldv, long ldw, float* rows, const int64_t* step, const ShTable* table,
+                         hipStream_t st) {
   const long th = (long)total * (K / 4);
   const int grid = (int)((th + 255) / 256);
   if (grid == 0) return 0;
-  if (tags && (!step || C <= 0)) return (int)hipErrorInvalidValue;
+  const ShTable T = table ? *table : ShTable{nullptr, nullptr, 0u, 0};
+  if (T.key && (!step || C <= 0 || (T.mask & (T.mask + 1)) != 0 || T.mask + 1 < 2u * (unsigned)total))
+    return (int)hipErrorInvalidValue;
 #define CALL(KK) hipLaunchKernelGGL(sh_serve_kernel<KK>, dim3(grid), dim3(256), 0, st, recv_ids, total, N, \
-                                    C, tv, tw, ldv, ldw, rows, step, (unsigned long long*)tags)
+                                    C, tv, tw, ldv, ldw, rows, step, T)
   HFM_K_DISPATCH(K, CALL)
 #undef CALL
   HFM_LAUNCH_CHECK();
@@ -273,7 +328,7 @@ struct ShApplyArgs {
   const int* recv_ids;
   int total, N, C, mode;
   const float* recv_g;
-  unsigned long long* tags;
+  ShTable table;
   float *tv, *tw, *s0v, *s1v, *s0w, *s1w;
   long ldv, ldw;
   float *Gv, *Gw;
@@ -287,10 +342,10 @@ static int sh_apply_k(int opt, const ShApplyArgs& A, hipStream_t st) {
   const int grid = (int)((th + 255) / 256);
   if (A.mode & 2)  // tags not stamped by this step's serve (eval-style fetch): stamp them here
     hipLaunchKernelGGL(sh_owner_tag_kernel, dim3((A.total + 255) / 256), dim3(256), 0, st, A.recv_ids,
-                       A.total, A.N, A.C, A.step, A.tags);
+                       A.total, A.N, A.C, A.step, A.table);
 #define L_(M, O)                                                                                      \
   hipLaunchKernelGGL((sh_owner_apply_kernel<K, M, O>), dim3(grid), dim3(256), 0, st, A.recv_ids, A.total, \
-                     A.N, A.C, A.recv_g, A.tags, A.tv, A.tw, A.s0v, A.s1v, A.s0w, A.s1w, A.ldv, A.ldw,  \
+                     A.N, A.C, A.recv_g, A.table, A.tv, A.tw, A.s0v, A.s1v, A.s0w, A.s1w, A.ldv, A.ldw, \
                      A.Gv, A.Gw, A.h, A.step)
   if ((A.mode & 1) == 1) {
     L_(1, 0);
@@ -313,6 +368,8 @@ static int sh_apply_k(int opt, const ShApplyArgs& A, hipStream_t st) {
 // into the tf1_dense gradient buffer (mode 1)
 HFM_API int hfm_sh_owner_apply(int K, int opt, const ShApplyArgs* A, hipStream_t st) {
   if (A->total <= 0) return 0;
+  const unsigned m = A->table.mask;
+  if (!A->table.key || (m & (m + 1)) != 0 || m + 1 < 2u * (unsigned)A->total) return (int)hipErrorInvalidValue;
   int rc = 0;
 #define CALL(KK) rc = sh_apply_k<KK>(opt, *A, st)
   HFM_K_DISPATCH(K, CALL)

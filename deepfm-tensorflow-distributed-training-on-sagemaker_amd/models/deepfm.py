@@ -444,12 +444,10 @@ class NativeDeepFM:
         self.shx = None
         if self.sharded and getattr(self.comm, "engine", None) is not None:
             from ..parallel.sharded import FixedCapacityExchange
-            old = getattr(self, "_shx_tags", None)
-            self.shx = FixedCapacityExchange(self, self.comm.engine, self.comm.capacity, tags=old,
+            self.shx = FixedCapacityExchange(self, self.comm.engine, self.comm.capacity,
                                              engine_route=getattr(self.comm, "engine_route", None))
             if self.shx.eng_route is None and not hasattr(self.comm, "route_engine"):
                 self.shx.eng_route = self.comm.engine
-            self._shx_tags = self.shx.tags
         self._own_in = (self.idx, self.vals, self.labels)
         self._graphs = {}
         self.max_graphs = 256
@@ -681,6 +679,8 @@ class NativeDeepFM:
         backwards (checkpoint restore) must not meet flags of its future."""
         if hasattr(self, "sf_flags"):
             self.sf_flags.zero_()
+        if getattr(self, "shx", None) is not None:
+            self.shx.reset_table()
 
     def refresh_shadows(self):
         KN.shadow_refresh(self.p, self.P, self._shadow_dev, self._nshadow)

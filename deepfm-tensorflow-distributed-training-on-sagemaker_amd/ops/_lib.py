@@ -88,9 +88,14 @@ class SfArgs(C.Structure):
                 ("flags", c_void_p), ("sync", c_void_p)]
 
 
+class ShTable(C.Structure):
+    """Owner-side request table (csrc/kernels/shard.hip): key [slots] u64, pos [slots][N] u64."""
+    _fields_ = [("key", c_void_p), ("pos", c_void_p), ("mask", C.c_uint32), ("pad", c_int)]
+
+
 class ShApplyArgs(C.Structure):
     _fields_ = [("recv_ids", c_void_p), ("total", c_int), ("N", c_int), ("C", c_int), ("mode", c_int),
-                ("recv_g", c_void_p), ("tags", c_void_p), ("tv", c_void_p), ("tw", c_void_p),
+                ("recv_g", c_void_p), ("table", ShTable), ("tv", c_void_p), ("tw", c_void_p),
                 ("s0v", c_void_p), ("s1v", c_void_p), ("s0w", c_void_p), ("s1w", c_void_p),
                 ("ldv", c_long), ("ldw", c_long), ("Gv", c_void_p), ("Gw", c_void_p), ("h", OptHyper),
                 ("step", c_void_p)]

@@ -402,11 +402,16 @@ def sh_slot_rows(perm, sid_incl, upos, n, idx):
           "sh_slot_rows")
 
 
-def sh_serve(K, recv_ids, total, N, tv, tw, rows, C: int = 0, step=None, tags=None):
-    """Owner side of the row fetch: rows[e] = {v, w} of every requested id.  With ``tags`` (training
-    steps) it also stamps the owner-side request tags {step + 1, slot} used by sh_owner_apply."""
+_byref = C.byref
+
+
+def sh_serve(K, recv_ids, total, N, tv, tw, rows, C: int = 0, step=None, table=None):
+    """Owner side of the row fetch: rows[e] = {v, w} of every requested id.  With ``table`` (a
+    ShTable; training steps) it also records each request (row, requester, slot) stamped with
+    step + 1 in the owner's request table read by sh_owner_apply."""
     check(L().hfm_sh_serve(K, ptr(recv_ids), total, N, C, ptr(tv), ptr(tw), *_ld(tv, tw), ptr(rows),
-                           ptr(step), ptr(tags), stream_handle()), "sh_serve")
+                           ptr(step), _byref(table) if table is not None else None, stream_handle()),
+          "sh_serve")
 
 
 def sh_owner_apply(K, opt, args: ShApplyArgs):

@@ -21,7 +21,7 @@ from typing import Iterable, Optional
 import torch
 
 from ..ops import kernels as KN
-from ..ops._lib import ShApplyArgs
+from ..ops._lib import ShApplyArgs, ShTable
 
 
 def estimate_capacity(id_batches: Iterable[torch.Tensor], world: int, slack: float = 1.25,
@@ -105,8 +105,7 @@ class FixedCapacityExchange:
     during step i — the sparse-input-dist pipelining of production DLRM trainers — so the
     critical path of a step keeps only the row fetch, the compute and the gradient exchange."""
 
-    def __init__(self, m, engine, capacity: Optional[int] = None, tags: Optional[torch.Tensor] = None,
-                 engine_route=None):
+    def __init__(self, m, engine, capacity: Optional[int] = None, engine_route=None):
         self.m, self.eng = m, engine
         self.eng_route = engine_route     # created on the first prefetching step (plan())
         self.N, self.rank = engine.world, engine.rank
@@ -126,8 +125,15 @@ class FixedCapacityExchange:
         self.rows_in = torch.zeros(T, self.RW, **f32)
         self.send_g = torch.zeros(T, self.RW, **f32)
         self.recv_g = torch.zeros(T, self.RW, **f32)
-        # owner-side request tags: [local rows][N] of {step + 1, slot} (64-bit)
-        self.tags = tags if tags is not None else torch.zeros(m.R * self.N, dtype=torch.int64, device=dev)
+        # owner-side request table (csrc/kernels/shard.hip): a power of two >= 2x the N*C request
+        # slots, keys and per-requester positions stamped with step + 1 -- sized by the exchange,
+        # not by the table (a direct [R_local][N] tag array is 7 GB per rank at the 1TB shape)
+        slots = 1
+        while slots < 2 * T:
+            slots *= 2
+        self.req_key = torch.zeros(slots, dtype=torch.int64, device=dev)
+        self.req_pos = torch.zeros(slots * self.N, dtype=torch.int64, device=dev)
+        self.table = ShTable(self.req_key.data_ptr(), self.req_pos.data_ptr(), slots - 1, 0)
         self._side = None
 
     # ------------------------------------------------------------------ host-side plan
@@ -208,7 +214,7 @@ class FixedCapacityExchange:
         rs = self.sets[plan[0]]
         if train:
             KN.sh_serve(m.K, rs.recv_ids, self.N * self.C, self.N, m.tv, m.tw, self.rows_out,
-                        C=self.C, step=m.step, tags=self.tags)
+                        C=self.C, step=m.step, table=self.table)
         else:
             KN.sh_serve(m.K, rs.recv_ids, self.N * self.C, self.N, m.tv, m.tw, self.rows_out)
         self.eng.alltoall(self.rows_out, self.rows_in, self.C * self.RW * 4)
@@ -229,7 +235,7 @@ class FixedCapacityExchange:
         S = ShApplyArgs()
         S.recv_ids, S.total, S.N, S.C = rs.recv_ids.data_ptr(), self.N * self.C, self.N, self.C
         S.mode = 0 if m.sparse_update == "lazy" else 1      # tags were stamped by fetch()
-        S.recv_g, S.tags = self.recv_g.data_ptr(), self.tags.data_ptr()
+        S.recv_g, S.table = self.recv_g.data_ptr(), self.table
         S.tv, S.tw = m.tv.data_ptr(), m.tw.data_ptr()
         S.s0v, S.s1v, S.s0w, S.s1w = (t.data_ptr() if t.numel() else 0 for t in m.sv)
         S.ldv, S.ldw = KN._ld(m.tv, m.tw)
@@ -240,6 +246,11 @@ class FixedCapacityExchange:
         KN.sh_owner_apply(m.K, m.opt_id, S)
         if m.sparse_update == "tf1_dense":
             KN.dense_sweep(m.K, m.opt_id, m.R, m.tv, m.tw, m.Gv, m.Gw, m.sv, m.h_sparse, m.step)
+
+    def reset_table(self):
+        """The table's stamps are step numbers: clear it when the step counter is rewritten."""
+        self.req_key.zero_()
+        self.req_pos.zero_()
 
     def error(self) -> int:
         return int(self.err.item())

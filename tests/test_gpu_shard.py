@@ -170,3 +170,84 @@ def test_sharded_exchange_matches_global_batch(N, opt, update, prefetch):
     assert (models[0].p - ref.p).abs().max().item() <= 2e-5 * ref.p.abs().max().item()
     # something was actually exchanged, and untouched rows kept their initial values
     assert models[0].comm.bytes_sent > 0
+
+
+def _fill_tables(m, N, r):
+    """Deterministic initial table values as a function of the GLOBAL id (row * N + r), so the
+    row-sharded ranks and the replicated reference start from identical rows."""
+    R, K = m.R, m.K
+    step = 1 << 25
+    with torch.no_grad():
+        for a in range(0, R, step):
+            b = min(R, a + step)
+            gid = torch.arange(a, b, device=DEV, dtype=torch.int64) * N + r
+            h = (gid * 2654435761) % 4294967296
+            m.tw[a:b] = ((h % 10007).float() / 10007.0 - 0.5) * 0.02
+            for k in range(K):
+                m.tv[a:b, k] = (((h >> (k + 3)) % 9973).float() / 9973.0 - 0.5) * 0.02
+
+
+def test_sharded_exchange_n8_criteo_1tb_shape():
+    """The bench's multi-GPU step at its real shape, emulated on one GPU: N = 8 row-sharded ranks
+    (Adam eps 1e-2 keeps the first update continuous in the gradient, so fp32 summation order
+    cannot flip a near-zero gradient's sign; the exchange itself is what is checked)
+    (882.8M-row table, 110M rows per rank), B = 16384 per rank, the capacity estimate bench.py
+    uses, prefetched routing.  The 8 shards must reproduce ONE model trained on the global batch
+    (131072) to 2e-5 on every touched row and on the dense parameters."""
+    free, _ = torch.cuda.mem_get_info()
+    if free < 245 * (1 << 30):
+        pytest.skip(f"needs ~240 GB of free HBM (have {free / (1 << 30):.0f} GB)")
+    from hipfm.models.reference import init_params as ip
+    from hipfm.parallel.sharded import estimate_capacity
+    synth = make_synth("criteo_1tb", seed=2024)
+    F, K, layers, keep, B, N = synth.F, 8, [128, 64, 32], [1.0, 1.0, 1.0], 16384, 8
+    V = synth.feature_size
+    lr = 5e-4
+    dense = ip(V, F, K, layers, False, seed=11, tables=False)
+    steps = 2
+    data = [synth.batch(N * B, step=s, device=DEV, id_dtype=torch.int32) for s in range(steps)]
+    batches = [[(ids[r * B:(r + 1) * B].contiguous(), vals[r * B:(r + 1) * B].contiguous(),
+                 lab[r * B:(r + 1) * B].contiguous()) for ids, vals, lab in data] for r in range(N)]
+    cap = max(estimate_capacity((batches[r][s][0] for s in range(steps)), N) for r in range(N))
+    hub = _Hub(N)
+    models = []
+    for r in range(N):
+        m = NativeDeepFM(V, F, K, layers, keep, optimizer="Adam", sparse_update="lazy", learning_rate=lr,
+                         batch_size=B, device=DEV, init=False, comm=MeshComm(hub, r, capacity=cap),
+                         field_ranges=synth.field_ranges(), adam_epsilon=1e-2)
+        m.load_tf_params(dense)
+        _fill_tables(m, N, r)
+        assert m.shx is not None and m.shx.N == N and m.shx.C == cap
+        # the request table follows the exchange size, not the 110M-row shard
+        assert m.shx.req_key.numel() * 8 * (1 + N) < 256 * (1 << 20)
+        models.append(m)
+    _run_ranks(models, batches, prefetch=True)
+    torch.cuda.synchronize()
+    for m in models:
+        m.check_errors()
+        assert torch.equal(m.p, models[0].p)
+    uids = torch.unique(torch.cat([d[0].reshape(-1) for d in data]).long())
+    got_v = torch.empty(uids.numel(), K, device=DEV)
+    got_w = torch.empty(uids.numel(), device=DEV)
+    for r, m in enumerate(models):
+        sel = (uids % N) == r
+        rows = uids[sel] // N
+        got_v[sel] = m.tv[rows]
+        got_w[sel] = m.tw[rows]
+    p_sh = models[0].p.clone()
+    del models, hub
+    torch.cuda.empty_cache()
+    ref = NativeDeepFM(V, F, K, layers, keep, optimizer="Adam", sparse_update="lazy", learning_rate=lr * N,
+                       batch_size=N * B, device=DEV, init=False, field_ranges=synth.field_ranges(),
+                       adam_epsilon=1e-2)
+    ref.load_tf_params(dense)
+    _fill_tables(ref, 1, 0)
+    for ids, vals, lab in data:
+        ref.train_step(ids, vals, lab)
+    torch.cuda.synchronize()
+    ref_v, ref_w = ref.tv[uids], ref.tw[uids]
+    assert (got_v - ref_v).abs().max().item() <= 2e-5 * ref_v.abs().max().item()
+    assert (got_w - ref_w).abs().max().item() <= 2e-5 * ref_w.abs().max().item()
+    assert (p_sh - ref.p).abs().max().item() <= 2e-5 * ref.p.abs().max().item()
+    del ref
+    torch.cuda.empty_cache()
