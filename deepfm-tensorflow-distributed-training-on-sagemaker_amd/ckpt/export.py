@@ -44,20 +44,33 @@ def export_servable(variables: Dict[str, torch.Tensor], model_config: dict, serv
     d = os.path.join(servable_dir, str(ts))
     tmp = d + ".tmp"
     os.makedirs(os.path.join(tmp, "variables"), exist_ok=True)
-    serve_vars = {k: v for k, v in variables.items() if not any(s in k for s in _TRAINING_ONLY)}
+    serve_vars = {k: v for k, v in variables.items() if not is_training_only(k)}
     write_bundle(os.path.join(tmp, "variables", "variables"), serve_vars)
+    return finish_servable(tmp, d, model_config)
+
+
+def is_training_only(name: str) -> bool:
+    return any(s in name for s in _TRAINING_ONLY)
+
+
+def finish_servable(tmp: str, final: str, model_config: dict) -> str:
+    """Complete an export whose ``variables/`` bundle is written: saved_model.pb (MetaGraphDef
+    with the serving graph and signature, ckpt/saved_model.py), saved_model.json (the same
+    signature + model config, read by load_servable), then the atomic rename."""
+    from .saved_model import write_saved_model
     sig = json.loads(json.dumps(SIGNATURE))
     F = model_config["field_size"]
     for spec in sig["serving_default"]["inputs"].values():
         spec["shape"] = [-1, F]
+    write_saved_model(os.path.join(tmp, "saved_model.pb"), model_config)
     with open(os.path.join(tmp, "saved_model.json"), "w") as f:
         json.dump({"signature_def": sig, "model": model_config, "format": "hipfm-servable-v1",
                    "tags": ["serve"]}, f, indent=1)
-    if os.path.exists(d):
+    if os.path.exists(final):
         import shutil
-        shutil.rmtree(d)
-    os.replace(tmp, d)
-    return d
+        shutil.rmtree(final)
+    os.replace(tmp, final)
+    return final
 
 
 def latest_export(servable_dir: str) -> Optional[str]:

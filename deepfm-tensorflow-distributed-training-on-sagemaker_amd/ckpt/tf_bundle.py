@@ -1,7 +1,9 @@
 """TensorFlow ``tensor_bundle`` checkpoint writer/reader without TensorFlow.
 
 A TF1 checkpoint ``model.ckpt-<step>`` is
-  * ``model.ckpt-<step>.data-00000-of-00001`` — raw little-endian tensor bytes, back to back;
+  * ``model.ckpt-<step>.data-0000r-of-0000N`` — raw little-endian tensor bytes, back to back;
+    every variable lives whole in one of the N data shards (TF1 PS jobs write one shard per
+    parameter-server task; ``ShardWriter`` lets each rank write its own);
   * ``model.ckpt-<step>.index`` — a LevelDB-format SSTable mapping tensor name ->
     ``BundleEntryProto{dtype, shape, shard_id, offset, size, crc32c}``, plus the header entry
     under the empty key -> ``BundleHeaderProto{num_shards, endianness, version}``;
@@ -275,12 +277,65 @@ def write_bundle(prefix: str, tensors: Dict[str, object], chunk_bytes: int = 1 <
     write_sstable(prefix + ".index", entries)
 
 
+def data_path(prefix: str, shard: int, num_shards: int) -> str:
+    return f"{prefix}.data-{shard:05d}-of-{num_shards:05d}"
+
+
+def parse_header(b: bytes) -> dict:
+    d = {"num_shards": 1}
+    for f, _, v in _fields(b):
+        if f == 1:
+            d["num_shards"] = v
+    return d
+
+
+class ShardWriter:
+    """One data shard ``prefix.data-<shard>-of-<num>`` of a multi-shard bundle.  ``add`` streams a
+    tensor (or an iterator of row chunks of it) into the shard and returns its index entry; the
+    entries of every shard go to ``write_index`` (one writer, e.g. rank 0).  Each rank writes only
+    its own shard -- no host ever holds the whole checkpoint."""
+
+    def __init__(self, prefix: str, shard: int, num_shards: int):
+        os.makedirs(os.path.dirname(os.path.abspath(prefix)), exist_ok=True)
+        self.shard, self.num = shard, num_shards
+        self.f = open(data_path(prefix, shard, num_shards), "wb")
+        self.off = 0
+        self.entries: List[Tuple[bytes, bytes]] = []
+
+    def add(self, name: str, shape: Tuple[int, ...], chunks: Iterable) -> Tuple[bytes, bytes]:
+        crc, size, dt = 0, 0, None
+        for c in chunks:
+            a = _as_numpy(c)
+            dt = _NP2DT[a.dtype]
+            b = a.tobytes()
+            self.f.write(b)
+            crc = _nio.crc32c_extend(crc, b)
+            size += len(b)
+        e = (name.encode(), bundle_entry(dt, tuple(int(x) for x in shape), self.off, size,
+                                         _nio.mask_crc(crc), shard_id=self.shard))
+        self.off += size
+        self.entries.append(e)
+        return e
+
+    def close(self):
+        self.f.close()
+
+
+def write_index(prefix: str, entries: List[Tuple[bytes, bytes]], num_shards: int) -> None:
+    write_sstable(prefix + ".index", list(entries) + [(b"", bundle_header(num_shards))])
+
+
 def read_bundle(prefix: str, verify: bool = True, names: Optional[Iterable[str]] = None
                 ) -> Dict[str, np.ndarray]:
     items = read_sstable(prefix + ".index", verify)
     want = set(names) if names is not None else None
+    num = 1
+    for k, v in items:
+        if not k:
+            num = parse_header(v)["num_shards"]
     out = {}
-    with open(prefix + ".data-00000-of-00001", "rb") as f:
+    files = {}
+    try:
         for k, v in items:
             if not k:
                 continue
@@ -288,11 +343,18 @@ def read_bundle(prefix: str, verify: bool = True, names: Optional[Iterable[str]]
             if want is not None and name not in want:
                 continue
             e = parse_entry(v)
+            sid = e["shard_id"]
+            if sid not in files:
+                files[sid] = open(data_path(prefix, sid, num), "rb")
+            f = files[sid]
             f.seek(e["offset"])
             b = f.read(e["size"])
             if verify and len(b) < (1 << 26) and _mcrc(b) != e["crc32c"]:
                 raise IOError(f"tensor {name}: data CRC mismatch")
             out[name] = np.frombuffer(b, dtype=_DT2NP[e["dtype"]]).reshape(e["shape"]).copy()
+    finally:
+        for f in files.values():
+            f.close()
     return out
 
 

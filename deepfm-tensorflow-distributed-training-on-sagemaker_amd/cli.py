@@ -185,6 +185,9 @@ def run(cfg: RunConfig) -> dict:
     if cfg.task_type in ("export", "train") and cfg.servable_model_dir:
         path = est.export(cfg.servable_model_dir)
         result["export_dir"] = path
+    if cfg.task_type in ("export", "train") and cfg.export_tf_bundle and cfg.ckpt_dir:
+        # the Estimator-style TF1 checkpoint model.ckpt-<step> next to the native one (§2.7.4)
+        result["tf_checkpoint"] = est.export_tf_checkpoint(cfg.ckpt_dir)
     est.log.close()
     return result
 

@@ -504,46 +504,103 @@ class Estimator:
                 "embedding_size": c.embedding_size, "deep_layers": c.layers,
                 "dropout_keep": c.keep_probs, "batch_norm": c.batch_norm, "loss_type": c.loss_type}
 
-    def _gathered_tf_variables(self):
-        """TF view with FULL tables for a row-sharded model: all-gather the shards (rank 0)."""
-        m = self.model
-        if not (self.native and m.sharded):
-            return m.tf_variables()
-        N = m.world
-
-        def gather_rows(local):
-            parts = [torch.empty_like(local) for _ in range(N)]
-            dist.all_gather(parts, local.contiguous())
-            full = torch.empty((m.R * N,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
-            for r in range(N):
-                full[r::N] = parts[r]
-            return full[: m.V].cpu()
-        tw, tv = gather_rows(m.tw), gather_rows(m.tv)
-        sv = [gather_rows(s) if s.numel() else s for s in m.sv]
-        return m.tf_variables(tables=(tw, tv, sv))
+    def _write_tf_bundle(self, prefix: str, serve_only: bool = False) -> None:
+        """Distributed TF1 ``tensor_bundle`` writer: one data shard per rank
+        (``prefix.data-0000r-of-0000N``, the reference PS job's layout of one shard per PS task),
+        every variable whole in one shard, the merged ``prefix.index`` by rank 0.  The big
+        embedding variables are spread over the ranks; a row-sharded one is gathered onto its
+        writer rank's GPU (never onto every rank or host) and streamed to disk in global row order
+        in 256 MB chunks.  Optimizer slots are left out with ``serve_only`` (servable export)."""
+        from .ckpt.export import is_training_only
+        from .ckpt.tf_bundle import ShardWriter, write_index
+        if self.native:
+            srcs = self.model.tf_variable_sources()
+        else:
+            srcs = {k: (v, False, tuple(v.shape)) for k, v in self.model.tf_variables().items()}
+        names = sorted(n for n in srcs if not (serve_only and is_training_only(n)))
+        world, rank = self.world, self.rank
+        big = sorted((n for n in names if srcs[n][0].numel() >= (1 << 20)),
+                     key=lambda n: -srcs[n][0].numel())
+        owner = {n: 0 for n in names}
+        for i, n in enumerate(big):
+            owner[n] = i % world
+        sw = ShardWriter(prefix, rank, world)
+        for n in names:
+            t, sharded, shape = srcs[n]
+            if sharded and world > 1:
+                loc = t.contiguous()
+                parts = [torch.empty_like(loc) for _ in range(world)] if rank == owner[n] else None
+                dist.gather(loc, parts, dst=owner[n])
+                if rank == owner[n]:
+                    sw.add(n, shape, _interleaved_chunks(parts, shape[0]))
+                del parts, loc
+            elif rank == owner[n]:
+                sw.add(n, shape, _row_chunks(t))
+        sw.close()
+        entries = sw.entries
+        if world > 1:
+            allv = [None] * world
+            dist.all_gather_object(allv, entries, group=self._ctl)
+            entries = [e for part in allv for e in part]
+        if rank == 0:
+            write_index(prefix, entries, world)
+        if _dist_on():
+            dist.barrier(group=self._ctl)
 
     def export(self, servable_dir: str) -> Optional[str]:
+        """SavedModel directory (reference C33, PS:451-467): ``<dir>/<unix ts>/saved_model.pb``
+        (MetaGraphDef with the serving_default signature) + ``variables/`` (multi-shard bundle
+        written by every rank)."""
         if not servable_dir:
             return None
-        variables = self._gathered_tf_variables() if self.native else self.model.tf_variables()
+        from .ckpt.export import finish_servable
+        ts = torch.tensor([int(time.time())], dtype=torch.int64)
+        if _dist_on():
+            dist.broadcast(ts, src=0, group=self._ctl)
+        d = os.path.join(servable_dir, str(int(ts.item())))
+        tmp = d + ".tmp"
+        self._write_tf_bundle(os.path.join(tmp, "variables", "variables"), serve_only=True)
         path = None
         if self.rank == 0:
-            path = export_servable(variables, self.model_config(), servable_dir)
+            path = finish_servable(tmp, d, self.model_config())
             self.log.info(f"SavedModel written to: {path}")
         if _dist_on():
-            dist.barrier()
+            dist.barrier(group=self._ctl)
         return path
 
     def export_tf_checkpoint(self, model_dir: str) -> Optional[str]:
-        """TF1 tensor_bundle ``model.ckpt-<step>`` + ``checkpoint`` state file (§2.7.4)."""
-        from .ckpt.tf_bundle import write_bundle, write_checkpoint_state
-        variables = self._gathered_tf_variables() if self.native else self.model.tf_variables()
+        """TF1 tensor_bundle ``model.ckpt-<step>`` + ``checkpoint`` state file (§2.7.4), one data
+        shard per rank."""
+        from .ckpt.tf_bundle import write_checkpoint_state
+        name = f"model.ckpt-{self.global_step}"
+        self._write_tf_bundle(os.path.join(model_dir, name))
         if self.rank != 0:
             return None
-        name = f"model.ckpt-{self.global_step}"
-        write_bundle(os.path.join(model_dir, name), variables)
         write_checkpoint_state(model_dir, name, [name])
         return os.path.join(model_dir, name)
+
+
+def _row_chunks(t: torch.Tensor, chunk_bytes: int = 1 << 28):
+    if t.dim() == 0 or t.numel() * t.element_size() <= chunk_bytes:
+        yield t
+        return
+    rows = max(1, chunk_bytes // max(1, t[0].numel() * t.element_size()))
+    for a in range(0, t.shape[0], rows):
+        yield t[a:a + rows]
+
+
+def _interleaved_chunks(parts, V: int, chunk_bytes: int = 1 << 28):
+    """Global row order of a row-sharded table from its per-rank parts (global row = local row *
+    N + rank), chunk by chunk on the device."""
+    N = len(parts)
+    R = parts[0].shape[0]
+    row_bytes = max(1, parts[0][0].numel() * parts[0].element_size())
+    rows = max(1, chunk_bytes // (row_bytes * N))
+    for a in range(0, R, rows):
+        blk = torch.stack([p[a:a + rows] for p in parts], dim=1)
+        blk = blk.reshape((-1,) + tuple(parts[0].shape[1:]))
+        lo = a * N
+        yield blk[: max(0, min(blk.shape[0], V - lo))]
 
 
 def train_and_evaluate(est: Estimator, train_spec: TrainSpec, eval_spec: EvalSpec) -> dict:

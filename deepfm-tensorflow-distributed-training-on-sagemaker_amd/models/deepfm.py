@@ -1447,6 +1447,26 @@ class NativeDeepFM:
             out["beta2_power"] = torch.tensor(0.999 ** (t + 1), dtype=torch.float32)
         return out
 
+    def tf_variable_sources(self) -> "OrderedDict[str, tuple]":
+        """name -> (tensor, row_sharded, TF shape) for a distributed TF checkpoint writer: the
+        embedding tables and their slots are THIS rank's local rows when row-sharded (global row =
+        local row * N + rank), everything else is the full tensor."""
+        out = OrderedDict()
+        full = self.tf_variables()
+        tables = {"fm_w": (self.tw, (self.V,)), "fm_v": (self.tv, (self.V, self.K))}
+        s0n, s1n = self.SLOT_NAMES[self.optimizer]
+        for slot_i, sname in ((0, s0n), (1, s1n)):
+            if sname is not None and self.sv[slot_i].numel():
+                tables[f"fm_v/{sname}"] = (self.sv[slot_i], (self.V, self.K))
+                tables[f"fm_w/{sname}"] = (self.sv[2 + slot_i], (self.V,))
+        for k, v in full.items():
+            if k in tables:
+                t, shape = tables[k]
+                out[k] = (t, self.sharded, shape)
+            else:
+                out[k] = (v, False, tuple(v.shape))
+        return out
+
     def load_tf_variables(self, tv: Dict[str, torch.Tensor]):
         """Inverse of ``tf_variables`` for replicated tables (params + slots + step)."""
         self.load_tf_params({k: torch.as_tensor(v) for k, v in tv.items()

@@ -96,3 +96,102 @@ def test_tf_bundle_streams_large_tensor(tmp_path):
     prefix = str(tmp_path / "big")
     tb.write_bundle(prefix, {"fm_v": t}, chunk_bytes=4096)     # forces the chunked CRC path
     assert np.array_equal(tb.read_bundle(prefix)["fm_v"], t.numpy())
+
+
+def test_multi_shard_bundle_roundtrip(tmp_path):
+    """Every variable whole in one of N data shards (the PS-job layout), one merged index."""
+    prefix = str(tmp_path / "model.ckpt-7")
+    rng = np.random.default_rng(0)
+    tensors = {"fm_v": rng.standard_normal((1000, 4)).astype(np.float32),
+               "fm_w": rng.standard_normal(1000).astype(np.float32),
+               "Deep-part/mlp0/weights": rng.standard_normal((156, 8)).astype(np.float32),
+               "global_step": np.array(7, dtype=np.int64)}
+    writers = [tb.ShardWriter(prefix, r, 3) for r in range(3)]
+    for i, (k, v) in enumerate(sorted(tensors.items())):
+        w = writers[i % 3]
+        if k == "fm_v":                                   # streamed in row chunks
+            w.add(k, v.shape, (v[a:a + 300] for a in range(0, 1000, 300)))
+        else:
+            w.add(k, v.shape, [v])
+    entries = []
+    for w in writers:
+        w.close()
+        entries += w.entries
+    tb.write_index(prefix, entries, 3)
+    for r in range(3):
+        assert os.path.exists(tb.data_path(prefix, r, 3))
+    got = tb.read_bundle(prefix)
+    assert set(got) == set(tensors)
+    for k in tensors:
+        np.testing.assert_array_equal(got[k], tensors[k])
+    hdr = [v for k, v in tb.read_sstable(prefix + ".index") if not k][0]
+    assert tb.parse_header(hdr)["num_shards"] == 3
+
+
+def _decode(b):
+    from hipfm.data.tfrecord import _fields
+    return list(_fields(b))
+
+
+def _map(entries, field):
+    out = {}
+    for f, _, v in entries:
+        if f == field:
+            kv = dict((ff, vv) for ff, _, vv in _decode(v))
+            out[kv[1].decode()] = kv.get(2, b"")
+    return out
+
+
+@pytest.mark.parametrize("bn", [False, True])
+def test_saved_model_pb_structure(tmp_path, bn):
+    """saved_model.pb decodes to one MetaGraphDef (tag serve) whose serving_default signature is
+    the reference's (feat_ids int64[-1,F], feat_vals float[-1,F] -> prob float[-1]), whose graph
+    holds the placeholders, a VariableV2 per variable of the exported bundle and the
+    Gather/MatMul/Sigmoid inference path, and whose V2 saver restores exactly the bundle's names."""
+    from hipfm.ckpt.export import export_servable
+    from hipfm.ckpt.saved_model import DT_FLOAT, DT_INT64
+    from hipfm.models.reference import init_params
+    V, F, K, layers = 500, 6, 4, [16, 8]
+    params = init_params(V, F, K, layers, bn, seed=1)
+    params["global_step"] = torch.tensor(3, dtype=torch.int64)
+    cfg = {"feature_size": V, "field_size": F, "embedding_size": K, "deep_layers": layers,
+           "dropout_keep": [1.0, 1.0], "batch_norm": bn, "loss_type": "log_loss"}
+    d = export_servable(params, cfg, str(tmp_path), timestamp=123)
+    sm = _decode(open(os.path.join(d, "saved_model.pb"), "rb").read())
+    assert [v for f, _, v in sm if f == 1] == [1]
+    metas = [v for f, _, v in sm if f == 2]
+    assert len(metas) == 1
+    meta = _decode(metas[0])
+    info = _decode([v for f, _, v in meta if f == 1][0])
+    assert b"serve" in [v for f, _, v in info if f == 4]
+    sig = _decode(_map(meta, 5)["serving_default"])
+    ins, outs = _map(sig, 1), _map(sig, 2)
+    assert set(ins) == {"feat_ids", "feat_vals"} and set(outs) == {"prob"}
+
+    def ti(b):
+        t = dict((f, v) for f, _, v in _decode(b))
+        dims = [dict((ff, vv) for ff, _, vv in _decode(d)).get(1, 0) for f2, _, d in _decode(t[3]) if f2 == 2]
+        dims = [x - (1 << 64) if x >= (1 << 63) else x for x in dims]
+        return t[1].decode(), t[2], dims
+    assert ti(ins["feat_ids"]) == ("feat_ids:0", DT_INT64, [-1, F])
+    assert ti(ins["feat_vals"]) == ("feat_vals:0", DT_FLOAT, [-1, F])
+    assert ti(outs["prob"]) == ("prob:0", DT_FLOAT, [-1])
+    assert [v for f, _, v in sig if f == 3] == [b"tensorflow/serving/predict"]
+    graph = _decode([v for f, _, v in meta if f == 2][0])
+    nodes = {}
+    for f, _, n in graph:
+        if f == 1:
+            nd = _decode(n)
+            nodes[[v for ff, _, v in nd if ff == 1][0].decode()] = (
+                [v for ff, _, v in nd if ff == 2][0].decode(), [v.decode() for ff, _, v in nd if ff == 3])
+    assert nodes["feat_ids"][0] == "Placeholder" and nodes["feat_vals"][0] == "Placeholder"
+    assert nodes["prob"][0] == "Sigmoid"
+    assert nodes["First-order/embedding_lookup"] == ("GatherV2", ["fm_w/read", "feat_ids", "Const/axis0"])
+    bundle = set(tb.read_bundle(os.path.join(d, "variables", "variables")))
+    var_nodes = {k for k, (op, _) in nodes.items() if op == "VariableV2"}
+    assert var_nodes == bundle, (var_nodes ^ bundle)
+    saver = dict((f, v) for f, _, v in _decode([v for f, _, v in meta if f == 3][0]))
+    assert saver[3] == b"save/restore_all" and saver[7] == 2
+    assert nodes["save/RestoreV2"][0] == "RestoreV2"
+    restore_inputs = [i for i in nodes["save/restore_all"][1]]
+    assert len(restore_inputs) == len(bundle)

@@ -5,6 +5,7 @@ import os
 import socket
 
 import pytest
+import numpy as np
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
@@ -208,3 +209,39 @@ def test_fixed_capacity_agreed_across_ranks():
         p.join(timeout=60)
         assert p.exitcode == 0
     assert all(v == 64 * world for v in got.values()), got
+
+
+def test_two_rank_export_writes_one_shard_per_rank(tmp_path):
+    """At world 2 every rank writes its own data shard of the TF1 checkpoint and of the
+    SavedModel's variables bundle (model.ckpt-<s>.data-0000r-of-00002), rank 0 the merged index
+    and saved_model.pb; the bundles read back complete."""
+    import subprocess
+    import sys
+    from hipfm.ckpt import tf_bundle as tb
+    from hipfm.ckpt.export import latest_export, load_servable
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    d = tmp_path / "data"
+    subprocess.check_call([sys.executable, os.path.join(repo, "tools", "gen_synthetic_criteo.py"),
+                           "--out", str(d), "--preset", "total:300000", "--train_rows", "1024",
+                           "--val_rows", "256", "--files", "2"], cwd=repo)
+    md, ex = tmp_path / "model", tmp_path / "export"
+    r = subprocess.run([sys.executable, "-m", "hipfm.launch", "--nproc_per_node", "2",
+                        "--master_port", str(_port()), "-m", "hipfm", "--task_type", "train",
+                        "--training_data_dir", str(d), "--val_data_dir", str(d), "--model_dir", str(md),
+                        "--servable_model_dir", str(ex), "--feature_size", "300000", "--field_size", "39",
+                        "--embedding_size", "4", "--batch_size", "64", "--deep_layers", "16",
+                        "--dropout", "1.0", "--num_epochs", "1", "--device", "cpu", "--log_steps", "100"],
+                       cwd=repo, env=dict(os.environ, PYTHONPATH=repo), capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    prefix = str(md / "model.ckpt-8")
+    for k in range(2):
+        assert os.path.getsize(tb.data_path(prefix, k, 2)) > 0      # both ranks wrote a shard
+    ck = tb.read_bundle(prefix)
+    assert ck["fm_v"].shape == (300000, 4) and "fm_v/Adam" in ck and int(ck["global_step"]) == 8
+    e = latest_export(str(ex))
+    assert os.path.exists(os.path.join(e, "saved_model.pb"))
+    sv = tb.read_bundle(os.path.join(e, "variables", "variables"))
+    assert "fm_v/Adam" not in sv and np.array_equal(sv["fm_v"], ck["fm_v"])
+    p = load_servable(e).predict(torch.zeros(3, 39, dtype=torch.int64), torch.ones(3, 39))
+    assert p.shape == (3,)

@@ -74,3 +74,43 @@ def test_native_tf_variables_roundtrip(tmp_path):
     est2.model.load_tf_variables({k: torch.from_numpy(a) for k, a in back.items()})
     assert torch.equal(est2.model.tv, est.model.tv) and torch.equal(est2.model.p, est.model.p)
     assert torch.equal(est2.model.sv[1], est.model.sv[1]) and est2.model.global_step() == 3
+
+
+@pytest.mark.parametrize("update", ["tf1_dense", "lazy"])
+def test_native_auc_parity_with_golden(update):
+    """SURVEY §6 parity: the native HIP path and the golden PyTorch transcription of the
+    reference's TF1 model (models/reference.py), trained from the same init on the same batches
+    with the same seeds (dropout masks are a shared counter hash) for 240 steps, reach the same
+    held-out AUC (|dAUC| <= 0.005) along loss curves that agree within 2% per 40-step window."""
+    from hipfm.data.synthetic import make_synth
+    from hipfm.models.deepfm import NativeDeepFM
+    from hipfm.models.reference import GoldenDeepFM, init_params
+    from hipfm.ops.metrics import auc_from_hist, hist_torch
+    dev = torch.device("cuda", 0)
+    synth = make_synth("total:60000", seed=31)
+    F, K, layers, keep, B = synth.F, 8, [128, 64, 32], [0.5, 0.5, 0.5], 512
+    V = synth.feature_size
+    params = init_params(V, F, K, layers, False, seed=12)
+    kw = dict(optimizer="Adam", sparse_update=update, learning_rate=1e-3, seed=77)
+    nat = NativeDeepFM(V, F, K, layers, keep, batch_size=B, device=dev, init=False, **kw)
+    nat.load_tf_params(params)
+    gold = GoldenDeepFM(V, F, K, layers, keep, params=params, **kw)
+    ln, lg = [], []
+    for s in range(240):
+        ids, vals, lab = synth.batch(B, step=s)
+        gold.train_step(ids, vals, lab)
+        lg.append(gold.last_loss)
+        nat.train_step(ids.to(dev, torch.int32), vals.to(dev), lab.to(dev), use_graph=True)
+        ln.append(nat.loss_value(B))
+    for w in range(0, 240, 40):
+        a, b = np.mean(ln[w:w + 40]), np.mean(lg[w:w + 40])
+        assert abs(a - b) <= 0.02 * b, (w, a, b)
+    assert np.mean(ln[-40:]) < np.mean(ln[:40]) - 0.02           # it actually learned
+    hn = torch.zeros(2, 201, dtype=torch.int64, device=dev)
+    hg = torch.zeros(2, 201, dtype=torch.int64)
+    for s in range(16):
+        ids, vals, lab = synth.batch(B, step=100000 + s)
+        nat.eval_batch(ids.to(dev, torch.int32), vals.to(dev), lab.to(dev), hn)
+        hg += hist_torch(gold.predict(ids, vals), lab)
+    an, ag = auc_from_hist(hn.cpu()), auc_from_hist(hg)
+    assert ag > 0.6 and abs(an - ag) <= 0.005, (an, ag)
