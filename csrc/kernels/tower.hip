@@ -1,7 +1,9 @@
-// Fused deep tower (SURVEY §2.5 rows 7, 9-12, 15-16 "small-N specialization fuses the whole
+// Fused deep tower (SURVEY §2.5 rows 2-7, 9-12, 15-16 "small-N specialization fuses the whole
 // tower, with activations kept in LDS"): for a block of 32 samples ONE workgroup runs
 //
-//   forward   H_i = dropout(relu(H_{i-1} W_i^T + b_i))      i = 0..nl-1   (H_{-1} = E, global)
+//   gather    (K1, optional) E = fm_v[ids] * x, y_w, y_v, S = sum_f E straight into an LDS tile:
+//             E never goes through HBM; E^T (wgrad operand) and S (sparse backward) are written
+//   forward   H_i = dropout(relu(H_{i-1} W_i^T + b_i))      i = 0..nl-1   (H_{-1} = E)
 //   head      y = y_fm + H_last . w_out + b_out, p, loss, dlogit, dZ_last
 //   dgrad     dZ_{i-1} = (dZ_i W_i) (.) [H_{i-1} > 0] / keep   (row-local: needs only this block)
 //             dX0      =  dZ_0 W_0
@@ -62,6 +64,19 @@ struct TowerArgs {
   const float* sE;                // [M]     row dequant factors of E8
   const uint8_t* W8[TW_MAXL];     // [Np_i, Kp_i]
   const float* sW[TW_MAXL];       // [Np_i]  channel dequant factors of W8
+  // fused FM gather (K1 in the prologue; template KE = embedding size, 0 = E read from global):
+  // per slot (b, f) row id = idx[b*F + f] of the table (tv, tw: row strides ldv, ldw)
+  const int* idx;
+  const float* vals;              // [M, F]
+  const float* tv;
+  const float* tw;
+  long ldv, ldw;
+  const float* fm_bias;           // [1]
+  int F;
+  int x_off;                      // LDS element offset of the bf16 E tile [32][K0p + 8]
+  int x8_off;                     // LDS byte offset of the fp8 E tile [32][K0p + 16] (fp8)
+  float* S;                       // [M, K]  sum_f E (sparse backward)
+  bf16* Et;                       // [K0p, M] (train: wgrad operand)
 };
 
 // One wave: c[2][2] += A[32 x 32*nk] . B[32 x 32*nk]^T, both K-contiguous (row strides lda/ldb
@@ -190,7 +205,96 @@ __device__ __forceinline__ void store_tile_t(const bf16* t, int ld, int N, bf16*
   }
 }
 
-template <bool FP8, int TW_PF0, int TW_PF1>
+// FM gather of one 32-sample block (K1): 8 threads per sample, each owning fields q, q+8, ...;
+// E rows go to the bf16 LDS tile (and the fp8 tile), per-sample S / sum E^2 / y_w are summed in
+// registers over the thread's fields, then over its 8 lanes (fixed xor order: deterministic).
+template <bool FP8, int KE>
+__device__ __forceinline__ void tower_gather(const TowerArgs& a, int row0, bf16* Xl, int ldx,
+                                             uint8_t* X8, int ld8, float* s_yfm, float* s_dq0) {
+  constexpr int V4 = KE / 4;
+  constexpr int FMAX = 5;  // fields per thread per pass, all loads in flight (Criteo: 39 <= 40)
+  const int tid = threadIdx.x, sl = tid >> 3, q = tid & 7;
+  const int b = row0 + sl, F = a.F;
+  f32x4 S[V4], Q[V4];
+#pragma unroll
+  for (int j = 0; j < V4; ++j) S[j] = Q[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float yw = 0.f, am = 0.f;
+  bf16* xr = Xl + sl * ldx;
+  for (int f0 = q; f0 < F; f0 += 8 * FMAX) {
+    int id[FMAX];
+    float x[FMAX];
+#pragma unroll
+    for (int t = 0; t < FMAX; ++t) {
+      const int f = f0 + 8 * t;
+      id[t] = f < F ? a.idx[(size_t)b * F + f] : 0;
+      x[t] = f < F ? a.vals[(size_t)b * F + f] : 0.f;
+    }
+    f32x4 v[FMAX][V4];
+    float w[FMAX];
+#pragma unroll
+    for (int t = 0; t < FMAX; ++t) {
+      const bool ok = f0 + 8 * t < F;
+      const f32x4* row = reinterpret_cast<const f32x4*>(a.tv + (size_t)id[t] * a.ldv);
+#pragma unroll
+      for (int j = 0; j < V4; ++j) v[t][j] = ok ? row[j] : f32x4{0.f, 0.f, 0.f, 0.f};
+      w[t] = ok ? a.tw[(size_t)id[t] * a.ldw] : 0.f;
+    }
+#pragma unroll
+    for (int t = 0; t < FMAX; ++t) {
+      const int f = f0 + 8 * t;
+      if (f >= F) break;
+      yw += w[t] * x[t];
+#pragma unroll
+      for (int j = 0; j < V4; ++j) {
+        const f32x4 e = v[t][j] * x[t];
+        S[j] += e;
+        Q[j] += e * e;
+        am = fmaxf(am, fmaxf(fmaxf(fabsf(e[0]), fabsf(e[1])), fmaxf(fabsf(e[2]), fabsf(e[3]))));
+        bf16x4 eh = {f2bf(e[0]), f2bf(e[1]), f2bf(e[2]), f2bf(e[3])};
+        *reinterpret_cast<bf16x4*>(xr + f * KE + 4 * j) = eh;
+      }
+    }
+  }
+  // zero the padding columns [F*K, K0p) of the row
+  for (int c = F * KE + q; c < a.K0p; c += 8) xr[c] = f2bf(0.f);
+#pragma unroll
+  for (int o = 1; o < 8; o <<= 1) {
+#pragma unroll
+    for (int j = 0; j < V4; ++j)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        S[j][c] += __shfl_xor(S[j][c], o, 64);
+        Q[j][c] += __shfl_xor(Q[j][c], o, 64);
+      }
+    yw += __shfl_xor(yw, o, 64);
+    am = fmaxf(am, __shfl_xor(am, o, 64));
+  }
+  float yv = 0.f;
+#pragma unroll
+  for (int j = 0; j < V4; ++j)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) yv += S[j][c] * S[j][c] - Q[j][c];
+  if (q == 0) {
+    s_yfm[sl] = a.fm_bias[0] + yw + 0.5f * yv;
+    if (a.S) {
+#pragma unroll
+      for (int j = 0; j < V4; ++j) *reinterpret_cast<f32x4*>(a.S + (size_t)b * KE + 4 * j) = S[j];
+    }
+  }
+  if (FP8) {  // per-row power-of-two scale of the fp8 layer-0 operand (current scaling)
+    const float qs = fp8_pow2_scale(am);
+    if (q == 0) s_dq0[sl] = 1.f / qs;
+    __syncthreads();  // the bf16 row is complete
+    uint8_t* r8 = X8 + sl * ld8;
+    for (int c4 = q; c4 < a.K0p / 4; c4 += 8) {
+      const bf16* e = xr + 4 * c4;
+      *reinterpret_cast<uint32_t*>(r8 + 4 * c4) =
+          pack4_fp8(bf2f(e[0]) * qs, bf2f(e[1]) * qs, bf2f(e[2]) * qs, bf2f(e[3]) * qs);
+    }
+  }
+}
+
+template <bool FP8, int KE, int TW_PF0, int TW_PF1>
 __global__ void __launch_bounds__(256) tower_kernel(TowerArgs a) {
   extern __shared__ __align__(16) unsigned char tw_lds_raw[];
   bf16* lds = reinterpret_cast<bf16*>(tw_lds_raw);
@@ -198,11 +302,23 @@ __global__ void __launch_bounds__(256) tower_kernel(TowerArgs a) {
   __shared__ float s_loss[TW_ROWS];
   __shared__ float s_q[TW_ROWS];   // fp8: quantization scales of the current H rows
   __shared__ float s_dq[TW_ROWS];  //      and their inverses
+  __shared__ float s_yfm[TW_ROWS];  // gather: y_b + y_w + y_v per sample
+  __shared__ float s_dq0[TW_ROWS];  // gather + fp8: dequant factors of the E rows
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int row0 = blockIdx.x * TW_ROWS;
   const int cr = (lane >> 4) * 4, cc = lane & 15;
   const uint32_t step = (uint32_t)(*a.step);
   const int nl = a.nl;
+  const int ldx = a.K0p + 8, ld8 = a.K0p + 16;
+  bf16* Xl = lds + (KE > 0 ? a.x_off : 0);
+  uint8_t* X8 = tw_lds_raw + (KE > 0 && FP8 ? a.x8_off : 0);
+
+  // ------------------------------------------------------------------ gather (K1)
+  if constexpr (KE > 0) {
+    tower_gather<FP8, KE>(a, row0, Xl, ldx, X8, ld8, s_yfm, s_dq0);
+    __syncthreads();
+    if (a.train) store_tile_t(Xl, ldx, a.K0p, a.Et, a.M, row0);
+  }
 
   // ------------------------------------------------------------------ forward
   for (int i = 0; i < nl; ++i) {
@@ -217,13 +333,17 @@ __global__ void __launch_bounds__(256) tower_kernel(TowerArgs a) {
       f32x4 c00 = {0, 0, 0, 0}, c01 = c00, c10 = c00, c11 = c00;
       if (FP8) {
         const uint8_t* Bw8 = a.W8[i] + (size_t)ct * 32 * Kp;
-        if (i == 0)
+        if (i == 0 && KE > 0)
+          mma32_f8<4>(X8, ld8, Bw8, Kp, Kp / 32, lane, c00, c01, c10, c11);
+        else if (i == 0)
           mma32_f8<4>(a.E8 + (size_t)row0 * a.K0p, a.K0p, Bw8, Kp, Kp / 32, lane, c00, c01, c10, c11);
         else
           mma32_f8_lds(lds + a.h_off[i - 1], Kp + 8, s_q, Bw8, Kp, Kp / 32, lane, c00, c01, c10, c11);
       } else {
         const bf16* Bw = a.W[i] + (size_t)ct * 32 * Kp;
-        if (i == 0)
+        if (i == 0 && KE > 0)
+          mma32<TW_PF0>(Xl, ldx, Bw, Kp, Kp / 32, lane, c00, c01, c10, c11);
+        else if (i == 0)
           mma32<TW_PF0>(a.E + (size_t)row0 * a.K0p, a.K0p, Bw, Kp, Kp / 32, lane, c00, c01, c10, c11);
         else
           mma32<TW_PF1>(lds + a.h_off[i - 1], Kp + 8, Bw, Kp, Kp / 32, lane, c00, c01, c10, c11);
@@ -239,7 +359,7 @@ __global__ void __launch_bounds__(256) tower_kernel(TowerArgs a) {
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             const int row = ti * 16 + cr + j;
-            const float dq = FP8 ? dqc * (i == 0 ? a.sE[row0 + row] : s_dq[row]) : 1.f;
+            const float dq = FP8 ? dqc * (i == 0 ? (KE > 0 ? s_dq0[row] : a.sE[row0 + row]) : s_dq[row]) : 1.f;
             float v = fmaxf(acc[ti][tj][j] * dq + bc, 0.f);
             if (drop)
               v = dropout_keep((uint32_t)((row0 + row) * N + col), salt, a.keep_thr[i]) ? v * sc : 0.f;
@@ -278,7 +398,7 @@ __global__ void __launch_bounds__(256) tower_kernel(TowerArgs a) {
     yd += __shfl_xor(yd, 1, 64);
     yd += __shfl_xor(yd, 2, 64);
     yd += __shfl_xor(yd, 4, 64);
-    const float y = a.y_fm[grow] + yd + a.b_out[0];
+    const float y = (KE > 0 ? s_yfm[row] : a.y_fm[grow]) + yd + a.b_out[0];
     const float p = 1.f / (1.f + __expf(-y));
     float dl = 0.f, lossb = 0.f;
     if (a.labels && grow < a.nvalid) {
@@ -380,20 +500,41 @@ __global__ void __launch_bounds__(256) tower_kernel(TowerArgs a) {
   }
 }
 
-HFM_API int hfm_tower(const TowerArgs* ap, hipStream_t st) {
+template <bool FP8>
+static int tower_launch(const TowerArgs& a, int KE, hipStream_t st) {
+  const dim3 g(a.M / TW_ROWS), blk(256);
+  switch (KE) {
+    case 0: hipLaunchKernelGGL((tower_kernel<FP8, 0, 4, 2>), g, blk, a.lds_bytes, st, a); break;
+    case 4: hipLaunchKernelGGL((tower_kernel<FP8, 4, 4, 2>), g, blk, a.lds_bytes, st, a); break;
+    case 8: hipLaunchKernelGGL((tower_kernel<FP8, 8, 4, 2>), g, blk, a.lds_bytes, st, a); break;
+    case 16: hipLaunchKernelGGL((tower_kernel<FP8, 16, 4, 2>), g, blk, a.lds_bytes, st, a); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+  return 0;
+}
+
+// KE: embedding size of the fused gather (4, 8 or 16), or 0 when E comes from fm_fwd (global)
+HFM_API int hfm_tower(const TowerArgs* ap, int KE, hipStream_t st) {
   const TowerArgs& a = *ap;
   if (a.M % TW_ROWS || a.nl < 1 || a.nl > TW_MAXL || a.K0p % 32) return (int)hipErrorInvalidValue;
   for (int i = 0; i < a.nl; ++i)
     if (a.Np[i] % 32 || a.Np[i] <= 0) return (int)hipErrorInvalidValue;
   if (a.Np[a.nl - 1] % 8) return (int)hipErrorInvalidValue;
   if (a.lds_bytes > 160 * 1024 - 1024) return (int)hipErrorInvalidValue;
+  if (KE) {
+    if (!a.idx || !a.vals || !a.tv || !a.tw || !a.fm_bias || a.F * KE > a.K0p || a.x_off < 0 ||
+        (a.train && !a.Et) || (a.fp8 && a.x8_off < 0) || (a.ldv & 3))
+      return (int)hipErrorInvalidValue;
+  }
   if (a.fp8) {
-    if (!a.E8 || !a.sE) return (int)hipErrorInvalidValue;
+    if (!KE && (!a.E8 || !a.sE)) return (int)hipErrorInvalidValue;
     for (int i = 0; i < a.nl; ++i)
       if (!a.W8[i] || !a.sW[i]) return (int)hipErrorInvalidValue;
-    hipLaunchKernelGGL((tower_kernel<true, 4, 2>), dim3(a.M / TW_ROWS), dim3(256), a.lds_bytes, st, a);
+    const int rc = tower_launch<true>(a, KE, st);
+    if (rc) return rc;
   } else {
-    hipLaunchKernelGGL((tower_kernel<false, 4, 2>), dim3(a.M / TW_ROWS), dim3(256), a.lds_bytes, st, a);
+    const int rc = tower_launch<false>(a, KE, st);
+    if (rc) return rc;
   }
   HFM_LAUNCH_CHECK();
 }

@@ -47,6 +47,7 @@ _FUSE_FIN_OPT = os.environ.get("HIPFM_FUSE_FIN_OPT", "1") == "1"  # dense optimi
 _SPARSE_IMPL = os.environ.get("HIPFM_SPARSE", "fused")             # fused | seg
 _SHARD_PIPELINE = os.environ.get("HIPFM_SHARD_PIPELINE", "1") == "1"
 _DENSE_SIDE_STREAM = os.environ.get("HIPFM_DENSE_SIDE_STREAM", "auto")   # auto | 1 | 0
+_TOWER_GATHER = os.environ.get("HIPFM_TOWER_GATHER", "1") == "1"   # FM gather fused into the tower
 
 
 def check_field_ranges(ranges, F: int, V: int) -> List[Tuple[int, int]]:
@@ -296,6 +297,11 @@ class NativeDeepFM:
                     self._tower_lds_bytes() <= 150 * 1024)
         want = os.environ.get("HIPFM_FUSED_TOWER", "1") != "0" if fused is None else bool(fused)
         self.fused = can_fuse and want
+        # the FM gather (K1) as the fused tower's prologue: E goes straight into the tower's LDS
+        # tile (no fm_fwd launch, no E round trip through HBM)
+        self.gather_fused = self.fused and _TOWER_GATHER and self.K in (4, 8, 16)
+        if self.gather_fused and self._tower_lds_bytes() > 150 * 1024:
+            self.gather_fused = False
         if self.fp8 and not self.fused:
             raise ValueError("mlp_dtype=fp8 runs on the fused tower kernel (no batch norm, "
                              "activations within LDS)")
@@ -343,10 +349,28 @@ class NativeDeepFM:
                 for t in (self.sv[0], self.sv[2], self.sd[0]):
                     t.fill_(init)
 
+    def _tower_lds_layout(self):
+        """(H tile offsets, dZ tile offsets, bf16 E tile offset, fp8 E tile byte offset, bytes):
+        H tiles, then the dZ region -- which also holds the gathered bf16 E tile, dead before the
+        first dZ tile is written -- then (fp8 + gather) the fp8 E tile."""
+        off, h_off = 0, []
+        for n in self.Np:
+            h_off.append(off)
+            off += 32 * (n + 8)
+        dz = 32 * (max(self.Np) + 8)
+        gather = getattr(self, "gather_fused", False)
+        region = max(2 * dz, 32 * (self.K0p + 8) if gather else 0)
+        dz_off = [off, off + dz]
+        x_off = off if gather else -1
+        nbytes = 2 * (off + region)
+        x8_off = -1
+        if gather and self.fp8:
+            x8_off = (nbytes + 15) // 16 * 16
+            nbytes = x8_off + 32 * (self.K0p + 16)
+        return h_off, dz_off, x_off, x8_off, nbytes
+
     def _tower_lds_bytes(self) -> int:
-        """H tiles + two dZ tiles (bf16, rows padded by 8 elements)."""
-        h = sum(32 * (n + 8) * 2 for n in self.Np)
-        return h + 2 * 32 * (max(self.Np) + 8) * 2
+        return self._tower_lds_layout()[4]
 
     @staticmethod
     def _padM(B: int) -> int:
@@ -549,12 +573,13 @@ class NativeDeepFM:
         self._nwg_jobs = len(jobs)
         self._wg_tasks = task0
 
-    def _tower_args(self, B: int, train: bool, with_labels: bool = True) -> TowerArgs:
+    def _tower_args(self, B: int, train: bool, with_labels: bool = True, gather=None) -> TowerArgs:
+        """``gather`` = (idx, tv, tw): the tower's prologue gathers the FM rows itself."""
         a = TowerArgs()
         nl = len(self.layers)
         a.M, a.nvalid, a.nl, a.K0p = self.M, B, nl, self.K0p
         pb = self.p.data_ptr()
-        off = 0
+        h_off, dz_off, x_off, x8_off, nbytes = self._tower_lds_layout()
         for i in range(nl):
             a.Np[i] = self.Np[i]
             a.W[i] = self.W16[i].data_ptr()
@@ -566,15 +591,24 @@ class NativeDeepFM:
             a.drop[i] = 1 if keep < 1.0 else 0
             a.Ht[i] = self.Ht[i].data_ptr()
             a.dZt[i] = self.dZt[i].data_ptr()
-            a.h_off[i] = off
-            off += 32 * (self.Np[i] + 8)
-        a.dz_off[0] = off
-        a.dz_off[1] = off + 32 * (max(self.Np) + 8)
-        a.lds_bytes = self._tower_lds_bytes()
-        a.E = self.E.data_ptr()
+            a.h_off[i] = h_off[i]
+        a.dz_off[0], a.dz_off[1] = dz_off
+        a.lds_bytes = nbytes
+        a.x_off, a.x8_off = x_off, x8_off
+        if gather is not None:
+            idx, tv, tw = gather
+            a.idx, a.vals, a.tv, a.tw = idx.data_ptr(), self.vals.data_ptr(), tv.data_ptr(), tw.data_ptr()
+            a.ldv, a.ldw = KN._ld(tv, tw)
+            a.fm_bias = pb + 4 * self.dense_segs["fm_bias"].off
+            a.F = self.F
+            a.S = self.S.data_ptr()
+            a.Et = self.Et.data_ptr() if train else 0
+        else:
+            a.E = self.E.data_ptr()
         if self.fp8:
             a.fp8 = 1
-            a.E8, a.sE = self.E8.data_ptr(), self.sE.data_ptr()
+            if gather is None:
+                a.E8, a.sE = self.E8.data_ptr(), self.sE.data_ptr()
             for i in range(nl):
                 a.W8[i], a.sW[i] = self.W8[i].data_ptr(), self.sW[i].data_ptr()
         a.seed = self.seed & 0xFFFFFFFF
@@ -597,6 +631,15 @@ class NativeDeepFM:
         for the FM backward).  Returns the (idx, table) pair the sparse backward uses.
         ``defer_wgrad``: stop after the fused tower (the caller runs wgrad + finalize).
         ``after_fm``: hook called once the FM forward is enqueued."""
+        if self.fused and self.gather_fused:
+            idx, tv, tw = self._fm_inputs(B, train=True)
+            KN.tower(self._tower_args(B, train=True, gather=(idx, tv, tw)), KE=self.K)
+            if after_fm is not None:
+                after_fm()
+            if not defer_wgrad:
+                KN.wgrad_group(self._wg_jobs, self._nwg_jobs, self._wg_tasks)
+                self._finalize_grads()
+            return idx, tv
         if self.fused:
             idx, tv = self._fm_forward(B, train=True)
             if after_fm is not None:
@@ -706,14 +749,18 @@ class NativeDeepFM:
         return B
 
     # ------------------------------------------------------------------ forward pieces
+    def _fm_inputs(self, B: int, train: bool):
+        """(slot -> row index, fm_v rows, fm_w rows) the FM gather reads: the local tables, or the
+        rows fetched from their owners (row-sharded)."""
+        if self.shx is not None:
+            return self.shx.fetch(self._shx_plan, train)
+        if self.sharded:
+            return self.comm.sharded_forward_gather(self, B)
+        return self.idx, self.tv, self.tw
+
     def _fm_forward(self, B: int, train: bool):
         M, F, K = self.M, self.F, self.K
-        idx = self.idx
-        tv, tw = self.tv, self.tw
-        if self.shx is not None:
-            idx, tv, tw = self.shx.fetch(self._shx_plan, train)
-        elif self.sharded:
-            idx, tv, tw = self.comm.sharded_forward_gather(self, B)
+        idx, tv, tw = self._fm_inputs(B, train)
         fm_bias = self.p[self.dense_segs["fm_bias"].off:]
         # the side-stream field sort forked after this launch reads the ids field-major from it
         ib = self._idsT_B if train else 0
@@ -1022,7 +1069,8 @@ class NativeDeepFM:
 
             # fm_fwd writes the ids field-major as it reads them, so the forked sort skips its
             # transpose launch (the sort branch is the step's critical path)
-            pre = (_FWD_IDST and self.uses_field_sort(B) and KN.fm_fwd_writes_idsT(self.F, self.K))
+            pre = (_FWD_IDST and not self.gather_fused and self.uses_field_sort(B) and
+                   KN.fm_fwd_writes_idsT(self.F, self.K))
             self._idsT_B = B if pre else 0
 
             def fork_sort():
@@ -1328,6 +1376,10 @@ class NativeDeepFM:
         self._predict_body(B, with_labels)
 
     def _predict_body(self, B: int, with_labels: bool):
+        if self.fused and self.gather_fused:
+            g = self._fm_inputs(B, train=False)
+            KN.tower(self._tower_args(B, train=False, with_labels=with_labels, gather=g), KE=self.K)
+            return
         if self.fused:
             self._fm_forward(B, train=False)
             KN.tower(self._tower_args(B, train=False, with_labels=with_labels))

@@ -116,7 +116,10 @@ class TowerArgs(C.Structure):
                 ("prob", c_void_p), ("dlogit", c_void_p), ("partial", c_void_p),
                 ("h_off", c_int * TW_MAXL), ("dz_off", c_int * 2), ("lds_bytes", c_int),
                 ("fp8", c_int), ("E8", c_void_p), ("sE", c_void_p), ("W8", c_void_p * TW_MAXL),
-                ("sW", c_void_p * TW_MAXL)]
+                ("sW", c_void_p * TW_MAXL),
+                ("idx", c_void_p), ("vals", c_void_p), ("tv", c_void_p), ("tw", c_void_p),
+                ("ldv", c_long), ("ldw", c_long), ("fm_bias", c_void_p), ("F", c_int),
+                ("x_off", c_int), ("x8_off", c_int), ("S", c_void_p), ("Et", c_void_p)]
 
 
 class W8Job(C.Structure):
@@ -200,7 +203,7 @@ _SIGS = {
     "hfm_seg_apply": [c_int, c_int, c_int, C.POINTER(SegApplyArgs), c_int, c_void_p],
     "hfm_seg_apply_args_bytes": [],
     "hfm_bn": [c_int, C.POINTER(BnArgs), c_void_p],
-    "hfm_tower": [C.POINTER(TowerArgs), c_void_p],
+    "hfm_tower": [C.POINTER(TowerArgs), c_int, c_void_p],
     "hfm_tower_args_bytes": [],
     "hfm_wgrad_group": [c_void_p, c_int, c_int, c_void_p],
     "hfm_wg_job_bytes": [],

@@ -291,9 +291,10 @@ def head(a: HeadArgs):
     check(L().hfm_head(C.byref(a), stream_handle()), "head")
 
 
-def tower(a: TowerArgs):
-    """Fused deep tower: forward + head (+ dgrad chain when a.train) (csrc/kernels/tower.hip)."""
-    check(L().hfm_tower(C.byref(a), stream_handle()), "tower")
+def tower(a: TowerArgs, KE: int = 0):
+    """Fused deep tower: [FM gather (KE = embedding size) +] forward + head (+ dgrad chain when
+    a.train) (csrc/kernels/tower.hip)."""
+    check(L().hfm_tower(C.byref(a), int(KE), stream_handle()), "tower")
 
 
 def w8_quant(jobs_dev, njobs: int, total_rows: int):
