@@ -59,8 +59,11 @@ __global__ void __launch_bounds__(256) fs_transpose_kernel(const int* __restrict
   }
 }
 
-// fr: per field {lo, hi, bits, pb}; work: per workgroup {field, partition}
-__global__ void __launch_bounds__(FS_THREADS) fs_sort_kernel(const int* __restrict__ idsT, int B, int F,
+// fr: per field {lo, hi, bits, pb}; work: per workgroup {field, partition}.  Row b of field f is
+// read at ids[f * fstride + b * rstride]: (B, 1) for field-major ids, (1, F) for the [B, F] batch
+// itself (no transpose launch: strided reads, for a sort that runs off the critical path).
+__global__ void __launch_bounds__(FS_THREADS) fs_sort_kernel(const int* __restrict__ ids, int B, int F,
+                                                            int fstride, int rstride,
                                                             const int* __restrict__ fr,
                                                             const int* __restrict__ work,
                                                             int* __restrict__ sorted_keys,
@@ -80,11 +83,11 @@ __global__ void __launch_bounds__(FS_THREADS) fs_sort_kernel(const int* __restri
   const unsigned long long lt = (1ull << lane) - 1ull;
   int* sko = sorted_keys + (size_t)f * B;
   int* pko = perm + (size_t)f * B;
-  const int* src = idsT + (size_t)f * B;
+  const int* src = ids + (size_t)f * fstride;
   bool bad = false;
   if (bits == 0) {
     for (int b = tid; b < B; b += FS_THREADS) {
-      const int id = src[b];
+      const int id = src[(size_t)b * rstride];
       bad |= id != lo;
       sko[b] = id;
       pko[b] = b * F + f;
@@ -103,7 +106,7 @@ __global__ void __launch_bounds__(FS_THREADS) fs_sort_kernel(const int* __restri
     key[k] = 0u;
     int kp = 1 << 30;
     if (p < B) {
-      const int id = src[p];
+      const int id = src[(size_t)p * rstride];
       bad |= (id < lo) | (id >= hi);
       key[k] = (unsigned)(id - lo) & ((1u << bits) - 1u);
       kp = (int)(key[k] >> rb);
@@ -253,7 +256,17 @@ HFM_API int hfm_field_sort(const int* ids, int B, int F, const int* fr_dev, cons
   if (B <= 0 || F <= 0) return 0;
   if (B > FS_MAXB) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(fs_transpose_kernel, dim3((B + 63) / 64), dim3(256), 0, st, ids, B, F, idsT);
-  hipLaunchKernelGGL(fs_sort_kernel, dim3(nwork), dim3(FS_THREADS), FS_LDS, st, idsT, B, F, fr_dev,
+  hipLaunchKernelGGL(fs_sort_kernel, dim3(nwork), dim3(FS_THREADS), FS_LDS, st, idsT, B, F, B, 1, fr_dev,
+                     work_dev, sorted_keys, perm, err);
+  HFM_LAUNCH_CHECK();
+}
+
+// One launch, straight from the row-major [B, F] ids (no transpose kernel, strided reads).
+HFM_API int hfm_field_sort_rowmajor(const int* ids, int B, int F, const int* fr_dev, const int* work_dev,
+                                    int nwork, int* sorted_keys, int* perm, unsigned* err, hipStream_t st) {
+  if (B <= 0 || F <= 0) return 0;
+  if (B > FS_MAXB) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(fs_sort_kernel, dim3(nwork), dim3(FS_THREADS), FS_LDS, st, ids, B, F, 1, F, fr_dev,
                      work_dev, sorted_keys, perm, err);
   HFM_LAUNCH_CHECK();
 }
@@ -263,7 +276,7 @@ HFM_API int hfm_field_sort_pre(const int* idsT, int B, int F, const int* fr_dev,
                                int nwork, int* sorted_keys, int* perm, unsigned* err, hipStream_t st) {
   if (B <= 0 || F <= 0) return 0;
   if (B > FS_MAXB) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(fs_sort_kernel, dim3(nwork), dim3(FS_THREADS), FS_LDS, st, idsT, B, F, fr_dev,
+  hipLaunchKernelGGL(fs_sort_kernel, dim3(nwork), dim3(FS_THREADS), FS_LDS, st, idsT, B, F, B, 1, fr_dev,
                      work_dev, sorted_keys, perm, err);
   HFM_LAUNCH_CHECK();
 }

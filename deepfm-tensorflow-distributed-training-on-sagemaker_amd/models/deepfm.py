@@ -33,7 +33,8 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import torch
 
 from ..ops import kernels as KN
-from ..ops._lib import TW_MAXL, BnArgs, EpiArgs, HeadArgs, TowerArgs, W8Job, WgJob, RowSumJob, SegApplyArgs, SfArgs, ShadowSeg, SlabJob
+from ..ops._lib import (TW_MAXL, BnArgs, EpiArgs, FinOpt, HeadArgs, TowerArgs, W8Job, WgFinArgs, WgFinJob,
+                        WgJob, RowSumJob, SegApplyArgs, SfArgs, ShadowSeg, SlabJob)
 from ..utils.rng import keep_threshold
 from .reference import glorot_std, init_params, pad32
 
@@ -48,6 +49,15 @@ _SPARSE_IMPL = os.environ.get("HIPFM_SPARSE", "fused")             # fused | seg
 _SHARD_PIPELINE = os.environ.get("HIPFM_SHARD_PIPELINE", "1") == "1"
 _DENSE_SIDE_STREAM = os.environ.get("HIPFM_DENSE_SIDE_STREAM", "auto")   # auto | 1 | 0
 _TOWER_GATHER = os.environ.get("HIPFM_TOWER_GATHER", "1") == "1"   # FM gather fused into the tower
+# weight gradients + split-K combine + bias/head reductions + dense optimizer in one launch
+_WGFIN = os.environ.get("HIPFM_WGFIN", "1") == "1"
+# where the next batch's sort branch is enqueued in the step's capture order (graph branches are
+# dispatched in capture order): tower | fin | end | start -- same-box sweep: 0.1318 / 0.1316 /
+# 0.1351 / 0.1365 ms/step
+_SORT_NEXT_AT = os.environ.get("HIPFM_SORT_NEXT_AT", "tower")
+# one-launch sort from the row-major ids (strided reads): measured slower than transpose + sort
+# (0.141 vs 0.132 ms/step), so off by default
+_SORT_NEXT_ROWMAJOR = os.environ.get("HIPFM_SORT_NEXT_ROWMAJOR", "0") == "1"
 
 
 def check_field_ranges(ranges, F: int, V: int) -> List[Tuple[int, int]]:
@@ -464,6 +474,7 @@ class NativeDeepFM:
         self._build_finalize_jobs()
         if self.fused:
             self._build_wgrad_jobs()
+            self._build_wgfin()
         self._bufs_M = M
         self.shx = None
         if self.sharded and getattr(self.comm, "engine", None) is not None:
@@ -554,6 +565,71 @@ class NativeDeepFM:
             need[s.off:s.off + int(torch.Size(s.shape).numel())] = True
         self._fin_covers_all = bool(cov[need].all()) and not self.batch_norm
 
+    def _build_wgfin(self):
+        """wgfin_kernel configuration (tower.hip): NS workgroup splits of the batch per 32x32
+        output tile, 4 waves each; slabs, bias slabs, arrival counters."""
+        M, dev = self.M, self.device
+        f32 = dict(dtype=torch.float32, device=dev)
+        ns = 8
+        while ns > 1 and (M % (ns * 4 * 32) or M // (ns * 4) < 32):
+            ns //= 2
+        self._wgfin_ns = ns
+        self.wf_slabs, self.wf_bslabs, jobs = [], [], []
+        tile0 = wg0 = 0
+        g0 = self.g.data_ptr()
+        for i in range(len(self.layers)):
+            Np, Kp = self.Np[i], self.Kp[i]
+            sl = torch.zeros(ns, Np, Kp, **f32)
+            bsl = torch.zeros(ns, Np, **f32)
+            self.wf_slabs.append(sl)
+            self.wf_bslabs.append(bsl)
+            Xt = self.Et if i == 0 else self.Ht[i - 1]
+            j = WgFinJob()
+            j.A, j.B, j.slab, j.bslab = self.dZt[i].data_ptr(), Xt.data_ptr(), sl.data_ptr(), bsl.data_ptr()
+            j.gw = g0 + 4 * self.dense_segs[f"Deep-part/mlp{i}/weights"].off
+            j.gb = g0 + 4 * self.dense_segs[f"Deep-part/mlp{i}/biases"].off
+            j.M, j.N, j.tiles_m, j.tiles_n = Np, Kp, Np // 32, Kp // 32
+            j.tile0, j.wg0 = tile0, wg0
+            tile0 += j.tiles_m * j.tiles_n
+            wg0 += j.tiles_m * j.tiles_n * ns
+            jobs.append(j)
+        self._wgfin_jobs = KN.struct_array_to_device(jobs, dev)
+        self._wgfin_ntiles, self._wgfin_wgs = tile0, wg0
+        self.wf_tile_ctr = torch.zeros(max(1, tile0), dtype=torch.int32, device=dev)
+        self.wf_done_ctr = torch.zeros(1, dtype=torch.int32, device=dev)
+
+    def _wgfin_args(self, with_opt: bool) -> WgFinArgs:
+        a = WgFinArgs()
+        a.jobs, a.njobs = self._wgfin_jobs.data_ptr(), len(self.layers)
+        a.ldk, a.ns = self.M, self._wgfin_ns
+        a.kchunk = self.M // (a.ns * 4)
+        a.tile_wgs = self._wgfin_wgs
+        a.tile_ctr, a.done_ctr = self.wf_tile_ctr.data_ptr(), self.wf_done_ctr.data_ptr()
+        a.partial, a.nhead, a.L = self.partial.data_ptr(), self.nhead, self.Np[-1]
+        g0 = self.g.data_ptr()
+        a.g_wout = g0 + 4 * self.dense_segs["Deep-part/deep_out/weights"].off
+        a.g_bout = g0 + 4 * self.dense_segs["Deep-part/deep_out/biases"].off
+        a.g_fmbias = g0 + 4 * self.dense_segs["fm_bias"].off
+        a.loss_sum = self.loss_sum.data_ptr()
+        o = FinOpt()
+        o.p, o.g, o.s0, o.s1, o.n = (self.p.data_ptr(), g0, self.sd[0].data_ptr() if self.sd[0].numel() else 0,
+                                     self.sd[1].data_ptr() if self.sd[1].numel() else 0, self.P)
+        o.h = self.h_dense
+        o.step = self.step.data_ptr()
+        o.segs, o.nseg = self._shadow_dev.data_ptr(), self._nshadow
+        a.o = o
+        a.opt_on = 1 if with_opt else 0
+        return a
+
+    def _dense_grads(self):
+        """Weight / bias / head gradients of the fused tower (+ the dense optimizer when this step
+        fuses it): one wgfin launch, or wgrad_group + finalize (HIPFM_WGFIN=0)."""
+        if _WGFIN:
+            KN.wgfin(self.opt_id if self._fuse_opt else -1, self._wgfin_args(self._fuse_opt))
+            return
+        KN.wgrad_group(self._wg_jobs, self._nwg_jobs, self._wg_tasks)
+        self._finalize_grads()
+
     def _build_wgrad_jobs(self):
         jobs, task0 = [], 0
         M = self.M
@@ -637,8 +713,7 @@ class NativeDeepFM:
             if after_fm is not None:
                 after_fm()
             if not defer_wgrad:
-                KN.wgrad_group(self._wg_jobs, self._nwg_jobs, self._wg_tasks)
-                self._finalize_grads()
+                self._dense_grads()
             return idx, tv
         if self.fused:
             idx, tv = self._fm_forward(B, train=True)
@@ -646,8 +721,7 @@ class NativeDeepFM:
                 after_fm()
             KN.tower(self._tower_args(B, train=True))
             if not defer_wgrad:
-                KN.wgrad_group(self._wg_jobs, self._nwg_jobs, self._wg_tasks)
-                self._finalize_grads()
+                self._dense_grads()
             return idx, tv
         idx, tv = self._forward(B, train=True)
         if after_fm is not None:
@@ -1047,6 +1121,7 @@ class NativeDeepFM:
         prefetch = plan is not None and plan[2] is not None
         inline = plan is None or plan[1]
         main = torch.cuda.current_stream(self.device)
+        late_sort = None
         if prefetch:
             # the next batch's sort: a ROOT branch of the step's graph (no dependency on this
             # step's kernels), enqueued after fm_fwd so the first kernel is launched first; it
@@ -1059,8 +1134,15 @@ class NativeDeepFM:
 
             def sort_next():
                 with torch.cuda.stream(self._side_next):
-                    self._fsort_next(nk_ids, nk_B, nxt_keys, nxt_perm)
-            after_fm = sort_next
+                    if _SORT_NEXT_ROWMAJOR:
+                        self._fsort_next.sort_rowmajor(nk_ids, nk_B, nxt_keys, nxt_perm)
+                    else:
+                        self._fsort_next(nk_ids, nk_B, nxt_keys, nxt_perm)
+            if _SORT_NEXT_AT == "start":
+                sort_next()
+            elif _SORT_NEXT_AT == "tower":
+                after_fm = sort_next
+            late_sort = sort_next if _SORT_NEXT_AT in ("fin", "end") else None
         if not inline:
             presorted = True            # sorted during the previous step
         elif not self.sharded and _SORT_SIDE_STREAM:
@@ -1120,6 +1202,8 @@ class NativeDeepFM:
             self._dense_opt()
         if presorted and inline:
             main.wait_stream(self._side)
+        if late_sort is not None and _SORT_NEXT_AT == "fin":
+            late_sort()
         work = None
         eng = getattr(self.comm, "engine_dense", None) if self.exchange else None
         if split or eng is not None:
@@ -1129,8 +1213,7 @@ class NativeDeepFM:
             self._comm_stream.wait_stream(main)
             with torch.cuda.stream(self._comm_stream):
                 if split:
-                    KN.wgrad_group(self._wg_jobs, self._nwg_jobs, self._wg_tasks)
-                    self._finalize_grads()
+                    self._dense_grads()
                 if eng is not None:
                     eng.allreduce_(self.g)
                 elif self.exchange:
@@ -1148,6 +1231,8 @@ class NativeDeepFM:
             self.shx.end(self._shx_plan)
         if not self._dense_early:
             self._dense_opt()
+        if late_sort is not None and _SORT_NEXT_AT == "end":
+            late_sort()
         if prefetch:
             main.wait_stream(self._side_next)
 

@@ -67,6 +67,26 @@ class ShadowSeg(C.Structure):
                 ("wt16", c_void_p)]
 
 
+class FinOpt(C.Structure):
+    _fields_ = [("p", c_void_p), ("g", c_void_p), ("s0", c_void_p), ("s1", c_void_p), ("n", c_long),
+                ("h", OptHyper), ("step", c_void_p), ("segs", c_void_p), ("nseg", c_int),
+                ("done_ctr", c_void_p)]
+
+
+class WgFinJob(C.Structure):
+    _fields_ = [("A", c_void_p), ("B", c_void_p), ("slab", c_void_p), ("bslab", c_void_p),
+                ("gw", c_void_p), ("gb", c_void_p), ("M", c_int), ("N", c_int), ("tiles_m", c_int),
+                ("tiles_n", c_int), ("tile0", c_int), ("wg0", c_int)]
+
+
+class WgFinArgs(C.Structure):
+    _fields_ = [("jobs", c_void_p), ("njobs", c_int), ("ldk", c_int), ("kchunk", c_int), ("ns", c_int),
+                ("tile_wgs", c_int), ("tile_ctr", c_void_p), ("done_ctr", c_void_p),
+                ("partial", c_void_p), ("nhead", c_int), ("L", c_int), ("g_wout", c_void_p),
+                ("g_bout", c_void_p), ("g_fmbias", c_void_p), ("loss_sum", c_void_p), ("o", FinOpt),
+                ("opt_on", c_int)]
+
+
 class SegApplyArgs(C.Structure):
     _fields_ = [("sorted_keys", c_void_p), ("ukeys", c_void_p), ("seg_start", c_void_p),
                 ("num", c_void_p), ("n", c_int), ("ntiles", c_int), ("compact", c_int),
@@ -197,6 +217,7 @@ _SIGS = {
     "hfm_field_sort_max_pb": [],
     "hfm_field_sort": [c_void_p, c_int, c_int, c_void_p, c_void_p, c_int] + [c_void_p] * 4 + [c_void_p],
     "hfm_field_sort_pre": [c_void_p, c_int, c_int, c_void_p, c_void_p, c_int] + [c_void_p] * 3 + [c_void_p],
+    "hfm_field_sort_rowmajor": [c_void_p, c_int, c_int, c_void_p, c_void_p, c_int] + [c_void_p] * 3 + [c_void_p],
     "hfm_radix_sort_ids": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_size_t, c_void_p],
     "hfm_segments": [c_void_p, c_int] + [c_void_p] * 5 + [c_void_p, c_size_t, c_void_p],
     "hfm_fm_bwd_seg": [c_int] + [c_void_p] * 7 + [c_int, c_int, c_int, c_void_p, c_void_p, c_void_p],
@@ -204,6 +225,9 @@ _SIGS = {
     "hfm_seg_apply_args_bytes": [],
     "hfm_bn": [c_int, C.POINTER(BnArgs), c_void_p],
     "hfm_tower": [C.POINTER(TowerArgs), c_int, c_void_p],
+    "hfm_wgfin": [c_int, C.POINTER(WgFinArgs), c_void_p],
+    "hfm_wgfin_job_bytes": [],
+    "hfm_wgfin_args_bytes": [],
     "hfm_tower_args_bytes": [],
     "hfm_wgrad_group": [c_void_p, c_int, c_int, c_void_p],
     "hfm_wg_job_bytes": [],
@@ -244,6 +268,7 @@ def get_lib():
                            ("hfm_shadow_seg_bytes", ShadowSeg), ("hfm_opt_hyper_bytes", OptHyper),
                            ("hfm_seg_apply_args_bytes", SegApplyArgs), ("hfm_bn_args_bytes", BnArgs),
                            ("hfm_tower_args_bytes", TowerArgs), ("hfm_wg_job_bytes", WgJob),
+                           ("hfm_wgfin_job_bytes", WgFinJob), ("hfm_wgfin_args_bytes", WgFinArgs),
                            ("hfm_w8_job_bytes", W8Job),
                            ("hfm_sparse_fused_args_bytes", SfArgs),
                            ("hfm_sh_apply_args_bytes", ShApplyArgs)):
