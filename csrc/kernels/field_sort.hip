@@ -261,16 +261,6 @@ HFM_API int hfm_field_sort(const int* ids, int B, int F, const int* fr_dev, cons
   HFM_LAUNCH_CHECK();
 }
 
-// One launch, straight from the row-major [B, F] ids (no transpose kernel, strided reads).
-HFM_API int hfm_field_sort_rowmajor(const int* ids, int B, int F, const int* fr_dev, const int* work_dev,
-                                    int nwork, int* sorted_keys, int* perm, unsigned* err, hipStream_t st) {
-  if (B <= 0 || F <= 0) return 0;
-  if (B > FS_MAXB) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(fs_sort_kernel, dim3(nwork), dim3(FS_THREADS), FS_LDS, st, ids, B, F, 1, F, fr_dev,
-                     work_dev, sorted_keys, perm, err);
-  HFM_LAUNCH_CHECK();
-}
-
 // Same sort from ids the FM forward already wrote field-major (hfm_fm_fwd's idsT): one launch.
 HFM_API int hfm_field_sort_pre(const int* idsT, int B, int F, const int* fr_dev, const int* work_dev,
                                int nwork, int* sorted_keys, int* perm, unsigned* err, hipStream_t st) {

@@ -51,13 +51,6 @@ _DENSE_SIDE_STREAM = os.environ.get("HIPFM_DENSE_SIDE_STREAM", "auto")   # auto 
 _TOWER_GATHER = os.environ.get("HIPFM_TOWER_GATHER", "1") == "1"   # FM gather fused into the tower
 # weight gradients + split-K combine + bias/head reductions + dense optimizer in one launch
 _WGFIN = os.environ.get("HIPFM_WGFIN", "1") == "1"
-# where the next batch's sort branch is enqueued in the step's capture order (graph branches are
-# dispatched in capture order): tower | fin | end | start -- same-box sweep: 0.1318 / 0.1316 /
-# 0.1351 / 0.1365 ms/step
-_SORT_NEXT_AT = os.environ.get("HIPFM_SORT_NEXT_AT", "tower")
-# one-launch sort from the row-major ids (strided reads): measured slower than transpose + sort
-# (0.141 vs 0.132 ms/step), so off by default
-_SORT_NEXT_ROWMAJOR = os.environ.get("HIPFM_SORT_NEXT_ROWMAJOR", "0") == "1"
 
 
 def check_field_ranges(ranges, F: int, V: int) -> List[Tuple[int, int]]:
@@ -570,7 +563,8 @@ class NativeDeepFM:
         output tile, 4 waves each; slabs, bias slabs, arrival counters."""
         M, dev = self.M, self.device
         f32 = dict(dtype=torch.float32, device=dev)
-        ns = 8
+        # 4 workgroup splits x 4 waves: same-box A/B 0.1214 (4) / 0.1228 (8) / 0.126 (16) ms/step
+        ns = 4
         while ns > 1 and (M % (ns * 4 * 32) or M // (ns * 4) < 32):
             ns //= 2
         self._wgfin_ns = ns
@@ -1121,7 +1115,6 @@ class NativeDeepFM:
         prefetch = plan is not None and plan[2] is not None
         inline = plan is None or plan[1]
         main = torch.cuda.current_stream(self.device)
-        late_sort = None
         if prefetch:
             # the next batch's sort: a ROOT branch of the step's graph (no dependency on this
             # step's kernels), enqueued after fm_fwd so the first kernel is launched first; it
@@ -1134,15 +1127,13 @@ class NativeDeepFM:
 
             def sort_next():
                 with torch.cuda.stream(self._side_next):
-                    if _SORT_NEXT_ROWMAJOR:
-                        self._fsort_next.sort_rowmajor(nk_ids, nk_B, nxt_keys, nxt_perm)
-                    else:
-                        self._fsort_next(nk_ids, nk_B, nxt_keys, nxt_perm)
-            if _SORT_NEXT_AT == "start":
-                sort_next()
-            elif _SORT_NEXT_AT == "tower":
-                after_fm = sort_next
-            late_sort = sort_next if _SORT_NEXT_AT in ("fin", "end") else None
+                    self._fsort_next(nk_ids, nk_B, nxt_keys, nxt_perm)
+            # enqueued right after the tower (graph branches are dispatched in capture order);
+            # same-box sweep of the enqueue point: after the tower 0.1318, after the dense
+            # gradients 0.1316, at the end 0.1351, at the start 0.1365 ms/step.  (Letting the
+            # tower write these ids field-major saves the transpose launch but makes the branch
+            # depend on the tower, so the sort no longer overlaps it: 0.1372 vs 0.1223 ms.)
+            after_fm = sort_next
         if not inline:
             presorted = True            # sorted during the previous step
         elif not self.sharded and _SORT_SIDE_STREAM:
@@ -1202,8 +1193,6 @@ class NativeDeepFM:
             self._dense_opt()
         if presorted and inline:
             main.wait_stream(self._side)
-        if late_sort is not None and _SORT_NEXT_AT == "fin":
-            late_sort()
         work = None
         eng = getattr(self.comm, "engine_dense", None) if self.exchange else None
         if split or eng is not None:
@@ -1231,8 +1220,6 @@ class NativeDeepFM:
             self.shx.end(self._shx_plan)
         if not self._dense_early:
             self._dense_opt()
-        if late_sort is not None and _SORT_NEXT_AT == "end":
-            late_sort()
         if prefetch:
             main.wait_stream(self._side_next)
 

@@ -217,7 +217,6 @@ _SIGS = {
     "hfm_field_sort_max_pb": [],
     "hfm_field_sort": [c_void_p, c_int, c_int, c_void_p, c_void_p, c_int] + [c_void_p] * 4 + [c_void_p],
     "hfm_field_sort_pre": [c_void_p, c_int, c_int, c_void_p, c_void_p, c_int] + [c_void_p] * 3 + [c_void_p],
-    "hfm_field_sort_rowmajor": [c_void_p, c_int, c_int, c_void_p, c_void_p, c_int] + [c_void_p] * 3 + [c_void_p],
     "hfm_radix_sort_ids": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_size_t, c_void_p],
     "hfm_segments": [c_void_p, c_int] + [c_void_p] * 5 + [c_void_p, c_size_t, c_void_p],
     "hfm_fm_bwd_seg": [c_int] + [c_void_p] * 7 + [c_int, c_int, c_int, c_void_p, c_void_p, c_void_p],

@@ -160,13 +160,6 @@ class FieldSort:
                                  ptr(self.idsT), ptr(keys_out), ptr(perm_out), ptr(self.err),
                                  stream_handle()), "field_sort")
 
-    def sort_rowmajor(self, ids, B: int, keys_out, perm_out):
-        """The sort in ONE launch straight from the [B, F] ids (strided reads, no transpose)."""
-        assert B <= self.max_rows and ids.numel() >= B * self.F
-        check(L().hfm_field_sort_rowmajor(ptr(ids), B, self.F, ptr(self.fr), ptr(self.work), self.nwork,
-                                          ptr(keys_out), ptr(perm_out), ptr(self.err), stream_handle()),
-              "field_sort_rowmajor")
-
     def sort_pre(self, B: int, keys_out, perm_out):
         """The sort alone, from ``self.idsT`` already filled field-major ([F, B]) by fm_fwd."""
         assert B <= self.max_rows

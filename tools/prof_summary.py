@@ -35,7 +35,10 @@ def main():
     if trace:
         rows = list(csv.DictReader(open(trace[0])))
         rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-        idx = [i for i, r in enumerate(rows) if r["Kernel_Name"].startswith(("step_inc", "void dense_opt_kernel", "void finalize_opt_kernel"))]
+        # one step = from the end of one step-closing kernel (the one that advances the step
+        # counter: dense optimizer / fused finalize / wgfin) to the end of the next
+        idx = [i for i, r in enumerate(rows) if r["Kernel_Name"].startswith(
+            ("step_inc", "void dense_opt_kernel", "void finalize_opt_kernel", "void wgfin_kernel<0"))]
         if len(idx) >= 3:
             a, b = idx[len(idx) // 2 - 1], idx[len(idx) // 2]
             t0 = int(rows[a]["End_Timestamp"])
