@@ -20,6 +20,10 @@
 //          wave-exclusive offsets.  The m keys are striped over all 16 waves (csz = m/16 rounded
 //          up to 64), so a partition of 1K keys costs each wave one 64-key step per pass;
 //       3. writes its run at the partition offset.
+// Batches above FS_MAXB rows per field are cut into row chunks of FS_MAXB: every (field,
+// partition, chunk) workgroup sorts its chunk as above into a scratch run, then fs_merge places
+// each key by merge-path ranks (its index in its own run plus, per other run, a binary-search
+// count of the keys that precede it: <= for earlier chunks, < for later ones -- stable).
 // Ballot ranking is VALU-bound (~10 instructions per key bit), so spreading a field over 16
 // CUs instead of one is what makes the sort fast when it is on the critical path (the multi-GPU
 // step, max_pb = 4: 405 workgroups at the Criteo-1TB shape); when it runs on a side stream
@@ -36,6 +40,7 @@ constexpr int FS_WAVES = FS_THREADS / 64;
 constexpr int FS_IT = 16;
 constexpr int FS_MAXB = FS_THREADS * FS_IT;  // rows per field
 constexpr int FS_PBMAX = 4;                   // up to 16 partitions per field
+constexpr int FS_MAXCHUNK = 16;               // row chunks per field (batches up to 256K)
 constexpr int FS_LDS = (2 * FS_MAXB + FS_WAVES * 256 + 256 + 64) * 4;
 }  // namespace
 
@@ -59,11 +64,10 @@ __global__ void __launch_bounds__(256) fs_transpose_kernel(const int* __restrict
   }
 }
 
-// fr: per field {lo, hi, bits, pb}; work: per workgroup {field, partition}.  Row b of field f is
-// read at ids[f * fstride + b * rstride]: (B, 1) for field-major ids, (1, F) for the [B, F] batch
-// itself (no transpose launch: strided reads, for a sort that runs off the critical path).
-__global__ void __launch_bounds__(FS_THREADS) fs_sort_kernel(const int* __restrict__ ids, int B, int F,
-                                                            int fstride, int rstride,
+// fr: per field {lo, hi, bits, pb}; work: per workgroup {field, partition, chunk}; ids are
+// field-major [F, B]; outputs land at [f * B + chunk * FS_MAXB, ...) (the final arrays when there
+// is one chunk, the runs fs_merge reads otherwise).
+__global__ void __launch_bounds__(FS_THREADS) fs_sort_kernel(const int* __restrict__ ids, int Btot, int F,
                                                             const int* __restrict__ fr,
                                                             const int* __restrict__ work,
                                                             int* __restrict__ sorted_keys,
@@ -76,21 +80,23 @@ __global__ void __launch_bounds__(FS_THREADS) fs_sort_kernel(const int* __restri
   unsigned* dbase = wc + FS_WAVES * 256;                    // [256]
   unsigned* wsum = dbase + 256;                             // [16]
   unsigned* wlow = wsum + 16;                               // [16]
-  const int f = work[2 * blockIdx.x], part = work[2 * blockIdx.x + 1];
+  const int f = work[3 * blockIdx.x], part = work[3 * blockIdx.x + 1];
+  const int row0 = work[3 * blockIdx.x + 2] * FS_MAXB;
+  const int B = min(FS_MAXB, Btot - row0);
   const int lo = fr[4 * f], hi = fr[4 * f + 1], bits = fr[4 * f + 2], pb = fr[4 * f + 3];
   const int rb = bits - pb;  // bits sorted inside the partition
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const unsigned long long lt = (1ull << lane) - 1ull;
-  int* sko = sorted_keys + (size_t)f * B;
-  int* pko = perm + (size_t)f * B;
-  const int* src = ids + (size_t)f * fstride;
+  int* sko = sorted_keys + (size_t)f * Btot + row0;
+  int* pko = perm + (size_t)f * Btot + row0;
+  const int* src = ids + (size_t)f * Btot + row0;
   bool bad = false;
   if (bits == 0) {
     for (int b = tid; b < B; b += FS_THREADS) {
-      const int id = src[(size_t)b * rstride];
+      const int id = src[b];
       bad |= id != lo;
       sko[b] = id;
-      pko[b] = b * F + f;
+      pko[b] = (row0 + b) * F + f;
     }
     if (__any(bad) && lane == 0) atomicOr(err, 1u);
     return;
@@ -106,7 +112,7 @@ __global__ void __launch_bounds__(FS_THREADS) fs_sort_kernel(const int* __restri
     key[k] = 0u;
     int kp = 1 << 30;
     if (p < B) {
-      const int id = src[(size_t)p * rstride];
+      const int id = src[p];
       bad |= (id < lo) | (id >= hi);
       key[k] = (unsigned)(id - lo) & ((1u << bits) - 1u);
       kp = (int)(key[k] >> rb);
@@ -239,34 +245,73 @@ __global__ void __launch_bounds__(FS_THREADS) fs_sort_kernel(const int* __restri
     const int q = wb + k * 64 + lane;
     if (q < (int)m) {
       sko[out_base + q] = kbase + (int)key[k];
-      pko[out_base + q] = (int)(val[k] & 0xFFFFu) * F + f;
+      pko[out_base + q] = (row0 + (int)(val[k] & 0xFFFFu)) * F + f;
     }
   }
 }
 
-HFM_API int hfm_field_sort_max_rows() { return FS_MAXB; }
+// runs of FS_MAXB sorted keys per field (the last one shorter) -> one sorted list per field
+__global__ void __launch_bounds__(256) fs_merge_kernel(const int* __restrict__ rk, const int* __restrict__ rp,
+                                                      int B, int* __restrict__ sko, int* __restrict__ pko) {
+  const int f = blockIdx.y;
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= B) return;
+  const int* keys = rk + (size_t)f * B;
+  const int c = e / FS_MAXB;
+  const int k = keys[e];
+  int pos = e - c * FS_MAXB;
+  const int nrun = (B + FS_MAXB - 1) / FS_MAXB;
+  for (int r = 0; r < nrun; ++r) {
+    if (r == c) continue;
+    const int* run = keys + r * FS_MAXB;
+    int lo = 0, hi = min(FS_MAXB, B - r * FS_MAXB);
+    while (lo < hi) {  // first index whose key is > k (earlier runs) or >= k (later runs)
+      const int mid = (lo + hi) >> 1;
+      const int v = run[mid];
+      if (r < c ? v <= k : v < k) lo = mid + 1; else hi = mid;
+    }
+    pos += lo;
+  }
+  sko[(size_t)f * B + pos] = k;
+  pko[(size_t)f * B + pos] = rp[(size_t)f * B + e];
+}
+
+HFM_API int hfm_field_sort_max_rows() { return FS_MAXB * FS_MAXCHUNK; }
+
+HFM_API int hfm_field_sort_chunk_rows() { return FS_MAXB; }
 
 HFM_API int hfm_field_sort_max_pb() { return FS_PBMAX; }
 
-// ids: [B, F] int32 (row-major slots); fr_dev: [F][4] {lo, hi, bits, pb}; work_dev: [nwork][2]
-// {field, partition}; idsT: [F, B] scratch.  Outputs: the n = B*F sorted keys and their slot
-// positions (field f occupies [f*B, (f+1)*B)).
-HFM_API int hfm_field_sort(const int* ids, int B, int F, const int* fr_dev, const int* work_dev, int nwork,
-                           int* idsT, int* sorted_keys, int* perm, unsigned* err, hipStream_t st) {
-  if (B <= 0 || F <= 0) return 0;
-  if (B > FS_MAXB) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(fs_transpose_kernel, dim3((B + 63) / 64), dim3(256), 0, st, ids, B, F, idsT);
-  hipLaunchKernelGGL(fs_sort_kernel, dim3(nwork), dim3(FS_THREADS), FS_LDS, st, idsT, B, F, B, 1, fr_dev,
-                     work_dev, sorted_keys, perm, err);
+// the sort of field-major ids [F, B]: one launch, plus the merge when B > FS_MAXB (runs in rk/rp,
+// [F, B] each; unused otherwise)
+static int fs_sort_launch(const int* idsT, int B, int F, const int* fr_dev, const int* work_dev, int nwork,
+                          int* rk, int* rp, int* sorted_keys, int* perm, unsigned* err, hipStream_t st) {
+  const bool merge = B > FS_MAXB;
+  if (merge && (!rk || !rp)) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(fs_sort_kernel, dim3(nwork), dim3(FS_THREADS), FS_LDS, st, idsT, B, F, fr_dev, work_dev,
+                     merge ? rk : sorted_keys, merge ? rp : perm, err);
+  if (merge)
+    hipLaunchKernelGGL(fs_merge_kernel, dim3((B + 255) / 256, F), dim3(256), 0, st, rk, rp, B, sorted_keys, perm);
   HFM_LAUNCH_CHECK();
 }
 
-// Same sort from ids the FM forward already wrote field-major (hfm_fm_fwd's idsT): one launch.
-HFM_API int hfm_field_sort_pre(const int* idsT, int B, int F, const int* fr_dev, const int* work_dev,
-                               int nwork, int* sorted_keys, int* perm, unsigned* err, hipStream_t st) {
+// ids: [B, F] int32 (row-major slots); fr_dev: [F][4] {lo, hi, bits, pb}; work_dev: [nwork][3]
+// {field, partition, chunk}; idsT: [F, B] scratch; rk / rp: [F, B] scratch runs (B > FS_MAXB).
+// Outputs: the n = B*F sorted keys and their slot positions (field f occupies [f*B, (f+1)*B)).
+HFM_API int hfm_field_sort(const int* ids, int B, int F, const int* fr_dev, const int* work_dev, int nwork,
+                           int* idsT, int* rk, int* rp, int* sorted_keys, int* perm, unsigned* err,
+                           hipStream_t st) {
   if (B <= 0 || F <= 0) return 0;
-  if (B > FS_MAXB) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(fs_sort_kernel, dim3(nwork), dim3(FS_THREADS), FS_LDS, st, idsT, B, F, B, 1, fr_dev,
-                     work_dev, sorted_keys, perm, err);
-  HFM_LAUNCH_CHECK();
+  if (B > FS_MAXB * FS_MAXCHUNK) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(fs_transpose_kernel, dim3((B + 63) / 64), dim3(256), 0, st, ids, B, F, idsT);
+  return fs_sort_launch(idsT, B, F, fr_dev, work_dev, nwork, rk, rp, sorted_keys, perm, err, st);
+}
+
+// Same sort from ids the FM forward already wrote field-major (hfm_fm_fwd's idsT).
+HFM_API int hfm_field_sort_pre(const int* idsT, int B, int F, const int* fr_dev, const int* work_dev,
+                               int nwork, int* rk, int* rp, int* sorted_keys, int* perm, unsigned* err,
+                               hipStream_t st) {
+  if (B <= 0 || F <= 0) return 0;
+  if (B > FS_MAXB * FS_MAXCHUNK) return (int)hipErrorInvalidValue;
+  return fs_sort_launch(idsT, B, F, fr_dev, work_dev, nwork, rk, rp, sorted_keys, perm, err, st);
 }

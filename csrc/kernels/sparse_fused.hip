@@ -196,22 +196,36 @@ __device__ __forceinline__ void sf_lookback(const SfArgs& A, int tile, unsigned 
   if (lane == 0) atomicOr(A.sync + 2, 4u);  // no origin before tile 0: impossible
 }
 
+template <int K>
+struct SfSmem {
+  float g[SfCfg<K>::TP][SfCfg<K>::C];
+  int skl[SfCfg<K>::TP];
+  float lead[SfCfg<K>::NCH][SfCfg<K>::C];
+  int fh[SfCfg<K>::NCH];  // offset of the first head in the chunk (CH: none)
+  int hl[SfCfg<K>::TP];   // head positions, ascending
+  int wcount[4];
+  int open_key_s, open_pos_s;
+  float own_lead[SfCfg<K>::C];
+};
+
+// tile `tile` of the sparse backward (the sf_tile_kernel workgroup, or one of sfwg_kernel's)
 template <int K, int MODE, int OPT>
-__global__ void __launch_bounds__(256) sf_tile_kernel(SfArgs A) {
+__device__ __forceinline__ void sf_tile_body(const SfArgs& A, const int tile, SfSmem<K>& sm) {
   using T = SfCfg<K>;
   constexpr int CH = T::CH;
-  __shared__ float g[T::TP][T::C];
-  __shared__ int skl[T::TP];
-  __shared__ float lead[T::NCH][T::C];
-  __shared__ int fh[T::NCH];  // offset of the first head in the chunk (CH: none)
-  __shared__ int hl[T::TP];   // head positions, ascending
-  __shared__ int wcount[4];
-  __shared__ int open_key_s, open_pos_s;
-  __shared__ float own_lead[T::C];
+  auto& g = sm.g;
+  auto& skl = sm.skl;
+  auto& lead = sm.lead;
+  auto& fh = sm.fh;
+  auto& hl = sm.hl;
+  auto& wcount = sm.wcount;
+  int& open_key_s = sm.open_key_s;
+  int& open_pos_s = sm.open_pos_s;
+  auto& own_lead = sm.own_lead;
   // publication tag of this step: its 1-based index (unique per training step; the host zeroes
   // the flags whenever the step counter is rewritten)
   const unsigned tag = (unsigned)(*A.step + A.step_off);
-  const int tile = blockIdx.x, b0 = tile * T::TP;
+  const int b0 = tile * T::TP;
   const int nloc = min(T::TP, A.n - b0);
   const int nch = (nloc + CH - 1) / CH;
   const int tid = threadIdx.x, sub = tid % T::LPS, lane = tid & 63, wv = tid >> 6;
@@ -352,6 +366,87 @@ __global__ void __launch_bounds__(256) sf_tile_kernel(SfArgs A) {
   // for a headless tile, at the tile's end when the next tile starts a new id (or there is none)
   const bool closes = nloc > 0 && skl[0] == prev_key && (nh > 0 || next_key != skl[nloc - 1]);
   if (closes && wv == 0) sf_lookback<K, MODE, OPT>(A, tile, tag, own_lead, lr_t);
+}
+
+template <int K, int MODE, int OPT>
+__global__ void __launch_bounds__(256) sf_tile_kernel(SfArgs A) {
+  __shared__ SfSmem<K> sm;
+  sf_tile_body<K, MODE, OPT>(A, blockIdx.x, sm);
+}
+
+// ---------------------------------------------------------------------------------------------
+// sfwg: the sparse backward (lazy rows) and the fused tower's wgfin work (wgfin.h: weight
+// gradients, split-K combine, dense optimizer) in ONE launch.  The two are independent -- the
+// sparse tiles need dX0 / S / dlogit from the tower, wgfin needs its dZ^T / H^T -- and both are
+// latency-bound, so sharing the chip hides most of wgfin under the sparse tiles instead of
+// running them back to back behind a kernel boundary.  wgfin workgroups take the LOWEST ids
+// (dispatched first: they never wait on anyone); the sparse tiles keep their look-back order
+// among themselves.  Every workgroup reads the step counter before it arrives on `done`; the last
+// arrival (any grid size: it resets the counter) advances it, so both halves use this step's
+// index (sparse: step_off = 1; wgfin: *step + 1).
+#include "wgfin.h"
+
+// the wgfin half's register footprint must not cut the sparse tiles' occupancy (6 waves / SIMD)
+constexpr int SFWG_PF = 2;
+constexpr int SFWG_MAXNS = 4;
+
+template <int K>
+union SfwgSmem {
+  SfSmem<K> sf;
+  WgfSmem wg;
+};
+
+// (4 waves / SIMD for K = 8; forcing 6 spills 22 VGPRs and measured slower: 0.1139 vs 0.1110 ms)
+template <int K, int OPT>
+__global__ void __launch_bounds__(256) sfwg_kernel(SfArgs A, WgFinArgs W, unsigned* done) {
+  __shared__ SfwgSmem<K> sm;
+  const int nw = W.tile_wgs + 1;
+  if ((int)blockIdx.x < nw) wgfin_body<OPT, SFWG_PF, SFWG_MAXNS>(W, blockIdx.x, sm.wg);
+  else sf_tile_body<K, 0, OPT>(A, (int)blockIdx.x - nw, sm.sf);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned prev = __hip_atomic_fetch_add(done, 1u, HFM_RLX_AGENT);
+    if (prev == gridDim.x - 1) {
+      __hip_atomic_store(done, 0u, HFM_RLX_AGENT);
+      *W.o.step += 1;
+    }
+  }
+}
+
+template <int K>
+static int sfwg_dispatch(int opt, const SfArgs& A, const WgFinArgs& W, unsigned* done, hipStream_t st) {
+  using T = SfCfg<K>;
+  const dim3 g(W.tile_wgs + 1 + (A.n + T::TP - 1) / T::TP), blk(256);
+  switch (opt) {
+    case OPT_ADAM: hipLaunchKernelGGL((sfwg_kernel<K, OPT_ADAM>), g, blk, 0, st, A, W, done); break;
+    case OPT_ADAGRAD: hipLaunchKernelGGL((sfwg_kernel<K, OPT_ADAGRAD>), g, blk, 0, st, A, W, done); break;
+    case OPT_MOMENTUM: hipLaunchKernelGGL((sfwg_kernel<K, OPT_MOMENTUM>), g, blk, 0, st, A, W, done); break;
+    case OPT_FTRL: hipLaunchKernelGGL((sfwg_kernel<K, OPT_FTRL>), g, blk, 0, st, A, W, done); break;
+    case OPT_GD: hipLaunchKernelGGL((sfwg_kernel<K, OPT_GD>), g, blk, 0, st, A, W, done); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+  return 0;
+}
+
+// lazy sparse rows (optimizer `opt`) + wgfin with the same dense optimizer; `done`: [1] arrival
+// counter, zero between launches.  A.step_off must be 1 (the step advances at the launch's end).
+HFM_API int hfm_sparse_wgfin(int K, int opt, const SfArgs* A, const WgFinArgs* W, unsigned* done,
+                             hipStream_t st) {
+  if (A->n <= 0 || !A->flags || !A->sync || !done || A->step_off != 1 || !W->opt_on || W->ns < 1 ||
+      W->ns > SFWG_MAXNS || W->kchunk % 32 || W->ldk != W->ns * 4 * W->kchunk || W->L + 2 > WGF_MAXC ||
+      !W->tile_ctr || (const void*)W->o.step != (const void*)A->step)
+    return (int)hipErrorInvalidValue;
+  int rc;
+  switch (K) {
+    case 4: rc = sfwg_dispatch<4>(opt, *A, *W, done, st); break;
+    case 8: rc = sfwg_dispatch<8>(opt, *A, *W, done, st); break;
+    case 16: rc = sfwg_dispatch<16>(opt, *A, *W, done, st); break;
+    case 32: rc = sfwg_dispatch<32>(opt, *A, *W, done, st); break;
+    case 64: rc = sfwg_dispatch<64>(opt, *A, *W, done, st); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+  if (rc) return rc;
+  HFM_LAUNCH_CHECK();
 }
 
 HFM_API int hfm_sparse_fused_tiles(int K, int n) {

@@ -21,6 +21,7 @@
 // A[l&15][8(l>>4)+j], B fragment B[8(l>>4)+j][l&15]; C: col = l&15, row = (l>>4)*4 + j.
 // Dropout masks: counter hash, flat index (global row) * Npad + col, identical to mlp.hip.
 #include "common.h"
+#include "mma32.h"
 
 constexpr int TW_MAXL = 8;
 constexpr int TW_ROWS = 32;
@@ -78,55 +79,6 @@ struct TowerArgs {
   float* S;                       // [M, K]  sum_f E (sparse backward)
   bf16* Et;                       // [K0p, M] (train: wgrad operand)
 };
-
-// One wave: c[2][2] += A[32 x 32*nk] . B[32 x 32*nk]^T, both K-contiguous (row strides lda/ldb
-// in elements).  Register ring of PF k-steps so PF fragment sets are in flight.
-template <int PF, bool ROWSUM = false>
-__device__ __forceinline__ void mma32(const bf16* __restrict__ A, int lda, const bf16* __restrict__ B,
-                                      int ldb, int nk, int lane, f32x4& c00, f32x4& c01, f32x4& c10,
-                                      f32x4& c11, float* rs = nullptr) {
-  const int r = lane & 15, kq = (lane >> 4) * 8;
-  const bf16* a0 = A + r * lda + kq;
-  const bf16* a1 = a0 + 16 * lda;
-  const bf16* b0 = B + r * ldb + kq;
-  const bf16* b1 = b0 + 16 * ldb;
-  bf16x8 ra0[PF], ra1[PF], rb0[PF], rb1[PF];
-#pragma unroll
-  for (int j = 0; j < PF; ++j) {
-    if (j < nk) {
-      ra0[j] = *reinterpret_cast<const bf16x8*>(a0 + j * 32);
-      ra1[j] = *reinterpret_cast<const bf16x8*>(a1 + j * 32);
-      rb0[j] = *reinterpret_cast<const bf16x8*>(b0 + j * 32);
-      rb1[j] = *reinterpret_cast<const bf16x8*>(b1 + j * 32);
-    }
-  }
-  for (int kb = 0; kb < nk; kb += PF) {
-#pragma unroll
-    for (int j = 0; j < PF; ++j) {
-      const int ks = kb + j;
-      if (ks < nk) {
-        c00 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ra0[j], rb0[j], c00, 0, 0, 0);
-        c01 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ra0[j], rb1[j], c01, 0, 0, 0);
-        c10 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ra1[j], rb0[j], c10, 0, 0, 0);
-        c11 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ra1[j], rb1[j], c11, 0, 0, 0);
-        if (ROWSUM) {  // A row sums on the side (bias gradients): lane's 8 elements of rows r, r+16
-#pragma unroll
-          for (int t = 0; t < 8; ++t) {
-            rs[0] += bf2f(ra0[j][t]);
-            rs[1] += bf2f(ra1[j][t]);
-          }
-        }
-        const int kn = (ks + PF) * 32;
-        if (ks + PF < nk) {
-          ra0[j] = *reinterpret_cast<const bf16x8*>(a0 + kn);
-          ra1[j] = *reinterpret_cast<const bf16x8*>(a1 + kn);
-          rb0[j] = *reinterpret_cast<const bf16x8*>(b0 + kn);
-          rb1[j] = *reinterpret_cast<const bf16x8*>(b1 + kn);
-        }
-      }
-    }
-  }
-}
 
 // fp8 variant of mma32 (16x16x32 fp8 MFMA; same fragment map as bf16 with 8 one-byte elements
 // per lane): A and B are e4m3 rows in global memory (row strides in bytes).
@@ -642,183 +594,19 @@ HFM_API int hfm_wgrad_group(const void* jobs_dev, int njobs, int ntasks, hipStre
 HFM_API int hfm_wg_job_bytes() { return (int)sizeof(WgJob); }
 
 // ---------------------------------------------------------------------------------------------
-// Weight gradients + split-K combine + bias gradients + head reductions + dense optimizer in ONE
-// launch (replaces wgrad_group + finalize[_opt] for the fused tower).  Output tile (layer, 32x32)
-// work is split over the batch into NS workgroup-splits of 4 waves; each wave reduces its own
-// k-chunk on MFMA, the 4 wave tiles are summed in LDS (fixed order), and the workgroup's partial
-// goes to its slab with write-through stores.  The workgroup that draws the NS-th arrival on the
-// tile's counter (counters only ever grow: arrival % NS == NS - 1, nothing to reset) sums the NS
-// slabs in slab order and applies the dense optimizer to its 32x32 parameters right away, with
-// the bf16 shadows (OPT < 0: writes the gradient only -- multi-rank, before the all-reduce).
-// Column-tile 0 workgroups also sum their dZ^T rows: the bias gradient, combined the same way.
-// One extra workgroup reduces the tower's per-block head partials (deep_out weights, its bias,
-// fm_bias, the loss sum).  The last workgroup of the launch advances the step counter.
-#include "sync.h"
-
-constexpr int WGF_MAXC = 264;   // head columns (last deep layer + 2)
-constexpr int WGF_MAXNS = 8;    // workgroup splits of the batch per tile
-
-struct WgFinJob {
-  const bf16* A;   // dZ_i^T [Np_i, ldk]
-  const bf16* B;   // X_i^T  [Kp_i, ldk]
-  float* slab;     // [NS][Np_i][Kp_i]
-  float* bslab;    // [NS][Np_i]
-  float* gw;       // gradient of W_i in the flat buffer [Np_i, Kp_i]
-  float* gb;       // gradient of b_i [Np_i]
-  int M, N;        // Np_i, Kp_i
-  int tiles_m, tiles_n;
-  int tile0;       // first counter of this job
-  int wg0;         // first workgroup of this job
-};
-
-struct WgFinArgs {
-  const WgFinJob* jobs;
-  int njobs, ldk, kchunk, ns;      // ldk = batch rows M; kchunk = rows per wave; NS splits
-  int tile_wgs;                    // workgroups of the tile work; workgroup tile_wgs = head
-  unsigned* tile_ctr;              // [tiles]
-  unsigned* done_ctr;              // [1]
-  const float* partial;            // [nhead][L + 2] tower head partials
-  int nhead, L;
-  float* g_wout;                   // [L]
-  float* g_bout;                   // [1]
-  float* g_fmbias;                 // [1]
-  float* loss_sum;                 // [1]
-  FinOpt o;
-  int opt_on;
-};
-
-template <int OPT>
-__device__ __forceinline__ void wgfin_apply(const WgFinArgs& a, float lr_t, float* dst, float gv) {
-  *dst = gv;
-  if (OPT >= 0) fin_opt_apply<OPT>(a.o, lr_t, dst, gv);
-}
+// wgfin: weight gradients + split-K combine + bias / head reductions + dense optimizer in ONE
+// launch (wgfin.h); the launch's last workgroup advances the step counter.  (The single-GPU lazy
+// step runs the same work inside the sparse backward's launch instead: sparse_fused.hip.)
+#include "wgfin.h"
 
 template <int OPT>
 __global__ void __launch_bounds__(256) wgfin_kernel(WgFinArgs a) {
-  __shared__ float red[4][32][33];
-  __shared__ float bred[4][32];
-  __shared__ int s_last;
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const float lr_t = OPT == OPT_ADAM ? adam_lr_t(a.o.h, *a.o.step + 1) : a.o.h.lr;
-  const int b = blockIdx.x;
-  if (b < a.tile_wgs) {
-    int j = 0;
-    while (j + 1 < a.njobs && b >= a.jobs[j + 1].wg0) ++j;
-    const WgFinJob jb = a.jobs[j];
-    const int local = b - jb.wg0;
-    const int tile = local / a.ns, wz = local - tile * a.ns;
-    const int tm = tile / jb.tiles_n, tn = tile - tm * jb.tiles_n;
-    const int row0 = tm * 32, col0 = tn * 32;
-    const int k0 = (wz * 4 + wave) * a.kchunk;
-    f32x4 c00 = {0, 0, 0, 0}, c01 = c00, c10 = c00, c11 = c00;
-    float rs[2] = {0.f, 0.f};
-    if (tn == 0)
-      mma32<4, true>(jb.A + (size_t)row0 * a.ldk + k0, a.ldk, jb.B + (size_t)col0 * a.ldk + k0, a.ldk,
-                     a.kchunk / 32, lane, c00, c01, c10, c11, rs);
-    else
-      mma32<4>(jb.A + (size_t)row0 * a.ldk + k0, a.ldk, jb.B + (size_t)col0 * a.ldk + k0, a.ldk,
-               a.kchunk / 32, lane, c00, c01, c10, c11);
-    const int cr = (lane >> 4) * 4, cc = lane & 15;
-    f32x4 acc[2][2] = {{c00, c01}, {c10, c11}};
-#pragma unroll
-    for (int ti = 0; ti < 2; ++ti)
-#pragma unroll
-      for (int tj = 0; tj < 2; ++tj)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) red[wave][ti * 16 + cr + q][tj * 16 + cc] = acc[ti][tj][q];
-    if (tn == 0) {  // bias gradient partial: the 4 k-groups of lanes holding rows r, r+16
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        rs[h] += __shfl_xor(rs[h], 16, 64);
-        rs[h] += __shfl_xor(rs[h], 32, 64);
-      }
-      if (lane < 16) {
-        bred[wave][lane] = rs[0];
-        bred[wave][16 + lane] = rs[1];
-      }
-    }
-    __syncthreads();
-    // workgroup partial tile -> slab wz (write-through stores: no release fence needed)
-    float* sl = jb.slab + ((size_t)wz * jb.M + row0) * jb.N + col0;
-    for (int e = tid; e < 1024; e += 256) {
-      const int r = e >> 5, c = e & 31;
-      const float v = ((red[0][r][c] + red[1][r][c]) + red[2][r][c]) + red[3][r][c];
-      __hip_atomic_store(sl + (size_t)r * jb.N + c, v, HFM_RLX_AGENT);
-    }
-    if (tn == 0 && tid < 32) {
-      const float v = ((bred[0][tid] + bred[1][tid]) + bred[2][tid]) + bred[3][tid];
-      __hip_atomic_store(jb.bslab + (size_t)wz * jb.M + row0 + tid, v, HFM_RLX_AGENT);
-    }
-    hx_drain();
-    __syncthreads();
-    if (tid == 0) {
-      const unsigned prev = __hip_atomic_fetch_add(a.tile_ctr + jb.tile0 + tile, 1u, HFM_RLX_AGENT);
-      s_last = (prev % (unsigned)a.ns) == (unsigned)(a.ns - 1);
-    }
-    __syncthreads();
-    if (s_last) {  // the tile's last workgroup: sum the NS slabs in slab order, then the optimizer
-      const float* base = jb.slab + (size_t)row0 * jb.N + col0;
-      float sv[4][WGF_MAXNS], bv[WGF_MAXNS];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {  // every slab load of this thread in flight at once
-        const int e = tid + q * 256, r = e >> 5, c = e & 31;
-#pragma unroll
-        for (int z = 0; z < WGF_MAXNS; ++z)
-          sv[q][z] = z < a.ns ? hx_ldf(base + ((size_t)z * jb.M + r) * jb.N + c) : 0.f;
-      }
-      const bool brow = tn == 0 && tid < 32;
-#pragma unroll
-      for (int z = 0; z < WGF_MAXNS; ++z)
-        bv[z] = (brow && z < a.ns) ? hx_ldf(jb.bslab + (size_t)z * jb.M + row0 + tid) : 0.f;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int e = tid + q * 256, r = e >> 5, c = e & 31;
-        float v = 0.f;
-#pragma unroll
-        for (int z = 0; z < WGF_MAXNS; ++z)
-          if (z < a.ns) v += sv[q][z];
-        wgfin_apply<OPT>(a, lr_t, jb.gw + (size_t)(row0 + r) * jb.N + col0 + c, v);
-      }
-      if (brow) {
-        float v = 0.f;
-#pragma unroll
-        for (int z = 0; z < WGF_MAXNS; ++z)
-          if (z < a.ns) v += bv[z];
-        wgfin_apply<OPT>(a, lr_t, jb.gb + row0 + tid, v);
-      }
-    }
-  } else if (b == a.tile_wgs) {
-    // head partials [nhead][L + 2]: columns 0..L-1 -> deep_out weights, L -> deep_out bias and
-    // fm_bias (both d/dy of the logit), L + 1 -> the loss sum.  Row chunks go through LDS with
-    // coalesced loads (all in flight); thread c keeps column c's sum in row order (deterministic).
-    float* buf = &red[0][0][0];
-    const int C = a.L + 2;
-    const int rows = (4 * 32 * 33) / C;
-    float acc = 0.f;
-    for (int r0 = 0; r0 < a.nhead; r0 += rows) {
-      const int nr = min(rows, a.nhead - r0);
-      __syncthreads();
-      for (int e = tid; e < nr * C; e += 256) buf[e] = a.partial[(size_t)r0 * C + e];
-      __syncthreads();
-      if (tid < C)
-        for (int r = 0; r < nr; ++r) acc += buf[r * C + tid];
-    }
-    if (tid < C) {
-      const float v = acc;
-      if (tid < a.L) {
-        wgfin_apply<OPT>(a, lr_t, a.g_wout + tid, v);
-      } else if (tid == a.L) {
-        wgfin_apply<OPT>(a, lr_t, a.g_bout, v);
-        wgfin_apply<OPT>(a, lr_t, a.g_fmbias, v);
-      } else {
-        *a.loss_sum = v;
-      }
-    }
-  }
+  __shared__ WgfSmem sm;
+  wgfin_body<OPT, 4, WGF_MAXNS>(a, blockIdx.x, sm);
   // the launch's last workgroup (arrivals only grow: % grid) advances the step counter
   if (OPT >= 0) {
     __syncthreads();
-    if (tid == 0) {
+    if (threadIdx.x == 0) {
       const unsigned prev = __hip_atomic_fetch_add(a.done_ctr, 1u, HFM_RLX_AGENT);
       if (prev % gridDim.x == gridDim.x - 1) *a.o.step += 1;
     }

@@ -51,6 +51,8 @@ _DENSE_SIDE_STREAM = os.environ.get("HIPFM_DENSE_SIDE_STREAM", "auto")   # auto 
 _TOWER_GATHER = os.environ.get("HIPFM_TOWER_GATHER", "1") == "1"   # FM gather fused into the tower
 # weight gradients + split-K combine + bias/head reductions + dense optimizer in one launch
 _WGFIN = os.environ.get("HIPFM_WGFIN", "1") == "1"
+# single GPU, lazy rows: wgfin inside the sparse backward's launch (sparse_fused.hip sfwg_kernel)
+_SFWG = os.environ.get("HIPFM_SFWG", "1") == "1"
 
 
 def check_field_ranges(ranges, F: int, V: int) -> List[Tuple[int, int]]:
@@ -291,6 +293,8 @@ class NativeDeepFM:
         self._shx_plan = None
         self._dense_early = False
         self._fuse_opt = False     # dense optimizer fused into the finalize launch (this step)
+        self._sfwg_now = False     # ... and that launch merged into the sparse backward (this step)
+        self._sfwg_step = False
         self._idsT_B = 0
         self.batch_size = int(batch_size)
         # fused deep tower (csrc/kernels/tower.hip): whole forward + head + dgrad chain in one
@@ -564,7 +568,7 @@ class NativeDeepFM:
         M, dev = self.M, self.device
         f32 = dict(dtype=torch.float32, device=dev)
         # 4 workgroup splits x 4 waves: same-box A/B 0.1214 (4) / 0.1228 (8) / 0.126 (16) ms/step
-        ns = 4
+        ns = int(os.environ.get("HIPFM_WGFIN_NS", "4"))
         while ns > 1 and (M % (ns * 4 * 32) or M // (ns * 4) < 32):
             ns //= 2
         self._wgfin_ns = ns
@@ -582,6 +586,7 @@ class NativeDeepFM:
             j.A, j.B, j.slab, j.bslab = self.dZt[i].data_ptr(), Xt.data_ptr(), sl.data_ptr(), bsl.data_ptr()
             j.gw = g0 + 4 * self.dense_segs[f"Deep-part/mlp{i}/weights"].off
             j.gb = g0 + 4 * self.dense_segs[f"Deep-part/mlp{i}/biases"].off
+            j.w16, j.wt16 = self.W16[i].data_ptr(), self.WT16[i].data_ptr()
             j.M, j.N, j.tiles_m, j.tiles_n = Np, Kp, Np // 32, Kp // 32
             j.tile0, j.wg0 = tile0, wg0
             tile0 += j.tiles_m * j.tiles_n
@@ -591,6 +596,7 @@ class NativeDeepFM:
         self._wgfin_ntiles, self._wgfin_wgs = tile0, wg0
         self.wf_tile_ctr = torch.zeros(max(1, tile0), dtype=torch.int32, device=dev)
         self.wf_done_ctr = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.sfwg_done = torch.zeros(1, dtype=torch.int32, device=dev)
 
     def _wgfin_args(self, with_opt: bool) -> WgFinArgs:
         a = WgFinArgs()
@@ -790,6 +796,8 @@ class NativeDeepFM:
         backwards (checkpoint restore) must not meet flags of its future."""
         if hasattr(self, "sf_flags"):
             self.sf_flags.zero_()
+        if hasattr(self, "sfwg_done"):
+            self.sfwg_done.zero_()
         if getattr(self, "shx", None) is not None:
             self.shx.reset_table()
 
@@ -1045,7 +1053,7 @@ class NativeDeepFM:
         A.h = self.h_sparse
         A.step = self.step.data_ptr()
         A.ldv, A.ldw = KN._ld(self.tv, self.tw)
-        A.step_off = 0 if self._dense_early else 1
+        A.step_off = 0 if (self._dense_early and not self._sfwg_now) else 1
         A.flags, A.sync = self.sf_flags.data_ptr(), self.sf_sync.data_ptr()
         return A
 
@@ -1060,6 +1068,9 @@ class NativeDeepFM:
             return self.comm.sharded_backward(self, B, idx, tv)
         if not presorted:
             self._sort_slots(B)
+        if self._sfwg_now:
+            KN.sparse_wgfin(self.K, self.opt_id, self.sf_args(n), self._wgfin_args(True), self.sfwg_done)
+            return None
         if not self.exchange and _SPARSE_IMPL == "fused":
             KN.sparse_fused(self.K, KN.SF_LAZY if self.sparse_update == "lazy" else KN.SF_SCATTER,
                             self.opt_id, self.sf_args(n))
@@ -1179,15 +1190,20 @@ class NativeDeepFM:
         self._dense_early = (presorted and not self.exchange and not split and _DENSE_EARLY and
                              self.sparse_update == "lazy" and _SPARSE_IMPL == "fused")
         self._fuse_opt = (self._dense_early and self.fused and _FUSE_FIN_OPT and self._fin_covers_all)
+        # ... and with wgfin, that whole dense-gradient launch rides inside the sparse backward's
+        # launch instead (sfwg: independent work, both latency-bound)
+        self._sfwg_now = (self._fuse_opt and _WGFIN and _SFWG and getattr(self, "_wgfin_ns", 1 << 30) <= KN.SFWG_MAX_NS and
+                          self.shx is None and not self.sharded)
         try:
-            idx, tv = self._dense_fwd_bwd(B, defer_wgrad=split, after_fm=after_fm)
+            idx, tv = self._dense_fwd_bwd(B, defer_wgrad=split or self._sfwg_now, after_fm=after_fm)
         finally:
             self._idsT_B = 0
             fused_opt, self._fuse_opt = self._fuse_opt, False
         main = torch.cuda.current_stream(self.device)
         self._fin_opt_step = fused_opt          # observable by tests: which dense-optimizer path ran
+        self._sfwg_step = self._sfwg_now
         if fused_opt:
-            if self.fp8:
+            if self.fp8 and not self._sfwg_now:
                 KN.w8_quant(self._w8_jobs, len(self.layers), self._w8_rows)
         elif self._dense_early:
             self._dense_opt()
@@ -1212,6 +1228,10 @@ class NativeDeepFM:
         out = self._sparse_backward(B, idx, tv, presorted=presorted)
         if out is not None:
             self._sparse_update(*out)
+        if self._sfwg_now:
+            self._sfwg_now = False
+            if self.fp8:
+                KN.w8_quant(self._w8_jobs, len(self.layers), self._w8_rows)
         if split or eng is not None:
             main.wait_stream(self._comm_stream)
         if work is not None:
@@ -1221,6 +1241,9 @@ class NativeDeepFM:
         if not self._dense_early:
             self._dense_opt()
         if prefetch:
+            # joined at the end of the step: deferring the join to the next step's sparse
+            # backward (so no cross-branch edge precedes the next tower) measured 0.155-0.186
+            # vs 0.121 ms/step in a 16-step graph -- the branch then lands in the towers' path
             main.wait_stream(self._side_next)
 
     def _dense_opt(self):

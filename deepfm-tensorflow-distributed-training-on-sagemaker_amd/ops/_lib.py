@@ -75,7 +75,8 @@ class FinOpt(C.Structure):
 
 class WgFinJob(C.Structure):
     _fields_ = [("A", c_void_p), ("B", c_void_p), ("slab", c_void_p), ("bslab", c_void_p),
-                ("gw", c_void_p), ("gb", c_void_p), ("M", c_int), ("N", c_int), ("tiles_m", c_int),
+                ("gw", c_void_p), ("gb", c_void_p), ("w16", c_void_p), ("wt16", c_void_p),
+                ("M", c_int), ("N", c_int), ("tiles_m", c_int),
                 ("tiles_n", c_int), ("tile0", c_int), ("wg0", c_int)]
 
 
@@ -197,6 +198,7 @@ _SIGS = {
     "hfm_onesweep_sort_ids": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_size_t, c_void_p],
     "hfm_onesweep_error_offset": [],
     "hfm_field_sort_max_rows": [],
+    "hfm_field_sort_chunk_rows": [],
     "hfm_comm_id_bytes": [],
     "hfm_comm_unique_id": [c_void_p],
     "hfm_comm_init": [C.POINTER(c_void_p), c_int, c_int, c_void_p],
@@ -215,8 +217,8 @@ _SIGS = {
     "hfm_sparse_fused": [c_int, c_int, c_int, c_void_p, c_void_p],
     "hfm_sparse_fused_args_bytes": [],
     "hfm_field_sort_max_pb": [],
-    "hfm_field_sort": [c_void_p, c_int, c_int, c_void_p, c_void_p, c_int] + [c_void_p] * 4 + [c_void_p],
-    "hfm_field_sort_pre": [c_void_p, c_int, c_int, c_void_p, c_void_p, c_int] + [c_void_p] * 3 + [c_void_p],
+    "hfm_field_sort": [c_void_p, c_int, c_int, c_void_p, c_void_p, c_int] + [c_void_p] * 6 + [c_void_p],
+    "hfm_field_sort_pre": [c_void_p, c_int, c_int, c_void_p, c_void_p, c_int] + [c_void_p] * 5 + [c_void_p],
     "hfm_radix_sort_ids": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_size_t, c_void_p],
     "hfm_segments": [c_void_p, c_int] + [c_void_p] * 5 + [c_void_p, c_size_t, c_void_p],
     "hfm_fm_bwd_seg": [c_int] + [c_void_p] * 7 + [c_int, c_int, c_int, c_void_p, c_void_p, c_void_p],
@@ -225,6 +227,7 @@ _SIGS = {
     "hfm_bn": [c_int, C.POINTER(BnArgs), c_void_p],
     "hfm_tower": [C.POINTER(TowerArgs), c_int, c_void_p],
     "hfm_wgfin": [c_int, C.POINTER(WgFinArgs), c_void_p],
+    "hfm_sparse_wgfin": [c_int, c_int, c_void_p, C.POINTER(WgFinArgs), c_void_p, c_void_p],
     "hfm_wgfin_job_bytes": [],
     "hfm_wgfin_args_bytes": [],
     "hfm_tower_args_bytes": [],

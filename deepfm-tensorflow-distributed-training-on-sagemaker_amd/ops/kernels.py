@@ -126,46 +126,72 @@ def sort_ids(keys_in, keys_out, vals_tmp, perm_out, n, end_bit, temp):
 
 
 def field_sort_max_rows() -> int:
-    """Largest batch the one-workgroup-per-field LDS sort handles (csrc/kernels/field_sort.hip)."""
+    """Largest batch the per-field LDS sort handles (csrc/kernels/field_sort.hip): row chunks of
+    ``field_sort_chunk_rows()`` are sorted per workgroup, then merged."""
     return int(L().hfm_field_sort_max_rows())
+
+
+def field_sort_chunk_rows() -> int:
+    return int(L().hfm_field_sort_chunk_rows())
 
 
 class FieldSort:
     """Per-field MSD-partitioned LDS sort of the B*F slot ids (csrc/kernels/field_sort.hip) for
     disjoint, increasing per-field id ranges [lo, hi): output identical to ``sort_ids`` on the
-    same slots.  ``err`` (int32 [1]) turns non-zero when an id lies outside its field's range."""
+    same slots.  ``err`` (int32 [1]) turns non-zero when an id lies outside its field's range.
+    Batches above ``field_sort_chunk_rows()`` are sorted in row chunks and merged (the work list
+    is built for ``max_rows``; a smaller batch skips the workgroups of chunks it does not have)."""
 
     def __init__(self, ranges, max_rows: int, device, max_pb: int = 0):
         """``max_pb``: each field is split into up to 2^max_pb workgroups (MSD partitions): 4 when
         the sort is on the critical path, 0 (one workgroup per field) when it overlaps other work."""
         import math
         max_pb = min(int(max_pb), int(L().hfm_field_sort_max_pb()))
-        fr, work = [], []
+        assert max_rows <= field_sort_max_rows()
+        self.chunk = field_sort_chunk_rows()
+        fr, self._fwork = [], []
         for f, (lo, hi) in enumerate(ranges):
             bits = int(math.ceil(math.log2(hi - lo))) if hi - lo > 1 else 0
             pb = min(bits, max_pb)
             fr.append((int(lo), int(hi), bits, pb))
-            work += [(f, p) for p in range(1 << pb)]
+            self._fwork.append(1 << pb)
         self.F = len(fr)
         self.fr = torch.tensor(fr, dtype=torch.int32).reshape(-1).to(device)
-        self.work = torch.tensor(work, dtype=torch.int32).reshape(-1).to(device)
-        self.nwork = len(work)
+        self.device = device
+        self._work = {}
+        for b in range(1, max(1, max_rows) + 1, self.chunk):    # all built now, never during capture
+            self.work(b)
         self.idsT = torch.zeros(self.F * max(1, max_rows), dtype=torch.int32, device=device)
+        big = max_rows > self.chunk
+        self.rk = torch.zeros(self.F * max_rows if big else 1, dtype=torch.int32, device=device)
+        self.rp = torch.zeros_like(self.rk)
         self.err = torch.zeros(1, dtype=torch.int32, device=device)
         self.max_rows = max_rows
 
+    def work(self, B: int):
+        """(work list on the device, its length) for a batch of B rows: {field, partition, chunk}."""
+        nc = max(1, -(-B // self.chunk))
+        w = self._work.get(nc)
+        if w is None:                                    # (only from __init__)
+            items = [(f, p, c) for f, n in enumerate(self._fwork) for c in range(nc) for p in range(n)]
+            w = (torch.tensor(items, dtype=torch.int32).reshape(-1).to(self.device), len(items))
+            self._work[nc] = w
+        return w
+
     def __call__(self, ids, B: int, keys_out, perm_out):
         assert B <= self.max_rows and ids.numel() >= B * self.F
-        check(L().hfm_field_sort(ptr(ids), B, self.F, ptr(self.fr), ptr(self.work), self.nwork,
-                                 ptr(self.idsT), ptr(keys_out), ptr(perm_out), ptr(self.err),
-                                 stream_handle()), "field_sort")
+        work, nwork = self.work(B)
+        check(L().hfm_field_sort(ptr(ids), B, self.F, ptr(self.fr), ptr(work), nwork,
+                                 ptr(self.idsT), ptr(self.rk), ptr(self.rp), ptr(keys_out), ptr(perm_out),
+                                 ptr(self.err), stream_handle()), "field_sort")
 
     def sort_pre(self, B: int, keys_out, perm_out):
         """The sort alone, from ``self.idsT`` already filled field-major ([F, B]) by fm_fwd."""
         assert B <= self.max_rows
-        check(L().hfm_field_sort_pre(ptr(self.idsT), B, self.F, ptr(self.fr), ptr(self.work),
-                                     self.nwork, ptr(keys_out), ptr(perm_out), ptr(self.err),
-                                     stream_handle()), "field_sort_pre")
+        work, nwork = self.work(B)
+        check(L().hfm_field_sort_pre(ptr(self.idsT), B, self.F, ptr(self.fr), ptr(work), nwork,
+                                     ptr(self.rk), ptr(self.rp), ptr(keys_out), ptr(perm_out),
+                                     ptr(self.err), stream_handle()), "field_sort_pre")
 
 
 def sort_error(temp) -> int:
@@ -221,6 +247,17 @@ def sparse_fused(K, mode, opt, args: SfArgs):
     """Fused embedding backward + row optimizer (lazy) or tf1_dense scatter over sorted slots
     (csrc/kernels/sparse_fused.hip): one tile kernel + one carry kernel."""
     check(L().hfm_sparse_fused(K, mode, opt, C.byref(args), stream_handle()), "sparse_fused")
+
+
+SFWG_MAX_NS = 4          # sparse_fused.hip SFWG_MAXNS: wgfin splits the merged launch supports
+
+
+def sparse_wgfin(K, opt, args: SfArgs, wf: "WgFinArgs", done):
+    """Lazy sparse backward + the fused tower's wgfin work (weight gradients, split-K combine,
+    dense optimizer) in ONE launch (sparse_fused.hip sfwg_kernel); ``done``: int32 [1] arrival
+    counter (zero between launches); the launch advances the step counter."""
+    check(L().hfm_sparse_wgfin(K, opt, C.byref(args), C.byref(wf), ptr(done), stream_handle()),
+          "sparse_wgfin")
 
 
 def seg_apply(K, mode, opt, args: SegApplyArgs, max_groups):

@@ -338,10 +338,12 @@ def test_sort_graph_replay_with_new_inputs(impl):
 
 @pytest.mark.parametrize("preset,B,max_pb", [("criteo_1tb", 16384, 4), ("criteo_1tb", 16384, 0),
                                              ("criteo_kaggle", 1000, 4), ("reference", 4096, 2),
-                                             ("criteo_1tb", 333, 4)])
+                                             ("criteo_1tb", 333, 4), ("criteo_1tb", 65536, 0),
+                                             ("criteo_kaggle", 40000, 2), ("criteo_1tb", 16385, 4)])
 def test_field_sort_equals_global_sort(preset, B, max_pb):
     """The per-field LDS sort (field_sort.hip) returns exactly the stable global sort of the
-    B*F slot ids, in eager mode and as a graph replayed on new batches."""
+    B*F slot ids, in eager mode and as a graph replayed on new batches (above 16384 rows: row
+    chunks sorted per workgroup, then merged)."""
     synth = make_synth(preset)
     F = synth.F
     fs = KN.FieldSort(synth.field_ranges(), B, DEV, max_pb=max_pb)
@@ -459,19 +461,22 @@ def test_fm_fwd_idsT_feeds_field_sort(preset, B, M):
     assert torch.equal(sk.long(), rk) and torch.equal(perm.long(), rp)
 
 
-@pytest.mark.parametrize("opt,mlp_dtype", [("Adam", "bf16"), ("ftrl", "bf16"), ("Adam", "fp8")])
+@pytest.mark.parametrize("opt,mlp_dtype", [("Adam", "bf16"), ("ftrl", "bf16"), ("Adam", "fp8"), ("Momentum", "bf16")])
 def test_finalize_fused_dense_opt_bitwise_equal(monkeypatch, opt, mlp_dtype):
-    """The 1-GPU lazy step runs the dense optimizer inside the finalize launch (mlp.hip
-    finalize_opt_kernel); parameters, optimizer slots and the bf16 shadows after graph-replayed
-    steps are bitwise those of the separate dense_opt launch, early or after the sparse join."""
+    """The 1-GPU lazy step runs the dense optimizer inside the wgfin work, which itself runs
+    inside the sparse backward's launch (sparse_fused.hip sfwg_kernel); parameters, optimizer
+    slots, the step counter and the bf16 shadows after graph-replayed steps are bitwise those of
+    wgfin as its own launch and of the separate dense_opt launch, early or after the sparse join."""
     import hipfm.models.deepfm as D
     synth = make_synth("criteo_kaggle", seed=5)
     F, K, layers, B = synth.F, 8, [128, 64, 32], 1024
     params = init_params(synth.feature_size, F, K, layers, False, seed=2)
     out = []
-    for fuse, early in ((True, True), (False, True), (False, False)):
+    for fuse, early, sfwg in ((True, True, True), (True, True, False), (False, True, False),
+                              (False, False, False)):
         monkeypatch.setattr(D, "_FUSE_FIN_OPT", fuse)
         monkeypatch.setattr(D, "_DENSE_EARLY", early)
+        monkeypatch.setattr(D, "_SFWG", sfwg)
         m = NativeDeepFM(synth.feature_size, F, K, layers, [0.5] * 3, batch_size=B, device=DEV,
                          init=False, optimizer=opt, sparse_update="lazy", mlp_dtype=mlp_dtype,
                          field_ranges=synth.field_ranges())
@@ -481,9 +486,12 @@ def test_finalize_fused_dense_opt_bitwise_equal(monkeypatch, opt, mlp_dtype):
             m.train_step(ids, vals, lab, use_graph=True)
         torch.cuda.synchronize()
         assert m._fin_opt_step == fuse
+        assert m._sfwg_step == sfwg
+        m.check_errors()
         out.append([m.p.clone(), m.tv.clone(), m.tw.clone(), m.sd[0].clone(), m.sd[1].clone(),
-                    m.step.clone()] + [w.clone() for w in m.W16])
-    names = ["p", "tv", "tw", "s0", "s1", "step"] + [f"W16[{i}]" for i in range(len(layers))]
+                    m.step.clone()] + [w.clone() for w in m.W16] + [w.clone() for w in m.WT16])
+    names = (["p", "tv", "tw", "s0", "s1", "step"] + [f"W16[{i}]" for i in range(len(layers))] +
+             [f"WT16[{i}]" for i in range(len(layers))])
     for k, ref in enumerate(out[1:]):
         for nm, x, y in zip(names, out[0], ref):
             if not torch.equal(x, y):

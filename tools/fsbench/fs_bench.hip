@@ -27,7 +27,8 @@ int main(int argc, char** argv) {
     while ((1L << bits) < card) ++bits;
     const int pb = bits < max_pb ? bits : max_pb;
     fr[4 * f] = (int)lo; fr[4 * f + 1] = (int)(lo + card); fr[4 * f + 2] = bits; fr[4 * f + 3] = pb;
-    for (int p = 0; p < (1 << pb); ++p) { work.push_back(f); work.push_back(p); }
+    for (int c = 0; c * FS_MAXB < B; ++c)
+      for (int p = 0; p < (1 << pb); ++p) { work.push_back(f); work.push_back(p); work.push_back(c); }
     lo += card;
   }
   std::mt19937_64 rng(1);
@@ -41,7 +42,9 @@ int main(int argc, char** argv) {
       ids[(size_t)b * F + f] = fr[4 * f] + (int)((r * 2654435761L) % card);
     }
   int *d_ids, *d_fr, *d_sk, *d_pm, *d_work, *d_idsT; unsigned* d_err;
-  const int nwork = (int)work.size() / 2;
+  const int nwork = (int)work.size() / 3;
+  int *d_rk, *d_rp;
+  CK(hipMalloc(&d_rk, (size_t)B * F * 4)); CK(hipMalloc(&d_rp, (size_t)B * F * 4));
   CK(hipMalloc(&d_work, work.size() * 4)); CK(hipMalloc(&d_idsT, ids.size() * 4));
   CK(hipMemcpy(d_work, work.data(), work.size() * 4, hipMemcpyHostToDevice));
   CK(hipMalloc(&d_ids, ids.size() * 4)); CK(hipMalloc(&d_fr, fr.size() * 4));
@@ -51,11 +54,11 @@ int main(int argc, char** argv) {
   CK(hipMemset(d_err, 0, 4));
   hipStream_t st; CK(hipStreamCreate(&st));
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
-  for (int it = 0; it < 5; ++it) hfm_field_sort(d_ids, B, F, d_fr, d_work, nwork, d_idsT, d_sk, d_pm, d_err, st);
+  for (int it = 0; it < 5; ++it) hfm_field_sort(d_ids, B, F, d_fr, d_work, nwork, d_idsT, d_rk, d_rp, d_sk, d_pm, d_err, st);
   CK(hipStreamSynchronize(st));
   const int R = 50;
   CK(hipEventRecord(e0, st));
-  for (int it = 0; it < R; ++it) hfm_field_sort(d_ids, B, F, d_fr, d_work, nwork, d_idsT, d_sk, d_pm, d_err, st);
+  for (int it = 0; it < R; ++it) hfm_field_sort(d_ids, B, F, d_fr, d_work, nwork, d_idsT, d_rk, d_rp, d_sk, d_pm, d_err, st);
   CK(hipEventRecord(e1, st));
   CK(hipEventSynchronize(e1));
   float ms; CK(hipEventElapsedTime(&ms, e0, e1));
