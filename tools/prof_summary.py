@@ -36,13 +36,22 @@ def main():
         rows = list(csv.DictReader(open(trace[0])))
         rows.sort(key=lambda r: int(r["Start_Timestamp"]))
         # one step = from the end of one step-closing kernel (the one that advances the step
-        # counter: dense optimizer / fused finalize / wgfin) to the end of the next
+        # counter: dense optimizer / fused finalize / wgfin / sparse+wgfin) to the end of the next;
+        # the median-span step of the timed steps (graph replays) is listed
         idx = [i for i, r in enumerate(rows) if r["Kernel_Name"].startswith(
-            ("step_inc", "void dense_opt_kernel", "void finalize_opt_kernel", "void wgfin_kernel<0"))]
-        if len(idx) >= 3:
-            a, b = idx[len(idx) // 2 - 1], idx[len(idx) // 2]
+            ("step_inc", "void dense_opt_kernel", "void finalize_opt_kernel", "void wgfin_kernel<0",
+             "void sfwg_kernel"))]
+        pairs = [(a, b, int(rows[b]["End_Timestamp"]) - int(rows[a]["End_Timestamp"]))
+                 for a, b in zip(idx, idx[1:])]
+        pairs = [p for p in pairs if p[2] < 1_000_000]       # steps, not eval / setup gaps
+        if pairs:
+            spans = sorted(p[2] for p in pairs)
+            med = spans[len(spans) // 2]
+            a, b, _ = min(pairs, key=lambda p: abs(p[2] - med))
             t0 = int(rows[a]["End_Timestamp"])
-            lines += ["## One steady-state training step (graph replay)", "",
+            lines += ["## One steady-state training step (graph replay; the median-span step)", "",
+                      f"{len(spans)} consecutive step spans: min {spans[0]/1e3:.1f} us, median "
+                      f"{med/1e3:.1f} us, max {spans[-1]/1e3:.1f} us", "",
                       "| start us | dur us | kernel |", "|---:|---:|---|"]
             tot = 0
             for r in rows[a + 1: b + 1]:
