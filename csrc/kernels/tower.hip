@@ -509,6 +509,7 @@ struct W8Job {
   int rows, cols;
   int row0;          // first global row of this job
   int pad;
+  unsigned* amax3;   // [3][rows] row |W| maxima (float bits) for wgfin's delayed scaling, or null
 };
 
 __global__ void __launch_bounds__(256) w8_quant_kernel(const W8Job* __restrict__ jobs, int njobs, int total) {
@@ -529,7 +530,11 @@ __global__ void __launch_bounds__(256) w8_quant_kernel(const W8Job* __restrict__
     const float* s4 = src + 4 * c4;
     *reinterpret_cast<uint32_t*>(dst + 4 * c4) = pack4_fp8(s4[0] * q, s4[1] * q, s4[2] * q, s4[3] * q);
   }
-  if (lane == 0) jb.sdq[r] = 1.f / q;
+  if (lane == 0) {
+    jb.sdq[r] = 1.f / q;
+    if (jb.amax3)  // every slot: the next fused step reads a valid previous-step maximum
+      for (int k = 0; k < 3; ++k) jb.amax3[k * jb.rows + r] = __float_as_uint(m);
+  }
 }
 
 HFM_API int hfm_w8_quant(const void* jobs_dev, int njobs, int total_rows, hipStream_t st) {

@@ -34,6 +34,13 @@ struct WgFinJob {
   float* gb;       // gradient of b_i [Np_i]
   bf16* w16;       // bf16 shadows of W_i: [Np_i, Kp_i] and [Kp_i, Np_i] (MFMA operands)
   bf16* wt16;
+  // fp8 tower (else null): e4m3 W_i [Np_i, Kp_i] with per-output-channel power-of-two scales
+  // (sdq = dequantization factor), from the row |W| max of the PREVIOUS step (delayed scaling,
+  // one binade of headroom); amax3 [3][Np_i] (float bits) rotates with the step: this step's
+  // row maxima are atomicMax-ed into slot (t % 3), slot (t - 1) % 3 is read, (t + 1) % 3 zeroed
+  uint8_t* w8;
+  float* sdq;
+  unsigned* amax3;
   int M, N;        // Np_i, Kp_i
   int tiles_m, tiles_n;
   int tile0;       // first counter of this job
@@ -176,6 +183,15 @@ __device__ __forceinline__ void wgfin_body(const WgFinArgs& a, int b, WgfSmem& s
       for (int z = 0; z < NSM; ++z)
         bv[z] = (brow && z < a.ns) ? hx_ldf(jb.bslab + (size_t)z * jb.M + row0 + tid) : 0.f;
       if (brow) wgf_load_state<OPT>(a, jb.gb + row0 + tid, bp, ba, bc);
+      const bool q8 = OPT >= 0 && jb.w8 != nullptr;
+      unsigned slot = 0;
+      float am[4] = {0.f, 0.f, 0.f, 0.f};
+      if (q8) {
+        slot = (unsigned)((*a.o.step + 1) % 3);
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          am[q] = __uint_as_float(jb.amax3[((slot + 2) % 3) * jb.M + row0 + ((tid + q * 256) >> 5)]);
+      }
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int e = tid + q * 256, r = e >> 5, c = e & 31;
@@ -189,7 +205,19 @@ __device__ __forceinline__ void wgfin_body(const WgFinArgs& a, int b, WgfSmem& s
           jb.w16[(size_t)(row0 + r) * jb.N + col0 + c] = f2bf(np);
           jb.wt16[(size_t)(col0 + c) * jb.M + row0 + r] = f2bf(np);
         }
+        if (q8) {  // row r's 32 columns sit in 32 consecutive lanes
+          const float qs = 0.5f * fp8_pow2_scale(am[q]);
+          jb.w8[(size_t)(row0 + r) * jb.N + col0 + c] = (uint8_t)(pack4_fp8(np * qs, 0.f, 0.f, 0.f) & 0xFFu);
+          float m = fabsf(np);
+#pragma unroll
+          for (int o = 1; o < 32; o <<= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+          if (c == 0) {
+            jb.sdq[row0 + r] = 1.f / qs;
+            atomicMax(jb.amax3 + slot * jb.M + row0 + r, __float_as_uint(m));
+          }
+        }
       }
+      if (q8 && tn == 0 && tid < 32) jb.amax3[((slot + 1) % 3) * jb.M + row0 + tid] = 0u;
       if (brow) {
         float v = 0.f;
 #pragma unroll

@@ -268,17 +268,19 @@ class NativeDeepFM:
             shadow.append(ShadowSeg(s.off, self.Np[i], self.Kp[i], w16.data_ptr(), wt16.data_ptr()))
         self._shadow_dev = KN.struct_array_to_device(shadow, dev)
         self._nshadow = len(shadow)
-        self.W8, self.sW = [], []
+        self.W8, self.sW, self.W8amax = [], [], []
         if self.fp8:
             jobs, row0 = [], 0
             for i in range(len(self.layers)):
                 s = self.dense_segs[f"Deep-part/mlp{i}/weights"]
                 w8 = torch.zeros(self.Np[i], self.Kp[i], dtype=torch.uint8, device=dev)
                 sw = torch.ones(self.Np[i], dtype=torch.float32, device=dev)
+                am = torch.zeros(3, self.Np[i], dtype=torch.int32, device=dev)   # wgfin delayed scaling
                 self.W8.append(w8)
                 self.sW.append(sw)
+                self.W8amax.append(am)
                 jobs.append(W8Job(self.p.data_ptr() + 4 * s.off, w8.data_ptr(), sw.data_ptr(),
-                                  self.Np[i], self.Kp[i], row0, 0))
+                                  self.Np[i], self.Kp[i], row0, 0, am.data_ptr()))
                 row0 += self.Np[i]
             self._w8_jobs = KN.struct_array_to_device(jobs, dev)
             self._w8_rows = row0
@@ -587,6 +589,9 @@ class NativeDeepFM:
             j.gw = g0 + 4 * self.dense_segs[f"Deep-part/mlp{i}/weights"].off
             j.gb = g0 + 4 * self.dense_segs[f"Deep-part/mlp{i}/biases"].off
             j.w16, j.wt16 = self.W16[i].data_ptr(), self.WT16[i].data_ptr()
+            if self.fp8:      # the optimizer tail also writes the fp8 weights (no w8_quant launch)
+                j.w8, j.sdq, j.amax3 = (self.W8[i].data_ptr(), self.sW[i].data_ptr(),
+                                        self.W8amax[i].data_ptr())
             j.M, j.N, j.tiles_m, j.tiles_n = Np, Kp, Np // 32, Kp // 32
             j.tile0, j.wg0 = tile0, wg0
             tile0 += j.tiles_m * j.tiles_n
@@ -1203,7 +1208,7 @@ class NativeDeepFM:
         self._fin_opt_step = fused_opt          # observable by tests: which dense-optimizer path ran
         self._sfwg_step = self._sfwg_now
         if fused_opt:
-            if self.fp8 and not self._sfwg_now:
+            if self.fp8 and not _WGFIN:       # (wgfin writes the fp8 weights itself)
                 KN.w8_quant(self._w8_jobs, len(self.layers), self._w8_rows)
         elif self._dense_early:
             self._dense_opt()
@@ -1228,10 +1233,7 @@ class NativeDeepFM:
         out = self._sparse_backward(B, idx, tv, presorted=presorted)
         if out is not None:
             self._sparse_update(*out)
-        if self._sfwg_now:
-            self._sfwg_now = False
-            if self.fp8:
-                KN.w8_quant(self._w8_jobs, len(self.layers), self._w8_rows)
+        self._sfwg_now = False
         if split or eng is not None:
             main.wait_stream(self._comm_stream)
         if work is not None:

@@ -76,6 +76,7 @@ class FinOpt(C.Structure):
 class WgFinJob(C.Structure):
     _fields_ = [("A", c_void_p), ("B", c_void_p), ("slab", c_void_p), ("bslab", c_void_p),
                 ("gw", c_void_p), ("gb", c_void_p), ("w16", c_void_p), ("wt16", c_void_p),
+                ("w8", c_void_p), ("sdq", c_void_p), ("amax3", c_void_p),
                 ("M", c_int), ("N", c_int), ("tiles_m", c_int),
                 ("tiles_n", c_int), ("tile0", c_int), ("wg0", c_int)]
 
@@ -145,7 +146,7 @@ class TowerArgs(C.Structure):
 
 class W8Job(C.Structure):
     _fields_ = [("src", c_void_p), ("dst", c_void_p), ("sdq", c_void_p), ("rows", c_int),
-                ("cols", c_int), ("row0", c_int), ("pad", c_int)]
+                ("cols", c_int), ("row0", c_int), ("pad", c_int), ("amax3", c_void_p)]
 
 
 class WgJob(C.Structure):

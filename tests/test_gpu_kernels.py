@@ -466,7 +466,8 @@ def test_finalize_fused_dense_opt_bitwise_equal(monkeypatch, opt, mlp_dtype):
     """The 1-GPU lazy step runs the dense optimizer inside the wgfin work, which itself runs
     inside the sparse backward's launch (sparse_fused.hip sfwg_kernel); parameters, optimizer
     slots, the step counter and the bf16 shadows after graph-replayed steps are bitwise those of
-    wgfin as its own launch and of the separate dense_opt launch, early or after the sparse join."""
+    wgfin as its own launch and of the separate dense_opt launch, early or after the sparse join
+    (fp8: bitwise between the two wgfin variants, close to the dense_opt ones)."""
     import hipfm.models.deepfm as D
     synth = make_synth("criteo_kaggle", seed=5)
     F, K, layers, B = synth.F, 8, [128, 64, 32], 1024
@@ -494,6 +495,12 @@ def test_finalize_fused_dense_opt_bitwise_equal(monkeypatch, opt, mlp_dtype):
              [f"WT16[{i}]" for i in range(len(layers))])
     for k, ref in enumerate(out[1:]):
         for nm, x, y in zip(names, out[0], ref):
+            if mlp_dtype == "fp8" and k >= 1:
+                # wgfin writes the fp8 weights from the previous step's row maxima (delayed
+                # scaling), the separate launch from the current ones: values agree up to fp8
+                # rounding of the few weights the two scales treat differently
+                assert torch.allclose(x.float(), y.float(), rtol=2e-2, atol=2e-4), (k + 1, nm)
+                continue
             if not torch.equal(x, y):
                 bad = (x != y).nonzero().flatten()[:8].tolist()
                 d = (x.float() - y.float()).abs().max().item()
