@@ -389,6 +389,9 @@ __global__ void __launch_bounds__(256) sf_tile_kernel(SfArgs A) {
 // the wgfin half's register footprint must not cut the sparse tiles' occupancy (6 waves / SIMD)
 constexpr int SFWG_PF = 2;
 constexpr int SFWG_MAXNS = 4;
+// combine tail one element at a time: 84 VGPRs (4 waves / SIMD) vs 113 (3) for all 4 at once;
+// same-box bf16 0.1109-0.1114 (1) / 0.1120-0.1128 (2) / 0.1169-0.1171 (4) ms/step
+constexpr int SFWG_TQ = 1;
 
 template <int K>
 union SfwgSmem {
@@ -401,7 +404,7 @@ template <int K, int OPT>
 __global__ void __launch_bounds__(256) sfwg_kernel(SfArgs A, WgFinArgs W, unsigned* done) {
   __shared__ SfwgSmem<K> sm;
   const int nw = W.tile_wgs + 1;
-  if ((int)blockIdx.x < nw) wgfin_body<OPT, SFWG_PF, SFWG_MAXNS>(W, blockIdx.x, sm.wg);
+  if ((int)blockIdx.x < nw) wgfin_body<OPT, SFWG_PF, SFWG_MAXNS, SFWG_TQ>(W, blockIdx.x, sm.wg);
   else sf_tile_body<K, 0, OPT>(A, (int)blockIdx.x - nw, sm.sf);
   __syncthreads();
   if (threadIdx.x == 0) {

@@ -106,8 +106,8 @@ __device__ __forceinline__ void wgf_apply(const WgFinArgs& a, float lr_t, float*
 }
 
 // workgroup b of the wgfin work (b < tile_wgs: a tile split; b == tile_wgs: the head reduction);
-// PF: k-steps in flight per wave, NSM: largest NS (both size the register footprint)
-template <int OPT, int PF, int NSM>
+// PF: k-steps in flight per wave, NSM: largest NS, TQ: combine batch (all size the registers)
+template <int OPT, int PF, int NSM, int TQ = 4>
 __device__ __forceinline__ void wgfin_body(const WgFinArgs& a, int b, WgfSmem& sm) {
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const float lr_t = OPT == OPT_ADAM ? adam_lr_t(a.o.h, *a.o.step + 1) : a.o.h.lr;
@@ -169,51 +169,50 @@ __device__ __forceinline__ void wgfin_body(const WgFinArgs& a, int b, WgfSmem& s
     if (sm.last) {  // the tile's last workgroup: sum the NS slabs in slab order, then the optimizer
       const float* base = jb.slab + (size_t)row0 * jb.N + col0;
       const bool brow = tn == 0 && tid < 32;
-      float sv[4][NSM], bv[NSM], pv[4], av[4], cv[4], bp = 0.f, ba = 0.f, bc = 0.f;
-      // every load of this thread in flight at once: slabs, parameters, optimizer slots
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int e = tid + q * 256, r = e >> 5, c = e & 31;
-#pragma unroll
-        for (int z = 0; z < NSM; ++z)
-          sv[q][z] = z < a.ns ? hx_ldf(base + ((size_t)z * jb.M + r) * jb.N + c) : 0.f;
-        wgf_load_state<OPT>(a, jb.gw + (size_t)(row0 + r) * jb.N + col0 + c, pv[q], av[q], cv[q]);
-      }
+      float bv[NSM], bp = 0.f, ba = 0.f, bc = 0.f;
 #pragma unroll
       for (int z = 0; z < NSM; ++z)
         bv[z] = (brow && z < a.ns) ? hx_ldf(jb.bslab + (size_t)z * jb.M + row0 + tid) : 0.f;
       if (brow) wgf_load_state<OPT>(a, jb.gb + row0 + tid, bp, ba, bc);
       const bool q8 = OPT >= 0 && jb.w8 != nullptr;
-      unsigned slot = 0;
-      float am[4] = {0.f, 0.f, 0.f, 0.f};
-      if (q8) {
-        slot = (unsigned)((*a.o.step + 1) % 3);
+      const unsigned slot = q8 ? (unsigned)((*a.o.step + 1) % 3) : 0u;
+      // this thread's 4 elements in batches of TQ, every load of a batch in flight at once:
+      // slabs, parameters, optimizer slots (TQ = 4: one round trip; 2: fewer live registers)
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
-          am[q] = __uint_as_float(jb.amax3[((slot + 2) % 3) * jb.M + row0 + ((tid + q * 256) >> 5)]);
-      }
+      for (int q0 = 0; q0 < 4; q0 += TQ) {
+        float sv[TQ][NSM], pv[TQ], av[TQ], cv[TQ], am[TQ];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int e = tid + q * 256, r = e >> 5, c = e & 31;
-        float v = 0.f;
+        for (int q = 0; q < TQ; ++q) {
+          const int e = tid + (q0 + q) * 256, r = e >> 5, c = e & 31;
 #pragma unroll
-        for (int z = 0; z < NSM; ++z)
-          if (z < a.ns) v += sv[q][z];
-        const float np = wgf_update<OPT>(a, lr_t, jb.gw + (size_t)(row0 + r) * jb.N + col0 + c, v, pv[q],
-                                         av[q], cv[q]);
-        if (OPT >= 0) {
-          jb.w16[(size_t)(row0 + r) * jb.N + col0 + c] = f2bf(np);
-          jb.wt16[(size_t)(col0 + c) * jb.M + row0 + r] = f2bf(np);
+          for (int z = 0; z < NSM; ++z)
+            sv[q][z] = z < a.ns ? hx_ldf(base + ((size_t)z * jb.M + r) * jb.N + c) : 0.f;
+          wgf_load_state<OPT>(a, jb.gw + (size_t)(row0 + r) * jb.N + col0 + c, pv[q], av[q], cv[q]);
+          am[q] = q8 ? __uint_as_float(jb.amax3[((slot + 2) % 3) * jb.M + row0 + r]) : 0.f;
         }
-        if (q8) {  // row r's 32 columns sit in 32 consecutive lanes
-          const float qs = 0.5f * fp8_pow2_scale(am[q]);
-          jb.w8[(size_t)(row0 + r) * jb.N + col0 + c] = (uint8_t)(pack4_fp8(np * qs, 0.f, 0.f, 0.f) & 0xFFu);
-          float m = fabsf(np);
 #pragma unroll
-          for (int o = 1; o < 32; o <<= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
-          if (c == 0) {
-            jb.sdq[row0 + r] = 1.f / qs;
-            atomicMax(jb.amax3 + slot * jb.M + row0 + r, __float_as_uint(m));
+        for (int q = 0; q < TQ; ++q) {
+          const int e = tid + (q0 + q) * 256, r = e >> 5, c = e & 31;
+          float v = 0.f;
+#pragma unroll
+          for (int z = 0; z < NSM; ++z)
+            if (z < a.ns) v += sv[q][z];
+          const float np = wgf_update<OPT>(a, lr_t, jb.gw + (size_t)(row0 + r) * jb.N + col0 + c, v, pv[q],
+                                           av[q], cv[q]);
+          if (OPT >= 0) {
+            jb.w16[(size_t)(row0 + r) * jb.N + col0 + c] = f2bf(np);
+            jb.wt16[(size_t)(col0 + c) * jb.M + row0 + r] = f2bf(np);
+          }
+          if (q8) {  // row r's 32 columns sit in 32 consecutive lanes
+            const float qs = 0.5f * fp8_pow2_scale(am[q]);
+            jb.w8[(size_t)(row0 + r) * jb.N + col0 + c] = (uint8_t)(pack4_fp8(np * qs, 0.f, 0.f, 0.f) & 0xFFu);
+            float m = fabsf(np);
+#pragma unroll
+            for (int o = 1; o < 32; o <<= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+            if (c == 0) {
+              jb.sdq[row0 + r] = 1.f / qs;
+              atomicMax(jb.amax3 + slot * jb.M + row0 + r, __float_as_uint(m));
+            }
           }
         }
       }

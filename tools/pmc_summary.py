@@ -13,10 +13,12 @@ import glob
 import os
 import sys
 
-OURS = ("tower_kernel", "wgfin_kernel", "fm_fwd", "wgrad_group", "finalize_kernel", "sf_tile", "sf_carry",
+OURS = ("tower_kernel", "wgfin_kernel", "sfwg_kernel", "dense_sweep", "fm_fwd", "wgrad_group", "finalize_kernel", "sf_tile", "sf_carry",
         "fs_sort", "fs_transpose", "dense_opt", "w8_quant", "sh_", "seg_", "onesweep", "lsd_",
         "gemm_nt", "head_kernel", "rcclGenericKernel")
 SIMDS = 1024
+HBM_BPS = 8e12       # MI355X HBM3E peak
+BF16_PEAK_TF = 2500.0  # dense bf16 MFMA peak (no sparsity)
 CLOCK_HZ = 2.4e9     # MI355X peak engine clock: MFMA util = busy SIMD-cycles / (SIMDs x duration x clock)
 
 
@@ -51,9 +53,9 @@ def main():
             durs[k] += list(dur[k].values())
     lines = [f"# {title}", "", "Mean per dispatch over the profiled run (warm-up, timed steps, eval).",
              "Sources: " + ", ".join(f"`{os.path.basename(d.rstrip('/'))}`" for d in dirs), "",
-             "| kernel | calls | us | fetch MB | fetch GB/s | write MB | write GB/s | MFMA util % | "
-             "MFMA TF/s | LDS conflict cyc / LDS inst |",
-             "|---|---:|---:|---:|---:|---:|---:|---:|---:|---:|"]
+             "| kernel | calls | us | fetch MB | fetch GB/s | write MB | write GB/s | HBM r+w % of 8 TB/s | "
+             "MFMA util % | MFMA TF/s | % of 2.5 PF bf16 | LDS conflict cyc / LDS inst |",
+             "|---|---:|---:|---:|---:|---:|---:|---:|---:|---:|---:|---:|"]
     for k in sorted(ctr, key=lambda k: -sum(durs[k])):
         c = ctr[k]
         t = sum(durs[k]) / max(1, len(durs[k]))
@@ -68,10 +70,12 @@ def main():
         util = None if busy is None else 100.0 * busy / (SIMDS * t * CLOCK_HZ)
         tf = None if not ("SQ_INSTS_VALU_MFMA_MOPS_BF16" in c or "SQ_INSTS_VALU_MFMA_MOPS_F8" in c) \
             else mops * 512 / t / 1e12
+        hbm = None if f is None or w is None else 100.0 * (f + w) * 1024 / t / HBM_BPS
         lines.append(
             f"| `{k}` | {len(durs[k])} | {t * 1e6:.1f} | {fmt(None if f is None else f / 1024, 2)} | "
             f"{fmt(None if f is None else f * 1024 / t / 1e9, 0)} | {fmt(None if w is None else w / 1024, 2)} | "
-            f"{fmt(None if w is None else w * 1024 / t / 1e9, 0)} | {fmt(util)} | {fmt(tf, 2)} | "
+            f"{fmt(None if w is None else w * 1024 / t / 1e9, 0)} | {fmt(hbm)} | {fmt(util)} | {fmt(tf, 2)} | "
+            f"{fmt(None if tf is None else 100.0 * tf / BF16_PEAK_TF, 2)} | "
             f"{fmt(None if not lds else conf / lds, 3)} |")
     lines += ["", "MFMA util = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x kernel duration x 2.4 GHz). "
               "The deep tower is 128/64/32 wide: its GEMMs are latency- and LDS-bound, not MFMA-bound; "
