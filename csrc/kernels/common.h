@@ -127,6 +127,38 @@ struct FinOpt {
   unsigned* done_ctr;
 };
 
+// One element of the dense optimizer sweep (+ bf16 shadows): dense_opt_kernel and the merged
+// owner-apply launch (shard.hip) share it, so their results are bitwise equal.
+template <int OPT>
+__device__ __forceinline__ void dense_opt_apply(float* __restrict__ p, float gi, float* __restrict__ s0,
+                                                float* __restrict__ s1, long i, const OptHyper& h, float lr_t,
+                                                const ShadowSeg* __restrict__ segs, int nseg) {
+  float pi = p[i];
+  float a = (OPT != OPT_GD) ? s0[i] : 0.f;
+  float c = (OPT == OPT_ADAM || OPT == OPT_FTRL) ? s1[i] : 0.f;
+  opt_update<OPT>(pi, gi, a, c, h, lr_t);
+  p[i] = pi;
+  if (OPT != OPT_GD) s0[i] = a;
+  if (OPT == OPT_ADAM || OPT == OPT_FTRL) s1[i] = c;
+  for (int s = 0; s < nseg; ++s) {
+    const long rel = i - segs[s].off;
+    const long sz = (long)segs[s].rows * segs[s].cols;
+    if (rel >= 0 && rel < sz) {
+      const int r = (int)(rel / segs[s].cols), cc = (int)(rel % segs[s].cols);
+      segs[s].w16[rel] = f2bf(pi);
+      segs[s].wt16[(long)cc * segs[s].rows + r] = f2bf(pi);
+    }
+  }
+}
+
+template <int OPT>
+__device__ __forceinline__ void dense_opt_elem(float* __restrict__ p, const float* __restrict__ g,
+                                               float* __restrict__ s0, float* __restrict__ s1, long i,
+                                               const OptHyper& h, float lr_t, const ShadowSeg* __restrict__ segs,
+                                               int nseg) {
+  dense_opt_apply<OPT>(p, g[i], s0, s1, i, h, lr_t, segs, nseg);
+}
+
 template <int OPT>
 __device__ __forceinline__ void fin_opt_apply(const FinOpt& o, float lr_t, const float* dst, float gv) {
   const long i = dst - o.g;

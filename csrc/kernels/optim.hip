@@ -141,24 +141,8 @@ __global__ void __launch_bounds__(256) dense_opt_kernel(
     long n, OptHyper h, int64_t* __restrict__ step, const ShadowSeg* __restrict__ segs, int nseg,
     unsigned* __restrict__ done_ctr) {
   const float lr_t = lr_t_of<OPT>(h, step);
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
-    float pi = p[i];
-    float a = (OPT != OPT_GD) ? s0[i] : 0.f;
-    float c = (OPT == OPT_ADAM || OPT == OPT_FTRL) ? s1[i] : 0.f;
-    opt_update<OPT>(pi, g[i], a, c, h, lr_t);
-    p[i] = pi;
-    if (OPT != OPT_GD) s0[i] = a;
-    if (OPT == OPT_ADAM || OPT == OPT_FTRL) s1[i] = c;
-    for (int s = 0; s < nseg; ++s) {
-      const long rel = i - segs[s].off;
-      const long sz = (long)segs[s].rows * segs[s].cols;
-      if (rel >= 0 && rel < sz) {
-        const int r = (int)(rel / segs[s].cols), cc = (int)(rel % segs[s].cols);
-        segs[s].w16[rel] = f2bf(pi);
-        segs[s].wt16[(long)cc * segs[s].rows + r] = f2bf(pi);
-      }
-    }
-  }
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    dense_opt_elem<OPT>(p, g, s0, s1, i, h, lr_t, segs, nseg);
   // the step counter advances once every block has read it (last block to finish does it):
   // replaces a separate 1-thread step_inc launch at the end of every training step
   if (done_ctr) {

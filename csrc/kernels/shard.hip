@@ -105,24 +105,26 @@ __global__ void __launch_bounds__(SH_THREADS) sh_scatter_kernel(
     const int* __restrict__ cnt, int nb, int* __restrict__ send_ids, int* __restrict__ upos,
     int* __restrict__ send_cnt, unsigned* __restrict__ err) {
   __shared__ int off[SH_MAXN];
+  __shared__ int tot[SH_MAXN];
   __shared__ int wc[4][SH_MAXN];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int U = *num_u;
-  if (tid < N) {
-    int s = 0, tot = 0;
-    for (int b = 0; b < nb; ++b) {
-      const int c = cnt[b * N + tid];
-      if (b < (int)blockIdx.x) s += c;
-      tot += c;
-    }
-    off[tid] = s;
-    if (blockIdx.x == 0) {
-      send_cnt[tid] = tot;
-      if (tot > C) atomicOr(err, 2u);
-    }
-  }
-  if (tid < SH_MAXN) wc[0][tid] = wc[1][tid] = wc[2][tid] = wc[3][tid] = 0;
+  if (tid < SH_MAXN) off[tid] = tot[tid] = wc[0][tid] = wc[1][tid] = wc[2][tid] = wc[3][tid] = 0;
   __syncthreads();
+  // owner offsets of this block (counts of the blocks before it) and totals: every count loaded
+  // by some thread at once (integer sums: order-free) -- a per-owner serial loop over the nb
+  // blocks cost one load latency per block (~47 us at nb = 156)
+  for (int e = tid; e < nb * N; e += SH_THREADS) {
+    const int b = e / N, o = e - b * N;
+    const int c = cnt[e];
+    if (b < (int)blockIdx.x) atomicAdd(&off[o], c);
+    atomicAdd(&tot[o], c);
+  }
+  __syncthreads();
+  if (blockIdx.x == 0 && tid < N) {
+    send_cnt[tid] = tot[tid];
+    if (tot[tid] > C) atomicOr(err, 2u);
+  }
   const int w0 = blockIdx.x * SH_TILE + wv * 64 * SH_ITEMS;
   const unsigned long long lt = (1ull << lane) - 1ull;
   int own[SH_ITEMS], rnk[SH_ITEMS];
@@ -161,6 +163,120 @@ __global__ void __launch_bounds__(SH_THREADS) sh_scatter_kernel(
   }
 }
 
+// Routing of the sorted slot ids in TWO launches (replaces segments + bucket: 7 launches).
+// The sorted list is cut into tiles of RT_TILE slots; a slot heads a run when its id differs from
+// the previous slot's.  sh_route_count: heads per owner and in total, per tile.  sh_route_scatter:
+// each tile sums the counts of the tiles before it (every count loaded at once), then ranks its
+// heads per owner within each wave (ballots on the owner bits; wave-contiguous slot chunks keep the
+// id order), so owner bucket o holds this rank's unique ids of owner o in id order -- the layout
+// segments + sh_bucket produced.  Outputs: sid_incl[i] (1-based unique index of slot i's id),
+// send_ids[o][c] (-1 past the bucket's count), upos[u] = o*C + c, send_cnt[o], num_u.
+constexpr int RT_ITEMS = 16;
+constexpr int RT_TILE = SH_THREADS * RT_ITEMS;
+
+__global__ void __launch_bounds__(SH_THREADS) sh_route_count_kernel(const int* __restrict__ sk, int n, int N,
+                                                                   int* __restrict__ tcnt) {
+  __shared__ int h[SH_MAXN + 1];
+  const int tid = threadIdx.x;
+  if (tid <= N) h[tid] = 0;
+  __syncthreads();
+  const int i0 = blockIdx.x * RT_TILE;
+  int nh = 0;
+#pragma unroll 4
+  for (int k = 0; k < RT_ITEMS; ++k) {
+    const int i = i0 + k * SH_THREADS + tid;
+    if (i < n) {
+      const int key = sk[i];
+      if (i == 0 || key != sk[i - 1]) {
+        atomicAdd(&h[key % N], 1);
+        ++nh;
+      }
+    }
+  }
+  atomicAdd(&h[N], nh);
+  __syncthreads();
+  if (tid <= N) tcnt[blockIdx.x * (N + 1) + tid] = h[tid];
+}
+
+__global__ void __launch_bounds__(SH_THREADS) sh_route_scatter_kernel(
+    const int* __restrict__ sk, int n, int N, int nbits, int C, const int* __restrict__ tcnt, int nt,
+    int* __restrict__ sid_incl, int* __restrict__ send_ids, int* __restrict__ upos, int* __restrict__ send_cnt,
+    int* __restrict__ num_u, unsigned* __restrict__ err) {
+  __shared__ int off[SH_MAXN + 1];
+  __shared__ int tot[SH_MAXN + 1];
+  __shared__ int wc[4][SH_MAXN + 1];  // per wave: heads per owner, [N]: all heads
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  if (tid <= SH_MAXN) off[tid] = tot[tid] = wc[0][tid] = wc[1][tid] = wc[2][tid] = wc[3][tid] = 0;
+  __syncthreads();
+  for (int e = tid; e < nt * (N + 1); e += SH_THREADS) {
+    const int b = e / (N + 1), o = e - b * (N + 1);
+    const int c = tcnt[e];
+    if (b < (int)blockIdx.x) atomicAdd(&off[o], c);
+    atomicAdd(&tot[o], c);
+  }
+  __syncthreads();
+  if (blockIdx.x == 0) {
+    if (tid < N) {
+      send_cnt[tid] = tot[tid];
+      if (tot[tid] > C) atomicOr(err, 2u);
+    }
+    if (tid == 0) *num_u = tot[N];
+  }
+  for (int e = blockIdx.x * SH_THREADS + tid; e < N * C; e += gridDim.x * SH_THREADS) {
+    const int o = e / C;
+    if (e - o * C >= tot[o]) send_ids[e] = -1;  // unused capacity: padding entries
+  }
+  const int w0 = blockIdx.x * RT_TILE + wv * 64 * RT_ITEMS;
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  int key[RT_ITEMS], own[RT_ITEMS], rnk[RT_ITEMS], hin[RT_ITEMS];
+  unsigned hmask = 0;
+  int run = 0;  // heads in this wave's earlier chunks (wave-uniform)
+#pragma unroll
+  for (int k = 0; k < RT_ITEMS; ++k) {
+    const int i = w0 + k * 64 + lane;
+    const bool valid = i < n;
+    key[k] = valid ? sk[i] : 0;
+    const bool head = valid && (i == 0 || key[k] != sk[i - 1]);
+    const unsigned long long hb = __ballot(head);
+    hin[k] = run + __popcll(hb & (lt | (1ull << lane)));  // heads up to and including slot i
+    run += __popcll(hb);
+    const int o = head ? key[k] % N : 0;
+    unsigned long long peers = hb;
+    for (int bit = 0; bit < nbits; ++bit) {
+      const bool bset = (o >> bit) & 1;
+      const unsigned long long bal = __ballot(bset);
+      peers &= bset ? bal : ~bal;
+    }
+    const int rk = __popcll(peers & lt);
+    const int old = wc[wv][o];  // in-order LDS ops of one wave: all lanes read before the update
+    own[k] = o;
+    rnk[k] = old + rk;
+    if (head) hmask |= 1u << k;
+    if (head && rk == 0) wc[wv][o] = old + __popcll(peers);
+  }
+  if (lane == 0) wc[wv][N] = run;
+  __syncthreads();
+  int hw = off[N];
+  for (int w = 0; w < wv; ++w) hw += wc[w][N];
+#pragma unroll
+  for (int k = 0; k < RT_ITEMS; ++k) {
+    const int i = w0 + k * 64 + lane;
+    if (i >= n) continue;
+    sid_incl[i] = hw + hin[k];
+    if (!((hmask >> k) & 1u)) continue;
+    const int o = own[k], u = hw + hin[k] - 1;
+    int pos = off[o] + rnk[k];
+    for (int w = 0; w < wv; ++w) pos += wc[w][o];
+    if (pos < C) {
+      send_ids[o * C + pos] = key[k];
+      upos[u] = o * C + pos;
+    } else {
+      upos[u] = -1;
+      atomicOr(err, 2u);
+    }
+  }
+}
+
 // fm_fwd row index of every slot: the received row of its unique id
 __global__ void sh_slot_rows_kernel(const int* __restrict__ perm, const int* __restrict__ sid_incl,
                                     const int* __restrict__ upos, int n, int* __restrict__ idx) {
@@ -174,8 +290,14 @@ __global__ void sh_slot_rows_kernel(const int* __restrict__ perm, const int* __r
 // Training steps (tags != null) also stamp the owner-side request tags here, at the start of the
 // step: the requests of the backward exchange are this step's requests, so the owner update at
 // the end of the step needs no separate tagging launch on the critical path.
+// request e = p*C + c of the received ids: [N][C] blocks (rstride == C, or 0 = contiguous), or
+// this rank's column of the all-gathered [N][N][C] requests (base + rank*C, rstride = N*C)
+__device__ __forceinline__ int sh_rid(const int* __restrict__ r, int e, int C, int rstride) {
+  return rstride > C ? r[(size_t)(e / C) * rstride + e % C] : r[e];
+}
+
 template <int K>
-__global__ void sh_serve_kernel(const int* __restrict__ recv_ids, int total, int N, int C,
+__global__ void sh_serve_kernel(const int* __restrict__ recv_ids, int total, int N, int C, int rstride,
                                 const float* __restrict__ tv, const float* __restrict__ tw, long ldv,
                                 long ldw, float* __restrict__ rows, const int64_t* __restrict__ step,
                                 ShTable T) {
@@ -183,7 +305,7 @@ __global__ void sh_serve_kernel(const int* __restrict__ recv_ids, int total, int
   const int gt = blockIdx.x * blockDim.x + threadIdx.x;
   const int e = gt / LPS, sub = gt % LPS;
   if (e >= total) return;
-  const int id = recv_ids[e];
+  const int id = sh_rid(recv_ids, e, C, rstride);
   f32x4 v = {0.f, 0.f, 0.f, 0.f};
   float w = 0.f;
   if (id >= 0) {
@@ -199,26 +321,26 @@ __global__ void sh_serve_kernel(const int* __restrict__ recv_ids, int total, int
   if (sub == 0) *reinterpret_cast<f32x4*>(o + K) = f32x4{w, 0.f, 0.f, 0.f};
 }
 
-__global__ void sh_owner_tag_kernel(const int* __restrict__ recv_ids, int total, int N, int C,
+__global__ void sh_owner_tag_kernel(const int* __restrict__ recv_ids, int total, int N, int C, int rstride,
                                     const int64_t* __restrict__ step, ShTable T) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= total) return;
-  const int id = recv_ids[e];
+  const int id = sh_rid(recv_ids, e, C, rstride);
   if (id < 0) return;
   sh_insert(T, N, (unsigned)(id / N), e / C, (unsigned)(e % C), (unsigned)(*step + 1));
 }
 
 // MODE 0: lazy optimizer OPT on the owner's row; 1: tf1_dense scatter into (Gv, Gw)
 template <int K, int MODE, int OPT>
-__global__ void sh_owner_apply_kernel(const int* __restrict__ recv_ids, int total, int N, int C,
-                                      const float* __restrict__ recv_g, ShTable T, float* tv, float* tw,
-                                      float* s0v, float* s1v, float* s0w, float* s1w, long ldv, long ldw,
-                                      float* Gv, float* Gw, OptHyper h, const int64_t* __restrict__ step) {
+__device__ __forceinline__ void sh_owner_apply_elem(int gt, const int* __restrict__ recv_ids, int total, int N,
+                                                    int C, int rstride, const float* __restrict__ recv_g,
+                                                    ShTable T, float* tv, float* tw, float* s0v, float* s1v,
+                                                    float* s0w, float* s1w, long ldv, long ldw, float* Gv,
+                                                    float* Gw, OptHyper h, const int64_t* __restrict__ step) {
   constexpr int LPS = K / 4, RW = K + 4;
-  const int gt = blockIdx.x * blockDim.x + threadIdx.x;
   const int e = gt / LPS, sub = gt % LPS;
   if (e >= total) return;
-  const int id = recv_ids[e];
+  const int id = sh_rid(recv_ids, e, C, rstride);
   if (id < 0) return;
   const int p = e / C;
   const size_t row = (size_t)(id / N);
@@ -271,6 +393,15 @@ __global__ void sh_owner_apply_kernel(const int* __restrict__ recv_ids, int tota
   }
 }
 
+template <int K, int MODE, int OPT>
+__global__ void sh_owner_apply_kernel(const int* __restrict__ recv_ids, int total, int N, int C, int rstride,
+                                      const float* __restrict__ recv_g, ShTable T, float* tv, float* tw,
+                                      float* s0v, float* s1v, float* s0w, float* s1w, long ldv, long ldw,
+                                      float* Gv, float* Gw, OptHyper h, const int64_t* __restrict__ step) {
+  sh_owner_apply_elem<K, MODE, OPT>(blockIdx.x * blockDim.x + threadIdx.x, recv_ids, total, N, C, rstride,
+                                    recv_g, T, tv, tw, s0v, s1v, s0w, s1w, ldv, ldw, Gv, Gw, h, step);
+}
+
 // ------------------------------------------------------------------------------------ host API
 HFM_API int hfm_sh_count_blocks(int nmax) { return (nmax + SH_TILE - 1) / SH_TILE; }
 
@@ -286,6 +417,21 @@ HFM_API int hfm_sh_bucket(const int* ukeys, const int* num_u, int nmax, int N, i
   hipLaunchKernelGGL(sh_count_kernel, dim3(nb), dim3(SH_THREADS), 0, st, ukeys, num_u, N, cnt_tmp);
   hipLaunchKernelGGL(sh_scatter_kernel, dim3(nb), dim3(SH_THREADS), 0, st, ukeys, num_u, N, nbits, C,
                      cnt_tmp, nb, send_ids, upos, send_cnt, err);
+  HFM_LAUNCH_CHECK();
+}
+
+HFM_API int hfm_sh_route_tiles(int n) { return (n + RT_TILE - 1) / RT_TILE; }
+
+// sorted slot ids -> sid_incl / owner buckets (see sh_route_scatter_kernel); tcnt: [tiles][N + 1]
+HFM_API int hfm_sh_route(const int* sorted_keys, int n, int N, int C, int* tcnt, int* sid_incl, int* send_ids,
+                         int* upos, int* send_cnt, int* num_u, unsigned* err, hipStream_t st) {
+  if (N < 1 || N > SH_MAXN || n <= 0 || C <= 0) return (int)hipErrorInvalidValue;
+  const int nt = hfm_sh_route_tiles(n);
+  int nbits = 0;
+  while ((1 << nbits) < N) ++nbits;
+  hipLaunchKernelGGL(sh_route_count_kernel, dim3(nt), dim3(SH_THREADS), 0, st, sorted_keys, n, N, tcnt);
+  hipLaunchKernelGGL(sh_route_scatter_kernel, dim3(nt), dim3(SH_THREADS), 0, st, sorted_keys, n, N, nbits, C,
+                     tcnt, nt, sid_incl, send_ids, upos, send_cnt, num_u, err);
   HFM_LAUNCH_CHECK();
 }
 
@@ -308,7 +454,8 @@ HFM_API int hfm_sh_slot_rows(const int* perm, const int* sid_incl, const int* up
   }
 
 // table = {key, pos, mask} of the request table, or key == null (eval-style fetch: no insert)
-HFM_API int hfm_sh_serve(int K, const int* recv_ids, int total, int N, int C, const float* tv, const float* tw,
+HFM_API int hfm_sh_serve(int K, const int* recv_ids, int total, int N, int C, int rstride, const float* tv,
+                         const float* tw,
                          long ldv, long ldw, float* rows, const int64_t* step, const ShTable* table,
                          hipStream_t st) {
   const long th = (long)total * (K / 4);
@@ -317,8 +464,9 @@ HFM_API int hfm_sh_serve(int K, const int* recv_ids, int total, int N, int C, co
   const ShTable T = table ? *table : ShTable{nullptr, nullptr, 0u, 0};
   if (T.key && (!step || C <= 0 || (T.mask & (T.mask + 1)) != 0 || T.mask + 1 < 2u * (unsigned)total))
     return (int)hipErrorInvalidValue;
+  if (rstride > C && (C <= 0 || rstride % C)) return (int)hipErrorInvalidValue;
 #define CALL(KK) hipLaunchKernelGGL(sh_serve_kernel<KK>, dim3(grid), dim3(256), 0, st, recv_ids, total, N, \
-                                    C, tv, tw, ldv, ldw, rows, step, T)
+                                    C, rstride, tv, tw, ldv, ldw, rows, step, T)
   HFM_K_DISPATCH(K, CALL)
 #undef CALL
   HFM_LAUNCH_CHECK();
@@ -327,6 +475,7 @@ HFM_API int hfm_sh_serve(int K, const int* recv_ids, int total, int N, int C, co
 struct ShApplyArgs {
   const int* recv_ids;
   int total, N, C, mode;
+  int rstride;  // request row stride (see sh_rid)
   const float* recv_g;
   ShTable table;
   float *tv, *tw, *s0v, *s1v, *s0w, *s1w;
@@ -342,10 +491,10 @@ static int sh_apply_k(int opt, const ShApplyArgs& A, hipStream_t st) {
   const int grid = (int)((th + 255) / 256);
   if (A.mode & 2)  // tags not stamped by this step's serve (eval-style fetch): stamp them here
     hipLaunchKernelGGL(sh_owner_tag_kernel, dim3((A.total + 255) / 256), dim3(256), 0, st, A.recv_ids,
-                       A.total, A.N, A.C, A.step, A.table);
+                       A.total, A.N, A.C, A.rstride, A.step, A.table);
 #define L_(M, O)                                                                                      \
   hipLaunchKernelGGL((sh_owner_apply_kernel<K, M, O>), dim3(grid), dim3(256), 0, st, A.recv_ids, A.total, \
-                     A.N, A.C, A.recv_g, A.table, A.tv, A.tw, A.s0v, A.s1v, A.s0w, A.s1w, A.ldv, A.ldw, \
+                     A.N, A.C, A.rstride, A.recv_g, A.table, A.tv, A.tw, A.s0v, A.s1v, A.s0w, A.s1w, A.ldv, A.ldw, \
                      A.Gv, A.Gw, A.h, A.step)
   if ((A.mode & 1) == 1) {
     L_(1, 0);
@@ -378,3 +527,74 @@ HFM_API int hfm_sh_owner_apply(int K, int opt, const ShApplyArgs* A, hipStream_t
   HFM_LAUNCH_CHECK();
 }
 HFM_API int hfm_sh_apply_args_bytes() { return (int)sizeof(ShApplyArgs); }
+
+// The lazy owner update and the dense optimizer (after the dense all-reduce) in ONE launch: the
+// two are independent, and the end of the multi-GPU step then has one kernel boundary less.
+// Workgroups [0, apply_blocks) run the owner update, the rest sweep the dense parameters
+// (dense_opt_elem, bitwise the dense_opt launch); every workgroup read the step counter before
+// it arrives on `done`, and the last arrival advances it (and re-arms the counter).
+struct ShDenseArgs {
+  float* p;
+  const float* g;
+  float* s0;
+  float* s1;
+  long n;
+  OptHyper h;
+  const ShadowSeg* segs;
+  int nseg;
+  int blocks;       // workgroups of the dense sweep
+  unsigned* done;   // [1], zero between launches
+  int nsum;         // 0: g is the gradient; R > 0: g holds R rank gradients [R][n], summed in rank order
+};
+
+template <int K, int OPT>
+__global__ void __launch_bounds__(256) sh_apply_dense_kernel(ShApplyArgs A, ShDenseArgs D, int apply_blocks) {
+  const int b = blockIdx.x;
+  if (b < apply_blocks) {
+    sh_owner_apply_elem<K, 0, OPT>(b * 256 + threadIdx.x, A.recv_ids, A.total, A.N, A.C, A.rstride, A.recv_g,
+                                   A.table, A.tv, A.tw, A.s0v, A.s1v, A.s0w, A.s1w, A.ldv, A.ldw, A.Gv, A.Gw,
+                                   A.h, A.step);
+  } else {
+    const float lr_t = OPT == OPT_ADAM ? adam_lr_t(D.h, *A.step + 1) : D.h.lr;
+    for (long i = (long)(b - apply_blocks) * 256 + threadIdx.x; i < D.n; i += (long)D.blocks * 256) {
+      if (D.nsum > 0) {  // the all-gathered per-rank dense gradients: the all-reduce, in rank order
+        float gi = D.g[i];
+        for (int q = 1; q < D.nsum; ++q) gi += D.g[(size_t)q * D.n + i];
+        dense_opt_apply<OPT>(D.p, gi, D.s0, D.s1, i, D.h, lr_t, D.segs, D.nseg);
+      } else {
+        dense_opt_elem<OPT>(D.p, D.g, D.s0, D.s1, i, D.h, lr_t, D.segs, D.nseg);
+      }
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned prev = __hip_atomic_fetch_add(D.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev == gridDim.x - 1) {
+      __hip_atomic_store(D.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *const_cast<int64_t*>(A.step) += 1;
+    }
+  }
+}
+
+// lazy rows only (mode 0; tags stamped by this step's serve)
+HFM_API int hfm_sh_apply_dense(int K, int opt, const ShApplyArgs* A, const ShDenseArgs* D, hipStream_t st) {
+  if (A->mode != 0 || !D->done || D->blocks < 1 || !A->step) return (int)hipErrorInvalidValue;
+  const long th = (long)A->total * (K / 4);
+  const int ab = (int)((th + 255) / 256);
+  const dim3 g(ab + D->blocks), blk(256);
+#define L_(KK, O) hipLaunchKernelGGL((sh_apply_dense_kernel<KK, O>), g, blk, 0, st, *A, *D, ab)
+#define OPTS(KK)                                         \
+  switch (opt) {                                         \
+    case OPT_ADAM: L_(KK, OPT_ADAM); break;              \
+    case OPT_ADAGRAD: L_(KK, OPT_ADAGRAD); break;        \
+    case OPT_MOMENTUM: L_(KK, OPT_MOMENTUM); break;      \
+    case OPT_FTRL: L_(KK, OPT_FTRL); break;              \
+    case OPT_GD: L_(KK, OPT_GD); break;                  \
+    default: return (int)hipErrorInvalidValue;           \
+  }
+  HFM_K_DISPATCH(K, OPTS)
+#undef OPTS
+#undef L_
+  HFM_LAUNCH_CHECK();
+}
+HFM_API int hfm_sh_dense_args_bytes() { return (int)sizeof(ShDenseArgs); }

@@ -431,6 +431,35 @@ static int sfwg_dispatch(int opt, const SfArgs& A, const WgFinArgs& W, unsigned*
   return 0;
 }
 
+// Row-sharded step: the sparse backward's gradient rows for the owner exchange (MODE 2) and the
+// wgfin gradient work (no optimizer: the dense gradient is exchanged first) in one launch.
+template <int K>
+__global__ void __launch_bounds__(256) sfwg_x_kernel(SfArgs A, WgFinArgs W) {
+  __shared__ SfwgSmem<K> sm;
+  const int nw = W.tile_wgs + 1;
+  if ((int)blockIdx.x < nw) wgfin_body<-1, SFWG_PF, SFWG_MAXNS, SFWG_TQ>(W, blockIdx.x, sm.wg);
+  else sf_tile_body<K, 2, 0>(A, (int)blockIdx.x - nw, sm.sf);
+}
+
+HFM_API int hfm_sparse_wgfin_x(int K, const SfArgs* A, const WgFinArgs* W, hipStream_t st) {
+  if (A->n <= 0 || !A->flags || !A->sync || !A->gout || W->opt_on || W->ns < 1 || W->ns > SFWG_MAXNS ||
+      W->kchunk % 32 || W->ldk != W->ns * 4 * W->kchunk || W->L + 2 > WGF_MAXC || !W->tile_ctr)
+    return (int)hipErrorInvalidValue;
+#define X_(KK)                                                                                    \
+  hipLaunchKernelGGL(sfwg_x_kernel<KK>, dim3(W->tile_wgs + 1 + (A->n + SfCfg<KK>::TP - 1) / SfCfg<KK>::TP), \
+                     dim3(256), 0, st, *A, *W)
+  switch (K) {
+    case 4: X_(4); break;
+    case 8: X_(8); break;
+    case 16: X_(16); break;
+    case 32: X_(32); break;
+    case 64: X_(64); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+#undef X_
+  HFM_LAUNCH_CHECK();
+}
+
 // lazy sparse rows (optimizer `opt`) + wgfin with the same dense optimizer; `done`: [1] arrival
 // counter, zero between launches.  A.step_off must be 1 (the step advances at the launch's end).
 HFM_API int hfm_sparse_wgfin(int K, int opt, const SfArgs* A, const WgFinArgs* W, unsigned* done,

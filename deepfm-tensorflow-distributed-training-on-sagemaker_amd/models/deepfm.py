@@ -53,6 +53,12 @@ _TOWER_GATHER = os.environ.get("HIPFM_TOWER_GATHER", "1") == "1"   # FM gather f
 _WGFIN = os.environ.get("HIPFM_WGFIN", "1") == "1"
 # single GPU, lazy rows: wgfin inside the sparse backward's launch (sparse_fused.hip sfwg_kernel)
 _SFWG = os.environ.get("HIPFM_SFWG", "1") == "1"
+# row-sharded step: where the next batch's routing branch is enqueued: start | fetch | tower
+_SHX_FORK = os.environ.get("HIPFM_SHX_FORK", "start")
+# row-sharded lazy step: dense optimizer inside the owner update's launch
+_SH_APPLY_DENSE = os.environ.get("HIPFM_SH_APPLY_DENSE", "1") == "1"
+# ... and the dense gradient computed in the sparse launch, exchanged by all-gather (no all-reduce)
+_SH_XFUSE = os.environ.get("HIPFM_SH_XFUSE", "1") == "1"
 
 
 def check_field_ranges(ranges, F: int, V: int) -> List[Tuple[int, int]]:
@@ -297,6 +303,8 @@ class NativeDeepFM:
         self._fuse_opt = False     # dense optimizer fused into the finalize launch (this step)
         self._sfwg_now = False     # ... and that launch merged into the sparse backward (this step)
         self._sfwg_step = False
+        self._sh_dense_join = None
+        self._sh_xfuse = False
         self._idsT_B = 0
         self.batch_size = int(batch_size)
         # fused deep tower (csrc/kernels/tower.hip): whole forward + head + dgrad chain in one
@@ -1067,7 +1075,9 @@ class NativeDeepFM:
         (returns None).  Multi-rank: returns compact unique-row gradients for the exchange."""
         n = B * self.F
         if self.shx is not None:
-            self.shx.backward(self._shx_plan, B)
+            j = self._sh_dense_join
+            self.shx.backward(self._shx_plan, B, dense=self._sh_dense_args() if j is not None else None,
+                              join=j, wgfin=self._wgfin_args(False) if self._sh_xfuse else None)
             return None
         if self.sharded:
             return self.comm.sharded_backward(self, B, idx, tv)
@@ -1125,7 +1135,7 @@ class NativeDeepFM:
         presorted = False
         if self.shx is not None:
             self._shx_start(B)
-        after_fm = None
+        after_fm = self.shx.fork_next if (self.shx is not None and _SHX_FORK == "tower") else None
         plan = self._sort_plan
         self.sorted_keys, self.perm = self._ss[plan[0] if plan is not None else self._ss_cur]
         prefetch = plan is not None and plan[2] is not None
@@ -1186,8 +1196,14 @@ class NativeDeepFM:
         # concurrently with the sparse exchange (which needs only dX0 / dlogit / S from the
         # tower): 0.210 -> 0.199 ms.  On one GPU the concurrent wgrad slows the sparse backward
         # more than it saves (0.156 -> 0.161 ms), so there it stays in line.
-        split = self.fused and (_DENSE_SIDE_STREAM == "1" or
-                                (_DENSE_SIDE_STREAM == "auto" and self.exchange))
+        # row-sharded lazy step with wgfin: the dense gradient is computed in the sparse backward's
+        # launch and travels with the gradient rows' exchange (all-gather, summed in rank order
+        # by the owner launch): no comm stream, no all-reduce, no cross-stream joins
+        xfuse = (self.shx is not None and self.sparse_update == "lazy" and _SH_XFUSE and _WGFIN and
+                 self.fused and _SH_APPLY_DENSE and getattr(self, "_wgfin_ns", 1 << 30) <= KN.SFWG_MAX_NS)
+        self._sh_xfuse = xfuse
+        split = self.fused and not xfuse and (_DENSE_SIDE_STREAM == "1" or
+                                              (_DENSE_SIDE_STREAM == "auto" and self.exchange))
         # single GPU, lazy rows: the dense optimizer needs only the finished dense gradient, so it
         # runs BEFORE the join with the side-stream sort, inside the gap the join costs anyway;
         # it advances the step counter, and the sparse kernels are told so (SfArgs.step_off).
@@ -1200,7 +1216,8 @@ class NativeDeepFM:
         self._sfwg_now = (self._fuse_opt and _WGFIN and _SFWG and getattr(self, "_wgfin_ns", 1 << 30) <= KN.SFWG_MAX_NS and
                           self.shx is None and not self.sharded)
         try:
-            idx, tv = self._dense_fwd_bwd(B, defer_wgrad=split or self._sfwg_now, after_fm=after_fm)
+            idx, tv = self._dense_fwd_bwd(B, defer_wgrad=split or self._sfwg_now or xfuse,
+                                          after_fm=after_fm)
         finally:
             self._idsT_B = 0
             fused_opt, self._fuse_opt = self._fuse_opt, False
@@ -1215,7 +1232,7 @@ class NativeDeepFM:
         if presorted and inline:
             main.wait_stream(self._side)
         work = None
-        eng = getattr(self.comm, "engine_dense", None) if self.exchange else None
+        eng = getattr(self.comm, "engine_dense", None) if (self.exchange and not xfuse) else None
         if split or eng is not None:
             # dense gradient branch (+ bucket all-reduce) overlapped with the sparse exchange
             if self._comm_stream is None:
@@ -1228,8 +1245,21 @@ class NativeDeepFM:
                     eng.allreduce_(self.g)
                 elif self.exchange:
                     work = self.comm.allreduce_dense_async(self.g)
-        elif self.exchange:
+        elif self.exchange and not xfuse:
             work = self.comm.allreduce_dense_async(self.g)
+        # row-sharded lazy step: the dense optimizer rides in the owner update's launch, which
+        # first joins the dense all-reduce (returns a join callable, or None)
+        self._sh_dense_join = None
+        if (self.shx is not None and self.sparse_update == "lazy" and _SH_APPLY_DENSE and
+                not self._dense_early):
+            cs = self._comm_stream if (split or eng is not None) else None
+
+            def _join(cs=cs, work=work):
+                if cs is not None:
+                    main.wait_stream(cs)
+                if work is not None:
+                    self.comm.wait(work)
+            self._sh_dense_join = _join
         out = self._sparse_backward(B, idx, tv, presorted=presorted)
         if out is not None:
             self._sparse_update(*out)
@@ -1240,13 +1270,29 @@ class NativeDeepFM:
             self.comm.wait(work)
         if self.shx is not None:
             self.shx.end(self._shx_plan)
-        if not self._dense_early:
+        if self._sh_dense_join is not None:
+            self._sh_dense_join = None
+            if self.fp8:
+                KN.w8_quant(self._w8_jobs, len(self.layers), self._w8_rows)
+        elif not self._dense_early:
             self._dense_opt()
         if prefetch:
             # joined at the end of the step: deferring the join to the next step's sparse
             # backward (so no cross-branch edge precedes the next tower) measured 0.155-0.186
             # vs 0.121 ms/step in a 16-step graph -- the branch then lands in the towers' path
             main.wait_stream(self._side_next)
+
+    def _sh_dense_args(self):
+        from ..ops._lib import ShDenseArgs
+        d = ShDenseArgs()
+        d.p, d.g = self.p.data_ptr(), self.g.data_ptr()
+        d.s0 = self.sd[0].data_ptr() if self.sd[0].numel() else 0
+        d.s1 = self.sd[1].data_ptr() if self.sd[1].numel() else 0
+        d.n, d.h = self.P, self.h_dense
+        d.segs, d.nseg = self._shadow_dev.data_ptr(), self._nshadow
+        d.blocks = max(1, min(1024, (self.P + 255) // 256))
+        d.done = self._done_ctr.data_ptr()
+        return d
 
     def _dense_opt(self):
         """Dense optimizer over the flat buffer (+ bf16 / fp8 weight shadows); advances the step."""
@@ -1260,7 +1306,7 @@ class NativeDeepFM:
         and the fork of the next batch's routing."""
         if self._shx_plan is None:
             self._shx_plan = self.shx.plan(self.idx, B, None, resident=False)
-        self.shx.begin(self._shx_plan, B)
+        self.shx.begin(self._shx_plan, B, fork=_SHX_FORK)
 
     def compute_grads(self, ids, vals, labels):
         """Forward + backward WITHOUT any update (tests / debugging): returns the flat dense

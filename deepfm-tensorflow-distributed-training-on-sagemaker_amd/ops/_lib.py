@@ -117,10 +117,16 @@ class ShTable(C.Structure):
 
 class ShApplyArgs(C.Structure):
     _fields_ = [("recv_ids", c_void_p), ("total", c_int), ("N", c_int), ("C", c_int), ("mode", c_int),
-                ("recv_g", c_void_p), ("table", ShTable), ("tv", c_void_p), ("tw", c_void_p),
+                ("rstride", c_int), ("recv_g", c_void_p), ("table", ShTable), ("tv", c_void_p), ("tw", c_void_p),
                 ("s0v", c_void_p), ("s1v", c_void_p), ("s0w", c_void_p), ("s1w", c_void_p),
                 ("ldv", c_long), ("ldw", c_long), ("Gv", c_void_p), ("Gw", c_void_p), ("h", OptHyper),
                 ("step", c_void_p)]
+
+
+class ShDenseArgs(C.Structure):
+    _fields_ = [("p", c_void_p), ("g", c_void_p), ("s0", c_void_p), ("s1", c_void_p), ("n", c_long),
+                ("h", OptHyper), ("segs", c_void_p), ("nseg", c_int), ("blocks", c_int), ("done", c_void_p),
+                ("nsum", c_int)]
 
 
 TW_MAXL = 8
@@ -208,12 +214,16 @@ _SIGS = {
     "hfm_comm_alltoall": [c_void_p, c_void_p, c_void_p, c_size_t, c_void_p],
     "hfm_comm_allgather": [c_void_p, c_void_p, c_void_p, c_size_t, c_void_p],
     "hfm_sh_count_blocks": [c_int],
+    "hfm_sh_route_tiles": [c_int],
+    "hfm_sh_route": [c_void_p, c_int, c_int, c_int] + [c_void_p] * 7 + [c_void_p],
     "hfm_sh_bucket": [c_void_p, c_void_p, c_int, c_int, c_int] + [c_void_p] * 5 + [c_void_p],
     "hfm_sh_slot_rows": [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p],
-    "hfm_sh_serve": [c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_long, c_long, c_void_p,
+    "hfm_sh_serve": [c_int, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_long, c_long, c_void_p,
                      c_void_p, c_void_p, c_void_p],
     "hfm_sh_owner_apply": [c_int, c_int, c_void_p, c_void_p],
     "hfm_sh_apply_args_bytes": [],
+    "hfm_sh_apply_dense": [c_int, c_int, c_void_p, c_void_p, c_void_p],
+    "hfm_sh_dense_args_bytes": [],
     "hfm_sparse_fused_tiles": [c_int, c_int],
     "hfm_sparse_fused": [c_int, c_int, c_int, c_void_p, c_void_p],
     "hfm_sparse_fused_args_bytes": [],
@@ -229,6 +239,7 @@ _SIGS = {
     "hfm_tower": [C.POINTER(TowerArgs), c_int, c_void_p],
     "hfm_wgfin": [c_int, C.POINTER(WgFinArgs), c_void_p],
     "hfm_sparse_wgfin": [c_int, c_int, c_void_p, C.POINTER(WgFinArgs), c_void_p, c_void_p],
+    "hfm_sparse_wgfin_x": [c_int, c_void_p, C.POINTER(WgFinArgs), c_void_p],
     "hfm_wgfin_job_bytes": [],
     "hfm_wgfin_args_bytes": [],
     "hfm_tower_args_bytes": [],
@@ -274,7 +285,8 @@ def get_lib():
                            ("hfm_wgfin_job_bytes", WgFinJob), ("hfm_wgfin_args_bytes", WgFinArgs),
                            ("hfm_w8_job_bytes", W8Job),
                            ("hfm_sparse_fused_args_bytes", SfArgs),
-                           ("hfm_sh_apply_args_bytes", ShApplyArgs)):
+                           ("hfm_sh_apply_args_bytes", ShApplyArgs),
+                           ("hfm_sh_dense_args_bytes", ShDenseArgs)):
             n = getattr(lib, cname)()
             if n != C.sizeof(pys):
                 raise RuntimeError(f"ABI mismatch {pys.__name__}: C {n} vs ctypes {C.sizeof(pys)}")

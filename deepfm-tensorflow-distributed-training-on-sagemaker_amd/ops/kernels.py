@@ -252,6 +252,12 @@ def sparse_fused(K, mode, opt, args: SfArgs):
 SFWG_MAX_NS = 4          # sparse_fused.hip SFWG_MAXNS: wgfin splits the merged launch supports
 
 
+def sparse_wgfin_x(K, args: SfArgs, wf: "WgFinArgs"):
+    """Row-sharded step: gradient rows for the owner exchange + wgfin gradients (no optimizer)
+    in one launch (sparse_fused.hip sfwg_x_kernel)."""
+    check(L().hfm_sparse_wgfin_x(K, C.byref(args), C.byref(wf), stream_handle()), "sparse_wgfin_x")
+
+
 def sparse_wgfin(K, opt, args: SfArgs, wf: "WgFinArgs", done):
     """Lazy sparse backward + the fused tower's wgfin work (weight gradients, split-K combine,
     dense optimizer) in ONE launch (sparse_fused.hip sfwg_kernel); ``done``: int32 [1] arrival
@@ -441,6 +447,17 @@ def sh_bucket(ukeys, num_u, nmax, N, Cap, cnt_tmp, send_ids, upos, send_cnt, err
                             ptr(send_cnt), ptr(err), stream_handle()), "sh_bucket")
 
 
+def sh_route_tiles(n: int) -> int:
+    return int(L().hfm_sh_route_tiles(n))
+
+
+def sh_route(sorted_keys, n, N, Cap, tcnt, sid_incl, send_ids, upos, send_cnt, num_u, err):
+    """Sorted slot ids -> 1-based unique index per slot + owner buckets in two launches
+    (shard.hip sh_route_*; same outputs as segments + sh_bucket)."""
+    check(L().hfm_sh_route(ptr(sorted_keys), n, N, Cap, ptr(tcnt), ptr(sid_incl), ptr(send_ids), ptr(upos),
+                           ptr(send_cnt), ptr(num_u), ptr(err), stream_handle()), "sh_route")
+
+
 def sh_slot_rows(perm, sid_incl, upos, n, idx):
     check(L().hfm_sh_slot_rows(ptr(perm), ptr(sid_incl), ptr(upos), n, ptr(idx), stream_handle()),
           "sh_slot_rows")
@@ -449,13 +466,21 @@ def sh_slot_rows(perm, sid_incl, upos, n, idx):
 _byref = C.byref
 
 
-def sh_serve(K, recv_ids, total, N, tv, tw, rows, C: int = 0, step=None, table=None):
+def sh_serve(K, recv_ids, total, N, tv, tw, rows, C: int = 0, step=None, table=None, rstride: int = 0):
     """Owner side of the row fetch: rows[e] = {v, w} of every requested id.  With ``table`` (a
     ShTable; training steps) it also records each request (row, requester, slot) stamped with
-    step + 1 in the owner's request table read by sh_owner_apply."""
-    check(L().hfm_sh_serve(K, ptr(recv_ids), total, N, C, ptr(tv), ptr(tw), *_ld(tv, tw), ptr(rows),
+    step + 1 in the owner's request table read by sh_owner_apply.  ``recv_ids``: a tensor or a
+    device address; ``rstride``: its request-row stride (0: contiguous [N][C])."""
+    rp = recv_ids if isinstance(recv_ids, int) else ptr(recv_ids)
+    check(L().hfm_sh_serve(K, rp, total, N, C, rstride, ptr(tv), ptr(tw), *_ld(tv, tw), ptr(rows),
                            ptr(step), _byref(table) if table is not None else None, stream_handle()),
           "sh_serve")
+
+
+def sh_apply_dense(K, opt, args: ShApplyArgs, dense):
+    """Lazy owner update + dense optimizer in one launch (shard.hip sh_apply_dense_kernel); the
+    launch advances the step counter."""
+    check(L().hfm_sh_apply_dense(K, opt, C.byref(args), C.byref(dense), stream_handle()), "sh_apply_dense")
 
 
 def sh_owner_apply(K, opt, args: ShApplyArgs):

@@ -16,12 +16,16 @@ measures sample batches; a bucket that overflows sets an error word that the mod
 from __future__ import annotations
 
 import math
+import os
 from typing import Iterable, Optional
 
 import torch
 
 from ..ops import kernels as KN
 from ..ops._lib import ShApplyArgs, ShTable
+
+# routing in two launches (sh_route) instead of segments + bucket (7 launches); same outputs
+_ROUTE2 = os.environ.get("HIPFM_SH_ROUTE2", "1") == "1"
 
 
 def estimate_capacity(id_batches: Iterable[torch.Tensor], world: int, slack: float = 1.25,
@@ -89,11 +93,13 @@ class _RouteSet:
         self.temp = torch.zeros(temp_bytes, dtype=torch.uint8, device=dev)
         self.upos = torch.zeros(n, **i32)
         self.cnt_tmp = torch.zeros(KN.sh_count_blocks(n) * N, **i32)
+        self.tcnt = torch.zeros(KN.sh_route_tiles(n) * (N + 1), **i32)
         self.send_ids = torch.full((N * C,), -1, **i32)
         self.recv_ids = torch.full((N * C,), -1, **i32)
         self.send_cnt = torch.zeros(N, **i32)
         self.gathered = None     # [N, N*C] all-gathered requests (side-stream routing)
         self.slot_row = torch.zeros(n, **i32)
+        self.recv = (self.recv_ids.data_ptr(), 0)   # (requests address, row stride) for the owner
         self.key = None          # host: (ids data_ptr, B) routed into this set
 
 
@@ -135,6 +141,9 @@ class FixedCapacityExchange:
         self.req_pos = torch.zeros(slots * self.N, dtype=torch.int64, device=dev)
         self.table = ShTable(self.req_key.data_ptr(), self.req_pos.data_ptr(), slots - 1, 0)
         self._side = None
+        self._fork_at = None
+        self._fork_plan = None
+        self.dense_recv = None               # [N][P] all-gathered dense gradients (fused exchange)
 
     # ------------------------------------------------------------------ host-side plan
     def plan(self, ids: torch.Tensor, B: int, nxt: Optional[torch.Tensor], resident: bool = True):
@@ -173,36 +182,57 @@ class FixedCapacityExchange:
             m._fsort(ids, B, rs.sorted_keys, rs.perm)
         else:
             KN.sort_ids(ids, rs.sorted_keys, None, rs.perm, n, m.end_bit, rs.temp)
-        KN.segments(rs.sorted_keys, n, rs.seg_flags, rs.sid_incl, rs.ukeys, rs.seg_start, rs.num_u, rs.temp)
-        KN.sh_bucket(rs.ukeys, rs.num_u, n, self.N, self.C, rs.cnt_tmp, rs.send_ids, rs.upos,
-                     rs.send_cnt, self.err)
+        if _ROUTE2:
+            KN.sh_route(rs.sorted_keys, n, self.N, self.C, rs.tcnt, rs.sid_incl, rs.send_ids, rs.upos,
+                        rs.send_cnt, rs.num_u, self.err)
+        else:
+            KN.segments(rs.sorted_keys, n, rs.seg_flags, rs.sid_incl, rs.ukeys, rs.seg_start, rs.num_u,
+                        rs.temp)
+            KN.sh_bucket(rs.ukeys, rs.num_u, n, self.N, self.C, rs.cnt_tmp, rs.send_ids, rs.upos,
+                         rs.send_cnt, self.err)
         if gather:
             if rs.gathered is None:
                 rs.gathered = torch.zeros(self.N * self.N * self.C, dtype=torch.int32, device=m.device)
             eng.allgather(rs.send_ids, rs.gathered, self.N * self.C * 4)
-            rs.recv_ids.view(self.N, self.C).copy_(
-                rs.gathered.view(self.N, self.N, self.C)[:, self.rank, :])
+            # the owner kernels read this rank's column of the gathered requests in place
+            rs.recv = (rs.gathered.data_ptr() + 4 * self.rank * self.C, self.N * self.C)
         else:
             eng.alltoall(rs.send_ids, rs.recv_ids, self.C * 4)
+            rs.recv = (rs.recv_ids.data_ptr(), 0)
         KN.sh_slot_rows(rs.perm, rs.sid_incl, rs.upos, n, rs.slot_row)
 
-    def begin(self, plan, B: int):
+    def begin(self, plan, B: int, fork: str = "start"):
         """Start of a step: route the current batch if it was not prefetched, then fork the
-        routing of the next batch onto a side stream."""
+        routing of the next batch onto a side stream -- here (``fork="start"``), right after the
+        row fetch is enqueued (``"fetch"``), or when the caller calls ``fork_next`` (graph
+        branches are dispatched in capture order: a branch enqueued first delays the main
+        stream's first kernels)."""
         m = self.m
         c, inline, nk = plan
         if inline:
             self.route(self.sets[c], m.idx, B, self.eng)
-        if nk is not None:
-            main = torch.cuda.current_stream(m.device)
-            if self._side is None:
-                self._side = torch.cuda.Stream(m.device)
-            self._side.wait_stream(main)
-            nxt_ids = self._next_ids
-            with torch.cuda.stream(self._side):
-                self.route(self.sets[1 - c], nxt_ids, nk[1], self.eng_route, gather=True)
+        self._fork_at = fork if nk is not None else None
+        self._fork_plan = plan
+        if self._fork_at == "start":
+            self.fork_next()
+
+    def fork_next(self):
+        """Enqueue the next batch's routing on the side stream (once per step)."""
+        if self._fork_at is None:
+            return
+        self._fork_at = None
+        m = self.m
+        c, _, nk = self._fork_plan
+        main = torch.cuda.current_stream(m.device)
+        if self._side is None:
+            self._side = torch.cuda.Stream(m.device)
+        self._side.wait_stream(main)
+        nxt_ids = self._next_ids
+        with torch.cuda.stream(self._side):
+            self.route(self.sets[1 - c], nxt_ids, nk[1], self.eng_route, gather=True)
 
     def end(self, plan):
+        self.fork_next()                     # (not forked yet: e.g. no tower in this step)
         if plan[2] is not None:
             torch.cuda.current_stream(self.m.device).wait_stream(self._side)
 
@@ -213,15 +243,23 @@ class FixedCapacityExchange:
         m = self.m
         rs = self.sets[plan[0]]
         if train:
-            KN.sh_serve(m.K, rs.recv_ids, self.N * self.C, self.N, m.tv, m.tw, self.rows_out,
-                        C=self.C, step=m.step, table=self.table)
+            KN.sh_serve(m.K, rs.recv[0], self.N * self.C, self.N, m.tv, m.tw, self.rows_out,
+                        C=self.C, step=m.step, table=self.table, rstride=rs.recv[1])
         else:
-            KN.sh_serve(m.K, rs.recv_ids, self.N * self.C, self.N, m.tv, m.tw, self.rows_out)
+            KN.sh_serve(m.K, rs.recv[0], self.N * self.C, self.N, m.tv, m.tw, self.rows_out, C=self.C,
+                        rstride=rs.recv[1])
         self.eng.alltoall(self.rows_out, self.rows_in, self.C * self.RW * 4)
+        if train and self._fork_at == "fetch":
+            self.fork_next()
         return rs.slot_row, self.rows_in[:, : m.K], self.rows_in[:, m.K]
 
-    def backward(self, plan, B: int):
-        """Per-unique gradient rows -> owners -> rank-ordered sum + row update on the owner."""
+    def backward(self, plan, B: int, dense=None, join=None, wgfin=None):
+        """Per-unique gradient rows -> owners -> rank-ordered sum + row update on the owner.
+        ``dense`` (ShDenseArgs, lazy rows): the dense optimizer runs in the owner update's launch,
+        after ``join()`` made the main stream wait for the dense gradient all-reduce.
+        ``wgfin`` (WgFinArgs): the fused tower's dense gradient is computed inside the sparse
+        backward's launch and all-gathered right after the gradient rows' all-to-all (no
+        all-reduce, no comm stream); the owner launch sums the N rank gradients in rank order."""
         m = self.m
         rs = self.sets[plan[0]]
         n = B * m.F
@@ -230,10 +268,19 @@ class FixedCapacityExchange:
         A.tv, A.tw = self.rows_in.data_ptr(), self.rows_in.data_ptr() + 4 * m.K
         A.ldv = A.ldw = self.RW
         A.sid, A.upos, A.gout = rs.sid_incl.data_ptr(), rs.upos.data_ptr(), self.send_g.data_ptr()
-        KN.sparse_fused(m.K, KN.SF_EXCHANGE, m.opt_id, A)
+        if wgfin is not None:
+            KN.sparse_wgfin_x(m.K, A, wgfin)
+        else:
+            KN.sparse_fused(m.K, KN.SF_EXCHANGE, m.opt_id, A)
         self.eng.alltoall(self.send_g, self.recv_g, self.C * self.RW * 4)
+        if wgfin is not None:
+            if self.dense_recv is None:
+                self.dense_recv = torch.zeros(self.N * m.P, dtype=torch.float32, device=m.device)
+            self.eng.allgather(m.g[: m.P], self.dense_recv, m.P * 4)
+            dense.g, dense.nsum = self.dense_recv.data_ptr(), self.N
         S = ShApplyArgs()
-        S.recv_ids, S.total, S.N, S.C = rs.recv_ids.data_ptr(), self.N * self.C, self.N, self.C
+        S.recv_ids, S.total, S.N, S.C = rs.recv[0], self.N * self.C, self.N, self.C
+        S.rstride = rs.recv[1]
         S.mode = 0 if m.sparse_update == "lazy" else 1      # tags were stamped by fetch()
         S.recv_g, S.table = self.recv_g.data_ptr(), self.table
         S.tv, S.tw = m.tv.data_ptr(), m.tw.data_ptr()
@@ -243,6 +290,11 @@ class FixedCapacityExchange:
             S.Gv, S.Gw = m.Gv.data_ptr(), m.Gw.data_ptr()
         S.h = m.h_sparse
         S.step = m.step.data_ptr()
+        if dense is not None:
+            if join is not None:
+                join()
+            KN.sh_apply_dense(m.K, m.opt_id, S, dense)
+            return
         KN.sh_owner_apply(m.K, m.opt_id, S)
         if m.sparse_update == "tf1_dense":
             KN.dense_sweep(m.K, m.opt_id, m.R, m.tv, m.tw, m.Gv, m.Gw, m.sv, m.h_sparse, m.step)

@@ -251,3 +251,41 @@ def test_sharded_exchange_n8_criteo_1tb_shape():
     assert (p_sh - ref.p).abs().max().item() <= 2e-5 * ref.p.abs().max().item()
     del ref
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("N,C_slack", [(1, 1.3), (3, 1.3), (8, 1.3), (8, 0.5)])
+def test_two_launch_routing_matches_segments_bucket(N, C_slack):
+    """sh_route (2 launches) gives exactly the outputs of segments + sh_bucket (7 launches):
+    1-based unique index per slot, owner buckets in id order with -1 padding, unique positions,
+    bucket counts, the unique count; an overflowing bucket (capacity below the need) flags err
+    the same way."""
+    from hipfm.ops import kernels as KN
+    synth = make_synth("criteo_1tb", seed=3)
+    B = 4096 + 77
+    ids = synth.batch(B, step=1, device=DEV, id_dtype=torch.int32)[0].reshape(-1)
+    n = ids.numel()
+    sk = torch.sort(ids)[0].contiguous()
+    U = int(torch.unique(sk).numel())
+    C = int(U / N * C_slack) // 64 * 64 + 64
+    i32 = dict(dtype=torch.int32, device=DEV)
+    temp = torch.zeros(KN.radix_temp_bytes(n), dtype=torch.uint8, device=DEV)
+    out = []
+    for two in (True, False):
+        sid, ukeys, seg, num = (torch.zeros(n, **i32), torch.zeros(n, **i32), torch.zeros(n + 1, **i32),
+                                torch.zeros(1, **i32))
+        send, upos, cnt, err = (torch.full((N * C,), 7, **i32), torch.full((n,), 7, **i32),
+                                torch.zeros(N, **i32), torch.zeros(1, **i32))
+        if two:
+            tcnt = torch.zeros(KN.sh_route_tiles(n) * (N + 1), **i32)
+            KN.sh_route(sk, n, N, C, tcnt, sid, send, upos, cnt, num, err)
+        else:
+            flags = torch.zeros(n, **i32)
+            KN.segments(sk, n, flags, sid, ukeys, seg, num, temp)
+            KN.sh_bucket(ukeys, num, n, N, C, torch.zeros(KN.sh_count_blocks(n) * N, **i32), send, upos,
+                         cnt, err)
+        torch.cuda.synchronize()
+        out.append((sid, send, upos[:U], cnt, num, err))
+    for name, a, b in zip(["sid_incl", "send_ids", "upos", "send_cnt", "num_u", "err"], out[0], out[1]):
+        assert torch.equal(a, b), name
+    assert int(out[0][4].item()) == U
+    assert (int(out[0][5].item()) != 0) == (C_slack < 1.0)
