@@ -32,10 +32,14 @@ METRIC = ("samples/sec (whole node) + eval AUC, Criteo-1TB-shape DeepFM at 1/2/4
 
 # Multi-GPU execution ladder (bench supervisor, below): the fastest path first, then paths with
 # fewer moving parts.  Every rung is the same full training step (same model, optimizer, data).
+# The step's collective pattern of round 1 (separate dense all-reduce on its own stream, 7-launch
+# routing) is the fallback when the fused exchange (grouped all-to-all + all-gather) fails.
+_R1_EXCHANGE = {"HIPFM_SH_XFUSE": "0", "HIPFM_SH_APPLY_DENSE": "0", "HIPFM_SH_ROUTE2": "0"}
 LADDER = [
     ("graph+prefetch", {}),                                  # HIP graphs, next-batch routing prefetch
-    ("eager+prefetch", {"HIPFM_BENCH_NO_GRAPH": "1"}),       # same collectives, launched eagerly
-    ("eager", {"HIPFM_BENCH_NO_GRAPH": "1", "HIPFM_SHARD_PIPELINE": "0"}),
+    ("graph+prefetch+allreduce", dict(_R1_EXCHANGE)),        # same, dense all-reduce on a comm stream
+    ("eager+prefetch", {"HIPFM_BENCH_NO_GRAPH": "1", **_R1_EXCHANGE}),   # launched eagerly
+    ("eager", {"HIPFM_BENCH_NO_GRAPH": "1", "HIPFM_SHARD_PIPELINE": "0", **_R1_EXCHANGE}),
 ]
 
 

@@ -57,6 +57,23 @@ HFM_API int hfm_comm_alltoall(void* comm, const void* send, void* recv, size_t b
   return nccl_rc(ncclAllToAll(send, recv, bytes_per_peer, ncclInt8, (ncclComm_t)comm, st));
 }
 
+// The gradient rows' all-to-all and the dense gradients' all-gather of the row-sharded step as ONE
+// aggregated RCCL operation (group): the small all-gather shares the all-to-all's launch and
+// latency instead of adding its own on the critical path.
+HFM_API int hfm_comm_alltoall_allgather(void* comm, const void* send, void* recv, size_t bytes_per_peer,
+                                        const void* gsend, void* grecv, size_t gbytes_per_rank,
+                                        hipStream_t st) {
+  if (bytes_per_peer % 4 || gbytes_per_rank % 4) return (int)hipErrorInvalidValue;
+  ncclResult_t r = ncclGroupStart();
+  if (r != ncclSuccess) return nccl_rc(r);
+  if (bytes_per_peer)
+    r = ncclAllToAll(send, recv, bytes_per_peer / 4, ncclInt32, (ncclComm_t)comm, st);
+  if (r == ncclSuccess && gbytes_per_rank)
+    r = ncclAllGather(gsend, grecv, gbytes_per_rank / 4, ncclInt32, (ncclComm_t)comm, st);
+  const ncclResult_t e = ncclGroupEnd();
+  return nccl_rc(r != ncclSuccess ? r : e);
+}
+
 // recv: nranks blocks of `bytes_per_rank` (block p = rank p's send buffer).  Used for the id
 // routing of the NEXT batch on a side stream: captured collectives (all-reduce / all-gather) are
 // safe on forked capture streams, where RCCL's peer-to-peer all-to-all is not (ROCm 7 / RCCL 2.26

@@ -213,6 +213,7 @@ _SIGS = {
     "hfm_comm_allreduce_f32": [c_void_p, c_void_p, c_size_t, c_void_p],
     "hfm_comm_alltoall": [c_void_p, c_void_p, c_void_p, c_size_t, c_void_p],
     "hfm_comm_allgather": [c_void_p, c_void_p, c_void_p, c_size_t, c_void_p],
+    "hfm_comm_alltoall_allgather": [c_void_p, c_void_p, c_void_p, c_size_t, c_void_p, c_void_p, c_size_t, c_void_p],
     "hfm_sh_count_blocks": [c_int],
     "hfm_sh_route_tiles": [c_int],
     "hfm_sh_route": [c_void_p, c_int, c_int, c_int] + [c_void_p] * 7 + [c_void_p],

@@ -432,6 +432,14 @@ def comm_alltoall(h: int, send: torch.Tensor, recv: torch.Tensor, bytes_per_peer
     check(L().hfm_comm_alltoall(h, ptr(send), ptr(recv), bytes_per_peer, stream_handle()), "comm_alltoall")
 
 
+def comm_alltoall_allgather(h: int, send, recv, bytes_per_peer: int, gsend, grecv, gbytes_per_rank: int):
+    """All-to-all + all-gather as one aggregated RCCL operation (comm.hip)."""
+    for t in (send, recv, gsend, grecv):
+        assert t.is_contiguous()
+    check(L().hfm_comm_alltoall_allgather(h, ptr(send), ptr(recv), bytes_per_peer, ptr(gsend), ptr(grecv),
+                                          gbytes_per_rank, stream_handle()), "comm_alltoall_allgather")
+
+
 def comm_allgather(h: int, send: torch.Tensor, recv: torch.Tensor, bytes_per_rank: int):
     assert send.is_contiguous() and recv.is_contiguous()
     check(L().hfm_comm_allgather(h, ptr(send), ptr(recv), bytes_per_rank, stream_handle()), "comm_allgather")

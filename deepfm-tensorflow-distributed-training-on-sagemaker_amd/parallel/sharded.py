@@ -65,6 +65,10 @@ class RcclEngine:
         self.bytes_sent += bytes_per_rank * self.world
         KN.comm_allgather(self.handle, send, recv, bytes_per_rank)
 
+    def alltoall_allgather(self, send, recv, bytes_per_peer: int, gsend, grecv, gbytes_per_rank: int):
+        self.bytes_sent += (bytes_per_peer + gbytes_per_rank) * self.world
+        KN.comm_alltoall_allgather(self.handle, send, recv, bytes_per_peer, gsend, grecv, gbytes_per_rank)
+
     def allreduce_(self, t: torch.Tensor):
         self.bytes_sent += t.numel() * 4
         KN.comm_allreduce_(self.handle, t)
@@ -272,12 +276,18 @@ class FixedCapacityExchange:
             KN.sparse_wgfin_x(m.K, A, wgfin)
         else:
             KN.sparse_fused(m.K, KN.SF_EXCHANGE, m.opt_id, A)
-        self.eng.alltoall(self.send_g, self.recv_g, self.C * self.RW * 4)
         if wgfin is not None:
             if self.dense_recv is None:
                 self.dense_recv = torch.zeros(self.N * m.P, dtype=torch.float32, device=m.device)
-            self.eng.allgather(m.g[: m.P], self.dense_recv, m.P * 4)
+            if hasattr(self.eng, "alltoall_allgather"):      # one aggregated RCCL operation
+                self.eng.alltoall_allgather(self.send_g, self.recv_g, self.C * self.RW * 4, m.g[: m.P],
+                                            self.dense_recv, m.P * 4)
+            else:
+                self.eng.alltoall(self.send_g, self.recv_g, self.C * self.RW * 4)
+                self.eng.allgather(m.g[: m.P], self.dense_recv, m.P * 4)
             dense.g, dense.nsum = self.dense_recv.data_ptr(), self.N
+        else:
+            self.eng.alltoall(self.send_g, self.recv_g, self.C * self.RW * 4)
         S = ShApplyArgs()
         S.recv_ids, S.total, S.N, S.C = rs.recv[0], self.N * self.C, self.N, self.C
         S.rstride = rs.recv[1]
