@@ -26,9 +26,13 @@
 // fields: one id in every row) cost one parallel lead read per 64 tiles they span.
 #include "sync.h"
 
+// slots per tile (K = 8, same-box: 256 -> 0.1116, 512 -> 0.1120, 1024 -> 0.1158 ms/step; 1024 drops
+// the merged launch to 3 workgroups per CU)
+__host__ __device__ constexpr int sf_tile_slots(int K) { return K <= 16 ? 512 : (K == 32 ? 256 : 128); }
+
 template <int K>
 struct SfCfg {
-  static constexpr int TP = (K <= 16) ? 512 : (K == 32 ? 256 : 128);  // slots per tile
+  static constexpr int TP = sf_tile_slots(K);  // slots per tile
   static constexpr int LPS = K / 4;                                    // lanes per slot (f32x4 each)
   static constexpr int PPP = 256 / LPS;                                // slots per pass
   static constexpr int PASSES = TP / PPP;
@@ -482,7 +486,7 @@ HFM_API int hfm_sparse_wgfin(int K, int opt, const SfArgs* A, const WgFinArgs* W
 }
 
 HFM_API int hfm_sparse_fused_tiles(int K, int n) {
-  const int tp = (K <= 16) ? 512 : (K == 32 ? 256 : 128);
+  const int tp = sf_tile_slots(K);
   return (n + tp - 1) / tp;
 }
 
