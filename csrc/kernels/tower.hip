@@ -296,6 +296,8 @@ __global__ void __launch_bounds__(256) tower_kernel(TowerArgs a) {
           mma32_f8<4>(X8, ld8, Bw8, Kp, Kp / 32, lane, c00, c01, c10, c11);
         else if (i == 0)
           mma32_f8<4>(a.E8 + (size_t)row0 * a.K0p, a.K0p, Bw8, Kp, Kp / 32, lane, c00, c01, c10, c11);
+        else if (KE > 0)  // H_{i-1} quantized once into the (dead) fp8 E tile below
+          mma32_f8<4>(X8, Kp + 16, Bw8, Kp, Kp / 32, lane, c00, c01, c10, c11);
         else
           mma32_f8_lds(lds + a.h_off[i - 1], Kp + 8, s_q, Bw8, Kp, Kp / 32, lane, c00, c01, c10, c11);
       } else {
@@ -328,7 +330,7 @@ __global__ void __launch_bounds__(256) tower_kernel(TowerArgs a) {
       }
     }
     __syncthreads();
-    if (a.train) store_tile_t(Hl, ldh, N, a.Ht[i], a.M, row0);
+    if (a.train && a.Ht[i]) store_tile_t(Hl, ldh, N, a.Ht[i], a.M, row0);
     if (FP8 && i + 1 < nl) {  // per-row scales of H_i, the next layer's fp8 A operand
       const int r = tid >> 3, q8 = tid & 7;
       float m = 0.f;
@@ -342,6 +344,20 @@ __global__ void __launch_bounds__(256) tower_kernel(TowerArgs a) {
         s_dq[r] = 1.f / q;
       }
       __syncthreads();
+      if constexpr (KE > 0) {
+        // quantize H_i once into the fp8 E tile's LDS (dead after layer 0; row stride N + 16
+        // bytes), so the next GEMM streams fp8 A fragments with the prefetch ring of layer 0
+        // instead of converting bf16 inside its k loop
+        for (int e = tid; e < TW_ROWS * (N / 8); e += 256) {
+          const int rr = e / (N / 8), c8 = (e - rr * (N / 8)) * 8;
+          const bf16* h = Hl + rr * ldh + c8;
+          const float q = s_q[rr];
+          const uint32_t lo = pack4_fp8(bf2f(h[0]) * q, bf2f(h[1]) * q, bf2f(h[2]) * q, bf2f(h[3]) * q);
+          const uint32_t hi = pack4_fp8(bf2f(h[4]) * q, bf2f(h[5]) * q, bf2f(h[6]) * q, bf2f(h[7]) * q);
+          *reinterpret_cast<uint2*>(X8 + rr * (N + 16) + c8) = uint2{lo, hi};
+        }
+        __syncthreads();
+      }
     }
   }
 
@@ -481,6 +497,9 @@ HFM_API int hfm_tower(const TowerArgs* ap, int KE, hipStream_t st) {
   if (a.Np[a.nl - 1] % 8) return (int)hipErrorInvalidValue;
   if (a.lds_bytes > 160 * 1024 - 1024) return (int)hipErrorInvalidValue;
   if (KE) {
+    if (a.fp8)  // H_i is re-quantized into the fp8 E tile (32 x (K0p + 16) bytes)
+      for (int i = 0; i + 1 < a.nl; ++i)
+        if (a.Np[i] > a.K0p) return (int)hipErrorInvalidValue;
     if (!a.idx || !a.vals || !a.tv || !a.tw || !a.fm_bias || a.F * KE > a.K0p || a.x_off < 0 ||
         (a.train && !a.Et) || (a.fp8 && a.x8_off < 0) || (a.ldv & 3))
       return (int)hipErrorInvalidValue;

@@ -678,7 +678,7 @@ class NativeDeepFM:
             a.keep_thr[i] = min(keep_threshold(keep), 0xFFFFFFFF)
             a.inv_keep[i] = (1.0 / keep) if keep < 1.0 else 1.0
             a.drop[i] = 1 if keep < 1.0 else 0
-            a.Ht[i] = self.Ht[i].data_ptr()
+            a.Ht[i] = self.Ht[i].data_ptr() if i + 1 < nl else 0    # (H_last^T feeds no GEMM)
             a.dZt[i] = self.dZt[i].data_ptr()
             a.h_off[i] = h_off[i]
         a.dz_off[0], a.dz_off[1] = dz_off
