@@ -37,6 +37,7 @@ struct SfCfg {
   static constexpr int PPP = 256 / LPS;                                // slots per pass
   static constexpr int PASSES = TP / PPP;
   static constexpr int C = K + 2;  // columns: a[K], g_w, c
+  static constexpr int CP = C | 1; // LDS row stride (odd: the chunk walk's lanes spread over banks)
   static constexpr int CH = 16;    // chunk length of the segmented sums
   static constexpr int NCH = TP / CH;
   static constexpr int RS = K + 4;  // ctail / lead row stride (16-B aligned)
@@ -202,10 +203,11 @@ __device__ __forceinline__ void sf_lookback(const SfArgs& A, int tile, unsigned 
 
 template <int K>
 struct SfSmem {
-  float g[SfCfg<K>::TP][SfCfg<K>::C];
+  float g[SfCfg<K>::TP][SfCfg<K>::CP];
   int skl[SfCfg<K>::TP];
-  float lead[SfCfg<K>::NCH][SfCfg<K>::C];
+  float lead[SfCfg<K>::NCH][SfCfg<K>::CP];
   int fh[SfCfg<K>::NCH];  // offset of the first head in the chunk (CH: none)
+  unsigned hb[SfCfg<K>::NCH];  // head bits of the chunk's CH slots (bit q: slot j*CH + q heads a run)
   int hl[SfCfg<K>::TP];   // head positions, ascending
   int wcount[4];
   int open_key_s, open_pos_s;
@@ -221,6 +223,7 @@ __device__ __forceinline__ void sf_tile_body(const SfArgs& A, const int tile, Sf
   auto& skl = sm.skl;
   auto& lead = sm.lead;
   auto& fh = sm.fh;
+  auto& hb = sm.hb;
   auto& hl = sm.hl;
   auto& wcount = sm.wcount;
   int& open_key_s = sm.open_key_s;
@@ -260,7 +263,9 @@ __device__ __forceinline__ void sf_tile_body(const SfArgs& A, const int tile, Sf
     }
   }
   __syncthreads();
-  // head flags -> compacted head list (ascending) and per-chunk first head
+  // head flags -> compacted head list (ascending), per-chunk head bits and first head (the
+  // ballot of 64 consecutive slots holds the bits of 64 / CH whole chunks)
+  static_assert(64 % CH == 0, "a chunk's slots sit in one wave's ballot");
   int nh = 0;
   for (int r = 0; r < T::TP; r += 256) {
     const int p = r + tid;
@@ -268,6 +273,11 @@ __device__ __forceinline__ void sf_tile_body(const SfArgs& A, const int tile, Sf
     if (p < nloc) head = (p == 0) ? (skl[0] != prev_key) : (skl[p] != skl[p - 1]);
     const unsigned long long bal = __ballot(head);
     if (lane == 0) wcount[wv] = __popcll(bal);
+    if (lane % CH == 0 && p < T::TP) {  // (TP < 256 for K >= 32: the upper lanes hold no slot)
+      const unsigned bits = (unsigned)(bal >> lane) & ((1u << CH) - 1u);
+      hb[p / CH] = bits;
+      fh[p / CH] = bits ? __builtin_ctz(bits) : CH;
+    }
     __syncthreads();
     int off = nh;
     for (int w = 0; w < wv; ++w) off += wcount[w];
@@ -275,26 +285,15 @@ __device__ __forceinline__ void sf_tile_body(const SfArgs& A, const int tile, Sf
     nh += wcount[0] + wcount[1] + wcount[2] + wcount[3];
     __syncthreads();
   }
-  if (tid < T::NCH) {
-    int f = CH;
-    for (int q = 0; q < CH; ++q) {
-      const int p = tid * CH + q;
-      if (p >= nloc) break;
-      if ((p == 0) ? (skl[0] != prev_key) : (skl[p] != skl[p - 1])) {
-        f = q;
-        break;
-      }
-    }
-    fh[tid] = f;
-  }
   // 2. chunk-local run pieces: in place at the head, leading piece into lead[j]
   for (int t = tid; t < T::NCH * T::C; t += 256) {
     const int j = t / T::C, c = t - j * T::C;
     const int p0 = j * CH, p1 = min(p0 + CH, nloc);
+    const unsigned bits = hb[j];
     float s = 0.f;
     int h = -1;
     for (int p = p0; p < p1; ++p) {
-      const bool head = (p == 0) ? (skl[0] != prev_key) : (skl[p] != skl[p - 1]);
+      const bool head = (bits >> (p - p0)) & 1u;
       if (head) {
         if (h < 0) lead[j][c] = s;
         else g[h][c] = s;
