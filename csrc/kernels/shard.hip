@@ -290,6 +290,9 @@ __global__ void sh_slot_rows_kernel(const int* __restrict__ perm, const int* __r
 // Training steps (tags != null) also stamp the owner-side request tags here, at the start of the
 // step: the requests of the backward exchange are this step's requests, so the owner update at
 // the end of the step needs no separate tagging launch on the critical path.
+// Stamp = counter + stamp_off: 1 when served at the start of its own step; 2 when SERVED AHEAD
+// during the previous step (whose counter is one lower) -- that step's owner update then patches
+// the served rows it changes (sh_owner_apply_elem), so the fetch leaves the critical path.
 // request e = p*C + c of the received ids: [N][C] blocks (rstride == C, or 0 = contiguous), or
 // this rank's column of the all-gathered [N][N][C] requests (base + rank*C, rstride = N*C)
 __device__ __forceinline__ int sh_rid(const int* __restrict__ r, int e, int C, int rstride) {
@@ -300,7 +303,7 @@ template <int K>
 __global__ void sh_serve_kernel(const int* __restrict__ recv_ids, int total, int N, int C, int rstride,
                                 const float* __restrict__ tv, const float* __restrict__ tw, long ldv,
                                 long ldw, float* __restrict__ rows, const int64_t* __restrict__ step,
-                                ShTable T) {
+                                ShTable T, int stamp_off) {
   constexpr int LPS = K / 4, RW = K + 4;
   const int gt = blockIdx.x * blockDim.x + threadIdx.x;
   const int e = gt / LPS, sub = gt % LPS;
@@ -313,7 +316,7 @@ __global__ void sh_serve_kernel(const int* __restrict__ recv_ids, int total, int
     v = *reinterpret_cast<const f32x4*>(tv + row * ldv + sub * 4);
     if (sub == 0) {
       w = tw[row * ldw];
-      if (T.key) sh_insert(T, N, (unsigned)row, e / C, (unsigned)(e % C), (unsigned)(*step + 1));
+      if (T.key) sh_insert(T, N, (unsigned)row, e / C, (unsigned)(e % C), (unsigned)(*step + stamp_off));
     }
   }
   float* o = rows + (size_t)e * RW;
@@ -336,7 +339,8 @@ __device__ __forceinline__ void sh_owner_apply_elem(int gt, const int* __restric
                                                     int C, int rstride, const float* __restrict__ recv_g,
                                                     ShTable T, float* tv, float* tw, float* s0v, float* s1v,
                                                     float* s0w, float* s1w, long ldv, long ldw, float* Gv,
-                                                    float* Gw, OptHyper h, const int64_t* __restrict__ step) {
+                                                    float* Gw, OptHyper h, const int64_t* __restrict__ step,
+                                                    const ShTable& NT, float* __restrict__ next_rows) {
   constexpr int LPS = K / 4, RW = K + 4;
   const int e = gt / LPS, sub = gt % LPS;
   if (e >= total) return;
@@ -381,6 +385,7 @@ __device__ __forceinline__ void sh_owner_apply_elem(int gt, const int* __restric
   *reinterpret_cast<f32x4*>(tv + o) = pv;
   if (OPT != OPT_GD) *reinterpret_cast<f32x4*>(s0v + o) = a;
   if (OPT == OPT_ADAM || OPT == OPT_FTRL) *reinterpret_cast<f32x4*>(s1v + o) = c;
+  float wnew = 0.f;
   if (sub == 0) {
     float pw = tw[ow];
     float g1 = gw + h.l2 * pw;
@@ -390,6 +395,21 @@ __device__ __forceinline__ void sh_owner_apply_elem(int gt, const int* __restric
     tw[ow] = pw;
     if (OPT != OPT_GD) s0w[ow] = aw;
     if (OPT == OPT_ADAM || OPT == OPT_FTRL) s1w[ow] = cw;
+    wnew = pw;
+  }
+  if (NT.key) {
+    // the next step's requests were served ahead (before this update): refresh the rows this
+    // update changed in every requester's block of the next fetch
+    const unsigned long long* nr = sh_find(NT, N, (unsigned)row, cur + 1);
+    if (nr) {
+      for (int q = 0; q < N; ++q) {
+        const unsigned long long t = nr[q];
+        if ((unsigned)(t >> 32) != cur + 1) continue;
+        float* dst = next_rows + ((size_t)q * C + (unsigned)t) * RW;
+        *reinterpret_cast<f32x4*>(dst + sub * 4) = pv;
+        if (sub == 0) *reinterpret_cast<f32x4*>(dst + K) = f32x4{wnew, 0.f, 0.f, 0.f};
+      }
+    }
   }
 }
 
@@ -397,9 +417,11 @@ template <int K, int MODE, int OPT>
 __global__ void sh_owner_apply_kernel(const int* __restrict__ recv_ids, int total, int N, int C, int rstride,
                                       const float* __restrict__ recv_g, ShTable T, float* tv, float* tw,
                                       float* s0v, float* s1v, float* s0w, float* s1w, long ldv, long ldw,
-                                      float* Gv, float* Gw, OptHyper h, const int64_t* __restrict__ step) {
+                                      float* Gv, float* Gw, OptHyper h, const int64_t* __restrict__ step,
+                                      ShTable NT, float* next_rows) {
   sh_owner_apply_elem<K, MODE, OPT>(blockIdx.x * blockDim.x + threadIdx.x, recv_ids, total, N, C, rstride,
-                                    recv_g, T, tv, tw, s0v, s1v, s0w, s1w, ldv, ldw, Gv, Gw, h, step);
+                                    recv_g, T, tv, tw, s0v, s1v, s0w, s1w, ldv, ldw, Gv, Gw, h, step, NT,
+                                    next_rows);
 }
 
 // ------------------------------------------------------------------------------------ host API
@@ -457,7 +479,7 @@ HFM_API int hfm_sh_slot_rows(const int* perm, const int* sid_incl, const int* up
 HFM_API int hfm_sh_serve(int K, const int* recv_ids, int total, int N, int C, int rstride, const float* tv,
                          const float* tw,
                          long ldv, long ldw, float* rows, const int64_t* step, const ShTable* table,
-                         hipStream_t st) {
+                         int stamp_off, hipStream_t st) {
   const long th = (long)total * (K / 4);
   const int grid = (int)((th + 255) / 256);
   if (grid == 0) return 0;
@@ -465,8 +487,9 @@ HFM_API int hfm_sh_serve(int K, const int* recv_ids, int total, int N, int C, in
   if (T.key && (!step || C <= 0 || (T.mask & (T.mask + 1)) != 0 || T.mask + 1 < 2u * (unsigned)total))
     return (int)hipErrorInvalidValue;
   if (rstride > C && (C <= 0 || rstride % C)) return (int)hipErrorInvalidValue;
+  if (stamp_off != 1 && stamp_off != 2) return (int)hipErrorInvalidValue;
 #define CALL(KK) hipLaunchKernelGGL(sh_serve_kernel<KK>, dim3(grid), dim3(256), 0, st, recv_ids, total, N, \
-                                    C, rstride, tv, tw, ldv, ldw, rows, step, T)
+                                    C, rstride, tv, tw, ldv, ldw, rows, step, T, stamp_off)
   HFM_K_DISPATCH(K, CALL)
 #undef CALL
   HFM_LAUNCH_CHECK();
@@ -483,6 +506,8 @@ struct ShApplyArgs {
   float *Gv, *Gw;
   OptHyper h;
   const int64_t* step;
+  ShTable next;       // lazy mode: the next step's request table when its rows were served ahead
+  float* next_rows;   //   (key == null: none) and its served rows, patched by this update
 };
 
 template <int K>
@@ -495,7 +520,7 @@ static int sh_apply_k(int opt, const ShApplyArgs& A, hipStream_t st) {
 #define L_(M, O)                                                                                      \
   hipLaunchKernelGGL((sh_owner_apply_kernel<K, M, O>), dim3(grid), dim3(256), 0, st, A.recv_ids, A.total, \
                      A.N, A.C, A.rstride, A.recv_g, A.table, A.tv, A.tw, A.s0v, A.s1v, A.s0w, A.s1w, A.ldv, A.ldw, \
-                     A.Gv, A.Gw, A.h, A.step)
+                     A.Gv, A.Gw, A.h, A.step, (M) == 0 ? A.next : ShTable{nullptr, nullptr, 0u, 0}, A.next_rows)
   if ((A.mode & 1) == 1) {
     L_(1, 0);
     return 0;
@@ -519,6 +544,7 @@ HFM_API int hfm_sh_owner_apply(int K, int opt, const ShApplyArgs* A, hipStream_t
   if (A->total <= 0) return 0;
   const unsigned m = A->table.mask;
   if (!A->table.key || (m & (m + 1)) != 0 || m + 1 < 2u * (unsigned)A->total) return (int)hipErrorInvalidValue;
+  if (A->next.key && (!A->next_rows || (A->next.mask & (A->next.mask + 1)) != 0)) return (int)hipErrorInvalidValue;
   int rc = 0;
 #define CALL(KK) rc = sh_apply_k<KK>(opt, *A, st)
   HFM_K_DISPATCH(K, CALL)
@@ -553,7 +579,7 @@ __global__ void __launch_bounds__(256) sh_apply_dense_kernel(ShApplyArgs A, ShDe
   if (b < apply_blocks) {
     sh_owner_apply_elem<K, 0, OPT>(b * 256 + threadIdx.x, A.recv_ids, A.total, A.N, A.C, A.rstride, A.recv_g,
                                    A.table, A.tv, A.tw, A.s0v, A.s1v, A.s0w, A.s1w, A.ldv, A.ldw, A.Gv, A.Gw,
-                                   A.h, A.step);
+                                   A.h, A.step, A.next, A.next_rows);
   } else {
     const float lr_t = OPT == OPT_ADAM ? adam_lr_t(D.h, *A.step + 1) : D.h.lr;
     for (long i = (long)(b - apply_blocks) * 256 + threadIdx.x; i < D.n; i += (long)D.blocks * 256) {
@@ -579,6 +605,7 @@ __global__ void __launch_bounds__(256) sh_apply_dense_kernel(ShApplyArgs A, ShDe
 // lazy rows only (mode 0; tags stamped by this step's serve)
 HFM_API int hfm_sh_apply_dense(int K, int opt, const ShApplyArgs* A, const ShDenseArgs* D, hipStream_t st) {
   if (A->mode != 0 || !D->done || D->blocks < 1 || !A->step) return (int)hipErrorInvalidValue;
+  if (A->next.key && (!A->next_rows || (A->next.mask & (A->next.mask + 1)) != 0)) return (int)hipErrorInvalidValue;
   const long th = (long)A->total * (K / 4);
   const int ab = (int)((th + 255) / 256);
   const dim3 g(ab + D->blocks), blk(256);

@@ -815,6 +815,10 @@ class NativeDeepFM:
             self.shx.reset_table()
 
     def refresh_shadows(self):
+        """Re-derive the bf16 / fp8 weight copies after parameters changed outside a step (load,
+        broadcast); rows served ahead for the next row-sharded step are dropped as well."""
+        if getattr(self, "shx", None) is not None:
+            self.shx.drop_served()
         KN.shadow_refresh(self.p, self.P, self._shadow_dev, self._nshadow)
         if self.fp8:
             KN.w8_quant(self._w8_jobs, len(self.layers), self._w8_rows)
@@ -1379,15 +1383,15 @@ class NativeDeepFM:
             self._host_step += 1
 
     def _plan_state(self):
-        sh = None if self.shx is None else (self.shx.cur, [rs.key for rs in self.shx.sets])
+        sh = None if self.shx is None else (self.shx.cur, [(rs.key, rs.ahead) for rs in self.shx.sets])
         return self._ss_cur, list(self._ss_key), sh
 
     def _set_plan_state(self, st):
         self._ss_cur, self._ss_key = st[0], list(st[1])
         if st[2] is not None:
             self.shx.cur = st[2][0]
-            for rs, k in zip(self.shx.sets, st[2][1]):
-                rs.key = k
+            for rs, (k, a) in zip(self.shx.sets, st[2][1]):
+                rs.key, rs.ahead = k, a
 
     def train_step(self, ids, vals, labels, use_graph: bool = False, next_ids=None,
                    stage: bool = False):

@@ -120,7 +120,7 @@ class ShApplyArgs(C.Structure):
                 ("rstride", c_int), ("recv_g", c_void_p), ("table", ShTable), ("tv", c_void_p), ("tw", c_void_p),
                 ("s0v", c_void_p), ("s1v", c_void_p), ("s0w", c_void_p), ("s1w", c_void_p),
                 ("ldv", c_long), ("ldw", c_long), ("Gv", c_void_p), ("Gw", c_void_p), ("h", OptHyper),
-                ("step", c_void_p)]
+                ("step", c_void_p), ("next", ShTable), ("next_rows", c_void_p)]
 
 
 class ShDenseArgs(C.Structure):
@@ -220,7 +220,7 @@ _SIGS = {
     "hfm_sh_bucket": [c_void_p, c_void_p, c_int, c_int, c_int] + [c_void_p] * 5 + [c_void_p],
     "hfm_sh_slot_rows": [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p],
     "hfm_sh_serve": [c_int, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_long, c_long, c_void_p,
-                     c_void_p, c_void_p, c_void_p],
+                     c_void_p, c_void_p, c_int, c_void_p],
     "hfm_sh_owner_apply": [c_int, c_int, c_void_p, c_void_p],
     "hfm_sh_apply_args_bytes": [],
     "hfm_sh_apply_dense": [c_int, c_int, c_void_p, c_void_p, c_void_p],

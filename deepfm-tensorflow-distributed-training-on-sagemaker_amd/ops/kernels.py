@@ -474,15 +474,18 @@ def sh_slot_rows(perm, sid_incl, upos, n, idx):
 _byref = C.byref
 
 
-def sh_serve(K, recv_ids, total, N, tv, tw, rows, C: int = 0, step=None, table=None, rstride: int = 0):
+def sh_serve(K, recv_ids, total, N, tv, tw, rows, C: int = 0, step=None, table=None, rstride: int = 0,
+             ahead: bool = False):
     """Owner side of the row fetch: rows[e] = {v, w} of every requested id.  With ``table`` (a
     ShTable; training steps) it also records each request (row, requester, slot) stamped with
-    step + 1 in the owner's request table read by sh_owner_apply.  ``recv_ids``: a tensor or a
-    device address; ``rstride``: its request-row stride (0: contiguous [N][C])."""
+    step + 1 in the owner's request table read by sh_owner_apply -- step + 2 with ``ahead`` (the
+    NEXT step's rows, served during this step; this step's owner update patches the rows it
+    changes).  ``recv_ids``: a tensor or a device address; ``rstride``: its request-row stride
+    (0: contiguous [N][C])."""
     rp = recv_ids if isinstance(recv_ids, int) else ptr(recv_ids)
     check(L().hfm_sh_serve(K, rp, total, N, C, rstride, ptr(tv), ptr(tw), *_ld(tv, tw), ptr(rows),
-                           ptr(step), _byref(table) if table is not None else None, stream_handle()),
-          "sh_serve")
+                           ptr(step), _byref(table) if table is not None else None, 2 if ahead else 1,
+                           stream_handle()), "sh_serve")
 
 
 def sh_apply_dense(K, opt, args: ShApplyArgs, dense):

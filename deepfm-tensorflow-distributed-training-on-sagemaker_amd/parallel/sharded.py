@@ -26,6 +26,10 @@ from ..ops._lib import ShApplyArgs, ShTable
 
 # routing in two launches (sh_route) instead of segments + bucket (7 launches); same outputs
 _ROUTE2 = os.environ.get("HIPFM_SH_ROUTE2", "1") == "1"
+# lazy rows: the NEXT batch's rows are served on the side stream during this step (after its
+# routing); this step's owner update patches the rows it changes, so the serve launch leaves
+# the critical path
+_SERVE_AHEAD = os.environ.get("HIPFM_SH_SERVE_AHEAD", "1") == "1"
 
 
 def estimate_capacity(id_batches: Iterable[torch.Tensor], world: int, slack: float = 1.25,
@@ -105,6 +109,21 @@ class _RouteSet:
         self.slot_row = torch.zeros(n, **i32)
         self.recv = (self.recv_ids.data_ptr(), 0)   # (requests address, row stride) for the owner
         self.key = None          # host: (ids data_ptr, B) routed into this set
+        # owner side: served rows and the request table (csrc/kernels/shard.hip) of this set's
+        # batch -- per set, because the next batch's rows are served (and its requests stamped)
+        # while the current batch's update still reads its own table.  The table has a power of
+        # two >= 2x the N*C request slots; keys and per-requester positions carry step stamps --
+        # sized by the exchange, not by the table (a direct [R_local][N] tag array is 7 GB per
+        # rank at the 1TB shape)
+        T = N * C
+        self.rows_out = torch.zeros(T, m.K + 4, dtype=torch.float32, device=dev)
+        slots = 1
+        while slots < 2 * T:
+            slots *= 2
+        self.req_key = torch.zeros(slots, dtype=torch.int64, device=dev)
+        self.req_pos = torch.zeros(slots * N, dtype=torch.int64, device=dev)
+        self.table = ShTable(self.req_key.data_ptr(), self.req_pos.data_ptr(), slots - 1, 0)
+        self.ahead = False       # host: rows_out holds this batch's rows, served ahead
 
 
 class FixedCapacityExchange:
@@ -131,20 +150,11 @@ class FixedCapacityExchange:
             rs.gathered = torch.zeros(self.N * self.N * self.C, dtype=torch.int32, device=dev)
         self.cur = 0
         self.err = torch.zeros(1, dtype=torch.int32, device=dev)
-        self.rows_out = torch.zeros(T, self.RW, **f32)
         self.rows_in = torch.zeros(T, self.RW, **f32)
         self.send_g = torch.zeros(T, self.RW, **f32)
         self.recv_g = torch.zeros(T, self.RW, **f32)
-        # owner-side request table (csrc/kernels/shard.hip): a power of two >= 2x the N*C request
-        # slots, keys and per-requester positions stamped with step + 1 -- sized by the exchange,
-        # not by the table (a direct [R_local][N] tag array is 7 GB per rank at the 1TB shape)
-        slots = 1
-        while slots < 2 * T:
-            slots *= 2
-        self.req_key = torch.zeros(slots, dtype=torch.int64, device=dev)
-        self.req_pos = torch.zeros(slots * self.N, dtype=torch.int64, device=dev)
-        self.table = ShTable(self.req_key.data_ptr(), self.req_pos.data_ptr(), slots - 1, 0)
         self._side = None
+        self._joined = False
         self._fork_at = None
         self._fork_plan = None
         self.dense_recv = None               # [N][P] all-gathered dense gradients (fused exchange)
@@ -152,15 +162,19 @@ class FixedCapacityExchange:
     # ------------------------------------------------------------------ host-side plan
     def plan(self, ids: torch.Tensor, B: int, nxt: Optional[torch.Tensor], resident: bool = True):
         """Routing decisions for one step (part of the graph key): (set index, route the current
-        batch inline?, next ids or None).  Only resident batches (fixed device buffers) can have
-        been prefetched: staged buffers change content under the same address."""
+        batch inline?, next ids or None, rows already served ahead?, serve the next batch's rows
+        ahead?).  Only resident batches (fixed device buffers) can have been prefetched: staged
+        buffers change content under the same address."""
         c = self.cur
         key = (ids.data_ptr(), B)
         inline = (not resident) or self.sets[c].key != key
+        ahead = (not inline) and self.sets[c].ahead
         if nxt is not None and self.eng_route is None:
             get = getattr(self.m.comm, "route_engine", None)
             self.eng_route = get() if get is not None else self.eng
-        return (c, inline, None if nxt is None else (nxt.data_ptr(), nxt.numel() // self.m.F))
+        serve_next = nxt is not None and _SERVE_AHEAD and self.m.sparse_update == "lazy"
+        return (c, inline, None if nxt is None else (nxt.data_ptr(), nxt.numel() // self.m.F), ahead,
+                serve_next)
 
     def commit(self, plan, ids: torch.Tensor, B: int, resident: bool = True):
         """Consecutive steps always use alternate routing sets (prefetched or not): a step's
@@ -169,10 +183,18 @@ class FixedCapacityExchange:
         caller declared as next (``next_ids``): a set is never matched again by address alone,
         since a freshly allocated batch can get the address of an earlier one back from the
         caching allocator."""
-        c, _, nk = plan
+        c, _, nk, _, serve_next = plan
         self.sets[c].key = None
+        self.sets[c].ahead = False
         self.sets[1 - c].key = nk
+        self.sets[1 - c].ahead = nk is not None and serve_next
         self.cur = 1 - c
+
+    def drop_served(self):
+        """Parameters changed outside a step (load / broadcast): rows served ahead are stale, so
+        the next step serves its rows itself (its prefetched routing stays valid)."""
+        for rs in self.sets:
+            rs.ahead = False
 
     # ------------------------------------------------------------------ pieces
     def route(self, rs: _RouteSet, ids: torch.Tensor, B: int, eng, gather: bool = False):
@@ -212,9 +234,10 @@ class FixedCapacityExchange:
         branches are dispatched in capture order: a branch enqueued first delays the main
         stream's first kernels)."""
         m = self.m
-        c, inline, nk = plan
+        c, inline, nk = plan[:3]
         if inline:
             self.route(self.sets[c], m.idx, B, self.eng)
+        self._joined = False
         self._fork_at = fork if nk is not None else None
         self._fork_plan = plan
         if self._fork_at == "start":
@@ -226,19 +249,29 @@ class FixedCapacityExchange:
             return
         self._fork_at = None
         m = self.m
-        c, _, nk = self._fork_plan
+        c, _, nk, _, serve_next = self._fork_plan
         main = torch.cuda.current_stream(m.device)
         if self._side is None:
             self._side = torch.cuda.Stream(m.device)
         self._side.wait_stream(main)
         nxt_ids = self._next_ids
+        rs = self.sets[1 - c]
         with torch.cuda.stream(self._side):
-            self.route(self.sets[1 - c], nxt_ids, nk[1], self.eng_route, gather=True)
+            self.route(rs, nxt_ids, nk[1], self.eng_route, gather=True)
+            if serve_next:
+                # the next batch's rows as of now (stamped step + 2); this step's owner update
+                # patches the rows it changes (it joins this branch first)
+                KN.sh_serve(m.K, rs.recv[0], self.N * self.C, self.N, m.tv, m.tw, rs.rows_out, C=self.C,
+                            step=m.step, table=rs.table, rstride=rs.recv[1], ahead=True)
+
+    def _join_side(self, plan):
+        if plan[2] is not None and not self._joined:
+            torch.cuda.current_stream(self.m.device).wait_stream(self._side)
+            self._joined = True
 
     def end(self, plan):
         self.fork_next()                     # (not forked yet: e.g. no tower in this step)
-        if plan[2] is not None:
-            torch.cuda.current_stream(self.m.device).wait_stream(self._side)
+        self._join_side(plan)
 
     def fetch(self, plan, train: bool = True):
         """Owners serve the requested rows (after the previous step's updates), rows come back.
@@ -247,12 +280,13 @@ class FixedCapacityExchange:
         m = self.m
         rs = self.sets[plan[0]]
         if train:
-            KN.sh_serve(m.K, rs.recv[0], self.N * self.C, self.N, m.tv, m.tw, self.rows_out,
-                        C=self.C, step=m.step, table=self.table, rstride=rs.recv[1])
+            if not plan[3]:                  # (else served during the previous step)
+                KN.sh_serve(m.K, rs.recv[0], self.N * self.C, self.N, m.tv, m.tw, rs.rows_out,
+                            C=self.C, step=m.step, table=rs.table, rstride=rs.recv[1])
         else:
-            KN.sh_serve(m.K, rs.recv[0], self.N * self.C, self.N, m.tv, m.tw, self.rows_out, C=self.C,
+            KN.sh_serve(m.K, rs.recv[0], self.N * self.C, self.N, m.tv, m.tw, rs.rows_out, C=self.C,
                         rstride=rs.recv[1])
-        self.eng.alltoall(self.rows_out, self.rows_in, self.C * self.RW * 4)
+        self.eng.alltoall(rs.rows_out, self.rows_in, self.C * self.RW * 4)
         if train and self._fork_at == "fetch":
             self.fork_next()
         return rs.slot_row, self.rows_in[:, : m.K], self.rows_in[:, m.K]
@@ -292,7 +326,7 @@ class FixedCapacityExchange:
         S.recv_ids, S.total, S.N, S.C = rs.recv[0], self.N * self.C, self.N, self.C
         S.rstride = rs.recv[1]
         S.mode = 0 if m.sparse_update == "lazy" else 1      # tags were stamped by fetch()
-        S.recv_g, S.table = self.recv_g.data_ptr(), self.table
+        S.recv_g, S.table = self.recv_g.data_ptr(), rs.table
         S.tv, S.tw = m.tv.data_ptr(), m.tw.data_ptr()
         S.s0v, S.s1v, S.s0w, S.s1w = (t.data_ptr() if t.numel() else 0 for t in m.sv)
         S.ldv, S.ldw = KN._ld(m.tv, m.tw)
@@ -300,6 +334,11 @@ class FixedCapacityExchange:
             S.Gv, S.Gw = m.Gv.data_ptr(), m.Gw.data_ptr()
         S.h = m.h_sparse
         S.step = m.step.data_ptr()
+        if plan[2] is not None and plan[4] and m.sparse_update == "lazy":
+            # the next batch's rows were served ahead: join that branch, patch what changes
+            nxt = self.sets[1 - plan[0]]
+            self._join_side(plan)
+            S.next, S.next_rows = nxt.table, nxt.rows_out.data_ptr()
         if dense is not None:
             if join is not None:
                 join()
@@ -310,9 +349,11 @@ class FixedCapacityExchange:
             KN.dense_sweep(m.K, m.opt_id, m.R, m.tv, m.tw, m.Gv, m.Gw, m.sv, m.h_sparse, m.step)
 
     def reset_table(self):
-        """The table's stamps are step numbers: clear it when the step counter is rewritten."""
-        self.req_key.zero_()
-        self.req_pos.zero_()
+        """The tables' stamps are step numbers: clear them when the step counter is rewritten."""
+        for rs in self.sets:
+            rs.req_key.zero_()
+            rs.req_pos.zero_()
+        self.drop_served()
 
     def error(self) -> int:
         return int(self.err.item())

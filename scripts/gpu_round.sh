@@ -16,8 +16,11 @@ fi
 i=0
 for spec in "$@"; do
   i=$((i + 1))
-  envs="${spec%%--*}"; args="${spec#*--}"
-  [ "$envs" = "$spec" ] && envs="" && args="$spec"
+  # "ENV=a ENV2=b -- bench args" or just "bench args"
+  case "$spec" in
+    *" -- "*) envs="${spec%% -- *}"; args="${spec#* -- }" ;;
+    *) envs=""; args="$spec" ;;
+  esac
   echo "bench[$i] env=[$envs] args=[$args]"
   env $envs timeout -k 10 300 python bench.py $args > gpurun_out/bench_$i.log 2>&1
   rc=$?; tail -1 gpurun_out/bench_$i.log

@@ -219,7 +219,7 @@ def test_sharded_exchange_n8_criteo_1tb_shape():
         _fill_tables(m, N, r)
         assert m.shx is not None and m.shx.N == N and m.shx.C == cap
         # the request table follows the exchange size, not the 110M-row shard
-        assert m.shx.req_key.numel() * 8 * (1 + N) < 256 * (1 << 20)
+        assert sum(rs.req_key.numel() * 8 * (1 + N) for rs in m.shx.sets) < 256 * (1 << 20)
         models.append(m)
     _run_ranks(models, batches, prefetch=True)
     torch.cuda.synchronize()

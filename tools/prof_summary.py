@@ -40,7 +40,7 @@ def main():
         # the median-span step of the timed steps (graph replays) is listed
         idx = [i for i, r in enumerate(rows) if r["Kernel_Name"].startswith(
             ("step_inc", "void dense_opt_kernel", "void finalize_opt_kernel", "void wgfin_kernel<0",
-             "void sfwg_kernel"))]
+             "void sfwg_kernel", "void sh_apply_dense_kernel"))]
         pairs = [(a, b, int(rows[b]["End_Timestamp"]) - int(rows[a]["End_Timestamp"]))
                  for a, b in zip(idx, idx[1:])]
         pairs = [p for p in pairs if p[2] < 1_000_000]       # steps, not eval / setup gaps
