@@ -160,7 +160,9 @@ def main():
     ap.add_argument("--embedding_mode", default="auto")
     ap.add_argument("--mlp_dtype", default="bf16", choices=["bf16", "fp8"],
                     help="deep-tower forward GEMM operands (fp8 = OCP e4m3 MFMA, config #5)")
-    ap.add_argument("--pool", type=int, default=16, help="resident synthetic batches per rank")
+    ap.add_argument("--pool", type=int, default=128,
+                    help="resident synthetic batches per rank (the HBM-cached epoch; a 16-batch pool "
+                         "replayed hundreds of times memorizes its ids: train loss -> 0, eval AUC drops)")
     ap.add_argument("--eval_batches", type=int, default=8)
     ap.add_argument("--no_graph", action="store_true")
     ap.add_argument("--graph_steps", type=int, default=int(os.environ.get("HIPFM_GRAPH_STEPS", "16")),
