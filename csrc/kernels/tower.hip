@@ -78,6 +78,8 @@ struct TowerArgs {
   int x8_off;                     // LDS byte offset of the fp8 E tile [32][K0p + 16] (fp8)
   float* S;                       // [M, K]  sum_f E (sparse backward)
   bf16* Et;                       // [K0p, M] (train: wgrad operand)
+  int idx_ld;                     // 0: idx row-major [M, F]; else field-major [F, idx_ld] (the
+                                  // layout the per-field sort reads, so it needs no transpose)
 };
 
 // fp8 variant of mma32 (16x16x32 fp8 MFMA; same fragment map as bf16 with 8 one-byte elements
@@ -185,7 +187,7 @@ __device__ __forceinline__ void tower_gather(const TowerArgs& a, int row0, bf16*
 #pragma unroll
     for (int t = 0; t < FMAX; ++t) {
       const int f = f0 + 8 * t;
-      id[t] = f < F ? a.idx[(size_t)b * F + f] : 0;
+      id[t] = f < F ? a.idx[a.idx_ld ? (size_t)f * a.idx_ld + b : (size_t)b * F + f] : 0;
       x[t] = f < F ? a.vals[(size_t)b * F + f] : 0.f;
     }
     f32x4 v[FMAX][V4];
@@ -501,7 +503,7 @@ HFM_API int hfm_tower(const TowerArgs* ap, int KE, hipStream_t st) {
       for (int i = 0; i + 1 < a.nl; ++i)
         if (a.Np[i] > a.K0p) return (int)hipErrorInvalidValue;
     if (!a.idx || !a.vals || !a.tv || !a.tw || !a.fm_bias || a.F * KE > a.K0p || a.x_off < 0 ||
-        (a.train && !a.Et) || (a.fp8 && a.x8_off < 0) || (a.ldv & 3))
+        (a.train && !a.Et) || (a.fp8 && a.x8_off < 0) || (a.ldv & 3) || (a.idx_ld && a.idx_ld < a.M))
       return (int)hipErrorInvalidValue;
   }
   if (a.fp8) {

@@ -296,6 +296,8 @@ class NativeDeepFM:
         self._side = None
         self._side_next = None
         self._next_sort_ids = None
+        self._next_fm = False      # the declared next batch's ids are field-major
+        self._idx_fm = False       # the bound batch's ids (self.idx) are field-major [F, M]
         self._comm_stream = None
         self.shx = None
         self._shx_plan = None
@@ -687,6 +689,8 @@ class NativeDeepFM:
         if gather is not None:
             idx, tv, tw = gather
             a.idx, a.vals, a.tv, a.tw = idx.data_ptr(), self.vals.data_ptr(), tv.data_ptr(), tw.data_ptr()
+            # field-major bound ids (the sharded step gathers through its row-major slot map)
+            a.idx_ld = self.M if (self._idx_fm and idx is self.idx) else 0
             a.ldv, a.ldw = KN._ld(tv, tw)
             a.fm_bias = pb + 4 * self.dense_segs["fm_bias"].off
             a.F = self.F
@@ -827,6 +831,7 @@ class NativeDeepFM:
     def stage_batch(self, ids: torch.Tensor, vals: torch.Tensor, labels: Optional[torch.Tensor]):
         """Copy a batch into the static input buffers (device->device when already resident)."""
         self.idx, self.vals, self.labels = self._own_in
+        self._idx_fm = False
         B = ids.shape[0]
         M = self._padM(B)
         if M > self._bufs_M:
@@ -1039,7 +1044,7 @@ class NativeDeepFM:
         the field id ranges are known, else the global radix sort."""
         n = B * self.F
         if self.uses_field_sort(B):
-            self._fsort(self.idx, B, self.sorted_keys, self.perm)
+            self._fsort(self.idx, B, self.sorted_keys, self.perm, field_major=self._idx_fm)
         else:
             KN.sort_ids(self.idx, self.sorted_keys, None, self.perm, n, self.end_bit, self.temp)
 
@@ -1152,12 +1157,12 @@ class NativeDeepFM:
             if self._side_next is None:
                 self._side_next = torch.cuda.Stream(self.device)
             self._side_next.wait_stream(main)
-            nk_ids, nk_B = self._next_sort_ids, plan[2][1]
+            nk_ids, nk_B, nk_fm = self._next_sort_ids, plan[2][1], self._next_fm
             nxt_keys, nxt_perm = self._ss[1 - plan[0]]
 
             def sort_next():
                 with torch.cuda.stream(self._side_next):
-                    self._fsort_next(nk_ids, nk_B, nxt_keys, nxt_perm)
+                    self._fsort_next(nk_ids, nk_B, nxt_keys, nxt_perm, field_major=nk_fm)
             # enqueued right after the tower (graph branches are dispatched in capture order);
             # same-box sweep of the enqueue point: after the tower 0.1318, after the dense
             # gradients 0.1316, at the end 0.1351, at the start 0.1365 ms/step.  (Letting the
@@ -1326,10 +1331,23 @@ class NativeDeepFM:
         U = int(self.num_u.item())
         return self.g.clone(), self.ukeys[:U].clone(), self.UG[:U].clone()
 
+    def _field_major(self, ids) -> bool:
+        """``ids`` [B, F] stored field-major (the transposed view of a contiguous [F, B] tensor,
+        e.g. ``idsT.t()``) and usable as such: the tower gathers through either layout, and the
+        per-field sort reads this one directly (no transpose launch).  Other paths take row-major
+        ids, so a field-major batch elsewhere is staged (copied row-major)."""
+        return (ids.dim() == 2 and ids.shape[0] > 1 and ids.stride() == (1, ids.shape[0]) and
+                self.gather_fused and self.uses_field_sort(ids.shape[0]))
+
+    @staticmethod
+    def _flat_ids(ids, fm: bool) -> torch.Tensor:
+        """The storage of a bound id batch as a flat view (field-major: [F * B])."""
+        return ids.t().reshape(-1) if fm else ids.reshape(-1)
+
     def _resident(self, ids, vals, labels) -> bool:
         return (ids.is_cuda and ids.dtype == torch.int32 and vals.dtype == torch.float32 and
-                ids.is_contiguous() and vals.is_contiguous() and labels.is_contiguous() and
-                ids.shape[0] == self.M and ids.numel() == self.M * self.F)
+                (ids.is_contiguous() or self._field_major(ids)) and vals.is_contiguous() and
+                labels.is_contiguous() and ids.shape[0] == self.M and ids.numel() == self.M * self.F)
 
     def _bind_step(self, ids, vals, labels, next_ids=None, stage: bool = False):
         """Bind one step's batch (in place when resident, else -- or with ``stage`` -- a copy into
@@ -1339,15 +1357,20 @@ class NativeDeepFM:
         direct = (not stage) and self._resident(ids, vals, labels)
         if direct:
             B = ids.shape[0]
-            self.idx, self.vals, self.labels = ids.reshape(-1), vals.reshape(-1), labels.reshape(-1)
-            key = (ids.data_ptr(), vals.data_ptr(), labels.data_ptr(), B)
+            fm = not ids.is_contiguous()
+            self.idx = self._flat_ids(ids, fm)
+            self.vals, self.labels = vals.reshape(-1), labels.reshape(-1)
+            self._idx_fm = fm
+            key = (ids.data_ptr(), vals.data_ptr(), labels.data_ptr(), B, fm)
         else:
             self.idx, self.vals, self.labels = self._own_in
             B = self.stage_batch(ids, vals, labels)
             key = ("staged", B)
         nxt_ok = (direct and next_ids is not None and next_ids.is_cuda and
-                  next_ids.dtype == torch.int32 and next_ids.is_contiguous() and
+                  next_ids.dtype == torch.int32 and
+                  (next_ids.is_contiguous() or self._field_major(next_ids)) and
                   next_ids.shape[0] == B and next_ids.numel() == B * self.F)
+        nxt_fm = nxt_ok and not next_ids.is_contiguous()
         self._shx_plan = None
         self._sort_plan = None
         if (not self.sharded and _SORT_SIDE_STREAM and self._fsort_next is not None and
@@ -1359,13 +1382,15 @@ class NativeDeepFM:
             nk = None
             if nxt_ok:
                 nk = (next_ids.data_ptr(), B)
-                self._next_sort_ids = next_ids.reshape(-1)
+                self._next_sort_ids = self._flat_ids(next_ids, nxt_fm)
+                self._next_fm = nxt_fm
             self._sort_plan = (c, inline, nk)
             key = key + ("sort",) + self._sort_plan
         if self.shx is not None:
-            nxt = next_ids.reshape(-1) if (nxt_ok and _SHARD_PIPELINE) else None
+            nxt = self._flat_ids(next_ids, nxt_fm) if (nxt_ok and _SHARD_PIPELINE) else None
             self._shx_plan = self.shx.plan(self.idx, B, nxt, resident=direct)
             self.shx._next_ids = nxt
+            self.shx._next_fm = nxt_fm
             key = key + self._shx_plan
         return B, direct, key
 

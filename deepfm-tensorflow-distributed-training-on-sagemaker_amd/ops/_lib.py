@@ -147,7 +147,7 @@ class TowerArgs(C.Structure):
                 ("sW", c_void_p * TW_MAXL),
                 ("idx", c_void_p), ("vals", c_void_p), ("tv", c_void_p), ("tw", c_void_p),
                 ("ldv", c_long), ("ldw", c_long), ("fm_bias", c_void_p), ("F", c_int),
-                ("x_off", c_int), ("x8_off", c_int), ("S", c_void_p), ("Et", c_void_p)]
+                ("x_off", c_int), ("x8_off", c_int), ("S", c_void_p), ("Et", c_void_p), ("idx_ld", c_int)]
 
 
 class W8Job(C.Structure):

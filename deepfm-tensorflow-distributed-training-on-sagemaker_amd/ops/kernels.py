@@ -178,8 +178,12 @@ class FieldSort:
             self._work[nc] = w
         return w
 
-    def __call__(self, ids, B: int, keys_out, perm_out):
+    def __call__(self, ids, B: int, keys_out, perm_out, field_major: bool = False):
+        """``ids``: row-major [B, F] slots (transposed first), or with ``field_major`` the [F, B]
+        layout the sort reads (no transpose launch)."""
         assert B <= self.max_rows and ids.numel() >= B * self.F
+        if field_major:
+            return self._sort(ids, B, keys_out, perm_out)
         work, nwork = self.work(B)
         check(L().hfm_field_sort(ptr(ids), B, self.F, ptr(self.fr), ptr(work), nwork,
                                  ptr(self.idsT), ptr(self.rk), ptr(self.rp), ptr(keys_out), ptr(perm_out),
@@ -187,9 +191,12 @@ class FieldSort:
 
     def sort_pre(self, B: int, keys_out, perm_out):
         """The sort alone, from ``self.idsT`` already filled field-major ([F, B]) by fm_fwd."""
+        self._sort(self.idsT, B, keys_out, perm_out)
+
+    def _sort(self, idsT, B: int, keys_out, perm_out):
         assert B <= self.max_rows
         work, nwork = self.work(B)
-        check(L().hfm_field_sort_pre(ptr(self.idsT), B, self.F, ptr(self.fr), ptr(work), nwork,
+        check(L().hfm_field_sort_pre(ptr(idsT), B, self.F, ptr(self.fr), ptr(work), nwork,
                                      ptr(self.rk), ptr(self.rp), ptr(keys_out), ptr(perm_out),
                                      ptr(self.err), stream_handle()), "field_sort_pre")
 

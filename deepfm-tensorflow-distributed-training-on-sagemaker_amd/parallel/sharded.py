@@ -155,6 +155,7 @@ class FixedCapacityExchange:
         self.recv_g = torch.zeros(T, self.RW, **f32)
         self._side = None
         self._joined = False
+        self._next_ids, self._next_fm = None, False
         self._fork_at = None
         self._fork_plan = None
         self.dense_recv = None               # [N][P] all-gathered dense gradients (fused exchange)
@@ -197,7 +198,7 @@ class FixedCapacityExchange:
             rs.ahead = False
 
     # ------------------------------------------------------------------ pieces
-    def route(self, rs: _RouteSet, ids: torch.Tensor, B: int, eng, gather: bool = False):
+    def route(self, rs: _RouteSet, ids: torch.Tensor, B: int, eng, gather: bool = False, fm: bool = False):
         """Sort + dedup the slot ids, bucket the unique ids by owner, send the requests.
         ``gather``: requests travel by all-gather (every rank's [N, C] block; this rank keeps
         column ``rank``) instead of all-to-all — RCCL's all-to-all cannot be captured on a forked
@@ -205,7 +206,7 @@ class FixedCapacityExchange:
         m = self.m
         n = B * m.F
         if m.uses_field_sort(B):
-            m._fsort(ids, B, rs.sorted_keys, rs.perm)
+            m._fsort(ids, B, rs.sorted_keys, rs.perm, field_major=fm)
         else:
             KN.sort_ids(ids, rs.sorted_keys, None, rs.perm, n, m.end_bit, rs.temp)
         if _ROUTE2:
@@ -236,7 +237,7 @@ class FixedCapacityExchange:
         m = self.m
         c, inline, nk = plan[:3]
         if inline:
-            self.route(self.sets[c], m.idx, B, self.eng)
+            self.route(self.sets[c], m.idx, B, self.eng, fm=m._idx_fm)
         self._joined = False
         self._fork_at = fork if nk is not None else None
         self._fork_plan = plan
@@ -257,7 +258,7 @@ class FixedCapacityExchange:
         nxt_ids = self._next_ids
         rs = self.sets[1 - c]
         with torch.cuda.stream(self._side):
-            self.route(rs, nxt_ids, nk[1], self.eng_route, gather=True)
+            self.route(rs, nxt_ids, nk[1], self.eng_route, gather=True, fm=self._next_fm)
             if serve_next:
                 # the next batch's rows as of now (stamped step + 2); this step's owner update
                 # patches the rows it changes (it joins this branch first)

@@ -113,3 +113,28 @@ def test_exchange_serve_ahead_bitwise(group):
     assert a.shx.sets[a.shx.cur].ahead and not b.shx.sets[b.shx.cur].ahead
     for x in (b, c):
         assert torch.equal(a.tv, x.tv) and torch.equal(a.tw, x.tw) and torch.equal(a.p, x.p)
+
+
+def test_exchange_field_major_batches_bitwise(group):
+    """Row-sharded step (1-rank RCCL group) on field-major resident batches: the routing sorts
+    read them without a transpose; bitwise equal to row-major batches."""
+    synth = make_synth("total:6000", seed=31)
+    F, K, layers, keep = synth.F, 8, [64, 32], [0.8, 0.8]
+    V = synth.feature_size
+    params = init_params(V, F, K, layers, False, seed=8)
+    pool = [synth.batch(512, step=s, device="cuda", id_dtype=torch.int32) for s in range(4)]
+    out = []
+    for fm in (True, False):
+        m = NativeDeepFM(V, F, K, layers, keep, sparse_update="lazy", batch_size=512, device="cuda",
+                         init=False, comm=Comm(sharded=True, force_exchange=True),
+                         field_ranges=synth.field_ranges())
+        m.load_tf_params(params)
+        bl = [(i.t().contiguous().t() if fm else i, v, lab) for i, v, lab in pool]
+        assert m._resident(*bl[0])
+        for _ in range(2):
+            m.train_steps(bl, next_ids=bl[0][0])
+        torch.cuda.synchronize()
+        m.check_errors()
+        out.append((m.tv.clone(), m.tw.clone(), m.p.clone()))
+    for x, y in zip(*out):
+        assert torch.equal(x, y)

@@ -579,3 +579,37 @@ def test_multi_step_graph_bitwise_equals_single_steps(G):
         out.append((m.tv.clone(), m.tw.clone(), m.p.clone(), m.sv[0].clone()))
     for x, y in zip(*out):
         assert torch.equal(x, y)
+
+
+def field_major(ids):
+    """[B, F] view of a field-major ([F, B] contiguous) copy of ``ids``."""
+    return ids.t().contiguous().t()
+
+
+def test_field_major_resident_batches_bitwise_equal():
+    """Resident batches whose ids are stored field-major (the layout the per-field sort reads,
+    no transpose launch) train bitwise like row-major ones: multi-step graphs with prefetched
+    next-batch sorts, then eager steps and predictions."""
+    synth = make_synth("criteo_kaggle", seed=24)
+    F, K, layers, keep, B = synth.F, 8, [128, 64, 32], [0.5] * 3, 1024
+    params = init_params(synth.feature_size, F, K, layers, False, seed=6)
+    pool = [synth.batch(B, step=s, device=DEV, id_dtype=torch.int32) for s in range(4)]
+    out = []
+    for fm in (True, False):
+        m = NativeDeepFM(synth.feature_size, F, K, layers, keep, batch_size=B, device=DEV, init=False,
+                         sparse_update="lazy", field_ranges=synth.field_ranges())
+        m.load_tf_params(params)
+        bl = [(field_major(i) if fm else i, v, lab) for i, v, lab in pool]
+        if fm:
+            assert m._resident(*bl[0]) and not bl[0][0].is_contiguous()
+        for rep in range(2):
+            m.train_steps(bl, next_ids=bl[0][0])
+        for s in range(3):
+            m.train_step(*bl[s], next_ids=bl[s + 1][0])
+        m.train_step(*bl[3])
+        p = m.predict(bl[2][0], bl[2][1])
+        torch.cuda.synchronize()
+        m.check_errors()
+        out.append((m.tv.clone(), m.tw.clone(), m.p.clone(), p.clone()))
+    for x, y in zip(*out):
+        assert torch.equal(x, y)
