@@ -33,8 +33,10 @@ METRIC = ("samples/sec (whole node) + eval AUC, Criteo-1TB-shape DeepFM at 1/2/4
 # Multi-GPU execution ladder (bench supervisor, below): the fastest path first, then paths with
 # fewer moving parts.  Every rung is the same full training step (same model, optimizer, data).
 # The step's collective pattern of round 1 (separate dense all-reduce on its own stream, 7-launch
-# routing) is the fallback when the fused exchange (grouped all-to-all + all-gather) fails.
-_R1_EXCHANGE = {"HIPFM_SH_XFUSE": "0", "HIPFM_SH_APPLY_DENSE": "0", "HIPFM_SH_ROUTE2": "0"}
+# routing, rows served in-step) is the fallback when the fused exchange (grouped all-to-all +
+# all-gather, rows served ahead) fails.
+_R1_EXCHANGE = {"HIPFM_SH_XFUSE": "0", "HIPFM_SH_APPLY_DENSE": "0", "HIPFM_SH_ROUTE2": "0",
+                "HIPFM_SH_SERVE_AHEAD": "0"}
 LADDER = [
     ("graph+prefetch", {}),                                  # HIP graphs, next-batch routing prefetch
     ("graph+prefetch+allreduce", dict(_R1_EXCHANGE)),        # same, dense all-reduce on a comm stream
@@ -71,7 +73,7 @@ def supervise(argv) -> int:
     world = int(os.environ["WORLD_SIZE"])
     store = dist.TCPStore(os.environ.get("MASTER_ADDR", "127.0.0.1"), int(os.environ["MASTER_PORT"]),
                           world, is_master=False, timeout=__import__("datetime").timedelta(seconds=600))
-    hang_s = float(os.environ.get("HIPFM_BENCH_HANG_S", "240"))
+    hang_s = float(os.environ.get("HIPFM_BENCH_HANG_S", "150"))
     ladder = LADDER[int(os.environ.get("HIPFM_BENCH_FIRST_RUNG", "0")):]
     for k, (name, extra) in enumerate(ladder):
         if rank == 0:
