@@ -132,6 +132,111 @@ __global__ void __launch_bounds__(256) dense_sweep_kernel(
   }
 }
 
+// ------------------------------------------------------------------ tf1_dense, split form
+// The same TF1 update as scatter + dense_sweep, split by row set (one GPU, record layout):
+//  * rows of this step's batch get their full update (g = G + l2*w) from the sparse kernel's
+//    lazy mode -- the arithmetic is the sweep's, so the result is bitwise the same;
+//  * every OTHER row gets g = 0 + l2*w here.  The sweep knows the batch's rows from a byte flag
+//    per row (set from the sorted slot keys before the step, cleared by the sweep as it skips
+//    the row), so it touches no row the step reads or writes and runs CONCURRENTLY with the
+//    step's tower / sparse launches on a graph side branch (no Gv/Gw gradient table at all).
+//  * the sweep keeps its OWN step counter (*sw_step + 1 = t; the last workgroup to finish
+//    advances it): the main counter is advanced by the step's own last launch while the sweep
+//    may still be running.
+__global__ void __launch_bounds__(256) stamp_rows_kernel(const int* __restrict__ keys, int n,
+                                                         int row_div, unsigned char* __restrict__ flags,
+                                                         unsigned char val) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int k = keys[i];
+  // sorted keys: one store per run (unsorted input is still correct: duplicates store alike)
+  if (i == 0 || keys[i - 1] != k) flags[k / row_div] = val;
+}
+
+template <int K, int OPT>
+__global__ void __launch_bounds__(256) tf1_sweep_kernel(
+    long R, float* __restrict__ rec, int ld, unsigned char* __restrict__ flags, OptHyper h,
+    int64_t* __restrict__ sw_step, unsigned* __restrict__ done_ctr) {
+  // record: [ v (K) | w, w_slot0, w_slot1, pad | v_slot0 (K) | v_slot1 (K) | pad ]
+  constexpr int NS = OPT == OPT_GD ? 0 : ((OPT == OPT_ADAM || OPT == OPT_FTRL) ? 2 : 1);
+  constexpr int Q = K / 4;
+  constexpr int USED = K + 4 + NS * K;   // record floats (deepfm.py table_record_floats)
+  constexpr int REC = USED <= 16 ? (USED + 15) / 16 * 16 : (USED + 31) / 32 * 32;
+  // U rows per thread per pass, all loads issued before any update: the sweep shares the chip
+  // with the step's launches, so it runs on few workgroups and needs memory-level parallelism
+  // per thread rather than more waves
+  constexpr int U = K <= 8 ? 4 : 2;
+  const float lr_t = lr_t_of<OPT>(h, sw_step);
+  const long nthr = (long)gridDim.x * blockDim.x;
+  for (long base = blockIdx.x * (long)blockDim.x + threadIdx.x; base < R; base += nthr * U) {
+    bool act[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long row = base + u * nthr;
+      act[u] = false;
+      if (row < R) {
+        if (flags[row]) flags[row] = 0;      // this step's batch row: the sparse kernel's
+        else act[u] = true;
+      }
+    }
+    f32x4 p[U][Q], a[U][Q], c[U][Q], wq[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (!act[u]) continue;
+      const float* r = rec + (size_t)(base + u * nthr) * ld;
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        p[u][q] = *reinterpret_cast<const f32x4*>(r + 4 * q);
+        if (NS >= 1) a[u][q] = *reinterpret_cast<const f32x4*>(r + K + 4 + 4 * q);
+        if (NS >= 2) c[u][q] = *reinterpret_cast<const f32x4*>(r + 2 * K + 4 + 4 * q);
+      }
+      wq[u] = *reinterpret_cast<const f32x4*>(r + K);   // {w, w_slot0, w_slot1, pad}
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (!act[u]) continue;
+      float* r = rec + (size_t)(base + u * nthr) * ld;
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        f32x4 pp = p[u][q], aa = {0, 0, 0, 0}, cc = {0, 0, 0, 0};
+        if (NS >= 1) aa = a[u][q];
+        if (NS >= 2) cc = c[u][q];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float gj = 0.f + h.l2 * pp[j];
+          float pj = pp[j], aj = aa[j], cj = cc[j];
+          opt_update<OPT>(pj, gj, aj, cj, h, lr_t);
+          pp[j] = pj; aa[j] = aj; cc[j] = cj;
+        }
+        *reinterpret_cast<f32x4*>(r + 4 * q) = pp;
+        if (NS >= 1) *reinterpret_cast<f32x4*>(r + K + 4 + 4 * q) = aa;
+        if (NS >= 2) *reinterpret_cast<f32x4*>(r + 2 * K + 4 + 4 * q) = cc;
+      }
+      f32x4 w = wq[u];
+      float pw = w[0], aw = w[1], cw = w[2];
+      float gw = 0.f + h.l2 * pw;
+      opt_update<OPT>(pw, gw, aw, cw, h, lr_t);
+      w[0] = pw;
+      if (NS >= 1) w[1] = aw;
+      if (NS >= 2) w[2] = cw;
+      *reinterpret_cast<f32x4*>(r + K) = w;
+      // the record's tail pad (always zero) is written too: whole 128-B lines leave L2 fully
+      // dirty, so their write-back needs no read-modify-write
+#pragma unroll
+      for (int q = (K + 4 + NS * K) / 4; q < REC / 4; ++q)
+        *reinterpret_cast<f32x4*>(r + 4 * q) = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned prev = atomicAdd(done_ctr, 1u);
+    if (prev == gridDim.x - 1) {
+      *sw_step += 1;
+      *done_ctr = 0u;
+    }
+  }
+}
+
 // ------------------------------------------------------------------ dense flat params
 // ShadowSeg: common.h
 
@@ -264,6 +369,43 @@ HFM_API int hfm_dense_sweep(int K, int opt, long R, float* tv, float* tw, float*
 #define CALL(KK) sweep_k<KK>(opt, R, tv, tw, Gv, Gw, s0v, s1v, s0w, s1w, *h, step, ldv, ldw, st)
   HFM_K_DISPATCH(K, CALL)
 #undef CALL
+}
+
+HFM_API int hfm_stamp_rows(const int* keys, int n, int row_div, unsigned char* flags, int val,
+                           hipStream_t st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(stamp_rows_kernel, dim3((n + 255) / 256), dim3(256), 0, st, keys, n, row_div,
+                     flags, (unsigned char)val);
+  HFM_LAUNCH_CHECK();
+}
+
+template <int K>
+static int tf1_sweep_k(int opt, long R, float* rec, int ld, unsigned char* flags, OptHyper h,
+                       int64_t* sw_step, unsigned* done_ctr, int max_wg, hipStream_t st) {
+  const int ns = opt == OPT_GD ? 0 : ((opt == OPT_ADAM || opt == OPT_FTRL) ? 2 : 1);
+  const int used = K + 4 + ns * K;
+  if (ld != (used <= 16 ? (used + 15) / 16 * 16 : (used + 31) / 32 * 32))
+    return (int)hipErrorInvalidValue;       // not the record layout the kernel writes
+  long g = (R + 255) / 256;
+  const int grid = (int)(g < max_wg ? g : max_wg);
+  if (grid == 0) return 0;
+#define CALL(O)                                                                                   \
+  hipLaunchKernelGGL((tf1_sweep_kernel<K, O>), dim3(grid), dim3(256), 0, st, R, rec, ld, flags, h, \
+                     sw_step, done_ctr)
+  HFM_OPT_DISPATCH(opt, CALL)
+#undef CALL
+  HFM_LAUNCH_CHECK();
+}
+
+HFM_API int hfm_tf1_sweep(int K, int opt, long R, float* rec, int ld, unsigned char* flags,
+                          const OptHyper* h, int64_t* sw_step, unsigned* done_ctr, int max_wg,
+                          hipStream_t st) {
+  switch (K) {
+    case 4: return tf1_sweep_k<4>(opt, R, rec, ld, flags, *h, sw_step, done_ctr, max_wg, st);
+    case 8: return tf1_sweep_k<8>(opt, R, rec, ld, flags, *h, sw_step, done_ctr, max_wg, st);
+    case 16: return tf1_sweep_k<16>(opt, R, rec, ld, flags, *h, sw_step, done_ctr, max_wg, st);
+    default: return (int)hipErrorInvalidValue;
+  }
 }
 
 HFM_API int hfm_dense_opt(int opt, float* p, const float* g, float* s0, float* s1, long n,

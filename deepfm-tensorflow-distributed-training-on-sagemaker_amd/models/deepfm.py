@@ -59,6 +59,10 @@ _SHX_FORK = os.environ.get("HIPFM_SHX_FORK", "start")
 _SH_APPLY_DENSE = os.environ.get("HIPFM_SH_APPLY_DENSE", "1") == "1"
 # ... and the dense gradient computed in the sparse launch, exchanged by all-gather (no all-reduce)
 _SH_XFUSE = os.environ.get("HIPFM_SH_XFUSE", "1") == "1"
+# tf1_dense on one GPU: split sweep concurrent with the step (0: scatter + full-table sweep)
+_TF1_SPLIT = os.environ.get("HIPFM_TF1_SPLIT", "1") == "1"
+_SWEEP_WG = int(os.environ.get("HIPFM_SWEEP_WG", "256"))   # 128: 0.178, 256: 0.160, 512: 0.179 ms
+_SWEEP_FORK = os.environ.get("HIPFM_SWEEP_FORK", "start")      # start | tower
 
 
 def check_field_ranges(ranges, F: int, V: int) -> List[Tuple[int, int]]:
@@ -260,7 +264,22 @@ class NativeDeepFM:
             for t in self.bn_mv:
                 t.fill_(1.0)
         self._alloc_slots()
-        if self.sparse_update == "tf1_dense":
+        # tf1_dense on one GPU (record layout, fused sparse kernel): the split form -- batch rows
+        # take their full update in the sparse kernel's lazy mode, every other row gets the
+        # l2-only update from a sweep that runs concurrently with the step (optim.hip
+        # tf1_sweep_kernel).  Byte flags per row per sorted-slot set mark the batch's rows.
+        self.tf1_split = (self.sparse_update == "tf1_dense" and self.record and not self.exchange and
+                          not self.sharded and
+                          _TF1_SPLIT and K in (4, 8, 16) and _SPARSE_IMPL == "fused" and
+                          _SORT_SIDE_STREAM)
+        self.lazy_rows = self.sparse_update == "lazy" or self.tf1_split   # sparse kernel mode
+        if self.tf1_split:
+            self._row_flags = [torch.zeros(self.R, dtype=torch.uint8, device=dev) for _ in range(2)]
+            self._stamp_n = [0, 0]          # keys whose flags are set in set c, not yet swept
+            self.sw_step = torch.zeros(1, dtype=torch.int64, device=dev)
+            self._sw_done = torch.zeros(1, dtype=torch.int32, device=dev)
+            self._sweep_stream = None
+        elif self.sparse_update == "tf1_dense":
             self.Gv = torch.zeros(self.R, K, **f32)
             self.Gw = torch.zeros(self.R, **f32)
         self.W16, self.WT16 = [], []
@@ -297,6 +316,7 @@ class NativeDeepFM:
         self._side_next = None
         self._next_sort_ids = None
         self._next_fm = False      # the declared next batch's ids are field-major
+        self._tf1_plan = None      # tf1_dense split sweep: (flag set, inline sort, stale keys)
         self._idx_fm = False       # the bound batch's ids (self.idx) are field-major [F, M]
         self._comm_stream = None
         self.shx = None
@@ -472,6 +492,10 @@ class NativeDeepFM:
         # sorted-slot sets: set c holds the sort of the batch this step trains, set 1 - c receives
         # the sort of the NEXT batch, computed on a side stream during this step (single GPU,
         # next batch declared by the caller); the two sets alternate step by step
+        if getattr(self, "tf1_split", False) and any(self._stamp_n):
+            for f in self._row_flags:
+                f.zero_()
+            self._stamp_n = [0, 0]
         self._ss = [(self.sorted_keys, self.perm),
                     (torch.zeros(n, **i32), torch.zeros(n, **i32))]
         self._ss_key = [None, None]
@@ -817,6 +841,9 @@ class NativeDeepFM:
             self.sfwg_done.zero_()
         if getattr(self, "shx", None) is not None:
             self.shx.reset_table()
+        if getattr(self, "tf1_split", False):
+            self.sw_step.copy_(self.step)
+            self._sw_done.zero_()
 
     def refresh_shadows(self):
         """Re-derive the bf16 / fp8 weight copies after parameters changed outside a step (load,
@@ -1029,7 +1056,7 @@ class NativeDeepFM:
         A.UG = self.UG.data_ptr()
         A.tv, A.tw = self.tv.data_ptr(), self.tw.data_ptr()
         A.s0v, A.s1v, A.s0w, A.s1w = (t.data_ptr() if t.numel() else 0 for t in self.sv)
-        if self.sparse_update == "tf1_dense":
+        if self.sparse_update == "tf1_dense" and not self.tf1_split:
             A.Gv, A.Gw = self.Gv.data_ptr(), self.Gw.data_ptr()
         A.h = self.h_sparse
         A.step = self.step.data_ptr()
@@ -1070,7 +1097,7 @@ class NativeDeepFM:
         A.ctail, A.lead, A.tinfo = self.sf_ctail.data_ptr(), self.sf_lead.data_ptr(), self.sf_tinfo.data_ptr()
         A.tv, A.tw = self.tv.data_ptr(), self.tw.data_ptr()
         A.s0v, A.s1v, A.s0w, A.s1w = (t.data_ptr() if t.numel() else 0 for t in self.sv)
-        if self.sparse_update == "tf1_dense":
+        if self.sparse_update == "tf1_dense" and not self.tf1_split:
             A.Gv, A.Gw = self.Gv.data_ptr(), self.Gw.data_ptr()
         A.h = self.h_sparse
         A.step = self.step.data_ptr()
@@ -1096,16 +1123,16 @@ class NativeDeepFM:
             KN.sparse_wgfin(self.K, self.opt_id, self.sf_args(n), self._wgfin_args(True), self.sfwg_done)
             return None
         if not self.exchange and _SPARSE_IMPL == "fused":
-            KN.sparse_fused(self.K, KN.SF_LAZY if self.sparse_update == "lazy" else KN.SF_SCATTER,
+            KN.sparse_fused(self.K, KN.SF_LAZY if self.lazy_rows else KN.SF_SCATTER,
                             self.opt_id, self.sf_args(n))
-            if self.sparse_update != "lazy":
+            if not self.lazy_rows:
                 KN.dense_sweep(self.K, self.opt_id, self.R, self.tv, self.tw, self.Gv, self.Gw,
                                self.sv, self.h_sparse, self.step)
             return None
         if not self.exchange:
             self._segment_reduce(n, compact=False)
             A = self.seg_args(n, compact=False)
-            if self.sparse_update == "lazy":
+            if self.lazy_rows:
                 KN.seg_apply(self.K, KN.SEG_LAZY, self.opt_id, A, n)
             else:
                 KN.seg_apply(self.K, KN.SEG_SCATTER, 0, A, n)
@@ -1160,9 +1187,13 @@ class NativeDeepFM:
             nk_ids, nk_B, nk_fm = self._next_sort_ids, plan[2][1], self._next_fm
             nxt_keys, nxt_perm = self._ss[1 - plan[0]]
 
+            tf1_next = self._row_flags[1 - plan[0]] if self.tf1_split else None
+
             def sort_next():
                 with torch.cuda.stream(self._side_next):
                     self._fsort_next(nk_ids, nk_B, nxt_keys, nxt_perm, field_major=nk_fm)
+                    if tf1_next is not None:
+                        KN.stamp_rows(nxt_keys, nk_B * self.F, self.row_div, tf1_next, 1)
             # enqueued right after the tower (graph branches are dispatched in capture order);
             # same-box sweep of the enqueue point: after the tower 0.1318, after the dense
             # gradients 0.1316, at the end 0.1351, at the start 0.1365 ms/step.  (Letting the
@@ -1171,6 +1202,18 @@ class NativeDeepFM:
             after_fm = sort_next
         if not inline:
             presorted = True            # sorted during the previous step
+            if self._tf1_plan is not None:
+                first_cb = after_fm
+                cset = self._tf1_plan[0]
+                if _SWEEP_FORK == "start":
+                    # a root branch like the next batch's sort: depends only on the step start;
+                    # its kernel is enqueued after the tower (branches launch in capture order)
+                    self._sweep_src().wait_stream(main)
+
+                def after_fm():
+                    if first_cb is not None:
+                        first_cb()
+                    self._fork_sweep(None if _SWEEP_FORK == "start" else main, cset)
         elif not self.sharded and _SORT_SIDE_STREAM:
             if self._side is None:
                 self._side = torch.cuda.Stream(self.device)
@@ -1181,13 +1224,24 @@ class NativeDeepFM:
                    KN.fm_fwd_writes_idsT(self.F, self.K))
             self._idsT_B = B if pre else 0
 
+            tfp = self._tf1_plan
+
             def fork_sort():
                 self._side.wait_stream(main)
                 with torch.cuda.stream(self._side):
+                    if tfp is not None and tfp[2]:
+                        # flags a discarded prefetch set from the keys still in this set
+                        KN.stamp_rows(self.sorted_keys, tfp[2], self.row_div,
+                                      self._row_flags[tfp[0]], 0)
                     if pre:
                         self._fsort.sort_pre(B, self.sorted_keys, self.perm)
                     else:
                         self._sort_slots(B)
+                    if tfp is not None:
+                        KN.stamp_rows(self.sorted_keys, B * self.F, self.row_div,
+                                      self._row_flags[tfp[0]], 1)
+                if tfp is not None:
+                    self._fork_sweep(self._side, tfp[0])
             # graph branches launch in capture order: forking after fm_fwd is enqueued lets the
             # step's first kernel start at once instead of after the sort's launches
             # (same-box A/B: 0.160 -> 0.154 ms/step, bitwise-identical results)
@@ -1218,7 +1272,7 @@ class NativeDeepFM:
         # it advances the step counter, and the sparse kernels are told so (SfArgs.step_off).
         # With the fused tower it rides on the finalize launch itself (one kernel boundary less)
         self._dense_early = (presorted and not self.exchange and not split and _DENSE_EARLY and
-                             self.sparse_update == "lazy" and _SPARSE_IMPL == "fused")
+                             self.lazy_rows and _SPARSE_IMPL == "fused")
         self._fuse_opt = (self._dense_early and self.fused and _FUSE_FIN_OPT and self._fin_covers_all)
         # ... and with wgfin, that whole dense-gradient launch rides inside the sparse backward's
         # launch instead (sfwg: independent work, both latency-bound)
@@ -1285,11 +1339,28 @@ class NativeDeepFM:
                 KN.w8_quant(self._w8_jobs, len(self.layers), self._w8_rows)
         elif not self._dense_early:
             self._dense_opt()
+        if self._tf1_plan is not None:
+            main.wait_stream(self._sweep_stream)
         if prefetch:
             # joined at the end of the step: deferring the join to the next step's sparse
             # backward (so no cross-branch edge precedes the next tower) measured 0.155-0.186
             # vs 0.121 ms/step in a 16-step graph -- the branch then lands in the towers' path
             main.wait_stream(self._side_next)
+
+    def _sweep_src(self):
+        if self._sweep_stream is None:
+            prio = int(os.environ.get("HIPFM_SWEEP_PRIO", "0"))
+            self._sweep_stream = torch.cuda.Stream(self.device, priority=prio)
+        return self._sweep_stream
+
+    def _fork_sweep(self, src, c: int):
+        """tf1_dense split form: the l2-only update of every row outside this step's batch, on its
+        own graph branch (forked from ``src`` once set c's flags are written; joined at the end)."""
+        if src is not None:
+            self._sweep_src().wait_stream(src)
+        with torch.cuda.stream(self._sweep_stream):
+            KN.tf1_sweep(self.K, self.opt_id, self.rec, self._row_flags[c], self.h_sparse,
+                         self.sw_step, self._sw_done, max_wg=_SWEEP_WG)
 
     def _sh_dense_args(self):
         from ..ops._lib import ShDenseArgs
@@ -1386,6 +1457,14 @@ class NativeDeepFM:
                 self._next_fm = nxt_fm
             self._sort_plan = (c, inline, nk)
             key = key + ("sort",) + self._sort_plan
+        self._tf1_plan = None
+        if self.tf1_split:
+            # flags of set c: this batch's rows (prefetched: set during the previous step); an
+            # inline sort first clears flags a discarded prefetch left in set c
+            c = self._sort_plan[0] if self._sort_plan is not None else self._ss_cur
+            inline = self._sort_plan is None or self._sort_plan[1]
+            self._tf1_plan = (c, inline, self._stamp_n[c] if inline else 0)
+            key = key + ("tf1",) + self._tf1_plan
         if self.shx is not None:
             nxt = self._flat_ids(next_ids, nxt_fm) if (nxt_ok and _SHARD_PIPELINE) else None
             self._shx_plan = self.shx.plan(self.idx, B, nxt, resident=direct)
@@ -1395,6 +1474,13 @@ class NativeDeepFM:
         return B, direct, key
 
     def _commit_step(self, B: int, direct: bool):
+        if self._tf1_plan is not None:
+            c = self._tf1_plan[0]
+            self._stamp_n[c] = 0                       # swept (flags cleared) by this step
+            nk = self._sort_plan[2] if self._sort_plan is not None else None
+            if nk is not None:
+                self._stamp_n[1 - c] = nk[1] * self.F  # set by this step's prefetched sort
+            self._tf1_plan = None
         if self.shx is not None:
             self.shx.commit(self._shx_plan, self.idx, B, resident=direct)
             self._shx_plan = None
@@ -1409,10 +1495,12 @@ class NativeDeepFM:
 
     def _plan_state(self):
         sh = None if self.shx is None else (self.shx.cur, [(rs.key, rs.ahead) for rs in self.shx.sets])
-        return self._ss_cur, list(self._ss_key), sh
+        return self._ss_cur, list(self._ss_key), sh, list(getattr(self, "_stamp_n", []))
 
     def _set_plan_state(self, st):
         self._ss_cur, self._ss_key = st[0], list(st[1])
+        if self.tf1_split:
+            self._stamp_n = list(st[3])
         if st[2] is not None:
             self.shx.cur = st[2][0]
             for rs, (k, a) in zip(self.shx.sets, st[2][1]):

@@ -179,7 +179,10 @@ _SIGS = {
     "hfm_scatter_rows": [c_int] + [c_void_p] * 3 + [c_int, c_int, c_void_p, c_void_p, c_void_p],
     "hfm_dense_sweep": [c_int, c_int, c_long] + [c_void_p] * 8 + [C.POINTER(OptHyper), c_void_p, c_long,
                                                                   c_long, c_void_p],
-    "hfm_dense_opt": [c_int] + [c_void_p] * 4 + [c_long, C.POINTER(OptHyper), c_void_p, c_void_p, c_int,
+    "hfm_stamp_rows": [c_void_p, c_int, c_int, c_void_p, c_int, c_void_p],
+    "hfm_tf1_sweep": [c_int, c_int, c_long, c_void_p, c_int, c_void_p, C.POINTER(OptHyper), c_void_p,
+                      c_void_p, c_int, c_void_p],
+    "hfm_dense_opt": [c_int] + [c_void_p] * 4+ [c_long, C.POINTER(OptHyper), c_void_p, c_void_p, c_int,
                                                  c_void_p, c_void_p],
     "hfm_finalize": [c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p],
     "hfm_finalize_opt": [c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_int] + [c_void_p] * 4

@@ -300,6 +300,23 @@ def dense_sweep(K, opt, R, tv, tw, Gv, Gw, slots, h: OptHyper, step):
           "dense_sweep")
 
 
+def stamp_rows(keys, n, row_div, flags, val):
+    """flags[key // row_div] = val for the first n (sorted) slot keys (tf1_dense split sweep)."""
+    assert keys.dtype == torch.int32 and flags.dtype == torch.uint8 and keys.numel() >= n
+    check(L().hfm_stamp_rows(ptr(keys), n, row_div, ptr(flags), val, stream_handle()), "stamp_rows")
+
+
+def tf1_sweep(K, opt, rec, flags, h: OptHyper, sw_step, done_ctr, max_wg=2048):
+    """TF1 dense-Adam (etc.) update with g = l2*w of every record row whose flag is 0; flagged
+    rows (this step's batch, updated by the sparse kernel) are skipped and their flag cleared.
+    The last workgroup advances ``sw_step`` (the sweep's own int64 step counter)."""
+    R, ld = rec.shape
+    assert rec.dtype == torch.float32 and rec.is_contiguous() and flags.numel() >= R
+    assert sw_step.dtype == torch.int64 and done_ctr.dtype == torch.int32
+    check(L().hfm_tf1_sweep(K, opt, R, ptr(rec), ld, ptr(flags), C.byref(h), ptr(sw_step),
+                            ptr(done_ctr), max_wg, stream_handle()), "tf1_sweep")
+
+
 def dense_opt(opt, p, g, s0, s1, n, h: OptHyper, step, segs_dev, nseg, done_ctr=None):
     """Fused dense optimizer + bf16 shadow refresh; with ``done_ctr`` (an int32 device word,
     zero-initialised) the last block also advances ``step`` (no separate step_inc launch)."""
