@@ -14,6 +14,7 @@
 // The optimizer step t is read from device memory (t = *step + 1), so one captured HIP graph
 // replays correctly for every step.
 #include "common.h"
+#include "tf1_sweep.h"
 
 template <int K>
 struct alignas(16) GradRowO {
@@ -157,76 +158,12 @@ template <int K, int OPT>
 __global__ void __launch_bounds__(256) tf1_sweep_kernel(
     long R, float* __restrict__ rec, int ld, unsigned char* __restrict__ flags, OptHyper h,
     int64_t* __restrict__ sw_step, unsigned* __restrict__ done_ctr) {
-  // record: [ v (K) | w, w_slot0, w_slot1, pad | v_slot0 (K) | v_slot1 (K) | pad ]
-  constexpr int NS = OPT == OPT_GD ? 0 : ((OPT == OPT_ADAM || OPT == OPT_FTRL) ? 2 : 1);
-  constexpr int Q = K / 4;
-  constexpr int USED = K + 4 + NS * K;   // record floats (deepfm.py table_record_floats)
-  constexpr int REC = USED <= 16 ? (USED + 15) / 16 * 16 : (USED + 31) / 32 * 32;
-  // U rows per thread per pass, all loads issued before any update: the sweep shares the chip
-  // with the step's launches, so it runs on few workgroups and needs memory-level parallelism
-  // per thread rather than more waves
-  constexpr int U = K <= 8 ? 4 : 2;
-  const float lr_t = lr_t_of<OPT>(h, sw_step);
-  const long nthr = (long)gridDim.x * blockDim.x;
-  for (long base = blockIdx.x * (long)blockDim.x + threadIdx.x; base < R; base += nthr * U) {
-    bool act[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const long row = base + u * nthr;
-      act[u] = false;
-      if (row < R) {
-        if (flags[row]) flags[row] = 0;      // this step's batch row: the sparse kernel's
-        else act[u] = true;
-      }
-    }
-    f32x4 p[U][Q], a[U][Q], c[U][Q], wq[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (!act[u]) continue;
-      const float* r = rec + (size_t)(base + u * nthr) * ld;
-#pragma unroll
-      for (int q = 0; q < Q; ++q) {
-        p[u][q] = *reinterpret_cast<const f32x4*>(r + 4 * q);
-        if (NS >= 1) a[u][q] = *reinterpret_cast<const f32x4*>(r + K + 4 + 4 * q);
-        if (NS >= 2) c[u][q] = *reinterpret_cast<const f32x4*>(r + 2 * K + 4 + 4 * q);
-      }
-      wq[u] = *reinterpret_cast<const f32x4*>(r + K);   // {w, w_slot0, w_slot1, pad}
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (!act[u]) continue;
-      float* r = rec + (size_t)(base + u * nthr) * ld;
-#pragma unroll
-      for (int q = 0; q < Q; ++q) {
-        f32x4 pp = p[u][q], aa = {0, 0, 0, 0}, cc = {0, 0, 0, 0};
-        if (NS >= 1) aa = a[u][q];
-        if (NS >= 2) cc = c[u][q];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          float gj = 0.f + h.l2 * pp[j];
-          float pj = pp[j], aj = aa[j], cj = cc[j];
-          opt_update<OPT>(pj, gj, aj, cj, h, lr_t);
-          pp[j] = pj; aa[j] = aj; cc[j] = cj;
-        }
-        *reinterpret_cast<f32x4*>(r + 4 * q) = pp;
-        if (NS >= 1) *reinterpret_cast<f32x4*>(r + K + 4 + 4 * q) = aa;
-        if (NS >= 2) *reinterpret_cast<f32x4*>(r + 2 * K + 4 + 4 * q) = cc;
-      }
-      f32x4 w = wq[u];
-      float pw = w[0], aw = w[1], cw = w[2];
-      float gw = 0.f + h.l2 * pw;
-      opt_update<OPT>(pw, gw, aw, cw, h, lr_t);
-      w[0] = pw;
-      if (NS >= 1) w[1] = aw;
-      if (NS >= 2) w[2] = cw;
-      *reinterpret_cast<f32x4*>(r + K) = w;
-      // the record's tail pad (always zero) is written too: whole 128-B lines leave L2 fully
-      // dirty, so their write-back needs no read-modify-write
-#pragma unroll
-      for (int q = (K + 4 + NS * K) / 4; q < REC / 4; ++q)
-        *reinterpret_cast<f32x4*>(r + 4 * q) = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-  }
+  // U rows per thread per pass, all loads issued before any update: on its own graph branch the
+  // sweep shares the chip with the step's launches, so it runs on few workgroups and needs
+  // memory-level parallelism per thread rather than more waves
+  tf1_sweep_rows<K, OPT, K <= 8 ? 4 : 2>(rec, ld, R, flags, h, lr_t_of<OPT>(h, sw_step),
+                                         blockIdx.x * (long)blockDim.x + threadIdx.x,
+                                         (long)gridDim.x * blockDim.x);
   __syncthreads();
   if (threadIdx.x == 0) {
     const unsigned prev = atomicAdd(done_ctr, 1u);

@@ -388,6 +388,7 @@ __global__ void __launch_bounds__(256) sf_tile_kernel(SfArgs A) {
 // arrival (any grid size: it resets the counter) advances it, so both halves use this step's
 // index (sparse: step_off = 1; wgfin: *step + 1).
 #include "wgfin.h"
+#include "tf1_sweep.h"
 
 // the wgfin half's register footprint must not cut the sparse tiles' occupancy (6 waves / SIMD)
 constexpr int SFWG_PF = 2;
@@ -403,32 +404,56 @@ union SfwgSmem {
 };
 
 // (4 waves / SIMD for K = 8; forcing 6 spills 22 VGPRs and measured slower: 0.1139 vs 0.1110 ms)
-template <int K, int OPT>
-__global__ void __launch_bounds__(256) sfwg_kernel(SfArgs A, WgFinArgs W, unsigned* done) {
+// SWEEP (tf1_dense split form): S.nblk more workgroups, dispatched after the sparse tiles, give
+// every row outside the batch its l2-only update (tf1_sweep.h) -- disjoint rows, same step t
+template <int K, int OPT, bool SWEEP>
+__global__ void __launch_bounds__(256) sfwg_kernel(SfArgs A, WgFinArgs W, unsigned* done, SweepArgs S) {
   __shared__ SfwgSmem<K> sm;
   const int nw = W.tile_wgs + 1;
-  if ((int)blockIdx.x < nw) wgfin_body<OPT, SFWG_PF, SFWG_MAXNS, SFWG_TQ>(W, blockIdx.x, sm.wg);
-  else sf_tile_body<K, 0, OPT>(A, (int)blockIdx.x - nw, sm.sf);
+  const int ntile = (A.n + SfCfg<K>::TP - 1) / SfCfg<K>::TP;
+  if ((int)blockIdx.x < nw) {
+    wgfin_body<OPT, SFWG_PF, SFWG_MAXNS, SFWG_TQ>(W, blockIdx.x, sm.wg);
+  } else if (!SWEEP || (int)blockIdx.x < nw + ntile) {
+    sf_tile_body<K, 0, OPT>(A, (int)blockIdx.x - nw, sm.sf);
+  } else if (SWEEP) {
+    const int sb = (int)blockIdx.x - nw - ntile;
+    tf1_sweep_rows<K, OPT, 1>(S.rec, S.ld, S.R, S.flags, A.h, sf_lr_t<OPT>(A),
+                              (long)sb * blockDim.x + threadIdx.x, (long)S.nblk * blockDim.x);
+  }
   __syncthreads();
   if (threadIdx.x == 0) {
     const unsigned prev = __hip_atomic_fetch_add(done, 1u, HFM_RLX_AGENT);
     if (prev == gridDim.x - 1) {
       __hip_atomic_store(done, 0u, HFM_RLX_AGENT);
-      *W.o.step += 1;
+      const int64_t t = *W.o.step + 1;
+      *W.o.step = t;
+      if (SWEEP) *S.sw_step = t;      // keeps the branch sweep's counter in step
     }
   }
 }
 
+template <int K, int OPT>
+static void sfwg_launch(const SfArgs& A, const WgFinArgs& W, unsigned* done, const SweepArgs& S,
+                        hipStream_t st) {
+  const dim3 g(W.tile_wgs + 1 + (A.n + SfCfg<K>::TP - 1) / SfCfg<K>::TP + S.nblk), blk(256);
+  if constexpr (K <= 16) {
+    if (S.nblk) {
+      hipLaunchKernelGGL((sfwg_kernel<K, OPT, true>), g, blk, 0, st, A, W, done, S);
+      return;
+    }
+  }
+  hipLaunchKernelGGL((sfwg_kernel<K, OPT, false>), g, blk, 0, st, A, W, done, S);
+}
+
 template <int K>
-static int sfwg_dispatch(int opt, const SfArgs& A, const WgFinArgs& W, unsigned* done, hipStream_t st) {
-  using T = SfCfg<K>;
-  const dim3 g(W.tile_wgs + 1 + (A.n + T::TP - 1) / T::TP), blk(256);
+static int sfwg_dispatch(int opt, const SfArgs& A, const WgFinArgs& W, unsigned* done,
+                         const SweepArgs& S, hipStream_t st) {
   switch (opt) {
-    case OPT_ADAM: hipLaunchKernelGGL((sfwg_kernel<K, OPT_ADAM>), g, blk, 0, st, A, W, done); break;
-    case OPT_ADAGRAD: hipLaunchKernelGGL((sfwg_kernel<K, OPT_ADAGRAD>), g, blk, 0, st, A, W, done); break;
-    case OPT_MOMENTUM: hipLaunchKernelGGL((sfwg_kernel<K, OPT_MOMENTUM>), g, blk, 0, st, A, W, done); break;
-    case OPT_FTRL: hipLaunchKernelGGL((sfwg_kernel<K, OPT_FTRL>), g, blk, 0, st, A, W, done); break;
-    case OPT_GD: hipLaunchKernelGGL((sfwg_kernel<K, OPT_GD>), g, blk, 0, st, A, W, done); break;
+    case OPT_ADAM: sfwg_launch<K, OPT_ADAM>(A, W, done, S, st); break;
+    case OPT_ADAGRAD: sfwg_launch<K, OPT_ADAGRAD>(A, W, done, S, st); break;
+    case OPT_MOMENTUM: sfwg_launch<K, OPT_MOMENTUM>(A, W, done, S, st); break;
+    case OPT_FTRL: sfwg_launch<K, OPT_FTRL>(A, W, done, S, st); break;
+    case OPT_GD: sfwg_launch<K, OPT_GD>(A, W, done, S, st); break;
     default: return (int)hipErrorInvalidValue;
   }
   return 0;
@@ -466,18 +491,27 @@ HFM_API int hfm_sparse_wgfin_x(int K, const SfArgs* A, const WgFinArgs* W, hipSt
 // lazy sparse rows (optimizer `opt`) + wgfin with the same dense optimizer; `done`: [1] arrival
 // counter, zero between launches.  A.step_off must be 1 (the step advances at the launch's end).
 HFM_API int hfm_sparse_wgfin(int K, int opt, const SfArgs* A, const WgFinArgs* W, unsigned* done,
-                             hipStream_t st) {
+                             const SweepArgs* sweep, hipStream_t st) {
+  SweepArgs S{};
+  if (sweep && sweep->nblk > 0) {
+    const int ns = opt == OPT_GD ? 0 : ((opt == OPT_ADAM || opt == OPT_FTRL) ? 2 : 1);
+    const int used = K + 4 + ns * K;
+    if (K > 16 || !sweep->rec || !sweep->flags || !sweep->sw_step || sweep->R <= 0 ||
+        sweep->ld != (used <= 16 ? (used + 15) / 16 * 16 : (used + 31) / 32 * 32))
+      return (int)hipErrorInvalidValue;
+    S = *sweep;
+  }
   if (A->n <= 0 || !A->flags || !A->sync || !done || A->step_off != 1 || !W->opt_on || W->ns < 1 ||
       W->ns > SFWG_MAXNS || W->kchunk % 32 || W->ldk != W->ns * 4 * W->kchunk || W->L + 2 > WGF_MAXC ||
       !W->tile_ctr || (const void*)W->o.step != (const void*)A->step)
     return (int)hipErrorInvalidValue;
   int rc;
   switch (K) {
-    case 4: rc = sfwg_dispatch<4>(opt, *A, *W, done, st); break;
-    case 8: rc = sfwg_dispatch<8>(opt, *A, *W, done, st); break;
-    case 16: rc = sfwg_dispatch<16>(opt, *A, *W, done, st); break;
-    case 32: rc = sfwg_dispatch<32>(opt, *A, *W, done, st); break;
-    case 64: rc = sfwg_dispatch<64>(opt, *A, *W, done, st); break;
+    case 4: rc = sfwg_dispatch<4>(opt, *A, *W, done, S, st); break;
+    case 8: rc = sfwg_dispatch<8>(opt, *A, *W, done, S, st); break;
+    case 16: rc = sfwg_dispatch<16>(opt, *A, *W, done, S, st); break;
+    case 32: rc = sfwg_dispatch<32>(opt, *A, *W, done, S, st); break;
+    case 64: rc = sfwg_dispatch<64>(opt, *A, *W, done, S, st); break;
     default: return (int)hipErrorInvalidValue;
   }
   if (rc) return rc;

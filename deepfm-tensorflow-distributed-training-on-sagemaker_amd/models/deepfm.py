@@ -61,8 +61,9 @@ _SH_APPLY_DENSE = os.environ.get("HIPFM_SH_APPLY_DENSE", "1") == "1"
 _SH_XFUSE = os.environ.get("HIPFM_SH_XFUSE", "1") == "1"
 # tf1_dense on one GPU: split sweep concurrent with the step (0: scatter + full-table sweep)
 _TF1_SPLIT = os.environ.get("HIPFM_TF1_SPLIT", "1") == "1"
+_SWEEP_MODE = os.environ.get("HIPFM_SWEEP_MODE", "merged")      # merged | branch
+_SWEEP_MBLK = int(os.environ.get("HIPFM_SWEEP_MBLK", "512"))     # sweep workgroups, merged mode
 _SWEEP_WG = int(os.environ.get("HIPFM_SWEEP_WG", "256"))   # 128: 0.178, 256: 0.160, 512: 0.179 ms
-_SWEEP_FORK = os.environ.get("HIPFM_SWEEP_FORK", "start")      # start | tower
 
 
 def check_field_ranges(ranges, F: int, V: int) -> List[Tuple[int, int]]:
@@ -324,6 +325,7 @@ class NativeDeepFM:
         self._next_sort_ids = None
         self._next_fm = False      # the declared next batch's ids are field-major
         self._tf1_plan = None      # tf1_dense split sweep: (flag set, inline sort, stale keys)
+        self._tf1_merged = False
         self._idx_fm = False       # the bound batch's ids (self.idx) are field-major [F, M]
         self._comm_stream = None
         self.shx = None
@@ -1129,7 +1131,8 @@ class NativeDeepFM:
         if not presorted:
             self._sort_slots(B)
         if self._sfwg_now:
-            KN.sparse_wgfin(self.K, self.opt_id, self.sf_args(n), self._wgfin_args(True), self.sfwg_done)
+            KN.sparse_wgfin(self.K, self.opt_id, self.sf_args(n), self._wgfin_args(True), self.sfwg_done,
+                            sweep=self._sweep_args() if self._tf1_merged else None)
             return None
         if not self.exchange and _SPARSE_IMPL == "fused":
             KN.sparse_fused(self.K, KN.SF_LAZY if self.lazy_rows else KN.SF_SCATTER,
@@ -1178,6 +1181,10 @@ class NativeDeepFM:
         sort depends only on the batch, so it runs on a side stream concurrently with the
         forward / tower backward (a parallel branch of the captured graph)."""
         presorted = False
+        # tf1_dense split sweep inside the merged sparse launch (needs the single-GPU sfwg path,
+        # which the split form always takes: its sort is always presorted on a side stream)
+        self._tf1_merged = (self._tf1_plan is not None and _SWEEP_MODE == "merged" and
+                            self._sfwg_possible())
         if self.shx is not None:
             self._shx_start(B)
         after_fm = self.shx.fork_next if (self.shx is not None and _SHX_FORK == "tower") else None
@@ -1211,18 +1218,18 @@ class NativeDeepFM:
             after_fm = sort_next
         if not inline:
             presorted = True            # sorted during the previous step
-            if self._tf1_plan is not None:
+            if self._tf1_plan is not None and not self._tf1_merged:
                 first_cb = after_fm
                 cset = self._tf1_plan[0]
-                if _SWEEP_FORK == "start":
-                    # a root branch like the next batch's sort: depends only on the step start;
-                    # its kernel is enqueued after the tower (branches launch in capture order)
-                    self._sweep_src().wait_stream(main)
+                # a root branch like the next batch's sort: depends only on the step start; its
+                # kernel is enqueued after the tower (branches launch in capture order).  Forked
+                # after the tower instead, the graph ran every kernel serially: 0.227 vs 0.160 ms
+                self._sweep_src().wait_stream(main)
 
                 def after_fm():
                     if first_cb is not None:
                         first_cb()
-                    self._fork_sweep(None if _SWEEP_FORK == "start" else main, cset)
+                    self._fork_sweep(None, cset)
         elif not self.sharded and _SORT_SIDE_STREAM:
             if self._side is None:
                 self._side = torch.cuda.Stream(self.device)
@@ -1249,7 +1256,7 @@ class NativeDeepFM:
                     if tfp is not None:
                         KN.stamp_rows(self.sorted_keys, B * self.F, self.row_div,
                                       self._row_flags[tfp[0]], 1)
-                if tfp is not None:
+                if tfp is not None and not self._tf1_merged:
                     self._fork_sweep(self._side, tfp[0])
             # graph branches launch in capture order: forking after fm_fwd is enqueued lets the
             # step's first kernel start at once instead of after the sort's launches
@@ -1285,8 +1292,9 @@ class NativeDeepFM:
         self._fuse_opt = (self._dense_early and self.fused and _FUSE_FIN_OPT and self._fin_covers_all)
         # ... and with wgfin, that whole dense-gradient launch rides inside the sparse backward's
         # launch instead (sfwg: independent work, both latency-bound)
-        self._sfwg_now = (self._fuse_opt and _WGFIN and _SFWG and getattr(self, "_wgfin_ns", 1 << 30) <= KN.SFWG_MAX_NS and
-                          self.shx is None and not self.sharded)
+        self._sfwg_now = self._fuse_opt and self._sfwg_possible()
+        if self._tf1_merged and not self._sfwg_now:
+            raise RuntimeError("tf1_dense merged sweep planned but the step took another path")
         try:
             idx, tv = self._dense_fwd_bwd(B, defer_wgrad=split or self._sfwg_now or xfuse,
                                           after_fm=after_fm)
@@ -1348,7 +1356,7 @@ class NativeDeepFM:
                 KN.w8_quant(self._w8_jobs, len(self.layers), self._w8_rows)
         elif not self._dense_early:
             self._dense_opt()
-        if self._tf1_plan is not None:
+        if self._tf1_plan is not None and not self._tf1_merged:
             main.wait_stream(self._sweep_stream)
         if prefetch:
             # joined at the end of the step: deferring the join to the next step's sparse
@@ -1356,10 +1364,24 @@ class NativeDeepFM:
             # vs 0.121 ms/step in a 16-step graph -- the branch then lands in the towers' path
             main.wait_stream(self._side_next)
 
+    def _sfwg_possible(self) -> bool:
+        """The sparse backward + wgfin merged launch applies (given the fused dense optimizer)."""
+        return (_WGFIN and _SFWG and getattr(self, "_wgfin_ns", 1 << 30) <= KN.SFWG_MAX_NS and
+                self.shx is None and not self.sharded and self.fused and _FUSE_FIN_OPT and
+                self._fin_covers_all and not self.exchange and _DENSE_EARLY and self.lazy_rows and
+                _SPARSE_IMPL == "fused" and _DENSE_SIDE_STREAM != "1")
+
+    def _sweep_args(self):
+        from ..ops._lib import SweepArgs
+        S = SweepArgs()
+        S.rec, S.flags = self.rec.data_ptr(), self._row_flags[self._tf1_plan[0]].data_ptr()
+        S.sw_step, S.R, S.ld, S.nblk = self.sw_step.data_ptr(), self.R, self.rec.shape[1], _SWEEP_MBLK
+        return S
+
     def _sweep_src(self):
         if self._sweep_stream is None:
-            prio = int(os.environ.get("HIPFM_SWEEP_PRIO", "0"))
-            self._sweep_stream = torch.cuda.Stream(self.device, priority=prio)
+            # (a low-priority stream measured no better: 0.170 vs 0.160 ms)
+            self._sweep_stream = torch.cuda.Stream(self.device)
         return self._sweep_stream
 
     def _fork_sweep(self, src, c: int):

@@ -99,6 +99,12 @@ class SegApplyArgs(C.Structure):
                 ("step", c_void_p), ("ldv", c_long), ("ldw", c_long)]
 
 
+class SweepArgs(C.Structure):
+    """tf1_sweep.h SweepArgs: the sweep workgroups of the merged sparse launch (nblk 0: none)."""
+    _fields_ = [("rec", c_void_p), ("flags", c_void_p), ("sw_step", c_void_p), ("R", c_long),
+                ("ld", c_int), ("nblk", c_int)]
+
+
 class SfArgs(C.Structure):
     _fields_ = [("sorted_keys", c_void_p), ("perm", c_void_p), ("vals", c_void_p), ("dlogit", c_void_p),
                 ("dX0", c_void_p), ("S", c_void_p), ("n", c_int), ("F", c_int), ("KP", c_int),
@@ -242,7 +248,7 @@ _SIGS = {
     "hfm_bn": [c_int, C.POINTER(BnArgs), c_void_p],
     "hfm_tower": [C.POINTER(TowerArgs), c_int, c_void_p],
     "hfm_wgfin": [c_int, C.POINTER(WgFinArgs), c_void_p],
-    "hfm_sparse_wgfin": [c_int, c_int, c_void_p, C.POINTER(WgFinArgs), c_void_p, c_void_p],
+    "hfm_sparse_wgfin": [c_int, c_int, c_void_p, C.POINTER(WgFinArgs), c_void_p, c_void_p, c_void_p],
     "hfm_sparse_wgfin_x": [c_int, c_void_p, C.POINTER(WgFinArgs), c_void_p],
     "hfm_wgfin_job_bytes": [],
     "hfm_wgfin_args_bytes": [],

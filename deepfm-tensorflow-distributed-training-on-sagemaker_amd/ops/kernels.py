@@ -265,11 +265,14 @@ def sparse_wgfin_x(K, args: SfArgs, wf: "WgFinArgs"):
     check(L().hfm_sparse_wgfin_x(K, C.byref(args), C.byref(wf), stream_handle()), "sparse_wgfin_x")
 
 
-def sparse_wgfin(K, opt, args: SfArgs, wf: "WgFinArgs", done):
+def sparse_wgfin(K, opt, args: SfArgs, wf: "WgFinArgs", done, sweep=None):
     """Lazy sparse backward + the fused tower's wgfin work (weight gradients, split-K combine,
     dense optimizer) in ONE launch (sparse_fused.hip sfwg_kernel); ``done``: int32 [1] arrival
-    counter (zero between launches); the launch advances the step counter."""
-    check(L().hfm_sparse_wgfin(K, opt, C.byref(args), C.byref(wf), ptr(done), stream_handle()),
+    counter (zero between launches); the launch advances the step counter.  ``sweep``
+    (``_lib.SweepArgs``, tf1_dense split form): extra workgroups give every row outside the batch
+    its l2-only update."""
+    check(L().hfm_sparse_wgfin(K, opt, C.byref(args), C.byref(wf), ptr(done),
+                               C.byref(sweep) if sweep is not None else None, stream_handle()),
           "sparse_wgfin")
 
 

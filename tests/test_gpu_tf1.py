@@ -45,9 +45,13 @@ def _assert_same(a, b):
     a.check_errors()
 
 
-@pytest.mark.parametrize("opt,K", [("Adam", 8), ("Adagrad", 16), ("Momentum", 4), ("ftrl", 8),
-                                   ("GD", 8)])
-def test_tf1_split_equals_scatter_sweep(opt, K):
+@pytest.mark.parametrize("opt,K,mode", [("Adam", 8, "merged"), ("Adam", 8, "branch"),
+                                        ("Adagrad", 16, "merged"), ("Momentum", 4, "branch"),
+                                        ("ftrl", 8, "merged"), ("GD", 8, "merged")])
+def test_tf1_split_equals_scatter_sweep(opt, K, mode, monkeypatch):
+    """merged: the sweep runs as extra workgroups of the sparse + wgfin launch; branch: as its own
+    kernel on a graph branch concurrent with the whole step."""
+    monkeypatch.setattr(dm, "_SWEEP_MODE", mode)
     synth = make_synth("criteo_kaggle")
     B = 2048
     a, b = _pair(opt, K, synth.feature_size, synth.field_ranges(), B)
@@ -74,6 +78,7 @@ def test_tf1_split_equals_scatter_sweep(opt, K):
         a.train_step(*pool[i], use_graph=True, next_ids=pool[i + 1][0])
         b.train_step(*pool[i], use_graph=True, next_ids=pool[i + 1][0])
     _assert_same(a, b)
+    assert a._sfwg_step and a._tf1_merged == (mode == "merged")
     # every row moved (non-lazy semantics): rows never in a batch changed too
     seen = torch.zeros(a.R, dtype=torch.bool, device=DEV)
     for ids, _, _ in pool:
