@@ -62,7 +62,7 @@ _SH_XFUSE = os.environ.get("HIPFM_SH_XFUSE", "1") == "1"
 # tf1_dense on one GPU: split sweep concurrent with the step (0: scatter + full-table sweep)
 _TF1_SPLIT = os.environ.get("HIPFM_TF1_SPLIT", "1") == "1"
 _SWEEP_MODE = os.environ.get("HIPFM_SWEEP_MODE", "merged")      # merged | branch
-_SWEEP_MBLK = int(os.environ.get("HIPFM_SWEEP_MBLK", "512"))     # sweep workgroups, merged mode
+_SWEEP_MBLK = int(os.environ.get("HIPFM_SWEEP_MBLK", "2048"))  # merged-mode sweep workgroups: 512 0.191, 1024 0.179, 2048 0.156, 3072 0.156, 6144 0.172 ms
 _SWEEP_WG = int(os.environ.get("HIPFM_SWEEP_WG", "256"))   # 128: 0.178, 256: 0.160, 512: 0.179 ms
 
 
