@@ -32,6 +32,7 @@ import numpy as np
 import torch
 
 from .native_io import FMT_LIBSVM, FMT_TFRECORD, NativeLoader, count_records
+from ..utils.knobs import knob
 
 PIPE_ROOT = "/opt/ml/input/data"
 _pipe_lock = threading.Lock()
@@ -82,7 +83,7 @@ def plan_shard(files: Sequence[str], n: int, i: int, policy: str = "file", seed:
 
 
 def pipe_root() -> str:
-    return os.environ.get("HIPFM_PIPE_ROOT", PIPE_ROOT)
+    return knob("HIPFM_PIPE_ROOT") or PIPE_ROOT
 
 
 def pipe_channel_path(channel: str, epoch: int) -> str:

@@ -37,33 +37,34 @@ from ..ops._lib import (TW_MAXL, BnArgs, EpiArgs, FinOpt, HeadArgs, TowerArgs, W
                         WgJob, RowSumJob, SegApplyArgs, SfArgs, ShadowSeg, SlabJob)
 from ..utils.rng import keep_threshold
 from .reference import glorot_std, init_params, pad32
+from ..utils.knobs import flag, knob
 
 
 # Execution-mode switches (each one is a supported, tested mode; rejected experiments are gone)
-_SORT_MODE = os.environ.get("HIPFM_SORT", "auto")                # auto | global
-_SORT_SIDE_STREAM = os.environ.get("HIPFM_SORT_SIDE_STREAM", "1") == "1"
-_DENSE_EARLY = os.environ.get("HIPFM_DENSE_EARLY", "1") == "1"
-_FWD_IDST = os.environ.get("HIPFM_FWD_IDST", "1") == "1"         # fm_fwd writes ids field-major
-_FUSE_FIN_OPT = os.environ.get("HIPFM_FUSE_FIN_OPT", "1") == "1"  # dense optimizer in finalize
-_SPARSE_IMPL = os.environ.get("HIPFM_SPARSE", "fused")             # fused | seg
-_SHARD_PIPELINE = os.environ.get("HIPFM_SHARD_PIPELINE", "1") == "1"
-_DENSE_SIDE_STREAM = os.environ.get("HIPFM_DENSE_SIDE_STREAM", "auto")   # auto | 1 | 0
-_TOWER_GATHER = os.environ.get("HIPFM_TOWER_GATHER", "1") == "1"   # FM gather fused into the tower
+_SORT_MODE = knob("HIPFM_SORT")                # auto | global
+_SORT_SIDE_STREAM = flag("HIPFM_SORT_SIDE_STREAM")
+_DENSE_EARLY = flag("HIPFM_DENSE_EARLY")
+_FWD_IDST = flag("HIPFM_FWD_IDST")         # fm_fwd writes ids field-major
+_FUSE_FIN_OPT = flag("HIPFM_FUSE_FIN_OPT")  # dense optimizer in finalize
+_SPARSE_IMPL = knob("HIPFM_SPARSE")             # fused | seg
+_SHARD_PIPELINE = flag("HIPFM_SHARD_PIPELINE")
+_DENSE_SIDE_STREAM = knob("HIPFM_DENSE_SIDE_STREAM")   # auto | 1 | 0
+_TOWER_GATHER = flag("HIPFM_TOWER_GATHER")   # FM gather fused into the tower
 # weight gradients + split-K combine + bias/head reductions + dense optimizer in one launch
-_WGFIN = os.environ.get("HIPFM_WGFIN", "1") == "1"
+_WGFIN = flag("HIPFM_WGFIN")
 # single GPU, lazy rows: wgfin inside the sparse backward's launch (sparse_fused.hip sfwg_kernel)
-_SFWG = os.environ.get("HIPFM_SFWG", "1") == "1"
+_SFWG = flag("HIPFM_SFWG")
 # row-sharded step: where the next batch's routing branch is enqueued: start | fetch | tower
-_SHX_FORK = os.environ.get("HIPFM_SHX_FORK", "start")
+_SHX_FORK = knob("HIPFM_SHX_FORK")
 # row-sharded lazy step: dense optimizer inside the owner update's launch
-_SH_APPLY_DENSE = os.environ.get("HIPFM_SH_APPLY_DENSE", "1") == "1"
+_SH_APPLY_DENSE = flag("HIPFM_SH_APPLY_DENSE")
 # ... and the dense gradient computed in the sparse launch, exchanged by all-gather (no all-reduce)
-_SH_XFUSE = os.environ.get("HIPFM_SH_XFUSE", "1") == "1"
+_SH_XFUSE = flag("HIPFM_SH_XFUSE")
 # tf1_dense on one GPU: split sweep concurrent with the step (0: scatter + full-table sweep)
-_TF1_SPLIT = os.environ.get("HIPFM_TF1_SPLIT", "1") == "1"
-_SWEEP_MODE = os.environ.get("HIPFM_SWEEP_MODE", "merged")      # merged | branch
-_SWEEP_MBLK = int(os.environ.get("HIPFM_SWEEP_MBLK", "2048"))  # merged-mode sweep workgroups: 512 0.191, 1024 0.179, 2048 0.156, 3072 0.156, 6144 0.172 ms
-_SWEEP_WG = int(os.environ.get("HIPFM_SWEEP_WG", "256"))   # 128: 0.178, 256: 0.160, 512: 0.179 ms
+_TF1_SPLIT = flag("HIPFM_TF1_SPLIT")
+_SWEEP_MODE = knob("HIPFM_SWEEP_MODE")      # merged | branch
+_SWEEP_MBLK = int(knob("HIPFM_SWEEP_MBLK"))  # merged-mode sweep workgroups: 512 0.191, 1024 0.179, 2048 0.156, 3072 0.156, 6144 0.172 ms
+_SWEEP_WG = int(knob("HIPFM_SWEEP_WG"))   # 128: 0.178, 256: 0.160, 512: 0.179 ms
 
 
 def check_field_ranges(ranges, F: int, V: int) -> List[Tuple[int, int]]:
@@ -91,7 +92,7 @@ def field_ranges_from_sizes(sizes: Sequence[int]) -> List[Tuple[int, int]]:
 
 
 _OPT_SLOTS = {"Adam": 2, "ftrl": 2, "Adagrad": 1, "Momentum": 1, "GD": 0}
-_TABLE_LAYOUT = os.environ.get("HIPFM_TABLE_LAYOUT", "record")     # record | split
+_TABLE_LAYOUT = knob("HIPFM_TABLE_LAYOUT")     # record | split
 
 
 def table_record_floats(K: int, optimizer: str) -> int:
@@ -343,7 +344,7 @@ class NativeDeepFM:
         # GEMMs) and towers whose activations do not fit in LDS use the per-layer kernels
         can_fuse = (not self.batch_norm and len(self.layers) <= TW_MAXL and
                     self._tower_lds_bytes() <= 150 * 1024)
-        want = os.environ.get("HIPFM_FUSED_TOWER", "1") != "0" if fused is None else bool(fused)
+        want = (knob("HIPFM_FUSED_TOWER") != "0") if fused is None else bool(fused)
         self.fused = can_fuse and want
         # the FM gather (K1) as the fused tower's prologue: E goes straight into the tower's LDS
         # tile (no fm_fwd launch, no E round trip through HBM)
@@ -465,7 +466,7 @@ class NativeDeepFM:
         for i in range(len(self.layers)):
             Mg, Ng, Kd = self.Np[i], self.Kp[i], M
             if self.fused:
-                s = int(os.environ.get("HIPFM_WG_SPLIT", "32"))
+                s = int(knob("HIPFM_WG_SPLIT"))
                 while s > 1 and (M % (32 * s) or M // s < 128):
                     s //= 2
                 self.wg_cfg.append((None, s))
@@ -540,7 +541,7 @@ class NativeDeepFM:
         # workgroup holds 148 KB of LDS: one workgroup per field on one GPU (0.160 ms/step vs
         # 0.162 / 0.169 / 0.179 with 2 / 4 / 16 per field); 4 per field for the next batch's
         # routing on the sharded step (0.198 ms vs 0.206 with 16; HIPFM_FSORT_PB overrides)
-        pb = os.environ.get("HIPFM_FSORT_PB")
+        pb = knob("HIPFM_FSORT_PB")
         self._fsort = KN.FieldSort(self.field_ranges, min(M, KN.field_sort_max_rows()), dev,
                                    max_pb=int(pb) if pb is not None else (2 if self.sharded else 0))
         if not self.sharded:
@@ -615,7 +616,7 @@ class NativeDeepFM:
         M, dev = self.M, self.device
         f32 = dict(dtype=torch.float32, device=dev)
         # 4 workgroup splits x 4 waves: same-box A/B 0.1214 (4) / 0.1228 (8) / 0.126 (16) ms/step
-        ns = int(os.environ.get("HIPFM_WGFIN_NS", "4"))
+        ns = int(knob("HIPFM_WGFIN_NS"))
         while ns > 1 and (M % (ns * 4 * 32) or M // (ns * 4) < 32):
             ns //= 2
         self._wgfin_ns = ns

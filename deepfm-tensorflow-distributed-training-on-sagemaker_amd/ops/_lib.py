@@ -16,6 +16,7 @@ import threading
 import torch
 
 from .build import KERNELS_SO
+from ..utils.knobs import knob
 
 _lock = threading.Lock()
 _lib = None
@@ -262,7 +263,7 @@ _SIGS = {
 
 
 def lib_path() -> str:
-    return os.environ.get("HIPFM_KERNELS_SO", KERNELS_SO)
+    return knob("HIPFM_KERNELS_SO") or KERNELS_SO
 
 
 def available() -> bool:

@@ -16,13 +16,14 @@ import os
 import shutil
 import subprocess
 import sys
+from ..utils.knobs import knob
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 REPO = os.path.dirname(PKG_DIR)
 CSRC = os.path.join(REPO, "csrc")
 LIB_DIR = os.path.join(PKG_DIR, "_lib")
 BUILD_DIR = os.path.join(REPO, "build", "obj")
-ARCH = os.environ.get("HIPFM_ARCH", "gfx950")
+ARCH = knob("HIPFM_ARCH")
 
 KERNELS_SO = os.path.join(LIB_DIR, "libhipfm_kernels.so")
 IO_SO = os.path.join(LIB_DIR, "libhipfm_io.so")

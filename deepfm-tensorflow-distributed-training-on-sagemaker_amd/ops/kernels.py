@@ -14,6 +14,7 @@ import torch
 from . import _lib
 from ._lib import (BnArgs, EpiArgs, HeadArgs, TowerArgs, W8Job, WgJob, OptHyper, RowSumJob, SegApplyArgs, SfArgs, ShApplyArgs, ShadowSeg, SlabJob, check,
                    ptr, stream_handle)
+from ..utils.knobs import knob
 
 EPI_F32, EPI_FWD, EPI_DGRAD, EPI_FWD_EVAL, EPI_RELU_F32 = 0, 1, 2, 3, 4
 OPT_IDS = {"Adam": 0, "Adagrad": 1, "Momentum": 2, "ftrl": 3, "GD": 4}
@@ -112,7 +113,7 @@ def onesweep_sort_ids(keys_in, keys_out, perm_out, n, end_bit, temp):
                                     ptr(temp), temp.numel(), stream_handle()), "onesweep_sort_ids")
 
 
-SORT_IMPL = os.environ.get("HIPFM_SORT_IMPL", "onesweep")
+SORT_IMPL = knob("HIPFM_SORT_IMPL")
 # A/B in tools/bench_sort.py (graph-timed): onesweep 56 us vs LSD 101 us at n = 640K, 30 bits
 
 

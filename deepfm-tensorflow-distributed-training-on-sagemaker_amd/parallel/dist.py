@@ -31,6 +31,7 @@ import torch.distributed as dist
 
 from ..ops import kernels as KN
 from .embedding import Router
+from ..utils.knobs import knob
 
 
 def init_distributed(backend: Optional[str] = None, timeout_s: int = 600):
@@ -74,7 +75,7 @@ class Comm:
         # sparse exchange, and one communicator must not carry concurrent operations.
         if native is None:
             native = (dist.get_backend(group) == "nccl" and self.sharded and
-                      os.environ.get("HIPFM_SHARD_EXCHANGE", "fixed") == "fixed")
+                      knob("HIPFM_SHARD_EXCHANGE") == "fixed")
         self.engine = self.engine_dense = self.engine_route = None
         if capacity is not None and self.world_size > 1:
             # every rank must use the SAME per-peer block size in the fixed-capacity all-to-alls:

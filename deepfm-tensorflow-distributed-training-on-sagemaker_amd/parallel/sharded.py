@@ -23,13 +23,14 @@ import torch
 
 from ..ops import kernels as KN
 from ..ops._lib import ShApplyArgs, ShTable
+from ..utils.knobs import flag
 
 # routing in two launches (sh_route) instead of segments + bucket (7 launches); same outputs
-_ROUTE2 = os.environ.get("HIPFM_SH_ROUTE2", "1") == "1"
+_ROUTE2 = flag("HIPFM_SH_ROUTE2")
 # lazy rows: the NEXT batch's rows are served on the side stream during this step (after its
 # routing); this step's owner update patches the rows it changes, so the serve launch leaves
 # the critical path
-_SERVE_AHEAD = os.environ.get("HIPFM_SH_SERVE_AHEAD", "1") == "1"
+_SERVE_AHEAD = flag("HIPFM_SH_SERVE_AHEAD")
 
 
 def estimate_capacity(id_batches: Iterable[torch.Tensor], world: int, slack: float = 1.25,

@@ -19,6 +19,7 @@ import os
 import sys
 import threading
 import time
+from ..utils.knobs import knob
 
 
 class Watchdog:
@@ -61,13 +62,13 @@ class InjectedFault(RuntimeError):
 
 
 def maybe_inject_fault(step: int, rank: int) -> None:
-    s = os.environ.get("HIPFM_FAULT_STEP")
+    s = knob("HIPFM_FAULT_STEP")
     if not s or int(s) != step:
         return
-    r = os.environ.get("HIPFM_FAULT_RANK")
+    r = knob("HIPFM_FAULT_RANK")
     if r is not None and int(r) != rank:
         return
-    if os.environ.get("HIPFM_FAULT_MODE", "exit") == "raise":
+    if knob("HIPFM_FAULT_MODE") == "raise":
         raise InjectedFault(f"injected fault at step {step} on rank {rank}")
     sys.stderr.write(f"[hipfm] injected fault: rank {rank} exits at step {step}\n")
     sys.stderr.flush()

@@ -1,0 +1,117 @@
+"""Every ``HIPFM_*`` environment knob, in one registry.
+
+The production path needs none of them: each default is the measured-best configuration.  Kinds:
+
+* ``variant`` -- selects an unfused / alternative execution path.  Each variant is kept because a
+  test uses it as the bitwise (or tolerance) oracle of the fused path, or because it is the
+  fallback of a fused path with a shape limit; the fused default is what ``bench.py`` measures.
+* ``tuning``  -- a launch-shape number; the comment says what it was measured against.
+* ``harness`` -- build / test / benchmark plumbing (library path, fault injection, the bench
+  supervisor's protocol between parent and child processes).
+
+``knob(name)`` returns the environment value or the registered default; reading an unregistered
+name raises, and ``tests/test_knobs.py`` checks that every ``HIPFM_*`` name in the sources is
+registered here, so a new switch cannot appear without its entry.
+"""
+from __future__ import annotations
+
+import os
+from typing import Dict, NamedTuple, Optional
+
+
+class Knob(NamedTuple):
+    default: Optional[str]
+    kind: str
+    doc: str
+
+
+KNOBS: Dict[str, Knob] = {
+    # ---- execution-path variants (oracles / fallbacks of the fused defaults)
+    "HIPFM_SORT": Knob("auto", "variant", "auto: per-field LDS sort when field id ranges are known; "
+                       "global: the 3-pass global radix sort (oracle of the field sort)"),
+    "HIPFM_SORT_IMPL": Knob("onesweep", "variant", "global sort: onesweep (56 us) or lsd (101 us at "
+                            "n = 640K, tools/bench_sort.py)"),
+    "HIPFM_SORT_SIDE_STREAM": Knob("1", "variant", "slot sort on a graph side branch (0: inline)"),
+    "HIPFM_DENSE_EARLY": Knob("1", "variant", "one GPU: dense optimizer before the join with the sort "
+                              "branch (0: after the sparse backward)"),
+    "HIPFM_FWD_IDST": Knob("1", "variant", "per-layer path: fm_fwd writes the ids field-major for the "
+                           "sort (saves its transpose launch)"),
+    "HIPFM_FUSE_FIN_OPT": Knob("1", "variant", "dense optimizer inside the gradient finalize launch"),
+    "HIPFM_SPARSE": Knob("fused", "variant", "fused: one-launch sparse backward; seg: fm_bwd_seg + "
+                         "seg_apply (oracle, tests/test_gpu_kernels.py)"),
+    "HIPFM_SHARD_PIPELINE": Knob("1", "variant", "row-sharded step: next batch's routing on a side "
+                                 "stream (0: inline)"),
+    "HIPFM_DENSE_SIDE_STREAM": Knob("auto", "variant", "dense-gradient branch on its own stream: auto "
+                                    "(multi-rank exchange only) | 1 | 0"),
+    "HIPFM_FUSED_TOWER": Knob("1", "variant", "one-launch deep tower (0: per-layer GEMM kernels)"),
+    "HIPFM_TOWER_GATHER": Knob("1", "variant", "FM gather in the tower's prologue (0: fm_fwd launch)"),
+    "HIPFM_WGFIN": Knob("1", "variant", "weight gradients + combine + dense optimizer in one launch "
+                        "(0: wgrad_group + finalize)"),
+    "HIPFM_SFWG": Knob("1", "variant", "wgfin work inside the sparse backward's launch"),
+    "HIPFM_SHX_FORK": Knob("start", "variant", "row-sharded step: fork point of the next batch's "
+                           "routing branch (start | tower)"),
+    "HIPFM_SH_APPLY_DENSE": Knob("1", "variant", "row-sharded step: dense optimizer in the owner "
+                                 "update's launch"),
+    "HIPFM_SH_XFUSE": Knob("1", "variant", "row-sharded step: gradient rows + dense gradients in one "
+                           "aggregated RCCL operation"),
+    "HIPFM_SH_ROUTE2": Knob("1", "variant", "two-launch routing (0: segments + bucket kernels, oracle)"),
+    "HIPFM_SH_SERVE_AHEAD": Knob("1", "variant", "row-sharded step: next batch's rows served during "
+                                 "this step"),
+    "HIPFM_SHARD_EXCHANGE": Knob("fixed", "variant", "fixed: fixed-capacity native RCCL exchange; "
+                                 "else the torch.distributed all-to-all-v path"),
+    "HIPFM_TF1_SPLIT": Knob("1", "variant", "tf1_dense on one GPU: split form (0: gradient scatter + "
+                            "full-table sweep, the oracle in tests/test_gpu_tf1.py)"),
+    "HIPFM_SWEEP_MODE": Knob("merged", "variant", "tf1_dense split sweep: merged (workgroups of the "
+                             "sparse launch, 0.156 ms) | branch (own graph branch, 0.160-0.163 ms)"),
+    "HIPFM_TABLE_LAYOUT": Knob("record", "variant", "record: one 128-B record per row (v, w, slots); "
+                               "split: separate tables"),
+    # ---- tuning
+    "HIPFM_SWEEP_MBLK": Knob("2048", "tuning", "merged sweep workgroups (512: 0.191, 1024: 0.179, "
+                             "2048: 0.156, 6144: 0.172 ms/step)"),
+    "HIPFM_SWEEP_WG": Knob("256", "tuning", "branch sweep workgroups (128: 0.178, 256: 0.160, "
+                           "512: 0.179 ms/step)"),
+    "HIPFM_WG_SPLIT": Knob("32", "tuning", "per-layer weight-gradient split-K workgroups"),
+    "HIPFM_WGFIN_NS": Knob("4", "tuning", "wgfin workgroups per output tile (8/16: equal or slower)"),
+    "HIPFM_FSORT_PB": Knob(None, "tuning", "field sort MSD partitions per field, log2 (default: 0 on "
+                           "one GPU, 2 for the sharded routing)"),
+    "HIPFM_FS_MAX_PB": Knob("4", "tuning", "tools/bench_sort.py: field sort partitions per field"),
+    "HIPFM_GRAPH_STEPS": Knob("16", "tuning", "training steps per captured HIP graph (bench.py default)"),
+    # ---- harness
+    "HIPFM_ARCH": Knob("gfx950", "harness", "offload arch of the HIP build"),
+    "HIPFM_KERNELS_SO": Knob(None, "harness", "path of the kernel library (default: in-tree _lib)"),
+    "HIPFM_PIPE_ROOT": Knob(None, "harness", "directory of SageMaker pipe-mode FIFOs (tests)"),
+    "HIPFM_FAULT_STEP": Knob(None, "harness", "fault injection: step at which a rank dies"),
+    "HIPFM_FAULT_RANK": Knob(None, "harness", "fault injection: the rank (default all)"),
+    "HIPFM_FAULT_MODE": Knob("exit", "harness", "fault injection: exit | raise"),
+    "HIPFM_PROFILE_STEPS": Knob("", "harness", "a:b -- roctx range around steps [a, b)"),
+    "HIPFM_OS_DEBUG_NOLB": Knob(None, "harness", "onesweep sort debug: disable the look-back"),
+    "HIPFM_BENCH_CHILD": Knob(None, "harness", "bench supervisor protocol: set in the child"),
+    "HIPFM_BENCH_SUPERVISE": Knob(None, "harness", "bench supervisor protocol: 0 runs unsupervised"),
+    "HIPFM_BENCH_RUNG": Knob(None, "harness", "bench supervisor protocol: the child's ladder rung"),
+    "HIPFM_BENCH_FIRST_RUNG": Knob(None, "harness", "bench: start the ladder at this rung"),
+    "HIPFM_BENCH_HANG_S": Knob(None, "harness", "bench: seconds without progress = hung"),
+    "HIPFM_BENCH_NO_GRAPH": Knob(None, "harness", "bench: eager steps only"),
+    "HIPFM_BENCH_PROGRESS": Knob(None, "harness", "bench supervisor protocol: progress file"),
+    "HIPFM_BENCH_RESULT": Knob(None, "harness", "bench supervisor protocol: result file"),
+    "HIPFM_BENCH_FAKE": Knob(None, "harness", "bench supervisor tests: CPU stand-in children"),
+}
+
+
+def knob(name: str) -> Optional[str]:
+    """The environment value of a registered knob, else its default."""
+    k = KNOBS[name]
+    return os.environ.get(name, k.default)
+
+
+def flag(name: str) -> bool:
+    """A registered on/off knob ("1" = on)."""
+    return knob(name) == "1"
+
+
+def describe() -> str:
+    """One line per knob (README / ``python -m hipfm.utils.knobs``)."""
+    return "\n".join(f"{n:26s} {k.kind:8s} default={k.default!s:8s} {k.doc}" for n, k in KNOBS.items())
+
+
+if __name__ == "__main__":
+    print(describe())

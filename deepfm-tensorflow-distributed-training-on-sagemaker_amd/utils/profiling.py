@@ -17,6 +17,7 @@ import contextlib
 import os
 
 import torch
+from ..utils.knobs import knob
 
 
 def _nvtx():
@@ -45,7 +46,7 @@ class StepWindow:
     """Emit a marker range around the steps of a window (e.g. ``HIPFM_PROFILE_STEPS=100:120``)."""
 
     def __init__(self, spec: str = None):
-        spec = spec if spec is not None else os.environ.get("HIPFM_PROFILE_STEPS", "")
+        spec = spec if spec is not None else knob("HIPFM_PROFILE_STEPS")
         self.a = self.b = -1
         if spec and ":" in spec:
             a, b = spec.split(":", 1)
