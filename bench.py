@@ -206,21 +206,27 @@ def main():
     dev = torch.device("cuda", local)
     synth = make_synth(args.preset, seed=2024)
     comm = None
+    B = args.batch_size
+    pool = [synth.batch(B, step=rank * 100000 + i, device=dev, id_dtype=torch.int32)
+            for i in range(args.pool)]
+    _progress()
     if world > 1 or args.force_exchange:
         init_distributed("nccl")
         _progress()
         mode = "sharded" if args.embedding_mode == "auto" else args.embedding_mode
         cap = None
         if mode == "sharded":
-            # per-peer capacity of the fixed-size all-to-alls, measured on sample batches of this
-            # rank's id distribution (x1.25 + 256 slack; overflow raises, never drops rows)
+            # per-peer capacity of the fixed-size all-to-alls: measured on EVERY batch this rank
+            # will route (the resident pool and the eval batches), +5 % + 256 margin, then agreed
+            # across ranks (MAX).  Overflow raises, never drops rows.  (Was 1.25x the max of 4
+            # sample batches: every exchange moved ~20 % more padding.)
             from hipfm.parallel.sharded import estimate_capacity
-            cap = estimate_capacity((synth.batch(args.batch_size, step=rank * 100000 + i, device=dev,
-                                                 id_dtype=torch.int32)[0] for i in range(4)), world)
+            ev = (synth.batch(B, step=10_000_000 + rank * 1000 + i, device=dev, id_dtype=torch.int32)[0]
+                  for i in range(args.eval_batches))
+            cap = estimate_capacity([b[0] for b in pool] + list(ev), world, slack=1.05)
         comm = Comm(sharded=(mode == "sharded"), force_exchange=args.force_exchange, capacity=cap)
 
     F = synth.F
-    B = args.batch_size
     layers = [int(x) for x in args.deep_layers.split(",")]
     keep = [float(x) for x in args.dropout.split(",")]
     model = NativeDeepFM(synth.feature_size, F, args.embedding_size, layers, keep, l2_reg=1e-4,
@@ -228,8 +234,6 @@ def main():
                          sparse_update=args.sparse_update, seed=1234, batch_size=B, device=dev,
                          comm=comm, field_ranges=synth.field_ranges(), mlp_dtype=args.mlp_dtype)
     _progress()
-    pool = [synth.batch(B, step=rank * 100000 + i, device=dev, id_dtype=torch.int32)
-            for i in range(args.pool)]
     if args.field_major_ids:
         # ids stored field-major ([F, B] storage, [B, F] view): the per-field slot sort reads them
         # without its transpose launch.  Not the default: on one GPU the sort branch then starts

@@ -26,3 +26,16 @@ for wg in (64, 128, 256, 512, 1024, 2048, 8192):
     torch.cuda.synchronize()
     us = e0.elapsed_time(e1) * 1000 / n
     print(f"wg={wg:5d}  {us:7.1f} us/sweep  {2 * R * 128 / us / 1e6:5.2f} TB/s (128 B read + written per row)")
+
+# reference point: a plain device copy of the same bytes (read + write), torch's copy kernel
+src = torch.empty_like(rec)
+for _ in range(3):
+    rec.copy_(src)
+e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+e0.record()
+for _ in range(20):
+    rec.copy_(src)
+e1.record()
+torch.cuda.synchronize()
+us = e0.elapsed_time(e1) * 1000 / 20
+print(f"torch copy_ of the table: {us:7.1f} us  {2 * R * 128 / us / 1e6:5.2f} TB/s")
