@@ -161,7 +161,7 @@ __global__ void __launch_bounds__(256) tf1_sweep_kernel(
   // U rows per thread per pass, all loads issued before any update: on its own graph branch the
   // sweep shares the chip with the step's launches, so it runs on few workgroups and needs
   // memory-level parallelism per thread rather than more waves
-  tf1_sweep_rows<K, OPT, K <= 8 ? 4 : 2>(rec, ld, R, flags, h, lr_t_of<OPT>(h, sw_step),
+  tf1_sweep_rows<K, OPT, K <= 8 ? 4 : (K <= 16 ? 2 : 1)>(rec, ld, R, flags, h, lr_t_of<OPT>(h, sw_step),
                                          blockIdx.x * (long)blockDim.x + threadIdx.x,
                                          (long)gridDim.x * blockDim.x);
   __syncthreads();
@@ -341,6 +341,7 @@ HFM_API int hfm_tf1_sweep(int K, int opt, long R, float* rec, int ld, unsigned c
     case 4: return tf1_sweep_k<4>(opt, R, rec, ld, flags, *h, sw_step, done_ctr, max_wg, st);
     case 8: return tf1_sweep_k<8>(opt, R, rec, ld, flags, *h, sw_step, done_ctr, max_wg, st);
     case 16: return tf1_sweep_k<16>(opt, R, rec, ld, flags, *h, sw_step, done_ctr, max_wg, st);
+    case 32: return tf1_sweep_k<32>(opt, R, rec, ld, flags, *h, sw_step, done_ctr, max_wg, st);
     default: return (int)hipErrorInvalidValue;
   }
 }

@@ -62,7 +62,7 @@ _SH_APPLY_DENSE = flag("HIPFM_SH_APPLY_DENSE")
 _SH_XFUSE = flag("HIPFM_SH_XFUSE")
 # tf1_dense on one GPU: split sweep concurrent with the step (0: scatter + full-table sweep)
 _TF1_SPLIT = flag("HIPFM_TF1_SPLIT")
-_SWEEP_MODE = knob("HIPFM_SWEEP_MODE")      # merged | branch
+_SWEEP_MODE = knob("HIPFM_SWEEP_MODE")      # auto | merged | branch
 _SWEEP_MBLK = int(knob("HIPFM_SWEEP_MBLK"))  # merged-mode sweep workgroups: 512 0.191, 1024 0.179, 2048 0.156, 3072 0.156, 6144 0.172 ms
 _SWEEP_WG = int(knob("HIPFM_SWEEP_WG"))   # 128: 0.178, 256: 0.160, 512: 0.179 ms
 
@@ -1184,7 +1184,12 @@ class NativeDeepFM:
         presorted = False
         # tf1_dense split sweep inside the merged sparse launch (needs the single-GPU sfwg path,
         # which the split form always takes: its sort is always presorted on a side stream)
-        self._tf1_merged = (self._tf1_plan is not None and _SWEEP_MODE == "merged" and
+        # Small batches take the branch: their tower / sparse launches leave most CUs idle
+        # (B = 1024, K = 8: branch 0.069 vs merged 0.077 ms/step; B = 16384: merged 0.156 vs
+        # branch 0.160-0.163).  (K = 32 stays on scatter + sweep: a concurrent K = 32 sweep
+        # slowed the latency-bound tower 41 -> 76 us, 0.138 vs 0.131 ms/step.)
+        self._tf1_merged = (self._tf1_plan is not None and
+                            (_SWEEP_MODE == "merged" or (_SWEEP_MODE == "auto" and B >= 8192)) and
                             self._sfwg_possible())
         if self.shx is not None:
             self._shx_start(B)

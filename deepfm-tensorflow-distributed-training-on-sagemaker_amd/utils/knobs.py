@@ -61,8 +61,9 @@ KNOBS: Dict[str, Knob] = {
                                  "else the torch.distributed all-to-all-v path"),
     "HIPFM_TF1_SPLIT": Knob("1", "variant", "tf1_dense on one GPU: split form (0: gradient scatter + "
                             "full-table sweep, the oracle in tests/test_gpu_tf1.py)"),
-    "HIPFM_SWEEP_MODE": Knob("merged", "variant", "tf1_dense split sweep: merged (workgroups of the "
-                             "sparse launch, 0.156 ms) | branch (own graph branch, 0.160-0.163 ms)"),
+    "HIPFM_SWEEP_MODE": Knob("auto", "variant", "tf1_dense split sweep: merged (workgroups of the "
+                             "sparse launch) | branch (own graph branch) | auto (merged from B = 8192: "
+                             "B=16384 0.156 vs 0.160-0.163 ms, B=1024 0.077 vs 0.069 ms)"),
     "HIPFM_TABLE_LAYOUT": Knob("record", "variant", "record: one 128-B record per row (v, w, slots); "
                                "split: separate tables"),
     # ---- tuning

@@ -35,7 +35,7 @@ def test_package_reads_knobs_through_the_registry():
 
 
 def test_defaults_and_describe(monkeypatch):
-    assert knob("HIPFM_SPARSE") == "fused" and knob("HIPFM_SWEEP_MODE") == "merged"
+    assert knob("HIPFM_SPARSE") == "fused" and knob("HIPFM_SWEEP_MODE") == "auto"
     monkeypatch.setenv("HIPFM_SPARSE", "seg")
     assert knob("HIPFM_SPARSE") == "seg"
     text = describe()
