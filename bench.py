@@ -37,9 +37,12 @@ METRIC = ("samples/sec (whole node) + eval AUC, Criteo-1TB-shape DeepFM at 1/2/4
 # all-gather, rows served ahead) fails.
 _R1_EXCHANGE = {"HIPFM_SH_XFUSE": "0", "HIPFM_SH_APPLY_DENSE": "0", "HIPFM_SH_ROUTE2": "0",
                 "HIPFM_SH_SERVE_AHEAD": "0"}
+# 1-rank proxy (--force_exchange), ms/step: 0.178 / 0.192 / 0.199 / 0.289 / 0.274.  A capture
+# failure is the likeliest multi-GPU surprise, so the fused exchange launched eagerly comes second.
 LADDER = [
     ("graph+prefetch", {}),                                  # HIP graphs, next-batch routing prefetch
-    ("graph+prefetch+allreduce", dict(_R1_EXCHANGE)),        # same, dense all-reduce on a comm stream
+    ("eager+prefetch+fused", {"HIPFM_BENCH_NO_GRAPH": "1"}),  # same step, launched eagerly
+    ("graph+prefetch+allreduce", dict(_R1_EXCHANGE)),        # graphs, dense all-reduce on a comm stream
     ("eager+prefetch", {"HIPFM_BENCH_NO_GRAPH": "1", **_R1_EXCHANGE}),   # launched eagerly
     ("eager", {"HIPFM_BENCH_NO_GRAPH": "1", "HIPFM_SHARD_PIPELINE": "0", **_R1_EXCHANGE}),
 ]

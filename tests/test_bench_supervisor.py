@@ -32,9 +32,12 @@ def _run(fake, hang_s="4"):
 
 @pytest.mark.parametrize("fake,rung", [
     ("none:0:fail", "graph+prefetch"),
-    ("graph+prefetch:1:fail", "graph+prefetch+allreduce"),
-    ("graph+prefetch:1:fail,graph+prefetch+allreduce:0:fail", "eager+prefetch"),
-    ("graph+prefetch:0:hang,graph+prefetch+allreduce:1:fail,eager+prefetch:1:fail", "eager"),
+    ("graph+prefetch:1:fail", "eager+prefetch+fused"),
+    ("graph+prefetch:1:fail,eager+prefetch+fused:0:fail", "graph+prefetch+allreduce"),
+    ("graph+prefetch:1:fail,eager+prefetch+fused:1:fail,graph+prefetch+allreduce:0:fail",
+     "eager+prefetch"),
+    ("graph+prefetch:0:hang,eager+prefetch+fused:0:fail,graph+prefetch+allreduce:1:fail,"
+     "eager+prefetch:1:fail", "eager"),
 ])
 def test_supervisor_falls_back_and_prints_one_line(fake, rung):
     rc, lines = _run(fake)
@@ -57,6 +60,6 @@ def test_plain_bench_gpus_n_spawns_n_ranks(n):
 
 
 def test_supervisor_fails_when_every_rung_fails():
-    rc, lines = _run("graph+prefetch:0:fail,graph+prefetch+allreduce:0:fail,eager+prefetch:0:fail,"
-                     "eager:1:fail")
+    rc, lines = _run("graph+prefetch:0:fail,eager+prefetch+fused:0:fail,graph+prefetch+allreduce:0:fail,"
+                     "eager+prefetch:0:fail,eager:1:fail")
     assert rc != 0 and not lines
