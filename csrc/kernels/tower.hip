@@ -45,7 +45,7 @@ struct TowerArgs {
   const int64_t* step;
   const float* w_out;             // [Np_last]
   const float* b_out;             // [1]
-  const float* y_fm;              // [M]
+  float* y_fm;                    // [M] (gather variant: written, the FM logit part)
   const float* labels;            // [M] or null
   bf16* Ht[TW_MAXL];              // [Np_i, M]   (train)
   bf16* dZt[TW_MAXL];             // [Np_i, M]   (train)
@@ -389,6 +389,7 @@ __global__ void __launch_bounds__(256) tower_kernel(TowerArgs a) {
       }
     }
     if (q == 0) {
+      if (KE > 0) a.y_fm[grow] = s_yfm[row];   // (the FM logit part, for tests / diagnostics)
       a.prob[grow] = p;
       s_dl[row] = dl;
       s_loss[row] = lossb;

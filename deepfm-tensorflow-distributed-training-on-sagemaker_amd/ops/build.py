@@ -29,6 +29,15 @@ KERNELS_SO = os.path.join(LIB_DIR, "libhipfm_kernels.so")
 IO_SO = os.path.join(LIB_DIR, "libhipfm_io.so")
 
 
+# No packed-FP32 VALU ops (v_pk_add/mul/fma_f32) in device code.  Measured on MI355X: a
+# v_pk_add_f32 whose result feeds a ds_bpermute (the __shfl_xor of a lane reduction) at once
+# read stale lanes for one 16-lane quarter-wave now and then -- only with two workgroups per CU
+# (tools/det5.py: the FM logit of 2 adjacent samples off by ~1e-5, a different pair every
+# run; tower_kernel's gather reduction, and training was not bitwise reproducible).  Without
+# the packed ops the same code is exact and deterministic (tests/test_gpu_determinism.py).
+NO_PACKED_F32 = ["-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops"]
+
+
 def _hipcc() -> str:
     for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
         if c and os.path.exists(c):
@@ -67,7 +76,7 @@ def build_kernels(force: bool = False, jobs: int = 8, verbose: bool = False) -> 
     def comp(so):
         s, o = so
         cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17",
-               "-fvisibility=hidden", "-Wno-unused-result", "-c", s, "-o", o]
+               "-fvisibility=hidden", "-Wno-unused-result", *NO_PACKED_F32, "-c", s, "-o", o]
         out = _run(cmd)
         if verbose and out.strip():
             print(out)
