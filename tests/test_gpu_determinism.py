@@ -18,10 +18,10 @@ DEV = torch.device("cuda", 0)
 B = 16384
 
 
-def _model(synth):
+def _model(synth, update="lazy"):
     return NativeDeepFM(synth.feature_size, synth.F, 8, [128, 64, 32], [0.5] * 3, seed=1234,
                         batch_size=B, device=DEV, field_ranges=synth.field_ranges(),
-                        sparse_update="lazy")
+                        sparse_update=update)
 
 
 def test_gather_tower_eval_is_exact_and_deterministic():
@@ -49,13 +49,17 @@ def test_gather_tower_eval_is_exact_and_deterministic():
     assert float((ys[0].double() - ex).abs().max()) < 1e-6
 
 
-def test_training_is_bitwise_reproducible():
+@pytest.mark.parametrize("update", ["lazy", "tf1_dense"])
+def test_training_is_bitwise_reproducible(update):
     synth = make_synth("criteo_kaggle", seed=2024)
-    batches = [synth.batch(B, step=7_000 + i, device=DEV, id_dtype=torch.int32) for i in range(3)]
-    ms = [_model(synth) for _ in range(2)]
+    batches = [synth.batch(B, step=7_000 + i, device=DEV, id_dtype=torch.int32) for i in range(4)]
+    ms = [_model(synth, update) for _ in range(2)]
     for mm in ms:
-        for i, b in enumerate(batches):
-            mm.train_step(*b, next_ids=batches[i + 1][0] if i + 1 < len(batches) else None)
+        for i, b in enumerate(batches[:2]):
+            mm.train_step(*b, next_ids=batches[i + 1][0])
+        mm.train_steps(batches[2:])              # captured multi-step graph
+        if update == "tf1_dense":
+            assert mm._tf1_merged                 # B = 16384: the merged sweep
     torch.cuda.synchronize()
     assert torch.equal(ms[0].rec, ms[1].rec)
     assert torch.equal(ms[0].p, ms[1].p)
