@@ -436,7 +436,7 @@ template <int K, int OPT>
 static void sfwg_launch(const SfArgs& A, const WgFinArgs& W, unsigned* done, const SweepArgs& S,
                         hipStream_t st) {
   const dim3 g(W.tile_wgs + 1 + (A.n + SfCfg<K>::TP - 1) / SfCfg<K>::TP + S.nblk), blk(256);
-  if constexpr (K <= 16) {
+  if constexpr (K <= 32) {
     if (S.nblk) {
       hipLaunchKernelGGL((sfwg_kernel<K, OPT, true>), g, blk, 0, st, A, W, done, S);
       return;
@@ -496,7 +496,7 @@ HFM_API int hfm_sparse_wgfin(int K, int opt, const SfArgs* A, const WgFinArgs* W
   if (sweep && sweep->nblk > 0) {
     const int ns = opt == OPT_GD ? 0 : ((opt == OPT_ADAM || opt == OPT_FTRL) ? 2 : 1);
     const int used = K + 4 + ns * K;
-    if (K > 16 || !sweep->rec || !sweep->flags || !sweep->sw_step || sweep->R <= 0 ||
+    if (K > 32 || !sweep->rec || !sweep->flags || !sweep->sw_step || sweep->R <= 0 ||
         sweep->ld != (used <= 16 ? (used + 15) / 16 * 16 : (used + 31) / 32 * 32))
       return (int)hipErrorInvalidValue;
     S = *sweep;

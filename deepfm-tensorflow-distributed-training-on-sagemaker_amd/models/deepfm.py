@@ -279,7 +279,7 @@ class NativeDeepFM:
         # tf1_sweep_kernel).  Byte flags per row per sorted-slot set mark the batch's rows.
         self.tf1_split = (self.sparse_update == "tf1_dense" and self.record and not self.exchange and
                           not self.sharded and
-                          _TF1_SPLIT and K in (4, 8, 16) and _SPARSE_IMPL == "fused" and
+                          _TF1_SPLIT and K in (4, 8, 16, 32) and _SPARSE_IMPL == "fused" and
                           _SORT_SIDE_STREAM)
         self.lazy_rows = self.sparse_update == "lazy" or self.tf1_split   # sparse kernel mode
         if self.tf1_split:
@@ -1186,10 +1186,11 @@ class NativeDeepFM:
         # which the split form always takes: its sort is always presorted on a side stream)
         # Small batches take the branch: their tower / sparse launches leave most CUs idle
         # (B = 1024, K = 8: branch 0.069 vs merged 0.077 ms/step; B = 16384: merged 0.156 vs
-        # branch 0.160-0.163).  (K = 32 stays on scatter + sweep: a concurrent K = 32 sweep
-        # slowed the latency-bound tower 41 -> 76 us, 0.138 vs 0.131 ms/step.)
+        # branch 0.160-0.163).  K = 32 always merges: a concurrent K = 32 sweep slowed its
+        # latency-bound tower 41 -> 76 us (0.138 vs 0.131 ms/step for scatter + sweep).
         self._tf1_merged = (self._tf1_plan is not None and
-                            (_SWEEP_MODE == "merged" or (_SWEEP_MODE == "auto" and B >= 8192)) and
+                            (_SWEEP_MODE == "merged" or
+                             (_SWEEP_MODE == "auto" and (B >= 8192 or self.K > 16))) and
                             self._sfwg_possible())
         if self.shx is not None:
             self._shx_start(B)

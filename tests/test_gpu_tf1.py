@@ -47,7 +47,8 @@ def _assert_same(a, b):
 
 @pytest.mark.parametrize("opt,K,mode", [("Adam", 8, "merged"), ("Adam", 8, "branch"),
                                         ("Adagrad", 16, "merged"), ("Momentum", 4, "branch"),
-                                        ("ftrl", 8, "merged"), ("GD", 8, "auto")])
+                                        ("ftrl", 8, "merged"), ("GD", 8, "auto"),
+                                        ("Adam", 32, "auto")])
 def test_tf1_split_equals_scatter_sweep(opt, K, mode, monkeypatch):
     """merged: the sweep runs as extra workgroups of the sparse + wgfin launch; branch: as its own
     kernel on a graph branch concurrent with the whole step."""
@@ -78,7 +79,8 @@ def test_tf1_split_equals_scatter_sweep(opt, K, mode, monkeypatch):
         a.train_step(*pool[i], use_graph=True, next_ids=pool[i + 1][0])
         b.train_step(*pool[i], use_graph=True, next_ids=pool[i + 1][0])
     _assert_same(a, b)
-    assert a._tf1_merged == (mode == "merged")      # (auto: B = 2048 takes the branch)
+    # (auto: B = 2048 takes the branch for K <= 16, the merged sweep for K = 32)
+    assert a._tf1_merged == (mode == "merged" or (mode == "auto" and K > 16))
     # every row moved (non-lazy semantics): rows never in a batch changed too
     seen = torch.zeros(a.R, dtype=torch.bool, device=DEV)
     for ids, _, _ in pool:
