@@ -170,7 +170,7 @@ def main():
                          "replayed hundreds of times memorizes its ids: train loss -> 0, eval AUC drops)")
     ap.add_argument("--eval_batches", type=int, default=8)
     ap.add_argument("--no_graph", action="store_true")
-    ap.add_argument("--graph_steps", type=int, default=int(os.environ.get("HIPFM_GRAPH_STEPS", "16")),
+    ap.add_argument("--graph_steps", type=int, default=int(os.environ.get("HIPFM_GRAPH_STEPS", "32")),
                     help="consecutive training steps captured per HIP graph (divides --pool)")
     ap.add_argument("--infer", action="store_true", help="serving mode (1 GPU): forward-only "
                     "predictions/s of the same model over resident batches, graph-captured")
@@ -249,19 +249,18 @@ def main():
         pool = [(ids.t().contiguous().t(), vals, labels) for ids, vals, labels in pool]
     use_graph = not args.no_graph
     P = len(pool)
-    G = max(1, min(args.graph_steps, P))
-    while P % G:
-        G -= 1
+    G = max(1, args.graph_steps)
     torch.cuda.synchronize()
     _progress()
 
     def chunks(lo, hi):
-        """Global step positions [lo, hi) cut into runs of consecutive pool batches: cuts at
-        multiples of G (so a run never wraps the pool) and at the warm-up / timed boundary, so
-        the timed runs are exactly runs already captured before timing."""
+        """Global step positions [lo, hi) cut into runs of consecutive pool batches: at most G
+        steps, never across a pool wrap, and cut at the warm-up / timed boundary -- so the timed
+        window starts a run, its runs are exactly runs captured before timing, and a short window
+        (the driver's 20 steps) is ONE graph replay."""
         t = lo
         while t < hi:
-            e = min(hi, (t // G + 1) * G)
+            e = min(hi, t + G, (t // P + 1) * P)
             if t < args.warmup < e:
                 e = args.warmup
             yield t, e

@@ -76,7 +76,7 @@ KNOBS: Dict[str, Knob] = {
     "HIPFM_FSORT_PB": Knob(None, "tuning", "field sort MSD partitions per field, log2 (default: 0 on "
                            "one GPU, 2 for the sharded routing)"),
     "HIPFM_FS_MAX_PB": Knob("4", "tuning", "tools/bench_sort.py: field sort partitions per field"),
-    "HIPFM_GRAPH_STEPS": Knob("16", "tuning", "training steps per captured HIP graph (bench.py default)"),
+    "HIPFM_GRAPH_STEPS": Knob("32", "tuning", "most training steps per captured HIP graph (bench.py)"),
     # ---- harness
     "HIPFM_ARCH": Knob("gfx950", "harness", "offload arch of the HIP build"),
     "HIPFM_KERNELS_SO": Knob(None, "harness", "path of the kernel library (default: in-tree _lib)"),
