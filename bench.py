@@ -249,7 +249,8 @@ def main():
         pool = [(ids.t().contiguous().t(), vals, labels) for ids, vals, labels in pool]
     use_graph = not args.no_graph
     P = len(pool)
-    G = max(1, args.graph_steps)
+    # (multi-rank graphs capture 3 RCCL operations per step: they keep 16-step graphs)
+    G = max(1, args.graph_steps if comm is None else min(args.graph_steps, 16))
     torch.cuda.synchronize()
     _progress()
 
