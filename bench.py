@@ -371,7 +371,7 @@ def infer_bench(args):
     import torch
     import hipfm  # noqa: F401
     from hipfm.data.synthetic import make_synth
-    from hipfm.models.deepfm import NativeDeepFM
+    from hipfm.models.deepfm import NativeDeepFM, graph_capture
 
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
@@ -400,7 +400,7 @@ def infer_bench(args):
     graphs = []
     for g0 in range(0, P, G):
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        with graph_capture(g):
             serve(g0, g0 + G)
         graphs.append(g)
     for g in graphs:

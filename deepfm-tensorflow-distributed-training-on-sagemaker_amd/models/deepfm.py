@@ -24,6 +24,8 @@ Reference parity cites: model_fn HVD:141-287, optimizer HVD:252-263, LR scaling 
 """
 from __future__ import annotations
 
+import contextlib
+import gc
 import math
 import os
 from collections import OrderedDict
@@ -103,6 +105,24 @@ def table_record_floats(K: int, optimizer: str) -> int:
     forward gather finds v and w in the same 64-B sector."""
     x = K + 4 + _OPT_SLOTS[optimizer] * K
     return (x + 15) // 16 * 16 if x <= 16 else (x + 31) // 32 * 32
+
+
+@contextlib.contextmanager
+def graph_capture(g):
+    """``torch.cuda.graph(g)`` with Python's automatic garbage collection off while capturing.
+    torch collects garbage once before the capture begins; an automatic collection DURING it
+    can finalize an object whose destructor calls a HIP / RCCL API that is illegal while a
+    stream captures (a dropped model's graphs, events or communicator), which aborts the
+    process (seen on MI355X when one test's models were collected inside the next test's
+    capture)."""
+    was = gc.isenabled()
+    gc.disable()
+    try:
+        with torch.cuda.graph(g):
+            yield
+    finally:
+        if was:
+            gc.enable()
 
 
 def _hashable(x):
@@ -1618,7 +1638,7 @@ class NativeDeepFM:
                     return 1
                 return 1 + self.train_steps(rest, next_ids)
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            with graph_capture(g):
                 for i, (ids, vals, labels) in enumerate(batches):
                     nxt = batches[i + 1][0] if i + 1 < len(batches) else next_ids
                     B, direct, _ = self._bind_step(ids, vals, labels, nxt)
@@ -1643,12 +1663,12 @@ class NativeDeepFM:
                 self.train_step_enqueue(B)
                 torch.cuda.synchronize()
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g):
+                with graph_capture(g):
                     self.train_step_enqueue(B)
                 self._graphs[key] = g
                 return
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            with graph_capture(g):
                 self.train_step_enqueue(B)
             if len(self._graphs) >= self.max_graphs:
                 self._graphs.pop(next(iter(self._graphs)))

@@ -12,7 +12,7 @@ if not torch.cuda.is_available():  # collected on CPU, skipped there
 
 import hipfm  # noqa: E402
 from hipfm.data.synthetic import make_synth  # noqa: E402
-from hipfm.models.deepfm import NativeDeepFM  # noqa: E402
+from hipfm.models.deepfm import NativeDeepFM, graph_capture  # noqa: E402
 from hipfm.models.reference import GoldenDeepFM, init_params  # noqa: E402
 from hipfm.ops import kernels as KN  # noqa: E402
 from hipfm.ops._lib import EpiArgs  # noqa: E402
@@ -319,7 +319,7 @@ def test_sort_graph_replay_with_new_inputs(impl):
         fn(keys, sk, perm, n, bits, temp)
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        with graph_capture(g):
             fn(keys, sk, perm, n, bits, temp)
         gen = torch.Generator(device=dev).manual_seed(n)
         for it in range(6):
@@ -355,7 +355,7 @@ def test_field_sort_equals_global_sort(preset, B, max_pb):
     fs(ids, B, sk, perm)
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
+    with graph_capture(g):
         fs(ids, B, sk, perm)
     for it in range(3):
         if it:
