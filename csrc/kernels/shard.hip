@@ -174,26 +174,39 @@ __global__ void __launch_bounds__(SH_THREADS) sh_scatter_kernel(
 constexpr int RT_ITEMS = 16;
 constexpr int RT_TILE = SH_THREADS * RT_ITEMS;
 
+// Per-tile head counts per owner.  Heads are counted per wave with ballots (lanes of one owner
+// found by nbits bit-ballots, as in sh_route_scatter_kernel): one LDS atomic per (wave, owner)
+// instead of one per head -- at N = 1 every head of a tile hit the same LDS word.
 __global__ void __launch_bounds__(SH_THREADS) sh_route_count_kernel(const int* __restrict__ sk, int n, int N,
-                                                                   int* __restrict__ tcnt) {
+                                                                   int nbits, int* __restrict__ tcnt) {
   __shared__ int h[SH_MAXN + 1];
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63;
   if (tid <= N) h[tid] = 0;
   __syncthreads();
   const int i0 = blockIdx.x * RT_TILE;
+  const unsigned long long lt = (1ull << lane) - 1ull;
   int nh = 0;
 #pragma unroll 4
   for (int k = 0; k < RT_ITEMS; ++k) {
     const int i = i0 + k * SH_THREADS + tid;
+    bool head = false;
+    int o = 0;
     if (i < n) {
       const int key = sk[i];
-      if (i == 0 || key != sk[i - 1]) {
-        atomicAdd(&h[key % N], 1);
-        ++nh;
-      }
+      head = (i == 0 || key != sk[i - 1]);
+      o = head ? key % N : 0;
     }
+    const unsigned long long hb = __ballot(head);
+    unsigned long long peers = hb;
+    for (int bit = 0; bit < nbits; ++bit) {
+      const bool bset = (o >> bit) & 1;
+      const unsigned long long bal = __ballot(bset);
+      peers &= bset ? bal : ~bal;
+    }
+    if (head && (peers & lt) == 0) atomicAdd(&h[o], __popcll(peers));   // the owner group's leader
+    if (lane == 0) nh += __popcll(hb);
   }
-  atomicAdd(&h[N], nh);
+  if (lane == 0) atomicAdd(&h[N], nh);
   __syncthreads();
   if (tid <= N) tcnt[blockIdx.x * (N + 1) + tid] = h[tid];
 }
@@ -451,7 +464,7 @@ HFM_API int hfm_sh_route(const int* sorted_keys, int n, int N, int C, int* tcnt,
   const int nt = hfm_sh_route_tiles(n);
   int nbits = 0;
   while ((1 << nbits) < N) ++nbits;
-  hipLaunchKernelGGL(sh_route_count_kernel, dim3(nt), dim3(SH_THREADS), 0, st, sorted_keys, n, N, tcnt);
+  hipLaunchKernelGGL(sh_route_count_kernel, dim3(nt), dim3(SH_THREADS), 0, st, sorted_keys, n, N, nbits, tcnt);
   hipLaunchKernelGGL(sh_route_scatter_kernel, dim3(nt), dim3(SH_THREADS), 0, st, sorted_keys, n, N, nbits, C,
                      tcnt, nt, sid_incl, send_ids, upos, send_cnt, num_u, err);
   HFM_LAUNCH_CHECK();
