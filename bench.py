@@ -384,7 +384,7 @@ def infer_bench(args):
                          batch_size=B, device=dev, field_ranges=synth.field_ranges(),
                          mlp_dtype=args.mlp_dtype)
     _progress()
-    P = max(16, min(args.pool, 64))
+    P = 16 * max(1, min(args.pool, 64) // 16)      # whole 16-request graphs
     reqs = [synth.batch(B, step=500_000 + i, device=dev, id_dtype=torch.int32) for i in range(P)]
     out = torch.zeros(P, B, device=dev)
 
