@@ -417,6 +417,7 @@ __global__ void __launch_bounds__(256) sfwg_kernel(SfArgs A, WgFinArgs W, unsign
     sf_tile_body<K, 0, OPT>(A, (int)blockIdx.x - nw, sm.sf);
   } else if (SWEEP) {
     const int sb = (int)blockIdx.x - nw - ntile;
+    // (2 rows per thread per pass: 98 VGPRs, 0.1596-0.1598 vs 0.1565-0.1619 ms -- no gain)
     tf1_sweep_rows<K, OPT, 1>(S.rec, S.ld, S.R, S.flags, A.h, sf_lr_t<OPT>(A),
                               (long)sb * blockDim.x + threadIdx.x, (long)S.nblk * blockDim.x);
   }
