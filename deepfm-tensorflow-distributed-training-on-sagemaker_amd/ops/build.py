@@ -35,6 +35,9 @@ IO_SO = os.path.join(LIB_DIR, "libhipfm_io.so")
 # (tools/det5.py: the FM logit of 2 adjacent samples off by ~1e-5, a different pair every
 # run; tower_kernel's gather reduction, and training was not bitwise reproducible).  Without
 # the packed ops the same code is exact and deterministic (tests/test_gpu_determinism.py).
+# (hipcc also hands the feature to the x86 host pass, which prints "'-packed-fp32-ops' is not a
+# recognized feature for this target (ignoring feature)": expected and harmless; -Xarch_device
+# cannot forward -Xclang pairs.)
 NO_PACKED_F32 = ["-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops"]
 
 
