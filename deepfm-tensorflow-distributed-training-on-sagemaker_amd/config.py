@@ -102,7 +102,8 @@ _DEFS = [
     ("eval_throttle_secs", float, 1200.0, "ps schedule: at most one evaluation per this many seconds "
      "(PS:441)"),
     ("time_check_steps", int, 20, "steps between the (rank-agreed) checks of time-based triggers"),
-    ("graph_steps", int, 8, "consecutive steps over the HBM-cached epoch captured per HIP graph"),
+    ("graph_steps", int, 32, "consecutive steps over the HBM-cached epoch captured per HIP graph "
+     "(Kaggle-shape CLI run: 32 -> 6,121 vs 8 -> 5,992 steps/s)"),
     ("field_sizes", str, "", "csv per-field vocabulary sizes (fields own consecutive id ranges): "
      "enables the per-field slot sort; empty: derived from the first cached epoch when possible"),
     ("pred_path", str, "", "predictions output file (default <val_data_dir>/pred.txt, Q9)"),
@@ -168,7 +169,7 @@ class RunConfig:
     eval_start_delay_secs: float = 1000.0
     eval_throttle_secs: float = 1200.0
     time_check_steps: int = 20
-    graph_steps: int = 8
+    graph_steps: int = 32
     field_sizes: str = ""
     pred_path: str = ""
     export_tf_bundle: bool = True
