@@ -31,21 +31,31 @@ if REPO not in sys.path:
 METRIC = ("samples/sec (whole node) + eval AUC, Criteo-1TB-shape DeepFM at 1/2/4/8 MI355X")
 
 # Multi-GPU execution ladder (bench supervisor, below): the fastest path first, then paths with
-# fewer moving parts.  Every rung is the same full training step (same model, optimizer, data).
-# The step's collective pattern of round 1 (separate dense all-reduce on its own stream, 7-launch
-# routing, rows served in-step) is the fallback when the fused exchange (grouped all-to-all +
-# all-gather, rows served ahead) fails.
-_R1_EXCHANGE = {"HIPFM_SH_XFUSE": "0", "HIPFM_SH_APPLY_DENSE": "0", "HIPFM_SH_ROUTE2": "0",
-                "HIPFM_SH_SERVE_AHEAD": "0"}
-# 1-rank proxy (--force_exchange), ms/step: 0.178 / 0.192 / 0.199 / 0.289 / 0.274.  A capture
-# failure is the likeliest multi-GPU surprise, so the fused exchange launched eagerly comes second.
+# fewer moving parts.  Every rung is the same full training step (same model, optimizer, data),
+# and in EVERY rung all collectives of a step run on one communicator, grouped, on the step's
+# main stream in a fixed order (parallel/sharded.py) -- no rung has side-stream collectives.
+# A capture failure is the likeliest multi-GPU surprise, so the same step launched eagerly comes
+# second; the last rung drops the routing prefetch and the fused dense exchange (dense all-reduce
+# in the gradient group, 7-launch routing).
+_PLAIN_EXCHANGE = {"HIPFM_SH_XFUSE": "0", "HIPFM_SH_APPLY_DENSE": "0", "HIPFM_SH_ROUTE2": "0"}
 LADDER = [
     ("graph+prefetch", {}),                                  # HIP graphs, next-batch routing prefetch
-    ("eager+prefetch+fused", {"HIPFM_BENCH_NO_GRAPH": "1"}),  # same step, launched eagerly
-    ("graph+prefetch+allreduce", dict(_R1_EXCHANGE)),        # graphs, dense all-reduce on a comm stream
-    ("eager+prefetch", {"HIPFM_BENCH_NO_GRAPH": "1", **_R1_EXCHANGE}),   # launched eagerly
-    ("eager", {"HIPFM_BENCH_NO_GRAPH": "1", "HIPFM_SHARD_PIPELINE": "0", **_R1_EXCHANGE}),
+    ("eager+prefetch", {"HIPFM_BENCH_NO_GRAPH": "1"}),       # same step, launched eagerly
+    ("eager", {"HIPFM_BENCH_NO_GRAPH": "1", "HIPFM_SHARD_PIPELINE": "0", **_PLAIN_EXCHANGE}),
 ]
+# hang detection: a rung's child must write its first progress mark within FIRST_S (the parent
+# supervisor already imported torch, so the child's imports hit a warm page cache) and then
+# update it at least every HANG_S (every graph run / step chunk marks progress)
+FIRST_S = 90.0
+HANG_S = 45.0
+
+
+def ladder_budget_s(rungs: int = len(LADDER), first_s: float = FIRST_S, hang_s: float = HANG_S,
+                    setup_s: float = 60.0) -> float:
+    """Worst-case wall time of a ladder whose every rung hangs: per rung, the child reaches its
+    last progress mark after at most ``setup_s`` (model + communicator setup, measured well under
+    that) or never marks (``first_s``), then ``hang_s`` of silence -- plus the teardown."""
+    return rungs * (max(first_s, setup_s + hang_s) + 5.0)
 
 
 def _free_port() -> int:
@@ -76,7 +86,8 @@ def supervise(argv) -> int:
     world = int(os.environ["WORLD_SIZE"])
     store = dist.TCPStore(os.environ.get("MASTER_ADDR", "127.0.0.1"), int(os.environ["MASTER_PORT"]),
                           world, is_master=False, timeout=__import__("datetime").timedelta(seconds=600))
-    hang_s = float(os.environ.get("HIPFM_BENCH_HANG_S", "150"))
+    hang_s = float(os.environ.get("HIPFM_BENCH_HANG_S", str(HANG_S)))
+    first_s = float(os.environ.get("HIPFM_BENCH_FIRST_S", str(FIRST_S)))
     ladder = LADDER[int(os.environ.get("HIPFM_BENCH_FIRST_RUNG", "0")):]
     for k, (name, extra) in enumerate(ladder):
         if rank == 0:
@@ -90,7 +101,8 @@ def supervise(argv) -> int:
         child = subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env,
                                  start_new_session=True)
         failed = False
-        last = time.time()
+        t_start = time.time()
+        last = None
         while True:
             rc = child.poll()
             if rc is not None:
@@ -100,11 +112,14 @@ def supervise(argv) -> int:
                 failed = True
                 break
             try:
-                last = max(last, os.path.getmtime(prog))
+                mt = os.path.getmtime(prog)
+                last = mt if last is None else max(last, mt)
             except OSError:
                 pass
-            if time.time() - last > hang_s:
-                print(f"[bench rank {rank}] rung {name}: no progress for {hang_s:.0f}s", flush=True)
+            now = time.time()
+            if (last is None and now - t_start > first_s) or (last is not None and now - last > hang_s):
+                print(f"[bench rank {rank}] rung {name}: no progress for "
+                      f"{(now - t_start) if last is None else (now - last):.0f}s", flush=True)
                 failed = True
                 break
             time.sleep(0.5)
@@ -269,8 +284,7 @@ def main():
 
     def run(lo, hi):
         for k, (t, e) in enumerate(chunks(lo, hi)):
-            if k % 8 == 0:
-                _progress()
+            _progress()
             i = t % P
             nxt = pool[e % P][0]                      # next batch: its sort / routing is prefetched
             if use_graph and G > 1:
@@ -504,8 +518,9 @@ def data_bench(args):
 
 
 def _fake_child(args, spec):
-    """CPU stand-in for a bench child (tests of the supervisor): ``spec`` = '<rung>:<rank>:<fail|hang>'
-    entries separated by commas make that rank fail / hang in that rung; others print a line."""
+    """CPU stand-in for a bench child (tests of the supervisor): ``spec`` =
+    '<rung>:<rank>:<fail|hang|stall>' entries separated by commas make that rank fail, hang before
+    its first progress mark, or stall after one, in that rung; others print a line."""
     import time
     rank = int(os.environ.get("RANK", "0"))
     rung = os.environ.get("HIPFM_BENCH_RUNG", "")
@@ -514,7 +529,9 @@ def _fake_child(args, spec):
         if r_name == rung and int(r_rank) == rank:
             if what == "fail":
                 sys.exit(3)
-            while True:             # hang without progress
+            if what == "stall":
+                _progress()
+            while True:             # hang without (further) progress
                 time.sleep(1)
     _progress()
     if rank == 0:

@@ -356,6 +356,7 @@ struct Loader {
   std::vector<std::string> paths;
   int format = 0, F = 0, B = 0, drop_remainder = 1, verify = 1;
   int shard_n = 1, shard_i = 0;   // record-level shard (1 = off)
+  int64_t id_limit = 0;            // > 0: every id must lie in [0, id_limit) (feature_size V)
   int depth = 4;
   int chunk = 1024;
   std::vector<std::unique_ptr<WorkerQueue>> queues;
@@ -401,6 +402,7 @@ struct Loader {
         fail("cannot open " + paths[fi]);
         return;
       }
+      long long frec = -1;   // record index within this file (every record, sharded or not)
       while (!stop.load()) {
         float* lab = c->label.data() + c->n;
         int64_t* ids = c->ids.data() + (size_t)c->n * F;
@@ -413,6 +415,7 @@ struct Loader {
             fail(g_err);
             return;
           }
+          ++frec;
           if (shard_n > 1 && (rec++ % shard_n) != shard_i) continue;
           okrec = decode_example(buf.data(), buf.size(), F, lab, ids, vals);
           if (!okrec) {
@@ -422,10 +425,23 @@ struct Loader {
         } else {
           if (!r.getline(line)) break;
           if (line.find_first_not_of(" \t\r") == std::string::npos) continue;
+          ++frec;
           if (shard_n > 1 && (rec++ % shard_n) != shard_i) continue;
           if (!parse_libsvm(line, F, lab, ids, vals)) {
             fail("bad libsvm line (expected label + " + std::to_string(F) + " id:val) in " + paths[fi]);
             return;
+          }
+        }
+        if (id_limit > 0) {
+          // the device gathers / updates table rows by id unchecked: reject out-of-vocabulary
+          // ids here, where the file and record are known (TF's CPU gather raises likewise)
+          for (int f = 0; f < F; ++f) {
+            if (ids[f] < 0 || ids[f] >= id_limit) {
+              fail("feature id " + std::to_string((long long)ids[f]) + " (field " + std::to_string(f) +
+                   ") outside [0, feature_size=" + std::to_string((long long)id_limit) + ") in " +
+                   paths[fi] + " record " + std::to_string(frec));
+              return;
+            }
           }
         }
         if (++c->n == chunk) {
@@ -521,8 +537,9 @@ struct Loader {
 
 HFMIO_API void* hfmio_loader_create(const char** paths, int npaths, int format, int F, int batch,
                                     int drop_remainder, int num_threads, int shard_n, int shard_i,
-                                    int verify_crc, int queue_depth) {
+                                    int verify_crc, int queue_depth, int64_t id_limit) {
   auto* L = new Loader();
+  L->id_limit = id_limit;
   for (int i = 0; i < npaths; ++i) L->paths.emplace_back(paths[i]);
   L->format = format;
   L->F = F;

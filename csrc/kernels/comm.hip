@@ -85,3 +85,40 @@ HFM_API int hfm_comm_allgather(void* comm, const void* send, void* recv, size_t 
     return nccl_rc(ncclAllGather(send, recv, bytes_per_rank / 4, ncclInt32, (ncclComm_t)comm, st));
   return nccl_rc(ncclAllGather(send, recv, bytes_per_rank, ncclInt8, (ncclComm_t)comm, st));
 }
+
+// One step's collectives as ONE aggregated RCCL operation (group), issued on the caller's stream.
+// The row-sharded step issues every collective it has through this entry, on its main stream and
+// on ONE communicator, at fixed points of the step: the sequence of groups is then the same on
+// every rank by construction (no concurrent operations on different communicators, no ordering
+// that depends on how graph branches are scheduled onto hardware queues -- the deadlock shape
+// RCCL only rules out for a consistent issue order).
+// kind 0: all-to-all, `bytes` per peer; 1: all-gather, `bytes` per rank; 2: f32 sum all-reduce
+// in place (send == recv allowed), `bytes` in total.
+struct CommOp {
+  int kind;
+  int pad;
+  const void* send;
+  void* recv;
+  size_t bytes;
+};
+
+HFM_API int hfm_comm_group(void* comm, const CommOp* ops, int nops, hipStream_t st) {
+  for (int i = 0; i < nops; ++i)
+    if (ops[i].bytes % 4 || ops[i].kind < 0 || ops[i].kind > 2) return (int)hipErrorInvalidValue;
+  ncclResult_t r = ncclGroupStart();
+  if (r != ncclSuccess) return nccl_rc(r);
+  const ncclComm_t c = (ncclComm_t)comm;
+  for (int i = 0; i < nops && r == ncclSuccess; ++i) {
+    const CommOp& o = ops[i];
+    if (o.bytes == 0) continue;
+    if (o.kind == 0)
+      r = ncclAllToAll(o.send, o.recv, o.bytes / 4, ncclInt32, c, st);
+    else if (o.kind == 1)
+      r = ncclAllGather(o.send, o.recv, o.bytes / 4, ncclInt32, c, st);
+    else
+      r = ncclAllReduce(o.send, o.recv, o.bytes / 4, ncclFloat32, ncclSum, c, st);
+  }
+  const ncclResult_t e = ncclGroupEnd();
+  return nccl_rc(r != ncclSuccess ? r : e);
+}
+

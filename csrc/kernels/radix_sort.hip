@@ -221,15 +221,26 @@ constexpr int OS_MAX_PASSES = 4;
 constexpr int OS_HIST_BLOCKS = 128;
 }  // namespace
 
+// key_lim > 0: a key outside [0, key_lim) is counted (and, in pass 0, sorted) as key_lim - 1 and
+// sets *key_err -- the sorted ids then index the table in bounds and the host raises on the flag
+__device__ __forceinline__ int os_clamp(int k, unsigned lim) {
+  return (lim && (unsigned)k >= lim) ? (int)(lim - 1) : k;
+}
+
 __global__ void __launch_bounds__(RS_THREADS) os_hist_kernel(const int* __restrict__ keys, int n,
-                                                            int passes, unsigned* __restrict__ ghist) {
+                                                            int passes, unsigned* __restrict__ ghist,
+                                                            unsigned key_lim, unsigned* __restrict__ key_err) {
   __shared__ unsigned h[OS_MAX_PASSES][RS_RADIX];
   for (int p = 0; p < OS_MAX_PASSES; ++p) h[p][threadIdx.x] = 0;
   __syncthreads();
+  bool bad = false;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    const int k = keys[i];
+    const int k0 = keys[i];
+    const int k = os_clamp(k0, key_lim);
+    bad |= k != k0;
     for (int p = 0; p < passes; ++p) atomicAdd(&h[p][(k >> (p * RS_BITS)) & (RS_RADIX - 1)], 1u);
   }
+  if (__any(bad) && (threadIdx.x & 63) == 0 && key_err) atomicOr(key_err, 1u);
   __syncthreads();
   for (int p = 0; p < passes; ++p)
     if (h[p][threadIdx.x]) atomicAdd(&ghist[p * RS_RADIX + threadIdx.x], h[p][threadIdx.x]);
@@ -270,7 +281,7 @@ __global__ void __launch_bounds__(RS_THREADS) os_pass_kernel(
     const int* __restrict__ keys_in, const int* __restrict__ vals_in, int* __restrict__ keys_out,
     int* __restrict__ vals_out, int n, int shift, const unsigned* __restrict__ ghist_p,
     unsigned* __restrict__ status, unsigned* __restrict__ ticket, unsigned* __restrict__ err,
-    int debug_nolb) {
+    int debug_nolb, unsigned key_lim) {
   constexpr int TILE = RS_THREADS * IT;
   __shared__ int whist[4][RS_RADIX];
   __shared__ int lbase[RS_RADIX];
@@ -290,7 +301,7 @@ __global__ void __launch_bounds__(RS_THREADS) os_pass_kernel(
 #pragma unroll
   for (int k = 0; k < IT; ++k) {
     const int i = w0 + k * 64 + lane;
-    kr[k] = i < n ? keys_in[i] : -1;
+    kr[k] = i < n ? os_clamp(keys_in[i], key_lim) : -1;
     vr[k] = i < n ? (vals_in ? vals_in[i] : i) : 0;
   }
   const unsigned long long lt = (1ull << lane) - 1ull;
@@ -398,8 +409,10 @@ HFM_API int hfm_onesweep_temp_bytes(int n, size_t* bytes) {
 }
 
 HFM_API int hfm_onesweep_sort_ids(const int* keys_in, int* keys_out, int* perm_out, int n, int end_bit,
-                                  void* temp, size_t temp_bytes, hipStream_t st) {
+                                  void* temp, size_t temp_bytes, unsigned key_lim, unsigned* key_err,
+                                  hipStream_t st) {
   if (n <= 0) return 0;
+  if (key_lim && key_lim - 1 >= (1u << end_bit)) return (int)hipErrorInvalidValue;
   const int tiles = os_tiles(n);
   const int passes = (end_bit + RS_BITS - 1) / RS_BITS;
   if (passes > OS_MAX_PASSES) return (int)hipErrorInvalidValue;
@@ -427,7 +440,8 @@ HFM_API int hfm_onesweep_sort_ids(const int* keys_in, int* keys_out, int* perm_o
   }
   int hg = (n + RS_THREADS - 1) / RS_THREADS;
   if (hg > OS_HIST_BLOCKS) hg = OS_HIST_BLOCKS;
-  hipLaunchKernelGGL(os_hist_kernel, dim3(hg), dim3(RS_THREADS), 0, st, keys_in, n, passes, ghist);
+  hipLaunchKernelGGL(os_hist_kernel, dim3(hg), dim3(RS_THREADS), 0, st, keys_in, n, passes, ghist, key_lim,
+                     key_err);
   const int* ki = keys_in;
   const int* vi = nullptr;
   for (int p = 0; p < passes; ++p) {
@@ -436,7 +450,7 @@ HFM_API int hfm_onesweep_sort_ids(const int* keys_in, int* keys_out, int* perm_o
     int* vo = to_out ? perm_out : pv;
     hipLaunchKernelGGL(os_pass_kernel<OS_ITEMS>, dim3(tiles), dim3(RS_THREADS), 0, st, ki, vi, ko, vo, n,
                        p * RS_BITS, ghist + p * RS_RADIX, status + (size_t)p * tiles * RS_RADIX,
-                       tickets + p, err, debug_nolb);
+                       tickets + p, err, debug_nolb, p == 0 ? key_lim : 0u);
     ki = ko;
     vi = vo;
   }

@@ -80,6 +80,8 @@ struct TowerArgs {
   bf16* Et;                       // [K0p, M] (train: wgrad operand)
   int idx_ld;                     // 0: idx row-major [M, F]; else field-major [F, idx_ld] (the
                                   // layout the per-field sort reads, so it needs no transpose)
+  unsigned id_lim;                // > 0: gathered row ids clamped to [0, id_lim) (a bad id never
+                                  // reads out of bounds; the slot sort flags it for the host)
 };
 
 // fp8 variant of mma32 (16x16x32 fp8 MFMA; same fragment map as bf16 with 8 one-byte elements
@@ -188,6 +190,7 @@ __device__ __forceinline__ void tower_gather(const TowerArgs& a, int row0, bf16*
     for (int t = 0; t < FMAX; ++t) {
       const int f = f0 + 8 * t;
       id[t] = f < F ? a.idx[a.idx_ld ? (size_t)f * a.idx_ld + b : (size_t)b * F + f] : 0;
+      if (a.id_lim && (unsigned)id[t] >= a.id_lim) id[t] = (int)a.id_lim - 1;
       x[t] = f < F ? a.vals[(size_t)b * F + f] : 0.f;
     }
     f32x4 v[FMAX][V4];

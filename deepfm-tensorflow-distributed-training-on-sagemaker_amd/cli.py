@@ -26,7 +26,7 @@ import torch.distributed as dist
 
 from .config import RunConfig, parse_flags
 from .data.pipeline import InputPipeline, discover_files, shard_spec
-from .estimator import Estimator
+from .estimator import Estimator, PositionedBatch
 
 
 def _channels() -> List[str]:
@@ -61,7 +61,7 @@ def build_pipelines(cfg: RunConfig, est: Estimator):
     dev = est.device if est.native else None
     id_dtype = torch.int32 if est.native else torch.int64
     common = dict(fmt=fmt, seed=cfg.seed, threads=max(1, min(os.cpu_count() or 1, cfg.num_threads)),
-                  device=dev, id_dtype=id_dtype)
+                  device=dev, id_dtype=id_dtype, id_limit=cfg.feature_size)
     if cfg.pipe_mode:
         ch = _channels()
         tr_ch = cfg.training_channel_name or (ch[1 + local_rank] if len(ch) > 1 + local_rank else "training")
@@ -128,13 +128,21 @@ def run(cfg: RunConfig) -> dict:
                 first, skip = 0, 0
 
             def all_epochs():
+                # every batch carries the data position AFTER it (PositionedBatch): the Estimator
+                # reads more than one batch ahead (graph runs), so the generator's own progress
+                # is not the trained position
                 for epoch in range(first, cfg.num_epochs):
-                    est.epoch, est.epoch_batch = epoch, (skip if epoch == first else 0)
-                    view = _EpochView(pipe, epoch, est.epoch_batch)
+                    k = skip if epoch == first else 0
+                    view = _EpochView(pipe, epoch, k)
                     est._enforce_equal_steps(view)
-                    yield from view
+                    it = iter(view)
+                    b = next(it, None)
+                    while b is not None:
+                        nb = next(it, None)
+                        yield PositionedBatch(b, (epoch, k + 1) if nb is not None else (epoch + 1, 0))
+                        k += 1
+                        b = nb
                     est.adopt_field_ranges(pipe)
-                est.epoch, est.epoch_batch = cfg.num_epochs, 0
 
             class _Run:                  # the whole run as one batch source (cache flag visible)
                 countable = True

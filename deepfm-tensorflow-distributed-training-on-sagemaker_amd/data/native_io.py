@@ -37,7 +37,7 @@ def lib():
             L.hfmio_decode_example.argtypes = [vp, C.c_size_t, ci, vp, vp, vp]
             L.hfmio_decode_example.restype = ci
             L.hfmio_loader_create.argtypes = [C.POINTER(C.c_char_p), ci, ci, ci, ci, ci, ci, ci, ci,
-                                              ci, ci]
+                                              ci, ci, C.c_int64]
             L.hfmio_loader_create.restype = vp
             L.hfmio_loader_next.argtypes = [vp, vp, vp, vp]
             L.hfmio_loader_next.restype = ci
@@ -124,18 +124,21 @@ class NativeLoader:
 
     ``record_shard=(n, i)`` reproduces ``dataset.shard(n, i)`` on the concatenated record
     stream (reference semantics); without it the files are read in parallel by ``threads``
-    workers with a deterministic round-robin interleave of 1024-record chunks."""
+    workers with a deterministic round-robin interleave of 1024-record chunks.
+    ``id_limit`` (> 0, the table size V): a record with an id outside [0, V) fails the read with
+    an error naming the file and the record index (the device gathers rows unchecked)."""
 
     def __init__(self, paths: Sequence[str], field_size: int, batch_size: int,
                  fmt: int = FMT_TFRECORD, drop_remainder: bool = True, threads: int = 4,
                  record_shard: Tuple[int, int] = (1, 0), verify_crc: bool = True,
-                 queue_depth: int = 4):
+                 queue_depth: int = 4, id_limit: int = 0):
         self.paths = [str(p) for p in paths]
         self.F, self.B = int(field_size), int(batch_size)
         arr = (C.c_char_p * max(1, len(self.paths)))(*[p.encode() for p in self.paths])
         self._h = lib().hfmio_loader_create(arr, len(self.paths), fmt, self.F, self.B,
                                             1 if drop_remainder else 0, threads, record_shard[0],
-                                            record_shard[1], 1 if verify_crc else 0, queue_depth)
+                                            record_shard[1], 1 if verify_crc else 0, queue_depth,
+                                            int(id_limit))
         self._done = False
 
     def next_into(self, labels, ids, vals) -> int:

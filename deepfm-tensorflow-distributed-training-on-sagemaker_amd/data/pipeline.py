@@ -167,6 +167,27 @@ def derive_field_ranges(fmin: torch.Tensor, fmax: torch.Tensor, V: int):
     return list(zip(lo, hi))
 
 
+def agreed_field_ranges(pipeline, V: int, world: int = 1, group=None):
+    """Per-field id ranges every rank agrees on: the per-field min / max ids of each rank's cached
+    shard are combined with MIN / MAX all-reduces (``group``: a host-side gloo group) before
+    ``derive_field_ranges`` -- so no rank's ids fall outside the ranges it sorts with.  None on
+    every rank when any rank has no cached epoch or the combined ranges are not disjoint."""
+    mm = pipeline.field_minmax() if hasattr(pipeline, "field_minmax") else None
+    if world > 1:
+        import torch.distributed as dist
+        have = torch.tensor([0 if mm is None else 1], dtype=torch.int64)
+        dist.all_reduce(have, op=dist.ReduceOp.MIN, group=group)
+        if int(have.item()) == 0:
+            return None
+        mn, mx = mm[0].clone(), mm[1].clone()
+        dist.all_reduce(mn, op=dist.ReduceOp.MIN, group=group)
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX, group=group)
+        mm = (mn, mx)
+    if mm is None:
+        return None
+    return derive_field_ranges(mm[0], mm[1], V)
+
+
 class InputPipeline:
     """Epoch-aware batch source (the reference's ``input_fn``, PS:76-133 / HVD:74-133)."""
 
@@ -174,7 +195,7 @@ class InputPipeline:
                  fmt: str = "tfrecord", shard: Tuple[int, int] = (1, 0), policy: str = "file",
                  seed: int = 0, shuffle_files: bool = True, threads: int = 4, cache: bool = False,
                  device=None, drop_remainder: bool = True, pipe_channel: Optional[str] = None,
-                 id_dtype=torch.int64):
+                 id_dtype=torch.int64, id_limit: int = 0):
         self.files = list(files)
         self.F, self.B = int(field_size), int(batch_size)
         self.num_epochs = max(1, int(num_epochs))
@@ -190,6 +211,7 @@ class InputPipeline:
         self.drop_remainder = drop_remainder
         self.pipe_channel = pipe_channel
         self.id_dtype = id_dtype
+        self.id_limit = int(id_limit)            # > 0: ids must lie in [0, V) (checked by the loader)
         self._cached: Optional[List[Tuple[torch.Tensor, ...]]] = None
         self.max_batches: Optional[int] = None   # equal-steps enforcement across ranks
         self.from_cache = False                  # the epoch being iterated replays the cache
@@ -237,7 +259,7 @@ class InputPipeline:
         self.from_cache = False
         plan = self.epoch_plan(epoch)
         loader = NativeLoader(plan.files, self.F, self.B, self.fmt, self.drop_remainder,
-                              self.threads, plan.record_shard)
+                              self.threads, plan.record_shard, id_limit=self.id_limit)
         store = [] if (self.cache and skip == 0) else None
         on_gpu = self.device is not None and torch.device(self.device).type == "cuda"
         src = (_DeviceFeeder(loader, self.F, self.B, torch.device(self.device), self.id_dtype)
@@ -266,12 +288,19 @@ class InputPipeline:
         if store is not None:
             self._cached = store
 
-    def field_ranges(self, V: int):
-        """Per-field id ranges derived from the cached epoch (None before it is cached, or when
-        the fields' ids are not disjoint and increasing)."""
+    def field_minmax(self):
+        """(per-field min ids, per-field max ids) over the cached epoch as CPU int64 tensors, or
+        None before an epoch was cached."""
         if self._fmin is None:
             return None
-        return derive_field_ranges(self._fmin.cpu(), self._fmax.cpu(), V)
+        return self._fmin.cpu().long(), self._fmax.cpu().long()
+
+    def field_ranges(self, V: int):
+        """Per-field id ranges derived from the cached epoch (None before it is cached, or when
+        the fields' ids are not disjoint and increasing).  This rank's shard only; the Estimator
+        combines every rank's min / max first."""
+        mm = self.field_minmax()
+        return None if mm is None else derive_field_ranges(mm[0], mm[1], V)
 
     @property
     def cached_batches(self) -> int:

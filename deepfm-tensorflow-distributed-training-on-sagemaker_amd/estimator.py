@@ -52,6 +52,17 @@ def resolve_device(cfg: RunConfig):
     return torch.device("cpu")
 
 
+class PositionedBatch(tuple):
+    """(ids, vals, labels) plus ``pos`` = the data position (epoch, batches of that epoch done)
+    once this batch is trained: set on the Estimator after the batch's step, so a checkpoint
+    records what was trained even when the source is read ahead."""
+
+    def __new__(cls, batch, pos):
+        t = super().__new__(cls, tuple(batch))
+        t.pos = (int(pos[0]), int(pos[1]))
+        return t
+
+
 @dataclass
 class TrainSpec:
     input_fn: Callable[[], Iterable]
@@ -153,6 +164,7 @@ class Estimator:
         t0 = time.perf_counter()
         if self.native:
             torch.cuda.synchronize(self.device)
+            self.model.check_errors()        # never publish a checkpoint of a flagged step
         with prof_range("checkpoint"):
             path = self.ckpt.save(self.global_step, self._state(), self._meta())
         self.timer.add("ckpt", time.perf_counter() - t0)
@@ -337,6 +349,7 @@ class Estimator:
                     nxt = self._next(it)
             t0 = time.perf_counter()
             B = int(run[0][0].shape[0])
+            pos = getattr(run[-1], "pos", None)      # data position after this run (if tagged)
             if self.native:
                 if not run[0][0].is_cuda:
                     t1 = time.perf_counter()
@@ -354,20 +367,27 @@ class Estimator:
                         self.model.train_step(ids, vals, labels, use_graph=use_graph,
                                               next_ids=nxt_ids if from_cache else None,
                                               stage=not from_cache)
+                # device error words (bad ids, capacity overflow, hand-off failures): copied
+                # asynchronously after every call, raised on at the next one
+                self.model.poll_errors()
                 if cfg.debug_sync:
                     torch.cuda.synchronize(self.device)
+                    self.model.check_errors()
                     self._nan_check()
             else:
                 for ids, vals, labels in run:
                     self.model.train_step(ids, vals, labels, grad_sync=self._golden_grad_sync)
             self.timer.add("step_enqueue", time.perf_counter() - t0)
             prev = self.global_step - len(run)
-            self.epoch_batch += len(run)
+            if pos is not None:
+                self.epoch, self.epoch_batch = pos
+            else:
+                self.epoch_batch += len(run)
             n_log += B * len(run)
             step = self.global_step
             wd.beat(step)
             window.step(step)
-            maybe_inject_fault(step, self.rank)
+            maybe_inject_fault(step, self.rank, prev)
             crossed = lambda every: bool(every) and step // every > prev // every  # noqa: E731
             if crossed(cfg.log_steps):
                 if self.native:
@@ -398,22 +418,25 @@ class Estimator:
             cur = nxt
         if self.native:
             torch.cuda.synchronize(self.device)
+            self.model.check_errors()
         wd.stop()
         return self.global_step - start_step
 
     def adopt_field_ranges(self, pipeline) -> bool:
         """After the first epoch was cached: per-field id ranges derived from it switch the slot
         sort to the per-field LDS sort (when the fields' ids are disjoint and increasing; with
-        --field_sizes they are known from the start).  Returns True if the model took them."""
-        if not self.native or self.model.field_ranges is not None or self.model.sharded:
+        --field_sizes they are known from the start).  Returns True if the model took them.
+        Every rank trains on its own shard, so the per-field min / max ids are combined over ALL
+        ranks (MIN / MAX all-reduce) before the ranges are derived: ranges from one rank's shard
+        could miss ids another rank sees.  The decision is then identical on every rank."""
+        if not self.native or self.model.field_ranges is not None:
             return False
-        r = pipeline.field_ranges(self.cfg.feature_size) if hasattr(pipeline, "field_ranges") else None
-        if self.world > 1:   # every rank must take the same decision (and the same ranges)
-            objs = [r]
-            dist.broadcast_object_list(objs, src=0, group=self._ctl)
-            r = objs[0]
+        from .data.pipeline import agreed_field_ranges
+        r = agreed_field_ranges(pipeline, self.cfg.feature_size, self.world, self._ctl)
         if r is None:
             return False
+        # earlier graph replays may still read the sort buffers this replaces
+        torch.cuda.synchronize(self.device)
         self.model.set_field_ranges(r)
         self.log.info("per-field id ranges derived from the cached epoch: per-field slot sort on")
         return True
@@ -433,6 +456,8 @@ class Estimator:
 
     def _evaluate(self, batches: Iterable, steps: Optional[int] = None) -> dict:
         dev = self.device if self.native else torch.device("cpu")
+        if self.native:
+            self.model.check_errors()
         hist = torch.zeros(2, 201, dtype=torch.int64, device=dev)
         loss_sum = torch.zeros(1, dtype=torch.float64, device=dev)
         n = torch.zeros(1, dtype=torch.float64, device=dev)

@@ -340,6 +340,14 @@ class NativeDeepFM:
             self._w8_rows = row0
         self.h_sparse = KN.hyper(self.lr, self.l2, eps=adam_epsilon)
         self.h_dense = KN.hyper(self.lr, 0.0, eps=adam_epsilon)
+        # device-side error words (sticky; one D2H copy reads them all, see poll_errors):
+        #   0 / 1  per-field sort (this / next batch): an id outside its field's range
+        #   2      row-sharded exchange: a bucket overflowed its per-peer capacity
+        #   3      global slot sort / routing: an id outside [0, V) (clamped, so nothing faults)
+        #   4..7   sparse backward hand-off words (sf_sync; [6] = error bits)
+        self.err_words = torch.zeros(16, dtype=torch.int32, device=dev)
+        self._err_host = torch.zeros(16, dtype=torch.int32, pin_memory=dev.type == "cuda")
+        self._err_ev = None
         self._bufs_M = 0
         self._side = None
         self._side_next = None
@@ -355,7 +363,9 @@ class NativeDeepFM:
         self._fuse_opt = False     # dense optimizer fused into the finalize launch (this step)
         self._sfwg_now = False     # ... and that launch merged into the sparse backward (this step)
         self._sfwg_step = False
-        self._sh_dense_join = None
+        self._sh_join = None
+        self._sh_apply_dense = False
+        self._sh_ar = False
         self._sh_xfuse = False
         self._idsT_B = 0
         self.batch_size = int(batch_size)
@@ -516,7 +526,8 @@ class NativeDeepFM:
         # publication flags (tagged with the step index) and error bits; zeroed whenever the
         # step counter is rewritten (_reset_sync)
         self.sf_flags = torch.zeros(nt, **i32)
-        self.sf_sync = torch.zeros(4, **i32)
+        self.sf_sync = self.err_words[4:8]
+        self.sf_sync.zero_()
         self._fsort = None
         self._fsort_next = None
         # sorted-slot sets: set c holds the sort of the batch this step trains, set 1 - c receives
@@ -542,10 +553,7 @@ class NativeDeepFM:
         self.shx = None
         if self.sharded and getattr(self.comm, "engine", None) is not None:
             from ..parallel.sharded import FixedCapacityExchange
-            self.shx = FixedCapacityExchange(self, self.comm.engine, self.comm.capacity,
-                                             engine_route=getattr(self.comm, "engine_route", None))
-            if self.shx.eng_route is None and not hasattr(self.comm, "route_engine"):
-                self.shx.eng_route = self.comm.engine
+            self.shx = FixedCapacityExchange(self, self.comm.engine, self.comm.capacity)
         self._own_in = (self.idx, self.vals, self.labels)
         self._graphs = {}
         self._run_memo = {}
@@ -563,10 +571,12 @@ class NativeDeepFM:
         # routing on the sharded step (0.198 ms vs 0.206 with 16; HIPFM_FSORT_PB overrides)
         pb = knob("HIPFM_FSORT_PB")
         self._fsort = KN.FieldSort(self.field_ranges, min(M, KN.field_sort_max_rows()), dev,
-                                   max_pb=int(pb) if pb is not None else (2 if self.sharded else 0))
+                                   max_pb=int(pb) if pb is not None else (2 if self.sharded else 0),
+                                   err=self.err_words[0:1])
         if not self.sharded:
             self._fsort_next = KN.FieldSort(self.field_ranges, min(M, KN.field_sort_max_rows()),
-                                            dev, max_pb=int(pb) if pb is not None else 0)
+                                            dev, max_pb=int(pb) if pb is not None else 0,
+                                            err=self.err_words[1:2])
 
     def set_field_ranges(self, ranges):
         """Per-field id ranges found after construction (e.g. derived while caching the first
@@ -752,6 +762,7 @@ class NativeDeepFM:
             a.F = self.F
             a.S = self.S.data_ptr()
             a.Et = self.Et.data_ptr() if train else 0
+            a.id_lim = tv.shape[0]
         else:
             a.E = self.E.data_ptr()
         if self.fp8:
@@ -1105,20 +1116,46 @@ class NativeDeepFM:
         if self.uses_field_sort(B):
             self._fsort(self.idx, B, self.sorted_keys, self.perm, field_major=self._idx_fm)
         else:
-            KN.sort_ids(self.idx, self.sorted_keys, None, self.perm, n, self.end_bit, self.temp)
+            KN.sort_ids(self.idx, self.sorted_keys, None, self.perm, n, self.end_bit, self.temp,
+                        limit=self.V, err=self.err_words[3:4])
 
-    def check_errors(self):
-        """Raise on device-side input errors flagged by earlier steps (host sync)."""
-        if any(fs is not None and int(fs.err.item()) != 0 for fs in (self._fsort, self._fsort_next)):
+    def _raise_errors(self, w):
+        """Raise on the first set error word of a host copy ``w`` of ``err_words``."""
+        if w[0] or w[1]:
             raise RuntimeError("an id lies outside its field's declared range (field_ranges): "
                                "the per-field sort is invalid for this data")
-        e = int(self.sf_sync[2].item())
-        if e != 0:
-            raise RuntimeError(f"sparse backward hand-off failed (error bits {e:#x}): a look-back "
+        if w[3]:
+            raise RuntimeError(f"a feature id lies outside [0, feature_size={self.V}) (the step "
+                               "clamped it; check the input data)")
+        if w[6]:
+            raise RuntimeError(f"sparse backward hand-off failed (error bits {w[6]:#x}): a look-back "
                                "timed out or read an inconsistent tile publication")
-        if self.shx is not None and self.shx.error() != 0:
-            raise RuntimeError(f"row-sharded exchange: a rank sent more than capacity={self.shx.C} "
+        if w[2]:
+            C = self.shx.C if self.shx is not None else "?"
+            raise RuntimeError(f"row-sharded exchange: a rank sent more than capacity={C} "
                                "unique ids to one owner (raise the capacity)")
+
+    def check_errors(self):
+        """Raise on device-side errors flagged by earlier steps (one host sync)."""
+        self._err_ev = None
+        self._raise_errors(self.err_words.tolist())
+
+    def poll_errors(self):
+        """Asynchronous error check, called after every enqueued step / graph replay: raises on
+        the error words copied after an EARLIER call if that copy has landed, then starts a new
+        non-blocking copy (one small D2H per call, never a host wait).  A bad step is thus
+        reported within a call or two instead of at the next ``log_steps`` sync."""
+        if self.device.type != "cuda":
+            return
+        ev = self._err_ev
+        if ev is not None:
+            if not ev.query():
+                return                   # the previous copy is still in flight: keep it
+            self._raise_errors(self._err_host.tolist())
+        self._err_host.copy_(self.err_words, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self._err_ev = ev
 
     def sf_args(self, n: int) -> SfArgs:
         A = SfArgs()
@@ -1143,9 +1180,11 @@ class NativeDeepFM:
         (returns None).  Multi-rank: returns compact unique-row gradients for the exchange."""
         n = B * self.F
         if self.shx is not None:
-            j = self._sh_dense_join
-            self.shx.backward(self._shx_plan, B, dense=self._sh_dense_args() if j is not None else None,
-                              join=j, wgfin=self._wgfin_args(False) if self._sh_xfuse else None)
+            self.shx.backward(self._shx_plan, B,
+                              dense=self._sh_dense_args() if self._sh_apply_dense else None,
+                              join=self._sh_join,
+                              wgfin=self._wgfin_args(False) if self._sh_xfuse else None,
+                              dense_ar=self.g if self._sh_ar else None)
             return None
         if self.sharded:
             return self.comm.sharded_backward(self, B, idx, tv)
@@ -1339,46 +1378,43 @@ class NativeDeepFM:
         if presorted and inline:
             main.wait_stream(self._side)
         work = None
-        eng = getattr(self.comm, "engine_dense", None) if (self.exchange and not xfuse) else None
-        if split or eng is not None:
-            # dense gradient branch (+ bucket all-reduce) overlapped with the sparse exchange
+        # row-sharded step: the dense all-reduce rides in the gradient exchange group on the main
+        # stream (parallel/sharded.py: one communicator, fixed order); replicated: the process
+        # group's all-reduce, overlapped with the sparse backward
+        shx_ar = self.shx is not None and not xfuse
+        if split:
+            # dense gradient branch overlapped with the sparse backward
             if self._comm_stream is None:
                 self._comm_stream = torch.cuda.Stream(self.device)
             self._comm_stream.wait_stream(main)
             with torch.cuda.stream(self._comm_stream):
-                if split:
-                    self._dense_grads()
-                if eng is not None:
-                    eng.allreduce_(self.g)
-                elif self.exchange:
+                self._dense_grads()
+                if self.exchange and not xfuse and not shx_ar:
                     work = self.comm.allreduce_dense_async(self.g)
-        elif self.exchange and not xfuse:
+        elif self.exchange and not xfuse and not shx_ar:
             work = self.comm.allreduce_dense_async(self.g)
-        # row-sharded lazy step: the dense optimizer rides in the owner update's launch, which
-        # first joins the dense all-reduce (returns a join callable, or None)
-        self._sh_dense_join = None
-        if (self.shx is not None and self.sparse_update == "lazy" and _SH_APPLY_DENSE and
-                not self._dense_early):
-            cs = self._comm_stream if (split or eng is not None) else None
-
-            def _join(cs=cs, work=work):
-                if cs is not None:
-                    main.wait_stream(cs)
-                if work is not None:
-                    self.comm.wait(work)
-            self._sh_dense_join = _join
+        # row-sharded step: the dense gradient's producer is joined right before the gradient
+        # exchange group; with lazy rows the dense optimizer rides in the owner update's launch
+        self._sh_join = None
+        self._sh_apply_dense = False
+        if self.shx is not None:
+            cs = self._comm_stream if split else None
+            self._sh_join = (lambda cs=cs: main.wait_stream(cs)) if cs is not None else None
+            self._sh_apply_dense = (self.sparse_update == "lazy" and _SH_APPLY_DENSE and
+                                    not self._dense_early)
+            self._sh_ar = shx_ar
         out = self._sparse_backward(B, idx, tv, presorted=presorted)
         if out is not None:
             self._sparse_update(*out)
         self._sfwg_now = False
-        if split or eng is not None:
+        if split:
             main.wait_stream(self._comm_stream)
         if work is not None:
             self.comm.wait(work)
         if self.shx is not None:
             self.shx.end(self._shx_plan)
-        if self._sh_dense_join is not None:
-            self._sh_dense_join = None
+        if self._sh_apply_dense:
+            self._sh_apply_dense = False
             if self.fp8:
                 KN.w8_quant(self._w8_jobs, len(self.layers), self._w8_rows)
         elif not self._dense_early:
@@ -1552,7 +1588,7 @@ class NativeDeepFM:
             self._host_step += 1
 
     def _plan_state(self):
-        sh = None if self.shx is None else (self.shx.cur, [(rs.key, rs.ahead) for rs in self.shx.sets])
+        sh = None if self.shx is None else (self.shx.cur, [rs.key for rs in self.shx.sets])
         return self._ss_cur, list(self._ss_key), sh, list(getattr(self, "_stamp_n", []))
 
     def _set_plan_state(self, st):
@@ -1561,8 +1597,8 @@ class NativeDeepFM:
             self._stamp_n = list(st[3])
         if st[2] is not None:
             self.shx.cur = st[2][0]
-            for rs, (k, a) in zip(self.shx.sets, st[2][1]):
-                rs.key, rs.ahead = k, a
+            for rs, k in zip(self.shx.sets, st[2][1]):
+                rs.key = k
 
     def train_step(self, ids, vals, labels, use_graph: bool = False, next_ids=None,
                    stage: bool = False):

@@ -154,7 +154,13 @@ class TowerArgs(C.Structure):
                 ("sW", c_void_p * TW_MAXL),
                 ("idx", c_void_p), ("vals", c_void_p), ("tv", c_void_p), ("tw", c_void_p),
                 ("ldv", c_long), ("ldw", c_long), ("fm_bias", c_void_p), ("F", c_int),
-                ("x_off", c_int), ("x8_off", c_int), ("S", c_void_p), ("Et", c_void_p), ("idx_ld", c_int)]
+                ("x_off", c_int), ("x8_off", c_int), ("S", c_void_p), ("Et", c_void_p), ("idx_ld", c_int),
+                ("id_lim", c_uint32)]
+
+
+class CommOp(C.Structure):
+    _fields_ = [("kind", c_int), ("pad", c_int), ("send", c_void_p), ("recv", c_void_p),
+                ("bytes", C.c_size_t)]
 
 
 class W8Job(C.Structure):
@@ -212,7 +218,8 @@ _SIGS = {
     "hfm_seg_tiles": [c_int, c_int],
     "hfm_radix_sort_temp_bytes": [c_int, C.POINTER(c_size_t)],
     "hfm_onesweep_temp_bytes": [c_int, C.POINTER(c_size_t)],
-    "hfm_onesweep_sort_ids": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_size_t, c_void_p],
+    "hfm_onesweep_sort_ids": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_size_t, c_uint32,
+                              c_void_p, c_void_p],
     "hfm_onesweep_error_offset": [],
     "hfm_field_sort_max_rows": [],
     "hfm_field_sort_chunk_rows": [],
@@ -224,6 +231,7 @@ _SIGS = {
     "hfm_comm_alltoall": [c_void_p, c_void_p, c_void_p, c_size_t, c_void_p],
     "hfm_comm_allgather": [c_void_p, c_void_p, c_void_p, c_size_t, c_void_p],
     "hfm_comm_alltoall_allgather": [c_void_p, c_void_p, c_void_p, c_size_t, c_void_p, c_void_p, c_size_t, c_void_p],
+    "hfm_comm_group": [c_void_p, c_void_p, c_int, c_void_p],
     "hfm_sh_count_blocks": [c_int],
     "hfm_sh_route_tiles": [c_int],
     "hfm_sh_route": [c_void_p, c_int, c_int, c_int] + [c_void_p] * 7 + [c_void_p],

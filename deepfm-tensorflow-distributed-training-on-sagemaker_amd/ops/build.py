@@ -5,7 +5,8 @@
 * ``_lib/libhipfm_io.so``      — ``csrc/io/*.cpp`` (TFRecord framing + CRC32C, tf.train.Example
   decoder, libsvm parser, threaded batch loader), host-only C++17.
 
-Objects are rebuilt only when a source or header is newer than the object.
+Objects are rebuilt when a source or header is newer than the object, or when the compile
+command (flags, arch, compiler) differs from the one recorded in the object's ``.cmd`` stamp.
 Usage: ``python -m hipfm.ops.build [--force]``.
 """
 from __future__ import annotations
@@ -55,6 +56,20 @@ def _newer(src_files, target) -> bool:
     return any(os.path.getmtime(s) > t for s in src_files)
 
 
+def _stamp_ok(obj: str, cmd) -> bool:
+    """The object was built by exactly this command (its ``.cmd`` stamp matches)."""
+    try:
+        with open(obj + ".cmd") as f:
+            return f.read() == "\x00".join(cmd)
+    except OSError:
+        return False
+
+
+def _write_stamp(obj: str, cmd) -> None:
+    with open(obj + ".cmd", "w") as f:
+        f.write("\x00".join(cmd))
+
+
 def _run(cmd):
     r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
     if r.returncode != 0:
@@ -70,17 +85,21 @@ def build_kernels(force: bool = False, jobs: int = 8, verbose: bool = False) -> 
     hipcc = _hipcc()
     objs = []
     todo = []
+    def cmd_of(s, o):
+        return [hipcc, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17",
+                "-fvisibility=hidden", "-Wno-unused-result", *NO_PACKED_F32, "-c", s, "-o", o]
+
     for s in srcs:
         o = os.path.join(BUILD_DIR, os.path.basename(s) + ".o")
         objs.append(o)
-        if force or _newer([s] + hdrs, o):
+        if force or _newer([s] + hdrs, o) or not _stamp_ok(o, cmd_of(s, o)):
             todo.append((s, o))
 
     def comp(so):
         s, o = so
-        cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17",
-               "-fvisibility=hidden", "-Wno-unused-result", *NO_PACKED_F32, "-c", s, "-o", o]
+        cmd = cmd_of(s, o)
         out = _run(cmd)
+        _write_stamp(o, cmd)
         if verbose and out.strip():
             print(out)
         return o

@@ -107,21 +107,26 @@ def lsd_sort_ids(keys_in, keys_out, perm_out, n, end_bit, temp):
                                  temp.numel(), stream_handle()), "radix_sort_ids")
 
 
-def onesweep_sort_ids(keys_in, keys_out, perm_out, n, end_bit, temp):
-    """Onesweep radix sort (global histogram + one decoupled-look-back pass per 8 bits)."""
+def onesweep_sort_ids(keys_in, keys_out, perm_out, n, end_bit, temp, limit: int = 0, err=None):
+    """Onesweep radix sort (global histogram + one decoupled-look-back pass per 8 bits).
+    ``limit`` > 0 (the table's rows): keys outside [0, limit) are sorted as limit - 1 and set the
+    int32 word ``err``, so a bad id never indexes a table out of bounds downstream."""
+    assert limit == 0 or err is not None
     check(L().hfm_onesweep_sort_ids(ptr(keys_in), ptr(keys_out), ptr(perm_out), n, end_bit,
-                                    ptr(temp), temp.numel(), stream_handle()), "onesweep_sort_ids")
+                                    ptr(temp), temp.numel(), int(limit), ptr(err), stream_handle()),
+          "onesweep_sort_ids")
 
 
 SORT_IMPL = knob("HIPFM_SORT_IMPL")
 # A/B in tools/bench_sort.py (graph-timed): onesweep 56 us vs LSD 101 us at n = 640K, 30 bits
 
 
-def sort_ids(keys_in, keys_out, vals_tmp, perm_out, n, end_bit, temp):
+def sort_ids(keys_in, keys_out, vals_tmp, perm_out, n, end_bit, temp, limit: int = 0, err=None):
     """Stable sort of slot ids -> (sorted keys, slot permutation) (csrc/kernels/radix_sort.hip).
-    ``temp`` must hold radix_temp_bytes(n) bytes; ``vals_tmp`` is unused."""
+    ``temp`` must hold radix_temp_bytes(n) bytes; ``vals_tmp`` is unused.  ``limit`` / ``err``:
+    id-range guard of the onesweep sort (see ``onesweep_sort_ids``)."""
     if SORT_IMPL == "onesweep":
-        onesweep_sort_ids(keys_in, keys_out, perm_out, n, end_bit, temp)
+        onesweep_sort_ids(keys_in, keys_out, perm_out, n, end_bit, temp, limit, err)
     else:
         lsd_sort_ids(keys_in, keys_out, perm_out, n, end_bit, temp)
 
@@ -143,7 +148,7 @@ class FieldSort:
     Batches above ``field_sort_chunk_rows()`` are sorted in row chunks and merged (the work list
     is built for ``max_rows``; a smaller batch skips the workgroups of chunks it does not have)."""
 
-    def __init__(self, ranges, max_rows: int, device, max_pb: int = 0):
+    def __init__(self, ranges, max_rows: int, device, max_pb: int = 0, err=None):
         """``max_pb``: each field is split into up to 2^max_pb workgroups (MSD partitions): 4 when
         the sort is on the critical path, 0 (one workgroup per field) when it overlaps other work."""
         import math
@@ -166,7 +171,8 @@ class FieldSort:
         big = max_rows > self.chunk
         self.rk = torch.zeros(self.F * max_rows if big else 1, dtype=torch.int32, device=device)
         self.rp = torch.zeros_like(self.rk)
-        self.err = torch.zeros(1, dtype=torch.int32, device=device)
+        # error word: a caller's (e.g. a view of the model's error words) or its own
+        self.err = err if err is not None else torch.zeros(1, dtype=torch.int32, device=device)
         self.max_rows = max_rows
 
     def work(self, B: int):
@@ -471,6 +477,21 @@ def comm_alltoall_allgather(h: int, send, recv, bytes_per_peer: int, gsend, grec
 def comm_allgather(h: int, send: torch.Tensor, recv: torch.Tensor, bytes_per_rank: int):
     assert send.is_contiguous() and recv.is_contiguous()
     check(L().hfm_comm_allgather(h, ptr(send), ptr(recv), bytes_per_rank, stream_handle()), "comm_allgather")
+
+
+COMM_A2A, COMM_ALLGATHER, COMM_ALLREDUCE = 0, 1, 2
+
+
+def comm_group(h: int, ops):
+    """Collectives as ONE aggregated RCCL operation on the current stream (comm.hip
+    hfm_comm_group).  ``ops``: (kind, send, recv, bytes) with kind COMM_A2A (bytes per peer),
+    COMM_ALLGATHER (bytes per rank) or COMM_ALLREDUCE (f32 sum, bytes in total)."""
+    from ._lib import CommOp
+    arr = (CommOp * max(1, len(ops)))()
+    for i, (kind, send, recv, nbytes) in enumerate(ops):
+        assert send.is_contiguous() and recv.is_contiguous()
+        arr[i].kind, arr[i].send, arr[i].recv, arr[i].bytes = int(kind), ptr(send), ptr(recv), int(nbytes)
+    check(L().hfm_comm_group(h, arr, len(ops), stream_handle()), "comm_group")
 
 
 # ------------------------------------------------------------------ row-sharded exchange (shard.hip)

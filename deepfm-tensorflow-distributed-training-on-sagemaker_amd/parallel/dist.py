@@ -69,14 +69,14 @@ class Comm:
         self.sharded = bool(sharded) and (self.world_size > 1 or self.force_exchange)
         self.router = Router(self.world_size, self.rank, group)
         self._bytes = 0
-        # native RCCL engine (csrc/kernels/comm.hip): fixed-capacity all-to-alls + dense
-        # all-reduce issued on our streams -> no host sync, graph-capturable step.  Two
-        # communicators: the dense all-reduce runs on a side stream concurrently with the
-        # sparse exchange, and one communicator must not carry concurrent operations.
+        # native RCCL engine (csrc/kernels/comm.hip): fixed-capacity all-to-alls + the dense
+        # gradient exchange, issued as grouped operations on the step's main stream -> no host
+        # sync, graph-capturable step.  ONE communicator carries every collective of the step
+        # in a fixed order (parallel/sharded.py module docstring: deadlock freedom)
         if native is None:
             native = (dist.get_backend(group) == "nccl" and self.sharded and
                       knob("HIPFM_SHARD_EXCHANGE") == "fixed")
-        self.engine = self.engine_dense = self.engine_route = None
+        self.engine = None
         if capacity is not None and self.world_size > 1:
             # every rank must use the SAME per-peer block size in the fixed-capacity all-to-alls:
             # take the max of the per-rank estimates (each rank measured its own batches)
@@ -88,17 +88,13 @@ class Comm:
         self.capacity = capacity
         if native:
             from .sharded import RcclEngine
-            self.engine = RcclEngine(group)          # row / gradient exchange (main stream)
-            self.engine_dense = RcclEngine(group)    # dense all-reduce (side stream)
-            # the next batch's id routing (side stream) gets its own communicator on first use:
-            # an idle RCCL communicator next to graph-captured ones faults replays (ROCm 7)
+            self.engine = RcclEngine(group)
         # steps with host-synchronous routing (variable all-to-all splits) cannot be graphed
         self.graph_safe = (self.world_size == 1 and not self.force_exchange) or self.engine is not None
 
     @property
     def bytes_sent(self) -> int:
-        eng = sum(e.bytes_sent for e in (self.engine, self.engine_dense, self.engine_route)
-                  if e is not None)
+        eng = self.engine.bytes_sent if self.engine is not None else 0
         return self._bytes + self.router.bytes_sent + eng
 
     @bytes_sent.setter
@@ -124,20 +120,11 @@ class Comm:
     def barrier(self):
         dist.barrier(group=self.group)
 
-    def route_engine(self):
-        """Communicator for the prefetched routing; created collectively on first use (every
-        rank reaches its first prefetching step together), never inside a graph capture."""
-        if self.engine_route is None and self.engine is not None:
-            from .sharded import RcclEngine
-            self.engine_route = RcclEngine(self.group)
-        return self.engine_route
-
     def close(self):
         """Destroy the native RCCL communicators (before the process group goes away).  Not for
         communicators captured into HIP graphs: ncclCommDestroy then blocks (ROCm 7)."""
-        for e in (self.engine, self.engine_dense, self.engine_route):
-            if e is not None:
-                e.close()
+        if self.engine is not None:
+            self.engine.close()
 
     # ------------------------------------------------------------------ helpers
     def _a2a_counts(self, send_counts: torch.Tensor) -> List[int]:

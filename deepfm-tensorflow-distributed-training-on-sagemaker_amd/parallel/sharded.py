@@ -5,9 +5,24 @@ The reference pulls embedding rows from parameter servers and pushes gradients b
 (owner = id % N, local row = id // N) and every exchange is an RCCL all-to-all of N equal blocks
 of ``capacity`` entries, issued from the native engine (csrc/kernels/comm.hip) on the compute
 stream.  No split size ever crosses to the host, so the whole multi-GPU step — sort, bucketing,
-three all-to-alls, forward, backward, owner update and the dense all-reduce — is captured into
-one HIP graph per resident batch, exactly like the single-GPU step (csrc/kernels/shard.hip has
-the protocol).
+the all-to-alls, forward, backward, owner update and the dense gradient exchange — is captured
+into one HIP graph per resident batch, exactly like the single-GPU step (csrc/kernels/shard.hip
+has the protocol).
+
+Collective order (deadlock freedom by construction).  Every collective of a step goes through
+ONE communicator, as a grouped RCCL operation on the step's MAIN stream, at fixed points:
+
+    [inline routing only]  G0 = {ids all-to-all of this batch}
+    fetch                  G1 = {rows all-to-all of this batch}
+    end of the backward    G2 = {gradient rows all-to-all, dense gradient all-gather (or
+                                 all-reduce), ids all-to-all of the NEXT batch (prefetched)}
+
+The next batch's routing KERNELS (sort, owner buckets, slot map) run on a side stream during
+the step, but its id exchange joins G2 on the main stream.  So each rank issues the same
+sequence of groups on one communicator in one stream order -- never two operations that could
+wait on each other across ranks -- whatever order the graph's branches reach the hardware
+queues in (``_issue`` refuses a collective off the main stream).  tests/test_gpu_shard.py
+records the sequence per emulated rank and checks it is identical.
 
 Capacity: the unique ids a rank sends to one owner must fit ``capacity``.  ``estimate_capacity``
 measures sample batches; a bucket that overflows sets an error word that the model checks
@@ -27,10 +42,6 @@ from ..utils.knobs import flag
 
 # routing in two launches (sh_route) instead of segments + bucket (7 launches); same outputs
 _ROUTE2 = flag("HIPFM_SH_ROUTE2")
-# lazy rows: the NEXT batch's rows are served on the side stream during this step (after its
-# routing); this step's owner update patches the rows it changes, so the serve launch leaves
-# the critical path
-_SERVE_AHEAD = flag("HIPFM_SH_SERVE_AHEAD")
 
 
 def estimate_capacity(id_batches: Iterable[torch.Tensor], world: int, slack: float = 1.25,
@@ -78,6 +89,12 @@ class RcclEngine:
         self.bytes_sent += t.numel() * 4
         KN.comm_allreduce_(self.handle, t)
 
+    def group(self, ops):
+        """(kind, send, recv, bytes) collectives as one grouped RCCL operation (KN.comm_group)."""
+        for kind, _, _, nb in ops:
+            self.bytes_sent += nb if kind == KN.COMM_ALLREDUCE else nb * self.world
+        KN.comm_group(self.handle, ops)
+
     def close(self):
         if self.handle:
             KN.comm_destroy(self.handle)
@@ -106,38 +123,37 @@ class _RouteSet:
         self.send_ids = torch.full((N * C,), -1, **i32)
         self.recv_ids = torch.full((N * C,), -1, **i32)
         self.send_cnt = torch.zeros(N, **i32)
-        self.gathered = None     # [N, N*C] all-gathered requests (side-stream routing)
         self.slot_row = torch.zeros(n, **i32)
-        self.recv = (self.recv_ids.data_ptr(), 0)   # (requests address, row stride) for the owner
-        self.key = None          # host: (ids data_ptr, B) routed into this set
-        # owner side: served rows and the request table (csrc/kernels/shard.hip) of this set's
-        # batch -- per set, because the next batch's rows are served (and its requests stamped)
-        # while the current batch's update still reads its own table.  The table has a power of
-        # two >= 2x the N*C request slots; keys and per-requester positions carry step stamps --
-        # sized by the exchange, not by the table (a direct [R_local][N] tag array is 7 GB per
-        # rank at the 1TB shape)
+        self.key = None          # host: (ids data_ptr, B) routed AND exchanged into this set
+        # owner side: the request table (csrc/kernels/shard.hip) of this set's batch.  It has a
+        # power of two >= 2x the N*C request slots; keys and per-requester positions carry step
+        # stamps -- sized by the exchange, not by the table (a direct [R_local][N] tag array is
+        # 7 GB per rank at the 1TB shape)
         T = N * C
-        self.rows_out = torch.zeros(T, m.K + 4, dtype=torch.float32, device=dev)
         slots = 1
         while slots < 2 * T:
             slots *= 2
         self.req_key = torch.zeros(slots, dtype=torch.int64, device=dev)
         self.req_pos = torch.zeros(slots * N, dtype=torch.int64, device=dev)
         self.table = ShTable(self.req_key.data_ptr(), self.req_pos.data_ptr(), slots - 1, 0)
-        self.ahead = False       # host: rows_out holds this batch's rows, served ahead
+
+
+class CollectiveOrderError(RuntimeError):
+    """A collective of the row-sharded step was about to be issued off the step's main stream."""
 
 
 class FixedCapacityExchange:
     """Buffers + step pieces of the row-sharded exchange for one NativeDeepFM (one rank).
 
     Two routing sets alternate: with ``next`` known (resident / prefetched batches), the routing
-    of batch i+1 (sort, dedup, owner buckets, id all-to-all, slot->row map) runs on a side stream
-    during step i — the sparse-input-dist pipelining of production DLRM trainers — so the
-    critical path of a step keeps only the row fetch, the compute and the gradient exchange."""
+    kernels of batch i+1 (sort, dedup, owner buckets, slot->row map) run on a side stream during
+    step i and its ids travel in step i's final collective group -- the sparse-input-dist
+    pipelining of production DLRM trainers -- so the critical path of a step keeps only the row
+    fetch, the compute and the gradient exchange.  See the module docstring for the collective
+    order."""
 
-    def __init__(self, m, engine, capacity: Optional[int] = None, engine_route=None):
+    def __init__(self, m, engine, capacity: Optional[int] = None):
         self.m, self.eng = m, engine
-        self.eng_route = engine_route     # created on the first prefetching step (plan())
         self.N, self.rank = engine.world, engine.rank
         dev = m.device
         K, n = m.K, m.M * m.F
@@ -147,36 +163,30 @@ class FixedCapacityExchange:
         T = self.N * self.C
         f32 = dict(dtype=torch.float32, device=dev)
         self.sets = [_RouteSet(m, n, self.N, self.C, m.temp.numel()) for _ in range(2)]
-        for rs in self.sets:
-            rs.gathered = torch.zeros(self.N * self.N * self.C, dtype=torch.int32, device=dev)
         self.cur = 0
-        self.err = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.err = m.err_words[2:3]          # capacity overflow (the model's error words)
+        self.rows_out = torch.zeros(T, self.RW, **f32)     # owner: served rows of this step
         self.rows_in = torch.zeros(T, self.RW, **f32)
         self.send_g = torch.zeros(T, self.RW, **f32)
         self.recv_g = torch.zeros(T, self.RW, **f32)
         self._side = None
-        self._joined = False
+        self._main = None
+        self._joined = True
         self._next_ids, self._next_fm = None, False
         self._fork_at = None
-        self._fork_plan = None
+        self._plan = None
         self.dense_recv = None               # [N][P] all-gathered dense gradients (fused exchange)
+        self.trace = None                    # list: record every issued group (tests)
 
     # ------------------------------------------------------------------ host-side plan
     def plan(self, ids: torch.Tensor, B: int, nxt: Optional[torch.Tensor], resident: bool = True):
         """Routing decisions for one step (part of the graph key): (set index, route the current
-        batch inline?, next ids or None, rows already served ahead?, serve the next batch's rows
-        ahead?).  Only resident batches (fixed device buffers) can have been prefetched: staged
-        buffers change content under the same address."""
+        batch inline?, (next ids address, next B) or None).  Only resident batches (fixed device
+        buffers) can have been prefetched: staged buffers change content under the same address."""
         c = self.cur
         key = (ids.data_ptr(), B)
         inline = (not resident) or self.sets[c].key != key
-        ahead = (not inline) and self.sets[c].ahead
-        if nxt is not None and self.eng_route is None:
-            get = getattr(self.m.comm, "route_engine", None)
-            self.eng_route = get() if get is not None else self.eng
-        serve_next = nxt is not None and _SERVE_AHEAD and self.m.sparse_update == "lazy"
-        return (c, inline, None if nxt is None else (nxt.data_ptr(), nxt.numel() // self.m.F), ahead,
-                serve_next)
+        return (c, inline, None if nxt is None else (nxt.data_ptr(), nxt.numel() // self.m.F))
 
     def commit(self, plan, ids: torch.Tensor, B: int, resident: bool = True):
         """Consecutive steps always use alternate routing sets (prefetched or not): a step's
@@ -185,31 +195,38 @@ class FixedCapacityExchange:
         caller declared as next (``next_ids``): a set is never matched again by address alone,
         since a freshly allocated batch can get the address of an earlier one back from the
         caching allocator."""
-        c, _, nk, _, serve_next = plan
+        c, _, nk = plan
         self.sets[c].key = None
-        self.sets[c].ahead = False
         self.sets[1 - c].key = nk
-        self.sets[1 - c].ahead = nk is not None and serve_next
         self.cur = 1 - c
 
     def drop_served(self):
-        """Parameters changed outside a step (load / broadcast): rows served ahead are stale, so
-        the next step serves its rows itself (its prefetched routing stays valid)."""
-        for rs in self.sets:
-            rs.ahead = False
+        """Parameters changed outside a step (load / broadcast).  Rows are served at the start of
+        every step, so nothing served can be stale; kept for the model's protocol."""
+
+    # ------------------------------------------------------------------ collectives
+    def _issue(self, ops):
+        """Every collective of the step, as one group on the MAIN stream (the stream ``begin``
+        ran on) -- the fixed issue order the module docstring argues deadlock freedom from."""
+        cur = torch.cuda.current_stream(self.m.device) if self.m.device.type == "cuda" else None
+        if self._main is not None and cur is not None and cur != self._main:
+            raise CollectiveOrderError("row-sharded exchange: collective issued off the step's main "
+                                       "stream (every collective must keep the fixed main-stream order)")
+        if self.trace is not None:
+            self.trace.append(tuple((k, int(nb)) for k, _, _, nb in ops))
+        self.eng.group(ops)
 
     # ------------------------------------------------------------------ pieces
-    def route(self, rs: _RouteSet, ids: torch.Tensor, B: int, eng, gather: bool = False, fm: bool = False):
-        """Sort + dedup the slot ids, bucket the unique ids by owner, send the requests.
-        ``gather``: requests travel by all-gather (every rank's [N, C] block; this rank keeps
-        column ``rank``) instead of all-to-all — RCCL's all-to-all cannot be captured on a forked
-        side stream (segfault at graph instantiation on ROCm 7), its collectives can."""
+    def route_kernels(self, rs: _RouteSet, ids: torch.Tensor, B: int, fm: bool = False):
+        """Sort + dedup the slot ids, bucket the unique ids by owner, slot -> received-row map
+        (kernels only; the ids' all-to-all is issued by the caller on the main stream)."""
         m = self.m
         n = B * m.F
         if m.uses_field_sort(B):
             m._fsort(ids, B, rs.sorted_keys, rs.perm, field_major=fm)
         else:
-            KN.sort_ids(ids, rs.sorted_keys, None, rs.perm, n, m.end_bit, rs.temp)
+            KN.sort_ids(ids, rs.sorted_keys, None, rs.perm, n, m.end_bit, rs.temp, limit=m.V,
+                        err=m.err_words[3:4])
         if _ROUTE2:
             KN.sh_route(rs.sorted_keys, n, self.N, self.C, rs.tcnt, rs.sid_incl, rs.send_ids, rs.upos,
                         rs.send_cnt, rs.num_u, self.err)
@@ -218,90 +235,79 @@ class FixedCapacityExchange:
                         rs.temp)
             KN.sh_bucket(rs.ukeys, rs.num_u, n, self.N, self.C, rs.cnt_tmp, rs.send_ids, rs.upos,
                          rs.send_cnt, self.err)
-        if gather:
-            if rs.gathered is None:
-                rs.gathered = torch.zeros(self.N * self.N * self.C, dtype=torch.int32, device=m.device)
-            eng.allgather(rs.send_ids, rs.gathered, self.N * self.C * 4)
-            # the owner kernels read this rank's column of the gathered requests in place
-            rs.recv = (rs.gathered.data_ptr() + 4 * self.rank * self.C, self.N * self.C)
-        else:
-            eng.alltoall(rs.send_ids, rs.recv_ids, self.C * 4)
-            rs.recv = (rs.recv_ids.data_ptr(), 0)
         KN.sh_slot_rows(rs.perm, rs.sid_incl, rs.upos, n, rs.slot_row)
 
+    def _ids_op(self, rs: _RouteSet):
+        return (KN.COMM_A2A, rs.send_ids, rs.recv_ids, self.C * 4)
+
     def begin(self, plan, B: int, fork: str = "start"):
-        """Start of a step: route the current batch if it was not prefetched, then fork the
-        routing of the next batch onto a side stream -- here (``fork="start"``), right after the
-        row fetch is enqueued (``"fetch"``), or when the caller calls ``fork_next`` (graph
-        branches are dispatched in capture order: a branch enqueued first delays the main
-        stream's first kernels)."""
+        """Start of a step (on its main stream): route the current batch if it was not prefetched
+        (kernels + G0), then fork the next batch's routing kernels onto a side stream -- here
+        (``fork="start"``), after the row fetch (``"fetch"``), or when the caller calls
+        ``fork_next`` (graph branches are dispatched in capture order)."""
         m = self.m
-        c, inline, nk = plan[:3]
+        c, inline, nk = plan
+        self._main = torch.cuda.current_stream(m.device)
+        self._plan = plan
         if inline:
-            self.route(self.sets[c], m.idx, B, self.eng, fm=m._idx_fm)
-        self._joined = False
+            rs = self.sets[c]
+            self.route_kernels(rs, m.idx, B, fm=m._idx_fm)
+            self._issue([self._ids_op(rs)])                            # G0
+        self._joined = nk is None
         self._fork_at = fork if nk is not None else None
-        self._fork_plan = plan
         if self._fork_at == "start":
             self.fork_next()
 
     def fork_next(self):
-        """Enqueue the next batch's routing on the side stream (once per step)."""
+        """Enqueue the next batch's routing kernels on the side stream (once per step)."""
         if self._fork_at is None:
             return
         self._fork_at = None
         m = self.m
-        c, _, nk, _, serve_next = self._fork_plan
-        main = torch.cuda.current_stream(m.device)
+        c, _, nk = self._plan
         if self._side is None:
             self._side = torch.cuda.Stream(m.device)
-        self._side.wait_stream(main)
-        nxt_ids = self._next_ids
-        rs = self.sets[1 - c]
+        self._side.wait_stream(self._main)
         with torch.cuda.stream(self._side):
-            self.route(rs, nxt_ids, nk[1], self.eng_route, gather=True, fm=self._next_fm)
-            if serve_next:
-                # the next batch's rows as of now (stamped step + 2); this step's owner update
-                # patches the rows it changes (it joins this branch first)
-                KN.sh_serve(m.K, rs.recv[0], self.N * self.C, self.N, m.tv, m.tw, rs.rows_out, C=self.C,
-                            step=m.step, table=rs.table, rstride=rs.recv[1], ahead=True)
+            self.route_kernels(self.sets[1 - c], self._next_ids, nk[1], fm=self._next_fm)
 
-    def _join_side(self, plan):
-        if plan[2] is not None and not self._joined:
-            torch.cuda.current_stream(self.m.device).wait_stream(self._side)
+    def _join_side(self):
+        if not self._joined:
+            self.fork_next()
+            self._main.wait_stream(self._side)
             self._joined = True
 
     def end(self, plan):
-        self.fork_next()                     # (not forked yet: e.g. no tower in this step)
-        self._join_side(plan)
+        self._join_side()
+        self._main = None
 
     def fetch(self, plan, train: bool = True):
-        """Owners serve the requested rows (after the previous step's updates), rows come back.
-        Training steps stamp the owner-side request tags here (read by the update at the end of
-        the step); eval / predict fetches leave them alone."""
+        """Owners serve the requested rows (after the previous step's updates), rows come back
+        (G1).  Training steps stamp the owner-side request tags here (read by the update at the
+        end of the step); eval / predict fetches leave them alone."""
         m = self.m
         rs = self.sets[plan[0]]
         if train:
-            if not plan[3]:                  # (else served during the previous step)
-                KN.sh_serve(m.K, rs.recv[0], self.N * self.C, self.N, m.tv, m.tw, rs.rows_out,
-                            C=self.C, step=m.step, table=rs.table, rstride=rs.recv[1])
+            KN.sh_serve(m.K, rs.recv_ids, self.N * self.C, self.N, m.tv, m.tw, self.rows_out, C=self.C,
+                        step=m.step, table=rs.table)
         else:
-            KN.sh_serve(m.K, rs.recv[0], self.N * self.C, self.N, m.tv, m.tw, rs.rows_out, C=self.C,
-                        rstride=rs.recv[1])
-        self.eng.alltoall(rs.rows_out, self.rows_in, self.C * self.RW * 4)
+            KN.sh_serve(m.K, rs.recv_ids, self.N * self.C, self.N, m.tv, m.tw, self.rows_out, C=self.C)
+        self._issue([(KN.COMM_A2A, self.rows_out, self.rows_in, self.C * self.RW * 4)])   # G1
         if train and self._fork_at == "fetch":
             self.fork_next()
         return rs.slot_row, self.rows_in[:, : m.K], self.rows_in[:, m.K]
 
-    def backward(self, plan, B: int, dense=None, join=None, wgfin=None):
+    def backward(self, plan, B: int, dense=None, join=None, wgfin=None, dense_ar=None):
         """Per-unique gradient rows -> owners -> rank-ordered sum + row update on the owner.
-        ``dense`` (ShDenseArgs, lazy rows): the dense optimizer runs in the owner update's launch,
-        after ``join()`` made the main stream wait for the dense gradient all-reduce.
         ``wgfin`` (WgFinArgs): the fused tower's dense gradient is computed inside the sparse
-        backward's launch and all-gathered right after the gradient rows' all-to-all (no
-        all-reduce, no comm stream); the owner launch sums the N rank gradients in rank order."""
+        backward's launch and all-gathered with the gradient rows (the owner launch sums the N
+        rank gradients in rank order); else ``dense_ar`` (the flat dense gradient) is all-reduced
+        in the same group, after ``join()`` made the main stream wait for its producer.
+        ``dense`` (ShDenseArgs, lazy rows): the dense optimizer runs in the owner update's launch.
+        The next batch's ids (routed on the side stream) travel in the same group (G2)."""
         m = self.m
-        rs = self.sets[plan[0]]
+        c, _, nk = plan
+        rs = self.sets[c]
         n = B * m.F
         A = m.sf_args(n)
         A.sorted_keys, A.perm = rs.sorted_keys.data_ptr(), rs.perm.data_ptr()
@@ -312,21 +318,23 @@ class FixedCapacityExchange:
             KN.sparse_wgfin_x(m.K, A, wgfin)
         else:
             KN.sparse_fused(m.K, KN.SF_EXCHANGE, m.opt_id, A)
+        if join is not None:
+            join()
+        ops = [(KN.COMM_A2A, self.send_g, self.recv_g, self.C * self.RW * 4)]
         if wgfin is not None:
             if self.dense_recv is None:
                 self.dense_recv = torch.zeros(self.N * m.P, dtype=torch.float32, device=m.device)
-            if hasattr(self.eng, "alltoall_allgather"):      # one aggregated RCCL operation
-                self.eng.alltoall_allgather(self.send_g, self.recv_g, self.C * self.RW * 4, m.g[: m.P],
-                                            self.dense_recv, m.P * 4)
-            else:
-                self.eng.alltoall(self.send_g, self.recv_g, self.C * self.RW * 4)
-                self.eng.allgather(m.g[: m.P], self.dense_recv, m.P * 4)
+            ops.append((KN.COMM_ALLGATHER, m.g[: m.P], self.dense_recv, m.P * 4))
             dense.g, dense.nsum = self.dense_recv.data_ptr(), self.N
-        else:
-            self.eng.alltoall(self.send_g, self.recv_g, self.C * self.RW * 4)
+        elif dense_ar is not None:
+            ops.append((KN.COMM_ALLREDUCE, dense_ar, dense_ar, dense_ar.numel() * 4))
+        if nk is not None:
+            self._join_side()                # the next batch's buckets are built
+            ops.append(self._ids_op(self.sets[1 - c]))
+        self._issue(ops)                                                 # G2
         S = ShApplyArgs()
-        S.recv_ids, S.total, S.N, S.C = rs.recv[0], self.N * self.C, self.N, self.C
-        S.rstride = rs.recv[1]
+        S.recv_ids, S.total, S.N, S.C = rs.recv_ids.data_ptr(), self.N * self.C, self.N, self.C
+        S.rstride = 0
         S.mode = 0 if m.sparse_update == "lazy" else 1      # tags were stamped by fetch()
         S.recv_g, S.table = self.recv_g.data_ptr(), rs.table
         S.tv, S.tw = m.tv.data_ptr(), m.tw.data_ptr()
@@ -336,14 +344,7 @@ class FixedCapacityExchange:
             S.Gv, S.Gw = m.Gv.data_ptr(), m.Gw.data_ptr()
         S.h = m.h_sparse
         S.step = m.step.data_ptr()
-        if plan[2] is not None and plan[4] and m.sparse_update == "lazy":
-            # the next batch's rows were served ahead: join that branch, patch what changes
-            nxt = self.sets[1 - plan[0]]
-            self._join_side(plan)
-            S.next, S.next_rows = nxt.table, nxt.rows_out.data_ptr()
         if dense is not None:
-            if join is not None:
-                join()
             KN.sh_apply_dense(m.K, m.opt_id, S, dense)
             return
         KN.sh_owner_apply(m.K, m.opt_id, S)
@@ -355,7 +356,6 @@ class FixedCapacityExchange:
         for rs in self.sets:
             rs.req_key.zero_()
             rs.req_pos.zero_()
-        self.drop_served()
 
     def error(self) -> int:
         return int(self.err.item())

@@ -61,9 +61,13 @@ class InjectedFault(RuntimeError):
     pass
 
 
-def maybe_inject_fault(step: int, rank: int) -> None:
+def maybe_inject_fault(step: int, rank: int, prev: int = None) -> None:
+    """Fires when the fault step lies in (prev, step]: a multi-step graph run advances the step
+    by up to ``graph_steps`` at once (``prev`` = the step before the run; default step - 1)."""
     s = knob("HIPFM_FAULT_STEP")
-    if not s or int(s) != step:
+    if prev is None:
+        prev = step - 1
+    if not s or not (prev < int(s) <= step):
         return
     r = knob("HIPFM_FAULT_RANK")
     if r is not None and int(r) != rank:

@@ -55,8 +55,6 @@ KNOBS: Dict[str, Knob] = {
     "HIPFM_SH_XFUSE": Knob("1", "variant", "row-sharded step: gradient rows + dense gradients in one "
                            "aggregated RCCL operation"),
     "HIPFM_SH_ROUTE2": Knob("1", "variant", "two-launch routing (0: segments + bucket kernels, oracle)"),
-    "HIPFM_SH_SERVE_AHEAD": Knob("1", "variant", "row-sharded step: next batch's rows served during "
-                                 "this step"),
     "HIPFM_SHARD_EXCHANGE": Knob("fixed", "variant", "fixed: fixed-capacity native RCCL exchange; "
                                  "else the torch.distributed all-to-all-v path"),
     "HIPFM_TF1_SPLIT": Knob("1", "variant", "tf1_dense on one GPU: split form (0: gradient scatter + "
@@ -90,7 +88,8 @@ KNOBS: Dict[str, Knob] = {
     "HIPFM_BENCH_SUPERVISE": Knob(None, "harness", "bench supervisor protocol: 0 runs unsupervised"),
     "HIPFM_BENCH_RUNG": Knob(None, "harness", "bench supervisor protocol: the child's ladder rung"),
     "HIPFM_BENCH_FIRST_RUNG": Knob(None, "harness", "bench: start the ladder at this rung"),
-    "HIPFM_BENCH_HANG_S": Knob(None, "harness", "bench: seconds without progress = hung"),
+    "HIPFM_BENCH_HANG_S": Knob(None, "harness", "bench: seconds without progress = hung (45)"),
+    "HIPFM_BENCH_FIRST_S": Knob(None, "harness", "bench: seconds to a rung's first progress mark (90)"),
     "HIPFM_BENCH_NO_GRAPH": Knob(None, "harness", "bench: eager steps only"),
     "HIPFM_BENCH_PROGRESS": Knob(None, "harness", "bench supervisor protocol: progress file"),
     "HIPFM_BENCH_RESULT": Knob(None, "harness", "bench supervisor protocol: result file"),

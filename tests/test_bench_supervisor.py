@@ -6,10 +6,13 @@ import os
 import socket
 import subprocess
 import sys
+import time
 
 import pytest
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if REPO not in sys.path:
+    sys.path.insert(0, REPO)
 
 
 def _port():
@@ -20,29 +23,42 @@ def _port():
     return p
 
 
-def _run(fake, hang_s="4"):
-    env = dict(os.environ, HIPFM_BENCH_FAKE=fake, HIPFM_BENCH_HANG_S=hang_s)
+def _run(fake, hang_s="4", first_s="6"):
+    env = dict(os.environ, HIPFM_BENCH_FAKE=fake, HIPFM_BENCH_HANG_S=hang_s, HIPFM_BENCH_FIRST_S=first_s)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(REPO, "bench.py"),
            "--gpus", "2"]
-    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=120, cwd=REPO)
+    t0 = time.time()
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=180, cwd=REPO)
     lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
-    return r.returncode, lines
+    return r.returncode, lines, time.time() - t0
 
 
 @pytest.mark.parametrize("fake,rung", [
     ("none:0:fail", "graph+prefetch"),
-    ("graph+prefetch:1:fail", "eager+prefetch+fused"),
-    ("graph+prefetch:1:fail,eager+prefetch+fused:0:fail", "graph+prefetch+allreduce"),
-    ("graph+prefetch:1:fail,eager+prefetch+fused:1:fail,graph+prefetch+allreduce:0:fail",
-     "eager+prefetch"),
-    ("graph+prefetch:0:hang,eager+prefetch+fused:0:fail,graph+prefetch+allreduce:1:fail,"
-     "eager+prefetch:1:fail", "eager"),
+    ("graph+prefetch:1:fail", "eager+prefetch"),
+    ("graph+prefetch:1:stall", "eager+prefetch"),
+    ("graph+prefetch:0:hang,eager+prefetch:1:stall", "eager"),
+    ("graph+prefetch:1:fail,eager+prefetch:0:fail", "eager"),
 ])
 def test_supervisor_falls_back_and_prints_one_line(fake, rung):
-    rc, lines = _run(fake)
+    rc, lines, _ = _run(fake)
     assert rc == 0
     assert len(lines) == 1 and lines[0]["config"]["exec"] == rung and lines[0]["n_gpus"] == 2
+
+
+def test_worst_case_ladder_fits_the_driver_timeout():
+    """hung rungs must hand over to the next one fast enough that the LAST rung still
+    runs inside a 600 s driver run.  With the production limits, every rung hanging costs at most
+    ladder_budget_s(); a fake run with every rung hung (scaled limits) ends within that bound."""
+    import bench
+    assert bench.ladder_budget_s() < 400
+    names = [n for n, _ in bench.LADDER]
+    spec = ",".join(f"{n}:{i % 2}:{'hang' if i % 2 else 'stall'}" for i, n in enumerate(names))
+    rc, lines, wall = _run(spec, hang_s="3", first_s="5")
+    assert rc != 0 and not lines
+    # scaled bound: per rung max(first_s, hang_s) + polling/teardown slack, plus process start-up
+    assert wall < len(names) * (5 + 6) + 60, wall
 
 
 @pytest.mark.parametrize("n", [2, 3])
@@ -60,6 +76,5 @@ def test_plain_bench_gpus_n_spawns_n_ranks(n):
 
 
 def test_supervisor_fails_when_every_rung_fails():
-    rc, lines = _run("graph+prefetch:0:fail,eager+prefetch+fused:0:fail,graph+prefetch+allreduce:0:fail,"
-                     "eager+prefetch:0:fail,eager:1:fail")
+    rc, lines, _ = _run("graph+prefetch:0:fail,eager+prefetch:0:fail,eager:1:fail")
     assert rc != 0 and not lines

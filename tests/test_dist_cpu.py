@@ -245,3 +245,44 @@ def test_two_rank_export_writes_one_shard_per_rank(tmp_path):
     assert "fm_v/Adam" not in sv and np.array_equal(sv["fm_v"], ck["fm_v"])
     p = load_servable(e).predict(torch.zeros(3, 39, dtype=torch.int64), torch.ones(3, 39))
     assert p.shape == (3,)
+
+
+def _ranges_worker(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from hipfm.data.pipeline import agreed_field_ranges
+
+        class _Shard:                   # a rank's cached epoch: field f ids in [100 f, 100 f + 100)
+            def field_minmax(self):
+                # rank 0 saw small ids of field 1, rank 1 only large ones (and vice versa field 2)
+                mn = torch.tensor([0, 130 if rank == 0 else 101, 200 if rank == 0 else 240])
+                mx = torch.tensor([50, 150 if rank == 0 else 190, 220 if rank == 0 else 299])
+                return mn, mx
+        r = agreed_field_ranges(_Shard(), 1000, world)
+        q.put({"rank": rank, "ranges": r})
+        dist.barrier()
+        dist.destroy_process_group()
+    except BaseException:
+        import traceback
+        q.put({"error": traceback.format_exc()})
+        raise
+
+
+def test_field_ranges_agreed_over_all_ranks_shards():
+    """ranges derived from one rank's shard can miss another rank's ids; the agreed
+    ranges cover the union of every rank's min / max (and are identical on every rank)."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_ranges_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in ps:
+        p.join(timeout=60)
+    for r in res:
+        assert "error" not in r, r.get("error")
+    a, b = (r["ranges"] for r in sorted(res, key=lambda r: r["rank"]))
+    assert a == b == [(0, 101), (101, 200), (200, 1000)]

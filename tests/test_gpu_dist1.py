@@ -83,34 +83,31 @@ def test_exchange_staged_batches_graph_replay(group):
     assert torch.allclose(a.tv, b.tv, atol=1e-6) and torch.allclose(a.p, b.p, atol=1e-6)
 
 
-def test_exchange_serve_ahead_bitwise(group):
-    """Row-sharded lazy step with multi-step graphs: the next batch's rows served during the
-    current step (and patched by its owner update) give bitwise the same parameters as serving
-    them at the start of their own step, and two runs of the same schedule are bitwise equal."""
-    from hipfm.parallel import sharded as SH
+def test_exchange_graph_runs_bitwise(group):
+    """Row-sharded lazy step with multi-step graphs (routing of the next batch prefetched, its ids
+    exchanged in the step's last collective group) gives bitwise the parameters of the same
+    schedule launched eagerly step by step, and two graph runs are bitwise equal."""
     synth = make_synth("total:6000", seed=29)
     F, K, layers, keep = synth.F, 8, [64, 32], [0.8, 0.8]
     V = synth.feature_size
     params = init_params(V, F, K, layers, False, seed=7)
     pool = [synth.batch(512, step=s, device="cuda", id_dtype=torch.int32) for s in range(4)]
 
-    def run(ahead):
-        old = SH._SERVE_AHEAD
-        SH._SERVE_AHEAD = ahead
-        try:
-            m = NativeDeepFM(V, F, K, layers, keep, sparse_update="lazy", batch_size=512, device="cuda",
-                             init=False, comm=Comm(sharded=True, force_exchange=True))
-            m.load_tf_params(params)
-            for _ in range(3):                       # capture, then replays of the 4-step graphs
+    def run(graph):
+        m = NativeDeepFM(V, F, K, layers, keep, sparse_update="lazy", batch_size=512, device="cuda",
+                         init=False, comm=Comm(sharded=True, force_exchange=True))
+        m.load_tf_params(params)
+        for _ in range(3):                       # capture, then replays of the 4-step graphs
+            if graph:
                 m.train_steps(pool, next_ids=pool[0][0])
-            torch.cuda.synchronize()
-            m.check_errors()
-            return m
-        finally:
-            SH._SERVE_AHEAD = old
+            else:
+                for i, (ids, vals, lab) in enumerate(pool):
+                    m.train_step(ids, vals, lab, next_ids=pool[(i + 1) % 4][0])
+        torch.cuda.synchronize()
+        m.check_errors()
+        return m
 
     a, b, c = run(True), run(False), run(True)
-    assert a.shx.sets[a.shx.cur].ahead and not b.shx.sets[b.shx.cur].ahead
     for x in (b, c):
         assert torch.equal(a.tv, x.tv) and torch.equal(a.tw, x.tw) and torch.equal(a.p, x.p)
 

@@ -84,6 +84,19 @@ class MeshEngine:
         self._finish(s)
         t.copy_(acc)
 
+    def group(self, ops):
+        """Grouped collectives (RcclEngine.group): run one after the other, same order on every
+        rank (every op is a barrier-synchronized exchange between the in-process ranks)."""
+        from hipfm.ops import kernels as KN
+        for kind, send, recv, nb in ops:
+            if kind == KN.COMM_A2A:
+                self.alltoall(send, recv, nb)
+            elif kind == KN.COMM_ALLGATHER:
+                self.allgather(send, recv, nb)
+            else:
+                assert send.data_ptr() == recv.data_ptr()
+                self.allreduce_(recv)
+
 
 class MeshComm:
     def __init__(self, hub, rank, capacity=None):
@@ -91,8 +104,6 @@ class MeshComm:
         self.sharded = True
         self.force_exchange = False
         self.engine = MeshEngine(hub, rank)
-        self.engine_dense = MeshEngine(hub, rank)
-        self.engine_route = MeshEngine(hub, rank)
         self.capacity = capacity
         self.graph_safe = False
 
@@ -170,6 +181,45 @@ def test_sharded_exchange_matches_global_batch(N, opt, update, prefetch):
     assert (models[0].p - ref.p).abs().max().item() <= 2e-5 * ref.p.abs().max().item()
     # something was actually exchanged, and untouched rows kept their initial values
     assert models[0].comm.bytes_sent > 0
+
+
+@pytest.mark.parametrize("update", ["lazy", "tf1_dense"])
+def test_collective_sequence_identical_across_ranks(update):
+    """Deadlock freedom by construction (parallel/sharded.py): every collective of a step is a
+    group on ONE engine, issued on the step's main stream (``_issue`` raises otherwise) in a fixed
+    order.  Record each emulated rank's sequence of groups (kinds + byte counts) over N = 4 ranks
+    and 3 prefetching steps: the sequences are identical on every rank, with the per-step shape
+    G0 (first step: inline ids) / G1 (rows) / G2 (gradients + dense + next ids)."""
+    from hipfm.ops import kernels as KN
+    N, B = 4, 256
+    synth = make_synth("total:40000", seed=5)
+    F, K, layers, keep = synth.F, 8, [64, 32], [1.0, 1.0]
+    params = init_params(synth.feature_size, F, K, layers, False, seed=3)
+    hub = _Hub(N)
+    models = []
+    for r in range(N):
+        m = NativeDeepFM(synth.feature_size, F, K, layers, keep, sparse_update=update, batch_size=B,
+                         device=DEV, init=False, comm=MeshComm(hub, r, capacity=2048))
+        m.load_tf_params(params)
+        m.shx.trace = []
+        models.append(m)
+    batches = [[tuple(t.to(DEV) for t in synth.batch(B, step=100 * r + s, id_dtype=torch.int32))
+                for s in range(3)] for r in range(N)]
+    _run_ranks(models, batches, prefetch=True)
+    torch.cuda.synchronize()
+    traces = [m.shx.trace for m in models]
+    for t in traces[1:]:
+        assert t == traces[0]
+    t = traces[0]
+    C, RW = models[0].shx.C, models[0].shx.RW
+    ids_op, rows_op = (KN.COMM_A2A, C * 4), (KN.COMM_A2A, C * RW * 4)
+    assert t[0] == (ids_op,) and t[1] == (rows_op,)            # step 0: inline ids, then rows
+    g2 = t[2]
+    assert g2[0] == rows_op and g2[-1] == ids_op                # gradients first, next ids last
+    assert len(t) == 7 and t[3] == (rows_op,) and t[5] == (rows_op,)
+    assert t[4][-1] == ids_op and t[6][-1] != ids_op            # last step: no next batch
+    for m in models:
+        m.check_errors()
 
 
 def _fill_tables(m, N, r):

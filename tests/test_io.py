@@ -171,3 +171,34 @@ def test_discover_and_pipeline_cache(tmp_path):
     e1 = [b[0] for b in pipe.iter_epoch(1)]
     assert len(e0) == 300 // 64 and all(torch.equal(a, b) for a, b in zip(e0, e1))
     assert pipe.local_records() == 300
+
+
+@pytest.mark.parametrize("fmt", ["tfrecord", "libsvm"])
+def test_loader_rejects_ids_outside_vocabulary(tmp_path, fmt):
+    """An id >= feature_size (or negative) fails the read with the file and record named, before
+    anything reaches the device (whose gathers / row updates index the table unchecked)."""
+    F, V = 3, 1000
+    lab, ids, vals = _rows(40, F, 5)
+    ids = ids % V
+    ids[17, 2] = V + 3                                  # corrupted record 17
+    if fmt == "tfrecord":
+        p = str(tmp_path / "tr-0.tfrecords")
+        nio.write_examples(p, lab, ids, vals)
+        kind = nio.FMT_TFRECORD
+    else:
+        p = str(tmp_path / "tr-0.txt")
+        with open(p, "w") as f:
+            for i in range(len(lab)):
+                f.write(f"{lab[i]:g} " + " ".join(f"{ids[i, j]}:{vals[i, j]:g}" for j in range(F)) + "\n")
+        kind = nio.FMT_LIBSVM
+    ok = [x for x in nio.NativeLoader([p], F, 8, fmt=kind)]          # unchecked: reads through
+    assert len(ok) == 5
+    with pytest.raises(IOError, match=r"feature id 1003 \(field 2\).*feature_size=1000.*record 17"):
+        list(nio.NativeLoader([p], F, 8, fmt=kind, id_limit=V))
+    pipe = InputPipeline([p], F, 8, fmt=fmt, id_limit=V)
+    with pytest.raises(IOError, match="tr-0"):
+        list(pipe.iter_epoch(0))
+    ids[17, 2] = 5
+    if fmt == "tfrecord":
+        nio.write_examples(p, lab, ids, vals)
+        assert len(list(nio.NativeLoader([p], F, 8, fmt=kind, id_limit=V))) == 5
