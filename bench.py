@@ -58,6 +58,10 @@ def ladder_budget_s(rungs: int = len(LADDER), first_s: float = FIRST_S, hang_s: 
     return rungs * (max(first_s, setup_s + hang_s) + 5.0)
 
 
+_SHAPE_NAMES = {"criteo_1tb": "Criteo-1TB-shape", "criteo_kaggle": "Criteo-Kaggle-shape",
+                "reference": "reference-notebook-shape"}
+
+
 def _free_port() -> int:
     import socket
     s = socket.socket()
@@ -236,16 +240,15 @@ def main():
         init_distributed("nccl")
         _progress()
         mode = "sharded" if args.embedding_mode == "auto" else args.embedding_mode
-        cap = None
-        if mode == "sharded":
-            # per-peer capacity of the fixed-size all-to-alls: measured on EVERY batch this rank
-            # will route (the resident pool and the eval batches), +5 % + 256 margin, then agreed
-            # across ranks (MAX).  Overflow raises, never drops rows.  (Was 1.25x the max of 4
-            # sample batches: every exchange moved ~20 % more padding.)
-            from hipfm.parallel.sharded import estimate_capacity
-            ev = (synth.batch(B, step=10_000_000 + rank * 1000 + i, device=dev, id_dtype=torch.int32)[0]
-                  for i in range(args.eval_batches))
-            cap = estimate_capacity([b[0] for b in pool] + list(ev), world, slack=1.05)
+        # capacity of the fixed-size exchanges: measured on EVERY batch this rank will route (the
+        # resident pool and the eval batches), +5 % + 256 margin, then agreed across ranks (MAX).
+        # Overflow raises, never drops rows.  sharded: unique ids per owner (all-to-all blocks);
+        # replicated: unique ids per batch (all-gather blocks)
+        ev = [synth.batch(B, step=10_000_000 + rank * 1000 + i, device=dev, id_dtype=torch.int32)[0]
+              for i in range(args.eval_batches)]
+        from hipfm.parallel.dist import exchange_capacity
+        cap = exchange_capacity([b[0] for b in pool] + (ev if mode == "sharded" else []), world,
+                                sharded=(mode == "sharded"))
         comm = Comm(sharded=(mode == "sharded"), force_exchange=args.force_exchange, capacity=cap)
 
     F = synth.F
@@ -350,8 +353,8 @@ def main():
             "dtype": args.mlp_dtype,
             "data": "synthetic (Criteo-shaped Zipf ids + teacher labels, HBM-resident), random-init weights",
             "config": {
-                "model": f"DeepFM Criteo-1TB-shape (F={F}, V={synth.feature_size}, K={args.embedding_size}, "
-                         f"deep {args.deep_layers}, keep {args.dropout})",
+                "model": f"DeepFM {_SHAPE_NAMES.get(args.preset, args.preset)} (F={F}, V={synth.feature_size}, "
+                         f"K={args.embedding_size}, deep {args.deep_layers}, keep {args.dropout})",
                 "global_batch": world * B,
                 "per_gpu_batch": B,
                 "seq_len": None,

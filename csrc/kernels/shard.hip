@@ -338,12 +338,12 @@ __global__ void sh_serve_kernel(const int* __restrict__ recv_ids, int total, int
 }
 
 __global__ void sh_owner_tag_kernel(const int* __restrict__ recv_ids, int total, int N, int C, int rstride,
-                                    const int64_t* __restrict__ step, ShTable T) {
+                                    const int64_t* __restrict__ step, ShTable T, int rdiv) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= total) return;
   const int id = sh_rid(recv_ids, e, C, rstride);
   if (id < 0) return;
-  sh_insert(T, N, (unsigned)(id / N), e / C, (unsigned)(e % C), (unsigned)(*step + 1));
+  sh_insert(T, N, (unsigned)(id / rdiv), e / C, (unsigned)(e % C), (unsigned)(*step + 1));
 }
 
 // MODE 0: lazy optimizer OPT on the owner's row; 1: tf1_dense scatter into (Gv, Gw)
@@ -353,14 +353,15 @@ __device__ __forceinline__ void sh_owner_apply_elem(int gt, const int* __restric
                                                     ShTable T, float* tv, float* tw, float* s0v, float* s1v,
                                                     float* s0w, float* s1w, long ldv, long ldw, float* Gv,
                                                     float* Gw, OptHyper h, const int64_t* __restrict__ step,
-                                                    const ShTable& NT, float* __restrict__ next_rows) {
+                                                    const ShTable& NT, float* __restrict__ next_rows,
+                                                    int rdiv) {
   constexpr int LPS = K / 4, RW = K + 4;
   const int e = gt / LPS, sub = gt % LPS;
   if (e >= total) return;
   const int id = sh_rid(recv_ids, e, C, rstride);
   if (id < 0) return;
   const int p = e / C;
-  const size_t row = (size_t)(id / N);
+  const size_t row = (size_t)(id / rdiv);
   const unsigned cur = (unsigned)(*step + 1);
   const unsigned long long* tr = sh_find(T, N, (unsigned)row, cur);
   if (!tr) return;  // cannot happen: every received row was inserted by this step's serve / tag
@@ -431,10 +432,10 @@ __global__ void sh_owner_apply_kernel(const int* __restrict__ recv_ids, int tota
                                       const float* __restrict__ recv_g, ShTable T, float* tv, float* tw,
                                       float* s0v, float* s1v, float* s0w, float* s1w, long ldv, long ldw,
                                       float* Gv, float* Gw, OptHyper h, const int64_t* __restrict__ step,
-                                      ShTable NT, float* next_rows) {
+                                      ShTable NT, float* next_rows, int rdiv) {
   sh_owner_apply_elem<K, MODE, OPT>(blockIdx.x * blockDim.x + threadIdx.x, recv_ids, total, N, C, rstride,
                                     recv_g, T, tv, tw, s0v, s1v, s0w, s1w, ldv, ldw, Gv, Gw, h, step, NT,
-                                    next_rows);
+                                    next_rows, rdiv);
 }
 
 // ------------------------------------------------------------------------------------ host API
@@ -521,7 +522,10 @@ struct ShApplyArgs {
   const int64_t* step;
   ShTable next;       // lazy mode: the next step's request table when its rows were served ahead
   float* next_rows;   //   (key == null: none) and its served rows, patched by this update
+  int rdiv;           // local row = id / rdiv (0: N, the row-sharded owner; 1: a replicated table)
 };
+
+__host__ __device__ static inline int sh_rdiv(const ShApplyArgs& A) { return A.rdiv > 0 ? A.rdiv : A.N; }
 
 template <int K>
 static int sh_apply_k(int opt, const ShApplyArgs& A, hipStream_t st) {
@@ -529,11 +533,12 @@ static int sh_apply_k(int opt, const ShApplyArgs& A, hipStream_t st) {
   const int grid = (int)((th + 255) / 256);
   if (A.mode & 2)  // tags not stamped by this step's serve (eval-style fetch): stamp them here
     hipLaunchKernelGGL(sh_owner_tag_kernel, dim3((A.total + 255) / 256), dim3(256), 0, st, A.recv_ids,
-                       A.total, A.N, A.C, A.rstride, A.step, A.table);
+                       A.total, A.N, A.C, A.rstride, A.step, A.table, sh_rdiv(A));
 #define L_(M, O)                                                                                      \
   hipLaunchKernelGGL((sh_owner_apply_kernel<K, M, O>), dim3(grid), dim3(256), 0, st, A.recv_ids, A.total, \
                      A.N, A.C, A.rstride, A.recv_g, A.table, A.tv, A.tw, A.s0v, A.s1v, A.s0w, A.s1w, A.ldv, A.ldw, \
-                     A.Gv, A.Gw, A.h, A.step, (M) == 0 ? A.next : ShTable{nullptr, nullptr, 0u, 0}, A.next_rows)
+                     A.Gv, A.Gw, A.h, A.step, (M) == 0 ? A.next : ShTable{nullptr, nullptr, 0u, 0}, A.next_rows, \
+                     sh_rdiv(A))
   if ((A.mode & 1) == 1) {
     L_(1, 0);
     return 0;
@@ -592,7 +597,7 @@ __global__ void __launch_bounds__(256) sh_apply_dense_kernel(ShApplyArgs A, ShDe
   if (b < apply_blocks) {
     sh_owner_apply_elem<K, 0, OPT>(b * 256 + threadIdx.x, A.recv_ids, A.total, A.N, A.C, A.rstride, A.recv_g,
                                    A.table, A.tv, A.tw, A.s0v, A.s1v, A.s0w, A.s1w, A.ldv, A.ldw, A.Gv, A.Gw,
-                                   A.h, A.step, A.next, A.next_rows);
+                                   A.h, A.step, A.next, A.next_rows, sh_rdiv(A));
   } else {
     const float lr_t = OPT == OPT_ADAM ? adam_lr_t(D.h, *A.step + 1) : D.h.lr;
     for (long i = (long)(b - apply_blocks) * 256 + threadIdx.x; i < D.n; i += (long)D.blocks * 256) {
@@ -615,9 +620,14 @@ __global__ void __launch_bounds__(256) sh_apply_dense_kernel(ShApplyArgs A, ShDe
   }
 }
 
-// lazy rows only (mode 0; tags stamped by this step's serve)
+// lazy rows only: mode 0 (tags stamped by this step's serve) or 2 (tagged here first: the
+// replicated-table exchange has no serve)
 HFM_API int hfm_sh_apply_dense(int K, int opt, const ShApplyArgs* A, const ShDenseArgs* D, hipStream_t st) {
-  if (A->mode != 0 || !D->done || D->blocks < 1 || !A->step) return (int)hipErrorInvalidValue;
+  if ((A->mode & 1) != 0 || !D->done || D->blocks < 1 || !A->step) return (int)hipErrorInvalidValue;
+  if (A->total <= 0) return (int)hipErrorInvalidValue;
+  if (A->mode & 2)
+    hipLaunchKernelGGL(sh_owner_tag_kernel, dim3((A->total + 255) / 256), dim3(256), 0, st, A->recv_ids,
+                       A->total, A->N, A->C, A->rstride, A->step, A->table, sh_rdiv(*A));
   if (A->next.key && (!A->next_rows || (A->next.mask & (A->next.mask + 1)) != 0)) return (int)hipErrorInvalidValue;
   const long th = (long)A->total * (K / 4);
   const int ab = (int)((th + 255) / 256);

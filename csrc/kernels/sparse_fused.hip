@@ -66,7 +66,9 @@ struct SfArgs {
   float* gout;
   int step_off;
   unsigned* flags;  // [tiles] publication flags: the step's 1-based index (*step + step_off)
-  unsigned* sync;   // {pad, pad, error bits, pad}    // 1: *step is this step's index - 1 (the dense optimizer advances it later);
+  unsigned* sync;   // {pad, pad, error bits, pad}
+  int v_by_key;     // MODE 2: 1 = V rows from the local table row key / row_div (replicated-table
+                    // exchange), 0 = from the received rows at upos (row-sharded exchange)    // 1: *step is this step's index - 1 (the dense optimizer advances it later);
                    // 0: the dense optimizer already ran and advanced it (single-GPU early mode)
 };
 
@@ -78,7 +80,8 @@ __device__ __forceinline__ void sf_apply_row(const SfArgs& A, int key, int hpos,
   if (MODE == 2) {
     const int r = A.upos[A.sid[hpos] - 1];
     if (r < 0) return;  // capacity overflow (flagged by the bucketing kernel)
-    const f32x4 pv = *reinterpret_cast<const f32x4*>(A.tv + (size_t)r * A.ldv + sub * 4);
+    const size_t vr = A.v_by_key ? (size_t)(key / A.row_div) : (size_t)r;
+    const f32x4 pv = *reinterpret_cast<const f32x4*>(A.tv + vr * A.ldv + sub * 4);
     float* go = A.gout + (size_t)r * (K + 4);
     *reinterpret_cast<f32x4*>(go + sub * 4) = a - pv * c;
     if (sub == 0) *reinterpret_cast<f32x4*>(go + K) = f32x4{w, 0.f, 0.f, 0.f};
@@ -149,7 +152,12 @@ __device__ __forceinline__ void sf_lookback(const SfArgs& A, int tile, unsigned 
       }
       __builtin_amdgcn_s_sleep(2);
     }
-    asm volatile("" ::: "memory");  // every handed-off word below is read write-through (sc1)
+    // agent-scope acquire after the poll matched (cdna guide §6 G16): the handed-off words below
+    // are written sc1 and read sc1, but that fence-free form is only validated for one workgroup
+    // per CU -- this kernel runs several, and without the acquire a look-back read stale partial
+    // sums now and then (wrong hot-row gradients, not bitwise reproducible across runs)
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const bool has_head = valid && !hx_ldi(A.tinfo + t2 * 4);
     const unsigned long long stop = __ballot(has_head);
     const int first = stop ? __ffsll((long long)stop) - 1 : 64;  // the run's origin tile (lane)

@@ -2,9 +2,12 @@
 //
 // Two forms.  (1) Small payloads: stored write-through (relaxed agent-scope atomic stores, sc1),
 // a drain of EVERY storing wave, a barrier, ONE relaxed atomic flag store; the consumer polls
-// relaxed and reads the payload with relaxed agent-scope atomic loads (sc1): no fences at all.  A
-// release fence per producer workgroup writes back its XCD's whole L2 -- with 1248 producers that
-// cost the sparse kernel 2x.  (2) Bulk payloads: plain stores, drain, barrier, ONE agent-scope
+// relaxed, runs ONE agent-scope acquire after the match (its workgroups share CUs: the fence-free
+// sc1-load form is validated for one workgroup per CU only -- without it the sparse look-back
+// and the wgfin split-K combine read stale partials now and then) and reads the payload with
+// relaxed agent-scope atomic loads (sc1).  A release fence per producer workgroup writes back its
+// XCD's whole L2 -- with 1248 producers that cost the sparse kernel 2x -- so producers stay
+// write-through.  (2) Bulk payloads: plain stores, drain, barrier, ONE agent-scope
 // release fence (+ a second drain) and ONE relaxed atomic on the counter; the consumer polls
 // relaxed with s_sleep back-off, then ONE agent-scope acquire before plain loads.
 // Waits are only ever on workgroups with a LOWER linear id (dispatched earlier on every XCD), so

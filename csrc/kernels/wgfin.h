@@ -164,6 +164,13 @@ __device__ __forceinline__ void wgfin_body(const WgFinArgs& a, int b, WgfSmem& s
     if (tid == 0) {
       const unsigned prev = __hip_atomic_fetch_add(a.tile_ctr + jb.tile0 + tile, 1u, HFM_RLX_AGENT);
       sm.last = (prev % (unsigned)a.ns) == (unsigned)(a.ns - 1);
+      if (sm.last) {
+        // the tile's last arriver reads the other splits' slabs: ONE agent-scope acquire first
+        // (cdna guide §6 G16; the sc1-only form is validated for one workgroup per CU only), its
+        // wait, then the barrier releases the reading waves
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
     }
     __syncthreads();
     if (sm.last) {  // the tile's last workgroup: sum the NS slabs in slab order, then the optimizer

@@ -143,6 +143,7 @@ def run(cfg: RunConfig) -> dict:
                         k += 1
                         b = nb
                     est.adopt_field_ranges(pipe)
+                    est.calibrate_exchange(pipe)
 
             class _Run:                  # the whole run as one batch source (cache flag visible)
                 countable = True
@@ -173,6 +174,7 @@ def run(cfg: RunConfig) -> dict:
                           eval_fn=lambda: est.evaluate(va()))
                 est.epoch, est.epoch_batch = epoch + 1, 0
                 est.adopt_field_ranges(pipe)
+                est.calibrate_exchange(pipe)
                 result = est.evaluate(va())
                 if max_steps is not None and est.global_step >= max_steps:
                     break

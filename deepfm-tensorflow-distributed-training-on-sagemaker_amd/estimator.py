@@ -441,6 +441,31 @@ class Estimator:
         self.log.info("per-field id ranges derived from the cached epoch: per-field slot sort on")
         return True
 
+    def calibrate_exchange(self, pipeline, slack: float = 1.3, pad: int = 1024) -> bool:
+        """After the first epoch was cached: measure the fixed-size exchange's capacity on the
+        cached batches (unique ids per owner / per batch), agree on the MAX over ranks, and
+        re-plan the exchange with it when it is smaller than the current (uncalibrated) one.  The
+        margin covers evaluation batches, which route through the same exchange (an overflow
+        raises, rows are never dropped).  Returns True if the exchange was re-planned."""
+        m = self.model if self.native else None
+        cached = getattr(pipeline, "_cached", None)
+        if m is None or not m.exchange or m.exchange_capacity() is None:
+            return False
+        from .parallel.dist import agree_max, exchange_capacity
+        have = agree_max(0 if not cached else 1, self._ctl)   # MAX: does any rank have a cache?
+        have_all = -agree_max(-(1 if cached else 0), self._ctl)
+        if not have or not have_all:
+            return False
+        cap = exchange_capacity((b[0] for b in cached), self.world, m.sharded, slack=slack, pad=pad,
+                                group=self._ctl)
+        if cap >= m.exchange_capacity():
+            return False
+        torch.cuda.synchronize(self.device)
+        m.set_exchange_capacity(cap)
+        self.log.info(f"exchange capacity calibrated on the cached epoch: {cap} "
+                      f"({'per owner' if m.sharded else 'per rank'})")
+        return True
+
     def _nan_check(self):
         for name, t in (("fm_v", self.model.tv), ("dense", self.model.p)):
             if not torch.isfinite(t).all():

@@ -551,9 +551,14 @@ class NativeDeepFM:
             self._build_wgfin()
         self._bufs_M = M
         self.shx = None
+        self.rpx = None
         if self.sharded and getattr(self.comm, "engine", None) is not None:
             from ..parallel.sharded import FixedCapacityExchange
             self.shx = FixedCapacityExchange(self, self.comm.engine, self.comm.capacity)
+        elif self.exchange and getattr(self.comm, "engine", None) is not None:
+            # replicated table (Horovod parity): fixed-capacity all-gather of unique gradient rows
+            from ..parallel.replicated import ReplicatedExchange
+            self.rpx = ReplicatedExchange(self, self.comm.engine, self.comm.capacity)
         self._own_in = (self.idx, self.vals, self.labels)
         self._graphs = {}
         self._run_memo = {}
@@ -577,6 +582,24 @@ class NativeDeepFM:
             self._fsort_next = KN.FieldSort(self.field_ranges, min(M, KN.field_sort_max_rows()),
                                             dev, max_pb=int(pb) if pb is not None else 0,
                                             err=self.err_words[1:2])
+
+    def exchange_capacity(self) -> Optional[int]:
+        """Block capacity of the native fixed-size exchange (None without one)."""
+        x = self.shx if self.shx is not None else self.rpx
+        return None if x is None else x.C
+
+    def set_exchange_capacity(self, capacity: int):
+        """Re-plan the fixed-size exchange with a measured capacity (every rank the same value):
+        new exchange buffers, routing sets and request tables; captured graphs are dropped."""
+        self.comm.capacity = int(capacity)
+        if self.shx is not None:
+            from ..parallel.sharded import FixedCapacityExchange
+            self.shx = FixedCapacityExchange(self, self.comm.engine, self.comm.capacity)
+        elif self.rpx is not None:
+            from ..parallel.replicated import ReplicatedExchange
+            self.rpx = ReplicatedExchange(self, self.comm.engine, self.comm.capacity)
+        self._graphs = {}
+        self._run_memo = {}
 
     def set_field_ranges(self, ranges):
         """Per-field id ranges found after construction (e.g. derived while caching the first
@@ -884,6 +907,8 @@ class NativeDeepFM:
             self.sfwg_done.zero_()
         if getattr(self, "shx", None) is not None:
             self.shx.reset_table()
+        if getattr(self, "rpx", None) is not None:
+            self.rpx.reset_table()
         if getattr(self, "tf1_split", False):
             self.sw_step.copy_(self.step)
             self._sw_done.zero_()
@@ -1131,6 +1156,9 @@ class NativeDeepFM:
             raise RuntimeError(f"sparse backward hand-off failed (error bits {w[6]:#x}): a look-back "
                                "timed out or read an inconsistent tile publication")
         if w[2]:
+            if getattr(self, "rpx", None) is not None:
+                raise RuntimeError(f"replicated exchange: a batch has more than capacity="
+                                   f"{self.rpx.C} unique ids (raise the capacity)")
             C = self.shx.C if self.shx is not None else "?"
             raise RuntimeError(f"row-sharded exchange: a rank sent more than capacity={C} "
                                "unique ids to one owner (raise the capacity)")
@@ -1139,6 +1167,10 @@ class NativeDeepFM:
         """Raise on device-side errors flagged by earlier steps (one host sync)."""
         self._err_ev = None
         self._raise_errors(self.err_words.tolist())
+        temps = [self.temp] + ([rs.temp for rs in self.shx.sets] if self.shx is not None else [])
+        if any(KN.sort_error(t) for t in temps):
+            raise RuntimeError("the global slot sort's look-back timed out (a tile's predecessor "
+                               "never published): the sort order of that step is invalid")
 
     def poll_errors(self):
         """Asynchronous error check, called after every enqueued step / graph replay: raises on
@@ -1190,6 +1222,12 @@ class NativeDeepFM:
             return self.comm.sharded_backward(self, B, idx, tv)
         if not presorted:
             self._sort_slots(B)
+        if self.rpx is not None:
+            self.rpx.backward(B, dense=self._sh_dense_args() if self._sh_apply_dense else None,
+                              join=self._sh_join,
+                              wgfin=self._wgfin_args(False) if self._sh_xfuse else None,
+                              dense_ar=self.g if self._sh_ar else None)
+            return None
         if self._sfwg_now:
             KN.sparse_wgfin(self.K, self.opt_id, self.sf_args(n), self._wgfin_args(True), self.sfwg_done,
                             sweep=self._sweep_args() if self._tf1_merged else None)
@@ -1344,7 +1382,8 @@ class NativeDeepFM:
         # row-sharded lazy step with wgfin: the dense gradient is computed in the sparse backward's
         # launch and travels with the gradient rows' exchange (all-gather, summed in rank order
         # by the owner launch): no comm stream, no all-reduce, no cross-stream joins
-        xfuse = (self.shx is not None and self.sparse_update == "lazy" and _SH_XFUSE and _WGFIN and
+        xch = self.shx if self.shx is not None else self.rpx     # native fixed-capacity exchange
+        xfuse = (xch is not None and self.sparse_update == "lazy" and _SH_XFUSE and _WGFIN and
                  self.fused and _SH_APPLY_DENSE and getattr(self, "_wgfin_ns", 1 << 30) <= KN.SFWG_MAX_NS)
         self._sh_xfuse = xfuse
         split = self.fused and not xfuse and (_DENSE_SIDE_STREAM == "1" or
@@ -1381,7 +1420,7 @@ class NativeDeepFM:
         # row-sharded step: the dense all-reduce rides in the gradient exchange group on the main
         # stream (parallel/sharded.py: one communicator, fixed order); replicated: the process
         # group's all-reduce, overlapped with the sparse backward
-        shx_ar = self.shx is not None and not xfuse
+        shx_ar = xch is not None and not xfuse
         if split:
             # dense gradient branch overlapped with the sparse backward
             if self._comm_stream is None:
@@ -1397,7 +1436,7 @@ class NativeDeepFM:
         # exchange group; with lazy rows the dense optimizer rides in the owner update's launch
         self._sh_join = None
         self._sh_apply_dense = False
-        if self.shx is not None:
+        if xch is not None:
             cs = self._comm_stream if split else None
             self._sh_join = (lambda cs=cs: main.wait_stream(cs)) if cs is not None else None
             self._sh_apply_dense = (self.sparse_update == "lazy" and _SH_APPLY_DENSE and

@@ -114,7 +114,7 @@ class SfArgs(C.Structure):
                 ("s0w", c_void_p), ("s1w", c_void_p), ("Gv", c_void_p), ("Gw", c_void_p),
                 ("h", OptHyper), ("step", c_void_p), ("ldv", c_long), ("ldw", c_long),
                 ("sid", c_void_p), ("upos", c_void_p), ("gout", c_void_p), ("step_off", c_int),
-                ("flags", c_void_p), ("sync", c_void_p)]
+                ("flags", c_void_p), ("sync", c_void_p), ("v_by_key", c_int)]
 
 
 class ShTable(C.Structure):
@@ -127,7 +127,7 @@ class ShApplyArgs(C.Structure):
                 ("rstride", c_int), ("recv_g", c_void_p), ("table", ShTable), ("tv", c_void_p), ("tw", c_void_p),
                 ("s0v", c_void_p), ("s1v", c_void_p), ("s0w", c_void_p), ("s1w", c_void_p),
                 ("ldv", c_long), ("ldw", c_long), ("Gv", c_void_p), ("Gw", c_void_p), ("h", OptHyper),
-                ("step", c_void_p), ("next", ShTable), ("next_rows", c_void_p)]
+                ("step", c_void_p), ("next", ShTable), ("next_rows", c_void_p), ("rdiv", c_int)]
 
 
 class ShDenseArgs(C.Structure):

@@ -16,7 +16,9 @@ Replaces the reference's two distribution paths:
   xGMI is a full mesh of point-to-point links, so all-to-all uses all 7 peer links at once,
   where a ring all-gather of the Horovod IndexedSlices is per-link bound.
 * ``replicated`` mode keeps a full table per rank (Horovod parity): the unique (id, row-grad)
-  pairs of every rank are all-gathered (not the reference's B*F+V rows) and reduced identically.
+  pairs of every rank are all-gathered in fixed-capacity blocks (not the reference's B*F+V
+  rows) and reduced in rank order, identically on every rank (parallel/replicated.py; the
+  torch.distributed ``replicated_exchange`` below is the host-synchronous fallback).
 
 Gradient averaging: the head kernel scales dlogit by 1/(B*N), so SUM all-reduces average.
 """
@@ -50,6 +52,32 @@ def init_distributed(backend: Optional[str] = None, timeout_s: int = 600):
     dist.init_process_group(**kw)
 
 
+def agree_max(value: int, group=None) -> int:
+    """The MAX of an int over the ranks of ``group`` (identical on every rank; gloo or RCCL)."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
+        return int(value)
+    dev = (torch.device("cuda", torch.cuda.current_device())
+           if dist.get_backend(group) == "nccl" else torch.device("cpu"))
+    t = torch.tensor([int(value)], dtype=torch.int64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return int(t.item())
+
+
+def exchange_capacity(id_batches, world: int, sharded: bool, slack: float = 1.05, pad: int = 256,
+                      group=None) -> int:
+    """Capacity of the fixed-size exchange, measured on every batch this rank will route and
+    agreed across ranks (MAX): unique ids per owner (row-sharded all-to-all blocks) or unique
+    ids per batch (replicated all-gather blocks).  Used by bench.py and the Estimator."""
+    ids = list(id_batches)
+    if sharded:
+        from .sharded import estimate_capacity
+        local = estimate_capacity(ids, world, slack=slack, pad=pad)
+    else:
+        from .replicated import estimate_unique_capacity
+        local = estimate_unique_capacity(ids, slack=slack, pad=pad)
+    return agree_max(local, group)
+
+
 def world_info():
     if dist.is_available() and dist.is_initialized():
         return dist.get_rank(), dist.get_world_size()
@@ -74,17 +102,13 @@ class Comm:
         # sync, graph-capturable step.  ONE communicator carries every collective of the step
         # in a fixed order (parallel/sharded.py module docstring: deadlock freedom)
         if native is None:
-            native = (dist.get_backend(group) == "nccl" and self.sharded and
-                      knob("HIPFM_SHARD_EXCHANGE") == "fixed")
+            native = (dist.get_backend(group) == "nccl" and (self.world_size > 1 or self.force_exchange)
+                      and knob("HIPFM_SHARD_EXCHANGE") == "fixed")
         self.engine = None
         if capacity is not None and self.world_size > 1:
-            # every rank must use the SAME per-peer block size in the fixed-capacity all-to-alls:
-            # take the max of the per-rank estimates (each rank measured its own batches)
-            cdev = (torch.device("cuda", torch.cuda.current_device())
-                    if dist.get_backend(group) == "nccl" else torch.device("cpu"))
-            t = torch.tensor([int(capacity)], dtype=torch.int64, device=cdev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
-            capacity = int(t.item())
+            # every rank must use the SAME block size in the fixed-capacity exchanges: take the
+            # max of the per-rank estimates (each rank measured its own batches)
+            capacity = agree_max(capacity, group)
         self.capacity = capacity
         if native:
             from .sharded import RcclEngine

@@ -1,0 +1,133 @@
+"""Replicated-table data parallelism (Horovod parity, BASELINE config #3) as a captured step.
+
+The reference's Horovod path keeps a full table per rank; ``DistributedOptimizer`` averages the
+dense gradients with an all-reduce and all-gathers the embedding ``IndexedSlices`` -- every
+slot's row gradient plus the whole-table L2 term, ``B*F + V`` rows per rank (HVD:262; SURVEY
+§2.6 X2-X4).  Here each rank sends only its UNIQUE ids and their summed row gradients, in a
+fixed-capacity block, so no size ever crosses to the host and the whole step is one HIP graph:
+
+  local   : slot sort (the single-GPU side-stream / prefetched sort) -> sh_route with ONE bucket
+            (unique ids in id order, per-slot unique index, capacity overflow flag) -> the fused
+            sparse backward in exchange mode writes one gradient row per unique id (V read from
+            the local table by id) -- and, with the fused tower, the dense gradient in the same
+            launch
+  exchange: ONE grouped RCCL operation on the main stream: all-gather of the [C] ids and the
+            [C, K+4] gradient rows (+ the dense gradients: all-gather, summed in rank order by
+            the update launch; or all-reduce)
+  update  : every rank runs the owner-update kernel of the row-sharded path over all N ranks'
+            blocks with ``rdiv = 1`` (local row = id): the lowest rank holding an id sums all
+            ranks' rows IN RANK ORDER and applies the optimizer (lazy), or scatters into the
+            tf1_dense gradient for the full-table sweep.  Identical arithmetic on every rank keeps
+            the replicas bitwise identical; no atomics, deterministic.
+
+The L2 term of the whole-table loss is applied inside the update (lazy: touched rows; tf1_dense:
+the sweep), identically on every rank, so it never travels.  LR x N and the 1/(B*N) gradient
+scale follow HVD:149 / the head kernel.
+"""
+from __future__ import annotations
+
+import math
+from typing import Iterable, Optional
+
+import torch
+
+from ..ops import kernels as KN
+from ..ops._lib import ShApplyArgs, ShTable
+
+
+def estimate_unique_capacity(id_batches: Iterable[torch.Tensor], slack: float = 1.05, pad: int = 256) -> int:
+    """Per-rank capacity of the replicated exchange: max unique ids of a batch, times ``slack``,
+    plus ``pad``, rounded to 64."""
+    mx = 0
+    for ids in id_batches:
+        mx = max(mx, int(torch.unique(ids.reshape(-1)).numel()))
+    return int(math.ceil((mx * slack + pad) / 64.0) * 64)
+
+
+class ReplicatedExchange:
+    """Buffers + the backward/exchange/update piece of the replicated-table step (one rank)."""
+
+    def __init__(self, m, engine, capacity: Optional[int] = None):
+        self.m, self.eng = m, engine
+        self.N, self.rank = engine.world, engine.rank
+        dev = m.device
+        n = m.M * m.F
+        self.C = min(n, int(capacity)) if capacity else n
+        self.C = (self.C + 63) // 64 * 64
+        self.RW = m.K + 4
+        i32 = dict(dtype=torch.int32, device=dev)
+        f32 = dict(dtype=torch.float32, device=dev)
+        self.send_ids = torch.full((self.C,), -1, **i32)
+        self.upos = torch.zeros(n, **i32)
+        self.tcnt = torch.zeros(KN.sh_route_tiles(n) * 2, **i32)
+        self.send_cnt = torch.zeros(1, **i32)
+        self.num_u = torch.zeros(1, **i32)
+        self.send_g = torch.zeros(self.C, self.RW, **f32)
+        T = self.N * self.C
+        self.g_ids = torch.full((T,), -1, **i32)
+        self.g_rows = torch.zeros(T, self.RW, **f32)
+        slots = 1
+        while slots < 2 * T:
+            slots *= 2
+        self.req_key = torch.zeros(slots, dtype=torch.int64, device=dev)
+        self.req_pos = torch.zeros(slots * self.N, dtype=torch.int64, device=dev)
+        self.table = ShTable(self.req_key.data_ptr(), self.req_pos.data_ptr(), slots - 1, 0)
+        self.err = m.err_words[2:3]           # capacity overflow (the model's error words)
+        self.dense_recv = None
+        self.trace = None
+        self._main = None
+
+    def _issue(self, ops):
+        if self.trace is not None:
+            self.trace.append(tuple((k, int(nb)) for k, _, _, nb in ops))
+        self.eng.group(ops)
+
+    def backward(self, B: int, dense=None, join=None, wgfin=None, dense_ar=None):
+        """Sorted slots (m.sorted_keys / m.perm) -> unique gradient rows -> all-gather -> rank-
+        ordered update of every rank's replica.  ``wgfin`` / ``dense`` / ``join`` / ``dense_ar`` as
+        in ``FixedCapacityExchange.backward``."""
+        m = self.m
+        n = B * m.F
+        KN.sh_route(m.sorted_keys, n, 1, self.C, self.tcnt, m.sid_incl, self.send_ids, self.upos,
+                    self.send_cnt, self.num_u, self.err)
+        A = m.sf_args(n)
+        A.sid, A.upos, A.gout = m.sid_incl.data_ptr(), self.upos.data_ptr(), self.send_g.data_ptr()
+        A.v_by_key = 1                      # V rows from the local replica, by id
+        if wgfin is not None:
+            KN.sparse_wgfin_x(m.K, A, wgfin)
+        else:
+            KN.sparse_fused(m.K, KN.SF_EXCHANGE, m.opt_id, A)
+        if join is not None:
+            join()
+        ops = [(KN.COMM_ALLGATHER, self.send_ids, self.g_ids, self.C * 4),
+               (KN.COMM_ALLGATHER, self.send_g, self.g_rows, self.C * self.RW * 4)]
+        if wgfin is not None:
+            if self.dense_recv is None:
+                self.dense_recv = torch.zeros(self.N * m.P, dtype=torch.float32, device=m.device)
+            ops.append((KN.COMM_ALLGATHER, m.g[: m.P], self.dense_recv, m.P * 4))
+            dense.g, dense.nsum = self.dense_recv.data_ptr(), self.N
+        elif dense_ar is not None:
+            ops.append((KN.COMM_ALLREDUCE, dense_ar, dense_ar, dense_ar.numel() * 4))
+        self._issue(ops)
+        S = ShApplyArgs()
+        S.recv_ids, S.total, S.N, S.C = self.g_ids.data_ptr(), self.N * self.C, self.N, self.C
+        S.rstride, S.rdiv = 0, 1
+        S.mode = (0 if m.sparse_update == "lazy" else 1) | 2          # tags stamped in the launch
+        S.recv_g, S.table = self.g_rows.data_ptr(), self.table
+        S.tv, S.tw = m.tv.data_ptr(), m.tw.data_ptr()
+        S.s0v, S.s1v, S.s0w, S.s1w = (t.data_ptr() if t.numel() else 0 for t in m.sv)
+        S.ldv, S.ldw = KN._ld(m.tv, m.tw)
+        if m.sparse_update == "tf1_dense":
+            S.Gv, S.Gw = m.Gv.data_ptr(), m.Gw.data_ptr()
+        S.h = m.h_sparse
+        S.step = m.step.data_ptr()
+        if dense is not None:
+            KN.sh_apply_dense(m.K, m.opt_id, S, dense)
+            return
+        KN.sh_owner_apply(m.K, m.opt_id, S)
+        if m.sparse_update == "tf1_dense":
+            KN.dense_sweep(m.K, m.opt_id, m.R, m.tv, m.tw, m.Gv, m.Gw, m.sv, m.h_sparse, m.step)
+
+    def reset_table(self):
+        self.req_key.zero_()
+        self.req_pos.zero_()

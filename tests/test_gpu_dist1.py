@@ -36,7 +36,8 @@ def group():
 
 
 @pytest.mark.parametrize("sharded,update,prefetch", [(True, "lazy", False), (True, "tf1_dense", False),
-                                                     (False, "lazy", False), (True, "lazy", True)])
+                                                     (False, "lazy", False), (True, "lazy", True),
+                                                     (False, "tf1_dense", False), (False, "lazy", True)])
 def test_exchange_paths_match_local(group, sharded, update, prefetch):
     synth = make_synth("total:6000", seed=21)
     F, K, layers, keep = synth.F, 8, [64, 32], [0.8, 0.8]
@@ -135,3 +136,44 @@ def test_exchange_field_major_batches_bitwise(group):
         out.append((m.tv.clone(), m.tw.clone(), m.p.clone()))
     for x, y in zip(*out):
         assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("sharded", [True, False])
+def test_estimator_calibrates_exchange_capacity(group, tmp_path, sharded):
+    """the CLI's multi-GPU path ran on default_capacity (1.5x slots / N, ~3-4x the
+    measured need).  After the first epoch is cached the Estimator measures the capacity on the
+    cached batches (agreed MAX over ranks) and re-plans the exchange; training then continues on
+    the calibrated exchange (graph replays from the cache) without a capacity error."""
+    from hipfm.config import RunConfig
+    from hipfm.data import native_io as nio
+    from hipfm.data.pipeline import InputPipeline
+    from hipfm.cli import _EpochView
+    from hipfm.estimator import Estimator
+    from hipfm.parallel.sharded import default_capacity
+    synth = make_synth("total:6000", seed=41)
+    F, B = synth.F, 512
+    for k in range(2):
+        ids, vals, lab = synth.batch(B * 4, step=k)
+        nio.write_examples(str(tmp_path / f"tr-{k}.tfrecords"), lab.numpy(), ids.numpy(), vals.numpy())
+    cfg = RunConfig(feature_size=synth.feature_size, field_size=F, embedding_size=8, batch_size=B,
+                    deep_layers="64,32", dropout="1,1", sparse_update="lazy", device="cuda", log_steps=0,
+                    watchdog_secs=0, graph_steps=4)
+    est = Estimator(cfg)
+    comm = Comm(sharded=sharded, force_exchange=True)
+    est.model = NativeDeepFM(synth.feature_size, F, 8, [64, 32], [1.0, 1.0], sparse_update="lazy",
+                             batch_size=B, device="cuda", comm=comm)
+    m = est.model
+    before = m.exchange_capacity()
+    n = B * F
+    assert before == (default_capacity(n, 1) + 63) // 64 * 64 if sharded else before >= n
+    pipe = InputPipeline(sorted(str(p) for p in tmp_path.glob("tr-*")), F, B, 1, cache=True,
+                         device=est.device, id_dtype=torch.int32, id_limit=synth.feature_size)
+    est.train(_EpochView(pipe, 0))
+    assert est.calibrate_exchange(pipe)
+    after = m.exchange_capacity()
+    uniq = max(int(torch.unique(b[0]).numel()) for b in pipe._cached)
+    assert uniq <= after < before and after <= int(uniq * 1.3 + 1024) + 64
+    est.train(_EpochView(pipe, 1))
+    torch.cuda.synchronize()
+    m.check_errors()
+    assert est.global_step == 2 * len(pipe._cached)
