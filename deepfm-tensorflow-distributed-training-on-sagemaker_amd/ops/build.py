@@ -27,6 +27,12 @@ BUILD_DIR = os.path.join(REPO, "build", "obj")
 ARCH = knob("HIPFM_ARCH")
 
 KERNELS_SO = os.path.join(LIB_DIR, "libhipfm_kernels.so")
+# experiment: packed-FP32 VALU ops left on (HIPFM_BUILD_PACKED=1 -> its own objects and library,
+# loaded with HIPFM_KERNELS_SO; tests/test_gpu_determinism.py is the check)
+PACKED = knob("HIPFM_BUILD_PACKED") == "1"
+if PACKED:
+    KERNELS_SO = os.path.join(LIB_DIR, "libhipfm_kernels_packed.so")
+    BUILD_DIR = BUILD_DIR + "_packed"
 IO_SO = os.path.join(LIB_DIR, "libhipfm_io.so")
 
 
@@ -87,7 +93,8 @@ def build_kernels(force: bool = False, jobs: int = 8, verbose: bool = False) -> 
     todo = []
     def cmd_of(s, o):
         return [hipcc, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17",
-                "-fvisibility=hidden", "-Wno-unused-result", *NO_PACKED_F32, "-c", s, "-o", o]
+                "-fvisibility=hidden", "-Wno-unused-result", *([] if PACKED else NO_PACKED_F32),
+                "-c", s, "-o", o]
 
     for s in srcs:
         o = os.path.join(BUILD_DIR, os.path.basename(s) + ".o")

@@ -78,6 +78,7 @@ KNOBS: Dict[str, Knob] = {
     # ---- harness
     "HIPFM_ARCH": Knob("gfx950", "harness", "offload arch of the HIP build"),
     "HIPFM_KERNELS_SO": Knob(None, "harness", "path of the kernel library (default: in-tree _lib)"),
+    "HIPFM_BUILD_PACKED": Knob(None, "harness", "build: packed-FP32 ops on (own objects / library)"),
     "HIPFM_PIPE_ROOT": Knob(None, "harness", "directory of SageMaker pipe-mode FIFOs (tests)"),
     "HIPFM_FAULT_STEP": Knob(None, "harness", "fault injection: step at which a rank dies"),
     "HIPFM_FAULT_RANK": Knob(None, "harness", "fault injection: the rank (default all)"),
