@@ -184,6 +184,8 @@ def main():
     ap.add_argument("--embedding_mode", default="auto")
     ap.add_argument("--mlp_dtype", default="bf16", choices=["bf16", "fp8"],
                     help="deep-tower forward GEMM operands (fp8 = OCP e4m3 MFMA, config #5)")
+    ap.add_argument("--emb_dtype", default="fp32", choices=["fp32", "bf16"],
+                    help="fm_v rows + optimizer slots (bf16 = mixed-precision embeddings, config #5)")
     ap.add_argument("--pool", type=int, default=128,
                     help="resident synthetic batches per rank (the HBM-cached epoch; a 16-batch pool "
                          "replayed hundreds of times memorizes its ids: train loss -> 0, eval AUC drops)")
@@ -257,7 +259,8 @@ def main():
     model = NativeDeepFM(synth.feature_size, F, args.embedding_size, layers, keep, l2_reg=1e-4,
                          learning_rate=5e-4, optimizer=args.optimizer,
                          sparse_update=args.sparse_update, seed=1234, batch_size=B, device=dev,
-                         comm=comm, field_ranges=synth.field_ranges(), mlp_dtype=args.mlp_dtype)
+                         comm=comm, field_ranges=synth.field_ranges(), mlp_dtype=args.mlp_dtype,
+                         emb_dtype=args.emb_dtype)
     _progress()
     if args.field_major_ids:
         # ids stored field-major ([F, B] storage, [B, F] view): the per-field slot sort reads them
@@ -366,6 +369,8 @@ def main():
                 "graph_steps": G if use_graph else 0,
                 "exec": os.environ.get("HIPFM_BENCH_RUNG", "graph+prefetch" if use_graph else "eager"),
                 "mlp_dtype": args.mlp_dtype + (" fwd GEMMs, bf16 backward" if args.mlp_dtype == "fp8" else ""),
+                "emb_dtype": args.emb_dtype + (" rows + slots (stochastic rounding), fp32 math"
+                                               if args.emb_dtype == "bf16" else " tables + slots"),
             },
             "eval_auc": round(auc, 5),
             "train_loss": round(loss, 5),
@@ -399,7 +404,7 @@ def infer_bench(args):
     model = NativeDeepFM(synth.feature_size, synth.F, args.embedding_size, layers, keep,
                          optimizer=args.optimizer, sparse_update=args.sparse_update, seed=1234,
                          batch_size=B, device=dev, field_ranges=synth.field_ranges(),
-                         mlp_dtype=args.mlp_dtype)
+                         mlp_dtype=args.mlp_dtype, emb_dtype=args.emb_dtype)
     _progress()
     P = 16 * max(1, min(args.pool, 64) // 16)      # whole 16-request graphs
     reqs = [synth.batch(B, step=500_000 + i, device=dev, id_dtype=torch.int32) for i in range(P)]

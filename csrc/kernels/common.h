@@ -37,6 +37,40 @@ __device__ __forceinline__ bool dropout_keep(uint32_t flat, uint32_t salt, uint3
 __device__ __forceinline__ float bf2f(bf16 x) { return (float)x; }
 __device__ __forceinline__ bf16 f2bf(float x) { return (bf16)x; }
 
+// ---- embedding-table rows: fp32, or bf16 (mixed-precision embeddings, BASELINE config #5) ----
+// A row (or optimizer-slot row) starts at a float* inside the table record; a bf16 row holds its
+// K values in the first K/2 floats.  4 consecutive elements from element e (e % 4 == 0):
+__device__ __forceinline__ f32x4 ld_row4(const float* row, int e, bool bf) {
+  if (!bf) return *reinterpret_cast<const f32x4*>(row + e);
+  const uint2 u = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(row) + e);
+  return f32x4{__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xFFFF0000u), __uint_as_float(u.y << 16),
+               __uint_as_float(u.y & 0xFFFF0000u)};
+}
+// Stochastic rounding fp32 -> bf16 (unbiased: lazy-Adam moments move by ~0.1 % per step, below
+// bf16's 0.4 % resolution, and would freeze under round-to-nearest).  Counter-based and
+// deterministic: the random low half comes from fmix32 of (seed, element), so a replayed step
+// rounds identically.  Non-finite values are truncated unchanged.
+__device__ __forceinline__ uint32_t f2bf_sr(float x, uint32_t rnd) {
+  uint32_t b = __float_as_uint(x);
+  if ((b & 0x7F800000u) != 0x7F800000u) b += rnd & 0xFFFFu;
+  return b >> 16;
+}
+__device__ __forceinline__ void st_row4(float* row, int e, f32x4 v, bool bf, uint32_t seed) {
+  if (!bf) {
+    *reinterpret_cast<f32x4*>(row + e) = v;
+    return;
+  }
+  uint2 u;
+  u.x = f2bf_sr(v[0], fmix32(seed + 4u * e)) | (f2bf_sr(v[1], fmix32(seed + 4u * e + 1u)) << 16);
+  u.y = f2bf_sr(v[2], fmix32(seed + 4u * e + 2u)) | (f2bf_sr(v[3], fmix32(seed + 4u * e + 3u)) << 16);
+  *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(row) + e) = u;
+}
+// rounding seed of (table row, optimizer step, which array: 0 = v, 1 / 2 = slots)
+__device__ __forceinline__ uint32_t row_sr_seed(size_t row, int64_t step, uint32_t which) {
+  return fmix32((uint32_t)row ^ fmix32((uint32_t)(row >> 32) ^ ((uint32_t)step * 0x9E3779B1u) ^
+                                       (which * 0x85EBCA77u)));
+}
+
 // ---- OCP fp8 e4m3 (gfx950 v_cvt_pk_fp8_f32 is OCP e4m3fn, max 448; NOT MI300's fnuz) ----
 constexpr float FP8_MAX = 448.f;
 // 4 floats -> 4 e4m3 bytes (little-endian: a in byte 0), round-to-nearest-even, saturating

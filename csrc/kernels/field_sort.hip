@@ -37,10 +37,13 @@
 namespace {
 constexpr int FS_THREADS = 1024;
 constexpr int FS_WAVES = FS_THREADS / 64;
-constexpr int FS_IT = 16;
+// 8K rows per workgroup: its LDS (2 x 32 KB keys / positions + 16 KB digit counts) leaves room
+// for two tower workgroups on the same CU, so the next batch's sort co-runs with the step instead
+// of waiting for whole CUs to drain (at 16K rows a 148 KB sort workgroup needed an EMPTY CU)
+constexpr int FS_IT = 8;
 constexpr int FS_MAXB = FS_THREADS * FS_IT;  // rows per field
 constexpr int FS_PBMAX = 4;                   // up to 16 partitions per field
-constexpr int FS_MAXCHUNK = 16;               // row chunks per field (batches up to 256K)
+constexpr int FS_MAXCHUNK = 32;               // row chunks per field (batches up to 256K)
 constexpr int FS_LDS = (2 * FS_MAXB + FS_WAVES * 256 + 256 + 64) * 4;
 }  // namespace
 

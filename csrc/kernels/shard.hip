@@ -316,7 +316,7 @@ template <int K>
 __global__ void sh_serve_kernel(const int* __restrict__ recv_ids, int total, int N, int C, int rstride,
                                 const float* __restrict__ tv, const float* __restrict__ tw, long ldv,
                                 long ldw, float* __restrict__ rows, const int64_t* __restrict__ step,
-                                ShTable T, int stamp_off) {
+                                ShTable T, int stamp_off, int vbf16) {
   constexpr int LPS = K / 4, RW = K + 4;
   const int gt = blockIdx.x * blockDim.x + threadIdx.x;
   const int e = gt / LPS, sub = gt % LPS;
@@ -326,7 +326,7 @@ __global__ void sh_serve_kernel(const int* __restrict__ recv_ids, int total, int
   float w = 0.f;
   if (id >= 0) {
     const size_t row = (size_t)(id / N);
-    v = *reinterpret_cast<const f32x4*>(tv + row * ldv + sub * 4);
+    v = ld_row4(tv + row * ldv, sub * 4, vbf16);
     if (sub == 0) {
       w = tw[row * ldw];
       if (T.key) sh_insert(T, N, (unsigned)row, e / C, (unsigned)(e % C), (unsigned)(*step + stamp_off));
@@ -354,7 +354,7 @@ __device__ __forceinline__ void sh_owner_apply_elem(int gt, const int* __restric
                                                     float* s0w, float* s1w, long ldv, long ldw, float* Gv,
                                                     float* Gw, OptHyper h, const int64_t* __restrict__ step,
                                                     const ShTable& NT, float* __restrict__ next_rows,
-                                                    int rdiv) {
+                                                    int rdiv, int vbf16) {
   constexpr int LPS = K / 4, RW = K + 4;
   const int e = gt / LPS, sub = gt % LPS;
   if (e >= total) return;
@@ -382,11 +382,12 @@ __device__ __forceinline__ void sh_owner_apply_elem(int gt, const int* __restric
     return;
   }
   const float lr_t = OPT == OPT_ADAM ? adam_lr_t(h, *step + 1) : h.lr;
-  const size_t o = row * ldv + sub * 4, ow = row * ldw;
-  f32x4 pv = *reinterpret_cast<const f32x4*>(tv + o);
+  const size_t rb = row * ldv, ow = row * ldw;
+  const bool bf = vbf16 != 0;
+  f32x4 pv = ld_row4(tv + rb, sub * 4, bf);
   f32x4 a = {0, 0, 0, 0}, c = {0, 0, 0, 0};
-  if (OPT != OPT_GD) a = *reinterpret_cast<const f32x4*>(s0v + o);
-  if (OPT == OPT_ADAM || OPT == OPT_FTRL) c = *reinterpret_cast<const f32x4*>(s1v + o);
+  if (OPT != OPT_GD) a = ld_row4(s0v + rb, sub * 4, bf);
+  if (OPT == OPT_ADAM || OPT == OPT_FTRL) c = ld_row4(s1v + rb, sub * 4, bf);
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     float gj = g[j] + h.l2 * pv[j];
@@ -396,9 +397,13 @@ __device__ __forceinline__ void sh_owner_apply_elem(int gt, const int* __restric
     a[j] = aj;
     c[j] = cj;
   }
-  *reinterpret_cast<f32x4*>(tv + o) = pv;
-  if (OPT != OPT_GD) *reinterpret_cast<f32x4*>(s0v + o) = a;
-  if (OPT == OPT_ADAM || OPT == OPT_FTRL) *reinterpret_cast<f32x4*>(s1v + o) = c;
+  // (bf16: the served-ahead patch below copies the rounded value's fp32 pre-image: it feeds the
+  // next forward exactly as the rounded row would only up to the rounding, so the host never
+  // combines serve-ahead with bf16 rows)
+  const int64_t st = *step;
+  st_row4(tv + rb, sub * 4, pv, bf, bf ? row_sr_seed(row, st, 0) : 0u);
+  if (OPT != OPT_GD) st_row4(s0v + rb, sub * 4, a, bf, bf ? row_sr_seed(row, st, 1) : 0u);
+  if (OPT == OPT_ADAM || OPT == OPT_FTRL) st_row4(s1v + rb, sub * 4, c, bf, bf ? row_sr_seed(row, st, 2) : 0u);
   float wnew = 0.f;
   if (sub == 0) {
     float pw = tw[ow];
@@ -432,10 +437,10 @@ __global__ void sh_owner_apply_kernel(const int* __restrict__ recv_ids, int tota
                                       const float* __restrict__ recv_g, ShTable T, float* tv, float* tw,
                                       float* s0v, float* s1v, float* s0w, float* s1w, long ldv, long ldw,
                                       float* Gv, float* Gw, OptHyper h, const int64_t* __restrict__ step,
-                                      ShTable NT, float* next_rows, int rdiv) {
+                                      ShTable NT, float* next_rows, int rdiv, int vbf16) {
   sh_owner_apply_elem<K, MODE, OPT>(blockIdx.x * blockDim.x + threadIdx.x, recv_ids, total, N, C, rstride,
                                     recv_g, T, tv, tw, s0v, s1v, s0w, s1w, ldv, ldw, Gv, Gw, h, step, NT,
-                                    next_rows, rdiv);
+                                    next_rows, rdiv, vbf16);
 }
 
 // ------------------------------------------------------------------------------------ host API
@@ -493,7 +498,7 @@ HFM_API int hfm_sh_slot_rows(const int* perm, const int* sid_incl, const int* up
 HFM_API int hfm_sh_serve(int K, const int* recv_ids, int total, int N, int C, int rstride, const float* tv,
                          const float* tw,
                          long ldv, long ldw, float* rows, const int64_t* step, const ShTable* table,
-                         int stamp_off, hipStream_t st) {
+                         int stamp_off, int vbf16, hipStream_t st) {
   const long th = (long)total * (K / 4);
   const int grid = (int)((th + 255) / 256);
   if (grid == 0) return 0;
@@ -503,7 +508,7 @@ HFM_API int hfm_sh_serve(int K, const int* recv_ids, int total, int N, int C, in
   if (rstride > C && (C <= 0 || rstride % C)) return (int)hipErrorInvalidValue;
   if (stamp_off != 1 && stamp_off != 2) return (int)hipErrorInvalidValue;
 #define CALL(KK) hipLaunchKernelGGL(sh_serve_kernel<KK>, dim3(grid), dim3(256), 0, st, recv_ids, total, N, \
-                                    C, rstride, tv, tw, ldv, ldw, rows, step, T, stamp_off)
+                                    C, rstride, tv, tw, ldv, ldw, rows, step, T, stamp_off, vbf16)
   HFM_K_DISPATCH(K, CALL)
 #undef CALL
   HFM_LAUNCH_CHECK();
@@ -523,6 +528,7 @@ struct ShApplyArgs {
   ShTable next;       // lazy mode: the next step's request table when its rows were served ahead
   float* next_rows;   //   (key == null: none) and its served rows, patched by this update
   int rdiv;           // local row = id / rdiv (0: N, the row-sharded owner; 1: a replicated table)
+  int vbf16;          // table v rows and v slots are bf16 (lazy mode only)
 };
 
 __host__ __device__ static inline int sh_rdiv(const ShApplyArgs& A) { return A.rdiv > 0 ? A.rdiv : A.N; }
@@ -538,7 +544,7 @@ static int sh_apply_k(int opt, const ShApplyArgs& A, hipStream_t st) {
   hipLaunchKernelGGL((sh_owner_apply_kernel<K, M, O>), dim3(grid), dim3(256), 0, st, A.recv_ids, A.total, \
                      A.N, A.C, A.rstride, A.recv_g, A.table, A.tv, A.tw, A.s0v, A.s1v, A.s0w, A.s1w, A.ldv, A.ldw, \
                      A.Gv, A.Gw, A.h, A.step, (M) == 0 ? A.next : ShTable{nullptr, nullptr, 0u, 0}, A.next_rows, \
-                     sh_rdiv(A))
+                     sh_rdiv(A), (M) == 0 ? A.vbf16 : 0)
   if ((A.mode & 1) == 1) {
     L_(1, 0);
     return 0;
@@ -597,7 +603,7 @@ __global__ void __launch_bounds__(256) sh_apply_dense_kernel(ShApplyArgs A, ShDe
   if (b < apply_blocks) {
     sh_owner_apply_elem<K, 0, OPT>(b * 256 + threadIdx.x, A.recv_ids, A.total, A.N, A.C, A.rstride, A.recv_g,
                                    A.table, A.tv, A.tw, A.s0v, A.s1v, A.s0w, A.s1w, A.ldv, A.ldw, A.Gv, A.Gw,
-                                   A.h, A.step, A.next, A.next_rows, sh_rdiv(A));
+                                   A.h, A.step, A.next, A.next_rows, sh_rdiv(A), A.vbf16);
   } else {
     const float lr_t = OPT == OPT_ADAM ? adam_lr_t(D.h, *A.step + 1) : D.h.lr;
     for (long i = (long)(b - apply_blocks) * 256 + threadIdx.x; i < D.n; i += (long)D.blocks * 256) {

@@ -68,7 +68,8 @@ struct SfArgs {
   unsigned* flags;  // [tiles] publication flags: the step's 1-based index (*step + step_off)
   unsigned* sync;   // {pad, pad, error bits, pad}
   int v_by_key;     // MODE 2: 1 = V rows from the local table row key / row_div (replicated-table
-                    // exchange), 0 = from the received rows at upos (row-sharded exchange)    // 1: *step is this step's index - 1 (the dense optimizer advances it later);
+                    // exchange), 0 = from the received rows at upos (row-sharded exchange)
+  int vbf16;        // table v rows and v slots are bf16 (mixed-precision embeddings; MODE 0 / 2)    // 1: *step is this step's index - 1 (the dense optimizer advances it later);
                    // 0: the dense optimizer already ran and advanced it (single-GPU early mode)
 };
 
@@ -80,17 +81,18 @@ __device__ __forceinline__ void sf_apply_row(const SfArgs& A, int key, int hpos,
   if (MODE == 2) {
     const int r = A.upos[A.sid[hpos] - 1];
     if (r < 0) return;  // capacity overflow (flagged by the bucketing kernel)
-    const size_t vr = A.v_by_key ? (size_t)(key / A.row_div) : (size_t)r;
-    const f32x4 pv = *reinterpret_cast<const f32x4*>(A.tv + vr * A.ldv + sub * 4);
+    const f32x4 pv = A.v_by_key ? ld_row4(A.tv + (size_t)(key / A.row_div) * A.ldv, sub * 4, A.vbf16)
+                                : *reinterpret_cast<const f32x4*>(A.tv + (size_t)r * A.ldv + sub * 4);
     float* go = A.gout + (size_t)r * (K + 4);
     *reinterpret_cast<f32x4*>(go + sub * 4) = a - pv * c;
     if (sub == 0) *reinterpret_cast<f32x4*>(go + K) = f32x4{w, 0.f, 0.f, 0.f};
     return;
   }
   const size_t row = (size_t)(key / A.row_div);
-  const size_t o = row * A.ldv + sub * 4;
+  const size_t rb = row * A.ldv;  // the row's record (v, and the v slots at their offsets)
   const size_t ow = row * A.ldw;
-  f32x4 p = *reinterpret_cast<const f32x4*>(A.tv + o);
+  const bool bf = MODE == 0 && A.vbf16;
+  f32x4 p = ld_row4(A.tv + rb, sub * 4, bf);
   const f32x4 gv = a - p * c;
   if (MODE == 1) {
     *reinterpret_cast<f32x4*>(A.Gv + row * K + sub * 4) = gv;
@@ -98,8 +100,8 @@ __device__ __forceinline__ void sf_apply_row(const SfArgs& A, int key, int hpos,
     return;
   }
   f32x4 s0 = {0, 0, 0, 0}, s1 = {0, 0, 0, 0};
-  if (OPT != OPT_GD) s0 = *reinterpret_cast<const f32x4*>(A.s0v + o);
-  if (OPT == OPT_ADAM || OPT == OPT_FTRL) s1 = *reinterpret_cast<const f32x4*>(A.s1v + o);
+  if (OPT != OPT_GD) s0 = ld_row4(A.s0v + rb, sub * 4, bf);
+  if (OPT == OPT_ADAM || OPT == OPT_FTRL) s1 = ld_row4(A.s1v + rb, sub * 4, bf);
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     float gj = gv[j] + A.h.l2 * p[j];
@@ -109,9 +111,10 @@ __device__ __forceinline__ void sf_apply_row(const SfArgs& A, int key, int hpos,
     s0[j] = aj;
     s1[j] = cj;
   }
-  *reinterpret_cast<f32x4*>(A.tv + o) = p;
-  if (OPT != OPT_GD) *reinterpret_cast<f32x4*>(A.s0v + o) = s0;
-  if (OPT == OPT_ADAM || OPT == OPT_FTRL) *reinterpret_cast<f32x4*>(A.s1v + o) = s1;
+  const int64_t st = *A.step;
+  st_row4(A.tv + rb, sub * 4, p, bf, bf ? row_sr_seed(row, st, 0) : 0u);
+  if (OPT != OPT_GD) st_row4(A.s0v + rb, sub * 4, s0, bf, bf ? row_sr_seed(row, st, 1) : 0u);
+  if (OPT == OPT_ADAM || OPT == OPT_FTRL) st_row4(A.s1v + rb, sub * 4, s1, bf, bf ? row_sr_seed(row, st, 2) : 0u);
   if (sub == 0) {
     float pw = A.tw[ow];
     float gw = w + A.h.l2 * pw;

@@ -82,6 +82,7 @@ struct TowerArgs {
                                   // layout the per-field sort reads, so it needs no transpose)
   unsigned id_lim;                // > 0: gathered row ids clamped to [0, id_lim) (a bad id never
                                   // reads out of bounds; the slot sort flags it for the host)
+  int vbf16;                      // table v rows are bf16 (mixed-precision embeddings)
 };
 
 // fp8 variant of mma32 (16x16x32 fp8 MFMA; same fragment map as bf16 with 8 one-byte elements
@@ -198,9 +199,9 @@ __device__ __forceinline__ void tower_gather(const TowerArgs& a, int row0, bf16*
 #pragma unroll
     for (int t = 0; t < FMAX; ++t) {
       const bool ok = f0 + 8 * t < F;
-      const f32x4* row = reinterpret_cast<const f32x4*>(a.tv + (size_t)id[t] * a.ldv);
+      const float* row = a.tv + (size_t)id[t] * a.ldv;
 #pragma unroll
-      for (int j = 0; j < V4; ++j) v[t][j] = ok ? row[j] : f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < V4; ++j) v[t][j] = ok ? ld_row4(row, 4 * j, a.vbf16) : f32x4{0.f, 0.f, 0.f, 0.f};
       w[t] = ok ? a.tw[(size_t)id[t] * a.ldw] : 0.f;
     }
 #pragma unroll

@@ -50,6 +50,18 @@ def _init_dist(cfg: RunConfig):
         init_distributed(backend)
 
 
+def cache_budget_bytes(device, fraction: float = 0.8, reserve: int = 4 << 30) -> int:
+    """Bytes the cached epoch may take: a fraction of the device memory still free once the
+    model is allocated (minus a reserve for step buffers / graphs), or of available host RAM for
+    the CPU path.  An epoch that outgrows it streams every epoch instead (data/pipeline.py)."""
+    if device is not None and torch.device(device).type == "cuda":
+        free, _ = torch.cuda.mem_get_info(device)
+    else:
+        import psutil
+        free = psutil.virtual_memory().available
+    return max(0, int(free * fraction) - reserve)
+
+
 def build_pipelines(cfg: RunConfig, est: Estimator):
     rank, world = est.rank, est.world
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -86,7 +98,8 @@ def build_pipelines(cfg: RunConfig, est: Estimator):
     est.log.info(f"va_files: {va_files}")
     est.log.info(f"te_files: {te_files}")
     cache_tr = InputPipeline(tr_files, cfg.field_size, cfg.batch_size, 1, shard=shard,
-                             cache=cfg.cache_data, **common)
+                             cache=cfg.cache_data, cache_budget=(cfg.cache_budget_mb << 20 if cfg.cache_budget_mb >= 0
+                                           else cache_budget_bytes(est.device)), **common)
 
     def tr(epochs):
         return cache_tr

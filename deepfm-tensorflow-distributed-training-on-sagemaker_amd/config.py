@@ -91,6 +91,8 @@ _DEFS = [
     ("sparse_update", str, "tf1_dense", "tf1_dense (reference non-lazy semantics: every row moves "
      "every step, full-table L2) | lazy (touched rows only)"),
     ("mlp_dtype", str, "bf16", "bf16 | fp8 (deep-part GEMM input precision; accumulation is fp32)"),
+    ("emb_dtype", str, "fp32", "fp32 | bf16: fm_v rows + their optimizer slots (bf16: stochastic "
+     "rounding, lazy updates, gather-fused tower; config #5 mixed-precision embeddings)"),
     ("save_checkpoints_steps", int, 0, "checkpoint every N steps (0: use save_checkpoints_secs)"),
     ("save_checkpoints_secs", int, 600, "checkpoint every N seconds (TF Estimator default 600)"),
     ("keep_checkpoint_max", int, 5, "checkpoints to keep (TF default 5)"),
@@ -110,6 +112,8 @@ _DEFS = [
     ("export_tf_bundle", _str2bool, True, "also write a TF1 tensor_bundle checkpoint on export"),
     ("metrics_file", str, "", "JSONL metrics output (default <model_dir>/metrics.jsonl)"),
     ("cache_data", _str2bool, True, "keep the decoded dataset resident in device memory (cache())"),
+    ("cache_budget_mb", int, -1, "most MB the cached epoch may take (-1: 80 % of the device memory "
+     "free after the model is allocated, minus 4 GB); a larger epoch streams every epoch"),
     ("graph", _str2bool, True, "capture the train step in a HIP graph when possible"),
     ("max_steps", int, 0, "stop after this many steps (0 = run num_epochs)"),
     ("debug_sync", _str2bool, False, "synchronize + NaN/Inf check after each step (debug mode)"),
@@ -161,6 +165,7 @@ class RunConfig:
     embedding_mode: str = "auto"
     sparse_update: str = "tf1_dense"
     mlp_dtype: str = "bf16"
+    emb_dtype: str = "fp32"
     save_checkpoints_steps: int = 0
     save_checkpoints_secs: int = 600
     keep_checkpoint_max: int = 5
@@ -175,6 +180,7 @@ class RunConfig:
     export_tf_bundle: bool = True
     metrics_file: str = ""
     cache_data: bool = True
+    cache_budget_mb: int = -1
     graph: bool = True
     max_steps: int = 0
     debug_sync: bool = False
@@ -218,6 +224,8 @@ class RunConfig:
             raise ValueError(f"unknown sparse_update {self.sparse_update!r}")
         if self.mlp_dtype not in ("bf16", "fp8"):
             raise ValueError(f"unknown mlp_dtype {self.mlp_dtype!r} (bf16 | fp8)")
+        if self.emb_dtype not in ("fp32", "bf16"):
+            raise ValueError(f"unknown emb_dtype {self.emb_dtype!r} (fp32 | bf16)")
         if self.schedule not in ("hvd", "ps"):
             raise ValueError(f"unknown schedule {self.schedule!r} (hvd | ps)")
         if self.field_sizes:

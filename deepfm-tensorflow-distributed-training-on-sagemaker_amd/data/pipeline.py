@@ -18,6 +18,9 @@ The shard (n, i) itself follows the reference's flag matrix (C06, HVD:95-120, RD
   pipe mode : enable_data_multi_path x enable_s3_shard as in HVD:107-120.
 ``cache=True`` keeps the decoded epoch resident (device memory when given a device) — the
 reference's commented-out ``dataset.cache()`` (PS:125) done right (before repeat, DOC p.43-44).
+``cache_budget`` bounds it: an epoch whose decoded batches outgrow the budget is not cached, and
+every epoch streams from the files instead (the reference's behaviour, which has no cache) -- a
+dataset larger than free HBM (Criteo-1TB decodes to ~1.4 TB) trains instead of failing.
 """
 from __future__ import annotations
 
@@ -72,9 +75,13 @@ class ShardPlan:
 
 def plan_shard(files: Sequence[str], n: int, i: int, policy: str = "file", seed: int = 0,
                epoch: int = 0, shuffle: bool = True) -> ShardPlan:
+    """The files (and record shard) this rank reads.  The seeded shuffle is identical on every
+    rank AND every epoch (``epoch`` does not enter it): the reference shuffles its file list once
+    per job (PS:375), and an epoch streamed from the files then trains exactly like the epoch-0
+    order the HBM cache replays (a cache-budget fallback or a resume mid-epoch reproduces it)."""
     files = list(files)
     if shuffle:
-        random.Random(seed * 1000003 + epoch).shuffle(files)   # identical on every rank
+        random.Random(seed * 1000003).shuffle(files)   # identical on every rank and epoch
     if n <= 1:
         return ShardPlan(files, (1, 0))
     if policy == "file" and len(files) >= n:
@@ -195,7 +202,7 @@ class InputPipeline:
                  fmt: str = "tfrecord", shard: Tuple[int, int] = (1, 0), policy: str = "file",
                  seed: int = 0, shuffle_files: bool = True, threads: int = 4, cache: bool = False,
                  device=None, drop_remainder: bool = True, pipe_channel: Optional[str] = None,
-                 id_dtype=torch.int64, id_limit: int = 0):
+                 id_dtype=torch.int64, id_limit: int = 0, cache_budget: Optional[int] = None):
         self.files = list(files)
         self.F, self.B = int(field_size), int(batch_size)
         self.num_epochs = max(1, int(num_epochs))
@@ -212,11 +219,14 @@ class InputPipeline:
         self.pipe_channel = pipe_channel
         self.id_dtype = id_dtype
         self.id_limit = int(id_limit)            # > 0: ids must lie in [0, V) (checked by the loader)
+        self.cache_budget = cache_budget          # bytes the cached epoch may take (None: no bound)
+        self.cache_overflow = False               # the epoch outgrew the budget: stream every epoch
         self._cached: Optional[List[Tuple[torch.Tensor, ...]]] = None
         self.max_batches: Optional[int] = None   # equal-steps enforcement across ranks
         self.from_cache = False                  # the epoch being iterated replays the cache
         self.h2d_s = 0.0                          # host time issuing H2D copies (last epoch)
-        self._fmin = self._fmax = None           # per-field id min / max over the cached epoch
+        self._fmin = self._fmax = None           # per-field id min / max over the first epoch
+        self._stats_done = False
 
     @property
     def countable(self) -> bool:
@@ -260,7 +270,12 @@ class InputPipeline:
         plan = self.epoch_plan(epoch)
         loader = NativeLoader(plan.files, self.F, self.B, self.fmt, self.drop_remainder,
                               self.threads, plan.record_shard, id_limit=self.id_limit)
-        store = [] if (self.cache and skip == 0) else None
+        store = [] if (self.cache and skip == 0 and not self.cache_overflow) else None
+        stored = 0
+        # per-field id min / max of the first complete epoch (cached or streamed)
+        stats = skip == 0 and not self._stats_done
+        if stats:
+            self._fmin = self._fmax = None
         on_gpu = self.device is not None and torch.device(self.device).type == "cuda"
         src = (_DeviceFeeder(loader, self.F, self.B, torch.device(self.device), self.id_dtype)
                if on_gpu else None)
@@ -274,7 +289,14 @@ class InputPipeline:
                     continue
                 t = item if src is not None else self._to_tensors(*item)
                 if store is not None:
+                    stored += sum(x.numel() * x.element_size() for x in t)
+                    if self.cache_budget is not None and stored > self.cache_budget:
+                        # over budget: give the partial cache back, stream every epoch from now on
+                        store = None
+                        self.cache_overflow = True
+                if store is not None:
                     store.append(t)
+                if stats:
                     ids = t[0]
                     mn, mx = ids.amin(0), ids.amax(0)
                     self._fmin = mn if self._fmin is None else torch.minimum(self._fmin, mn)
@@ -285,13 +307,15 @@ class InputPipeline:
             loader.close()
             if src is not None:
                 self.h2d_s = src.h2d_s
+        if stats:                    # (reached only when the epoch was read to its end)
+            self._stats_done = True
         if store is not None:
             self._cached = store
 
     def field_minmax(self):
-        """(per-field min ids, per-field max ids) over the cached epoch as CPU int64 tensors, or
-        None before an epoch was cached."""
-        if self._fmin is None:
+        """(per-field min ids, per-field max ids) over the first complete epoch as CPU int64
+        tensors, or None before one was read."""
+        if self._fmin is None or not self._stats_done:
             return None
         return self._fmin.cpu().long(), self._fmax.cpu().long()
 

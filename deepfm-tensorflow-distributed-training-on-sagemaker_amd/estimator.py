@@ -110,7 +110,7 @@ class Estimator:
                                       sparse_update=cfg.sparse_update, seed=cfg.seed,
                                       batch_size=cfg.batch_size, device=self.device, comm=self.comm,
                                       batch_norm=cfg.batch_norm, batch_norm_decay=cfg.batch_norm_decay,
-                                      mlp_dtype=cfg.mlp_dtype, field_ranges=ranges)
+                                      mlp_dtype=cfg.mlp_dtype, emb_dtype=cfg.emb_dtype, field_ranges=ranges)
         else:
             from .models.reference import GoldenDeepFM
             self.model = GoldenDeepFM(cfg.feature_size, cfg.field_size, cfg.embedding_size, cfg.layers,
@@ -631,12 +631,15 @@ class Estimator:
 
 
 def _row_chunks(t: torch.Tensor, chunk_bytes: int = 1 << 28):
-    if t.dim() == 0 or t.numel() * t.element_size() <= chunk_bytes:
-        yield t
+    """Row blocks of a tensor for the bundle writer; bf16 embedding rows (mixed precision) are
+    upcast to the fp32 TF variables block by block."""
+    up = (lambda x: x.float()) if t.dtype == torch.bfloat16 else (lambda x: x)
+    if t.dim() == 0 or t.numel() * 4 <= chunk_bytes:
+        yield up(t)
         return
-    rows = max(1, chunk_bytes // max(1, t[0].numel() * t.element_size()))
+    rows = max(1, chunk_bytes // max(1, t[0].numel() * 4))
     for a in range(0, t.shape[0], rows):
-        yield t[a:a + rows]
+        yield up(t[a:a + rows])
 
 
 def _interleaved_chunks(parts, V: int, chunk_bytes: int = 1 << 28):
@@ -647,7 +650,7 @@ def _interleaved_chunks(parts, V: int, chunk_bytes: int = 1 << 28):
     row_bytes = max(1, parts[0][0].numel() * parts[0].element_size())
     rows = max(1, chunk_bytes // (row_bytes * N))
     for a in range(0, R, rows):
-        blk = torch.stack([p[a:a + rows] for p in parts], dim=1)
+        blk = torch.stack([p[a:a + rows].float() for p in parts], dim=1)
         blk = blk.reshape((-1,) + tuple(parts[0].shape[1:]))
         lo = a * N
         yield blk[: max(0, min(blk.shape[0], V - lo))]

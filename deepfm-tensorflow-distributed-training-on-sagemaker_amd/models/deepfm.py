@@ -97,13 +97,16 @@ _OPT_SLOTS = {"Adam": 2, "ftrl": 2, "Adagrad": 1, "Momentum": 1, "GD": 0}
 _TABLE_LAYOUT = knob("HIPFM_TABLE_LAYOUT")     # record | split
 
 
-def table_record_floats(K: int, optimizer: str) -> int:
+def table_record_floats(K: int, optimizer: str, bf16: bool = False) -> int:
     """Floats per embedding-row record in the interleaved table layout:
         [ v (K) | w, w_slot0, w_slot1, pad | v_slot0 (K) | v_slot1 (K) ]  rounded up to 64 B
     (<= 16 floats) or to whole 128-B lines.  A lazy row update then reads and writes one record
     (K = 8 with Adam: exactly one 128-B line) instead of one row in each of six tables, and the
-    forward gather finds v and w in the same 64-B sector."""
-    x = K + 4 + _OPT_SLOTS[optimizer] * K
+    forward gather finds v and w in the same 64-B sector.  ``bf16`` (mixed-precision embeddings):
+    v and its slots are bf16 (K/2 floats each), w and its slots stay fp32 -- K = 8 with Adam is one
+    64-B record, K = 32 with Adam 256 B (the Criteo-1TB table at K = 32: 226 GB, one MI355X)."""
+    kv = K // 2 if bf16 else K
+    x = kv + 4 + _OPT_SLOTS[optimizer] * kv
     return (x + 15) // 16 * 16 if x <= 16 else (x + 31) // 32 * 32
 
 
@@ -194,7 +197,8 @@ class NativeDeepFM:
                  device="cuda", comm=None, init: bool = True, batch_norm: bool = False,
                  batch_norm_decay: float = 0.9, adam_epsilon: float = 1e-8,
                  adagrad_init: float = 1e-8, fused: Optional[bool] = None,
-                 field_ranges: Optional[Sequence[Tuple[int, int]]] = None, mlp_dtype: str = "bf16"):
+                 field_ranges: Optional[Sequence[Tuple[int, int]]] = None, mlp_dtype: str = "bf16",
+                 emb_dtype: str = "fp32"):
         self.batch_norm = bool(batch_norm)
         self.bn_decay = float(batch_norm_decay)
         if mlp_dtype not in ("bf16", "fp8"):
@@ -202,6 +206,14 @@ class NativeDeepFM:
         # fp8: the deep tower's forward GEMMs take OCP e4m3 operands (per-row / per-channel
         # power-of-two scales, fp32 accumulation); backward and master weights stay bf16 / fp32
         self.fp8 = mlp_dtype == "fp8"
+        # mixed-precision embeddings (BASELINE config #5): fm_v rows and their optimizer slots
+        # stored bf16 (stochastically rounded, counter-based: reproducible), fm_w and every
+        # computation fp32 -- half the table bytes and traffic of the gather and the row update
+        if emb_dtype not in ("fp32", "bf16"):
+            raise ValueError(f"emb_dtype must be fp32 or bf16, got {emb_dtype!r}")
+        self.emb_bf16 = emb_dtype == "bf16"
+        if self.emb_bf16 and (sparse_update != "lazy" or _TABLE_LAYOUT != "record"):
+            raise ValueError("emb_dtype=bf16 needs sparse_update=lazy and the record table layout")
         self.bn_eps = 1e-3          # tf.contrib.layers.batch_norm default epsilon (PS:289)
         self.V, self.F, self.K = int(feature_size), int(field_size), int(embedding_size)
         if self.K not in (4, 8, 16, 32, 64):
@@ -266,11 +278,12 @@ class NativeDeepFM:
         # one [R, RS] record buffer (table_record_floats); HIPFM_TABLE_LAYOUT=split keeps six
         # separate contiguous tables (A/B)
         self.record = _TABLE_LAYOUT == "record"
+        self._kv = K // 2 if self.emb_bf16 else K          # floats of the v part of a record
         if self.record:
-            self.rec_stride = table_record_floats(K, optimizer)
+            self.rec_stride = table_record_floats(K, optimizer, self.emb_bf16)
             self.rec = torch.zeros(self.R, self.rec_stride, **f32)
-            self.tv = self.rec[:, :K]
-            self.tw = self.rec[:, K]
+            self.tv = self.rec.view(torch.bfloat16)[:, :K] if self.emb_bf16 else self.rec[:, :K]
+            self.tw = self.rec[:, self._kv]
         else:
             self.rec = None
             self.tv = torch.zeros(self.R, K, **f32)
@@ -384,6 +397,9 @@ class NativeDeepFM:
         if self.fp8 and not self.fused:
             raise ValueError("mlp_dtype=fp8 runs on the fused tower kernel (no batch norm, "
                              "activations within LDS)")
+        if self.emb_bf16 and not self.gather_fused:
+            raise ValueError("emb_dtype=bf16 runs on the gather-fused tower (K in 4, 8, 16, 32; no "
+                             "batch norm)")
         if init:
             if self.V * self.K <= (1 << 24):
                 # small tables: the exact golden initialization (CPU generator, bit-reproducible)
@@ -404,7 +420,14 @@ class NativeDeepFM:
         with torch.no_grad():
             for t, shape in ((self.tw, (self.V,)), (self.tv, (self.V, self.K))):
                 std = glorot_std(shape)
-                torch.nn.init.trunc_normal_(t, 0.0, std, -2 * std, 2 * std, generator=g)
+                if t.dtype == torch.float32:
+                    torch.nn.init.trunc_normal_(t, 0.0, std, -2 * std, 2 * std, generator=g)
+                    continue
+                step = 1 << 24              # bf16 rows: drawn in fp32, rounded per row block
+                for a in range(0, t.shape[0], step):
+                    blk = torch.empty(t[a:a + step].shape, dtype=torch.float32, device=t.device)
+                    torch.nn.init.trunc_normal_(blk, 0.0, std, -2 * std, 2 * std, generator=g)
+                    t[a:a + step].copy_(blk)
 
     def _alloc_slots(self):
         f32 = dict(dtype=torch.float32, device=self.device)
@@ -414,9 +437,13 @@ class NativeDeepFM:
         ns = _OPT_SLOTS[o]
         init = {"Adagrad": self.adagrad_init, "ftrl": 0.1}.get(o, 0.0)   # slot-0 initial value
         if self.record:
-            rec = self.rec
-            s0v, s1v = rec[:, K + 4: 2 * K + 4], rec[:, 2 * K + 4: 3 * K + 4]
-            s0w, s1w = rec[:, K + 1], rec[:, K + 2]
+            rec, kv = self.rec, self._kv
+            if self.emb_bf16:
+                rb, o = rec.view(torch.bfloat16), 2 * (kv + 4)
+                s0v, s1v = rb[:, o: o + K], rb[:, o + K: o + 2 * K]
+            else:
+                s0v, s1v = rec[:, kv + 4: kv + 4 + K], rec[:, kv + 4 + K: kv + 4 + 2 * K]
+            s0w, s1w = rec[:, kv + 1], rec[:, kv + 2]
         else:
             s0v, s1v = torch.zeros(R, K, **f32), torch.zeros(R, K, **f32)
             s0w, s1w = torch.zeros(R, **f32), torch.zeros(R, **f32)
@@ -786,6 +813,7 @@ class NativeDeepFM:
             a.S = self.S.data_ptr()
             a.Et = self.Et.data_ptr() if train else 0
             a.id_lim = tv.shape[0]
+            a.vbf16 = KN._bf(tv)
         else:
             a.E = self.E.data_ptr()
         if self.fp8:
@@ -1205,6 +1233,7 @@ class NativeDeepFM:
         A.ldv, A.ldw = KN._ld(self.tv, self.tw)
         A.step_off = 0 if (self._dense_early and not self._sfwg_now) else 1
         A.flags, A.sync = self.sf_flags.data_ptr(), self.sf_sync.data_ptr()
+        A.vbf16 = 1 if self.emb_bf16 else 0
         return A
 
     def _sparse_backward(self, B: int, idx, tv, presorted: bool = False):
@@ -1858,6 +1887,7 @@ class NativeDeepFM:
         return {"format": "hipfm-native", "V": self.V, "F": self.F, "K": self.K,
                 "layers": self.layers, "keep": self.keep, "optimizer": self.optimizer,
                 "world": self.world, "rank": self.rank, "R": self.R, "batch_norm": self.batch_norm,
+                "emb_dtype": "bf16" if self.emb_bf16 else "fp32",
                 "sharding": "mod" if self.sharded else "replicated", "P": self.P,
                 "dense_segs": [[s.name, s.off, list(s.shape), list(s.tf_shape)]
                                for s in self.dense_segs.values()]}
@@ -1877,14 +1907,19 @@ class NativeDeepFM:
         self._graphs = {}
         self._run_memo = {}
 
-    def tf_variables(self, tables=None) -> "OrderedDict[str, torch.Tensor]":
+    def tf_variables(self, tables=None, upcast: bool = True) -> "OrderedDict[str, torch.Tensor]":
         """TF1 checkpoint view: reference variable names, [in,out] weights,
         optimizer slots ``<var>/Adam`` ..., ``beta{1,2}_power``, ``global_step``.
-        ``tables=(fm_w, fm_v, slots...)`` overrides the local tables (gathered full tables)."""
+        ``tables=(fm_w, fm_v, slots...)`` overrides the local tables (gathered full tables).
+        bf16 embedding rows are returned as fp32 (TF's variables are fp32) unless ``upcast`` is
+        off (the chunked bundle writer upcasts chunk by chunk)."""
         out = OrderedDict()
         dense = self.dense_tf_params()
         tw, tv = (self.tw, self.tv) if tables is None else tables[:2]
         sv = self.sv if tables is None else tables[2]
+        if upcast and tv.dtype != torch.float32:
+            tv = tv.float()
+            sv = [t.float() if t.dtype != torch.float32 else t for t in sv]
         out["fm_bias"] = dense["fm_bias"]
         out["fm_w"], out["fm_v"] = tw, tv
         for k, v in dense.items():
@@ -1916,7 +1951,7 @@ class NativeDeepFM:
         embedding tables and their slots are THIS rank's local rows when row-sharded (global row =
         local row * N + rank), everything else is the full tensor."""
         out = OrderedDict()
-        full = self.tf_variables()
+        full = self.tf_variables(upcast=False)
         tables = {"fm_w": (self.tw, (self.V,)), "fm_v": (self.tv, (self.V, self.K))}
         s0n, s1n = self.SLOT_NAMES[self.optimizer]
         for slot_i, sname in ((0, s0n), (1, s1n)):

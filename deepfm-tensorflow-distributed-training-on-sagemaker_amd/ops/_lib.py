@@ -114,7 +114,7 @@ class SfArgs(C.Structure):
                 ("s0w", c_void_p), ("s1w", c_void_p), ("Gv", c_void_p), ("Gw", c_void_p),
                 ("h", OptHyper), ("step", c_void_p), ("ldv", c_long), ("ldw", c_long),
                 ("sid", c_void_p), ("upos", c_void_p), ("gout", c_void_p), ("step_off", c_int),
-                ("flags", c_void_p), ("sync", c_void_p), ("v_by_key", c_int)]
+                ("flags", c_void_p), ("sync", c_void_p), ("v_by_key", c_int), ("vbf16", c_int)]
 
 
 class ShTable(C.Structure):
@@ -127,7 +127,8 @@ class ShApplyArgs(C.Structure):
                 ("rstride", c_int), ("recv_g", c_void_p), ("table", ShTable), ("tv", c_void_p), ("tw", c_void_p),
                 ("s0v", c_void_p), ("s1v", c_void_p), ("s0w", c_void_p), ("s1w", c_void_p),
                 ("ldv", c_long), ("ldw", c_long), ("Gv", c_void_p), ("Gw", c_void_p), ("h", OptHyper),
-                ("step", c_void_p), ("next", ShTable), ("next_rows", c_void_p), ("rdiv", c_int)]
+                ("step", c_void_p), ("next", ShTable), ("next_rows", c_void_p), ("rdiv", c_int),
+                ("vbf16", c_int)]
 
 
 class ShDenseArgs(C.Structure):
@@ -155,7 +156,7 @@ class TowerArgs(C.Structure):
                 ("idx", c_void_p), ("vals", c_void_p), ("tv", c_void_p), ("tw", c_void_p),
                 ("ldv", c_long), ("ldw", c_long), ("fm_bias", c_void_p), ("F", c_int),
                 ("x_off", c_int), ("x8_off", c_int), ("S", c_void_p), ("Et", c_void_p), ("idx_ld", c_int),
-                ("id_lim", c_uint32)]
+                ("id_lim", c_uint32), ("vbf16", c_int)]
 
 
 class CommOp(C.Structure):
@@ -238,7 +239,7 @@ _SIGS = {
     "hfm_sh_bucket": [c_void_p, c_void_p, c_int, c_int, c_int] + [c_void_p] * 5 + [c_void_p],
     "hfm_sh_slot_rows": [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p],
     "hfm_sh_serve": [c_int, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_long, c_long, c_void_p,
-                     c_void_p, c_void_p, c_int, c_void_p],
+                     c_void_p, c_void_p, c_int, c_int, c_void_p],
     "hfm_sh_owner_apply": [c_int, c_int, c_void_p, c_void_p],
     "hfm_sh_apply_args_bytes": [],
     "hfm_sh_apply_dense": [c_int, c_int, c_void_p, c_void_p, c_void_p],

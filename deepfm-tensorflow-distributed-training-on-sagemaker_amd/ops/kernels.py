@@ -29,10 +29,16 @@ def L():
 
 
 def _ld(tv, tw):
-    """Row strides (in floats) of a v table [R, K] and a w table [R] (plain or record views)."""
+    """Row strides (in floats) of a v table [R, K] and a w table [R] (plain or record views; a
+    bf16 v table -- mixed-precision embeddings -- is a view of the fp32 record)."""
     ldv = tv.stride(0) if tv.dim() == 2 else tv.shape[-1]
+    ldv = ldv * tv.element_size() // 4
     ldw = tw.stride(0) if tw.dim() == 1 else 1
     return ldv, ldw
+
+
+def _bf(t) -> int:
+    return 1 if t.dtype == torch.bfloat16 else 0
 
 
 def fm_fwd(idx, vals, tv, tw, bias, B, F, K, KP, y_fm, S, E, Et, E8=None, sE=None, idsT=None,
@@ -414,11 +420,11 @@ def auc_hist(pred, label, n, hist):
 
 
 def sumsq(x: torch.Tensor, nblocks: int = 512) -> torch.Tensor:
-    if not x.is_contiguous():       # strided table views (record layout): row blocks
+    if x.dtype == torch.bfloat16 or not x.is_contiguous():   # record views / bf16 rows: row blocks
         tot = torch.zeros((), dtype=torch.float64, device=x.device)
         step = 1 << 22
         for i in range(0, x.shape[0], step):
-            tot += sumsq(x[i: i + step].contiguous(), nblocks)
+            tot += sumsq(x[i: i + step].float().contiguous(), nblocks)
         return tot
     out = torch.empty(nblocks, dtype=torch.float64, device=x.device)
     check(L().hfm_sumsq_partials(ptr(x), x.numel(), ptr(out), nblocks, stream_handle()), "sumsq")
@@ -534,7 +540,7 @@ def sh_serve(K, recv_ids, total, N, tv, tw, rows, C: int = 0, step=None, table=N
     rp = recv_ids if isinstance(recv_ids, int) else ptr(recv_ids)
     check(L().hfm_sh_serve(K, rp, total, N, C, rstride, ptr(tv), ptr(tw), *_ld(tv, tw), ptr(rows),
                            ptr(step), _byref(table) if table is not None else None, 2 if ahead else 1,
-                           stream_handle()), "sh_serve")
+                           _bf(tv), stream_handle()), "sh_serve")
 
 
 def sh_apply_dense(K, opt, args: ShApplyArgs, dense):

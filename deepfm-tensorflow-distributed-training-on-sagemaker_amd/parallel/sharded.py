@@ -344,6 +344,7 @@ class FixedCapacityExchange:
             S.Gv, S.Gw = m.Gv.data_ptr(), m.Gw.data_ptr()
         S.h = m.h_sparse
         S.step = m.step.data_ptr()
+        S.vbf16 = 1 if m.emb_bf16 else 0
         if dense is not None:
             KN.sh_apply_dense(m.K, m.opt_id, S, dense)
             return

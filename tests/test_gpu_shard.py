@@ -399,3 +399,51 @@ def test_two_launch_routing_matches_segments_bucket(N, C_slack):
         assert torch.equal(a, b), name
     assert int(out[0][4].item()) == U
     assert (int(out[0][5].item()) != 0) == (C_slack < 1.0)
+
+
+@pytest.mark.parametrize("sharded", [True, False])
+def test_bf16_tables_through_the_exchanges(sharded):
+    """Mixed-precision embeddings (config #5) on the multi-GPU paths: bf16 rows are served /
+    updated by the owner (row-sharded) or updated on every replica (replicated); N = 2 emulated
+    ranks track one bf16 model on the global batch to bf16 precision (stochastic rounding of
+    values whose fp32 pre-images differ in the last bits may pick the other neighbour: 1 ulp)."""
+    from hipfm.parallel.dist import exchange_capacity
+    N, B = 2, 512
+    synth = make_synth("criteo_kaggle", seed=8)
+    F, K, layers, keep = synth.F, 8, [64, 32], [1.0, 1.0]
+    V = synth.feature_size
+    params = init_params(V, F, K, layers, False, seed=4)
+    okw = dict(adam_epsilon=1e-2, sparse_update="lazy", emb_dtype="bf16", device=DEV, init=False,
+               field_ranges=synth.field_ranges())
+    data = [synth.batch(N * B, step=s, device=DEV, id_dtype=torch.int32) for s in range(3)]
+    batches = [[(ids[r * B:(r + 1) * B].contiguous(), vals[r * B:(r + 1) * B].contiguous(),
+                 lab[r * B:(r + 1) * B].contiguous()) for ids, vals, lab in data] for r in range(N)]
+    cap = max(exchange_capacity((b[0] for b in batches[r]), N, sharded) for r in range(N))
+    ref = NativeDeepFM(V, F, K, layers, keep, learning_rate=1e-3 * N, batch_size=N * B, **okw)
+    ref.load_tf_params(params)
+    for ids, vals, lab in data:
+        ref.train_step(ids, vals, lab)
+    hub = _Hub(N)
+    models = []
+    for r in range(N):
+        m = NativeDeepFM(V, F, K, layers, keep, learning_rate=1e-3, batch_size=B,
+                         comm=MeshComm(hub, r, capacity=cap, sharded=sharded), **okw)
+        m.load_tf_params(params)
+        models.append(m)
+    _run_ranks(models, batches, prefetch=True)
+    torch.cuda.synchronize()
+    for m in models:
+        m.check_errors()
+    uids = torch.unique(torch.cat([d[0].reshape(-1) for d in data]).long())
+    if sharded:
+        got = torch.empty(uids.numel(), K, device=DEV)
+        for r, m in enumerate(models):
+            sel = (uids % N) == r
+            got[sel] = m.tv[uids[sel] // N].float()
+    else:
+        assert torch.equal(models[0].rec, models[1].rec)
+        got = models[0].tv[uids].float()
+    want = ref.tv[uids].float()
+    ulp = want.abs() * 2.0 ** -7 + 1e-8
+    assert ((got - want).abs() <= ulp).float().mean().item() > 0.999
+    assert (models[0].p - ref.p).abs().max().item() <= 1e-3 * ref.p.abs().max().item()
