@@ -176,7 +176,9 @@ template <bool FP8, int KE>
 __device__ __forceinline__ void tower_gather(const TowerArgs& a, int row0, bf16* Xl, int ldx,
                                              uint8_t* X8, int ld8, float* s_yfm, float* s_dq0) {
   constexpr int V4 = KE / 4;
-  constexpr int FMAX = 5;  // fields per thread per pass, all loads in flight (Criteo: 39 <= 40)
+  // fields per thread per pass, all loads in flight (Criteo: 39 <= 40); K = 32 rows are 8 f32x4
+  // each, so fewer fields per pass keep the loads in registers
+  constexpr int FMAX = KE >= 32 ? 2 : 5;
   const int tid = threadIdx.x, sl = tid >> 3, q = tid & 7;
   const int b = row0 + sl, F = a.F;
   f32x4 S[V4], Q[V4];
@@ -490,12 +492,13 @@ static int tower_launch(const TowerArgs& a, int KE, hipStream_t st) {
     case 4: hipLaunchKernelGGL((tower_kernel<FP8, 4, 4, 2>), g, blk, a.lds_bytes, st, a); break;
     case 8: hipLaunchKernelGGL((tower_kernel<FP8, 8, 4, 2>), g, blk, a.lds_bytes, st, a); break;
     case 16: hipLaunchKernelGGL((tower_kernel<FP8, 16, 4, 2>), g, blk, a.lds_bytes, st, a); break;
+    case 32: hipLaunchKernelGGL((tower_kernel<FP8, 32, 4, 2>), g, blk, a.lds_bytes, st, a); break;
     default: return (int)hipErrorInvalidValue;
   }
   return 0;
 }
 
-// KE: embedding size of the fused gather (4, 8 or 16), or 0 when E comes from fm_fwd (global)
+// KE: embedding size of the fused gather (4, 8, 16 or 32), or 0 when E comes from fm_fwd (global)
 HFM_API int hfm_tower(const TowerArgs* ap, int KE, hipStream_t st) {
   const TowerArgs& a = *ap;
   if (a.M % TW_ROWS || a.nl < 1 || a.nl > TW_MAXL || a.K0p % 32) return (int)hipErrorInvalidValue;

@@ -391,7 +391,7 @@ class NativeDeepFM:
         self.fused = can_fuse and want
         # the FM gather (K1) as the fused tower's prologue: E goes straight into the tower's LDS
         # tile (no fm_fwd launch, no E round trip through HBM)
-        self.gather_fused = self.fused and _TOWER_GATHER and self.K in (4, 8, 16)
+        self.gather_fused = self.fused and _TOWER_GATHER and self.K in (4, 8, 16, 32)
         if self.gather_fused and self._tower_lds_bytes() > 150 * 1024:
             self.gather_fused = False
         if self.fp8 and not self.fused:

@@ -271,7 +271,7 @@ def test_graph_replay_equals_eager():
     assert torch.equal(a.tv, b.tv) and torch.equal(a.p, b.p)   # bitwise: deterministic kernels
 
 
-@pytest.mark.parametrize("layers,K", [([64, 32], 8), ([256, 128, 64], 16)])
+@pytest.mark.parametrize("layers,K", [([64, 32], 8), ([256, 128, 64], 16), ([128, 64, 32], 32)])
 def test_fused_tower_matches_per_layer_kernels(layers, K):
     """tower.hip (one launch: fwd + head + dgrad chain, grouped wgrad) vs the per-layer GEMMs."""
     synth = make_synth("total:4000", seed=13)
@@ -281,7 +281,7 @@ def test_fused_tower_matches_per_layer_kernels(layers, K):
     params = init_params(V, F, K, layers, False, seed=8)
     a = NativeDeepFM(V, F, K, layers, keep, batch_size=500, device=DEV, init=False, fused=True)
     b = NativeDeepFM(V, F, K, layers, keep, batch_size=500, device=DEV, init=False, fused=False)
-    assert a.fused and not b.fused
+    assert a.fused and not b.fused and a.gather_fused        # (K = 32: the gather fused too)
     a.load_tf_params(params)
     b.load_tf_params(params)
     ids, vals, labels = synth.batch(500, step=0)

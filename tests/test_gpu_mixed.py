@@ -29,8 +29,10 @@ def test_bf16_rows_track_fp32_training(opt):
     synth = make_synth("criteo_kaggle", seed=11)
     F, K, layers, keep, B = synth.F, 8, [64, 32], [1.0, 1.0], 2048
     params = init_params(synth.feature_size, F, K, layers, False, seed=5)
+    # eps / initial accumulator 1e-2: updates stay continuous in the gradient (with 1e-8 the first
+    # steps are ~lr * sign(g), and bf16-level noise flips near-zero gradients by a full 2 lr)
     kw = dict(optimizer=opt, sparse_update="lazy", batch_size=B, device=DEV, init=False,
-              field_ranges=synth.field_ranges(), learning_rate=1e-3)
+              field_ranges=synth.field_ranges(), learning_rate=1e-3, adam_epsilon=1e-2, adagrad_init=1e-2)
     a = NativeDeepFM(synth.feature_size, F, K, layers, keep, **kw)
     b = NativeDeepFM(synth.feature_size, F, K, layers, keep, emb_dtype="bf16", **kw)
     c = NativeDeepFM(synth.feature_size, F, K, layers, keep, emb_dtype="bf16", **kw)
@@ -55,7 +57,9 @@ def test_bf16_rows_track_fp32_training(opt):
     ids = torch.unique(torch.cat([bt[0].reshape(-1) for bt in batches]).long())
     va, vb = a.tv[ids].float(), b.tv[ids].float()
     upd = (va - torch.as_tensor(params["fm_v"], device=DEV)[ids]).abs().max().item()
-    assert (va - vb).abs().max().item() < 0.1 * upd + 1e-4
+    # bf16 storage: ~|v| * 2^-8 per rounding (stochastic, so a random walk over the steps)
+    err = (va - vb).abs()
+    assert err.max().item() < 0.25 * upd + 3e-4 and err.mean().item() < 0.05 * upd + 3e-5
     # export view is fp32
     tfv = b.tf_variables()
     assert tfv["fm_v"].dtype == torch.float32 and tfv[f"fm_v/{b.SLOT_NAMES[opt][0]}"].dtype == torch.float32

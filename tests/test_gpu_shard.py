@@ -444,6 +444,10 @@ def test_bf16_tables_through_the_exchanges(sharded):
         assert torch.equal(models[0].rec, models[1].rec)
         got = models[0].tv[uids].float()
     want = ref.tv[uids].float()
-    ulp = want.abs() * 2.0 ** -7 + 1e-8
-    assert ((got - want).abs() <= ulp).float().mean().item() > 0.999
+    # a row's fp32 pre-image differs in the last bits (rank-ordered vs one segmented sum), so a
+    # stochastic rounding can pick the other bf16 neighbour; hot rows (every step) random-walk a few
+    # such ulps over the steps
+    d = (got - want).abs()
+    assert (d <= want.abs() * 2.0 ** -7 + 1e-8).float().mean().item() > 0.99
+    assert (d <= want.abs() * 2.0 ** -5 + 1e-6).all()
     assert (models[0].p - ref.p).abs().max().item() <= 1e-3 * ref.p.abs().max().item()
