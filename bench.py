@@ -292,22 +292,25 @@ def main():
         for k, (t, e) in enumerate(chunks(lo, hi)):
             _progress()
             i = t % P
-            nxt = pool[e % P][0]                      # next batch: its sort / routing is prefetched
+            # the two batches after the run: their sort / routing is prefetched
+            nxt = (pool[e % P][0], pool[(e + 1) % P][0])
             if use_graph and G > 1:
                 model.train_steps(pool[i:i + (e - t)], next_ids=nxt)
             else:
                 for j in range(e - t):
                     ids, vals, labels = pool[i + j]
                     model.train_step(ids, vals, labels, use_graph=use_graph,
-                                     next_ids=pool[(i + j + 1) % P][0])
+                                     next_ids=(pool[(i + j + 1) % P][0], pool[(i + j + 2) % P][0]))
 
     if use_graph and (comm is None or comm.graph_safe):
         # every graph the warm-up and timed runs replay is captured here first (real steps)
         run(0, args.warmup + args.steps)
-        if (args.warmup + args.steps) % 2:
-            # the sorted-slot / routing sets alternate step by step: an even number of steps
-            # before the warm-up keeps every run's set parity equal to its parity at capture
-            model.train_step(*pool[0], use_graph=use_graph, next_ids=pool[1 % P][0])
+        # the sorted-slot (2) and routing (3, row-sharded) sets rotate step by step: padding the
+        # steps before the warm-up to a multiple of their period keeps every run's set phase
+        # equal to its phase at capture (else the timed window re-captures graphs)
+        for j in range(-(args.warmup + args.steps) % model.plan_period):
+            model.train_step(*pool[j % P], use_graph=use_graph,
+                             next_ids=(pool[(j + 1) % P][0], pool[(j + 2) % P][0]))
         torch.cuda.synchronize()
     _progress()
     run(0, args.warmup)
@@ -316,6 +319,7 @@ def main():
     if comm is not None:
         dist.barrier()
     torch.cuda.synchronize()
+    n_graphs = len(model._graphs)
     t0 = time.perf_counter()
     run(args.warmup, args.warmup + args.steps)
     torch.cuda.synchronize()
@@ -323,6 +327,11 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    # graphs captured inside the timed window (should be 0: every run was captured before)
+    timed_captures = len(model._graphs) - n_graphs
+    if timed_captures and rank == 0:
+        print(f"[bench] WARNING: {timed_captures} graph capture(s) inside the timed window",
+              file=sys.stderr, flush=True)
     loss = model.loss_value(B)
     ms = elapsed * 1000.0 / max(1, args.steps)
     if comm is not None:
@@ -366,6 +375,7 @@ def main():
                                                 f"+{'row-sharded' if comm.sharded else 'replicated'}-embedding"),
                 "optimizer": f"{args.optimizer} ({args.sparse_update})",
                 "hip_graph": use_graph,
+                "timed_graph_captures": timed_captures,
                 "graph_steps": G if use_graph else 0,
                 "exec": os.environ.get("HIPFM_BENCH_RUNG", "graph+prefetch" if use_graph else "eager"),
                 "mlp_dtype": args.mlp_dtype + (" fwd GEMMs, bf16 backward" if args.mlp_dtype == "fp8" else ""),

@@ -65,6 +65,14 @@ __device__ __forceinline__ void st_row4(float* row, int e, f32x4 v, bool bf, uin
   u.y = f2bf_sr(v[2], fmix32(seed + 4u * e + 2u)) | (f2bf_sr(v[3], fmix32(seed + 4u * e + 3u)) << 16);
   *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(row) + e) = u;
 }
+// the values st_row4 stores, as fp32 (a copy of an updated row that must equal the stored row)
+__device__ __forceinline__ f32x4 rounded_row4(f32x4 v, int e, bool bf, uint32_t seed) {
+  if (!bf) return v;
+  f32x4 r;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) r[j] = __uint_as_float(f2bf_sr(v[j], fmix32(seed + 4u * e + j)) << 16);
+  return r;
+}
 // rounding seed of (table row, optimizer step, which array: 0 = v, 1 / 2 = slots)
 __device__ __forceinline__ uint32_t row_sr_seed(size_t row, int64_t step, uint32_t which) {
   return fmix32((uint32_t)row ^ fmix32((uint32_t)(row >> 32) ^ ((uint32_t)step * 0x9E3779B1u) ^

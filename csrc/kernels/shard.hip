@@ -397,11 +397,10 @@ __device__ __forceinline__ void sh_owner_apply_elem(int gt, const int* __restric
     a[j] = aj;
     c[j] = cj;
   }
-  // (bf16: the served-ahead patch below copies the rounded value's fp32 pre-image: it feeds the
-  // next forward exactly as the rounded row would only up to the rounding, so the host never
-  // combines serve-ahead with bf16 rows)
   const int64_t st = *step;
-  st_row4(tv + rb, sub * 4, pv, bf, bf ? row_sr_seed(row, st, 0) : 0u);
+  const uint32_t sv_seed = bf ? row_sr_seed(row, st, 0) : 0u;
+  st_row4(tv + rb, sub * 4, pv, bf, sv_seed);
+  pv = rounded_row4(pv, sub * 4, bf, sv_seed);   // (bf16) the stored value, for the served-ahead patch
   if (OPT != OPT_GD) st_row4(s0v + rb, sub * 4, a, bf, bf ? row_sr_seed(row, st, 1) : 0u);
   if (OPT == OPT_ADAM || OPT == OPT_FTRL) st_row4(s1v + rb, sub * 4, c, bf, bf ? row_sr_seed(row, st, 2) : 0u);
   float wnew = 0.f;

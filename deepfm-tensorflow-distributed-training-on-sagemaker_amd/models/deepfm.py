@@ -1582,6 +1582,20 @@ class NativeDeepFM:
                 (ids.is_contiguous() or self._field_major(ids)) and vals.is_contiguous() and
                 labels.is_contiguous() and ids.shape[0] == self.M and ids.numel() == self.M * self.F)
 
+    @staticmethod
+    def _split_next(next_ids):
+        """``next_ids``: the next batch's ids, or (next, the one after) -- the row-sharded step
+        routes two batches ahead when it knows both (parallel/sharded.py, pipeline depth)."""
+        if isinstance(next_ids, (tuple, list)):
+            n1 = next_ids[0] if len(next_ids) > 0 else None
+            n2 = next_ids[1] if len(next_ids) > 1 else None
+            return n1, (n2 if n1 is not None else None)
+        return next_ids, None
+
+    def _next_ok(self, t, B: int) -> bool:
+        return (t is not None and t.is_cuda and t.dtype == torch.int32 and
+                (t.is_contiguous() or self._field_major(t)) and t.shape[0] == B and t.numel() == B * self.F)
+
     def _bind_step(self, ids, vals, labels, next_ids=None, stage: bool = False):
         """Bind one step's batch (in place when resident, else -- or with ``stage`` -- a copy into
         the static input buffers) and decide its host-side plans (sort / routing: inline or
@@ -1599,11 +1613,11 @@ class NativeDeepFM:
             self.idx, self.vals, self.labels = self._own_in
             B = self.stage_batch(ids, vals, labels)
             key = ("staged", B)
-        nxt_ok = (direct and next_ids is not None and next_ids.is_cuda and
-                  next_ids.dtype == torch.int32 and
-                  (next_ids.is_contiguous() or self._field_major(next_ids)) and
-                  next_ids.shape[0] == B and next_ids.numel() == B * self.F)
+        next_ids, next2_ids = self._split_next(next_ids)
+        nxt_ok = direct and self._next_ok(next_ids, B)
         nxt_fm = nxt_ok and not next_ids.is_contiguous()
+        nxt2_ok = nxt_ok and self._next_ok(next2_ids, B)
+        nxt2_fm = nxt2_ok and not next2_ids.is_contiguous()
         self._shx_plan = None
         self._sort_plan = None
         if (not self.sharded and _SORT_SIDE_STREAM and self._fsort_next is not None and
@@ -1629,10 +1643,10 @@ class NativeDeepFM:
             key = key + ("tf1",) + self._tf1_plan
         if self.shx is not None:
             nxt = self._flat_ids(next_ids, nxt_fm) if (nxt_ok and _SHARD_PIPELINE) else None
-            self._shx_plan = self.shx.plan(self.idx, B, nxt, resident=direct)
-            self.shx._next_ids = nxt
-            self.shx._next_fm = nxt_fm
-            key = key + self._shx_plan
+            nxt2 = self._flat_ids(next2_ids, nxt2_fm) if (nxt2_ok and _SHARD_PIPELINE) else None
+            self._shx_plan = self.shx.plan(self.idx, B, nxt, resident=direct, nxt2=nxt2)
+            self.shx._next = (nxt, nxt_fm, nxt2, nxt2_fm)
+            key = key + tuple(self._shx_plan)
         return B, direct, key
 
     def _commit_step(self, B: int, direct: bool):
@@ -1655,8 +1669,18 @@ class NativeDeepFM:
         if self._host_step is not None:
             self._host_step += 1
 
+    @property
+    def plan_period(self) -> int:
+        """Steps after which the rotating prefetch sets (2 slot-sort sets, NSETS routing sets of
+        the row-sharded step) return to the same phase: a replay loop that advances by a multiple
+        of it between capture and replay finds every run's graph under the same plan state."""
+        n = 2
+        if self.shx is not None:
+            n = n * self.shx.NSETS // math.gcd(n, self.shx.NSETS)
+        return n
+
     def _plan_state(self):
-        sh = None if self.shx is None else (self.shx.cur, [rs.key for rs in self.shx.sets])
+        sh = None if self.shx is None else (self.shx.cur, [(rs.key, rs.stage) for rs in self.shx.sets])
         return self._ss_cur, list(self._ss_key), sh, list(getattr(self, "_stamp_n", []))
 
     def _set_plan_state(self, st):
@@ -1665,8 +1689,8 @@ class NativeDeepFM:
             self._stamp_n = list(st[3])
         if st[2] is not None:
             self.shx.cur = st[2][0]
-            for rs, k in zip(self.shx.sets, st[2][1]):
-                rs.key = k
+            for rs, (k, stg) in zip(self.shx.sets, st[2][1]):
+                rs.key, rs.stage = k, stg
 
     def train_step(self, ids, vals, labels, use_graph: bool = False, next_ids=None,
                    stage: bool = False):
@@ -1690,15 +1714,20 @@ class NativeDeepFM:
         launch-bound inner loop per replay: the per-replay launch and branch-join cost is paid
         once per run of steps instead of once per step).  Every step is complete -- forward,
         backward, sparse and dense optimizer -- and identical to ``train_step`` (bitwise, tested).
-        Batch i declares batch i+1 as its next batch (prefetched sort / routing); ``next_ids``
-        is the batch after the last one.  Returns the number of steps."""
+        Batch i declares batches i+1 and i+2 as its upcoming batches (prefetched sort / routing);
+        ``next_ids`` is the batch after the last one, or (that batch, the one after it).  Returns
+        the number of steps."""
         batches = list(batches)
         if not batches:
             return 0
+        la1, la2 = self._split_next(next_ids)
+        seq = [b[0] for b in batches] + [x for x in (la1, la2) if x is not None]
+
+        def nxt_of(i):
+            return (seq[i + 1] if i + 1 < len(seq) else None, seq[i + 2] if i + 2 < len(seq) else None)
         if not all(self._resident(*b) for b in batches) or not (self.comm is None or self.comm.graph_safe):
             for i, (ids, vals, labels) in enumerate(batches):
-                nxt = batches[i + 1][0] if i + 1 < len(batches) else next_ids
-                self.train_step(ids, vals, labels, use_graph=True, next_ids=nxt)
+                self.train_step(ids, vals, labels, use_graph=True, next_ids=nxt_of(i))
             return len(batches)
         st0 = self._plan_state()
         # a run seen before from the same plan state replays its graph without re-planning
@@ -1706,7 +1735,7 @@ class NativeDeepFM:
         # 16-step graph of ~0.11 ms steps cannot always hide behind the GPU)
         mkey = (tuple((b[0].data_ptr(), b[0].stride(), b[1].data_ptr(), b[2].data_ptr(), b[0].shape[0])
                       for b in batches),
-                None if next_ids is None else (next_ids.data_ptr(), next_ids.stride()),
+                tuple((t.data_ptr(), t.stride()) for t in (la1, la2) if t is not None),
                 _hashable(st0))
         hit = self._run_memo.get(mkey)
         if hit is not None and self._graphs.get(hit[0]) is hit[1]:
@@ -1719,8 +1748,7 @@ class NativeDeepFM:
         h0 = self._host_step
         keys, Bs = [], []
         for i, (ids, vals, labels) in enumerate(batches):       # plans only: the graph key
-            nxt = batches[i + 1][0] if i + 1 < len(batches) else next_ids
-            B, direct, k = self._bind_step(ids, vals, labels, nxt)
+            B, direct, k = self._bind_step(ids, vals, labels, nxt_of(i))
             keys.append(k)
             Bs.append(B)
             self._commit_step(B, direct)
@@ -1734,8 +1762,7 @@ class NativeDeepFM:
                 self._warm = True
                 # the very first step of the model runs eagerly (warms up lazy library state)
                 ids, vals, labels = batches[0]
-                self.train_step(ids, vals, labels, use_graph=False,
-                                next_ids=batches[1][0] if len(batches) > 1 else next_ids)
+                self.train_step(ids, vals, labels, use_graph=False, next_ids=nxt_of(0))
                 torch.cuda.synchronize()
                 rest = batches[1:]
                 if not rest:
@@ -1744,8 +1771,7 @@ class NativeDeepFM:
             g = torch.cuda.CUDAGraph()
             with graph_capture(g):
                 for i, (ids, vals, labels) in enumerate(batches):
-                    nxt = batches[i + 1][0] if i + 1 < len(batches) else next_ids
-                    B, direct, _ = self._bind_step(ids, vals, labels, nxt)
+                    B, direct, _ = self._bind_step(ids, vals, labels, nxt_of(i))
                     self.train_step_enqueue(B)
                     self._commit_step(B, direct)
             if len(self._graphs) >= self.max_graphs:
@@ -1786,7 +1812,8 @@ class NativeDeepFM:
         training steps (use them as warm-up)."""
         P = len(batches)
         for i, (ids, vals, labels) in enumerate(batches):
-            self.train_step(ids, vals, labels, use_graph=True, next_ids=batches[(i + 1) % P][0])
+            self.train_step(ids, vals, labels, use_graph=True,
+                            next_ids=(batches[(i + 1) % P][0], batches[(i + 2) % P][0]))
             if progress is not None:
                 progress()
         torch.cuda.synchronize()
@@ -1811,6 +1838,7 @@ class NativeDeepFM:
             self.shx.begin(self._shx_plan, B)
             self._predict_body(B, with_labels)
             self.shx.commit(self._shx_plan, self.idx, B, resident=False)
+            self.shx.invalidate()        # (it used a set a prefetched batch may have been in)
             self._shx_plan = None
             return
         self._predict_body(B, with_labels)

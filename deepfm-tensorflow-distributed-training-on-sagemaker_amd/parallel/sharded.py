@@ -13,16 +13,25 @@ Collective order (deadlock freedom by construction).  Every collective of a step
 ONE communicator, as a grouped RCCL operation on the step's MAIN stream, at fixed points:
 
     [inline routing only]  G0 = {ids all-to-all of this batch}
-    fetch                  G1 = {rows all-to-all of this batch}
+    fetch                  G1 = {rows all-to-all of this batch [, ids all-to-all of the NEXT
+                                 batch when it was routed during the previous step]}
     end of the backward    G2 = {gradient rows all-to-all, dense gradient all-gather (or
-                                 all-reduce), ids all-to-all of the NEXT batch (prefetched)}
+                                 all-reduce) [, ids all-to-all of the NEXT batch when it is
+                                 routed during this step]}
 
-The next batch's routing KERNELS (sort, owner buckets, slot map) run on a side stream during
-the step, but its id exchange joins G2 on the main stream.  So each rank issues the same
-sequence of groups on one communicator in one stream order -- never two operations that could
-wait on each other across ranks -- whatever order the graph's branches reach the hardware
-queues in (``_issue`` refuses a collective off the main stream).  tests/test_gpu_shard.py
-records the sequence per emulated rank and checks it is identical.
+Routing KERNELS (sort, owner buckets, slot map) of upcoming batches run on a side stream; their
+id exchanges join G1 / G2 on the main stream.  So each rank issues the same sequence of groups
+on one communicator in one stream order -- never two operations that could wait on each other
+across ranks -- whatever order the graph's branches reach the hardware queues in (``_issue``
+refuses a collective off the main stream).  tests/test_gpu_shard.py records the sequence per
+emulated rank and checks it is identical.
+
+Pipeline depth.  Three routing sets rotate.  With the next TWO batches known (resident pool,
+cached epoch), batch i+2 is routed during step i, its ids travel in step i+1's G1, and its rows
+are then SERVED AHEAD on a side stream during step i+1 (the owner update of step i+1 patches the
+rows it changes; lazy rows only) -- the serve leaves the critical path.  With only the next batch
+known, it is routed during the step and its ids travel in G2 (depth 1); rows are served at the
+start of their own step.
 
 Capacity: the unique ids a rank sends to one owner must fit ``capacity``.  ``estimate_capacity``
 measures sample batches; a bucket that overflows sets an error word that the model checks
@@ -32,7 +41,7 @@ from __future__ import annotations
 
 import math
 import os
-from typing import Iterable, Optional
+from typing import Iterable, NamedTuple, Optional
 
 import torch
 
@@ -101,12 +110,15 @@ class RcclEngine:
             self.handle = 0
 
 
-class _RouteSet:
-    """Routing state of one batch: sorted slots, unique ids, owner buckets, received requests.
-    Depends only on the batch ids (not on the table), so the next batch's set can be built while
-    the current batch trains."""
+_ROUTED, _XCHG, _SERVED = "routed", "xchg", "served"
 
-    def __init__(self, m, n: int, N: int, C: int, temp_bytes: int):
+
+class _RouteSet:
+    """Routing state of one batch: sorted slots, unique ids, owner buckets, received requests,
+    the owner-side request table and served rows.  Depends only on the batch ids (not on the
+    table) up to the serve, so upcoming batches' sets are built while the current batch trains."""
+
+    def __init__(self, m, n: int, N: int, C: int, temp_bytes: int, RW: int):
         dev = m.device
         i32 = dict(dtype=torch.int32, device=dev)
         self.sorted_keys = torch.zeros(n, **i32)
@@ -124,12 +136,14 @@ class _RouteSet:
         self.recv_ids = torch.full((N * C,), -1, **i32)
         self.send_cnt = torch.zeros(N, **i32)
         self.slot_row = torch.zeros(n, **i32)
-        self.key = None          # host: (ids data_ptr, B) routed AND exchanged into this set
-        # owner side: the request table (csrc/kernels/shard.hip) of this set's batch.  It has a
-        # power of two >= 2x the N*C request slots; keys and per-requester positions carry step
-        # stamps -- sized by the exchange, not by the table (a direct [R_local][N] tag array is
-        # 7 GB per rank at the 1TB shape)
+        self.key = None          # host: (ids data_ptr, B) of the batch in this set
+        self.stage = None        # host: _ROUTED (kernels done) / _XCHG (ids exchanged) / _SERVED
+        # owner side: the request table (csrc/kernels/shard.hip) of this set's batch and its
+        # served rows.  The table has a power of two >= 2x the N*C request slots; keys and per-
+        # requester positions carry step stamps -- sized by the exchange, not by the table (a
+        # direct [R_local][N] tag array is 7 GB per rank at the 1TB shape)
         T = N * C
+        self.rows_out = torch.zeros(T, RW, dtype=torch.float32, device=dev)
         slots = 1
         while slots < 2 * T:
             slots *= 2
@@ -142,15 +156,23 @@ class CollectiveOrderError(RuntimeError):
     """A collective of the row-sharded step was about to be issued off the step's main stream."""
 
 
-class FixedCapacityExchange:
-    """Buffers + step pieces of the row-sharded exchange for one NativeDeepFM (one rank).
+class ShPlan(NamedTuple):
+    """Host-side routing decisions of one step (part of the captured graph's key)."""
+    c: int                       # routing set of this batch
+    route: bool                  # run this batch's routing kernels inline
+    ids: bool                    # exchange this batch's ids inline (G0)
+    serve: bool                  # serve this batch's rows at the start of the step
+    n1: Optional[tuple]          # (ids address, B) of the next batch
+    n1_mode: Optional[str]       # "xchg": routed earlier, ids in G1 (+ serve ahead); "route": now, ids in G2
+    serve_ahead: bool            # serve the next batch's rows during this step
+    n2: Optional[tuple]          # (ids address, B) of the batch after: routed during this step
 
-    Two routing sets alternate: with ``next`` known (resident / prefetched batches), the routing
-    kernels of batch i+1 (sort, dedup, owner buckets, slot->row map) run on a side stream during
-    step i and its ids travel in step i's final collective group -- the sparse-input-dist
-    pipelining of production DLRM trainers -- so the critical path of a step keeps only the row
-    fetch, the compute and the gradient exchange.  See the module docstring for the collective
-    order."""
+
+class FixedCapacityExchange:
+    """Buffers + step pieces of the row-sharded exchange for one NativeDeepFM (one rank).  See
+    the module docstring for the collective order and the pipeline depth."""
+
+    NSETS = 3
 
     def __init__(self, m, engine, capacity: Optional[int] = None):
         self.m, self.eng = m, engine
@@ -162,47 +184,76 @@ class FixedCapacityExchange:
         self.RW = K + 4                      # exchanged row: {v[K], w, 0, 0, 0} / {g_v, g_w, 0, 0, 0}
         T = self.N * self.C
         f32 = dict(dtype=torch.float32, device=dev)
-        self.sets = [_RouteSet(m, n, self.N, self.C, m.temp.numel()) for _ in range(2)]
+        self.sets = [_RouteSet(m, n, self.N, self.C, m.temp.numel(), self.RW) for _ in range(self.NSETS)]
         self.cur = 0
         self.err = m.err_words[2:3]          # capacity overflow (the model's error words)
-        self.rows_out = torch.zeros(T, self.RW, **f32)     # owner: served rows of this step
         self.rows_in = torch.zeros(T, self.RW, **f32)
         self.send_g = torch.zeros(T, self.RW, **f32)
         self.recv_g = torch.zeros(T, self.RW, **f32)
         self._side = None
+        self._serve_stream = None
         self._main = None
         self._joined = True
-        self._next_ids, self._next_fm = None, False
+        self._served_ev = None
+        self._next = (None, False, None, False)     # (n1 ids, n1 field-major, n2 ids, n2 fm)
         self._fork_at = None
         self._plan = None
         self.dense_recv = None               # [N][P] all-gathered dense gradients (fused exchange)
         self.trace = None                    # list: record every issued group (tests)
 
     # ------------------------------------------------------------------ host-side plan
-    def plan(self, ids: torch.Tensor, B: int, nxt: Optional[torch.Tensor], resident: bool = True):
-        """Routing decisions for one step (part of the graph key): (set index, route the current
-        batch inline?, (next ids address, next B) or None).  Only resident batches (fixed device
-        buffers) can have been prefetched: staged buffers change content under the same address."""
+    def plan(self, ids: torch.Tensor, B: int, nxt: Optional[torch.Tensor], resident: bool = True,
+             nxt2: Optional[torch.Tensor] = None) -> ShPlan:
+        """Routing decisions for one step.  Only resident batches (fixed device buffers) can have
+        been prefetched: staged buffers change content under the same address."""
         c = self.cur
         key = (ids.data_ptr(), B)
-        inline = (not resident) or self.sets[c].key != key
-        return (c, inline, None if nxt is None else (nxt.data_ptr(), nxt.numel() // self.m.F))
+        sc = self.sets[c]
+        match = resident and sc.key == key
+        route = not (match and sc.stage in (_ROUTED, _XCHG, _SERVED))
+        ids_x = not (match and sc.stage in (_XCHG, _SERVED))
+        serve = not (match and sc.stage == _SERVED)
+        n1 = n2 = n1_mode = None
+        ahead = False
+        if nxt is not None:
+            n1 = (nxt.data_ptr(), nxt.numel() // self.m.F)
+            s1 = self.sets[(c + 1) % self.NSETS]
+            n1_mode = "xchg" if (s1.key == n1 and s1.stage == _ROUTED) else "route"
+            ahead = n1_mode == "xchg" and self.m.sparse_update == "lazy"
+            if nxt2 is not None:
+                n2 = (nxt2.data_ptr(), nxt2.numel() // self.m.F)
+        return ShPlan(c, route, ids_x, serve, n1, n1_mode, ahead, n2)
 
-    def commit(self, plan, ids: torch.Tensor, B: int, resident: bool = True):
-        """Consecutive steps always use alternate routing sets (prefetched or not): a step's
-        routing kernels never overwrite buffers the previous step's backward still reads, even
-        when graph replays run back to back.  A routing set is reused ONLY for the batch the
-        caller declared as next (``next_ids``): a set is never matched again by address alone,
-        since a freshly allocated batch can get the address of an earlier one back from the
-        caching allocator."""
-        c, _, nk = plan
-        self.sets[c].key = None
-        self.sets[1 - c].key = nk
-        self.cur = 1 - c
+    def commit(self, plan: ShPlan, ids: torch.Tensor = None, B: int = 0, resident: bool = True):
+        """Consecutive steps rotate through the routing sets (prefetched or not), so a step's
+        routing kernels never overwrite buffers an earlier step's backward still reads, even when
+        graph replays run back to back.  A set is reused ONLY for the batch a caller declared as
+        upcoming: never matched again by address alone (a fresh batch can get the address of an
+        earlier one back from the caching allocator)."""
+        c = plan.c
+        self.sets[c].key = self.sets[c].stage = None
+        s1, s2 = self.sets[(c + 1) % self.NSETS], self.sets[(c + 2) % self.NSETS]
+        if plan.n1 is not None:
+            s1.key, s1.stage = plan.n1, (_SERVED if plan.serve_ahead else _XCHG)
+        else:
+            s1.key = s1.stage = None
+        if plan.n2 is not None:
+            s2.key, s2.stage = plan.n2, _ROUTED
+        else:
+            s2.key = s2.stage = None
+        self.cur = (c + 1) % self.NSETS
+
+    def invalidate(self):
+        """Forget every prefetched set (after an out-of-band use of the exchange, e.g. predict)."""
+        for rs in self.sets:
+            rs.key = rs.stage = None
 
     def drop_served(self):
-        """Parameters changed outside a step (load / broadcast).  Rows are served at the start of
-        every step, so nothing served can be stale; kept for the model's protocol."""
+        """Parameters changed outside a step (load / broadcast): rows served ahead are stale, so
+        the next step serves its rows itself (its routing and exchanged ids stay valid)."""
+        for rs in self.sets:
+            if rs.stage == _SERVED:
+                rs.stage = _XCHG
 
     # ------------------------------------------------------------------ collectives
     def _issue(self, ops):
@@ -240,36 +291,44 @@ class FixedCapacityExchange:
     def _ids_op(self, rs: _RouteSet):
         return (KN.COMM_A2A, rs.send_ids, rs.recv_ids, self.C * 4)
 
-    def begin(self, plan, B: int, fork: str = "start"):
+    def _set(self, plan: ShPlan, k: int) -> _RouteSet:
+        return self.sets[(plan.c + k) % self.NSETS]
+
+    def begin(self, plan: ShPlan, B: int, fork: str = "start"):
         """Start of a step (on its main stream): route the current batch if it was not prefetched
-        (kernels + G0), then fork the next batch's routing kernels onto a side stream -- here
-        (``fork="start"``), after the row fetch (``"fetch"``), or when the caller calls
+        (kernels, G0), then fork the routing kernels of the upcoming batches onto a side stream --
+        here (``fork="start"``), after the row fetch (``"fetch"``), or when the caller calls
         ``fork_next`` (graph branches are dispatched in capture order)."""
         m = self.m
-        c, inline, nk = plan
         self._main = torch.cuda.current_stream(m.device)
         self._plan = plan
-        if inline:
-            rs = self.sets[c]
+        rs = self.sets[plan.c]
+        if plan.route:
             self.route_kernels(rs, m.idx, B, fm=m._idx_fm)
-            self._issue([self._ids_op(rs)])                            # G0
-        self._joined = nk is None
-        self._fork_at = fork if nk is not None else None
+        if plan.ids:
+            self._issue([self._ids_op(rs)])                           # G0
+        side_work = plan.n1_mode == "route" or plan.n2 is not None
+        self._joined = not side_work
+        self._fork_at = fork if side_work else None
+        self._served_ev = None
         if self._fork_at == "start":
             self.fork_next()
 
     def fork_next(self):
-        """Enqueue the next batch's routing kernels on the side stream (once per step)."""
+        """Enqueue the upcoming batches' routing kernels on the side stream (once per step)."""
         if self._fork_at is None:
             return
         self._fork_at = None
-        m = self.m
-        c, _, nk = self._plan
+        m, plan = self.m, self._plan
+        n1_ids, n1_fm, n2_ids, n2_fm = self._next
         if self._side is None:
             self._side = torch.cuda.Stream(m.device)
         self._side.wait_stream(self._main)
         with torch.cuda.stream(self._side):
-            self.route_kernels(self.sets[1 - c], self._next_ids, nk[1], fm=self._next_fm)
+            if plan.n1_mode == "route":
+                self.route_kernels(self._set(plan, 1), n1_ids, plan.n1[1], fm=n1_fm)
+            if plan.n2 is not None:
+                self.route_kernels(self._set(plan, 2), n2_ids, plan.n2[1], fm=n2_fm)
 
     def _join_side(self):
         if not self._joined:
@@ -281,33 +340,50 @@ class FixedCapacityExchange:
         self._join_side()
         self._main = None
 
-    def fetch(self, plan, train: bool = True):
-        """Owners serve the requested rows (after the previous step's updates), rows come back
-        (G1).  Training steps stamp the owner-side request tags here (read by the update at the
-        end of the step); eval / predict fetches leave them alone."""
+    def fetch(self, plan: ShPlan, train: bool = True):
+        """Owners serve the requested rows (after the previous step's updates) unless they were
+        served ahead, rows come back (G1, with the next batch's ids when routed earlier; its rows
+        are then served ahead on a side stream).  Training steps stamp the owner-side request
+        tags with the serve (read by the update at the end of the step); eval / predict fetches
+        leave them alone."""
         m = self.m
-        rs = self.sets[plan[0]]
-        if train:
-            KN.sh_serve(m.K, rs.recv_ids, self.N * self.C, self.N, m.tv, m.tw, self.rows_out, C=self.C,
-                        step=m.step, table=rs.table)
-        else:
-            KN.sh_serve(m.K, rs.recv_ids, self.N * self.C, self.N, m.tv, m.tw, self.rows_out, C=self.C)
-        self._issue([(KN.COMM_A2A, self.rows_out, self.rows_in, self.C * self.RW * 4)])   # G1
+        rs = self.sets[plan.c]
+        if plan.serve:
+            if train:
+                KN.sh_serve(m.K, rs.recv_ids, self.N * self.C, self.N, m.tv, m.tw, rs.rows_out,
+                            C=self.C, step=m.step, table=rs.table)
+            else:
+                KN.sh_serve(m.K, rs.recv_ids, self.N * self.C, self.N, m.tv, m.tw, rs.rows_out, C=self.C)
+        ops = [(KN.COMM_A2A, rs.rows_out, self.rows_in, self.C * self.RW * 4)]
+        if train and plan.n1_mode == "xchg":
+            ops.append(self._ids_op(self._set(plan, 1)))
+        self._issue(ops)                                                 # G1
+        if train and plan.serve_ahead:
+            # the next batch's rows as of now (stamped step + 2); this step's owner update
+            # patches the rows it changes (it waits for this branch first)
+            nx = self._set(plan, 1)
+            if self._serve_stream is None:
+                self._serve_stream = torch.cuda.Stream(m.device)
+            self._serve_stream.wait_stream(self._main)
+            with torch.cuda.stream(self._serve_stream):
+                KN.sh_serve(m.K, nx.recv_ids, self.N * self.C, self.N, m.tv, m.tw, nx.rows_out, C=self.C,
+                            step=m.step, table=nx.table, ahead=True)
+                self._served_ev = torch.cuda.Event()
+                self._served_ev.record(self._serve_stream)
         if train and self._fork_at == "fetch":
             self.fork_next()
         return rs.slot_row, self.rows_in[:, : m.K], self.rows_in[:, m.K]
 
-    def backward(self, plan, B: int, dense=None, join=None, wgfin=None, dense_ar=None):
+    def backward(self, plan: ShPlan, B: int, dense=None, join=None, wgfin=None, dense_ar=None):
         """Per-unique gradient rows -> owners -> rank-ordered sum + row update on the owner.
         ``wgfin`` (WgFinArgs): the fused tower's dense gradient is computed inside the sparse
         backward's launch and all-gathered with the gradient rows (the owner launch sums the N
         rank gradients in rank order); else ``dense_ar`` (the flat dense gradient) is all-reduced
         in the same group, after ``join()`` made the main stream wait for its producer.
         ``dense`` (ShDenseArgs, lazy rows): the dense optimizer runs in the owner update's launch.
-        The next batch's ids (routed on the side stream) travel in the same group (G2)."""
+        The next batch's ids, when routed during this step, travel in the same group (G2)."""
         m = self.m
-        c, _, nk = plan
-        rs = self.sets[c]
+        rs = self.sets[plan.c]
         n = B * m.F
         A = m.sf_args(n)
         A.sorted_keys, A.perm = rs.sorted_keys.data_ptr(), rs.perm.data_ptr()
@@ -328,14 +404,14 @@ class FixedCapacityExchange:
             dense.g, dense.nsum = self.dense_recv.data_ptr(), self.N
         elif dense_ar is not None:
             ops.append((KN.COMM_ALLREDUCE, dense_ar, dense_ar, dense_ar.numel() * 4))
-        if nk is not None:
+        if plan.n1_mode == "route":
             self._join_side()                # the next batch's buckets are built
-            ops.append(self._ids_op(self.sets[1 - c]))
+            ops.append(self._ids_op(self._set(plan, 1)))
         self._issue(ops)                                                 # G2
         S = ShApplyArgs()
         S.recv_ids, S.total, S.N, S.C = rs.recv_ids.data_ptr(), self.N * self.C, self.N, self.C
         S.rstride = 0
-        S.mode = 0 if m.sparse_update == "lazy" else 1      # tags were stamped by fetch()
+        S.mode = 0 if m.sparse_update == "lazy" else 1      # tags were stamped by the serve
         S.recv_g, S.table = self.recv_g.data_ptr(), rs.table
         S.tv, S.tw = m.tv.data_ptr(), m.tw.data_ptr()
         S.s0v, S.s1v, S.s0w, S.s1w = (t.data_ptr() if t.numel() else 0 for t in m.sv)
@@ -345,6 +421,11 @@ class FixedCapacityExchange:
         S.h = m.h_sparse
         S.step = m.step.data_ptr()
         S.vbf16 = 1 if m.emb_bf16 else 0
+        if self._served_ev is not None:
+            # the next batch's rows were served ahead: wait for them, patch what changes
+            self._main.wait_event(self._served_ev)
+            nx = self._set(plan, 1)
+            S.next, S.next_rows = nx.table, nx.rows_out.data_ptr()
         if dense is not None:
             KN.sh_apply_dense(m.K, m.opt_id, S, dense)
             return
@@ -357,6 +438,7 @@ class FixedCapacityExchange:
         for rs in self.sets:
             rs.req_key.zero_()
             rs.req_pos.zero_()
+        self.drop_served()
 
     def error(self) -> int:
         return int(self.err.item())

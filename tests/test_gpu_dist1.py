@@ -65,7 +65,7 @@ def test_exchange_paths_match_local(group, sharded, update, prefetch):
 def test_exchange_staged_batches_graph_replay(group):
     """Loader-style batches (int64 ids, staged into the model's own input buffers every step) on
     the row-sharded exchange with HIP graphs: routing is inline every step (staged content changes
-    under the same addresses) and the two routing sets alternate; must equal the local path."""
+    under the same addresses) and the routing sets rotate; must equal the local path."""
     synth = make_synth("total:6000", seed=23)
     F, K, layers, keep = synth.F, 8, [64, 32], [0.8, 0.8]
     V = synth.feature_size
@@ -80,7 +80,7 @@ def test_exchange_staged_batches_graph_replay(group):
         a.train_step(ids, vals, labels)
         b.train_step(ids, vals, labels, use_graph=True)
     torch.cuda.synchronize()
-    assert len(b._graphs) == 2                                     # ("staged", B) x 2 routing sets
+    assert len(b._graphs) == b.shx.NSETS                           # ("staged", B) x routing sets
     assert torch.allclose(a.tv, b.tv, atol=1e-6) and torch.allclose(a.p, b.p, atol=1e-6)
 
 

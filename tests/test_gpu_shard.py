@@ -123,6 +123,8 @@ def _run_ranks(models, batches, prefetch=False):
                 bl = batches[r]
                 for i, (ids, vals, lab) in enumerate(bl):
                     nxt = bl[i + 1][0] if (prefetch and i + 1 < len(bl)) else None
+                    if prefetch == 2 and nxt is not None:      # two batches ahead
+                        nxt = (nxt, bl[i + 2][0] if i + 2 < len(bl) else None)
                     models[r].train_step(ids, vals, lab, next_ids=nxt)
             s.synchronize()
         except BaseException as e:          # surface failures instead of hanging the barrier
@@ -139,7 +141,8 @@ def _run_ranks(models, batches, prefetch=False):
 
 
 @pytest.mark.parametrize("N,opt,update,prefetch", [(2, "Adam", "lazy", False), (3, "Adagrad", "lazy", True),
-                                                   (4, "Adam", "tf1_dense", False), (4, "Adam", "lazy", True)])
+                                                   (4, "Adam", "tf1_dense", False), (4, "Adam", "lazy", True),
+                                                   (3, "Adam", "lazy", 2), (2, "ftrl", "tf1_dense", 2)])
 def test_sharded_exchange_matches_global_batch(N, opt, update, prefetch):
     synth = make_synth("criteo_kaggle", seed=4)
     F, K, layers, keep, B = synth.F, 8, [64, 32], [1.0, 1.0], 512
@@ -183,8 +186,8 @@ def test_sharded_exchange_matches_global_batch(N, opt, update, prefetch):
     assert models[0].comm.bytes_sent > 0
 
 
-@pytest.mark.parametrize("update", ["lazy", "tf1_dense"])
-def test_collective_sequence_identical_across_ranks(update):
+@pytest.mark.parametrize("update,depth", [("lazy", 1), ("tf1_dense", 1), ("lazy", 2)])
+def test_collective_sequence_identical_across_ranks(update, depth):
     """Deadlock freedom by construction (parallel/sharded.py): every collective of a step is a
     group on ONE engine, issued on the step's main stream (``_issue`` raises otherwise) in a fixed
     order.  Record each emulated rank's sequence of groups (kinds + byte counts) over N = 4 ranks
@@ -205,7 +208,7 @@ def test_collective_sequence_identical_across_ranks(update):
         models.append(m)
     batches = [[tuple(t.to(DEV) for t in synth.batch(B, step=100 * r + s, id_dtype=torch.int32))
                 for s in range(3)] for r in range(N)]
-    _run_ranks(models, batches, prefetch=True)
+    _run_ranks(models, batches, prefetch=depth)
     torch.cuda.synchronize()
     traces = [m.shx.trace for m in models]
     for t in traces[1:]:
@@ -216,8 +219,15 @@ def test_collective_sequence_identical_across_ranks(update):
     assert t[0] == (ids_op,) and t[1] == (rows_op,)            # step 0: inline ids, then rows
     g2 = t[2]
     assert g2[0] == rows_op and g2[-1] == ids_op                # gradients first, next ids last
-    assert len(t) == 7 and t[3] == (rows_op,) and t[5] == (rows_op,)
-    assert t[4][-1] == ids_op and t[6][-1] != ids_op            # last step: no next batch
+    assert len(t) == 7 and t[5] == (rows_op,)
+    if depth == 1:
+        assert t[3] == (rows_op,) and t[4][-1] == ids_op        # next ids with the gradients
+    else:
+        # batch 2 was routed during step 0: its ids travel with step 1's rows, its rows are
+        # served ahead during step 1 (step 2 then neither routes nor serves)
+        assert t[3] == (rows_op, ids_op) and t[4][-1] != ids_op
+        assert models[0].shx.sets[models[0].shx.cur].stage is None
+    assert t[6][-1] != ids_op                                   # last step: no next batch
     for m in models:
         m.check_errors()
 
@@ -323,7 +333,7 @@ def test_sharded_exchange_n8_criteo_1tb_shape():
         # the request table follows the exchange size, not the 110M-row shard
         assert sum(rs.req_key.numel() * 8 * (1 + N) for rs in m.shx.sets) < 256 * (1 << 20)
         models.append(m)
-    _run_ranks(models, batches, prefetch=True)
+    _run_ranks(models, batches, prefetch=2)
     torch.cuda.synchronize()
     for m in models:
         m.check_errors()
