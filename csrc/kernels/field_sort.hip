@@ -33,6 +33,7 @@
 // Output is bit-identical to the stable global sort (ties keep row order b, i.e. slot order
 // b*F+f).  An id outside its field's declared range sets *err (the host raises on it).
 #include "common.h"
+#include "fsort_run.h"
 
 namespace {
 constexpr int FS_THREADS = 1024;
@@ -278,6 +279,38 @@ __global__ void __launch_bounds__(256) fs_merge_kernel(const int* __restrict__ r
   sko[(size_t)f * B + pos] = k;
   pko[(size_t)f * B + pos] = rp[(size_t)f * B + e];
 }
+
+// Run-level sort (fsort_run.h): items are (job, work item) pairs over the run's batches
+__global__ void __launch_bounds__(FS2_THREADS) fs2_sort_run_kernel(const FsJob* __restrict__ jobs,
+                                                                   const int* __restrict__ items) {
+  extern __shared__ __align__(16) unsigned char lds[];
+  const FsJob J = jobs[items[2 * blockIdx.x]];
+  fs2_sort_item(J, items[2 * blockIdx.x + 1], lds);
+}
+
+__global__ void __launch_bounds__(FSM_THREADS) fs2_merge_run_kernel(const FsJob* __restrict__ jobs,
+                                                                    const int* __restrict__ items) {
+  extern __shared__ int stage[];
+  const FsJob J = jobs[items[2 * blockIdx.x]];
+  fs2_merge_item(J, items[2 * blockIdx.x + 1], stage);
+}
+
+// jobs: [njobs] device FsJobs (one per batch; B <= 8 chunks); items: [nitems][2] {job, sort item};
+// mitems: [nmitems][2] {job, merge workgroup}
+HFM_API int hfm_field_sort_run(const FsJob* jobs, const int* items, int nitems, const int* mitems, int nmitems,
+                               hipStream_t st) {
+  if (!jobs || !items || nitems <= 0 || nmitems < 0 || (nmitems && !mitems)) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(fs2_sort_run_kernel, dim3(nitems), dim3(FS2_THREADS), FS2_LDS, st, jobs, items);
+  if (nmitems)
+    hipLaunchKernelGGL(fs2_merge_run_kernel, dim3(nmitems), dim3(FSM_THREADS), FS2_MAXB * 4, st, jobs, mitems);
+  HFM_LAUNCH_CHECK();
+}
+
+HFM_API int hfm_fs_job_bytes() { return (int)sizeof(FsJob); }
+
+HFM_API int hfm_fs2_chunk_rows() { return FS2_MAXB; }
+
+HFM_API int hfm_fs2_merge_wgs_per_run() { return FSM_WPR; }
 
 HFM_API int hfm_field_sort_max_rows() { return FS_MAXB * FS_MAXCHUNK; }
 

@@ -64,13 +64,13 @@ struct SfArgs {
   const int* sid;
   const int* upos;
   float* gout;
-  int step_off;
+  int step_off;     // 1: *step is this step's index - 1 (the dense optimizer advances it later);
+                    // 0: the dense optimizer already ran and advanced it (single-GPU early mode)
   unsigned* flags;  // [tiles] publication flags: the step's 1-based index (*step + step_off)
   unsigned* sync;   // {pad, pad, error bits, pad}
   int v_by_key;     // MODE 2: 1 = V rows from the local table row key / row_div (replicated-table
                     // exchange), 0 = from the received rows at upos (row-sharded exchange)
-  int vbf16;        // table v rows and v slots are bf16 (mixed-precision embeddings; MODE 0 / 2)    // 1: *step is this step's index - 1 (the dense optimizer advances it later);
-                   // 0: the dense optimizer already ran and advanced it (single-GPU early mode)
+  int vbf16;        // table v rows and v slots are bf16 (mixed-precision embeddings; MODE 0 / 2)
 };
 
 // MODE 0: lazy optimizer OPT on the row; 1: tf1_dense scatter of the row gradient;

@@ -56,6 +56,9 @@ _TOWER_GATHER = flag("HIPFM_TOWER_GATHER")   # FM gather fused into the tower
 _WGFIN = flag("HIPFM_WGFIN")
 # single GPU, lazy rows: wgfin inside the sparse backward's launch (sparse_fused.hip sfwg_kernel)
 _SFWG = flag("HIPFM_SFWG")
+# one GPU, multi-step graphs: the run's batches sorted up front (fsort_run.h) instead of each
+# next batch on a side branch of the step before
+_RUN_SORT = flag("HIPFM_RUN_SORT")
 # row-sharded step: where the next batch's routing branch is enqueued: start | fetch | tower
 _SHX_FORK = knob("HIPFM_SHX_FORK")
 # row-sharded lazy step: dense optimizer inside the owner update's launch
@@ -364,6 +367,8 @@ class NativeDeepFM:
         self._bufs_M = 0
         self._side = None
         self._side_next = None
+        self._run_j = None          # run-level sort: this step's index in the run (train_steps)
+        self._run_ss = []           # run-level sort: (keys, perm) per step of the run
         self._next_sort_ids = None
         self._next_fm = False      # the declared next batch's ids are field-major
         self._tf1_plan = None      # tf1_dense split sweep: (flag set, inline sort, stale keys)
@@ -1322,7 +1327,10 @@ class NativeDeepFM:
             self._shx_start(B)
         after_fm = self.shx.fork_next if (self.shx is not None and _SHX_FORK == "tower") else None
         plan = self._sort_plan
-        self.sorted_keys, self.perm = self._ss[plan[0] if plan is not None else self._ss_cur]
+        if plan is not None and plan[0] == "run":        # sorted at the start of the run
+            self.sorted_keys, self.perm = self._run_ss[plan[3]]
+        else:
+            self.sorted_keys, self.perm = self._ss[plan[0] if plan is not None else self._ss_cur]
         prefetch = plan is not None and plan[2] is not None
         inline = plan is None or plan[1]
         main = torch.cuda.current_stream(self.device)
@@ -1620,7 +1628,11 @@ class NativeDeepFM:
         nxt2_fm = nxt2_ok and not next2_ids.is_contiguous()
         self._shx_plan = None
         self._sort_plan = None
-        if (not self.sharded and _SORT_SIDE_STREAM and self._fsort_next is not None and
+        if self._run_j is not None:
+            # run-level sort: this batch was sorted at the start of the run (train_steps)
+            self._sort_plan = ("run", False, None, self._run_j)
+            key = key + self._sort_plan
+        elif (not self.sharded and _SORT_SIDE_STREAM and self._fsort_next is not None and
                 self.uses_field_sort(B)):
             # the sort of a batch the caller declared as next (resident, unchanged until its step)
             # was computed during the previous step: reuse it when that batch is this one
@@ -1660,6 +1672,9 @@ class NativeDeepFM:
         if self.shx is not None:
             self.shx.commit(self._shx_plan, self.idx, B, resident=direct)
             self._shx_plan = None
+        if self._sort_plan is not None and self._sort_plan[0] == "run":
+            self._ss_key = [None, None]     # nothing prefetched for the step after the run
+            self._sort_plan = None
         if self._sort_plan is not None:
             c, _, nk = self._sort_plan
             self._ss_key[c] = None          # consumed: reused only through a next-batch declaration
@@ -1729,6 +1744,9 @@ class NativeDeepFM:
             for i, (ids, vals, labels) in enumerate(batches):
                 self.train_step(ids, vals, labels, use_graph=True, next_ids=nxt_of(i))
             return len(batches)
+        run_sort = self._run_sort_ok(batches)
+        if run_sort:
+            return self._train_run_sorted(batches)
         st0 = self._plan_state()
         # a run seen before from the same plan state replays its graph without re-planning
         # each step in Python (the per-step bind costs tens of us of host time, which a
@@ -1782,6 +1800,66 @@ class NativeDeepFM:
             self._run_memo.pop(next(iter(self._run_memo)))
         self._run_memo[mkey] = (key, g, self._plan_state(), len(batches))
         return len(batches)
+
+    def _run_sort_ok(self, batches) -> bool:
+        """The run's batches can be sorted up front (fsort_run.h): one GPU, lazy rows, field
+        ranges, equal batch sizes of at most 8 sort chunks, no tf1 row flags."""
+        if not (_RUN_SORT and len(batches) > 1 and self._fsort_next is not None and not self.sharded and
+                self.shx is None and self.rpx is None and not self.exchange and not self.tf1_split and
+                self.lazy_rows and _SORT_SIDE_STREAM):
+            return False
+        B = batches[0][0].shape[0]
+        return (all(b[0].shape[0] == B for b in batches) and self.uses_field_sort(B) and
+                B <= min(self._fsort_next.max_rows, 8 * KN.fs2_chunk_rows()))
+
+    def _run_sets(self, G: int):
+        n = self.M * self.F
+        while len(self._run_ss) < G:
+            self._run_ss.append((torch.zeros(n, dtype=torch.int32, device=self.device),
+                                 torch.zeros(n, dtype=torch.int32, device=self.device)))
+        return self._run_ss[:G]
+
+    def _train_run_sorted(self, batches) -> int:
+        """``train_steps`` with the run-level sort: ONE graph = the sort of every batch of the run
+        (two launches, fsort_run.h) followed by the steps, all on one queue (no per-step side
+        branch and no cross-queue join).  Bitwise equal to the per-step sorts (tested)."""
+        G = len(batches)
+        sets = self._run_sets(G)
+        fms = [not b[0].is_contiguous() for b in batches]
+        rplan = self._fsort_next.run_plan(
+            [(self._flat_ids(b[0], fm), b[0].shape[0], fm, k, p) for b, fm, (k, p) in zip(batches, fms, sets)])
+        mkey = ("runsort",) + tuple((b[0].data_ptr(), b[0].stride(), b[1].data_ptr(), b[2].data_ptr(),
+                                     b[0].shape[0]) for b in batches)
+        g = self._graphs.get(mkey)
+        if g is None and not self._graphs and not getattr(self, "_warm", False):
+            # the model's very first step runs eagerly (warms up lazy library state)
+            self._warm = True
+            ids, vals, labels = batches[0]
+            self.train_step(ids, vals, labels, use_graph=False)
+            torch.cuda.synchronize()
+            return 1 + self.train_steps(batches[1:])
+        if g is None:
+            g = torch.cuda.CUDAGraph()
+            h0 = self._host_step
+            with graph_capture(g):
+                self._fsort_next.run_sort(rplan)
+                for j, (ids, vals, labels) in enumerate(batches):
+                    self._run_j = j
+                    try:
+                        B, direct, _ = self._bind_step(ids, vals, labels)
+                        self.train_step_enqueue(B)
+                        self._commit_step(B, direct)
+                    finally:
+                        self._run_j = None
+            self._host_step = h0
+            if len(self._graphs) >= self.max_graphs:
+                self._graphs.pop(next(iter(self._graphs)))
+            self._graphs[mkey] = g
+        g.replay()
+        self._ss_key = [None, None]
+        if self._host_step is not None:
+            self._host_step += G
+        return G
 
     def _replay_graph(self, key, B: int):
         g = self._graphs.get(key)

@@ -137,6 +137,14 @@ class ShDenseArgs(C.Structure):
                 ("nsum", c_int)]
 
 
+class FsJob(C.Structure):
+    """fsort_run.h FsJob: one batch of the run-level field sort (chunk sorts + merge)."""
+    _fields_ = [("ids", c_void_p), ("ld", c_int), ("B", c_int), ("F", c_int), ("fr", c_void_p),
+                ("work", c_void_p), ("nwork", c_int), ("rk", c_void_p), ("rp", c_void_p),
+                ("keys", c_void_p), ("perm", c_void_p), ("err", c_void_p), ("mfields", c_void_p),
+                ("nmf", c_int), ("mwpf", c_int)]
+
+
 TW_MAXL = 8
 
 
@@ -259,6 +267,10 @@ _SIGS = {
     "hfm_tower": [C.POINTER(TowerArgs), c_int, c_void_p],
     "hfm_wgfin": [c_int, C.POINTER(WgFinArgs), c_void_p],
     "hfm_sparse_wgfin": [c_int, c_int, c_void_p, C.POINTER(WgFinArgs), c_void_p, c_void_p, c_void_p],
+    "hfm_fs_job_bytes": [],
+    "hfm_fs2_chunk_rows": [],
+    "hfm_fs2_merge_wgs_per_run": [],
+    "hfm_field_sort_run": [c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p],
     "hfm_sparse_wgfin_x": [c_int, c_void_p, C.POINTER(WgFinArgs), c_void_p],
     "hfm_wgfin_job_bytes": [],
     "hfm_wgfin_args_bytes": [],
@@ -306,7 +318,7 @@ def get_lib():
                            ("hfm_w8_job_bytes", W8Job),
                            ("hfm_sparse_fused_args_bytes", SfArgs),
                            ("hfm_sh_apply_args_bytes", ShApplyArgs),
-                           ("hfm_sh_dense_args_bytes", ShDenseArgs)):
+                           ("hfm_sh_dense_args_bytes", ShDenseArgs), ("hfm_fs_job_bytes", FsJob)):
             n = getattr(lib, cname)()
             if n != C.sizeof(pys):
                 raise RuntimeError(f"ABI mismatch {pys.__name__}: C {n} vs ctypes {C.sizeof(pys)}")

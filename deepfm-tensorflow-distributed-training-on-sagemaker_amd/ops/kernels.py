@@ -137,6 +137,11 @@ def sort_ids(keys_in, keys_out, vals_tmp, perm_out, n, end_bit, temp, limit: int
         lsd_sort_ids(keys_in, keys_out, perm_out, n, end_bit, temp)
 
 
+def fs2_chunk_rows() -> int:
+    """Rows per chunk of the run-level sort (fsort_run.h FS2_MAXB)."""
+    return int(L().hfm_fs2_chunk_rows())
+
+
 def field_sort_max_rows() -> int:
     """Largest batch the per-field LDS sort handles (csrc/kernels/field_sort.hip): row chunks of
     ``field_sort_chunk_rows()`` are sorted per workgroup, then merged."""
@@ -201,6 +206,60 @@ class FieldSort:
         check(L().hfm_field_sort(ptr(ids), B, self.F, ptr(self.fr), ptr(work), nwork,
                                  ptr(self.idsT), ptr(self.rk), ptr(self.rp), ptr(keys_out), ptr(perm_out),
                                  ptr(self.err), stream_handle()), "field_sort")
+
+    def run_plan(self, batches):
+        """Device plan of the run-level sort (fsort_run.h) of ``batches`` = [(ids, B, field_major,
+        keys_out, perm_out)]: one FsJob per batch (own chunk-run scratch), the sort items (batch,
+        field, 16K-row chunk; big fields first) and the merge items (B > 16K only).  Built on the host before any
+        capture and cached under the buffers' addresses."""
+        key = tuple((ptr(i), int(B), bool(fm), ptr(k), ptr(p)) for i, B, fm, k, p in batches)
+        cache = self.__dict__.setdefault("_run_plans", {})
+        hit = cache.get(key)
+        if hit is not None:
+            return hit
+        ch, wpr = fs2_chunk_rows(), int(L().hfm_fs2_merge_wgs_per_run())
+        fr = self.fr.view(-1, 4).cpu()
+        G = len(batches)
+        n = self.F * self.max_rows
+        rs = self.__dict__.get("_run_scratch")
+        if rs is None or rs.shape[0] < G:
+            rs = torch.zeros(G, 2, n, dtype=torch.int32, device=self.device)
+            self._run_scratch = rs
+            cache.clear()
+        jobs, items, mitems, keep = [], [], [], [rs]
+        for g, (ids, B, fm, kout, pout) in enumerate(batches):
+            assert B <= min(self.max_rows, 8 * ch) and ids.numel() >= B * self.F
+            nc = max(1, -(-B // ch))
+            wl = [(f, c) for f in range(self.F) for c in range(nc)]
+            wl.sort(key=lambda t: -int(fr[t[0], 2]))                 # big fields first
+            mf = [f for f in range(self.F) if int(fr[f, 2]) > 0] if nc > 1 else []
+            work = torch.tensor(wl, dtype=torch.int32).reshape(-1).to(self.device)
+            mft = torch.tensor(mf or [0], dtype=torch.int32).to(self.device)
+            keep += [work, mft]
+            j = _lib.FsJob()
+            j.ids, j.ld = ptr(ids), (B if fm else 0)                    # field-major: [F, B]
+            j.B, j.F, j.fr, j.work, j.nwork = B, self.F, ptr(self.fr), ptr(work), len(wl)
+            j.rk, j.rp = ptr(rs[g, 0]), ptr(rs[g, 1])
+            j.keys, j.perm, j.err = ptr(kout), ptr(pout), ptr(self.err)
+            j.mfields, j.nmf, j.mwpf = ptr(mft), len(mf), wpr * nc
+            jobs.append(j)
+            items.append([(g, it) for it in range(len(wl))])
+            mitems.append([(g, mw) for mw in range(len(mf) * wpr * nc)])
+        # interleave the batches: item k of every batch, then item k + 1 (big fields first overall)
+        flat = [t[k] for k in range(max(len(t) for t in items)) for t in items if k < len(t)]
+        mflat = [t[k] for k in range(max(len(t) for t in mitems)) for t in mitems if k < len(t)]
+        jobs_dev = struct_array_to_device(jobs, self.device)
+        it_dev = torch.tensor(flat, dtype=torch.int32).reshape(-1).to(self.device)
+        mit_dev = torch.tensor(mflat or [(0, 0)], dtype=torch.int32).reshape(-1).to(self.device)
+        plan = (jobs_dev, it_dev, len(flat), mit_dev, len(mflat), keep)
+        cache[key] = plan
+        return plan
+
+    def run_sort(self, plan):
+        """Enqueue the run-level sort of ``run_plan``'s batches (two launches)."""
+        jobs_dev, it_dev, nit, mit_dev, nmit, _ = plan
+        check(L().hfm_field_sort_run(ptr(jobs_dev), ptr(it_dev), nit, ptr(mit_dev), nmit, stream_handle()),
+              "field_sort_run")
 
     def sort_pre(self, B: int, keys_out, perm_out):
         """The sort alone, from ``self.idsT`` already filled field-major ([F, B]) by fm_fwd."""
