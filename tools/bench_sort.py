@@ -52,10 +52,28 @@ def field_main(dev):
               flush=True)
 
 
+def run_main(dev):
+    """Run-level sort (fsort_run.h) of G Criteo-1TB-shape batches vs G per-step field sorts."""
+    from hipfm.data.synthetic import make_synth
+    synth = make_synth("criteo_1tb")
+    F, B = synth.F, 16384
+    fs = KN.FieldSort(synth.field_ranges(), B, dev, max_pb=0)
+    for G in (1, 4, 20):
+        ids = [synth.batch(B, s, device=dev, id_dtype=torch.int32)[0].reshape(-1).contiguous() for s in range(G)]
+        outs = [(torch.empty_like(i), torch.empty_like(i)) for i in ids]
+        plan = fs.run_plan([(i, B, False, k, p) for i, (k, p) in zip(ids, outs)])
+        tr = timeit(lambda: fs.run_sort(plan), reps=10, inner=5)
+        ts = timeit(lambda: [fs(i, B, k, p) for i, (k, p) in zip(ids, outs)], reps=10, inner=5)
+        print(f"criteo_1tb B={B} G={G:3d}: run_sort {tr:8.1f} us ({tr / G:6.1f}/batch)  "
+              f"per-step field_sort x G {ts:8.1f} us", flush=True)
+
+
 def main():
     dev = torch.device("cuda", 0)
     if "--field" in sys.argv:
         return field_main(dev)
+    if "--run" in sys.argv:
+        return run_main(dev)
     sizes = (39 * 1024, 39 * 16384, 39 * 32768, 39 * 65536)
     if "--only" in sys.argv:
         sizes = (int(sys.argv[sys.argv.index("--only") + 1]),)
