@@ -177,13 +177,13 @@ constexpr int RT_TILE = SH_THREADS * RT_ITEMS;
 // Per-tile head counts per owner.  Heads are counted per wave with ballots (lanes of one owner
 // found by nbits bit-ballots, as in sh_route_scatter_kernel): one LDS atomic per (wave, owner)
 // instead of one per head -- at N = 1 every head of a tile hit the same LDS word.
-__global__ void __launch_bounds__(SH_THREADS) sh_route_count_kernel(const int* __restrict__ sk, int n, int N,
-                                                                   int nbits, int* __restrict__ tcnt) {
+__device__ __forceinline__ void sh_route_count_body(const int* __restrict__ sk, int n, int N, int nbits,
+                                                    int* __restrict__ tcnt, int bx) {
   __shared__ int h[SH_MAXN + 1];
   const int tid = threadIdx.x, lane = tid & 63;
   if (tid <= N) h[tid] = 0;
   __syncthreads();
-  const int i0 = blockIdx.x * RT_TILE;
+  const int i0 = bx * RT_TILE;
   const unsigned long long lt = (1ull << lane) - 1ull;
   int nh = 0;
 #pragma unroll 4
@@ -208,13 +208,19 @@ __global__ void __launch_bounds__(SH_THREADS) sh_route_count_kernel(const int* _
   }
   if (lane == 0) atomicAdd(&h[N], nh);
   __syncthreads();
-  if (tid <= N) tcnt[blockIdx.x * (N + 1) + tid] = h[tid];
+  if (tid <= N) tcnt[bx * (N + 1) + tid] = h[tid];
 }
 
-__global__ void __launch_bounds__(SH_THREADS) sh_route_scatter_kernel(
+__global__ void __launch_bounds__(SH_THREADS) sh_route_count_kernel(const int* __restrict__ sk, int n, int N,
+                                                                   int nbits, int* __restrict__ tcnt) {
+  sh_route_count_body(sk, n, N, nbits, tcnt, blockIdx.x);
+}
+
+// tile bx of the scatter (grid of nt tiles per batch)
+__device__ __forceinline__ void sh_route_scatter_body(
     const int* __restrict__ sk, int n, int N, int nbits, int C, const int* __restrict__ tcnt, int nt,
     int* __restrict__ sid_incl, int* __restrict__ send_ids, int* __restrict__ upos, int* __restrict__ send_cnt,
-    int* __restrict__ num_u, unsigned* __restrict__ err) {
+    int* __restrict__ num_u, unsigned* __restrict__ err, int bx) {
   __shared__ int off[SH_MAXN + 1];
   __shared__ int tot[SH_MAXN + 1];
   __shared__ int wc[4][SH_MAXN + 1];  // per wave: heads per owner, [N]: all heads
@@ -224,22 +230,22 @@ __global__ void __launch_bounds__(SH_THREADS) sh_route_scatter_kernel(
   for (int e = tid; e < nt * (N + 1); e += SH_THREADS) {
     const int b = e / (N + 1), o = e - b * (N + 1);
     const int c = tcnt[e];
-    if (b < (int)blockIdx.x) atomicAdd(&off[o], c);
+    if (b < bx) atomicAdd(&off[o], c);
     atomicAdd(&tot[o], c);
   }
   __syncthreads();
-  if (blockIdx.x == 0) {
+  if (bx == 0) {
     if (tid < N) {
       send_cnt[tid] = tot[tid];
       if (tot[tid] > C) atomicOr(err, 2u);
     }
     if (tid == 0) *num_u = tot[N];
   }
-  for (int e = blockIdx.x * SH_THREADS + tid; e < N * C; e += gridDim.x * SH_THREADS) {
+  for (int e = bx * SH_THREADS + tid; e < N * C; e += nt * SH_THREADS) {
     const int o = e / C;
     if (e - o * C >= tot[o]) send_ids[e] = -1;  // unused capacity: padding entries
   }
-  const int w0 = blockIdx.x * RT_TILE + wv * 64 * RT_ITEMS;
+  const int w0 = bx * RT_TILE + wv * 64 * RT_ITEMS;
   const unsigned long long lt = (1ull << lane) - 1ull;
   int key[RT_ITEMS], own[RT_ITEMS], rnk[RT_ITEMS], hin[RT_ITEMS];
   unsigned hmask = 0;
@@ -290,6 +296,13 @@ __global__ void __launch_bounds__(SH_THREADS) sh_route_scatter_kernel(
   }
 }
 
+__global__ void __launch_bounds__(SH_THREADS) sh_route_scatter_kernel(
+    const int* __restrict__ sk, int n, int N, int nbits, int C, const int* __restrict__ tcnt, int nt,
+    int* __restrict__ sid_incl, int* __restrict__ send_ids, int* __restrict__ upos, int* __restrict__ send_cnt,
+    int* __restrict__ num_u, unsigned* __restrict__ err) {
+  sh_route_scatter_body(sk, n, N, nbits, C, tcnt, nt, sid_incl, send_ids, upos, send_cnt, num_u, err, blockIdx.x);
+}
+
 // fm_fwd row index of every slot: the received row of its unique id
 __global__ void sh_slot_rows_kernel(const int* __restrict__ perm, const int* __restrict__ sid_incl,
                                     const int* __restrict__ upos, int n, int* __restrict__ idx) {
@@ -297,6 +310,43 @@ __global__ void sh_slot_rows_kernel(const int* __restrict__ perm, const int* __r
   if (i >= n) return;
   const int r = upos[sid_incl[i] - 1];
   idx[perm[i]] = r < 0 ? 0 : r;
+}
+
+// Run-level routing (the row-sharded analogue of fsort_run.h): the routing of EVERY batch of a
+// multi-step graph in three launches at its start (blockIdx.y = batch), so the steps that follow
+// carry no routing branch and no cross-queue join.  One descriptor per batch (its routing set).
+struct ShRouteBatch {
+  const int* sk;    // sorted slot ids [n]
+  const int* perm;  // their slot positions [n]
+  int* tcnt;        // [tiles][N + 1]
+  int* sid_incl;
+  int* send_ids;    // [N][C]
+  int* upos;
+  int* send_cnt;
+  int* num_u;
+  int* slot_row;    // [n] fm_fwd row index of every slot
+};
+
+__global__ void __launch_bounds__(SH_THREADS) sh_route_count_run_kernel(const ShRouteBatch* __restrict__ rb, int n,
+                                                                       int N, int nbits) {
+  const ShRouteBatch R = rb[blockIdx.y];
+  sh_route_count_body(R.sk, n, N, nbits, R.tcnt, blockIdx.x);
+}
+
+__global__ void __launch_bounds__(SH_THREADS) sh_route_scatter_run_kernel(const ShRouteBatch* __restrict__ rb, int n,
+                                                                         int N, int nbits, int C, int nt,
+                                                                         unsigned* __restrict__ err) {
+  const ShRouteBatch R = rb[blockIdx.y];
+  sh_route_scatter_body(R.sk, n, N, nbits, C, R.tcnt, nt, R.sid_incl, R.send_ids, R.upos, R.send_cnt, R.num_u,
+                        err, blockIdx.x);
+}
+
+__global__ void sh_slot_rows_run_kernel(const ShRouteBatch* __restrict__ rb, int n) {
+  const ShRouteBatch R = rb[blockIdx.y];
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int r = R.upos[R.sid_incl[i] - 1];
+  R.slot_row[R.perm[i]] = r < 0 ? 0 : r;
 }
 
 // Owner: rows[e] = {v[K], w, 0, 0, 0} of each requested id (zeros for padding entries)
@@ -474,6 +524,20 @@ HFM_API int hfm_sh_route(const int* sorted_keys, int n, int N, int C, int* tcnt,
                      tcnt, nt, sid_incl, send_ids, upos, send_cnt, num_u, err);
   HFM_LAUNCH_CHECK();
 }
+
+// G batches' routing (descriptors rb [G], device): count, scatter, slot rows -- three launches
+HFM_API int hfm_sh_route_run(const ShRouteBatch* rb, int G, int n, int N, int C, unsigned* err, hipStream_t st) {
+  if (!rb || G <= 0 || G > 65535 || N < 1 || N > SH_MAXN || n <= 0 || C <= 0) return (int)hipErrorInvalidValue;
+  const int nt = hfm_sh_route_tiles(n);
+  int nbits = 0;
+  while ((1 << nbits) < N) ++nbits;
+  hipLaunchKernelGGL(sh_route_count_run_kernel, dim3(nt, G), dim3(SH_THREADS), 0, st, rb, n, N, nbits);
+  hipLaunchKernelGGL(sh_route_scatter_run_kernel, dim3(nt, G), dim3(SH_THREADS), 0, st, rb, n, N, nbits, C, nt, err);
+  hipLaunchKernelGGL(sh_slot_rows_run_kernel, dim3((n + 255) / 256, G), dim3(256), 0, st, rb, n);
+  HFM_LAUNCH_CHECK();
+}
+
+HFM_API int hfm_sh_route_batch_bytes() { return (int)sizeof(ShRouteBatch); }
 
 HFM_API int hfm_sh_slot_rows(const int* perm, const int* sid_incl, const int* upos, int n, int* idx,
                              hipStream_t st) {

@@ -1628,7 +1628,7 @@ class NativeDeepFM:
         nxt2_fm = nxt2_ok and not next2_ids.is_contiguous()
         self._shx_plan = None
         self._sort_plan = None
-        if self._run_j is not None:
+        if self._run_j is not None and self.shx is None:
             # run-level sort: this batch was sorted at the start of the run (train_steps)
             self._sort_plan = ("run", False, None, self._run_j)
             key = key + self._sort_plan
@@ -1653,7 +1653,11 @@ class NativeDeepFM:
             inline = self._sort_plan is None or self._sort_plan[1]
             self._tf1_plan = (c, inline, self._stamp_n[c] if inline else 0)
             key = key + ("tf1",) + self._tf1_plan
-        if self.shx is not None:
+        if self.shx is not None and self._run_j is not None:
+            # run-level routing: routed and its ids exchanged at the start of the run
+            self._shx_plan = self.shx.run_plan(self._run_j)
+            key = key + tuple(self._shx_plan)
+        elif self.shx is not None:
             nxt = self._flat_ids(next_ids, nxt_fm) if (nxt_ok and _SHARD_PIPELINE) else None
             nxt2 = self._flat_ids(next2_ids, nxt2_fm) if (nxt2_ok and _SHARD_PIPELINE) else None
             self._shx_plan = self.shx.plan(self.idx, B, nxt, resident=direct, nxt2=nxt2)
@@ -1744,8 +1748,7 @@ class NativeDeepFM:
             for i, (ids, vals, labels) in enumerate(batches):
                 self.train_step(ids, vals, labels, use_graph=True, next_ids=nxt_of(i))
             return len(batches)
-        run_sort = self._run_sort_ok(batches)
-        if run_sort:
+        if self._run_sort_ok(batches) or self._run_route_ok(batches):
             return self._train_run_sorted(batches)
         st0 = self._plan_state()
         # a run seen before from the same plan state replays its graph without re-planning
@@ -1812,6 +1815,16 @@ class NativeDeepFM:
         return (all(b[0].shape[0] == B for b in batches) and self.uses_field_sort(B) and
                 B <= min(self._fsort_next.max_rows, 8 * KN.fs2_chunk_rows()))
 
+    def _run_route_ok(self, batches) -> bool:
+        """Run-level routing (parallel/sharded.py ``route_run``): the row-sharded step over
+        resident batches of one size, with the per-field sort and graph-safe collectives."""
+        if not (_RUN_SORT and len(batches) > 1 and self.shx is not None and self._fsort is not None and
+                self.comm is not None and self.comm.graph_safe):
+            return False
+        B = batches[0][0].shape[0]
+        return (all(b[0].shape[0] == B for b in batches) and self.uses_field_sort(B) and
+                B <= min(self._fsort.max_rows, 8 * KN.fs2_chunk_rows()))
+
     def _run_sets(self, G: int):
         n = self.M * self.F
         while len(self._run_ss) < G:
@@ -1821,13 +1834,20 @@ class NativeDeepFM:
 
     def _train_run_sorted(self, batches) -> int:
         """``train_steps`` with the run-level sort: ONE graph = the sort of every batch of the run
-        (two launches, fsort_run.h) followed by the steps, all on one queue (no per-step side
-        branch and no cross-queue join).  Bitwise equal to the per-step sorts (tested)."""
+        (two launches, fsort_run.h) -- or, row-sharded, its whole routing incl. the id exchange
+        (``FixedCapacityExchange.route_run``) -- followed by the steps, all on one queue (no
+        per-step side branch and no cross-queue join).  Bitwise equal to the per-step sorts /
+        routing (tested)."""
         G = len(batches)
-        sets = self._run_sets(G)
         fms = [not b[0].is_contiguous() for b in batches]
-        rplan = self._fsort_next.run_plan(
-            [(self._flat_ids(b[0], fm), b[0].shape[0], fm, k, p) for b, fm, (k, p) in zip(batches, fms, sets)])
+        routed = self.shx is not None
+        if routed:
+            rlist = [(self._flat_ids(b[0], fm), b[0].shape[0], fm) for b, fm in zip(batches, fms)]
+            self.shx.route_run_prepare(rlist)           # allocations / device plans: not in a capture
+        else:
+            sets = self._run_sets(G)
+            rplan = self._fsort_next.run_plan(
+                [(self._flat_ids(b[0], fm), b[0].shape[0], fm, k, p) for b, fm, (k, p) in zip(batches, fms, sets)])
         mkey = ("runsort",) + tuple((b[0].data_ptr(), b[0].stride(), b[1].data_ptr(), b[2].data_ptr(),
                                      b[0].shape[0]) for b in batches)
         g = self._graphs.get(mkey)
@@ -1842,7 +1862,10 @@ class NativeDeepFM:
             g = torch.cuda.CUDAGraph()
             h0 = self._host_step
             with graph_capture(g):
-                self._fsort_next.run_sort(rplan)
+                if routed:
+                    self.shx.route_run(rlist)
+                else:
+                    self._fsort_next.run_sort(rplan)
                 for j, (ids, vals, labels) in enumerate(batches):
                     self._run_j = j
                     try:

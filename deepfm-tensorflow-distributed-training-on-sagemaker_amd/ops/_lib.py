@@ -137,6 +137,13 @@ class ShDenseArgs(C.Structure):
                 ("nsum", c_int)]
 
 
+class ShRouteBatch(C.Structure):
+    """shard.hip ShRouteBatch: one batch's routing set for the run-level routing launches."""
+    _fields_ = [("sk", c_void_p), ("perm", c_void_p), ("tcnt", c_void_p), ("sid_incl", c_void_p),
+                ("send_ids", c_void_p), ("upos", c_void_p), ("send_cnt", c_void_p), ("num_u", c_void_p),
+                ("slot_row", c_void_p)]
+
+
 class FsJob(C.Structure):
     """fsort_run.h FsJob: one batch of the run-level field sort (chunk sorts + merge)."""
     _fields_ = [("ids", c_void_p), ("ld", c_int), ("B", c_int), ("F", c_int), ("fr", c_void_p),
@@ -244,6 +251,8 @@ _SIGS = {
     "hfm_sh_count_blocks": [c_int],
     "hfm_sh_route_tiles": [c_int],
     "hfm_sh_route": [c_void_p, c_int, c_int, c_int] + [c_void_p] * 7 + [c_void_p],
+    "hfm_sh_route_run": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
+    "hfm_sh_route_batch_bytes": [],
     "hfm_sh_bucket": [c_void_p, c_void_p, c_int, c_int, c_int] + [c_void_p] * 5 + [c_void_p],
     "hfm_sh_slot_rows": [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p],
     "hfm_sh_serve": [c_int, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_long, c_long, c_void_p,
@@ -318,7 +327,8 @@ def get_lib():
                            ("hfm_w8_job_bytes", W8Job),
                            ("hfm_sparse_fused_args_bytes", SfArgs),
                            ("hfm_sh_apply_args_bytes", ShApplyArgs),
-                           ("hfm_sh_dense_args_bytes", ShDenseArgs), ("hfm_fs_job_bytes", FsJob)):
+                           ("hfm_sh_dense_args_bytes", ShDenseArgs), ("hfm_fs_job_bytes", FsJob),
+                           ("hfm_sh_route_batch_bytes", ShRouteBatch)):
             n = getattr(lib, cname)()
             if n != C.sizeof(pys):
                 raise RuntimeError(f"ABI mismatch {pys.__name__}: C {n} vs ctypes {C.sizeof(pys)}")

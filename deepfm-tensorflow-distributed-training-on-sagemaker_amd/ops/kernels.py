@@ -580,6 +580,12 @@ def sh_route(sorted_keys, n, N, Cap, tcnt, sid_incl, send_ids, upos, send_cnt, n
                            ptr(send_cnt), ptr(num_u), ptr(err), stream_handle()), "sh_route")
 
 
+def sh_route_run(descs_dev, G: int, n: int, N: int, Cap: int, err):
+    """Routing of G batches (``descs_dev``: device array of ``_lib.ShRouteBatch``) in three
+    launches: owner buckets, unique indices and the slot -> row maps of every batch."""
+    check(L().hfm_sh_route_run(ptr(descs_dev), G, n, N, Cap, ptr(err), stream_handle()), "sh_route_run")
+
+
 def sh_slot_rows(perm, sid_incl, upos, n, idx):
     check(L().hfm_sh_slot_rows(ptr(perm), ptr(sid_incl), ptr(upos), n, ptr(idx), stream_handle()),
           "sh_slot_rows")

@@ -33,6 +33,13 @@ rows it changes; lazy rows only) -- the serve leaves the critical path.  With on
 known, it is routed during the step and its ids travel in G2 (depth 1); rows are served at the
 start of their own step.
 
+Run-level routing.  A multi-step graph over resident batches instead routes EVERY batch of the
+run at its start (``route_run``: batched sort + routing launches and ONE grouped ids all-to-all,
+G0 of the run) into one routing set per step; each step then only serves its rows inline, G1
+(rows) and G2 (gradients + dense) -- one queue, no side branch, no cross-queue join (each join
+of a branch costs the step ~10 us on MI355X, profiles/r3c_fx_kernels.md).  The collective
+sequence is still fixed by the host plan alone: identical on every rank.
+
 Capacity: the unique ids a rank sends to one owner must fit ``capacity``.  ``estimate_capacity``
 measures sample batches; a bucket that overflows sets an error word that the model checks
 (``NativeDeepFM.check_errors``) and raises on — rows are never silently dropped.
@@ -158,7 +165,7 @@ class CollectiveOrderError(RuntimeError):
 
 class ShPlan(NamedTuple):
     """Host-side routing decisions of one step (part of the captured graph's key)."""
-    c: int                       # routing set of this batch
+    c: int                       # routing set of this batch (run mode: index into run_sets)
     route: bool                  # run this batch's routing kernels inline
     ids: bool                    # exchange this batch's ids inline (G0)
     serve: bool                  # serve this batch's rows at the start of the step
@@ -166,6 +173,8 @@ class ShPlan(NamedTuple):
     n1_mode: Optional[str]       # "xchg": routed earlier, ids in G1 (+ serve ahead); "route": now, ids in G2
     serve_ahead: bool            # serve the next batch's rows during this step
     n2: Optional[tuple]          # (ids address, B) of the batch after: routed during this step
+    run: bool = False            # run-level routing: set c of run_sets, routed + ids exchanged at
+                                 # the start of the run (route_run)
 
 
 class FixedCapacityExchange:
@@ -200,6 +209,8 @@ class FixedCapacityExchange:
         self._plan = None
         self.dense_recv = None               # [N][P] all-gathered dense gradients (fused exchange)
         self.trace = None                    # list: record every issued group (tests)
+        self.run_sets = []                   # run-level routing: one set per step of the run
+        self._run_descs = {}
 
     # ------------------------------------------------------------------ host-side plan
     def plan(self, ids: torch.Tensor, B: int, nxt: Optional[torch.Tensor], resident: bool = True,
@@ -224,12 +235,64 @@ class FixedCapacityExchange:
                 n2 = (nxt2.data_ptr(), nxt2.numel() // self.m.F)
         return ShPlan(c, route, ids_x, serve, n1, n1_mode, ahead, n2)
 
+    # ------------------------------------------------------------------ run-level routing
+    def route_run(self, batches):
+        """Run-level routing (a multi-step graph's start): the field sort, routing kernels and id
+        exchange of EVERY batch of the run -- 2 + 3 launches and ONE grouped all-to-all on the main
+        stream -- so each step of the run (``run_plan``) serves its rows, fetches them and pushes
+        its gradients with no side branch and no cross-queue join.  ``batches``: [(ids [B*F] as
+        the step binds them, B, field-major)], all of one B; needs the per-field sort."""
+        sets, n, sort_plan, d = self.route_run_prepare(batches)
+        self._main = torch.cuda.current_stream(self.m.device)
+        self.m._fsort.run_sort(sort_plan)
+        KN.sh_route_run(d, len(sets), n, self.N, self.C, self.err)
+        self._issue([self._ids_op(rs) for rs in sets])                   # G0 of the whole run
+        self._main = None
+
+    def route_run_prepare(self, batches):
+        """Host side of ``route_run`` (allocations and device plans; call it before a capture)."""
+        m = self.m
+        G = len(batches)
+        B = batches[0][1]
+        n = B * m.F
+        while len(self.run_sets) < G:
+            self.run_sets.append(_RouteSet(m, m.M * m.F, self.N, self.C, m.temp.numel(), self.RW))
+        sets = self.run_sets[:G]
+        sort_plan = m._fsort.run_plan([(ids, b, fm, rs.sorted_keys, rs.perm)
+                                       for (ids, b, fm), rs in zip(batches, sets)])
+        key = (G, n)
+        d = self._run_descs.get(key)
+        if d is None:
+            from ..ops._lib import ShRouteBatch
+            descs = []
+            for rs in sets:
+                r = ShRouteBatch()
+                r.sk, r.perm, r.tcnt, r.sid_incl = (rs.sorted_keys.data_ptr(), rs.perm.data_ptr(),
+                                                    rs.tcnt.data_ptr(), rs.sid_incl.data_ptr())
+                r.send_ids, r.upos, r.send_cnt = rs.send_ids.data_ptr(), rs.upos.data_ptr(), rs.send_cnt.data_ptr()
+                r.num_u, r.slot_row = rs.num_u.data_ptr(), rs.slot_row.data_ptr()
+                descs.append(r)
+            d = KN.struct_array_to_device(descs, m.device)
+            self._run_descs[key] = d
+        return sets, n, sort_plan, d
+
+    def run_plan(self, j: int) -> ShPlan:
+        """Step j of a run routed by ``route_run``: rows served at the step start (inline), then
+        the rows all-to-all (G1) and the gradient group (G2) -- nothing routed or forked."""
+        return ShPlan(j, False, False, True, None, None, False, None, True)
+
+    def _rs(self, plan: ShPlan) -> _RouteSet:
+        return self.run_sets[plan.c] if plan.run else self.sets[plan.c]
+
     def commit(self, plan: ShPlan, ids: torch.Tensor = None, B: int = 0, resident: bool = True):
         """Consecutive steps rotate through the routing sets (prefetched or not), so a step's
         routing kernels never overwrite buffers an earlier step's backward still reads, even when
         graph replays run back to back.  A set is reused ONLY for the batch a caller declared as
         upcoming: never matched again by address alone (a fresh batch can get the address of an
         earlier one back from the caching allocator)."""
+        if plan.run:                     # the rotating sets hold nothing for the next step
+            self.invalidate()
+            return
         c = plan.c
         self.sets[c].key = self.sets[c].stage = None
         s1, s2 = self.sets[(c + 1) % self.NSETS], self.sets[(c + 2) % self.NSETS]
@@ -302,7 +365,7 @@ class FixedCapacityExchange:
         m = self.m
         self._main = torch.cuda.current_stream(m.device)
         self._plan = plan
-        rs = self.sets[plan.c]
+        rs = self._rs(plan)
         if plan.route:
             self.route_kernels(rs, m.idx, B, fm=m._idx_fm)
         if plan.ids:
@@ -347,7 +410,7 @@ class FixedCapacityExchange:
         tags with the serve (read by the update at the end of the step); eval / predict fetches
         leave them alone."""
         m = self.m
-        rs = self.sets[plan.c]
+        rs = self._rs(plan)
         if plan.serve:
             if train:
                 KN.sh_serve(m.K, rs.recv_ids, self.N * self.C, self.N, m.tv, m.tw, rs.rows_out,
@@ -383,7 +446,7 @@ class FixedCapacityExchange:
         ``dense`` (ShDenseArgs, lazy rows): the dense optimizer runs in the owner update's launch.
         The next batch's ids, when routed during this step, travel in the same group (G2)."""
         m = self.m
-        rs = self.sets[plan.c]
+        rs = self._rs(plan)
         n = B * m.F
         A = m.sf_args(n)
         A.sorted_keys, A.perm = rs.sorted_keys.data_ptr(), rs.perm.data_ptr()
@@ -435,7 +498,7 @@ class FixedCapacityExchange:
 
     def reset_table(self):
         """The tables' stamps are step numbers: clear them when the step counter is rewritten."""
-        for rs in self.sets:
+        for rs in self.sets + self.run_sets:
             rs.req_key.zero_()
             rs.req_pos.zero_()
         self.drop_served()

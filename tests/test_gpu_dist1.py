@@ -138,6 +138,50 @@ def test_exchange_field_major_batches_bitwise(group):
         assert torch.equal(x, y)
 
 
+@pytest.mark.parametrize("update,fm", [("lazy", False), ("tf1_dense", False), ("lazy", True)])
+def test_exchange_run_routing_bitwise(group, monkeypatch, update, fm):
+    """Run-level routing (FixedCapacityExchange.route_run: every batch of a multi-step graph
+    sorted, routed and its ids exchanged at the graph's start; each step serves its rows inline)
+    gives bitwise the parameters of the per-step pipelined routing (side-stream routing, serve
+    ahead) and of single steps; the routed sets hold exactly each batch's routing."""
+    import hipfm.models.deepfm as D
+    synth = make_synth("total:6000", seed=37)
+    F, K, layers, keep = synth.F, 8, [64, 32], [0.8, 0.8]
+    V = synth.feature_size
+    params = init_params(V, F, K, layers, False, seed=9)
+    pool = [synth.batch(512, step=s, device="cuda", id_dtype=torch.int32) for s in range(5)]
+    pool = [(i.t().contiguous().t() if fm else i, v, lab) for i, v, lab in pool]
+    out = []
+    for run, graph in ((True, True), (False, True), (False, False)):
+        monkeypatch.setattr(D, "_RUN_SORT", run)
+        m = NativeDeepFM(V, F, K, layers, keep, sparse_update=update, batch_size=512, device="cuda",
+                         init=False, comm=Comm(sharded=True, force_exchange=True),
+                         field_ranges=synth.field_ranges())
+        m.load_tf_params(params)
+        for _ in range(3):
+            if graph:
+                m.train_steps(pool[:3], next_ids=(pool[3][0], pool[4][0]))
+                m.train_steps(pool[3:], next_ids=(pool[0][0], pool[1][0]))
+            else:
+                for i, (ids, vals, lab) in enumerate(pool):
+                    m.train_step(ids, vals, lab, next_ids=pool[(i + 1) % 5][0])
+        torch.cuda.synchronize()
+        m.check_errors()
+        if run:
+            assert len(m.shx.run_sets) == 3
+            rs = m.shx.run_sets[0]                 # the last run routed pool[3], pool[4]
+            n = 512 * F
+            ids = pool[3][0].reshape(-1) if not fm else pool[3][0].contiguous().reshape(-1)
+            rk, _ = torch.sort(ids.long(), stable=True)
+            assert torch.equal(rs.sorted_keys[:n].long(), rk)
+            assert int(rs.num_u.item()) == int(torch.unique(ids).numel())
+        out.append((m.tv.clone(), m.tw.clone(), m.p.clone(), m.step.clone()))
+        del m
+    for ref in out[1:]:
+        for x, y in zip(out[0], ref):
+            assert torch.equal(x, y)
+
+
 @pytest.mark.parametrize("sharded", [True, False])
 def test_estimator_calibrates_exchange_capacity(group, tmp_path, sharded):
     """the CLI's multi-GPU path ran on default_capacity (1.5x slots / N, ~3-4x the

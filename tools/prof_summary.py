@@ -60,6 +60,25 @@ def main():
                 lines.append(f"| {(s - t0)/1e3:.2f} | {(e - s)/1e3:.2f} | `{r['Kernel_Name'][:80]}` |")
             span = (int(rows[b]["End_Timestamp"]) - t0) / 1e3
             lines += ["", f"step span {span:.1f} us, sum of kernel durations {tot/1e3:.1f} us", ""]
+        # run-level sort / routing (multi-step graphs): the kernels from a run's sort to its
+        # first tower, for the median-length run start
+        starts = [i for i, r in enumerate(rows) if r["Kernel_Name"].startswith("fs2_sort_run_kernel")]
+        spans = []
+        for i in starts:
+            j = next((k for k in range(i + 1, len(rows)) if rows[k]["Kernel_Name"].startswith("void tower_kernel")),
+                     None)
+            if j is not None:
+                spans.append((int(rows[j]["Start_Timestamp"]) - int(rows[i]["Start_Timestamp"]), i, j))
+        if spans:
+            spans.sort()
+            d, i, j = spans[len(spans) // 2]
+            t0 = int(rows[i]["Start_Timestamp"])
+            lines += ["## Run start (run-level sort / routing, median of %d runs): %.1f us to the first tower"
+                      % (len(spans), d / 1e3), "", "| start us | dur us | kernel |", "|---:|---:|---|"]
+            for r in rows[i:j]:
+                s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+                lines.append(f"| {(s - t0)/1e3:.2f} | {(e - s)/1e3:.2f} | `{r['Kernel_Name'][:80]}` |")
+            lines.append("")
     open(out, "w").write("\n".join(lines) + "\n")
     print(out)
 
