@@ -220,7 +220,7 @@ __global__ void __launch_bounds__(SH_THREADS) sh_route_count_kernel(const int* _
 __device__ __forceinline__ void sh_route_scatter_body(
     const int* __restrict__ sk, int n, int N, int nbits, int C, const int* __restrict__ tcnt, int nt,
     int* __restrict__ sid_incl, int* __restrict__ send_ids, int* __restrict__ upos, int* __restrict__ send_cnt,
-    int* __restrict__ num_u, unsigned* __restrict__ err, int bx) {
+    int* __restrict__ num_u, unsigned* __restrict__ err, int bx, int ostride) {
   __shared__ int off[SH_MAXN + 1];
   __shared__ int tot[SH_MAXN + 1];
   __shared__ int wc[4][SH_MAXN + 1];  // per wave: heads per owner, [N]: all heads
@@ -242,8 +242,8 @@ __device__ __forceinline__ void sh_route_scatter_body(
     if (tid == 0) *num_u = tot[N];
   }
   for (int e = bx * SH_THREADS + tid; e < N * C; e += nt * SH_THREADS) {
-    const int o = e / C;
-    if (e - o * C >= tot[o]) send_ids[e] = -1;  // unused capacity: padding entries
+    const int o = e / C, c = e - o * C;
+    if (c >= tot[o]) send_ids[(size_t)o * ostride + c] = -1;  // unused capacity: padding entries
   }
   const int w0 = bx * RT_TILE + wv * 64 * RT_ITEMS;
   const unsigned long long lt = (1ull << lane) - 1ull;
@@ -287,7 +287,7 @@ __device__ __forceinline__ void sh_route_scatter_body(
     int pos = off[o] + rnk[k];
     for (int w = 0; w < wv; ++w) pos += wc[w][o];
     if (pos < C) {
-      send_ids[o * C + pos] = key[k];
+      send_ids[(size_t)o * ostride + pos] = key[k];
       upos[u] = o * C + pos;
     } else {
       upos[u] = -1;
@@ -300,7 +300,7 @@ __global__ void __launch_bounds__(SH_THREADS) sh_route_scatter_kernel(
     const int* __restrict__ sk, int n, int N, int nbits, int C, const int* __restrict__ tcnt, int nt,
     int* __restrict__ sid_incl, int* __restrict__ send_ids, int* __restrict__ upos, int* __restrict__ send_cnt,
     int* __restrict__ num_u, unsigned* __restrict__ err) {
-  sh_route_scatter_body(sk, n, N, nbits, C, tcnt, nt, sid_incl, send_ids, upos, send_cnt, num_u, err, blockIdx.x);
+  sh_route_scatter_body(sk, n, N, nbits, C, tcnt, nt, sid_incl, send_ids, upos, send_cnt, num_u, err, blockIdx.x, C);
 }
 
 // fm_fwd row index of every slot: the received row of its unique id
@@ -320,7 +320,8 @@ struct ShRouteBatch {
   const int* perm;  // their slot positions [n]
   int* tcnt;        // [tiles][N + 1]
   int* sid_incl;
-  int* send_ids;    // [N][C]
+  int* send_ids;    // owner o's block at send_ids + o * ostride (the run's ids travel packed
+                    // [N][G][C]: ONE all-to-all for the whole run)
   int* upos;
   int* send_cnt;
   int* num_u;
@@ -335,18 +336,22 @@ __global__ void __launch_bounds__(SH_THREADS) sh_route_count_run_kernel(const Sh
 
 __global__ void __launch_bounds__(SH_THREADS) sh_route_scatter_run_kernel(const ShRouteBatch* __restrict__ rb, int n,
                                                                          int N, int nbits, int C, int nt,
-                                                                         unsigned* __restrict__ err) {
+                                                                         unsigned* __restrict__ err, int ostride) {
   const ShRouteBatch R = rb[blockIdx.y];
   sh_route_scatter_body(R.sk, n, N, nbits, C, R.tcnt, nt, R.sid_incl, R.send_ids, R.upos, R.send_cnt, R.num_u,
-                        err, blockIdx.x);
+                        err, blockIdx.x, ostride);
 }
 
-__global__ void sh_slot_rows_run_kernel(const ShRouteBatch* __restrict__ rb, int n) {
+// slot -> row map; ld > 0: field-major [F][ld] (the tower gathers through idx_ld): the sorted
+// order scatters each field's writes over one 4*ld-byte span that L2 merges, where the row-major
+// map's stride-F writes each dirtied a line of their own (77 us for a 16-batch run vs ~10)
+__global__ void sh_slot_rows_run_kernel(const ShRouteBatch* __restrict__ rb, int n, int F, int ld) {
   const ShRouteBatch R = rb[blockIdx.y];
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const int r = R.upos[R.sid_incl[i] - 1];
-  R.slot_row[R.perm[i]] = r < 0 ? 0 : r;
+  const int q = R.perm[i];
+  R.slot_row[ld ? (size_t)(q % F) * ld + q / F : (size_t)q] = r < 0 ? 0 : r;
 }
 
 // Owner: rows[e] = {v[K], w, 0, 0, 0} of each requested id (zeros for padding entries)
@@ -525,15 +530,21 @@ HFM_API int hfm_sh_route(const int* sorted_keys, int n, int N, int C, int* tcnt,
   HFM_LAUNCH_CHECK();
 }
 
-// G batches' routing (descriptors rb [G], device): count, scatter, slot rows -- three launches
-HFM_API int hfm_sh_route_run(const ShRouteBatch* rb, int G, int n, int N, int C, unsigned* err, hipStream_t st) {
-  if (!rb || G <= 0 || G > 65535 || N < 1 || N > SH_MAXN || n <= 0 || C <= 0) return (int)hipErrorInvalidValue;
+// G batches' routing (descriptors rb [G], device): count, scatter, slot rows -- three launches;
+// ostride: owner block stride of every batch's send_ids (>= C); F, ld: slot map layout (ld = 0:
+// row-major [n], else field-major [F][ld], ld >= n / F)
+HFM_API int hfm_sh_route_run(const ShRouteBatch* rb, int G, int n, int N, int C, int ostride, int F, int ld,
+                             unsigned* err, hipStream_t st) {
+  if (!rb || G <= 0 || G > 65535 || N < 1 || N > SH_MAXN || n <= 0 || C <= 0 || ostride < C || F <= 0 ||
+      n % F || (ld && ld < n / F))
+    return (int)hipErrorInvalidValue;
   const int nt = hfm_sh_route_tiles(n);
   int nbits = 0;
   while ((1 << nbits) < N) ++nbits;
   hipLaunchKernelGGL(sh_route_count_run_kernel, dim3(nt, G), dim3(SH_THREADS), 0, st, rb, n, N, nbits);
-  hipLaunchKernelGGL(sh_route_scatter_run_kernel, dim3(nt, G), dim3(SH_THREADS), 0, st, rb, n, N, nbits, C, nt, err);
-  hipLaunchKernelGGL(sh_slot_rows_run_kernel, dim3((n + 255) / 256, G), dim3(256), 0, st, rb, n);
+  hipLaunchKernelGGL(sh_route_scatter_run_kernel, dim3(nt, G), dim3(SH_THREADS), 0, st, rb, n, N, nbits, C, nt, err,
+                     ostride);
+  hipLaunchKernelGGL(sh_slot_rows_run_kernel, dim3((n + 255) / 256, G), dim3(256), 0, st, rb, n, F, ld);
   HFM_LAUNCH_CHECK();
 }
 

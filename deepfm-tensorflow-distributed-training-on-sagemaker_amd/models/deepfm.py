@@ -812,6 +812,8 @@ class NativeDeepFM:
             a.idx, a.vals, a.tv, a.tw = idx.data_ptr(), self.vals.data_ptr(), tv.data_ptr(), tw.data_ptr()
             # field-major bound ids (the sharded step gathers through its row-major slot map)
             a.idx_ld = self.M if (self._idx_fm and idx is self.idx) else 0
+            if self.shx is not None and idx is not self.idx:
+                a.idx_ld = self.shx.gather_ld           # run-routed slot maps are field-major
             a.ldv, a.ldw = KN._ld(tv, tw)
             a.fm_bias = pb + 4 * self.dense_segs["fm_bias"].off
             a.F = self.F

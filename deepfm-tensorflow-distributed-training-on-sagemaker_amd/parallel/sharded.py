@@ -143,6 +143,9 @@ class _RouteSet:
         self.recv_ids = torch.full((N * C,), -1, **i32)
         self.send_cnt = torch.zeros(N, **i32)
         self.slot_row = torch.zeros(n, **i32)
+        self.recv_ptr = self.recv_ids.data_ptr()   # requests as the owner kernels read them
+        self.rstride = 0                           # (run sets: a column of the packed run buffer)
+        self.slot_ld = 0                           # slot_row layout: 0 row-major, else [F][slot_ld]
         self.key = None          # host: (ids data_ptr, B) of the batch in this set
         self.stage = None        # host: _ROUTED (kernels done) / _XCHG (ids exchanged) / _SERVED
         # owner side: the request table (csrc/kernels/shard.hip) of this set's batch and its
@@ -211,6 +214,8 @@ class FixedCapacityExchange:
         self.trace = None                    # list: record every issued group (tests)
         self.run_sets = []                   # run-level routing: one set per step of the run
         self._run_descs = {}
+        self._run_ids = None                 # packed [2][N][G][C] ids of a run (send, recv)
+        self.gather_ld = 0                   # slot_row layout of the last fetch (tower idx_ld)
 
     # ------------------------------------------------------------------ host-side plan
     def plan(self, ids: torch.Tensor, B: int, nxt: Optional[torch.Tensor], resident: bool = True,
@@ -243,10 +248,15 @@ class FixedCapacityExchange:
         its gradients with no side branch and no cross-queue join.  ``batches``: [(ids [B*F] as
         the step binds them, B, field-major)], all of one B; needs the per-field sort."""
         sets, n, sort_plan, d = self.route_run_prepare(batches)
-        self._main = torch.cuda.current_stream(self.m.device)
-        self.m._fsort.run_sort(sort_plan)
-        KN.sh_route_run(d, len(sets), n, self.N, self.C, self.err)
-        self._issue([self._ids_op(rs) for rs in sets])                   # G0 of the whole run
+        G = len(sets)
+        m = self.m
+        self._main = torch.cuda.current_stream(m.device)
+        m._fsort.run_sort(sort_plan)
+        KN.sh_route_run(d, G, n, self.N, self.C, self.err, G * self.C, m.F, sets[0].slot_ld)
+        send, recv = self._run_ids[0], self._run_ids[1]
+        # G0 of the whole run: ONE all-to-all of the packed [N][G][C] ids (16 grouped all-to-alls
+        # of [N][C] cost 92 us on the 1-rank proxy, RCCL's per-operation cost)
+        self._issue([(KN.COMM_A2A, send, recv, G * self.C * 4)])
         self._main = None
 
     def route_run_prepare(self, batches):
@@ -260,16 +270,26 @@ class FixedCapacityExchange:
         sets = self.run_sets[:G]
         sort_plan = m._fsort.run_plan([(ids, b, fm, rs.sorted_keys, rs.perm)
                                        for (ids, b, fm), rs in zip(batches, sets)])
-        key = (G, n)
+        T = self.N * G * self.C
+        if self._run_ids is None or self._run_ids.shape[1] < T:
+            self._run_ids = torch.full((2, T), -1, dtype=torch.int32, device=m.device)
+            self._run_descs.clear()
+        ld = m.M if (m.fused and m.gather_fused) else 0     # field-major slot maps for the tower
+        for g, rs in enumerate(sets):
+            rs.recv_ptr = self._run_ids[1].data_ptr() + 4 * g * self.C
+            rs.rstride = G * self.C
+            rs.slot_ld = ld
+        key = (G, n, self._run_ids.data_ptr())
         d = self._run_descs.get(key)
         if d is None:
             from ..ops._lib import ShRouteBatch
             descs = []
-            for rs in sets:
+            for g, rs in enumerate(sets):
                 r = ShRouteBatch()
                 r.sk, r.perm, r.tcnt, r.sid_incl = (rs.sorted_keys.data_ptr(), rs.perm.data_ptr(),
                                                     rs.tcnt.data_ptr(), rs.sid_incl.data_ptr())
-                r.send_ids, r.upos, r.send_cnt = rs.send_ids.data_ptr(), rs.upos.data_ptr(), rs.send_cnt.data_ptr()
+                r.send_ids = self._run_ids[0].data_ptr() + 4 * g * self.C
+                r.upos, r.send_cnt = rs.upos.data_ptr(), rs.send_cnt.data_ptr()
                 r.num_u, r.slot_row = rs.num_u.data_ptr(), rs.slot_row.data_ptr()
                 descs.append(r)
             d = KN.struct_array_to_device(descs, m.device)
@@ -413,10 +433,11 @@ class FixedCapacityExchange:
         rs = self._rs(plan)
         if plan.serve:
             if train:
-                KN.sh_serve(m.K, rs.recv_ids, self.N * self.C, self.N, m.tv, m.tw, rs.rows_out,
-                            C=self.C, step=m.step, table=rs.table)
+                KN.sh_serve(m.K, rs.recv_ptr, self.N * self.C, self.N, m.tv, m.tw, rs.rows_out,
+                            C=self.C, step=m.step, table=rs.table, rstride=rs.rstride)
             else:
-                KN.sh_serve(m.K, rs.recv_ids, self.N * self.C, self.N, m.tv, m.tw, rs.rows_out, C=self.C)
+                KN.sh_serve(m.K, rs.recv_ptr, self.N * self.C, self.N, m.tv, m.tw, rs.rows_out, C=self.C,
+                            rstride=rs.rstride)
         ops = [(KN.COMM_A2A, rs.rows_out, self.rows_in, self.C * self.RW * 4)]
         if train and plan.n1_mode == "xchg":
             ops.append(self._ids_op(self._set(plan, 1)))
@@ -435,6 +456,7 @@ class FixedCapacityExchange:
                 self._served_ev.record(self._serve_stream)
         if train and self._fork_at == "fetch":
             self.fork_next()
+        self.gather_ld = rs.slot_ld
         return rs.slot_row, self.rows_in[:, : m.K], self.rows_in[:, m.K]
 
     def backward(self, plan: ShPlan, B: int, dense=None, join=None, wgfin=None, dense_ar=None):
@@ -472,8 +494,8 @@ class FixedCapacityExchange:
             ops.append(self._ids_op(self._set(plan, 1)))
         self._issue(ops)                                                 # G2
         S = ShApplyArgs()
-        S.recv_ids, S.total, S.N, S.C = rs.recv_ids.data_ptr(), self.N * self.C, self.N, self.C
-        S.rstride = 0
+        S.recv_ids, S.total, S.N, S.C = rs.recv_ptr, self.N * self.C, self.N, self.C
+        S.rstride = rs.rstride
         S.mode = 0 if m.sparse_update == "lazy" else 1      # tags were stamped by the serve
         S.recv_g, S.table = self.recv_g.data_ptr(), rs.table
         S.tv, S.tw = m.tv.data_ptr(), m.tw.data_ptr()
