@@ -27,53 +27,7 @@
 // A bucket larger than C sets err bit 2 (the host raises).
 #include "common.h"
 
-// hash table of the owner's requested rows: key[slot] = {stamp, row}, pos[slot][p] = {stamp, c}
-struct ShTable {
-  unsigned long long* key;  // [slots]
-  unsigned long long* pos;  // [slots][N]
-  unsigned mask;            // slots - 1 (power of two)
-  int pad;
-};
-
-__device__ __forceinline__ unsigned sh_hash(unsigned row) {
-  unsigned h = row * 0x9E3779B1u;
-  return h ^ (h >> 15);
-}
-
-// insert `row` (requested by rank p at position c) for the step `stamp`; returns nothing: the
-// position is recorded in the row's slot.  Stale slots (older stamps) count as empty.
-__device__ __forceinline__ void sh_insert(const ShTable& T, int N, unsigned row, int p, unsigned c,
-                                          unsigned stamp) {
-  const unsigned long long want = ((unsigned long long)stamp << 32) | row;
-  unsigned s = sh_hash(row) & T.mask;
-  for (unsigned probe = 0; probe <= T.mask; ++probe, s = (s + 1) & T.mask) {
-    unsigned long long cur = T.key[s];
-    if (cur != want) {
-      if ((unsigned)(cur >> 32) == stamp) continue;  // taken by another row this step
-      const unsigned long long prev = atomicCAS(T.key + s, cur, want);
-      if (prev != cur && prev != want) {  // lost the slot to another row: re-examine it
-        if ((unsigned)(prev >> 32) == stamp) continue;
-        --probe;
-        s = (s - 1) & T.mask;
-        continue;
-      }
-    }
-    T.pos[(size_t)s * N + p] = ((unsigned long long)stamp << 32) | c;
-    return;
-  }
-}
-
-__device__ __forceinline__ const unsigned long long* sh_find(const ShTable& T, int N, unsigned row,
-                                                             unsigned stamp) {
-  const unsigned long long want = ((unsigned long long)stamp << 32) | row;
-  unsigned s = sh_hash(row) & T.mask;
-  for (unsigned probe = 0; probe <= T.mask; ++probe, s = (s + 1) & T.mask) {
-    const unsigned long long cur = T.key[s];
-    if (cur == want) return T.pos + (size_t)s * N;
-    if ((unsigned)(cur >> 32) != stamp) return nullptr;  // an empty slot ends the probe chain
-  }
-  return nullptr;
-}
+#include "shard_table.h"
 
 namespace {
 constexpr int SH_THREADS = 256;
@@ -361,35 +315,13 @@ __global__ void sh_slot_rows_run_kernel(const ShRouteBatch* __restrict__ rb, int
 // Stamp = counter + stamp_off: 1 when served at the start of its own step; 2 when SERVED AHEAD
 // during the previous step (whose counter is one lower) -- that step's owner update then patches
 // the served rows it changes (sh_owner_apply_elem), so the fetch leaves the critical path.
-// request e = p*C + c of the received ids: [N][C] blocks (rstride == C, or 0 = contiguous), or
-// this rank's column of the all-gathered [N][N][C] requests (base + rank*C, rstride = N*C)
-__device__ __forceinline__ int sh_rid(const int* __restrict__ r, int e, int C, int rstride) {
-  return rstride > C ? r[(size_t)(e / C) * rstride + e % C] : r[e];
-}
-
 template <int K>
 __global__ void sh_serve_kernel(const int* __restrict__ recv_ids, int total, int N, int C, int rstride,
                                 const float* __restrict__ tv, const float* __restrict__ tw, long ldv,
                                 long ldw, float* __restrict__ rows, const int64_t* __restrict__ step,
                                 ShTable T, int stamp_off, int vbf16) {
-  constexpr int LPS = K / 4, RW = K + 4;
-  const int gt = blockIdx.x * blockDim.x + threadIdx.x;
-  const int e = gt / LPS, sub = gt % LPS;
-  if (e >= total) return;
-  const int id = sh_rid(recv_ids, e, C, rstride);
-  f32x4 v = {0.f, 0.f, 0.f, 0.f};
-  float w = 0.f;
-  if (id >= 0) {
-    const size_t row = (size_t)(id / N);
-    v = ld_row4(tv + row * ldv, sub * 4, vbf16);
-    if (sub == 0) {
-      w = tw[row * ldw];
-      if (T.key) sh_insert(T, N, (unsigned)row, e / C, (unsigned)(e % C), (unsigned)(*step + stamp_off));
-    }
-  }
-  float* o = rows + (size_t)e * RW;
-  *reinterpret_cast<f32x4*>(o + sub * 4) = v;
-  if (sub == 0) *reinterpret_cast<f32x4*>(o + K) = f32x4{w, 0.f, 0.f, 0.f};
+  const ShServeArgs A{recv_ids, total, N, C, rstride, tv, tw, ldv, ldw, rows, step, T, stamp_off, vbf16};
+  sh_serve_elem<K>(A, blockIdx.x * blockDim.x + threadIdx.x);
 }
 
 __global__ void sh_owner_tag_kernel(const int* __restrict__ recv_ids, int total, int N, int C, int rstride,

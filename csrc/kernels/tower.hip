@@ -22,6 +22,7 @@
 // Dropout masks: counter hash, flat index (global row) * Npad + col, identical to mlp.hip.
 #include "common.h"
 #include "mma32.h"
+#include "shard_table.h"
 
 constexpr int TW_MAXL = 8;
 constexpr int TW_ROWS = 32;
@@ -83,6 +84,10 @@ struct TowerArgs {
   unsigned id_lim;                // > 0: gathered row ids clamped to [0, id_lim) (a bad id never
                                   // reads out of bounds; the slot sort flags it for the host)
   int vbf16;                      // table v rows are bf16 (mixed-precision embeddings)
+  // run-routed row-sharded step: serve_wgs workgroups AFTER the tower's serve the NEXT batch's
+  // rows ahead (shard_table.h; the owner update of this step patches the rows it changes)
+  int serve_wgs;
+  ShServeArgs sv;
 };
 
 // fp8 variant of mma32 (16x16x32 fp8 MFMA; same fragment map as bf16 with 8 one-byte elements
@@ -272,6 +277,13 @@ __global__ void __launch_bounds__(256) tower_kernel(TowerArgs a) {
   __shared__ float s_yfm[TW_ROWS];  // gather: y_b + y_w + y_v per sample
   __shared__ float s_dq0[TW_ROWS];  // gather + fp8: dequant factors of the E rows
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  if constexpr (KE > 0) {
+    const int sb = (int)blockIdx.x - a.M / TW_ROWS;
+    if (sb >= 0) {  // a serve workgroup (run-routed sharded step)
+      sh_serve_elem<KE>(a.sv, sb * 256 + tid);
+      return;
+    }
+  }
   const int row0 = blockIdx.x * TW_ROWS;
   const int cr = (lane >> 4) * 4, cc = lane & 15;
   const uint32_t step = (uint32_t)(*a.step);
@@ -486,7 +498,7 @@ __global__ void __launch_bounds__(256) tower_kernel(TowerArgs a) {
 
 template <bool FP8>
 static int tower_launch(const TowerArgs& a, int KE, hipStream_t st) {
-  const dim3 g(a.M / TW_ROWS), blk(256);
+  const dim3 g(a.M / TW_ROWS + (KE > 0 ? a.serve_wgs : 0)), blk(256);
   switch (KE) {
     case 0: hipLaunchKernelGGL((tower_kernel<FP8, 0, 4, 2>), g, blk, a.lds_bytes, st, a); break;
     case 4: hipLaunchKernelGGL((tower_kernel<FP8, 4, 4, 2>), g, blk, a.lds_bytes, st, a); break;
@@ -506,6 +518,10 @@ HFM_API int hfm_tower(const TowerArgs* ap, int KE, hipStream_t st) {
     if (a.Np[i] % 32 || a.Np[i] <= 0) return (int)hipErrorInvalidValue;
   if (a.Np[a.nl - 1] % 8) return (int)hipErrorInvalidValue;
   if (a.lds_bytes > 160 * 1024 - 1024) return (int)hipErrorInvalidValue;
+  if (a.serve_wgs < 0 || (a.serve_wgs && (!KE || !a.train || !a.sv.recv_ids || !a.sv.rows || !a.sv.step ||
+                                          !a.sv.T.key || a.sv.C <= 0 || a.sv.stamp_off != 2 ||
+                                          (long)a.serve_wgs * 256 < (long)a.sv.total * (KE / 4))))
+    return (int)hipErrorInvalidValue;
   if (KE) {
     if (a.fp8)  // H_i is re-quantized into the fp8 E tile (32 x (K0p + 16) bytes)
       for (int i = 0; i + 1 < a.nl; ++i)

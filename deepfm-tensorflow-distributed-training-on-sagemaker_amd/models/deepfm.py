@@ -368,6 +368,7 @@ class NativeDeepFM:
         self._side = None
         self._side_next = None
         self._run_j = None          # run-level sort: this step's index in the run (train_steps)
+        self._run_n = 0             # run-level sort / routing: steps in the run being captured
         self._run_ss = []           # run-level sort: (keys, perm) per step of the run
         self._next_sort_ids = None
         self._next_fm = False      # the declared next batch's ids are field-major
@@ -851,7 +852,12 @@ class NativeDeepFM:
         ``after_fm``: hook called once the FM forward is enqueued."""
         if self.fused and self.gather_fused:
             idx, tv, tw = self._fm_inputs(B, train=True)
-            KN.tower(self._tower_args(B, train=True, gather=(idx, tv, tw)), KE=self.K)
+            ta = self._tower_args(B, train=True, gather=(idx, tv, tw))
+            if self.shx is not None and self.shx.tower_serve is not None:
+                # run-routed step: the next step's rows served by extra tower workgroups
+                ta.sv, self.shx.tower_serve = self.shx.tower_serve, None
+                ta.serve_wgs = -(-ta.sv.total * (self.K // 4) // 256)
+            KN.tower(ta, KE=self.K)
             if after_fm is not None:
                 after_fm()
             if not defer_wgrad:
@@ -1657,7 +1663,7 @@ class NativeDeepFM:
             key = key + ("tf1",) + self._tf1_plan
         if self.shx is not None and self._run_j is not None:
             # run-level routing: routed and its ids exchanged at the start of the run
-            self._shx_plan = self.shx.run_plan(self._run_j)
+            self._shx_plan = self.shx.run_plan(self._run_j, self._run_n)
             key = key + tuple(self._shx_plan)
         elif self.shx is not None:
             nxt = self._flat_ids(next_ids, nxt_fm) if (nxt_ok and _SHARD_PIPELINE) else None
@@ -1868,6 +1874,7 @@ class NativeDeepFM:
                     self.shx.route_run(rlist)
                 else:
                     self._fsort_next.run_sort(rplan)
+                self._run_n = G
                 for j, (ids, vals, labels) in enumerate(batches):
                     self._run_j = j
                     try:

@@ -122,6 +122,13 @@ class ShTable(C.Structure):
     _fields_ = [("key", c_void_p), ("pos", c_void_p), ("mask", C.c_uint32), ("pad", c_int)]
 
 
+class ShServeArgs(C.Structure):
+    """shard_table.h ShServeArgs: a row serve (here: the next batch's, inside the tower launch)."""
+    _fields_ = [("recv_ids", c_void_p), ("total", c_int), ("N", c_int), ("C", c_int), ("rstride", c_int),
+                ("tv", c_void_p), ("tw", c_void_p), ("ldv", c_long), ("ldw", c_long), ("rows", c_void_p),
+                ("step", c_void_p), ("T", ShTable), ("stamp_off", c_int), ("vbf16", c_int)]
+
+
 class ShApplyArgs(C.Structure):
     _fields_ = [("recv_ids", c_void_p), ("total", c_int), ("N", c_int), ("C", c_int), ("mode", c_int),
                 ("rstride", c_int), ("recv_g", c_void_p), ("table", ShTable), ("tv", c_void_p), ("tw", c_void_p),
@@ -171,7 +178,7 @@ class TowerArgs(C.Structure):
                 ("idx", c_void_p), ("vals", c_void_p), ("tv", c_void_p), ("tw", c_void_p),
                 ("ldv", c_long), ("ldw", c_long), ("fm_bias", c_void_p), ("F", c_int),
                 ("x_off", c_int), ("x8_off", c_int), ("S", c_void_p), ("Et", c_void_p), ("idx_ld", c_int),
-                ("id_lim", c_uint32), ("vbf16", c_int)]
+                ("id_lim", c_uint32), ("vbf16", c_int), ("serve_wgs", c_int), ("sv", ShServeArgs)]
 
 
 class CommOp(C.Structure):

@@ -216,6 +216,7 @@ class FixedCapacityExchange:
         self._run_descs = {}
         self._run_ids = None                 # packed [2][N][G][C] ids of a run (send, recv)
         self.gather_ld = 0                   # slot_row layout of the last fetch (tower idx_ld)
+        self.tower_serve = None              # ShServeArgs the next tower launch serves (run mode)
 
     # ------------------------------------------------------------------ host-side plan
     def plan(self, ids: torch.Tensor, B: int, nxt: Optional[torch.Tensor], resident: bool = True,
@@ -296,10 +297,25 @@ class FixedCapacityExchange:
             self._run_descs[key] = d
         return sets, n, sort_plan, d
 
-    def run_plan(self, j: int) -> ShPlan:
-        """Step j of a run routed by ``route_run``: rows served at the step start (inline), then
-        the rows all-to-all (G1) and the gradient group (G2) -- nothing routed or forked."""
-        return ShPlan(j, False, False, True, None, None, False, None, True)
+    def run_plan(self, j: int, G: int) -> ShPlan:
+        """Step j of a G-step run routed by ``route_run``: G1 (rows) and G2 (gradients) only --
+        nothing routed, no ids exchanged, nothing forked.  The run's first step serves its rows
+        at its start; every step then serves the NEXT step's rows inside its own tower launch
+        (``tower_serve``; lazy rows, fused gather tower: its owner update patches what it
+        changes), so later steps start at their row all-to-all."""
+        ahead = self.m.sparse_update == "lazy" and self.m.fused and self.m.gather_fused
+        return ShPlan(j, False, False, j == 0 or not ahead, None, None, ahead and j + 1 < G, None, True)
+
+    def _serve_args(self, rs: "_RouteSet", ahead: bool):
+        from ..ops._lib import ShServeArgs
+        m = self.m
+        a = ShServeArgs()
+        a.recv_ids, a.total, a.N, a.C, a.rstride = rs.recv_ptr, self.N * self.C, self.N, self.C, rs.rstride
+        a.tv, a.tw = m.tv.data_ptr(), m.tw.data_ptr()
+        a.ldv, a.ldw = KN._ld(m.tv, m.tw)
+        a.rows, a.step, a.T = rs.rows_out.data_ptr(), m.step.data_ptr(), rs.table
+        a.stamp_off, a.vbf16 = (2 if ahead else 1), KN._bf(m.tv)
+        return a
 
     def _rs(self, plan: ShPlan) -> _RouteSet:
         return self.run_sets[plan.c] if plan.run else self.sets[plan.c]
@@ -442,7 +458,10 @@ class FixedCapacityExchange:
         if train and plan.n1_mode == "xchg":
             ops.append(self._ids_op(self._set(plan, 1)))
         self._issue(ops)                                                 # G1
-        if train and plan.serve_ahead:
+        if train and plan.serve_ahead and plan.run:
+            # the next run step's rows, served by extra workgroups of this step's tower launch
+            self.tower_serve = self._serve_args(self.run_sets[plan.c + 1], ahead=True)
+        elif train and plan.serve_ahead:
             # the next batch's rows as of now (stamped step + 2); this step's owner update
             # patches the rows it changes (it waits for this branch first)
             nx = self._set(plan, 1)
@@ -506,7 +525,11 @@ class FixedCapacityExchange:
         S.h = m.h_sparse
         S.step = m.step.data_ptr()
         S.vbf16 = 1 if m.emb_bf16 else 0
-        if self._served_ev is not None:
+        if plan.run and plan.serve_ahead:
+            # the next run step's rows were served in this step's tower launch: patch what changes
+            nx = self.run_sets[plan.c + 1]
+            S.next, S.next_rows = nx.table, nx.rows_out.data_ptr()
+        elif self._served_ev is not None:
             # the next batch's rows were served ahead: wait for them, patch what changes
             self._main.wait_event(self._served_ev)
             nx = self._set(plan, 1)
