@@ -127,7 +127,11 @@ __device__ __forceinline__ void fs2_sort_item(const FsJob& J, int item, unsigned
   }
   if (__any(bad) && lane == 0) atomicOr(J.err, 1u);
   unsigned short* wh = wc + wv * 256;
+#ifdef FS2_DBG_PASSES  // timing harness only (tools/fsbench/fs2_bench.hip): cap the LSD passes
+  const int passes = min((bits + 7) >> 3, FS2_DBG_PASSES);
+#else
   const int passes = (bits + 7) >> 3;
+#endif
   for (int pass = 0; pass < passes; ++pass) {
     const int shift = pass * 8;
     __syncthreads();  // the key arrays are complete (initial fill / previous scatter)
