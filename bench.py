@@ -34,13 +34,15 @@ METRIC = ("samples/sec (whole node) + eval AUC, Criteo-1TB-shape DeepFM at 1/2/4
 # fewer moving parts.  Every rung is the same full training step (same model, optimizer, data),
 # and in EVERY rung all collectives of a step run on one communicator, grouped, on the step's
 # main stream in a fixed order (parallel/sharded.py) -- no rung has side-stream collectives.
-# A capture failure is the likeliest multi-GPU surprise, so the same step launched eagerly comes
-# second; the last rung drops the routing prefetch and the fused dense exchange (dense all-reduce
-# in the gradient group, 7-launch routing).
+# The first rung routes every batch of a captured run at its start (one grouped ids all-to-all,
+# then per step G1 + G2 on one queue: parallel/sharded.py "Run-level routing"); the second is the
+# per-step pipelined routing of round 2 (side-stream routing kernels, serve ahead), also
+# captured; the last launches eagerly without the routing prefetch and without the fused dense
+# exchange (dense all-reduce in the gradient group, 7-launch routing).
 _PLAIN_EXCHANGE = {"HIPFM_SH_XFUSE": "0", "HIPFM_SH_APPLY_DENSE": "0", "HIPFM_SH_ROUTE2": "0"}
 LADDER = [
-    ("graph+prefetch", {}),                                  # HIP graphs, next-batch routing prefetch
-    ("eager+prefetch", {"HIPFM_BENCH_NO_GRAPH": "1"}),       # same step, launched eagerly
+    ("graph+run-routing", {}),                               # HIP graphs, run-level routing
+    ("graph+prefetch", {"HIPFM_RUN_SORT": "0"}),             # HIP graphs, next-batch routing prefetch
     ("eager", {"HIPFM_BENCH_NO_GRAPH": "1", "HIPFM_SHARD_PIPELINE": "0", **_PLAIN_EXCHANGE}),
 ]
 # hang detection: a rung's child must write its first progress mark within FIRST_S (the parent
@@ -377,7 +379,8 @@ def main():
                 "hip_graph": use_graph,
                 "timed_graph_captures": timed_captures,
                 "graph_steps": G if use_graph else 0,
-                "exec": os.environ.get("HIPFM_BENCH_RUNG", "graph+prefetch" if use_graph else "eager"),
+                "exec": os.environ.get("HIPFM_BENCH_RUNG", ("graph+run-sort" if os.environ.get("HIPFM_RUN_SORT", "1") == "1"
+                                                              else "graph+prefetch") if use_graph else "eager"),
                 "mlp_dtype": args.mlp_dtype + (" fwd GEMMs, bf16 backward" if args.mlp_dtype == "fp8" else ""),
                 "emb_dtype": args.emb_dtype + (" rows + slots (stochastic rounding), fp32 math"
                                                if args.emb_dtype == "bf16" else " tables + slots"),

@@ -48,9 +48,10 @@ KNOBS: Dict[str, Knob] = {
     "HIPFM_WGFIN": Knob("1", "variant", "weight gradients + combine + dense optimizer in one launch "
                         "(0: wgrad_group + finalize)"),
     "HIPFM_SFWG": Knob("1", "variant", "wgfin work inside the sparse backward's launch"),
-    "HIPFM_RUN_SORT": Knob("1", "variant", "one GPU, multi-step graphs: every batch of the run sorted "
-                           "at the graph's start (0: the next batch's sort on a side branch of each "
-                           "step, the oracle)"),
+    "HIPFM_RUN_SORT": Knob("1", "variant", "multi-step graphs: every batch of the run sorted (one GPU) "
+                           "or sorted + routed + its ids exchanged (row-sharded) at the graph's start "
+                           "(0: the next batch's sort / routing on a side branch of each step, the "
+                           "oracle and the bench ladder's second rung)"),
     "HIPFM_SHX_FORK": Knob("start", "variant", "row-sharded step: fork point of the next batch's "
                            "routing branch (start | tower)"),
     "HIPFM_SH_APPLY_DENSE": Knob("1", "variant", "row-sharded step: dense optimizer in the owner "

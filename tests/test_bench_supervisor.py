@@ -35,11 +35,11 @@ def _run(fake, hang_s="4", first_s="6"):
 
 
 @pytest.mark.parametrize("fake,rung", [
-    ("none:0:fail", "graph+prefetch"),
-    ("graph+prefetch:1:fail", "eager+prefetch"),
-    ("graph+prefetch:1:stall", "eager+prefetch"),
-    ("graph+prefetch:0:hang,eager+prefetch:1:stall", "eager"),
-    ("graph+prefetch:1:fail,eager+prefetch:0:fail", "eager"),
+    ("none:0:fail", "graph+run-routing"),
+    ("graph+run-routing:1:fail", "graph+prefetch"),
+    ("graph+run-routing:1:stall", "graph+prefetch"),
+    ("graph+run-routing:0:hang,graph+prefetch:1:stall", "eager"),
+    ("graph+run-routing:1:fail,graph+prefetch:0:fail", "eager"),
 ])
 def test_supervisor_falls_back_and_prints_one_line(fake, rung):
     rc, lines, _ = _run(fake)
@@ -76,5 +76,5 @@ def test_plain_bench_gpus_n_spawns_n_ranks(n):
 
 
 def test_supervisor_fails_when_every_rung_fails():
-    rc, lines, _ = _run("graph+prefetch:0:fail,eager+prefetch:0:fail,eager:1:fail")
+    rc, lines, _ = _run("graph+run-routing:0:fail,graph+prefetch:0:fail,eager:1:fail")
     assert rc != 0 and not lines
