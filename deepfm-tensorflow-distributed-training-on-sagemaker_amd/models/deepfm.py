@@ -1752,12 +1752,13 @@ class NativeDeepFM:
 
         def nxt_of(i):
             return (seq[i + 1] if i + 1 < len(seq) else None, seq[i + 2] if i + 2 < len(seq) else None)
+        if all(self._resident(*b) for b in batches) and (self._run_sort_ok(batches) or
+                                                          self._run_route_ok(batches)):
+            return self._train_run_sorted(batches)
         if not all(self._resident(*b) for b in batches) or not (self.comm is None or self.comm.graph_safe):
             for i, (ids, vals, labels) in enumerate(batches):
                 self.train_step(ids, vals, labels, use_graph=True, next_ids=nxt_of(i))
             return len(batches)
-        if self._run_sort_ok(batches) or self._run_route_ok(batches):
-            return self._train_run_sorted(batches)
         st0 = self._plan_state()
         # a run seen before from the same plan state replays its graph without re-planning
         # each step in Python (the per-step bind costs tens of us of host time, which a
@@ -1826,8 +1827,7 @@ class NativeDeepFM:
     def _run_route_ok(self, batches) -> bool:
         """Run-level routing (parallel/sharded.py ``route_run``): the row-sharded step over
         resident batches of one size, with the per-field sort and graph-safe collectives."""
-        if not (_RUN_SORT and len(batches) > 1 and self.shx is not None and self._fsort is not None and
-                self.comm is not None and self.comm.graph_safe):
+        if not (_RUN_SORT and len(batches) > 1 and self.shx is not None and self._fsort is not None):
             return False
         B = batches[0][0].shape[0]
         return (all(b[0].shape[0] == B for b in batches) and self.uses_field_sort(B) and
@@ -1856,6 +1856,27 @@ class NativeDeepFM:
             sets = self._run_sets(G)
             rplan = self._fsort_next.run_plan(
                 [(self._flat_ids(b[0], fm), b[0].shape[0], fm, k, p) for b, fm, (k, p) in zip(batches, fms, sets)])
+        def enqueue():
+            if routed:
+                self.shx.route_run(rlist)
+            else:
+                self._fsort_next.run_sort(rplan)
+            self._run_n = G
+            for j, (ids, vals, labels) in enumerate(batches):
+                self._run_j = j
+                try:
+                    B, direct, _ = self._bind_step(ids, vals, labels)
+                    self.train_step_enqueue(B)
+                    self._commit_step(B, direct)
+                finally:
+                    self._run_j = None
+
+        if self.comm is not None and not self.comm.graph_safe:
+            # collectives that cannot be captured (the in-process emulation engine of the tests):
+            # the same run, launched eagerly
+            enqueue()
+            self._ss_key = [None, None]
+            return G
         mkey = ("runsort",) + tuple((b[0].data_ptr(), b[0].stride(), b[1].data_ptr(), b[2].data_ptr(),
                                      b[0].shape[0]) for b in batches)
         g = self._graphs.get(mkey)
@@ -1870,19 +1891,7 @@ class NativeDeepFM:
             g = torch.cuda.CUDAGraph()
             h0 = self._host_step
             with graph_capture(g):
-                if routed:
-                    self.shx.route_run(rlist)
-                else:
-                    self._fsort_next.run_sort(rplan)
-                self._run_n = G
-                for j, (ids, vals, labels) in enumerate(batches):
-                    self._run_j = j
-                    try:
-                        B, direct, _ = self._bind_step(ids, vals, labels)
-                        self.train_step_enqueue(B)
-                        self._commit_step(B, direct)
-                    finally:
-                        self._run_j = None
+                enqueue()
             self._host_step = h0
             if len(self._graphs) >= self.max_graphs:
                 self._graphs.pop(next(iter(self._graphs)))

@@ -186,6 +186,105 @@ def test_sharded_exchange_matches_global_batch(N, opt, update, prefetch):
     assert models[0].comm.bytes_sent > 0
 
 
+def _run_ranks_steps(models, batches):
+    """Each emulated rank trains its batches as ONE run (train_steps: run-level routing)."""
+    errs = []
+
+    def body(r):
+        try:
+            torch.cuda.set_device(0)
+            s = torch.cuda.Stream()
+            with torch.cuda.stream(s):
+                models[r].train_steps(batches[r])
+            s.synchronize()
+        except BaseException as e:
+            errs.append(e)
+            for m in models:
+                m.comm.engine.hub.bar.abort()
+    th = [threading.Thread(target=body, args=(r,)) for r in range(len(models))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    if errs:
+        raise errs[0]
+
+
+@pytest.mark.parametrize("N,update,steps", [(2, "lazy", 3), (4, "lazy", 3), (3, "tf1_dense", 3), (4, "lazy", 5),
+                                            (3, "lazy", 4)])
+def test_run_routing_matches_global_batch(N, update, steps):
+    """Run-level routing at N > 1 (emulated ranks, real data movement between them): every batch
+    of the run routed and its ids exchanged in ONE packed all-to-all at the start, each step then
+    G1 (rows) + G2 (gradients + dense), the next step's rows served inside the tower launch and
+    patched by the owner update.  Bitwise equal to the per-step pipelined routing on the same
+    emulated ranks; close to the global-batch model (the per-step test's tolerance: 3 steps --
+    longer runs of Adam amplify fp32 summation-order differences on near-zero gradients); every
+    rank issues the same collective sequence."""
+    from hipfm.ops import kernels as KN
+    import hipfm.models.deepfm as D
+    synth = make_synth("criteo_kaggle", seed=4)
+    F, K, layers, keep, B = synth.F, 8, [64, 32], [1.0, 1.0], 512
+    V = synth.feature_size
+    params = init_params(V, F, K, layers, False, seed=7)
+    lr = 1e-3
+    data = [synth.batch(N * B, step=s, device=DEV, id_dtype=torch.int32) for s in range(steps)]
+    batches = [[(ids[r * B:(r + 1) * B].contiguous(), vals[r * B:(r + 1) * B].contiguous(),
+                 lab[r * B:(r + 1) * B].contiguous()) for ids, vals, lab in data] for r in range(N)]
+    outs = []
+    old = D._RUN_SORT
+    try:
+        for run in (True, False):
+            D._RUN_SORT = run
+            hub = _Hub(N)
+            models = []
+            for r in range(N):
+                m = NativeDeepFM(V, F, K, layers, keep, sparse_update=update, learning_rate=lr, batch_size=B,
+                                 device=DEV, init=False, comm=MeshComm(hub, r), field_ranges=synth.field_ranges())
+                m.load_tf_params(params)
+                m.shx.trace = []
+                models.append(m)
+            if run:
+                _run_ranks_steps(models, batches)
+            else:
+                _run_ranks(models, batches, prefetch=2)
+            torch.cuda.synchronize()
+            for m in models:
+                m.check_errors()
+                assert torch.equal(m.p, models[0].p)
+                assert len(m.shx.run_sets) == (steps if run else 0)
+            outs.append(models)
+    finally:
+        D._RUN_SORT = old
+    for a, b in zip(*outs):                               # run routing == pipelined, bitwise
+        assert torch.equal(a.tv, b.tv) and torch.equal(a.tw, b.tw) and torch.equal(a.p, b.p)
+    models = outs[0]
+    if steps == 3:
+        ref = NativeDeepFM(V, F, K, layers, keep, sparse_update=update, learning_rate=lr * N,
+                           batch_size=N * B, device=DEV, init=False, field_ranges=synth.field_ranges())
+        ref.load_tf_params(params)
+        for ids, vals, lab in data:
+            ref.train_step(ids, vals, lab)
+        full_v, full_w = torch.zeros_like(ref.tv), torch.zeros_like(ref.tw)
+        for r, m in enumerate(models):
+            rows = full_v[r::N].shape[0]
+            full_v[r::N] = m.tv[:rows]
+            full_w[r::N] = m.tw[:rows]
+        scale = ref.tv.abs().max().item()
+        assert (full_v - ref.tv).abs().max().item() <= 2e-5 * scale
+        assert (full_w - ref.tw).abs().max().item() <= 2e-5 * max(1.0, ref.tw.abs().max().item())
+        assert (models[0].p - ref.p).abs().max().item() <= 2e-5 * ref.p.abs().max().item()
+    traces = [m.shx.trace for m in models]
+    for t in traces[1:]:
+        assert t == traces[0]
+    C, RW = models[0].shx.C, models[0].shx.RW
+    t = traces[0]
+    assert t[0] == ((KN.COMM_A2A, steps * C * 4),)               # the run's ids, one all-to-all
+    assert len(t) == 1 + 2 * steps
+    for j in range(steps):
+        assert t[1 + 2 * j] == ((KN.COMM_A2A, C * RW * 4),)       # G1: rows only
+        assert t[2 + 2 * j][0] == (KN.COMM_A2A, C * RW * 4)       # G2: gradient rows first
+
+
 @pytest.mark.parametrize("update,depth", [("lazy", 1), ("tf1_dense", 1), ("lazy", 2)])
 def test_collective_sequence_identical_across_ranks(update, depth):
     """Deadlock freedom by construction (parallel/sharded.py): every collective of a step is a
