@@ -221,3 +221,43 @@ def test_estimator_calibrates_exchange_capacity(group, tmp_path, sharded):
     torch.cuda.synchronize()
     m.check_errors()
     assert est.global_step == 2 * len(pipe._cached)
+
+
+@pytest.mark.parametrize("mode", ["fp8", "emb_bf16", "batch_norm", "tf1_dense_momentum", "replicated_fp8"])
+def test_exchange_mode_matrix(group, mode):
+    """the mode combinations the executor supports on the exchange path, each on
+    the 1-rank RCCL group (force_exchange: the complete multi-GPU step, collectives included)
+    against the local step over multi-step graphs: fp8 MLP x row-sharded, bf16 embeddings x
+    row-sharded, batch norm x row-sharded (per-layer tower), tf1_dense x Momentum x row-sharded
+    graphs, fp8 x replicated-table DP."""
+    synth = make_synth("total:6000", seed=43)
+    F, K, layers, keep = synth.F, 8, [64, 32], [0.8, 0.8]
+    V = synth.feature_size
+    params = init_params(V, F, K, layers, mode == "batch_norm", seed=11)
+    kw = dict(sparse_update="lazy", batch_size=512, device="cuda", init=False,
+              field_ranges=synth.field_ranges())
+    sharded = True
+    if mode in ("fp8", "replicated_fp8"):
+        kw["mlp_dtype"] = "fp8"
+        sharded = mode == "fp8"
+    elif mode == "emb_bf16":
+        kw["emb_dtype"] = "bf16"
+    elif mode == "batch_norm":
+        kw["batch_norm"] = True
+    else:
+        kw.update(sparse_update="tf1_dense", optimizer="Momentum")
+    a = NativeDeepFM(V, F, K, layers, keep, **kw)
+    b = NativeDeepFM(V, F, K, layers, keep, comm=Comm(sharded=sharded, force_exchange=True), **kw)
+    a.load_tf_params(params)
+    b.load_tf_params(params)
+    assert b.exchange
+    pool = [synth.batch(512, step=s, device="cuda", id_dtype=torch.int32) for s in range(4)]
+    for _ in range(2):
+        a.train_steps(pool)
+        b.train_steps(pool)
+    torch.cuda.synchronize()
+    b.check_errors()
+    assert a.global_step() == b.global_step() == 8
+    tol = 1e-6 if mode != "emb_bf16" else 2e-3
+    assert torch.allclose(a.tv.float(), b.tv.float(), atol=tol) and torch.allclose(a.tw, b.tw, atol=1e-6)
+    assert torch.allclose(a.p, b.p, atol=1e-6)
