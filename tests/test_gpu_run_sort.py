@@ -65,9 +65,11 @@ def test_run_sort_flags_out_of_range_ids():
     assert int(fs.err.item()) != 0
 
 
-@pytest.mark.parametrize("B,mlp_dtype,emb_dtype", [(16384, "bf16", "fp32"), (1024, "bf16", "fp32"),
-                                                   (6000, "fp8", "bf16")])
-def test_run_sort_training_bitwise_equals_side_stream(monkeypatch, B, mlp_dtype, emb_dtype):
+@pytest.mark.parametrize("B,mlp_dtype,emb_dtype,update", [(16384, "bf16", "fp32", "lazy"), (1024, "bf16", "fp32", "lazy"),
+                                                          (6000, "fp8", "bf16", "lazy"),
+                                                          (16384, "bf16", "fp32", "tf1_dense"),
+                                                          (8192, "bf16", "fp32", "tf1_dense")])
+def test_run_sort_training_bitwise_equals_side_stream(monkeypatch, B, mlp_dtype, emb_dtype, update):
     """Multi-step graphs with the run-level sort give bitwise the parameters, slots and step
     counter of multi-step graphs with the per-step side-stream sort and of single steps."""
     synth = make_synth("criteo_kaggle", seed=32)
@@ -78,7 +80,7 @@ def test_run_sort_training_bitwise_equals_side_stream(monkeypatch, B, mlp_dtype,
     for run, multi in ((True, True), (False, True), (False, False)):
         monkeypatch.setattr(D, "_RUN_SORT", run)
         m = NativeDeepFM(synth.feature_size, synth.F, K, layers, [0.5] * 3, batch_size=B, device=DEV,
-                         init=False, sparse_update="lazy", mlp_dtype=mlp_dtype, emb_dtype=emb_dtype,
+                         init=False, sparse_update=update, mlp_dtype=mlp_dtype, emb_dtype=emb_dtype,
                          field_ranges=synth.field_ranges())
         m.load_tf_params(params)
         if multi:
@@ -92,6 +94,8 @@ def test_run_sort_training_bitwise_equals_side_stream(monkeypatch, B, mlp_dtype,
         torch.cuda.synchronize()
         m.check_errors()
         assert m.global_step() == 12
+        if run and multi:
+            assert m._run_sort_ok(pool[:2])            # the run path ran (tf1_dense: merged sweep)
         out.append([m.tv.clone(), m.tw.clone(), m.p.clone(), m.step.clone()] +
                    [s.clone() for s in m.sv if s.numel()])
         del m
