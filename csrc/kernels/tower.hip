@@ -88,7 +88,14 @@ struct TowerArgs {
   // rows ahead (shard_table.h; the owner update of this step patches the rows it changes)
   int serve_wgs;
   ShServeArgs sv;
+  // tf1_dense run-sorted step: stamp_wgs workgroups after those flag this batch's rows for the
+  // sparse launch's merged sweep (stamp_flags[key / stamp_div] = 1 per run of the sorted keys)
+  int stamp_wgs, stamp_n, stamp_div;
+  const int* stamp_keys;
+  unsigned char* stamp_flags;
 };
+
+constexpr int TW_STAMP_EPT = 16;  // sorted keys per thread of a stamp workgroup
 
 // fp8 variant of mma32 (16x16x32 fp8 MFMA; same fragment map as bf16 with 8 one-byte elements
 // per lane): A and B are e4m3 rows in global memory (row strides in bytes).
@@ -279,8 +286,20 @@ __global__ void __launch_bounds__(256) tower_kernel(TowerArgs a) {
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   if constexpr (KE > 0) {
     const int sb = (int)blockIdx.x - a.M / TW_ROWS;
-    if (sb >= 0) {  // a serve workgroup (run-routed sharded step)
-      sh_serve_elem<KE>(a.sv, sb * 256 + tid);
+    if (sb >= 0) {
+      if (sb < a.serve_wgs) {  // a serve workgroup (run-routed sharded step)
+        sh_serve_elem<KE>(a.sv, sb * 256 + tid);
+        return;
+      }
+      const int i0 = (sb - a.serve_wgs) * 256 * TW_STAMP_EPT + tid;  // a stamp workgroup
+#pragma unroll
+      for (int k = 0; k < TW_STAMP_EPT; ++k) {
+        const int i = i0 + k * 256;
+        if (i < a.stamp_n) {
+          const int key = a.stamp_keys[i];
+          if (i == 0 || a.stamp_keys[i - 1] != key) a.stamp_flags[key / a.stamp_div] = 1;
+        }
+      }
       return;
     }
   }
@@ -498,7 +517,7 @@ __global__ void __launch_bounds__(256) tower_kernel(TowerArgs a) {
 
 template <bool FP8>
 static int tower_launch(const TowerArgs& a, int KE, hipStream_t st) {
-  const dim3 g(a.M / TW_ROWS + (KE > 0 ? a.serve_wgs : 0)), blk(256);
+  const dim3 g(a.M / TW_ROWS + (KE > 0 ? a.serve_wgs + a.stamp_wgs : 0)), blk(256);
   switch (KE) {
     case 0: hipLaunchKernelGGL((tower_kernel<FP8, 0, 4, 2>), g, blk, a.lds_bytes, st, a); break;
     case 4: hipLaunchKernelGGL((tower_kernel<FP8, 4, 4, 2>), g, blk, a.lds_bytes, st, a); break;
@@ -511,6 +530,8 @@ static int tower_launch(const TowerArgs& a, int KE, hipStream_t st) {
 }
 
 // KE: embedding size of the fused gather (4, 8, 16 or 32), or 0 when E comes from fm_fwd (global)
+HFM_API int hfm_tower_stamp_rows_per_wg() { return 256 * TW_STAMP_EPT; }
+
 HFM_API int hfm_tower(const TowerArgs* ap, int KE, hipStream_t st) {
   const TowerArgs& a = *ap;
   if (a.M % TW_ROWS || a.nl < 1 || a.nl > TW_MAXL || a.K0p % 32) return (int)hipErrorInvalidValue;
@@ -521,6 +542,9 @@ HFM_API int hfm_tower(const TowerArgs* ap, int KE, hipStream_t st) {
   if (a.serve_wgs < 0 || (a.serve_wgs && (!KE || !a.train || !a.sv.recv_ids || !a.sv.rows || !a.sv.step ||
                                           !a.sv.T.key || a.sv.C <= 0 || a.sv.stamp_off != 2 ||
                                           (long)a.serve_wgs * 256 < (long)a.sv.total * (KE / 4))))
+    return (int)hipErrorInvalidValue;
+  if (a.stamp_wgs < 0 || (a.stamp_wgs && (!KE || !a.train || !a.stamp_keys || !a.stamp_flags || a.stamp_div <= 0 ||
+                                          (long)a.stamp_wgs * 256 * TW_STAMP_EPT < a.stamp_n)))
     return (int)hipErrorInvalidValue;
   if (KE) {
     if (a.fp8)  // H_i is re-quantized into the fp8 E tile (32 x (K0p + 16) bytes)

@@ -370,6 +370,7 @@ class NativeDeepFM(NativeStateMixin):
         self._side_next = None
         self._run_j = None          # run-level sort: this step's index in the run (train_steps)
         self._run_n = 0             # run-level sort / routing: steps in the run being captured
+        self._tower_stamp = None    # tf1_dense run step: (keys, n, flags) the tower launch stamps
         self._run_ss = []           # run-level sort: (keys, perm) per step of the run
         self._next_sort_ids = None
         self._next_fm = False      # the declared next batch's ids are field-major
@@ -858,6 +859,12 @@ class NativeDeepFM(NativeStateMixin):
                 # run-routed step: the next step's rows served by extra tower workgroups
                 ta.sv, self.shx.tower_serve = self.shx.tower_serve, None
                 ta.serve_wgs = -(-ta.sv.total * (self.K // 4) // 256)
+            if self._tower_stamp is not None:
+                # tf1_dense run-sorted step: this batch's row flags set by extra tower workgroups
+                keys, n, flags = self._tower_stamp
+                self._tower_stamp = None
+                ta.stamp_keys, ta.stamp_n, ta.stamp_div, ta.stamp_flags = keys.data_ptr(), n, self.row_div, flags.data_ptr()
+                ta.stamp_wgs = -(-n // KN.tower_stamp_rows_per_wg())
             KN.tower(ta, KE=self.K)
             if after_fm is not None:
                 after_fm()
@@ -1280,7 +1287,12 @@ class NativeDeepFM(NativeStateMixin):
             if self._tf1_plan is not None:
                 if not self._tf1_merged:
                     raise RuntimeError("run-level sort with tf1_dense needs the merged sweep")
-                KN.stamp_rows(self.sorted_keys, B * self.F, self.row_div, self._row_flags[self._tf1_plan[0]], 1)
+                flags = self._row_flags[self._tf1_plan[0]]
+                if self.fused and self.gather_fused:
+                    # stamped by extra workgroups of this step's tower launch (no launch of its own)
+                    self._tower_stamp = (self.sorted_keys, B * self.F, flags)
+                else:
+                    KN.stamp_rows(self.sorted_keys, B * self.F, self.row_div, flags, 1)
         else:
             self.sorted_keys, self.perm = self._ss[plan[0] if plan is not None else self._ss_cur]
         prefetch = plan is not None and plan[2] is not None

@@ -178,7 +178,9 @@ class TowerArgs(C.Structure):
                 ("idx", c_void_p), ("vals", c_void_p), ("tv", c_void_p), ("tw", c_void_p),
                 ("ldv", c_long), ("ldw", c_long), ("fm_bias", c_void_p), ("F", c_int),
                 ("x_off", c_int), ("x8_off", c_int), ("S", c_void_p), ("Et", c_void_p), ("idx_ld", c_int),
-                ("id_lim", c_uint32), ("vbf16", c_int), ("serve_wgs", c_int), ("sv", ShServeArgs)]
+                ("id_lim", c_uint32), ("vbf16", c_int), ("serve_wgs", c_int), ("sv", ShServeArgs),
+                ("stamp_wgs", c_int), ("stamp_n", c_int), ("stamp_div", c_int), ("stamp_keys", c_void_p),
+                ("stamp_flags", c_void_p)]
 
 
 class CommOp(C.Structure):
@@ -291,6 +293,7 @@ _SIGS = {
     "hfm_wgfin_job_bytes": [],
     "hfm_wgfin_args_bytes": [],
     "hfm_tower_args_bytes": [],
+    "hfm_tower_stamp_rows_per_wg": [],
     "hfm_wgrad_group": [c_void_p, c_int, c_int, c_void_p],
     "hfm_wg_job_bytes": [],
     "hfm_w8_quant": [c_void_p, c_int, c_int, c_void_p],

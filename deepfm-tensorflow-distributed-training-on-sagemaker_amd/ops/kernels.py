@@ -439,6 +439,11 @@ def wgfin(opt: int, a):
     check(L().hfm_wgfin(int(opt), C.byref(a), stream_handle()), "wgfin")
 
 
+def tower_stamp_rows_per_wg() -> int:
+    """Sorted keys per row-flag stamping workgroup of the tower launch (tower.hip)."""
+    return int(L().hfm_tower_stamp_rows_per_wg())
+
+
 def tower(a: TowerArgs, KE: int = 0):
     """Fused deep tower: [FM gather (KE = embedding size) +] forward + head (+ dgrad chain when
     a.train) (csrc/kernels/tower.hip)."""
