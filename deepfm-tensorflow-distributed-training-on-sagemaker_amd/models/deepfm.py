@@ -35,7 +35,9 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import torch
 
 from ..ops import kernels as KN
+from .runner import GraphRunnerMixin, graph_capture  # noqa: F401  (graph_capture: re-exported)
 from .state import NativeStateMixin
+from .step_plan import IDLE, ModeSpec, StepKnobs, StepPlan, plan_step, sfwg_possible, sweep_merges
 from ..ops._lib import (TW_MAXL, BnArgs, EpiArgs, FinOpt, HeadArgs, TowerArgs, W8Job, WgFinArgs, WgFinJob,
                         WgJob, RowSumJob, SegApplyArgs, SfArgs, ShadowSeg, SlabJob)
 from ..utils.rng import keep_threshold
@@ -71,6 +73,15 @@ _TF1_SPLIT = flag("HIPFM_TF1_SPLIT")
 _SWEEP_MODE = knob("HIPFM_SWEEP_MODE")      # auto | merged | branch
 _SWEEP_MBLK = int(knob("HIPFM_SWEEP_MBLK"))  # merged-mode sweep workgroups: 512 0.191, 1024 0.179, 2048 0.156, 3072 0.156, 6144 0.172 ms
 _SWEEP_WG = int(knob("HIPFM_SWEEP_WG"))   # 128: 0.178, 256: 0.160, 512: 0.179 ms
+
+
+def step_knobs() -> StepKnobs:
+    """The step planner's knob snapshot (read at call time: tests switch these module values)."""
+    return StepKnobs(sort_side_stream=_SORT_SIDE_STREAM, dense_early=_DENSE_EARLY, fwd_idst=_FWD_IDST,
+                     fuse_fin_opt=_FUSE_FIN_OPT, sparse_impl=_SPARSE_IMPL, dense_side_stream=_DENSE_SIDE_STREAM,
+                     wgfin=_WGFIN, sfwg=_SFWG, shx_fork=_SHX_FORK, sh_apply_dense=_SH_APPLY_DENSE,
+                     sh_xfuse=_SH_XFUSE, sweep_mode=_SWEEP_MODE, run_sort=_RUN_SORT,
+                     shard_pipeline=_SHARD_PIPELINE)
 
 
 def check_field_ranges(ranges, F: int, V: int) -> List[Tuple[int, int]]:
@@ -112,31 +123,6 @@ def table_record_floats(K: int, optimizer: str, bf16: bool = False) -> int:
     kv = K // 2 if bf16 else K
     x = kv + 4 + _OPT_SLOTS[optimizer] * kv
     return (x + 15) // 16 * 16 if x <= 16 else (x + 31) // 32 * 32
-
-
-@contextlib.contextmanager
-def graph_capture(g):
-    """``torch.cuda.graph(g)`` with Python's automatic garbage collection off while capturing.
-    torch collects garbage once before the capture begins; an automatic collection DURING it
-    can finalize an object whose destructor calls a HIP / RCCL API that is illegal while a
-    stream captures (a dropped model's graphs, events or communicator), which aborts the
-    process (seen on MI355X when one test's models were collected inside the next test's
-    capture)."""
-    was = gc.isenabled()
-    gc.disable()
-    try:
-        with torch.cuda.graph(g):
-            yield
-    finally:
-        if was:
-            gc.enable()
-
-
-def _hashable(x):
-    """Nested lists / tuples (a plan state) as nested tuples, usable as a dict key."""
-    if isinstance(x, (list, tuple)):
-        return tuple(_hashable(v) for v in x)
-    return x
 
 
 def _align(n: int, a: int = 64) -> int:
@@ -191,7 +177,7 @@ class DenseSeg:
     tf_shape: tuple     # TF checkpoint shape
 
 
-class NativeDeepFM(NativeStateMixin):
+class NativeDeepFM(GraphRunnerMixin, NativeStateMixin):
     """DeepFM on one GPU (one rank).  ``comm`` (parallel.dist.Comm) adds data parallelism."""
 
     def __init__(self, feature_size: int, field_size: int, embedding_size: int = 32,
@@ -375,19 +361,13 @@ class NativeDeepFM(NativeStateMixin):
         self._next_sort_ids = None
         self._next_fm = False      # the declared next batch's ids are field-major
         self._tf1_plan = None      # tf1_dense split sweep: (flag set, inline sort, stale keys)
-        self._tf1_merged = False
         self._idx_fm = False       # the bound batch's ids (self.idx) are field-major [F, M]
         self._comm_stream = None
         self.shx = None
         self._shx_plan = None
-        self._dense_early = False
-        self._fuse_opt = False     # dense optimizer fused into the finalize launch (this step)
-        self._sfwg_now = False     # ... and that launch merged into the sparse backward (this step)
-        self._sfwg_step = False
+        self._sp = IDLE            # the plan of the step being enqueued (models/step_plan.py)
+        self._last_plan = IDLE
         self._sh_join = None
-        self._sh_apply_dense = False
-        self._sh_ar = False
-        self._sh_xfuse = False
         self._idsT_B = 0
         self.batch_size = int(batch_size)
         # fused deep tower (csrc/kernels/tower.hip): whole forward + head + dgrad chain in one
@@ -764,7 +744,7 @@ class NativeDeepFM(NativeStateMixin):
         """Weight / bias / head gradients of the fused tower (+ the dense optimizer when this step
         fuses it): one wgfin launch, or wgrad_group + finalize (HIPFM_WGFIN=0)."""
         if _WGFIN:
-            KN.wgfin(self.opt_id if self._fuse_opt else -1, self._wgfin_args(self._fuse_opt))
+            KN.wgfin(self.opt_id if self._sp.fuse_opt else -1, self._wgfin_args(self._sp.fuse_opt))
             return
         KN.wgrad_group(self._wg_jobs, self._nwg_jobs, self._wg_tasks)
         self._finalize_grads()
@@ -1086,7 +1066,7 @@ class NativeDeepFM(NativeStateMixin):
         self._finalize_grads()
 
     def _finalize_grads(self):
-        if self._fuse_opt:
+        if self._sp.fuse_opt:
             KN.finalize_opt(self.opt_id, self._slab_jobs, self._nslab_jobs, self._slab_blocks,
                             self._row_jobs, self._nrow_jobs, self._row_total, self.p, self.g,
                             self.sd[0], self.sd[1], self.P, self.h_dense, self.step,
@@ -1191,7 +1171,7 @@ class NativeDeepFM(NativeStateMixin):
         A.h = self.h_sparse
         A.step = self.step.data_ptr()
         A.ldv, A.ldw = KN._ld(self.tv, self.tw)
-        A.step_off = 0 if (self._dense_early and not self._sfwg_now) else 1
+        A.step_off = 0 if (self._sp.dense_early and not self._sp.sfwg) else 1
         A.flags, A.sync = self.sf_flags.data_ptr(), self.sf_sync.data_ptr()
         A.vbf16 = 1 if self.emb_bf16 else 0
         return A
@@ -1202,24 +1182,24 @@ class NativeDeepFM(NativeStateMixin):
         n = B * self.F
         if self.shx is not None:
             self.shx.backward(self._shx_plan, B,
-                              dense=self._sh_dense_args() if self._sh_apply_dense else None,
+                              dense=self._sh_dense_args() if self._sp.sh_apply_dense else None,
                               join=self._sh_join,
-                              wgfin=self._wgfin_args(False) if self._sh_xfuse else None,
-                              dense_ar=self.g if self._sh_ar else None)
+                              wgfin=self._wgfin_args(False) if self._sp.xfuse else None,
+                              dense_ar=self.g if self._sp.exchange_allreduce else None)
             return None
         if self.sharded:
             return self.comm.sharded_backward(self, B, idx, tv)
         if not presorted:
             self._sort_slots(B)
         if self.rpx is not None:
-            self.rpx.backward(B, dense=self._sh_dense_args() if self._sh_apply_dense else None,
+            self.rpx.backward(B, dense=self._sh_dense_args() if self._sp.sh_apply_dense else None,
                               join=self._sh_join,
-                              wgfin=self._wgfin_args(False) if self._sh_xfuse else None,
-                              dense_ar=self.g if self._sh_ar else None)
+                              wgfin=self._wgfin_args(False) if self._sp.xfuse else None,
+                              dense_ar=self.g if self._sp.exchange_allreduce else None)
             return None
-        if self._sfwg_now:
+        if self._sp.sfwg:
             KN.sparse_wgfin(self.K, self.opt_id, self.sf_args(n), self._wgfin_args(True), self.sfwg_done,
-                            sweep=self._sweep_args() if self._tf1_merged else None)
+                            sweep=self._sweep_args() if self._sp.tf1_merged else None)
             return None
         if not self.exchange and _SPARSE_IMPL == "fused":
             KN.sparse_fused(self.K, KN.SF_LAZY if self.lazy_rows else KN.SF_SCATTER,
@@ -1263,51 +1243,59 @@ class NativeDeepFM(NativeStateMixin):
                            self.h_sparse, self.step)
 
     # ------------------------------------------------------------------ public step API
+    _knobs = staticmethod(step_knobs)
+
+    def _mode_spec(self) -> ModeSpec:
+        return ModeSpec(K=self.K, fused=self.fused, gather_fused=self.gather_fused, sharded=self.sharded,
+                        exchange=self.exchange, native_exchange=(self.shx is not None or self.rpx is not None),
+                        row_sharded=self.shx is not None, lazy_rows=self.lazy_rows,
+                        lazy=self.sparse_update == "lazy", tf1_split=self.tf1_split, fp8=self.fp8,
+                        wgfin_fits=getattr(self, "_wgfin_ns", 1 << 30) <= KN.SFWG_MAX_NS,
+                        fin_covers_all=self._fin_covers_all)
+
+    def step_plan(self, B: int) -> StepPlan:
+        """The plan (models/step_plan.py) of the step bound by ``_bind_step`` at batch size B."""
+        fs = self.uses_field_sort(B)
+        return plan_step(self._mode_spec(), step_knobs(), B, self._sort_plan, self._tf1_plan is not None,
+                         field_sort=fs, idst_capable=fs and KN.fm_fwd_writes_idsT(self.F, self.K))
+
+    # the last step's plan, observable by tests (which dense-optimizer / sweep path ran)
+    _tf1_merged = property(lambda self: self._last_plan.tf1_merged)
+    _fin_opt_step = property(lambda self: self._last_plan.fuse_opt)
+    _sfwg_step = property(lambda self: self._last_plan.sfwg)
+
     def train_step_enqueue(self, B: int):
-        """Enqueue one full training step on the current stream (no host sync).  The slot-id
-        sort depends only on the batch, so it runs on a side stream concurrently with the
-        forward / tower backward (a parallel branch of the captured graph)."""
-        presorted = False
-        # tf1_dense split sweep inside the merged sparse launch (needs the single-GPU sfwg path,
-        # which the split form always takes: its sort is always presorted on a side stream)
-        # Small batches take the branch: their tower / sparse launches leave most CUs idle
-        # (B = 1024, K = 8: branch 0.069 vs merged 0.077 ms/step; B = 16384: merged 0.156 vs
-        # branch 0.160-0.163).  K = 32 always merges: a concurrent K = 32 sweep slowed its
-        # latency-bound tower 41 -> 76 us (0.138 vs 0.131 ms/step for scatter + sweep).
-        self._tf1_merged = (self._tf1_plan is not None and
-                            (_SWEEP_MODE == "merged" or
-                             (_SWEEP_MODE == "auto" and (B >= 8192 or self.K > 16))) and
-                            self._sfwg_possible())
+        """Enqueue one full training step on the current stream (no host sync), following its
+        plan (models/step_plan.py).  Graph branches launch in capture order, so every forked
+        branch is enqueued right after the tower: the step's first kernel starts at once."""
+        sp = self.step_plan(B)
+        main = torch.cuda.current_stream(self.device)
         if self.shx is not None:
             self._shx_start(B)
-        after_fm = self.shx.fork_next if (self.shx is not None and _SHX_FORK == "tower") else None
+        hooks = []          # called once the tower (or FM forward) is enqueued
+        if self.shx is not None and _SHX_FORK == "tower":
+            hooks.append(self.shx.fork_next)
         plan = self._sort_plan
-        if plan is not None and plan[0] == "run":        # sorted at the start of the run
+        if sp.run_sorted:                                   # sorted at the start of the run
             self.sorted_keys, self.perm = self._run_ss[plan[3]]
             if self._tf1_plan is not None:
-                if not self._tf1_merged:
-                    raise RuntimeError("run-level sort with tf1_dense needs the merged sweep")
                 flags = self._row_flags[self._tf1_plan[0]]
-                if self.fused and self.gather_fused:
-                    # stamped by extra workgroups of this step's tower launch (no launch of its own)
+                if sp.tower_stamp:      # stamped by extra workgroups of this step's tower launch
                     self._tower_stamp = (self.sorted_keys, B * self.F, flags)
                 else:
                     KN.stamp_rows(self.sorted_keys, B * self.F, self.row_div, flags, 1)
         else:
             self.sorted_keys, self.perm = self._ss[plan[0] if plan is not None else self._ss_cur]
-        prefetch = plan is not None and plan[2] is not None
-        inline = plan is None or plan[1]
-        main = torch.cuda.current_stream(self.device)
-        if prefetch:
+        if sp.prefetch_next:
             # the next batch's sort: a ROOT branch of the step's graph (no dependency on this
-            # step's kernels), enqueued after fm_fwd so the first kernel is launched first; it
-            # overlaps the whole step and is joined only at its end
+            # step's kernels), enqueued after the tower; it overlaps the whole step and is joined
+            # only at its end (enqueue point sweep: after the tower 0.1318, after the dense
+            # gradients 0.1316, at the end 0.1351, at the start 0.1365 ms/step)
             if self._side_next is None:
                 self._side_next = torch.cuda.Stream(self.device)
             self._side_next.wait_stream(main)
             nk_ids, nk_B, nk_fm = self._next_sort_ids, plan[2][1], self._next_fm
             nxt_keys, nxt_perm = self._ss[1 - plan[0]]
-
             tf1_next = self._row_flags[1 - plan[0]] if self.tf1_split else None
 
             def sort_next():
@@ -1315,36 +1303,17 @@ class NativeDeepFM(NativeStateMixin):
                     self._fsort_next(nk_ids, nk_B, nxt_keys, nxt_perm, field_major=nk_fm)
                     if tf1_next is not None:
                         KN.stamp_rows(nxt_keys, nk_B * self.F, self.row_div, tf1_next, 1)
-            # enqueued right after the tower (graph branches are dispatched in capture order);
-            # same-box sweep of the enqueue point: after the tower 0.1318, after the dense
-            # gradients 0.1316, at the end 0.1351, at the start 0.1365 ms/step.  (Letting the
-            # tower write these ids field-major saves the transpose launch but makes the branch
-            # depend on the tower, so the sort no longer overlaps it: 0.1372 vs 0.1223 ms.)
-            after_fm = sort_next
-        if not inline:
-            presorted = True            # sorted during the previous step
-            if self._tf1_plan is not None and not self._tf1_merged:
-                first_cb = after_fm
-                cset = self._tf1_plan[0]
-                # a root branch like the next batch's sort: depends only on the step start; its
-                # kernel is enqueued after the tower (branches launch in capture order).  Forked
-                # after the tower instead, the graph ran every kernel serially: 0.227 vs 0.160 ms
-                self._sweep_src().wait_stream(main)
-
-                def after_fm():
-                    if first_cb is not None:
-                        first_cb()
-                    self._fork_sweep(None, cset)
-        elif not self.sharded and _SORT_SIDE_STREAM:
+            hooks = [sort_next]
+        if sp.tf1_branch and sp.presorted and not sp.fork_sort:
+            # prefetched sort: the sweep is a root branch like the next batch's sort (forked after
+            # the tower instead, the graph ran every kernel serially: 0.227 vs 0.160 ms)
+            self._sweep_src().wait_stream(main)
+            cset = self._tf1_plan[0]
+            hooks.append(lambda: self._fork_sweep(None, cset))
+        if sp.fork_sort:
             if self._side is None:
                 self._side = torch.cuda.Stream(self.device)
-
-            # fm_fwd writes the ids field-major as it reads them, so the forked sort skips its
-            # transpose launch (the sort branch is the step's critical path)
-            pre = (_FWD_IDST and not self.gather_fused and self.uses_field_sort(B) and
-                   KN.fm_fwd_writes_idsT(self.F, self.K))
-            self._idsT_B = B if pre else 0
-
+            self._idsT_B = B if sp.sort_idst else 0
             tfp = self._tf1_plan
 
             def fork_sort():
@@ -1352,127 +1321,68 @@ class NativeDeepFM(NativeStateMixin):
                 with torch.cuda.stream(self._side):
                     if tfp is not None and tfp[2]:
                         # flags a discarded prefetch set from the keys still in this set
-                        KN.stamp_rows(self.sorted_keys, tfp[2], self.row_div,
-                                      self._row_flags[tfp[0]], 0)
-                    if pre:
+                        KN.stamp_rows(self.sorted_keys, tfp[2], self.row_div, self._row_flags[tfp[0]], 0)
+                    if sp.sort_idst:
                         self._fsort.sort_pre(B, self.sorted_keys, self.perm)
                     else:
                         self._sort_slots(B)
                     if tfp is not None:
-                        KN.stamp_rows(self.sorted_keys, B * self.F, self.row_div,
-                                      self._row_flags[tfp[0]], 1)
-                if tfp is not None and not self._tf1_merged:
+                        KN.stamp_rows(self.sorted_keys, B * self.F, self.row_div, self._row_flags[tfp[0]], 1)
+                if sp.tf1_branch:
                     self._fork_sweep(self._side, tfp[0])
-            # graph branches launch in capture order: forking after fm_fwd is enqueued lets the
-            # step's first kernel start at once instead of after the sort's launches
-            # (same-box A/B: 0.160 -> 0.154 ms/step, bitwise-identical results)
-            if after_fm is None:
-                after_fm = fork_sort
-            else:
-                first = after_fm
-
-                def after_fm():
-                    fork_sort()
-                    first()
-            presorted = True
-        # fused tower: the weight gradients (wgrad + finalize, then the dense all-reduce) only
-        # feed the dense optimizer, so on the multi-rank step they run on their own stream
-        # concurrently with the sparse exchange (which needs only dX0 / dlogit / S from the
-        # tower): 0.210 -> 0.199 ms.  On one GPU the concurrent wgrad slows the sparse backward
-        # more than it saves (0.156 -> 0.161 ms), so there it stays in line.
-        # row-sharded lazy step with wgfin: the dense gradient is computed in the sparse backward's
-        # launch and travels with the gradient rows' exchange (all-gather, summed in rank order
-        # by the owner launch): no comm stream, no all-reduce, no cross-stream joins
-        xch = self.shx if self.shx is not None else self.rpx     # native fixed-capacity exchange
-        xfuse = (xch is not None and self.sparse_update == "lazy" and _SH_XFUSE and _WGFIN and
-                 self.fused and _SH_APPLY_DENSE and getattr(self, "_wgfin_ns", 1 << 30) <= KN.SFWG_MAX_NS)
-        self._sh_xfuse = xfuse
-        split = self.fused and not xfuse and (_DENSE_SIDE_STREAM == "1" or
-                                              (_DENSE_SIDE_STREAM == "auto" and self.exchange))
-        # single GPU, lazy rows: the dense optimizer needs only the finished dense gradient, so it
-        # runs BEFORE the join with the side-stream sort, inside the gap the join costs anyway;
-        # it advances the step counter, and the sparse kernels are told so (SfArgs.step_off).
-        # With the fused tower it rides on the finalize launch itself (one kernel boundary less)
-        self._dense_early = (presorted and not self.exchange and not split and _DENSE_EARLY and
-                             self.lazy_rows and _SPARSE_IMPL == "fused")
-        self._fuse_opt = (self._dense_early and self.fused and _FUSE_FIN_OPT and self._fin_covers_all)
-        # ... and with wgfin, that whole dense-gradient launch rides inside the sparse backward's
-        # launch instead (sfwg: independent work, both latency-bound)
-        self._sfwg_now = self._fuse_opt and self._sfwg_possible()
-        if self._tf1_merged and not self._sfwg_now:
-            raise RuntimeError("tf1_dense merged sweep planned but the step took another path")
+            # (forking after the tower rather than before it: 0.160 -> 0.154 ms/step)
+            hooks.insert(0, fork_sort)
+        self._sp = sp
         try:
-            idx, tv = self._dense_fwd_bwd(B, defer_wgrad=split or self._sfwg_now or xfuse,
-                                          after_fm=after_fm)
+            idx, tv = self._dense_fwd_bwd(B, defer_wgrad=sp.defer_wgrad,
+                                          after_fm=(lambda: [h() for h in hooks]) if hooks else None)
         finally:
             self._idsT_B = 0
-            fused_opt, self._fuse_opt = self._fuse_opt, False
-        main = torch.cuda.current_stream(self.device)
-        self._fin_opt_step = fused_opt          # observable by tests: which dense-optimizer path ran
-        self._sfwg_step = self._sfwg_now
-        if fused_opt:
-            if self.fp8 and not _WGFIN:       # (wgfin writes the fp8 weights itself)
-                KN.w8_quant(self._w8_jobs, len(self.layers), self._w8_rows)
-        elif self._dense_early:
+        if sp.w8_after_fin:
+            KN.w8_quant(self._w8_jobs, len(self.layers), self._w8_rows)
+        elif sp.dense_early and not sp.fuse_opt:
             self._dense_opt()
-        if presorted and inline:
+        if sp.join_sort:
             main.wait_stream(self._side)
         work = None
-        # row-sharded step: the dense all-reduce rides in the gradient exchange group on the main
-        # stream (parallel/sharded.py: one communicator, fixed order); replicated: the process
-        # group's all-reduce, overlapped with the sparse backward
-        shx_ar = xch is not None and not xfuse
-        if split:
-            # dense gradient branch overlapped with the sparse backward
+        if sp.dense_branch:
+            # weight gradients (+ the process-group all-reduce) beside the sparse backward
             if self._comm_stream is None:
                 self._comm_stream = torch.cuda.Stream(self.device)
             self._comm_stream.wait_stream(main)
             with torch.cuda.stream(self._comm_stream):
                 self._dense_grads()
-                if self.exchange and not xfuse and not shx_ar:
+                if sp.dense_allreduce:
                     work = self.comm.allreduce_dense_async(self.g)
-        elif self.exchange and not xfuse and not shx_ar:
+        elif sp.dense_allreduce:
             work = self.comm.allreduce_dense_async(self.g)
-        # row-sharded step: the dense gradient's producer is joined right before the gradient
-        # exchange group; with lazy rows the dense optimizer rides in the owner update's launch
-        self._sh_join = None
-        self._sh_apply_dense = False
-        if xch is not None:
-            cs = self._comm_stream if split else None
-            self._sh_join = (lambda cs=cs: main.wait_stream(cs)) if cs is not None else None
-            self._sh_apply_dense = (self.sparse_update == "lazy" and _SH_APPLY_DENSE and
-                                    not self._dense_early)
-            self._sh_ar = shx_ar
-        out = self._sparse_backward(B, idx, tv, presorted=presorted)
-        if out is not None:
-            self._sparse_update(*out)
-        self._sfwg_now = False
-        if split:
+        # native exchange: the dense gradient's producer is joined right before the gradient
+        # exchange group (parallel/sharded.py: one communicator, fixed order)
+        cs = self._comm_stream if sp.dense_branch else None
+        self._sh_join = (lambda: main.wait_stream(cs)) if cs is not None else None
+        try:
+            out = self._sparse_backward(B, idx, tv, presorted=sp.presorted)
+            if out is not None:
+                self._sparse_update(*out)
+        finally:
+            self._sp, self._last_plan = IDLE, sp
+            self._sh_join = None
+        if sp.dense_branch:
             main.wait_stream(self._comm_stream)
         if work is not None:
             self.comm.wait(work)
         if self.shx is not None:
             self.shx.end(self._shx_plan)
-        if self._sh_apply_dense:
-            self._sh_apply_dense = False
-            if self.fp8:
-                KN.w8_quant(self._w8_jobs, len(self.layers), self._w8_rows)
-        elif not self._dense_early:
+        if sp.w8_after_owner:
+            KN.w8_quant(self._w8_jobs, len(self.layers), self._w8_rows)
+        elif sp.dense_opt_after:
             self._dense_opt()
-        if self._tf1_plan is not None and not self._tf1_merged:
+        if sp.tf1_branch:
             main.wait_stream(self._sweep_stream)
-        if prefetch:
+        if sp.prefetch_next:
             # joined at the end of the step: deferring the join to the next step's sparse
-            # backward (so no cross-branch edge precedes the next tower) measured 0.155-0.186
-            # vs 0.121 ms/step in a 16-step graph -- the branch then lands in the towers' path
+            # backward measured 0.155-0.186 vs 0.121 ms/step (the branch lands in the towers' path)
             main.wait_stream(self._side_next)
-
-    def _sfwg_possible(self) -> bool:
-        """The sparse backward + wgfin merged launch applies (given the fused dense optimizer)."""
-        return (_WGFIN and _SFWG and getattr(self, "_wgfin_ns", 1 << 30) <= KN.SFWG_MAX_NS and
-                self.shx is None and not self.sharded and self.fused and _FUSE_FIN_OPT and
-                self._fin_covers_all and not self.exchange and _DENSE_EARLY and self.lazy_rows and
-                _SPARSE_IMPL == "fused" and _DENSE_SIDE_STREAM != "1")
 
     def _sweep_args(self):
         from ..ops._lib import SweepArgs
@@ -1535,374 +1445,6 @@ class NativeDeepFM(NativeStateMixin):
         KN.seg_apply(self.K, KN.SEG_WRITE_UG, 0, self.seg_args(n, compact=True), n)
         U = int(self.num_u.item())
         return self.g.clone(), self.ukeys[:U].clone(), self.UG[:U].clone()
-
-    def _field_major(self, ids) -> bool:
-        """``ids`` [B, F] stored field-major (the transposed view of a contiguous [F, B] tensor,
-        e.g. ``idsT.t()``) and usable as such: the tower gathers through either layout, and the
-        per-field sort reads this one directly (no transpose launch).  Other paths take row-major
-        ids, so a field-major batch elsewhere is staged (copied row-major)."""
-        return (ids.dim() == 2 and ids.shape[0] > 1 and ids.stride() == (1, ids.shape[0]) and
-                self.gather_fused and self.uses_field_sort(ids.shape[0]))
-
-    @staticmethod
-    def _flat_ids(ids, fm: bool) -> torch.Tensor:
-        """The storage of a bound id batch as a flat view (field-major: [F * B])."""
-        return ids.t().reshape(-1) if fm else ids.reshape(-1)
-
-    def _resident(self, ids, vals, labels) -> bool:
-        return (ids.is_cuda and ids.dtype == torch.int32 and vals.dtype == torch.float32 and
-                (ids.is_contiguous() or self._field_major(ids)) and vals.is_contiguous() and
-                labels.is_contiguous() and ids.shape[0] == self.M and ids.numel() == self.M * self.F)
-
-    @staticmethod
-    def _split_next(next_ids):
-        """``next_ids``: the next batch's ids, or (next, the one after) -- the row-sharded step
-        routes two batches ahead when it knows both (parallel/sharded.py, pipeline depth)."""
-        if isinstance(next_ids, (tuple, list)):
-            n1 = next_ids[0] if len(next_ids) > 0 else None
-            n2 = next_ids[1] if len(next_ids) > 1 else None
-            return n1, (n2 if n1 is not None else None)
-        return next_ids, None
-
-    def _next_ok(self, t, B: int) -> bool:
-        return (t is not None and t.is_cuda and t.dtype == torch.int32 and
-                (t.is_contiguous() or self._field_major(t)) and t.shape[0] == B and t.numel() == B * self.F)
-
-    def _bind_step(self, ids, vals, labels, next_ids=None, stage: bool = False):
-        """Bind one step's batch (in place when resident, else -- or with ``stage`` -- a copy into
-        the static input buffers) and decide its host-side plans (sort / routing: inline or
-        prefetched, next batch or none).  Returns (B, direct, key) -- ``key`` identifies the
-        step's captured graph (staged steps of one batch size share one graph)."""
-        direct = (not stage) and self._resident(ids, vals, labels)
-        if direct:
-            B = ids.shape[0]
-            fm = not ids.is_contiguous()
-            self.idx = self._flat_ids(ids, fm)
-            self.vals, self.labels = vals.reshape(-1), labels.reshape(-1)
-            self._idx_fm = fm
-            key = (ids.data_ptr(), vals.data_ptr(), labels.data_ptr(), B, fm)
-        else:
-            self.idx, self.vals, self.labels = self._own_in
-            B = self.stage_batch(ids, vals, labels)
-            key = ("staged", B)
-        next_ids, next2_ids = self._split_next(next_ids)
-        nxt_ok = direct and self._next_ok(next_ids, B)
-        nxt_fm = nxt_ok and not next_ids.is_contiguous()
-        nxt2_ok = nxt_ok and self._next_ok(next2_ids, B)
-        nxt2_fm = nxt2_ok and not next2_ids.is_contiguous()
-        self._shx_plan = None
-        self._sort_plan = None
-        if self._run_j is not None and self.shx is None:
-            # run-level sort: this batch was sorted at the start of the run (train_steps)
-            self._sort_plan = ("run", False, None, self._run_j)
-            key = key + self._sort_plan
-        elif (not self.sharded and _SORT_SIDE_STREAM and self._fsort_next is not None and
-                self.uses_field_sort(B)):
-            # the sort of a batch the caller declared as next (resident, unchanged until its step)
-            # was computed during the previous step: reuse it when that batch is this one
-            c = self._ss_cur
-            inline = not (direct and self._ss_key[c] == (ids.data_ptr(), B))
-            nk = None
-            if nxt_ok:
-                nk = (next_ids.data_ptr(), B)
-                self._next_sort_ids = self._flat_ids(next_ids, nxt_fm)
-                self._next_fm = nxt_fm
-            self._sort_plan = (c, inline, nk)
-            key = key + ("sort",) + self._sort_plan
-        self._tf1_plan = None
-        if self.tf1_split and self._sort_plan is not None and self._sort_plan[0] == "run":
-            # run-level sort: this step stamps its rows into a flag set with no stale stamps (a
-            # discarded prefetch can have left them in at most one set) at its start; its merged
-            # sweep clears them
-            c = 0 if self._stamp_n[0] == 0 else 1
-            self._tf1_plan = (c, "run", 0)
-            key = key + ("tf1",) + self._tf1_plan
-        elif self.tf1_split:
-            # flags of set c: this batch's rows (prefetched: set during the previous step); an
-            # inline sort first clears flags a discarded prefetch left in set c
-            c = self._sort_plan[0] if self._sort_plan is not None else self._ss_cur
-            inline = self._sort_plan is None or self._sort_plan[1]
-            self._tf1_plan = (c, inline, self._stamp_n[c] if inline else 0)
-            key = key + ("tf1",) + self._tf1_plan
-        if self.shx is not None and self._run_j is not None:
-            # run-level routing: routed and its ids exchanged at the start of the run
-            self._shx_plan = self.shx.run_plan(self._run_j, self._run_n)
-            key = key + tuple(self._shx_plan)
-        elif self.shx is not None:
-            nxt = self._flat_ids(next_ids, nxt_fm) if (nxt_ok and _SHARD_PIPELINE) else None
-            nxt2 = self._flat_ids(next2_ids, nxt2_fm) if (nxt2_ok and _SHARD_PIPELINE) else None
-            self._shx_plan = self.shx.plan(self.idx, B, nxt, resident=direct, nxt2=nxt2)
-            self.shx._next = (nxt, nxt_fm, nxt2, nxt2_fm)
-            key = key + tuple(self._shx_plan)
-        return B, direct, key
-
-    def _commit_step(self, B: int, direct: bool):
-        if self._tf1_plan is not None:
-            c = self._tf1_plan[0]
-            self._stamp_n[c] = 0                       # swept (flags cleared) by this step
-            nk = self._sort_plan[2] if self._sort_plan is not None else None
-            if nk is not None:
-                self._stamp_n[1 - c] = nk[1] * self.F  # set by this step's prefetched sort
-            self._tf1_plan = None
-        if self.shx is not None:
-            self.shx.commit(self._shx_plan, self.idx, B, resident=direct)
-            self._shx_plan = None
-        if self._sort_plan is not None and self._sort_plan[0] == "run":
-            self._ss_key = [None, None]     # nothing prefetched for the step after the run
-            self._sort_plan = None
-        if self._sort_plan is not None:
-            c, _, nk = self._sort_plan
-            self._ss_key[c] = None          # consumed: reused only through a next-batch declaration
-            self._ss_key[1 - c] = nk
-            self._ss_cur = 1 - c
-            self._sort_plan = None
-        if self._host_step is not None:
-            self._host_step += 1
-
-    @property
-    def plan_period(self) -> int:
-        """Steps after which the rotating prefetch sets (2 slot-sort sets, NSETS routing sets of
-        the row-sharded step) return to the same phase: a replay loop that advances by a multiple
-        of it between capture and replay finds every run's graph under the same plan state."""
-        n = 2
-        if self.shx is not None:
-            n = n * self.shx.NSETS // math.gcd(n, self.shx.NSETS)
-        return n
-
-    def _plan_state(self):
-        sh = None if self.shx is None else (self.shx.cur, [(rs.key, rs.stage) for rs in self.shx.sets])
-        return self._ss_cur, list(self._ss_key), sh, list(getattr(self, "_stamp_n", []))
-
-    def _set_plan_state(self, st):
-        self._ss_cur, self._ss_key = st[0], list(st[1])
-        if self.tf1_split:
-            self._stamp_n = list(st[3])
-        if st[2] is not None:
-            self.shx.cur = st[2][0]
-            for rs, (k, stg) in zip(self.shx.sets, st[2][1]):
-                rs.key, rs.stage = k, stg
-
-    def train_step(self, ids, vals, labels, use_graph: bool = False, next_ids=None,
-                   stage: bool = False):
-        """One training step.  A device-resident int32 batch whose size equals the allocated
-        batch is bound in place (no staging copy); with ``use_graph`` each such resident batch
-        gets its own captured HIP graph (the HBM-cached epoch replays graphs back to back).
-        ``next_ids`` (resident ids of the NEXT step's batch, unchanged until that step): its
-        slot sort (one GPU) or its routing (row-sharded multi-GPU step) is computed on a side
-        stream during this step.  ``stage``: copy the batch into the static input buffers even if
-        it is resident (a stream of one-off batches then replays ONE graph)."""
-        B, direct, key = self._bind_step(ids, vals, labels, next_ids, stage)
-        if use_graph and (self.comm is None or self.comm.graph_safe):
-            self._replay_graph(key, B)
-        else:
-            self.train_step_enqueue(B)
-        self._commit_step(B, direct)
-        return B
-
-    def train_steps(self, batches, next_ids=None) -> int:
-        """Consecutive training steps over resident batches as ONE captured HIP graph (a whole
-        launch-bound inner loop per replay: the per-replay launch and branch-join cost is paid
-        once per run of steps instead of once per step).  Every step is complete -- forward,
-        backward, sparse and dense optimizer -- and identical to ``train_step`` (bitwise, tested).
-        Batch i declares batches i+1 and i+2 as its upcoming batches (prefetched sort / routing);
-        ``next_ids`` is the batch after the last one, or (that batch, the one after it).  Returns
-        the number of steps."""
-        batches = list(batches)
-        if not batches:
-            return 0
-        la1, la2 = self._split_next(next_ids)
-        seq = [b[0] for b in batches] + [x for x in (la1, la2) if x is not None]
-
-        def nxt_of(i):
-            return (seq[i + 1] if i + 1 < len(seq) else None, seq[i + 2] if i + 2 < len(seq) else None)
-        if all(self._resident(*b) for b in batches) and (self._run_sort_ok(batches) or
-                                                          self._run_route_ok(batches)):
-            return self._train_run_sorted(batches)
-        if not all(self._resident(*b) for b in batches) or not (self.comm is None or self.comm.graph_safe):
-            for i, (ids, vals, labels) in enumerate(batches):
-                self.train_step(ids, vals, labels, use_graph=True, next_ids=nxt_of(i))
-            return len(batches)
-        st0 = self._plan_state()
-        # a run seen before from the same plan state replays its graph without re-planning
-        # each step in Python (the per-step bind costs tens of us of host time, which a
-        # 16-step graph of ~0.11 ms steps cannot always hide behind the GPU)
-        mkey = (tuple((b[0].data_ptr(), b[0].stride(), b[1].data_ptr(), b[2].data_ptr(), b[0].shape[0])
-                      for b in batches),
-                tuple((t.data_ptr(), t.stride()) for t in (la1, la2) if t is not None),
-                _hashable(st0))
-        hit = self._run_memo.get(mkey)
-        if hit is not None and self._graphs.get(hit[0]) is hit[1]:
-            _, g, st1, n = hit
-            g.replay()
-            self._set_plan_state(st1)
-            if self._host_step is not None:
-                self._host_step += n
-            return n
-        h0 = self._host_step
-        keys, Bs = [], []
-        for i, (ids, vals, labels) in enumerate(batches):       # plans only: the graph key
-            B, direct, k = self._bind_step(ids, vals, labels, nxt_of(i))
-            keys.append(k)
-            Bs.append(B)
-            self._commit_step(B, direct)
-        key = ("run",) + tuple(keys)
-        g = self._graphs.get(key)
-        if g is None:
-            self._set_plan_state(st0)
-            self._host_step = h0
-            eager_first = not self._graphs and not getattr(self, "_warm", False)
-            if eager_first:
-                self._warm = True
-                # the very first step of the model runs eagerly (warms up lazy library state)
-                ids, vals, labels = batches[0]
-                self.train_step(ids, vals, labels, use_graph=False, next_ids=nxt_of(0))
-                torch.cuda.synchronize()
-                rest = batches[1:]
-                if not rest:
-                    return 1
-                return 1 + self.train_steps(rest, next_ids)
-            g = torch.cuda.CUDAGraph()
-            with graph_capture(g):
-                for i, (ids, vals, labels) in enumerate(batches):
-                    B, direct, _ = self._bind_step(ids, vals, labels, nxt_of(i))
-                    self.train_step_enqueue(B)
-                    self._commit_step(B, direct)
-            if len(self._graphs) >= self.max_graphs:
-                self._graphs.pop(next(iter(self._graphs)))
-            self._graphs[key] = g
-        g.replay()
-        if len(self._run_memo) >= self.max_graphs:
-            self._run_memo.pop(next(iter(self._run_memo)))
-        self._run_memo[mkey] = (key, g, self._plan_state(), len(batches))
-        return len(batches)
-
-    def _run_sort_ok(self, batches) -> bool:
-        """The run's batches can be sorted up front (fsort_run.h): one GPU, lazy rows (or the
-        tf1_dense split form with its sweep merged into the sparse launch), field ranges, equal
-        batch sizes of at most 8 sort chunks."""
-        if not (_RUN_SORT and len(batches) > 1 and self._fsort_next is not None and not self.sharded and
-                self.shx is None and self.rpx is None and not self.exchange and
-                self.lazy_rows and _SORT_SIDE_STREAM):
-            return False
-        B = batches[0][0].shape[0]
-        if self.tf1_split and not ((_SWEEP_MODE == "merged" or (_SWEEP_MODE == "auto" and (B >= 8192 or self.K > 16)))
-                                   and self._sfwg_possible()):
-            return False          # (tf1_dense: the step's sweep must ride in its sparse launch)
-        return (all(b[0].shape[0] == B for b in batches) and self.uses_field_sort(B) and
-                B <= min(self._fsort_next.max_rows, 8 * KN.fs2_chunk_rows()))
-
-    def _run_route_ok(self, batches) -> bool:
-        """Run-level routing (parallel/sharded.py ``route_run``): the row-sharded step over
-        resident batches of one size, with the per-field sort and graph-safe collectives."""
-        if not (_RUN_SORT and len(batches) > 1 and self.shx is not None and self._fsort is not None):
-            return False
-        B = batches[0][0].shape[0]
-        return (all(b[0].shape[0] == B for b in batches) and self.uses_field_sort(B) and
-                B <= min(self._fsort.max_rows, 8 * KN.fs2_chunk_rows()))
-
-    def _run_sets(self, G: int):
-        n = self.M * self.F
-        while len(self._run_ss) < G:
-            self._run_ss.append((torch.zeros(n, dtype=torch.int32, device=self.device),
-                                 torch.zeros(n, dtype=torch.int32, device=self.device)))
-        return self._run_ss[:G]
-
-    def _train_run_sorted(self, batches) -> int:
-        """``train_steps`` with the run-level sort: ONE graph = the sort of every batch of the run
-        (two launches, fsort_run.h) -- or, row-sharded, its whole routing incl. the id exchange
-        (``FixedCapacityExchange.route_run``) -- followed by the steps, all on one queue (no
-        per-step side branch and no cross-queue join).  Bitwise equal to the per-step sorts /
-        routing (tested)."""
-        G = len(batches)
-        fms = [not b[0].is_contiguous() for b in batches]
-        routed = self.shx is not None
-        if routed:
-            rlist = [(self._flat_ids(b[0], fm), b[0].shape[0], fm) for b, fm in zip(batches, fms)]
-            self.shx.route_run_prepare(rlist)           # allocations / device plans: not in a capture
-        else:
-            sets = self._run_sets(G)
-            rplan = self._fsort_next.run_plan(
-                [(self._flat_ids(b[0], fm), b[0].shape[0], fm, k, p) for b, fm, (k, p) in zip(batches, fms, sets)])
-        def enqueue():
-            if routed:
-                self.shx.route_run(rlist)
-            else:
-                self._fsort_next.run_sort(rplan)
-            self._run_n = G
-            for j, (ids, vals, labels) in enumerate(batches):
-                self._run_j = j
-                try:
-                    B, direct, _ = self._bind_step(ids, vals, labels)
-                    self.train_step_enqueue(B)
-                    self._commit_step(B, direct)
-                finally:
-                    self._run_j = None
-
-        if self.comm is not None and not self.comm.graph_safe:
-            # collectives that cannot be captured (the in-process emulation engine of the tests):
-            # the same run, launched eagerly
-            enqueue()
-            self._ss_key = [None, None]
-            return G
-        mkey = ("runsort",) + tuple((b[0].data_ptr(), b[0].stride(), b[1].data_ptr(), b[2].data_ptr(),
-                                     b[0].shape[0]) for b in batches)
-        g = self._graphs.get(mkey)
-        if g is None and not self._graphs and not getattr(self, "_warm", False):
-            # the model's very first step runs eagerly (warms up lazy library state)
-            self._warm = True
-            ids, vals, labels = batches[0]
-            self.train_step(ids, vals, labels, use_graph=False)
-            torch.cuda.synchronize()
-            return 1 + self.train_steps(batches[1:])
-        if g is None:
-            g = torch.cuda.CUDAGraph()
-            h0 = self._host_step
-            with graph_capture(g):
-                enqueue()
-            self._host_step = h0
-            if len(self._graphs) >= self.max_graphs:
-                self._graphs.pop(next(iter(self._graphs)))
-            self._graphs[mkey] = g
-        g.replay()
-        self._ss_key = [None, None]
-        if self._host_step is not None:
-            self._host_step += G
-        return G
-
-    def _replay_graph(self, key, B: int):
-        g = self._graphs.get(key)
-        if g is None:
-            # The very first step runs eagerly (it is a real step and warms up lazy library
-            # state), then it is captured (capture records, it does not execute); every later
-            # step of the same input binding is one graph replay.
-            if not self._graphs:
-                self.train_step_enqueue(B)
-                torch.cuda.synchronize()
-                g = torch.cuda.CUDAGraph()
-                with graph_capture(g):
-                    self.train_step_enqueue(B)
-                self._graphs[key] = g
-                return
-            g = torch.cuda.CUDAGraph()
-            with graph_capture(g):
-                self.train_step_enqueue(B)
-            if len(self._graphs) >= self.max_graphs:
-                self._graphs.pop(next(iter(self._graphs)))
-            self._graphs[key] = g
-        g.replay()
-
-    def precapture(self, batches, progress=None):
-        """One pass over the resident batches with graph capture (the first step eager, every new
-        binding captured then replayed), so timed loops only replay graphs.  Consecutive batches
-        are chained: the row-sharded step prefetches the next batch's routing.  These are real
-        training steps (use them as warm-up)."""
-        P = len(batches)
-        for i, (ids, vals, labels) in enumerate(batches):
-            self.train_step(ids, vals, labels, use_graph=True,
-                            next_ids=(batches[(i + 1) % P][0], batches[(i + 2) % P][0]))
-            if progress is not None:
-                progress()
-        torch.cuda.synchronize()
 
     def loss_value(self, B: int, include_l2: bool = False) -> float:
         """Mean data loss of the last step (+ l2 terms over the whole tables if asked)."""
