@@ -305,18 +305,26 @@ def main():
                                      next_ids=(pool[(i + j + 1) % P][0], pool[(i + j + 2) % P][0]))
 
     if use_graph and (comm is None or comm.graph_safe):
+        # the model's very first step runs eagerly (it warms up lazy library state); taking it
+        # here lets the pass below capture EVERY run the warm-up and timed windows replay.  (Else
+        # the warm-up captured its own first run right before the timed window, and the GPU,
+        # idle during that capture, ran the short 20-step window 0.160-0.173 ms/step instead of
+        # 0.116-0.117 in about half the runs.)
+        model.train_step(*pool[0], use_graph=True, next_ids=(pool[1 % P][0], pool[2 % P][0]))
         # every graph the warm-up and timed runs replay is captured here first (real steps)
         run(0, args.warmup + args.steps)
         # the sorted-slot (2) and routing (3, row-sharded) sets rotate step by step: padding the
         # steps before the warm-up to a multiple of their period keeps every run's set phase
         # equal to its phase at capture (else the timed window re-captures graphs)
-        for j in range(-(args.warmup + args.steps) % model.plan_period):
+        for j in range(-(1 + args.warmup + args.steps) % model.plan_period):
             model.train_step(*pool[j % P], use_graph=use_graph,
                              next_ids=(pool[(j + 1) % P][0], pool[(j + 2) % P][0]))
         torch.cuda.synchronize()
     _progress()
+    n_graphs = len(model._graphs)
     run(0, args.warmup)
     torch.cuda.synchronize()
+    warm_captures = len(model._graphs) - n_graphs
     _progress()
     if comm is not None:
         dist.barrier()
@@ -334,6 +342,15 @@ def main():
     if timed_captures and rank == 0:
         print(f"[bench] WARNING: {timed_captures} graph capture(s) inside the timed window",
               file=sys.stderr, flush=True)
+    if os.environ.get("HIPFM_BENCH_DIAG") == "1" and rank == 0:
+        # diagnostics (not part of the reported value): the same window re-timed after idle gaps
+        for gap in (0.0, 0.0, 0.001, 0.01, 0.1, 0.5, 0.0):
+            time.sleep(gap)
+            t1 = time.perf_counter()
+            run(args.warmup, args.warmup + args.steps)
+            torch.cuda.synchronize()
+            print(f"[bench diag] idle {gap * 1e3:6.1f} ms -> window {(time.perf_counter() - t1) * 1e3 / args.steps:.4f}"
+                  f" ms/step", file=sys.stderr, flush=True)
     loss = model.loss_value(B)
     ms = elapsed * 1000.0 / max(1, args.steps)
     if comm is not None:
@@ -378,6 +395,7 @@ def main():
                 "optimizer": f"{args.optimizer} ({args.sparse_update})",
                 "hip_graph": use_graph,
                 "timed_graph_captures": timed_captures,
+                "warmup_graph_captures": warm_captures,
                 "graph_steps": G if use_graph else 0,
                 "exec": os.environ.get("HIPFM_BENCH_RUNG", ("graph+run-sort" if os.environ.get("HIPFM_RUN_SORT", "1") == "1"
                                                               else "graph+prefetch") if use_graph else "eager"),

@@ -223,9 +223,11 @@ class FieldSort:
         n = self.F * self.max_rows
         rs = self.__dict__.get("_run_scratch")
         if rs is None or rs.shape[0] < G:
+            # a larger run: new scratch for plans built from now on.  Cached plans are NOT dropped:
+            # graphs captured from them still read their FsJob arrays and scratch (each plan
+            # holds its own in ``keep``), and freeing those let a replay fault on reused memory
             rs = torch.zeros(G, 2, n, dtype=torch.int32, device=self.device)
             self._run_scratch = rs
-            cache.clear()
         jobs, items, mitems, keep = [], [], [], [rs]
         for g, (ids, B, fm, kout, pout) in enumerate(batches):
             assert B <= min(self.max_rows, 8 * ch) and ids.numel() >= B * self.F

@@ -215,6 +215,7 @@ class FixedCapacityExchange:
         self.run_sets = []                   # run-level routing: one set per step of the run
         self._run_descs = {}
         self._run_ids = None                 # packed [2][N][G][C] ids of a run (send, recv)
+        self._run_retired = []               # superseded packed ids buffers (captured graphs read them)
         self.gather_ld = 0                   # slot_row layout of the last fetch (tower idx_ld)
         self.tower_serve = None              # ShServeArgs the next tower launch serves (run mode)
 
@@ -273,8 +274,12 @@ class FixedCapacityExchange:
                                        for (ids, b, fm), rs in zip(batches, sets)])
         T = self.N * G * self.C
         if self._run_ids is None or self._run_ids.shape[1] < T:
+            # a larger run: a new packed ids buffer.  The old one and the descriptors built on it
+            # stay alive (graphs captured from earlier runs still read them: never freed under a
+            # captured graph, which would let a replay fault on reused memory)
+            if self._run_ids is not None:
+                self._run_retired.append(self._run_ids)
             self._run_ids = torch.full((2, T), -1, dtype=torch.int32, device=m.device)
-            self._run_descs.clear()
         ld = m.M if (m.fused and m.gather_fused) else 0     # field-major slot maps for the tower
         for g, rs in enumerate(sets):
             rs.recv_ptr = self._run_ids[1].data_ptr() + 4 * g * self.C

@@ -96,6 +96,8 @@ KNOBS: Dict[str, Knob] = {
     "HIPFM_BENCH_HANG_S": Knob(None, "harness", "bench: seconds without progress = hung (45)"),
     "HIPFM_BENCH_FIRST_S": Knob(None, "harness", "bench: seconds to a rung's first progress mark (90)"),
     "HIPFM_BENCH_NO_GRAPH": Knob(None, "harness", "bench: eager steps only"),
+    "HIPFM_BENCH_DIAG": Knob(None, "harness", "bench: after the measurement, re-time the window after "
+                             "idle gaps (stderr; diagnostics only)"),
     "HIPFM_BENCH_PROGRESS": Knob(None, "harness", "bench supervisor protocol: progress file"),
     "HIPFM_BENCH_RESULT": Knob(None, "harness", "bench supervisor protocol: result file"),
     "HIPFM_BENCH_FAKE": Knob(None, "harness", "bench supervisor tests: CPU stand-in children"),

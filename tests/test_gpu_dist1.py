@@ -182,6 +182,35 @@ def test_exchange_run_routing_bitwise(group, monkeypatch, update, fm):
             assert torch.equal(x, y)
 
 
+def test_exchange_growing_runs_keep_earlier_graphs_valid(group, monkeypatch):
+    """Run routing: a longer run grows the packed ids buffer; graphs captured from shorter runs
+    keep reading their own (retired, not freed) buffers and descriptors, so replaying them after
+    the growth is bitwise the per-step pipelined routing."""
+    import hipfm.models.deepfm as D
+    synth = make_synth("total:6000", seed=38)
+    F, K, layers, keep = synth.F, 8, [64, 32], [0.8, 0.8]
+    V = synth.feature_size
+    params = init_params(V, F, K, layers, False, seed=10)
+    pool = [synth.batch(512, step=s, device="cuda", id_dtype=torch.int32) for s in range(6)]
+    order = [(0, 2), (2, 4), (0, 6), (2, 4), (4, 6), (0, 6), (2, 4)]
+    out = []
+    for run in (True, False):
+        monkeypatch.setattr(D, "_RUN_SORT", run)
+        m = NativeDeepFM(V, F, K, layers, keep, batch_size=512, device="cuda", init=False,
+                         comm=Comm(sharded=True, force_exchange=True), field_ranges=synth.field_ranges())
+        m.load_tf_params(params)
+        for lo, hi in order:
+            m.train_steps(pool[lo:hi], next_ids=(pool[hi % 6][0], pool[(hi + 1) % 6][0]))
+        torch.cuda.synchronize()
+        m.check_errors()
+        if run:
+            assert len(m.shx._run_retired) >= 1          # the growth happened
+        out.append((m.tv.clone(), m.tw.clone(), m.p.clone(), m.step.clone()))
+        del m
+    for x, y in zip(*out):
+        assert torch.equal(x, y)
+
+
 @pytest.mark.parametrize("sharded", [True, False])
 def test_estimator_calibrates_exchange_capacity(group, tmp_path, sharded):
     """the CLI's multi-GPU path ran on default_capacity (1.5x slots / N, ~3-4x the

@@ -102,3 +102,30 @@ def test_run_sort_training_bitwise_equals_side_stream(monkeypatch, B, mlp_dtype,
     for k, ref in enumerate(out[1:]):
         for i, (x, y) in enumerate(zip(out[0], ref)):
             assert torch.equal(x, y), (k, i, (x.float() - y.float()).abs().max().item())
+
+
+def test_growing_runs_keep_earlier_graphs_valid(monkeypatch):
+    """A run longer than every earlier one grows the run-sort scratch; the graphs captured from
+    the shorter runs still read their own plans (FsJob arrays, scratch), so replaying them after
+    the growth is bitwise the per-step sorted training (a freed plan under a captured graph made
+    the bench's warm-up replay fault)."""
+    synth = make_synth("criteo_kaggle", seed=36)
+    B, K, layers = 1024, 8, [128, 64, 32]
+    params = init_params(synth.feature_size, synth.F, K, layers, False, seed=6)
+    pool = [synth.batch(B, step=s, device=DEV, id_dtype=torch.int32) for s in range(6)]
+    order = [(0, 2), (2, 4), (0, 6), (2, 4), (4, 6), (0, 6), (2, 4)]
+    out = []
+    for run in (True, False):
+        monkeypatch.setattr(D, "_RUN_SORT", run)
+        m = NativeDeepFM(synth.feature_size, synth.F, K, layers, [0.5] * 3, batch_size=B, device=DEV,
+                         init=False, field_ranges=synth.field_ranges())
+        m.load_tf_params(params)
+        for lo, hi in order:
+            m.train_steps(pool[lo:hi], next_ids=(pool[hi % 6][0], pool[(hi + 1) % 6][0]))
+        torch.cuda.synchronize()
+        m.check_errors()
+        assert m.global_step() == sum(hi - lo for lo, hi in order)
+        out.append([m.tv.clone(), m.tw.clone(), m.p.clone(), m.step.clone()] + [s.clone() for s in m.sv if s.numel()])
+        del m
+    for i, (x, y) in enumerate(zip(*out)):
+        assert torch.equal(x, y), (i, (x.float() - y.float()).abs().max().item())
