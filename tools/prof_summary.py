@@ -79,6 +79,31 @@ def main():
                 s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
                 lines.append(f"| {(s - t0)/1e3:.2f} | {(e - s)/1e3:.2f} | `{r['Kernel_Name'][:80]}` |")
             lines.append("")
+        # every multi-step graph replay in order (the bench's timed window is the last long one
+        # before eval): steps, run span from the sort's start, sort time and median step span
+        if starts:
+            closers = set(idx) if trace else set()
+            lines += ["## Every run (graph replay) in order", "",
+                      "| run | steps | span us | sort+routing us | median step us | max step us |",
+                      "|---:|---:|---:|---:|---:|---:|"]
+            for n_, i in enumerate(starts):
+                hi = starts[n_ + 1] if n_ + 1 < len(starts) else len(rows)
+                ends, last = [], int(rows[i]["End_Timestamp"])
+                for k in range(i + 1, hi):
+                    if int(rows[k]["Start_Timestamp"]) - last > 1_000_000:
+                        break                      # an idle gap: the run has ended
+                    last = max(last, int(rows[k]["End_Timestamp"]))
+                    if k in closers:
+                        ends.append(int(rows[k]["End_Timestamp"]))
+                if not ends:
+                    continue
+                j = next((k for k in range(i + 1, hi) if rows[k]["Kernel_Name"].startswith("void tower_kernel")), i)
+                st = [b - a for a, b in zip(ends, ends[1:])]
+                st.sort()
+                lines.append(f"| {n_} | {len(ends)} | {(ends[-1] - int(rows[i]['Start_Timestamp'])) / 1e3:.1f} | "
+                             f"{(int(rows[j]['Start_Timestamp']) - int(rows[i]['Start_Timestamp'])) / 1e3:.1f} | "
+                             f"{(st[len(st) // 2] / 1e3) if st else 0:.1f} | {(st[-1] / 1e3) if st else 0:.1f} |")
+            lines.append("")
     open(out, "w").write("\n".join(lines) + "\n")
     print(out)
 
