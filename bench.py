@@ -311,7 +311,7 @@ def main():
         # the warm-up captured its own first run right before the timed window, and the GPU,
         # idle during that capture, ran the short 20-step window 0.160-0.173 ms/step instead of
         # 0.116-0.117 in about half the runs.)
-        model.train_step(*pool[0], use_graph=True, next_ids=(pool[1 % P][0], pool[2 % P][0]))
+        model.warm_step(*pool[0])
         # every graph the warm-up and timed runs replay is captured here first (real steps)
         run(0, args.warmup + args.steps)
         # the sorted-slot (2) and routing (3, row-sharded) sets rotate step by step: padding the

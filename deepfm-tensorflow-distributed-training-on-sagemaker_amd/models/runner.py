@@ -391,13 +391,21 @@ class GraphRunnerMixin:
             self._host_step += G
         return G
 
+    def warm_step(self, ids, vals, labels) -> int:
+        """One eager training step that warms up lazy library state; afterwards every step or
+        run is captured at its first use (no eager first step inside ``train_steps``)."""
+        B = self.train_step(ids, vals, labels, use_graph=False)
+        torch.cuda.synchronize()
+        self._warm = True
+        return B
+
     def _replay_graph(self, key, B: int):
         g = self._graphs.get(key)
         if g is None:
             # The very first step runs eagerly (it is a real step and warms up lazy library
             # state), then it is captured (capture records, it does not execute); every later
             # step of the same input binding is one graph replay.
-            if not self._graphs:
+            if not self._graphs and not getattr(self, "_warm", False):
                 self.train_step_enqueue(B)
                 torch.cuda.synchronize()
                 g = torch.cuda.CUDAGraph()
