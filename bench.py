@@ -307,19 +307,15 @@ def main():
 
     if use_graph and (comm is None or comm.graph_safe):
         # the model's very first step runs eagerly (it warms up lazy library state); taking it
-        # here lets the pass below capture EVERY run the warm-up and timed windows replay.  (Else
-        # the warm-up captured its own first run right before the timed window, and the GPU,
-        # idle during that capture, ran the short 20-step window 0.160-0.173 ms/step instead of
-        # 0.116-0.117 in about half the runs.)
+        # here lets the pass below capture EVERY run the warm-up and timed windows replay (else
+        # the warm-up captured its own first run right before the timed window)
         model.warm_step(*pool[0])
-        # every graph the warm-up and timed runs replay is captured here first (real steps)
+        # every graph the warm-up and timed runs replay is captured here first (real steps), from
+        # the same canonical plan state (nothing prefetched, set rotation at 0) the warm-up below
+        # starts from: its runs and the timed runs then find their graphs under the same keys
+        model.reset_plan_state()
         run(0, args.warmup + args.steps)
-        # the sorted-slot (2) and routing (3, row-sharded) sets rotate step by step: padding the
-        # steps before the warm-up to a multiple of their period keeps every run's set phase
-        # equal to its phase at capture (else the timed window re-captures graphs)
-        for j in range(-(1 + args.warmup + args.steps) % model.plan_period):
-            model.train_step(*pool[j % P], use_graph=use_graph,
-                             next_ids=(pool[(j + 1) % P][0], pool[(j + 2) % P][0]))
+        model.reset_plan_state()
         torch.cuda.synchronize()
     _progress()
     # every long-lived object exists now (model, pool, captured graphs and their plans): move them

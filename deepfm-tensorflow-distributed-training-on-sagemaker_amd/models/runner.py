@@ -391,6 +391,16 @@ class GraphRunnerMixin:
             self._host_step += G
         return G
 
+    def reset_plan_state(self):
+        """Drop every prefetched sort / routing set and restart the set rotation (host-synchronous;
+        no buffer is touched: the next step just sorts / routes its batch itself).  A caller that
+        replays captured runs calls it before capturing them and before replaying them, so every
+        run finds its graph under the plan state it was captured in."""
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        sh = None if self.shx is None else (0, [(None, None)] * len(self.shx.sets))
+        self._set_plan_state((0, [None, None], sh, list(getattr(self, "_stamp_n", []))))
+
     def warm_step(self, ids, vals, labels) -> int:
         """One eager training step that warms up lazy library state; afterwards every step or
         run is captured at its first use (no eager first step inside ``train_steps``)."""
