@@ -129,3 +129,40 @@ def test_growing_runs_keep_earlier_graphs_valid(monkeypatch):
         del m
     for i, (x, y) in enumerate(zip(*out)):
         assert torch.equal(x, y), (i, (x.float() - y.float()).abs().max().item())
+
+
+@pytest.mark.parametrize("run", [True, False])
+def test_reset_plan_state_replays_without_recapture(monkeypatch, run):
+    """bench's capture pass and its warm-up / timed windows start from ``reset_plan_state``: the
+    second pass over the same runs replays every graph (no capture) and trains bitwise like
+    eager single steps over the same batches."""
+    monkeypatch.setattr(D, "_RUN_SORT", run)
+    synth = make_synth("criteo_kaggle", seed=37)
+    B, K, layers = 1024, 8, [128, 64, 32]
+    params = init_params(synth.feature_size, synth.F, K, layers, False, seed=7)
+    pool = [synth.batch(B, step=s, device=DEV, id_dtype=torch.int32) for s in range(6)]
+    seq = [pool[0]] + pool + pool
+    out = []
+    for graphs in (True, False):
+        m = NativeDeepFM(synth.feature_size, synth.F, K, layers, [0.5] * 3, batch_size=B, device=DEV,
+                         init=False, field_ranges=synth.field_ranges())
+        m.load_tf_params(params)
+        if graphs:
+            m.warm_step(*pool[0])
+            for p in range(2):
+                m.reset_plan_state()
+                n0 = len(m._graphs)
+                m.train_steps(pool[:3], next_ids=(pool[3][0], pool[4][0]))
+                m.train_steps(pool[3:], next_ids=(pool[0][0], pool[1][0]))
+                if p:
+                    assert len(m._graphs) == n0           # replays only
+        else:
+            for b in seq:
+                m.train_step(*b, use_graph=False)
+        torch.cuda.synchronize()
+        m.check_errors()
+        assert m.global_step() == len(seq)
+        out.append([m.tv.clone(), m.tw.clone(), m.p.clone(), m.step.clone()] + [s.clone() for s in m.sv if s.numel()])
+        del m
+    for i, (x, y) in enumerate(zip(*out)):
+        assert torch.equal(x, y), (i, (x.float() - y.float()).abs().max().item())
