@@ -396,6 +396,8 @@ class GraphRunnerMixin:
         no buffer is touched: the next step just sorts / routes its batch itself).  A caller that
         replays captured runs calls it before capturing them and before replaying them, so every
         run finds its graph under the plan state it was captured in."""
+        if self.shx is not None:
+            self.shx.invalidate()            # (clears the tables of sets served ahead)
         if self.device.type == "cuda":
             torch.cuda.synchronize(self.device)
         sh = None if self.shx is None else (0, [(None, None)] * len(self.shx.sets))

@@ -348,8 +348,16 @@ class FixedCapacityExchange:
         self.cur = (c + 1) % self.NSETS
 
     def invalidate(self):
-        """Forget every prefetched set (after an out-of-band use of the exchange, e.g. predict)."""
+        """Forget every prefetched set (after an out-of-band use of the exchange, e.g. predict).
+        A set served ahead holds request-table stamps of the NEXT step number for a batch that may
+        now not be stepped: its table is cleared, or a different batch routed through it at that
+        step would find stale requesters stamped current (wrong gradient sums on the owner).
+        (Not inside a capture: a run graph's own steps move the step number past those stamps.)"""
+        capturing = self.m.device.type == "cuda" and torch.cuda.is_current_stream_capturing()
         for rs in self.sets:
+            if rs.stage == _SERVED and not capturing:
+                rs.req_key.zero_()
+                rs.req_pos.zero_()
             rs.key = rs.stage = None
 
     def drop_served(self):
