@@ -398,6 +398,12 @@ class GraphRunnerMixin:
         run finds its graph under the plan state it was captured in."""
         if self.shx is not None:
             self.shx.invalidate()            # (clears the tables of sets served ahead)
+        if getattr(self, "tf1_split", False):
+            # tf1_dense split form: clear the row flags a dropped prefetched sort stamped
+            for c in (0, 1):
+                if self._stamp_n[c]:
+                    KN.stamp_rows(self._ss[c][0], self._stamp_n[c], self.row_div, self._row_flags[c], 0)
+                    self._stamp_n[c] = 0
         if self.device.type == "cuda":
             torch.cuda.synchronize(self.device)
         sh = None if self.shx is None else (0, [(None, None)] * len(self.shx.sets))

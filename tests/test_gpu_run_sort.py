@@ -131,8 +131,8 @@ def test_growing_runs_keep_earlier_graphs_valid(monkeypatch):
         assert torch.equal(x, y), (i, (x.float() - y.float()).abs().max().item())
 
 
-@pytest.mark.parametrize("run", [True, False])
-def test_reset_plan_state_replays_without_recapture(monkeypatch, run):
+@pytest.mark.parametrize("run,update", [(True, "lazy"), (False, "lazy"), (False, "tf1_dense")])
+def test_reset_plan_state_replays_without_recapture(monkeypatch, run, update):
     """bench's capture pass and its warm-up / timed windows start from ``reset_plan_state``: the
     second pass over the same runs replays every graph (no capture) and trains bitwise like
     eager single steps over the same batches."""
@@ -145,10 +145,12 @@ def test_reset_plan_state_replays_without_recapture(monkeypatch, run):
     out = []
     for graphs in (True, False):
         m = NativeDeepFM(synth.feature_size, synth.F, K, layers, [0.5] * 3, batch_size=B, device=DEV,
-                         init=False, field_ranges=synth.field_ranges())
+                         init=False, field_ranges=synth.field_ranges(), sparse_update=update)
         m.load_tf_params(params)
         if graphs:
             m.warm_step(*pool[0])
+            if run:
+                assert m._run_sort_ok(pool[:3])
             for p in range(2):
                 m.reset_plan_state()
                 n0 = len(m._graphs)
