@@ -340,6 +340,10 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    if os.environ.get("HIPFM_BENCH_STAMPS") and rank == 0:
+        # diagnostic stamp build: per-workgroup phase stamps of the last timed step (tools/stamps.py)
+        from hipfm.ops._lib import dump_stamps
+        dump_stamps(os.environ["HIPFM_BENCH_STAMPS"])
     # graphs captured inside the timed window (should be 0: every run was captured before)
     timed_captures = len(model._graphs) - n_graphs
     if timed_captures and rank == 0:

@@ -18,6 +18,33 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 #define HFM_LAUNCH_CHECK() return (int)hipGetLastError()
 
+// ---- phase stamps (diagnostic build only: HIPFM_BUILD_STAMPS=1 compiles with -DHFM_STAMPS into
+// its own library; the production kernels contain none of this).  HFM_STAMP_BUF(name) defines a
+// per-translation-unit buffer of 100-MHz wall-clock stamps [slot][16] and C entry points
+// name_read / name_clear; HFM_STAMP(name, slot, k) has thread 0 of the workgroup record stamp k
+// of `slot` (a vector store from a VGPR; nothing in any kernel reads the buffer).
+#ifdef HFM_STAMPS
+#define HFM_STAMP_SLOTS (1 << 16)
+#define HFM_STAMP_BUF(name)                                                                 \
+  __device__ unsigned long long name[HFM_STAMP_SLOTS * 16];                                \
+  HFM_API int name##_read(void* dst, size_t bytes) {                                        \
+    return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(name), bytes, 0, hipMemcpyDeviceToHost); \
+  }                                                                                         \
+  HFM_API int name##_slots() { return HFM_STAMP_SLOTS; }
+#define HFM_STAMP(name, slot, k)                                                            \
+  do {                                                                                      \
+    if (threadIdx.x == 0) {                                                                 \
+      volatile unsigned long long t = __builtin_amdgcn_s_memrealtime();                     \
+      name[((unsigned)(slot) % HFM_STAMP_SLOTS) * 16 + (k)] = t + threadIdx.x;              \
+    }                                                                                       \
+  } while (0)
+#else
+#define HFM_STAMP_BUF(name)
+#define HFM_STAMP(name, slot, k) \
+  do {                           \
+  } while (0)
+#endif
+
 // ---- counter-based RNG (mirrors hipfm/utils/rng.py bit-for-bit) ----
 __device__ __forceinline__ uint32_t fmix32(uint32_t h) {
   h ^= h >> 16;

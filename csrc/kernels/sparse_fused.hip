@@ -225,6 +225,9 @@ struct SfSmem {
   float own_lead[SfCfg<K>::C];
 };
 
+HFM_STAMP_BUF(hfm_st_sf)
+#define SF_ST(k) HFM_STAMP(hfm_st_sf, blockIdx.x, k)
+
 // tile `tile` of the sparse backward (the sf_tile_kernel workgroup, or one of sfwg_kernel's)
 template <int K, int MODE, int OPT>
 __device__ __forceinline__ void sf_tile_body(const SfArgs& A, const int tile, SfSmem<K>& sm) {
@@ -250,6 +253,7 @@ __device__ __forceinline__ void sf_tile_body(const SfArgs& A, const int tile, Sf
   const int prev_key = b0 > 0 ? A.sorted_keys[b0 - 1] : -1;
   const int next_key = (b0 + nloc < A.n) ? A.sorted_keys[b0 + nloc] : -1;
   if (tid == 0) open_key_s = open_pos_s = -1;
+  SF_ST(0);
   // 1. per-slot contributions
 #pragma unroll
   for (int ps = 0; ps < T::PASSES; ++ps) {
@@ -274,6 +278,7 @@ __device__ __forceinline__ void sf_tile_body(const SfArgs& A, const int tile, Sf
     }
   }
   __syncthreads();
+  SF_ST(1);
   // head flags -> compacted head list (ascending), per-chunk head bits and first head (the
   // ballot of 64 consecutive slots holds the bits of 64 / CH whole chunks)
   static_assert(64 % CH == 0, "a chunk's slots sit in one wave's ballot");
@@ -296,6 +301,7 @@ __device__ __forceinline__ void sf_tile_body(const SfArgs& A, const int tile, Sf
     nh += wcount[0] + wcount[1] + wcount[2] + wcount[3];
     __syncthreads();
   }
+  SF_ST(2);
   // 2. chunk-local run pieces: in place at the head, leading piece into lead[j]
   for (int t = tid; t < T::NCH * T::C; t += 256) {
     const int j = t / T::C, c = t - j * T::C;
@@ -317,6 +323,7 @@ __device__ __forceinline__ void sf_tile_body(const SfArgs& A, const int tile, Sf
     else g[h][c] = s;
   }
   __syncthreads();
+  SF_ST(3);
   // tile leading piece (continuation of an earlier tile's run) + headless flag
   if (tid < T::C) {
     float s = 0.f;
@@ -368,6 +375,7 @@ __device__ __forceinline__ void sf_tile_body(const SfArgs& A, const int tile, Sf
     }
   }
   __syncthreads();
+  SF_ST(4);
   if (tid == 0) {
     hx_sti(A.tinfo + tile * 4 + 1, open_key_s);
     hx_sti(A.tinfo + tile * 4 + 2, open_pos_s);
@@ -376,10 +384,12 @@ __device__ __forceinline__ void sf_tile_body(const SfArgs& A, const int tile, Sf
   hx_drain();
   __syncthreads();
   if (tid == 0) hx_flag(A.flags + tile, tag);
+  SF_ST(5);
   // the leading piece continues an earlier run; it ends inside this tile (at the first head) or,
   // for a headless tile, at the tile's end when the next tile starts a new id (or there is none)
   const bool closes = nloc > 0 && skl[0] == prev_key && (nh > 0 || next_key != skl[nloc - 1]);
   if (closes && wv == 0) sf_lookback<K, MODE, OPT>(A, tile, tag, own_lead, lr_t);
+  SF_ST(6);
 }
 
 template <int K, int MODE, int OPT>
@@ -423,7 +433,9 @@ __global__ void __launch_bounds__(256) sfwg_kernel(SfArgs A, WgFinArgs W, unsign
   const int nw = W.tile_wgs + 1;
   const int ntile = (A.n + SfCfg<K>::TP - 1) / SfCfg<K>::TP;
   if ((int)blockIdx.x < nw) {
+    SF_ST(8);
     wgfin_body<OPT, SFWG_PF, SFWG_MAXNS, SFWG_TQ>(W, blockIdx.x, sm.wg);
+    SF_ST(9);
   } else if (!SWEEP || (int)blockIdx.x < nw + ntile) {
     sf_tile_body<K, 0, OPT>(A, (int)blockIdx.x - nw, sm.sf);
   } else if (SWEEP) {
@@ -442,6 +454,7 @@ __global__ void __launch_bounds__(256) sfwg_kernel(SfArgs A, WgFinArgs W, unsign
       if (SWEEP) *S.sw_step = t;      // keeps the branch sweep's counter in step
     }
   }
+  SF_ST(7);
 }
 
 template <int K, int OPT>

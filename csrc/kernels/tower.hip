@@ -96,6 +96,8 @@ struct TowerArgs {
 };
 
 constexpr int TW_STAMP_EPT = 16;  // sorted keys per thread of a stamp workgroup
+HFM_STAMP_BUF(hfm_st_tower)
+#define TW_ST(k) HFM_STAMP(hfm_st_tower, blockIdx.x, (k) < 15 ? (k) : 15)
 
 // fp8 variant of mma32 (16x16x32 fp8 MFMA; same fragment map as bf16 with 8 one-byte elements
 // per lane): A and B are e4m3 rows in global memory (row strides in bytes).
@@ -304,6 +306,7 @@ __global__ void __launch_bounds__(256) tower_kernel(TowerArgs a) {
     }
   }
   const int row0 = blockIdx.x * TW_ROWS;
+  TW_ST(0);
   const int cr = (lane >> 4) * 4, cc = lane & 15;
   const uint32_t step = (uint32_t)(*a.step);
   const int nl = a.nl;
@@ -315,7 +318,9 @@ __global__ void __launch_bounds__(256) tower_kernel(TowerArgs a) {
   if constexpr (KE > 0) {
     tower_gather<FP8, KE>(a, row0, Xl, ldx, X8, ld8, s_yfm, s_dq0);
     __syncthreads();
+    TW_ST(1);
     if (a.train) store_tile_t(Xl, ldx, a.K0p, a.Et, a.M, row0);
+    TW_ST(2);
   }
 
   // ------------------------------------------------------------------ forward
@@ -369,6 +374,7 @@ __global__ void __launch_bounds__(256) tower_kernel(TowerArgs a) {
       }
     }
     __syncthreads();
+    TW_ST(3 + i);
     if (a.train && a.Ht[i]) store_tile_t(Hl, ldh, N, a.Ht[i], a.M, row0);
     if (FP8 && i + 1 < nl) {  // per-row scales of H_i, the next layer's fp8 A operand
       const int r = tid >> 3, q8 = tid & 7;
@@ -458,8 +464,10 @@ __global__ void __launch_bounds__(256) tower_kernel(TowerArgs a) {
       part[c] = s;
     }
   }
+  TW_ST(7);
   if (!a.train) return;
   store_tile_t(lds + a.dz_off[0], L + 8, L, a.dZt[nl - 1], a.M, row0);
+  TW_ST(8);
 
   // ------------------------------------------------------------------ dgrad chain
   int cur = 0;
@@ -489,7 +497,9 @@ __global__ void __launch_bounds__(256) tower_kernel(TowerArgs a) {
       }
     }
     __syncthreads();
+    TW_ST(8 + 2 * (nl - i) - 1);
     store_tile_t(Zo, ldz_out, Nout, a.dZt[i - 1], a.M, row0);
+    TW_ST(8 + 2 * (nl - i));
     cur ^= 1;
   }
   {
@@ -513,6 +523,7 @@ __global__ void __launch_bounds__(256) tower_kernel(TowerArgs a) {
       }
     }
   }
+  TW_ST(15);
 }
 
 template <bool FP8>

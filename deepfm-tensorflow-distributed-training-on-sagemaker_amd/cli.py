@@ -155,6 +155,7 @@ def run(cfg: RunConfig) -> dict:
                         yield PositionedBatch(b, (epoch, k + 1) if nb is not None else (epoch + 1, 0))
                         k += 1
                         b = nb
+                    est.agree_cache(pipe)
                     est.adopt_field_ranges(pipe)
                     est.calibrate_exchange(pipe)
 
@@ -186,6 +187,7 @@ def run(cfg: RunConfig) -> dict:
                 est.train(_EpochView(pipe, epoch, est.epoch_batch), max_steps,
                           eval_fn=lambda: est.evaluate(va()))
                 est.epoch, est.epoch_batch = epoch + 1, 0
+                est.agree_cache(pipe)
                 est.adopt_field_ranges(pipe)
                 est.calibrate_exchange(pipe)
                 result = est.evaluate(va())
@@ -205,6 +207,11 @@ def run(cfg: RunConfig) -> dict:
                         n += 1
             result = {"pred_path": path, "rows": n}
             est.log.info(f"wrote {n} predictions to {path}")
+        elif est.forward_collective:
+            # row-sharded table: rank 0's test batches need every rank's rows (each forward is a
+            # collective); the other ranks serve them, batch for batch, and write nothing
+            for _ in est.predict([]):
+                pass
     if cfg.task_type in ("export", "train") and cfg.servable_model_dir:
         path = est.export(cfg.servable_model_dir)
         result["export_dir"] = path

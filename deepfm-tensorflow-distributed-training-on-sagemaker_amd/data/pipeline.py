@@ -312,6 +312,13 @@ class InputPipeline:
         if store is not None:
             self._cached = store
 
+    def drop_cache(self):
+        """Give the cached epoch back and stream every later epoch (a rank-agreed decision:
+        Estimator.agree_cache)."""
+        self._cached = None
+        self.cache_overflow = True
+        self.from_cache = False
+
     def field_minmax(self):
         """(per-field min ids, per-field max ids) over the first complete epoch as CPU int64
         tensors, or None before one was read."""

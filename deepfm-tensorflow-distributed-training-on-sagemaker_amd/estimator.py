@@ -422,6 +422,10 @@ class Estimator:
         wd.stop()
         return self.global_step - start_step
 
+    def agree_cache(self, pipeline) -> bool:
+        """See ``agree_cache`` (module level): keep the cached epoch only if every rank has one."""
+        return agree_cache(pipeline, self.world, self._ctl, self.log.info)
+
     def adopt_field_ranges(self, pipeline) -> bool:
         """After the first epoch was cached: per-field id ranges derived from it switch the slot
         sort to the per-field LDS sort (when the fields' ids are disjoint and increasing; with
@@ -486,10 +490,11 @@ class Estimator:
         hist = torch.zeros(2, 201, dtype=torch.int64, device=dev)
         loss_sum = torch.zeros(1, dtype=torch.float64, device=dev)
         n = torch.zeros(1, dtype=torch.float64, device=dev)
-        k = 0
-        for ids, vals, labels in batches:
-            if steps is not None and k >= steps:
-                break
+        for b in self._lockstep(batches, steps):
+            if b is None:                 # this rank's shard is done; the others' is not
+                self.model.join_forward()
+                continue
+            ids, vals, labels = b
             B = ids.shape[0]
             if self.native:
                 self.model.eval_batch(ids.to(dev), vals.to(dev), labels.to(dev), hist)
@@ -502,7 +507,6 @@ class Estimator:
                     _, data = self.model.loss(y, labels)
                     loss_sum += float(data) * B
             n += B
-            k += 1
         if _dist_on():
             dist.all_reduce(hist)
             dist.all_reduce(loss_sum)
@@ -534,8 +538,23 @@ class Estimator:
                 self._tb_eval = EventFileWriter(os.path.join(self.cfg.ckpt_dir, "eval"))
             self._tb_eval.scalars(step, values)
 
+    @property
+    def forward_collective(self) -> bool:
+        """Every rank must run each forward pass together (row-sharded table at N > 1)."""
+        return self.native and self.world > 1 and bool(getattr(self.model, "forward_collective", False))
+
+    def _lockstep(self, batches: Iterable, steps: Optional[int] = None) -> Iterator:
+        return lockstep_batches(batches, steps, self.forward_collective, self._ctl)
+
     def predict(self, batches: Iterable) -> Iterator[torch.Tensor]:
-        for ids, vals, _ in batches:
+        """Probabilities per batch.  Collective forward passes (row-sharded table at N > 1): call
+        it on EVERY rank -- ranks without batches (``[]``) join the others' passes and yield
+        nothing."""
+        for b in self._lockstep(batches):
+            if b is None:
+                self.model.join_forward()
+                continue
+            ids, vals, _ = b
             if self.native:
                 yield self.model.predict(ids.to(self.device), vals.to(self.device)).cpu()
             else:
@@ -630,6 +649,49 @@ class Estimator:
         return os.path.join(model_dir, name)
 
 
+def lockstep_batches(batches: Iterable, steps: Optional[int], collective: bool, group=None) -> Iterator:
+    """Batches of an evaluation / predict pass.  With ``collective`` forward passes (row-sharded
+    table at N > 1) the ranks vote before every batch (MAX over the host control ``group``: does
+    ANY rank still have one?) and a rank whose shard is exhausted gets ``None`` -- it joins that
+    batch's collectives with a dummy batch -- until every rank is done.  Shards of unequal length
+    (file-level sharding of va files, Pipe-mode evaluation read by rank 0 alone, predict on rank
+    0's test files) then never leave a rank waiting inside an all-to-all its peers never issue."""
+    it = iter(batches)
+    k = 0
+    while True:
+        b = next(it, None) if (steps is None or k < steps) else None
+        if collective:
+            t = torch.tensor([0 if b is None else 1], dtype=torch.int32)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+            if int(t.item()) == 0:
+                return
+        elif b is None:
+            return
+        k += 1
+        yield b
+
+
+def agree_cache(pipeline, world: int, group=None, log=None) -> bool:
+    """After an epoch that may have filled the HBM cache: every rank keeps its cache only if EVERY
+    rank has one (MIN over the host control ``group``).  Each rank checks its own shard against a
+    budget from its own device, so one rank can overflow while another caches; the step path
+    depends on the cache (captured multi-step runs with run-level routing vs staged single steps),
+    so mixed decisions would issue different collective sequences on the shared communicator.
+    Returns True if this rank's cache stays."""
+    have = getattr(pipeline, "_cached", None) is not None
+    if world == 1:
+        return have
+    t = torch.tensor([1 if have else 0], dtype=torch.int64)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+    if int(t.item()) == 1:
+        return True
+    if have and log is not None:
+        log("another rank's epoch outgrew its cache budget: every rank streams")
+    if hasattr(pipeline, "drop_cache"):
+        pipeline.drop_cache()
+    return False
+
+
 def _row_chunks(t: torch.Tensor, chunk_bytes: int = 1 << 28):
     """Row blocks of a tensor for the bundle writer; bf16 embedding rows (mixed precision) are
     upcast to the fp32 TF variables block by block."""
@@ -647,7 +709,7 @@ def _interleaved_chunks(parts, V: int, chunk_bytes: int = 1 << 28):
     N + rank), chunk by chunk on the device."""
     N = len(parts)
     R = parts[0].shape[0]
-    row_bytes = max(1, parts[0][0].numel() * parts[0].element_size())
+    row_bytes = max(1, parts[0][0].numel() * 4)        # blocks are upcast to fp32 below
     rows = max(1, chunk_bytes // (row_bytes * N))
     for a in range(0, R, rows):
         blk = torch.stack([p[a:a + rows].float() for p in parts], dim=1)

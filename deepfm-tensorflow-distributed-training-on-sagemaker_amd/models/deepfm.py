@@ -10,7 +10,6 @@ replayed), with the backward written out explicitly:
   K6 gemm(F32)     per layer: wgrad slabs (split over the batch)                  mlp.hip
   K6 gemm(DGRAD)   per layer: dZ_{i-1} = (dZ_i W_i) masked by H_{i-1} > 0         mlp.hip
   finalize         slab sums + bias row-sums -> flat dense gradient               mlp.hip
-  [dense all-reduce over RCCL, async, overlapped with the sparse backward]
   K3 sort          radix sort of the batch ids (hipCUB)                           sparse.hip
   K2 fm_bwd        per-slot embedding row gradients in sorted order               fm.hip
   K3 reduce        reduce-by-key -> one gradient row per unique id                sparse.hip
@@ -225,6 +224,9 @@ class NativeDeepFM(GraphRunnerMixin, NativeStateMixin):
         self.sharded = comm is not None and comm.sharded
         # multi-rank code path (also forced on a 1-rank group by tests: comm.force_exchange)
         self.exchange = comm is not None and (self.world > 1 or getattr(comm, "force_exchange", False))
+        if self.exchange and getattr(comm, "engine", None) is None:
+            raise ValueError("a multi-rank NativeDeepFM needs the native RCCL engine (parallel.dist.Comm "
+                             "on an RCCL process group)")
         # local rows of the embedding tables (row-sharded: id -> rank id % N, row id // N)
         self.R = (self.V + self.world - 1) // self.world if self.sharded else self.V
         self.row_div = self.world if self.sharded else 1
@@ -566,6 +568,7 @@ class NativeDeepFM(GraphRunnerMixin, NativeStateMixin):
             self._build_wgfin()
         self._bufs_M = M
         self.shx = None
+        self._shx_eval = None
         self.rpx = None
         if self.sharded and getattr(self.comm, "engine", None) is not None:
             from ..parallel.sharded import FixedCapacityExchange
@@ -609,7 +612,13 @@ class NativeDeepFM(GraphRunnerMixin, NativeStateMixin):
         self.comm.capacity = int(capacity)
         if self.shx is not None:
             from ..parallel.sharded import FixedCapacityExchange
+            old = self.shx
             self.shx = FixedCapacityExchange(self, self.comm.engine, self.comm.capacity)
+            # the capacity was measured on training batches: evaluation / predict keep the larger
+            # exchange (same capacity on every rank: the uncalibrated default)
+            if self.shx.C < old.C and getattr(self, "_shx_eval", None) is None:
+                old.invalidate()
+                self._shx_eval = old
         elif self.rpx is not None:
             from ..parallel.replicated import ReplicatedExchange
             self.rpx = ReplicatedExchange(self, self.comm.engine, self.comm.capacity)
@@ -915,8 +924,6 @@ class NativeDeepFM(GraphRunnerMixin, NativeStateMixin):
         rows fetched from their owners (row-sharded)."""
         if self.shx is not None:
             return self.shx.fetch(self._shx_plan, train)
-        if self.sharded:
-            return self.comm.sharded_forward_gather(self, B)
         return self.idx, self.tv, self.tw
 
     def _fm_forward(self, B: int, train: bool):
@@ -1187,8 +1194,6 @@ class NativeDeepFM(GraphRunnerMixin, NativeStateMixin):
                               wgfin=self._wgfin_args(False) if self._sp.xfuse else None,
                               dense_ar=self.g if self._sp.exchange_allreduce else None)
             return None
-        if self.sharded:
-            return self.comm.sharded_backward(self, B, idx, tv)
         if not presorted:
             self._sort_slots(B)
         if self.rpx is not None:
@@ -1217,10 +1222,7 @@ class NativeDeepFM(GraphRunnerMixin, NativeStateMixin):
                 KN.seg_apply(self.K, KN.SEG_SCATTER, 0, A, n)
                 KN.dense_sweep(self.K, self.opt_id, self.R, self.tv, self.tw, self.Gv, self.Gw,
                                self.sv, self.h_sparse, self.step)
-            return None
-        self._segment_reduce(n, compact=True)
-        KN.seg_apply(self.K, KN.SEG_WRITE_UG, 0, self.seg_args(n, compact=True), n)
-        return self.comm.replicated_exchange(self, n)
+        raise RuntimeError("multi-rank step without its native exchange")
 
     def _segment_reduce(self, n: int, compact: bool):
         """Per-slot gradients + per-tile run sums (K2+K3).  compact: partials indexed by the
@@ -1232,15 +1234,6 @@ class NativeDeepFM(GraphRunnerMixin, NativeStateMixin):
             sid = self.sid_incl
         KN.fm_bwd_seg(self.K, self.sorted_keys, self.perm, sid, self.vals, self.dlogit, self.dX0,
                       self.S, n, self.F, self.K0p, self.G, self.cont)
-
-    def _sparse_update(self, ukeys, UG, num, max_n):
-        if self.sparse_update == "lazy":
-            KN.sparse_rows_update(self.K, self.opt_id, ukeys, UG, num, max_n, self.row_div, self.tv,
-                                  self.tw, self.sv, self.h_sparse, self.step)
-        else:
-            KN.scatter_rows(self.K, ukeys, UG, num, max_n, self.row_div, self.Gv, self.Gw)
-            KN.dense_sweep(self.K, self.opt_id, self.R, self.tv, self.tw, self.Gv, self.Gw, self.sv,
-                           self.h_sparse, self.step)
 
     # ------------------------------------------------------------------ public step API
     _knobs = staticmethod(step_knobs)
@@ -1344,33 +1337,24 @@ class NativeDeepFM(GraphRunnerMixin, NativeStateMixin):
             self._dense_opt()
         if sp.join_sort:
             main.wait_stream(self._side)
-        work = None
         if sp.dense_branch:
-            # weight gradients (+ the process-group all-reduce) beside the sparse backward
+            # weight gradients beside the sparse backward
             if self._comm_stream is None:
                 self._comm_stream = torch.cuda.Stream(self.device)
             self._comm_stream.wait_stream(main)
             with torch.cuda.stream(self._comm_stream):
                 self._dense_grads()
-                if sp.dense_allreduce:
-                    work = self.comm.allreduce_dense_async(self.g)
-        elif sp.dense_allreduce:
-            work = self.comm.allreduce_dense_async(self.g)
         # native exchange: the dense gradient's producer is joined right before the gradient
         # exchange group (parallel/sharded.py: one communicator, fixed order)
         cs = self._comm_stream if sp.dense_branch else None
         self._sh_join = (lambda: main.wait_stream(cs)) if cs is not None else None
         try:
-            out = self._sparse_backward(B, idx, tv, presorted=sp.presorted)
-            if out is not None:
-                self._sparse_update(*out)
+            self._sparse_backward(B, idx, tv, presorted=sp.presorted)
         finally:
             self._sp, self._last_plan = IDLE, sp
             self._sh_join = None
         if sp.dense_branch:
             main.wait_stream(self._comm_stream)
-        if work is not None:
-            self.comm.wait(work)
         if self.shx is not None:
             self.shx.end(self._shx_plan)
         if sp.w8_after_owner:
@@ -1460,16 +1444,44 @@ class NativeDeepFM(GraphRunnerMixin, NativeStateMixin):
             s = self.comm.allreduce_scalar(s)
         return float(self.l2 * 0.5 * s)
 
+    @property
+    def forward_collective(self) -> bool:
+        """Forward passes (evaluate / predict) issue collectives (the row-sharded table's id and
+        row all-to-alls): every rank has to join each one, batch for batch."""
+        return self.shx is not None and self.world > 1
+
     def predict_enqueue(self, B: int, with_labels: bool = False):
         if self.shx is not None:           # row-sharded: route this batch inline, then fetch
-            self._shx_plan = self.shx.plan(self.idx, B, None, resident=False)
-            self.shx.begin(self._shx_plan, B)
-            self._predict_body(B, with_labels)
-            self.shx.commit(self._shx_plan, self.idx, B, resident=False)
-            self.shx.invalidate()        # (it used a set a prefetched batch may have been in)
-            self._shx_plan = None
+            # evaluation / predict batches go through the full-capacity exchange when the training
+            # one was calibrated on the training epoch (an eval batch may have more unique ids)
+            train_x = self.shx
+            x = self._shx_eval if getattr(self, "_shx_eval", None) is not None else train_x
+            self.shx = x
+            try:
+                self._shx_plan = x.plan(self.idx, B, None, resident=False)
+                x.begin(self._shx_plan, B)
+                self._predict_body(B, with_labels)
+                x.commit(self._shx_plan, self.idx, B, resident=False)
+                x.invalidate()        # (it used a set a prefetched batch may have been in)
+            finally:
+                self.shx = train_x
+                self._shx_plan = None
+            if x is not train_x:
+                train_x.invalidate()
             return
         self._predict_body(B, with_labels)
+
+    def join_forward(self):
+        """A rank without a batch left joins the other ranks' forward collectives with a dummy
+        one-row batch whose outputs nobody reads (distributed evaluation / predict over shards of
+        unequal length)."""
+        d = getattr(self, "_dummy_in", None)
+        if d is None:
+            d = (torch.zeros(1, self.F, dtype=torch.int32, device=self.device),
+                 torch.zeros(1, self.F, dtype=torch.float32, device=self.device))
+            self._dummy_in = d
+        B = self.stage_batch(d[0], d[1], None)
+        self.predict_enqueue(B, with_labels=False)
 
     def _predict_body(self, B: int, with_labels: bool):
         if self.fused and self.gather_fused:

@@ -366,8 +366,12 @@ class GraphRunnerMixin:
             enqueue()
             self._ss_key = [None, None]
             return G
-        mkey = ("runsort",) + tuple((b[0].data_ptr(), b[0].stride(), b[1].data_ptr(), b[2].data_ptr(),
-                                     b[0].shape[0]) for b in batches)
+        # tf1_dense split form: every step of the run stamps the flag set _bind_step picks from the
+        # host stamp counts at the run's start (a set without stale stamps); part of the key, and
+        # a replay commits it like the capture did
+        tf1c = (0 if self._stamp_n[0] == 0 else 1) if self.tf1_split else None
+        mkey = ("runsort", tf1c) + tuple((b[0].data_ptr(), b[0].stride(), b[1].data_ptr(), b[2].data_ptr(),
+                                          b[0].shape[0]) for b in batches)
         g = self._graphs.get(mkey)
         if g is None and not self._graphs and not getattr(self, "_warm", False):
             # the model's very first step runs eagerly (warms up lazy library state)
@@ -386,6 +390,14 @@ class GraphRunnerMixin:
                 self._graphs.pop(next(iter(self._graphs)))
             self._graphs[mkey] = g
         g.replay()
+        # the host commit the captured steps made, applied again for THIS replay: no rotating
+        # routing set holds a prefetched batch any more (a set served ahead before the run would
+        # otherwise be matched by a later step and read rows served before the run's updates),
+        # and the run's flag set is swept clean
+        if routed:
+            self.shx.invalidate()
+        if tf1c is not None:
+            self._stamp_n[tf1c] = 0
         self._ss_key = [None, None]
         if self._host_step is not None:
             self._host_step += G

@@ -53,7 +53,7 @@ class ModeSpec:
     K: int
     fused: bool                # one-launch deep tower
     gather_fused: bool         # ... with the FM gather as its prologue
-    sharded: bool              # the legacy torch.distributed row-sharded path (comm.sharded_backward)
+    sharded: bool              # row-sharded table (owner = id % N)
     exchange: bool             # multi-rank (or forced) exchange of sparse gradients
     native_exchange: bool      # the exchange runs on the native fixed-capacity engine (shx / rpx)
     row_sharded: bool          # ... and it is the row-sharded one (shx; rpx: replicated table)
@@ -85,7 +85,6 @@ class StepPlan:
     fuse_opt: bool = False         # ... inside the finalize / wgfin launch
     sfwg: bool = False             # ... and that launch merged into the sparse backward
     dense_opt_after: bool = False  # dense optimizer launched at the end of the step
-    dense_allreduce: bool = False  # process-group all-reduce of the dense gradient (async)
     # native exchange
     xfuse: bool = False            # dense gradient from the sparse launch, all-gathered with the rows
     exchange_allreduce: bool = False  # dense gradient all-reduced inside the exchange group
@@ -147,7 +146,6 @@ def plan_step(mode: ModeSpec, kn: StepKnobs, B: int, sort_plan: Optional[Tuple],
     if merged and not sfwg:
         raise RuntimeError("tf1_dense merged sweep planned but the step took another path")
     ex_ar = mode.native_exchange and not xfuse
-    dense_ar = mode.exchange and not xfuse and not ex_ar
     sh_dense = mode.native_exchange and mode.lazy and kn.sh_apply_dense and not early
     return StepPlan(
         run_sorted=run, presorted=presorted, fork_sort=fork,
@@ -156,6 +154,6 @@ def plan_step(mode: ModeSpec, kn: StepKnobs, B: int, sort_plan: Optional[Tuple],
         tf1_merged=merged, tf1_branch=tf1 and not merged,
         tower_stamp=run and tf1 and mode.fused and mode.gather_fused,
         defer_wgrad=split or sfwg or xfuse, dense_branch=split, dense_early=early, fuse_opt=fuse_opt,
-        sfwg=sfwg, dense_opt_after=not sh_dense and not early, dense_allreduce=dense_ar,
+        sfwg=sfwg, dense_opt_after=not sh_dense and not early,
         xfuse=xfuse, exchange_allreduce=ex_ar, sh_apply_dense=sh_dense,
         w8_after_fin=mode.fp8 and fuse_opt and not kn.wgfin, w8_after_owner=mode.fp8 and sh_dense)

@@ -358,3 +358,29 @@ def stream_handle(stream=None) -> int:
 
 def ptr(t) -> int:
     return 0 if t is None else t.data_ptr()
+
+
+STAMP_BUFS = ("hfm_st_tower", "hfm_st_sf")
+
+
+def dump_stamps(path: str) -> bool:
+    """Diagnostic stamp build (HIPFM_BUILD_STAMPS=1): save every stamp buffer the loaded library
+    has ([slots, 16] uint64 100-MHz wall-clock stamps per workgroup) to ``path`` (.npz).  Returns
+    False for a production library (it has no stamp buffers)."""
+    import numpy as np
+    lib = get_lib()
+    out = {}
+    for name in STAMP_BUFS:
+        fn = getattr(lib, name + "_read", None)
+        if fn is None:
+            continue
+        slots = getattr(lib, name + "_slots")()
+        buf = np.zeros((slots, 16), dtype=np.uint64)
+        fn.argtypes = [c_void_p, C.c_size_t]
+        fn.restype = c_int
+        check(fn(buf.ctypes.data, buf.nbytes), name + "_read")
+        out[name] = buf
+    if not out:
+        return False
+    np.savez_compressed(path, **out)
+    return True

@@ -33,6 +33,12 @@ PACKED = knob("HIPFM_BUILD_PACKED") == "1"
 if PACKED:
     KERNELS_SO = os.path.join(LIB_DIR, "libhipfm_kernels_packed.so")
     BUILD_DIR = BUILD_DIR + "_packed"
+# diagnostic: per-workgroup phase stamps (HIPFM_BUILD_STAMPS=1 -> -DHFM_STAMPS, own objects and
+# library; tools/stamps.py loads it with HIPFM_KERNELS_SO and reads the stamp buffers)
+STAMPS = knob("HIPFM_BUILD_STAMPS") == "1"
+if STAMPS:
+    KERNELS_SO = os.path.join(LIB_DIR, "libhipfm_kernels_stamps.so")
+    BUILD_DIR = BUILD_DIR + "_stamps"
 IO_SO = os.path.join(LIB_DIR, "libhipfm_io.so")
 
 
@@ -94,6 +100,7 @@ def build_kernels(force: bool = False, jobs: int = 8, verbose: bool = False) -> 
     def cmd_of(s, o):
         return [hipcc, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17",
                 "-fvisibility=hidden", "-Wno-unused-result", *([] if PACKED else NO_PACKED_F32),
+                *(["-DHFM_STAMPS"] if STAMPS else []),
                 "-c", s, "-o", o]
 
     for s in srcs:

@@ -59,8 +59,6 @@ KNOBS: Dict[str, Knob] = {
     "HIPFM_SH_XFUSE": Knob("1", "variant", "row-sharded step: gradient rows + dense gradients in one "
                            "aggregated RCCL operation"),
     "HIPFM_SH_ROUTE2": Knob("1", "variant", "two-launch routing (0: segments + bucket kernels, oracle)"),
-    "HIPFM_SHARD_EXCHANGE": Knob("fixed", "variant", "fixed: fixed-capacity native RCCL exchange; "
-                                 "else the torch.distributed all-to-all-v path"),
     "HIPFM_TF1_SPLIT": Knob("1", "variant", "tf1_dense on one GPU: split form (0: gradient scatter + "
                             "full-table sweep, the oracle in tests/test_gpu_tf1.py)"),
     "HIPFM_SWEEP_MODE": Knob("auto", "variant", "tf1_dense split sweep: merged (workgroups of the "
@@ -83,6 +81,8 @@ KNOBS: Dict[str, Knob] = {
     "HIPFM_ARCH": Knob("gfx950", "harness", "offload arch of the HIP build"),
     "HIPFM_KERNELS_SO": Knob(None, "harness", "path of the kernel library (default: in-tree _lib)"),
     "HIPFM_BUILD_PACKED": Knob(None, "harness", "build: packed-FP32 ops on (own objects / library)"),
+    "HIPFM_BUILD_STAMPS": Knob(None, "harness", "build: per-workgroup phase stamps (own objects / library)"),
+    "HIPFM_BENCH_STAMPS": Knob(None, "harness", "bench: save the stamp build's phase stamps (.npz path)"),
     "HIPFM_PIPE_ROOT": Knob(None, "harness", "directory of SageMaker pipe-mode FIFOs (tests)"),
     "HIPFM_FAULT_STEP": Knob(None, "harness", "fault injection: step at which a rank dies"),
     "HIPFM_FAULT_RANK": Knob(None, "harness", "fault injection: the rank (default all)"),

@@ -1,4 +1,7 @@
-"""Row-sharded embedding routing (SURVEY P4 / §2.6 "row-sharded mode", BASELINE config #4).
+"""Test oracle: host-synchronous row-sharded embedding routing over torch.distributed (the
+algorithm of the native fixed-capacity exchange, parallel/sharded.py, in plain torch code with
+variable all-to-all splits).  Only the multi-process CPU tests use it (gloo); the package runs the
+native engine.  SURVEY P4 / §2.6 "row-sharded mode", BASELINE config #4.
 
 The reference spreads variables over Parameter-Server tasks and documents
 ``fixed_size_partitioner`` for big embeddings (DOC p.32); every step the workers pull rows over
@@ -13,9 +16,7 @@ the table in HBM, row-sharded over the ranks of one process group, synchronously
   backward: per-unique-id gradient rows -> all-to-all to the owners -> owner sums duplicates
             (ids requested by several ranks) -> row update on the owner only
 
-``Router`` is device-agnostic torch code (CPU/gloo in the tests, GPU/RCCL in
-``parallel.dist.Comm``), so the same routing logic is exercised by the multi-process CPU tests
-and by the MI355X executor.
+``Router`` is device-agnostic torch code; ``make_sharded_golden`` wraps the golden model with it.
 """
 from __future__ import annotations
 
@@ -108,7 +109,7 @@ def make_sharded_golden(*args, world: int, rank: int, group=None, **kw):
     """A GoldenDeepFM whose fm_w / fm_v (and their optimizer slots) hold only this rank's rows
     (ids r, r+N, ...), trained with the Router exchange — the algorithm of the MI355X sharded
     path in plain PyTorch (distributed logic tested without a cluster)."""
-    from ..models.reference import GoldenDeepFM
+    from hipfm.models.reference import GoldenDeepFM
 
     class ShardedGoldenDeepFM(GoldenDeepFM):
         def __init__(self):

@@ -46,7 +46,7 @@ def _worker_body(rank, world, port, mode, opt, update, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from hipfm.models.reference import GoldenDeepFM, init_params
-    from hipfm.parallel.embedding import make_sharded_golden
+    from sharded_oracle import make_sharded_golden
     params = init_params(V, F, K, LAYERS, False, seed=9)
     kw = dict(keep_probs=[1.0], optimizer=opt, sparse_update=update, learning_rate=0.01, params=params)
     B = 32
@@ -286,3 +286,53 @@ def test_field_ranges_agreed_over_all_ranks_shards():
         assert "error" not in r, r.get("error")
     a, b = (r["ranges"] for r in sorted(res, key=lambda r: r["rank"]))
     assert a == b == [(0, 101), (101, 200), (200, 1000)]
+
+
+def _lockstep_worker(rank, world, port, lens, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from hipfm.estimator import agree_cache, lockstep_batches
+        seen = [b for b in lockstep_batches(list(range(lens[rank])), None, True)]
+        capped = [b for b in lockstep_batches(list(range(lens[rank])), 2, True)]
+
+        class _Pipe:                           # rank 0 alone outgrew its cache budget
+            def __init__(self, cached):
+                self._cached = [1] if cached else None
+                self.dropped = False
+
+            def drop_cache(self):
+                self._cached, self.dropped = None, True
+        p = _Pipe(cached=rank != 0)
+        kept = agree_cache(p, world)
+        q.put({"rank": rank, "seen": seen, "capped": capped, "kept": kept, "cached": p._cached})
+        dist.destroy_process_group()
+    except BaseException:
+        import traceback
+        q.put({"error": traceback.format_exc()})
+        raise
+
+
+def test_eval_lockstep_and_cache_agreement_unequal_shards():
+    """Distributed evaluation / predict over shards of unequal length (3 gloo ranks with 4, 1 and
+    0 batches): every rank takes the same number of steps -- exhausted ranks get None, the slot in
+    which they join the others' collective forward with a dummy batch -- and a rank alone over its
+    cache budget makes EVERY rank drop its cache (one collective sequence on the communicator)."""
+    world, lens = 3, [4, 1, 0]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_lockstep_worker, args=(r, world, port, lens, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in ps:
+        p.join(60)
+    for r in res:
+        assert "error" not in r, r.get("error")
+    for r in res:
+        n = lens[r["rank"]]
+        assert len(r["seen"]) == 4
+        assert r["seen"] == list(range(n)) + [None] * (4 - n)
+        assert len(r["capped"]) == 2
+        assert r["kept"] is False and r["cached"] is None

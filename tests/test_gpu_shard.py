@@ -560,3 +560,77 @@ def test_bf16_tables_through_the_exchanges(sharded):
     assert (d <= want.abs() * 2.0 ** -7 + 1e-8).float().mean().item() > 0.99
     assert (d <= want.abs() * 2.0 ** -5 + 1e-6).all()
     assert (models[0].p - ref.p).abs().max().item() <= 1e-3 * ref.p.abs().max().item()
+
+
+def test_sharded_eval_and_predict_unequal_shards():
+    """Evaluation / predict on a row-sharded table at N = 3 with shards of unequal length (ranks
+    with 3, 1 and 0 batches, as file-level sharding of va files or Pipe-mode evaluation gives):
+    ranks run in lockstep (Estimator.lockstep_batches) and a rank whose shard is done joins each
+    remaining forward with a dummy batch (join_forward).  No hang; the summed AUC histogram equals
+    that of one unsharded model over every batch, and rank 0's predictions -- the other ranks only
+    serving rows -- equal the unsharded model's."""
+    from hipfm.ops.metrics import auc_from_hist
+    synth = make_synth("criteo_kaggle", seed=4)
+    F, K, layers, keep, B, N = synth.F, 8, [64, 32], [0.5, 0.5], 256, 3
+    V = synth.feature_size
+    params = init_params(V, F, K, layers, False, seed=7)
+    data = [synth.batch(B - 32 * s, step=100 + s, device=DEV, id_dtype=torch.int32) for s in range(4)]
+    shards = [[data[0], data[1], data[3]], [data[2]], []]
+    ref = NativeDeepFM(V, F, K, layers, keep, batch_size=B, device=DEV, init=False,
+                       field_ranges=synth.field_ranges())
+    ref.load_tf_params(params)
+    h_ref = torch.zeros(2, 201, dtype=torch.int64, device=DEV)
+    for ids, vals, lab in data:
+        ref.eval_batch(ids, vals, lab, h_ref)
+    p_ref = [ref.predict(ids, vals) for ids, vals, _ in shards[0]]
+    hub = _Hub(N)
+    models = []
+    for r in range(N):
+        m = NativeDeepFM(V, F, K, layers, keep, batch_size=B, device=DEV, init=False, comm=MeshComm(hub, r),
+                         field_ranges=synth.field_ranges())
+        m.load_tf_params(params)
+        assert m.forward_collective
+        models.append(m)
+    hists = [torch.zeros(2, 201, dtype=torch.int64, device=DEV) for _ in range(N)]
+    preds = []
+    steps = max(len(s) for s in shards)
+    errs = []
+
+    def body(r):
+        try:
+            torch.cuda.set_device(0)
+            s = torch.cuda.Stream()
+            with torch.cuda.stream(s):
+                m = models[r]
+                for k in range(steps):                      # evaluate: every rank, lockstep
+                    if k < len(shards[r]):
+                        ids, vals, lab = shards[r][k]
+                        m.eval_batch(ids, vals, lab, hists[r])
+                    else:
+                        m.join_forward()
+                for k in range(len(shards[0])):             # predict: rank 0's batches only
+                    if r == 0:
+                        ids, vals, _ = shards[0][k]
+                        preds.append(m.predict(ids, vals))
+                    else:
+                        m.join_forward()
+            s.synchronize()
+        except BaseException as e:
+            errs.append(e)
+            for mm in models:
+                mm.comm.engine.hub.bar.abort()
+    th = [threading.Thread(target=body, args=(r,)) for r in range(N)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    if errs:
+        raise errs[0]
+    torch.cuda.synchronize()
+    for m in models:
+        m.check_errors()
+    h = sum(hists)
+    assert torch.equal(h, h_ref), (auc_from_hist(h.cpu()), auc_from_hist(h_ref.cpu()))
+    assert len(preds) == len(p_ref)
+    for a, b in zip(preds, p_ref):
+        assert torch.equal(a, b)

@@ -25,7 +25,6 @@ ONE_GPU = mode()
 ONE_GPU_TF1 = mode(lazy=False, tf1_split=True)
 ROW_SHARDED = mode(sharded=True, exchange=True, native_exchange=True, row_sharded=True)
 REPLICATED = mode(exchange=True, native_exchange=True)
-LEGACY_SHARDED = mode(sharded=True, exchange=True)
 PER_LAYER = mode(fused=False, gather_fused=False, fin_covers_all=False)     # batch norm
 
 
@@ -37,7 +36,7 @@ def test_one_gpu_run_sorted_is_tower_plus_sfwg():
     p = plan_step(ONE_GPU, StepKnobs(), 16384, RUN, tf1=False)
     assert p.run_sorted and p.presorted and not p.fork_sort and not p.prefetch_next
     assert p.sfwg and p.fuse_opt and p.dense_early and p.defer_wgrad
-    assert not (p.dense_branch or p.dense_opt_after or p.dense_allreduce or p.xfuse)
+    assert not (p.dense_branch or p.dense_opt_after or p.xfuse)
 
 
 def test_one_gpu_prefetched_and_inline_sorts():
@@ -68,16 +67,11 @@ def test_native_exchange_steps():
         # dense gradient from the sparse launch, all-gathered with the rows; dense optimizer in the
         # owner launch; no process-group all-reduce and no dense branch
         assert p.xfuse and p.sh_apply_dense and p.defer_wgrad
-        assert not (p.dense_allreduce or p.exchange_allreduce or p.dense_branch or p.dense_early or p.sfwg)
+        assert not (p.exchange_allreduce or p.dense_branch or p.dense_early or p.sfwg)
         tf1 = plan_step(mode(**{**m.__dict__, "lazy": False, "lazy_rows": False}), StepKnobs(), 16384, None,
                         tf1=False)
         assert tf1.exchange_allreduce and tf1.dense_branch and tf1.dense_opt_after and not tf1.xfuse
     assert not plan_step(ROW_SHARDED, StepKnobs(), 16384, INLINE, tf1=False).fork_sort
-
-
-def test_legacy_process_group_exchange_all_reduces():
-    p = plan_step(LEGACY_SHARDED, StepKnobs(), 4096, None, tf1=False)
-    assert p.dense_allreduce and p.dense_branch and p.dense_opt_after and not p.fork_sort
 
 
 def test_per_layer_tower_and_fp8_quantize_sites():
@@ -140,7 +134,6 @@ def test_plan_invariants_over_the_mode_matrix():
                         assert not p.tf1_merged or p.sfwg
                         assert not (p.tf1_merged and p.tf1_branch)
                         assert not p.xfuse or (m.native_exchange and p.sh_apply_dense and m.lazy)
-                        assert not p.dense_allreduce or (m.exchange and not m.native_exchange)
                         assert not p.exchange_allreduce or (m.native_exchange and not p.xfuse)
                         assert not p.sh_apply_dense or m.native_exchange
                         assert not (p.run_sorted and (p.fork_sort or p.prefetch_next))
