@@ -398,8 +398,7 @@ def main():
                 "per_gpu_batch": B,
                 "seq_len": None,
                 "fields": F,
-                "parallelism": f"dp{world}" + ("" if world == 1 else
-                                                f"+{'row-sharded' if comm.sharded else 'replicated'}-embedding"),
+                "parallelism": _parallelism(world, comm),
                 "optimizer": f"{args.optimizer} ({args.sparse_update})",
                 "hip_graph": use_graph,
                 "timed_graph_captures": timed_captures,
@@ -414,6 +413,13 @@ def main():
             "eval_auc": round(auc, 5),
             "train_loss": round(loss, 5),
         }
+        x = model.shx if model.shx is not None else model.rpx
+        if x is not None:
+            # modelled per-rank traffic of one step (fixed-capacity blocks): bytes sent to other
+            # ranks, and bytes the step's collectives deliver incl. the rank's own block
+            sb = x.step_bytes(G if use_graph else 0)
+            out["comm_bytes_per_step"] = sb["sent"]
+            out["comm_bytes_moved_per_step"] = sb["moved"]
         _emit(json.dumps(out))
     model.check_errors()
     if comm is not None:
@@ -422,6 +428,16 @@ def main():
         # (native RCCL communicators are left to process exit: ncclCommDestroy after graph
         # capture blocks on ROCm 7)
         dist.destroy_process_group()
+
+
+def _parallelism(world: int, comm) -> str:
+    """The config's parallelism label; a 1-rank run of the multi-GPU step says so (a proxy)."""
+    if comm is None:
+        return f"dp{world}"
+    emb = "row-sharded" if comm.sharded else "replicated"
+    if world == 1:
+        return f"dp1 (1-rank {emb}-exchange proxy)"
+    return f"dp{world}+{emb}-embedding"
 
 
 def infer_bench(args):
@@ -525,36 +541,55 @@ def data_bench(args):
     ingest = rows / (time.perf_counter() - t0)
     ld.close()
     _progress()
-    # 2. training through the Estimator (same code path as the CLI)
-    cfg = RunConfig(feature_size=synth.feature_size, field_size=F, embedding_size=args.embedding_size,
-                    batch_size=B, deep_layers=args.deep_layers, dropout=args.dropout,
-                    optimizer=args.optimizer, sparse_update=args.sparse_update, device="cuda",
-                    log_steps=0, mlp_dtype=args.mlp_dtype, watchdog_secs=0,
-                    graph_steps=args.graph_steps, num_threads=args.threads)
-    est = Estimator(cfg)
-    pipe = InputPipeline(files, F, B, 1, cache=True, device=est.device, id_dtype=torch.int32,
-                         threads=args.threads, seed=cfg.seed)
-    per_epoch = []
-    for e in range(args.epochs):
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        n = est.train(_EpochView(pipe, e))
-        torch.cuda.synchronize()
-        per_epoch.append((n, time.perf_counter() - t0))
-        if e == 0:
-            est.adopt_field_ranges(pipe)
-        _progress()
+    # 2. training through the Estimator (same code path as the CLI): the per-field vocabularies are
+    # the data's (--field_sizes), so epoch 0 already sorts per field; streamed epochs go through
+    # the staging ring as captured multi-step runs
+    fr = synth.field_ranges()
+    sizes = ",".join(str(hi - lo) for lo, hi in fr) if fr[0][0] == 0 and all(
+        fr[i][1] == fr[i + 1][0] for i in range(len(fr) - 1)) else ""
+
+    def train_arm(cache: bool):
+        cfg = RunConfig(feature_size=synth.feature_size, field_size=F, embedding_size=args.embedding_size,
+                        batch_size=B, deep_layers=args.deep_layers, dropout=args.dropout,
+                        optimizer=args.optimizer, sparse_update=args.sparse_update, device="cuda",
+                        log_steps=0, mlp_dtype=args.mlp_dtype, watchdog_secs=0, field_sizes=sizes,
+                        graph_steps=args.graph_steps, num_threads=args.threads)
+        est = Estimator(cfg)
+        pipe = InputPipeline(files, F, B, 1, cache=cache, device=est.device, id_dtype=torch.int32,
+                             threads=args.threads, seed=cfg.seed)
+        per_epoch = []
+        for e in range(args.epochs):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            n = est.train(_EpochView(pipe, e))
+            torch.cuda.synchronize()
+            per_epoch.append((n, time.perf_counter() - t0))
+            if e == 0:
+                est.adopt_field_ranges(pipe)
+            _progress()
+        return est, per_epoch
+
+    est_s, per_epoch_s = train_arm(cache=False)        # every epoch streamed from the files
+    sig_s = (est_s.model.p.double().sum().item(), est_s.model.rec.double().sum().item())
+    del est_s
+    torch.cuda.empty_cache()
+    est, per_epoch = train_arm(cache=True)              # epoch 0 streamed + cached, then replayed
+    sig = (est.model.p.double().sum().item(), est.model.rec.double().sum().item())
     ev = est.evaluate(InputPipeline(va, F, B, 1, device=est.device, id_dtype=torch.int32,
                                     shuffle_files=False, threads=args.threads)) if va else {"auc": None}
     sps = [n * B / t for n, t in per_epoch]
     steady = per_epoch[2:] if len(per_epoch) > 2 else per_epoch[-1:]
     steady_sps = sum(n for n, _ in steady) * B / sum(t for _, t in steady)
+    sps_s = [n * B / t for n, t in per_epoch_s]
     out = {"metric": "file-fed training samples/s (1 GPU) + host ingest rows/s",
            "value": round(steady_sps, 1), "unit": "samples/s", "n_gpus": 1,
            "ingest_rows_per_s": round(ingest, 1), "ingest_threads": args.threads, "rows": rows,
            "epoch_samples_per_s": [round(x, 1) for x in sps],
-           "epoch0": "streamed from files (pinned ring + copy stream) and cached in HBM",
+           "streamed_epoch_samples_per_s": [round(x, 1) for x in sps_s],
+           "streamed_bitwise_equal_cached": sig == sig_s,
+           "epoch0": "streamed from files (pinned ring + copy stream + staging ring of run graphs) and cached in HBM",
            "epoch1": "cache replay, graphs captured", "steady": "cache replay of captured graphs",
+           "streamed": "no cache: every epoch streamed through the staging ring",
            "graph_steps": args.graph_steps, "per_field_sort": est.model.field_ranges is not None,
            "eval_auc": None if ev["auc"] is None else round(ev["auc"], 5),
            "config": {"preset": args.preset, "batch": B, "K": args.embedding_size,

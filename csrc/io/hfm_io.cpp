@@ -24,10 +24,12 @@
 #include <atomic>
 #include <condition_variable>
 #include <deque>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
+#include <functional>
 #include <vector>
 
 #define HFMIO_API extern "C" __attribute__((visibility("default")))
@@ -352,6 +354,78 @@ struct WorkerQueue {
   std::string err;
 };
 
+// Parallel copy of one batch's chunk pieces into the caller's (pinned) buffers: a batch is 16+
+// pieces (1024-record chunks), each memcpy'd / narrowed by whichever pool thread takes it.  The
+// single consumer thread copying 5-10 MB per batch capped ingest below the decode workers' rate.
+class CopyPool {
+ public:
+  explicit CopyPool(int n) {
+    for (int i = 0; i < n; ++i) th_.emplace_back([this] { loop(); });
+  }
+  ~CopyPool() {
+    {
+      std::lock_guard<std::mutex> lk(m_);
+      quit_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+  int size() const { return (int)th_.size(); }
+  // run f(0..n-1) on the pool and the calling thread; returns when every call finished
+  void run(int n, std::function<void(int)> f) {
+    auto job = std::make_shared<Job>();
+    job->f = std::move(f);
+    job->n = n;
+    {
+      std::lock_guard<std::mutex> lk(m_);
+      cur_ = job;
+      ++gen_;
+    }
+    cv_.notify_all();
+    work(*job);
+    std::unique_lock<std::mutex> lk(job->m);
+    job->cv.wait(lk, [&] { return job->done == job->n; });
+  }
+
+ private:
+  struct Job {
+    std::function<void(int)> f;
+    int n = 0;
+    std::atomic<int> next{0};
+    std::mutex m;
+    std::condition_variable cv;
+    int done = 0;
+  };
+  static void work(Job& j) {
+    int i;
+    while ((i = j.next.fetch_add(1)) < j.n) {
+      j.f(i);
+      std::lock_guard<std::mutex> lk(j.m);
+      if (++j.done == j.n) j.cv.notify_all();
+    }
+  }
+  void loop() {
+    uint64_t seen = 0;
+    for (;;) {
+      std::shared_ptr<Job> j;
+      {
+        std::unique_lock<std::mutex> lk(m_);
+        cv_.wait(lk, [&] { return quit_ || gen_ != seen; });
+        if (quit_) return;
+        seen = gen_;
+        j = cur_;
+      }
+      work(*j);   // (a job this thread joins late just finds its pieces taken)
+    }
+  }
+  std::vector<std::thread> th_;
+  std::mutex m_;
+  std::condition_variable cv_;
+  std::shared_ptr<Job> cur_;
+  uint64_t gen_ = 0;
+  bool quit_ = false;
+};
+
 struct Loader {
   std::vector<std::string> paths;
   int format = 0, F = 0, B = 0, drop_remainder = 1, verify = 1;
@@ -367,6 +441,7 @@ struct Loader {
   std::unique_ptr<Chunk> cur;
   int cur_off = 0;
   std::string err;
+  std::unique_ptr<CopyPool> pool;            // parallel batch assembly (null: the consumer copies)
 
   void worker(int w, int W) {
     WorkerQueue& Q = *queues[w];
@@ -484,11 +559,19 @@ struct Loader {
 
   // returns rows written (B, or < B for the final partial batch), 0 at end, -1 error.
   // ids32 != null: ids are narrowed to int32 (the device id type) while copying, straight into
-  // the caller's (pinned) buffer; an id outside [0, 2^31) is an error.
+  // the caller's (pinned) buffer; an id outside [0, 2^31) is an error.  The batch is assembled
+  // from pieces (chunk, chunk row, batch row, rows) copied in parallel by the copy pool.
   int next(float* lab, int64_t* ids, float* vals, int32_t* ids32 = nullptr) {
+    struct Piece {
+      const Chunk* c;
+      int src, dst, k;
+    };
+    std::vector<Piece> pieces;
+    std::vector<std::unique_ptr<Chunk>> done_chunks;
     int got = 0;
     while (got < B) {
       if (!cur || cur_off >= cur->n) {
+        if (cur) done_chunks.push_back(std::move(cur));
         cur = take();
         cur_off = 0;
         if (!cur) {
@@ -497,29 +580,40 @@ struct Loader {
         }
       }
       int k = std::min(B - got, cur->n - cur_off);
-      memcpy(lab + got, cur->label.data() + cur_off, k * 4);
-      if (ids32) {
-        const int64_t* src = cur->ids.data() + (size_t)cur_off * F;
-        int32_t* dst = ids32 + (size_t)got * F;
-        const size_t m = (size_t)k * F;
-        int64_t bad = 0;
-        for (size_t i = 0; i < m; ++i) {
-          const int64_t v = src[i];
-          bad |= v >> 31;  // non-zero for negatives and ids >= 2^31
-          dst[i] = (int32_t)v;
-        }
-        if (bad) {
-          err = "feature id outside [0, 2^31) for the int32 device path";
-          return -1;
-        }
-      } else {
-        memcpy(ids + (size_t)got * F, cur->ids.data() + (size_t)cur_off * F, (size_t)k * F * 8);
-      }
-      memcpy(vals + (size_t)got * F, cur->vals.data() + (size_t)cur_off * F, (size_t)k * F * 4);
+      pieces.push_back({cur.get(), cur_off, got, k});
       got += k;
       cur_off += k;
     }
     if (got < B && drop_remainder) return 0;
+    std::atomic<int64_t> bad{0};
+    auto copy = [&](int pi) {
+      const Piece& p = pieces[pi];
+      memcpy(lab + p.dst, p.c->label.data() + p.src, p.k * 4);
+      const size_t m = (size_t)p.k * F;
+      if (ids32) {
+        const int64_t* src = p.c->ids.data() + (size_t)p.src * F;
+        int32_t* dst = ids32 + (size_t)p.dst * F;
+        int64_t b = 0;
+        for (size_t i = 0; i < m; ++i) {
+          const int64_t v = src[i];
+          b |= v >> 31;  // non-zero for negatives and ids >= 2^31
+          dst[i] = (int32_t)v;
+        }
+        if (b) bad.store(1);
+      } else {
+        memcpy(ids + (size_t)p.dst * F, p.c->ids.data() + (size_t)p.src * F, m * 8);
+      }
+      memcpy(vals + (size_t)p.dst * F, p.c->vals.data() + (size_t)p.src * F, m * 4);
+    };
+    if (pool && pieces.size() > 1) {
+      pool->run((int)pieces.size(), copy);
+    } else {
+      for (int i = 0; i < (int)pieces.size(); ++i) copy(i);
+    }
+    if (bad.load()) {
+      err = "feature id outside [0, 2^31) for the int32 device path";
+      return -1;
+    }
     return got;
   }
 
@@ -569,6 +663,12 @@ HFMIO_API int hfmio_loader_next32(void* h, float* labels, int32_t* ids, float* v
   int r = L->next(labels, nullptr, vals, ids);
   if (r < 0) set_err(L->err);
   return r;
+}
+
+// Assemble batches with n copy threads (the consumer plus n - 1 pool threads); 1: serial.
+HFMIO_API void hfmio_loader_set_copy_threads(void* h, int n) {
+  auto* L = (Loader*)h;
+  L->pool.reset(n > 1 ? new CopyPool(n - 1) : nullptr);
 }
 
 HFMIO_API void hfmio_loader_destroy(void* h) {

@@ -64,6 +64,15 @@ __device__ __forceinline__ bool dropout_keep(uint32_t flat, uint32_t salt, uint3
 __device__ __forceinline__ float bf2f(bf16 x) { return (float)x; }
 __device__ __forceinline__ bf16 f2bf(float x) { return (bf16)x; }
 
+// Per-slot embedding gradient terms of the FM + MLP backward (sparse_fused.hip derivation): for
+// slot (b, f) with value x, dX0 slice dx (bf16-rounded), dlogit dy and S_b = sum_f E:
+//   a = x * (dx + dy * S_b),  g_w = dy * x,  c = dy * x * x.
+// One definition for the sparse kernel's own gather and the tower's sorted-row emission, so the
+// two produce the same bits.
+__device__ __forceinline__ f32x4 sf_slot_a(f32x4 dx, float dy, f32x4 s, float x) { return (dx + dy * s) * x; }
+__device__ __forceinline__ float sf_slot_gw(float dy, float x) { return dy * x; }
+__device__ __forceinline__ float sf_slot_c(float dy, float x) { return dy * x * x; }
+
 // ---- embedding-table rows: fp32, or bf16 (mixed-precision embeddings, BASELINE config #5) ----
 // A row (or optimizer-slot row) starts at a float* inside the table record; a bf16 row holds its
 // K values in the first K/2 floats.  4 consecutive elements from element e (e % 4 == 0):

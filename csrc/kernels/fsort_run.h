@@ -56,6 +56,9 @@ struct FsJob {
   const int* mfields;  // fields that need the merge (bits > 0, B > FS2_MAXB)
   int nmf;
   int mwpf;          // merge workgroups per field (FSM_WPR per chunk run)
+  int* inv;          // [F][B] or null: sorted index of slot (b, f) at inv[f * B + b] (the inverse
+                     // of perm, field-major: each sort workgroup's writes stay inside its field's
+                     // B ints; the tower writes each slot's gradient row to its sorted position)
 };
 
 // one (field, chunk) work item; lds: FS2_LDS bytes.  The keys live in LDS between passes and
@@ -91,6 +94,7 @@ __device__ __forceinline__ void fs2_sort_item(const FsJob& J, int item, unsigned
         bad |= idv[k] != lo;
         sk[b] = idv[k];
         pk[b] = (row0 + b) * F + f;
+        if (J.inv) J.inv[(size_t)f * J.B + row0 + b] = f * J.B + row0 + b;
       }
     }
     if (__any(bad) && lane == 0) atomicOr(J.err, 1u);
@@ -205,6 +209,7 @@ __device__ __forceinline__ void fs2_sort_item(const FsJob& J, int item, unsigned
   for (int q = tid; q < B; q += FS2_THREADS) {  // sentinels sit past B
     sko[q] = lo + (int)lk[q];
     pko[q] = (row0 + (int)lv[q]) * F + f;
+    if (direct && J.inv) J.inv[(size_t)f * J.B + row0 + (int)lv[q]] = f * J.B + row0 + q;
   }
 }
 
@@ -270,6 +275,7 @@ __device__ __forceinline__ void fs2_merge_item(const FsJob& J, int wg, int* lds)
     if (e < clen) {
       sko[pos[j]] = k[j];
       pko[pos[j]] = rperm[c0 + e];
+      if (J.inv) J.inv[(size_t)f * B + rperm[c0 + e] / J.F] = f * B + pos[j];
     }
   }
 }

@@ -71,6 +71,10 @@ struct SfArgs {
   int v_by_key;     // MODE 2: 1 = V rows from the local table row key / row_div (replicated-table
                     // exchange), 0 = from the received rows at upos (row-sharded exchange)
   int vbf16;        // table v rows and v slots are bf16 (mixed-precision embeddings; MODE 0 / 2)
+  // or null: [n][K + 4] per-slot rows {a[K], g_w, c, 0, 0} already in SORTED order (written by the
+  // tower straight to each slot's sorted position): step 1 streams them instead of gathering
+  // perm -> vals / dlogit / S / dX0 per slot
+  const float* grow;
 };
 
 // MODE 0: lazy optimizer OPT on the row; 1: tf1_dense scatter of the row gradient;
@@ -255,6 +259,24 @@ __device__ __forceinline__ void sf_tile_body(const SfArgs& A, const int tile, Sf
   if (tid == 0) open_key_s = open_pos_s = -1;
   SF_ST(0);
   // 1. per-slot contributions
+  if (A.grow) {  // sorted rows from the tower: coalesced streams, no per-slot gather
+#pragma unroll
+    for (int ps = 0; ps < T::PASSES; ++ps) {
+      const int p = ps * T::PPP + tid / T::LPS;
+      if (p < nloc) {
+        const float* gr = A.grow + (size_t)(b0 + p) * T::RS;
+        const f32x4 av = *reinterpret_cast<const f32x4*>(gr + sub * 4);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) g[p][sub * 4 + j] = av[j];
+        if (sub == 0) {
+          const float2 wc = *reinterpret_cast<const float2*>(gr + K);
+          g[p][K] = wc.x;
+          g[p][K + 1] = wc.y;
+          skl[p] = A.sorted_keys[b0 + p];
+        }
+      }
+    }
+  } else {
 #pragma unroll
   for (int ps = 0; ps < T::PASSES; ++ps) {
     const int p = ps * T::PPP + tid / T::LPS;
@@ -267,15 +289,16 @@ __device__ __forceinline__ void sf_tile_body(const SfArgs& A, const int tile, Sf
       const f32x4 s = *reinterpret_cast<const f32x4*>(A.S + (size_t)b * K + sub * 4);
       const bf16x4 dxh = *reinterpret_cast<const bf16x4*>(A.dX0 + (size_t)b * A.KP + f * K + sub * 4);
       const f32x4 dx = {bf2f(dxh[0]), bf2f(dxh[1]), bf2f(dxh[2]), bf2f(dxh[3])};
-      const f32x4 av = (dx + dy * s) * x;
+      const f32x4 av = sf_slot_a(dx, dy, s, x);
 #pragma unroll
       for (int j = 0; j < 4; ++j) g[p][sub * 4 + j] = av[j];
       if (sub == 0) {
-        g[p][K] = dy * x;
-        g[p][K + 1] = dy * x * x;
+        g[p][K] = sf_slot_gw(dy, x);
+        g[p][K + 1] = sf_slot_c(dy, x);
         skl[p] = A.sorted_keys[i];
       }
     }
+  }
   }
   __syncthreads();
   SF_ST(1);

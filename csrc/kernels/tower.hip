@@ -93,7 +93,16 @@ struct TowerArgs {
   int stamp_wgs, stamp_n, stamp_div;
   const int* stamp_keys;
   unsigned char* stamp_flags;
+  // sorted gradient rows (bf16 gather tower, train, run-sorted step): every slot's embedding
+  // gradient row {a[K], g_w, c, 0, 0} is written to grow[inv[slot]] -- its SORTED position -- so
+  // the sparse backward streams them (no per-slot gather); dX0 / S are then not written.  g_off:
+  // LDS byte offset of the scratch [x 32 x F][S 32 x K][inv 32 x F][4 wave tiles 32 x 40 bf16].
+  float* grow;
+  const int* inv;   // [F][inv_ld] field-major sorted index of slot (b, f) (fsort_run.h FsJob.inv)
+  int g_off;
+  int inv_ld;
 };
+constexpr int TW_GINV = 8;  // inv entries prefetched per thread (32 F / 256 <= 8: F <= 64)
 
 constexpr int TW_STAMP_EPT = 16;  // sorted keys per thread of a stamp workgroup
 HFM_STAMP_BUF(hfm_st_tower)
@@ -186,9 +195,16 @@ __device__ __forceinline__ void store_tile_t(const bf16* t, int ld, int N, bf16*
 // FM gather of one 32-sample block (K1): 8 threads per sample, each owning fields q, q+8, ...;
 // E rows go to the bf16 LDS tile (and the fp8 tile), per-sample S / sum E^2 / y_w are summed in
 // registers over the thread's fields, then over its 8 lanes (fixed xor order: deterministic).
-template <bool FP8, int KE>
+struct TwNoHook {
+  __device__ void operator()() const {}
+};
+
+// ``hook()`` runs once, right after the first pass's table-row loads are issued (their HBM round
+// trip is the gather's longest wait: the tower issues its first GEMM's weight loads there)
+template <bool FP8, int KE, class Hook = TwNoHook>
 __device__ __forceinline__ void tower_gather(const TowerArgs& a, int row0, bf16* Xl, int ldx,
-                                             uint8_t* X8, int ld8, float* s_yfm, float* s_dq0) {
+                                             uint8_t* X8, int ld8, float* s_yfm, float* s_dq0,
+                                             float* gx = nullptr, float* gS = nullptr, Hook hook = Hook()) {
   constexpr int V4 = KE / 4;
   // fields per thread per pass, all loads in flight (Criteo: 39 <= 40); K = 32 rows are 8 f32x4
   // each, so fewer fields per pass keep the loads in registers
@@ -220,10 +236,12 @@ __device__ __forceinline__ void tower_gather(const TowerArgs& a, int row0, bf16*
       for (int j = 0; j < V4; ++j) v[t][j] = ok ? ld_row4(row, 4 * j, a.vbf16) : f32x4{0.f, 0.f, 0.f, 0.f};
       w[t] = ok ? a.tw[(size_t)id[t] * a.ldw] : 0.f;
     }
+    if (f0 == q) hook();
 #pragma unroll
     for (int t = 0; t < FMAX; ++t) {
       const int f = f0 + 8 * t;
       if (f >= F) break;
+      if (gx) gx[sl * F + f] = x[t];
       yw += w[t] * x[t];
 #pragma unroll
       for (int j = 0; j < V4; ++j) {
@@ -261,6 +279,10 @@ __device__ __forceinline__ void tower_gather(const TowerArgs& a, int row0, bf16*
 #pragma unroll
       for (int j = 0; j < V4; ++j) *reinterpret_cast<f32x4*>(a.S + (size_t)b * KE + 4 * j) = S[j];
     }
+    if (gS) {
+#pragma unroll
+      for (int j = 0; j < V4; ++j) *reinterpret_cast<f32x4*>(gS + sl * KE + 4 * j) = S[j];
+    }
   }
   if (FP8) {  // per-row power-of-two scale of the fp8 layer-0 operand (current scaling)
     const float qs = fp8_pow2_scale(am);
@@ -273,6 +295,341 @@ __device__ __forceinline__ void tower_gather(const TowerArgs& a, int row0, bf16*
           pack4_fp8(bf2f(e[0]) * qs, bf2f(e[1]) * qs, bf2f(e[2]) * qs, bf2f(e[3]) * qs);
     }
   }
+}
+
+// ---------------------------------------------------------------------------------------------
+// bf16 tower body (everything after the serve / stamp workgroup split).  Same math, same outputs,
+// bit for bit, as the generic body below; the difference is WHEN operands arrive: every GEMM
+// tile's weight fragments (and the forward bias, the head's w_out / labels) are loaded one phase
+// ahead -- the first tile's during the FM gather -- so no phase starts with an L2 round trip.
+// Phases: fwd 0..nl-1, dgrad nl-1..1, dX0 (tile ct of phase ph: tw_phase_b).
+// primed k-steps: K0p / 32 = 10 for Criteo at K = 8 (layer 0 entirely on registers); K = 32 rings
+// through 6 (two waves / SIMD need <= 256 registers)
+__host__ __device__ constexpr int tw_np(int KE) { return KE >= 16 ? 6 : (KE == 0 ? 4 : 10); }
+constexpr int TW_HQ = 8;   // head w_out values prefetched per thread (L / 8 <= 8)
+
+__device__ __forceinline__ int tw_nphase(const TowerArgs& a) { return a.train ? 2 * a.nl : a.nl; }
+
+// B operand / row stride / k-steps / tiles of phase ph (tile ct)
+struct TwPhase {
+  const bf16* B;
+  int ld, nk, ntile;
+};
+__device__ __forceinline__ TwPhase tw_phase_b(const TowerArgs& a, int ph, int ct) {
+  const int nl = a.nl;
+  TwPhase r;
+  if (ph < nl) {  // forward layer ph: H_ph = X W_ph^T
+    r.ld = ph == 0 ? a.K0p : a.Np[ph - 1];
+    r.ntile = a.Np[ph] / 32;
+    r.nk = r.ld / 32;
+    r.B = a.W[ph] + (size_t)ct * 32 * r.ld;
+    return r;
+  }
+  const int i = 2 * nl - 1 - ph;  // dgrad i (nl-1 .. 1), then dX0 (i = 0)
+  r.ld = a.Np[i];
+  r.nk = r.ld / 32;
+  r.ntile = i > 0 ? a.Np[i - 1] / 32 : a.K0p / 32;
+  r.B = a.WT[i] + (size_t)ct * 32 * r.ld;
+  return r;
+}
+
+// One dX0 tile (32 rows x 32 columns = 32 / K fields) -> the sorted gradient rows of its slots:
+// bf16-rounded dX0 (the values the unsorted path stores) staged in the wave's own LDS tile, then
+// a = x (dx + dy S), g_w, c per slot (sf_slot_*), written to grow[inv[slot]].  Wave-local: only
+// this wave reads its tile.
+template <int KE>
+__device__ __forceinline__ void tw_grow_tile(const TowerArgs& a, const f32x4 (&acc)[2][2], int ct, int row0, int lane,
+                                             bf16* wt, const float* gx, const float* gS, const int* ginv,
+                                             const float* s_dl) {
+  constexpr int FPT = 32 / KE, LPS = KE / 4, RS = KE + 4;
+  const int cr = (lane >> 4) * 4, cc = lane & 15, F = a.F;
+#pragma unroll
+  for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+    for (int tj = 0; tj < 2; ++tj)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) wt[(ti * 16 + cr + j) * 40 + tj * 16 + cc] = f2bf(acc[ti][tj][j]);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int t = lane + 64 * k;
+    const int sub = t % LPS, sl = t / LPS;
+    const int row = sl / FPT, fl = sl - row * FPT;
+    const int f = ct * FPT + fl;
+    if (f < F) {
+      const bf16x4 dxh = *reinterpret_cast<const bf16x4*>(wt + row * 40 + fl * KE + sub * 4);
+      const f32x4 dx = {bf2f(dxh[0]), bf2f(dxh[1]), bf2f(dxh[2]), bf2f(dxh[3])};
+      const f32x4 s = *reinterpret_cast<const f32x4*>(gS + row * KE + sub * 4);
+      const float x = gx[row * F + f], dy = s_dl[row];
+      float* gr = a.grow + (size_t)ginv[f * 32 + row] * RS;
+      *reinterpret_cast<f32x4*>(gr + sub * 4) = sf_slot_a(dx, dy, s, x);
+      if (sub == 0) *reinterpret_cast<f32x4*>(gr + KE) = f32x4{sf_slot_gw(dy, x), sf_slot_c(dy, x), 0.f, 0.f};
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int KE>
+__device__ __forceinline__ void tower_bf16_body(const TowerArgs& a, bf16* lds, float* s_dl, float* s_loss,
+                                                float* s_yfm) {
+  constexpr int TW_NP = tw_np(KE);
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int row0 = blockIdx.x * TW_ROWS;
+  const int cr = (lane >> 4) * 4, cc = lane & 15;
+  const int nl = a.nl, nph = tw_nphase(a);
+  bf16x8 pb0[TW_NP], pb1[TW_NP];
+  float pbias0 = 0.f, pbias1 = 0.f;
+  // prime the B fragments of (phase ph, tile ct) if that tile exists
+  auto prime = [&](int ph, int ct) __attribute__((always_inline)) {
+    if (ph >= nph) return;
+    const TwPhase q = tw_phase_b(a, ph, ct);
+    if (ct >= q.ntile) return;
+    bfrag_prime<TW_NP>(pb0, pb1, q.B, q.ld, q.nk, lane);
+    if (ph < nl) {
+      pbias0 = a.bias[ph][ct * 32 + cc];
+      pbias1 = a.bias[ph][ct * 32 + 16 + cc];
+    }
+  };
+  const uint32_t step = (uint32_t)(*a.step);
+  const int L = a.Np[nl - 1];
+  const int hrow = tid >> 3, hq = tid & 7, Q = L / 8;
+  const int ldx = a.K0p + 8;
+  bf16* Xl = lds + (KE > 0 ? a.x_off : 0);
+  // sorted gradient rows: LDS scratch and this block's inverse permutation (prefetched now)
+  const bool grow = KE > 0 && a.train && a.grow != nullptr;
+  float* gx = reinterpret_cast<float*>(reinterpret_cast<unsigned char*>(lds) + (grow ? a.g_off : 0));
+  float* gS = gx + TW_ROWS * a.F;
+  int* ginv = reinterpret_cast<int*>(gS + TW_ROWS * (KE > 0 ? KE : 1));
+  bf16* gwt = reinterpret_cast<bf16*>(ginv + TW_ROWS * a.F) + wave * TW_ROWS * 40;
+  int ivr[TW_GINV];
+  if constexpr (KE > 0) {
+    // (weights primed DURING the gather slowed it more than they saved: its table-row loads
+    // compete with them for the same address path)
+    tower_gather<false, KE>(a, row0, Xl, ldx, nullptr, 0, s_yfm, nullptr, grow ? gx : nullptr,
+                            grow ? gS : nullptr);
+    __syncthreads();
+    TW_ST(1);
+  }
+  // the head's operands, then (behind the E^T stores in the memory queue) the first GEMM tile's
+  // weights
+  float wo[TW_HQ];
+#pragma unroll
+  for (int j = 0; j < TW_HQ; ++j) wo[j] = j < Q ? a.w_out[hq * Q + j] : 0.f;
+  const float bout = a.b_out[0];
+  const bool hvalid = a.labels && row0 + hrow < a.nvalid;
+  const float hlab = hvalid ? a.labels[row0 + hrow] : 0.f;
+  const float yfm_g = KE > 0 ? 0.f : a.y_fm[row0 + hrow];
+  if constexpr (KE > 0) {
+    if (a.train) store_tile_t(Xl, ldx, a.K0p, a.Et, a.M, row0);
+    prime(0, wave);
+    TW_ST(2);
+  }
+  // ---------------------------------------------------------------- forward
+  for (int i = 0; i < nl; ++i) {
+    const int N = a.Np[i];
+    const int Kp = i == 0 ? a.K0p : a.Np[i - 1];
+    const int ldh = N + 8;
+    bf16* Hl = lds + a.h_off[i];
+    const bool drop = a.train && a.drop[i];
+    const uint32_t salt = drop ? dropout_salt(a.seed, step, (uint32_t)i) : 0u;
+    const float sc = a.inv_keep[i];
+    const bf16* Asrc = i == 0 ? (KE > 0 ? Xl : nullptr) : lds + a.h_off[i - 1];
+    const int lda = i == 0 ? ldx : Kp + 8;
+    for (int ct = wave; ct < N / 32; ct += 4) {
+      f32x4 c00 = {0, 0, 0, 0}, c01 = c00, c10 = c00, c11 = c00;
+      float bc[2];
+      if (KE == 0 && i == 0) {
+        mma32<TW_NP>(a.E + (size_t)row0 * a.K0p, a.K0p, a.W[0] + (size_t)ct * 32 * Kp, Kp, Kp / 32, lane, c00,
+                     c01, c10, c11);
+      } else if (i == 0) {  // layer 0 (the longest reduction): weights primed one tile ahead
+        mma32_primed<TW_NP>(Asrc, lda, a.W[0] + (size_t)ct * 32 * Kp, Kp, Kp / 32, lane, pb0, pb1, c00, c01,
+                            c10, c11);
+        bc[0] = pbias0;
+        bc[1] = pbias1;
+        if (ct + 4 < N / 32) prime(0, ct + 4);
+      } else {
+        // (priming the short layers' weights measured no faster: 2-4 k-steps, one L2 trip)
+        mma32<2>(Asrc, lda, a.W[i] + (size_t)ct * 32 * Kp, Kp, Kp / 32, lane, c00, c01, c10, c11);
+      }
+      if (KE == 0 || i > 0) {
+        bc[0] = a.bias[i][ct * 32 + cc];
+        bc[1] = a.bias[i][ct * 32 + 16 + cc];
+      }
+      f32x4 acc[2][2] = {{c00, c01}, {c10, c11}};
+#pragma unroll
+      for (int ti = 0; ti < 2; ++ti) {
+#pragma unroll
+        for (int tj = 0; tj < 2; ++tj) {
+          const int col = ct * 32 + tj * 16 + cc;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int row = ti * 16 + cr + j;
+            float v = fmaxf(acc[ti][tj][j] + bc[tj], 0.f);
+            if (drop)
+              v = dropout_keep((uint32_t)((row0 + row) * N + col), salt, a.keep_thr[i]) ? v * sc : 0.f;
+            Hl[row * ldh + col] = f2bf(v);
+          }
+        }
+      }
+    }
+    __syncthreads();
+    TW_ST(3 + i);
+    if (a.train && a.Ht[i]) store_tile_t(Hl, ldh, N, a.Ht[i], a.M, row0);
+  }
+  // ---------------------------------------------------------------- head
+  {
+    const bf16* H = lds + a.h_off[nl - 1];
+    const int ldh = L + 8;
+    const int grow = row0 + hrow;
+    float yd = 0.f;
+#pragma unroll
+    for (int j = 0; j < TW_HQ; ++j)
+      if (j < Q) yd += bf2f(H[hrow * ldh + hq * Q + j]) * wo[j];
+    for (int j = TW_HQ; j < Q; ++j) yd += bf2f(H[hrow * ldh + hq * Q + j]) * a.w_out[hq * Q + j];
+    yd += __shfl_xor(yd, 1, 64);
+    yd += __shfl_xor(yd, 2, 64);
+    yd += __shfl_xor(yd, 4, 64);
+    const float y = (KE > 0 ? s_yfm[hrow] : yfm_g) + yd + bout;
+    const float p = 1.f / (1.f + __expf(-y));
+    float dl = 0.f, lossb = 0.f;
+    if (hvalid) {
+      if (a.square_loss) {
+        lossb = (p - hlab) * (p - hlab);
+        dl = 2.f * (p - hlab) * p * (1.f - p) * a.gscale;
+      } else {
+        lossb = fmaxf(y, 0.f) - y * hlab + log1pf(__expf(-fabsf(y)));
+        dl = (p - hlab) * a.gscale;
+      }
+    }
+    if (hq == 0) {
+      if (KE > 0) a.y_fm[grow] = s_yfm[hrow];
+      a.prob[grow] = p;
+      s_dl[hrow] = dl;
+      s_loss[hrow] = lossb;
+      if (a.train) a.dlogit[grow] = dl;
+    }
+    if (a.train) {
+      bf16* Z = lds + a.dz_off[0];
+      const int ldz = L + 8;
+      const float sl = a.inv_keep[nl - 1];
+#pragma unroll
+      for (int j = 0; j < TW_HQ; ++j) {
+        if (j < Q) {
+          const int col = hq * Q + j;
+          const float g = bf2f(H[hrow * ldh + col]) > 0.f ? dl * wo[j] * sl : 0.f;
+          Z[hrow * ldz + col] = f2bf(g);
+        }
+      }
+      for (int j = TW_HQ; j < Q; ++j) {
+        const int col = hq * Q + j;
+        const float g = bf2f(H[hrow * ldh + col]) > 0.f ? dl * a.w_out[col] * sl : 0.f;
+        Z[hrow * ldz + col] = f2bf(g);
+      }
+    }
+    __syncthreads();
+    float* part = a.partial + (size_t)blockIdx.x * (L + 2);
+    for (int c = tid; c < L + 2; c += blockDim.x) {
+      float s = 0.f;
+      if (c < L) {
+        if (a.train)
+          for (int r = 0; r < TW_ROWS; ++r) s += s_dl[r] * bf2f(H[r * ldh + c]);
+      } else if (c == L) {
+        for (int r = 0; r < TW_ROWS; ++r) s += s_dl[r];
+      } else {
+        for (int r = 0; r < TW_ROWS; ++r) s += s_loss[r];
+      }
+      part[c] = s;
+    }
+  }
+  TW_ST(7);
+  if (!a.train) return;
+  store_tile_t(lds + a.dz_off[0], L + 8, L, a.dZt[nl - 1], a.M, row0);
+  TW_ST(8);
+  // ---------------------------------------------------------------- dgrad chain
+  if (grow) {  // this block's inverse permutation, for the dX0 phase's sorted rows
+#pragma unroll
+    for (int k = 0; k < TW_GINV; ++k) {  // block entry e = f * 32 + r (32 contiguous ints per field)
+      const int e = tid + 256 * k;
+      ivr[k] = e < TW_ROWS * a.F ? a.inv[(size_t)(e / TW_ROWS) * a.inv_ld + row0 + (e % TW_ROWS)] : 0;
+    }
+  }
+  if (nl == 1) prime(1, wave);
+  int cur = 0;
+  for (int i = nl - 1; i >= 1; --i) {
+    const int ph = 2 * nl - 1 - i;
+    const int Nout = a.Np[i - 1], Kin = a.Np[i];
+    const bf16* Az = lds + a.dz_off[cur];
+    bf16* Zo = lds + a.dz_off[cur ^ 1];
+    const bf16* Hp = lds + a.h_off[i - 1];
+    const int ldh = Nout + 8, ldz_in = Kin + 8, ldz_out = Nout + 8;
+    const float sc = a.inv_keep[i - 1];
+    for (int ct = wave; ct < Nout / 32; ct += 4) {
+      f32x4 c00 = {0, 0, 0, 0}, c01 = c00, c10 = c00, c11 = c00;
+      mma32<2>(Az, ldz_in, a.WT[i] + (size_t)ct * 32 * Kin, Kin, Kin / 32, lane, c00, c01, c10, c11);
+      if (i == 1) prime(ph + 1, wave);  // dX0's first tile: its weights while this epilogue runs
+      f32x4 acc[2][2] = {{c00, c01}, {c10, c11}};
+#pragma unroll
+      for (int ti = 0; ti < 2; ++ti) {
+#pragma unroll
+        for (int tj = 0; tj < 2; ++tj) {
+          const int col = ct * 32 + tj * 16 + cc;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int row = ti * 16 + cr + j;
+            const float v = bf2f(Hp[row * ldh + col]) > 0.f ? acc[ti][tj][j] * sc : 0.f;
+            Zo[row * ldz_out + col] = f2bf(v);
+          }
+        }
+      }
+    }
+    if (i == 1 && wave >= Nout / 32) prime(ph + 1, wave);
+    __syncthreads();
+    TW_ST(8 + 2 * (nl - i) - 1);
+    store_tile_t(Zo, ldz_out, Nout, a.dZt[i - 1], a.M, row0);
+    TW_ST(8 + 2 * (nl - i));
+    cur ^= 1;
+  }
+  {
+    const int N0 = a.Np[0];
+    const bf16* Az = lds + a.dz_off[cur];
+    const int ph = 2 * nl - 1;
+    if (grow) {
+#pragma unroll
+      for (int k = 0; k < TW_GINV; ++k) {
+        const int e = tid + 256 * k;
+        if (e < TW_ROWS * a.F) ginv[e] = ivr[k];
+      }
+      __syncthreads();
+    }
+    for (int ct = wave; ct < a.K0p / 32; ct += 4) {
+      f32x4 c00 = {0, 0, 0, 0}, c01 = c00, c10 = c00, c11 = c00;
+      mma32_primed<TW_NP>(Az, N0 + 8, a.WT[0] + (size_t)ct * 32 * N0, N0, N0 / 32, lane, pb0, pb1, c00, c01,
+                          c10, c11);
+      if (ct + 4 < a.K0p / 32) prime(ph, ct + 4);
+      f32x4 acc[2][2] = {{c00, c01}, {c10, c11}};
+      if (grow) {
+        if constexpr (KE > 0) tw_grow_tile<KE>(a, acc, ct, row0, lane, gwt, gx, gS, ginv, s_dl);
+        continue;
+      }
+#pragma unroll
+      for (int ti = 0; ti < 2; ++ti) {
+#pragma unroll
+        for (int tj = 0; tj < 2; ++tj) {
+          const int col = ct * 32 + tj * 16 + cc;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int rl = ti * 16 + cr + j;
+            a.dX0[(size_t)(row0 + rl) * a.K0p + col] = f2bf(acc[ti][tj][j]);
+          }
+        }
+      }
+    }
+  }
+  TW_ST(15);
 }
 
 template <bool FP8, int KE, int TW_PF0, int TW_PF1>
@@ -307,6 +664,10 @@ __global__ void __launch_bounds__(256) tower_kernel(TowerArgs a) {
   }
   const int row0 = blockIdx.x * TW_ROWS;
   TW_ST(0);
+  if constexpr (!FP8) {
+    tower_bf16_body<KE>(a, lds, s_dl, s_loss, s_yfm);
+    return;
+  }
   const int cr = (lane >> 4) * 4, cc = lane & 15;
   const uint32_t step = (uint32_t)(*a.step);
   const int nl = a.nl;
@@ -553,6 +914,9 @@ HFM_API int hfm_tower(const TowerArgs* ap, int KE, hipStream_t st) {
   if (a.serve_wgs < 0 || (a.serve_wgs && (!KE || !a.train || !a.sv.recv_ids || !a.sv.rows || !a.sv.step ||
                                           !a.sv.T.key || a.sv.C <= 0 || a.sv.stamp_off != 2 ||
                                           (long)a.serve_wgs * 256 < (long)a.sv.total * (KE / 4))))
+    return (int)hipErrorInvalidValue;
+  if (a.grow && (!KE || a.fp8 || !a.train || !a.inv || a.inv_ld < a.M || a.F > TW_GINV * 256 / TW_ROWS || a.g_off < 0 || (a.g_off & 15) ||
+                 KE > 16 || a.g_off + TW_ROWS * (8 * a.F + 4 * KE) + 4 * TW_ROWS * 40 * 2 > a.lds_bytes))
     return (int)hipErrorInvalidValue;
   if (a.stamp_wgs < 0 || (a.stamp_wgs && (!KE || !a.train || !a.stamp_keys || !a.stamp_flags || a.stamp_div <= 0 ||
                                           (long)a.stamp_wgs * 256 * TW_STAMP_EPT < a.stamp_n)))

@@ -342,9 +342,13 @@ class Estimator:
                 getattr(getattr(src, "pipe", None), "from_cache", False))
             run = [cur]
             nxt = self._next(it)
-            if self.native and use_graph and from_cache and gsteps > 1:
+            # streamed batches: a run of them is copied into a ring of static device buffers and
+            # trained as ONE captured multi-step graph keyed by the ring (run-level sort), replayed
+            # for every later run -- the cached epoch's fast path, without a cache
+            ring = self.native and use_graph and gsteps > 1 and not from_cache and self._ring_ok(cur)
+            if self.native and use_graph and gsteps > 1 and (from_cache or ring):
                 lim = gsteps if max_steps is None else min(gsteps, max_steps - self.global_step)
-                while len(run) < lim and nxt is not None:
+                while len(run) < lim and nxt is not None and (from_cache or self._ring_ok(nxt)):
                     run.append(nxt)
                     nxt = self._next(it)
             t0 = time.perf_counter()
@@ -356,10 +360,12 @@ class Estimator:
                     with prof_range("h2d"):
                         run = [tuple(x.to(self.device, non_blocking=True) for x in b) for b in run]
                     self.timer.add("h2d", time.perf_counter() - t1)
+                if ring and len(run) > 1:
+                    run = self._to_ring(run)
                 nxt_ids = nxt[0] if (nxt is not None and nxt[0].is_cuda) else None
                 with prof_range("step"):
                     if len(run) > 1:
-                        self.model.train_steps(run, next_ids=nxt_ids)
+                        self.model.train_steps(run, next_ids=None if ring else nxt_ids)
                     else:
                         ids, vals, labels = run[0]
                         # replayed cache batches: bound in place (one graph per batch); one-off
@@ -425,6 +431,30 @@ class Estimator:
     def agree_cache(self, pipeline) -> bool:
         """See ``agree_cache`` (module level): keep the cached epoch only if every rank has one."""
         return agree_cache(pipeline, self.world, self._ctl, self.log.info)
+
+    def _ring_ok(self, b) -> bool:
+        """A streamed batch can go through the staging ring: full batch of the model's size."""
+        return (b is not None and int(b[0].shape[0]) == self.model.M and b[0].dim() == 2 and
+                int(b[0].shape[1]) == self.cfg.field_size)
+
+    def _to_ring(self, run):
+        """Copy a run of streamed device batches into the staging ring (static buffers, so the
+        run's captured graph is found again by the next run).  Stream-ordered: a slot is
+        overwritten only after the previous run's graph, which read it, was enqueued."""
+        m = self.model
+        ring = getattr(self, "_ring", None)
+        G = max(1, int(getattr(self.cfg, "graph_steps", 1)))
+        if ring is None:
+            dev, M, F = self.device, m.M, self.cfg.field_size
+            ring = [(torch.empty(M, F, dtype=torch.int32, device=dev), torch.empty(M, F, dtype=torch.float32, device=dev),
+                     torch.empty(M, dtype=torch.float32, device=dev)) for _ in range(G)]
+            self._ring = ring
+        out = []
+        for slot, b in zip(ring, run):
+            for dst, src in zip(slot, b):
+                dst.copy_(src.reshape(dst.shape), non_blocking=True)
+            out.append(PositionedBatch(slot, b.pos) if hasattr(b, "pos") else slot)
+        return out
 
     def adopt_field_ranges(self, pipeline) -> bool:
         """After the first epoch was cached: per-field id ranges derived from it switch the slot

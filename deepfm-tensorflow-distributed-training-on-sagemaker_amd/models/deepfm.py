@@ -67,6 +67,9 @@ _SHX_FORK = knob("HIPFM_SHX_FORK")
 _SH_APPLY_DENSE = flag("HIPFM_SH_APPLY_DENSE")
 # ... and the dense gradient computed in the sparse launch, exchanged by all-gather (no all-reduce)
 _SH_XFUSE = flag("HIPFM_SH_XFUSE")
+# run-sorted single-GPU steps: the tower writes sorted per-slot gradient rows (0: the sparse launch
+# gathers vals / dlogit / S / dX0 per slot)
+_GROW = flag("HIPFM_GROW")
 # tf1_dense on one GPU: split sweep concurrent with the step (0: scatter + full-table sweep)
 _TF1_SPLIT = flag("HIPFM_TF1_SPLIT")
 _SWEEP_MODE = knob("HIPFM_SWEEP_MODE")      # auto | merged | branch
@@ -390,6 +393,10 @@ class NativeDeepFM(GraphRunnerMixin, NativeStateMixin):
         if self.emb_bf16 and not self.gather_fused:
             raise ValueError("emb_dtype=bf16 runs on the gather-fused tower (K in 4, 8, 16, 32; no "
                              "batch norm)")
+        # sorted gradient rows (run-sorted single-GPU steps): the bf16 gather tower writes every
+        # slot's embedding gradient row to its sorted position; the sparse launch streams them
+        self.grow_ok = (self.gather_fused and not self.fp8 and self.K in (4, 8, 16) and self.F <= 64 and
+                        _GROW and self._tower_grow_layout()[1] <= 150 * 1024)
         if init:
             if self.V * self.K <= (1 << 24):
                 # small tables: the exact golden initialization (CPU generator, bit-reproducible)
@@ -468,6 +475,13 @@ class NativeDeepFM(GraphRunnerMixin, NativeStateMixin):
     def _tower_lds_bytes(self) -> int:
         return self._tower_lds_layout()[4]
 
+    def _tower_grow_layout(self):
+        """(byte offset, total LDS bytes) of the tower's sorted-gradient-row scratch, appended to
+        the layout above: x [32][F] f32, S [32][K] f32, inverse perm [32][F] i32, 4 wave tiles
+        [32][40] bf16 (tower.hip tw_grow_tile)."""
+        g_off = (self._tower_lds_bytes() + 15) // 16 * 16
+        return g_off, g_off + 32 * (8 * self.F + 4 * self.K) + 4 * 32 * 40 * 2
+
     @staticmethod
     def _padM(B: int) -> int:
         return max(128, (B + 127) // 128 * 128)
@@ -497,6 +511,9 @@ class NativeDeepFM(GraphRunnerMixin, NativeStateMixin):
         self.dZ = [torch.zeros(M, n, **bf) for n in self.Np]
         self.dZt = [torch.zeros(n, M, **bf) for n in self.Np]
         self.dX0 = torch.zeros(M, K0p, **bf)            # layer-1 input gradient (bf16)
+        # per-slot gradient rows in sorted order (run-sorted steps, tower.hip tw_grow_tile)
+        self.grow = torch.zeros(M * F, K + 4, **f32) if getattr(self, "grow_ok", False) else None
+        self._grow_inv = None
         if self.batch_norm:
             self.Rb = [torch.zeros(M, n, **f32) for n in self.Np]         # relu output (pre-BN)
             self.dH = [torch.zeros(M, n, **f32) for n in self.Np]         # dL/d(layer output)
@@ -777,8 +794,9 @@ class NativeDeepFM(GraphRunnerMixin, NativeStateMixin):
         self._nwg_jobs = len(jobs)
         self._wg_tasks = task0
 
-    def _tower_args(self, B: int, train: bool, with_labels: bool = True, gather=None) -> TowerArgs:
-        """``gather`` = (idx, tv, tw): the tower's prologue gathers the FM rows itself."""
+    def _tower_args(self, B: int, train: bool, with_labels: bool = True, gather=None, grow_inv=None) -> TowerArgs:
+        """``gather`` = (idx, tv, tw): the tower's prologue gathers the FM rows itself.
+        ``grow_inv`` (the batch's inverse sort permutation): write sorted gradient rows."""
         a = TowerArgs()
         nl = len(self.layers)
         a.M, a.nvalid, a.nl, a.K0p = self.M, B, nl, self.K0p
@@ -821,6 +839,10 @@ class NativeDeepFM(GraphRunnerMixin, NativeStateMixin):
                 a.E8, a.sE = self.E8.data_ptr(), self.sE.data_ptr()
             for i in range(nl):
                 a.W8[i], a.sW[i] = self.W8[i].data_ptr(), self.sW[i].data_ptr()
+        if grow_inv is not None:
+            a.grow, a.inv, a.inv_ld = self.grow.data_ptr(), grow_inv.data_ptr(), B   # (run-sorted: B == M)
+            a.g_off, a.lds_bytes = self._tower_grow_layout()
+            a.S = 0                            # (the sparse launch reads the rows instead)
         a.seed = self.seed & 0xFFFFFFFF
         a.train = 1 if train else 0
         a.square_loss = 1 if self.loss_type == "square_loss" else 0
@@ -843,7 +865,8 @@ class NativeDeepFM(GraphRunnerMixin, NativeStateMixin):
         ``after_fm``: hook called once the FM forward is enqueued."""
         if self.fused and self.gather_fused:
             idx, tv, tw = self._fm_inputs(B, train=True)
-            ta = self._tower_args(B, train=True, gather=(idx, tv, tw))
+            ta = self._tower_args(B, train=True, gather=(idx, tv, tw),
+                                  grow_inv=self._grow_inv if self._sp.grow_rows else None)
             if self.shx is not None and self.shx.tower_serve is not None:
                 # run-routed step: the next step's rows served by extra tower workgroups
                 ta.sv, self.shx.tower_serve = self.shx.tower_serve, None
@@ -1181,6 +1204,7 @@ class NativeDeepFM(GraphRunnerMixin, NativeStateMixin):
         A.step_off = 0 if (self._sp.dense_early and not self._sp.sfwg) else 1
         A.flags, A.sync = self.sf_flags.data_ptr(), self.sf_sync.data_ptr()
         A.vbf16 = 1 if self.emb_bf16 else 0
+        A.grow = self.grow.data_ptr() if self._sp.grow_rows else 0
         return A
 
     def _sparse_backward(self, B: int, idx, tv, presorted: bool = False):
@@ -1222,6 +1246,7 @@ class NativeDeepFM(GraphRunnerMixin, NativeStateMixin):
                 KN.seg_apply(self.K, KN.SEG_SCATTER, 0, A, n)
                 KN.dense_sweep(self.K, self.opt_id, self.R, self.tv, self.tw, self.Gv, self.Gw,
                                self.sv, self.h_sparse, self.step)
+            return None
         raise RuntimeError("multi-rank step without its native exchange")
 
     def _segment_reduce(self, n: int, compact: bool):
@@ -1244,7 +1269,7 @@ class NativeDeepFM(GraphRunnerMixin, NativeStateMixin):
                         row_sharded=self.shx is not None, lazy_rows=self.lazy_rows,
                         lazy=self.sparse_update == "lazy", tf1_split=self.tf1_split, fp8=self.fp8,
                         wgfin_fits=getattr(self, "_wgfin_ns", 1 << 30) <= KN.SFWG_MAX_NS,
-                        fin_covers_all=self._fin_covers_all)
+                        fin_covers_all=self._fin_covers_all, grow_ok=self.grow is not None)
 
     def step_plan(self, B: int) -> StepPlan:
         """The plan (models/step_plan.py) of the step bound by ``_bind_step`` at batch size B."""
@@ -1270,7 +1295,7 @@ class NativeDeepFM(GraphRunnerMixin, NativeStateMixin):
             hooks.append(self.shx.fork_next)
         plan = self._sort_plan
         if sp.run_sorted:                                   # sorted at the start of the run
-            self.sorted_keys, self.perm = self._run_ss[plan[3]]
+            self.sorted_keys, self.perm, self._grow_inv = self._run_ss[plan[3]]
             if self._tf1_plan is not None:
                 flags = self._row_flags[self._tf1_plan[0]]
                 if sp.tower_stamp:      # stamped by extra workgroups of this step's tower launch
@@ -1476,9 +1501,12 @@ class NativeDeepFM(GraphRunnerMixin, NativeStateMixin):
         one-row batch whose outputs nobody reads (distributed evaluation / predict over shards of
         unequal length)."""
         d = getattr(self, "_dummy_in", None)
-        if d is None:
-            d = (torch.zeros(1, self.F, dtype=torch.int32, device=self.device),
-                 torch.zeros(1, self.F, dtype=torch.float32, device=self.device))
+        if d is None or d[2] != self.field_ranges:
+            # one valid id per field: the first id of its declared range (the per-field sort
+            # flags an id outside it)
+            lo = [r[0] for r in self.field_ranges] if self.field_ranges is not None else [0] * self.F
+            d = (torch.tensor([lo], dtype=torch.int32, device=self.device),
+                 torch.zeros(1, self.F, dtype=torch.float32, device=self.device), self.field_ranges)
             self._dummy_in = d
         B = self.stage_batch(d[0], d[1], None)
         self.predict_enqueue(B, with_labels=False)

@@ -323,10 +323,10 @@ class GraphRunnerMixin:
                 B <= min(self._fsort.max_rows, 8 * KN.fs2_chunk_rows()))
 
     def _run_sets(self, G: int):
+        """(sorted keys, perm, inverse perm) per step of a run-sorted graph."""
         n = self.M * self.F
         while len(self._run_ss) < G:
-            self._run_ss.append((torch.zeros(n, dtype=torch.int32, device=self.device),
-                                 torch.zeros(n, dtype=torch.int32, device=self.device)))
+            self._run_ss.append(tuple(torch.zeros(n, dtype=torch.int32, device=self.device) for _ in range(3)))
         return self._run_ss[:G]
 
     def _train_run_sorted(self, batches) -> int:
@@ -343,8 +343,10 @@ class GraphRunnerMixin:
             self.shx.route_run_prepare(rlist)           # allocations / device plans: not in a capture
         else:
             sets = self._run_sets(G)
+            # (the inverse permutation only where the tower writes sorted gradient rows)
             rplan = self._fsort_next.run_plan(
-                [(self._flat_ids(b[0], fm), b[0].shape[0], fm, k, p) for b, fm, (k, p) in zip(batches, fms, sets)])
+                [(self._flat_ids(b[0], fm), b[0].shape[0], fm, k, p, iv if self.grow is not None else None)
+                 for b, fm, (k, p, iv) in zip(batches, fms, sets)])
         def enqueue():
             if routed:
                 self.shx.route_run(rlist)

@@ -63,6 +63,7 @@ class ModeSpec:
     fp8: bool
     wgfin_fits: bool           # the wgfin work fits the sparse + wgfin launch (splits <= SFWG_MAX_NS)
     fin_covers_all: bool       # the finalize launch covers every dense parameter
+    grow_ok: bool = False      # the tower can write sorted gradient rows (bf16 gather tower, K <= 16)
 
 
 @dataclass(frozen=True)
@@ -91,6 +92,8 @@ class StepPlan:
     sh_apply_dense: bool = False   # dense optimizer inside the owner update launch
     w8_after_fin: bool = False     # fp8: quantize the weights after the fused finalize optimizer
     w8_after_owner: bool = False   # fp8: ... after the owner launch's dense optimizer
+    grow_rows: bool = False        # run-sorted sfwg step: the tower writes each slot's gradient row
+                                   # to its sorted position; the sparse launch streams them
 
 
 IDLE = StepPlan()
@@ -156,4 +159,5 @@ def plan_step(mode: ModeSpec, kn: StepKnobs, B: int, sort_plan: Optional[Tuple],
         defer_wgrad=split or sfwg or xfuse, dense_branch=split, dense_early=early, fuse_opt=fuse_opt,
         sfwg=sfwg, dense_opt_after=not sh_dense and not early,
         xfuse=xfuse, exchange_allreduce=ex_ar, sh_apply_dense=sh_dense,
-        w8_after_fin=mode.fp8 and fuse_opt and not kn.wgfin, w8_after_owner=mode.fp8 and sh_dense)
+        w8_after_fin=mode.fp8 and fuse_opt and not kn.wgfin, w8_after_owner=mode.fp8 and sh_dense,
+        grow_rows=run and sfwg and mode.grow_ok)

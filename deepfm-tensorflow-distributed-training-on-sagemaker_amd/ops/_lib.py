@@ -114,7 +114,8 @@ class SfArgs(C.Structure):
                 ("s0w", c_void_p), ("s1w", c_void_p), ("Gv", c_void_p), ("Gw", c_void_p),
                 ("h", OptHyper), ("step", c_void_p), ("ldv", c_long), ("ldw", c_long),
                 ("sid", c_void_p), ("upos", c_void_p), ("gout", c_void_p), ("step_off", c_int),
-                ("flags", c_void_p), ("sync", c_void_p), ("v_by_key", c_int), ("vbf16", c_int)]
+                ("flags", c_void_p), ("sync", c_void_p), ("v_by_key", c_int), ("vbf16", c_int),
+                ("grow", c_void_p)]
 
 
 class ShTable(C.Structure):
@@ -156,7 +157,7 @@ class FsJob(C.Structure):
     _fields_ = [("ids", c_void_p), ("ld", c_int), ("B", c_int), ("F", c_int), ("fr", c_void_p),
                 ("work", c_void_p), ("nwork", c_int), ("rk", c_void_p), ("rp", c_void_p),
                 ("keys", c_void_p), ("perm", c_void_p), ("err", c_void_p), ("mfields", c_void_p),
-                ("nmf", c_int), ("mwpf", c_int)]
+                ("nmf", c_int), ("mwpf", c_int), ("inv", c_void_p)]
 
 
 TW_MAXL = 8
@@ -180,7 +181,7 @@ class TowerArgs(C.Structure):
                 ("x_off", c_int), ("x8_off", c_int), ("S", c_void_p), ("Et", c_void_p), ("idx_ld", c_int),
                 ("id_lim", c_uint32), ("vbf16", c_int), ("serve_wgs", c_int), ("sv", ShServeArgs),
                 ("stamp_wgs", c_int), ("stamp_n", c_int), ("stamp_div", c_int), ("stamp_keys", c_void_p),
-                ("stamp_flags", c_void_p)]
+                ("stamp_flags", c_void_p), ("grow", c_void_p), ("inv", c_void_p), ("g_off", c_int), ("inv_ld", c_int)]
 
 
 class CommOp(C.Structure):

@@ -212,7 +212,8 @@ class FieldSort:
         keys_out, perm_out)]: one FsJob per batch (own chunk-run scratch), the sort items (batch,
         field, 16K-row chunk; big fields first) and the merge items (B > 16K only).  Built on the host before any
         capture and cached under the buffers' addresses."""
-        key = tuple((ptr(i), int(B), bool(fm), ptr(k), ptr(p)) for i, B, fm, k, p in batches)
+        batches = [tuple(b) + (None,) * (6 - len(b)) for b in batches]      # (..., inv_out or None)
+        key = tuple((ptr(i), int(B), bool(fm), ptr(k), ptr(p), ptr(v)) for i, B, fm, k, p, v in batches)
         cache = self.__dict__.setdefault("_run_plans", {})
         hit = cache.get(key)
         if hit is not None:
@@ -229,7 +230,7 @@ class FieldSort:
             rs = torch.zeros(G, 2, n, dtype=torch.int32, device=self.device)
             self._run_scratch = rs
         jobs, items, mitems, keep = [], [], [], [rs]
-        for g, (ids, B, fm, kout, pout) in enumerate(batches):
+        for g, (ids, B, fm, kout, pout, iout) in enumerate(batches):
             assert B <= min(self.max_rows, 8 * ch) and ids.numel() >= B * self.F
             nc = max(1, -(-B // ch))
             wl = [(f, c) for f in range(self.F) for c in range(nc)]
@@ -243,6 +244,7 @@ class FieldSort:
             j.B, j.F, j.fr, j.work, j.nwork = B, self.F, ptr(self.fr), ptr(work), len(wl)
             j.rk, j.rp = ptr(rs[g, 0]), ptr(rs[g, 1])
             j.keys, j.perm, j.err = ptr(kout), ptr(pout), ptr(self.err)
+            j.inv = ptr(iout)
             j.mfields, j.nmf, j.mwpf = ptr(mft), len(mf), wpr * nc
             jobs.append(j)
             items.append([(g, it) for it in range(len(wl))])

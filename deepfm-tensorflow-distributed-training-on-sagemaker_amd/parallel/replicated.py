@@ -129,6 +129,12 @@ class ReplicatedExchange:
         if m.sparse_update == "tf1_dense":
             KN.dense_sweep(m.K, m.opt_id, m.R, m.tv, m.tw, m.Gv, m.Gw, m.sv, m.h_sparse, m.step)
 
+    def step_bytes(self, run_steps: int = 1) -> dict:
+        """Modelled traffic of one step per rank (see FixedCapacityExchange.step_bytes): this rank's
+        ids + gradient-row block + dense gradient, all-gathered to the N - 1 other ranks."""
+        blk = self.C * 4 + self.C * self.RW * 4 + self.m.P * 4
+        return {"sent": int((self.N - 1) * blk), "moved": int(self.N * blk)}
+
     def reset_table(self):
         self.req_key.zero_()
         self.req_pos.zero_()

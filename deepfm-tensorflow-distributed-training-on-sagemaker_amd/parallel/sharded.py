@@ -554,6 +554,16 @@ class FixedCapacityExchange:
         if m.sparse_update == "tf1_dense":
             KN.dense_sweep(m.K, m.opt_id, m.R, m.tv, m.tw, m.Gv, m.Gw, m.sv, m.h_sparse, m.step)
 
+    def step_bytes(self, run_steps: int = 1) -> dict:
+        """Modelled traffic of one training step per rank: ``sent`` = bytes this rank sends to OTHER
+        ranks (rows G1 + gradient rows G2 + dense gradient all-gather + its share of the run's ids
+        all-to-all), ``moved`` = bytes its collectives deliver including its own block (what a
+        1-rank proxy copies).  Fixed-capacity blocks: independent of the batch's contents."""
+        N, C, RW, P = self.N, self.C, self.RW, self.m.P
+        per_peer = C * RW * 4 * 2 + C * 4 / max(1, run_steps) * (1 if run_steps else 0)
+        dense = P * 4
+        return {"sent": int((N - 1) * (per_peer + dense)), "moved": int(N * (per_peer + dense))}
+
     def reset_table(self):
         """The tables' stamps are step numbers: clear them when the step counter is rewritten."""
         for rs in self.sets + self.run_sets:

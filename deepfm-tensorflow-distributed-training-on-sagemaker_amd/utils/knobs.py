@@ -59,6 +59,8 @@ KNOBS: Dict[str, Knob] = {
     "HIPFM_SH_XFUSE": Knob("1", "variant", "row-sharded step: gradient rows + dense gradients in one "
                            "aggregated RCCL operation"),
     "HIPFM_SH_ROUTE2": Knob("1", "variant", "two-launch routing (0: segments + bucket kernels, oracle)"),
+    "HIPFM_GROW": Knob("1", "variant", "run-sorted steps: the tower writes sorted per-slot gradient rows "
+                       "(0: the sparse launch gathers dX0 / S / vals / dlogit per slot)"),
     "HIPFM_TF1_SPLIT": Knob("1", "variant", "tf1_dense on one GPU: split form (0: gradient scatter + "
                             "full-table sweep, the oracle in tests/test_gpu_tf1.py)"),
     "HIPFM_SWEEP_MODE": Knob("auto", "variant", "tf1_dense split sweep: merged (workgroups of the "

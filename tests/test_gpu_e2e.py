@@ -114,3 +114,33 @@ def test_native_auc_parity_with_golden(update):
         hg += hist_torch(gold.predict(ids, vals), lab)
     an, ag = auc_from_hist(hn.cpu()), auc_from_hist(hg)
     assert ag > 0.6 and abs(an - ag) <= 0.005, (an, ag)
+
+
+def test_streamed_epochs_through_the_ring_train_like_the_cached_run(dataset):
+    """Streamed epochs (no HBM cache, e.g. a dataset over the cache budget) go through the staging
+    ring as captured multi-step runs; they train bitwise like the cached run (epoch 0 streamed
+    through the ring, later epochs replayed from the cache), with the per-field sort from
+    --field_sizes from the first step on."""
+    from hipfm.cli import _EpochView
+    from hipfm.config import RunConfig
+    from hipfm.data.pipeline import InputPipeline, discover_files
+    files = discover_files(dataset, "tr")
+    from hipfm.data.synthetic import make_synth
+    sizes = ",".join(str(hi - lo) for lo, hi in make_synth("total:50000").field_ranges())
+    out = []
+    for cache in (False, True):
+        cfg = RunConfig(feature_size=50000, field_size=39, embedding_size=8, batch_size=512,
+                        deep_layers="64,32", dropout="0.9,0.9", device="cuda", log_steps=0,
+                        watchdog_secs=0, graph_steps=8, num_threads=4, field_sizes=sizes)
+        est = Estimator(cfg)
+        pipe = InputPipeline(files, 39, 512, 1, cache=cache, device=est.device, id_dtype=torch.int32,
+                             threads=4, seed=cfg.seed)
+        for e in range(3):
+            est.train(_EpochView(pipe, e))
+        assert est.model.field_ranges is not None
+        if not cache:
+            assert pipe.cached_batches == 0 and getattr(est, "_ring", None) is not None
+        torch.cuda.synchronize()
+        out.append((est.model.p.clone(), est.model.rec.clone(), est.global_step))
+    assert out[0][2] == out[1][2] == 3 * (20000 // 512)
+    assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
