@@ -40,7 +40,7 @@ METRIC = ("samples/sec (whole node) + eval AUC, Criteo-1TB-shape DeepFM at 1/2/4
 # per-step pipelined routing of round 2 (side-stream routing kernels, serve ahead), also
 # captured; the last launches eagerly without the routing prefetch and without the fused dense
 # exchange (dense all-reduce in the gradient group, 7-launch routing).
-_PLAIN_EXCHANGE = {"HIPFM_SH_XFUSE": "0", "HIPFM_SH_APPLY_DENSE": "0", "HIPFM_SH_ROUTE2": "0"}
+_PLAIN_EXCHANGE = {"HIPFM_SH_APPLY_DENSE": "0", "HIPFM_SH_ROUTE2": "0"}
 LADDER = [
     ("graph+run-routing", {}),                               # HIP graphs, run-level routing
     ("graph+prefetch", {"HIPFM_RUN_SORT": "0"}),             # HIP graphs, next-batch routing prefetch
@@ -209,6 +209,8 @@ def main():
     args = ap.parse_args()
     if os.environ.get("HIPFM_BENCH_NO_GRAPH") == "1":
         args.no_graph = True
+    if os.environ.get("HIPFM_BENCH_FM_IDS") == "1":
+        args.field_major_ids = True
     fake = os.environ.get("HIPFM_BENCH_FAKE")          # supervisor tests (CPU): fake rank work
     if fake:
         return _fake_child(args, fake)

@@ -350,6 +350,23 @@ __device__ __forceinline__ void sh_owner_apply_elem(int gt, const int* __restric
   const int p = e / C;
   const size_t row = (size_t)(id / rdiv);
   const unsigned cur = (unsigned)(*step + 1);
+  // the owner's record (row, slots) is loaded up front, beside the request-table probes: its
+  // HBM round trip overlaps theirs instead of following them (a non-lead requester's copy of the
+  // loads is simply dropped)
+  const size_t rb = row * ldv, ow = row * ldw;
+  const bool bf = vbf16 != 0;
+  f32x4 pv = {0, 0, 0, 0}, a = {0, 0, 0, 0}, c = {0, 0, 0, 0};
+  float pw = 0.f, aw = 0.f, cw = 0.f;
+  if (MODE == 0) {
+    pv = ld_row4(tv + rb, sub * 4, bf);
+    if (OPT != OPT_GD) a = ld_row4(s0v + rb, sub * 4, bf);
+    if (OPT == OPT_ADAM || OPT == OPT_FTRL) c = ld_row4(s1v + rb, sub * 4, bf);
+    if (sub == 0) {
+      pw = tw[ow];
+      if (OPT != OPT_GD) aw = s0w[ow];
+      if (OPT == OPT_ADAM || OPT == OPT_FTRL) cw = s1w[ow];
+    }
+  }
   const unsigned long long* tr = sh_find(T, N, (unsigned)row, cur);
   if (!tr) return;  // cannot happen: every received row was inserted by this step's serve / tag
   for (int q = 0; q < p; ++q)
@@ -369,12 +386,6 @@ __device__ __forceinline__ void sh_owner_apply_elem(int gt, const int* __restric
     return;
   }
   const float lr_t = OPT == OPT_ADAM ? adam_lr_t(h, *step + 1) : h.lr;
-  const size_t rb = row * ldv, ow = row * ldw;
-  const bool bf = vbf16 != 0;
-  f32x4 pv = ld_row4(tv + rb, sub * 4, bf);
-  f32x4 a = {0, 0, 0, 0}, c = {0, 0, 0, 0};
-  if (OPT != OPT_GD) a = ld_row4(s0v + rb, sub * 4, bf);
-  if (OPT == OPT_ADAM || OPT == OPT_FTRL) c = ld_row4(s1v + rb, sub * 4, bf);
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     float gj = g[j] + h.l2 * pv[j];
@@ -392,10 +403,7 @@ __device__ __forceinline__ void sh_owner_apply_elem(int gt, const int* __restric
   if (OPT == OPT_ADAM || OPT == OPT_FTRL) st_row4(s1v + rb, sub * 4, c, bf, bf ? row_sr_seed(row, st, 2) : 0u);
   float wnew = 0.f;
   if (sub == 0) {
-    float pw = tw[ow];
     float g1 = gw + h.l2 * pw;
-    float aw = (OPT != OPT_GD) ? s0w[ow] : 0.f;
-    float cw = (OPT == OPT_ADAM || OPT == OPT_FTRL) ? s1w[ow] : 0.f;
     opt_update<OPT>(pw, g1, aw, cw, h, lr_t);
     tw[ow] = pw;
     if (OPT != OPT_GD) s0w[ow] = aw;

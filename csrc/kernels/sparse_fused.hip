@@ -75,6 +75,7 @@ struct SfArgs {
   // tower straight to each slot's sorted position): step 1 streams them instead of gathering
   // perm -> vals / dlogit / S / dX0 per slot
   const float* grow;
+  int grow_perm;    // 1: grow rows are in SLOT order (b*F + f): gathered through perm, one 48-B row per slot
 };
 
 // MODE 0: lazy optimizer OPT on the row; 1: tf1_dense scatter of the row gradient;
@@ -264,7 +265,7 @@ __device__ __forceinline__ void sf_tile_body(const SfArgs& A, const int tile, Sf
     for (int ps = 0; ps < T::PASSES; ++ps) {
       const int p = ps * T::PPP + tid / T::LPS;
       if (p < nloc) {
-        const float* gr = A.grow + (size_t)(b0 + p) * T::RS;
+        const float* gr = A.grow + (size_t)(A.grow_perm ? A.perm[b0 + p] : b0 + p) * T::RS;
         const f32x4 av = *reinterpret_cast<const f32x4*>(gr + sub * 4);
 #pragma unroll
         for (int j = 0; j < 4; ++j) g[p][sub * 4 + j] = av[j];

@@ -363,7 +363,7 @@ __device__ __forceinline__ void tw_grow_tile(const TowerArgs& a, const f32x4 (&a
       const f32x4 dx = {bf2f(dxh[0]), bf2f(dxh[1]), bf2f(dxh[2]), bf2f(dxh[3])};
       const f32x4 s = *reinterpret_cast<const f32x4*>(gS + row * KE + sub * 4);
       const float x = gx[row * F + f], dy = s_dl[row];
-      float* gr = a.grow + (size_t)ginv[f * 32 + row] * RS;
+      float* gr = a.grow + (size_t)(a.inv ? ginv[f * 32 + row] : (row0 + row) * F + f) * RS;
       *reinterpret_cast<f32x4*>(gr + sub * 4) = sf_slot_a(dx, dy, s, x);
       if (sub == 0) *reinterpret_cast<f32x4*>(gr + KE) = f32x4{sf_slot_gw(dy, x), sf_slot_c(dy, x), 0.f, 0.f};
     }
@@ -401,6 +401,7 @@ __device__ __forceinline__ void tower_bf16_body(const TowerArgs& a, bf16* lds, f
   bf16* Xl = lds + (KE > 0 ? a.x_off : 0);
   // sorted gradient rows: LDS scratch and this block's inverse permutation (prefetched now)
   const bool grow = KE > 0 && a.train && a.grow != nullptr;
+  const bool ginv_on = grow && a.inv != nullptr;  // sorted positions (else rows in slot order)
   float* gx = reinterpret_cast<float*>(reinterpret_cast<unsigned char*>(lds) + (grow ? a.g_off : 0));
   float* gS = gx + TW_ROWS * a.F;
   int* ginv = reinterpret_cast<int*>(gS + TW_ROWS * (KE > 0 ? KE : 1));
@@ -550,7 +551,7 @@ __device__ __forceinline__ void tower_bf16_body(const TowerArgs& a, bf16* lds, f
   store_tile_t(lds + a.dz_off[0], L + 8, L, a.dZt[nl - 1], a.M, row0);
   TW_ST(8);
   // ---------------------------------------------------------------- dgrad chain
-  if (grow) {  // this block's inverse permutation, for the dX0 phase's sorted rows
+  if (ginv_on) {  // this block's inverse permutation, for the dX0 phase's sorted rows
 #pragma unroll
     for (int k = 0; k < TW_GINV; ++k) {  // block entry e = f * 32 + r (32 contiguous ints per field)
       const int e = tid + 256 * k;
@@ -597,7 +598,7 @@ __device__ __forceinline__ void tower_bf16_body(const TowerArgs& a, bf16* lds, f
     const int N0 = a.Np[0];
     const bf16* Az = lds + a.dz_off[cur];
     const int ph = 2 * nl - 1;
-    if (grow) {
+    if (ginv_on) {
 #pragma unroll
       for (int k = 0; k < TW_GINV; ++k) {
         const int e = tid + 256 * k;
@@ -915,7 +916,7 @@ HFM_API int hfm_tower(const TowerArgs* ap, int KE, hipStream_t st) {
                                           !a.sv.T.key || a.sv.C <= 0 || a.sv.stamp_off != 2 ||
                                           (long)a.serve_wgs * 256 < (long)a.sv.total * (KE / 4))))
     return (int)hipErrorInvalidValue;
-  if (a.grow && (!KE || a.fp8 || !a.train || !a.inv || a.inv_ld < a.M || a.F > TW_GINV * 256 / TW_ROWS || a.g_off < 0 || (a.g_off & 15) ||
+  if (a.grow && (!KE || a.fp8 || !a.train || (a.inv && a.inv_ld < a.M) || a.F > TW_GINV * 256 / TW_ROWS || a.g_off < 0 || (a.g_off & 15) ||
                  KE > 16 || a.g_off + TW_ROWS * (8 * a.F + 4 * KE) + 4 * TW_ROWS * 40 * 2 > a.lds_bytes))
     return (int)hipErrorInvalidValue;
   if (a.stamp_wgs < 0 || (a.stamp_wgs && (!KE || !a.train || !a.stamp_keys || !a.stamp_flags || a.stamp_div <= 0 ||

@@ -111,13 +111,15 @@ def next_pipe_stream(channel: str) -> str:
 
 
 class _DeviceFeeder:
-    """Loader batches -> device batches: the C++ loader threads decode straight into a ring of
-    pinned host buffers (ids narrowed to the device id type there), and each buffer goes to the
-    GPU with an async copy on a dedicated copy stream.  The compute stream waits on the copy's
-    event, never the host; a pinned buffer is refilled only after its previous copy finished
-    (3-deep ring: decode of batch i+2, copy of i+1 and compute of i overlap)."""
+    """Loader batches -> device batches: the C++ loader threads decode and a copy pool assembles
+    each batch straight into a ring of pinned host buffers (ids narrowed to the device id type
+    there) -- driven by a background fill thread, so the training loop never waits on the
+    assembly -- and each buffer goes to the GPU with an async copy on a dedicated copy stream.
+    The compute stream waits on the copy's event, never the host; a pinned buffer is refilled only
+    after its previous copy finished (depth-deep ring: assembly of batches i+1.., copy of i and
+    compute of i-1 overlap)."""
 
-    def __init__(self, loader, F: int, B: int, device, id_dtype, depth: int = 3):
+    def __init__(self, loader, F: int, B: int, device, id_dtype, depth: int = 4):
         self.loader, self.F, self.B, self.device, self.id_dtype = loader, F, B, device, id_dtype
         self.copy = torch.cuda.Stream(device)
         pin = dict(pin_memory=True)
@@ -126,35 +128,70 @@ class _DeviceFeeder:
                       torch.empty(B, F, dtype=torch.float32, **pin)) for _ in range(depth)]
         self.done = [None] * depth
         self.h2d_s = 0.0         # host time spent issuing copies (the copies themselves are async)
+        import queue
+        self._free, self._full = queue.Queue(), queue.Queue()
+        for i in range(depth):
+            self._free.put(i)
+        self._stop = False
+        self._th = None
+
+    def _fill(self):
+        try:
+            while True:
+                slot = self._free.get()
+                if slot is None or self._stop:
+                    return
+                ev = self.done[slot]
+                if ev is not None:
+                    ev.synchronize()                 # this pinned buffer's last copy is over
+                lab, ids, vals = self.ring[slot]
+                r = self.loader.next_into(lab, ids, vals)   # (ctypes: the GIL is released)
+                self._full.put((slot, r, None))
+                if r == 0:
+                    return
+        except BaseException as e:  # noqa: BLE001  (surfaced in the consumer)
+            self._full.put((None, 0, e))
+
+    def close(self):
+        """Stop the fill thread (before the loader it reads from is closed)."""
+        if self._th is not None:
+            self._stop = True
+            self._free.put(None)
+            self._th.join()
+            self._th = None
 
     def __iter__(self):
+        import threading
         import time
-        k = 0
         compute = torch.cuda.current_stream(self.device)
-        while True:
-            slot = k % len(self.ring)
-            if self.done[slot] is not None:
-                self.done[slot].synchronize()          # this pinned buffer's last copy is over
-            lab, ids, vals = self.ring[slot]
-            r = self.loader.next_into(lab, ids, vals)
-            if r == 0:
-                return
-            t0 = time.perf_counter()
-            d_ids = torch.empty(r, self.F, dtype=self.id_dtype, device=self.device)
-            d_vals = torch.empty(r, self.F, dtype=torch.float32, device=self.device)
-            d_lab = torch.empty(r, dtype=torch.float32, device=self.device)
-            self.copy.wait_stream(compute)             # the new buffers are free on the copy stream
-            with torch.cuda.stream(self.copy):
-                d_ids.copy_(ids[:r], non_blocking=True)
-                d_vals.copy_(vals[:r], non_blocking=True)
-                d_lab.copy_(lab[:r], non_blocking=True)
-                ev = torch.cuda.Event()
-                ev.record(self.copy)
-            self.done[slot] = ev
-            compute.wait_event(ev)
-            self.h2d_s += time.perf_counter() - t0
-            k += 1
-            yield d_ids, d_vals, d_lab
+        self._th = threading.Thread(target=self._fill, daemon=True)
+        self._th.start()
+        try:
+            while True:
+                slot, r, err = self._full.get()
+                if err is not None:
+                    raise err
+                if r == 0:
+                    return
+                lab, ids, vals = self.ring[slot]
+                t0 = time.perf_counter()
+                d_ids = torch.empty(r, self.F, dtype=self.id_dtype, device=self.device)
+                d_vals = torch.empty(r, self.F, dtype=torch.float32, device=self.device)
+                d_lab = torch.empty(r, dtype=torch.float32, device=self.device)
+                self.copy.wait_stream(compute)             # the new buffers are free on the copy stream
+                with torch.cuda.stream(self.copy):
+                    d_ids.copy_(ids[:r], non_blocking=True)
+                    d_vals.copy_(vals[:r], non_blocking=True)
+                    d_lab.copy_(lab[:r], non_blocking=True)
+                    ev = torch.cuda.Event()
+                    ev.record(self.copy)
+                self.done[slot] = ev
+                self._free.put(slot)
+                compute.wait_event(ev)
+                self.h2d_s += time.perf_counter() - t0
+                yield d_ids, d_vals, d_lab
+        finally:
+            self.close()
 
 
 def derive_field_ranges(fmin: torch.Tensor, fmax: torch.Tensor, V: int):
@@ -304,9 +341,10 @@ class InputPipeline:
                 k += 1
                 yield t
         finally:
-            loader.close()
             if src is not None:
+                src.close()                  # (its fill thread reads the loader)
                 self.h2d_s = src.h2d_s
+            loader.close()
         if stats:                    # (reached only when the epoch was read to its end)
             self._stats_done = True
         if store is not None:

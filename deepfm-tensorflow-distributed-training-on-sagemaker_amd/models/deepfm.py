@@ -47,12 +47,8 @@ from ..utils.knobs import flag, knob
 # Execution-mode switches (each one is a supported, tested mode; rejected experiments are gone)
 _SORT_MODE = knob("HIPFM_SORT")                # auto | global
 _SORT_SIDE_STREAM = flag("HIPFM_SORT_SIDE_STREAM")
-_DENSE_EARLY = flag("HIPFM_DENSE_EARLY")
-_FWD_IDST = flag("HIPFM_FWD_IDST")         # fm_fwd writes ids field-major
-_FUSE_FIN_OPT = flag("HIPFM_FUSE_FIN_OPT")  # dense optimizer in finalize
 _SPARSE_IMPL = knob("HIPFM_SPARSE")             # fused | seg
 _SHARD_PIPELINE = flag("HIPFM_SHARD_PIPELINE")
-_DENSE_SIDE_STREAM = knob("HIPFM_DENSE_SIDE_STREAM")   # auto | 1 | 0
 _TOWER_GATHER = flag("HIPFM_TOWER_GATHER")   # FM gather fused into the tower
 # weight gradients + split-K combine + bias/head reductions + dense optimizer in one launch
 _WGFIN = flag("HIPFM_WGFIN")
@@ -61,15 +57,11 @@ _SFWG = flag("HIPFM_SFWG")
 # one GPU, multi-step graphs: the run's batches sorted up front (fsort_run.h) instead of each
 # next batch on a side branch of the step before
 _RUN_SORT = flag("HIPFM_RUN_SORT")
-# row-sharded step: where the next batch's routing branch is enqueued: start | fetch | tower
-_SHX_FORK = knob("HIPFM_SHX_FORK")
 # row-sharded lazy step: dense optimizer inside the owner update's launch
 _SH_APPLY_DENSE = flag("HIPFM_SH_APPLY_DENSE")
-# ... and the dense gradient computed in the sparse launch, exchanged by all-gather (no all-reduce)
-_SH_XFUSE = flag("HIPFM_SH_XFUSE")
 # run-sorted single-GPU steps: the tower writes sorted per-slot gradient rows (0: the sparse launch
 # gathers vals / dlogit / S / dX0 per slot)
-_GROW = flag("HIPFM_GROW")
+_GROW = knob("HIPFM_GROW")     # 0 off | 1 rows at their sorted positions | 2 rows in slot order
 # tf1_dense on one GPU: split sweep concurrent with the step (0: scatter + full-table sweep)
 _TF1_SPLIT = flag("HIPFM_TF1_SPLIT")
 _SWEEP_MODE = knob("HIPFM_SWEEP_MODE")      # auto | merged | branch
@@ -79,10 +71,9 @@ _SWEEP_WG = int(knob("HIPFM_SWEEP_WG"))   # 128: 0.178, 256: 0.160, 512: 0.179 m
 
 def step_knobs() -> StepKnobs:
     """The step planner's knob snapshot (read at call time: tests switch these module values)."""
-    return StepKnobs(sort_side_stream=_SORT_SIDE_STREAM, dense_early=_DENSE_EARLY, fwd_idst=_FWD_IDST,
-                     fuse_fin_opt=_FUSE_FIN_OPT, sparse_impl=_SPARSE_IMPL, dense_side_stream=_DENSE_SIDE_STREAM,
-                     wgfin=_WGFIN, sfwg=_SFWG, shx_fork=_SHX_FORK, sh_apply_dense=_SH_APPLY_DENSE,
-                     sh_xfuse=_SH_XFUSE, sweep_mode=_SWEEP_MODE, run_sort=_RUN_SORT,
+    return StepKnobs(sort_side_stream=_SORT_SIDE_STREAM, sparse_impl=_SPARSE_IMPL,
+                     wgfin=_WGFIN, sfwg=_SFWG, sh_apply_dense=_SH_APPLY_DENSE,
+                     sweep_mode=_SWEEP_MODE, run_sort=_RUN_SORT,
                      shard_pipeline=_SHARD_PIPELINE)
 
 
@@ -396,7 +387,8 @@ class NativeDeepFM(GraphRunnerMixin, NativeStateMixin):
         # sorted gradient rows (run-sorted single-GPU steps): the bf16 gather tower writes every
         # slot's embedding gradient row to its sorted position; the sparse launch streams them
         self.grow_ok = (self.gather_fused and not self.fp8 and self.K in (4, 8, 16) and self.F <= 64 and
-                        _GROW and self._tower_grow_layout()[1] <= 150 * 1024)
+                        _GROW != "0" and self._tower_grow_layout()[1] <= 150 * 1024)
+        self.grow_sorted = _GROW == "1"      # (else slot order: the sparse launch gathers through perm)
         if init:
             if self.V * self.K <= (1 << 24):
                 # small tables: the exact golden initialization (CPU generator, bit-reproducible)
@@ -794,9 +786,11 @@ class NativeDeepFM(GraphRunnerMixin, NativeStateMixin):
         self._nwg_jobs = len(jobs)
         self._wg_tasks = task0
 
-    def _tower_args(self, B: int, train: bool, with_labels: bool = True, gather=None, grow_inv=None) -> TowerArgs:
+    def _tower_args(self, B: int, train: bool, with_labels: bool = True, gather=None, grow: bool = False,
+                    grow_inv=None) -> TowerArgs:
         """``gather`` = (idx, tv, tw): the tower's prologue gathers the FM rows itself.
-        ``grow_inv`` (the batch's inverse sort permutation): write sorted gradient rows."""
+        ``grow``: write per-slot gradient rows -- at their sorted positions (``grow_inv``, the
+        batch's inverse sort permutation) or in slot order (``grow_sorted`` off)."""
         a = TowerArgs()
         nl = len(self.layers)
         a.M, a.nvalid, a.nl, a.K0p = self.M, B, nl, self.K0p
@@ -839,8 +833,9 @@ class NativeDeepFM(GraphRunnerMixin, NativeStateMixin):
                 a.E8, a.sE = self.E8.data_ptr(), self.sE.data_ptr()
             for i in range(nl):
                 a.W8[i], a.sW[i] = self.W8[i].data_ptr(), self.sW[i].data_ptr()
-        if grow_inv is not None:
-            a.grow, a.inv, a.inv_ld = self.grow.data_ptr(), grow_inv.data_ptr(), B   # (run-sorted: B == M)
+        if grow:
+            a.grow, a.inv_ld = self.grow.data_ptr(), B                  # (run-sorted: B == M)
+            a.inv = grow_inv.data_ptr() if self.grow_sorted else 0
             a.g_off, a.lds_bytes = self._tower_grow_layout()
             a.S = 0                            # (the sparse launch reads the rows instead)
         a.seed = self.seed & 0xFFFFFFFF
@@ -866,7 +861,7 @@ class NativeDeepFM(GraphRunnerMixin, NativeStateMixin):
         if self.fused and self.gather_fused:
             idx, tv, tw = self._fm_inputs(B, train=True)
             ta = self._tower_args(B, train=True, gather=(idx, tv, tw),
-                                  grow_inv=self._grow_inv if self._sp.grow_rows else None)
+                                  grow=self._sp.grow_rows, grow_inv=self._grow_inv)
             if self.shx is not None and self.shx.tower_serve is not None:
                 # run-routed step: the next step's rows served by extra tower workgroups
                 ta.sv, self.shx.tower_serve = self.shx.tower_serve, None
@@ -1205,6 +1200,7 @@ class NativeDeepFM(GraphRunnerMixin, NativeStateMixin):
         A.flags, A.sync = self.sf_flags.data_ptr(), self.sf_sync.data_ptr()
         A.vbf16 = 1 if self.emb_bf16 else 0
         A.grow = self.grow.data_ptr() if self._sp.grow_rows else 0
+        A.grow_perm = 0 if self.grow_sorted else 1
         return A
 
     def _sparse_backward(self, B: int, idx, tv, presorted: bool = False):
@@ -1275,7 +1271,8 @@ class NativeDeepFM(GraphRunnerMixin, NativeStateMixin):
         """The plan (models/step_plan.py) of the step bound by ``_bind_step`` at batch size B."""
         fs = self.uses_field_sort(B)
         return plan_step(self._mode_spec(), step_knobs(), B, self._sort_plan, self._tf1_plan is not None,
-                         field_sort=fs, idst_capable=fs and KN.fm_fwd_writes_idsT(self.F, self.K))
+                         field_sort=fs, idst_capable=fs and KN.fm_fwd_writes_idsT(self.F, self.K),
+                         routed_run=self._shx_plan is not None and self._shx_plan.run)
 
     # the last step's plan, observable by tests (which dense-optimizer / sweep path ran)
     _tf1_merged = property(lambda self: self._last_plan.tf1_merged)
@@ -1288,11 +1285,11 @@ class NativeDeepFM(GraphRunnerMixin, NativeStateMixin):
         branch is enqueued right after the tower: the step's first kernel starts at once."""
         sp = self.step_plan(B)
         main = torch.cuda.current_stream(self.device)
+        if sp.grow_rows and self.shx is not None:           # run-routed: the set's inverse perm
+            self._grow_inv = self.shx.run_sets[self._shx_plan.c].inv
         if self.shx is not None:
             self._shx_start(B)
         hooks = []          # called once the tower (or FM forward) is enqueued
-        if self.shx is not None and _SHX_FORK == "tower":
-            hooks.append(self.shx.fork_next)
         plan = self._sort_plan
         if sp.run_sorted:                                   # sorted at the start of the run
             self.sorted_keys, self.perm, self._grow_inv = self._run_ss[plan[3]]
@@ -1439,7 +1436,7 @@ class NativeDeepFM(GraphRunnerMixin, NativeStateMixin):
         and the fork of the next batch's routing."""
         if self._shx_plan is None:
             self._shx_plan = self.shx.plan(self.idx, B, None, resident=False)
-        self.shx.begin(self._shx_plan, B, fork=_SHX_FORK)
+        self.shx.begin(self._shx_plan, B, fork="start")
 
     def compute_grads(self, ids, vals, labels):
         """Forward + backward WITHOUT any update (tests / debugging): returns the flat dense

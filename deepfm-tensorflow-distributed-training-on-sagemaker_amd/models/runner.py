@@ -345,7 +345,8 @@ class GraphRunnerMixin:
             sets = self._run_sets(G)
             # (the inverse permutation only where the tower writes sorted gradient rows)
             rplan = self._fsort_next.run_plan(
-                [(self._flat_ids(b[0], fm), b[0].shape[0], fm, k, p, iv if self.grow is not None else None)
+                [(self._flat_ids(b[0], fm), b[0].shape[0], fm, k, p,
+                  iv if (self.grow is not None and self.grow_sorted) else None)
                  for b, fm, (k, p, iv) in zip(batches, fms, sets)])
         def enqueue():
             if routed:

@@ -29,18 +29,16 @@ from typing import Optional, Tuple
 @dataclass(frozen=True)
 class StepKnobs:
     """Snapshot of the execution-mode knobs a step plan depends on (read at plan time, so
-    tests that switch a knob between steps see the switch)."""
+    tests that switch a knob between steps see the switch).
+    (Round 4 fixed the experiments that had settled: the dense optimizer runs early and inside the
+    finalize / wgfin launch, fm_fwd writes field-major ids for the per-layer path's sort, the
+    dense-gradient branch forks only under an exchange, the next routing forks at the step start,
+    and the fused exchange carries the dense gradient whenever the owner launch applies it.)"""
     sort_side_stream: bool = True    # HIPFM_SORT_SIDE_STREAM: the inline slot sort on a graph branch
-    dense_early: bool = True         # HIPFM_DENSE_EARLY: dense optimizer before the sort join
-    fwd_idst: bool = True            # HIPFM_FWD_IDST: fm_fwd writes ids field-major for the sort
-    fuse_fin_opt: bool = True        # HIPFM_FUSE_FIN_OPT: dense optimizer in the finalize launch
-    sparse_impl: str = "fused"       # HIPFM_SPARSE: fused | seg
-    dense_side_stream: str = "auto"  # HIPFM_DENSE_SIDE_STREAM: auto | 1 | 0
+    sparse_impl: str = "fused"       # HIPFM_SPARSE: fused | seg (two-kernel test oracle)
     wgfin: bool = True               # HIPFM_WGFIN: one weight-gradient + optimizer launch
     sfwg: bool = True                # HIPFM_SFWG: wgfin inside the sparse backward's launch
-    shx_fork: str = "start"          # HIPFM_SHX_FORK: where the next routing branch forks
-    sh_apply_dense: bool = True      # HIPFM_SH_APPLY_DENSE: dense optimizer in the owner launch
-    sh_xfuse: bool = True            # HIPFM_SH_XFUSE: dense gradient all-gathered with the rows
+    sh_apply_dense: bool = True      # HIPFM_SH_APPLY_DENSE: dense optimizer (+ fused dense exchange) in the owner launch
     sweep_mode: str = "auto"         # HIPFM_SWEEP_MODE: auto | merged | branch
     # multi-step execution (models/runner.py)
     run_sort: bool = True            # HIPFM_RUN_SORT: a run's batches sorted / routed up front
@@ -110,17 +108,18 @@ def sweep_merges(mode: ModeSpec, kn: StepKnobs, B: int) -> bool:
 def sfwg_possible(mode: ModeSpec, kn: StepKnobs) -> bool:
     """The sparse backward + wgfin merged launch applies (given the fused dense optimizer)."""
     return (kn.wgfin and kn.sfwg and mode.wgfin_fits and not mode.native_exchange and not mode.sharded and
-            mode.fused and kn.fuse_fin_opt and mode.fin_covers_all and not mode.exchange and kn.dense_early and
-            mode.lazy_rows and kn.sparse_impl == "fused" and kn.dense_side_stream != "1")
+            mode.fused and mode.fin_covers_all and not mode.exchange and
+            mode.lazy_rows and kn.sparse_impl == "fused")
 
 
 def plan_step(mode: ModeSpec, kn: StepKnobs, B: int, sort_plan: Optional[Tuple], tf1: bool,
-              field_sort: bool = False, idst_capable: bool = False) -> StepPlan:
+              field_sort: bool = False, idst_capable: bool = False, routed_run: bool = False) -> StepPlan:
     """The plan of one training step.  ``sort_plan``: the host-side slot-sort binding (None:
     sort inline; ("run", ...): sorted at the run start; (set, inline, next_key): per-step sets,
     prefetched by the previous step unless ``inline``, the next batch's sort forked when
     ``next_key``); ``tf1``: a tf1_dense split flag-set plan is bound; ``field_sort`` /
-    ``idst_capable``: the batch takes the per-field sort / fm_fwd can write its ids field-major."""
+    ``idst_capable``: the batch takes the per-field sort / fm_fwd can write its ids field-major;
+    ``routed_run``: a row-sharded step of a run routed at its start (parallel/sharded.py)."""
     run = sort_plan is not None and sort_plan[0] == "run"
     prefetch = sort_plan is not None and not run and sort_plan[2] is not None
     inline = sort_plan is None or (not run and bool(sort_plan[1]))
@@ -132,19 +131,18 @@ def plan_step(mode: ModeSpec, kn: StepKnobs, B: int, sort_plan: Optional[Tuple],
     # row-sharded / replicated lazy step with wgfin: the dense gradient is computed in the sparse
     # backward's launch and travels with the gradient rows (all-gather, summed in rank order by
     # the owner launch): no comm stream, no all-reduce, no cross-stream joins
-    xfuse = (mode.native_exchange and mode.lazy and kn.sh_xfuse and kn.wgfin and mode.fused and
+    xfuse = (mode.native_exchange and mode.lazy and kn.wgfin and mode.fused and
              kn.sh_apply_dense and mode.wgfin_fits)
     # fused tower, multi-rank: the weight gradients only feed the dense optimizer, so they run on
     # their own branch beside the sparse exchange (0.210 -> 0.199 ms); on one GPU a concurrent
     # wgrad slows the sparse backward more than it saves (0.156 -> 0.161 ms)
-    split = mode.fused and not xfuse and (kn.dense_side_stream == "1" or
-                                          (kn.dense_side_stream == "auto" and mode.exchange))
+    split = mode.fused and not xfuse and mode.exchange
     # one GPU, lazy rows: the dense optimizer needs only the finished dense gradient, so it runs
     # before the sparse backward (inside the gap a join costs anyway); with the fused tower it
     # rides on the finalize launch, and with wgfin inside the sparse backward's launch (sfwg)
-    early = (presorted and not mode.exchange and not split and kn.dense_early and mode.lazy_rows and
+    early = (presorted and not mode.exchange and not split and mode.lazy_rows and
              kn.sparse_impl == "fused")
-    fuse_opt = early and mode.fused and kn.fuse_fin_opt and mode.fin_covers_all
+    fuse_opt = early and mode.fused and mode.fin_covers_all
     sfwg = fuse_opt and sfwg_possible(mode, kn)
     if merged and not sfwg:
         raise RuntimeError("tf1_dense merged sweep planned but the step took another path")
@@ -152,7 +150,7 @@ def plan_step(mode: ModeSpec, kn: StepKnobs, B: int, sort_plan: Optional[Tuple],
     sh_dense = mode.native_exchange and mode.lazy and kn.sh_apply_dense and not early
     return StepPlan(
         run_sorted=run, presorted=presorted, fork_sort=fork,
-        sort_idst=fork and kn.fwd_idst and not mode.gather_fused and field_sort and idst_capable,
+        sort_idst=fork and not mode.gather_fused and field_sort and idst_capable,
         prefetch_next=prefetch, join_sort=fork,
         tf1_merged=merged, tf1_branch=tf1 and not merged,
         tower_stamp=run and tf1 and mode.fused and mode.gather_fused,
@@ -160,4 +158,4 @@ def plan_step(mode: ModeSpec, kn: StepKnobs, B: int, sort_plan: Optional[Tuple],
         sfwg=sfwg, dense_opt_after=not sh_dense and not early,
         xfuse=xfuse, exchange_allreduce=ex_ar, sh_apply_dense=sh_dense,
         w8_after_fin=mode.fp8 and fuse_opt and not kn.wgfin, w8_after_owner=mode.fp8 and sh_dense,
-        grow_rows=run and sfwg and mode.grow_ok)
+        grow_rows=mode.grow_ok and ((run and sfwg) or (routed_run and xfuse and mode.row_sharded)))

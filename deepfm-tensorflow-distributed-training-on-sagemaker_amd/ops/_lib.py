@@ -115,7 +115,7 @@ class SfArgs(C.Structure):
                 ("h", OptHyper), ("step", c_void_p), ("ldv", c_long), ("ldw", c_long),
                 ("sid", c_void_p), ("upos", c_void_p), ("gout", c_void_p), ("step_off", c_int),
                 ("flags", c_void_p), ("sync", c_void_p), ("v_by_key", c_int), ("vbf16", c_int),
-                ("grow", c_void_p)]
+                ("grow", c_void_p), ("grow_perm", c_int)]
 
 
 class ShTable(C.Structure):

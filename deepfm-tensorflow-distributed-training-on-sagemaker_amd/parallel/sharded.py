@@ -143,6 +143,7 @@ class _RouteSet:
         self.recv_ids = torch.full((N * C,), -1, **i32)
         self.send_cnt = torch.zeros(N, **i32)
         self.slot_row = torch.zeros(n, **i32)
+        self.inv = None                            # run sets: inverse sort perm (sorted gradient rows)
         self.recv_ptr = self.recv_ids.data_ptr()   # requests as the owner kernels read them
         self.rstride = 0                           # (run sets: a column of the packed run buffer)
         self.slot_ld = 0                           # slot_row layout: 0 row-major, else [F][slot_ld]
@@ -270,7 +271,11 @@ class FixedCapacityExchange:
         while len(self.run_sets) < G:
             self.run_sets.append(_RouteSet(m, m.M * m.F, self.N, self.C, m.temp.numel(), self.RW))
         sets = self.run_sets[:G]
-        sort_plan = m._fsort.run_plan([(ids, b, fm, rs.sorted_keys, rs.perm)
+        grow = m.grow is not None and m.grow_sorted
+        for rs in sets:
+            if grow and rs.inv is None:
+                rs.inv = torch.zeros(m.M * m.F, dtype=torch.int32, device=m.device)
+        sort_plan = m._fsort.run_plan([(ids, b, fm, rs.sorted_keys, rs.perm, rs.inv if grow else None)
                                        for (ids, b, fm), rs in zip(batches, sets)])
         T = self.N * G * self.C
         if self._run_ids is None or self._run_ids.shape[1] < T:

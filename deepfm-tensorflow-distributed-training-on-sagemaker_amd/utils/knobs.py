@@ -32,17 +32,10 @@ KNOBS: Dict[str, Knob] = {
     "HIPFM_SORT_IMPL": Knob("onesweep", "variant", "global sort: onesweep (56 us) or lsd (101 us at "
                             "n = 640K, tools/bench_sort.py)"),
     "HIPFM_SORT_SIDE_STREAM": Knob("1", "variant", "slot sort on a graph side branch (0: inline)"),
-    "HIPFM_DENSE_EARLY": Knob("1", "variant", "one GPU: dense optimizer before the join with the sort "
-                              "branch (0: after the sparse backward)"),
-    "HIPFM_FWD_IDST": Knob("1", "variant", "per-layer path: fm_fwd writes the ids field-major for the "
-                           "sort (saves its transpose launch)"),
-    "HIPFM_FUSE_FIN_OPT": Knob("1", "variant", "dense optimizer inside the gradient finalize launch"),
     "HIPFM_SPARSE": Knob("fused", "variant", "fused: one-launch sparse backward; seg: fm_bwd_seg + "
                          "seg_apply (oracle, tests/test_gpu_kernels.py)"),
     "HIPFM_SHARD_PIPELINE": Knob("1", "variant", "row-sharded step: next batch's routing on a side "
                                  "stream (0: inline)"),
-    "HIPFM_DENSE_SIDE_STREAM": Knob("auto", "variant", "dense-gradient branch on its own stream: auto "
-                                    "(multi-rank exchange only) | 1 | 0"),
     "HIPFM_FUSED_TOWER": Knob("1", "variant", "one-launch deep tower (0: per-layer GEMM kernels)"),
     "HIPFM_TOWER_GATHER": Knob("1", "variant", "FM gather in the tower's prologue (0: fm_fwd launch)"),
     "HIPFM_WGFIN": Knob("1", "variant", "weight gradients + combine + dense optimizer in one launch "
@@ -52,15 +45,12 @@ KNOBS: Dict[str, Knob] = {
                            "or sorted + routed + its ids exchanged (row-sharded) at the graph's start "
                            "(0: the next batch's sort / routing on a side branch of each step, the "
                            "oracle and the bench ladder's second rung)"),
-    "HIPFM_SHX_FORK": Knob("start", "variant", "row-sharded step: fork point of the next batch's "
-                           "routing branch (start | tower)"),
     "HIPFM_SH_APPLY_DENSE": Knob("1", "variant", "row-sharded step: dense optimizer in the owner "
                                  "update's launch"),
-    "HIPFM_SH_XFUSE": Knob("1", "variant", "row-sharded step: gradient rows + dense gradients in one "
-                           "aggregated RCCL operation"),
     "HIPFM_SH_ROUTE2": Knob("1", "variant", "two-launch routing (0: segments + bucket kernels, oracle)"),
-    "HIPFM_GROW": Knob("1", "variant", "run-sorted steps: the tower writes sorted per-slot gradient rows "
-                       "(0: the sparse launch gathers dX0 / S / vals / dlogit per slot)"),
+    "HIPFM_GROW": Knob("1", "variant", "run-sorted steps: the tower writes per-slot gradient rows, 1 at "
+                       "their sorted positions (streamed), 2 in slot order (gathered through perm); 0: the "
+                       "sparse launch gathers dX0 / S / vals / dlogit per slot"),
     "HIPFM_TF1_SPLIT": Knob("1", "variant", "tf1_dense on one GPU: split form (0: gradient scatter + "
                             "full-table sweep, the oracle in tests/test_gpu_tf1.py)"),
     "HIPFM_SWEEP_MODE": Knob("auto", "variant", "tf1_dense split sweep: merged (workgroups of the "
@@ -84,6 +74,7 @@ KNOBS: Dict[str, Knob] = {
     "HIPFM_KERNELS_SO": Knob(None, "harness", "path of the kernel library (default: in-tree _lib)"),
     "HIPFM_BUILD_PACKED": Knob(None, "harness", "build: packed-FP32 ops on (own objects / library)"),
     "HIPFM_BUILD_STAMPS": Knob(None, "harness", "build: per-workgroup phase stamps (own objects / library)"),
+    "HIPFM_BENCH_FM_IDS": Knob(None, "harness", "bench: resident batches' ids stored field-major (= --field_major_ids)"),
     "HIPFM_BENCH_STAMPS": Knob(None, "harness", "bench: save the stamp build's phase stamps (.npz path)"),
     "HIPFM_PIPE_ROOT": Knob(None, "harness", "directory of SageMaker pipe-mode FIFOs (tests)"),
     "HIPFM_FAULT_STEP": Knob(None, "harness", "fault injection: step at which a rank dies"),

@@ -466,17 +466,15 @@ def test_finalize_fused_dense_opt_bitwise_equal(monkeypatch, opt, mlp_dtype):
     """The 1-GPU lazy step runs the dense optimizer inside the wgfin work, which itself runs
     inside the sparse backward's launch (sparse_fused.hip sfwg_kernel); parameters, optimizer
     slots, the step counter and the bf16 shadows after graph-replayed steps are bitwise those of
-    wgfin as its own launch and of the separate dense_opt launch, early or after the sparse join
-    (fp8: bitwise between the two wgfin variants, close to the dense_opt ones)."""
+    wgfin as its own launch and of the finalize launch with its fused optimizer (HIPFM_WGFIN=0)
+    (fp8: bitwise between the two wgfin variants, close to the finalize one)."""
     import hipfm.models.deepfm as D
     synth = make_synth("criteo_kaggle", seed=5)
     F, K, layers, B = synth.F, 8, [128, 64, 32], 1024
     params = init_params(synth.feature_size, F, K, layers, False, seed=2)
     out = []
-    for fuse, early, sfwg in ((True, True, True), (True, True, False), (False, True, False),
-                              (False, False, False)):
-        monkeypatch.setattr(D, "_FUSE_FIN_OPT", fuse)
-        monkeypatch.setattr(D, "_DENSE_EARLY", early)
+    for wgfin, sfwg in ((True, True), (True, False), (False, False)):
+        monkeypatch.setattr(D, "_WGFIN", wgfin)
         monkeypatch.setattr(D, "_SFWG", sfwg)
         m = NativeDeepFM(synth.feature_size, F, K, layers, [0.5] * 3, batch_size=B, device=DEV,
                          init=False, optimizer=opt, sparse_update="lazy", mlp_dtype=mlp_dtype,
@@ -486,7 +484,7 @@ def test_finalize_fused_dense_opt_bitwise_equal(monkeypatch, opt, mlp_dtype):
             ids, vals, lab = synth.batch(B, step=s, device=DEV, id_dtype=torch.int32)
             m.train_step(ids, vals, lab, use_graph=True)
         torch.cuda.synchronize()
-        assert m._fin_opt_step == fuse
+        assert m._fin_opt_step
         assert m._sfwg_step == sfwg
         m.check_errors()
         out.append([m.p.clone(), m.tv.clone(), m.tw.clone(), m.sd[0].clone(), m.sd[1].clone(),

@@ -101,11 +101,10 @@ def _modes():
 
 def _knob_sets():
     bools = [True, False]
-    for (sss, early, fin, wg, sf, shd, shx, ds, impl, sw) in itertools.product(
-            bools, bools, bools, bools, bools, bools, bools, ("auto", "1", "0"), ("fused", "seg"),
-            ("auto", "merged", "branch")):
-        yield StepKnobs(sort_side_stream=sss, dense_early=early, fuse_fin_opt=fin, wgfin=wg, sfwg=sf,
-                        sh_apply_dense=shd, sh_xfuse=shx, dense_side_stream=ds, sparse_impl=impl, sweep_mode=sw)
+    for (sss, wg, sf, shd, impl, sw, rs, pipe) in itertools.product(
+            bools, bools, bools, bools, ("fused", "seg"), ("auto", "merged", "branch"), bools, bools):
+        yield StepKnobs(sort_side_stream=sss, wgfin=wg, sfwg=sf, sh_apply_dense=shd, sparse_impl=impl,
+                        sweep_mode=sw, run_sort=rs, shard_pipeline=pipe)
 
 
 def test_plan_invariants_over_the_mode_matrix():
