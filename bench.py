@@ -202,15 +202,16 @@ def main():
                     "host ingest rate and the CLI/Estimator train rate (epoch 0 streamed, then cached)")
     ap.add_argument("--epochs", type=int, default=4, help="--data: epochs (0 streams + caches)")
     ap.add_argument("--threads", type=int, default=16, help="--data: loader threads")
-    ap.add_argument("--field_major_ids", action="store_true",
-                    help="store the resident batches' ids field-major (no transpose before the sorts)")
+    ap.add_argument("--field_major_ids", type=int, default=1,
+                    help="1: store the resident batches' ids field-major ([F, B] storage: the run sort "
+                         "and the tower gather read each field contiguously); 0: row-major")
     ap.add_argument("--force_exchange", action="store_true",
                     help="run the multi-GPU (row-sharded exchange) step on a 1-rank group")
     args = ap.parse_args()
     if os.environ.get("HIPFM_BENCH_NO_GRAPH") == "1":
         args.no_graph = True
-    if os.environ.get("HIPFM_BENCH_FM_IDS") == "1":
-        args.field_major_ids = True
+    if os.environ.get("HIPFM_BENCH_FM_IDS") in ("0", "1"):
+        args.field_major_ids = int(os.environ["HIPFM_BENCH_FM_IDS"])
     fake = os.environ.get("HIPFM_BENCH_FAKE")          # supervisor tests (CPU): fake rank work
     if fake:
         return _fake_child(args, fake)
@@ -268,10 +269,10 @@ def main():
                          emb_dtype=args.emb_dtype)
     _progress()
     if args.field_major_ids:
-        # ids stored field-major ([F, B] storage, [B, F] view): the per-field slot sort reads them
-        # without its transpose launch.  Not the default: on one GPU the sort branch then starts
-        # at once and its 39 LDS-heavy workgroups slow the tower's gather (0.1157-0.1168 vs
-        # 0.1120-0.1123 ms/step); the row-sharded step measured 0.1752 vs 0.1786 (noise level)
+        # ids stored field-major ([F, B] storage, [B, F] view, the layout the input pipeline's
+        # device feeder produces): the run-level sort's 39 per-field workgroups each read one
+        # contiguous field (row-major: a 4-B id per 156-B row, 107 vs 201 us per 20-batch run
+        # sort, 0.1121 vs 0.1141 ms/step; profiles/r4c_*)
         pool = [(ids.t().contiguous().t(), vals, labels) for ids, vals, labels in pool]
     use_graph = not args.no_graph
     P = len(pool)
@@ -293,6 +294,8 @@ def main():
             yield t, e
             t = e
 
+    runs = {}          # each run's batch list, built once: a replay of a known run skips host planning
+
     def run(lo, hi):
         for k, (t, e) in enumerate(chunks(lo, hi)):
             _progress()
@@ -300,7 +303,10 @@ def main():
             # the two batches after the run: their sort / routing is prefetched
             nxt = (pool[e % P][0], pool[(e + 1) % P][0])
             if use_graph and G > 1:
-                model.train_steps(pool[i:i + (e - t)], next_ids=nxt)
+                r = runs.get((i, e - t))
+                if r is None:
+                    r = runs[(i, e - t)] = pool[i:i + (e - t)]
+                model.train_steps(r, next_ids=nxt)
             else:
                 for j in range(e - t):
                     ids, vals, labels = pool[i + j]
@@ -411,6 +417,7 @@ def main():
                 "mlp_dtype": args.mlp_dtype + (" fwd GEMMs, bf16 backward" if args.mlp_dtype == "fp8" else ""),
                 "emb_dtype": args.emb_dtype + (" rows + slots (stochastic rounding), fp32 math"
                                                if args.emb_dtype == "bf16" else " tables + slots"),
+                "ids_layout": "field-major [F, B]" if args.field_major_ids else "row-major [B, F]",
             },
             "eval_auc": round(auc, 5),
             "train_loss": round(loss, 5),

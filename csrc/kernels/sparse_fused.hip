@@ -78,6 +78,18 @@ struct SfArgs {
   int grow_perm;    // 1: grow rows are in SLOT order (b*F + f): gathered through perm, one 48-B row per slot
 };
 
+// one row's record as the lazy optimizer reads it (the f32x4 column group `sub` of v and its
+// slots; w and its slots on sub 0)
+struct SfRec {
+  f32x4 p, s0, s1;
+  float pw, aw, cw;
+};
+template <int K, int OPT>
+__device__ __forceinline__ SfRec sf_load_rec(const SfArgs& A, int key, int sub);
+template <int K, int OPT>
+__device__ __forceinline__ void sf_apply_rec(const SfArgs& A, int key, int sub, f32x4 a, float w, float c,
+                                             float lr_t, SfRec R);
+
 // MODE 0: lazy optimizer OPT on the row; 1: tf1_dense scatter of the row gradient;
 // 2: compact gradient row for the owner exchange
 template <int K, int MODE, int OPT>
@@ -95,18 +107,46 @@ __device__ __forceinline__ void sf_apply_row(const SfArgs& A, int key, int hpos,
   }
   const size_t row = (size_t)(key / A.row_div);
   const size_t rb = row * A.ldv;  // the row's record (v, and the v slots at their offsets)
-  const size_t ow = row * A.ldw;
   const bool bf = MODE == 0 && A.vbf16;
-  f32x4 p = ld_row4(A.tv + rb, sub * 4, bf);
-  const f32x4 gv = a - p * c;
   if (MODE == 1) {
-    *reinterpret_cast<f32x4*>(A.Gv + row * K + sub * 4) = gv;
+    const f32x4 p = ld_row4(A.tv + rb, sub * 4, bf);
+    *reinterpret_cast<f32x4*>(A.Gv + row * K + sub * 4) = a - p * c;
     if (sub == 0) A.Gw[row] = w;
     return;
   }
-  f32x4 s0 = {0, 0, 0, 0}, s1 = {0, 0, 0, 0};
-  if (OPT != OPT_GD) s0 = ld_row4(A.s0v + rb, sub * 4, bf);
-  if (OPT == OPT_ADAM || OPT == OPT_FTRL) s1 = ld_row4(A.s1v + rb, sub * 4, bf);
+  sf_apply_rec<K, OPT>(A, key, sub, a, w, c, lr_t, sf_load_rec<K, OPT>(A, key, sub));
+}
+
+template <int K, int OPT>
+__device__ __forceinline__ SfRec sf_load_rec(const SfArgs& A, int key, int sub) {
+  const size_t row = (size_t)(key / A.row_div);
+  const size_t rb = row * A.ldv, ow = row * A.ldw;
+  const bool bf = A.vbf16;
+  SfRec r;
+  r.p = ld_row4(A.tv + rb, sub * 4, bf);
+  r.s0 = r.s1 = f32x4{0, 0, 0, 0};
+  r.pw = r.aw = r.cw = 0.f;
+  if (OPT != OPT_GD) r.s0 = ld_row4(A.s0v + rb, sub * 4, bf);
+  if (OPT == OPT_ADAM || OPT == OPT_FTRL) r.s1 = ld_row4(A.s1v + rb, sub * 4, bf);
+  if (sub == 0) {
+    r.pw = A.tw[ow];
+    if (OPT != OPT_GD) r.aw = A.s0w[ow];
+    if (OPT == OPT_ADAM || OPT == OPT_FTRL) r.cw = A.s1w[ow];
+  }
+  return r;
+}
+
+// the lazy optimizer on one row whose record ``R`` was loaded (sf_load_rec) -- possibly early, by
+// the tile that owns the row's update (no other workgroup writes it in this launch)
+template <int K, int OPT>
+__device__ __forceinline__ void sf_apply_rec(const SfArgs& A, int key, int sub, f32x4 a, float w, float c,
+                                             float lr_t, SfRec R) {
+  const size_t row = (size_t)(key / A.row_div);
+  const size_t rb = row * A.ldv;
+  const size_t ow = row * A.ldw;
+  const bool bf = A.vbf16;
+  f32x4 p = R.p, s0 = R.s0, s1 = R.s1;
+  const f32x4 gv = a - p * c;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     float gj = gv[j] + A.h.l2 * p[j];
@@ -121,10 +161,10 @@ __device__ __forceinline__ void sf_apply_row(const SfArgs& A, int key, int hpos,
   if (OPT != OPT_GD) st_row4(A.s0v + rb, sub * 4, s0, bf, bf ? row_sr_seed(row, st, 1) : 0u);
   if (OPT == OPT_ADAM || OPT == OPT_FTRL) st_row4(A.s1v + rb, sub * 4, s1, bf, bf ? row_sr_seed(row, st, 2) : 0u);
   if (sub == 0) {
-    float pw = A.tw[ow];
+    float pw = R.pw;
     float gw = w + A.h.l2 * pw;
-    float aw = (OPT != OPT_GD) ? A.s0w[ow] : 0.f;
-    float cw = (OPT == OPT_ADAM || OPT == OPT_FTRL) ? A.s1w[ow] : 0.f;
+    float aw = R.aw;
+    float cw = R.cw;
     opt_update<OPT>(pw, gw, aw, cw, A.h, lr_t);
     A.tw[ow] = pw;
     if (OPT != OPT_GD) A.s0w[ow] = aw;
@@ -326,6 +366,11 @@ __device__ __forceinline__ void sf_tile_body(const SfArgs& A, const int tile, Sf
     __syncthreads();
   }
   SF_ST(2);
+  // the record of this thread's first run head, loaded now: its HBM round trip overlaps the chunk
+  // sums below instead of following them (used if that run closes in this tile)
+  const int pre_u = tid / T::LPS;
+  SfRec pre;
+  if (MODE == 0 && pre_u < nh) pre = sf_load_rec<K, OPT>(A, skl[hl[pre_u]], sub);
   // 2. chunk-local run pieces: in place at the head, leading piece into lead[j]
   for (int t = tid; t < T::NCH * T::C; t += 256) {
     const int j = t / T::C, c = t - j * T::C;
@@ -385,7 +430,10 @@ __device__ __forceinline__ void sf_tile_body(const SfArgs& A, const int tile, Sf
       if (!closed) closed = (next_key != key);
     }
     if (closed) {
-      sf_apply_row<K, MODE, OPT>(A, key, b0 + hp, sub, a, w, c, lr_t);
+      if (MODE == 0 && u == pre_u)
+        sf_apply_rec<K, OPT>(A, key, sub, a, w, c, lr_t, pre);
+      else
+        sf_apply_row<K, MODE, OPT>(A, key, b0 + hp, sub, a, w, c, lr_t);
     } else {
       float* ct = A.ctail + (size_t)tile * T::RS;
 #pragma unroll

@@ -405,7 +405,12 @@ __device__ __forceinline__ void tower_bf16_body(const TowerArgs& a, bf16* lds, f
   float* gx = reinterpret_cast<float*>(reinterpret_cast<unsigned char*>(lds) + (grow ? a.g_off : 0));
   float* gS = gx + TW_ROWS * a.F;
   int* ginv = reinterpret_cast<int*>(gS + TW_ROWS * (KE > 0 ? KE : 1));
-  bf16* gwt = reinterpret_cast<bf16*>(ginv + TW_ROWS * a.F) + wave * TW_ROWS * 40;
+  // the 4 wave tiles of the dX0 phase live in the H tiles' region (dead by then) when it is large
+  // enough: the launch's LDS stays small enough for serve / stamp workgroups to co-reside
+  int hbytes = 0;
+  for (int i = 0; i < nl; ++i) hbytes += 2 * TW_ROWS * (a.Np[i] + 8);
+  bf16* gwt = (hbytes >= 4 * TW_ROWS * 40 * 2 ? lds + a.h_off[0] : reinterpret_cast<bf16*>(ginv + TW_ROWS * a.F)) +
+              wave * TW_ROWS * 40;
   int ivr[TW_GINV];
   if constexpr (KE > 0) {
     // (weights primed DURING the gather slowed it more than they saved: its table-row loads
@@ -916,8 +921,11 @@ HFM_API int hfm_tower(const TowerArgs* ap, int KE, hipStream_t st) {
                                           !a.sv.T.key || a.sv.C <= 0 || a.sv.stamp_off != 2 ||
                                           (long)a.serve_wgs * 256 < (long)a.sv.total * (KE / 4))))
     return (int)hipErrorInvalidValue;
+  int hbytes = 0;
+  for (int i = 0; i < a.nl; ++i) hbytes += 2 * TW_ROWS * (a.Np[i] + 8);
+  const int gwt_bytes = hbytes >= 4 * TW_ROWS * 40 * 2 ? 0 : 4 * TW_ROWS * 40 * 2;
   if (a.grow && (!KE || a.fp8 || !a.train || (a.inv && a.inv_ld < a.M) || a.F > TW_GINV * 256 / TW_ROWS || a.g_off < 0 || (a.g_off & 15) ||
-                 KE > 16 || a.g_off + TW_ROWS * (8 * a.F + 4 * KE) + 4 * TW_ROWS * 40 * 2 > a.lds_bytes))
+                 KE > 16 || a.g_off + TW_ROWS * (8 * a.F + 4 * KE) + gwt_bytes > a.lds_bytes))
     return (int)hipErrorInvalidValue;
   if (a.stamp_wgs < 0 || (a.stamp_wgs && (!KE || !a.train || !a.stamp_keys || !a.stamp_flags || a.stamp_div <= 0 ||
                                           (long)a.stamp_wgs * 256 * TW_STAMP_EPT < a.stamp_n)))

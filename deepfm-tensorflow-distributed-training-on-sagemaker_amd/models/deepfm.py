@@ -469,10 +469,14 @@ class NativeDeepFM(GraphRunnerMixin, NativeStateMixin):
 
     def _tower_grow_layout(self):
         """(byte offset, total LDS bytes) of the tower's sorted-gradient-row scratch, appended to
-        the layout above: x [32][F] f32, S [32][K] f32, inverse perm [32][F] i32, 4 wave tiles
-        [32][40] bf16 (tower.hip tw_grow_tile)."""
+        the layout above: x [32][F] f32, S [32][K] f32, inverse perm [32][F] i32, and the 4 wave
+        tiles [32][40] bf16 of tower.hip tw_grow_tile -- in the H tiles' region (dead by the dX0
+        phase) when it holds them, so the launch stays small enough for 3 workgroups per CU (the
+        run-routed step's serve workgroups co-reside with the tower's two per CU)."""
         g_off = (self._tower_lds_bytes() + 15) // 16 * 16
-        return g_off, g_off + 32 * (8 * self.F + 4 * self.K) + 4 * 32 * 40 * 2
+        hbytes = sum(2 * 32 * (n + 8) for n in self.Np)
+        wt = 0 if hbytes >= 4 * 32 * 40 * 2 else 4 * 32 * 40 * 2
+        return g_off, g_off + 32 * (8 * self.F + 4 * self.K) + wt
 
     @staticmethod
     def _padM(B: int) -> int:
