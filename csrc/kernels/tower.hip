@@ -363,7 +363,9 @@ __device__ __forceinline__ void tw_grow_tile(const TowerArgs& a, const f32x4 (&a
       const f32x4 dx = {bf2f(dxh[0]), bf2f(dxh[1]), bf2f(dxh[2]), bf2f(dxh[3])};
       const f32x4 s = *reinterpret_cast<const f32x4*>(gS + row * KE + sub * 4);
       const float x = gx[row * F + f], dy = s_dl[row];
-      float* gr = a.grow + (size_t)(a.inv ? ginv[f * 32 + row] : (row0 + row) * F + f) * RS;
+      const int pos = !a.inv ? (row0 + row) * F + f
+                             : ginv ? ginv[f * 32 + row] : a.inv[(size_t)f * a.inv_ld + row0 + row];
+      float* gr = a.grow + (size_t)pos * RS;
       *reinterpret_cast<f32x4*>(gr + sub * 4) = sf_slot_a(dx, dy, s, x);
       if (sub == 0) *reinterpret_cast<f32x4*>(gr + KE) = f32x4{sf_slot_gw(dy, x), sf_slot_c(dy, x), 0.f, 0.f};
     }
@@ -373,10 +375,14 @@ __device__ __forceinline__ void tw_grow_tile(const TowerArgs& a, const f32x4 (&a
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-template <int KE>
+// LIGHT: a 2-deep ring instead of the primed layer-0 / dX0 weights -- a launch that carries serve
+// workgroups (run-routed row-sharded step) keeps the register count low enough for them to
+// co-reside with two tower workgroups per CU (240 registers left them queued behind the tower:
+// 68.7 vs 47.3 us)
+template <int KE, bool LIGHT>
 __device__ __forceinline__ void tower_bf16_body(const TowerArgs& a, bf16* lds, float* s_dl, float* s_loss,
                                                 float* s_yfm) {
-  constexpr int TW_NP = tw_np(KE);
+  constexpr int TW_NP = LIGHT ? 2 : tw_np(KE);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int row0 = blockIdx.x * TW_ROWS;
   const int cr = (lane >> 4) * 4, cc = lane & 15;
@@ -401,7 +407,9 @@ __device__ __forceinline__ void tower_bf16_body(const TowerArgs& a, bf16* lds, f
   bf16* Xl = lds + (KE > 0 ? a.x_off : 0);
   // sorted gradient rows: LDS scratch and this block's inverse permutation (prefetched now)
   const bool grow = KE > 0 && a.train && a.grow != nullptr;
-  const bool ginv_on = grow && a.inv != nullptr;  // sorted positions (else rows in slot order)
+  // sorted positions (else rows in slot order); LIGHT reads them from global in the dX0 phase
+  // instead of staging this block's share in LDS (registers held across the dgrad chain)
+  const bool ginv_on = grow && a.inv != nullptr && !LIGHT;
   float* gx = reinterpret_cast<float*>(reinterpret_cast<unsigned char*>(lds) + (grow ? a.g_off : 0));
   float* gS = gx + TW_ROWS * a.F;
   int* ginv = reinterpret_cast<int*>(gS + TW_ROWS * (KE > 0 ? KE : 1));
@@ -423,8 +431,10 @@ __device__ __forceinline__ void tower_bf16_body(const TowerArgs& a, bf16* lds, f
   // the head's operands, then (behind the E^T stores in the memory queue) the first GEMM tile's
   // weights
   float wo[TW_HQ];
+  if (!LIGHT) {
 #pragma unroll
-  for (int j = 0; j < TW_HQ; ++j) wo[j] = j < Q ? a.w_out[hq * Q + j] : 0.f;
+    for (int j = 0; j < TW_HQ; ++j) wo[j] = j < Q ? a.w_out[hq * Q + j] : 0.f;
+  }
   const float bout = a.b_out[0];
   const bool hvalid = a.labels && row0 + hrow < a.nvalid;
   const float hlab = hvalid ? a.labels[row0 + hrow] : 0.f;
@@ -494,7 +504,7 @@ __device__ __forceinline__ void tower_bf16_body(const TowerArgs& a, bf16* lds, f
     float yd = 0.f;
 #pragma unroll
     for (int j = 0; j < TW_HQ; ++j)
-      if (j < Q) yd += bf2f(H[hrow * ldh + hq * Q + j]) * wo[j];
+      if (j < Q) yd += bf2f(H[hrow * ldh + hq * Q + j]) * (LIGHT ? a.w_out[hq * Q + j] : wo[j]);
     for (int j = TW_HQ; j < Q; ++j) yd += bf2f(H[hrow * ldh + hq * Q + j]) * a.w_out[hq * Q + j];
     yd += __shfl_xor(yd, 1, 64);
     yd += __shfl_xor(yd, 2, 64);
@@ -526,7 +536,7 @@ __device__ __forceinline__ void tower_bf16_body(const TowerArgs& a, bf16* lds, f
       for (int j = 0; j < TW_HQ; ++j) {
         if (j < Q) {
           const int col = hq * Q + j;
-          const float g = bf2f(H[hrow * ldh + col]) > 0.f ? dl * wo[j] * sl : 0.f;
+          const float g = bf2f(H[hrow * ldh + col]) > 0.f ? dl * (LIGHT ? a.w_out[col] : wo[j]) * sl : 0.f;
           Z[hrow * ldz + col] = f2bf(g);
         }
       }
@@ -618,7 +628,7 @@ __device__ __forceinline__ void tower_bf16_body(const TowerArgs& a, bf16* lds, f
       if (ct + 4 < a.K0p / 32) prime(ph, ct + 4);
       f32x4 acc[2][2] = {{c00, c01}, {c10, c11}};
       if (grow) {
-        if constexpr (KE > 0) tw_grow_tile<KE>(a, acc, ct, row0, lane, gwt, gx, gS, ginv, s_dl);
+        if constexpr (KE > 0) tw_grow_tile<KE>(a, acc, ct, row0, lane, gwt, gx, gS, ginv_on ? ginv : nullptr, s_dl);
         continue;
       }
 #pragma unroll
@@ -636,6 +646,43 @@ __device__ __forceinline__ void tower_bf16_body(const TowerArgs& a, bf16* lds, f
     }
   }
   TW_ST(15);
+}
+
+template <int KE>
+__device__ __forceinline__ bool tower_aux_wg(const TowerArgs& a) {
+  // the workgroups after the tower's blocks: serve (run-routed sharded step) or stamp (tf1_dense)
+  const int tid = threadIdx.x;
+  const int sb = (int)blockIdx.x - a.M / TW_ROWS;
+  if (sb < 0) return false;
+  if (sb < a.serve_wgs) {
+    sh_serve_elem<KE>(a.sv, sb * 256 + tid);
+    return true;
+  }
+  const int i0 = (sb - a.serve_wgs) * 256 * TW_STAMP_EPT + tid;
+#pragma unroll
+  for (int k = 0; k < TW_STAMP_EPT; ++k) {
+    const int i = i0 + k * 256;
+    if (i < a.stamp_n) {
+      const int key = a.stamp_keys[i];
+      if (i == 0 || a.stamp_keys[i - 1] != key) a.stamp_flags[key / a.stamp_div] = 1;
+    }
+  }
+  return true;
+}
+
+// the run-routed sharded step's launch (tower blocks + serve workgroups): LIGHT body, and the
+// register budget of three workgroups per CU, so the serve workgroups share the CUs with the
+// tower's blocks instead of waiting for them
+template <int KE>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3)))
+tower_light_kernel(TowerArgs a) {
+  extern __shared__ __align__(16) unsigned char tw_lds_raw[];
+  __shared__ float s_dl[TW_ROWS];
+  __shared__ float s_loss[TW_ROWS];
+  __shared__ float s_yfm[TW_ROWS];
+  if (tower_aux_wg<KE>(a)) return;
+  TW_ST(0);
+  tower_bf16_body<KE, true>(a, reinterpret_cast<bf16*>(tw_lds_raw), s_dl, s_loss, s_yfm);
 }
 
 template <bool FP8, int KE, int TW_PF0, int TW_PF1>
@@ -671,7 +718,7 @@ __global__ void __launch_bounds__(256) tower_kernel(TowerArgs a) {
   const int row0 = blockIdx.x * TW_ROWS;
   TW_ST(0);
   if constexpr (!FP8) {
-    tower_bf16_body<KE>(a, lds, s_dl, s_loss, s_yfm);
+    tower_bf16_body<KE, false>(a, lds, s_dl, s_loss, s_yfm);
     return;
   }
   const int cr = (lane >> 4) * 4, cc = lane & 15;
@@ -896,6 +943,15 @@ __global__ void __launch_bounds__(256) tower_kernel(TowerArgs a) {
 template <bool FP8>
 static int tower_launch(const TowerArgs& a, int KE, hipStream_t st) {
   const dim3 g(a.M / TW_ROWS + (KE > 0 ? a.serve_wgs + a.stamp_wgs : 0)), blk(256);
+  if (!FP8 && a.serve_wgs > 0) {
+    switch (KE) {
+      case 4: hipLaunchKernelGGL((tower_light_kernel<4>), g, blk, a.lds_bytes, st, a); return 0;
+      case 8: hipLaunchKernelGGL((tower_light_kernel<8>), g, blk, a.lds_bytes, st, a); return 0;
+      case 16: hipLaunchKernelGGL((tower_light_kernel<16>), g, blk, a.lds_bytes, st, a); return 0;
+      case 32: hipLaunchKernelGGL((tower_light_kernel<32>), g, blk, a.lds_bytes, st, a); return 0;
+      default: return (int)hipErrorInvalidValue;
+    }
+  }
   switch (KE) {
     case 0: hipLaunchKernelGGL((tower_kernel<FP8, 0, 4, 2>), g, blk, a.lds_bytes, st, a); break;
     case 4: hipLaunchKernelGGL((tower_kernel<FP8, 4, 4, 2>), g, blk, a.lds_bytes, st, a); break;
