@@ -202,6 +202,7 @@ def main():
                     "host ingest rate and the CLI/Estimator train rate (epoch 0 streamed, then cached)")
     ap.add_argument("--epochs", type=int, default=4, help="--data: epochs (0 streams + caches)")
     ap.add_argument("--threads", type=int, default=16, help="--data: loader threads")
+    ap.add_argument("--stream_only", action="store_true", help="--data: only the streamed (uncached) arm")
     ap.add_argument("--field_major_ids", type=int, default=1,
                     help="1: store the resident batches' ids field-major ([F, B] storage: the run sort "
                          "and the tower gather read each field contiguously); 0: row-major")
@@ -429,6 +430,10 @@ def main():
             sb = x.step_bytes(G if use_graph else 0)
             out["comm_bytes_per_step"] = sb["sent"]
             out["comm_bytes_moved_per_step"] = sb["moved"]
+            if model.shx is not None:
+                out["config"]["exchange_rows"] = (
+                    f"served {'bf16 v + fp32 w' if model.shx.rbf16 else 'fp32 v + w'} ({model.shx.RWS * 4} B), "
+                    f"gradient fp32 ({model.shx.RWG * 4} B); owners keep fp32 master rows + slots")
         _emit(json.dumps(out))
     model.check_errors()
     if comm is not None:
@@ -579,6 +584,13 @@ def data_bench(args):
         return est, per_epoch
 
     est_s, per_epoch_s = train_arm(cache=False)        # every epoch streamed from the files
+    if args.stream_only:                               # (profiling the streamed path alone)
+        _emit(json.dumps({"metric": "streamed epochs samples/s (1 GPU)", "ingest_rows_per_s": round(ingest, 1),
+                          "streamed_epoch_samples_per_s": [round(n * B / t, 1) for n, t in per_epoch_s],
+                          "epoch_s": [round(t, 4) for _, t in per_epoch_s],
+                          "host_timer_totals_s": {k: round(v, 4) for k, v in est_s.timer.t.items()},
+                          "host_timer_calls": dict(est_s.timer.n)}))
+        return
     sig_s = (est_s.model.p.double().sum().item(), est_s.model.rec.double().sum().item())
     del est_s
     torch.cuda.empty_cache()

@@ -72,6 +72,14 @@ __device__ __forceinline__ bf16 f2bf(float x) { return (bf16)x; }
 __device__ __forceinline__ f32x4 sf_slot_a(f32x4 dx, float dy, f32x4 s, float x) { return (dx + dy * s) * x; }
 __device__ __forceinline__ float sf_slot_gw(float dy, float x) { return dy * x; }
 __device__ __forceinline__ float sf_slot_c(float dy, float x) { return dy * x * x; }
+// A row's gradient from its summed slot terms, g_v = a - v * c, and the whole-table l2 term,
+// g + l2 * p: written as explicit fmas so every kernel that forms them (sparse tile lazy / scatter /
+// exchange rows, owner update, sweeps) rounds identically -- left to contraction, the compiler
+// fused them differently in different kernels (1-ulp slot differences, tf1 split vs scatter).
+__device__ __forceinline__ f32x4 row_grad4(f32x4 a, f32x4 v, float c) {
+  return f32x4{fmaf(-v[0], c, a[0]), fmaf(-v[1], c, a[1]), fmaf(-v[2], c, a[2]), fmaf(-v[3], c, a[3])};
+}
+__device__ __forceinline__ float l2_grad(float g, float l2, float p) { return fmaf(l2, p, g); }
 
 // ---- embedding-table rows: fp32, or bf16 (mixed-precision embeddings, BASELINE config #5) ----
 // A row (or optimizer-slot row) starts at a float* inside the table record; a bf16 row holds its

@@ -50,7 +50,7 @@ __global__ void __launch_bounds__(256) sparse_rows_kernel(
   if (OPT == OPT_ADAM || OPT == OPT_FTRL) c = *reinterpret_cast<f32x4*>(s1v + o);
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    float gj = g[j] + h.l2 * p[j];
+    float gj = l2_grad(g[j], h.l2, p[j]);
     float pj = p[j], aj = a[j], cj = c[j];
     opt_update<OPT>(pj, gj, aj, cj, h, lr_t);
     p[j] = pj; a[j] = aj; c[j] = cj;
@@ -60,7 +60,7 @@ __global__ void __launch_bounds__(256) sparse_rows_kernel(
   if (OPT == OPT_ADAM || OPT == OPT_FTRL) *reinterpret_cast<f32x4*>(s1v + o) = c;
   if (sub == 0) {
     float pw = tw[ow];
-    float gw = UG[u].w + h.l2 * pw;
+    float gw = l2_grad(UG[u].w, h.l2, pw);
     float aw = (OPT != OPT_GD) ? s0w[ow] : 0.f;
     float cw = (OPT == OPT_ADAM || OPT == OPT_FTRL) ? s1w[ow] : 0.f;
     opt_update<OPT>(pw, gw, aw, cw, h, lr_t);
@@ -109,7 +109,7 @@ __global__ void __launch_bounds__(256) dense_sweep_kernel(
     const bool touched = (g[0] != 0.f) | (g[1] != 0.f) | (g[2] != 0.f) | (g[3] != 0.f);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      float gj = g[j] + h.l2 * p[j];
+      float gj = l2_grad(g[j], h.l2, p[j]);
       float pj = p[j], aj = a[j], cj = c[j];
       opt_update<OPT>(pj, gj, aj, cj, h, lr_t);
       p[j] = pj; a[j] = aj; c[j] = cj;
@@ -121,7 +121,7 @@ __global__ void __launch_bounds__(256) dense_sweep_kernel(
     if (sub == 0) {
       float pw = tw[ow];
       float g0 = Gw[row];
-      float gw = g0 + h.l2 * pw;
+      float gw = l2_grad(g0, h.l2, pw);
       float aw = (OPT != OPT_GD) ? s0w[ow] : 0.f;
       float cw = (OPT == OPT_ADAM || OPT == OPT_FTRL) ? s1w[ow] : 0.f;
       opt_update<OPT>(pw, gw, aw, cw, h, lr_t);

@@ -28,6 +28,7 @@
 #include "common.h"
 
 #include "shard_table.h"
+#include "tf1_sweep.h"
 
 namespace {
 constexpr int SH_THREADS = 256;
@@ -308,7 +309,7 @@ __global__ void sh_slot_rows_run_kernel(const ShRouteBatch* __restrict__ rb, int
   R.slot_row[ld ? (size_t)(q % F) * ld + q / F : (size_t)q] = r < 0 ? 0 : r;
 }
 
-// Owner: rows[e] = {v[K], w, 0, 0, 0} of each requested id (zeros for padding entries)
+// Owner: rows[e] = the served row of each requested id (sh_row_words; zeros for padding entries)
 // Training steps (tags != null) also stamp the owner-side request tags here, at the start of the
 // step: the requests of the backward exchange are this step's requests, so the owner update at
 // the end of the step needs no separate tagging launch on the critical path.
@@ -319,18 +320,21 @@ template <int K>
 __global__ void sh_serve_kernel(const int* __restrict__ recv_ids, int total, int N, int C, int rstride,
                                 const float* __restrict__ tv, const float* __restrict__ tw, long ldv,
                                 long ldw, float* __restrict__ rows, const int64_t* __restrict__ step,
-                                ShTable T, int stamp_off, int vbf16) {
-  const ShServeArgs A{recv_ids, total, N, C, rstride, tv, tw, ldv, ldw, rows, step, T, stamp_off, vbf16};
+                                ShTable T, int stamp_off, int vbf16, int rbf16, unsigned char* rflag) {
+  const ShServeArgs A{recv_ids, total, N, C, rstride, tv, tw, ldv, ldw, rows, step, T, stamp_off, vbf16, rbf16,
+                      rflag};
   sh_serve_elem<K>(A, blockIdx.x * blockDim.x + threadIdx.x);
 }
 
 __global__ void sh_owner_tag_kernel(const int* __restrict__ recv_ids, int total, int N, int C, int rstride,
-                                    const int64_t* __restrict__ step, ShTable T, int rdiv) {
+                                    const int64_t* __restrict__ step, ShTable T, int rdiv,
+                                    unsigned char* __restrict__ rflag) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= total) return;
   const int id = sh_rid(recv_ids, e, C, rstride);
   if (id < 0) return;
   sh_insert(T, N, (unsigned)(id / rdiv), e / C, (unsigned)(e % C), (unsigned)(*step + 1));
+  if (rflag) rflag[id / rdiv] = 1;        // tf1_dense split form: this step's row (see the sweep)
 }
 
 // MODE 0: lazy optimizer OPT on the owner's row; 1: tf1_dense scatter into (Gv, Gw)
@@ -341,8 +345,8 @@ __device__ __forceinline__ void sh_owner_apply_elem(int gt, const int* __restric
                                                     float* s0w, float* s1w, long ldv, long ldw, float* Gv,
                                                     float* Gw, OptHyper h, const int64_t* __restrict__ step,
                                                     const ShTable& NT, float* __restrict__ next_rows,
-                                                    int rdiv, int vbf16) {
-  constexpr int LPS = K / 4, RW = K + 4;
+                                                    int rdiv, int vbf16, int rbf16) {
+  constexpr int LPS = K / 4, RWG = sh_grad_words<K>();
   const int e = gt / LPS, sub = gt % LPS;
   if (e >= total) return;
   const int id = sh_rid(recv_ids, e, C, rstride);
@@ -367,19 +371,27 @@ __device__ __forceinline__ void sh_owner_apply_elem(int gt, const int* __restric
       if (OPT == OPT_ADAM || OPT == OPT_FTRL) cw = s1w[ow];
     }
   }
+  f32x4 g = {0.f, 0.f, 0.f, 0.f};
+  float gw = 0.f;
+#ifdef SH_DIAG_NOPROBE
+  {
+    const float* src = recv_g + (size_t)e * RWG;
+    g += f32x4{src[sub * 4], src[sub * 4 + 1], src[sub * 4 + 2], src[sub * 4 + 3]};
+    gw += src[K];
+  }
+#else
   const unsigned long long* tr = sh_find(T, N, (unsigned)row, cur);
   if (!tr) return;  // cannot happen: every received row was inserted by this step's serve / tag
   for (int q = 0; q < p; ++q)
     if ((unsigned)(tr[q] >> 32) == cur) return;  // a lower rank also requested it: it leads
-  f32x4 g = {0.f, 0.f, 0.f, 0.f};
-  float gw = 0.f;
   for (int q = p; q < N; ++q) {
     const unsigned long long t = tr[q];
     if ((unsigned)(t >> 32) != cur) continue;
-    const float* src = recv_g + ((size_t)q * C + (unsigned)t) * RW;
-    g += *reinterpret_cast<const f32x4*>(src + sub * 4);
+    const float* src = recv_g + ((size_t)q * C + (unsigned)t) * RWG;   // (dword-aligned rows)
+    g += f32x4{src[sub * 4], src[sub * 4 + 1], src[sub * 4 + 2], src[sub * 4 + 3]};
     gw += src[K];
   }
+#endif
   if (MODE == 1) {
     *reinterpret_cast<f32x4*>(Gv + row * K + sub * 4) = g;
     if (sub == 0) Gw[row] = gw;
@@ -388,7 +400,7 @@ __device__ __forceinline__ void sh_owner_apply_elem(int gt, const int* __restric
   const float lr_t = OPT == OPT_ADAM ? adam_lr_t(h, *step + 1) : h.lr;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    float gj = g[j] + h.l2 * pv[j];
+    float gj = l2_grad(g[j], h.l2, pv[j]);
     float pj = pv[j], aj = a[j], cj = c[j];
     opt_update<OPT>(pj, gj, aj, cj, h, lr_t);
     pv[j] = pj;
@@ -403,14 +415,18 @@ __device__ __forceinline__ void sh_owner_apply_elem(int gt, const int* __restric
   if (OPT == OPT_ADAM || OPT == OPT_FTRL) st_row4(s1v + rb, sub * 4, c, bf, bf ? row_sr_seed(row, st, 2) : 0u);
   float wnew = 0.f;
   if (sub == 0) {
-    float g1 = gw + h.l2 * pw;
+    float g1 = l2_grad(gw, h.l2, pw);
     opt_update<OPT>(pw, g1, aw, cw, h, lr_t);
     tw[ow] = pw;
     if (OPT != OPT_GD) s0w[ow] = aw;
     if (OPT == OPT_ADAM || OPT == OPT_FTRL) s1w[ow] = cw;
     wnew = pw;
   }
+#ifdef SH_DIAG_NOPATCH
+  if (false) {
+#else
   if (NT.key) {
+#endif
     // the next step's requests were served ahead (before this update): refresh the rows this
     // update changed in every requester's block of the next fetch
     const unsigned long long* nr = sh_find(NT, N, (unsigned)row, cur + 1);
@@ -418,9 +434,8 @@ __device__ __forceinline__ void sh_owner_apply_elem(int gt, const int* __restric
       for (int q = 0; q < N; ++q) {
         const unsigned long long t = nr[q];
         if ((unsigned)(t >> 32) != cur + 1) continue;
-        float* dst = next_rows + ((size_t)q * C + (unsigned)t) * RW;
-        *reinterpret_cast<f32x4*>(dst + sub * 4) = pv;
-        if (sub == 0) *reinterpret_cast<f32x4*>(dst + K) = f32x4{wnew, 0.f, 0.f, 0.f};
+        sh_put_row<K>(next_rows + ((size_t)q * C + (unsigned)t) * sh_row_words<K>(rbf16), sub, pv, wnew,
+                      rbf16 != 0);
       }
     }
   }
@@ -431,10 +446,10 @@ __global__ void sh_owner_apply_kernel(const int* __restrict__ recv_ids, int tota
                                       const float* __restrict__ recv_g, ShTable T, float* tv, float* tw,
                                       float* s0v, float* s1v, float* s0w, float* s1w, long ldv, long ldw,
                                       float* Gv, float* Gw, OptHyper h, const int64_t* __restrict__ step,
-                                      ShTable NT, float* next_rows, int rdiv, int vbf16) {
+                                      ShTable NT, float* next_rows, int rdiv, int vbf16, int rbf16) {
   sh_owner_apply_elem<K, MODE, OPT>(blockIdx.x * blockDim.x + threadIdx.x, recv_ids, total, N, C, rstride,
                                     recv_g, T, tv, tw, s0v, s1v, s0w, s1w, ldv, ldw, Gv, Gw, h, step, NT,
-                                    next_rows, rdiv, vbf16);
+                                    next_rows, rdiv, vbf16, rbf16);
 }
 
 // ------------------------------------------------------------------------------------ host API
@@ -512,7 +527,7 @@ HFM_API int hfm_sh_slot_rows(const int* perm, const int* sid_incl, const int* up
 HFM_API int hfm_sh_serve(int K, const int* recv_ids, int total, int N, int C, int rstride, const float* tv,
                          const float* tw,
                          long ldv, long ldw, float* rows, const int64_t* step, const ShTable* table,
-                         int stamp_off, int vbf16, hipStream_t st) {
+                         int stamp_off, int vbf16, int rbf16, unsigned char* rflag, hipStream_t st) {
   const long th = (long)total * (K / 4);
   const int grid = (int)((th + 255) / 256);
   if (grid == 0) return 0;
@@ -522,7 +537,8 @@ HFM_API int hfm_sh_serve(int K, const int* recv_ids, int total, int N, int C, in
   if (rstride > C && (C <= 0 || rstride % C)) return (int)hipErrorInvalidValue;
   if (stamp_off != 1 && stamp_off != 2) return (int)hipErrorInvalidValue;
 #define CALL(KK) hipLaunchKernelGGL(sh_serve_kernel<KK>, dim3(grid), dim3(256), 0, st, recv_ids, total, N, \
-                                    C, rstride, tv, tw, ldv, ldw, rows, step, T, stamp_off, vbf16)
+                                    C, rstride, tv, tw, ldv, ldw, rows, step, T, stamp_off, vbf16, rbf16, \
+                                    T.key ? rflag : nullptr)
   HFM_K_DISPATCH(K, CALL)
 #undef CALL
   HFM_LAUNCH_CHECK();
@@ -543,6 +559,14 @@ struct ShApplyArgs {
   float* next_rows;   //   (key == null: none) and its served rows, patched by this update
   int rdiv;           // local row = id / rdiv (0: N, the row-sharded owner; 1: a replicated table)
   int vbf16;          // table v rows and v slots are bf16 (lazy mode only)
+  int rbf16;          // the served rows (next_rows) are compact bf16 rows (sh_row_words)
+  // tf1_dense split form (sh_apply_dense): the l2-only update of every local row NOT requested this
+  // step (byte flag rflag, set by the serve / tag kernel), as sweep workgroups of the launch; the
+  // requested rows take their full update from the lazy owner apply
+  float* rec;         // table records [R][rec_ld] (deepfm.py record layout), or null: no sweep
+  unsigned char* rflag;
+  long R;
+  int rec_ld, sweep_blocks;
 };
 
 __host__ __device__ static inline int sh_rdiv(const ShApplyArgs& A) { return A.rdiv > 0 ? A.rdiv : A.N; }
@@ -553,12 +577,12 @@ static int sh_apply_k(int opt, const ShApplyArgs& A, hipStream_t st) {
   const int grid = (int)((th + 255) / 256);
   if (A.mode & 2)  // tags not stamped by this step's serve (eval-style fetch): stamp them here
     hipLaunchKernelGGL(sh_owner_tag_kernel, dim3((A.total + 255) / 256), dim3(256), 0, st, A.recv_ids,
-                       A.total, A.N, A.C, A.rstride, A.step, A.table, sh_rdiv(A));
+                       A.total, A.N, A.C, A.rstride, A.step, A.table, sh_rdiv(A), (unsigned char*)nullptr);
 #define L_(M, O)                                                                                      \
   hipLaunchKernelGGL((sh_owner_apply_kernel<K, M, O>), dim3(grid), dim3(256), 0, st, A.recv_ids, A.total, \
                      A.N, A.C, A.rstride, A.recv_g, A.table, A.tv, A.tw, A.s0v, A.s1v, A.s0w, A.s1w, A.ldv, A.ldw, \
                      A.Gv, A.Gw, A.h, A.step, (M) == 0 ? A.next : ShTable{nullptr, nullptr, 0u, 0}, A.next_rows, \
-                     sh_rdiv(A), (M) == 0 ? A.vbf16 : 0)
+                     sh_rdiv(A), (M) == 0 ? A.vbf16 : 0, A.rbf16)
   if ((A.mode & 1) == 1) {
     L_(1, 0);
     return 0;
@@ -617,7 +641,11 @@ __global__ void __launch_bounds__(256) sh_apply_dense_kernel(ShApplyArgs A, ShDe
   if (b < apply_blocks) {
     sh_owner_apply_elem<K, 0, OPT>(b * 256 + threadIdx.x, A.recv_ids, A.total, A.N, A.C, A.rstride, A.recv_g,
                                    A.table, A.tv, A.tw, A.s0v, A.s1v, A.s0w, A.s1w, A.ldv, A.ldw, A.Gv, A.Gw,
-                                   A.h, A.step, A.next, A.next_rows, sh_rdiv(A), A.vbf16);
+                                   A.h, A.step, A.next, A.next_rows, sh_rdiv(A), A.vbf16, A.rbf16);
+  } else if (b >= apply_blocks + D.blocks) {   // tf1_dense split form: the l2-only sweep
+    const float lr_t = OPT == OPT_ADAM ? adam_lr_t(A.h, *A.step + 1) : A.h.lr;
+    tf1_sweep_rows<K, OPT, 2>(A.rec, A.rec_ld, A.R, A.rflag, A.h, lr_t,
+                              (long)(b - apply_blocks - D.blocks) * 256 + threadIdx.x, (long)A.sweep_blocks * 256);
   } else {
     const float lr_t = OPT == OPT_ADAM ? adam_lr_t(D.h, *A.step + 1) : D.h.lr;
     for (long i = (long)(b - apply_blocks) * 256 + threadIdx.x; i < D.n; i += (long)D.blocks * 256) {
@@ -645,13 +673,18 @@ __global__ void __launch_bounds__(256) sh_apply_dense_kernel(ShApplyArgs A, ShDe
 HFM_API int hfm_sh_apply_dense(int K, int opt, const ShApplyArgs* A, const ShDenseArgs* D, hipStream_t st) {
   if ((A->mode & 1) != 0 || !D->done || D->blocks < 1 || !A->step) return (int)hipErrorInvalidValue;
   if (A->total <= 0) return (int)hipErrorInvalidValue;
+  const bool sweep = A->rec != nullptr;
+  if (sweep && (!A->rflag || A->R <= 0 || A->sweep_blocks < 1 || A->vbf16 || A->next.key ||
+                A->rec_ld < K + 4))
+    return (int)hipErrorInvalidValue;
   if (A->mode & 2)
     hipLaunchKernelGGL(sh_owner_tag_kernel, dim3((A->total + 255) / 256), dim3(256), 0, st, A->recv_ids,
-                       A->total, A->N, A->C, A->rstride, A->step, A->table, sh_rdiv(*A));
+                       A->total, A->N, A->C, A->rstride, A->step, A->table, sh_rdiv(*A),
+                       sweep ? A->rflag : (unsigned char*)nullptr);
   if (A->next.key && (!A->next_rows || (A->next.mask & (A->next.mask + 1)) != 0)) return (int)hipErrorInvalidValue;
   const long th = (long)A->total * (K / 4);
   const int ab = (int)((th + 255) / 256);
-  const dim3 g(ab + D->blocks), blk(256);
+  const dim3 g(ab + D->blocks + (sweep ? A->sweep_blocks : 0)), blk(256);
 #define L_(KK, O) hipLaunchKernelGGL((sh_apply_dense_kernel<KK, O>), g, blk, 0, st, *A, *D, ab)
 #define OPTS(KK)                                         \
   switch (opt) {                                         \

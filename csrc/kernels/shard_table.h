@@ -64,17 +64,45 @@ struct ShServeArgs {
   const float* tv;
   const float* tw;
   long ldv, ldw;
-  float* rows;            // [total][K + 4] {v, w, 0, 0, 0}
+  float* rows;            // [total][sh_row_words<K>(rbf16)] (see sh_row_words)
   const int64_t* step;
   ShTable T;              // key == null: eval-style fetch (no request recorded)
   int stamp_off;          // 1: served at its own step's start; 2: served ahead (previous step)
-  int vbf16;
+  int vbf16;              // the TABLE's v rows are bf16
+  int rbf16;              // served rows carry v as bf16 (compact rows)
+  unsigned char* rflag;   // tf1_dense split form: byte flag of every row requested this step (the
+                          // owner launch's sweep skips and clears it), or null
 };
+
+// Exchanged rows.  Served rows: fp32 {v[K], w, 0, 0, 0} (K + 4 words, 16-B aligned v), or compact
+// {v as K bf16 (round to nearest), w, 0} (K/2 + 2 words: 24 B at K = 8 instead of 48; 8-B aligned,
+// so a 4-element bf16 group is one 8-B load).  Gradient rows: {g_v[K], g_w} (K + 1 words, dword
+// loads / stores).
+template <int K>
+__host__ __device__ constexpr int sh_row_words(int rbf16) { return rbf16 ? K / 2 + 2 : K + 4; }
+template <int K>
+__host__ __device__ constexpr int sh_grad_words() { return K + 1; }
+
+// write the 4 v elements [4*sub, 4*sub + 4) of a served row (and w, on sub 0)
+template <int K>
+__device__ __forceinline__ void sh_put_row(float* o, int sub, f32x4 v, float w, bool rbf) {
+  if (rbf) {
+    const uint32_t lo = (uint32_t)__builtin_bit_cast(uint16_t, f2bf(v[0])) |
+                        ((uint32_t)__builtin_bit_cast(uint16_t, f2bf(v[1])) << 16);
+    const uint32_t hi = (uint32_t)__builtin_bit_cast(uint16_t, f2bf(v[2])) |
+                        ((uint32_t)__builtin_bit_cast(uint16_t, f2bf(v[3])) << 16);
+    *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(o) + sub * 4) = uint2{lo, hi};
+    if (sub == 0) *reinterpret_cast<float2*>(o + K / 2) = float2{w, 0.f};
+  } else {
+    *reinterpret_cast<f32x4*>(o + sub * 4) = v;
+    if (sub == 0) *reinterpret_cast<f32x4*>(o + K) = f32x4{w, 0.f, 0.f, 0.f};
+  }
+}
 
 // thread gt of a serve: request gt / (K/4), f32x4 column gt % (K/4)
 template <int K>
 __device__ __forceinline__ void sh_serve_elem(const ShServeArgs& A, int gt) {
-  constexpr int LPS = K / 4, RW = K + 4;
+  constexpr int LPS = K / 4;
   const int e = gt / LPS, sub = gt % LPS;
   if (e >= A.total) return;
   const int id = sh_rid(A.recv_ids, e, A.C, A.rstride);
@@ -85,11 +113,11 @@ __device__ __forceinline__ void sh_serve_elem(const ShServeArgs& A, int gt) {
     v = ld_row4(A.tv + row * A.ldv, sub * 4, A.vbf16);
     if (sub == 0) {
       w = A.tw[row * A.ldw];
-      if (A.T.key)
+      if (A.T.key) {
         sh_insert(A.T, A.N, (unsigned)row, e / A.C, (unsigned)(e % A.C), (unsigned)(*A.step + A.stamp_off));
+        if (A.rflag) A.rflag[row] = 1;
+      }
     }
   }
-  float* o = A.rows + (size_t)e * RW;
-  *reinterpret_cast<f32x4*>(o + sub * 4) = v;
-  if (sub == 0) *reinterpret_cast<f32x4*>(o + K) = f32x4{w, 0.f, 0.f, 0.f};
+  sh_put_row<K>(A.rows + (size_t)e * sh_row_words<K>(A.rbf16), sub, v, w, A.rbf16 != 0);
 }

@@ -203,7 +203,7 @@ __global__ void __launch_bounds__(256) seg_apply_kernel(SegApplyArgs A) {
   const size_t row = (size_t)(key / A.row_div);
   const float* vrow = A.vsrc ? (A.vsrc + (size_t)(A.vsrc_compact ? u : row) * K) : (A.tv + row * A.ldv);
   const f32x4 v = *reinterpret_cast<const f32x4*>(vrow + sub * 4);
-  const f32x4 gv = a - v * c;
+  const f32x4 gv = row_grad4(a, v, c);
   if (MODE == 2) {
     *reinterpret_cast<f32x4*>(A.UG + (size_t)u * T::RS + sub * 4) = gv;
     if (sub == 0) *reinterpret_cast<f32x4*>(A.UG + (size_t)u * T::RS + K) = f32x4{w, 0.f, 0.f, 0.f};
@@ -221,7 +221,7 @@ __global__ void __launch_bounds__(256) seg_apply_kernel(SegApplyArgs A) {
     if (O == OPT_ADAM || O == OPT_FTRL) s1 = *reinterpret_cast<f32x4*>(A.s1v + o);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      float gj = gv[j] + A.h.l2 * p[j];
+      float gj = l2_grad(gv[j], A.h.l2, p[j]);
       float pj = p[j], aj = s0[j], cj = s1[j];
       opt_update<O>(pj, gj, aj, cj, A.h, lr_t);
       p[j] = pj; s0[j] = aj; s1[j] = cj;
@@ -231,7 +231,7 @@ __global__ void __launch_bounds__(256) seg_apply_kernel(SegApplyArgs A) {
     if (O == OPT_ADAM || O == OPT_FTRL) *reinterpret_cast<f32x4*>(A.s1v + o) = s1;
     if (sub == 0) {
       float pw = A.tw[ow];
-      float gw = w + A.h.l2 * pw;
+      float gw = l2_grad(w, A.h.l2, pw);
       float aw = (O != OPT_GD) ? A.s0w[ow] : 0.f;
       float cw = (O == OPT_ADAM || O == OPT_FTRL) ? A.s1w[ow] : 0.f;
       opt_update<O>(pw, gw, aw, cw, A.h, lr_t);

@@ -59,8 +59,8 @@ struct SfArgs {
   OptHyper h;
   const int64_t* step;
   long ldv, ldw;  // table row strides (record layout: both = record floats)
-  // MODE 2 (row-sharded exchange): gradient row of unique u -> gout[upos[u]] ({g_v, g_w, 0, 0, 0}),
-  // V from the received rows (tv = rows_in, ldv = K + 4); u = sid[head position] - 1
+  // MODE 2 (row-sharded exchange): gradient row of unique u -> gout[upos[u]] ({g_v[K], g_w}), V from
+  // the received rows (tv = rows_in, ldv = their words, vbf16 = their format); u = sid[head] - 1
   const int* sid;
   const int* upos;
   float* gout;
@@ -98,11 +98,15 @@ __device__ __forceinline__ void sf_apply_row(const SfArgs& A, int key, int hpos,
   if (MODE == 2) {
     const int r = A.upos[A.sid[hpos] - 1];
     if (r < 0) return;  // capacity overflow (flagged by the bucketing kernel)
-    const f32x4 pv = A.v_by_key ? ld_row4(A.tv + (size_t)(key / A.row_div) * A.ldv, sub * 4, A.vbf16)
-                                : *reinterpret_cast<const f32x4*>(A.tv + (size_t)r * A.ldv + sub * 4);
-    float* go = A.gout + (size_t)r * (K + 4);
-    *reinterpret_cast<f32x4*>(go + sub * 4) = a - pv * c;
-    if (sub == 0) *reinterpret_cast<f32x4*>(go + K) = f32x4{w, 0.f, 0.f, 0.f};
+    // v from the local table (replicated) or the received row r (row-sharded: vbf16 = the
+    // received rows' format, fp32 or compact bf16)
+    const f32x4 pv = ld_row4(A.tv + (A.v_by_key ? (size_t)(key / A.row_div) : (size_t)r) * A.ldv, sub * 4,
+                             A.vbf16);
+    float* go = A.gout + (size_t)r * (K + 1);      // {g_v[K], g_w}: dword stores
+    const f32x4 gv = row_grad4(a, pv, c);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) go[sub * 4 + j] = gv[j];
+    if (sub == 0) go[K] = w;
     return;
   }
   const size_t row = (size_t)(key / A.row_div);
@@ -110,7 +114,7 @@ __device__ __forceinline__ void sf_apply_row(const SfArgs& A, int key, int hpos,
   const bool bf = MODE == 0 && A.vbf16;
   if (MODE == 1) {
     const f32x4 p = ld_row4(A.tv + rb, sub * 4, bf);
-    *reinterpret_cast<f32x4*>(A.Gv + row * K + sub * 4) = a - p * c;
+    *reinterpret_cast<f32x4*>(A.Gv + row * K + sub * 4) = row_grad4(a, p, c);
     if (sub == 0) A.Gw[row] = w;
     return;
   }
@@ -146,10 +150,10 @@ __device__ __forceinline__ void sf_apply_rec(const SfArgs& A, int key, int sub, 
   const size_t ow = row * A.ldw;
   const bool bf = A.vbf16;
   f32x4 p = R.p, s0 = R.s0, s1 = R.s1;
-  const f32x4 gv = a - p * c;
+  const f32x4 gv = row_grad4(a, p, c);
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    float gj = gv[j] + A.h.l2 * p[j];
+    float gj = l2_grad(gv[j], A.h.l2, p[j]);
     float pj = p[j], aj = s0[j], cj = s1[j];
     opt_update<OPT>(pj, gj, aj, cj, A.h, lr_t);
     p[j] = pj;
@@ -162,7 +166,7 @@ __device__ __forceinline__ void sf_apply_rec(const SfArgs& A, int key, int sub, 
   if (OPT == OPT_ADAM || OPT == OPT_FTRL) st_row4(A.s1v + rb, sub * 4, s1, bf, bf ? row_sr_seed(row, st, 2) : 0u);
   if (sub == 0) {
     float pw = R.pw;
-    float gw = w + A.h.l2 * pw;
+    float gw = l2_grad(w, A.h.l2, pw);
     float aw = R.aw;
     float cw = R.cw;
     opt_update<OPT>(pw, gw, aw, cw, A.h, lr_t);

@@ -56,7 +56,7 @@ __device__ __forceinline__ void tf1_sweep_rows(float* __restrict__ rec, int ld, 
         if (NS >= 2) cc = c[u][q];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          float gj = 0.f + h.l2 * pp[j];
+          float gj = l2_grad(0.f, h.l2, pp[j]);
           float pj = pp[j], aj = aa[j], cj = cc[j];
           opt_update<OPT>(pj, gj, aj, cj, h, lr_t);
           pp[j] = pj; aa[j] = aj; cc[j] = cj;
@@ -67,7 +67,7 @@ __device__ __forceinline__ void tf1_sweep_rows(float* __restrict__ rec, int ld, 
       }
       f32x4 w = wq[u];
       float pw = w[0], aw = w[1], cw = w[2];
-      float gw = 0.f + h.l2 * pw;
+      float gw = l2_grad(0.f, h.l2, pw);
       opt_update<OPT>(pw, gw, aw, cw, h, lr_t);
       w[0] = pw;
       if (NS >= 1) w[1] = aw;

@@ -991,7 +991,7 @@ HFM_API int hfm_tower(const TowerArgs* ap, int KE, hipStream_t st) {
       for (int i = 0; i + 1 < a.nl; ++i)
         if (a.Np[i] > a.K0p) return (int)hipErrorInvalidValue;
     if (!a.idx || !a.vals || !a.tv || !a.tw || !a.fm_bias || a.F * KE > a.K0p || a.x_off < 0 ||
-        (a.train && !a.Et) || (a.fp8 && a.x8_off < 0) || (a.ldv & 3) || (a.idx_ld && a.idx_ld < a.M))
+        (a.train && !a.Et) || (a.fp8 && a.x8_off < 0) || (a.ldv & (a.vbf16 ? 1 : 3)) || (a.idx_ld && a.idx_ld < a.M))
       return (int)hipErrorInvalidValue;
   }
   if (a.fp8) {

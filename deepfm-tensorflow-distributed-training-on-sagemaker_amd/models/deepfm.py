@@ -64,6 +64,7 @@ _SH_APPLY_DENSE = flag("HIPFM_SH_APPLY_DENSE")
 _GROW = knob("HIPFM_GROW")     # 0 off | 1 rows at their sorted positions | 2 rows in slot order
 # tf1_dense on one GPU: split sweep concurrent with the step (0: scatter + full-table sweep)
 _TF1_SPLIT = flag("HIPFM_TF1_SPLIT")
+_XROWS = knob("HIPFM_XROWS")
 _SWEEP_MODE = knob("HIPFM_SWEEP_MODE")      # auto | merged | branch
 _SWEEP_MBLK = int(knob("HIPFM_SWEEP_MBLK"))  # merged-mode sweep workgroups: 512 0.191, 1024 0.179, 2048 0.156, 3072 0.156, 6144 0.172 ms
 _SWEEP_WG = int(knob("HIPFM_SWEEP_WG"))   # 128: 0.178, 256: 0.160, 512: 0.179 ms
@@ -181,8 +182,13 @@ class NativeDeepFM(GraphRunnerMixin, NativeStateMixin):
                  batch_norm_decay: float = 0.9, adam_epsilon: float = 1e-8,
                  adagrad_init: float = 1e-8, fused: Optional[bool] = None,
                  field_ranges: Optional[Sequence[Tuple[int, int]]] = None, mlp_dtype: str = "bf16",
-                 emb_dtype: str = "fp32"):
+                 emb_dtype: str = "fp32", exchange_rows: Optional[str] = None):
         self.batch_norm = bool(batch_norm)
+        # row-sharded exchange: the served rows carry v as bf16 (the compute dtype; owners keep fp32
+        # master rows and optimizer state) or fp32 (bitwise the one-GPU step's reads)
+        self.exchange_rows = exchange_rows or _XROWS
+        if self.exchange_rows not in ("bf16", "fp32"):
+            raise ValueError(f"exchange_rows must be bf16 or fp32, got {self.exchange_rows!r}")
         self.bn_decay = float(batch_norm_decay)
         if mlp_dtype not in ("bf16", "fp8"):
             raise ValueError(f"mlp_dtype must be bf16 or fp8, got {mlp_dtype!r}")
@@ -590,6 +596,15 @@ class NativeDeepFM(GraphRunnerMixin, NativeStateMixin):
             # replicated table (Horovod parity): fixed-capacity all-gather of unique gradient rows
             from ..parallel.replicated import ReplicatedExchange
             self.rpx = ReplicatedExchange(self, self.comm.engine, self.comm.capacity)
+        # tf1_dense under the native exchange, split form: the rows requested this step (any rank)
+        # take their full update in the lazy owner launch and get a byte flag (set by the serve /
+        # tag kernel); every other local row gets its l2-only update from sweep workgroups of the
+        # same launch (instead of a [R, K] gradient scatter plus a full-table sweep)
+        self.tf1_xsplit = (self.sparse_update == "tf1_dense" and self.record and _TF1_SPLIT and self.fused and
+                           (self.shx is not None or self.rpx is not None) and self.K in (4, 8, 16, 32) and
+                           not self.emb_bf16 and _SH_APPLY_DENSE and _WGFIN and
+                           getattr(self, "_wgfin_ns", 1 << 30) <= KN.SFWG_MAX_NS)
+        self._xflags = torch.zeros(self.R, dtype=torch.uint8, device=dev) if self.tf1_xsplit else None
         self._own_in = (self.idx, self.vals, self.labels)
         self._graphs = {}
         self._run_memo = {}
@@ -1268,6 +1283,7 @@ class NativeDeepFM(GraphRunnerMixin, NativeStateMixin):
                         exchange=self.exchange, native_exchange=(self.shx is not None or self.rpx is not None),
                         row_sharded=self.shx is not None, lazy_rows=self.lazy_rows,
                         lazy=self.sparse_update == "lazy", tf1_split=self.tf1_split, fp8=self.fp8,
+                        tf1x=getattr(self, "tf1_xsplit", False),
                         wgfin_fits=getattr(self, "_wgfin_ns", 1 << 30) <= KN.SFWG_MAX_NS,
                         fin_covers_all=self._fin_covers_all, grow_ok=self.grow is not None)
 
@@ -1400,6 +1416,11 @@ class NativeDeepFM(GraphRunnerMixin, NativeStateMixin):
         S.rec, S.flags = self.rec.data_ptr(), self._row_flags[self._tf1_plan[0]].data_ptr()
         S.sw_step, S.R, S.ld, S.nblk = self.sw_step.data_ptr(), self.R, self.rec.shape[1], _SWEEP_MBLK
         return S
+
+    def sweep_fields(self, S):
+        """tf1_dense split form under the exchange: the owner launch's sweep workgroups (ShApplyArgs)."""
+        S.rec, S.rflag = self.rec.data_ptr(), self._xflags.data_ptr()
+        S.R, S.rec_ld, S.sweep_blocks = self.R, self.rec.shape[1], _SWEEP_MBLK
 
     def _sweep_src(self):
         if self._sweep_stream is None:

@@ -62,6 +62,8 @@ class ModeSpec:
     wgfin_fits: bool           # the wgfin work fits the sparse + wgfin launch (splits <= SFWG_MAX_NS)
     fin_covers_all: bool       # the finalize launch covers every dense parameter
     grow_ok: bool = False      # the tower can write sorted gradient rows (bf16 gather tower, K <= 16)
+    tf1x: bool = False         # tf1_dense split form under the native exchange (lazy owner update +
+                               # flagged l2-only sweep in the owner launch)
 
 
 @dataclass(frozen=True)
@@ -131,7 +133,8 @@ def plan_step(mode: ModeSpec, kn: StepKnobs, B: int, sort_plan: Optional[Tuple],
     # row-sharded / replicated lazy step with wgfin: the dense gradient is computed in the sparse
     # backward's launch and travels with the gradient rows (all-gather, summed in rank order by
     # the owner launch): no comm stream, no all-reduce, no cross-stream joins
-    xfuse = (mode.native_exchange and mode.lazy and kn.wgfin and mode.fused and
+    owner_lazy = mode.lazy or mode.tf1x          # the owner launch applies the rows lazily
+    xfuse = (mode.native_exchange and owner_lazy and kn.wgfin and mode.fused and
              kn.sh_apply_dense and mode.wgfin_fits)
     # fused tower, multi-rank: the weight gradients only feed the dense optimizer, so they run on
     # their own branch beside the sparse exchange (0.210 -> 0.199 ms); on one GPU a concurrent
@@ -147,7 +150,7 @@ def plan_step(mode: ModeSpec, kn: StepKnobs, B: int, sort_plan: Optional[Tuple],
     if merged and not sfwg:
         raise RuntimeError("tf1_dense merged sweep planned but the step took another path")
     ex_ar = mode.native_exchange and not xfuse
-    sh_dense = mode.native_exchange and mode.lazy and kn.sh_apply_dense and not early
+    sh_dense = mode.native_exchange and owner_lazy and kn.sh_apply_dense and not early
     return StepPlan(
         run_sorted=run, presorted=presorted, fork_sort=fork,
         sort_idst=fork and not mode.gather_fused and field_sort and idst_capable,

@@ -127,7 +127,8 @@ class ShServeArgs(C.Structure):
     """shard_table.h ShServeArgs: a row serve (here: the next batch's, inside the tower launch)."""
     _fields_ = [("recv_ids", c_void_p), ("total", c_int), ("N", c_int), ("C", c_int), ("rstride", c_int),
                 ("tv", c_void_p), ("tw", c_void_p), ("ldv", c_long), ("ldw", c_long), ("rows", c_void_p),
-                ("step", c_void_p), ("T", ShTable), ("stamp_off", c_int), ("vbf16", c_int)]
+                ("step", c_void_p), ("T", ShTable), ("stamp_off", c_int), ("vbf16", c_int),
+                ("rbf16", c_int), ("rflag", c_void_p)]
 
 
 class ShApplyArgs(C.Structure):
@@ -136,7 +137,8 @@ class ShApplyArgs(C.Structure):
                 ("s0v", c_void_p), ("s1v", c_void_p), ("s0w", c_void_p), ("s1w", c_void_p),
                 ("ldv", c_long), ("ldw", c_long), ("Gv", c_void_p), ("Gw", c_void_p), ("h", OptHyper),
                 ("step", c_void_p), ("next", ShTable), ("next_rows", c_void_p), ("rdiv", c_int),
-                ("vbf16", c_int)]
+                ("vbf16", c_int), ("rbf16", c_int), ("rec", c_void_p), ("rflag", c_void_p), ("R", c_long),
+                ("rec_ld", c_int), ("sweep_blocks", c_int)]
 
 
 class ShDenseArgs(C.Structure):
@@ -266,7 +268,7 @@ _SIGS = {
     "hfm_sh_bucket": [c_void_p, c_void_p, c_int, c_int, c_int] + [c_void_p] * 5 + [c_void_p],
     "hfm_sh_slot_rows": [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p],
     "hfm_sh_serve": [c_int, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_long, c_long, c_void_p,
-                     c_void_p, c_void_p, c_int, c_int, c_void_p],
+                     c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p],
     "hfm_sh_owner_apply": [c_int, c_int, c_void_p, c_void_p],
     "hfm_sh_apply_args_bytes": [],
     "hfm_sh_apply_dense": [c_int, c_int, c_void_p, c_void_p, c_void_p],

@@ -39,6 +39,15 @@ STAMPS = knob("HIPFM_BUILD_STAMPS") == "1"
 if STAMPS:
     KERNELS_SO = os.path.join(LIB_DIR, "libhipfm_kernels_stamps.so")
     BUILD_DIR = BUILD_DIR + "_stamps"
+# diagnostic variants: HIPFM_BUILD_VARIANT=<tag>:<DEF1>,<DEF2> -> -D<DEF> for each, own objects and
+# library libhipfm_kernels_<tag>.so (loaded with HIPFM_KERNELS_SO; delete it after the experiment)
+VARIANT = knob("HIPFM_BUILD_VARIANT")
+VDEFS = []
+if VARIANT:
+    _vtag, _, _vdefs = VARIANT.partition(":")
+    KERNELS_SO = os.path.join(LIB_DIR, f"libhipfm_kernels_{_vtag}.so")
+    BUILD_DIR = BUILD_DIR + "_" + _vtag
+    VDEFS = ["-D" + d for d in _vdefs.split(",") if d]
 IO_SO = os.path.join(LIB_DIR, "libhipfm_io.so")
 
 
@@ -100,7 +109,7 @@ def build_kernels(force: bool = False, jobs: int = 8, verbose: bool = False) -> 
     def cmd_of(s, o):
         return [hipcc, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17",
                 "-fvisibility=hidden", "-Wno-unused-result", *([] if PACKED else NO_PACKED_F32),
-                *(["-DHFM_STAMPS"] if STAMPS else []),
+                *(["-DHFM_STAMPS"] if STAMPS else []), *VDEFS,
                 "-c", s, "-o", o]
 
     for s in srcs:

@@ -606,8 +606,10 @@ _byref = C.byref
 
 
 def sh_serve(K, recv_ids, total, N, tv, tw, rows, C: int = 0, step=None, table=None, rstride: int = 0,
-             ahead: bool = False):
-    """Owner side of the row fetch: rows[e] = {v, w} of every requested id.  With ``table`` (a
+             ahead: bool = False, rbf16: bool = False, rflag=None):
+    """Owner side of the row fetch: rows[e] = {v, w} of every requested id (``rbf16``: compact rows,
+    v as bf16 -- shard_table.h sh_row_words; ``rflag``: tf1_dense split form, a byte flag set per
+    requested row).  With ``table`` (a
     ShTable; training steps) it also records each request (row, requester, slot) stamped with
     step + 1 in the owner's request table read by sh_owner_apply -- step + 2 with ``ahead`` (the
     NEXT step's rows, served during this step; this step's owner update patches the rows it
@@ -616,7 +618,7 @@ def sh_serve(K, recv_ids, total, N, tv, tw, rows, C: int = 0, step=None, table=N
     rp = recv_ids if isinstance(recv_ids, int) else ptr(recv_ids)
     check(L().hfm_sh_serve(K, rp, total, N, C, rstride, ptr(tv), ptr(tw), *_ld(tv, tw), ptr(rows),
                            ptr(step), _byref(table) if table is not None else None, 2 if ahead else 1,
-                           _bf(tv), stream_handle()), "sh_serve")
+                           _bf(tv), 1 if rbf16 else 0, ptr(rflag), stream_handle()), "sh_serve")
 
 
 def sh_apply_dense(K, opt, args: ShApplyArgs, dense):

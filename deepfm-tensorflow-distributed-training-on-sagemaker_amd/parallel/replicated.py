@@ -54,7 +54,7 @@ class ReplicatedExchange:
         n = m.M * m.F
         self.C = min(n, int(capacity)) if capacity else n
         self.C = (self.C + 63) // 64 * 64
-        self.RW = m.K + 4
+        self.RW = m.K + 1                     # gradient rows {g_v[K], g_w} (shard_table.h sh_grad_words)
         i32 = dict(dtype=torch.int32, device=dev)
         f32 = dict(dtype=torch.float32, device=dev)
         self.send_ids = torch.full((self.C,), -1, **i32)
@@ -112,7 +112,7 @@ class ReplicatedExchange:
         S = ShApplyArgs()
         S.recv_ids, S.total, S.N, S.C = self.g_ids.data_ptr(), self.N * self.C, self.N, self.C
         S.rstride, S.rdiv = 0, 1
-        S.mode = (0 if m.sparse_update == "lazy" else 1) | 2          # tags stamped in the launch
+        S.mode = (0 if (m.sparse_update == "lazy" or m.tf1_xsplit) else 1) | 2   # tags stamped in the launch
         S.recv_g, S.table = self.g_rows.data_ptr(), self.table
         S.tv, S.tw = m.tv.data_ptr(), m.tw.data_ptr()
         S.s0v, S.s1v, S.s0w, S.s1w = (t.data_ptr() if t.numel() else 0 for t in m.sv)
@@ -122,6 +122,10 @@ class ReplicatedExchange:
         S.h = m.h_sparse
         S.step = m.step.data_ptr()
         S.vbf16 = 1 if m.emb_bf16 else 0
+        if m.tf1_xsplit:                    # flags from the tag kernel, l2-only sweep of the rest
+            if dense is None:
+                raise RuntimeError("tf1_dense split form: the sweep rides in the owner + dense launch")
+            m.sweep_fields(S)
         if dense is not None:
             KN.sh_apply_dense(m.K, m.opt_id, S, dense)
             return

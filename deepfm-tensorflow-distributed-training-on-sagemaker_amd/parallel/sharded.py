@@ -194,15 +194,20 @@ class FixedCapacityExchange:
         K, n = m.K, m.M * m.F
         self.C = int(capacity) if capacity else default_capacity(n, self.N)
         self.C = (self.C + 63) // 64 * 64
-        self.RW = K + 4                      # exchanged row: {v[K], w, 0, 0, 0} / {g_v, g_w, 0, 0, 0}
+        # exchanged rows (csrc/kernels/shard_table.h sh_row_words): served rows {v as bf16, w, 0}
+        # (K/2 + 2 words; the fused gather tower reads bf16 v) or {v[K], w, 0, 0, 0} (K + 4 words);
+        # gradient rows {g_v[K], g_w} (K + 1 words)
+        self.rbf16 = m.exchange_rows == "bf16" and m.fused and m.gather_fused
+        self.RWS = K // 2 + 2 if self.rbf16 else K + 4
+        self.RWG = K + 1
         T = self.N * self.C
         f32 = dict(dtype=torch.float32, device=dev)
-        self.sets = [_RouteSet(m, n, self.N, self.C, m.temp.numel(), self.RW) for _ in range(self.NSETS)]
+        self.sets = [_RouteSet(m, n, self.N, self.C, m.temp.numel(), self.RWS) for _ in range(self.NSETS)]
         self.cur = 0
         self.err = m.err_words[2:3]          # capacity overflow (the model's error words)
-        self.rows_in = torch.zeros(T, self.RW, **f32)
-        self.send_g = torch.zeros(T, self.RW, **f32)
-        self.recv_g = torch.zeros(T, self.RW, **f32)
+        self.rows_in = torch.zeros(T, self.RWS, **f32)
+        self.send_g = torch.zeros(T, self.RWG, **f32)
+        self.recv_g = torch.zeros(T, self.RWG, **f32)
         self._side = None
         self._serve_stream = None
         self._main = None
@@ -269,7 +274,7 @@ class FixedCapacityExchange:
         B = batches[0][1]
         n = B * m.F
         while len(self.run_sets) < G:
-            self.run_sets.append(_RouteSet(m, m.M * m.F, self.N, self.C, m.temp.numel(), self.RW))
+            self.run_sets.append(_RouteSet(m, m.M * m.F, self.N, self.C, m.temp.numel(), self.RWS))
         sets = self.run_sets[:G]
         grow = m.grow is not None and m.grow_sorted
         for rs in sets:
@@ -324,7 +329,7 @@ class FixedCapacityExchange:
         a.tv, a.tw = m.tv.data_ptr(), m.tw.data_ptr()
         a.ldv, a.ldw = KN._ld(m.tv, m.tw)
         a.rows, a.step, a.T = rs.rows_out.data_ptr(), m.step.data_ptr(), rs.table
-        a.stamp_off, a.vbf16 = (2 if ahead else 1), KN._bf(m.tv)
+        a.stamp_off, a.vbf16, a.rbf16 = (2 if ahead else 1), KN._bf(m.tv), int(self.rbf16)
         return a
 
     def _rs(self, plan: ShPlan) -> _RouteSet:
@@ -468,11 +473,12 @@ class FixedCapacityExchange:
         if plan.serve:
             if train:
                 KN.sh_serve(m.K, rs.recv_ptr, self.N * self.C, self.N, m.tv, m.tw, rs.rows_out,
-                            C=self.C, step=m.step, table=rs.table, rstride=rs.rstride)
+                            C=self.C, step=m.step, table=rs.table, rstride=rs.rstride, rbf16=self.rbf16,
+                            rflag=m._xflags)
             else:
                 KN.sh_serve(m.K, rs.recv_ptr, self.N * self.C, self.N, m.tv, m.tw, rs.rows_out, C=self.C,
-                            rstride=rs.rstride)
-        ops = [(KN.COMM_A2A, rs.rows_out, self.rows_in, self.C * self.RW * 4)]
+                            rstride=rs.rstride, rbf16=self.rbf16)
+        ops = [(KN.COMM_A2A, rs.rows_out, self.rows_in, self.C * self.RWS * 4)]
         if train and plan.n1_mode == "xchg":
             ops.append(self._ids_op(self._set(plan, 1)))
         self._issue(ops)                                                 # G1
@@ -488,13 +494,21 @@ class FixedCapacityExchange:
             self._serve_stream.wait_stream(self._main)
             with torch.cuda.stream(self._serve_stream):
                 KN.sh_serve(m.K, nx.recv_ids, self.N * self.C, self.N, m.tv, m.tw, nx.rows_out, C=self.C,
-                            step=m.step, table=nx.table, ahead=True)
+                            step=m.step, table=nx.table, ahead=True, rbf16=self.rbf16)
                 self._served_ev = torch.cuda.Event()
                 self._served_ev.record(self._serve_stream)
         if train and self._fork_at == "fetch":
             self.fork_next()
         self.gather_ld = rs.slot_ld
-        return rs.slot_row, self.rows_in[:, : m.K], self.rows_in[:, m.K]
+        return (rs.slot_row,) + self.row_views()
+
+    def row_views(self):
+        """(v, w) views of the received rows as the tower's gather reads them (a bf16 v view of the
+        compact rows: row stride RWS words, KN._bf true)."""
+        K = self.m.K
+        if self.rbf16:
+            return self.rows_in.view(torch.bfloat16)[:, :K], self.rows_in[:, K // 2]
+        return self.rows_in[:, :K], self.rows_in[:, K]
 
     def backward(self, plan: ShPlan, B: int, dense=None, join=None, wgfin=None, dense_ar=None):
         """Per-unique gradient rows -> owners -> rank-ordered sum + row update on the owner.
@@ -509,8 +523,10 @@ class FixedCapacityExchange:
         n = B * m.F
         A = m.sf_args(n)
         A.sorted_keys, A.perm = rs.sorted_keys.data_ptr(), rs.perm.data_ptr()
-        A.tv, A.tw = self.rows_in.data_ptr(), self.rows_in.data_ptr() + 4 * m.K
-        A.ldv = A.ldw = self.RW
+        A.tv = self.rows_in.data_ptr()
+        A.tw = A.tv + 4 * (m.K // 2 if self.rbf16 else m.K)
+        A.ldv = A.ldw = self.RWS
+        A.vbf16 = int(self.rbf16)            # (MODE 2 reads v from the received rows)
         A.sid, A.upos, A.gout = rs.sid_incl.data_ptr(), rs.upos.data_ptr(), self.send_g.data_ptr()
         if wgfin is not None:
             KN.sparse_wgfin_x(m.K, A, wgfin)
@@ -518,7 +534,7 @@ class FixedCapacityExchange:
             KN.sparse_fused(m.K, KN.SF_EXCHANGE, m.opt_id, A)
         if join is not None:
             join()
-        ops = [(KN.COMM_A2A, self.send_g, self.recv_g, self.C * self.RW * 4)]
+        ops = [(KN.COMM_A2A, self.send_g, self.recv_g, self.C * self.RWG * 4)]
         if wgfin is not None:
             if self.dense_recv is None:
                 self.dense_recv = torch.zeros(self.N * m.P, dtype=torch.float32, device=m.device)
@@ -533,7 +549,10 @@ class FixedCapacityExchange:
         S = ShApplyArgs()
         S.recv_ids, S.total, S.N, S.C = rs.recv_ptr, self.N * self.C, self.N, self.C
         S.rstride = rs.rstride
-        S.mode = 0 if m.sparse_update == "lazy" else 1      # tags were stamped by the serve
+        # lazy owner update (lazy rows, or the tf1_dense split form: the flagged requested rows;
+        # the sweep workgroups take every other row) or the tf1_dense gradient scatter; the tags
+        # were stamped by the serve
+        S.mode = 0 if (m.sparse_update == "lazy" or m.tf1_xsplit) else 1
         S.recv_g, S.table = self.recv_g.data_ptr(), rs.table
         S.tv, S.tw = m.tv.data_ptr(), m.tw.data_ptr()
         S.s0v, S.s1v, S.s0w, S.s1w = (t.data_ptr() if t.numel() else 0 for t in m.sv)
@@ -543,6 +562,7 @@ class FixedCapacityExchange:
         S.h = m.h_sparse
         S.step = m.step.data_ptr()
         S.vbf16 = 1 if m.emb_bf16 else 0
+        S.rbf16 = int(self.rbf16)
         if plan.run and plan.serve_ahead:
             # the next run step's rows were served in this step's tower launch: patch what changes
             nx = self.run_sets[plan.c + 1]
@@ -552,6 +572,10 @@ class FixedCapacityExchange:
             self._main.wait_event(self._served_ev)
             nx = self._set(plan, 1)
             S.next, S.next_rows = nx.table, nx.rows_out.data_ptr()
+        if m.tf1_xsplit:
+            if dense is None:
+                raise RuntimeError("tf1_dense split form: the sweep rides in the owner + dense launch")
+            m.sweep_fields(S)
         if dense is not None:
             KN.sh_apply_dense(m.K, m.opt_id, S, dense)
             return
@@ -564,8 +588,8 @@ class FixedCapacityExchange:
         ranks (rows G1 + gradient rows G2 + dense gradient all-gather + its share of the run's ids
         all-to-all), ``moved`` = bytes its collectives deliver including its own block (what a
         1-rank proxy copies).  Fixed-capacity blocks: independent of the batch's contents."""
-        N, C, RW, P = self.N, self.C, self.RW, self.m.P
-        per_peer = C * RW * 4 * 2 + C * 4 / max(1, run_steps) * (1 if run_steps else 0)
+        N, C, P = self.N, self.C, self.m.P
+        per_peer = C * (self.RWS + self.RWG) * 4 + C * 4 / max(1, run_steps) * (1 if run_steps else 0)
         dense = P * 4
         return {"sent": int((N - 1) * (per_peer + dense)), "moved": int(N * (per_peer + dense))}
 

@@ -51,6 +51,8 @@ KNOBS: Dict[str, Knob] = {
     "HIPFM_GROW": Knob("1", "variant", "run-sorted steps: the tower writes per-slot gradient rows, 1 at "
                        "their sorted positions (streamed), 2 in slot order (gathered through perm); 0: the "
                        "sparse launch gathers dX0 / S / vals / dlogit per slot"),
+    "HIPFM_XROWS": Knob("bf16", "variant", "row-sharded exchange rows: bf16 (v as bf16 + fp32 w, 24 B at "
+                        "K = 8; fused gather tower) | fp32 (48 B, bitwise the one-GPU reads)"),
     "HIPFM_TF1_SPLIT": Knob("1", "variant", "tf1_dense on one GPU: split form (0: gradient scatter + "
                             "full-table sweep, the oracle in tests/test_gpu_tf1.py)"),
     "HIPFM_SWEEP_MODE": Knob("auto", "variant", "tf1_dense split sweep: merged (workgroups of the "
@@ -73,6 +75,7 @@ KNOBS: Dict[str, Knob] = {
     "HIPFM_ARCH": Knob("gfx950", "harness", "offload arch of the HIP build"),
     "HIPFM_KERNELS_SO": Knob(None, "harness", "path of the kernel library (default: in-tree _lib)"),
     "HIPFM_BUILD_PACKED": Knob(None, "harness", "build: packed-FP32 ops on (own objects / library)"),
+    "HIPFM_BUILD_VARIANT": Knob(None, "harness", "build: diagnostic variant <tag>:<DEF>,<DEF> (own objects / library)"),
     "HIPFM_BUILD_STAMPS": Knob(None, "harness", "build: per-workgroup phase stamps (own objects / library)"),
     "HIPFM_BENCH_FM_IDS": Knob(None, "harness", "bench: resident batches' ids stored field-major (= --field_major_ids)"),
     "HIPFM_BENCH_STAMPS": Knob(None, "harness", "bench: save the stamp build's phase stamps (.npz path)"),

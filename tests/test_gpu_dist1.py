@@ -35,6 +35,13 @@ def group():
     dist.destroy_process_group()
 
 
+@pytest.fixture(autouse=True)
+def _xrows(monkeypatch, request):
+    """Exchanged rows: fp32 (bitwise the local step's reads) unless a test asks for bf16."""
+    import hipfm.models.deepfm as D
+    monkeypatch.setattr(D, "_XROWS", getattr(request, "param", "fp32"))
+
+
 @pytest.mark.parametrize("sharded,update,prefetch", [(True, "lazy", False), (True, "tf1_dense", False),
                                                      (False, "lazy", False), (True, "lazy", True),
                                                      (False, "tf1_dense", False), (False, "lazy", True)])
@@ -138,8 +145,10 @@ def test_exchange_field_major_batches_bitwise(group):
         assert torch.equal(x, y)
 
 
-@pytest.mark.parametrize("update,fm", [("lazy", False), ("tf1_dense", False), ("lazy", True)])
-def test_exchange_run_routing_bitwise(group, monkeypatch, update, fm):
+@pytest.mark.parametrize("update,fm,_xrows", [("lazy", False, "fp32"), ("tf1_dense", False, "fp32"),
+                                              ("lazy", True, "fp32"), ("lazy", True, "bf16"),
+                                              ("tf1_dense", False, "bf16")], indirect=["_xrows"])
+def test_exchange_run_routing_bitwise(group, monkeypatch, update, fm, _xrows):
     """Run-level routing (FixedCapacityExchange.route_run: every batch of a multi-step graph
     sorted, routed and its ids exchanged at the graph's start; each step serves its rows inline)
     gives bitwise the parameters of the per-step pipelined routing (side-stream routing, serve
@@ -290,3 +299,116 @@ def test_exchange_mode_matrix(group, mode):
     tol = 1e-6 if mode != "emb_bf16" else 2e-3
     assert torch.allclose(a.tv.float(), b.tv.float(), atol=tol) and torch.allclose(a.tw, b.tw, atol=1e-6)
     assert torch.allclose(a.p, b.p, atol=1e-6)
+
+
+@pytest.mark.parametrize("emb", ["fp32", "bf16"])
+def test_bf16_exchange_rows(group, emb):
+    """Compact exchanged rows (v as bf16 + fp32 w: 24 B instead of 48 at K = 8; gradient rows
+    K + 1 words).  A bf16 table's rows convert exactly: bitwise the fp32-row exchange.  An fp32
+    table's forward / backward read bf16-rounded v (the compute dtype) while the owner keeps fp32
+    master rows and optimizer state: close to the local step, not bitwise."""
+    synth = make_synth("total:6000", seed=47)
+    F, K, layers, keep = synth.F, 8, [64, 32], [0.8, 0.8]
+    V = synth.feature_size
+    params = init_params(V, F, K, layers, False, seed=12)
+    kw = dict(sparse_update="lazy", batch_size=512, device="cuda", init=False,
+              field_ranges=synth.field_ranges(), emb_dtype=emb)
+    pool = [synth.batch(512, step=s, device="cuda", id_dtype=torch.int32) for s in range(4)]
+    out = []
+    for xr in ("bf16", "fp32", None):
+        comm = Comm(sharded=True, force_exchange=True) if xr else None
+        m = NativeDeepFM(V, F, K, layers, keep, comm=comm, exchange_rows=xr, **kw)
+        m.load_tf_params(params)
+        p0 = m.p.clone()
+        if xr:
+            assert m.shx.rbf16 == (xr == "bf16")
+            assert m.shx.RWS == (K // 2 + 2 if xr == "bf16" else K + 4) and m.shx.RWG == K + 1
+        for _ in range(2):
+            m.train_steps(pool, next_ids=(pool[0][0], pool[1][0]))
+        torch.cuda.synchronize()
+        m.check_errors()
+        out.append((m.tv.float().clone(), m.tw.clone(), m.p.clone()))
+        del m
+    (bv, bw, bp), (fv, fw, fp), (lv, lw, lp) = out
+    if emb == "bf16":
+        assert torch.equal(bv, fv) and torch.equal(bw, fw) and torch.equal(bp, fp)
+    else:
+        assert torch.equal(fv, lv) or torch.allclose(fv, lv, atol=1e-6)
+        # Adam normalizes each row's step, so a near-zero gradient whose sign the bf16 reads flip
+        # moves that element by ~2 lr: compare the whole update, not the worst element
+        v0 = torch.as_tensor(params["fm_v"]).to("cuda").float()
+        w0 = torch.as_tensor(params["fm_w"]).to("cuda").float().reshape(-1)
+        for b_, l_, x0 in ((bv, lv, v0), (bw, lw, w0)):
+            b_, l_ = b_[: x0.shape[0]].reshape(x0.shape), l_[: x0.shape[0]].reshape(x0.shape)
+            du = (b_ - x0) - (l_ - x0)
+            assert du.norm().item() <= 0.05 * (l_ - x0).norm().item()
+        assert ((bp - p0) - (lp - p0)).norm().item() <= 0.05 * (lp - p0).norm().item()
+        assert not torch.equal(bv, lv)           # the bf16 reads did change the arithmetic
+
+
+def test_replicated_run_sort_bitwise(group, monkeypatch):
+    """Replicated-table exchange (config #3) on the run-level sort: every batch of a multi-step
+    graph sorted at the graph's start, each step then routes its unique rows from its run set --
+    one queue, no per-step sort branch.  Bitwise the per-step prefetched-sort path."""
+    import hipfm.models.deepfm as D
+    synth = make_synth("total:6000", seed=53)
+    F, K, layers, keep = synth.F, 8, [64, 32], [0.8, 0.8]
+    V = synth.feature_size
+    params = init_params(V, F, K, layers, False, seed=13)
+    pool = [synth.batch(512, step=s, device="cuda", id_dtype=torch.int32) for s in range(4)]
+    out = []
+    for run in (True, False):
+        monkeypatch.setattr(D, "_RUN_SORT", run)
+        m = NativeDeepFM(V, F, K, layers, keep, sparse_update="lazy", batch_size=512, device="cuda",
+                         init=False, comm=Comm(sharded=False, force_exchange=True),
+                         field_ranges=synth.field_ranges())
+        m.load_tf_params(params)
+        assert m.rpx is not None
+        for _ in range(3):
+            m.train_steps(pool, next_ids=pool[0][0])
+        torch.cuda.synchronize()
+        m.check_errors()
+        assert any(k[0] == "runsort" for k in m._graphs) == run
+        out.append((m.tv.clone(), m.tw.clone(), m.p.clone(), m.step.clone()))
+        del m
+    for x, y in zip(*out):
+        assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("sharded,opt", [(True, "Adam"), (False, "Adam"), (True, "Adagrad")])
+def test_tf1_split_under_exchange_equals_scatter_sweep(group, monkeypatch, sharded, opt):
+    """tf1_dense (TF1 non-lazy optimizer semantics) under the native exchange: the split form --
+    requested rows updated by the lazy owner launch and flagged (serve / tag kernel), every other
+    row by the l2-only sweep workgroups of the same launch -- equals the gradient scatter + full
+    table sweep form bitwise, over run graphs and single steps; every row moved."""
+    import hipfm.models.deepfm as D
+    synth = make_synth("total:6000", seed=59)
+    F, K, layers, keep = synth.F, 8, [64, 32], [0.8, 0.8]
+    V = synth.feature_size
+    params = init_params(V, F, K, layers, False, seed=14)
+    pool = [synth.batch(512, step=s, device="cuda", id_dtype=torch.int32) for s in range(4)]
+    out = []
+    for split in (True, False):
+        monkeypatch.setattr(D, "_TF1_SPLIT", split)
+        m = NativeDeepFM(V, F, K, layers, keep, sparse_update="tf1_dense", optimizer=opt, l2_reg=1e-3,
+                         adam_epsilon=1e-2, batch_size=512, device="cuda", init=False,
+                         comm=Comm(sharded=sharded, force_exchange=True), field_ranges=synth.field_ranges())
+        m.load_tf_params(params)
+        assert m.tf1_xsplit == split
+        t0 = m.tv.clone()
+        for _ in range(2):
+            m.train_steps(pool, next_ids=(pool[0][0], pool[1][0]))
+        for i in range(3):
+            m.train_step(*pool[i], use_graph=True)
+        torch.cuda.synchronize()
+        m.check_errors()
+        if split:
+            assert int(m._xflags.sum().item()) == 0          # the sweep cleared every flag
+            moved = (m.tv != t0).any(dim=1)
+            assert bool(moved[:V].all())                      # non-lazy: every row moved
+        out.append((m.tv.clone(), m.tw.clone(), [s.clone() for s in m.sv], m.p.clone(), m.step.clone()))
+        del m
+    (av, aw, asv, ap, ast), (bv, bw, bsv, bp, bst) = out
+    assert torch.equal(av, bv) and torch.equal(aw, bw) and torch.equal(ap, bp) and torch.equal(ast, bst)
+    for x, y in zip(asv, bsv):
+        assert torch.equal(x, y)

@@ -21,6 +21,14 @@ from hipfm.models.reference import init_params  # noqa: E402
 DEV = torch.device("cuda", 0)
 
 
+@pytest.fixture(autouse=True)
+def _fp32_exchange_rows(monkeypatch):
+    """These tests compare N emulated ranks with ONE model on the global batch to 2e-5: fp32
+    exchanged rows (the one-GPU step's reads).  bf16 rows: tests/test_gpu_dist1.py."""
+    import hipfm.models.deepfm as D
+    monkeypatch.setattr(D, "_XROWS", "fp32")
+
+
 class _Hub:
     def __init__(self, N):
         self.N = N
@@ -276,13 +284,13 @@ def test_run_routing_matches_global_batch(N, update, steps):
     traces = [m.shx.trace for m in models]
     for t in traces[1:]:
         assert t == traces[0]
-    C, RW = models[0].shx.C, models[0].shx.RW
+    C, RWS, RWG = models[0].shx.C, models[0].shx.RWS, models[0].shx.RWG
     t = traces[0]
     assert t[0] == ((KN.COMM_A2A, steps * C * 4),)               # the run's ids, one all-to-all
     assert len(t) == 1 + 2 * steps
     for j in range(steps):
-        assert t[1 + 2 * j] == ((KN.COMM_A2A, C * RW * 4),)       # G1: rows only
-        assert t[2 + 2 * j][0] == (KN.COMM_A2A, C * RW * 4)       # G2: gradient rows first
+        assert t[1 + 2 * j] == ((KN.COMM_A2A, C * RWS * 4),)      # G1: rows only
+        assert t[2 + 2 * j][0] == (KN.COMM_A2A, C * RWG * 4)      # G2: gradient rows first
 
 
 @pytest.mark.parametrize("update,depth", [("lazy", 1), ("tf1_dense", 1), ("lazy", 2)])
@@ -313,11 +321,12 @@ def test_collective_sequence_identical_across_ranks(update, depth):
     for t in traces[1:]:
         assert t == traces[0]
     t = traces[0]
-    C, RW = models[0].shx.C, models[0].shx.RW
-    ids_op, rows_op = (KN.COMM_A2A, C * 4), (KN.COMM_A2A, C * RW * 4)
+    C, RWS, RWG = models[0].shx.C, models[0].shx.RWS, models[0].shx.RWG
+    ids_op, rows_op = (KN.COMM_A2A, C * 4), (KN.COMM_A2A, C * RWS * 4)
+    grads_op = (KN.COMM_A2A, C * RWG * 4)
     assert t[0] == (ids_op,) and t[1] == (rows_op,)            # step 0: inline ids, then rows
     g2 = t[2]
-    assert g2[0] == rows_op and g2[-1] == ids_op                # gradients first, next ids last
+    assert g2[0] == grads_op and g2[-1] == ids_op               # gradients first, next ids last
     assert len(t) == 7 and t[5] == (rows_op,)
     if depth == 1:
         assert t[3] == (rows_op,) and t[4][-1] == ids_op        # next ids with the gradients

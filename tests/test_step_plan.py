@@ -87,16 +87,18 @@ def _modes():
     for (fused, gather, fp8, K) in ((True, True, False, 8), (True, True, True, 32), (True, False, False, 8),
                                     (False, False, False, 16)):
         for ex in ("local", "row_sharded", "replicated", "legacy_sharded", "legacy_replicated"):
-            for upd in ("lazy", "tf1_split", "tf1_scatter"):
+            for upd in ("lazy", "tf1_split", "tf1_scatter", "tf1_xsplit"):
                 if upd == "tf1_split" and ex != "local":
+                    continue
+                if upd == "tf1_xsplit" and ex not in ("row_sharded", "replicated"):
                     continue
                 for fits, covers in ((True, True), (False, True), (True, False)):
                     yield ModeSpec(K=K, fused=fused, gather_fused=gather, fp8=fp8,
                                    sharded=ex in ("row_sharded", "legacy_sharded"), exchange=ex != "local",
                                    native_exchange=ex in ("row_sharded", "replicated"),
-                                   row_sharded=ex == "row_sharded", lazy_rows=upd != "tf1_scatter",
+                                   row_sharded=ex == "row_sharded", lazy_rows=upd in ("lazy", "tf1_split"),
                                    lazy=upd == "lazy", tf1_split=upd == "tf1_split", wgfin_fits=fits,
-                                   fin_covers_all=covers and fused)
+                                   fin_covers_all=covers and fused, tf1x=upd == "tf1_xsplit")
 
 
 def _knob_sets():
@@ -132,7 +134,9 @@ def test_plan_invariants_over_the_mode_matrix():
                         assert not p.fuse_opt or (m.fused and p.dense_early)
                         assert not p.tf1_merged or p.sfwg
                         assert not (p.tf1_merged and p.tf1_branch)
-                        assert not p.xfuse or (m.native_exchange and p.sh_apply_dense and m.lazy)
+                        assert not p.xfuse or (m.native_exchange and p.sh_apply_dense and (m.lazy or m.tf1x))
+                        if m.tf1x and m.fused and m.wgfin_fits and kn.wgfin and kn.sh_apply_dense:
+                            assert p.xfuse and p.sh_apply_dense      # the sweep's owner launch
                         assert not p.exchange_allreduce or (m.native_exchange and not p.xfuse)
                         assert not p.sh_apply_dense or m.native_exchange
                         assert not (p.run_sorted and (p.fork_sort or p.prefetch_next))

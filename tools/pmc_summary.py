@@ -13,7 +13,7 @@ import glob
 import os
 import sys
 
-OURS = ("tower_kernel", "wgfin_kernel", "sfwg_kernel", "dense_sweep", "fm_fwd", "wgrad_group", "finalize_kernel", "sf_tile", "sf_carry",
+OURS = ("tower_kernel", "tower_light", "wgfin_kernel", "sfwg_kernel", "sfwg_x", "fs2_",  "dense_sweep", "fm_fwd", "wgrad_group", "finalize_kernel", "sf_tile", "sf_carry",
         "fs_sort", "fs_transpose", "dense_opt", "w8_quant", "sh_", "seg_", "onesweep", "lsd_",
         "gemm_nt", "head_kernel", "rcclGenericKernel")
 SIMDS = 1024
