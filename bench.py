@@ -545,7 +545,7 @@ def data_bench(args):
     lab = torch.empty(B, pin_memory=True)
     ids = torch.empty(B, F, dtype=torch.int32, pin_memory=True)
     vals = torch.empty(B, F, pin_memory=True)
-    ld = NativeLoader(files, F, B, threads=args.threads)
+    ld = NativeLoader(files, F, B, threads=args.threads, ids32=True)
     rows, t0 = 0, time.perf_counter()
     while True:
         r = ld.next_into(lab, ids, vals)

@@ -437,7 +437,8 @@ static bool parse_libsvm(const std::string& line, int F, float* label, int64_t* 
 struct Chunk {
   int n = 0;
   std::vector<float> label;
-  std::vector<int64_t> ids;
+  std::vector<int64_t> ids;     // (empty when the loader narrows at decode time: ids32)
+  std::vector<int32_t> ids32;
   std::vector<float> vals;
 };
 
@@ -527,6 +528,8 @@ struct Loader {
   int format = 0, F = 0, B = 0, drop_remainder = 1, verify = 1;
   int shard_n = 1, shard_i = 0;   // record-level shard (1 = off)
   int64_t id_limit = 0;            // > 0: every id must lie in [0, id_limit) (feature_size V)
+  int narrow32 = 0;                // workers narrow ids to int32 while decoding (the device id type):
+                                   // batch assembly is then a plain copy (it was the ingest bound)
   int depth = 4;
   int chunk = 1024;
   std::vector<std::unique_ptr<WorkerQueue>> queues;
@@ -559,10 +562,12 @@ struct Loader {
     auto fresh = [&] {
       auto c = std::make_unique<Chunk>();
       c->label.resize(chunk);
-      c->ids.resize((size_t)chunk * F);
+      if (narrow32) c->ids32.resize((size_t)chunk * F);
+      else c->ids.resize((size_t)chunk * F);
       c->vals.resize((size_t)chunk * F);
       return c;
     };
+    std::vector<int64_t> idrow((size_t)F);   // one record's ids before narrowing
     std::unique_ptr<Chunk> c = fresh();
     std::string line;
     long long rec = 0;   // record index in this worker's stream (record sharding uses W == 1)
@@ -579,7 +584,7 @@ struct Loader {
       long long frec = -1;   // record index within this file (every record, sharded or not)
       while (!stop.load()) {
         float* lab = c->label.data() + c->n;
-        int64_t* ids = c->ids.data() + (size_t)c->n * F;
+        int64_t* ids = narrow32 ? idrow.data() : c->ids.data() + (size_t)c->n * F;
         float* vals = c->vals.data() + (size_t)c->n * F;
         bool okrec;
         if (format == 0) {
@@ -618,6 +623,17 @@ struct Loader {
                    paths[fi] + " record " + std::to_string(frec));
               return;
             }
+          }
+        }
+        if (narrow32) {
+          int32_t* d = c->ids32.data() + (size_t)c->n * F;
+          for (int f = 0; f < F; ++f) {
+            if (ids[f] < 0 || ids[f] > 0x7FFFFFFF) {
+              fail("feature id " + std::to_string((long long)ids[f]) + " outside [0, 2^31) for the int32 "
+                   "device path in " + paths[fi] + " record " + std::to_string(frec));
+              return;
+            }
+            d[f] = (int32_t)ids[f];
           }
         }
         if (++c->n == chunk) {
@@ -691,7 +707,9 @@ struct Loader {
       const Piece& p = pieces[pi];
       memcpy(lab + p.dst, p.c->label.data() + p.src, p.k * 4);
       const size_t m = (size_t)p.k * F;
-      if (ids32) {
+      if (ids32 && !p.c->ids32.empty()) {
+        memcpy(ids32 + (size_t)p.dst * F, p.c->ids32.data() + (size_t)p.src * F, m * 4);
+      } else if (ids32) {
         const int64_t* src = p.c->ids.data() + (size_t)p.src * F;
         int32_t* dst = ids32 + (size_t)p.dst * F;
         int64_t b = 0;
@@ -701,6 +719,10 @@ struct Loader {
           dst[i] = (int32_t)v;
         }
         if (b) bad.store(1);
+      } else if (p.c->ids.empty()) {  // narrowed at decode, read back as int64
+        const int32_t* src = p.c->ids32.data() + (size_t)p.src * F;
+        int64_t* dst = ids + (size_t)p.dst * F;
+        for (size_t i = 0; i < m; ++i) dst[i] = src[i];
       } else {
         memcpy(ids + (size_t)p.dst * F, p.c->ids.data() + (size_t)p.src * F, m * 8);
       }
@@ -732,9 +754,10 @@ struct Loader {
 
 HFMIO_API void* hfmio_loader_create(const char** paths, int npaths, int format, int F, int batch,
                                     int drop_remainder, int num_threads, int shard_n, int shard_i,
-                                    int verify_crc, int queue_depth, int64_t id_limit) {
+                                    int verify_crc, int queue_depth, int64_t id_limit, int narrow32) {
   auto* L = new Loader();
   L->id_limit = id_limit;
+  L->narrow32 = narrow32 ? 1 : 0;
   for (int i = 0; i < npaths; ++i) L->paths.emplace_back(paths[i]);
   L->format = format;
   L->F = F;

@@ -21,7 +21,7 @@ uint32_t hfmio_crc32c(const uint8_t* p, size_t n);
 int hfmio_decode_example(const uint8_t* p, size_t len, int F, float* label, int64_t* ids, float* vals);
 void* hfmio_loader_create(const char** paths, int npaths, int format, int F, int batch,
                           int drop_remainder, int num_threads, int shard_n, int shard_i,
-                          int verify_crc, int queue_depth);
+                          int verify_crc, int queue_depth, int64_t id_limit, int narrow32);
 int hfmio_loader_next(void* h, float* labels, int64_t* ids, float* vals);
 void hfmio_loader_destroy(void* h);
 int hfmio_write_examples(const char* path, const float* labels, const int64_t* ids,
@@ -47,10 +47,12 @@ struct Sum {
   long rows = 0;
 };
 
-static Sum read_all(const std::vector<std::string>& files, int threads, int shard_n, int shard_i) {
+static Sum read_all(const std::vector<std::string>& files, int threads, int shard_n, int shard_i,
+                    int narrow32 = 0) {
   std::vector<const char*> p;
   for (auto& f : files) p.push_back(f.c_str());
-  void* h = hfmio_loader_create(p.data(), (int)p.size(), 0, F, 64, 0, threads, shard_n, shard_i, 1, 8);
+  void* h = hfmio_loader_create(p.data(), (int)p.size(), 0, F, 64, 0, threads, shard_n, shard_i, 1, 8, 0,
+                                narrow32);
   CHECK(h != nullptr);
   std::vector<float> lab(64), vals(64 * F);
   std::vector<int64_t> ids(64 * F);
@@ -102,6 +104,9 @@ int main(int argc, char** argv) {
   const Sum a = read_all(files, 4, 1, 0), b = read_all(files, 4, 1, 0);
   CHECK(a.rows == want.rows && a.ids == want.ids && a.lab == want.lab && a.val == want.val);
   CHECK(a.order == b.order);
+  // ids narrowed to int32 while decoding (the device path) read back identically
+  const Sum n32 = read_all(files, 4, 1, 0, 1);
+  CHECK(n32.rows == a.rows && n32.ids == a.ids && n32.order == a.order && n32.val == a.val);
   // 2) record-level sharding partitions the data
   const Sum s0 = read_all(files, 3, 2, 0), s1 = read_all(files, 3, 2, 1);
   CHECK(s0.rows + s1.rows == want.rows && s0.ids + s1.ids == want.ids);

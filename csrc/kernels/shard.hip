@@ -637,11 +637,13 @@ struct ShDenseArgs {
 
 template <int K, int OPT>
 __global__ void __launch_bounds__(256) sh_apply_dense_kernel(ShApplyArgs A, ShDenseArgs D, int apply_blocks) {
+  // block order: the owner apply, the dense sweep, then the tf1 sweep (the dense workgroups first
+  // measured 30.2 vs 27.0 us)
   const int b = blockIdx.x;
   if (b < apply_blocks) {
-    sh_owner_apply_elem<K, 0, OPT>(b * 256 + threadIdx.x, A.recv_ids, A.total, A.N, A.C, A.rstride, A.recv_g,
-                                   A.table, A.tv, A.tw, A.s0v, A.s1v, A.s0w, A.s1w, A.ldv, A.ldw, A.Gv, A.Gw,
-                                   A.h, A.step, A.next, A.next_rows, sh_rdiv(A), A.vbf16, A.rbf16);
+    sh_owner_apply_elem<K, 0, OPT>(b * 256 + threadIdx.x, A.recv_ids, A.total, A.N, A.C, A.rstride,
+                                   A.recv_g, A.table, A.tv, A.tw, A.s0v, A.s1v, A.s0w, A.s1w, A.ldv, A.ldw, A.Gv,
+                                   A.Gw, A.h, A.step, A.next, A.next_rows, sh_rdiv(A), A.vbf16, A.rbf16);
   } else if (b >= apply_blocks + D.blocks) {   // tf1_dense split form: the l2-only sweep
     const float lr_t = OPT == OPT_ADAM ? adam_lr_t(A.h, *A.step + 1) : A.h.lr;
     tf1_sweep_rows<K, OPT, 2>(A.rec, A.rec_ld, A.R, A.rflag, A.h, lr_t,

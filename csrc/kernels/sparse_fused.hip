@@ -486,6 +486,7 @@ __global__ void __launch_bounds__(256) sf_tile_kernel(SfArgs A) {
 // index (sparse: step_off = 1; wgfin: *step + 1).
 #include "wgfin.h"
 #include "tf1_sweep.h"
+#include "shard_table.h"
 
 // the wgfin half's register footprint must not cut the sparse tiles' occupancy (6 waves / SIMD)
 constexpr int SFWG_PF = 2;
@@ -562,21 +563,34 @@ static int sfwg_dispatch(int opt, const SfArgs& A, const WgFinArgs& W, unsigned*
 
 // Row-sharded step: the sparse backward's gradient rows for the owner exchange (MODE 2) and the
 // wgfin gradient work (no optimizer: the dense gradient is exchanged first) in one launch.
+// Run-routed steps: `S.total` > 0 adds workgroups AFTER the sparse tiles that serve the NEXT step's
+// rows (shard_table.h sh_serve_elem, stamped step + 2; this step's owner update patches what it
+// changes).  The highest block indices are dispatched last: they fill the CUs the tiles' look-back
+// tail leaves idle, instead of competing with the tower's workgroups in its launch.
 template <int K>
-__global__ void __launch_bounds__(256) sfwg_x_kernel(SfArgs A, WgFinArgs W) {
+__global__ void __launch_bounds__(256) sfwg_x_kernel(SfArgs A, WgFinArgs W, ShServeArgs S, int tiles) {
   __shared__ SfwgSmem<K> sm;
   const int nw = W.tile_wgs + 1;
   if ((int)blockIdx.x < nw) wgfin_body<-1, SFWG_PF, SFWG_MAXNS, SFWG_TQ>(W, blockIdx.x, sm.wg);
-  else sf_tile_body<K, 2, 0>(A, (int)blockIdx.x - nw, sm.sf);
+  else if ((int)blockIdx.x < nw + tiles) sf_tile_body<K, 2, 0>(A, (int)blockIdx.x - nw, sm.sf);
+  else sh_serve_elem<K>(S, ((int)blockIdx.x - nw - tiles) * 256 + (int)threadIdx.x);
 }
 
-HFM_API int hfm_sparse_wgfin_x(int K, const SfArgs* A, const WgFinArgs* W, hipStream_t st) {
+HFM_API int hfm_sparse_wgfin_x(int K, const SfArgs* A, const WgFinArgs* W, const ShServeArgs* S,
+                               hipStream_t st) {
   if (A->n <= 0 || !A->flags || !A->sync || !A->gout || W->opt_on || W->ns < 1 || W->ns > SFWG_MAXNS ||
       W->kchunk % 32 || W->ldk != W->ns * 4 * W->kchunk || W->L + 2 > WGF_MAXC || !W->tile_ctr)
     return (int)hipErrorInvalidValue;
+  const ShServeArgs sv = S ? *S : ShServeArgs{};
+  if (S && (!sv.recv_ids || !sv.rows || !sv.step || !sv.T.key || sv.total <= 0 || sv.stamp_off != 2 ||
+            (sv.T.mask & (sv.T.mask + 1)) != 0 || sv.T.mask + 1 < 2u * (unsigned)sv.total))
+    return (int)hipErrorInvalidValue;
+  const long sth = S ? (long)sv.total * (K / 4) : 0;
+  const int swg = (int)((sth + 255) / 256);
 #define X_(KK)                                                                                    \
-  hipLaunchKernelGGL(sfwg_x_kernel<KK>, dim3(W->tile_wgs + 1 + (A->n + SfCfg<KK>::TP - 1) / SfCfg<KK>::TP), \
-                     dim3(256), 0, st, *A, *W)
+  hipLaunchKernelGGL(sfwg_x_kernel<KK>,                                                           \
+                     dim3(W->tile_wgs + 1 + (A->n + SfCfg<KK>::TP - 1) / SfCfg<KK>::TP + swg), dim3(256), \
+                     0, st, *A, *W, sv, (A->n + SfCfg<KK>::TP - 1) / SfCfg<KK>::TP)
   switch (K) {
     case 4: X_(4); break;
     case 8: X_(8); break;

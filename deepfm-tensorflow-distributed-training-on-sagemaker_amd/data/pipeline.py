@@ -110,6 +110,74 @@ def next_pipe_stream(channel: str) -> str:
     return pipe_channel_path(channel, k)
 
 
+class RingBatch(tuple):
+    """(ids, vals, labels) views of one slot of a ``_DeviceRing``: the consumer calls
+    ``ring.release`` once every kernel that reads the slot is enqueued."""
+
+    def __new__(cls, views, ring, slot):
+        t = super().__new__(cls, views)
+        t.ring, t.slot = ring, slot
+        return t
+
+
+def _flat_views(flat, B: int, F: int, id_dtype, off):
+    """(ids [B, F], vals [B, F], labels [B]) typed views of one flat [ids | vals | labels] buffer."""
+    return (flat[off[0]:off[1]].view(id_dtype).view(B, F), flat[off[1]:off[2]].view(torch.float32).view(B, F),
+            flat[off[2]:off[3]].view(torch.float32))
+
+
+class _DeviceRing:
+    """Persistent device staging ring of the streamed (uncached) input path: ``nslots`` flat
+    [ids | vals | labels] buffers, filled by ONE host-to-device copy each, straight from the
+    pinned buffer the loader assembled the batch into.  The same slot views serve every epoch, so
+    a run of consecutive slots is one captured multi-step graph, replayed (with the executor's
+    host fast path: ``run_list`` returns the same list object for the same slots).  A slot is
+    refilled only after the consumer released it (``release``: every kernel reading it is enqueued;
+    the refill's copy waits on that point of the compute stream)."""
+
+    def __init__(self, B: int, F: int, device, id_dtype, nslots: int):
+        import threading
+        esz = torch.empty(0, dtype=id_dtype).element_size()
+        self.B, self.F, self.id_dtype, self.nslots = B, F, id_dtype, nslots
+        self.off = (0, B * F * esz, B * F * (esz + 4), B * F * (esz + 4) + B * 4)
+        self.flat = [torch.empty(self.off[3], dtype=torch.uint8, device=device) for _ in range(nslots)]
+        self.views = [_flat_views(x, B, F, id_dtype, self.off) for x in self.flat]
+        self.ev = [None] * nslots
+        self.free = [True] * nslots
+        self.cv = threading.Condition()
+        self._runs = {}
+
+    def fits(self, B: int, F: int, id_dtype, nslots: int) -> bool:
+        return (self.B, self.F, self.id_dtype, self.nslots) == (B, F, id_dtype, nslots)
+
+    def acquire(self, slot: int, stop) -> Optional[torch.cuda.Event]:
+        """(fill thread) Wait until ``slot`` was released; returns the compute-stream event its
+        refill must wait for."""
+        with self.cv:
+            while not self.free[slot]:
+                if stop():
+                    return None
+                self.cv.wait(0.05)
+            self.free[slot] = False
+            return self.ev[slot]
+
+    def release(self, slots, stream):
+        ev = torch.cuda.Event()
+        ev.record(stream)
+        with self.cv:
+            for s in slots:
+                self.ev[s] = ev
+                self.free[s] = True
+            self.cv.notify_all()
+
+    def run_list(self, first: int, n: int):
+        key = (first, n)
+        r = self._runs.get(key)
+        if r is None:
+            r = self._runs[key] = [self.views[first + i] for i in range(n)]
+        return r
+
+
 class _DeviceFeeder:
     """Loader batches -> device batches: the C++ loader threads decode and a copy pool assembles
     each batch straight into a ring of pinned host buffers (ids narrowed to the device id type
@@ -117,15 +185,23 @@ class _DeviceFeeder:
     assembly -- and each buffer goes to the GPU with an async copy on a dedicated copy stream.
     The compute stream waits on the copy's event, never the host; a pinned buffer is refilled only
     after its previous copy finished (depth-deep ring: assembly of batches i+1.., copy of i and
-    compute of i-1 overlap)."""
+    compute of i-1 overlap).  With a ``_DeviceRing`` (streamed epochs trained by a consumer that
+    releases slots) the fill thread also issues the copy -- one per batch, into the next ring slot
+    -- and the consumer receives ``RingBatch`` views: no per-batch allocation, copy or Python work
+    on the training thread."""
 
-    def __init__(self, loader, F: int, B: int, device, id_dtype, depth: int = 4):
+    def __init__(self, loader, F: int, B: int, device, id_dtype, depth: int = 4, ring=None):
         self.loader, self.F, self.B, self.device, self.id_dtype = loader, F, B, device, id_dtype
         self.copy = torch.cuda.Stream(device)
+        self.dev_ring = ring
         pin = dict(pin_memory=True)
-        self.ring = [(torch.empty(B, dtype=torch.float32, **pin),
-                      torch.empty(B, F, dtype=id_dtype, **pin),
-                      torch.empty(B, F, dtype=torch.float32, **pin)) for _ in range(depth)]
+        if ring is not None:
+            self.pflat = [torch.empty(ring.off[3], dtype=torch.uint8, **pin) for _ in range(depth)]
+            self.ring = [_flat_views(x, B, F, id_dtype, ring.off)[::-1] for x in self.pflat]   # (lab, ids, vals)
+        else:
+            self.ring = [(torch.empty(B, dtype=torch.float32, **pin),
+                          torch.empty(B, F, dtype=id_dtype, **pin),
+                          torch.empty(B, F, dtype=torch.float32, **pin)) for _ in range(depth)]
         self.done = [None] * depth
         self.h2d_s = 0.0         # host time spent issuing copies (the copies themselves are async)
         import queue
@@ -137,6 +213,8 @@ class _DeviceFeeder:
 
     def _fill(self):
         try:
+            k = 0
+            R = self.dev_ring
             while True:
                 slot = self._free.get()
                 if slot is None or self._stop:
@@ -146,6 +224,22 @@ class _DeviceFeeder:
                     ev.synchronize()                 # this pinned buffer's last copy is over
                 lab, ids, vals = self.ring[slot]
                 r = self.loader.next_into(lab, ids, vals)   # (ctypes: the GIL is released)
+                if R is not None and r == self.B:
+                    s = k % R.nslots
+                    k += 1
+                    wait = R.acquire(s, lambda: self._stop)
+                    if self._stop:
+                        return
+                    with torch.cuda.stream(self.copy):
+                        if wait is not None:
+                            self.copy.wait_event(wait)
+                        R.flat[s].copy_(self.pflat[slot], non_blocking=True)
+                        ev = torch.cuda.Event()
+                        ev.record(self.copy)
+                    self.done[slot] = ev
+                    self._free.put(slot)
+                    self._full.put((("ring", s), r, ev))
+                    continue
                 self._full.put((slot, r, None))
                 if r == 0:
                     return
@@ -168,9 +262,13 @@ class _DeviceFeeder:
         self._th.start()
         try:
             while True:
-                slot, r, err = self._full.get()
-                if err is not None:
-                    raise err
+                slot, r, x = self._full.get()
+                if isinstance(x, BaseException):
+                    raise x
+                if isinstance(slot, tuple):          # a ring slot, copied by the fill thread
+                    compute.wait_event(x)
+                    yield RingBatch(self.dev_ring.views[slot[1]], self.dev_ring, slot[1])
+                    continue
                 if r == 0:
                     return
                 lab, ids, vals = self.ring[slot]
@@ -269,6 +367,10 @@ class InputPipeline:
         self.h2d_s = 0.0                          # host time issuing H2D copies (last epoch)
         self._fmin = self._fmax = None           # per-field id min / max over the first epoch
         self._stats_done = False
+        # > 1: the consumer trains streamed batches in runs of this many steps and releases ring
+        # slots (RingBatch.ring.release) -- set by Estimator.train around its loop
+        self.ring_steps = 0
+        self._ring = None
 
     @property
     def countable(self) -> bool:
@@ -311,7 +413,8 @@ class InputPipeline:
         self.from_cache = False
         plan = self.epoch_plan(epoch)
         loader = NativeLoader(plan.files, self.F, self.B, self.fmt, self.drop_remainder,
-                              self.threads, plan.record_shard, id_limit=self.id_limit)
+                              self.threads, plan.record_shard, id_limit=self.id_limit,
+                              ids32=self.id_dtype == torch.int32)
         store = [] if (self.cache and skip == 0 and not self.cache_overflow) else None
         stored = 0
         # per-field id min / max of the first complete epoch (cached or streamed)
@@ -319,7 +422,15 @@ class InputPipeline:
         if stats:
             self._fmin = self._fmax = None
         on_gpu = self.device is not None and torch.device(self.device).type == "cuda"
-        src = (_DeviceFeeder(loader, self.F, self.B, torch.device(self.device), self.id_dtype)
+        ring = None
+        if on_gpu and self.ring_steps > 1 and store is None:
+            # streamed epoch whose consumer releases ring slots (Estimator.train): batches land in
+            # the persistent device ring, two runs deep
+            n = 2 * int(self.ring_steps)
+            if self._ring is None or not self._ring.fits(self.B, self.F, self.id_dtype, n):
+                self._ring = _DeviceRing(self.B, self.F, torch.device(self.device), self.id_dtype, n)
+            ring = self._ring
+        src = (_DeviceFeeder(loader, self.F, self.B, torch.device(self.device), self.id_dtype, ring=ring)
                if on_gpu else None)
         k = 0
         try:

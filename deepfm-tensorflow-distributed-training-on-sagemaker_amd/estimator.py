@@ -60,6 +60,7 @@ class PositionedBatch(tuple):
     def __new__(cls, batch, pos):
         t = super().__new__(cls, tuple(batch))
         t.pos = (int(pos[0]), int(pos[1]))
+        t.ring, t.slot = getattr(batch, "ring", None), getattr(batch, "slot", None)   # (RingBatch)
         return t
 
 
@@ -325,15 +326,39 @@ class Estimator:
         src = batches
         if self.world > 1 and not getattr(batches, "countable", True):
             batches = self._agreed_batches(batches)
-        t_log = time.time()
-        n_log = 0
         start_step = self.global_step
         use_graph = cfg.graph and self.native
         gsteps = max(1, int(getattr(cfg, "graph_steps", 1)))
         check_every = max(1, int(getattr(cfg, "time_check_steps", 20)))
         wd = Watchdog(cfg.watchdog_secs, self.rank).start()
         window = StepWindow()
-        it = iter(batches)
+        # streamed epochs of an InputPipeline land in its device ring when this loop releases the
+        # slots (every run enqueued -> RingBatch.ring.release): no per-batch copy on this thread
+        rpipe = getattr(src, "pipe", None)
+        if rpipe is None and hasattr(src, "ring_steps"):
+            rpipe = src
+        if rpipe is not None and hasattr(rpipe, "ring_steps") and self.native and use_graph and gsteps > 1:
+            rpipe.ring_steps = gsteps
+        else:
+            rpipe = None
+        try:
+            self._train_loop(batches, src, it=iter(batches), max_steps=max_steps, eval_fn=eval_fn,
+                             eval_due=eval_due, wd=wd, window=window, use_graph=use_graph, gsteps=gsteps,
+                             check_every=check_every)
+        finally:
+            if rpipe is not None:
+                rpipe.ring_steps = 0
+        if self.native:
+            torch.cuda.synchronize(self.device)
+            self.model.check_errors()
+        wd.stop()
+        return self.global_step - start_step
+
+    def _train_loop(self, batches, src, it, max_steps, eval_fn, eval_due, wd, window, use_graph, gsteps,
+                    check_every):
+        cfg = self.cfg
+        t_log = time.time()
+        n_log = 0
         cur = self._next(it)
         while cur is not None:
             if max_steps is not None and self.global_step >= max_steps:
@@ -360,8 +385,9 @@ class Estimator:
                     with prof_range("h2d"):
                         run = [tuple(x.to(self.device, non_blocking=True) for x in b) for b in run]
                     self.timer.add("h2d", time.perf_counter() - t1)
+                released = [b for b in run if getattr(b, "ring", None) is not None]
                 if ring and len(run) > 1:
-                    run = self._to_ring(run)
+                    run = self._ring_run(run)
                 nxt_ids = nxt[0] if (nxt is not None and nxt[0].is_cuda) else None
                 with prof_range("step"):
                     if len(run) > 1:
@@ -373,6 +399,9 @@ class Estimator:
                         self.model.train_step(ids, vals, labels, use_graph=use_graph,
                                               next_ids=nxt_ids if from_cache else None,
                                               stage=not from_cache)
+                if released:               # every kernel reading these ring slots is enqueued
+                    released[0].ring.release([b.slot for b in released],
+                                             torch.cuda.current_stream(self.device))
                 # device error words (bad ids, capacity overflow, hand-off failures): copied
                 # asynchronously after every call, raised on at the next one
                 self.model.poll_errors()
@@ -422,11 +451,6 @@ class Estimator:
                 if eval_fn_ps is not None:
                     eval_fn_ps()
             cur = nxt
-        if self.native:
-            torch.cuda.synchronize(self.device)
-            self.model.check_errors()
-        wd.stop()
-        return self.global_step - start_step
 
     def agree_cache(self, pipeline) -> bool:
         """See ``agree_cache`` (module level): keep the cached epoch only if every rank has one."""
@@ -436,6 +460,18 @@ class Estimator:
         """A streamed batch can go through the staging ring: full batch of the model's size."""
         return (b is not None and int(b[0].shape[0]) == self.model.M and b[0].dim() == 2 and
                 int(b[0].shape[1]) == self.cfg.field_size)
+
+    def _ring_run(self, run):
+        """A run of streamed batches as the executor trains it: consecutive slots of the pipeline's
+        device ring -> that ring's persistent slot list (same list and buffers every time: one
+        captured graph, replayed through the host fast path); anything else is copied into the
+        estimator's own staging ring."""
+        r0 = getattr(run[0], "ring", None)
+        if r0 is not None:
+            first = run[0].slot
+            if all(getattr(b, "ring", None) is r0 and b.slot == first + i for i, b in enumerate(run)):
+                return r0.run_list(first, len(run))
+        return self._to_ring(run)
 
     def _to_ring(self, run):
         """Copy a run of streamed device batches into the staging ring (static buffers, so the

@@ -292,7 +292,7 @@ _SIGS = {
     "hfm_fs2_chunk_rows": [],
     "hfm_fs2_merge_wgs_per_run": [],
     "hfm_field_sort_run": [c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p],
-    "hfm_sparse_wgfin_x": [c_int, c_void_p, C.POINTER(WgFinArgs), c_void_p],
+    "hfm_sparse_wgfin_x": [c_int, c_void_p, C.POINTER(WgFinArgs), c_void_p, c_void_p],
     "hfm_wgfin_job_bytes": [],
     "hfm_wgfin_args_bytes": [],
     "hfm_tower_args_bytes": [],

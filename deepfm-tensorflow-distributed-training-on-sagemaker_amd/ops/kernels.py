@@ -335,10 +335,12 @@ def sparse_fused(K, mode, opt, args: SfArgs):
 SFWG_MAX_NS = 4          # sparse_fused.hip SFWG_MAXNS: wgfin splits the merged launch supports
 
 
-def sparse_wgfin_x(K, args: SfArgs, wf: "WgFinArgs"):
+def sparse_wgfin_x(K, args: SfArgs, wf: "WgFinArgs", serve=None):
     """Row-sharded step: gradient rows for the owner exchange + wgfin gradients (no optimizer)
-    in one launch (sparse_fused.hip sfwg_x_kernel)."""
-    check(L().hfm_sparse_wgfin_x(K, C.byref(args), C.byref(wf), stream_handle()), "sparse_wgfin_x")
+    in one launch (sparse_fused.hip sfwg_x_kernel); ``serve`` (ShServeArgs): the next run step's
+    rows served by extra workgroups of the same launch."""
+    check(L().hfm_sparse_wgfin_x(K, C.byref(args), C.byref(wf), C.byref(serve) if serve is not None else None,
+                                 stream_handle()), "sparse_wgfin_x")
 
 
 def sparse_wgfin(K, opt, args: SfArgs, wf: "WgFinArgs", done, sweep=None):

@@ -54,10 +54,13 @@ import torch
 
 from ..ops import kernels as KN
 from ..ops._lib import ShApplyArgs, ShTable
-from ..utils.knobs import flag
+from ..utils.knobs import flag, knob
 
 # routing in two launches (sh_route) instead of segments + bucket (7 launches); same outputs
 _ROUTE2 = flag("HIPFM_SH_ROUTE2")
+# run-routed steps: the next step's rows are served by extra workgroups of the sparse backward's
+# launch (sfwg) or of the tower's launch (tower)
+_SERVE_SITE = knob("HIPFM_SERVE_SITE")
 
 
 def estimate_capacity(id_batches: Iterable[torch.Tensor], world: int, slack: float = 1.25,
@@ -224,6 +227,7 @@ class FixedCapacityExchange:
         self._run_retired = []               # superseded packed ids buffers (captured graphs read them)
         self.gather_ld = 0                   # slot_row layout of the last fetch (tower idx_ld)
         self.tower_serve = None              # ShServeArgs the next tower launch serves (run mode)
+        self.x_serve = None                  # ... or the next sparse backward launch (sfwg_x)
 
     # ------------------------------------------------------------------ host-side plan
     def plan(self, ids: torch.Tensor, B: int, nxt: Optional[torch.Tensor], resident: bool = True,
@@ -364,6 +368,7 @@ class FixedCapacityExchange:
         step would find stale requesters stamped current (wrong gradient sums on the owner).
         (Not inside a capture: a run graph's own steps move the step number past those stamps.)"""
         capturing = self.m.device.type == "cuda" and torch.cuda.is_current_stream_capturing()
+        self.tower_serve = self.x_serve = None
         for rs in self.sets:
             if rs.stage == _SERVED and not capturing:
                 rs.req_key.zero_()
@@ -483,8 +488,13 @@ class FixedCapacityExchange:
             ops.append(self._ids_op(self._set(plan, 1)))
         self._issue(ops)                                                 # G1
         if train and plan.serve_ahead and plan.run:
-            # the next run step's rows, served by extra workgroups of this step's tower launch
-            self.tower_serve = self._serve_args(self.run_sets[plan.c + 1], ahead=True)
+            # the next run step's rows, served by extra workgroups of this step's sparse backward
+            # launch (or of its tower launch)
+            sv = self._serve_args(self.run_sets[plan.c + 1], ahead=True)
+            if _SERVE_SITE == "sfwg" and m._sp.xfuse:
+                self.x_serve = sv
+            else:
+                self.tower_serve = sv
         elif train and plan.serve_ahead:
             # the next batch's rows as of now (stamped step + 2); this step's owner update
             # patches the rows it changes (it waits for this branch first)
@@ -529,7 +539,8 @@ class FixedCapacityExchange:
         A.vbf16 = int(self.rbf16)            # (MODE 2 reads v from the received rows)
         A.sid, A.upos, A.gout = rs.sid_incl.data_ptr(), rs.upos.data_ptr(), self.send_g.data_ptr()
         if wgfin is not None:
-            KN.sparse_wgfin_x(m.K, A, wgfin)
+            sv, self.x_serve = self.x_serve, None
+            KN.sparse_wgfin_x(m.K, A, wgfin, serve=sv)
         else:
             KN.sparse_fused(m.K, KN.SF_EXCHANGE, m.opt_id, A)
         if join is not None:

@@ -51,6 +51,8 @@ KNOBS: Dict[str, Knob] = {
     "HIPFM_GROW": Knob("1", "variant", "run-sorted steps: the tower writes per-slot gradient rows, 1 at "
                        "their sorted positions (streamed), 2 in slot order (gathered through perm); 0: the "
                        "sparse launch gathers dX0 / S / vals / dlogit per slot"),
+    "HIPFM_SERVE_SITE": Knob("sfwg", "variant", "run-routed row-sharded step: the next step's rows served "
+                             "by workgroups of the sparse backward's launch (sfwg) or of the tower's (tower)"),
     "HIPFM_XROWS": Knob("bf16", "variant", "row-sharded exchange rows: bf16 (v as bf16 + fp32 w, 24 B at "
                         "K = 8; fused gather tower) | fp32 (48 B, bitwise the one-GPU reads)"),
     "HIPFM_TF1_SPLIT": Knob("1", "variant", "tf1_dense on one GPU: split form (0: gradient scatter + "
