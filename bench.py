@@ -422,6 +422,7 @@ def main():
             },
             "eval_auc": round(auc, 5),
             "train_loss": round(loss, 5),
+            "hbm_peak_gb": round(torch.cuda.max_memory_allocated() / 1e9, 1),
         }
         x = model.shx if model.shx is not None else model.rpx
         if x is not None:

@@ -248,7 +248,7 @@ __global__ void __launch_bounds__(FS_THREADS) fs_sort_kernel(const int* __restri
     if (k >= its) break;
     const int q = wb + k * 64 + lane;
     if (q < (int)m) {
-      sko[out_base + q] = kbase + (int)key[k];
+      sko[out_base + q] = min(kbase + (int)key[k], hi - 1);   // (out-of-field ids: flagged, kept valid)
       pko[out_base + q] = (row0 + (int)(val[k] & 0xFFFFu)) * F + f;
     }
   }

@@ -207,7 +207,7 @@ __device__ __forceinline__ void fs2_sort_item(const FsJob& J, int item, unsigned
   }
   __syncthreads();
   for (int q = tid; q < B; q += FS2_THREADS) {  // sentinels sit past B
-    sko[q] = lo + (int)lk[q];
+    sko[q] = min(lo + (int)lk[q], hi - 1);   // (an id outside its field -- flagged above -- stays a valid row)
     pko[q] = (row0 + (int)lv[q]) * F + f;
     if (direct && J.inv) J.inv[(size_t)f * J.B + row0 + (int)lv[q]] = f * J.B + row0 + q;
   }

@@ -636,7 +636,7 @@ struct ShDenseArgs {
 };
 
 template <int K, int OPT>
-__global__ void __launch_bounds__(256) sh_apply_dense_kernel(ShApplyArgs A, ShDenseArgs D, int apply_blocks) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) sh_apply_dense_kernel(ShApplyArgs A, ShDenseArgs D, int apply_blocks) {
   // block order: the owner apply, the dense sweep, then the tf1 sweep (the dense workgroups first
   // measured 30.2 vs 27.0 us)
   const int b = blockIdx.x;
@@ -646,7 +646,7 @@ __global__ void __launch_bounds__(256) sh_apply_dense_kernel(ShApplyArgs A, ShDe
                                    A.Gw, A.h, A.step, A.next, A.next_rows, sh_rdiv(A), A.vbf16, A.rbf16);
   } else if (b >= apply_blocks + D.blocks) {   // tf1_dense split form: the l2-only sweep
     const float lr_t = OPT == OPT_ADAM ? adam_lr_t(A.h, *A.step + 1) : A.h.lr;
-    tf1_sweep_rows<K, OPT, 2>(A.rec, A.rec_ld, A.R, A.rflag, A.h, lr_t,
+    tf1_sweep_rows<K, OPT, 1>(A.rec, A.rec_ld, A.R, A.rflag, A.h, lr_t,
                               (long)(b - apply_blocks - D.blocks) * 256 + threadIdx.x, (long)A.sweep_blocks * 256);
   } else {
     const float lr_t = OPT == OPT_ADAM ? adam_lr_t(D.h, *A.step + 1) : D.h.lr;

@@ -427,6 +427,10 @@ __device__ __forceinline__ void tower_bf16_body(const TowerArgs& a, bf16* lds, f
                             grow ? gS : nullptr);
     __syncthreads();
     TW_ST(1);
+#if defined(TW_BISECT) && TW_BISECT == 1   // tools/pkhazard: stop after the gather
+    if ((tid & 7) == 0) a.y_fm[row0 + (tid >> 3)] = s_yfm[tid >> 3];
+    return;
+#endif
   }
   // the head's operands, then (behind the E^T stores in the memory queue) the first GEMM tile's
   // weights
@@ -496,6 +500,10 @@ __device__ __forceinline__ void tower_bf16_body(const TowerArgs& a, bf16* lds, f
     TW_ST(3 + i);
     if (a.train && a.Ht[i]) store_tile_t(Hl, ldh, N, a.Ht[i], a.M, row0);
   }
+#if defined(TW_BISECT) && TW_BISECT == 2   // tools/pkhazard: stop after the forward layers
+  if (KE > 0 && (tid & 7) == 0) a.y_fm[row0 + (tid >> 3)] = s_yfm[tid >> 3];
+  return;
+#endif
   // ---------------------------------------------------------------- head
   {
     const bf16* H = lds + a.h_off[nl - 1];

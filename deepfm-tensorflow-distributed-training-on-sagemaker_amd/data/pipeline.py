@@ -146,6 +146,8 @@ class _DeviceRing:
         self.free = [True] * nslots
         self.cv = threading.Condition()
         self._runs = {}
+        self.G = max(1, nslots // 2)
+        self.next = 0             # the next slot a fill thread writes (continues across epochs)
 
     def fits(self, B: int, F: int, id_dtype, nslots: int) -> bool:
         return (self.B, self.F, self.id_dtype, self.nslots) == (B, F, id_dtype, nslots)
@@ -161,6 +163,16 @@ class _DeviceRing:
             self.free[slot] = False
             return self.ev[slot]
 
+    def start(self) -> int:
+        """First slot of a new epoch's feeder: the next run-aligned slot after the last one used.
+        Numbering continues across epochs (a consumer looking one batch ahead still holds the last
+        run of the previous epoch while the next epoch's first batch is filled: restarting at slot
+        0 would wait for that run's release forever), and stays aligned to runs of G, so the
+        captured run graphs are few."""
+        with self.cv:
+            self.next = (-(-self.next // self.G) * self.G) % self.nslots
+            return self.next
+
     def release(self, slots, stream):
         ev = torch.cuda.Event()
         ev.record(stream)
@@ -169,6 +181,11 @@ class _DeviceRing:
                 self.ev[s] = ev
                 self.free[s] = True
             self.cv.notify_all()
+
+    def release_all(self, stream):
+        """The consumer stopped (early exit): slots it still held are free once the work enqueued
+        so far is done."""
+        self.release([s for s in range(self.nslots) if not self.free[s]], stream)
 
     def run_list(self, first: int, n: int):
         key = (first, n)
@@ -197,11 +214,18 @@ class _DeviceFeeder:
         pin = dict(pin_memory=True)
         if ring is not None:
             self.pflat = [torch.empty(ring.off[3], dtype=torch.uint8, **pin) for _ in range(depth)]
-            self.ring = [_flat_views(x, B, F, id_dtype, ring.off)[::-1] for x in self.pflat]   # (lab, ids, vals)
+            self.ring = []
+            for x in self.pflat:
+                ids, vals, lab = _flat_views(x, B, F, id_dtype, ring.off)
+                self.ring.append((lab, ids, vals))             # (the loader's argument order)
         else:
             self.ring = [(torch.empty(B, dtype=torch.float32, **pin),
                           torch.empty(B, F, dtype=id_dtype, **pin),
                           torch.empty(B, F, dtype=torch.float32, **pin)) for _ in range(depth)]
+        for lab, ids, vals in self.ring:     # (labels, ids, vals) in the loader's argument order
+            assert lab.shape == (B,) and lab.dtype == torch.float32
+            assert ids.shape == (B, F) and ids.dtype == id_dtype
+            assert vals.shape == (B, F) and vals.dtype == torch.float32
         self.done = [None] * depth
         self.h2d_s = 0.0         # host time spent issuing copies (the copies themselves are async)
         import queue
@@ -213,8 +237,8 @@ class _DeviceFeeder:
 
     def _fill(self):
         try:
-            k = 0
             R = self.dev_ring
+            k = R.start() if R is not None else 0
             while True:
                 slot = self._free.get()
                 if slot is None or self._stop:
@@ -227,6 +251,7 @@ class _DeviceFeeder:
                 if R is not None and r == self.B:
                     s = k % R.nslots
                     k += 1
+                    R.next = k
                     wait = R.acquire(s, lambda: self._stop)
                     if self._stop:
                         return

@@ -348,6 +348,8 @@ class Estimator:
         finally:
             if rpipe is not None:
                 rpipe.ring_steps = 0
+                if getattr(rpipe, "_ring", None) is not None:     # (slots an early exit still held)
+                    rpipe._ring.release_all(torch.cuda.current_stream(self.device))
         if self.native:
             torch.cuda.synchronize(self.device)
             self.model.check_errors()

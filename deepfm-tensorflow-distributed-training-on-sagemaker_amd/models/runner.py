@@ -40,7 +40,9 @@ def graph_capture(g):
     was = gc.isenabled()
     gc.disable()
     try:
-        with torch.cuda.graph(g):
+        # thread-local capture: the input pipeline's fill thread keeps issuing its host-to-device
+        # copies and event calls on its own stream while a run is captured here
+        with torch.cuda.graph(g, capture_error_mode="thread_local"):
             yield
     finally:
         if was:

@@ -47,7 +47,8 @@ if VARIANT:
     _vtag, _, _vdefs = VARIANT.partition(":")
     KERNELS_SO = os.path.join(LIB_DIR, f"libhipfm_kernels_{_vtag}.so")
     BUILD_DIR = BUILD_DIR + "_" + _vtag
-    VDEFS = ["-D" + d for d in _vdefs.split(",") if d]
+    VDEFS = ["-D" + d for d in _vdefs.split(",") if d and d != "PACKED"]
+    PACKED = PACKED or "PACKED" in _vdefs.split(",")      # (a variant with packed-FP32 ops on)
 IO_SO = os.path.join(LIB_DIR, "libhipfm_io.so")
 
 

@@ -11,7 +11,7 @@ timeout -k 10 600 python tools/gen_synthetic_criteo.py --out "$D" --preset crite
   --train_rows "$ROWS" --val_rows 16384 --files 16 > gpurun_out/${TAG}_datagen.log 2>&1 || { echo datagen failed; exit 1; }
 timeout -k 10 300 python bench.py --data "$D" --preset criteo_kaggle --epochs 3 --stream_only > gpurun_out/${TAG}_plain.log 2>&1; rc=$?
 echo "plain rc=$rc: $(tail -1 gpurun_out/${TAG}_plain.log)"
-case $rc in 124|134|137|139) rm -rf "$D"; exit $rc;; esac
+[ $rc -ne 0 ] && { rm -rf "$D"; exit $rc; }
 mkdir -p gpurun_out/prof_$TAG
 timeout -k 10 400 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d "$ROOT/gpurun_out/prof_$TAG" -o run -- \
   python3 "$ROOT/bench.py" --data "$D" --preset criteo_kaggle --epochs 3 --stream_only > gpurun_out/${TAG}_prof.log 2>&1; rc=$?
