@@ -164,14 +164,21 @@ class _DeviceRing:
             return self.ev[slot]
 
     def start(self) -> int:
-        """First slot of a new epoch's feeder: the next run-aligned slot after the last one used.
-        Numbering continues across epochs (a consumer looking one batch ahead still holds the last
-        run of the previous epoch while the next epoch's first batch is filled: restarting at slot
-        0 would wait for that run's release forever), and stays aligned to runs of G, so the
-        captured run graphs are few."""
+        """First slot of a new epoch's feeder.  Numbering continues across epochs: a consumer
+        looking one batch ahead still holds the last run of the previous epoch (and a run may span
+        the epoch boundary) while the next epoch's first batches are filled, so restarting at slot
+        0 could wait for a slot that is only released after those batches arrive.  Filling the
+        slots in cyclic order is safe (the consumer holds at most G + 1 of the 2G slots, the most
+        recently filled ones); the start may jump ahead to the next run-aligned block (fewer
+        distinct run graphs) only when that whole block is free, so the next G batches never wait.
+        (tests/test_ring_cpu.py)"""
         with self.cv:
-            self.next = (-(-self.next // self.G) * self.G) % self.nslots
-            return self.next
+            cur = self.next % self.nslots
+            t = (-(-self.next // self.G) * self.G) % self.nslots
+            if t != cur and all(self.free[(t + i) % self.nslots] for i in range(self.G)):
+                cur = t
+            self.next = cur
+            return cur
 
     def release(self, slots, stream):
         ev = torch.cuda.Event()

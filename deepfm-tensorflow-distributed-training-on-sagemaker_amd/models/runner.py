@@ -182,6 +182,30 @@ class GraphRunnerMixin:
             self._sort_plan = None
         if self._host_step is not None:
             self._host_step += 1
+        self._check_plan_state()
+
+    def _check_plan_state(self):
+        """Invariants of the host-side plan state after every committed step (cheap host checks;
+        a violation is a stale-state bug that would otherwise surface as wrong numerics):
+        the slot-sort set just consumed holds no prefetched key; tf1_dense row flags are stamped
+        in at most one set, and only for a batch that can still be stepped or swept; at most one
+        routing set holds rows served ahead, and every staged routing set names its batch."""
+        bad = []
+        if self._ss_cur not in (0, 1) or self._ss_key[1 - self._ss_cur] is not None:
+            bad.append(f"sort sets: cur {self._ss_cur}, keys {self._ss_key}")
+        if getattr(self, "tf1_split", False):
+            n = list(self._stamp_n)
+            if sum(1 for x in n if x) > 1 or any(x < 0 or x > self.M * self.F for x in n):
+                bad.append(f"tf1 flag stamps {n}")
+        if self.shx is not None:
+            from ..parallel.sharded import _SERVED
+            st = [(rs.key, rs.stage) for rs in self.shx.sets]
+            if sum(1 for _, g in st if g == _SERVED) > 1 or any((k is None) != (g is None) for k, g in st):
+                bad.append(f"routing sets {st}")
+            if not 0 <= self.shx.cur < self.shx.NSETS:
+                bad.append(f"routing set index {self.shx.cur}")
+        if bad:
+            raise RuntimeError("executor plan-state invariant violated: " + "; ".join(bad))
 
     @property
     def plan_period(self) -> int:

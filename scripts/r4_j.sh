@@ -4,14 +4,15 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 TAG=${1:-r4j}
 fatal() { case $1 in 124|134|137|139) echo "fatal rc=$1 at $2"; exit $1;; esac; }
+timeout -k 10 900 python -u -m pytest -x -q --timeout 600 --timeout-method thread tests/test_gpu_plan_state.py tests/test_gpu_determinism.py > gpurun_out/${TAG}_pytest.log 2>&1; rc=$?
+fatal $rc pytest
+echo "pytest rc=$rc: $(tail -1 gpurun_out/${TAG}_pytest.log)"
+[ $rc -ne 0 ] && grep -E "Error|FAILED|invariant" gpurun_out/${TAG}_pytest.log | head -10
 for e in fp32 bf16; do
   timeout -k 10 300 python bench.py --steps 20 --warmup 5 --emb_dtype $e > gpurun_out/${TAG}_emb_$e.log 2>&1; rc=$?
   fatal $rc emb_$e
   echo "emb $e: $(tail -1 gpurun_out/${TAG}_emb_$e.log | grep -o '"ms_per_step": [0-9.]*'), auc $(tail -1 gpurun_out/${TAG}_emb_$e.log | grep -o '"eval_auc": [0-9.]*')"
 done
-bash scripts/r4_pmc.sh ${TAG}_pmc_fp32 --steps 20 --warmup 5 > gpurun_out/${TAG}_pmc_fp32.log 2>&1; rc=$?; fatal $rc pmc_fp32
-bash scripts/r4_pmc.sh ${TAG}_pmc_bf16 --steps 20 --warmup 5 --emb_dtype bf16 > gpurun_out/${TAG}_pmc_bf16.log 2>&1; rc=$?; fatal $rc pmc_bf16
-echo "pmc done"
 timeout -k 10 900 python bench.py --steps 20 --warmup 5 --embedding_size 32 --emb_dtype bf16 > gpurun_out/${TAG}_k32_bf16.log 2>&1; rc=$?
 fatal $rc k32
 echo "k32 bf16 1TB: rc=$rc $(tail -1 gpurun_out/${TAG}_k32_bf16.log | cut -c1-600)"

@@ -25,8 +25,8 @@ from hipfm.models.reference import init_params  # noqa: E402
 
 B = 512
 P = 5            # resident pool
-SEQS = 6         # random sequences per mode
-OPS = 12         # operations per sequence
+SEQS = 67        # random sequences per mode (~200 over the three modes)
+OPS = 8          # operations per sequence
 
 
 @pytest.fixture(scope="module")

@@ -1,0 +1,111 @@
+"""The streamed input path's device ring protocol (data/pipeline.py ``_DeviceRing``) on the CPU:
+a fill thread per epoch writes batches into ring slots, a consumer that looks one batch ahead (the
+Estimator / CLI all-epochs generator) trains runs of up to G consecutive batches and releases their
+slots.  Across epoch boundaries, short epochs and early exits: no deadlock, and no slot is ever
+refilled while the consumer still holds it."""
+import queue
+import threading
+
+import pytest
+import torch
+
+import hipfm  # noqa: F401
+from hipfm.data import pipeline as P
+
+
+class _Ev:                                   # stands in for torch.cuda.Event on the CPU
+    def record(self, stream=None):
+        pass
+
+
+@pytest.fixture(autouse=True)
+def _cpu_events(monkeypatch):
+    monkeypatch.setattr(torch.cuda, "Event", _Ev)
+
+
+def _producer(ring, n, content, q, stop):
+    """One epoch's fill thread: the slot order of ``_DeviceFeeder._fill``."""
+    k = ring.start()
+    for i in range(n):
+        s = k % ring.nslots
+        k += 1
+        ring.next = k
+        ring.acquire(s, lambda: stop.is_set())
+        if stop.is_set():
+            return
+        content[s] = (id(q), i)                   # "the copy": the slot now holds batch i
+        q.put((s, (id(q), i)))
+    q.put(None)
+
+
+def _all_batches(ring, lengths, content, stop, threads=None):
+    """The CLI's all-epochs generator: epoch e + 1's producer starts once epoch e is exhausted."""
+    for n in lengths:
+        q = queue.Queue()
+        th = threading.Thread(target=_producer, args=(ring, n, content, q, stop), daemon=True)
+        if threads is not None:
+            threads.append(th)
+        th.start()
+        while True:
+            item = q.get(timeout=5)               # (a deadlock surfaces as queue.Empty)
+            if item is None:
+                break
+            yield item
+        th.join(timeout=5)
+
+
+@pytest.mark.parametrize("G,lengths", [(4, [13, 7, 16, 3]), (8, [39, 39, 39]), (3, [1, 2, 10, 5, 6])])
+def test_ring_runs_across_epochs_never_overwrite_held_slots(G, lengths):
+    ring = P._DeviceRing(2, 3, "cpu", torch.int32, 2 * G)
+    content, stop = {}, threading.Event()
+    it = _all_batches(ring, lengths, content, stop)
+    cur = next(it, None)
+    trained = 0
+    try:
+        while cur is not None:
+            run = [cur]
+            nxt = next(it, None)
+            while len(run) < G and nxt is not None:
+                run.append(nxt)
+                nxt = next(it, None)
+            # "enqueue the run": every slot still holds the batch it was handed out with
+            for s, tag in run:
+                assert content[s] == tag, (s, content[s], tag)
+            if nxt is not None:
+                assert content[nxt[0]] == nxt[1]
+            trained += len(run)
+            ring.release([s for s, _ in run], None)
+            cur = nxt
+    finally:
+        stop.set()
+    assert trained == sum(lengths)
+    assert all(ring.free)
+
+
+def test_ring_early_exit_releases_held_slots():
+    G = 4
+    ring = P._DeviceRing(2, 3, "cpu", torch.int32, 2 * G)
+    content, stop, ths = {}, threading.Event(), []
+    it = _all_batches(ring, [20], content, stop, ths)
+    held = [next(it) for _ in range(G + 1)]          # a run plus the look-ahead batch, never trained
+    stop.set()
+    for th in ths:                                   # (the feeder joins its fill thread on close)
+        th.join(timeout=5)
+    assert sum(1 for f in ring.free if not f) >= len(held)
+    ring.release_all(None)
+    assert all(ring.free)
+    # a later epoch of the same pipeline starts on the next run boundary and is not blocked
+    stop2 = threading.Event()
+    it2 = _all_batches(ring, [5], content, stop2)
+    got = [next(it2) for _ in range(5)]
+    assert got[0][0] % G == 0
+    stop2.set()
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_ring_random_epochs(seed):
+    import random
+    rng = random.Random(seed)
+    G = rng.choice([2, 3, 4, 5, 8])
+    lengths = [rng.randint(1, 3 * G + 2) for _ in range(rng.randint(2, 6))]
+    test_ring_runs_across_epochs_never_overwrite_held_slots(G, lengths)
