@@ -37,6 +37,8 @@ import torch
 from .native_io import FMT_LIBSVM, FMT_TFRECORD, NativeLoader, count_records
 from ..utils.knobs import knob
 
+_H2D_STREAMS = int(knob("HIPFM_H2D_STREAMS"))
+
 PIPE_ROOT = "/opt/ml/input/data"
 _pipe_lock = threading.Lock()
 _pipe_opened = {}        # channel -> number of epoch streams opened so far (this process)
@@ -217,6 +219,9 @@ class _DeviceFeeder:
     def __init__(self, loader, F: int, B: int, device, id_dtype, depth: int = 4, ring=None):
         self.loader, self.F, self.B, self.device, self.id_dtype = loader, F, B, device, id_dtype
         self.copy = torch.cuda.Stream(device)
+        # ring mode: consecutive batches alternate over copy streams (each its own DMA queue; one
+        # stream measured ~35 GB/s host-to-device, one 5.2 MB batch per ~150 us)
+        self.copies = [self.copy] + [torch.cuda.Stream(device) for _ in range(max(0, _H2D_STREAMS - 1))]
         self.dev_ring = ring
         pin = dict(pin_memory=True)
         if ring is not None:
@@ -262,12 +267,13 @@ class _DeviceFeeder:
                     wait = R.acquire(s, lambda: self._stop)
                     if self._stop:
                         return
-                    with torch.cuda.stream(self.copy):
+                    cs = self.copies[k % len(self.copies)]
+                    with torch.cuda.stream(cs):
                         if wait is not None:
-                            self.copy.wait_event(wait)
+                            cs.wait_event(wait)
                         R.flat[s].copy_(self.pflat[slot], non_blocking=True)
                         ev = torch.cuda.Event()
-                        ev.record(self.copy)
+                        ev.record(cs)
                     self.done[slot] = ev
                     self._free.put(slot)
                     self._full.put((("ring", s), r, ev))
@@ -462,7 +468,8 @@ class InputPipeline:
             if self._ring is None or not self._ring.fits(self.B, self.F, self.id_dtype, n):
                 self._ring = _DeviceRing(self.B, self.F, torch.device(self.device), self.id_dtype, n)
             ring = self._ring
-        src = (_DeviceFeeder(loader, self.F, self.B, torch.device(self.device), self.id_dtype, ring=ring)
+        src = (_DeviceFeeder(loader, self.F, self.B, torch.device(self.device), self.id_dtype, ring=ring,
+                             depth=8 if ring is not None else 4)
                if on_gpu else None)
         k = 0
         try:

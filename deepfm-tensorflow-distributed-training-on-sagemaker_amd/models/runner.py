@@ -400,6 +400,7 @@ class GraphRunnerMixin:
         G = len(batches)
         fms = [not b[0].is_contiguous() for b in batches]
         routed = self.shx is not None
+        rdesc = nB = None
         if routed:
             rlist = [(self._flat_ids(b[0], fm), b[0].shape[0], fm) for b, fm in zip(batches, fms)]
             self.shx.route_run_prepare(rlist)           # allocations / device plans: not in a capture
@@ -410,20 +411,29 @@ class GraphRunnerMixin:
                 [(self._flat_ids(b[0], fm), b[0].shape[0], fm, k, p,
                   iv if (self.grow is not None and self.grow_sorted) else None)
                  for b, fm, (k, p, iv) in zip(batches, fms, sets)])
+            nB = batches[0][0].shape[0] * self.F
+            # replicated-table exchange: every batch's unique rows routed at the run start too
+            rdesc = self.rpx.route_run_prepare(G, nB, sets) if self.rpx is not None else None
         def enqueue():
             if routed:
                 self.shx.route_run(rlist)
             else:
                 self._fsort_next.run_sort(rplan)
+                if rdesc is not None:
+                    self.rpx.route_run(rdesc, G, nB)
             self._run_n = G
             for j, (ids, vals, labels) in enumerate(batches):
                 self._run_j = j
+                if self.rpx is not None and rdesc is not None:
+                    self.rpx._run_j = j
                 try:
                     B, direct, _ = self._bind_step(ids, vals, labels)
                     self.train_step_enqueue(B)
                     self._commit_step(B, direct)
                 finally:
                     self._run_j = None
+                    if self.rpx is not None:
+                        self.rpx._run_j = None
 
         if self.comm is not None and not self.comm.graph_safe:
             # collectives that cannot be captured (the in-process emulation engine of the tests):

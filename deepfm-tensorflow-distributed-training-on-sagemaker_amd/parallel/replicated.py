@@ -76,11 +76,46 @@ class ReplicatedExchange:
         self.dense_recv = None
         self.trace = None
         self._main = None
+        self.run_sets = []               # run-level routing: (sid_incl, upos, send_ids, ...) per step
+        self._run_descs = {}
+        self._run_j = None               # the step of the run being enqueued (runner)
 
     def _issue(self, ops):
         if self.trace is not None:
             self.trace.append(tuple((k, int(nb)) for k, _, _, nb in ops))
         self.eng.group(ops)
+
+    # ------------------------------------------------------------------ run-level routing
+    def route_run_prepare(self, G: int, n: int, sets):
+        """Allocations and device descriptors for routing every batch of a G-step run sorted at
+        its start (``sets``: the runner's (sorted keys, perm, inverse) per step).  Not in a capture."""
+        m = self.m
+        i32 = dict(dtype=torch.int32, device=m.device)
+        while len(self.run_sets) < G:
+            self.run_sets.append(dict(sid=torch.zeros(m.M * m.F, **i32), upos=torch.zeros(m.M * m.F, **i32),
+                                      send_ids=torch.full((self.C,), -1, **i32), send_cnt=torch.zeros(1, **i32),
+                                      num_u=torch.zeros(1, **i32),
+                                      tcnt=torch.zeros(KN.sh_route_tiles(m.M * m.F) * 2, **i32)))
+        if getattr(self, "_slot_sink", None) is None or self._slot_sink.numel() < m.M * m.F:
+            self._slot_sink = torch.zeros(m.M * m.F, **i32)   # (slot maps: unused by this exchange)
+        key = (G, n) + tuple(s[0].data_ptr() for s in sets[:G])
+        d = self._run_descs.get(key)
+        if d is None:
+            from ..ops._lib import ShRouteBatch
+            descs = []
+            for (sk, perm, _), rs in zip(sets[:G], self.run_sets[:G]):
+                r = ShRouteBatch()
+                r.sk, r.perm, r.tcnt, r.sid_incl = sk.data_ptr(), perm.data_ptr(), rs["tcnt"].data_ptr(), rs["sid"].data_ptr()
+                r.send_ids, r.upos = rs["send_ids"].data_ptr(), rs["upos"].data_ptr()
+                r.send_cnt, r.num_u, r.slot_row = rs["send_cnt"].data_ptr(), rs["num_u"].data_ptr(), self._slot_sink.data_ptr()
+                descs.append(r)
+            d = KN.struct_array_to_device(descs, m.device)
+            self._run_descs[key] = d
+        return d
+
+    def route_run(self, d, G: int, n: int):
+        """Unique rows + gradient-row positions of every batch of the run (three launches)."""
+        KN.sh_route_run(d, G, n, 1, self.C, self.err, self.C, self.m.F, 0)
 
     def backward(self, B: int, dense=None, join=None, wgfin=None, dense_ar=None):
         """Sorted slots (m.sorted_keys / m.perm) -> unique gradient rows -> all-gather -> rank-
@@ -88,10 +123,15 @@ class ReplicatedExchange:
         in ``FixedCapacityExchange.backward``."""
         m = self.m
         n = B * m.F
-        KN.sh_route(m.sorted_keys, n, 1, self.C, self.tcnt, m.sid_incl, self.send_ids, self.upos,
-                    self.send_cnt, self.num_u, self.err)
+        if self._run_j is not None:      # routed at the run's start (route_run)
+            rs = self.run_sets[self._run_j]
+            sid, upos, send_ids = rs["sid"], rs["upos"], rs["send_ids"]
+        else:
+            sid, upos, send_ids = m.sid_incl, self.upos, self.send_ids
+            KN.sh_route(m.sorted_keys, n, 1, self.C, self.tcnt, sid, send_ids, upos,
+                        self.send_cnt, self.num_u, self.err)
         A = m.sf_args(n)
-        A.sid, A.upos, A.gout = m.sid_incl.data_ptr(), self.upos.data_ptr(), self.send_g.data_ptr()
+        A.sid, A.upos, A.gout = sid.data_ptr(), upos.data_ptr(), self.send_g.data_ptr()
         A.v_by_key = 1                      # V rows from the local replica, by id
         if wgfin is not None:
             KN.sparse_wgfin_x(m.K, A, wgfin)
@@ -99,7 +139,7 @@ class ReplicatedExchange:
             KN.sparse_fused(m.K, KN.SF_EXCHANGE, m.opt_id, A)
         if join is not None:
             join()
-        ops = [(KN.COMM_ALLGATHER, self.send_ids, self.g_ids, self.C * 4),
+        ops = [(KN.COMM_ALLGATHER, send_ids, self.g_ids, self.C * 4),
                (KN.COMM_ALLGATHER, self.send_g, self.g_rows, self.C * self.RW * 4)]
         if wgfin is not None:
             if self.dense_recv is None:

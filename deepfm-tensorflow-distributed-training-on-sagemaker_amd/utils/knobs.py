@@ -72,6 +72,7 @@ KNOBS: Dict[str, Knob] = {
     "HIPFM_FSORT_PB": Knob(None, "tuning", "field sort MSD partitions per field, log2 (default: 0 on "
                            "one GPU, 2 for the sharded routing)"),
     "HIPFM_FS_MAX_PB": Knob("4", "tuning", "tools/bench_sort.py: field sort partitions per field"),
+    "HIPFM_H2D_STREAMS": Knob("2", "tuning", "streamed input: copy streams the device-ring batches alternate over"),
     "HIPFM_GRAPH_STEPS": Knob("32", "tuning", "most training steps per captured HIP graph (bench.py)"),
     # ---- harness
     "HIPFM_ARCH": Knob("gfx950", "harness", "offload arch of the HIP build"),

@@ -340,9 +340,10 @@ def test_collective_sequence_identical_across_ranks(update, depth):
         m.check_errors()
 
 
-@pytest.mark.parametrize("N,opt,update,fused", [(4, "Adam", "lazy", True), (3, "Adagrad", "lazy", True),
-                                                (4, "Adam", "tf1_dense", True), (2, "Adam", "lazy", False)])
-def test_replicated_exchange_matches_global_batch(N, opt, update, fused):
+@pytest.mark.parametrize("N,opt,update,fused,run", [(4, "Adam", "lazy", True, False), (3, "Adagrad", "lazy", True, False),
+                                                    (4, "Adam", "tf1_dense", True, False), (2, "Adam", "lazy", False, False),
+                                                    (4, "Adam", "lazy", True, True), (3, "Adam", "tf1_dense", True, True)])
+def test_replicated_exchange_matches_global_batch(N, opt, update, fused, run):
     """Config #3 (Horovod parity) as a captured step: N replicated tables, each rank's unique
     (id, gradient row) pairs all-gathered in fixed-capacity blocks and summed in rank order by
     every rank.  The replicas stay bitwise identical, the collective sequence is identical on
@@ -377,7 +378,11 @@ def test_replicated_exchange_matches_global_batch(N, opt, update, fused):
         assert m.rpx is not None and m.shx is None and m.R == V
         m.rpx.trace = []
         models.append(m)
-    _run_ranks(models, batches, prefetch=True)
+    if run:      # one run per rank: run-level sort + routing of every batch at the run start (lazy)
+        _run_ranks_steps(models, batches)
+        assert update != "lazy" or len(models[0].rpx.run_sets) == steps
+    else:
+        _run_ranks(models, batches, prefetch=True)
     torch.cuda.synchronize()
     for m in models:
         m.check_errors()
