@@ -509,14 +509,20 @@ __global__ void __launch_bounds__(256) sfwg_kernel(SfArgs A, WgFinArgs W, unsign
   __shared__ SfwgSmem<K> sm;
   const int nw = W.tile_wgs + 1;
   const int ntile = (A.n + SfCfg<K>::TP - 1) / SfCfg<K>::TP;
-  if ((int)blockIdx.x < nw) {
+#ifdef SFWG_WGFIN_LAST   // (experiment) sparse tiles first, the wgfin workgroups after them
+  const int bid = (int)blockIdx.x < ntile ? (int)blockIdx.x + nw
+                : (int)blockIdx.x < ntile + nw ? (int)blockIdx.x - ntile : (int)blockIdx.x;
+#else
+  const int bid = (int)blockIdx.x;
+#endif
+  if (bid < nw) {
     SF_ST(8);
-    wgfin_body<OPT, SFWG_PF, SFWG_MAXNS, SFWG_TQ>(W, blockIdx.x, sm.wg);
+    wgfin_body<OPT, SFWG_PF, SFWG_MAXNS, SFWG_TQ>(W, bid, sm.wg);
     SF_ST(9);
-  } else if (!SWEEP || (int)blockIdx.x < nw + ntile) {
-    sf_tile_body<K, 0, OPT>(A, (int)blockIdx.x - nw, sm.sf);
+  } else if (!SWEEP || bid < nw + ntile) {
+    sf_tile_body<K, 0, OPT>(A, bid - nw, sm.sf);
   } else if (SWEEP) {
-    const int sb = (int)blockIdx.x - nw - ntile;
+    const int sb = bid - nw - ntile;
     // (2 rows per thread per pass: 98 VGPRs, 0.1596-0.1598 vs 0.1565-0.1619 ms -- no gain)
     tf1_sweep_rows<K, OPT, 1>(S.rec, S.ld, S.R, S.flags, A.h, sf_lr_t<OPT>(A),
                               (long)sb * blockDim.x + threadIdx.x, (long)S.nblk * blockDim.x);

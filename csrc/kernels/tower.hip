@@ -201,14 +201,15 @@ struct TwNoHook {
 
 // ``hook()`` runs once, right after the first pass's table-row loads are issued (their HBM round
 // trip is the gather's longest wait: the tower issues its first GEMM's weight loads there)
-template <bool FP8, int KE, class Hook = TwNoHook>
+template <bool FP8, int KE, int FMX = 0, class Hook = TwNoHook>
 __device__ __forceinline__ void tower_gather(const TowerArgs& a, int row0, bf16* Xl, int ldx,
                                              uint8_t* X8, int ld8, float* s_yfm, float* s_dq0,
                                              float* gx = nullptr, float* gS = nullptr, Hook hook = Hook()) {
   constexpr int V4 = KE / 4;
   // fields per thread per pass, all loads in flight (Criteo: 39 <= 40); K = 32 rows are 8 f32x4
-  // each, so fewer fields per pass keep the loads in registers
-  constexpr int FMAX = KE >= 32 ? 2 : 5;
+  // each, so fewer fields per pass keep the loads in registers (3 per pass: 2 dependent load
+  // rounds for 5 fields instead of 3; the register-capped light kernel keeps 2)
+  constexpr int FMAX = FMX ? FMX : (KE >= 32 ? 3 : 5);
   const int tid = threadIdx.x, sl = tid >> 3, q = tid & 7;
   const int b = row0 + sl, F = a.F;
   f32x4 S[V4], Q[V4];
@@ -375,6 +376,32 @@ __device__ __forceinline__ void tw_grow_tile(const TowerArgs& a, const f32x4 (&a
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// One dX0 tile (32 rows x 32 columns) -> dX0 in HBM through the wave's LDS tile: each lane stores
+// 2 x 16 B of contiguous row data instead of 16 scattered 2-B values (the dX0 phase of a K = 32
+// tower, whose rows go to HBM, measured 15 us of its 51: r4j reference-workload stamps)
+__device__ __forceinline__ void tw_dx0_tile(const TowerArgs& a, const f32x4 (&acc)[2][2], int ct, int row0, int lane,
+                                            bf16* wt) {
+  const int cr = (lane >> 4) * 4, cc = lane & 15;
+#pragma unroll
+  for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+    for (int tj = 0; tj < 2; ++tj)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) wt[(ti * 16 + cr + j) * 40 + tj * 16 + cc] = f2bf(acc[ti][tj][j]);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int q = lane + 64 * k, row = q >> 2, part = q & 3;   // 32 rows x 4 chunks of 8 bf16
+    const uint4 v = *reinterpret_cast<const uint4*>(wt + row * 40 + part * 8);
+    *reinterpret_cast<uint4*>(a.dX0 + (size_t)(row0 + row) * a.K0p + ct * 32 + part * 8) = v;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // LIGHT: a 2-deep ring instead of the primed layer-0 / dX0 weights -- a launch that carries serve
 // workgroups (run-routed row-sharded step) keeps the register count low enough for them to
 // co-reside with two tower workgroups per CU (240 registers left them queued behind the tower:
@@ -423,7 +450,7 @@ __device__ __forceinline__ void tower_bf16_body(const TowerArgs& a, bf16* lds, f
   if constexpr (KE > 0) {
     // (weights primed DURING the gather slowed it more than they saved: its table-row loads
     // compete with them for the same address path)
-    tower_gather<false, KE>(a, row0, Xl, ldx, nullptr, 0, s_yfm, nullptr, grow ? gx : nullptr,
+    tower_gather<false, KE, (LIGHT && KE >= 32) ? 2 : 0>(a, row0, Xl, ldx, nullptr, 0, s_yfm, nullptr, grow ? gx : nullptr,
                             grow ? gS : nullptr);
     __syncthreads();
     TW_ST(1);
@@ -637,6 +664,10 @@ __device__ __forceinline__ void tower_bf16_body(const TowerArgs& a, bf16* lds, f
       f32x4 acc[2][2] = {{c00, c01}, {c10, c11}};
       if (grow) {
         if constexpr (KE > 0) tw_grow_tile<KE>(a, acc, ct, row0, lane, gwt, gx, gS, ginv_on ? ginv : nullptr, s_dl);
+        continue;
+      }
+      if (hbytes >= 4 * TW_ROWS * 40 * 2) {   // (the dead H region holds the 4 wave tiles)
+        tw_dx0_tile(a, acc, ct, row0, lane, gwt);
         continue;
       }
 #pragma unroll
