@@ -509,12 +509,9 @@ __global__ void __launch_bounds__(256) sfwg_kernel(SfArgs A, WgFinArgs W, unsign
   __shared__ SfwgSmem<K> sm;
   const int nw = W.tile_wgs + 1;
   const int ntile = (A.n + SfCfg<K>::TP - 1) / SfCfg<K>::TP;
-#ifdef SFWG_WGFIN_LAST   // (experiment) sparse tiles first, the wgfin workgroups after them
-  const int bid = (int)blockIdx.x < ntile ? (int)blockIdx.x + nw
-                : (int)blockIdx.x < ntile + nw ? (int)blockIdx.x - ntile : (int)blockIdx.x;
-#else
+  // (the wgfin workgroups first: with the sparse tiles first and wgfin in the tail the launch
+  // measured 0.1202-0.1213 vs 0.1032-0.1043 ms/step)
   const int bid = (int)blockIdx.x;
-#endif
   if (bid < nw) {
     SF_ST(8);
     wgfin_body<OPT, SFWG_PF, SFWG_MAXNS, SFWG_TQ>(W, bid, sm.wg);
