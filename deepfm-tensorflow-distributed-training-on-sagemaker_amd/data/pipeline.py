@@ -128,6 +128,13 @@ def _flat_views(flat, B: int, F: int, id_dtype, off):
             flat[off[2]:off[3]].view(torch.float32))
 
 
+def _release_unread(item):
+    """A ring batch the pipeline drops unread (skipped on resume, past max_batches): its slot is
+    free again at once (no kernel will read it)."""
+    if isinstance(item, RingBatch):
+        item.ring.release([item.slot], torch.cuda.current_stream())
+
+
 class _DeviceRing:
     """Persistent device staging ring of the streamed (uncached) input path: ``nslots`` flat
     [ids | vals | labels] buffers, filled by ONE host-to-device copy each, straight from the
@@ -285,12 +292,21 @@ class _DeviceFeeder:
             self._full.put((None, 0, e))
 
     def close(self):
-        """Stop the fill thread (before the loader it reads from is closed)."""
+        """Stop the fill thread (before the loader it reads from is closed); ring slots it filled
+        that were never handed to the consumer are released (nothing reads them)."""
         if self._th is not None:
             self._stop = True
             self._free.put(None)
             self._th.join()
             self._th = None
+            if self.dev_ring is not None:
+                left = []
+                while not self._full.empty():
+                    slot, _, _ = self._full.get_nowait()
+                    if isinstance(slot, tuple):
+                        left.append(slot[1])
+                if left:
+                    self.dev_ring.release(left, torch.cuda.current_stream(self.device))
 
     def __iter__(self):
         import threading
@@ -475,8 +491,10 @@ class InputPipeline:
         try:
             for item in (src if src is not None else loader):
                 if self.max_batches is not None and k >= self.max_batches:
+                    _release_unread(item)
                     break
-                if k < skip:
+                if k < skip:                 # (resume: read past, never trained)
+                    _release_unread(item)
                     k += 1
                     continue
                 t = item if src is not None else self._to_tensors(*item)

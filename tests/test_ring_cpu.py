@@ -109,3 +109,32 @@ def test_ring_random_epochs(seed):
     G = rng.choice([2, 3, 4, 5, 8])
     lengths = [rng.randint(1, 3 * G + 2) for _ in range(rng.randint(2, 6))]
     test_ring_runs_across_epochs_never_overwrite_held_slots(G, lengths)
+
+
+@pytest.mark.parametrize("skip", [1, 5, 9, 16])
+def test_ring_skipped_batches_are_released(skip):
+    """Resume mid-epoch: the pipeline reads past the first ``skip`` batches and releases their
+    slots at once (pipeline._release_unread); the rest of the epoch trains in runs."""
+    G = 4
+    ring = P._DeviceRing(2, 3, "cpu", torch.int32, 2 * G)
+    content, stop = {}, threading.Event()
+    it = _all_batches(ring, [skip + 11, 7], content, stop)
+    for _ in range(skip):
+        s, _ = next(it)
+        ring.release([s], None)
+    cur, trained = next(it, None), skip
+    try:
+        while cur is not None:
+            run = [cur]
+            nxt = next(it, None)
+            while len(run) < G and nxt is not None:
+                run.append(nxt)
+                nxt = next(it, None)
+            for s, tag in run:
+                assert content[s] == tag
+            trained += len(run)
+            ring.release([s for s, _ in run], None)
+            cur = nxt
+    finally:
+        stop.set()
+    assert trained == skip + 11 + 7
