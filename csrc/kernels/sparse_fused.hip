@@ -274,6 +274,10 @@ struct SfSmem {
   float own_lead[SfCfg<K>::C];
 };
 
+#ifndef SF_PRE_ALL
+#define SF_PRE_ALL 0
+#endif
+
 HFM_STAMP_BUF(hfm_st_sf)
 #define SF_ST(k) HFM_STAMP(hfm_st_sf, blockIdx.x, k)
 
@@ -372,9 +376,11 @@ __device__ __forceinline__ void sf_tile_body(const SfArgs& A, const int tile, Sf
   SF_ST(2);
   // the record of this thread's first run head, loaded now: its HBM round trip overlaps the chunk
   // sums below instead of following them (used if that run closes in this tile)
+  // (K <= 16 unless SF_PRE_ALL: at K = 32 the record is held in 15 registers across the chunk sums)
   const int pre_u = tid / T::LPS;
+  constexpr bool PRE = MODE == 0 && (K <= 16 || SF_PRE_ALL);
   SfRec pre;
-  if (MODE == 0 && pre_u < nh) pre = sf_load_rec<K, OPT>(A, skl[hl[pre_u]], sub);
+  if (PRE && pre_u < nh) pre = sf_load_rec<K, OPT>(A, skl[hl[pre_u]], sub);
   // 2. chunk-local run pieces: in place at the head, leading piece into lead[j]
   for (int t = tid; t < T::NCH * T::C; t += 256) {
     const int j = t / T::C, c = t - j * T::C;
@@ -434,7 +440,7 @@ __device__ __forceinline__ void sf_tile_body(const SfArgs& A, const int tile, Sf
       if (!closed) closed = (next_key != key);
     }
     if (closed) {
-      if (MODE == 0 && u == pre_u)
+      if (PRE && u == pre_u)
         sf_apply_rec<K, OPT>(A, key, sub, a, w, c, lr_t, pre);
       else
         sf_apply_row<K, MODE, OPT>(A, key, b0 + hp, sub, a, w, c, lr_t);

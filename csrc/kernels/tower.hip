@@ -207,13 +207,10 @@ __device__ __forceinline__ void tower_gather(const TowerArgs& a, int row0, bf16*
                                              float* gx = nullptr, float* gS = nullptr, Hook hook = Hook()) {
   constexpr int V4 = KE / 4;
   // fields per thread per pass, all loads in flight (Criteo: 39 <= 40); K = 32 rows are 8 f32x4
-  // each, so fewer fields per pass keep the loads in registers (3 per pass: 2 dependent load
-  // rounds for 5 fields instead of 3; the register-capped light kernel keeps 2)
-#ifdef TW_FMAX32_2   // (A/B variant)
+  // each, so fewer fields per pass keep the loads in registers
+  // (3 per pass for K = 32 -- 2 dependent load rounds instead of 3 -- measured no faster on the
+  // B = 1024 reference workload: 0.0981-0.0997 vs 0.0974-0.0979 ms/step, profiles/r4o_ref_ab.log)
   constexpr int FMAX = FMX ? FMX : (KE >= 32 ? 2 : 5);
-#else
-  constexpr int FMAX = FMX ? FMX : (KE >= 32 ? 3 : 5);
-#endif
   const int tid = threadIdx.x, sl = tid >> 3, q = tid & 7;
   const int b = row0 + sl, F = a.F;
   f32x4 S[V4], Q[V4];
@@ -670,11 +667,7 @@ __device__ __forceinline__ void tower_bf16_body(const TowerArgs& a, bf16* lds, f
         if constexpr (KE > 0) tw_grow_tile<KE>(a, acc, ct, row0, lane, gwt, gx, gS, ginv_on ? ginv : nullptr, s_dl);
         continue;
       }
-#ifdef TW_DX0_DIRECT  // (A/B variant)
-      if (false) {
-#else
       if (hbytes >= 4 * TW_ROWS * 40 * 2) {   // (the dead H region holds the 4 wave tiles)
-#endif
         tw_dx0_tile(a, acc, ct, row0, lane, gwt);
         continue;
       }
