@@ -274,10 +274,6 @@ struct SfSmem {
   float own_lead[SfCfg<K>::C];
 };
 
-#ifndef SF_PRE_ALL
-#define SF_PRE_ALL 0
-#endif
-
 HFM_STAMP_BUF(hfm_st_sf)
 #define SF_ST(k) HFM_STAMP(hfm_st_sf, blockIdx.x, k)
 
@@ -376,9 +372,10 @@ __device__ __forceinline__ void sf_tile_body(const SfArgs& A, const int tile, Sf
   SF_ST(2);
   // the record of this thread's first run head, loaded now: its HBM round trip overlaps the chunk
   // sums below instead of following them (used if that run closes in this tile)
-  // (K <= 16 unless SF_PRE_ALL: at K = 32 the record is held in 15 registers across the chunk sums)
+  // (also at K = 32, where it holds 15 registers across the chunk sums: A/B on the reference
+  // workload 0.0961-0.0979 ms/step with, 0.0976-0.0979 without; profiles/r4p_ref_ab.log)
   const int pre_u = tid / T::LPS;
-  constexpr bool PRE = MODE == 0 && (K <= 16 || SF_PRE_ALL);
+  constexpr bool PRE = MODE == 0;
   SfRec pre;
   if (PRE && pre_u < nh) pre = sf_load_rec<K, OPT>(A, skl[hl[pre_u]], sub);
   // 2. chunk-local run pieces: in place at the head, leading piece into lead[j]
