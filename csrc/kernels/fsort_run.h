@@ -13,9 +13,10 @@
 // chains are latency-bound.  Up front, the run's sorts have the chip to themselves.
 //
 //   sort launch:   one 1024-thread workgroup per (batch, field, 16K-row chunk): stable LSD passes
-//                  of 8-bit digits in LDS with wave-ballot ranks (field_sort.hip step 2), ids read
-//                  row-major or field-major (no transpose launch).  A single chunk (B <= 16K) or a
-//                  single-id field writes the final arrays; else the chunk's run.
+//                  of 4-bit digits in LDS with per-(digit, thread) counter ranks (fs2_sort_item;
+//                  the round-3 8-bit wave-ballot form, fs2_sort_item_ballot, stays for A/B), ids
+//                  read row-major or field-major (no transpose launch).  A single chunk (B <= 16K)
+//                  or a single-id field writes the final arrays; else the chunk's run.
 //   merge launch:  (B > 16K only) FSM_WPR 256-thread workgroups per (batch, multi-id field, chunk
 //                  run): merge-path placement of
 //                  every key (fs_merge_kernel's rule: own index + per other run the count of keys
@@ -23,19 +24,24 @@
 //                  staged in LDS one at a time.
 // Output is bit-identical to the per-step field sort (and to the stable global sort).
 #pragma once
+#include <type_traits>
 #include "common.h"
 
-// sort: 1024-thread workgroups over 16K-row chunks (16 keys + 16 packed (row, position) words
-// per lane per pass, 104.6 KB of LDS: one workgroup per CU -- the run's sort has the chip to
-// itself), so a batch of up to 16K rows needs no merge at all
+// sort: 1024-thread workgroups over 16K-row chunks (one workgroup per CU -- the run's sort has the
+// chip to itself), so a batch of up to 16K rows needs no merge at all
 constexpr int FS2_THREADS = 1024;
 constexpr int FS2_WAVES = FS2_THREADS / 64;
 constexpr int FS2_MAXB = 16384;
 constexpr int FS2_IT = FS2_MAXB / FS2_THREADS;      // keys per thread
-constexpr int FS2_WROWS = FS2_MAXB / FS2_WAVES;     // positions per wave
-// LDS: keys u32 [16K], row indices u16 [16K], per-wave digit counts u16 [16][256], digit bases
-// u16 [256], wave sums u32 [4] (the 4 digit-scan waves)
-constexpr int FS2_LDS = FS2_MAXB * 4 + FS2_MAXB * 2 + FS2_WAVES * 256 * 2 + 256 * 2 + 4 * 4;
+constexpr int FS2_WROWS = FS2_MAXB / FS2_WAVES;     // positions per wave (ballot form)
+// counter-rank form (fs2_sort_item): 4-bit digits; LDS: keys u32 [16K], row indices u16 [16K]
+// (both position-swizzled), per-(digit, thread) counters u16 [16][1024], wave sums u32 [16]
+constexpr int FS2_RB = 4;
+constexpr int FS2_ND = 1 << FS2_RB;
+constexpr int FS2_LDS = FS2_MAXB * 4 + FS2_MAXB * 2 + FS2_ND * FS2_THREADS * 2 + FS2_WAVES * 4;
+// ballot form (fs2_sort_item_ballot, kept for tools/fsbench A/B): 8-bit digits; keys u32 [16K],
+// row indices u16 [16K], per-wave digit counts u16 [16][256], digit bases u16 [256], wave sums u32 [4]
+constexpr int FS2_LDS_BALLOT = FS2_MAXB * 4 + FS2_MAXB * 2 + FS2_WAVES * 256 * 2 + 256 * 2 + 4 * 4;
 // merge (batches above one chunk): 256-thread workgroups, 8 keys per thread each
 constexpr int FSM_THREADS = 256;
 constexpr int FSM_EPT = 8;
@@ -61,9 +67,11 @@ struct FsJob {
                      // B ints; the tower writes each slot's gradient row to its sorted position)
 };
 
-// one (field, chunk) work item; lds: FS2_LDS bytes.  The keys live in LDS between passes and
-// each pass holds at most 16 keys + 16 packed (row, position) words per lane.
-__device__ __forceinline__ void fs2_sort_item(const FsJob& J, int item, unsigned char* lds) {
+// one (field, chunk) work item, ballot ranks; lds: FS2_LDS_BALLOT bytes.  The keys live in LDS
+// between passes and each pass holds at most 16 keys + 16 packed (row, position) words per lane.
+// Each 8-bit pass ranks a key among the same-digit keys of its wave with 8 ballots (~6 VALU per
+// key bit): 12 us per pass per workgroup, 55 us for a 28-bit field (profiles/r3f_fs2_bench.log).
+__device__ __forceinline__ void fs2_sort_item_ballot(const FsJob& J, int item, unsigned char* lds) {
   unsigned* lk = reinterpret_cast<unsigned*>(lds);
   unsigned short* lv = reinterpret_cast<unsigned short*>(lk + FS2_MAXB);
   unsigned short* wc = lv + FS2_MAXB;
@@ -211,6 +219,211 @@ __device__ __forceinline__ void fs2_sort_item(const FsJob& J, int item, unsigned
     pko[q] = (row0 + (int)lv[q]) * F + f;
     if (direct && J.inv) J.inv[(size_t)f * J.B + row0 + (int)lv[q]] = f * J.B + row0 + q;
   }
+}
+
+// inclusive wave64 prefix sum in DPP steps: row_shr 1/2/4/8 inside each 16-lane row, then
+// row_bcast 15 / 31 carry the row totals up (no LDS round trips, unlike a shuffle scan)
+__device__ __forceinline__ unsigned fs2_wave_incl_scan(unsigned x) {
+  x += (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);  // row_shr:1
+  x += (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);  // row_shr:2
+  x += (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);  // row_shr:4
+  x += (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);  // row_shr:8
+  x += (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15
+  x += (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31
+  return x;
+}
+
+// LDS word of sort position p: rotated inside its 16-word block by p / 64, so that the blocked
+// reads below (thread t reads positions 16 t + j, j fixed per instruction) hit 64 distinct banks
+__device__ __forceinline__ int fs2_swz(int p) { return (p & ~15) | ((p + (p >> 6)) & 15); }
+
+// one (field, chunk) work item, counter ranks; lds: FS2_LDS bytes.  Stable LSD passes of 4-bit
+// digits over a blocked arrangement: thread t holds the keys at positions [t ipt, t ipt + ipt)
+// (ipt = keys per thread, the smallest power of two with 1024 ipt >= B).  Per pass:
+//   count:   each key increments its thread's counter for its digit (a column of the [16 digits]
+//            [1024 threads] u16 counter table no other thread touches); the value before the
+//            increment is the key's rank among its thread's earlier same-digit keys;
+//   scan:    one exclusive scan of the table in (digit, thread) order -- thread t rakes 16
+//            consecutive counters, a wave scan and the 16 wave sums;
+//   scatter: key -> counter (now: # keys of lower digits + same-digit keys of lower threads) +
+//            its rank; then the blocked keys are read back for the next pass.
+// A key costs ~4 VALU and 6 LDS accesses per 4-bit pass instead of ~48 VALU of ballots per 8-bit
+// pass.  Output is bit-identical to the ballot form (both are the stable sort).
+__device__ __forceinline__ void fs2_sort_item(const FsJob& J, int item, unsigned char* lds) {
+  unsigned* lk = reinterpret_cast<unsigned*>(lds);
+  unsigned short* lv = reinterpret_cast<unsigned short*>(lk + FS2_MAXB);
+  unsigned short* cnt = lv + FS2_MAXB;                       // [FS2_ND][FS2_THREADS]
+  unsigned* wsum = reinterpret_cast<unsigned*>(cnt + FS2_ND * FS2_THREADS);
+  const int f = J.work[2 * item], row0 = J.work[2 * item + 1] * FS2_MAXB;
+  const int B = min(FS2_MAXB, J.B - row0);
+  if (B <= 0) return;
+  const int F = J.F;
+  const int lo = J.fr[4 * f], hi = J.fr[4 * f + 1], bits = J.fr[4 * f + 2];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int* src = J.ld ? J.ids + (size_t)f * J.ld + row0 : J.ids + (size_t)row0 * F + f;
+  const int sst = J.ld ? 1 : F;
+  bool bad = false;
+  if (bits == 0) {  // single-id field: row order is the sorted order; final arrays directly
+    int* sk = J.keys + (size_t)f * J.B + row0;
+    int* pk = J.perm + (size_t)f * J.B + row0;
+    int idv[FS2_IT];
+#pragma unroll
+    for (int k = 0; k < FS2_IT; ++k) {
+      const int b = k * FS2_THREADS + tid;
+      idv[k] = b < B ? src[(size_t)b * sst] : lo;
+    }
+#pragma unroll
+    for (int k = 0; k < FS2_IT; ++k) {
+      const int b = k * FS2_THREADS + tid;
+      if (b < B) {
+        bad |= idv[k] != lo;
+        sk[b] = idv[k];
+        pk[b] = (row0 + b) * F + f;
+        if (J.inv) J.inv[(size_t)f * J.B + row0 + b] = f * J.B + row0 + b;
+      }
+    }
+    if (__any(bad) && lane == 0) atomicOr(J.err, 1u);
+    return;
+  }
+  const bool direct = J.B <= FS2_MAXB;
+  int* sko = (direct ? J.keys : J.rk) + (size_t)f * J.B + row0;
+  int* pko = (direct ? J.perm : J.rp) + (size_t)f * J.B + row0;
+  const unsigned mask = bits >= 32 ? 0xFFFFFFFFu : ((1u << bits) - 1u);
+  const int ipt = B <= 1024 ? 1 : B <= 2048 ? 2 : B <= 4096 ? 4 : B <= 8192 ? 8 : 16;
+  const int np = ((B + ipt - 1) / ipt) * ipt;   // positions in use (sentinels in [B, np))
+  const bool act = tid * ipt < np;              // this thread holds keys
+  const int p0 = tid * ipt;
+  unsigned short* mc = cnt + tid;               // this thread's counter column (stride FS2_THREADS)
+#ifdef FS2_DBG_PASSES  // timing harness only (tools/fsbench/fs2_bench.hip): cap the LSD passes
+  const int passes = min((bits + FS2_RB - 1) / FS2_RB, FS2_DBG_PASSES);
+#else
+  const int passes = (bits + FS2_RB - 1) / FS2_RB;
+#endif
+  // PACK (keys of <= 18 bits): key and row index travel as one word (key << 14 | row), so a pass
+  // moves one LDS array instead of two; else keys u32 in lk, row indices u16 in lv.
+  auto body = [&](auto pack_tag) {
+    constexpr bool PACK = decltype(pack_tag)::value;
+    constexpr int KS = PACK ? 14 : 0;           // key bit offset inside an element
+    // keys (coalesced, row order) into LDS; sentinels past B sort last: their digit is all ones
+    // in every pass, and they start after every real key.  Counters zeroed.
+    {
+      int idv[FS2_IT];
+#pragma unroll
+      for (int k = 0; k < FS2_IT; ++k) {
+        const int p = k * FS2_THREADS + tid;
+        idv[k] = p < B ? src[(size_t)p * sst] : lo;
+      }
+#pragma unroll
+      for (int k = 0; k < FS2_IT; ++k) {
+        const int p = k * FS2_THREADS + tid;
+        if (p < np) {
+          unsigned e = 0xFFFFFFFFu;
+          if (p < B) {
+            bad |= (idv[k] < lo) | (idv[k] >= hi);
+            e = PACK ? ((((unsigned)(idv[k] - lo) & mask) << KS) | (unsigned)p) : ((unsigned)(idv[k] - lo) & mask);
+          }
+          lk[fs2_swz(p)] = e;
+          if (!PACK) lv[fs2_swz(p)] = (unsigned short)p;
+        }
+      }
+      uint4* cz = reinterpret_cast<uint4*>(cnt);
+      for (int i = tid; i < FS2_ND * FS2_THREADS / 8; i += FS2_THREADS) cz[i] = make_uint4(0u, 0u, 0u, 0u);
+    }
+    if (__any(bad) && lane == 0) atomicOr(J.err, 1u);
+    __syncthreads();
+    unsigned kr[FS2_IT], vr[FS2_IT];
+#pragma unroll
+    for (int j = 0; j < FS2_IT; ++j) {
+      kr[j] = 0xFFFFFFFFu;
+      vr[j] = 0u;
+      if (act && j < ipt) {
+        kr[j] = lk[fs2_swz(p0 + j)];
+        vr[j] = (unsigned)(p0 + j);
+      }
+    }
+    for (int pass = 0; pass < passes; ++pass) {
+      const int shift = KS + pass * FS2_RB;
+      // 1. count (own column only: the read-increment-write of one thread's keys run in order)
+      unsigned lr[FS2_IT];
+#pragma unroll
+      for (int j = 0; j < FS2_IT; ++j) {
+        lr[j] = 0u;
+        if (act && j < ipt) {
+          const unsigned d = (kr[j] >> shift) & (FS2_ND - 1);
+          const unsigned c = mc[d * FS2_THREADS];
+          lr[j] = c;
+          mc[d * FS2_THREADS] = (unsigned short)(c + 1u);
+        }
+      }
+      __syncthreads();
+      // 2. exclusive scan of the table in (digit, thread) order: thread t owns counters [16 t, 16 t + 16)
+      {
+        uint4* cw = reinterpret_cast<uint4*>(cnt) + 2 * tid;
+        const uint4 a = cw[0], b = cw[1];
+        const unsigned w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+        unsigned sum = 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) sum += (w[i] & 0xFFFFu) + (w[i] >> 16);
+        const unsigned x = fs2_wave_incl_scan(sum);
+        if (lane == 63) wsum[wv] = x;
+        __syncthreads();
+        unsigned run = x - sum;
+        const uint4* ws4 = reinterpret_cast<const uint4*>(wsum);
+#pragma unroll
+        for (int v4 = 0; v4 < FS2_WAVES / 4; ++v4) {
+          const uint4 q = ws4[v4];   // (one address for the whole wave: a broadcast read)
+          run += (4 * v4 < wv ? q.x : 0u) + (4 * v4 + 1 < wv ? q.y : 0u) + (4 * v4 + 2 < wv ? q.z : 0u) +
+                 (4 * v4 + 3 < wv ? q.w : 0u);
+        }
+        unsigned o[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const unsigned e0 = run, e1 = run + (w[i] & 0xFFFFu);
+          run = e1 + (w[i] >> 16);
+          o[i] = e0 | (e1 << 16);   // offsets <= 16384
+        }
+        cw[0] = make_uint4(o[0], o[1], o[2], o[3]);
+        cw[1] = make_uint4(o[4], o[5], o[6], o[7]);
+      }
+      __syncthreads();
+      // 3. scatter to the new positions, then clear this thread's column for the next pass
+      if (act) {
+#pragma unroll
+        for (int j = 0; j < FS2_IT; ++j) {
+          if (j < ipt) {
+            const unsigned d = (kr[j] >> shift) & (FS2_ND - 1);
+            const int q = fs2_swz((int)(mc[d * FS2_THREADS] + lr[j]));
+            lk[q] = kr[j];
+            if (!PACK) lv[q] = (unsigned short)vr[j];
+          }
+        }
+      }
+      // (every thread, holding keys or not: the scan wrote offsets into every column)
+#pragma unroll
+      for (int d = 0; d < FS2_ND; ++d) mc[d * FS2_THREADS] = 0;
+      __syncthreads();
+      if (act && pass + 1 < passes) {
+#pragma unroll
+        for (int j = 0; j < FS2_IT; ++j) {
+          if (j < ipt) {
+            const int q = fs2_swz(p0 + j);
+            kr[j] = lk[q];
+            if (!PACK) vr[j] = lv[q];
+          }
+        }
+      }
+    }
+    for (int q = tid; q < B; q += FS2_THREADS) {  // sentinels sit past B
+      const int sq = fs2_swz(q);
+      const unsigned e = lk[sq];
+      const int key = (int)(e >> KS), row = PACK ? (int)(e & 0x3FFFu) : (int)lv[sq];
+      sko[q] = min(lo + key, hi - 1);   // (an id outside its field -- flagged above -- stays a valid row)
+      pko[q] = (row0 + row) * F + f;
+      if (direct && J.inv) J.inv[(size_t)f * J.B + row0 + row] = f * J.B + row0 + q;
+    }
+  };
+  if (bits <= 32 - 14) body(std::true_type{});
+  else body(std::false_type{});
 }
 
 // merge workgroup `wg` of the multi-chunk fields: half of run c of field mfields[wg / (2 nrun)] (runs in

@@ -101,6 +101,10 @@ struct TowerArgs {
   const int* inv;   // [F][inv_ld] field-major sorted index of slot (b, f) (fsort_run.h FsJob.inv)
   int g_off;
   int inv_ld;
+  // dX0 in a launch of its own (hfm_tower enqueues tower_dx0_kernel after the tower; bf16 tower,
+  // train, no gradient rows): at B = 1024 the tower has 32 blocks on 256 CUs and its dX0 phase
+  // (K0p / 32 tiles of W_0 per block) was 15 of its 51 us at K = 32
+  int dx0_split;
 };
 constexpr int TW_GINV = 8;  // inv entries prefetched per thread (32 F / 256 <= 8: F <= 64)
 
@@ -310,7 +314,7 @@ __device__ __forceinline__ void tower_gather(const TowerArgs& a, int row0, bf16*
 __host__ __device__ constexpr int tw_np(int KE) { return KE >= 16 ? 6 : (KE == 0 ? 4 : 10); }
 constexpr int TW_HQ = 8;   // head w_out values prefetched per thread (L / 8 <= 8)
 
-__device__ __forceinline__ int tw_nphase(const TowerArgs& a) { return a.train ? 2 * a.nl : a.nl; }
+__device__ __forceinline__ int tw_nphase(const TowerArgs& a) { return a.train ? 2 * a.nl - (a.dx0_split ? 1 : 0) : a.nl; }
 
 // B operand / row stride / k-steps / tiles of phase ph (tile ct)
 struct TwPhase {
@@ -644,6 +648,10 @@ __device__ __forceinline__ void tower_bf16_body(const TowerArgs& a, bf16* lds, f
     store_tile_t(Zo, ldz_out, Nout, a.dZt[i - 1], a.M, row0);
     TW_ST(8 + 2 * (nl - i));
     cur ^= 1;
+  }
+  if (a.dx0_split) {  // dX0 from dZ_0^T by tower_dx0_kernel
+    TW_ST(15);
+    return;
   }
   {
     const int N0 = a.Np[0];
@@ -1003,6 +1011,34 @@ static int tower_launch(const TowerArgs& a, int KE, hipStream_t st) {
   return 0;
 }
 
+// dX0 = dZ_0 W_0 for the tower's row block blockIdx.x, column tiles 4 blockIdx.y .. + 3 (one per
+// wave): dZ_0 (the tower's bf16 tile, from dZ_0^T) transposed into LDS, then the same MFMA chain
+// in the same k order as the tower's dX0 phase, so dX0 is bit-identical to the fused launch's.
+// LDS: [32][N0 + 8] bf16 dZ_0 + 4 wave tiles [32][40] bf16 (16-B row stores, tw_dx0_tile).
+__global__ void __launch_bounds__(256) tower_dx0_kernel(TowerArgs a) {
+  extern __shared__ __align__(16) unsigned char dx_lds_raw[];
+  bf16* Az = reinterpret_cast<bf16*>(dx_lds_raw);
+  const int N0 = a.Np[0], ldz = N0 + 8;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int row0 = blockIdx.x * TW_ROWS;
+  const bf16* zt = a.dZt[0];
+  for (int e = tid; e < N0 * 4; e += 256) {  // (n, 8-row chunk c): 16 B of dZ_0^T row n
+    const int n = e >> 2, c = e & 3;
+    const bf16x8 v = *reinterpret_cast<const bf16x8*>(zt + (size_t)n * a.M + row0 + c * 8);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) Az[(c * 8 + j) * ldz + n] = v[j];
+  }
+  __syncthreads();
+  const int ct = blockIdx.y * 4 + wave;
+  if (ct >= a.K0p / 32) return;
+  f32x4 c00 = {0, 0, 0, 0}, c01 = c00, c10 = c00, c11 = c00;
+  mma32<4>(Az, ldz, a.WT[0] + (size_t)ct * 32 * N0, N0, N0 / 32, lane, c00, c01, c10, c11);
+  const f32x4 acc[2][2] = {{c00, c01}, {c10, c11}};
+  tw_dx0_tile(a, acc, ct, row0, lane, Az + TW_ROWS * ldz + wave * TW_ROWS * 40);
+}
+
+static int tower_dx0_lds(const TowerArgs& a) { return 2 * TW_ROWS * (a.Np[0] + 8) + 4 * TW_ROWS * 40 * 2; }
+
 // KE: embedding size of the fused gather (4, 8, 16 or 32), or 0 when E comes from fm_fwd (global)
 HFM_API int hfm_tower_stamp_rows_per_wg() { return 256 * TW_STAMP_EPT; }
 
@@ -1034,6 +1070,8 @@ HFM_API int hfm_tower(const TowerArgs* ap, int KE, hipStream_t st) {
         (a.train && !a.Et) || (a.fp8 && a.x8_off < 0) || (a.ldv & (a.vbf16 ? 1 : 3)) || (a.idx_ld && a.idx_ld < a.M))
       return (int)hipErrorInvalidValue;
   }
+  if (a.dx0_split && (a.fp8 || !a.train || a.grow || !a.dX0 || !a.dZt[0] || tower_dx0_lds(a) > 64 * 1024))
+    return (int)hipErrorInvalidValue;
   if (a.fp8) {
     if (!KE && (!a.E8 || !a.sE)) return (int)hipErrorInvalidValue;
     for (int i = 0; i < a.nl; ++i)
@@ -1043,6 +1081,9 @@ HFM_API int hfm_tower(const TowerArgs* ap, int KE, hipStream_t st) {
   } else {
     const int rc = tower_launch<false>(a, KE, st);
     if (rc) return rc;
+    if (a.dx0_split)
+      hipLaunchKernelGGL(tower_dx0_kernel, dim3(a.M / TW_ROWS, (a.K0p / 32 + 3) / 4), dim3(256), tower_dx0_lds(a), st,
+                         a);
   }
   HFM_LAUNCH_CHECK();
 }

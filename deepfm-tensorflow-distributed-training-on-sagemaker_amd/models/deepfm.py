@@ -65,6 +65,7 @@ _GROW = knob("HIPFM_GROW")     # 0 off | 1 rows at their sorted positions | 2 ro
 # tf1_dense on one GPU: split sweep concurrent with the step (0: scatter + full-table sweep)
 _TF1_SPLIT = flag("HIPFM_TF1_SPLIT")
 _XROWS = knob("HIPFM_XROWS")
+_DX0_SPLIT = knob("HIPFM_DX0_SPLIT")      # auto | 1 | 0 (tower.hip tower_dx0_kernel)
 _SWEEP_MODE = knob("HIPFM_SWEEP_MODE")      # auto | merged | branch
 _SWEEP_MBLK = int(knob("HIPFM_SWEEP_MBLK"))  # merged-mode sweep workgroups: 512 0.191, 1024 0.179, 2048 0.156, 3072 0.156, 6144 0.172 ms
 _SWEEP_WG = int(knob("HIPFM_SWEEP_WG"))   # 128: 0.178, 256: 0.160, 512: 0.179 ms
@@ -857,6 +858,10 @@ class NativeDeepFM(GraphRunnerMixin, NativeStateMixin):
             a.inv = grow_inv.data_ptr() if self.grow_sorted else 0
             a.g_off, a.lds_bytes = self._tower_grow_layout()
             a.S = 0                            # (the sparse launch reads the rows instead)
+        # dX0 in its own launch (tower.hip tower_dx0_kernel, bit-identical): below 4096 rows the
+        # tower has < 128 blocks, and each would compute all K0p / 32 dX0 tiles alone
+        if train and not grow and not self.fp8 and (_DX0_SPLIT == "1" or (_DX0_SPLIT == "auto" and self.M < 4096)):
+            a.dx0_split = 1
         a.seed = self.seed & 0xFFFFFFFF
         a.train = 1 if train else 0
         a.square_loss = 1 if self.loss_type == "square_loss" else 0

@@ -183,7 +183,8 @@ class TowerArgs(C.Structure):
                 ("x_off", c_int), ("x8_off", c_int), ("S", c_void_p), ("Et", c_void_p), ("idx_ld", c_int),
                 ("id_lim", c_uint32), ("vbf16", c_int), ("serve_wgs", c_int), ("sv", ShServeArgs),
                 ("stamp_wgs", c_int), ("stamp_n", c_int), ("stamp_div", c_int), ("stamp_keys", c_void_p),
-                ("stamp_flags", c_void_p), ("grow", c_void_p), ("inv", c_void_p), ("g_off", c_int), ("inv_ld", c_int)]
+                ("stamp_flags", c_void_p), ("grow", c_void_p), ("inv", c_void_p), ("g_off", c_int), ("inv_ld", c_int),
+                ("dx0_split", c_int)]
 
 
 class CommOp(C.Structure):

@@ -53,6 +53,8 @@ KNOBS: Dict[str, Knob] = {
                        "sparse launch gathers dX0 / S / vals / dlogit per slot"),
     "HIPFM_SERVE_SITE": Knob("sfwg", "variant", "run-routed row-sharded step: the next step's rows served "
                              "by workgroups of the sparse backward's launch (sfwg) or of the tower's (tower)"),
+    "HIPFM_DX0_SPLIT": Knob("auto", "variant", "the tower's dX0 phase in a launch of its own: auto (batches "
+                            "below 4096 rows, where the tower has < 128 blocks) | 1 | 0"),
     "HIPFM_XROWS": Knob("bf16", "variant", "row-sharded exchange rows: bf16 (v as bf16 + fp32 w, 24 B at "
                         "K = 8; fused gather tower) | fp32 (48 B, bitwise the one-GPU reads)"),
     "HIPFM_TF1_SPLIT": Knob("1", "variant", "tf1_dense on one GPU: split form (0: gradient scatter + "
