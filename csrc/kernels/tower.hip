@@ -1021,6 +1021,14 @@ __global__ void __launch_bounds__(256) tower_dx0_kernel(TowerArgs a) {
   const int N0 = a.Np[0], ldz = N0 + 8;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int row0 = blockIdx.x * TW_ROWS;
+  const int ct = blockIdx.y * 4 + wave;
+  const bool has_tile = ct < a.K0p / 32;
+  // the tile's W_0 fragments first (up to 4 k-steps: N0 <= 128 entirely on registers), so their L2
+  // round trip overlaps the dZ_0 load + transpose below
+  constexpr int NP = 4;
+  bf16x8 pb0[NP], pb1[NP];
+  const bf16* Bw = a.WT[0] + (size_t)(has_tile ? ct : 0) * 32 * N0;
+  bfrag_prime<NP>(pb0, pb1, Bw, N0, N0 / 32, lane);
   const bf16* zt = a.dZt[0];
   for (int e = tid; e < N0 * 4; e += 256) {  // (n, 8-row chunk c): 16 B of dZ_0^T row n
     const int n = e >> 2, c = e & 3;
@@ -1029,10 +1037,9 @@ __global__ void __launch_bounds__(256) tower_dx0_kernel(TowerArgs a) {
     for (int j = 0; j < 8; ++j) Az[(c * 8 + j) * ldz + n] = v[j];
   }
   __syncthreads();
-  const int ct = blockIdx.y * 4 + wave;
-  if (ct >= a.K0p / 32) return;
+  if (!has_tile) return;
   f32x4 c00 = {0, 0, 0, 0}, c01 = c00, c10 = c00, c11 = c00;
-  mma32<4>(Az, ldz, a.WT[0] + (size_t)ct * 32 * N0, N0, N0 / 32, lane, c00, c01, c10, c11);
+  mma32_primed<NP>(Az, ldz, Bw, N0, N0 / 32, lane, pb0, pb1, c00, c01, c10, c11);
   const f32x4 acc[2][2] = {{c00, c01}, {c10, c11}};
   tw_dx0_tile(a, acc, ct, row0, lane, Az + TW_ROWS * ldz + wave * TW_ROWS * 40);
 }
