@@ -199,6 +199,9 @@ __device__ __forceinline__ void store_tile_t(const bf16* t, int ld, int N, bf16*
 // FM gather of one 32-sample block (K1): 8 threads per sample, each owning fields q, q+8, ...;
 // E rows go to the bf16 LDS tile (and the fp8 tile), per-sample S / sum E^2 / y_w are summed in
 // registers over the thread's fields, then over its 8 lanes (fixed xor order: deterministic).
+#ifndef TW_ID_PREFETCH
+#define TW_ID_PREFETCH 1
+#endif
 struct TwNoHook {
   __device__ void operator()() const {}
 };
@@ -222,16 +225,23 @@ __device__ __forceinline__ void tower_gather(const TowerArgs& a, int row0, bf16*
   for (int j = 0; j < V4; ++j) S[j] = Q[j] = f32x4{0.f, 0.f, 0.f, 0.f};
   float yw = 0.f, am = 0.f;
   bf16* xr = Xl + sl * ldx;
-  for (int f0 = q; f0 < F; f0 += 8 * FMAX) {
-    int id[FMAX];
-    float x[FMAX];
+  // the ids / values of a pass are loaded during the pass before (issued after its table-row
+  // loads): a pass then waits one dependent round trip (the rows), not two (ids, then rows) --
+  // K = 32 takes ceil(F / 16) passes
+  int id[FMAX];
+  float x[FMAX];
+  auto load_ids = [&](int f0, int (&idv)[FMAX], float (&xv)[FMAX]) __attribute__((always_inline)) {
 #pragma unroll
     for (int t = 0; t < FMAX; ++t) {
       const int f = f0 + 8 * t;
-      id[t] = f < F ? a.idx[a.idx_ld ? (size_t)f * a.idx_ld + b : (size_t)b * F + f] : 0;
-      if (a.id_lim && (unsigned)id[t] >= a.id_lim) id[t] = (int)a.id_lim - 1;
-      x[t] = f < F ? a.vals[(size_t)b * F + f] : 0.f;
+      idv[t] = f < F ? a.idx[a.idx_ld ? (size_t)f * a.idx_ld + b : (size_t)b * F + f] : 0;
+      if (a.id_lim && (unsigned)idv[t] >= a.id_lim) idv[t] = (int)a.id_lim - 1;
+      xv[t] = f < F ? a.vals[(size_t)b * F + f] : 0.f;
     }
+  };
+  load_ids(q, id, x);
+  for (int f0 = q; f0 < F; f0 += 8 * FMAX) {
+    if (!TW_ID_PREFETCH && f0 != q) load_ids(f0, id, x);   // (diagnostic build: the round-3 order)
     f32x4 v[FMAX][V4];
     float w[FMAX];
 #pragma unroll
@@ -242,6 +252,10 @@ __device__ __forceinline__ void tower_gather(const TowerArgs& a, int row0, bf16*
       for (int j = 0; j < V4; ++j) v[t][j] = ok ? ld_row4(row, 4 * j, a.vbf16) : f32x4{0.f, 0.f, 0.f, 0.f};
       w[t] = ok ? a.tw[(size_t)id[t] * a.ldw] : 0.f;
     }
+    int idn[FMAX];
+    float xn[FMAX];
+    const bool more = TW_ID_PREFETCH && f0 + 8 * FMAX < F;   // (K <= 16 at Criteo's F: one pass)
+    if (more) load_ids(f0 + 8 * FMAX, idn, xn);
     if (f0 == q) hook();
 #pragma unroll
     for (int t = 0; t < FMAX; ++t) {
@@ -257,6 +271,13 @@ __device__ __forceinline__ void tower_gather(const TowerArgs& a, int row0, bf16*
         am = fmaxf(am, fmaxf(fmaxf(fabsf(e[0]), fabsf(e[1])), fmaxf(fabsf(e[2]), fabsf(e[3]))));
         bf16x4 eh = {f2bf(e[0]), f2bf(e[1]), f2bf(e[2]), f2bf(e[3])};
         *reinterpret_cast<bf16x4*>(xr + f * KE + 4 * j) = eh;
+      }
+    }
+    if (more) {
+#pragma unroll
+      for (int t = 0; t < FMAX; ++t) {
+        id[t] = idn[t];
+        x[t] = xn[t];
       }
     }
   }
