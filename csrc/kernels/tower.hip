@@ -459,7 +459,8 @@ __device__ __forceinline__ void tower_bf16_body(const TowerArgs& a, bf16* lds, f
   const int ldx = a.K0p + 8;
   bf16* Xl = lds + (KE > 0 ? a.x_off : 0);
   // sorted gradient rows: LDS scratch and this block's inverse permutation (prefetched now)
-  const bool grow = KE > 0 && a.train && a.grow != nullptr;
+  // (with dx0_split the dX0 launch writes the gradient rows: the tower runs its plain layout)
+  const bool grow = KE > 0 && a.train && a.grow != nullptr && !a.dx0_split;
   // sorted positions (else rows in slot order); LIGHT reads them from global in the dX0 phase
   // instead of staging this block's share in LDS (registers held across the dgrad chain)
   const bool ginv_on = grow && a.inv != nullptr && !LIGHT;
@@ -1035,7 +1036,11 @@ static int tower_launch(const TowerArgs& a, int KE, hipStream_t st) {
 // dX0 = dZ_0 W_0 for the tower's row block blockIdx.x, column tiles 4 blockIdx.y .. + 3 (one per
 // wave): dZ_0 (the tower's bf16 tile, from dZ_0^T) transposed into LDS, then the same MFMA chain
 // in the same k order as the tower's dX0 phase, so dX0 is bit-identical to the fused launch's.
-// LDS: [32][N0 + 8] bf16 dZ_0 + 4 wave tiles [32][40] bf16 (16-B row stores, tw_dx0_tile).
+// With gradient rows (a.grow, run-sorted step) each tile becomes its slots' sorted gradient rows
+// (tw_grow_tile, from the block's x / S / dlogit staged in LDS) instead of dX0 -- the path that
+// brings sorted rows to K = 32, whose tower has no LDS left for the rows' scratch.
+// LDS: [32][N0 + 8] bf16 dZ_0 + 4 wave tiles [32][40] bf16 (+ grow: x [32][F], S [32][KE], dl [32]).
+template <int KE>
 __global__ void __launch_bounds__(256) tower_dx0_kernel(TowerArgs a) {
   extern __shared__ __align__(16) unsigned char dx_lds_raw[];
   bf16* Az = reinterpret_cast<bf16*>(dx_lds_raw);
@@ -1044,6 +1049,11 @@ __global__ void __launch_bounds__(256) tower_dx0_kernel(TowerArgs a) {
   const int row0 = blockIdx.x * TW_ROWS;
   const int ct = blockIdx.y * 4 + wave;
   const bool has_tile = ct < a.K0p / 32;
+  bf16* wt = Az + TW_ROWS * ldz + wave * TW_ROWS * 40;
+  float* gx = reinterpret_cast<float*>(Az + TW_ROWS * ldz + 4 * TW_ROWS * 40);
+  float* gS = gx + TW_ROWS * a.F;
+  float* s_dl = gS + TW_ROWS * (KE > 0 ? KE : 1);
+  const bool grow = KE > 0 && a.grow != nullptr;
   // the tile's W_0 fragments first (up to 4 k-steps: N0 <= 128 entirely on registers), so their L2
   // round trip overlaps the dZ_0 load + transpose below
   constexpr int NP = 4;
@@ -1057,15 +1067,29 @@ __global__ void __launch_bounds__(256) tower_dx0_kernel(TowerArgs a) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) Az[(c * 8 + j) * ldz + n] = v[j];
   }
+  if (grow) {  // the block's x, S and dlogit (the tower wrote S and dlogit; x = the slot values)
+    for (int e = tid; e < TW_ROWS * a.F; e += 256) gx[e] = a.vals[(size_t)row0 * a.F + e];
+    for (int e = tid; e < TW_ROWS * KE; e += 256) gS[e] = a.S[(size_t)row0 * KE + e];
+    if (tid < TW_ROWS) s_dl[tid] = a.dlogit[row0 + tid];
+  }
   __syncthreads();
   if (!has_tile) return;
   f32x4 c00 = {0, 0, 0, 0}, c01 = c00, c10 = c00, c11 = c00;
   mma32_primed<NP>(Az, ldz, Bw, N0, N0 / 32, lane, pb0, pb1, c00, c01, c10, c11);
   const f32x4 acc[2][2] = {{c00, c01}, {c10, c11}};
-  tw_dx0_tile(a, acc, ct, row0, lane, Az + TW_ROWS * ldz + wave * TW_ROWS * 40);
+  if constexpr (KE > 0) {
+    if (grow) {
+      tw_grow_tile<KE>(a, acc, ct, row0, lane, wt, gx, gS, nullptr, s_dl);
+      return;
+    }
+  }
+  tw_dx0_tile(a, acc, ct, row0, lane, wt);
 }
 
-static int tower_dx0_lds(const TowerArgs& a) { return 2 * TW_ROWS * (a.Np[0] + 8) + 4 * TW_ROWS * 40 * 2; }
+static int tower_dx0_lds(const TowerArgs& a, int KE) {
+  return 2 * TW_ROWS * (a.Np[0] + 8) + 4 * TW_ROWS * 40 * 2 +
+         (a.grow ? 4 * TW_ROWS * (a.F + (KE > 0 ? KE : 1) + 1) : 0);
+}
 
 // KE: embedding size of the fused gather (4, 8, 16 or 32), or 0 when E comes from fm_fwd (global)
 HFM_API int hfm_tower_stamp_rows_per_wg() { return 256 * TW_STAMP_EPT; }
@@ -1084,7 +1108,9 @@ HFM_API int hfm_tower(const TowerArgs* ap, int KE, hipStream_t st) {
   int hbytes = 0;
   for (int i = 0; i < a.nl; ++i) hbytes += 2 * TW_ROWS * (a.Np[i] + 8);
   const int gwt_bytes = hbytes >= 4 * TW_ROWS * 40 * 2 ? 0 : 4 * TW_ROWS * 40 * 2;
-  if (a.grow && (!KE || a.fp8 || !a.train || (a.inv && a.inv_ld < a.M) || a.F > TW_GINV * 256 / TW_ROWS || a.g_off < 0 || (a.g_off & 15) ||
+  if (a.grow && a.dx0_split && (!KE || a.fp8 || !a.train || !a.S || !a.vals || !a.dlogit || (a.inv && a.inv_ld < a.M)))
+    return (int)hipErrorInvalidValue;
+  if (a.grow && !a.dx0_split && (!KE || a.fp8 || !a.train || (a.inv && a.inv_ld < a.M) || a.F > TW_GINV * 256 / TW_ROWS || a.g_off < 0 || (a.g_off & 15) ||
                  KE > 16 || a.g_off + TW_ROWS * (8 * a.F + 4 * KE) + gwt_bytes > a.lds_bytes))
     return (int)hipErrorInvalidValue;
   if (a.stamp_wgs < 0 || (a.stamp_wgs && (!KE || !a.train || !a.stamp_keys || !a.stamp_flags || a.stamp_div <= 0 ||
@@ -1098,7 +1124,7 @@ HFM_API int hfm_tower(const TowerArgs* ap, int KE, hipStream_t st) {
         (a.train && !a.Et) || (a.fp8 && a.x8_off < 0) || (a.ldv & (a.vbf16 ? 1 : 3)) || (a.idx_ld && a.idx_ld < a.M))
       return (int)hipErrorInvalidValue;
   }
-  if (a.dx0_split && (a.fp8 || !a.train || a.grow || !a.dX0 || !a.dZt[0] || tower_dx0_lds(a) > 64 * 1024))
+  if (a.dx0_split && (a.fp8 || !a.train || !a.dX0 || !a.dZt[0] || tower_dx0_lds(a, KE) > 64 * 1024))
     return (int)hipErrorInvalidValue;
   if (a.fp8) {
     if (!KE && (!a.E8 || !a.sE)) return (int)hipErrorInvalidValue;
@@ -1109,9 +1135,18 @@ HFM_API int hfm_tower(const TowerArgs* ap, int KE, hipStream_t st) {
   } else {
     const int rc = tower_launch<false>(a, KE, st);
     if (rc) return rc;
-    if (a.dx0_split)
-      hipLaunchKernelGGL(tower_dx0_kernel, dim3(a.M / TW_ROWS, (a.K0p / 32 + 3) / 4), dim3(256), tower_dx0_lds(a), st,
-                         a);
+    if (a.dx0_split) {
+      const dim3 g(a.M / TW_ROWS, (a.K0p / 32 + 3) / 4), blk(256);
+      const int lb = tower_dx0_lds(a, KE);
+      switch (KE) {
+        case 0: hipLaunchKernelGGL(tower_dx0_kernel<0>, g, blk, lb, st, a); break;
+        case 4: hipLaunchKernelGGL(tower_dx0_kernel<4>, g, blk, lb, st, a); break;
+        case 8: hipLaunchKernelGGL(tower_dx0_kernel<8>, g, blk, lb, st, a); break;
+        case 16: hipLaunchKernelGGL(tower_dx0_kernel<16>, g, blk, lb, st, a); break;
+        case 32: hipLaunchKernelGGL(tower_dx0_kernel<32>, g, blk, lb, st, a); break;
+        default: return (int)hipErrorInvalidValue;
+      }
+    }
   }
   HFM_LAUNCH_CHECK();
 }

@@ -393,8 +393,15 @@ class NativeDeepFM(GraphRunnerMixin, NativeStateMixin):
                              "batch norm)")
         # sorted gradient rows (run-sorted single-GPU steps): the bf16 gather tower writes every
         # slot's embedding gradient row to its sorted position; the sparse launch streams them
-        self.grow_ok = (self.gather_fused and not self.fp8 and self.K in (4, 8, 16) and self.F <= 64 and
-                        _GROW != "0" and self._tower_grow_layout()[1] <= 150 * 1024)
+        # dX0 in a launch of its own (tower.hip tower_dx0_kernel, bit-identical): below 4096 rows
+        # the tower has < 128 blocks, and each would compute all K0p / 32 dX0 tiles alone
+        # (decided once, from the constructed batch: the K = 32 gradient rows depend on it)
+        self.dx0_split = self.fused and not self.fp8 and (
+            _DX0_SPLIT == "1" or (_DX0_SPLIT == "auto" and self._padM(self.batch_size) < 4096))
+        # (K = 32: the dX0 launch writes the rows -- the tower has no LDS left for their scratch)
+        self.grow_ok = (self.gather_fused and not self.fp8 and self.F <= 64 and _GROW != "0" and
+                        ((self.K in (4, 8, 16) and self._tower_grow_layout()[1] <= 150 * 1024) or
+                         (self.K == 32 and self.dx0_split)))
         self.grow_sorted = _GROW == "1"      # (else slot order: the sparse launch gathers through perm)
         if init:
             if self.V * self.K <= (1 << 24):
@@ -853,15 +860,14 @@ class NativeDeepFM(GraphRunnerMixin, NativeStateMixin):
                 a.E8, a.sE = self.E8.data_ptr(), self.sE.data_ptr()
             for i in range(nl):
                 a.W8[i], a.sW[i] = self.W8[i].data_ptr(), self.sW[i].data_ptr()
+        if train and self.dx0_split:
+            a.dx0_split = 1
         if grow:
             a.grow, a.inv_ld = self.grow.data_ptr(), B                  # (run-sorted: B == M)
             a.inv = grow_inv.data_ptr() if self.grow_sorted else 0
-            a.g_off, a.lds_bytes = self._tower_grow_layout()
-            a.S = 0                            # (the sparse launch reads the rows instead)
-        # dX0 in its own launch (tower.hip tower_dx0_kernel, bit-identical): below 4096 rows the
-        # tower has < 128 blocks, and each would compute all K0p / 32 dX0 tiles alone
-        if train and not grow and not self.fp8 and (_DX0_SPLIT == "1" or (_DX0_SPLIT == "auto" and self.M < 4096)):
-            a.dx0_split = 1
+            if not a.dx0_split:    # (the tower writes the rows: its scratch layout; else the dX0
+                a.g_off, a.lds_bytes = self._tower_grow_layout()      # launch reads S from HBM)
+                a.S = 0                        # (the sparse launch reads the rows instead)
         a.seed = self.seed & 0xFFFFFFFF
         a.train = 1 if train else 0
         a.square_loss = 1 if self.loss_type == "square_loss" else 0

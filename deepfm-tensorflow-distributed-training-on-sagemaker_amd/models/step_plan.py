@@ -61,7 +61,7 @@ class ModeSpec:
     fp8: bool
     wgfin_fits: bool           # the wgfin work fits the sparse + wgfin launch (splits <= SFWG_MAX_NS)
     fin_covers_all: bool       # the finalize launch covers every dense parameter
-    grow_ok: bool = False      # the tower can write sorted gradient rows (bf16 gather tower, K <= 16)
+    grow_ok: bool = False      # the tower (K <= 16) or its dX0 launch (K = 32) can write sorted gradient rows
     tf1x: bool = False         # tf1_dense split form under the native exchange (lazy owner update +
                                # flagged l2-only sweep in the owner launch)
 
