@@ -1039,7 +1039,8 @@ static int tower_launch(const TowerArgs& a, int KE, hipStream_t st) {
 // With gradient rows (a.grow, run-sorted step) each tile becomes its slots' sorted gradient rows
 // (tw_grow_tile, from the block's x / S / dlogit staged in LDS) instead of dX0 -- the path that
 // brings sorted rows to K = 32, whose tower has no LDS left for the rows' scratch.
-// LDS: [32][N0 + 8] bf16 dZ_0 + 4 wave tiles [32][40] bf16 (+ grow: x [32][F], S [32][KE], dl [32]).
+// LDS: [32][N0 + 8] bf16 dZ_0 + 4 wave tiles [32][40] bf16 (+ grow: x [32][F], S [32][KE], dl [32],
+// sorted positions [F][32]).
 template <int KE>
 __global__ void __launch_bounds__(256) tower_dx0_kernel(TowerArgs a) {
   extern __shared__ __align__(16) unsigned char dx_lds_raw[];
@@ -1053,6 +1054,7 @@ __global__ void __launch_bounds__(256) tower_dx0_kernel(TowerArgs a) {
   float* gx = reinterpret_cast<float*>(Az + TW_ROWS * ldz + 4 * TW_ROWS * 40);
   float* gS = gx + TW_ROWS * a.F;
   float* s_dl = gS + TW_ROWS * (KE > 0 ? KE : 1);
+  int* ginv = reinterpret_cast<int*>(s_dl + TW_ROWS);   // [F][32] the block's sorted positions
   const bool grow = KE > 0 && a.grow != nullptr;
   // the tile's W_0 fragments first (up to 4 k-steps: N0 <= 128 entirely on registers), so their L2
   // round trip overlaps the dZ_0 load + transpose below
@@ -1071,6 +1073,9 @@ __global__ void __launch_bounds__(256) tower_dx0_kernel(TowerArgs a) {
     for (int e = tid; e < TW_ROWS * a.F; e += 256) gx[e] = a.vals[(size_t)row0 * a.F + e];
     for (int e = tid; e < TW_ROWS * KE; e += 256) gS[e] = a.S[(size_t)row0 * KE + e];
     if (tid < TW_ROWS) s_dl[tid] = a.dlogit[row0 + tid];
+    if (a.inv)  // (loaded with the rest: the row stores then wait on no dependent load)
+      for (int e = tid; e < TW_ROWS * a.F; e += 256)
+        ginv[e] = a.inv[(size_t)(e / TW_ROWS) * a.inv_ld + row0 + (e % TW_ROWS)];
   }
   __syncthreads();
   if (!has_tile) return;
@@ -1079,7 +1084,7 @@ __global__ void __launch_bounds__(256) tower_dx0_kernel(TowerArgs a) {
   const f32x4 acc[2][2] = {{c00, c01}, {c10, c11}};
   if constexpr (KE > 0) {
     if (grow) {
-      tw_grow_tile<KE>(a, acc, ct, row0, lane, wt, gx, gS, nullptr, s_dl);
+      tw_grow_tile<KE>(a, acc, ct, row0, lane, wt, gx, gS, a.inv ? ginv : nullptr, s_dl);
       return;
     }
   }
@@ -1088,7 +1093,7 @@ __global__ void __launch_bounds__(256) tower_dx0_kernel(TowerArgs a) {
 
 static int tower_dx0_lds(const TowerArgs& a, int KE) {
   return 2 * TW_ROWS * (a.Np[0] + 8) + 4 * TW_ROWS * 40 * 2 +
-         (a.grow ? 4 * TW_ROWS * (a.F + (KE > 0 ? KE : 1) + 1) : 0);
+         (a.grow ? 4 * TW_ROWS * (2 * a.F + (KE > 0 ? KE : 1) + 1) : 0);
 }
 
 // KE: embedding size of the fused gather (4, 8, 16 or 32), or 0 when E comes from fm_fwd (global)
