@@ -492,7 +492,10 @@ __global__ void __launch_bounds__(256) sf_tile_kernel(SfArgs A) {
 #include "shard_table.h"
 
 // the wgfin half's register footprint must not cut the sparse tiles' occupancy (6 waves / SIMD)
-constexpr int SFWG_PF = 2;
+#ifndef SFWG_PF_DEF   // (diagnostic builds may lower it: HIPFM_BUILD_VARIANT=tag:SFWG_PF_DEF=1)
+#define SFWG_PF_DEF 2
+#endif
+constexpr int SFWG_PF = SFWG_PF_DEF;
 constexpr int SFWG_MAXNS = 4;
 // combine tail one element at a time: 84 VGPRs (4 waves / SIMD) vs 113 (3) for all 4 at once;
 // same-box bf16 0.1109-0.1114 (1) / 0.1120-0.1128 (2) / 0.1169-0.1171 (4) ms/step
@@ -507,8 +510,13 @@ union SfwgSmem {
 // (4 waves / SIMD for K = 8; forcing 6 spills 22 VGPRs and measured slower: 0.1139 vs 0.1110 ms)
 // SWEEP (tf1_dense split form): S.nblk more workgroups, dispatched after the sparse tiles, give
 // every row outside the batch its l2-only update (tf1_sweep.h) -- disjoint rows, same step t
+#ifdef SFWG_WPE   // diagnostic build: a waves-per-SIMD floor for the merged launch
+#define SFWG_ATTR __attribute__((amdgpu_waves_per_eu(SFWG_WPE)))
+#else
+#define SFWG_ATTR
+#endif
 template <int K, int OPT, bool SWEEP>
-__global__ void __launch_bounds__(256) sfwg_kernel(SfArgs A, WgFinArgs W, unsigned* done, SweepArgs S) {
+__global__ void __launch_bounds__(256) SFWG_ATTR sfwg_kernel(SfArgs A, WgFinArgs W, unsigned* done, SweepArgs S) {
   __shared__ SfwgSmem<K> sm;
   const int nw = W.tile_wgs + 1;
   const int ntile = (A.n + SfCfg<K>::TP - 1) / SfCfg<K>::TP;
