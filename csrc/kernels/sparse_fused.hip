@@ -510,13 +510,13 @@ union SfwgSmem {
 // (forcing 6 waves / SIMD at K = 8 spills 22 VGPRs and measured slower: 0.1139 vs 0.1110 ms)
 // SWEEP (tf1_dense split form): S.nblk more workgroups, dispatched after the sparse tiles, give
 // every row outside the batch its l2-only update (tf1_sweep.h) -- disjoint rows, same step t
-// 5 waves / SIMD for K <= 8 (5 tile workgroups per CU instead of 4: 1280 of the launch's 1449
-// workgroups resident at once at the Criteo-1TB shape; 8 VGPRs spill in the wgfin half, and the
-// wgfin prefetch ring stays 2 deep -- 1 deep fits without spills but measured slower):
-// 0.1020-0.1032 vs 0.1043-0.1047 ms/step (profiles/r4y_sfwg_occupancy_ab.log).  K >= 16 keeps its
-// 3 (the attribute cannot be met there and changes nothing).  SFWG_WPE=0: no attribute (A/B).
+// Diagnostic: a waves-per-SIMD floor (SFWG_WPE=5: 5 tile workgroups per CU at K <= 8 instead of
+// 4, with 8 VGPRs spilled in the wgfin half).  A first A/B showed 0.1020-0.1032 vs 0.1043-0.1047
+// ms/step (profiles/r4y_sfwg_occupancy_ab.log); a 3 x 3 confirmation on another box did not
+// (0.1043-0.1062 vs 0.1034-0.1053; Kaggle tf1_dense 0.1646 vs 0.1616; the launch 53.4 vs 53.6 us,
+// profiles/r4zz_sfwg_occupancy_confirm.log), so the default stays without the attribute.
 #ifndef SFWG_WPE
-#define SFWG_WPE 5
+#define SFWG_WPE 0
 #endif
 #if SFWG_WPE > 0
 #define SFWG_ATTR __attribute__((amdgpu_waves_per_eu(SFWG_WPE)))
