@@ -2,7 +2,7 @@
 # Kernel trace + three PMC passes of a bench run, summarised ON the box (the raw CSVs exceed
 # gpurun's 64 MiB copy-back): gpurun_out/<tag>_kernels.md and <tag>_pmc.md.
 # usage: scripts/r2q_prof.sh <tag> [bench args...]
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 TAG=${1:-r2q}; shift
 A="${@:---steps 100 --warmup 10}"
 bash scripts/profile.sh "$TAG" $A || exit $?

@@ -2,7 +2,7 @@
 # A/B of bench configurations (env prefixes) in one GPU call: kernel trace summary per arm
 # (gpurun_out/<tag>_<i>_kernels.md) + the bench line, then the stamp profile of the first arm.
 # usage: scripts/r4_ab.sh <tag> "<env for arm 1>" "<env for arm 2>" ... (bench args in $BARGS)
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 TAG=$1; shift
 A="${BARGS:---steps 20 --warmup 5}"
 i=0

@@ -2,7 +2,7 @@
 # Bench A/B over env arms, each arm run twice alternating (A B A B) to expose box noise, plus the
 # kernel trace of the sharded proxy and an emb_dtype=bf16 bench.  Stops on a fatal exit code.
 # usage: scripts/r4_ab2.sh <tag> "<env arm 1>" "<env arm 2>"
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 TAG=$1; shift
 fatal() { case $1 in 124|134|137|139) echo "fatal rc=$1 at $2"; exit $1;; esac; }
 for rep in 1 2; do

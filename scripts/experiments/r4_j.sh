@@ -1,7 +1,7 @@
 #!/bin/bash
 # bf16 embeddings vs fp32 (PMC of both at the headline config), the K = 32 Criteo-1TB table with
 # bf16 records on one GPU, and the Kaggle replicated proxy's kernel timeline.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 TAG=${1:-r4j}
 fatal() { case $1 in 124|134|137|139) echo "fatal rc=$1 at $2"; exit $1;; esac; }
 timeout -k 10 900 python -u -m pytest -x -q --timeout 600 --timeout-method thread tests/test_gpu_plan_state.py tests/test_gpu_determinism.py > gpurun_out/${TAG}_pytest.log 2>&1; rc=$?
@@ -20,6 +20,6 @@ bash scripts/profile.sh "${TAG}_repl" --preset criteo_kaggle --steps 50 --warmup
 python tools/prof_summary.py "gpurun_out/prof_${TAG}_repl" "gpurun_out/${TAG}_repl_kernels.md" "$TAG: Kaggle replicated proxy" > /dev/null
 rm -rf "gpurun_out/prof_${TAG}_repl"
 grep -A14 "One steady-state" gpurun_out/${TAG}_repl_kernels.md
-bash scripts/r4_stamps.sh ${TAG}_ref --preset reference --embedding_size 32 --batch_size 1024 --steps 50 --warmup 5; rc=$?; fatal $rc ref_stamps
+bash scripts/experiments/r4_stamps.sh ${TAG}_ref --preset reference --embedding_size 32 --batch_size 1024 --steps 50 --warmup 5; rc=$?; fatal $rc ref_stamps
 bash scripts/pk_bisect.sh 300; rc=$?; fatal $rc pk
 exit 0

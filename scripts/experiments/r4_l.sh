@@ -1,6 +1,6 @@
 #!/bin/bash
 # Replicated run-level routing (tests + Kaggle mode sweep) and the streamed path with two copy streams.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 TAG=${1:-r4l}
 fatal() { case $1 in 124|134|137|139) echo "fatal rc=$1 at $2"; exit $1;; esac; }
 timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_kernels.py tests/test_gpu_determinism.py > gpurun_out/${TAG}_pytest0.log 2>&1; rc=$?
@@ -11,7 +11,7 @@ timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method threa
 fatal $rc pytest
 echo "pytest rc=$rc: $(tail -1 gpurun_out/${TAG}_pytest.log)"
 [ $rc -ne 0 ] && { grep -E "Error|FAILED" gpurun_out/${TAG}_pytest.log | head -10; exit $rc; }
-bash scripts/r4_modes.sh ${TAG}m; rc=$?; fatal $rc modes
+bash scripts/experiments/r4_modes.sh ${TAG}m; rc=$?; fatal $rc modes
 for k in 1 2; do
   timeout -k 10 300 python bench.py --preset reference --embedding_size 32 --batch_size 1024 --steps 100 --warmup 5 > gpurun_out/${TAG}_ref.log 2>&1; rc=$?; fatal $rc ref
   echo "ref lazy: $(tail -1 gpurun_out/${TAG}_ref.log | grep -o '"ms_per_step": [0-9.]*')"

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Full GPU test suite, then the reference workload (B = 1024, K = 32) A/B over the K = 32 tower
 # variants and its stamps.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 TAG=${1:-r4m}
 fatal() { case $1 in 124|134|137|139) echo "fatal rc=$1 at $2"; exit $1;; esac; }
 timeout -k 10 1000 python -u -m pytest -q --timeout 300 --timeout-method thread -m gpu tests/ > gpurun_out/${TAG}_pytest.log 2>&1; rc=$?

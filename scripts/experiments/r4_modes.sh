@@ -1,7 +1,7 @@
 #!/bin/bash
 # Kaggle-shape step times across the execution modes (1 GPU; the exchange modes as 1-rank
-# proxies): local / replicated / row-sharded x lazy / tf1_dense.  usage: scripts/r4_modes.sh <tag>
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+# proxies): local / replicated / row-sharded x lazy / tf1_dense.  usage: scripts/experiments/r4_modes.sh <tag>
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 TAG=${1:-modes}
 fatal() { case $1 in 124|134|137|139) echo "fatal rc=$1 at $2"; exit $1;; esac; }
 run() {  # name, args...

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Resume (skip) through the streamed ring: the fault test and the e2e tests, then the reference
 # workload A/B over the K = 32 tower variants.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 TAG=${1:-r4o}
 fatal() { case $1 in 124|134|137|139) echo "fatal rc=$1 at $2"; exit $1;; esac; }
 timeout -k 10 600 python -u -m pytest -v --timeout 240 --timeout-method thread tests/test_gpu_fault.py tests/test_gpu_e2e.py > gpurun_out/${TAG}_pytest.log 2>&1; rc=$?

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Reference workload A/B: the sparse tile's early record load at K = 32 on (pa) or off (base);
 # headline driver-window benches.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 TAG=${1:-r4p}
 fatal() { case $1 in 124|134|137|139) echo "fatal rc=$1 at $2"; exit $1;; esac; }
 L=$PWD/deepfm-tensorflow-distributed-training-on-sagemaker_amd/_lib

@@ -2,8 +2,8 @@
 # Kernel trace + occupancy / stall / memory PMC passes of one bench configuration, summarised on
 # the box (gpurun_out/<tag>_kernels.md, <tag>_pmc_raw.md).  One pass per counter group (rocprofv3
 # does not split counters over passes); a pass that times out or crashes ends the script.
-# usage: scripts/r4_pmc.sh <tag> [bench args...]
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+# usage: scripts/experiments/r4_pmc.sh <tag> [bench args...]
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 ROOT=$(pwd)
 TAG=$1; shift
 A="${@:---steps 20 --warmup 5}"

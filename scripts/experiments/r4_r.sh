@@ -1,7 +1,7 @@
 #!/bin/bash
 # Counter-rank run sort: sort tests, then A/B against the ballot-rank build (bl) on the headline
 # and reference-workload benches.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 TAG=${1:-r4r}
 fatal() { case $1 in 0) ;; 124|134|137|139) echo "fatal rc=$1 at $2"; exit $1;; *) echo "rc=$1 at $2";; esac; }
 L=$PWD/deepfm-tensorflow-distributed-training-on-sagemaker_amd/_lib

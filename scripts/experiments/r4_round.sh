@@ -3,7 +3,7 @@
 # GPU test files, and (optionally) the file-fed data bench.  Stops at the first step that times
 # out, aborts or faults (exit 124 / 134 / 137 / 139); a plain test failure does not stop the
 # benches that follow.   usage: TESTS="tests/a.py ..." DATA=1 scripts/r4_round.sh <tag>
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 TAG=${1:-r4}
 fatal() { case $1 in 124|134|137|139) echo "fatal rc=$1 at $2"; exit $1;; esac; }
 for k in 1 2; do

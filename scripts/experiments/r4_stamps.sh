@@ -1,8 +1,8 @@
 #!/bin/bash
 # Phase stamps of the tower / sparse launches (diagnostic stamp library, built on the CPU with
 # HIPFM_BUILD_STAMPS=1) for one bench configuration: gpurun_out/<tag>_stamps.md
-# usage: scripts/r4_stamps.sh <tag> [bench args...]
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+# usage: scripts/experiments/r4_stamps.sh <tag> [bench args...]
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 TAG=$1; shift
 A="${@:---steps 20 --warmup 5}"
 LIB=$(pwd)/deepfm-tensorflow-distributed-training-on-sagemaker_amd/_lib/libhipfm_kernels_stamps.so

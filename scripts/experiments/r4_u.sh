@@ -1,7 +1,7 @@
 #!/bin/bash
 # Reference workload: the FM gather in the tower's prologue (default) vs an fm_fwd launch across
 # the chip (HIPFM_TOWER_GATHER=0), lazy and tf1_dense; timeline of the unfused step
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 TAG=${1:-r4u}
 fatal() { case $1 in 0) ;; 124|134|137|139) echo "fatal rc=$1 at $2"; exit $1;; *) echo "rc=$1 at $2"; exit $1;; esac; }
 R="--preset reference --embedding_size 32 --batch_size 1024 --steps 100 --warmup 5"

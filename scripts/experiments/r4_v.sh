@@ -1,7 +1,7 @@
 #!/bin/bash
 # Tower gather: next pass's ids prefetched (base) vs loaded at the pass start (np), reference
 # workload lazy + tf1_dense and the headline; the dX0 split test and the tower numerics tests
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 TAG=${1:-r4v}
 fatal() { case $1 in 0) ;; 124|134|137|139) echo "fatal rc=$1 at $2"; exit $1;; *) echo "rc=$1 at $2"; exit $1;; esac; }
 L=$PWD/deepfm-tensorflow-distributed-training-on-sagemaker_amd/_lib

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Sorted gradient rows from the dX0 launch (K = 32 and B < 4096): the affected GPU test files one
 # by one, then the reference-workload and headline benches
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 TAG=${1:-r4w}
 fatal() { case $1 in 0) ;; 124|134|137|139) echo "fatal rc=$1 at $2"; exit $1;; *) echo "rc=$1 at $2"; exit $1;; esac; }
 for t in test_gpu_dx0_split test_gpu_run_sort test_gpu_tf1 test_gpu_dist1 test_gpu_shard test_gpu_determinism; do

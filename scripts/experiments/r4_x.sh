@@ -1,7 +1,7 @@
 #!/bin/bash
 # dX0 launch with the block's sorted positions staged in LDS: its test, the reference workload,
 # and the timeline
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 TAG=${1:-r4x}
 fatal() { case $1 in 0) ;; 124|134|137|139) echo "fatal rc=$1 at $2"; exit $1;; *) echo "rc=$1 at $2"; exit $1;; esac; }
 for t in test_gpu_dx0_split test_gpu_run_sort; do

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Exchange-row formats on the 1-rank sharded proxy: GPU exchange tests, then the proxy bench with
 # bf16 and fp32 rows and a kernel trace of the default.  usage: scripts/r4_xrows.sh <tag>
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 TAG=${1:-xr}
 export PYTHONPATH=$PWD
 fatal() { case $1 in 124|134|137|139) echo "fatal rc=$1 at $2"; exit $1;; esac; }

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Merged sparse + wgfin launch at 5 waves / SIMD (w5: 8 spilled VGPRs) vs 4 (base): headline,
 # reference workload; timeline of w5
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 TAG=${1:-r4y}
 fatal() { case $1 in 0) ;; 124|134|137|139) echo "fatal rc=$1 at $2"; exit $1;; *) echo "rc=$1 at $2"; exit $1;; esac; }
 L=$PWD/deepfm-tensorflow-distributed-training-on-sagemaker_amd/_lib

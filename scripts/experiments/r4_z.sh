@@ -1,7 +1,7 @@
 #!/bin/bash
 # 5 waves / SIMD merged launch (now the default) vs no attribute (w0): kernels + determinism
 # tests, 3 headline benches each, Kaggle lazy + tf1 (K = 8), timeline of the default
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 TAG=${1:-r4zz}
 fatal() { case $1 in 0) ;; 124|134|137|139) echo "fatal rc=$1 at $2"; exit $1;; *) echo "rc=$1 at $2"; exit $1;; esac; }
 L=$PWD/deepfm-tensorflow-distributed-training-on-sagemaker_amd/_lib

@@ -1,6 +1,6 @@
 #!/bin/bash
 # 1-GPU bench over warm-up / step counts (the driver runs --steps 20 --warmup 5)
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 for v in "5 20" "10 20" "6 20" "5 21" "4 20" "5 20" "6 20" "4 20" "5 20"; do
   set -- $v
