@@ -185,8 +185,12 @@ __device__ __forceinline__ void mma32_f8_lds(const bf16* A, int lda, const float
 }
 
 // Copy a [32 x N] bf16 LDS tile (row stride ld) to its transpose in global memory:
-// out[c * M + row0 + r]; each thread moves 8 consecutive rows of one column (16-B stores).
+// out[c * M + row0 + r].  Each thread moves 8 consecutive rows of 4 adjacent columns: 8 LDS reads
+// of 8 B and four 16-B stores (N % 4 == 0, ld % 4 == 0: every tile here has N % 32 == 0 and
+// ld = N + 8) -- a quarter of the LDS read instructions of one column per thread (TW_TSTORE1:
+// that form, for A/B).
 __device__ __forceinline__ void store_tile_t(const bf16* t, int ld, int N, bf16* out, int M, int row0) {
+#ifdef TW_TSTORE1
   for (int e = threadIdx.x; e < N * 4; e += blockDim.x) {
     const int c = e >> 2, r8 = (e & 3) * 8;
     bf16x8 v;
@@ -194,6 +198,25 @@ __device__ __forceinline__ void store_tile_t(const bf16* t, int ld, int N, bf16*
     for (int j = 0; j < 8; ++j) v[j] = t[(r8 + j) * ld + c];
     *reinterpret_cast<bf16x8*>(out + (size_t)c * M + row0 + r8) = v;
   }
+#else
+  for (int e = threadIdx.x; e < N; e += blockDim.x) {   // N / 4 column quads x 4 row octets
+    const int c = (e >> 2) * 4, r8 = (e & 3) * 8;
+    bf16x8 v0, v1, v2, v3;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const bf16x4 q = *reinterpret_cast<const bf16x4*>(t + (r8 + j) * ld + c);
+      v0[j] = q[0];
+      v1[j] = q[1];
+      v2[j] = q[2];
+      v3[j] = q[3];
+    }
+    bf16* o = out + (size_t)c * M + row0 + r8;
+    *reinterpret_cast<bf16x8*>(o) = v0;
+    *reinterpret_cast<bf16x8*>(o + M) = v1;
+    *reinterpret_cast<bf16x8*>(o + 2 * (size_t)M) = v2;
+    *reinterpret_cast<bf16x8*>(o + 3 * (size_t)M) = v3;
+  }
+#endif
 }
 
 // FM gather of one 32-sample block (K1): 8 threads per sample, each owning fields q, q+8, ...;
