@@ -1086,12 +1086,25 @@ __global__ void __launch_bounds__(256) tower_dx0_kernel(TowerArgs a) {
   const bf16* Bw = a.WT[0] + (size_t)(has_tile ? ct : 0) * 32 * N0;
   bfrag_prime<NP>(pb0, pb1, Bw, N0, N0 / 32, lane);
   const bf16* zt = a.dZt[0];
+#ifdef TW_DX0_SINGLE   // (A/B build: one dZ_0^T row per item, 2-B LDS writes)
   for (int e = tid; e < N0 * 4; e += 256) {  // (n, 8-row chunk c): 16 B of dZ_0^T row n
     const int n = e >> 2, c = e & 3;
     const bf16x8 v = *reinterpret_cast<const bf16x8*>(zt + (size_t)n * a.M + row0 + c * 8);
 #pragma unroll
     for (int j = 0; j < 8; ++j) Az[(c * 8 + j) * ldz + n] = v[j];
   }
+#else
+  for (int e = tid; e < N0 * 2; e += 256) {  // (n pair, 8-row chunk c): 16 B of rows n, n + 1
+    const int n = (e >> 2) * 2, c = e & 3;
+    const bf16x8 v0 = *reinterpret_cast<const bf16x8*>(zt + (size_t)n * a.M + row0 + c * 8);
+    const bf16x8 v1 = *reinterpret_cast<const bf16x8*>(zt + (size_t)(n + 1) * a.M + row0 + c * 8);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {   // 4-B LDS writes (N0 and ldz even)
+      bf16 pr[2] = {v0[j], v1[j]};
+      *reinterpret_cast<uint32_t*>(Az + (c * 8 + j) * ldz + n) = *reinterpret_cast<const uint32_t*>(pr);
+    }
+  }
+#endif
   if (grow) {  // the block's x, S and dlogit (the tower wrote S and dlogit; x = the slot values)
     for (int e = tid; e < TW_ROWS * a.F; e += 256) gx[e] = a.vals[(size_t)row0 * a.F + e];
     for (int e = tid; e < TW_ROWS * KE; e += 256) gS[e] = a.S[(size_t)row0 * KE + e];
