@@ -3,8 +3,9 @@
 // The data-parallel step issues its collectives straight into RCCL on the HIP streams the
 // kernels run on, so the whole multi-GPU step (exchanges included) is one capturable sequence
 // with no host synchronisation:
-//   * all_reduce   : the flat dense-gradient bucket (Horovod DistributedOptimizer, HVD:262),
-//                    issued on a side stream and overlapped with the sparse backward;
+//   * all_reduce / all_gather : the flat dense-gradient bucket (Horovod DistributedOptimizer,
+//                    HVD:262), grouped with the sparse gradient rows' all-to-all on the step's
+//                    main stream (one communicator, host-fixed order);
 //   * all_to_all   : fixed-capacity id / row / gradient exchanges of the row-sharded embedding
 //                    (every peer block has the same byte size, so no split sizes ever travel
 //                    through the host; xGMI is a full mesh, so all 7 peer links run at once).

@@ -171,11 +171,7 @@ __global__ void __launch_bounds__(FS_THREADS) fs_sort_kernel(const int* __restri
     }
   }
   unsigned* wh = wc + wv * 256;
-#ifdef FS_DEBUG_MAX_PASSES  // timing harness only (tools/fsbench): cap the LSD passes
-  const int passes = min((rb + 7) >> 3, FS_DEBUG_MAX_PASSES);
-#else
   const int passes = (rb + 7) >> 3;
-#endif
   for (int pass = 0; pass < passes; ++pass) {
     const int shift = pass * 8;
     __syncthreads();  // everyone's previous reloads are done before the LDS arrays are rewritten
@@ -285,11 +281,7 @@ __global__ void __launch_bounds__(FS2_THREADS) fs2_sort_run_kernel(const FsJob* 
                                                                    const int* __restrict__ items) {
   extern __shared__ __align__(16) unsigned char lds[];
   const FsJob J = jobs[items[2 * blockIdx.x]];
-#ifdef FS2_BALLOT  // diagnostic build (HIPFM_BUILD_VARIANT=bl:FS2_BALLOT): the round-3 ballot ranks
-  fs2_sort_item_ballot(J, items[2 * blockIdx.x + 1], lds);
-#else
   fs2_sort_item(J, items[2 * blockIdx.x + 1], lds);
-#endif
 }
 
 __global__ void __launch_bounds__(FSM_THREADS) fs2_merge_run_kernel(const FsJob* __restrict__ jobs,
@@ -304,11 +296,7 @@ __global__ void __launch_bounds__(FSM_THREADS) fs2_merge_run_kernel(const FsJob*
 HFM_API int hfm_field_sort_run(const FsJob* jobs, const int* items, int nitems, const int* mitems, int nmitems,
                                hipStream_t st) {
   if (!jobs || !items || nitems <= 0 || nmitems < 0 || (nmitems && !mitems)) return (int)hipErrorInvalidValue;
-#ifdef FS2_BALLOT
-  hipLaunchKernelGGL(fs2_sort_run_kernel, dim3(nitems), dim3(FS2_THREADS), FS2_LDS_BALLOT, st, jobs, items);
-#else
   hipLaunchKernelGGL(fs2_sort_run_kernel, dim3(nitems), dim3(FS2_THREADS), FS2_LDS, st, jobs, items);
-#endif
   if (nmitems)
     hipLaunchKernelGGL(fs2_merge_run_kernel, dim3(nmitems), dim3(FSM_THREADS), FS2_MAXB * 4, st, jobs, mitems);
   HFM_LAUNCH_CHECK();

@@ -139,11 +139,7 @@ __device__ __forceinline__ void fs2_sort_item_ballot(const FsJob& J, int item, u
   }
   if (__any(bad) && lane == 0) atomicOr(J.err, 1u);
   unsigned short* wh = wc + wv * 256;
-#ifdef FS2_DBG_PASSES  // timing harness only (tools/fsbench/fs2_bench.hip): cap the LSD passes
-  const int passes = min((bits + 7) >> 3, FS2_DBG_PASSES);
-#else
   const int passes = (bits + 7) >> 3;
-#endif
   for (int pass = 0; pass < passes; ++pass) {
     const int shift = pass * 8;
     __syncthreads();  // the key arrays are complete (initial fill / previous scatter)
@@ -294,11 +290,7 @@ __device__ __forceinline__ void fs2_sort_item(const FsJob& J, int item, unsigned
   const bool act = tid * ipt < np;              // this thread holds keys
   const int p0 = tid * ipt;
   unsigned short* mc = cnt + tid;               // this thread's counter column (stride FS2_THREADS)
-#ifdef FS2_DBG_PASSES  // timing harness only (tools/fsbench/fs2_bench.hip): cap the LSD passes
-  const int passes = min((bits + FS2_RB - 1) / FS2_RB, FS2_DBG_PASSES);
-#else
   const int passes = (bits + FS2_RB - 1) / FS2_RB;
-#endif
   // PACK (keys of <= 18 bits): key and row index travel as one word (key << 14 | row), so a pass
   // moves one LDS array instead of two; else keys u32 in lk, row indices u16 in lv.
   auto body = [&](auto pack_tag) {

@@ -361,11 +361,7 @@ __device__ __forceinline__ void sh_owner_apply_elem(int gt, const int* __restric
   const bool bf = vbf16 != 0;
   f32x4 pv = {0, 0, 0, 0}, a = {0, 0, 0, 0}, c = {0, 0, 0, 0};
   float pw = 0.f, aw = 0.f, cw = 0.f;
-#ifdef SH_DIAG_NOREC
-  if (false) {
-#else
   if (MODE == 0) {
-#endif
     pv = ld_row4(tv + rb, sub * 4, bf);
     if (OPT != OPT_GD) a = ld_row4(s0v + rb, sub * 4, bf);
     if (OPT == OPT_ADAM || OPT == OPT_FTRL) c = ld_row4(s1v + rb, sub * 4, bf);
@@ -377,13 +373,6 @@ __device__ __forceinline__ void sh_owner_apply_elem(int gt, const int* __restric
   }
   f32x4 g = {0.f, 0.f, 0.f, 0.f};
   float gw = 0.f;
-#ifdef SH_DIAG_NOPROBE
-  {
-    const float* src = recv_g + (size_t)e * RWG;
-    g += f32x4{src[sub * 4], src[sub * 4 + 1], src[sub * 4 + 2], src[sub * 4 + 3]};
-    gw += src[K];
-  }
-#else
   const unsigned long long* tr = sh_find(T, N, (unsigned)row, cur);
   if (!tr) return;  // cannot happen: every received row was inserted by this step's serve / tag
   for (int q = 0; q < p; ++q)
@@ -395,16 +384,11 @@ __device__ __forceinline__ void sh_owner_apply_elem(int gt, const int* __restric
     g += f32x4{src[sub * 4], src[sub * 4 + 1], src[sub * 4 + 2], src[sub * 4 + 3]};
     gw += src[K];
   }
-#endif
   if (MODE == 1) {
     *reinterpret_cast<f32x4*>(Gv + row * K + sub * 4) = g;
     if (sub == 0) Gw[row] = gw;
     return;
   }
-#ifdef SH_DIAG_NOREC   // (diagnostic: the gradient loads stay live, no record traffic)
-  if (g[0] + g[1] + g[2] + g[3] + gw == 1e30f) tv[0] = 0.f;
-  return;
-#endif
   const float lr_t = OPT == OPT_ADAM ? adam_lr_t(h, *step + 1) : h.lr;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -430,11 +414,7 @@ __device__ __forceinline__ void sh_owner_apply_elem(int gt, const int* __restric
     if (OPT == OPT_ADAM || OPT == OPT_FTRL) s1w[ow] = cw;
     wnew = pw;
   }
-#ifdef SH_DIAG_NOPATCH
-  if (false) {
-#else
   if (NT.key) {
-#endif
     // the next step's requests were served ahead (before this update): refresh the rows this
     // update changed in every requester's block of the next fetch
     const unsigned long long* nr = sh_find(NT, N, (unsigned)row, cur + 1);
@@ -658,9 +638,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) s
                               (long)(b - apply_blocks - D.blocks) * 256 + threadIdx.x, (long)A.sweep_blocks * 256);
   } else {
     const float lr_t = OPT == OPT_ADAM ? adam_lr_t(D.h, *A.step + 1) : D.h.lr;
-#ifdef SH_DIAG_NODENSE
-    if (lr_t != 12345.f) goto arrive;
-#endif
     for (long i = (long)(b - apply_blocks) * 256 + threadIdx.x; i < D.n; i += (long)D.blocks * 256) {
       if (D.nsum > 0) {  // the all-gathered per-rank dense gradients: the all-reduce, in rank order
         float gi = D.g[i];
@@ -671,9 +648,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) s
       }
     }
   }
-#ifdef SH_DIAG_NODENSE
-arrive:
-#endif
   __syncthreads();
   if (threadIdx.x == 0) {
     const unsigned prev = __hip_atomic_fetch_add(D.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -492,10 +492,7 @@ __global__ void __launch_bounds__(256) sf_tile_kernel(SfArgs A) {
 #include "shard_table.h"
 
 // the wgfin half's register footprint must not cut the sparse tiles' occupancy (6 waves / SIMD)
-#ifndef SFWG_PF_DEF   // (diagnostic builds may lower it: HIPFM_BUILD_VARIANT=tag:SFWG_PF_DEF=1)
-#define SFWG_PF_DEF 2
-#endif
-constexpr int SFWG_PF = SFWG_PF_DEF;
+constexpr int SFWG_PF = 2;
 constexpr int SFWG_MAXNS = 4;
 // combine tail one element at a time: 84 VGPRs (4 waves / SIMD) vs 113 (3) for all 4 at once;
 // same-box bf16 0.1109-0.1114 (1) / 0.1120-0.1128 (2) / 0.1169-0.1171 (4) ms/step
@@ -510,21 +507,10 @@ union SfwgSmem {
 // (forcing 6 waves / SIMD at K = 8 spills 22 VGPRs and measured slower: 0.1139 vs 0.1110 ms)
 // SWEEP (tf1_dense split form): S.nblk more workgroups, dispatched after the sparse tiles, give
 // every row outside the batch its l2-only update (tf1_sweep.h) -- disjoint rows, same step t
-// Diagnostic: a waves-per-SIMD floor (SFWG_WPE=5: 5 tile workgroups per CU at K <= 8 instead of
-// 4, with 8 VGPRs spilled in the wgfin half).  A first A/B showed 0.1020-0.1032 vs 0.1043-0.1047
-// ms/step (profiles/r4y_sfwg_occupancy_ab.log); a 3 x 3 confirmation on another box did not
-// (0.1043-0.1062 vs 0.1034-0.1053; Kaggle tf1_dense 0.1646 vs 0.1616; the launch 53.4 vs 53.6 us,
-// profiles/r4zz_sfwg_occupancy_confirm.log), so the default stays without the attribute.
-#ifndef SFWG_WPE
-#define SFWG_WPE 0
-#endif
-#if SFWG_WPE > 0
-#define SFWG_ATTR __attribute__((amdgpu_waves_per_eu(SFWG_WPE)))
-#else
-#define SFWG_ATTR
-#endif
+// (a waves-per-SIMD floor of 5 -- 5 tile workgroups per CU at K <= 8, 8 VGPRs spilled in the
+// wgfin half -- did not hold up in a 3 x 3 A/B: profiles/r4zz_sfwg_occupancy_confirm.log)
 template <int K, int OPT, bool SWEEP>
-__global__ void __launch_bounds__(256) SFWG_ATTR sfwg_kernel(SfArgs A, WgFinArgs W, unsigned* done, SweepArgs S) {
+__global__ void __launch_bounds__(256) sfwg_kernel(SfArgs A, WgFinArgs W, unsigned* done, SweepArgs S) {
   __shared__ SfwgSmem<K> sm;
   const int nw = W.tile_wgs + 1;
   const int ntile = (A.n + SfCfg<K>::TP - 1) / SfCfg<K>::TP;

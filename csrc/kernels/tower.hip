@@ -190,15 +190,6 @@ __device__ __forceinline__ void mma32_f8_lds(const bf16* A, int lda, const float
 // ld = N + 8) -- a quarter of the LDS read instructions of one column per thread (TW_TSTORE1:
 // that form, for A/B).
 __device__ __forceinline__ void store_tile_t(const bf16* t, int ld, int N, bf16* out, int M, int row0) {
-#ifdef TW_TSTORE1
-  for (int e = threadIdx.x; e < N * 4; e += blockDim.x) {
-    const int c = e >> 2, r8 = (e & 3) * 8;
-    bf16x8 v;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = t[(r8 + j) * ld + c];
-    *reinterpret_cast<bf16x8*>(out + (size_t)c * M + row0 + r8) = v;
-  }
-#else
   for (int e = threadIdx.x; e < N; e += blockDim.x) {   // N / 4 column quads x 4 row octets
     const int c = (e >> 2) * 4, r8 = (e & 3) * 8;
     bf16x8 v0, v1, v2, v3;
@@ -216,15 +207,11 @@ __device__ __forceinline__ void store_tile_t(const bf16* t, int ld, int N, bf16*
     *reinterpret_cast<bf16x8*>(o + 2 * (size_t)M) = v2;
     *reinterpret_cast<bf16x8*>(o + 3 * (size_t)M) = v3;
   }
-#endif
 }
 
 // FM gather of one 32-sample block (K1): 8 threads per sample, each owning fields q, q+8, ...;
 // E rows go to the bf16 LDS tile (and the fp8 tile), per-sample S / sum E^2 / y_w are summed in
 // registers over the thread's fields, then over its 8 lanes (fixed xor order: deterministic).
-#ifndef TW_ID_PREFETCH
-#define TW_ID_PREFETCH 1
-#endif
 struct TwNoHook {
   __device__ void operator()() const {}
 };
@@ -264,7 +251,6 @@ __device__ __forceinline__ void tower_gather(const TowerArgs& a, int row0, bf16*
   };
   load_ids(q, id, x);
   for (int f0 = q; f0 < F; f0 += 8 * FMAX) {
-    if (!TW_ID_PREFETCH && f0 != q) load_ids(f0, id, x);   // (diagnostic build: the round-3 order)
     f32x4 v[FMAX][V4];
     float w[FMAX];
 #pragma unroll
@@ -277,7 +263,7 @@ __device__ __forceinline__ void tower_gather(const TowerArgs& a, int row0, bf16*
     }
     int idn[FMAX];
     float xn[FMAX];
-    const bool more = TW_ID_PREFETCH && f0 + 8 * FMAX < F;   // (K <= 16 at Criteo's F: one pass)
+    const bool more = f0 + 8 * FMAX < F;   // (K <= 16 at Criteo's F: one pass)
     if (more) load_ids(f0 + 8 * FMAX, idn, xn);
     if (f0 == q) hook();
 #pragma unroll
@@ -504,10 +490,6 @@ __device__ __forceinline__ void tower_bf16_body(const TowerArgs& a, bf16* lds, f
                             grow ? gS : nullptr);
     __syncthreads();
     TW_ST(1);
-#if defined(TW_BISECT) && TW_BISECT == 1   // tools/pkhazard: stop after the gather
-    if ((tid & 7) == 0) a.y_fm[row0 + (tid >> 3)] = s_yfm[tid >> 3];
-    return;
-#endif
   }
   // the head's operands, then (behind the E^T stores in the memory queue) the first GEMM tile's
   // weights
@@ -577,10 +559,6 @@ __device__ __forceinline__ void tower_bf16_body(const TowerArgs& a, bf16* lds, f
     TW_ST(3 + i);
     if (a.train && a.Ht[i]) store_tile_t(Hl, ldh, N, a.Ht[i], a.M, row0);
   }
-#if defined(TW_BISECT) && TW_BISECT == 2   // tools/pkhazard: stop after the forward layers
-  if (KE > 0 && (tid & 7) == 0) a.y_fm[row0 + (tid >> 3)] = s_yfm[tid >> 3];
-  return;
-#endif
   // ---------------------------------------------------------------- head
   {
     const bf16* H = lds + a.h_off[nl - 1];
@@ -708,6 +686,10 @@ __device__ __forceinline__ void tower_bf16_body(const TowerArgs& a, bf16* lds, f
         const int e = tid + 256 * k;
         if (e < TW_ROWS * a.F) ginv[e] = ivr[k];
       }
+      __syncthreads();
+    } else if (nl == 1) {
+      // one hidden layer: no dgrad chain (and its barriers) since the head's partial sums read
+      // H_0, and the dX0 wave tiles (gwt) may live in that region -- wait for every reader
       __syncthreads();
     }
     for (int ct = wave; ct < a.K0p / 32; ct += 4) {
@@ -1086,14 +1068,6 @@ __global__ void __launch_bounds__(256) tower_dx0_kernel(TowerArgs a) {
   const bf16* Bw = a.WT[0] + (size_t)(has_tile ? ct : 0) * 32 * N0;
   bfrag_prime<NP>(pb0, pb1, Bw, N0, N0 / 32, lane);
   const bf16* zt = a.dZt[0];
-#ifdef TW_DX0_SINGLE   // (A/B build: one dZ_0^T row per item, 2-B LDS writes)
-  for (int e = tid; e < N0 * 4; e += 256) {  // (n, 8-row chunk c): 16 B of dZ_0^T row n
-    const int n = e >> 2, c = e & 3;
-    const bf16x8 v = *reinterpret_cast<const bf16x8*>(zt + (size_t)n * a.M + row0 + c * 8);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) Az[(c * 8 + j) * ldz + n] = v[j];
-  }
-#else
   for (int e = tid; e < N0 * 2; e += 256) {  // (n pair, 8-row chunk c): 16 B of rows n, n + 1
     const int n = (e >> 2) * 2, c = e & 3;
     const bf16x8 v0 = *reinterpret_cast<const bf16x8*>(zt + (size_t)n * a.M + row0 + c * 8);
@@ -1104,7 +1078,6 @@ __global__ void __launch_bounds__(256) tower_dx0_kernel(TowerArgs a) {
       *reinterpret_cast<uint32_t*>(Az + (c * 8 + j) * ldz + n) = *reinterpret_cast<const uint32_t*>(pr);
     }
   }
-#endif
   if (grow) {  // the block's x, S and dlogit (the tower wrote S and dlogit; x = the slot values)
     for (int e = tid; e < TW_ROWS * a.F; e += 256) gx[e] = a.vals[(size_t)row0 * a.F + e];
     for (int e = tid; e < TW_ROWS * KE; e += 256) gS[e] = a.S[(size_t)row0 * KE + e];

@@ -161,16 +161,26 @@ class _DeviceRing:
     def fits(self, B: int, F: int, id_dtype, nslots: int) -> bool:
         return (self.B, self.F, self.id_dtype, self.nslots) == (B, F, id_dtype, nslots)
 
+    STOPPED = object()      # acquire(): ``stop()`` turned true before the slot was taken
+
     def acquire(self, slot: int, stop) -> Optional[torch.cuda.Event]:
-        """(fill thread) Wait until ``slot`` was released; returns the compute-stream event its
-        refill must wait for."""
+        """(fill thread) Wait until ``slot`` was released and take it; returns the compute-stream
+        event its refill must wait for (or ``STOPPED``: the slot was not taken)."""
         with self.cv:
             while not self.free[slot]:
                 if stop():
-                    return None
+                    return _DeviceRing.STOPPED
                 self.cv.wait(0.05)
             self.free[slot] = False
             return self.ev[slot]
+
+    def giveback(self, slot: int, ev) -> None:
+        """(fill thread) Return a slot taken by ``acquire`` but never filled (the feeder stopped):
+        free again, with the same compute-stream event its next refill must wait for."""
+        with self.cv:
+            self.ev[slot] = ev
+            self.free[slot] = True
+            self.cv.notify_all()
 
     def start(self) -> int:
         """First slot of a new epoch's feeder.  Numbering continues across epochs: a consumer
@@ -272,7 +282,12 @@ class _DeviceFeeder:
                     k += 1
                     R.next = k
                     wait = R.acquire(s, lambda: self._stop)
+                    if wait is _DeviceRing.STOPPED:      # stopped before the slot was taken
+                        return
                     if self._stop:
+                        # stopped right after taking slot s: hand it back untouched, or a later
+                        # epoch's fill thread waits on it forever
+                        R.giveback(s, wait)
                         return
                     cs = self.copies[k % len(self.copies)]
                     with torch.cuda.stream(cs):

@@ -614,8 +614,7 @@ class NativeDeepFM(GraphRunnerMixin, NativeStateMixin):
                            getattr(self, "_wgfin_ns", 1 << 30) <= KN.SFWG_MAX_NS)
         self._xflags = torch.zeros(self.R, dtype=torch.uint8, device=dev) if self.tf1_xsplit else None
         self._own_in = (self.idx, self.vals, self.labels)
-        self._graphs = {}
-        self._run_memo = {}
+        self._drop_graphs()
         self.max_graphs = 256
         self._graph = None
 
@@ -658,8 +657,7 @@ class NativeDeepFM(GraphRunnerMixin, NativeStateMixin):
         elif self.rpx is not None:
             from ..parallel.replicated import ReplicatedExchange
             self.rpx = ReplicatedExchange(self, self.comm.engine, self.comm.capacity)
-        self._graphs = {}
-        self._run_memo = {}
+        self._drop_graphs()
 
     def set_field_ranges(self, ranges):
         """Per-field id ranges found after construction (e.g. derived while caching the first
@@ -667,8 +665,7 @@ class NativeDeepFM(GraphRunnerMixin, NativeStateMixin):
         self.field_ranges = None if ranges is None else check_field_ranges(ranges, self.F, self.V)
         self._make_field_sorts()
         self._ss_key = [None, None]
-        self._graphs = {}
-        self._run_memo = {}
+        self._drop_graphs()
 
     def _build_finalize_jobs(self):
         jobs = []

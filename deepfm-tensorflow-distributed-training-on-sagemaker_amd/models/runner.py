@@ -477,6 +477,13 @@ class GraphRunnerMixin:
             known[id(src)] = (src, tuple(src), mkey, g, tf1c, self._knobs())
         return G
 
+    def _drop_graphs(self):
+        """Forget every captured graph (parameters / plans they baked in changed): the graph
+        table, the run memo and the host fast path's run entries, which hold graphs too."""
+        self._graphs = {}
+        self._run_memo = {}
+        self.__dict__.pop("_known_runs", None)
+
     def reset_plan_state(self):
         """Drop every prefetched sort / routing set and restart the set rotation (host-synchronous;
         no buffer is touched: the next step just sorts / routes its batch itself).  A caller that

@@ -141,8 +141,7 @@ class NativeStateMixin:
                     cur[k].copy_(v.to(cur[k].device, cur[k].dtype))
         self.refresh_shadows()
         self._reset_sync()
-        self._graphs = {}
-        self._run_memo = {}
+        self._drop_graphs()
 
     def tf_variables(self, tables=None, upcast: bool = True) -> "OrderedDict[str, torch.Tensor]":
         """TF1 checkpoint view: reference variable names, [in,out] weights,
@@ -226,5 +225,4 @@ class NativeStateMixin:
                 self.step.fill_(int(torch.as_tensor(tv["global_step"])))
                 self._host_step = None
                 self._reset_sync()
-        self._graphs = {}
-        self._run_memo = {}
+        self._drop_graphs()

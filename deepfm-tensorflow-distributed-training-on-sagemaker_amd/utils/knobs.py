@@ -55,8 +55,9 @@ KNOBS: Dict[str, Knob] = {
                              "by workgroups of the sparse backward's launch (sfwg) or of the tower's (tower)"),
     "HIPFM_DX0_SPLIT": Knob("auto", "variant", "the tower's dX0 phase in a launch of its own: auto (batches "
                             "below 4096 rows, where the tower has < 128 blocks) | 1 | 0"),
-    "HIPFM_XROWS": Knob("bf16", "variant", "row-sharded exchange rows: bf16 (v as bf16 + fp32 w, 24 B at "
-                        "K = 8; fused gather tower) | fp32 (48 B, bitwise the one-GPU reads)"),
+    "HIPFM_XROWS": Knob("fp32", "variant", "row-sharded exchange rows: fp32 (48 B at K = 8, bitwise the "
+                        "one-GPU reads: the default, numerically the single-GPU step) | bf16 (opt-in: v as "
+                        "bf16 + fp32 w, 24 B; fused gather tower; the FM terms then read bf16-rounded v)"),
     "HIPFM_TF1_SPLIT": Knob("1", "variant", "tf1_dense on one GPU: split form (0: gradient scatter + "
                             "full-table sweep, the oracle in tests/test_gpu_tf1.py)"),
     "HIPFM_SWEEP_MODE": Knob("auto", "variant", "tf1_dense split sweep: merged (workgroups of the "

@@ -30,8 +30,11 @@ def _producer(ring, n, content, q, stop):
         s = k % ring.nslots
         k += 1
         ring.next = k
-        ring.acquire(s, lambda: stop.is_set())
+        w = ring.acquire(s, lambda: stop.is_set())
+        if w is P._DeviceRing.STOPPED:
+            return
         if stop.is_set():
+            ring.giveback(s, w)
             return
         content[s] = (id(q), i)                   # "the copy": the slot now holds batch i
         q.put((s, (id(q), i)))
@@ -138,3 +141,33 @@ def test_ring_skipped_batches_are_released(skip):
     finally:
         stop.set()
     assert trained == skip + 11 + 7
+
+
+def test_ring_stop_right_after_acquire_gives_the_slot_back():
+    """max_batches / close() can set the stop flag between a successful acquire and the copy: the
+    fill thread must return that slot, or the next epoch's fill thread waits on it forever."""
+    G = 2
+    ring = P._DeviceRing(2, 3, "cpu", torch.int32, 2 * G)
+    s = ring.start()
+    w = ring.acquire(s, lambda: False)            # taken ...
+    assert w is not P._DeviceRing.STOPPED and not ring.free[s]
+    ring.giveback(s, w)                           # ... and the stop is seen: handed back
+    assert all(ring.free)
+    # a consumer holds every slot: a stopped acquire returns STOPPED without taking anything
+    for k in range(ring.nslots):
+        ring.acquire(k, lambda: False)
+    stop = threading.Event()
+    out = []
+    th = threading.Thread(target=lambda: out.append(ring.acquire(0, stop.is_set)), daemon=True)
+    th.start()
+    stop.set()
+    th.join(timeout=5)
+    assert out == [P._DeviceRing.STOPPED] and not any(ring.free)
+    ring.release_all(None)
+    # the next epoch is not blocked
+    content, stop2 = {}, threading.Event()
+    n = 0
+    for s_, _ in _all_batches(ring, [5], content, stop2):
+        ring.release([s_], None)
+        n += 1
+    assert n == 5
