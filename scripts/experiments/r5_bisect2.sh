@@ -14,4 +14,4 @@ run() {
 T=tests/test_gpu_
 ALL="${T}bn.py ${T}determinism.py ${T}dist1.py ${T}dx0_split.py ${T}e2e.py ${T}fault.py ${T}fp8.py ${T}kernels.py ${T}mixed.py ${T}plan_state.py ${T}run_sort.py ${T}safety.py"
 
-R5_N8_DIAG=1 run D $ALL ${T}shard.py -s || exit 1
+run D $ALL ${T}shard.py || exit 1
