@@ -13,6 +13,11 @@ typedef __bf16 bf16;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+// sorted gradient rows (tower -> sparse backward) are {a[K], g_w, c}: K + 2 floats, so a row
+// start is only 8-B aligned -- these types say so (the compiler must not assume 16 B)
+typedef float f32x4a8 __attribute__((ext_vector_type(4), aligned(8)));
+typedef float f32x2a8 __attribute__((ext_vector_type(2), aligned(8)));
+__host__ __device__ constexpr int grow_stride(int K) { return K + 2; }
 
 #define HFM_API extern "C" __attribute__((visibility("default")))
 

@@ -71,11 +71,11 @@ struct SfArgs {
   int v_by_key;     // MODE 2: 1 = V rows from the local table row key / row_div (replicated-table
                     // exchange), 0 = from the received rows at upos (row-sharded exchange)
   int vbf16;        // table v rows and v slots are bf16 (mixed-precision embeddings; MODE 0 / 2)
-  // or null: [n][K + 4] per-slot rows {a[K], g_w, c, 0, 0} already in SORTED order (written by the
+  // or null: [n][K + 2] per-slot rows {a[K], g_w, c} already in SORTED order (written by the
   // tower straight to each slot's sorted position): step 1 streams them instead of gathering
   // perm -> vals / dlogit / S / dX0 per slot
   const float* grow;
-  int grow_perm;    // 1: grow rows are in SLOT order (b*F + f): gathered through perm, one 48-B row per slot
+  int grow_perm;    // 1: grow rows are in SLOT order (b*F + f): gathered through perm, one 40-B row per slot
 };
 
 // one row's record as the lazy optimizer reads it (the f32x4 column group `sub` of v and its
@@ -309,12 +309,12 @@ __device__ __forceinline__ void sf_tile_body(const SfArgs& A, const int tile, Sf
     for (int ps = 0; ps < T::PASSES; ++ps) {
       const int p = ps * T::PPP + tid / T::LPS;
       if (p < nloc) {
-        const float* gr = A.grow + (size_t)(A.grow_perm ? A.perm[b0 + p] : b0 + p) * T::RS;
-        const f32x4 av = *reinterpret_cast<const f32x4*>(gr + sub * 4);
+        const float* gr = A.grow + (size_t)(A.grow_perm ? A.perm[b0 + p] : b0 + p) * grow_stride(K);
+        const f32x4 av = *reinterpret_cast<const f32x4a8*>(gr + sub * 4);
 #pragma unroll
         for (int j = 0; j < 4; ++j) g[p][sub * 4 + j] = av[j];
         if (sub == 0) {
-          const float2 wc = *reinterpret_cast<const float2*>(gr + K);
+          const f32x2a8 wc = *reinterpret_cast<const f32x2a8*>(gr + K);
           g[p][K] = wc.x;
           g[p][K + 1] = wc.y;
           skl[p] = A.sorted_keys[b0 + p];

@@ -94,7 +94,7 @@ struct TowerArgs {
   const int* stamp_keys;
   unsigned char* stamp_flags;
   // sorted gradient rows (bf16 gather tower, train, run-sorted step): every slot's embedding
-  // gradient row {a[K], g_w, c, 0, 0} is written to grow[inv[slot]] -- its SORTED position -- so
+  // gradient row {a[K], g_w, c} is written to grow[inv[slot]] -- its SORTED position -- so
   // the sparse backward streams them (no per-slot gather); dX0 / S are then not written.  g_off:
   // LDS byte offset of the scratch [x 32 x F][S 32 x K][inv 32 x F][4 wave tiles 32 x 40 bf16].
   float* grow;
@@ -377,7 +377,7 @@ template <int KE>
 __device__ __forceinline__ void tw_grow_tile(const TowerArgs& a, const f32x4 (&acc)[2][2], int ct, int row0, int lane,
                                              bf16* wt, const float* gx, const float* gS, const int* ginv,
                                              const float* s_dl) {
-  constexpr int FPT = 32 / KE, LPS = KE / 4, RS = KE + 4;
+  constexpr int FPT = 32 / KE, LPS = KE / 4, RS = grow_stride(KE);
   const int cr = (lane >> 4) * 4, cc = lane & 15, F = a.F;
 #pragma unroll
   for (int ti = 0; ti < 2; ++ti)
@@ -402,8 +402,8 @@ __device__ __forceinline__ void tw_grow_tile(const TowerArgs& a, const f32x4 (&a
       const int pos = !a.inv ? (row0 + row) * F + f
                              : ginv ? ginv[f * 32 + row] : a.inv[(size_t)f * a.inv_ld + row0 + row];
       float* gr = a.grow + (size_t)pos * RS;
-      *reinterpret_cast<f32x4*>(gr + sub * 4) = sf_slot_a(dx, dy, s, x);
-      if (sub == 0) *reinterpret_cast<f32x4*>(gr + KE) = f32x4{sf_slot_gw(dy, x), sf_slot_c(dy, x), 0.f, 0.f};
+      *reinterpret_cast<f32x4a8*>(gr + sub * 4) = sf_slot_a(dx, dy, s, x);
+      if (sub == 0) *reinterpret_cast<f32x2a8*>(gr + KE) = f32x2a8{sf_slot_gw(dy, x), sf_slot_c(dy, x)};
     }
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");

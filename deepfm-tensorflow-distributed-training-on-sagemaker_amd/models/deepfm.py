@@ -522,7 +522,7 @@ class NativeDeepFM(GraphRunnerMixin, NativeStateMixin):
         self.dZt = [torch.zeros(n, M, **bf) for n in self.Np]
         self.dX0 = torch.zeros(M, K0p, **bf)            # layer-1 input gradient (bf16)
         # per-slot gradient rows in sorted order (run-sorted steps, tower.hip tw_grow_tile)
-        self.grow = torch.zeros(M * F, K + 4, **f32) if getattr(self, "grow_ok", False) else None
+        self.grow = torch.zeros(M * F, K + 2, **f32) if getattr(self, "grow_ok", False) else None   # {a[K], g_w, c}
         self._grow_inv = None
         if self.batch_norm:
             self.Rb = [torch.zeros(M, n, **f32) for n in self.Np]         # relu output (pre-BN)
