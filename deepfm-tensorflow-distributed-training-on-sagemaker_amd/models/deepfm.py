@@ -282,7 +282,15 @@ class NativeDeepFM(GraphRunnerMixin, NativeStateMixin):
             self.tv = torch.zeros(self.R, K, **f32)
             self.tw = torch.zeros(self.R, **f32)
         self.p = torch.zeros(self.P, **f32)
-        self.g = torch.zeros(self.P, **f32)
+        # multi-rank fused exchange: the dense gradients are all-gathered IN PLACE (RCCL then
+        # skips the own block's copy -- a 5.3 us copy kernel per step on the 1-rank proxy,
+        # profiles/r4i_px_kernels.md): this rank's gradient buffer is its slot of the gather buffer
+        if self.exchange:
+            self.g_gather = torch.zeros(self.world * self.P, **f32)
+            self.g = self.g_gather[self.rank * self.P:(self.rank + 1) * self.P]
+        else:
+            self.g_gather = None
+            self.g = torch.zeros(self.P, **f32)
         self.step = torch.zeros(1, dtype=torch.int64, device=dev)
         self._done_ctr = torch.zeros(1, dtype=torch.int32, device=dev)   # dense_opt block counter
         self._host_step = 0

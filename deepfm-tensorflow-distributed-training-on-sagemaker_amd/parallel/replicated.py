@@ -142,8 +142,8 @@ class ReplicatedExchange:
         ops = [(KN.COMM_ALLGATHER, send_ids, self.g_ids, self.C * 4),
                (KN.COMM_ALLGATHER, self.send_g, self.g_rows, self.C * self.RW * 4)]
         if wgfin is not None:
-            if self.dense_recv is None:
-                self.dense_recv = torch.zeros(self.N * m.P, dtype=torch.float32, device=m.device)
+            if self.dense_recv is None:      # (m.g is this rank's slot of it: an in-place gather)
+                self.dense_recv = m.g_gather
             ops.append((KN.COMM_ALLGATHER, m.g[: m.P], self.dense_recv, m.P * 4))
             dense.g, dense.nsum = self.dense_recv.data_ptr(), self.N
         elif dense_ar is not None:
