@@ -187,6 +187,10 @@ def main():
     ap.add_argument("--embedding_mode", default="auto")
     ap.add_argument("--mlp_dtype", default="bf16", choices=["bf16", "fp8"],
                     help="deep-tower forward GEMM operands (fp8 = OCP e4m3 MFMA, config #5)")
+    ap.add_argument("--exchange_rows", default="bf16", choices=["fp32", "bf16"],
+                    help="row-sharded exchange (N > 1): the served rows' v in the compute dtype "
+                         "(bf16, half the G1 bytes over xGMI; owners keep fp32 master rows and "
+                         "Adam slots) or fp32 (the library default: bitwise the one-GPU reads)")
     ap.add_argument("--emb_dtype", default="fp32", choices=["fp32", "bf16"],
                     help="fm_v rows + optimizer slots (bf16 = mixed-precision embeddings, config #5)")
     ap.add_argument("--pool", type=int, default=128,
@@ -267,7 +271,7 @@ def main():
                          learning_rate=5e-4, optimizer=args.optimizer,
                          sparse_update=args.sparse_update, seed=1234, batch_size=B, device=dev,
                          comm=comm, field_ranges=synth.field_ranges(), mlp_dtype=args.mlp_dtype,
-                         emb_dtype=args.emb_dtype)
+                         emb_dtype=args.emb_dtype, exchange_rows=args.exchange_rows)
     _progress()
     if args.field_major_ids:
         # ids stored field-major ([F, B] storage, [B, F] view, the layout the input pipeline's
@@ -431,6 +435,9 @@ def main():
             sb = x.step_bytes(G if use_graph else 0)
             out["comm_bytes_per_step"] = sb["sent"]
             out["comm_bytes_moved_per_step"] = sb["moved"]
+            out["config"]["exchange_overlap"] = (
+                "dense all-reduce beside the sparse backward (HIPFM_SH_OVERLAP=1)"
+                if model._last_plan.overlap_dense else "off (one queue: dense gradient all-gathered with the rows)")
             if model.shx is not None:
                 out["config"]["exchange_rows"] = (
                     f"served {'bf16 v + fp32 w' if model.shx.rbf16 else 'fp32 v + w'} ({model.shx.RWS * 4} B), "

@@ -59,6 +59,8 @@ _SFWG = flag("HIPFM_SFWG")
 _RUN_SORT = flag("HIPFM_RUN_SORT")
 # row-sharded lazy step: dense optimizer inside the owner update's launch
 _SH_APPLY_DENSE = flag("HIPFM_SH_APPLY_DENSE")
+# multi-rank lazy step: the dense all-reduce overlapped with the sparse backward (graph branch)
+_SH_OVERLAP = flag("HIPFM_SH_OVERLAP")
 # run-sorted single-GPU steps: the tower writes sorted per-slot gradient rows (0: the sparse launch
 # gathers vals / dlogit / S / dX0 per slot)
 _GROW = knob("HIPFM_GROW")     # 0 off | 1 rows at their sorted positions | 2 rows in slot order
@@ -76,7 +78,7 @@ def step_knobs() -> StepKnobs:
     return StepKnobs(sort_side_stream=_SORT_SIDE_STREAM, sparse_impl=_SPARSE_IMPL,
                      wgfin=_WGFIN, sfwg=_SFWG, sh_apply_dense=_SH_APPLY_DENSE,
                      sweep_mode=_SWEEP_MODE, run_sort=_RUN_SORT,
-                     shard_pipeline=_SHARD_PIPELINE)
+                     shard_pipeline=_SHARD_PIPELINE, sh_overlap=_SH_OVERLAP)
 
 
 def check_field_ranges(ranges, F: int, V: int) -> List[Tuple[int, int]]:
@@ -1247,7 +1249,8 @@ class NativeDeepFM(GraphRunnerMixin, NativeStateMixin):
                               dense=self._sh_dense_args() if self._sp.sh_apply_dense else None,
                               join=self._sh_join,
                               wgfin=self._wgfin_args(False) if self._sp.xfuse else None,
-                              dense_ar=self.g if self._sp.exchange_allreduce else None)
+                              dense_ar=self.g if self._sp.exchange_allreduce else None,
+                              overlap=self._dense_grads if self._sp.overlap_dense else None)
             return None
         if not presorted:
             self._sort_slots(B)
@@ -1255,7 +1258,8 @@ class NativeDeepFM(GraphRunnerMixin, NativeStateMixin):
             self.rpx.backward(B, dense=self._sh_dense_args() if self._sp.sh_apply_dense else None,
                               join=self._sh_join,
                               wgfin=self._wgfin_args(False) if self._sp.xfuse else None,
-                              dense_ar=self.g if self._sp.exchange_allreduce else None)
+                              dense_ar=self.g if self._sp.exchange_allreduce else None,
+                              overlap=self._dense_grads if self._sp.overlap_dense else None)
             return None
         if self._sp.sfwg:
             KN.sparse_wgfin(self.K, self.opt_id, self.sf_args(n), self._wgfin_args(True), self.sfwg_done,

@@ -43,6 +43,7 @@ class StepKnobs:
     # multi-step execution (models/runner.py)
     run_sort: bool = True            # HIPFM_RUN_SORT: a run's batches sorted / routed up front
     shard_pipeline: bool = True      # HIPFM_SHARD_PIPELINE: next batches' routing prefetched
+    sh_overlap: bool = False         # HIPFM_SH_OVERLAP: the dense all-reduce beside the sparse backward
 
 
 @dataclass(frozen=True)
@@ -94,6 +95,9 @@ class StepPlan:
     w8_after_owner: bool = False   # fp8: ... after the owner launch's dense optimizer
     grow_rows: bool = False        # run-sorted sfwg step: the tower writes each slot's gradient row
                                    # to its sorted position; the sparse launch streams them
+    overlap_dense: bool = False    # multi-rank lazy step: the dense gradient (its own wgfin launch
+                                   # after the tower) is all-reduced on the main stream WHILE the
+                                   # sparse backward runs on a graph branch
 
 
 IDLE = StepPlan()
@@ -134,12 +138,17 @@ def plan_step(mode: ModeSpec, kn: StepKnobs, B: int, sort_plan: Optional[Tuple],
     # backward's launch and travels with the gradient rows (all-gather, summed in rank order by
     # the owner launch): no comm stream, no all-reduce, no cross-stream joins
     owner_lazy = mode.lazy or mode.tf1x          # the owner launch applies the rows lazily
+    # overlap: the dense gradient leaves the sparse launch (its own wgfin launch, gradient only,
+    # right after the tower) so its all-reduce (G2a) runs on the main stream while the sparse
+    # backward runs on a branch; the gradient rows follow in G2b after the join
+    ovl = (kn.sh_overlap and mode.native_exchange and mode.lazy and mode.fused and kn.wgfin and
+           kn.sh_apply_dense)
     xfuse = (mode.native_exchange and owner_lazy and kn.wgfin and mode.fused and
-             kn.sh_apply_dense and mode.wgfin_fits)
+             kn.sh_apply_dense and mode.wgfin_fits and not ovl)
     # fused tower, multi-rank: the weight gradients only feed the dense optimizer, so they run on
     # their own branch beside the sparse exchange (0.210 -> 0.199 ms); on one GPU a concurrent
     # wgrad slows the sparse backward more than it saves (0.156 -> 0.161 ms)
-    split = mode.fused and not xfuse and mode.exchange
+    split = mode.fused and not xfuse and mode.exchange and not ovl
     # one GPU, lazy rows: the dense optimizer needs only the finished dense gradient, so it runs
     # before the sparse backward (inside the gap a join costs anyway); with the fused tower it
     # rides on the finalize launch, and with wgfin inside the sparse backward's launch (sfwg)
@@ -157,8 +166,9 @@ def plan_step(mode: ModeSpec, kn: StepKnobs, B: int, sort_plan: Optional[Tuple],
         prefetch_next=prefetch, join_sort=fork,
         tf1_merged=merged, tf1_branch=tf1 and not merged,
         tower_stamp=run and tf1 and mode.fused and mode.gather_fused,
-        defer_wgrad=split or sfwg or xfuse, dense_branch=split, dense_early=early, fuse_opt=fuse_opt,
+        defer_wgrad=split or sfwg or xfuse or ovl, dense_branch=split, dense_early=early, fuse_opt=fuse_opt,
         sfwg=sfwg, dense_opt_after=not sh_dense and not early,
         xfuse=xfuse, exchange_allreduce=ex_ar, sh_apply_dense=sh_dense,
         w8_after_fin=mode.fp8 and fuse_opt and not kn.wgfin, w8_after_owner=mode.fp8 and sh_dense,
-        grow_rows=mode.grow_ok and ((run and sfwg) or (routed_run and xfuse and mode.row_sharded)))
+        grow_rows=mode.grow_ok and ((run and sfwg) or (routed_run and xfuse and mode.row_sharded)),
+        overlap_dense=ovl)

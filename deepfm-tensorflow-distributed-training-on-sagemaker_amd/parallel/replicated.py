@@ -33,6 +33,7 @@ import torch
 
 from ..ops import kernels as KN
 from ..ops._lib import ShApplyArgs, ShTable
+from .sharded import overlap_branch
 
 
 def estimate_unique_capacity(id_batches: Iterable[torch.Tensor], slack: float = 1.05, pad: int = 256) -> int:
@@ -117,7 +118,7 @@ class ReplicatedExchange:
         """Unique rows + gradient-row positions of every batch of the run (three launches)."""
         KN.sh_route_run(d, G, n, 1, self.C, self.err, self.C, self.m.F, 0)
 
-    def backward(self, B: int, dense=None, join=None, wgfin=None, dense_ar=None):
+    def backward(self, B: int, dense=None, join=None, wgfin=None, dense_ar=None, overlap=None):
         """Sorted slots (m.sorted_keys / m.perm) -> unique gradient rows -> all-gather -> rank-
         ordered update of every rank's replica.  ``wgfin`` / ``dense`` / ``join`` / ``dense_ar`` as
         in ``FixedCapacityExchange.backward``."""
@@ -133,11 +134,25 @@ class ReplicatedExchange:
         A = m.sf_args(n)
         A.sid, A.upos, A.gout = sid.data_ptr(), upos.data_ptr(), self.send_g.data_ptr()
         A.v_by_key = 1                      # V rows from the local replica, by id
-        if wgfin is not None:
+        if overlap is not None:             # (HIPFM_SH_OVERLAP: see FixedCapacityExchange.backward)
+            if dense_ar is None or wgfin is not None:
+                raise RuntimeError("overlapped exchange: the dense gradient is all-reduced on its own")
+            main = torch.cuda.current_stream(m.device)
+            side = overlap_branch(self, m.device)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                KN.sparse_fused(m.K, KN.SF_EXCHANGE, m.opt_id, A)
+            overlap()                        # the dense gradient (wgfin launch) on the main stream
+            if join is not None:
+                join()
+            self._issue([(KN.COMM_ALLREDUCE, dense_ar, dense_ar, dense_ar.numel() * 4)])   # G2a
+            main.wait_stream(side)
+            dense_ar = None
+        elif wgfin is not None:
             KN.sparse_wgfin_x(m.K, A, wgfin)
         else:
             KN.sparse_fused(m.K, KN.SF_EXCHANGE, m.opt_id, A)
-        if join is not None:
+        if join is not None and overlap is None:
             join()
         ops = [(KN.COMM_ALLGATHER, send_ids, self.g_ids, self.C * 4),
                (KN.COMM_ALLGATHER, self.send_g, self.g_rows, self.C * self.RW * 4)]

@@ -63,6 +63,15 @@ _ROUTE2 = flag("HIPFM_SH_ROUTE2")
 _SERVE_SITE = knob("HIPFM_SERVE_SITE")
 
 
+def overlap_branch(owner, device) -> "torch.cuda.Stream":
+    """The graph branch an exchange runs its sparse backward on while the main stream carries the
+    dense all-reduce (HIPFM_SH_OVERLAP); one per exchange object, created on first use."""
+    st = getattr(owner, "_ovl_stream", None)
+    if st is None:
+        st = owner._ovl_stream = torch.cuda.Stream(device)
+    return st
+
+
 def estimate_capacity(id_batches: Iterable[torch.Tensor], world: int, slack: float = 1.25,
                       pad: int = 256) -> int:
     """Per-peer capacity from sample batches: max over batches and owners of the number of
@@ -520,14 +529,20 @@ class FixedCapacityExchange:
             return self.rows_in.view(torch.bfloat16)[:, :K], self.rows_in[:, K // 2]
         return self.rows_in[:, :K], self.rows_in[:, K]
 
-    def backward(self, plan: ShPlan, B: int, dense=None, join=None, wgfin=None, dense_ar=None):
+    def backward(self, plan: ShPlan, B: int, dense=None, join=None, wgfin=None, dense_ar=None,
+                 overlap=None):
         """Per-unique gradient rows -> owners -> rank-ordered sum + row update on the owner.
         ``wgfin`` (WgFinArgs): the fused tower's dense gradient is computed inside the sparse
         backward's launch and all-gathered with the gradient rows (the owner launch sums the N
         rank gradients in rank order); else ``dense_ar`` (the flat dense gradient) is all-reduced
         in the same group, after ``join()`` made the main stream wait for its producer.
         ``dense`` (ShDenseArgs, lazy rows): the dense optimizer runs in the owner update's launch.
-        The next batch's ids, when routed during this step, travel in the same group (G2)."""
+        The next batch's ids, when routed during this step, travel in the same group (G2).
+        ``overlap`` (HIPFM_SH_OVERLAP; the callable that enqueues the dense gradient): the sparse
+        backward forks onto a graph branch right after the tower, the main stream computes the dense
+        gradient (``overlap()``) and all-reduces ``dense_ar`` (G2a) beside it, and the gradient rows
+        follow after the join (G2b) -- two groups, still issued on the main stream in a host-fixed
+        order."""
         m = self.m
         rs = self._rs(plan)
         n = B * m.F
@@ -538,12 +553,25 @@ class FixedCapacityExchange:
         A.ldv = A.ldw = self.RWS
         A.vbf16 = int(self.rbf16)            # (MODE 2 reads v from the received rows)
         A.sid, A.upos, A.gout = rs.sid_incl.data_ptr(), rs.upos.data_ptr(), self.send_g.data_ptr()
-        if wgfin is not None:
+        if overlap is not None:
+            if dense_ar is None or wgfin is not None:
+                raise RuntimeError("overlapped exchange: the dense gradient is all-reduced on its own")
+            side = overlap_branch(self, m.device)
+            side.wait_stream(self._main)
+            with torch.cuda.stream(side):
+                KN.sparse_fused(m.K, KN.SF_EXCHANGE, m.opt_id, A)
+            overlap()                        # the dense gradient (wgfin launch) on the main stream
+            if join is not None:
+                join()
+            self._issue([(KN.COMM_ALLREDUCE, dense_ar, dense_ar, dense_ar.numel() * 4)])   # G2a
+            self._main.wait_stream(side)
+            dense_ar = None
+        elif wgfin is not None:
             sv, self.x_serve = self.x_serve, None
             KN.sparse_wgfin_x(m.K, A, wgfin, serve=sv)
         else:
             KN.sparse_fused(m.K, KN.SF_EXCHANGE, m.opt_id, A)
-        if join is not None:
+        if join is not None and overlap is None:
             join()
         ops = [(KN.COMM_A2A, self.send_g, self.recv_g, self.C * self.RWG * 4)]
         if wgfin is not None:

@@ -47,6 +47,10 @@ KNOBS: Dict[str, Knob] = {
                            "oracle and the bench ladder's second rung)"),
     "HIPFM_SH_APPLY_DENSE": Knob("1", "variant", "row-sharded step: dense optimizer in the owner "
                                  "update's launch"),
+    "HIPFM_SH_OVERLAP": Knob("0", "variant", "multi-rank lazy step: the dense gradient in its own "
+                             "launch after the tower, all-reduced on the main stream while the sparse "
+                             "backward runs on a graph branch (1), instead of all-gathered with the "
+                             "gradient rows after it (0: one queue, no join; the 1-rank proxy's best)"),
     "HIPFM_SH_ROUTE2": Knob("1", "variant", "two-launch routing (0: segments + bucket kernels, oracle)"),
     "HIPFM_GROW": Knob("1", "variant", "run-sorted steps: the tower writes per-slot gradient rows, 1 at "
                        "their sorted positions (streamed), 2 in slot order (gathered through perm); 0: the "

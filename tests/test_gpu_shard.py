@@ -291,6 +291,65 @@ def test_run_routing_matches_global_batch(N, update, steps):
         assert t[2 + 2 * j][0] == (KN.COMM_A2A, C * RWG * 4)      # G2: gradient rows first
 
 
+@pytest.mark.parametrize("N,run,sharded", [(2, True, True), (4, True, True), (3, False, True), (3, False, False)])
+def test_overlapped_exchange_matches_default(monkeypatch, N, run, sharded):
+    """HIPFM_SH_OVERLAP: the dense gradient in its own launch after the tower,
+    all-reduced on the main stream (G2a) while the sparse backward runs on a graph branch, the
+    gradient rows after the join (G2b).  Same parameters as the default exchange (all-gathered
+    dense gradient summed in rank order by the owner launch) to fp32 reassociation, identical on
+    every rank, one G2a all-reduce + one G2b group per step, identical sequences on every rank."""
+    from hipfm.ops import kernels as KN
+    import hipfm.models.deepfm as D
+    synth = make_synth("criteo_kaggle", seed=6)
+    F, K, layers, keep, B, steps = synth.F, 8, [64, 32], [0.5, 0.5], 512, 3
+    V = synth.feature_size
+    params = init_params(V, F, K, layers, False, seed=8)
+    data = [synth.batch(N * B, step=s, device=DEV, id_dtype=torch.int32) for s in range(steps)]
+    batches = [[(ids[r * B:(r + 1) * B].contiguous(), vals[r * B:(r + 1) * B].contiguous(),
+                 lab[r * B:(r + 1) * B].contiguous()) for ids, vals, lab in data] for r in range(N)]
+    monkeypatch.setattr(D, "_RUN_SORT", run)
+    outs = []
+    for ovl in (False, True):
+        monkeypatch.setattr(D, "_SH_OVERLAP", ovl)
+        hub = _Hub(N)
+        models = []
+        for r in range(N):
+            m = NativeDeepFM(V, F, K, layers, keep, sparse_update="lazy", learning_rate=1e-3, batch_size=B,
+                             device=DEV, init=False, comm=MeshComm(hub, r, sharded=sharded),
+                             field_ranges=synth.field_ranges())
+            m.load_tf_params(params)
+            x = m.shx if sharded else m.rpx
+            x.trace = []
+            models.append(m)
+        if run:
+            _run_ranks_steps(models, batches)
+        else:
+            _run_ranks(models, batches, prefetch=2)
+        torch.cuda.synchronize()
+        for m in models:
+            m.check_errors()
+            assert m._last_plan.overlap_dense == ovl
+            assert torch.equal(m.p, models[0].p)
+            assert sharded or torch.equal(m.tv, models[0].tv)       # (replicas: bitwise equal)
+        x = [(m.shx if sharded else m.rpx) for m in models]
+        for t in x[1:]:
+            assert t.trace == x[0].trace
+        ar = [g for g in x[0].trace if g == ((KN.COMM_ALLREDUCE, models[0].P * 4),)]
+        assert len(ar) == (steps if ovl else 0)
+        m0 = models[0]
+        if sharded:                       # the whole table, reassembled from the row shards
+            full_v = torch.zeros(V, K, device=DEV)
+            full_w = torch.zeros(V, device=DEV)
+            for r, m in enumerate(models):
+                rows = full_v[r::N].shape[0]
+                full_v[r::N], full_w[r::N] = m.tv[:rows], m.tw[:rows]
+        else:
+            full_v, full_w = m0.tv, m0.tw
+        outs.append((full_v, full_w, m0.p))
+    for u, v in zip(*outs):
+        assert (u - v).abs().max().item() <= 2e-6 * max(1e-3, u.abs().max().item())
+
+
 @pytest.mark.parametrize("update,depth", [("lazy", 1), ("tf1_dense", 1), ("lazy", 2)])
 def test_collective_sequence_identical_across_ranks(update, depth):
     """Deadlock freedom by construction (parallel/sharded.py): every collective of a step is a

@@ -74,6 +74,20 @@ def test_native_exchange_steps():
     assert not plan_step(ROW_SHARDED, StepKnobs(), 16384, INLINE, tf1=False).fork_sort
 
 
+def test_overlapped_exchange_step():
+    """HIPFM_SH_OVERLAP: the dense gradient leaves the sparse launch (deferred past the tower, then
+    its own wgfin launch) and is all-reduced while the sparse backward runs on a branch; the
+    owner launch keeps the dense optimizer.  tf1_dense exchange steps keep their plan."""
+    for m in (ROW_SHARDED, REPLICATED):
+        p = plan_step(m, StepKnobs(sh_overlap=True), 16384, None, tf1=False)
+        assert p.overlap_dense and p.exchange_allreduce and p.sh_apply_dense and p.defer_wgrad
+        assert not (p.xfuse or p.dense_branch or p.dense_early or p.sfwg or p.grow_rows)
+        tf1 = plan_step(mode(**{**m.__dict__, "lazy": False, "lazy_rows": False}), StepKnobs(sh_overlap=True),
+                        16384, None, tf1=False)
+        assert not tf1.overlap_dense
+    assert not plan_step(ONE_GPU, StepKnobs(sh_overlap=True), 16384, RUN, tf1=False).overlap_dense
+
+
 def test_per_layer_tower_and_fp8_quantize_sites():
     p = plan_step(PER_LAYER, StepKnobs(), 4096, INLINE, tf1=False)
     assert p.dense_early and not p.fuse_opt and not p.sfwg and not p.defer_wgrad
@@ -105,8 +119,9 @@ def _knob_sets():
     bools = [True, False]
     for (sss, wg, sf, shd, impl, sw, rs, pipe) in itertools.product(
             bools, bools, bools, bools, ("fused", "seg"), ("auto", "merged", "branch"), bools, bools):
-        yield StepKnobs(sort_side_stream=sss, wgfin=wg, sfwg=sf, sh_apply_dense=shd, sparse_impl=impl,
-                        sweep_mode=sw, run_sort=rs, shard_pipeline=pipe)
+        for ovl in ((False, True) if pipe else (False,)):
+            yield StepKnobs(sort_side_stream=sss, wgfin=wg, sfwg=sf, sh_apply_dense=shd, sparse_impl=impl,
+                            sweep_mode=sw, run_sort=rs, shard_pipeline=pipe, sh_overlap=ovl)
 
 
 def test_plan_invariants_over_the_mode_matrix():
@@ -129,7 +144,9 @@ def test_plan_invariants_over_the_mode_matrix():
                             continue
                         n += 1
                         assert sum(dense_opt_sites(p)) == 1, (m, kn, B, sp, p)
-                        assert p.defer_wgrad == (p.dense_branch or p.sfwg or p.xfuse)
+                        assert p.defer_wgrad == (p.dense_branch or p.sfwg or p.xfuse or p.overlap_dense)
+                        assert not p.overlap_dense or (m.native_exchange and m.lazy and p.exchange_allreduce
+                                                       and p.sh_apply_dense and not p.xfuse)
                         assert not p.sfwg or (p.fuse_opt and p.dense_early and not m.exchange)
                         assert not p.fuse_opt or (m.fused and p.dense_early)
                         assert not p.tf1_merged or p.sfwg
