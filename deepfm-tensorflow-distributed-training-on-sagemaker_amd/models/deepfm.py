@@ -69,8 +69,8 @@ _TF1_SPLIT = flag("HIPFM_TF1_SPLIT")
 _XROWS = knob("HIPFM_XROWS")
 _DX0_SPLIT = knob("HIPFM_DX0_SPLIT")      # auto | 1 | 0 (tower.hip tower_dx0_kernel)
 _SWEEP_MODE = knob("HIPFM_SWEEP_MODE")      # auto | merged | branch
-_SWEEP_MBLK = int(knob("HIPFM_SWEEP_MBLK"))  # merged-mode sweep workgroups: 512 0.191, 1024 0.179, 2048 0.156, 3072 0.156, 6144 0.172 ms
-_SWEEP_WG = int(knob("HIPFM_SWEEP_WG"))   # 128: 0.178, 256: 0.160, 512: 0.179 ms
+_SWEEP_MBLK = 2048   # merged-mode sweep workgroups: 512 0.191, 1024 0.179, 2048 0.156, 3072 0.156, 6144 0.172 ms
+_SWEEP_WG = 256      # branch sweep workgroups: 128: 0.178, 256: 0.160, 512: 0.179 ms
 
 
 def step_knobs() -> StepKnobs:
@@ -550,7 +550,7 @@ class NativeDeepFM(GraphRunnerMixin, NativeStateMixin):
         for i in range(len(self.layers)):
             Mg, Ng, Kd = self.Np[i], self.Kp[i], M
             if self.fused:
-                s = int(knob("HIPFM_WG_SPLIT"))
+                s = 32          # per-layer weight-gradient split-K workgroups
                 while s > 1 and (M % (32 * s) or M // s < 128):
                     s //= 2
                 self.wg_cfg.append((None, s))
@@ -736,7 +736,7 @@ class NativeDeepFM(GraphRunnerMixin, NativeStateMixin):
         M, dev = self.M, self.device
         f32 = dict(dtype=torch.float32, device=dev)
         # 4 workgroup splits x 4 waves: same-box A/B 0.1214 (4) / 0.1228 (8) / 0.126 (16) ms/step
-        ns = int(knob("HIPFM_WGFIN_NS"))
+        ns = 4          # wgfin workgroups per output tile (8 / 16: equal or slower)
         while ns > 1 and (M % (ns * 4 * 32) or M // (ns * 4) < 32):
             ns //= 2
         self._wgfin_ns = ns

@@ -14,7 +14,6 @@ import torch
 from . import _lib
 from ._lib import (BnArgs, EpiArgs, HeadArgs, TowerArgs, W8Job, WgJob, OptHyper, RowSumJob, SegApplyArgs, SfArgs, ShApplyArgs, ShadowSeg, SlabJob, check,
                    ptr, stream_handle)
-from ..utils.knobs import knob
 
 EPI_F32, EPI_FWD, EPI_DGRAD, EPI_FWD_EVAL, EPI_RELU_F32 = 0, 1, 2, 3, 4
 OPT_IDS = {"Adam": 0, "Adagrad": 1, "Momentum": 2, "ftrl": 3, "GD": 4}
@@ -123,18 +122,13 @@ def onesweep_sort_ids(keys_in, keys_out, perm_out, n, end_bit, temp, limit: int 
           "onesweep_sort_ids")
 
 
-SORT_IMPL = knob("HIPFM_SORT_IMPL")
-# A/B in tools/bench_sort.py (graph-timed): onesweep 56 us vs LSD 101 us at n = 640K, 30 bits
-
-
 def sort_ids(keys_in, keys_out, vals_tmp, perm_out, n, end_bit, temp, limit: int = 0, err=None):
-    """Stable sort of slot ids -> (sorted keys, slot permutation) (csrc/kernels/radix_sort.hip).
-    ``temp`` must hold radix_temp_bytes(n) bytes; ``vals_tmp`` is unused.  ``limit`` / ``err``:
-    id-range guard of the onesweep sort (see ``onesweep_sort_ids``)."""
-    if SORT_IMPL == "onesweep":
-        onesweep_sort_ids(keys_in, keys_out, perm_out, n, end_bit, temp, limit, err)
-    else:
-        lsd_sort_ids(keys_in, keys_out, perm_out, n, end_bit, temp)
+    """Stable sort of slot ids -> (sorted keys, slot permutation) (csrc/kernels/radix_sort.hip):
+    the onesweep sort (A/B in tools/bench_sort.py, graph-timed: onesweep 56 us vs the LSD sort
+    101 us at n = 640K, 30 bits; ``lsd_sort_ids`` stays for that tool).  ``temp`` must hold
+    radix_temp_bytes(n) bytes; ``vals_tmp`` is unused.  ``limit`` / ``err``: id-range guard of
+    the onesweep sort (see ``onesweep_sort_ids``)."""
+    onesweep_sort_ids(keys_in, keys_out, perm_out, n, end_bit, temp, limit, err)
 
 
 def fs2_chunk_rows() -> int:

@@ -54,13 +54,13 @@ import torch
 
 from ..ops import kernels as KN
 from ..ops._lib import ShApplyArgs, ShTable
-from ..utils.knobs import flag, knob
+from ..utils.knobs import flag
 
 # routing in two launches (sh_route) instead of segments + bucket (7 launches); same outputs
 _ROUTE2 = flag("HIPFM_SH_ROUTE2")
 # run-routed steps: the next step's rows are served by extra workgroups of the sparse backward's
-# launch (sfwg) or of the tower's launch (tower)
-_SERVE_SITE = knob("HIPFM_SERVE_SITE")
+# launch when it is the fused sfwg_x launch (profiles/r4h_px_serve_in_sfwg_kernels.md), else by
+# workgroups of the tower's launch
 
 
 def overlap_branch(owner, device) -> "torch.cuda.Stream":
@@ -500,7 +500,7 @@ class FixedCapacityExchange:
             # the next run step's rows, served by extra workgroups of this step's sparse backward
             # launch (or of its tower launch)
             sv = self._serve_args(self.run_sets[plan.c + 1], ahead=True)
-            if _SERVE_SITE == "sfwg" and m._sp.xfuse:
+            if m._sp.xfuse:
                 self.x_serve = sv
             else:
                 self.tower_serve = sv

@@ -29,8 +29,6 @@ KNOBS: Dict[str, Knob] = {
     # ---- execution-path variants (oracles / fallbacks of the fused defaults)
     "HIPFM_SORT": Knob("auto", "variant", "auto: per-field LDS sort when field id ranges are known; "
                        "global: the 3-pass global radix sort (oracle of the field sort)"),
-    "HIPFM_SORT_IMPL": Knob("onesweep", "variant", "global sort: onesweep (56 us) or lsd (101 us at "
-                            "n = 640K, tools/bench_sort.py)"),
     "HIPFM_SORT_SIDE_STREAM": Knob("1", "variant", "slot sort on a graph side branch (0: inline)"),
     "HIPFM_SPARSE": Knob("fused", "variant", "fused: one-launch sparse backward; seg: fm_bwd_seg + "
                          "seg_apply (oracle, tests/test_gpu_kernels.py)"),
@@ -55,8 +53,6 @@ KNOBS: Dict[str, Knob] = {
     "HIPFM_GROW": Knob("1", "variant", "run-sorted steps: the tower writes per-slot gradient rows, 1 at "
                        "their sorted positions (streamed), 2 in slot order (gathered through perm); 0: the "
                        "sparse launch gathers dX0 / S / vals / dlogit per slot"),
-    "HIPFM_SERVE_SITE": Knob("sfwg", "variant", "run-routed row-sharded step: the next step's rows served "
-                             "by workgroups of the sparse backward's launch (sfwg) or of the tower's (tower)"),
     "HIPFM_DX0_SPLIT": Knob("auto", "variant", "the tower's dX0 phase in a launch of its own: auto (batches "
                             "below 4096 rows, where the tower has < 128 blocks) | 1 | 0"),
     "HIPFM_XROWS": Knob("fp32", "variant", "row-sharded exchange rows: fp32 (48 B at K = 8, bitwise the "
@@ -70,12 +66,6 @@ KNOBS: Dict[str, Knob] = {
     "HIPFM_TABLE_LAYOUT": Knob("record", "variant", "record: one 128-B record per row (v, w, slots); "
                                "split: separate tables"),
     # ---- tuning
-    "HIPFM_SWEEP_MBLK": Knob("2048", "tuning", "merged sweep workgroups (512: 0.191, 1024: 0.179, "
-                             "2048: 0.156, 6144: 0.172 ms/step)"),
-    "HIPFM_SWEEP_WG": Knob("256", "tuning", "branch sweep workgroups (128: 0.178, 256: 0.160, "
-                           "512: 0.179 ms/step)"),
-    "HIPFM_WG_SPLIT": Knob("32", "tuning", "per-layer weight-gradient split-K workgroups"),
-    "HIPFM_WGFIN_NS": Knob("4", "tuning", "wgfin workgroups per output tile (8/16: equal or slower)"),
     "HIPFM_FSORT_PB": Knob(None, "tuning", "field sort MSD partitions per field, log2 (default: 0 on "
                            "one GPU, 2 for the sharded routing)"),
     "HIPFM_FS_MAX_PB": Knob("4", "tuning", "tools/bench_sort.py: field sort partitions per field"),
