@@ -105,6 +105,15 @@ struct TowerArgs {
   // train, no gradient rows): at B = 1024 the tower has 32 blocks on 256 CUs and its dX0 phase
   // (K0p / 32 tiles of W_0 per block) was 15 of its 51 us at K = 32
   int dx0_split;
+  // FM gather + layer 0 split over field slices (small batches: at B = 1024 the tower has 32
+  // blocks on 256 CUs and its gather + layer-0 reduction over 39 fields was 18 of its 36 us):
+  // tower_l0s_kernel, l0s workgroups per 32-row block, each gathers the fields of l0_ks k-steps
+  // (32 columns of E each), stores its E^T columns and writes fp32 partials -- layer 0's pre-
+  // activations l0z [l0s][M][Np0] and the FM sums l0fm [l0s][M][KE + 2] = {S[KE], sum_k Q_k, y_w};
+  // the tower then sums the partials in slice order instead of gathering
+  int l0s, l0_ks;
+  float* l0z;
+  float* l0fm;
 };
 constexpr int TW_GINV = 8;  // inv entries prefetched per thread (32 F / 256 <= 8: F <= 64)
 
@@ -334,6 +343,175 @@ __device__ __forceinline__ void tower_gather(const TowerArgs& a, int row0, bf16*
 }
 
 // ---------------------------------------------------------------------------------------------
+// Split gather + layer 0 (a.l0s slices): block (rb, s) gathers rows [32 rb, 32 rb + 32) x the
+// fields of k-steps [s l0_ks, (s + 1) l0_ks) into an LDS tile, stores those E^T columns (train),
+// and writes its partial FM sums and its partial layer-0 pre-activation tile (one 32 x 32 MFMA
+// tile per wave and column tile, the slice's k-steps in order).  KE divides 32, so a k-step holds
+// whole fields.
+template <int KE>
+__global__ void __launch_bounds__(256) tower_l0s_kernel(TowerArgs a) {
+  extern __shared__ __align__(16) unsigned char tw_lds_raw[];
+  bf16* Xs = reinterpret_cast<bf16*>(tw_lds_raw);
+  constexpr int V4 = KE / 4;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int sl = tid >> 3, q = tid & 7;
+  const int row0 = blockIdx.x * TW_ROWS, s = blockIdx.y, F = a.F;
+  const int T = a.K0p / 32;
+  const int ks0 = s * a.l0_ks, nk = min(a.l0_ks, T - ks0);
+  if (nk <= 0) return;
+  const int c0 = ks0 * 32, ncol = nk * 32, ldx = ncol + 8;
+  const int f_lo = c0 / KE, f_hi = min(F, (c0 + ncol) / KE);
+  const int b = row0 + sl;
+  bf16* xr = Xs + sl * ldx;
+  f32x4 S[V4];
+#pragma unroll
+  for (int j = 0; j < V4; ++j) S[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float Q = 0.f, yw = 0.f;
+  // up to FPS fields per thread per pass, every id, then every row in flight at once
+  constexpr int FPS = KE >= 32 ? 2 : 4;
+  for (int f0 = f_lo + q; f0 < f_hi; f0 += 8 * FPS) {
+    int id[FPS];
+    float x[FPS];
+#pragma unroll
+    for (int t = 0; t < FPS; ++t) {
+      const int f = f0 + 8 * t;
+      id[t] = f < f_hi ? a.idx[a.idx_ld ? (size_t)f * a.idx_ld + b : (size_t)b * F + f] : 0;
+      if (a.id_lim && (unsigned)id[t] >= a.id_lim) id[t] = (int)a.id_lim - 1;
+      x[t] = f < f_hi ? a.vals[(size_t)b * F + f] : 0.f;
+    }
+    f32x4 v[FPS][V4];
+    float w[FPS];
+#pragma unroll
+    for (int t = 0; t < FPS; ++t) {
+      const bool ok = f0 + 8 * t < f_hi;
+      const float* row = a.tv + (size_t)id[t] * a.ldv;
+#pragma unroll
+      for (int j = 0; j < V4; ++j) v[t][j] = ok ? ld_row4(row, 4 * j, a.vbf16) : f32x4{0.f, 0.f, 0.f, 0.f};
+      w[t] = ok ? a.tw[(size_t)id[t] * a.ldw] : 0.f;
+    }
+#pragma unroll
+    for (int t = 0; t < FPS; ++t) {
+      const int f = f0 + 8 * t;
+      if (f >= f_hi) break;
+      yw += w[t] * x[t];
+#pragma unroll
+      for (int j = 0; j < V4; ++j) {
+        const f32x4 e = v[t][j] * x[t];
+        S[j] += e;
+        Q += (e[0] * e[0] + e[1] * e[1]) + (e[2] * e[2] + e[3] * e[3]);
+        bf16x4 eh = {f2bf(e[0]), f2bf(e[1]), f2bf(e[2]), f2bf(e[3])};
+        *reinterpret_cast<bf16x4*>(xr + f * KE - c0 + 4 * j) = eh;
+      }
+    }
+  }
+  for (int c = max(F * KE - c0, 0) + q; c < ncol; c += 8) xr[c] = f2bf(0.f);   // padding columns
+#pragma unroll
+  for (int o = 1; o < 8; o <<= 1) {
+#pragma unroll
+    for (int j = 0; j < V4; ++j)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) S[j][c] += __shfl_xor(S[j][c], o, 64);
+    Q += __shfl_xor(Q, o, 64);
+    yw += __shfl_xor(yw, o, 64);
+  }
+  if (q == 0) {
+    float* fm = a.l0fm + ((size_t)s * a.M + b) * (KE + 2);
+#pragma unroll
+    for (int j = 0; j < V4; ++j) *reinterpret_cast<f32x4*>(fm + 4 * j) = S[j];
+    fm[KE] = Q;
+    fm[KE + 1] = yw;
+  }
+  __syncthreads();
+  if (a.train) store_tile_t(Xs, ldx, ncol, a.Et + (size_t)c0 * a.M, a.M, row0);
+  const int N0 = a.Np[0], cr = (lane >> 4) * 4, cc = lane & 15;
+  for (int ct = wave; ct < N0 / 32; ct += 4) {
+    f32x4 c00 = {0, 0, 0, 0}, c01 = c00, c10 = c00, c11 = c00;
+    mma32<2>(Xs, ldx, a.W[0] + (size_t)ct * 32 * a.K0p + c0, a.K0p, nk, lane, c00, c01, c10, c11);
+    const f32x4 acc[2][2] = {{c00, c01}, {c10, c11}};
+    float* z = a.l0z + ((size_t)s * a.M + row0) * N0 + ct * 32;
+#pragma unroll
+    for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+      for (int tj = 0; tj < 2; ++tj)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) z[(size_t)(ti * 16 + cr + j) * N0 + tj * 16 + cc] = acc[ti][tj][j];
+  }
+}
+
+// The tower's side of the split: y_fm, S (and the grow scratch's S) from the slices' FM partials,
+// summed in slice order (8 threads per row, as the gather's lanes).  Every partial is loaded before
+// the first add (one round trip, not one per slice).
+constexpr int TW_L0S_MAX = 8;
+template <int KE>
+__device__ __forceinline__ void tower_l0s_fm(const TowerArgs& a, int row0, float* s_yfm, float* gS) {
+  constexpr int KQ = (KE + 7) / 8;   // components per thread
+  const int tid = threadIdx.x, sl = tid >> 3, q = tid & 7, b = row0 + sl;
+  float part[TW_L0S_MAX][KQ], pq[TW_L0S_MAX], pw[TW_L0S_MAX];
+#pragma unroll
+  for (int s = 0; s < TW_L0S_MAX; ++s) {
+    const float* fm = a.l0fm + ((size_t)s * a.M + b) * (KE + 2);
+#pragma unroll
+    for (int t = 0; t < KQ; ++t) part[s][t] = (s < a.l0s && q + 8 * t < KE) ? fm[q + 8 * t] : 0.f;
+    pq[s] = (s < a.l0s && q == 0) ? fm[KE] : 0.f;
+    pw[s] = (s < a.l0s && q == 0) ? fm[KE + 1] : 0.f;
+  }
+  float yv = 0.f, Q = 0.f, yw = 0.f;
+#pragma unroll
+  for (int t = 0; t < KQ; ++t) {
+    float sk = 0.f;
+#pragma unroll
+    for (int s = 0; s < TW_L0S_MAX; ++s)
+      if (s < a.l0s) sk += part[s][t];
+    const int k = q + 8 * t;
+    if (k < KE) {
+      yv += sk * sk;
+      if (a.S) a.S[(size_t)b * KE + k] = sk;
+      if (gS) gS[sl * KE + k] = sk;
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < TW_L0S_MAX; ++s)
+    if (s < a.l0s) {
+      Q += pq[s];
+      yw += pw[s];
+    }
+#pragma unroll
+  for (int o = 1; o < 8; o <<= 1) yv += __shfl_xor(yv, o, 64);
+  if (q == 0) s_yfm[sl] = a.fm_bias[0] + yw + 0.5f * (yv - Q);
+}
+
+// one wave's 32 x 32 layer-0 pre-activation tile from the slices' partials, in slice order: the
+// loads of 4 slices (64 registers: the layer-0 B-fragment ring is idle in this mode) per round
+__device__ __forceinline__ void tower_l0s_tile(const TowerArgs& a, int row0, int N, int ct, int lane,
+                                               f32x4& c00, f32x4& c01, f32x4& c10, f32x4& c11) {
+  const int cr = (lane >> 4) * 4, cc = lane & 15;
+  f32x4* cs[2][2] = {{&c00, &c01}, {&c10, &c11}};
+  for (int s0 = 0; s0 < a.l0s; s0 += 4) {
+    float v[4][2][2][4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const float* z = a.l0z + ((size_t)(s0 + u) * a.M + row0) * N + ct * 32;
+#pragma unroll
+      for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+        for (int tj = 0; tj < 2; ++tj)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            v[u][ti][tj][j] = s0 + u < a.l0s ? z[(size_t)(ti * 16 + cr + j) * N + tj * 16 + cc] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (s0 + u < a.l0s)
+#pragma unroll
+        for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+          for (int tj = 0; tj < 2; ++tj)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) (*cs[ti][tj])[j] += v[u][ti][tj][j];
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // bf16 tower body (everything after the serve / stamp workgroup split).  Same math, same outputs,
 // bit for bit, as the generic body below; the difference is WHEN operands arrive: every GEMM
 // tile's weight fragments (and the forward bias, the head's w_out / labels) are loaded one phase
@@ -441,7 +619,7 @@ __device__ __forceinline__ void tw_dx0_tile(const TowerArgs& a, const f32x4 (&ac
 // workgroups (run-routed row-sharded step) keeps the register count low enough for them to
 // co-reside with two tower workgroups per CU (240 registers left them queued behind the tower:
 // 68.7 vs 47.3 us)
-template <int KE, bool LIGHT>
+template <int KE, bool LIGHT, bool L0S = false>
 __device__ __forceinline__ void tower_bf16_body(const TowerArgs& a, bf16* lds, float* s_dl, float* s_loss,
                                                 float* s_yfm) {
   constexpr int TW_NP = LIGHT ? 2 : tw_np(KE);
@@ -486,8 +664,11 @@ __device__ __forceinline__ void tower_bf16_body(const TowerArgs& a, bf16* lds, f
   if constexpr (KE > 0) {
     // (weights primed DURING the gather slowed it more than they saved: its table-row loads
     // compete with them for the same address path)
-    tower_gather<false, KE, (LIGHT && KE >= 32) ? 2 : 0>(a, row0, Xl, ldx, nullptr, 0, s_yfm, nullptr, grow ? gx : nullptr,
-                            grow ? gS : nullptr);
+    if constexpr (L0S)   // gather + layer 0 done by tower_l0s_kernel: sum its FM partials
+      tower_l0s_fm<KE>(a, row0, s_yfm, grow ? gS : nullptr);
+    else
+      tower_gather<false, KE, (LIGHT && KE >= 32) ? 2 : 0>(a, row0, Xl, ldx, nullptr, 0, s_yfm, nullptr,
+                                                           grow ? gx : nullptr, grow ? gS : nullptr);
     __syncthreads();
     TW_ST(1);
   }
@@ -503,8 +684,10 @@ __device__ __forceinline__ void tower_bf16_body(const TowerArgs& a, bf16* lds, f
   const float hlab = hvalid ? a.labels[row0 + hrow] : 0.f;
   const float yfm_g = KE > 0 ? 0.f : a.y_fm[row0 + hrow];
   if constexpr (KE > 0) {
-    if (a.train) store_tile_t(Xl, ldx, a.K0p, a.Et, a.M, row0);
-    prime(0, wave);
+    if constexpr (!L0S) {
+      if (a.train) store_tile_t(Xl, ldx, a.K0p, a.Et, a.M, row0);
+      prime(0, wave);
+    }
     TW_ST(2);
   }
   // ---------------------------------------------------------------- forward
@@ -521,7 +704,9 @@ __device__ __forceinline__ void tower_bf16_body(const TowerArgs& a, bf16* lds, f
     for (int ct = wave; ct < N / 32; ct += 4) {
       f32x4 c00 = {0, 0, 0, 0}, c01 = c00, c10 = c00, c11 = c00;
       float bc[2];
-      if (KE == 0 && i == 0) {
+      if (L0S && i == 0) {   // the slices' partial pre-activations, in slice order
+        tower_l0s_tile(a, row0, N, ct, lane, c00, c01, c10, c11);
+      } else if (KE == 0 && i == 0) {
         mma32<TW_NP>(a.E + (size_t)row0 * a.K0p, a.K0p, a.W[0] + (size_t)ct * 32 * Kp, Kp, Kp / 32, lane, c00,
                      c01, c10, c11);
       } else if (i == 0) {  // layer 0 (the longest reduction): weights primed one tile ahead
@@ -534,7 +719,7 @@ __device__ __forceinline__ void tower_bf16_body(const TowerArgs& a, bf16* lds, f
         // (priming the short layers' weights measured no faster: 2-4 k-steps, one L2 trip)
         mma32<2>(Asrc, lda, a.W[i] + (size_t)ct * 32 * Kp, Kp, Kp / 32, lane, c00, c01, c10, c11);
       }
-      if (KE == 0 || i > 0) {
+      if (KE == 0 || i > 0 || L0S) {
         bc[0] = a.bias[i][ct * 32 + cc];
         bc[1] = a.bias[i][ct * 32 + 16 + cc];
       }
@@ -758,6 +943,19 @@ tower_light_kernel(TowerArgs a) {
   if (tower_aux_wg<KE>(a)) return;
   TW_ST(0);
   tower_bf16_body<KE, true>(a, reinterpret_cast<bf16*>(tw_lds_raw), s_dl, s_loss, s_yfm);
+}
+
+// the tower after tower_l0s_kernel (split gather + layer 0): its own instantiation, so the
+// partial sums' registers never count against the default towers' occupancy
+template <int KE>
+__global__ void __launch_bounds__(256) tower_l0s_tower_kernel(TowerArgs a) {
+  extern __shared__ __align__(16) unsigned char tw_lds_raw[];
+  __shared__ float s_dl[TW_ROWS];
+  __shared__ float s_loss[TW_ROWS];
+  __shared__ float s_yfm[TW_ROWS];
+  if (tower_aux_wg<KE>(a)) return;
+  TW_ST(0);
+  tower_bf16_body<KE, false, true>(a, reinterpret_cast<bf16*>(tw_lds_raw), s_dl, s_loss, s_yfm);
 }
 
 template <bool FP8, int KE, int TW_PF0, int TW_PF1>
@@ -1018,6 +1216,15 @@ __global__ void __launch_bounds__(256) tower_kernel(TowerArgs a) {
 template <bool FP8>
 static int tower_launch(const TowerArgs& a, int KE, hipStream_t st) {
   const dim3 g(a.M / TW_ROWS + (KE > 0 ? a.serve_wgs + a.stamp_wgs : 0)), blk(256);
+  if (!FP8 && a.l0s) {
+    switch (KE) {
+      case 4: hipLaunchKernelGGL((tower_l0s_tower_kernel<4>), g, blk, a.lds_bytes, st, a); return 0;
+      case 8: hipLaunchKernelGGL((tower_l0s_tower_kernel<8>), g, blk, a.lds_bytes, st, a); return 0;
+      case 16: hipLaunchKernelGGL((tower_l0s_tower_kernel<16>), g, blk, a.lds_bytes, st, a); return 0;
+      case 32: hipLaunchKernelGGL((tower_l0s_tower_kernel<32>), g, blk, a.lds_bytes, st, a); return 0;
+      default: return (int)hipErrorInvalidValue;
+    }
+  }
   if (!FP8 && a.serve_wgs > 0) {
     switch (KE) {
       case 4: hipLaunchKernelGGL((tower_light_kernel<4>), g, blk, a.lds_bytes, st, a); return 0;
@@ -1140,6 +1347,7 @@ HFM_API int hfm_tower(const TowerArgs* ap, int KE, hipStream_t st) {
   }
   if (a.dx0_split && (a.fp8 || !a.train || !a.dX0 || !a.dZt[0] || tower_dx0_lds(a, KE) > 64 * 1024))
     return (int)hipErrorInvalidValue;
+  if (a.l0s && (a.fp8 || !KE)) return (int)hipErrorInvalidValue;
   if (a.fp8) {
     if (!KE && (!a.E8 || !a.sE)) return (int)hipErrorInvalidValue;
     for (int i = 0; i < a.nl; ++i)
@@ -1147,6 +1355,21 @@ HFM_API int hfm_tower(const TowerArgs* ap, int KE, hipStream_t st) {
     const int rc = tower_launch<true>(a, KE, st);
     if (rc) return rc;
   } else {
+    if (a.l0s) {
+      if (!(KE == 4 || KE == 8 || KE == 16 || KE == 32) || a.l0s < 2 || a.l0s > TW_L0S_MAX || a.l0_ks < 1 ||
+          !a.l0z || !a.l0fm ||
+          (a.l0s - 1) * a.l0_ks >= a.K0p / 32 || a.l0s * a.l0_ks < a.K0p / 32 || (a.grow && !a.dx0_split) ||
+          a.Np[0] % 32)
+        return (int)hipErrorInvalidValue;
+      const dim3 g(a.M / TW_ROWS, a.l0s), blk(256);
+      const int lb = 2 * TW_ROWS * (a.l0_ks * 32 + 8);
+      switch (KE) {
+        case 4: hipLaunchKernelGGL(tower_l0s_kernel<4>, g, blk, lb, st, a); break;
+        case 8: hipLaunchKernelGGL(tower_l0s_kernel<8>, g, blk, lb, st, a); break;
+        case 16: hipLaunchKernelGGL(tower_l0s_kernel<16>, g, blk, lb, st, a); break;
+        case 32: hipLaunchKernelGGL(tower_l0s_kernel<32>, g, blk, lb, st, a); break;
+      }
+    }
     const int rc = tower_launch<false>(a, KE, st);
     if (rc) return rc;
     if (a.dx0_split) {

@@ -68,6 +68,7 @@ _GROW = knob("HIPFM_GROW")     # 0 off | 1 rows at their sorted positions | 2 ro
 _TF1_SPLIT = flag("HIPFM_TF1_SPLIT")
 _XROWS = knob("HIPFM_XROWS")
 _DX0_SPLIT = knob("HIPFM_DX0_SPLIT")      # auto | 1 | 0 (tower.hip tower_dx0_kernel)
+_L0_SPLIT = knob("HIPFM_L0_SPLIT")        # auto | 0 (tower.hip tower_l0s_kernel)
 _SWEEP_MODE = knob("HIPFM_SWEEP_MODE")      # auto | merged | branch
 _SWEEP_MBLK = 2048   # merged-mode sweep workgroups: 512 0.191, 1024 0.179, 2048 0.156, 3072 0.156, 6144 0.172 ms
 _SWEEP_WG = 256      # branch sweep workgroups: 128: 0.178, 256: 0.160, 512: 0.179 ms
@@ -413,6 +414,16 @@ class NativeDeepFM(GraphRunnerMixin, NativeStateMixin):
                         ((self.K in (4, 8, 16) and self._tower_grow_layout()[1] <= 150 * 1024) or
                          (self.K == 32 and self.dx0_split)))
         self.grow_sorted = _GROW == "1"      # (else slot order: the sparse launch gathers through perm)
+        # the FM gather + layer 0 over ~8 field slices in a launch of their own (tower.hip
+        # tower_l0s_kernel; the batches of the dX0 split: the tower's 32-row blocks are too few
+        # to fill the GPU, and each gathered all F fields and reduced all K0p / 32 k-steps alone)
+        self.l0s = self.l0_ks = 0
+        if (_L0_SPLIT != "0" and self.gather_fused and not self.fp8 and self.K in (4, 8, 16, 32) and
+                self.dx0_split):
+            T = self.K0p // 32
+            ks = max(1, -(-T // 8))
+            if -(-T // ks) >= 2:
+                self.l0s, self.l0_ks = -(-T // ks), ks
         if init:
             if self.V * self.K <= (1 << 24):
                 # small tables: the exact golden initialization (CPU generator, bit-reproducible)
@@ -531,6 +542,9 @@ class NativeDeepFM(GraphRunnerMixin, NativeStateMixin):
         self.dZ = [torch.zeros(M, n, **bf) for n in self.Np]
         self.dZt = [torch.zeros(n, M, **bf) for n in self.Np]
         self.dX0 = torch.zeros(M, K0p, **bf)            # layer-1 input gradient (bf16)
+        if getattr(self, "l0s", 0):                      # split gather + layer 0: fp32 partials
+            self.l0z = torch.zeros(self.l0s, M, self.Np[0], **f32)
+            self.l0fm = torch.zeros(self.l0s, M, K + 2, **f32)
         # per-slot gradient rows in sorted order (run-sorted steps, tower.hip tw_grow_tile)
         self.grow = torch.zeros(M * F, K + 2, **f32) if getattr(self, "grow_ok", False) else None   # {a[K], g_w, c}
         self._grow_inv = None
@@ -869,6 +883,9 @@ class NativeDeepFM(GraphRunnerMixin, NativeStateMixin):
                 a.W8[i], a.sW[i] = self.W8[i].data_ptr(), self.sW[i].data_ptr()
         if train and self.dx0_split:
             a.dx0_split = 1
+        if gather is not None and self.l0s and (a.dx0_split or not grow):
+            a.l0s, a.l0_ks = self.l0s, self.l0_ks
+            a.l0z, a.l0fm = self.l0z.data_ptr(), self.l0fm.data_ptr()
         if grow:
             a.grow, a.inv_ld = self.grow.data_ptr(), B                  # (run-sorted: B == M)
             a.inv = grow_inv.data_ptr() if self.grow_sorted else 0

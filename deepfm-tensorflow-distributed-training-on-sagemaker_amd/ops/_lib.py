@@ -184,7 +184,7 @@ class TowerArgs(C.Structure):
                 ("id_lim", c_uint32), ("vbf16", c_int), ("serve_wgs", c_int), ("sv", ShServeArgs),
                 ("stamp_wgs", c_int), ("stamp_n", c_int), ("stamp_div", c_int), ("stamp_keys", c_void_p),
                 ("stamp_flags", c_void_p), ("grow", c_void_p), ("inv", c_void_p), ("g_off", c_int), ("inv_ld", c_int),
-                ("dx0_split", c_int)]
+                ("dx0_split", c_int), ("l0s", c_int), ("l0_ks", c_int), ("l0z", c_void_p), ("l0fm", c_void_p)]
 
 
 class CommOp(C.Structure):

@@ -55,6 +55,8 @@ KNOBS: Dict[str, Knob] = {
                        "sparse launch gathers dX0 / S / vals / dlogit per slot"),
     "HIPFM_DX0_SPLIT": Knob("auto", "variant", "the tower's dX0 phase in a launch of its own: auto (batches "
                             "below 4096 rows, where the tower has < 128 blocks) | 1 | 0"),
+    "HIPFM_L0_SPLIT": Knob("auto", "variant", "the fused tower's FM gather + layer 0 over ~8 field slices "
+                           "in a launch of their own (auto: with the dX0 split, batches below 4096 rows) | 0"),
     "HIPFM_XROWS": Knob("fp32", "variant", "row-sharded exchange rows: fp32 (48 B at K = 8, bitwise the "
                         "one-GPU reads: the default, numerically the single-GPU step) | bf16 (opt-in: v as "
                         "bf16 + fp32 w, 24 B; fused gather tower; the FM terms then read bf16-rounded v)"),

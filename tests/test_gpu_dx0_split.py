@@ -32,6 +32,7 @@ def test_dx0_split_trains_bitwise_like_the_fused_tower(monkeypatch, preset, K, B
     params = init_params(synth.feature_size, synth.F, K, layers, False, seed=9)
     pool = [synth.batch(B, step=s, device=DEV, id_dtype=torch.int32) for s in range(4)]
     out = []
+    monkeypatch.setattr(D, "_L0_SPLIT", "0")      # (the layer-0 split reassociates: its own test)
     for split in ("1", "0"):
         monkeypatch.setattr(D, "_DX0_SPLIT", split)
         m = NativeDeepFM(synth.feature_size, synth.F, K, layers, [0.5] * 3, batch_size=B, device=DEV,
@@ -56,3 +57,47 @@ def test_dx0_split_trains_bitwise_like_the_fused_tower(monkeypatch, preset, K, B
     for i, (x, y) in enumerate(zip(*out)):
         assert torch.equal(x, y), (i, (x.float() - y.float()).abs().max().item())
     assert multi or out[0][-1].abs().sum().item() > 0          # dX0 was written
+
+
+@pytest.mark.parametrize("preset,K,B", [("reference", 32, 1024), ("criteo_kaggle", 8, 1024),
+                                       ("criteo_kaggle", 16, 2000)])
+def test_layer0_split_matches_the_fused_gather(monkeypatch, preset, K, B):
+    """HIPFM_L0_SPLIT (tower.hip tower_l0s_kernel): the FM gather + layer 0 over ~8 field slices in
+    a launch of their own, the tower summing the slices' fp32 partials in slice order.  The same
+    function as the tower's own gather + layer-0 MFMA chain up to fp32 reassociation: one step's
+    loss, predictions and gradients agree to rounding, and training stays close (Adam eps 1e-2
+    keeps the update continuous in the gradient)."""
+    synth = make_synth(preset, seed=43)
+    layers = [128, 64, 32]
+    params = init_params(synth.feature_size, synth.F, K, layers, False, seed=10)
+    pool = [synth.batch(B, step=s, device=DEV, id_dtype=torch.int32) for s in range(4)]
+    ev = synth.batch(700, step=99, device=DEV, id_dtype=torch.int32)
+    res = []
+    for l0 in ("auto", "0"):
+        monkeypatch.setattr(D, "_L0_SPLIT", l0)
+        m = NativeDeepFM(synth.feature_size, synth.F, K, layers, [0.5] * 3, batch_size=B, device=DEV,
+                         init=False, sparse_update="lazy", field_ranges=synth.field_ranges(), adam_epsilon=1e-2)
+        m.load_tf_params(params)
+        assert (m.l0s > 1) == (l0 == "auto") and m.dx0_split
+        g, _, UG = m.compute_grads(*pool[0])
+        loss1 = m.loss_value(B)
+        p1 = m.prob[:B].clone()
+        for r in range(2):
+            m.train_steps(pool[:2], next_ids=(pool[2][0], pool[3][0]))
+            m.train_steps(pool[2:], next_ids=(pool[0][0], pool[1][0]))
+        pred = m.predict(ev[0], ev[1])
+        torch.cuda.synchronize()
+        m.check_errors()
+        res.append(dict(g=g.clone(), UG=UG.clone(), loss=loss1, p1=p1, tv=m.tv.clone(), tw=m.tw.clone(),
+                        p=m.p.clone(), pred=pred.clone()))
+        del m
+    a, b = res
+    assert abs(a["loss"] - b["loss"]) <= 1e-5
+    assert (a["p1"] - b["p1"]).abs().max().item() <= 2e-5
+    assert (a["g"] - b["g"]).abs().max().item() <= 1e-2 * b["g"].abs().max().item()
+    assert (a["UG"] - b["UG"]).abs().max().item() <= 1e-2 * b["UG"].abs().max().item()
+    for k in ("tv", "tw", "p"):
+        d = (a[k] - b[k]).abs()
+        scale = b[k].abs().max().item()
+        assert (d <= 1e-3 * scale).float().mean().item() >= 0.999 and d.max().item() <= 2e-2 * scale, k
+    assert (a["pred"] - b["pred"]).abs().max().item() <= 2e-3
