@@ -33,7 +33,7 @@ import torch
 
 from ..ops import kernels as KN
 from ..ops._lib import ShApplyArgs, ShTable
-from .sharded import overlap_branch
+from .sharded import dense_allreduce, overlap_branch
 
 
 def estimate_unique_capacity(id_batches: Iterable[torch.Tensor], slack: float = 1.05, pad: int = 256) -> int:
@@ -156,7 +156,9 @@ class ReplicatedExchange:
             join()
         ops = [(KN.COMM_ALLGATHER, send_ids, self.g_ids, self.C * 4),
                (KN.COMM_ALLGATHER, self.send_g, self.g_rows, self.C * self.RW * 4)]
-        if wgfin is not None:
+        if wgfin is not None and dense_allreduce(self.N):
+            ops.append((KN.COMM_ALLREDUCE, m.g[: m.P], m.g[: m.P], m.P * 4))   # dense.g: m.g, nsum 0
+        elif wgfin is not None:
             if self.dense_recv is None:      # (m.g is this rank's slot of it: an in-place gather)
                 self.dense_recv = m.g_gather
             ops.append((KN.COMM_ALLGATHER, m.g[: m.P], self.dense_recv, m.P * 4))
@@ -191,8 +193,13 @@ class ReplicatedExchange:
     def step_bytes(self, run_steps: int = 1) -> dict:
         """Modelled traffic of one step per rank (see FixedCapacityExchange.step_bytes): this rank's
         ids + gradient-row block + dense gradient, all-gathered to the N - 1 other ranks."""
-        blk = self.C * 4 + self.C * self.RW * 4 + self.m.P * 4
-        return {"sent": int((self.N - 1) * blk), "moved": int(self.N * blk)}
+        N, P = self.N, self.m.P
+        blk = self.C * 4 + self.C * self.RW * 4
+        if dense_allreduce(N):
+            ds, dm = 2 * (N - 1) * P * 4 / N, 2 * P * 4
+        else:
+            ds, dm = (N - 1) * P * 4, N * P * 4
+        return {"sent": int((N - 1) * blk + ds), "moved": int(N * blk + dm)}
 
     def reset_table(self):
         self.req_key.zero_()

@@ -54,13 +54,24 @@ import torch
 
 from ..ops import kernels as KN
 from ..ops._lib import ShApplyArgs, ShTable
-from ..utils.knobs import flag
+from ..utils.knobs import flag, knob
 
 # routing in two launches (sh_route) instead of segments + bucket (7 launches); same outputs
 _ROUTE2 = flag("HIPFM_SH_ROUTE2")
 # run-routed steps: the next step's rows are served by extra workgroups of the sparse backward's
 # launch when it is the fused sfwg_x launch (profiles/r4h_px_serve_in_sfwg_kernels.md), else by
 # workgroups of the tower's launch
+
+
+_DENSE_XCHG = knob("HIPFM_DENSE_XCHG")
+
+
+def dense_allreduce(world: int) -> bool:
+    """The fused exchange's dense gradient: all-reduced (ring: 2 (N-1)/N x P floats per rank) or
+    all-gathered and summed in rank order by the owner launch (N x P floats received, no RCCL
+    reduction, in place).  auto: all-reduce from 4 ranks, where the all-gather's 7 x 0.68 MB at
+    N = 8 outweighs the all-reduce's extra ring steps; the 1-rank proxy and N = 2 gather."""
+    return _DENSE_XCHG == "allreduce" or (_DENSE_XCHG == "auto" and world >= 4)
 
 
 def overlap_branch(owner, device) -> "torch.cuda.Stream":
@@ -574,7 +585,9 @@ class FixedCapacityExchange:
         if join is not None and overlap is None:
             join()
         ops = [(KN.COMM_A2A, self.send_g, self.recv_g, self.C * self.RWG * 4)]
-        if wgfin is not None:
+        if wgfin is not None and dense_allreduce(self.N):
+            ops.append((KN.COMM_ALLREDUCE, m.g[: m.P], m.g[: m.P], m.P * 4))   # dense.g: m.g, nsum 0
+        elif wgfin is not None:
             if self.dense_recv is None:      # (m.g is this rank's slot of it: an in-place gather)
                 self.dense_recv = m.g_gather
             ops.append((KN.COMM_ALLGATHER, m.g[: m.P], self.dense_recv, m.P * 4))
@@ -629,8 +642,11 @@ class FixedCapacityExchange:
         1-rank proxy copies).  Fixed-capacity blocks: independent of the batch's contents."""
         N, C, P = self.N, self.C, self.m.P
         per_peer = C * (self.RWS + self.RWG) * 4 + C * 4 / max(1, run_steps) * (1 if run_steps else 0)
-        dense = P * 4
-        return {"sent": int((N - 1) * (per_peer + dense)), "moved": int(N * (per_peer + dense))}
+        if dense_allreduce(N):           # ring all-reduce: 2 (N - 1) / N of the buffer out
+            ds, dm = 2 * (N - 1) * P * 4 / N, 2 * P * 4
+        else:                            # all-gather: the own block to every other rank
+            ds, dm = (N - 1) * P * 4, N * P * 4
+        return {"sent": int((N - 1) * per_peer + ds), "moved": int(N * per_peer + dm)}
 
     def reset_table(self):
         """The tables' stamps are step numbers: clear them when the step counter is rewritten."""

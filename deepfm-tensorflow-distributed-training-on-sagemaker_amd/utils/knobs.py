@@ -45,6 +45,9 @@ KNOBS: Dict[str, Knob] = {
                            "oracle and the bench ladder's second rung)"),
     "HIPFM_SH_APPLY_DENSE": Knob("1", "variant", "row-sharded step: dense optimizer in the owner "
                                  "update's launch"),
+    "HIPFM_DENSE_XCHG": Knob("auto", "variant", "fused multi-rank exchange: the dense gradient all-gathered "
+                             "and summed in rank order by the owner launch (allgather) or all-reduced "
+                             "(allreduce); auto: all-reduce from 4 ranks"),
     "HIPFM_SH_OVERLAP": Knob("0", "variant", "multi-rank lazy step: the dense gradient in its own "
                              "launch after the tower, all-reduced on the main stream while the sparse "
                              "backward runs on a graph branch (1), instead of all-gathered with the "

@@ -350,6 +350,47 @@ def test_overlapped_exchange_matches_default(monkeypatch, N, run, sharded):
         assert (u - v).abs().max().item() <= 2e-6 * max(1e-3, u.abs().max().item())
 
 
+@pytest.mark.parametrize("sharded", [True, False])
+def test_dense_allreduce_equals_rank_order_gather(monkeypatch, sharded):
+    """HIPFM_DENSE_XCHG: the fused exchange's dense gradient all-reduced (default from 4 ranks)
+    or all-gathered and summed in rank order by the owner launch.  The emulated all-reduce sums
+    in rank order too, so the two are bitwise equal here (RCCL's ring order differs only by
+    reassociation); every rank ends identical."""
+    from hipfm.ops import kernels as KN
+    import hipfm.parallel.sharded as SH
+    synth = make_synth("criteo_kaggle", seed=8)
+    F, K, layers, keep, B, N, steps = synth.F, 8, [64, 32], [0.5, 0.5], 512, 4, 3
+    V = synth.feature_size
+    params = init_params(V, F, K, layers, False, seed=12)
+    data = [synth.batch(N * B, step=s, device=DEV, id_dtype=torch.int32) for s in range(steps)]
+    batches = [[(ids[r * B:(r + 1) * B].contiguous(), vals[r * B:(r + 1) * B].contiguous(),
+                 lab[r * B:(r + 1) * B].contiguous()) for ids, vals, lab in data] for r in range(N)]
+    outs = []
+    for how in ("allgather", "allreduce"):
+        monkeypatch.setattr(SH, "_DENSE_XCHG", how)
+        hub = _Hub(N)
+        models = []
+        for r in range(N):
+            m = NativeDeepFM(V, F, K, layers, keep, sparse_update="lazy", learning_rate=1e-3, batch_size=B,
+                             device=DEV, init=False, comm=MeshComm(hub, r, sharded=sharded),
+                             field_ranges=synth.field_ranges())
+            m.load_tf_params(params)
+            x = m.shx if sharded else m.rpx
+            x.trace = []
+            models.append(m)
+        _run_ranks_steps(models, batches)
+        torch.cuda.synchronize()
+        for m in models:
+            m.check_errors()
+            assert torch.equal(m.p, models[0].p)
+        x = models[0].shx if sharded else models[0].rpx
+        kinds = {k for g in x.trace for k, _ in g}
+        assert (KN.COMM_ALLREDUCE in kinds) == (how == "allreduce")
+        outs.append([torch.cat([m.tv.reshape(-1) for m in models]), models[0].p.clone()])
+    for u, v in zip(*outs):
+        assert torch.equal(u, v)
+
+
 @pytest.mark.parametrize("update,depth", [("lazy", 1), ("tf1_dense", 1), ("lazy", 2)])
 def test_collective_sequence_identical_across_ranks(update, depth):
     """Deadlock freedom by construction (parallel/sharded.py): every collective of a step is a
