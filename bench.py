@@ -281,8 +281,10 @@ def main():
         pool = [(ids.t().contiguous().t(), vals, labels) for ids, vals, labels in pool]
     use_graph = not args.no_graph
     P = len(pool)
-    # (multi-rank graphs capture 3 RCCL operations per step: they keep 16-step graphs)
-    G = max(1, args.graph_steps if comm is None else min(args.graph_steps, 16))
+    # (multi-rank graphs capture 2 RCCL groups per step + 1 per run; HIPFM_BENCH_XGRAPH caps them:
+    # 1-rank proxy, driver window: 16 -> 0.162-0.166, 20 -> 0.156-0.158, 32 -> 0.159 ms/step)
+    G = max(1, args.graph_steps if comm is None else
+            min(args.graph_steps, int(os.environ.get("HIPFM_BENCH_XGRAPH", "32"))))
     torch.cuda.synchronize()
     _progress()
 

@@ -96,6 +96,7 @@ KNOBS: Dict[str, Knob] = {
     "HIPFM_BENCH_FIRST_RUNG": Knob(None, "harness", "bench: start the ladder at this rung"),
     "HIPFM_BENCH_HANG_S": Knob(None, "harness", "bench: seconds without progress = hung (45)"),
     "HIPFM_BENCH_FIRST_S": Knob(None, "harness", "bench: seconds to a rung's first progress mark (90)"),
+    "HIPFM_BENCH_XGRAPH": Knob(None, "harness", "bench: most steps per captured multi-rank graph (32)"),
     "HIPFM_BENCH_NO_GRAPH": Knob(None, "harness", "bench: eager steps only"),
     "HIPFM_BENCH_DIAG": Knob(None, "harness", "bench: after the measurement, re-time the window after "
                              "idle gaps (stderr; diagnostics only)"),
