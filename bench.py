@@ -591,20 +591,22 @@ def data_bench(args):
             if e == 0:
                 est.adopt_field_ranges(pipe)
             _progress()
-        return est, per_epoch
+        return est, per_epoch, pipe
 
-    est_s, per_epoch_s = train_arm(cache=False)        # every epoch streamed from the files
+    est_s, per_epoch_s, pipe_s = train_arm(cache=False)    # every epoch streamed from the files
+    # host-to-device bytes per streamed row (the last epoch's ring copies; HIPFM_WIRE_COMPACT)
+    wire = round(pipe_s.h2d_bytes / max(1, per_epoch_s[-1][0] * B), 1)
     if args.stream_only:                               # (profiling the streamed path alone)
         _emit(json.dumps({"metric": "streamed epochs samples/s (1 GPU)", "ingest_rows_per_s": round(ingest, 1),
                           "streamed_epoch_samples_per_s": [round(n * B / t, 1) for n, t in per_epoch_s],
-                          "epoch_s": [round(t, 4) for _, t in per_epoch_s],
+                          "epoch_s": [round(t, 4) for _, t in per_epoch_s], "wire_bytes_per_row": wire,
                           "host_timer_totals_s": {k: round(v, 4) for k, v in est_s.timer.t.items()},
                           "host_timer_calls": dict(est_s.timer.n)}))
         return
     sig_s = (est_s.model.p.double().sum().item(), est_s.model.rec.double().sum().item())
     del est_s
     torch.cuda.empty_cache()
-    est, per_epoch = train_arm(cache=True)              # epoch 0 streamed + cached, then replayed
+    est, per_epoch, _ = train_arm(cache=True)           # epoch 0 streamed + cached, then replayed
     sig = (est.model.p.double().sum().item(), est.model.rec.double().sum().item())
     ev = est.evaluate(InputPipeline(va, F, B, 1, device=est.device, id_dtype=torch.int32,
                                     shuffle_files=False, threads=args.threads)) if va else {"auc": None}
@@ -617,7 +619,7 @@ def data_bench(args):
            "ingest_rows_per_s": round(ingest, 1), "ingest_threads": args.threads, "rows": rows,
            "epoch_samples_per_s": [round(x, 1) for x in sps],
            "streamed_epoch_samples_per_s": [round(x, 1) for x in sps_s],
-           "streamed_bitwise_equal_cached": sig == sig_s,
+           "streamed_bitwise_equal_cached": sig == sig_s, "wire_bytes_per_row": wire,
            "epoch0": "streamed from files (pinned ring + copy stream + staging ring of run graphs) and cached in HBM",
            "epoch1": "cache replay, graphs captured", "steady": "cache replay of captured graphs",
            "streamed": "no cache: every epoch streamed through the staging ring",

@@ -440,6 +440,7 @@ struct Chunk {
   std::vector<int64_t> ids;     // (empty when the loader narrows at decode time: ids32)
   std::vector<int32_t> ids32;
   std::vector<float> vals;
+  uint64_t vmask = 0;           // bit f: some row of the chunk has a field-f value other than 1.0
 };
 
 struct WorkerQueue {
@@ -625,6 +626,17 @@ struct Loader {
             }
           }
         }
+        if (F <= 64) {
+          // per-chunk mask of the fields whose values are not all exactly 1.0 (bit pattern, so
+          // -0 / NaN / denormals count as values): the compact wire format ships only those columns
+          uint64_t m = 0;
+          for (int f = 0; f < F; ++f) {
+            uint32_t u;
+            memcpy(&u, vals + f, 4);
+            m |= (uint64_t)(u != 0x3F800000u) << f;
+          }
+          c->vmask |= m;
+        }
         if (narrow32) {
           int32_t* d = c->ids32.data() + (size_t)c->n * F;
           for (int f = 0; f < F; ++f) {
@@ -678,7 +690,11 @@ struct Loader {
   // ids32 != null: ids are narrowed to int32 (the device id type) while copying, straight into
   // the caller's (pinned) buffer; an id outside [0, 2^31) is an error.  The batch is assembled
   // from pieces (chunk, chunk row, batch row, rows) copied in parallel by the copy pool.
-  int next(float* lab, int64_t* ids, float* vals, int32_t* ids32 = nullptr) {
+  // vmask != null: compact values -- only the columns of the fields whose values are not all
+  // 1.0 in the batch's chunks (mask returned in *vmask, bit f = field f shipped; columns in field
+  // order, ``vals`` then holds [rows, popcount(mask)]).  Requires F <= 64.  Lossless: the omitted
+  // columns are exactly 1.0f in every row of the batch.
+  int next(float* lab, int64_t* ids, float* vals, int32_t* ids32 = nullptr, uint64_t* vmask = nullptr) {
     struct Piece {
       const Chunk* c;
       int src, dst, k;
@@ -702,6 +718,20 @@ struct Loader {
       cur_off += k;
     }
     if (got < B && drop_remainder) return 0;
+    int cols[64];
+    int nc = F;
+    if (vmask) {
+      if (F > 64) {
+        err = "compact values need F <= 64 fields";
+        return -1;
+      }
+      uint64_t m = 0;
+      for (const Piece& p : pieces) m |= p.c->vmask;
+      nc = 0;
+      for (int f = 0; f < F; ++f)
+        if ((m >> f) & 1) cols[nc++] = f;
+      *vmask = m;
+    }
     std::atomic<int64_t> bad{0};
     auto copy = [&](int pi) {
       const Piece& p = pieces[pi];
@@ -726,7 +756,14 @@ struct Loader {
       } else {
         memcpy(ids + (size_t)p.dst * F, p.c->ids.data() + (size_t)p.src * F, m * 8);
       }
-      memcpy(vals + (size_t)p.dst * F, p.c->vals.data() + (size_t)p.src * F, m * 4);
+      if (nc == F) {
+        memcpy(vals + (size_t)p.dst * F, p.c->vals.data() + (size_t)p.src * F, m * 4);
+      } else {
+        const float* src = p.c->vals.data() + (size_t)p.src * F;
+        float* dst = vals + (size_t)p.dst * nc;
+        for (int i = 0; i < p.k; ++i, src += F, dst += nc)
+          for (int j = 0; j < nc; ++j) dst[j] = src[cols[j]];
+      }
     };
     if (pool && pieces.size() > 1) {
       pool->run((int)pieces.size(), copy);
@@ -785,6 +822,14 @@ HFMIO_API int hfmio_loader_next(void* h, float* labels, int64_t* ids, float* val
 HFMIO_API int hfmio_loader_next32(void* h, float* labels, int32_t* ids, float* vals) {
   auto* L = (Loader*)h;
   int r = L->next(labels, nullptr, vals, ids);
+  if (r < 0) set_err(L->err);
+  return r;
+}
+
+// next32 with compact values (Loader::next): vals_c gets [rows, popcount(*mask)] floats.
+HFMIO_API int hfmio_loader_next32c(void* h, float* labels, int32_t* ids, float* vals_c, uint64_t* mask) {
+  auto* L = (Loader*)h;
+  int r = L->next(labels, nullptr, vals_c, ids, mask);
   if (r < 0) set_err(L->err);
   return r;
 }

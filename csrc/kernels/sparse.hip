@@ -178,6 +178,33 @@ __global__ void gather_i32_kernel(const int* __restrict__ src, const int* __rest
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) out[i] = src[perm[i]];
 }
+// Streamed-input wire format (hfm_io.cpp Loader::next with a value mask, data/pipeline.py
+// _DeviceRing): a batch's values arrive as [rows, nc] -- only the nc fields of ``mask`` whose values
+// are not all 1.0 -- and are expanded here, on the copy stream, into the [rows, F] layout every
+// kernel reads.  One thread per output element; the shipped column of field f is the popcount of
+// the mask bits below f.
+__global__ __launch_bounds__(256) void expand_vals_kernel(const float* __restrict__ vc, int nc,
+                                                          unsigned long long mask, int F, long n,
+                                                          float* __restrict__ out) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const long b = i / F;
+  const int f = (int)(i - b * F);
+  float v = 1.0f;
+  if ((mask >> f) & 1ull) v = vc[b * nc + __popcll(mask & ((1ull << f) - 1ull))];
+  out[i] = v;
+}
+
+HFM_API int hfm_expand_vals(const float* vc, int nc, unsigned long long mask, int F, long rows, float* out,
+                            hipStream_t st) {
+  if (rows <= 0) return 0;
+  if (F <= 0 || F > 64 || nc != __builtin_popcountll(mask) || (F < 64 && (mask >> F) != 0)) return (int)hipErrorInvalidValue;
+  const long n = rows * F;
+  hipLaunchKernelGGL(expand_vals_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, vc, nc, mask, F, n,
+                     out);
+  HFM_LAUNCH_CHECK();
+}
+
 HFM_API int hfm_gather_i32(const int* src, const int* perm, int n, int* out, hipStream_t st) {
   if (n <= 0) return 0;
   hipLaunchKernelGGL(gather_i32_kernel, dim3((n + 255) / 256), dim3(256), 0, st, src, perm, n, out);

@@ -43,6 +43,8 @@ def lib():
             L.hfmio_loader_next.restype = ci
             L.hfmio_loader_next32.argtypes = [vp, vp, vp, vp]
             L.hfmio_loader_next32.restype = ci
+            L.hfmio_loader_next32c.argtypes = [vp, vp, vp, vp, vp]
+            L.hfmio_loader_next32c.restype = ci
             L.hfmio_loader_destroy.argtypes = [vp]
             L.hfmio_loader_set_copy_threads.argtypes = [vp, ci]
             L.hfmio_loader_set_copy_threads.restype = None
@@ -121,6 +123,21 @@ def _dtype_of(a) -> int:
     return a.dtype.itemsize if isinstance(a, np.ndarray) else a.element_size()
 
 
+def mask_fields(mask: int, F: int):
+    """The shipped (non-constant) fields of a compact-values mask, in column order."""
+    return [f for f in range(F) if (mask >> f) & 1]
+
+
+def expand_values(vals_c, rows: int, F: int, mask: int) -> np.ndarray:
+    """Host inverse of the compact value format: [rows, F] float32 with the shipped columns in
+    place and 1.0 elsewhere (the device does the same in ops.kernels.expand_vals)."""
+    cols = mask_fields(mask, F)
+    out = np.ones((rows, F), np.float32)
+    src = np.asarray(vals_c).reshape(-1)[:rows * len(cols)]
+    out[:, cols] = src.reshape(rows, len(cols))
+    return out
+
+
 class NativeLoader:
     """Iterator of (labels f32[B], ids i64[B,F], vals f32[B,F]) numpy batches.
 
@@ -162,6 +179,23 @@ class NativeLoader:
         if r == 0:
             self._done = True
         return r
+
+    def next_into_compact(self, labels, ids32, vals_c) -> Tuple[int, int]:
+        """``next_into`` with int32 ids and compact values: ``vals_c`` (>= B*F floats) receives
+        only the columns of the fields whose values are not all exactly 1.0 in the batch, [rows,
+        nc] row-major in field order; returns (rows, mask) with bit f of ``mask`` set for each
+        shipped field f (nc = popcount(mask)).  Lossless: the other fields' values are 1.0f in
+        every row (``expand_values``).  Needs F <= 64."""
+        if self._done:
+            return 0, 0
+        assert _dtype_of(ids32) == 4 and self.F <= 64
+        m = C.c_uint64(0)
+        r = lib().hfmio_loader_next32c(self._h, _addr(labels), _addr(ids32), _addr(vals_c), C.addressof(m))
+        if r < 0:
+            raise IOError(_err())
+        if r == 0:
+            self._done = True
+        return r, int(m.value)
 
     def __iter__(self) -> Iterator[Tuple[np.ndarray, np.ndarray, np.ndarray]]:
         while True:

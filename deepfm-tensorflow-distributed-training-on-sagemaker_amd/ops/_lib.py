@@ -216,6 +216,7 @@ _SIGS = {
     "hfm_unique_inverse": [c_void_p, c_void_p, c_int] + [c_void_p] * 6 + [c_size_t, c_void_p],
     "hfm_owner_keys": [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p],
     "hfm_gather_i32": [c_void_p, c_void_p, c_int, c_void_p, c_void_p],
+    "hfm_expand_vals": [c_void_p, c_int, C.c_uint64, c_int, c_long, c_void_p, c_void_p],
     "hfm_sparse_rows_update": [c_int, c_int] + [c_void_p] * 3 + [c_int, c_int] + [c_void_p] * 6
                               + [C.POINTER(OptHyper), c_void_p, c_long, c_long, c_void_p],
     "hfm_scatter_rows": [c_int] + [c_void_p] * 3 + [c_int, c_int, c_void_p, c_void_p, c_void_p],

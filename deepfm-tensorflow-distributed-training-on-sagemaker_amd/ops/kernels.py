@@ -292,6 +292,13 @@ def gather_i32(src, perm, n, out):
     check(L().hfm_gather_i32(ptr(src), ptr(perm), n, ptr(out), stream_handle()), "gather_i32")
 
 
+def expand_vals(vc, nc: int, mask: int, F: int, rows: int, out):
+    """Compact streamed values [rows, nc] (fields of ``mask``) -> ``out`` [rows, F], 1.0 in the
+    fields not shipped (data/native_io.py next_into_compact)."""
+    assert out.dtype == torch.float32 and out.numel() >= rows * F and vc.numel() >= rows * nc
+    check(L().hfm_expand_vals(ptr(vc), nc, mask, F, rows, ptr(out), stream_handle()), "expand_vals")
+
+
 def seg_tiles(K: int, n: int) -> int:
     return L().hfm_seg_tiles(K, n)
 

@@ -63,10 +63,12 @@ class ReplicatedExchange:
         self.tcnt = torch.zeros(KN.sh_route_tiles(n) * 2, **i32)
         self.send_cnt = torch.zeros(1, **i32)
         self.num_u = torch.zeros(1, **i32)
-        self.send_g = torch.zeros(self.C, self.RW, **f32)
         T = self.N * self.C
         self.g_ids = torch.full((T,), -1, **i32)
         self.g_rows = torch.zeros(T, self.RW, **f32)
+        # the sparse launch writes this rank's gradient rows straight into its block of the
+        # gathered rows: an in-place all-gather (no 1-rank self-copy, no local copy at N ranks)
+        self.send_g = self.g_rows[self.rank * self.C:(self.rank + 1) * self.C]
         slots = 1
         while slots < 2 * T:
             slots *= 2

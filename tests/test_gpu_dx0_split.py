@@ -101,3 +101,46 @@ def test_layer0_split_matches_the_fused_gather(monkeypatch, preset, K, B):
         scale = b[k].abs().max().item()
         assert (d <= 1e-3 * scale).float().mean().item() >= 0.999 and d.max().item() <= 2e-2 * scale, k
     assert (a["pred"] - b["pred"]).abs().max().item() <= 2e-3
+
+
+@pytest.mark.parametrize("B", [4096, 1024])
+def test_single_wide_hidden_layer_tower(monkeypatch, B):
+    """One hidden layer of 256 (nl == 1): the tower's H region is then large enough that the dX0 /
+    gradient-row wave tiles share the H_0 region, and with no dgrad chain only the barrier before
+    the dX0 phase (tower.hip) keeps those tiles from overwriting H_0 while the head still reads it
+    for the output-layer gradient.  Checked three ways: two runs are bitwise equal, the sorted
+    gradient rows (HIPFM_GROW=1) train like the per-slot gather path (HIPFM_GROW=0), and one
+    step's gradients match the per-layer kernels (B = 4096: the tower's own dX0 phase; 1024: the
+    dX0 launch)."""
+    synth = make_synth("criteo_kaggle", seed=47)
+    K, layers = 8, [256]
+    params = init_params(synth.feature_size, synth.F, K, layers, False, seed=11)
+    pool = [synth.batch(B, step=s, device=DEV, id_dtype=torch.int32) for s in range(4)]
+    res = {}
+    for tag, grow, fused in (("a", "1", True), ("b", "1", True), ("nogrow", "0", True), ("layers", "1", False)):
+        monkeypatch.setattr(D, "_GROW", grow)
+        m = NativeDeepFM(synth.feature_size, synth.F, K, layers, [0.5], batch_size=B, device=DEV, init=False,
+                         sparse_update="lazy", field_ranges=synth.field_ranges(), fused=fused)
+        m.load_tf_params(params)
+        assert m.fused == fused and (m.dx0_split == (B < 4096) or not fused)
+        g, _, UG = m.compute_grads(*pool[0])
+        out = dict(g=g.clone(), UG=UG.clone())
+        if fused:
+            assert (m.grow is not None) == (grow == "1") or not m._run_sort_ok(pool[:2])
+            for r in range(2):
+                m.train_steps(pool[:2], next_ids=(pool[2][0], pool[3][0]))
+                m.train_steps(pool[2:], next_ids=(pool[0][0], pool[1][0]))
+            torch.cuda.synchronize()
+            m.check_errors()
+            out.update(tv=m.tv.clone(), tw=m.tw.clone(), p=m.p.clone())
+        res[tag] = out
+        del m
+    a, b, c, lay = res["a"], res["b"], res["nogrow"], res["layers"]
+    for k in ("g", "UG", "tv", "tw", "p"):
+        assert torch.equal(a[k], b[k]), k                        # deterministic (no LDS race)
+    for k in ("tv", "tw", "p"):
+        d = (a[k] - c[k]).abs().max().item()
+        assert d <= 1e-5 * max(1.0, c[k].abs().max().item()), (k, d)
+    scale = lay["g"].abs().max().item()
+    assert (a["g"] - lay["g"]).abs().max().item() <= 1e-2 * scale + 1e-7
+    assert (a["UG"] - lay["UG"]).abs().max().item() <= 1e-2 * lay["UG"].abs().max().item()

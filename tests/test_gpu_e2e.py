@@ -116,11 +116,12 @@ def test_native_auc_parity_with_golden(update):
     assert ag > 0.6 and abs(an - ag) <= 0.005, (an, ag)
 
 
-def test_streamed_epochs_through_the_ring_train_like_the_cached_run(dataset):
+def test_streamed_epochs_through_the_ring_train_like_the_cached_run(dataset, monkeypatch):
     """Streamed epochs (no HBM cache, e.g. a dataset over the cache budget) go through the staging
     ring as captured multi-step runs; they train bitwise like the cached run (epoch 0 streamed
     through the ring, later epochs replayed from the cache), with the per-field sort from
-    --field_sizes from the first step on."""
+    --field_sizes from the first step on.  Both wire formats: compact (the 26 categorical fields'
+    1.0 values never cross the link, sparse.hip expand_vals rebuilds them on the device) and full."""
     from hipfm.cli import _EpochView
     from hipfm.config import RunConfig
     from hipfm.data.pipeline import InputPipeline, discover_files
@@ -128,7 +129,8 @@ def test_streamed_epochs_through_the_ring_train_like_the_cached_run(dataset):
     from hipfm.data.synthetic import make_synth
     sizes = ",".join(str(hi - lo) for lo, hi in make_synth("total:50000").field_ranges())
     out = []
-    for cache in (False, True):
+    for cache, compact in ((False, "1"), (False, "0"), (True, "1")):
+        monkeypatch.setenv("HIPFM_WIRE_COMPACT", compact)
         cfg = RunConfig(feature_size=50000, field_size=39, embedding_size=8, batch_size=512,
                         deep_layers="64,32", dropout="0.9,0.9", device="cuda", log_steps=0,
                         watchdog_secs=0, graph_steps=8, num_threads=4, field_sizes=sizes)
@@ -144,7 +146,12 @@ def test_streamed_epochs_through_the_ring_train_like_the_cached_run(dataset):
             # own copy-in staging ring was never needed
             assert pipe.cached_batches == 0 and pipe._ring is not None
             assert getattr(est, "_ring", None) is None
+            assert pipe._ring.compact == (compact == "1")
+            # (the generator's values: 13 real-valued fields, 26 fields of 1.0)
+            per_row = pipe.h2d_bytes / ((20000 // 512) * 512)
+            assert per_row == (39 * 4 + 4 + 13 * 4 if compact == "1" else 39 * 8 + 4), per_row
         torch.cuda.synchronize()
         out.append((est.model.p.clone(), est.model.rec.clone(), est.global_step))
-    assert out[0][2] == out[1][2] == 3 * (20000 // 512)
-    assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
+    assert out[0][2] == out[1][2] == out[2][2] == 3 * (20000 // 512)
+    for a in out[1:]:
+        assert torch.equal(out[0][0], a[0]) and torch.equal(out[0][1], a[1])

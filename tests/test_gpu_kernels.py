@@ -615,3 +615,19 @@ def test_field_major_resident_batches_bitwise_equal():
         out.append((m.tv.clone(), m.tw.clone(), m.p.clone(), p.clone()))
     for x, y in zip(*out):
         assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("F,mask", [(39, (1 << 13) - 1), (39, 0), (39, (1 << 39) - 1), (64, (1 << 63) | 5),
+                                    (7, 0b1010010)])
+def test_expand_vals_matches_torch(F, mask):
+    """sparse.hip expand_vals (the compact streamed wire format): the shipped [rows, nc] columns
+    land in the fields of ``mask``, 1.0 elsewhere -- against a torch scatter of the same columns."""
+    rows = 3001
+    cols = [f for f in range(F) if (mask >> f) & 1]
+    vc = torch.randn(rows * len(cols) + 5, device=DEV)
+    out = torch.full((rows, F), -7.0, device=DEV)
+    KN.expand_vals(vc, len(cols), mask, F, rows, out)
+    want = torch.ones(rows, F, device=DEV)
+    want[:, cols] = vc[:rows * len(cols)].view(rows, len(cols))
+    torch.cuda.synchronize()
+    assert torch.equal(out, want)

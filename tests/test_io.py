@@ -122,6 +122,56 @@ def test_native_loader_batches_deterministic(tmp_path, threads):
     assert sorted(map(tuple, full.tolist())) == sorted(map(tuple, want.tolist()))
 
 
+@pytest.mark.parametrize("threads,drop", [(1, True), (3, True), (3, False)])
+def test_compact_values_are_lossless(tmp_path, threads, drop):
+    """Compact wire format (hfm_io.cpp Loader::next with a value mask): a batch ships only the
+    value columns of fields that are not all exactly 1.0 in its chunks; expanding them back gives
+    the plain batch bit for bit.  Fields: always 1.0 (categorical, never shipped), real-valued
+    (always shipped), 1.0 except in one record of one file (shipped only in the batches that
+    touch that record's chunk), and -0.0 / NaN patterns (not 1.0: shipped)."""
+    F = 7
+    files = []
+    for k in range(4):
+        lab, ids, _ = _rows(900 + 37 * k, F, k)
+        ids = ids % 100_000
+        vals = np.ones(ids.shape, np.float32)
+        vals[:, 1] = np.random.default_rng(k).standard_normal(len(ids)).astype(np.float32)
+        vals[:, 4] = np.where(np.arange(len(ids)) % 5 == 0, 0.5, 1.0)
+        if k == 2:
+            vals[300, 5] = 2.0
+        if k == 3:
+            vals[10, 6] = -0.0
+            vals[11, 6] = np.nan
+        p = str(tmp_path / f"c-{k}.tfrecords")
+        nio.write_examples(p, lab, ids, vals)
+        files.append(p)
+    B = 256
+    plain = nio.NativeLoader(files, F, B, threads=threads, drop_remainder=drop, ids32=True)
+    comp = nio.NativeLoader(files, F, B, threads=threads, drop_remainder=drop, ids32=True)
+    masks = []
+    while True:
+        lab0, ids0, val0 = (np.empty(B, np.float32), np.empty((B, F), np.int32), np.empty((B, F), np.float32))
+        r0 = plain.next_into(lab0, ids0, val0)
+        lab1, ids1, vc = np.empty(B, np.float32), np.empty((B, F), np.int32), np.empty(B * F, np.float32)
+        r1, mask = comp.next_into_compact(lab1, ids1, vc)
+        assert r0 == r1
+        if r0 == 0:
+            break
+        masks.append(mask)
+        assert mask & 0b11 == 0b10                       # field 0 never shipped, field 1 always
+        assert np.array_equal(lab0[:r0], lab1[:r0]) and np.array_equal(ids0[:r0], ids1[:r0])
+        full = nio.expand_values(vc, r0, F, mask)
+        assert np.array_equal(full.view(np.uint32), val0[:r0].view(np.uint32))
+        # a field left out is exactly 1.0 in every row of the batch
+        for f in range(F):
+            if not (mask >> f) & 1:
+                assert (val0[:r0, f].view(np.uint32) == np.float32(1.0).view(np.uint32)).all()
+    assert any(m >> 5 & 1 for m in masks) and not all(m >> 5 & 1 for m in masks)
+    assert any(m >> 6 & 1 for m in masks)
+    plain.close()
+    comp.close()
+
+
 def test_record_shard_matches_reference_semantics(tmp_path):
     F = 3
     lab, ids, vals = _rows(50, F, 9)

@@ -171,3 +171,47 @@ def test_ring_stop_right_after_acquire_gives_the_slot_back():
         ring.release([s_], None)
         n += 1
     assert n == 5
+
+
+@pytest.mark.parametrize("compact", [True, False])
+def test_wire_layout_one_copy_of_a_prefix(tmp_path, compact):
+    """Ring slot layout (``_ring_layout``): the host buffer is a prefix of the device slot's
+    layout, so one copy of ``wire_bytes(mask)`` bytes moves ids + labels (+ the shipped value
+    columns in compact mode); expanding the staged columns (the host twin of sparse.hip
+    expand_vals) then fills the vals view bit for bit.  Fed by the real loader."""
+    import numpy as np
+    from hipfm.data import native_io as nio
+    B, F = 64, 6
+    rng = np.random.default_rng(3)
+    ids = rng.integers(0, 1000, (B, F)).astype(np.int64)
+    vals = np.ones((B, F), np.float32)
+    vals[:, 2] = rng.standard_normal(B)
+    vals[:, 5] = rng.random(B)
+    lab = (rng.random(B) < 0.3).astype(np.float32)
+    p = str(tmp_path / "w.tfrecords")
+    nio.write_examples(p, lab, ids, vals)
+    ring = P._DeviceRing(B, F, "cpu", torch.int32, 2, compact=compact)
+    lay = ring.lay
+    host = torch.zeros(lay["host"], dtype=torch.uint8)
+    h_ids, h_vals, h_lab = P._flat_views(host, B, F, torch.int32, lay)
+    ld = nio.NativeLoader([p], F, B, ids32=True)
+    if compact:
+        assert h_vals is None and lay["host"] < lay["total"]
+        st = lay["stage"]
+        r, mask = ld.next_into_compact(h_lab, h_ids, host[st[0]:st[1]].view(torch.float32))
+        assert mask == (1 << 2) | (1 << 5)
+        assert ring.wire_bytes(mask) == B * F * 4 + B * 4 + B * 2 * 4
+    else:
+        r, mask = ld.next_into(h_lab, h_ids, h_vals), 0
+        assert lay["host"] == lay["total"] == ring.wire_bytes(0)
+    ld.close()
+    assert r == B
+    nb = ring.wire_bytes(mask)
+    ring.flat[0][:nb].copy_(host[:nb])                   # the one host-to-device copy
+    d_ids, d_vals, d_lab = ring.views[0]
+    if compact:
+        cols = ring.stage[0][:B * 2].view(B, 2).numpy()
+        d_vals.copy_(torch.from_numpy(nio.expand_values(cols, B, F, mask)))
+    assert torch.equal(d_ids, torch.from_numpy(ids.astype(np.int32)))
+    assert torch.equal(d_lab, torch.from_numpy(lab))
+    assert np.array_equal(d_vals.numpy().view(np.uint32), vals.view(np.uint32))
