@@ -543,6 +543,87 @@ struct Loader {
   std::string err;
   std::unique_ptr<CopyPool> pool;            // parallel batch assembly (null: the consumer copies)
 
+  // Assembly ring (start_ring): an assembler thread fills caller-registered (pinned) buffers in
+  // cyclic slot order ahead of the consumer, so batch i+1 is assembled while the consumer issues
+  // batch i's device copy (with next() the assembly and the caller's per-batch work alternate on
+  // one thread: the streamed epochs ran at ~65 % of the loader's own rate).  take() returns the
+  // slots in order; give() hands one back once the caller is done with its contents.
+  struct Ring {
+    int n = 0;
+    bool compact = false;
+    std::vector<float*> lab, vals;
+    std::vector<int32_t*> ids;
+    std::vector<int> state;      // 0 free, 1 assembling, 2 assembled
+    std::vector<int> rows;
+    std::vector<uint64_t> mask;
+    std::deque<int> ready;
+    int fill = 0;                // next slot the assembler fills
+    std::mutex m;
+    std::condition_variable cv_free, cv_ready;
+    std::thread th;
+  } ring;
+
+  void assemble_loop() {
+    Ring& R = ring;
+    for (;;) {
+      int s;
+      {
+        std::unique_lock<std::mutex> lk(R.m);
+        R.cv_free.wait(lk, [&] { return stop.load() || R.state[R.fill] == 0; });
+        if (stop.load()) return;
+        s = R.fill;
+        R.state[s] = 1;
+        R.fill = (s + 1) % R.n;
+      }
+      uint64_t mk = 0;
+      const int r = next(R.lab[s], nullptr, R.vals[s], R.ids[s], R.compact ? &mk : nullptr);
+      {
+        std::lock_guard<std::mutex> lk(R.m);
+        R.rows[s] = r;
+        R.mask[s] = mk;
+        R.state[s] = 2;
+        R.ready.push_back(s);
+      }
+      R.cv_ready.notify_all();
+      if (r <= 0) return;        // end of data (0) or error (-1, err holds it): the last slot says so
+    }
+  }
+
+  int start_ring(int n, float** lab, int32_t** ids, float** vals, int compact) {
+    if (ring.n || n < 2 || (compact && F > 64)) return -1;
+    ring.n = n;
+    ring.compact = compact != 0;
+    ring.lab.assign(lab, lab + n);
+    ring.ids.assign(ids, ids + n);
+    ring.vals.assign(vals, vals + n);
+    ring.state.assign(n, 0);
+    ring.rows.assign(n, 0);
+    ring.mask.assign(n, 0);
+    ring.th = std::thread(&Loader::assemble_loop, this);
+    return 0;
+  }
+
+  // next assembled slot in order: rows (B, fewer for a final partial batch, 0 at end, -1 error)
+  int ring_take(int* slot, uint64_t* mask) {
+    std::unique_lock<std::mutex> lk(ring.m);
+    ring.cv_ready.wait(lk, [&] { return !ring.ready.empty() || stop.load(); });
+    if (ring.ready.empty()) return 0;
+    const int s = ring.ready.front();
+    const int r = ring.rows[s];
+    if (r > 0) ring.ready.pop_front();   // (the end / error slot stays: every later take sees it)
+    *slot = s;
+    *mask = ring.mask[s];
+    return r;
+  }
+
+  void ring_give(int slot) {
+    {
+      std::lock_guard<std::mutex> lk(ring.m);
+      if (slot >= 0 && slot < ring.n && ring.state[slot] == 2) ring.state[slot] = 0;
+    }
+    ring.cv_free.notify_all();
+  }
+
   void worker(int w, int W) {
     WorkerQueue& Q = *queues[w];
     auto push = [&](std::unique_ptr<Chunk> c) {
@@ -667,7 +748,8 @@ struct Loader {
     while (idle < W) {
       WorkerQueue& Q = *queues[turn];
       std::unique_lock<std::mutex> lk(Q.m);
-      Q.cv_get.wait(lk, [&] { return !Q.q.empty() || Q.done; });
+      Q.cv_get.wait(lk, [&] { return !Q.q.empty() || Q.done || stop.load(); });
+      if (Q.q.empty() && !Q.done) return nullptr;   // shutting down (a stopped worker never sets done)
       if (Q.failed) {
         err = Q.err;
         return nullptr;
@@ -784,6 +866,12 @@ struct Loader {
       q->cv_put.notify_all();
       q->cv_get.notify_all();
     }
+    {
+      std::lock_guard<std::mutex> lk(ring.m);
+      ring.cv_free.notify_all();
+      ring.cv_ready.notify_all();
+    }
+    if (ring.th.joinable()) ring.th.join();
     for (auto& t : threads)
       if (t.joinable()) t.join();
   }
@@ -833,6 +921,22 @@ HFMIO_API int hfmio_loader_next32c(void* h, float* labels, int32_t* ids, float* 
   if (r < 0) set_err(L->err);
   return r;
 }
+
+// Assembly ring over n caller buffers (Loader::start_ring); vals[i] receives [B, nc] compact
+// columns when compact != 0 (hfmio_loader_next32c), else [B, F].  Ids are int32.
+HFMIO_API int hfmio_loader_start_ring(void* h, int n, float** labels, int32_t** ids, float** vals, int compact) {
+  auto* L = (Loader*)h;
+  int r = L->start_ring(n, labels, ids, vals, compact);
+  if (r < 0) set_err("assembly ring: needs >= 2 slots, once per loader (compact: F <= 64)");
+  return r;
+}
+HFMIO_API int hfmio_loader_ring_take(void* h, int* slot, uint64_t* mask) {
+  auto* L = (Loader*)h;
+  int r = L->ring_take(slot, mask);
+  if (r < 0) set_err(L->err);
+  return r;
+}
+HFMIO_API void hfmio_loader_ring_give(void* h, int slot) { ((Loader*)h)->ring_give(slot); }
 
 // Assemble batches with n copy threads (the consumer plus n - 1 pool threads); 1: serial.
 HFMIO_API void hfmio_loader_set_copy_threads(void* h, int n) {

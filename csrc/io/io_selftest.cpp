@@ -24,6 +24,10 @@ void* hfmio_loader_create(const char** paths, int npaths, int format, int F, int
                           int verify_crc, int queue_depth, int64_t id_limit, int narrow32);
 int hfmio_loader_next(void* h, float* labels, int64_t* ids, float* vals);
 void hfmio_loader_destroy(void* h);
+void hfmio_loader_set_copy_threads(void* h, int n);
+int hfmio_loader_start_ring(void* h, int n, float** labels, int32_t** ids, float** vals, int compact);
+int hfmio_loader_ring_take(void* h, int* slot, uint64_t* mask);
+void hfmio_loader_ring_give(void* h, int slot);
 int hfmio_write_examples(const char* path, const float* labels, const int64_t* ids,
                          const float* vals, long n, int F, int append);
 long hfmio_libsvm_to_tfrecord(const char* src, const char* dst, int F);
@@ -75,6 +79,53 @@ static Sum read_all(const std::vector<std::string>& files, int threads, int shar
   return s;
 }
 
+// the assembly ring (assembler thread + copy pool + taker, compact values): every record once, in
+// the order next() gives, the constant-1.0 fields never shipped; then destroyed mid-stream while
+// the assembler waits for a slot (TSan: the ring hand-offs and the shutdown)
+static Sum read_ring(const std::vector<std::string>& files, int threads, int copy_threads) {
+  std::vector<const char*> p;
+  for (auto& f : files) p.push_back(f.c_str());
+  const int n = 3, Bt = 64;
+  Sum s;
+  for (int pass = 0; pass < 2; ++pass) {
+    void* h = hfmio_loader_create(p.data(), (int)p.size(), 0, F, Bt, 0, threads, 1, 0, 1, 8, 0, 1);
+    CHECK(h != nullptr);
+    hfmio_loader_set_copy_threads(h, copy_threads);
+    std::vector<std::vector<float>> lab(n, std::vector<float>(Bt)), vals(n, std::vector<float>(Bt * F));
+    std::vector<std::vector<int32_t>> ids(n, std::vector<int32_t>(Bt * F));
+    float* lp[n];
+    float* vp[n];
+    int32_t* ip[n];
+    for (int i = 0; i < n; ++i) lp[i] = lab[i].data(), vp[i] = vals[i].data(), ip[i] = ids[i].data();
+    CHECK(hfmio_loader_start_ring(h, n, lp, ip, vp, 1) == 0);
+    for (int taken = 0;; ++taken) {
+      int slot = -1;
+      uint64_t mask = 0;
+      const int r = hfmio_loader_ring_take(h, &slot, &mask);
+      CHECK(r >= 0);
+      if (r == 0 || (pass == 1 && taken == n - 1)) break;   // pass 1: every slot held, assembler waiting
+      CHECK(slot >= 0 && slot < n && (mask >> 13) == 0);  // fields 13.. are all 1.0: not shipped
+      const int nc = __builtin_popcountll(mask);
+      if (pass == 0) {
+        for (int i = 0; i < r; ++i) {
+          s.lab += lab[slot][i];
+          for (int f = 0; f < F; ++f) {
+            s.ids += (uint64_t)ids[slot][i * F + f];
+            float v = 1.0f;
+            if ((mask >> f) & 1) v = vals[slot][i * nc + __builtin_popcountll(mask & ((1ull << f) - 1))];
+            s.val += v;
+          }
+          s.order = s.order * 1000003ull + (uint64_t)ids[slot][i * F];
+          ++s.rows;
+        }
+        hfmio_loader_ring_give(h, slot);
+      }
+    }
+    hfmio_loader_destroy(h);
+  }
+  return s;
+}
+
 int main(int argc, char** argv) {
   const std::string dir = argc > 1 ? argv[1] : "/tmp";
   const long n_per = 1500;
@@ -107,6 +158,9 @@ int main(int argc, char** argv) {
   // ids narrowed to int32 while decoding (the device path) read back identically
   const Sum n32 = read_all(files, 4, 1, 0, 1);
   CHECK(n32.rows == a.rows && n32.ids == a.ids && n32.order == a.order && n32.val == a.val);
+  // the assembly ring reads the same stream, in the same order, through compact values
+  const Sum rg = read_ring(files, 4, 3);
+  CHECK(rg.rows == a.rows && rg.ids == a.ids && rg.order == a.order && rg.val == a.val && rg.lab == a.lab);
   // 2) record-level sharding partitions the data
   const Sum s0 = read_all(files, 3, 2, 0), s1 = read_all(files, 3, 2, 1);
   CHECK(s0.rows + s1.rows == want.rows && s0.ids + s1.ids == want.ids);

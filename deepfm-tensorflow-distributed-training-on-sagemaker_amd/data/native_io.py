@@ -45,6 +45,12 @@ def lib():
             L.hfmio_loader_next32.restype = ci
             L.hfmio_loader_next32c.argtypes = [vp, vp, vp, vp, vp]
             L.hfmio_loader_next32c.restype = ci
+            L.hfmio_loader_start_ring.argtypes = [vp, ci, vp, vp, vp, ci]
+            L.hfmio_loader_start_ring.restype = ci
+            L.hfmio_loader_ring_take.argtypes = [vp, vp, vp]
+            L.hfmio_loader_ring_take.restype = ci
+            L.hfmio_loader_ring_give.argtypes = [vp, ci]
+            L.hfmio_loader_ring_give.restype = None
             L.hfmio_loader_destroy.argtypes = [vp]
             L.hfmio_loader_set_copy_threads.argtypes = [vp, ci]
             L.hfmio_loader_set_copy_threads.restype = None
@@ -196,6 +202,32 @@ class NativeLoader:
         if r == 0:
             self._done = True
         return r, int(m.value)
+
+    def start_ring(self, bufs, compact: bool = False) -> None:
+        """Assemble ahead into ``bufs`` = [(labels, ids32, vals), ...] (>= 2 slots; pinned CPU
+        tensors or numpy arrays that outlive the loader's use of them) on a C++ assembler thread,
+        in cyclic slot order; ``compact``: ``vals`` get the compact columns (next_into_compact).
+        Then ``ring_take`` / ``ring_give`` instead of ``next_into``."""
+        n = len(bufs)
+        arr = lambda xs: (C.c_void_p * n)(*[_addr(x) for x in xs])  # noqa: E731
+        for lab, ids, vals in bufs:
+            assert _dtype_of(ids) == 4, "the assembly ring writes int32 ids"
+        self._ring_keep = bufs
+        if lib().hfmio_loader_start_ring(self._h, n, arr([b[0] for b in bufs]), arr([b[1] for b in bufs]),
+                                         arr([b[2] for b in bufs]), 1 if compact else 0) != 0:
+            raise IOError(_err())
+
+    def ring_take(self) -> Tuple[int, int, int]:
+        """(rows, slot, mask) of the next assembled slot (blocks; the GIL is released); rows 0 at
+        the end.  The slot's buffers are the caller's until ``ring_give(slot)``."""
+        slot, m = C.c_int(0), C.c_uint64(0)
+        r = lib().hfmio_loader_ring_take(self._h, C.addressof(slot), C.addressof(m))
+        if r < 0:
+            raise IOError(_err())
+        return r, slot.value, int(m.value)
+
+    def ring_give(self, slot: int) -> None:
+        lib().hfmio_loader_ring_give(self._h, int(slot))
 
     def __iter__(self) -> Iterator[Tuple[np.ndarray, np.ndarray, np.ndarray]]:
         while True:

@@ -297,6 +297,14 @@ class _DeviceFeeder:
             assert lab.shape == (B,) and lab.dtype == torch.float32
             assert ids.shape == (B, F) and ids.dtype == id_dtype
             assert vals.shape == (B, F) and vals.dtype == torch.float32
+        # ring mode with int32 ids: the loader assembles ahead into the pinned buffers on its own
+        # C++ thread (NativeLoader.start_ring), so this feeder's per-batch Python work overlaps
+        # the next batch's assembly instead of alternating with it
+        self.asm = (ring is not None and id_dtype == torch.int32 and knob("HIPFM_ASM_RING") == "1"
+                    and hasattr(loader, "start_ring"))
+        if self.asm:
+            loader.start_ring([(lab, ids, self.pstage[i] if self.compact else vals)
+                               for i, (lab, ids, vals) in enumerate(self.ring)], compact=self.compact)
         self.done = [None] * depth
         self.h2d_s = 0.0         # host time spent issuing copies (the copies themselves are async)
         self.h2d_bytes = 0       # host-to-device bytes of the ring copies (the wire format's size)
@@ -307,10 +315,74 @@ class _DeviceFeeder:
         self._stop = False
         self._th = None
 
+    def _issue(self, R, k: int, slot: int, mask):
+        """Copy pinned buffer ``slot`` (a full batch) into ring slot k % nslots on the next copy
+        stream (compact values expanded there); returns the copy's event, or None when the feeder
+        stopped before the ring slot was free (the slot is handed back untouched)."""
+        s = k % R.nslots
+        wait = R.acquire(s, lambda: self._stop)
+        if wait is _DeviceRing.STOPPED:      # stopped before the slot was taken
+            return None, s
+        if self._stop:
+            # stopped right after taking slot s: hand it back untouched, or a later epoch's fill
+            # thread waits on it forever
+            R.giveback(s, wait)
+            return None, s
+        cs = self.copies[(k + 1) % len(self.copies)]
+        with torch.cuda.stream(cs):
+            if wait is not None:
+                cs.wait_event(wait)
+            if mask is None:
+                R.flat[s].copy_(self.pflat[slot], non_blocking=True)
+            else:
+                nb = R.wire_bytes(mask)
+                R.flat[s][:nb].copy_(self.pflat[slot][:nb], non_blocking=True)
+                from ..ops import kernels as K
+                K.expand_vals(R.stage[s], bin(mask).count("1"), mask, self.F, self.B, R.views[s][1])
+            ev = torch.cuda.Event()
+            ev.record(cs)
+        self.h2d_bytes += R.wire_bytes(mask or 0)
+        return ev, s
+
+    def _fill_asm(self, R, k: int):
+        """Ring mode over the loader's assembler thread: take assembled pinned slots in order,
+        issue their copies, hand each pinned slot back once its copy finished."""
+        from collections import deque
+        inflight = deque()                      # (pinned slot, copy event), in take order
+        depth = len(self.ring)
+        while True:
+            # the assembler fills slots in cyclic order: the oldest in-flight slot goes back first
+            while inflight and (len(inflight) >= depth - 1 or inflight[0][1].query()):
+                slot, ev = inflight.popleft()
+                ev.synchronize()
+                self.loader.ring_give(slot)
+            if self._stop:
+                return
+            r, slot, mask = self.loader.ring_take()      # (ctypes: the GIL is released)
+            if self._stop:
+                return
+            if r == self.B:
+                k += 1
+                R.next = k
+                ev, s = self._issue(R, k - 1, slot, mask if self.compact else None)
+                if ev is None:
+                    return
+                inflight.append((slot, ev))
+                self._full.put((("ring", s), r, ev))
+                continue
+            if r > 0 and self.compact:           # final partial batch: the plain path
+                from .native_io import expand_values
+                lab, ids, vals = self.ring[slot]
+                vals.numpy()[:r] = expand_values(self.pstage[slot].numpy(), r, self.F, mask)
+            self._full.put((slot, r, None))
+            return
+
     def _fill(self):
         try:
             R = self.dev_ring
             k = R.start() if R is not None else 0
+            if self.asm:
+                return self._fill_asm(R, k)
             while True:
                 slot = self._free.get()
                 if slot is None or self._stop:
@@ -328,32 +400,11 @@ class _DeviceFeeder:
                 else:
                     r = self.loader.next_into(lab, ids, vals)   # (ctypes: the GIL is released)
                 if R is not None and r == self.B:
-                    s = k % R.nslots
                     k += 1
                     R.next = k
-                    wait = R.acquire(s, lambda: self._stop)
-                    if wait is _DeviceRing.STOPPED:      # stopped before the slot was taken
+                    ev, s = self._issue(R, k - 1, slot, mask)
+                    if ev is None:
                         return
-                    if self._stop:
-                        # stopped right after taking slot s: hand it back untouched, or a later
-                        # epoch's fill thread waits on it forever
-                        R.giveback(s, wait)
-                        return
-                    cs = self.copies[k % len(self.copies)]
-                    with torch.cuda.stream(cs):
-                        if wait is not None:
-                            cs.wait_event(wait)
-                        if mask is None:
-                            R.flat[s].copy_(self.pflat[slot], non_blocking=True)
-                        else:
-                            nb = R.wire_bytes(mask)
-                            R.flat[s][:nb].copy_(self.pflat[slot][:nb], non_blocking=True)
-                            from ..ops import kernels as K
-                            K.expand_vals(R.stage[s], bin(mask).count("1"), mask, self.F, self.B,
-                                          R.views[s][1])
-                        self.h2d_bytes += R.wire_bytes(mask or 0)
-                        ev = torch.cuda.Event()
-                        ev.record(cs)
                     self.done[slot] = ev
                     self._free.put(slot)
                     self._full.put((("ring", s), r, ev))

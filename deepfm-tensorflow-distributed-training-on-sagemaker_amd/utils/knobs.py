@@ -65,6 +65,9 @@ KNOBS: Dict[str, Knob] = {
                         "bf16 + fp32 w, 24 B; fused gather tower; the FM terms then read bf16-rounded v)"),
     "HIPFM_WIRE_COMPACT": Knob("1", "variant", "streamed input: a batch ships only the value columns of "
                                "fields not all 1.0 (expanded on the device; lossless) | 0: full [B, F] values"),
+    "HIPFM_ASM_RING": Knob("1", "variant", "streamed input: the loader's C++ assembler thread fills the "
+                           "pinned buffers ahead of the copy-issuing thread (0: that thread assembles "
+                           "each batch itself, next_into)"),
     "HIPFM_TF1_SPLIT": Knob("1", "variant", "tf1_dense on one GPU: split form (0: gradient scatter + "
                             "full-table sweep, the oracle in tests/test_gpu_tf1.py)"),
     "HIPFM_SWEEP_MODE": Knob("auto", "variant", "tf1_dense split sweep: merged (workgroups of the "

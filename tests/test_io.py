@@ -172,6 +172,72 @@ def test_compact_values_are_lossless(tmp_path, threads, drop):
     comp.close()
 
 
+@pytest.mark.parametrize("compact,threads", [(False, 1), (True, 3)])
+def test_assembly_ring_matches_next_into(tmp_path, compact, threads):
+    """hfm_io.cpp Loader::start_ring: an assembler thread fills registered buffers ahead of the
+    consumer in cyclic slot order; ring_take returns the same batches, in the same order, as
+    next_into (values compact or not), whatever order the consumer holds and hands slots back in.
+    A loader destroyed while its assembler waits for a slot, and a bad id, end cleanly."""
+    F, B = 5, 128
+    files = []
+    for k in range(3):
+        lab, ids, vals = _rows(700 + 41 * k, F, k)
+        ids = ids % 50_000
+        vals[:, 0] = 1.0
+        p = str(tmp_path / f"a-{k}.tfrecords")
+        nio.write_examples(p, lab, ids, vals)
+        files.append(p)
+    want = []
+    ld = nio.NativeLoader(files, F, B, threads=threads, drop_remainder=False, ids32=True)
+    while True:
+        bl, bi, bv = np.empty(B, np.float32), np.empty((B, F), np.int32), np.empty((B, F), np.float32)
+        r = ld.next_into(bl, bi, bv)
+        if r == 0:
+            break
+        want.append((bl[:r].copy(), bi[:r].copy(), bv[:r].copy()))
+    ld.close()
+    n = 4
+    bufs = [(np.empty(B, np.float32), np.empty((B, F), np.int32), np.empty(B * F, np.float32)) for _ in range(n)]
+    ld = nio.NativeLoader(files, F, B, threads=threads, drop_remainder=False, ids32=True)
+    ld.start_ring(bufs, compact=compact)
+    got, held = [], []
+    while True:
+        r, slot, mask = ld.ring_take()
+        if r == 0:
+            break
+        bl, bi, bv = bufs[slot]
+        vals = nio.expand_values(bv, r, F, mask) if compact else bv[:r * F].reshape(r, F)
+        if compact:
+            assert not mask & 1                       # field 0 is all 1.0: never shipped
+        got.append((bl[:r].copy(), bi[:r].copy(), vals.copy()))
+        held.append(slot)
+        if len(held) == n - 1:                     # hand back the oldest two (out of take order)
+            ld.ring_give(held.pop(1))
+            ld.ring_give(held.pop(0))
+    for s in held:
+        ld.ring_give(s)
+    assert ld.ring_take()[0] == 0                  # the end stays the end
+    ld.close()
+    assert len(got) == len(want)
+    for (a1, a2, a3), (b1, b2, b3) in zip(got, want):
+        assert np.array_equal(a1, b1) and np.array_equal(a2, b2)
+        assert np.array_equal(a3.view(np.uint32), b3.view(np.uint32))
+    # destroyed while the assembler waits for a slot (every slot taken, none given back)
+    ld = nio.NativeLoader(files, F, B, threads=threads, ids32=True)
+    ld.start_ring(bufs[:2], compact=compact)
+    ld.ring_take()
+    ld.ring_take()
+    ld.close()
+    # a decode error reaches the taker
+    ld = nio.NativeLoader(files, F, B, threads=threads, ids32=True, id_limit=10)
+    ld.start_ring(bufs[:2], compact=compact)
+    with pytest.raises(IOError, match="outside"):
+        for _ in range(20):
+            r, slot, _ = ld.ring_take()
+            ld.ring_give(slot)
+    ld.close()
+
+
 def test_record_shard_matches_reference_semantics(tmp_path):
     F = 3
     lab, ids, vals = _rows(50, F, 9)
