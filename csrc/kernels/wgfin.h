@@ -22,7 +22,7 @@
 #include "mma32.h"
 #include "sync.h"
 
-constexpr int WGF_MAXC = 264;   // head columns (last deep layer + 2)
+constexpr int WGF_MAXC = 512;   // head columns (last deep layer + 2): two per thread of the head workgroup
 constexpr int WGF_MAXNS = 8;    // workgroup splits of the batch per tile
 
 struct WgFinJob {
@@ -235,27 +235,34 @@ __device__ __forceinline__ void wgfin_body(const WgFinArgs& a, int b, WgfSmem& s
   } else if (b == a.tile_wgs) {
     // head partials [nhead][L + 2]: columns 0..L-1 -> deep_out weights, L -> deep_out bias and
     // fm_bias (both d/dy of the logit), L + 1 -> the loss sum.  Row chunks go through LDS with
-    // coalesced loads (all in flight); thread c keeps column c's sum in row order (deterministic).
+    // coalesced loads (all in flight); thread t keeps columns t and t + 256 (a last layer of 256
+    // has 258 columns), each summed in row order (deterministic).
     float* buf = &sm.red[0][0][0];
     const int C = a.L + 2;
     const int rows = (4 * 32 * 33) / C;
-    float acc = 0.f;
+    float acc[2] = {0.f, 0.f};
     for (int r0 = 0; r0 < a.nhead; r0 += rows) {
       const int nr = min(rows, a.nhead - r0);
       __syncthreads();
       for (int e = tid; e < nr * C; e += 256) buf[e] = a.partial[(size_t)r0 * C + e];
       __syncthreads();
-      if (tid < C)
-        for (int r = 0; r < nr; ++r) acc += buf[r * C + tid];
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int c = tid + 256 * k;
+        if (c < C)
+          for (int r = 0; r < nr; ++r) acc[k] += buf[r * C + c];
+      }
     }
-    if (tid < C) {
-      const float v = acc;
-      if (tid < a.L) {
-        wgf_apply<OPT>(a, lr_t, a.g_wout + tid, v);
-      } else if (tid == a.L) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int c = tid + 256 * k;
+      const float v = acc[k];
+      if (c < a.L) {
+        wgf_apply<OPT>(a, lr_t, a.g_wout + c, v);
+      } else if (c == a.L) {
         wgf_apply<OPT>(a, lr_t, a.g_bout, v);
         wgf_apply<OPT>(a, lr_t, a.g_fmbias, v);
-      } else {
+      } else if (c == a.L + 1) {
         *a.loss_sum = v;
       }
     }
