@@ -322,7 +322,7 @@ __global__ void sh_serve_kernel(const int* __restrict__ recv_ids, int total, int
                                 long ldw, float* __restrict__ rows, const int64_t* __restrict__ step,
                                 ShTable T, int stamp_off, int vbf16, int rbf16, unsigned char* rflag) {
   const ShServeArgs A{recv_ids, total, N, C, rstride, tv, tw, ldv, ldw, rows, step, T, stamp_off, vbf16, rbf16,
-                      rflag};
+                      0, rflag};
   sh_serve_elem<K>(A, blockIdx.x * blockDim.x + threadIdx.x);
 }
 

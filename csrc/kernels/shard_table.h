@@ -70,6 +70,7 @@ struct ShServeArgs {
   int stamp_off;          // 1: served at its own step's start; 2: served ahead (previous step)
   int vbf16;              // the TABLE's v rows are bf16
   int rbf16;              // served rows carry v as bf16 (compact rows)
+  int rdiv;               // local row = id / rdiv (0: N, the row-sharded owner; 1: a replicated table)
   unsigned char* rflag;   // tf1_dense split form: byte flag of every row requested this step (the
                           // owner launch's sweep skips and clears it), or null
 };
@@ -99,6 +100,17 @@ __device__ __forceinline__ void sh_put_row(float* o, int sub, f32x4 v, float w, 
   }
 }
 
+// tag only (rows == null; the replicated exchange's run steps): request gt of this step recorded
+// in the table, one thread per request
+__device__ __forceinline__ void sh_tag_elem(const ShServeArgs& A, int gt) {
+  if (gt >= A.total || !A.T.key) return;
+  const int id = sh_rid(A.recv_ids, gt, A.C, A.rstride);
+  if (id < 0) return;
+  const unsigned row = (unsigned)(id / (A.rdiv > 0 ? A.rdiv : A.N));
+  sh_insert(A.T, A.N, row, gt / A.C, (unsigned)(gt % A.C), (unsigned)(*A.step + A.stamp_off));
+  if (A.rflag) A.rflag[row] = 1;
+}
+
 // thread gt of a serve: request gt / (K/4), f32x4 column gt % (K/4)
 template <int K>
 __device__ __forceinline__ void sh_serve_elem(const ShServeArgs& A, int gt) {
@@ -109,7 +121,7 @@ __device__ __forceinline__ void sh_serve_elem(const ShServeArgs& A, int gt) {
   f32x4 v = {0.f, 0.f, 0.f, 0.f};
   float w = 0.f;
   if (id >= 0) {
-    const size_t row = (size_t)(id / A.N);
+    const size_t row = (size_t)(id / (A.rdiv > 0 ? A.rdiv : A.N));
     v = ld_row4(A.tv + row * A.ldv, sub * 4, A.vbf16);
     if (sub == 0) {
       w = A.tw[row * A.ldw];

@@ -915,7 +915,8 @@ __device__ __forceinline__ bool tower_aux_wg(const TowerArgs& a) {
   const int sb = (int)blockIdx.x - a.M / TW_ROWS;
   if (sb < 0) return false;
   if (sb < a.serve_wgs) {
-    sh_serve_elem<KE>(a.sv, sb * 256 + tid);
+    if (a.sv.rows) sh_serve_elem<KE>(a.sv, sb * 256 + tid);
+    else sh_tag_elem(a.sv, sb * 256 + tid);
     return true;
   }
   const int i0 = (sb - a.serve_wgs) * 256 * TW_STAMP_EPT + tid;
@@ -972,8 +973,9 @@ __global__ void __launch_bounds__(256) tower_kernel(TowerArgs a) {
   if constexpr (KE > 0) {
     const int sb = (int)blockIdx.x - a.M / TW_ROWS;
     if (sb >= 0) {
-      if (sb < a.serve_wgs) {  // a serve workgroup (run-routed sharded step)
-        sh_serve_elem<KE>(a.sv, sb * 256 + tid);
+      if (sb < a.serve_wgs) {  // a serve workgroup (run-routed sharded step) or a tag one (replicated)
+        if (a.sv.rows) sh_serve_elem<KE>(a.sv, sb * 256 + tid);
+        else sh_tag_elem(a.sv, sb * 256 + tid);
         return;
       }
       const int i0 = (sb - a.serve_wgs) * 256 * TW_STAMP_EPT + tid;  // a stamp workgroup
@@ -1225,7 +1227,7 @@ static int tower_launch(const TowerArgs& a, int KE, hipStream_t st) {
       default: return (int)hipErrorInvalidValue;
     }
   }
-  if (!FP8 && a.serve_wgs > 0) {
+  if (!FP8 && a.serve_wgs > 0 && a.sv.rows) {   // (tag-only workgroups: the default tower)
     switch (KE) {
       case 4: hipLaunchKernelGGL((tower_light_kernel<4>), g, blk, a.lds_bytes, st, a); return 0;
       case 8: hipLaunchKernelGGL((tower_light_kernel<8>), g, blk, a.lds_bytes, st, a); return 0;
@@ -1322,9 +1324,11 @@ HFM_API int hfm_tower(const TowerArgs* ap, int KE, hipStream_t st) {
     if (a.Np[i] % 32 || a.Np[i] <= 0) return (int)hipErrorInvalidValue;
   if (a.Np[a.nl - 1] % 8) return (int)hipErrorInvalidValue;
   if (a.lds_bytes > 160 * 1024 - 1024) return (int)hipErrorInvalidValue;
-  if (a.serve_wgs < 0 || (a.serve_wgs && (!KE || !a.train || !a.sv.recv_ids || !a.sv.rows || !a.sv.step ||
-                                          !a.sv.T.key || a.sv.C <= 0 || a.sv.stamp_off != 2 ||
-                                          (long)a.serve_wgs * 256 < (long)a.sv.total * (KE / 4))))
+  // serve workgroups: the next step's rows served ahead (stamp 2), or -- rows == null -- this step's
+  // requests tagged (stamp 1: the replicated exchange's run steps)
+  if (a.serve_wgs < 0 || (a.serve_wgs && (!KE || !a.train || !a.sv.recv_ids || !a.sv.step || !a.sv.T.key ||
+                                          a.sv.C <= 0 || a.sv.stamp_off != (a.sv.rows ? 2 : 1) ||
+                                          (long)a.serve_wgs * 256 < (long)a.sv.total * (a.sv.rows ? KE / 4 : 1))))
     return (int)hipErrorInvalidValue;
   int hbytes = 0;
   for (int i = 0; i < a.nl; ++i) hbytes += 2 * TW_ROWS * (a.Np[i] + 8);

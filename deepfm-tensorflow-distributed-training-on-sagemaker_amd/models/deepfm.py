@@ -920,6 +920,10 @@ class NativeDeepFM(GraphRunnerMixin, NativeStateMixin):
                 # run-routed step: the next step's rows served by extra tower workgroups
                 ta.sv, self.shx.tower_serve = self.shx.tower_serve, None
                 ta.serve_wgs = -(-ta.sv.total * (self.K // 4) // 256)
+            elif self.rpx is not None and (sv := self.rpx.tower_tags()) is not None:
+                # replicated run step: this step's requests tagged by extra tower workgroups
+                ta.sv = sv
+                ta.serve_wgs = -(-sv.total // 256)         # (one thread per request)
             if self._tower_stamp is not None:
                 # tf1_dense run-sorted step: this batch's row flags set by extra tower workgroups
                 keys, n, flags = self._tower_stamp

@@ -128,7 +128,7 @@ class ShServeArgs(C.Structure):
     _fields_ = [("recv_ids", c_void_p), ("total", c_int), ("N", c_int), ("C", c_int), ("rstride", c_int),
                 ("tv", c_void_p), ("tw", c_void_p), ("ldv", c_long), ("ldw", c_long), ("rows", c_void_p),
                 ("step", c_void_p), ("T", ShTable), ("stamp_off", c_int), ("vbf16", c_int),
-                ("rbf16", c_int), ("rflag", c_void_p)]
+                ("rbf16", c_int), ("rdiv", c_int), ("rflag", c_void_p)]
 
 
 class ShApplyArgs(C.Structure):

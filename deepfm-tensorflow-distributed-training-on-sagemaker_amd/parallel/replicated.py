@@ -82,6 +82,15 @@ class ReplicatedExchange:
         self.run_sets = []               # run-level routing: (sid_incl, upos, send_ids, ...) per step
         self._run_descs = {}
         self._run_j = None               # the step of the run being enqueued (runner)
+        # run-level routing: every step's unique ids packed [G][C] (run_sets' send_ids are views),
+        # all-gathered ONCE at the run start into [N][G][C]; each step's requests are then tagged
+        # by workgroups of its own tower launch (lazy rows), off the owner update's chain, and the
+        # step's exchange carries gradient rows (+ dense) only
+        self.run_ids = None
+        self.g_run_ids = None
+        self._run_G = 0
+        self._retired = []               # buffers of earlier run layouts (captured graphs use them)
+        self._tagged = False
 
     def _issue(self, ops):
         if self.trace is not None:
@@ -94,9 +103,18 @@ class ReplicatedExchange:
         its start (``sets``: the runner's (sorted keys, perm, inverse) per step).  Not in a capture."""
         m = self.m
         i32 = dict(dtype=torch.int32, device=m.device)
+        if self.run_ids is None or self.run_ids.shape[0] < G:
+            if self.run_ids is not None:
+                self._retired.append((self.run_ids, self.g_run_ids, [dict(r) for r in self.run_sets]))
+                self._run_descs = {}
+            cap = max(G, 32)
+            self.run_ids = torch.full((cap, self.C), -1, **i32)
+            self.g_run_ids = torch.full((self.N * cap * self.C,), -1, **i32)
+            for j, rs in enumerate(self.run_sets):
+                rs["send_ids"] = self.run_ids[j]
         while len(self.run_sets) < G:
             self.run_sets.append(dict(sid=torch.zeros(m.M * m.F, **i32), upos=torch.zeros(m.M * m.F, **i32),
-                                      send_ids=torch.full((self.C,), -1, **i32), send_cnt=torch.zeros(1, **i32),
+                                      send_ids=self.run_ids[len(self.run_sets)], send_cnt=torch.zeros(1, **i32),
                                       num_u=torch.zeros(1, **i32),
                                       tcnt=torch.zeros(KN.sh_route_tiles(m.M * m.F) * 2, **i32)))
         if getattr(self, "_slot_sink", None) is None or self._slot_sink.numel() < m.M * m.F:
@@ -117,8 +135,33 @@ class ReplicatedExchange:
         return d
 
     def route_run(self, d, G: int, n: int):
-        """Unique rows + gradient-row positions of every batch of the run (three launches)."""
+        """Unique rows + gradient-row positions of every batch of the run (three launches), then
+        one all-gather of the run's ids (G0)."""
         KN.sh_route_run(d, G, n, 1, self.C, self.err, self.C, self.m.F, 0)
+        self._run_G = G
+        self._issue([(KN.COMM_ALLGATHER, self.run_ids[:G], self.g_run_ids[: self.N * G * self.C], G * self.C * 4)])
+
+    def _run_recv(self):
+        """(ids pointer, rstride) of the current run step's gathered requests ([N][G][C])."""
+        G, C = self._run_G, self.C
+        return self.g_run_ids.data_ptr() + 4 * self._run_j * C, G * C
+
+    def tower_tags(self):
+        """ShServeArgs (rows == null: tag only) for the tower launch of the current run step:
+        its workgroups after the tower's blocks record this step's requests in the table, so the
+        owner update needs no tag launch.  None outside a run step, or for tf1_dense (the tag
+        launch also flags the rows of its sweep)."""
+        m = self.m
+        if self._run_j is None or m.sparse_update != "lazy":
+            return None
+        from ..ops._lib import ShServeArgs
+        a = ShServeArgs()
+        a.recv_ids, a.rstride = self._run_recv()
+        a.total, a.N, a.C = self.N * self.C, self.N, self.C
+        a.rows, a.step, a.T = 0, m.step.data_ptr(), self.table
+        a.stamp_off, a.rdiv = 1, 1
+        self._tagged = True
+        return a
 
     def backward(self, B: int, dense=None, join=None, wgfin=None, dense_ar=None, overlap=None):
         """Sorted slots (m.sorted_keys / m.perm) -> unique gradient rows -> all-gather -> rank-
@@ -156,8 +199,14 @@ class ReplicatedExchange:
             KN.sparse_fused(m.K, KN.SF_EXCHANGE, m.opt_id, A)
         if join is not None and overlap is None:
             join()
-        ops = [(KN.COMM_ALLGATHER, send_ids, self.g_ids, self.C * 4),
-               (KN.COMM_ALLGATHER, self.send_g, self.g_rows, self.C * self.RW * 4)]
+        tagged, self._tagged = self._tagged, False
+        if self._run_j is not None:     # ids gathered at the run start
+            recv_ids, rstride = self._run_recv()
+            ops = [(KN.COMM_ALLGATHER, self.send_g, self.g_rows, self.C * self.RW * 4)]
+        else:
+            recv_ids, rstride = self.g_ids.data_ptr(), 0
+            ops = [(KN.COMM_ALLGATHER, send_ids, self.g_ids, self.C * 4),
+                   (KN.COMM_ALLGATHER, self.send_g, self.g_rows, self.C * self.RW * 4)]
         if wgfin is not None and dense_allreduce(self.N):
             ops.append((KN.COMM_ALLREDUCE, m.g[: m.P], m.g[: m.P], m.P * 4))   # dense.g: m.g, nsum 0
         elif wgfin is not None:
@@ -169,9 +218,11 @@ class ReplicatedExchange:
             ops.append((KN.COMM_ALLREDUCE, dense_ar, dense_ar, dense_ar.numel() * 4))
         self._issue(ops)
         S = ShApplyArgs()
-        S.recv_ids, S.total, S.N, S.C = self.g_ids.data_ptr(), self.N * self.C, self.N, self.C
-        S.rstride, S.rdiv = 0, 1
-        S.mode = (0 if (m.sparse_update == "lazy" or m.tf1_xsplit) else 1) | 2   # tags stamped in the launch
+        S.recv_ids, S.total, S.N, S.C = recv_ids, self.N * self.C, self.N, self.C
+        S.rstride, S.rdiv = rstride, 1
+        # the requests' tags: stamped by the tower launch's workgroups (run steps), else by a tag
+        # launch ahead of the update (mode bit 2)
+        S.mode = (0 if (m.sparse_update == "lazy" or m.tf1_xsplit) else 1) | (0 if tagged else 2)
         S.recv_g, S.table = self.g_rows.data_ptr(), self.table
         S.tv, S.tw = m.tv.data_ptr(), m.tw.data_ptr()
         S.s0v, S.s1v, S.s0w, S.s1w = (t.data_ptr() if t.numel() else 0 for t in m.sv)
@@ -194,7 +245,8 @@ class ReplicatedExchange:
 
     def step_bytes(self, run_steps: int = 1) -> dict:
         """Modelled traffic of one step per rank (see FixedCapacityExchange.step_bytes): this rank's
-        ids + gradient-row block + dense gradient, all-gathered to the N - 1 other ranks."""
+        ids + gradient-row block + dense gradient, all-gathered to the N - 1 other ranks (the ids
+        once per run, the run's share per step)."""
         N, P = self.N, self.m.P
         blk = self.C * 4 + self.C * self.RW * 4
         if dense_allreduce(N):
