@@ -476,8 +476,10 @@ HFM_API int hfm_sh_route(const int* sorted_keys, int n, int N, int C, int* tcnt,
 // G batches' routing (descriptors rb [G], device): count, scatter, slot rows -- three launches;
 // ostride: owner block stride of every batch's send_ids (>= C); F, ld: slot map layout (ld = 0:
 // row-major [n], else field-major [F][ld], ld >= n / F)
+// slot_rows == 0: no slot -> row maps (the replicated exchange reads its gradient rows by unique
+// index, never through them)
 HFM_API int hfm_sh_route_run(const ShRouteBatch* rb, int G, int n, int N, int C, int ostride, int F, int ld,
-                             unsigned* err, hipStream_t st) {
+                             int slot_rows, unsigned* err, hipStream_t st) {
   if (!rb || G <= 0 || G > 65535 || N < 1 || N > SH_MAXN || n <= 0 || C <= 0 || ostride < C || F <= 0 ||
       n % F || (ld && ld < n / F))
     return (int)hipErrorInvalidValue;
@@ -487,7 +489,8 @@ HFM_API int hfm_sh_route_run(const ShRouteBatch* rb, int G, int n, int N, int C,
   hipLaunchKernelGGL(sh_route_count_run_kernel, dim3(nt, G), dim3(SH_THREADS), 0, st, rb, n, N, nbits);
   hipLaunchKernelGGL(sh_route_scatter_run_kernel, dim3(nt, G), dim3(SH_THREADS), 0, st, rb, n, N, nbits, C, nt, err,
                      ostride);
-  hipLaunchKernelGGL(sh_slot_rows_run_kernel, dim3((n + 255) / 256, G), dim3(256), 0, st, rb, n, F, ld);
+  if (slot_rows)
+    hipLaunchKernelGGL(sh_slot_rows_run_kernel, dim3((n + 255) / 256, G), dim3(256), 0, st, rb, n, F, ld);
   HFM_LAUNCH_CHECK();
 }
 

@@ -581,7 +581,8 @@ __global__ void __launch_bounds__(256) sfwg_x_kernel(SfArgs A, WgFinArgs W, ShSe
   const int nw = W.tile_wgs + 1;
   if ((int)blockIdx.x < nw) wgfin_body<-1, SFWG_PF, SFWG_MAXNS, SFWG_TQ>(W, blockIdx.x, sm.wg);
   else if ((int)blockIdx.x < nw + tiles) sf_tile_body<K, 2, 0>(A, (int)blockIdx.x - nw, sm.sf);
-  else sh_serve_elem<K>(S, ((int)blockIdx.x - nw - tiles) * 256 + (int)threadIdx.x);
+  else if (S.rows) sh_serve_elem<K>(S, ((int)blockIdx.x - nw - tiles) * 256 + (int)threadIdx.x);
+  else sh_tag_elem(S, ((int)blockIdx.x - nw - tiles) * 256 + (int)threadIdx.x);   // (replicated run step)
 }
 
 HFM_API int hfm_sparse_wgfin_x(int K, const SfArgs* A, const WgFinArgs* W, const ShServeArgs* S,
@@ -590,10 +591,12 @@ HFM_API int hfm_sparse_wgfin_x(int K, const SfArgs* A, const WgFinArgs* W, const
       W->kchunk % 32 || W->ldk != W->ns * 4 * W->kchunk || W->L + 2 > WGF_MAXC || !W->tile_ctr)
     return (int)hipErrorInvalidValue;
   const ShServeArgs sv = S ? *S : ShServeArgs{};
-  if (S && (!sv.recv_ids || !sv.rows || !sv.step || !sv.T.key || sv.total <= 0 || sv.stamp_off != 2 ||
+  // serve workgroups: the next step's rows (stamp 2), or -- rows == null -- this step's requests
+  // tagged for the owner update that follows (stamp 1: the replicated exchange's run steps)
+  if (S && (!sv.recv_ids || !sv.step || !sv.T.key || sv.total <= 0 || sv.stamp_off != (sv.rows ? 2 : 1) ||
             (sv.T.mask & (sv.T.mask + 1)) != 0 || sv.T.mask + 1 < 2u * (unsigned)sv.total))
     return (int)hipErrorInvalidValue;
-  const long sth = S ? (long)sv.total * (K / 4) : 0;
+  const long sth = S ? (long)sv.total * (sv.rows ? K / 4 : 1) : 0;
   const int swg = (int)((sth + 255) / 256);
 #define X_(KK)                                                                                    \
   hipLaunchKernelGGL(sfwg_x_kernel<KK>,                                                           \

@@ -265,7 +265,7 @@ _SIGS = {
     "hfm_sh_count_blocks": [c_int],
     "hfm_sh_route_tiles": [c_int],
     "hfm_sh_route": [c_void_p, c_int, c_int, c_int] + [c_void_p] * 7 + [c_void_p],
-    "hfm_sh_route_run": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
+    "hfm_sh_route_run": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
     "hfm_sh_route_batch_bytes": [],
     "hfm_sh_bucket": [c_void_p, c_void_p, c_int, c_int, c_int] + [c_void_p] * 5 + [c_void_p],
     "hfm_sh_slot_rows": [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p],

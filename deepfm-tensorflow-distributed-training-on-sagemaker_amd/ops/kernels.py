@@ -592,11 +592,14 @@ def sh_route(sorted_keys, n, N, Cap, tcnt, sid_incl, send_ids, upos, send_cnt, n
                            ptr(send_cnt), ptr(num_u), ptr(err), stream_handle()), "sh_route")
 
 
-def sh_route_run(descs_dev, G: int, n: int, N: int, Cap: int, err, ostride: int, F: int, ld: int = 0):
+def sh_route_run(descs_dev, G: int, n: int, N: int, Cap: int, err, ostride: int, F: int, ld: int = 0,
+                 slot_rows: bool = True):
     """Routing of G batches (``descs_dev``: device array of ``_lib.ShRouteBatch``) in three
     launches: owner buckets (owner o's ids at send_ids + o * ostride), unique indices and the slot
-    -> row maps of every batch (row-major, or field-major [F][ld] with ``ld``)."""
-    check(L().hfm_sh_route_run(ptr(descs_dev), G, n, N, Cap, ostride, F, ld, ptr(err), stream_handle()),
+    -> row maps of every batch (row-major, or field-major [F][ld] with ``ld``; not with
+    ``slot_rows=False``)."""
+    check(L().hfm_sh_route_run(ptr(descs_dev), G, n, N, Cap, ostride, F, ld, 1 if slot_rows else 0, ptr(err),
+                               stream_handle()),
           "sh_route_run")
 
 

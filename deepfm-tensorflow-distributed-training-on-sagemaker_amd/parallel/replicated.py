@@ -137,7 +137,7 @@ class ReplicatedExchange:
     def route_run(self, d, G: int, n: int):
         """Unique rows + gradient-row positions of every batch of the run (three launches), then
         one all-gather of the run's ids (G0)."""
-        KN.sh_route_run(d, G, n, 1, self.C, self.err, self.C, self.m.F, 0)
+        KN.sh_route_run(d, G, n, 1, self.C, self.err, self.C, self.m.F, 0, slot_rows=False)
         self._run_G = G
         self._issue([(KN.COMM_ALLGATHER, self.run_ids[:G], self.g_run_ids[: self.N * G * self.C], G * self.C * 4)])
 
@@ -147,10 +147,19 @@ class ReplicatedExchange:
         return self.g_run_ids.data_ptr() + 4 * self._run_j * C, G * C
 
     def tower_tags(self):
-        """ShServeArgs (rows == null: tag only) for the tower launch of the current run step:
-        its workgroups after the tower's blocks record this step's requests in the table, so the
-        owner update needs no tag launch.  None outside a run step, or for tf1_dense (the tag
-        launch also flags the rows of its sweep)."""
+        """Tag-only ShServeArgs for the tower launch of the current run step (when its sparse
+        backward is not the fused sfwg_x launch, which takes them itself): workgroups after the
+        tower's blocks record this step's requests in the table, so the owner update needs no tag
+        launch."""
+        if self.m._sp.xfuse:
+            return None
+        a = self._tag_args()
+        self._tagged = a is not None
+        return a
+
+    def _tag_args(self):
+        """ShServeArgs with rows == null (tag only) of the current run step's gathered requests;
+        None outside a run step, or for tf1_dense (the tag launch also flags its sweep's rows)."""
         m = self.m
         if self._run_j is None or m.sparse_update != "lazy":
             return None
@@ -160,7 +169,6 @@ class ReplicatedExchange:
         a.total, a.N, a.C = self.N * self.C, self.N, self.C
         a.rows, a.step, a.T = 0, m.step.data_ptr(), self.table
         a.stamp_off, a.rdiv = 1, 1
-        self._tagged = True
         return a
 
     def backward(self, B: int, dense=None, join=None, wgfin=None, dense_ar=None, overlap=None):
@@ -194,7 +202,11 @@ class ReplicatedExchange:
             main.wait_stream(side)
             dense_ar = None
         elif wgfin is not None:
-            KN.sparse_wgfin_x(m.K, A, wgfin)
+            # run steps: this step's requests tagged by the launch's last workgroups (dispatched
+            # into the CUs the sparse tiles' tail leaves idle)
+            tags = self._tag_args()
+            KN.sparse_wgfin_x(m.K, A, wgfin, serve=tags)
+            self._tagged = self._tagged or tags is not None
         else:
             KN.sparse_fused(m.K, KN.SF_EXCHANGE, m.opt_id, A)
         if join is not None and overlap is None:
