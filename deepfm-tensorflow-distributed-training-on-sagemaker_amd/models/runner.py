@@ -330,13 +330,15 @@ class GraphRunnerMixin:
 
     def _run_sort_ok(self, batches) -> bool:
         """The run's batches can be sorted up front (fsort_run.h): one GPU or the replicated-table
-        exchange (its routing of the unique rows runs per step on the sorted keys), lazy rows (or,
-        one GPU, the tf1_dense split form with its sweep merged into the sparse launch), field
-        ranges, equal batch sizes of at most 8 sort chunks."""
-        replicated = self.rpx is not None and self.sparse_update == "lazy"
+        exchange (its routing of the unique rows runs at the run start too), lazy rows (or the
+        tf1_dense split form: one GPU with its sweep merged into the sparse launch, replicated with
+        its sweep in the owner launch), field ranges, equal batch sizes of at most 8 sort chunks."""
+        # (replicated tf1_dense: the split form, its requested rows flagged by the run step's tag
+        # workgroups and every other row swept by the owner launch)
+        replicated = self.rpx is not None and (self.sparse_update == "lazy" or self.tf1_xsplit)
         if not (self._knobs().run_sort and len(batches) > 1 and self._fsort_next is not None and not self.sharded and
                 self.shx is None and (replicated or (self.rpx is None and not self.exchange)) and
-                self.lazy_rows and self._knobs().sort_side_stream):
+                (self.lazy_rows or replicated) and self._knobs().sort_side_stream):
             return False
         B = batches[0][0].shape[0]
         kn, mode = self._knobs(), self._mode_spec()

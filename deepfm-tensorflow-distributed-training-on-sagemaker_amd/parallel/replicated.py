@@ -158,10 +158,11 @@ class ReplicatedExchange:
         return a
 
     def _tag_args(self):
-        """ShServeArgs with rows == null (tag only) of the current run step's gathered requests;
-        None outside a run step, or for tf1_dense (the tag launch also flags its sweep's rows)."""
+        """ShServeArgs with rows == null (tag only) of the current run step's gathered requests
+        (tf1_dense split form: also flagging them for the owner launch's sweep); None outside a
+        run step."""
         m = self.m
-        if self._run_j is None or m.sparse_update != "lazy":
+        if self._run_j is None or not (m.sparse_update == "lazy" or m.tf1_xsplit):
             return None
         from ..ops._lib import ShServeArgs
         a = ShServeArgs()
@@ -169,6 +170,8 @@ class ReplicatedExchange:
         a.total, a.N, a.C = self.N * self.C, self.N, self.C
         a.rows, a.step, a.T = 0, m.step.data_ptr(), self.table
         a.stamp_off, a.rdiv = 1, 1
+        if m.tf1_xsplit:
+            a.rflag = m._xflags.data_ptr()
         return a
 
     def backward(self, B: int, dense=None, join=None, wgfin=None, dense_ar=None, overlap=None):

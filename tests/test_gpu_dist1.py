@@ -346,10 +346,12 @@ def test_bf16_exchange_rows(group, emb):
         assert not torch.equal(bv, lv)           # the bf16 reads did change the arithmetic
 
 
-def test_replicated_run_sort_bitwise(group, monkeypatch):
+@pytest.mark.parametrize("update", ["lazy", "tf1_dense"])
+def test_replicated_run_sort_bitwise(group, monkeypatch, update):
     """Replicated-table exchange (config #3) on the run-level sort: every batch of a multi-step
-    graph sorted at the graph's start, each step then routes its unique rows from its run set --
-    one queue, no per-step sort branch.  Bitwise the per-step prefetched-sort path."""
+    graph sorted and routed at the graph's start, its ids gathered once, each step's requests
+    tagged by its own sparse launch (tf1_dense split form: flagged for the owner launch's sweep
+    too) -- one queue, no per-step sort branch.  Bitwise the per-step prefetched-sort path."""
     import hipfm.models.deepfm as D
     synth = make_synth("total:6000", seed=53)
     F, K, layers, keep = synth.F, 8, [64, 32], [0.8, 0.8]
@@ -359,11 +361,11 @@ def test_replicated_run_sort_bitwise(group, monkeypatch):
     out = []
     for run in (True, False):
         monkeypatch.setattr(D, "_RUN_SORT", run)
-        m = NativeDeepFM(V, F, K, layers, keep, sparse_update="lazy", batch_size=512, device="cuda",
+        m = NativeDeepFM(V, F, K, layers, keep, sparse_update=update, batch_size=512, device="cuda",
                          init=False, comm=Comm(sharded=False, force_exchange=True),
                          field_ranges=synth.field_ranges())
         m.load_tf_params(params)
-        assert m.rpx is not None
+        assert m.rpx is not None and (update == "lazy" or m.tf1_xsplit)
         for _ in range(3):
             m.train_steps(pool, next_ids=pool[0][0])
         torch.cuda.synchronize()

@@ -478,14 +478,14 @@ def test_replicated_exchange_matches_global_batch(N, opt, update, fused, run):
         models.append(m)
     if run:      # one run per rank: run-level sort + routing of every batch at the run start (lazy)
         _run_ranks_steps(models, batches)
-        assert update != "lazy" or len(models[0].rpx.run_sets) == steps
+        assert len(models[0].rpx.run_sets) == steps
     else:
         _run_ranks(models, batches, prefetch=True)
     torch.cuda.synchronize()
     for m in models:
         m.check_errors()
         # (run mode: one more group at the run start, the all-gather of every step's ids)
-        assert m.rpx.trace == models[0].rpx.trace and len(m.rpx.trace) == steps + (1 if run and update == "lazy" else 0)
+        assert m.rpx.trace == models[0].rpx.trace and len(m.rpx.trace) == steps + (1 if run else 0)
         for a, b in ((m.tv, models[0].tv), (m.tw, models[0].tw), (m.p, models[0].p)):
             assert torch.equal(a, b)                          # replicas bitwise identical
     m = models[0]
