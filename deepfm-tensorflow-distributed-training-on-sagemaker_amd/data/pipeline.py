@@ -35,6 +35,7 @@ import numpy as np
 import torch
 
 from .native_io import FMT_LIBSVM, FMT_TFRECORD, NativeLoader, count_records
+from ..utils.capture import CAPTURE_LOCK
 from ..utils.knobs import knob
 
 _H2D_STREAMS = int(knob("HIPFM_H2D_STREAMS"))
@@ -329,7 +330,7 @@ class _DeviceFeeder:
             R.giveback(s, wait)
             return None, s
         cs = self.copies[(k + 1) % len(self.copies)]
-        with torch.cuda.stream(cs):
+        with CAPTURE_LOCK, torch.cuda.stream(cs):     # (never inside a graph capture)
             if wait is not None:
                 cs.wait_event(wait)
             if mask is None:
@@ -351,10 +352,15 @@ class _DeviceFeeder:
         inflight = deque()                      # (pinned slot, copy event), in take order
         depth = len(self.ring)
         while True:
-            # the assembler fills slots in cyclic order: the oldest in-flight slot goes back first
-            while inflight and (len(inflight) >= depth - 1 or inflight[0][1].query()):
+            # the assembler fills slots in cyclic order: the oldest in-flight slot goes back first,
+            # once two newer copies are queued behind it (long finished by then: the wait is a
+            # formality).  No event queries: hipEventQuery from this thread while the training
+            # thread captures a run graph invalidated the capture (hipErrorStreamCaptureInvalidated
+            # in the one-process GPU suite); the synchronize the old path used is safe.
+            while len(inflight) > 2 or (inflight and len(inflight) >= depth - 1):
                 slot, ev = inflight.popleft()
-                ev.synchronize()
+                with CAPTURE_LOCK:
+                    ev.synchronize()
                 self.loader.ring_give(slot)
             if self._stop:
                 return
@@ -389,7 +395,8 @@ class _DeviceFeeder:
                     return
                 ev = self.done[slot]
                 if ev is not None:
-                    ev.synchronize()                 # this pinned buffer's last copy is over
+                    with CAPTURE_LOCK:
+                        ev.synchronize()             # this pinned buffer's last copy is over
                 lab, ids, vals = self.ring[slot]
                 mask = None
                 if self.compact:

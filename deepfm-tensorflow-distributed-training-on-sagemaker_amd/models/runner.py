@@ -26,6 +26,7 @@ import math
 import torch
 
 from ..ops import kernels as KN
+from ..utils.capture import CAPTURE_LOCK
 from .step_plan import sfwg_possible, sweep_merges
 
 
@@ -40,9 +41,9 @@ def graph_capture(g):
     was = gc.isenabled()
     gc.disable()
     try:
-        # thread-local capture: the input pipeline's fill thread keeps issuing its host-to-device
-        # copies and event calls on its own stream while a run is captured here
-        with torch.cuda.graph(g, capture_error_mode="thread_local"):
+        # no GPU work issued by other threads of this process while a run is captured (the input
+        # pipeline's fill thread takes the same lock around its copies: utils/capture.py)
+        with CAPTURE_LOCK, torch.cuda.graph(g, capture_error_mode="thread_local"):
             yield
     finally:
         if was:
