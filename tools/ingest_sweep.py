@@ -12,11 +12,11 @@ import hipfm  # noqa: E402,F401
 from hipfm.data.native_io import NativeLoader  # noqa: E402
 
 
-def rate(files, F, B, th, ct, n32=True):
+def rate(files, F, B, th, ct, n32=True, qd=4):
     lab = np.empty(B, np.float32)
     ids = np.empty((B, F), np.int32)
     vals = np.empty((B, F), np.float32)
-    ld = NativeLoader(files, F, B, threads=th, copy_threads=ct, ids32=n32)
+    ld = NativeLoader(files, F, B, threads=th, copy_threads=ct, ids32=n32, queue_depth=qd)
     rows, t0 = 0, time.perf_counter()
     while True:
         r = ld.next_into(lab, ids, vals)
@@ -33,10 +33,10 @@ def main():
     F = int(sys.argv[2]) if len(sys.argv) > 2 else 39
     B = int(sys.argv[3]) if len(sys.argv) > 3 else 16384
     files = sorted(glob.glob(f"{d}/tr*"))
-    for th, ct, n32 in ((16, 8, False), (8, 4, True), (12, 4, True), (12, 6, True), (16, 4, True), (16, 8, True),
-                        (14, 2, True), (24, 8, True)):
-        print(f"threads {th:2d} copy {ct} narrow-at-decode {n32}: {rate(files, F, B, th, ct, n32) / 1e6:.1f} M rows/s",
-              flush=True)
+    for rep in range(2):
+        for th, ct, qd in ((16, 8, 4), (16, 8, 16), (16, 8, 64), (16, 4, 16), (12, 4, 16), (24, 8, 16)):
+            print(f"threads {th:2d} copy {ct} queue depth {qd:2d}: {rate(files, F, B, th, ct, True, qd) / 1e6:.1f} M rows/s",
+                  flush=True)
 
 
 if __name__ == "__main__":
