@@ -12,8 +12,11 @@ fixed-capacity block, so no size ever crosses to the host and the whole step is 
             the local table by id) -- and, with the fused tower, the dense gradient in the same
             launch
   exchange: ONE grouped RCCL operation on the main stream: all-gather of the [C] ids and the
-            [C, K+4] gradient rows (+ the dense gradients: all-gather, summed in rank order by
-            the update launch; or all-reduce)
+            [C, K+1] gradient rows (+ the dense gradients: all-gather, summed in rank order by
+            the update launch; or all-reduce).  Run-sorted steps (multi-step graphs): every
+            step's ids are routed and all-gathered once at the run start, each step's requests
+            are tagged by extra workgroups of its sparse launch, and its group carries the
+            gradient rows (+ dense) only
   update  : every rank runs the owner-update kernel of the row-sharded path over all N ranks'
             blocks with ``rdiv = 1`` (local row = id): the lowest rank holding an id sums all
             ranks' rows IN RANK ORDER and applies the optimizer (lazy), or scatters into the
@@ -84,8 +87,8 @@ class ReplicatedExchange:
         self._run_j = None               # the step of the run being enqueued (runner)
         # run-level routing: every step's unique ids packed [G][C] (run_sets' send_ids are views),
         # all-gathered ONCE at the run start into [N][G][C]; each step's requests are then tagged
-        # by workgroups of its own tower launch (lazy rows), off the owner update's chain, and the
-        # step's exchange carries gradient rows (+ dense) only
+        # by extra workgroups of its own sparse launch (sfwg_x; else of its tower launch), off the
+        # owner update's chain, and the step's exchange carries gradient rows (+ dense) only
         self.run_ids = None
         self.g_run_ids = None
         self._run_G = 0
