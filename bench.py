@@ -596,10 +596,12 @@ def data_bench(args):
     est_s, per_epoch_s, pipe_s = train_arm(cache=False)    # every epoch streamed from the files
     # host-to-device bytes per streamed row (the last epoch's ring copies; HIPFM_WIRE_COMPACT)
     wire = round(pipe_s.h2d_bytes / max(1, per_epoch_s[-1][0] * B), 1)
+    fill = {"take_s": round(pipe_s.fill_take_s, 4), "issue_s": round(pipe_s.fill_issue_s, 4)}   # (last epoch)
     if args.stream_only:                               # (profiling the streamed path alone)
         _emit(json.dumps({"metric": "streamed epochs samples/s (1 GPU)", "ingest_rows_per_s": round(ingest, 1),
                           "streamed_epoch_samples_per_s": [round(n * B / t, 1) for n, t in per_epoch_s],
                           "epoch_s": [round(t, 4) for _, t in per_epoch_s], "wire_bytes_per_row": wire,
+                          "fill_thread_last_epoch": fill,
                           "host_timer_totals_s": {k: round(v, 4) for k, v in est_s.timer.t.items()},
                           "host_timer_calls": dict(est_s.timer.n)}))
         return

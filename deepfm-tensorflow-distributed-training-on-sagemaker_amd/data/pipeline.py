@@ -309,6 +309,8 @@ class _DeviceFeeder:
         self.done = [None] * depth
         self.h2d_s = 0.0         # host time spent issuing copies (the copies themselves are async)
         self.h2d_bytes = 0       # host-to-device bytes of the ring copies (the wire format's size)
+        self.fill_take_s = 0.0   # fill thread: waiting for assembled batches (the loader's pace)
+        self.fill_issue_s = 0.0  # fill thread: slot acquire + copy / expand / event issue
         import queue
         self._free, self._full = queue.Queue(), queue.Queue()
         for i in range(depth):
@@ -348,6 +350,7 @@ class _DeviceFeeder:
     def _fill_asm(self, R, k: int):
         """Ring mode over the loader's assembler thread: take assembled pinned slots in order,
         issue their copies, hand each pinned slot back once its copy finished."""
+        import time
         from collections import deque
         inflight = deque()                      # (pinned slot, copy event), in take order
         depth = len(self.ring)
@@ -364,13 +367,17 @@ class _DeviceFeeder:
                 self.loader.ring_give(slot)
             if self._stop:
                 return
+            t0 = time.perf_counter()
             r, slot, mask = self.loader.ring_take()      # (ctypes: the GIL is released)
+            t1 = time.perf_counter()
+            self.fill_take_s += t1 - t0
             if self._stop:
                 return
             if r == self.B:
                 k += 1
                 R.next = k
                 ev, s = self._issue(R, k - 1, slot, mask if self.compact else None)
+                self.fill_issue_s += time.perf_counter() - t1
                 if ev is None:
                     return
                 inflight.append((slot, ev))
@@ -551,6 +558,7 @@ class InputPipeline:
         self.from_cache = False                  # the epoch being iterated replays the cache
         self.h2d_s = 0.0                          # host time issuing H2D copies (last epoch)
         self.h2d_bytes = 0                        # ring copies' host-to-device bytes (last epoch)
+        self.fill_take_s = self.fill_issue_s = 0.0   # fill thread's wait / issue time (last epoch)
         self._fmin = self._fmax = None           # per-field id min / max over the first epoch
         self._stats_done = False
         # > 1: the consumer trains streamed batches in runs of this many steps and releases ring
@@ -650,6 +658,7 @@ class InputPipeline:
                 src.close()                  # (its fill thread reads the loader)
                 self.h2d_s = src.h2d_s
                 self.h2d_bytes = src.h2d_bytes
+                self.fill_take_s, self.fill_issue_s = src.fill_take_s, src.fill_issue_s
             loader.close()
         if stats:                    # (reached only when the epoch was read to its end)
             self._stats_done = True
