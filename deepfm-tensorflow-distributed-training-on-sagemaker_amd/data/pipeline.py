@@ -320,32 +320,37 @@ class _DeviceFeeder:
 
     def _issue(self, R, k: int, slot: int, mask):
         """Copy pinned buffer ``slot`` (a full batch) into ring slot k % nslots on the next copy
-        stream (compact values expanded there); returns the copy's event, or None when the feeder
+        stream (compact values expanded there); returns (event after the whole batch, ring slot,
+        event after the host-to-device copy alone: the pinned buffer is free again from there, the
+        expand kernel may queue behind a run's kernels), or (None, ring slot, None) when the feeder
         stopped before the ring slot was free (the slot is handed back untouched)."""
         s = k % R.nslots
         wait = R.acquire(s, lambda: self._stop)
         if wait is _DeviceRing.STOPPED:      # stopped before the slot was taken
-            return None, s
+            return None, s, None
         if self._stop:
             # stopped right after taking slot s: hand it back untouched, or a later epoch's fill
             # thread waits on it forever
             R.giveback(s, wait)
-            return None, s
+            return None, s, None
         cs = self.copies[(k + 1) % len(self.copies)]
         with CAPTURE_LOCK, torch.cuda.stream(cs):     # (never inside a graph capture)
             if wait is not None:
                 cs.wait_event(wait)
+            ev_copy = None
             if mask is None:
                 R.flat[s].copy_(self.pflat[slot], non_blocking=True)
             else:
                 nb = R.wire_bytes(mask)
                 R.flat[s][:nb].copy_(self.pflat[slot][:nb], non_blocking=True)
+                ev_copy = torch.cuda.Event()
+                ev_copy.record(cs)
                 from ..ops import kernels as K
                 K.expand_vals(R.stage[s], bin(mask).count("1"), mask, self.F, self.B, R.views[s][1])
             ev = torch.cuda.Event()
             ev.record(cs)
         self.h2d_bytes += R.wire_bytes(mask or 0)
-        return ev, s
+        return ev, s, (ev_copy or ev)
 
     def _fill_asm(self, R, k: int):
         """Ring mode over the loader's assembler thread: take assembled pinned slots in order,
@@ -376,11 +381,11 @@ class _DeviceFeeder:
             if r == self.B:
                 k += 1
                 R.next = k
-                ev, s = self._issue(R, k - 1, slot, mask if self.compact else None)
+                ev, s, ev_copy = self._issue(R, k - 1, slot, mask if self.compact else None)
                 self.fill_issue_s += time.perf_counter() - t1
                 if ev is None:
                     return
-                inflight.append((slot, ev))
+                inflight.append((slot, ev_copy))
                 self._full.put((("ring", s), r, ev))
                 continue
             if r > 0 and self.compact:           # final partial batch: the plain path
@@ -416,10 +421,10 @@ class _DeviceFeeder:
                 if R is not None and r == self.B:
                     k += 1
                     R.next = k
-                    ev, s = self._issue(R, k - 1, slot, mask)
+                    ev, s, ev_copy = self._issue(R, k - 1, slot, mask)
                     if ev is None:
                         return
-                    self.done[slot] = ev
+                    self.done[slot] = ev_copy
                     self._free.put(slot)
                     self._full.put((("ring", s), r, ev))
                     continue
