@@ -20,8 +20,6 @@
 #include <fcntl.h>
 #include <nmmintrin.h>
 #include <stdint.h>
-#include <sys/resource.h>
-#include <sys/syscall.h>
 #include <unistd.h>
 #include <stdio.h>
 #include <string.h>
@@ -436,11 +434,6 @@ static bool parse_libsvm(const std::string& line, int F, float* label, int64_t* 
 }
 
 // ------------------------------------------------------------------------------ loader
-// Nice increment of the decode workers (hfmio_set_decode_nice): they are throughput work, while
-// the consumer side (batch assembly, the Python threads issuing copies and training steps) is
-// latency-bound -- on an oversubscribed CPU share the workers yield to it.
-static std::atomic<int> g_decode_nice{0};
-
 struct Chunk {
   int n = 0;
   std::vector<float> label;
@@ -632,8 +625,6 @@ struct Loader {
   }
 
   void worker(int w, int W) {
-    if (const int nv = g_decode_nice.load())     // (per-thread on Linux; raising it needs no privilege)
-      (void)setpriority(PRIO_PROCESS, (id_t)syscall(SYS_gettid), nv);
     WorkerQueue& Q = *queues[w];
     auto push = [&](std::unique_ptr<Chunk> c) {
       std::unique_lock<std::mutex> lk(Q.m);
@@ -946,8 +937,6 @@ HFMIO_API int hfmio_loader_ring_take(void* h, int* slot, uint64_t* mask) {
   return r;
 }
 HFMIO_API void hfmio_loader_ring_give(void* h, int slot) { ((Loader*)h)->ring_give(slot); }
-
-HFMIO_API void hfmio_set_decode_nice(int n) { g_decode_nice.store(n < 0 ? 0 : (n > 19 ? 19 : n)); }
 
 // Assemble batches with n copy threads (the consumer plus n - 1 pool threads); 1: serial.
 HFMIO_API void hfmio_loader_set_copy_threads(void* h, int n) {

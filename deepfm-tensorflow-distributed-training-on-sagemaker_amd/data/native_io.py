@@ -10,7 +10,6 @@ from typing import Iterator, List, Optional, Sequence, Tuple
 import numpy as np
 
 from ..ops.build import IO_SO, build_io
-from ..utils.knobs import knob
 
 _lib = None
 _lock = threading.Lock()
@@ -52,9 +51,6 @@ def lib():
             L.hfmio_loader_ring_take.restype = ci
             L.hfmio_loader_ring_give.argtypes = [vp, ci]
             L.hfmio_loader_ring_give.restype = None
-            L.hfmio_set_decode_nice.argtypes = [ci]
-            L.hfmio_set_decode_nice.restype = None
-            L.hfmio_set_decode_nice(int(knob("HIPFM_DECODE_NICE")))
             L.hfmio_loader_destroy.argtypes = [vp]
             L.hfmio_loader_set_copy_threads.argtypes = [vp, ci]
             L.hfmio_loader_set_copy_threads.restype = None

@@ -79,8 +79,6 @@ KNOBS: Dict[str, Knob] = {
     "HIPFM_FSORT_PB": Knob(None, "tuning", "field sort MSD partitions per field, log2 (default: 0 on "
                            "one GPU, 2 for the sharded routing)"),
     "HIPFM_FS_MAX_PB": Knob("4", "tuning", "tools/bench_sort.py: field sort partitions per field"),
-    "HIPFM_DECODE_NICE": Knob("0", "tuning", "nice increment of the loader's decode worker threads (the "
-                              "batch assembly and the Python threads keep normal priority)"),
     "HIPFM_H2D_STREAMS": Knob("2", "tuning", "streamed input: copy streams the device-ring batches alternate over"),
     "HIPFM_GRAPH_STEPS": Knob("32", "tuning", "most training steps per captured HIP graph (bench.py)"),
     # ---- harness

@@ -1,5 +1,5 @@
 #!/bin/bash
-# streamed epochs vs the decode workers' nice increment (HIPFM_DECODE_NICE 0 / 5 / 10), 16M rows
+# streamed epochs vs the decode workers' nice increment (HIPFM_DECODE_NICE 0 / 5 / 10, a knob since removed: no reproducible effect), 16M rows
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 D=/tmp/hipfm_nice_$$
