@@ -51,6 +51,8 @@ def estimate_unique_capacity(id_batches: Iterable[torch.Tensor], slack: float = 
 class ReplicatedExchange:
     """Buffers + the backward/exchange/update piece of the replicated-table step (one rank)."""
 
+    RUN_CAP0 = 32        # steps the packed run-ids buffers are first sized for (grown on demand)
+
     def __init__(self, m, engine, capacity: Optional[int] = None):
         self.m, self.eng = m, engine
         self.N, self.rank = engine.world, engine.rank
@@ -108,9 +110,12 @@ class ReplicatedExchange:
         i32 = dict(dtype=torch.int32, device=m.device)
         if self.run_ids is None or self.run_ids.shape[0] < G:
             if self.run_ids is not None:
-                self._retired.append((self.run_ids, self.g_run_ids, [dict(r) for r in self.run_sets]))
+                # graphs captured from shorter runs keep using these buffers and the device
+                # descriptors that point at them: retired, never freed
+                self._retired.append((self.run_ids, self.g_run_ids, [dict(r) for r in self.run_sets],
+                                      self._run_descs))
                 self._run_descs = {}
-            cap = max(G, 32)
+            cap = max(G, self.RUN_CAP0)
             self.run_ids = torch.full((cap, self.C), -1, **i32)
             self.g_run_ids = torch.full((self.N * cap * self.C,), -1, **i32)
             for j, rs in enumerate(self.run_sets):

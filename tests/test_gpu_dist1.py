@@ -220,6 +220,38 @@ def test_exchange_growing_runs_keep_earlier_graphs_valid(group, monkeypatch):
         assert torch.equal(x, y)
 
 
+def test_replicated_growing_runs_keep_earlier_graphs_valid(group, monkeypatch):
+    """Replicated run steps: a run longer than the packed run-ids buffers regrows them; graphs
+    captured from shorter runs keep their own (retired) ids buffers and route descriptors, so
+    replaying them after the growth is bitwise the per-step path."""
+    import hipfm.models.deepfm as D
+    from hipfm.parallel.replicated import ReplicatedExchange
+    monkeypatch.setattr(ReplicatedExchange, "RUN_CAP0", 2)
+    synth = make_synth("total:6000", seed=39)
+    F, K, layers, keep = synth.F, 8, [64, 32], [0.8, 0.8]
+    V = synth.feature_size
+    params = init_params(V, F, K, layers, False, seed=11)
+    pool = [synth.batch(512, step=s, device="cuda", id_dtype=torch.int32) for s in range(6)]
+    order = [(0, 2), (2, 4), (0, 6), (2, 4), (4, 6), (0, 6), (2, 4)]
+    out = []
+    for run in (True, False):
+        monkeypatch.setattr(D, "_RUN_SORT", run)
+        m = NativeDeepFM(V, F, K, layers, keep, sparse_update="lazy", batch_size=512, device="cuda",
+                         init=False, comm=Comm(sharded=False, force_exchange=True),
+                         field_ranges=synth.field_ranges())
+        m.load_tf_params(params)
+        for lo, hi in order:
+            m.train_steps(pool[lo:hi], next_ids=pool[hi % 6][0])
+        torch.cuda.synchronize()
+        m.check_errors()
+        if run:
+            assert len(m.rpx._retired) >= 1 and m.rpx.run_ids.shape[0] >= 6     # the growth happened
+        out.append((m.tv.clone(), m.tw.clone(), m.p.clone(), m.step.clone()))
+        del m
+    for x, y in zip(*out):
+        assert torch.equal(x, y)
+
+
 @pytest.mark.parametrize("sharded", [True, False])
 def test_estimator_calibrates_exchange_capacity(group, tmp_path, sharded):
     """the CLI's multi-GPU path ran on default_capacity (1.5x slots / N, ~3-4x the
