@@ -231,7 +231,6 @@ def main():
     import hipfm
     from hipfm.data.synthetic import make_synth
     from hipfm.models.deepfm import NativeDeepFM
-    from hipfm.ops import kernels as KN
     from hipfm.ops.metrics import auc_from_hist
     from hipfm.parallel.dist import Comm, init_distributed
 

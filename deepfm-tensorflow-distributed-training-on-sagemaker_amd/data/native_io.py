@@ -5,7 +5,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 import threading
-from typing import Iterator, List, Optional, Sequence, Tuple
+from typing import Iterator, Optional, Sequence, Tuple
 
 import numpy as np
 
