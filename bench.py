@@ -187,10 +187,10 @@ def main():
     ap.add_argument("--embedding_mode", default="auto")
     ap.add_argument("--mlp_dtype", default="bf16", choices=["bf16", "fp8"],
                     help="deep-tower forward GEMM operands (fp8 = OCP e4m3 MFMA, config #5)")
-    ap.add_argument("--exchange_rows", default="bf16", choices=["fp32", "bf16"],
-                    help="row-sharded exchange (N > 1): the served rows' v in the compute dtype "
-                         "(bf16, half the G1 bytes over xGMI; owners keep fp32 master rows and "
-                         "Adam slots) or fp32 (the library default: bitwise the one-GPU reads)")
+    ap.add_argument("--exchange_rows", default="fp32", choices=["fp32", "bf16"],
+                    help="row-sharded exchange (N > 1): fp32 served rows (the default, the library's "
+                         "and the reference's precision: bitwise the one-GPU reads) or bf16 v (a "
+                         "labelled variant: half the G1 bytes; the FM terms then read bf16-rounded v)")
     ap.add_argument("--emb_dtype", default="fp32", choices=["fp32", "bf16"],
                     help="fm_v rows + optimizer slots (bf16 = mixed-precision embeddings, config #5)")
     ap.add_argument("--pool", type=int, default=128,
@@ -232,11 +232,11 @@ def main():
     from hipfm.data.synthetic import make_synth
     from hipfm.models.deepfm import NativeDeepFM
     from hipfm.ops.metrics import auc_from_hist
-    from hipfm.parallel.dist import Comm, init_distributed
+    from hipfm.parallel.dist import Comm, init_distributed, local_device_index, same_device
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = local_device_index()        # LOCAL_RANK; 0 for every rank under HIPFM_SAME_DEVICE=1
     if args.gpus != world and rank == 0:
         print(f"[bench] --gpus {args.gpus} but WORLD_SIZE={world}: measuring {world} rank(s)",
               file=sys.stderr, flush=True)
@@ -249,7 +249,7 @@ def main():
             for i in range(args.pool)]
     _progress()
     if world > 1 or args.force_exchange:
-        init_distributed("nccl")
+        init_distributed("nccl")         # (gloo + the same-device engine under HIPFM_SAME_DEVICE=1)
         _progress()
         mode = "sharded" if args.embedding_mode == "auto" else args.embedding_mode
         # capacity of the fixed-size exchanges: measured on EVERY batch this rank will route (the
@@ -424,6 +424,9 @@ def main():
                 "emb_dtype": args.emb_dtype + (" rows + slots (stochastic rounding), fp32 math"
                                                if args.emb_dtype == "bf16" else " tables + slots"),
                 "ids_layout": "field-major [F, B]" if args.field_major_ids else "row-major [B, F]",
+                "transport": ("same-device rehearsal: every rank on GPU 0, IPC staging + host barrier "
+                              "(HIPFM_SAME_DEVICE=1)" if (comm is not None and same_device()) else
+                              "RCCL" if comm is not None else "none (1 GPU)"),
             },
             "eval_auc": round(auc, 5),
             "train_loss": round(loss, 5),
@@ -460,6 +463,9 @@ def _parallelism(world: int, comm) -> str:
     emb = "row-sharded" if comm.sharded else "replicated"
     if world == 1:
         return f"dp1 (1-rank {emb}-exchange proxy)"
+    from hipfm.parallel.dist import same_device
+    if same_device():
+        return f"dp{world}+{emb}-embedding ({world} ranks on ONE GPU: same-device rehearsal)"
     return f"dp{world}+{emb}-embedding"
 
 

@@ -42,11 +42,11 @@ def _channels() -> List[str]:
 def _init_dist(cfg: RunConfig):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world > 1 and not dist.is_initialized():
-        from .parallel.dist import init_distributed
+        from .parallel.dist import init_distributed, local_device_index
         dev = cfg.device
         backend = "gloo" if dev == "cpu" or (dev == "auto" and not torch.cuda.is_available()) else "nccl"
         if backend == "nccl":
-            torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+            torch.cuda.set_device(local_device_index())
         init_distributed(backend)
 
 

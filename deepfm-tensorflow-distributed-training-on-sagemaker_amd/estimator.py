@@ -48,7 +48,8 @@ def resolve_device(cfg: RunConfig):
     if cfg.device in ("cuda", "gpu") or (cfg.device == "auto" and torch.cuda.is_available()):
         if not torch.cuda.is_available():
             raise RuntimeError("--device cuda requested but no GPU is visible")
-        return torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
+        from .parallel.dist import local_device_index
+        return torch.device("cuda", local_device_index())
     return torch.device("cpu")
 
 
@@ -666,6 +667,8 @@ class Estimator:
             t, sharded, shape = srcs[n]
             if sharded and world > 1:
                 loc = t.contiguous()
+                if dist.get_backend() == "gloo" and loc.is_cuda:
+                    loc = loc.cpu()          # (gloo gathers host tensors: the same-device rehearsal)
                 parts = [torch.empty_like(loc) for _ in range(world)] if rank == owner[n] else None
                 dist.gather(loc, parts, dst=owner[n])
                 if rank == owner[n]:

@@ -1196,7 +1196,11 @@ class NativeDeepFM(GraphRunnerMixin, NativeStateMixin):
                         limit=self.V, err=self.err_words[3:4])
 
     def _raise_errors(self, w):
-        """Raise on the first set error word of a host copy ``w`` of ``err_words``."""
+        """Raise on the first set error word of a host copy ``w`` of ``err_words`` (and on a
+        poisoned same-device transport, whose error word lives on the host)."""
+        eng = getattr(self.comm, "engine", None) if self.comm is not None else None
+        if eng is not None and hasattr(eng, "check"):
+            eng.check()
         if w[0] or w[1]:
             raise RuntimeError("an id lies outside its field's declared range (field_ranges): "
                                "the per-field sort is invalid for this data")

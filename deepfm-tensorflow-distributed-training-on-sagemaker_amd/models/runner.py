@@ -437,6 +437,7 @@ class GraphRunnerMixin:
                     self._run_j = None
                     if self.rpx is not None:
                         self.rpx._run_j = None
+                        self.rpx._tagged = False     # (a step that raised must not leak its tag state)
 
         if self.comm is not None and not self.comm.graph_safe:
             # collectives that cannot be captured (the in-process emulation engine of the tests):

@@ -262,6 +262,15 @@ _SIGS = {
     "hfm_comm_allgather": [c_void_p, c_void_p, c_void_p, c_size_t, c_void_p],
     "hfm_comm_alltoall_allgather": [c_void_p, c_void_p, c_void_p, c_size_t, c_void_p, c_void_p, c_size_t, c_void_p],
     "hfm_comm_group": [c_void_p, c_void_p, c_int, c_void_p],
+    "hfm_lb_shared_bytes": [],
+    "hfm_lb_create": [C.POINTER(c_void_p), c_int, c_int, C.c_char_p, c_int, c_int],
+    "hfm_lb_ipc_handle_bytes": [],
+    "hfm_lb_alloc_stage": [c_void_p, c_size_t, c_void_p],
+    "hfm_lb_open_peers": [c_void_p, c_void_p],
+    "hfm_lb_group": [c_void_p, c_void_p, c_int, c_void_p],
+    "hfm_lb_stage_half_kb": [c_void_p],
+    "hfm_lb_error": [c_void_p],
+    "hfm_lb_destroy": [c_void_p],
     "hfm_sh_count_blocks": [c_int],
     "hfm_sh_route_tiles": [c_int],
     "hfm_sh_route": [c_void_p, c_int, c_int, c_int] + [c_void_p] * 7 + [c_void_p],

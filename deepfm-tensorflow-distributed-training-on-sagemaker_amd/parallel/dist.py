@@ -4,10 +4,11 @@ Replaces the reference's two distribution paths:
 
 * P2 Horovod synchronous DP (HVD:149,262,295,355-372): ``hvd.init`` -> ``init_distributed``
   (torchrun-style env, one process per GPU, ``127.0.0.1`` rendezvous), DistributedOptimizer's
-  tensor-fusion all-reduce -> ONE flat dense-gradient bucket (0.68 MB at the notebook config:
-  latency-bound, so a single bucket) launched asynchronously right after the MLP backward and
-  overlapped with the whole sparse backward (sort / reduce / exchange / row update) on RCCL's
-  stream; ``BroadcastGlobalVariablesHook`` -> deterministic identical init on every rank
+  tensor-fusion all-reduce -> ONE flat dense-gradient bucket (latency-bound at these sizes, so a
+  single bucket).  By default it travels in the step's last grouped collective with the sparse
+  gradient rows (all-gathered, summed in rank order by the owner launch: parallel/sharded.py G2);
+  HIPFM_SH_OVERLAP=1 instead all-reduces it on the main stream while the sparse backward runs on
+  a graph branch.  ``BroadcastGlobalVariablesHook`` -> deterministic identical init on every rank
   (+ ``broadcast_dense`` for resumed state).
 * P1/P4 Parameter Server + variable partitioning (PS:414-442, DOC p.32): the embedding table
   is ROW-SHARDED over ranks (owner = id % N, local row = id // N) with synchronous updates:
@@ -20,7 +21,9 @@ Replaces the reference's two distribution paths:
   rows) and reduced in rank order, identically on every rank (parallel/replicated.py).
 Every multi-rank step runs on the native RCCL engine (csrc/kernels/comm.hip); the host-
 synchronous torch.distributed exchange of earlier rounds survives only as a CPU test oracle
-(tests/sharded_oracle.py).
+(tests/sharded_oracle.py).  HIPFM_SAME_DEVICE=1 maps every rank to device 0 and swaps the RCCL
+engine for the same-device transport (parallel/loopback.py): the N-GPU job's exact processes and
+step, rehearsed on one GPU.
 
 Gradient averaging: the head kernel scales dlogit by 1/(B*N), so SUM all-reduces average.
 """
@@ -34,6 +37,18 @@ import torch
 import torch.distributed as dist
 
 from ..ops import kernels as KN
+from ..utils.knobs import flag
+
+
+def same_device() -> bool:
+    """HIPFM_SAME_DEVICE=1: every rank of this node runs on device 0 (one-GPU rehearsal of the
+    N-GPU job: gloo process group + the same-device collective engine, parallel/loopback.py)."""
+    return flag("HIPFM_SAME_DEVICE")
+
+
+def local_device_index() -> int:
+    """The HIP device of this rank: LOCAL_RANK (one process per GPU), or 0 under same_device()."""
+    return 0 if same_device() else int(os.environ.get("LOCAL_RANK", "0"))
 
 
 def init_distributed(backend: Optional[str] = None, timeout_s: int = 600):
@@ -46,9 +61,11 @@ def init_distributed(backend: Optional[str] = None, timeout_s: int = 600):
     os.environ.setdefault("WORLD_SIZE", "1")
     if backend is None:
         backend = "nccl" if torch.cuda.is_available() else "gloo"
+    if same_device():
+        backend = "gloo"         # RCCL refuses two ranks on one device; gloo carries setup only
     kw = dict(backend=backend, timeout=datetime.timedelta(seconds=timeout_s))
     if backend == "nccl":
-        kw["device_id"] = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
+        kw["device_id"] = torch.device("cuda", local_device_index())
     dist.init_process_group(**kw)
 
 
@@ -101,15 +118,20 @@ class Comm:
         # gradient exchange, issued as grouped operations on the step's main stream -> no host
         # sync, graph-capturable step.  ONE communicator carries every collective of the step
         # in a fixed order (parallel/sharded.py module docstring: deadlock freedom)
+        loop = same_device() and torch.cuda.is_available()
         if native is None:
-            native = dist.get_backend(group) == "nccl" and (self.world_size > 1 or self.force_exchange)
+            native = ((dist.get_backend(group) == "nccl" or loop)
+                      and (self.world_size > 1 or self.force_exchange))
         self.engine = None
         if capacity is not None and self.world_size > 1:
             # every rank must use the SAME block size in the fixed-capacity exchanges: take the
             # max of the per-rank estimates (each rank measured its own batches)
             capacity = agree_max(capacity, group)
         self.capacity = capacity
-        if native:
+        if native and loop:
+            from .loopback import LoopbackEngine
+            self.engine = LoopbackEngine(group)
+        elif native:
             from .sharded import RcclEngine
             self.engine = RcclEngine(group)
         self.graph_safe = True

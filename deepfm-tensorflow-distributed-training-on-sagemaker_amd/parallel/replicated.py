@@ -96,6 +96,8 @@ class ReplicatedExchange:
         self._run_G = 0
         self._retired = []               # buffers of earlier run layouts (captured graphs use them)
         self._tagged = False
+        from .sharded import reserve_staging
+        reserve_staging(engine, 4 * self.C * (self.RW + 1) + 8 * m.P + (64 << 10))
 
     def _issue(self, ops):
         if self.trace is not None:
@@ -120,6 +122,8 @@ class ReplicatedExchange:
             self.g_run_ids = torch.full((self.N * cap * self.C,), -1, **i32)
             for j, rs in enumerate(self.run_sets):
                 rs["send_ids"] = self.run_ids[j]
+        from .sharded import reserve_staging
+        reserve_staging(self.eng, 4 * self.run_ids.shape[0] * self.C + (64 << 10))   # G0 of the run
         while len(self.run_sets) < G:
             self.run_sets.append(dict(sid=torch.zeros(m.M * m.F, **i32), upos=torch.zeros(m.M * m.F, **i32),
                                       send_ids=self.run_ids[len(self.run_sets)], send_cnt=torch.zeros(1, **i32),

@@ -69,8 +69,10 @@ _DENSE_XCHG = knob("HIPFM_DENSE_XCHG")
 def dense_allreduce(world: int) -> bool:
     """The fused exchange's dense gradient: all-reduced (ring: 2 (N-1)/N x P floats per rank) or
     all-gathered and summed in rank order by the owner launch (N x P floats received, no RCCL
-    reduction, in place).  auto: all-reduce from 4 ranks, where the all-gather's 7 x 0.68 MB at
-    N = 8 outweighs the all-reduce's extra ring steps; the 1-rank proxy and N = 2 gather."""
+    reduction, in place: the default -- bitwise the same sum on every rank count's emulation and
+    on hardware).  ``allreduce`` / ``auto`` (all-reduce from 4 ranks) are opt-in: RCCL's ring sum
+    reassociates the rank gradients, and neither has been compared with the rank-ordered sum on
+    an N >= 4 node yet."""
     return _DENSE_XCHG == "allreduce" or (_DENSE_XCHG == "auto" and world >= 4)
 
 
@@ -81,6 +83,14 @@ def overlap_branch(owner, device) -> "torch.cuda.Stream":
     if st is None:
         st = owner._ovl_stream = torch.cuda.Stream(device)
     return st
+
+
+def reserve_staging(engine, nbytes: int):
+    """Collective on transports with staging buffers (parallel/loopback.py), a no-op on RCCL:
+    every rank calls it at the same host point with the same size, before any capture needs it."""
+    r = getattr(engine, "reserve", None)
+    if r is not None:
+        r(nbytes)
 
 
 def estimate_capacity(id_batches: Iterable[torch.Tensor], world: int, slack: float = 1.25,
@@ -248,6 +258,9 @@ class FixedCapacityExchange:
         self.gather_ld = 0                   # slot_row layout of the last fetch (tower idx_ld)
         self.tower_serve = None              # ShServeArgs the next tower launch serves (run mode)
         self.x_serve = None                  # ... or the next sparse backward launch (sfwg_x)
+        # staging of a transport that needs it (the same-device engine): the largest group of a
+        # step -- G1 rows + ids, or G2 gradient rows + dense gradient + ids
+        reserve_staging(engine, 4 * T * (max(self.RWS, self.RWG) + 1) + 8 * m.P + (64 << 10))
 
     # ------------------------------------------------------------------ host-side plan
     def plan(self, ids: torch.Tensor, B: int, nxt: Optional[torch.Tensor], resident: bool = True,
@@ -307,6 +320,7 @@ class FixedCapacityExchange:
         sort_plan = m._fsort.run_plan([(ids, b, fm, rs.sorted_keys, rs.perm, rs.inv if grow else None)
                                        for (ids, b, fm), rs in zip(batches, sets)])
         T = self.N * G * self.C
+        reserve_staging(self.eng, 4 * T + (64 << 10))       # G0 of the run (packed ids all-to-all)
         if self._run_ids is None or self._run_ids.shape[1] < T:
             # a larger run: a new packed ids buffer.  The old one and the descriptors built on it
             # stay alive (graphs captured from earlier runs still read them: never freed under a

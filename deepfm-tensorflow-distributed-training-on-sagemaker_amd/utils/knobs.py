@@ -45,9 +45,10 @@ KNOBS: Dict[str, Knob] = {
                            "oracle and the bench ladder's second rung)"),
     "HIPFM_SH_APPLY_DENSE": Knob("1", "variant", "row-sharded step: dense optimizer in the owner "
                                  "update's launch"),
-    "HIPFM_DENSE_XCHG": Knob("auto", "variant", "fused multi-rank exchange: the dense gradient all-gathered "
-                             "and summed in rank order by the owner launch (allgather) or all-reduced "
-                             "(allreduce); auto: all-reduce from 4 ranks"),
+    "HIPFM_DENSE_XCHG": Knob("allgather", "variant", "fused multi-rank exchange: the dense gradient "
+                             "all-gathered and summed in rank order by the owner launch (allgather: the "
+                             "default, deterministic, 7 x 0.2 MB per rank at N = 8) or all-reduced by RCCL "
+                             "(allreduce; auto: all-reduce from 4 ranks -- both reassociate the sum)"),
     "HIPFM_SH_OVERLAP": Knob("0", "variant", "multi-rank lazy step: the dense gradient in its own "
                              "launch after the tower, all-reduced on the main stream while the sparse "
                              "backward runs on a graph branch (1), instead of all-gathered with the "
@@ -82,6 +83,11 @@ KNOBS: Dict[str, Knob] = {
     "HIPFM_H2D_STREAMS": Knob("2", "tuning", "streamed input: copy streams the device-ring batches alternate over"),
     "HIPFM_GRAPH_STEPS": Knob("32", "tuning", "most training steps per captured HIP graph (bench.py)"),
     # ---- harness
+    "HIPFM_SAME_DEVICE": Knob("0", "harness", "multi-rank runs with every rank on device 0: gloo process "
+                              "group + the same-device collective engine (parallel/loopback.py) -- the "
+                              "N-GPU job's processes and step rehearsed on one GPU"),
+    "HIPFM_LB_TIMEOUT_MS": Knob("60000", "harness", "same-device engine: a collective barrier waits at "
+                                "most this long, then poisons the transport (every rank raises)"),
     "HIPFM_ARCH": Knob("gfx950", "harness", "offload arch of the HIP build"),
     "HIPFM_KERNELS_SO": Knob(None, "harness", "path of the kernel library (default: in-tree _lib)"),
     "HIPFM_BUILD_PACKED": Knob(None, "harness", "build: packed-FP32 ops on (own objects / library)"),
