@@ -273,10 +273,10 @@ def main():
                          emb_dtype=args.emb_dtype, exchange_rows=args.exchange_rows)
     _progress()
     if args.field_major_ids:
-        # ids stored field-major ([F, B] storage, [B, F] view, the layout the input pipeline's
-        # device feeder produces): the run-level sort's 39 per-field workgroups each read one
-        # contiguous field (row-major: a 4-B id per 156-B row, 107 vs 201 us per 20-batch run
-        # sort, 0.1121 vs 0.1141 ms/step; profiles/r4c_*)
+        # ids stored field-major ([F, B] storage, [B, F] view: the layout the Estimator's HBM
+        # cache stores, data/pipeline.py iter_epoch): the run-level sort's 39 per-field
+        # workgroups each read one contiguous field (row-major: a 4-B id per 156-B row, 107 vs
+        # 201 us per 20-batch run sort, 0.1121 vs 0.1141 ms/step; profiles/r4c_*)
         pool = [(ids.t().contiguous().t(), vals, labels) for ids, vals, labels in pool]
     use_graph = not args.no_graph
     P = len(pool)

@@ -37,6 +37,41 @@ struct EpiArgs {
   bf16* out_t;             // transposed copy (nullable)
 };
 
+// One 16x16 accumulator tile's epilogue: lane (rowb.., col) holds rows rowb + j, j = 0..3 (MFMA C/D
+// map), shared by every NT GEMM kernel below.
+template <int EPI>
+__device__ __forceinline__ void epi_store(const EpiArgs& ep, const f32x4 acc, int rowb, int col, int M,
+                                          int N, uint32_t salt) {
+  if (EPI == EPI_F32) {
+    float* C = reinterpret_cast<float*>(ep.out) + (size_t)blockIdx.z * M * N;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) C[(size_t)(rowb + j) * N + col] = acc[j];
+  } else if (EPI == EPI_RELU_F32) {
+    float* C = reinterpret_cast<float*>(ep.out);
+    const float bc = ep.bias[col];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) C[(size_t)(rowb + j) * N + col] = fmaxf(acc[j] + bc, 0.f);
+  } else {
+    bf16x4 tv;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int row = rowb + j;
+      float v = acc[j];
+      if (EPI == EPI_FWD || EPI == EPI_FWD_EVAL) {
+        v = fmaxf(v + ep.bias[col], 0.f);
+        if (EPI == EPI_FWD && ep.drop)
+          v = dropout_keep((uint32_t)(row * N + col), salt, ep.keep_thr) ? v * ep.scale : 0.f;
+      } else {  // EPI_DGRAD (hprev == nullptr: plain bf16 store, e.g. dX0 of layer 1)
+        v = (!ep.hprev || bf2f(ep.hprev[(size_t)row * N + col]) > 0.f) ? v * ep.scale : 0.f;
+      }
+      const bf16 hv = f2bf(v);
+      reinterpret_cast<bf16*>(ep.out)[(size_t)row * N + col] = hv;
+      tv[j] = hv;
+    }
+    if (ep.out_t) *reinterpret_cast<bf16x4*>(ep.out_t + (size_t)col * M + rowb) = tv;
+  }
+}
+
 template <int WM, int WN, int EPI>
 __global__ void __launch_bounds__(WM * WN * 64) gemm_nt_kernel(
     const bf16* __restrict__ A, int lda, const bf16* __restrict__ Bm, int ldb, int M, int N,
@@ -95,44 +130,12 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_nt_kernel(
   const int cr = (lane >> 4) * 4, cc = lane & 15;
   uint32_t salt = 0;
   if (EPI == EPI_FWD && ep.drop) salt = dropout_salt(ep.seed, (uint32_t)(*ep.step), ep.layer);
-  f32x4 accs[2][2] = {{c00, c01}, {c10, c11}};
+  const f32x4 accs[2][2] = {{c00, c01}, {c10, c11}};
 #pragma unroll
-  for (int ti = 0; ti < 2; ++ti) {
+  for (int ti = 0; ti < 2; ++ti)
 #pragma unroll
-    for (int tj = 0; tj < 2; ++tj) {
-      const int col = col0 + tj * 16 + cc;
-      const int rowb = row0 + ti * 16 + cr;
-      const f32x4 acc = accs[ti][tj];
-      if (EPI == EPI_F32) {
-        float* C = reinterpret_cast<float*>(ep.out) + (size_t)blockIdx.z * M * N;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) C[(size_t)(rowb + j) * N + col] = acc[j];
-      } else if (EPI == EPI_RELU_F32) {
-        float* C = reinterpret_cast<float*>(ep.out);
-        const float bc = ep.bias[col];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) C[(size_t)(rowb + j) * N + col] = fmaxf(acc[j] + bc, 0.f);
-      } else {
-        bf16x4 tv;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int row = rowb + j;
-          float v = acc[j];
-          if (EPI == EPI_FWD || EPI == EPI_FWD_EVAL) {
-            v = fmaxf(v + ep.bias[col], 0.f);
-            if (EPI == EPI_FWD && ep.drop)
-              v = dropout_keep((uint32_t)(row * N + col), salt, ep.keep_thr) ? v * ep.scale : 0.f;
-          } else {  // EPI_DGRAD (hprev == nullptr: plain bf16 store, e.g. dX0 of layer 1)
-            v = (!ep.hprev || bf2f(ep.hprev[(size_t)row * N + col]) > 0.f) ? v * ep.scale : 0.f;
-          }
-          const bf16 hv = f2bf(v);
-          reinterpret_cast<bf16*>(ep.out)[(size_t)row * N + col] = hv;
-          tv[j] = hv;
-        }
-        if (ep.out_t) *reinterpret_cast<bf16x4*>(ep.out_t + (size_t)col * M + rowb) = tv;
-      }
-    }
-  }
+    for (int tj = 0; tj < 2; ++tj)
+      epi_store<EPI>(ep, accs[ti][tj], row0 + ti * 16 + cr, col0 + tj * 16 + cc, M, N, salt);
 }
 
 template <int WM, int WN, int EPI>
@@ -145,8 +148,123 @@ static int launch_gemm(const bf16* A, int lda, const bf16* B, int ldb, int M, in
   HFM_LAUNCH_CHECK();
 }
 
+// ------------------------------------------------------------------ wide-layer GEMM (tile 8)
+// The per-layer path of towers the fused kernel cannot hold (the reference's GPU recipe,
+// deep_layers 4096,4096,4096, DOC p.37; batch norm, HVD:204-210): GEMMs of 2 * 16384 * 4096 *
+// 4096 = 0.55 TFLOP each, where the register-fed 32x32 tiles above re-read every operand from
+// L2 per wave.  Here a 256-thread workgroup (2 x 2 waves) owns a 128 x 128 output tile; the
+// k-loop stages 64-deep A and B panels HBM -> LDS with 16-B LDS-DMA loads
+// (global_load_lds_dwordx4, no VGPR round trip) into two buffers, so panel t+1 streams in while
+// the MFMAs consume panel t.  Each wave computes 64 x 64 = 4 x 4 MFMA 16x16x32 tiles (16 f32x4
+// accumulators) from bf16x8 fragments read with ds_read_b128.
+//   LDS image of a panel: [128 rows][64 bf16] = 128-B rows, the 16-B chunk c of row r stored
+//   at slot c ^ ((r >> 1) & 7).  A 16-lane ds_read group reads 16 consecutive rows at one chunk:
+//   rows of equal parity share a 256-B bank row only at distinct slots -> conflict-free.  The
+//   DMA writes lane-linear (wave base + 16 * lane), so the swizzle is applied to the per-lane
+//   GLOBAL source address (lane l of an 8-row piece fetches chunk (l & 7) ^ swz(row)).
+//   Tiles are numbered XCD-aware: consecutive tile ids (same 128-row A panel, neighbouring B
+//   panels) run on the same XCD and share its L2.
+constexpr int GL_BM = 128, GL_BN = 128, GL_BK = 64, GL_THREADS = 256;
+constexpr int GL_PANEL = GL_BM * GL_BK * 2;       // bytes of one A (or B) panel
+static_assert(GL_BM == GL_BN, "square tile: A and B panels share the staging code");
+
+__device__ __forceinline__ int gl_slot(int r, int c) { return r * 128 + ((c ^ ((r >> 1) & 7)) << 4); }
+
+// stage one 128 x 64 panel (rows row0.., k from k0) into `lds`: 16 DMA pieces of 8 rows, 4 per wave
+__device__ __forceinline__ void gl_stage(char* lds, const bf16* __restrict__ g, int ld, int row0, int k0,
+                                         int wave, int lane) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int piece = wave * 4 + i;
+    const int r = piece * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ ((r >> 1) & 7);
+    const bf16* src = g + (size_t)(row0 + r) * ld + k0 + c * 8;
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                     (__attribute__((address_space(3))) void*)(lds + piece * 1024), 16, 0, 0);
+  }
+}
+
+template <int EPI>
+__global__ void __launch_bounds__(GL_THREADS, 2) gemm_lds_kernel(
+    const bf16* __restrict__ A, int lda, const bf16* __restrict__ Bm, int ldb, int M, int N,
+    int kchunk, EpiArgs ep) {
+  // ONE __shared__ array (a second one can make hipcc drain the DMA queue before every ds_read)
+  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * GL_PANEL];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wm = wave >> 1, wn = wave & 1;
+  // XCD-aware tile id (bijective for any tile count): the blocks the hardware sends to one XCD
+  // (bid % 8) take a contiguous range of tile ids
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q = nwg >> 3, rr = nwg & 7;
+  const int tid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
+  const int tiles_n = N / GL_BN;
+  const int m0 = (tid / tiles_n) * GL_BM, n0 = (tid % tiles_n) * GL_BN;
+  const int kb = blockIdx.z * kchunk;
+  const int nt = kchunk / GL_BK;
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  gl_stage(smem, A, lda, m0, kb, wave, lane);
+  gl_stage(smem + GL_PANEL, Bm, ldb, n0, kb, wave, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const int fr = lane & 15, fq = lane >> 4;
+  for (int t = 0; t < nt; ++t) {
+    char* cur = smem + (t & 1) * 2 * GL_PANEL;
+    if (t + 1 < nt) {                     // the next panels stream in behind this step's MFMAs
+      char* nxt = smem + ((t + 1) & 1) * 2 * GL_PANEL;
+      gl_stage(nxt, A, lda, m0, kb + (t + 1) * GL_BK, wave, lane);
+      gl_stage(nxt + GL_PANEL, Bm, ldb, n0, kb + (t + 1) * GL_BK, wave, lane);
+    }
+    const char* pa = cur;
+    const char* pb = cur + GL_PANEL;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int c = ks * 4 + fq;
+      bf16x8 a[4], b[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        a[i] = *reinterpret_cast<const bf16x8*>(pa + gl_slot(wm * 64 + i * 16 + fr, c));
+        b[i] = *reinterpret_cast<const bf16x8*>(pb + gl_slot(wn * 64 + i * 16 + fr, c));
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+    // the next panels have landed (this wave's DMA) and every wave is done reading `cur`
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  uint32_t salt = 0;
+  if (EPI == EPI_FWD && ep.drop) salt = dropout_salt(ep.seed, (uint32_t)(*ep.step), ep.layer);
+  const int cr = fq * 4;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      epi_store<EPI>(ep, acc[i][j], m0 + wm * 64 + i * 16 + cr, n0 + wn * 64 + j * 16 + fr, M, N, salt);
+}
+
+template <int EPI>
+static int launch_gemm_lds(const bf16* A, int lda, const bf16* B, int ldb, int M, int N, int Kd,
+                           int splitk, const EpiArgs& ep, hipStream_t st) {
+  if (M % GL_BM || N % GL_BN || splitk < 1 || Kd % (GL_BK * splitk) || lda % 8 || ldb % 8 ||
+      ((uintptr_t)A & 15) || ((uintptr_t)B & 15))
+    return (int)hipErrorInvalidValue;
+  dim3 grid((M / GL_BM) * (N / GL_BN), 1, splitk);
+  hipLaunchKernelGGL((gemm_lds_kernel<EPI>), grid, dim3(GL_THREADS), 0, st, A, lda, B, ldb, M, N,
+                     Kd / splitk, ep);
+  HFM_LAUNCH_CHECK();
+}
+
 // tile: 0 = 64x64 (2x2 waves), 1 = 128x32 (4x1), 2 = 32x128 (1x4), 3 = 32x32 (1x1), 4 = 32x64 (1x2),
-//       5 = 32x160 (1x5), 6 = 32x320 (1x10), 7 = 32x256 (1x8)
+//       5 = 32x160 (1x5), 6 = 32x320 (1x10), 7 = 32x256 (1x8), 8 = 128x128 LDS-staged (wide layers)
 template <int EPI>
 static int gemm_tile(int tile, const bf16* A, int lda, const bf16* B, int ldb, int M, int N, int Kd,
                      int splitk, const EpiArgs& ep, hipStream_t st) {
@@ -159,6 +277,7 @@ static int gemm_tile(int tile, const bf16* A, int lda, const bf16* B, int ldb, i
     case 5: return launch_gemm<1, 5, EPI>(A, lda, B, ldb, M, N, Kd, splitk, ep, st);
     case 6: return launch_gemm<1, 10, EPI>(A, lda, B, ldb, M, N, Kd, splitk, ep, st);
     case 7: return launch_gemm<1, 8, EPI>(A, lda, B, ldb, M, N, Kd, splitk, ep, st);
+    case 8: return launch_gemm_lds<EPI>(A, lda, B, ldb, M, N, Kd, splitk, ep, st);
     default: return (int)hipErrorInvalidValue;
   }
 }

@@ -70,6 +70,7 @@ _XROWS = knob("HIPFM_XROWS")
 _DX0_SPLIT = knob("HIPFM_DX0_SPLIT")      # auto | 1 | 0 (tower.hip tower_dx0_kernel)
 _L0_SPLIT = knob("HIPFM_L0_SPLIT")        # auto | 0 (tower.hip tower_l0s_kernel)
 _SWEEP_MODE = knob("HIPFM_SWEEP_MODE")      # auto | merged | branch
+_LDS_GEMM = flag("HIPFM_LDS_GEMM")           # wide per-layer GEMMs on the 128 x 128 LDS tile
 _SWEEP_MBLK = 2048   # merged-mode sweep workgroups: 512 0.191, 1024 0.179, 2048 0.156, 3072 0.156, 6144 0.172 ms
 _SWEEP_WG = 256      # branch sweep workgroups: 128: 0.178, 256: 0.160, 512: 0.179 ms
 
@@ -127,9 +128,22 @@ def _align(n: int, a: int = 64) -> int:
     return (n + a - 1) // a * a
 
 
-def _pick_tile(M: int, N: int, row_major_stream: bool = True) -> int:
-    """Tile for an NT GEMM.  Activation GEMMs (M = batch) take the widest column tile that
-    covers N in one workgroup row, so the big A operand (E, H, dZ) is streamed exactly once."""
+def _lds_tile_ok(M: int, N: int, Kd: Optional[int], splitk: int = 1) -> bool:
+    """The 128 x 128 LDS-staged tile (mlp.hip gemm_lds_kernel) for a GEMM with at least 256
+    output tiles (a 4096-wide layer at any batch >= 1024; the reference's GPU tower, DOC p.37):
+    there the register-fed 32-row tiles re-read both operands from L2 per wave."""
+    return (Kd is not None and M % 128 == 0 and N % 128 == 0 and Kd % (64 * splitk) == 0
+            and (M // 128) * (N // 128) * splitk >= 256)
+
+
+def _pick_tile(M: int, N: int, row_major_stream: bool = True, Kd: Optional[int] = None,
+               allow_lds: bool = True) -> int:
+    """Tile for an NT GEMM.  Wide layers (``_lds_tile_ok``, the reduction depth ``Kd`` given) take
+    the LDS-staged 128 x 128 workgroup tile; otherwise activation GEMMs (M = batch) take the
+    widest column tile that covers N in one workgroup row, so the big A operand (E, H, dZ) is
+    streamed exactly once."""
+    if allow_lds and _LDS_GEMM and _lds_tile_ok(M, N, Kd):
+        return KN.TILE_LDS
     if row_major_stream and M % 32 == 0:
         for t, w in ((3, 32), (4, 64), (2, 128), (5, 160), (7, 256), (6, 320)):
             if N == w:
@@ -159,7 +173,7 @@ def _pick_splitk(M: int, N: int, Kd: int, tile: int, target_blocks: int = 512,
     256 CUs, but few enough slabs that the finalize pass stays a short, coalesced read."""
     bm, bn = KN.TILES[tile]
     tiles = (M // bm) * (N // bn)
-    ksteps = Kd // 32
+    ksteps = Kd // (64 if tile == KN.TILE_LDS else 32)
     want = max(1, min(ksteps, max_split, target_blocks // max(1, tiles)))
     for s in range(want, 0, -1):
         if ksteps % s == 0:
@@ -569,7 +583,7 @@ class NativeDeepFM(GraphRunnerMixin, NativeStateMixin):
                     s //= 2
                 self.wg_cfg.append((None, s))
                 continue
-            t = _pick_tile(Mg, Ng, row_major_stream=False)
+            t = _pick_tile(Mg, Ng, row_major_stream=False, Kd=Kd)
             s = _pick_splitk(Mg, Ng, Kd, t)
             self.wg_cfg.append((t, s))
         self.slabs = [torch.zeros(s, self.Np[i], self.Kp[i], **f32) for i, (t, s) in enumerate(self.wg_cfg)]
@@ -1038,11 +1052,11 @@ class NativeDeepFM(GraphRunnerMixin, NativeStateMixin):
             N = self.Np[i]
             if self.batch_norm:
                 ep.out, ep.out_t = self.Rb[i].data_ptr(), 0
-                KN.gemm_nt(KN.EPI_RELU_F32, _pick_tile(M, N), X, self.Kp[i], self.W16[i],
+                KN.gemm_nt(KN.EPI_RELU_F32, _pick_tile(M, N, Kd=self.Kp[i]), X, self.Kp[i], self.W16[i],
                            self.Kp[i], M, N, self.Kp[i], 1, ep)
                 self._bn_forward(i, B, train)
             else:
-                KN.gemm_nt(KN.EPI_FWD if train else KN.EPI_FWD_EVAL, _pick_tile(M, N), X,
+                KN.gemm_nt(KN.EPI_FWD if train else KN.EPI_FWD_EVAL, _pick_tile(M, N, Kd=self.Kp[i]), X,
                            self.Kp[i], self.W16[i], self.Kp[i], M, N, self.Kp[i], 1, ep)
             X = self.H[i]
         return idx, tv
@@ -1130,7 +1144,7 @@ class NativeDeepFM(GraphRunnerMixin, NativeStateMixin):
             if i > 0 and self.batch_norm:
                 ep.out = self.dH[i - 1].data_ptr()    # f32 dL/dH_{i-1}; BN backward masks it
                 N = self.Np[i - 1]
-                KN.gemm_nt(KN.EPI_F32, _pick_tile(M, N), self.dZ[i], self.Np[i], self.WT16[i],
+                KN.gemm_nt(KN.EPI_F32, _pick_tile(M, N, Kd=self.Np[i]), self.dZ[i], self.Np[i], self.WT16[i],
                            self.Np[i], M, N, self.Np[i], 1, ep)
             elif i > 0:
                 keep = self.keep[i - 1]
@@ -1139,12 +1153,12 @@ class NativeDeepFM(GraphRunnerMixin, NativeStateMixin):
                 ep.out = self.dZ[i - 1].data_ptr()
                 ep.out_t = self.dZt[i - 1].data_ptr()
                 N = self.Np[i - 1]
-                KN.gemm_nt(KN.EPI_DGRAD, _pick_tile(M, N), self.dZ[i], self.Np[i], self.WT16[i],
+                KN.gemm_nt(KN.EPI_DGRAD, _pick_tile(M, N, Kd=self.Np[i]), self.dZ[i], self.Np[i], self.WT16[i],
                            self.Np[i], M, N, self.Np[i], 1, ep)
             else:
                 ep.out = self.dX0.data_ptr()          # hprev = 0: unmasked bf16 store
                 ep.scale = 1.0
-                KN.gemm_nt(KN.EPI_DGRAD, _pick_tile(M, self.K0p), self.dZ[0], self.Np[0],
+                KN.gemm_nt(KN.EPI_DGRAD, _pick_tile(M, self.K0p, Kd=self.Np[0]), self.dZ[0], self.Np[0],
                            self.WT16[0], self.Np[0], M, self.K0p, self.Np[0], 1, ep)
         self._finalize_grads()
 

@@ -74,6 +74,9 @@ KNOBS: Dict[str, Knob] = {
     "HIPFM_SWEEP_MODE": Knob("auto", "variant", "tf1_dense split sweep: merged (workgroups of the "
                              "sparse launch) | branch (own graph branch) | auto (merged from B = 8192: "
                              "B=16384 0.156 vs 0.160-0.163 ms, B=1024 0.077 vs 0.069 ms)"),
+    "HIPFM_LDS_GEMM": Knob("1", "variant", "per-layer tower GEMMs with >= 256 128x128 output tiles on the "
+                           "LDS-staged workgroup tile (mlp.hip gemm_lds_kernel); 0: the register-fed "
+                           "32-row tiles (bitwise the same sums: tests/test_gpu_gemm.py)"),
     "HIPFM_TABLE_LAYOUT": Knob("record", "variant", "record: one 128-B record per row (v, w, slots); "
                                "split: separate tables"),
     # ---- tuning

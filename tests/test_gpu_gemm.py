@@ -1,0 +1,91 @@
+"""The wide-layer GEMM (csrc/kernels/mlp.hip gemm_lds_kernel, tile 8: 128 x 128 workgroup tile,
+LDS-DMA double-buffered 64-deep panels) against a PyTorch fp32 reference of the same op, for every
+epilogue the per-layer tower uses, and bitwise against the register-fed tiles it replaces where
+their reduction order is the same (one MFMA chain per output over k in order)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+if not torch.cuda.is_available():
+    pytest.skip("needs a GPU", allow_module_level=True)
+
+import hipfm  # noqa: E402
+from hipfm.ops import kernels as KN  # noqa: E402
+from hipfm.ops._lib import EpiArgs  # noqa: E402
+from hipfm.utils.rng import keep_threshold  # noqa: E402
+
+DEV = torch.device("cuda", 0)
+
+
+def _ops(M, N, K, seed=0):
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    A = (torch.rand(M, K, generator=g, device=DEV) * 2 - 1).bfloat16()
+    B = (torch.rand(N, K, generator=g, device=DEV) * 2 - 1).bfloat16()
+    return A, B
+
+
+def _ref(A, B):
+    return A.float() @ B.float().t()
+
+
+@pytest.mark.parametrize("M,N,K,split", [(256, 128, 64, 1), (384, 256, 320, 1), (256, 512, 4096, 1),
+                                         (512, 256, 2048, 4), (1024, 1024, 1024, 2)])
+def test_lds_gemm_f32_matches_reference(M, N, K, split):
+    A, B = _ops(M, N, K, seed=M + N + K)
+    out = torch.full((split, M, N), float("nan"), device=DEV)
+    ep = EpiArgs()
+    ep.out = out.data_ptr()
+    KN.gemm_nt(KN.EPI_F32, KN.TILE_LDS, A, K, B, K, M, N, K, split, ep)
+    torch.cuda.synchronize()
+    ref = _ref(A, B)
+    got = out.sum(0)
+    assert torch.isfinite(got).all()
+    assert (got - ref).abs().max().item() <= 1e-4 * max(1.0, ref.abs().max().item()) + 1e-3
+    # the register-fed 64x64 tile sums k in the same MFMA order: bitwise equal
+    o2 = torch.zeros(split, M, N, device=DEV)
+    ep.out = o2.data_ptr()
+    KN.gemm_nt(KN.EPI_F32, 0, A, K, B, K, M, N, K, split, ep)
+    torch.cuda.synchronize()
+    assert torch.equal(out, o2)
+
+
+@pytest.mark.parametrize("epi", ["fwd", "fwd_eval", "dgrad", "relu_f32"])
+def test_lds_gemm_epilogues_match_register_tile(epi):
+    M, N, K = 512, 256, 640
+    A, B = _ops(M, N, K, seed=3)
+    bias = torch.randn(N, device=DEV)
+    step = torch.tensor([7], dtype=torch.int64, device=DEV)
+    hprev = torch.randn(M, N, device=DEV).bfloat16()
+    outs = []
+    for tile in (KN.TILE_LDS, 0):
+        f32 = epi == "relu_f32"
+        o = torch.zeros(M, N, device=DEV, dtype=torch.float32 if f32 else torch.bfloat16)
+        ot = torch.zeros(N, M, device=DEV, dtype=torch.bfloat16)
+        ep = EpiArgs()
+        ep.bias, ep.step, ep.out = bias.data_ptr(), step.data_ptr(), o.data_ptr()
+        ep.out_t = 0 if f32 else ot.data_ptr()
+        ep.seed, ep.layer, ep.keep_thr, ep.drop, ep.scale = 1234, 1, keep_threshold(0.5), 1, 2.0
+        kind = {"fwd": KN.EPI_FWD, "fwd_eval": KN.EPI_FWD_EVAL, "dgrad": KN.EPI_DGRAD,
+                "relu_f32": KN.EPI_RELU_F32}[epi]
+        if epi == "dgrad":
+            ep.hprev = hprev.data_ptr()
+        KN.gemm_nt(kind, tile, A, K, B, K, M, N, K, 1, ep)
+        torch.cuda.synchronize()
+        outs.append((o, ot))
+    (o8, ot8), (o0, ot0) = outs
+    assert torch.equal(o8, o0) and torch.equal(ot8, ot0)
+    ref = _ref(A, B)
+    if epi in ("fwd_eval", "relu_f32"):
+        r = torch.relu(ref + bias)
+        assert (o8.float() - r).abs().max().item() <= 2e-2 * r.abs().max().item()
+    if not epi == "relu_f32":
+        assert torch.equal(ot8.t(), o8)                  # the transposed copy
+
+
+def test_lds_gemm_rejects_bad_shapes():
+    A, B = _ops(256, 256, 96)
+    ep = EpiArgs()
+    out = torch.zeros(256, 256, device=DEV)
+    ep.out = out.data_ptr()
+    with pytest.raises(RuntimeError):
+        KN.gemm_nt(KN.EPI_F32, KN.TILE_LDS, A, 96, B, 96, 256, 256, 96, 1, ep)   # K % 64 != 0

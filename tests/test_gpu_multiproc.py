@@ -98,3 +98,34 @@ def test_processes_match_global_batch(tmp_path, N, sharded, update, mode):
     assert (full_v - rtv).abs().max().item() <= 2e-5 * scale
     assert (full_w - rtw).abs().max().item() <= 2e-5 * max(1.0, rtw.abs().max().item())
     assert (outs[0]["p"] - rp).abs().max().item() <= 2e-5 * rp.abs().max().item()
+
+
+def test_launch_cli_two_ranks_train_eval_infer_export(tmp_path):
+    """The reference user's flow with the launcher at N = 2 (mpirun -np / processes_per_host,
+    NBHVD:87-92): train (epoch 0 streamed + cached, epoch 1 replayed from the HBM cache as graphs),
+    eval, infer and export through ``python -m hipfm.launch --nproc_per_node 2 -m hipfm``, every
+    rank a real process on the one GPU (row-sharded table, same-device engine)."""
+    data = tmp_path / "data"
+    subprocess.check_call([sys.executable, os.path.join(REPO, "tools", "gen_synthetic_criteo.py"),
+                           "--out", str(data), "--preset", "total:50000", "--train_rows", "20000",
+                           "--val_rows", "4000", "--test_rows", "500", "--files", "4"], cwd=REPO)
+    md, sd, pred = tmp_path / "m", tmp_path / "s", tmp_path / "pred.txt"
+    common = ["--training_data_dir", str(data), "--val_data_dir", str(data), "--model_dir", str(md),
+              "--servable_model_dir", str(sd), "--pred_path", str(pred), "--feature_size", "50000",
+              "--field_size", "39", "--embedding_size", "8", "--batch_size", "512", "--deep_layers", "64,32",
+              "--dropout", "0.9,0.9", "--learning_rate", "0.003", "--log_steps", "10", "--device", "cuda",
+              "--embedding_mode", "sharded"]
+    env = dict(os.environ, HIPFM_SAME_DEVICE="1", HSA_ENABLE_IPC_MODE_LEGACY="0", PYTHONUNBUFFERED="1")
+    for task, extra in (("train", ["--num_epochs", "2"]), ("eval", []), ("infer", []), ("export", [])):
+        cmd = [sys.executable, "-m", "hipfm.launch", "--nproc_per_node", "2", "--master_port", str(_free_port()),
+               "-m", "hipfm", "--task_type", task] + common + extra
+        r = subprocess.run(cmd, env=env, cwd=REPO, timeout=300, stdout=subprocess.PIPE,
+                           stderr=subprocess.STDOUT, text=True)
+        assert r.returncode == 0, f"{task}:\n" + r.stdout[-6000:]
+    evals = [json.loads(line) for line in open(md / "metrics.jsonl") if '"eval"' in line]
+    assert evals and evals[-1]["auc"] > 0.70, evals[-1:]
+    steps = 2 * (20000 // 2 // 512)
+    assert evals[-1]["global_step"] == steps, evals[-1]
+    assert sum(1 for _ in open(pred)) == 500
+    exports = [p for p in sd.iterdir() if p.is_dir()]
+    assert exports and (exports[0] / "saved_model.pb").exists()

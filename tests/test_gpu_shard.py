@@ -623,10 +623,11 @@ def n8_sharded(synth, data, batches, uids):
         got_v[sel] = m.tv[rows]
         got_w[sel] = m.tw[rows]
     p = models[0].p.clone()
+    got_dense = {k: v.clone() for k, v in models[0].dense_tf_params().items()}
     del models, hub, m
     gc.collect()            # (the models sit in reference cycles: free their ~100 GB now)
     torch.cuda.empty_cache()
-    return got_v, got_w, p
+    return got_v, got_w, p, got_dense
 
 
 def n8_single(synth, data, uids):
@@ -642,7 +643,8 @@ def n8_single(synth, data, uids):
         ref.train_step(ids, vals, lab)
     torch.cuda.synchronize()
     ref.check_errors()
-    out = ref.tv[uids].clone(), ref.tw[uids].clone(), ref.p.clone()
+    out = (ref.tv[uids].clone(), ref.tw[uids].clone(), ref.p.clone(),
+           {k: v.clone() for k, v in ref.dense_tf_params().items()})
     del ref
     gc.collect()
     torch.cuda.empty_cache()
@@ -691,8 +693,8 @@ def test_sharded_exchange_n8_criteo_1tb_shape():
         pytest.skip(f"needs ~240 GB of free HBM (have {free / (1 << 30):.0f} GB)")
     synth, data, batches = n8_data()
     uids = torch.unique(torch.cat([d[0].reshape(-1) for d in data]).long())
-    got_v, got_w, p_sh = n8_sharded(synth, data, batches, uids)
-    ref_v, ref_w, ref_p = n8_single(synth, data, uids)
+    got_v, got_w, p_sh, d_sh = n8_sharded(synth, data, batches, uids)
+    ref_v, ref_w, ref_p, d_ref = n8_single(synth, data, uids)
     dv = (got_v - ref_v).abs()
     badu = uids[dv.max(1).values > 2e-7]
     bad_samples = sorted({(s, r) for s, d in enumerate(data)
@@ -705,10 +707,14 @@ def test_sharded_exchange_n8_criteo_1tb_shape():
     assert (p_sh - ref_p).abs().max().item() <= 2e-5 * ref_p.abs().max().item()
     # both native sides against the fp32 golden model (a bug shared by the sharded step and the
     # one-model step at B = 131072 -- chunked field sort + merge -- is invisible to the above)
-    gold_v, gold_w, v0, w0, _ = n8_golden(synth, data, uids)
-    for nm, v, w in (("sharded", got_v, got_w), ("one model", ref_v, ref_w)):
+    gold_v, gold_w, v0, w0, gold = n8_golden(synth, data, uids)
+    d0 = n8_dense(synth)
+    for nm, v, w, d in (("sharded", got_v, got_w, d_sh), ("one model", ref_v, ref_w, d_ref)):
         _golden_close(v, gold_v, v0, f"{nm} fm_v")
         _golden_close(w, gold_w, w0, f"{nm} fm_w")
+        # the dense parameters too (MLP weights / biases, FM bias, output layer)
+        for k, t in d.items():
+            _golden_close(t.float().cpu(), gold.params[k].float().cpu(), d0[k].float().cpu(), f"{nm} {k}")
 
 
 @pytest.mark.parametrize("N,C_slack", [(1, 1.3), (3, 1.3), (8, 1.3), (8, 0.5)])
