@@ -105,6 +105,7 @@ def supervise(argv) -> int:
         env = dict(os.environ, HIPFM_BENCH_CHILD="1", HIPFM_BENCH_RUNG=name, MASTER_PORT=port,
                    TORCHELASTIC_USE_AGENT_STORE="False", HIPFM_BENCH_PROGRESS=prog,
                    HIPFM_BENCH_RESULT=result, **extra)
+        env.update(_same_device_env())
         child = subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env,
                                  start_new_session=True)
         failed = False
@@ -152,6 +153,15 @@ def supervise(argv) -> int:
         store.set(f"hipfm_bench/down{k}_{rank}", "1")
         store.wait([f"hipfm_bench/down{k}_{r}" for r in range(world)])
     return 1
+
+
+def _same_device_env() -> dict:
+    """(HIPFM_SAME_DEVICE=1 only) this rank's CU slice of the shared GPU (parallel/dist.py)."""
+    if os.environ.get("HIPFM_SAME_DEVICE") != "1":
+        return {}
+    from hipfm.parallel.dist import same_device_env
+    return same_device_env(int(os.environ.get("LOCAL_RANK", "0")),
+                           int(os.environ.get("LOCAL_WORLD_SIZE", os.environ.get("WORLD_SIZE", "1"))))
 
 
 def _emit(line: str):

@@ -251,6 +251,184 @@ __global__ void __launch_bounds__(GL_THREADS, 2) gemm_lds_kernel(
       epi_store<EPI>(ep, acc[i][j], m0 + wm * 64 + i * 16 + cr, n0 + wn * 64 + j * 16 + fr, M, N, salt);
 }
 
+// ------------------------------------------------------------------ ping-pong GEMM (tile 9)
+// 256 x 256 workgroup tile, 512 threads = 8 waves in two groups of 4 (group g owns output rows
+// g*128.., wave c of a group owns columns c*64..: a 128 x 64 block per wave, 8 x 4 MFMA 16x16x32
+// tiles = 32 f32x4 accumulators).  Each SIMD hosts one wave of each group, and the groups run one
+// barrier apart ("ping-pong"): between two consecutive s_barriers one group issues the LDS
+// fragment reads (and LDS-DMA staging) of its next phase while the other group's 16 MFMAs run, so
+// the matrix pipe of every SIMD alternates between its two waves instead of idling through each
+// wave's reads.  A 64-deep K-tile is 4 phases, one 64 x 32 output quadrant each, in the snake
+// order (A0,B0) (A0,B1) (A1,B1) (A1,B0): a phase re-reads only the operand half that changes.
+//   slot s (the interval between two barriers): group 0 loads phase s/2 when s is even and
+//   computes it when s is odd; group 1 is one slot later.  K-tile t occupies slots 8t .. 8t+8.
+//   Staging of K-tile t+1 into buffer (t+1)&1 (last read by K-tile t-1, whose reads every wave
+//   retired by slot 8t): group 1 in its load slots 8t+1, 8t+3, group 0 in 8t+2, 8t+4 (4 pieces of
+//   1 KB per slot per wave); each wave waits for its own DMA (vmcnt(0)) in its phase-3 load slot
+//   (slots 8t+6 / 8t+7), so the barrier before slot 8t+8 publishes all of K-tile t+1 to every
+//   wave -- one counted wait per K-tile, DMA in flight across 2-5 barriers.
+// LDS: 2 buffers x (A 256 x 64 + B 256 x 64) bf16 = 128 KB, the swizzled image of tile 8.
+constexpr int PP_BM = 256, PP_BK = 64, PP_THREADS = 512;
+constexpr int PP_PANEL = PP_BM * PP_BK * 2;            // 32 KB: one operand's K-tile
+constexpr int PP_BUF = 2 * PP_PANEL;                   // A + B of one K-tile
+
+// 4 DMA pieces (8 rows x 128 B each) of a 256-row panel: pieces [first, first + 4)
+__device__ __forceinline__ void pp_stage4(char* lds, const bf16* __restrict__ g, int ld, int row0, int k0,
+                                          int first, int lane) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int piece = first + i;
+    const int r = piece * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ ((r >> 1) & 7);
+    const bf16* src = g + (size_t)(row0 + r) * ld + k0 + c * 8;
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                     (__attribute__((address_space(3))) void*)(lds + piece * 1024), 16, 0, 0);
+  }
+}
+
+// pieces [P0, P1) of a wave's 8 staging pieces of one K-tile: 0..3 = A pieces 4w.., 4..7 = B pieces 4w..
+template <int P0, int P1>
+__device__ __forceinline__ void pp_stage_pieces(char* buf, const bf16* __restrict__ A, int lda, int m0,
+                                                const bf16* __restrict__ Bm, int ldb, int n0, int k0,
+                                                int wave, int lane) {
+#pragma unroll
+  for (int p = P0; p < P1; ++p) {
+    const bool isb = p >= 4;
+    const int piece = wave * 4 + (p & 3);
+    const int r = piece * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ ((r >> 1) & 7);
+    const bf16* src = isb ? Bm + (size_t)(n0 + r) * ldb + k0 + c * 8 : A + (size_t)(m0 + r) * lda + k0 + c * 8;
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                     (__attribute__((address_space(3))) void*)(buf + (isb ? PP_PANEL : 0) + piece * 1024),
+                                     16, 0, 0);
+  }
+}
+
+// SPREAD 0: 4 + 4 pieces in two load slots per group (group 1: phases 0, 1; group 0: 1, 2), each
+//           wave's vmcnt(0) in its phase-3 load slot.
+// SPREAD 1: 3 + 3 + 2 pieces over three load slots (group 1: phases 0-2; group 0: 1-3); group 1
+//           waits in its phase-3 load slot, group 0 at the end of its phase-3 compute slot (its
+//           last pieces leave in that phase's load slot; the barrier after the wait publishes
+//           them before either group reads the K-tile).
+template <int EPI, int SPREAD>
+__global__ void __launch_bounds__(PP_THREADS, 1) gemm_pp_kernel(
+    const bf16* __restrict__ A, int lda, const bf16* __restrict__ Bm, int ldb, int M, int N,
+    int kchunk, EpiArgs ep) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * PP_BUF];   // (the only __shared__ object)
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int grp = wave >> 2, wc = wave & 3;
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, rr = nwg & 7;
+  const int tid = (xcd < rr ? xcd * (q8 + 1) : rr * (q8 + 1) + (xcd - rr) * q8) + (bid >> 3);
+  const int tiles_n = N / PP_BM;
+  const int m0 = (tid / tiles_n) * PP_BM, n0 = (tid % tiles_n) * PP_BM;
+  const int kb = blockIdx.z * kchunk;
+  const int nt = kchunk / PP_BK;
+  const int fr = lane & 15, fq = lane >> 4;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // prologue: K-tile 0 into buffer 0 (pieces 4w..4w+3 of A and of B per wave)
+  pp_stage4(smem, A, lda, m0, kb, wave * 4, lane);
+  pp_stage4(smem + PP_PANEL, Bm, ldb, n0, kb, wave * 4, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  if (grp == 1) {                         // the stagger: group 1 runs one slot behind
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  }
+
+  bf16x8 fa[4][2], fb[2][2];
+  for (int t = 0; t < nt; ++t) {
+    const char* pa = smem + (t & 1) * PP_BUF;
+    const char* pb = pa + PP_PANEL;
+    char* nxt = smem + ((t + 1) & 1) * PP_BUF;
+    const bool more = t + 1 < nt;
+    const int kn = kb + (t + 1) * PP_BK;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int qa = (q == 0 || q == 1) ? 0 : 1;     // snake: (0,0) (0,1) (1,1) (1,0)
+      const int qb = (q == 0 || q == 3) ? 0 : 1;
+      // ---- load slot: this phase's fragments (+ staging of the next K-tile)
+      if (q == 3 && (SPREAD == 0 || grp == 1))
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // my DMA of K-tile t+1 landed
+      if (q == 0 || q == 2) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks)
+            fa[i][ks] = *reinterpret_cast<const bf16x8*>(
+                pa + gl_slot(grp * 128 + qa * 64 + i * 16 + fr, ks * 4 + fq));
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+          fb[j][ks] = *reinterpret_cast<const bf16x8*>(
+              pb + gl_slot(wc * 64 + qb * 32 + j * 16 + fr, ks * 4 + fq));
+      if (SPREAD == 0) {
+        // group 1 stages in its phase-0/1 load slots, group 0 in its phase-1/2 slots
+        if (more && ((grp == 1 && q == 0) || (grp == 0 && q == 1)))
+          pp_stage4(nxt, A, lda, m0, kn, wave * 4, lane);
+        if (more && ((grp == 1 && q == 1) || (grp == 0 && q == 2)))
+          pp_stage4(nxt + PP_PANEL, Bm, ldb, n0, kn, wave * 4, lane);
+      } else if (more) {
+        const int sl = q - (grp == 0 ? 1 : 0);     // this group's staging slot 0..2
+        if (sl == 0) pp_stage_pieces<0, 3>(nxt, A, lda, m0, Bm, ldb, n0, kn, wave, lane);
+        if (sl == 1) pp_stage_pieces<3, 6>(nxt, A, lda, m0, Bm, ldb, n0, kn, wave, lane);
+        if (sl == 2) pp_stage_pieces<6, 8>(nxt, A, lda, m0, Bm, ldb, n0, kn, wave, lane);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      // ---- compute slot
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[qa * 4 + i][qb * 2 + j] =
+                __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][ks], fb[j][ks], acc[qa * 4 + i][qb * 2 + j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      if (SPREAD == 1 && q == 3 && grp == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  if (grp == 0) __builtin_amdgcn_s_barrier();   // (every wave passes the same number of barriers)
+
+  uint32_t salt = 0;
+  if (EPI == EPI_FWD && ep.drop) salt = dropout_salt(ep.seed, (uint32_t)(*ep.step), ep.layer);
+  const int cr = fq * 4;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      epi_store<EPI>(ep, acc[i][j], m0 + grp * 128 + i * 16 + cr, n0 + wc * 64 + j * 16 + fr, M, N, salt);
+}
+
+template <int EPI, int SPREAD>
+static int launch_gemm_pp(const bf16* A, int lda, const bf16* B, int ldb, int M, int N, int Kd,
+                          int splitk, const EpiArgs& ep, hipStream_t st) {
+  if (M % PP_BM || N % PP_BM || splitk < 1 || Kd % (PP_BK * splitk) || lda % 8 || ldb % 8 ||
+      ((uintptr_t)A & 15) || ((uintptr_t)B & 15))
+    return (int)hipErrorInvalidValue;
+  dim3 grid((M / PP_BM) * (N / PP_BM), 1, splitk);
+  hipLaunchKernelGGL((gemm_pp_kernel<EPI, SPREAD>), grid, dim3(PP_THREADS), 0, st, A, lda, B, ldb, M, N,
+                     Kd / splitk, ep);
+  HFM_LAUNCH_CHECK();
+}
+
 template <int EPI>
 static int launch_gemm_lds(const bf16* A, int lda, const bf16* B, int ldb, int M, int N, int Kd,
                            int splitk, const EpiArgs& ep, hipStream_t st) {
@@ -264,7 +442,8 @@ static int launch_gemm_lds(const bf16* A, int lda, const bf16* B, int ldb, int M
 }
 
 // tile: 0 = 64x64 (2x2 waves), 1 = 128x32 (4x1), 2 = 32x128 (1x4), 3 = 32x32 (1x1), 4 = 32x64 (1x2),
-//       5 = 32x160 (1x5), 6 = 32x320 (1x10), 7 = 32x256 (1x8), 8 = 128x128 LDS-staged (wide layers)
+//       5 = 32x160 (1x5), 6 = 32x320 (1x10), 7 = 32x256 (1x8), 8 = 128x128 LDS-staged (wide layers),
+//       9 = 256x256 ping-pong (wide layers, 8 waves)
 template <int EPI>
 static int gemm_tile(int tile, const bf16* A, int lda, const bf16* B, int ldb, int M, int N, int Kd,
                      int splitk, const EpiArgs& ep, hipStream_t st) {
@@ -278,6 +457,8 @@ static int gemm_tile(int tile, const bf16* A, int lda, const bf16* B, int ldb, i
     case 6: return launch_gemm<1, 10, EPI>(A, lda, B, ldb, M, N, Kd, splitk, ep, st);
     case 7: return launch_gemm<1, 8, EPI>(A, lda, B, ldb, M, N, Kd, splitk, ep, st);
     case 8: return launch_gemm_lds<EPI>(A, lda, B, ldb, M, N, Kd, splitk, ep, st);
+    case 9: return launch_gemm_pp<EPI, 0>(A, lda, B, ldb, M, N, Kd, splitk, ep, st);
+    case 10: return launch_gemm_pp<EPI, 1>(A, lda, B, ldb, M, N, Kd, splitk, ep, st);
     default: return (int)hipErrorInvalidValue;
   }
 }

@@ -116,6 +116,9 @@ def main(argv=None) -> int:
         env.update(RANK=str(node_rank * nproc + lr), LOCAL_RANK=str(lr), WORLD_SIZE=str(world),
                    LOCAL_WORLD_SIZE=str(nproc), MASTER_ADDR=master, MASTER_PORT=str(a.master_port),
                    GROUP_RANK=str(node_rank))
+        if env.get("HIPFM_SAME_DEVICE") == "1":        # one-GPU rehearsal: a CU slice per rank
+            from .parallel.dist import same_device_env
+            env.update(same_device_env(lr, nproc))
         procs.append(subprocess.Popen([sys.executable] + cmd_tail, env=env))
     rc = 0
     try:

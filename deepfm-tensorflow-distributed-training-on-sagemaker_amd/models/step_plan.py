@@ -95,7 +95,7 @@ class StepPlan:
     w8_after_owner: bool = False   # fp8: ... after the owner launch's dense optimizer
     grow_rows: bool = False        # run-sorted sfwg step: the tower writes each slot's gradient row
                                    # to its sorted position; the sparse launch streams them
-    overlap_dense: bool = False    # multi-rank lazy step: the dense gradient (its own wgfin launch
+    overlap_dense: bool = False    # multi-rank lazy / tf1 split step: the dense gradient (its own wgfin launch
                                    # after the tower) is all-reduced on the main stream WHILE the
                                    # sparse backward runs on a graph branch
 
@@ -141,7 +141,9 @@ def plan_step(mode: ModeSpec, kn: StepKnobs, B: int, sort_plan: Optional[Tuple],
     # overlap: the dense gradient leaves the sparse launch (its own wgfin launch, gradient only,
     # right after the tower) so its all-reduce (G2a) runs on the main stream while the sparse
     # backward runs on a branch; the gradient rows follow in G2b after the join
-    ovl = (kn.sh_overlap and mode.native_exchange and mode.lazy and mode.fused and kn.wgfin and
+    # (the tf1_dense split form too: its flagged rows take the lazy owner update and the owner
+    # launch sweeps every other row, whichever way the dense gradient travelled)
+    ovl = (kn.sh_overlap and mode.native_exchange and owner_lazy and mode.fused and kn.wgfin and
            kn.sh_apply_dense)
     xfuse = (mode.native_exchange and owner_lazy and kn.wgfin and mode.fused and
              kn.sh_apply_dense and mode.wgfin_fits and not ovl)

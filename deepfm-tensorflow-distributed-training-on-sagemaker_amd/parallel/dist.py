@@ -37,7 +37,7 @@ import torch
 import torch.distributed as dist
 
 from ..ops import kernels as KN
-from ..utils.knobs import flag
+from ..utils.knobs import flag, knob
 
 
 def same_device() -> bool:
@@ -49,6 +49,40 @@ def same_device() -> bool:
 def local_device_index() -> int:
     """The HIP device of this rank: LOCAL_RANK (one process per GPU), or 0 under same_device()."""
     return 0 if same_device() else int(os.environ.get("LOCAL_RANK", "0"))
+
+
+def _device_cu_count(default: int = 256) -> int:
+    """CUs of GPU 0 from the KFD topology (no HIP call: usable before any process touches the GPU)."""
+    root = "/sys/class/kfd/kfd/topology/nodes"
+    try:
+        for node in sorted(os.listdir(root), key=lambda x: int(x) if x.isdigit() else 0):
+            props = {}
+            with open(os.path.join(root, node, "properties")) as f:
+                for line in f:
+                    k, _, v = line.partition(" ")
+                    props[k] = v.strip()
+            simd, per = int(props.get("simd_count", "0")), int(props.get("simd_per_cu", "0") or 0)
+            if simd > 0 and per > 0:
+                return simd // per
+    except (OSError, ValueError):
+        pass
+    return default
+
+
+def same_device_env(local_rank: int, local_world: int) -> dict:
+    """Environment of one rank under HIPFM_SAME_DEVICE=1: a disjoint slice of the GPU's CUs
+    (ROC_GLOBAL_CU_MASK, applied by the HIP runtime to every queue the process creates).  Ranks
+    sharing every CU can starve each other's in-launch hand-offs -- a workgroup spinning on an
+    earlier workgroup of its own launch that another process's spinning workgroups keep from being
+    dispatched (the 8-rank rehearsal's sparse look-back timed out that way); with disjoint CUs each
+    rank is a smaller GPU of its own, as one process per GPU is.  Empty unless the mode is on."""
+    if not same_device() or local_world <= 1 or knob("HIPFM_SAME_DEVICE_CU_SPLIT") != "1":
+        return {}
+    n = _device_cu_count()
+    per = n // local_world
+    lo = local_rank * per
+    mask = ((1 << per) - 1) << lo
+    return {"ROC_GLOBAL_CU_MASK": hex(mask)}
 
 
 def init_distributed(backend: Optional[str] = None, timeout_s: int = 600):

@@ -49,7 +49,7 @@ KNOBS: Dict[str, Knob] = {
                              "all-gathered and summed in rank order by the owner launch (allgather: the "
                              "default, deterministic, 7 x 0.2 MB per rank at N = 8) or all-reduced by RCCL "
                              "(allreduce; auto: all-reduce from 4 ranks -- both reassociate the sum)"),
-    "HIPFM_SH_OVERLAP": Knob("0", "variant", "multi-rank lazy step: the dense gradient in its own "
+    "HIPFM_SH_OVERLAP": Knob("0", "variant", "multi-rank step (lazy or the tf1_dense split form): the dense gradient in its own "
                              "launch after the tower, all-reduced on the main stream while the sparse "
                              "backward runs on a graph branch (1), instead of all-gathered with the "
                              "gradient rows after it (0: one queue, no join; the 1-rank proxy's best)"),
@@ -89,6 +89,8 @@ KNOBS: Dict[str, Knob] = {
     "HIPFM_SAME_DEVICE": Knob("0", "harness", "multi-rank runs with every rank on device 0: gloo process "
                               "group + the same-device collective engine (parallel/loopback.py) -- the "
                               "N-GPU job's processes and step rehearsed on one GPU"),
+    "HIPFM_SAME_DEVICE_CU_SPLIT": Knob("1", "harness", "same-device rehearsal: each rank's queues get a disjoint "
+                                      "slice of the CUs (ROC_GLOBAL_CU_MASK; 0: every rank on every CU)"),
     "HIPFM_LB_TIMEOUT_MS": Knob("60000", "harness", "same-device engine: a collective barrier waits at "
                                 "most this long, then poisons the transport (every rank raises)"),
     "HIPFM_ARCH": Knob("gfx950", "harness", "offload arch of the HIP build"),

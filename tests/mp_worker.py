@@ -21,6 +21,10 @@ if REPO not in sys.path:
 
 def main():
     cfg = json.loads(sys.argv[1])
+    import hipfm  # noqa: F401
+    from hipfm.parallel.dist import same_device_env
+    # this rank's CU slice, before the first HIP call of the process creates a queue
+    os.environ.update(same_device_env(int(os.environ["LOCAL_RANK"]), int(os.environ["LOCAL_WORLD_SIZE"])))
     import torch
     import torch.distributed as dist
     import hipfm  # noqa: F401

@@ -28,14 +28,17 @@ def _ref(A, B):
     return A.float() @ B.float().t()
 
 
-@pytest.mark.parametrize("M,N,K,split", [(256, 128, 64, 1), (384, 256, 320, 1), (256, 512, 4096, 1),
-                                         (512, 256, 2048, 4), (1024, 1024, 1024, 2)])
-def test_lds_gemm_f32_matches_reference(M, N, K, split):
+@pytest.mark.parametrize("tile,M,N,K,split", [(8, 256, 128, 64, 1), (8, 384, 256, 320, 1), (8, 256, 512, 4096, 1),
+                                              (8, 512, 256, 2048, 4), (8, 1024, 1024, 1024, 2),
+                                              (9, 256, 256, 64, 1), (9, 512, 768, 320, 1), (9, 512, 512, 4096, 1),
+                                              (9, 768, 256, 2048, 4), (9, 1024, 1024, 1024, 2),
+                                              (10, 512, 768, 320, 1), (10, 768, 256, 2048, 4), (10, 1024, 1024, 1024, 2)])
+def test_lds_gemm_f32_matches_reference(tile, M, N, K, split):
     A, B = _ops(M, N, K, seed=M + N + K)
     out = torch.full((split, M, N), float("nan"), device=DEV)
     ep = EpiArgs()
     ep.out = out.data_ptr()
-    KN.gemm_nt(KN.EPI_F32, KN.TILE_LDS, A, K, B, K, M, N, K, split, ep)
+    KN.gemm_nt(KN.EPI_F32, tile, A, K, B, K, M, N, K, split, ep)
     torch.cuda.synchronize()
     ref = _ref(A, B)
     got = out.sum(0)
@@ -49,15 +52,17 @@ def test_lds_gemm_f32_matches_reference(M, N, K, split):
     assert torch.equal(out, o2)
 
 
+@pytest.mark.parametrize("tile", [8, 9, 10])
 @pytest.mark.parametrize("epi", ["fwd", "fwd_eval", "dgrad", "relu_f32"])
-def test_lds_gemm_epilogues_match_register_tile(epi):
+def test_lds_gemm_epilogues_match_register_tile(tile, epi):
     M, N, K = 512, 256, 640
     A, B = _ops(M, N, K, seed=3)
+    big = tile
     bias = torch.randn(N, device=DEV)
     step = torch.tensor([7], dtype=torch.int64, device=DEV)
     hprev = torch.randn(M, N, device=DEV).bfloat16()
     outs = []
-    for tile in (KN.TILE_LDS, 0):
+    for tile in (big, 0):
         f32 = epi == "relu_f32"
         o = torch.zeros(M, N, device=DEV, dtype=torch.float32 if f32 else torch.bfloat16)
         ot = torch.zeros(N, M, device=DEV, dtype=torch.bfloat16)

@@ -291,8 +291,11 @@ def test_run_routing_matches_global_batch(N, update, steps):
         assert t[2 + 2 * j][0] == (KN.COMM_A2A, C * RWG * 4)      # G2: gradient rows first
 
 
-@pytest.mark.parametrize("N,run,sharded", [(2, True, True), (4, True, True), (3, False, True), (3, False, False)])
-def test_overlapped_exchange_matches_default(monkeypatch, N, run, sharded):
+@pytest.mark.parametrize("N,run,sharded,update", [(2, True, True, "lazy"), (4, True, True, "lazy"),
+                                                   (3, False, True, "lazy"), (3, False, False, "lazy"),
+                                                   (3, False, True, "tf1_dense"), (2, True, True, "tf1_dense"),
+                                                   (2, False, False, "tf1_dense")])
+def test_overlapped_exchange_matches_default(monkeypatch, N, run, sharded, update):
     """HIPFM_SH_OVERLAP: the dense gradient in its own launch after the tower,
     all-reduced on the main stream (G2a) while the sparse backward runs on a graph branch, the
     gradient rows after the join (G2b).  Same parameters as the default exchange (all-gathered
@@ -314,10 +317,11 @@ def test_overlapped_exchange_matches_default(monkeypatch, N, run, sharded):
         hub = _Hub(N)
         models = []
         for r in range(N):
-            m = NativeDeepFM(V, F, K, layers, keep, sparse_update="lazy", learning_rate=1e-3, batch_size=B,
+            m = NativeDeepFM(V, F, K, layers, keep, sparse_update=update, learning_rate=1e-3, batch_size=B,
                              device=DEV, init=False, comm=MeshComm(hub, r, sharded=sharded),
                              field_ranges=synth.field_ranges())
             m.load_tf_params(params)
+            assert update == "lazy" or m.tf1_xsplit          # (tf1_dense: the split form's owner sweep)
             x = m.shx if sharded else m.rpx
             x.trace = []
             models.append(m)
@@ -371,10 +375,11 @@ def test_dense_allreduce_equals_rank_order_gather(monkeypatch, sharded):
         hub = _Hub(N)
         models = []
         for r in range(N):
-            m = NativeDeepFM(V, F, K, layers, keep, sparse_update="lazy", learning_rate=1e-3, batch_size=B,
+            m = NativeDeepFM(V, F, K, layers, keep, sparse_update=update, learning_rate=1e-3, batch_size=B,
                              device=DEV, init=False, comm=MeshComm(hub, r, sharded=sharded),
                              field_ranges=synth.field_ranges())
             m.load_tf_params(params)
+            assert update == "lazy" or m.tf1_xsplit          # (tf1_dense: the split form's owner sweep)
             x = m.shx if sharded else m.rpx
             x.trace = []
             models.append(m)

@@ -145,15 +145,16 @@ def test_plan_invariants_over_the_mode_matrix():
                         n += 1
                         assert sum(dense_opt_sites(p)) == 1, (m, kn, B, sp, p)
                         assert p.defer_wgrad == (p.dense_branch or p.sfwg or p.xfuse or p.overlap_dense)
-                        assert not p.overlap_dense or (m.native_exchange and m.lazy and p.exchange_allreduce
-                                                       and p.sh_apply_dense and not p.xfuse)
+                        assert not p.overlap_dense or (m.native_exchange and (m.lazy or m.tf1x)
+                                                       and p.exchange_allreduce and p.sh_apply_dense
+                                                       and not p.xfuse)
                         assert not p.sfwg or (p.fuse_opt and p.dense_early and not m.exchange)
                         assert not p.fuse_opt or (m.fused and p.dense_early)
                         assert not p.tf1_merged or p.sfwg
                         assert not (p.tf1_merged and p.tf1_branch)
                         assert not p.xfuse or (m.native_exchange and p.sh_apply_dense and (m.lazy or m.tf1x))
                         if m.tf1x and m.fused and m.wgfin_fits and kn.wgfin and kn.sh_apply_dense:
-                            assert p.xfuse and p.sh_apply_dense      # the sweep's owner launch
+                            assert (p.xfuse or p.overlap_dense) and p.sh_apply_dense   # the sweep's owner launch
                         assert not p.exchange_allreduce or (m.native_exchange and not p.xfuse)
                         assert not p.sh_apply_dense or m.native_exchange
                         assert not (p.run_sorted and (p.fork_sort or p.prefetch_next))
