@@ -192,6 +192,7 @@ def main():
     ap.add_argument("--embedding_size", type=int, default=8)
     ap.add_argument("--deep_layers", default="128,64,32")
     ap.add_argument("--dropout", default="0.5,0.5,0.5")
+    ap.add_argument("--batch_norm", action="store_true", help="batch norm after each hidden layer (HVD:207-208)")
     ap.add_argument("--optimizer", default="Adam")
     ap.add_argument("--sparse_update", default="lazy")
     ap.add_argument("--embedding_mode", default="auto")
@@ -280,7 +281,8 @@ def main():
                          learning_rate=5e-4, optimizer=args.optimizer,
                          sparse_update=args.sparse_update, seed=1234, batch_size=B, device=dev,
                          comm=comm, field_ranges=synth.field_ranges(), mlp_dtype=args.mlp_dtype,
-                         emb_dtype=args.emb_dtype, exchange_rows=args.exchange_rows)
+                         emb_dtype=args.emb_dtype, exchange_rows=args.exchange_rows,
+                         batch_norm=args.batch_norm)
     _progress()
     if args.field_major_ids:
         # ids stored field-major ([F, B] storage, [B, F] view: the layout the Estimator's HBM
@@ -417,7 +419,9 @@ def main():
             "data": "synthetic (Criteo-shaped Zipf ids + teacher labels, HBM-resident), random-init weights",
             "config": {
                 "model": f"DeepFM {_SHAPE_NAMES.get(args.preset, args.preset)} (F={F}, V={synth.feature_size}, "
-                         f"K={args.embedding_size}, deep {args.deep_layers}, keep {args.dropout})",
+                         f"K={args.embedding_size}, deep {args.deep_layers}, keep {args.dropout}"
+                         f"{', batch norm' if args.batch_norm else ''})",
+                "tower": "fused one-launch tower" if model.fused else "per-layer GEMMs (mlp.hip)",
                 "global_batch": world * B,
                 "per_gpu_batch": B,
                 "seq_len": None,

@@ -287,17 +287,16 @@ __device__ __forceinline__ void pp_stage4(char* lds, const bf16* __restrict__ g,
 }
 
 // pieces [P0, P1) of a wave's 8 staging pieces of one K-tile: 0..3 = A pieces 4w.., 4..7 = B pieces 4w..
+// `off[p]`: the lane's element offset of piece p in its operand at k = 0 (hoisted out of the loop:
+// a piece then costs one address add instead of the row / swizzle arithmetic)
 template <int P0, int P1>
-__device__ __forceinline__ void pp_stage_pieces(char* buf, const bf16* __restrict__ A, int lda, int m0,
-                                                const bf16* __restrict__ Bm, int ldb, int n0, int k0,
-                                                int wave, int lane) {
+__device__ __forceinline__ void pp_stage_pieces(char* buf, const bf16* __restrict__ A, const bf16* __restrict__ Bm,
+                                                const int* off, int k0, int wave) {
 #pragma unroll
   for (int p = P0; p < P1; ++p) {
     const bool isb = p >= 4;
     const int piece = wave * 4 + (p & 3);
-    const int r = piece * 8 + (lane >> 3);
-    const int c = (lane & 7) ^ ((r >> 1) & 7);
-    const bf16* src = isb ? Bm + (size_t)(n0 + r) * ldb + k0 + c * 8 : A + (size_t)(m0 + r) * lda + k0 + c * 8;
+    const bf16* src = (isb ? Bm : A) + off[p] + k0;
     __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                      (__attribute__((address_space(3))) void*)(buf + (isb ? PP_PANEL : 0) + piece * 1024),
                                      16, 0, 0);
@@ -325,6 +324,18 @@ __global__ void __launch_bounds__(PP_THREADS, 1) gemm_pp_kernel(
   const int kb = blockIdx.z * kchunk;
   const int nt = kchunk / PP_BK;
   const int fr = lane & 15, fq = lane >> 4;
+  // fragment byte offsets in a panel: row r = base + 16 i + fr has swizzle (r >> 1) & 7 = (fr >> 1) & 7
+  // (the row bases are multiples of 16), so a read is a lane base + a compile-time offset
+  const int swz = (fr >> 1) & 7;
+  const int la[2] = {(grp * 128 + fr) * 128 + ((fq ^ swz) << 4), (grp * 128 + fr) * 128 + (((4 + fq) ^ swz) << 4)};
+  const int lb[2] = {(wc * 64 + fr) * 128 + ((fq ^ swz) << 4), (wc * 64 + fr) * 128 + (((4 + fq) ^ swz) << 4)};
+  int soff[8];                            // (SPREAD 1) per-piece source offsets at k = 0
+#pragma unroll
+  for (int p = 0; p < 8; ++p) {
+    const int r = (wave * 4 + (p & 3)) * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ ((r >> 1) & 7);
+    soff[p] = p < 4 ? (m0 + r) * lda + c * 8 : (n0 + r) * ldb + c * 8;
+  }
 
   f32x4 acc[8][4];
 #pragma unroll
@@ -362,15 +373,13 @@ __global__ void __launch_bounds__(PP_THREADS, 1) gemm_pp_kernel(
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int ks = 0; ks < 2; ++ks)
-            fa[i][ks] = *reinterpret_cast<const bf16x8*>(
-                pa + gl_slot(grp * 128 + qa * 64 + i * 16 + fr, ks * 4 + fq));
+            fa[i][ks] = *reinterpret_cast<const bf16x8*>(pa + la[ks] + (qa * 64 + i * 16) * 128);
       }
 #pragma unroll
       for (int j = 0; j < 2; ++j)
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks)
-          fb[j][ks] = *reinterpret_cast<const bf16x8*>(
-              pb + gl_slot(wc * 64 + qb * 32 + j * 16 + fr, ks * 4 + fq));
+          fb[j][ks] = *reinterpret_cast<const bf16x8*>(pb + lb[ks] + (qb * 32 + j * 16) * 128);
       if (SPREAD == 0) {
         // group 1 stages in its phase-0/1 load slots, group 0 in its phase-1/2 slots
         if (more && ((grp == 1 && q == 0) || (grp == 0 && q == 1)))
@@ -379,9 +388,9 @@ __global__ void __launch_bounds__(PP_THREADS, 1) gemm_pp_kernel(
           pp_stage4(nxt + PP_PANEL, Bm, ldb, n0, kn, wave * 4, lane);
       } else if (more) {
         const int sl = q - (grp == 0 ? 1 : 0);     // this group's staging slot 0..2
-        if (sl == 0) pp_stage_pieces<0, 3>(nxt, A, lda, m0, Bm, ldb, n0, kn, wave, lane);
-        if (sl == 1) pp_stage_pieces<3, 6>(nxt, A, lda, m0, Bm, ldb, n0, kn, wave, lane);
-        if (sl == 2) pp_stage_pieces<6, 8>(nxt, A, lda, m0, Bm, ldb, n0, kn, wave, lane);
+        if (sl == 0) pp_stage_pieces<0, 3>(nxt, A, Bm, soff, kn, wave);
+        if (sl == 1) pp_stage_pieces<3, 6>(nxt, A, Bm, soff, kn, wave);
+        if (sl == 2) pp_stage_pieces<6, 8>(nxt, A, Bm, soff, kn, wave);
       }
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_barrier();
@@ -415,6 +424,100 @@ __global__ void __launch_bounds__(PP_THREADS, 1) gemm_pp_kernel(
 #pragma unroll
     for (int j = 0; j < 4; ++j)
       epi_store<EPI>(ep, acc[i][j], m0 + grp * 128 + i * 16 + cr, n0 + wc * 64 + j * 16 + fr, M, N, salt);
+}
+
+// ------------------------------------------------------------------ register-blocked GEMM (tile 11)
+// 256 x 256 workgroup tile, 4 waves (one per SIMD), each owning a 128 x 128 block: 8 x 8 MFMA
+// 16x16x32 tiles = 64 f32x4 accumulators (256 registers, the accumulation file).  Per 64-deep
+// K-tile a wave reads 2 x (8 + 8) fragments for 128 MFMAs -- a quarter of an LDS read per MFMA,
+// half the ping-pong tile's (profiles/r6_gemm_pmc_raw.md: its LDS-issue stalls and barrier waits
+// held MFMA busy at 39 %).  Fragments of the second 32-deep half are read while the first half's
+// 64 MFMAs run; the next K-tile streams in by LDS-DMA (16 pieces per wave) into the other buffer,
+// one vmcnt(0) + barrier per K-tile.  LDS: 2 x (A 256 x 64 + B 256 x 64) bf16 = 128 KB.
+constexpr int RB_THREADS = 256;
+
+template <int EPI>
+__global__ void __launch_bounds__(RB_THREADS) __attribute__((amdgpu_waves_per_eu(1, 1))) gemm_rb_kernel(
+    const bf16* __restrict__ A, int lda, const bf16* __restrict__ Bm, int ldb, int M, int N,
+    int kchunk, EpiArgs ep) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * PP_BUF];   // (the only __shared__ object)
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wr = wave >> 1, wcn = wave & 1;
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, rr = nwg & 7;
+  const int tid = (xcd < rr ? xcd * (q8 + 1) : rr * (q8 + 1) + (xcd - rr) * q8) + (bid >> 3);
+  const int tiles_n = N / PP_BM;
+  const int m0 = (tid / tiles_n) * PP_BM, n0 = (tid % tiles_n) * PP_BM;
+  const int kb = blockIdx.z * kchunk;
+  const int nt = kchunk / PP_BK;
+  const int fr = lane & 15, fq = lane >> 4;
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // K-tile staging: 32 A pieces + 32 B pieces of 1 KB, 8 + 8 per wave
+  auto stage = [&](char* buf, int k0) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int piece = wave * 8 + i;
+      const int r = piece * 8 + (lane >> 3);
+      const int c = (lane & 7) ^ ((r >> 1) & 7);
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(A + (size_t)(m0 + r) * lda + k0 + c * 8),
+          (__attribute__((address_space(3))) void*)(buf + piece * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(Bm + (size_t)(n0 + r) * ldb + k0 + c * 8),
+          (__attribute__((address_space(3))) void*)(buf + PP_PANEL + piece * 1024), 16, 0, 0);
+    }
+  };
+  stage(smem, kb);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int t = 0; t < nt; ++t) {
+    const char* pa = smem + (t & 1) * PP_BUF;
+    const char* pb = pa + PP_PANEL;
+    if (t + 1 < nt) stage(smem + ((t + 1) & 1) * PP_BUF, kb + (t + 1) * PP_BK);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 fa[8], fb[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        fa[i] = *reinterpret_cast<const bf16x8*>(pa + gl_slot(wr * 128 + i * 16 + fr, ks * 4 + fq));
+        fb[i] = *reinterpret_cast<const bf16x8*>(pb + gl_slot(wcn * 128 + i * 16 + fr, ks * 4 + fq));
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  uint32_t salt = 0;
+  if (EPI == EPI_FWD && ep.drop) salt = dropout_salt(ep.seed, (uint32_t)(*ep.step), ep.layer);
+  const int cr = fq * 4;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      epi_store<EPI>(ep, acc[i][j], m0 + wr * 128 + i * 16 + cr, n0 + wcn * 128 + j * 16 + fr, M, N, salt);
+}
+
+template <int EPI>
+static int launch_gemm_rb(const bf16* A, int lda, const bf16* B, int ldb, int M, int N, int Kd,
+                          int splitk, const EpiArgs& ep, hipStream_t st) {
+  if (M % PP_BM || N % PP_BM || splitk < 1 || Kd % (PP_BK * splitk) || lda % 8 || ldb % 8 ||
+      ((uintptr_t)A & 15) || ((uintptr_t)B & 15))
+    return (int)hipErrorInvalidValue;
+  dim3 grid((M / PP_BM) * (N / PP_BM), 1, splitk);
+  hipLaunchKernelGGL((gemm_rb_kernel<EPI>), grid, dim3(RB_THREADS), 0, st, A, lda, B, ldb, M, N,
+                     Kd / splitk, ep);
+  HFM_LAUNCH_CHECK();
 }
 
 template <int EPI, int SPREAD>
@@ -459,6 +562,7 @@ static int gemm_tile(int tile, const bf16* A, int lda, const bf16* B, int ldb, i
     case 8: return launch_gemm_lds<EPI>(A, lda, B, ldb, M, N, Kd, splitk, ep, st);
     case 9: return launch_gemm_pp<EPI, 0>(A, lda, B, ldb, M, N, Kd, splitk, ep, st);
     case 10: return launch_gemm_pp<EPI, 1>(A, lda, B, ldb, M, N, Kd, splitk, ep, st);
+    case 11: return launch_gemm_rb<EPI>(A, lda, B, ldb, M, N, Kd, splitk, ep, st);
     default: return (int)hipErrorInvalidValue;
   }
 }
@@ -600,8 +704,107 @@ __global__ void __launch_bounds__(256) head_kernel(HeadArgs a) {
     part[c] = ((wsum[0][c] + wsum[1][c]) + wsum[2][c]) + wsum[3][c];
 }
 
+// Wide last layers (L > 256, multiple of 64: the reference's 4096-wide GPU tower, DOC p.37), 64
+// samples per 256-thread workgroup like head_kernel (same partial rows and finalize jobs):
+//   pass 1: each wave takes 16 samples: y_d by a lane-strided dot + butterfly, then p / loss /
+//           dlogit; the 64 dlogits go to LDS;
+//   pass 2: each lane owns columns (wave w: c = 64 w + lane + 256 k) and walks the 64 samples:
+//           dZ row-major stores (coalesced across lanes), the transposed copy as 16-B stores of 8
+//           consecutive samples, and the column's partial sum dl * h in sample order.
+__global__ void __launch_bounds__(256) head_wide_kernel(HeadArgs a) {
+  __shared__ float hw_dl[64], hw_loss[64];
+  const int L = a.L;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int bb = blockIdx.x * 64;
+  for (int s = 0; s < 16; ++s) {
+    const int b = bb + wv * 16 + s;
+    float yd = 0.f;
+    if (b < a.M) {
+      const bf16* hr = a.h + (size_t)b * L;
+      for (int c = lane; c < L; c += 64) yd += bf2f(hr[c]) * a.w_out[c];
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) yd += __shfl_xor(yd, o, 64);
+    float dl = 0.f, lossb = 0.f;
+    if (b < a.M) {
+      const float y = a.y_fm[b] + yd + a.b_out[0];
+      const float p = 1.f / (1.f + __expf(-y));
+      if (lane == 0) {
+        a.prob[b] = p;
+        if (a.logit) a.logit[b] = y;
+      }
+      if (a.labels && b < a.nvalid) {
+        const float lab = a.labels[b];
+        if (a.square_loss) {
+          lossb = (p - lab) * (p - lab);
+          dl = 2.f * (p - lab) * p * (1.f - p) * a.gscale;
+        } else {
+          lossb = fmaxf(y, 0.f) - y * lab + log1pf(__expf(-fabsf(y)));
+          dl = (p - lab) * a.gscale;
+        }
+      }
+      if (a.train && lane == 0) a.dlogit[b] = dl;
+    }
+    if (lane == 0) {
+      hw_dl[wv * 16 + s] = dl;
+      hw_loss[wv * 16 + s] = lossb;
+    }
+  }
+  __syncthreads();
+  float* part = a.partial + (size_t)blockIdx.x * (L + 2);
+  const bool full = bb + 64 <= a.M && (a.M % 8) == 0;
+  for (int c = wv * 64 + lane; c < L; c += 256) {
+    const float w = a.w_out[c];
+    float cs = 0.f;
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {
+      bf16x8 col;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int s = g * 8 + j, b = bb + s;
+        const float dl = hw_dl[s];
+        const float h = b < a.M ? bf2f(a.h[(size_t)b * L + c]) : 0.f;
+        cs += dl * h;
+        float v = 0.f;
+        if (a.train && b < a.M) {
+          if (a.dh) a.dh[(size_t)b * L + c] = dl * w;
+          else {
+            v = h > 0.f ? dl * w * a.scale_l : 0.f;
+            a.dz[(size_t)b * L + c] = f2bf(v);
+          }
+        }
+        col[j] = f2bf(v);
+      }
+      if (a.train && !a.dh) {
+        if (full) {
+          *reinterpret_cast<bf16x8*>(a.dz_t + (size_t)c * a.M + bb + g * 8) = col;
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            if (bb + g * 8 + j < a.M) a.dz_t[(size_t)c * a.M + bb + g * 8 + j] = col[j];
+        }
+      }
+    }
+    part[c] = a.train ? cs : 0.f;
+  }
+  if (threadIdx.x == 0) {
+    float d = 0.f, l = 0.f;
+    for (int s = 0; s < 64; ++s) {
+      d += hw_dl[s];
+      l += hw_loss[s];
+    }
+    part[L] = d;
+    part[L + 1] = l;
+  }
+}
+
 HFM_API int hfm_head(const HeadArgs* a, hipStream_t st) {
   const int grid = (a->M + 63) / 64;
+  if (a->L > 256) {
+    if (a->L % 64) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(head_wide_kernel, dim3(grid), dim3(256), 0, st, *a);
+    HFM_LAUNCH_CHECK();
+  }
   switch (a->L) {
 #define HL(LL) case LL: hipLaunchKernelGGL(head_kernel<LL>, dim3(grid), dim3(256), 0, st, *a); break;
     HL(32) HL(64) HL(96) HL(128) HL(160) HL(192) HL(224) HL(256)

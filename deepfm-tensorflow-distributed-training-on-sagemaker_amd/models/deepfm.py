@@ -143,6 +143,10 @@ def _pick_tile(M: int, N: int, row_major_stream: bool = True, Kd: Optional[int] 
     widest column tile that covers N in one workgroup row, so the big A operand (E, H, dZ) is
     streamed exactly once."""
     if allow_lds and _LDS_GEMM and _lds_tile_ok(M, N, Kd):
+        # 256 x 256 ping-pong tile where it tiles the output 128+ times (0.45-0.66x hipBLASLt at the
+        # 4096-wide tower, 1.15-1.3x the 128 x 128 tile: profiles/r6_gemm_bench_pingpong.log)
+        if M % 256 == 0 and N % 256 == 0 and (M // 256) * (N // 256) >= 128:
+            return KN.TILE_PP
         return KN.TILE_LDS
     if row_major_stream and M % 32 == 0:
         for t, w in ((3, 32), (4, 64), (2, 128), (5, 160), (7, 256), (6, 320)):
@@ -173,7 +177,7 @@ def _pick_splitk(M: int, N: int, Kd: int, tile: int, target_blocks: int = 512,
     256 CUs, but few enough slabs that the finalize pass stays a short, coalesced read."""
     bm, bn = KN.TILES[tile]
     tiles = (M // bm) * (N // bn)
-    ksteps = Kd // (64 if tile == KN.TILE_LDS else 32)
+    ksteps = Kd // (64 if tile in (KN.TILE_LDS, KN.TILE_PP) else 32)
     want = max(1, min(ksteps, max_split, target_blocks // max(1, tiles)))
     for s in range(want, 0, -1):
         if ksteps % s == 0:

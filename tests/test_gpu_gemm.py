@@ -32,7 +32,9 @@ def _ref(A, B):
                                               (8, 512, 256, 2048, 4), (8, 1024, 1024, 1024, 2),
                                               (9, 256, 256, 64, 1), (9, 512, 768, 320, 1), (9, 512, 512, 4096, 1),
                                               (9, 768, 256, 2048, 4), (9, 1024, 1024, 1024, 2),
-                                              (10, 512, 768, 320, 1), (10, 768, 256, 2048, 4), (10, 1024, 1024, 1024, 2)])
+                                              (10, 512, 768, 320, 1), (10, 768, 256, 2048, 4), (10, 1024, 1024, 1024, 2),
+                                              (11, 256, 256, 64, 1), (11, 512, 768, 320, 1), (11, 512, 512, 4096, 1),
+                                              (11, 768, 256, 2048, 4), (11, 1024, 1024, 1024, 2)])
 def test_lds_gemm_f32_matches_reference(tile, M, N, K, split):
     A, B = _ops(M, N, K, seed=M + N + K)
     out = torch.full((split, M, N), float("nan"), device=DEV)
@@ -52,7 +54,7 @@ def test_lds_gemm_f32_matches_reference(tile, M, N, K, split):
     assert torch.equal(out, o2)
 
 
-@pytest.mark.parametrize("tile", [8, 9, 10])
+@pytest.mark.parametrize("tile", [8, 9, 10, 11])
 @pytest.mark.parametrize("epi", ["fwd", "fwd_eval", "dgrad", "relu_f32"])
 def test_lds_gemm_epilogues_match_register_tile(tile, epi):
     M, N, K = 512, 256, 640
@@ -94,3 +96,32 @@ def test_lds_gemm_rejects_bad_shapes():
     ep.out = out.data_ptr()
     with pytest.raises(RuntimeError):
         KN.gemm_nt(KN.EPI_F32, KN.TILE_LDS, A, 96, B, 96, 256, 256, 96, 1, ep)   # K % 64 != 0
+
+
+@pytest.mark.parametrize("bn", [False, True])
+def test_wide_tower_step_matches_register_tiles(monkeypatch, bn):
+    """A per-layer (wide) tower trained with the LDS / ping-pong tiles equals the same model on the
+    register-fed tiles to fp32 reassociation (split-K counts differ), batch norm included."""
+    import hipfm.models.deepfm as D
+    from hipfm.data.synthetic import make_synth
+    from hipfm.models.deepfm import NativeDeepFM
+    from hipfm.models.reference import init_params
+    synth = make_synth("total:20000", seed=5)
+    F, K, layers, keep, B = synth.F, 8, [512, 512], [0.5, 0.5], 8192
+    params = init_params(synth.feature_size, F, K, layers, bn, seed=2)
+    data = [synth.batch(B, step=s, device=DEV, id_dtype=torch.int32) for s in range(2)]
+    outs = []
+    for lds in (True, False):
+        monkeypatch.setattr(D, "_LDS_GEMM", lds)
+        m = NativeDeepFM(synth.feature_size, F, K, layers, keep, batch_size=B, device=DEV, init=False,
+                         batch_norm=bn, learning_rate=1e-3, fused=False)
+        m.load_tf_params(params)
+        assert not m.fused                                # the per-layer path
+        for ids, vals, lab in data:
+            m.train_step(ids, vals, lab)
+        torch.cuda.synchronize()
+        m.check_errors()
+        outs.append((m.p.clone(), m.tv[:synth.feature_size].clone()))
+    (p8, v8), (p0, v0) = outs
+    assert (p8 - p0).abs().max().item() <= 1e-4 * p0.abs().max().item()
+    assert (v8 - v0).abs().max().item() <= 1e-4 * v0.abs().max().item()

@@ -15,7 +15,7 @@ import sys
 
 OURS = ("tower_kernel", "tower_light", "wgfin_kernel", "sfwg_kernel", "sfwg_x", "fs2_",  "dense_sweep", "fm_fwd", "wgrad_group", "finalize_kernel", "sf_tile", "sf_carry",
         "fs_sort", "fs_transpose", "dense_opt", "w8_quant", "sh_", "seg_", "onesweep", "lsd_",
-        "gemm_nt", "head_kernel", "rcclGenericKernel")
+        "gemm_nt", "gemm_lds", "gemm_pp", "Cijk", "head_kernel", "rcclGenericKernel")
 SIMDS = 1024
 HBM_BPS = 8e12       # MI355X HBM3E peak
 BF16_PEAK_TF = 2500.0  # dense bf16 MFMA peak (no sparsity)
