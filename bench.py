@@ -583,6 +583,22 @@ def data_bench(args):
         rows += r
     ingest = rows / (time.perf_counter() - t0)
     ld.close()
+    # 1b. host ingest of the GPU-decode wire: framing + CRC + raw Example bytes assembled into a
+    # ring of pinned slots (the streamed path's host side, nothing on the GPU)
+    ld = NativeLoader(files, F, B, threads=args.threads, raw=True)
+    slots = [(torch.empty(B * 2048, dtype=torch.uint8, pin_memory=True),
+              torch.empty(B + 1, dtype=torch.int32, pin_memory=True)) for _ in range(8)]
+    ld.start_ring_raw(slots)
+    rows_raw, bytes_raw, t0 = 0, 0, time.perf_counter()
+    while True:
+        r, slot, nb = ld.ring_take()
+        if r <= 0:
+            break
+        rows_raw += r
+        bytes_raw += nb
+        ld.ring_give(slot)
+    ingest_raw = rows_raw / (time.perf_counter() - t0)
+    ld.close()
     _progress()
     # 2. training through the Estimator (same code path as the CLI): the per-field vocabularies are
     # the data's (--field_sizes), so epoch 0 already sorts per field; streamed epochs go through
@@ -618,6 +634,8 @@ def data_bench(args):
     fill = {"take_s": round(pipe_s.fill_take_s, 4), "issue_s": round(pipe_s.fill_issue_s, 4)}   # (last epoch)
     if args.stream_only:                               # (profiling the streamed path alone)
         _emit(json.dumps({"metric": "streamed epochs samples/s (1 GPU)", "ingest_rows_per_s": round(ingest, 1),
+                          "ingest_raw_rows_per_s": round(ingest_raw, 1),
+                          "raw_bytes_per_row": round(bytes_raw / max(1, rows_raw), 1),
                           "streamed_epoch_samples_per_s": [round(n * B / t, 1) for n, t in per_epoch_s],
                           "epoch_s": [round(t, 4) for _, t in per_epoch_s], "wire_bytes_per_row": wire,
                           "fill_thread_last_epoch": fill,

@@ -23,6 +23,8 @@
 #include <unistd.h>
 #include <stdio.h>
 #include <string.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
 
 #include <atomic>
 #include <condition_variable>
@@ -441,6 +443,38 @@ struct Chunk {
   std::vector<int32_t> ids32;
   std::vector<float> vals;
   uint64_t vmask = 0;           // bit f: some row of the chunk has a field-f value other than 1.0
+  // raw mode (Loader::raw): each record's serialized Example, decoded later on the GPU
+  // (csrc/kernels/decode.hip).  Records of a mapped file stay in the mapping (rptr); records read
+  // from a stream (FIFO) are copied into `raw` (rptr null, rcopy = offset); `maps` keeps the
+  // mappings alive until the chunk has been assembled
+  std::vector<uint8_t> raw;
+  std::vector<const uint8_t*> rptr;
+  std::vector<uint32_t> rcopy, rlen;
+  std::vector<std::shared_ptr<struct Mapping>> maps;
+  size_t rbytes = 0;            // sum of rlen
+  void add_mapped(const uint8_t* p, uint32_t len) {
+    rptr.push_back(p);
+    rcopy.push_back(0);
+    rlen.push_back(len);
+    rbytes += len;
+  }
+  void add_copied(const uint8_t* p, uint32_t len) {
+    rptr.push_back(nullptr);
+    rcopy.push_back((uint32_t)raw.size());
+    rlen.push_back(len);
+    raw.insert(raw.end(), p, p + len);
+    rbytes += len;
+  }
+  const uint8_t* rec(int i) const { return rptr[i] ? rptr[i] : raw.data() + rcopy[i]; }
+};
+
+// A read-only private mapping of a whole regular file (pre-faulted, sequential read-ahead).
+struct Mapping {
+  const uint8_t* p = nullptr;
+  size_t n = 0;
+  ~Mapping() {
+    if (p) munmap((void*)p, n);
+  }
 };
 
 struct WorkerQueue {
@@ -529,6 +563,8 @@ struct Loader {
   int format = 0, F = 0, B = 0, drop_remainder = 1, verify = 1;
   int shard_n = 1, shard_i = 0;   // record-level shard (1 = off)
   int64_t id_limit = 0;            // > 0: every id must lie in [0, id_limit) (feature_size V)
+  int raw = 0;                     // workers only frame + CRC-check TFRecords and keep the Example
+                                   // bytes; batches ship raw records + offsets (next_raw)
   int narrow32 = 0;                // workers narrow ids to int32 while decoding (the device id type):
                                    // batch assembly is then a plain copy (it was the ingest bound)
   int depth = 4;
@@ -553,6 +589,9 @@ struct Loader {
     bool compact = false;
     std::vector<float*> lab, vals;
     std::vector<int32_t*> ids;
+    std::vector<uint8_t*> rawb;  // raw mode: record bytes + offsets per slot, `cap` bytes each
+    std::vector<uint32_t*> offs;
+    size_t cap = 0;
     std::vector<int> state;      // 0 free, 1 assembling, 2 assembled
     std::vector<int> rows;
     std::vector<uint64_t> mask;
@@ -576,7 +615,8 @@ struct Loader {
         R.fill = (s + 1) % R.n;
       }
       uint64_t mk = 0;
-      const int r = next(R.lab[s], nullptr, R.vals[s], R.ids[s], R.compact ? &mk : nullptr);
+      const int r = raw ? next_raw(R.rawb[s], R.cap, R.offs[s], &mk)
+                        : next(R.lab[s], nullptr, R.vals[s], R.ids[s], R.compact ? &mk : nullptr);
       {
         std::lock_guard<std::mutex> lk(R.m);
         R.rows[s] = r;
@@ -589,8 +629,23 @@ struct Loader {
     }
   }
 
+  // raw mode: slot s receives up to `cap` record bytes in rawb[s] and B + 1 offsets in offs[s];
+  // ring_take's mask then returns the slot's byte count
+  int start_ring_raw(int n, uint8_t** rawb, size_t cap, uint32_t** offs) {
+    if (!raw || ring.n || n < 2) return -1;
+    ring.rawb.assign(rawb, rawb + n);
+    ring.offs.assign(offs, offs + n);
+    ring.cap = cap;
+    ring.n = n;
+    ring.state.assign(n, 0);
+    ring.rows.assign(n, 0);
+    ring.mask.assign(n, 0);
+    ring.th = std::thread(&Loader::assemble_loop, this);
+    return 0;
+  }
+
   int start_ring(int n, float** lab, int32_t** ids, float** vals, int compact) {
-    if (ring.n || n < 2 || (compact && F > 64)) return -1;
+    if (raw || ring.n || n < 2 || (compact && F > 64)) return -1;
     ring.n = n;
     ring.compact = compact != 0;
     ring.lab.assign(lab, lab + n);
@@ -624,6 +679,165 @@ struct Loader {
     ring.cv_free.notify_all();
   }
 
+  // Chunk recycling: a chunk's buffers (160-512 KB each) come from a free list instead of a fresh
+  // allocation per 1024 records -- glibc serves such sizes with mmap, so every chunk paid ~128 page
+  // faults on first touch and a munmap at free (~125 ns per record: a lone worker managed ~5 M
+  // records/s whatever the record format).
+  std::mutex pool_m;
+  std::vector<std::unique_ptr<Chunk>> pool_free;
+
+  std::unique_ptr<Chunk> get_chunk() {
+    std::unique_ptr<Chunk> c;
+    {
+      std::lock_guard<std::mutex> lk(pool_m);
+      if (!pool_free.empty()) {
+        c = std::move(pool_free.back());
+        pool_free.pop_back();
+      }
+    }
+    if (!c) {
+      c = std::make_unique<Chunk>();
+      if (raw) {
+        c->rptr.reserve(chunk);
+        c->rcopy.reserve(chunk);
+        c->rlen.reserve(chunk);
+      } else {
+        c->label.resize(chunk);
+        if (narrow32) c->ids32.resize((size_t)chunk * F);
+        else c->ids.resize((size_t)chunk * F);
+        c->vals.resize((size_t)chunk * F);
+      }
+    }
+    c->n = 0;
+    c->vmask = 0;
+    if (raw) {
+      c->raw.clear();                    // (vectors keep their capacity)
+      c->rptr.clear();
+      c->rcopy.clear();
+      c->rlen.clear();
+      c->maps.clear();
+      c->rbytes = 0;
+    }
+    return c;
+  }
+
+  void put_chunk(std::unique_ptr<Chunk> c) {
+    if (!c) return;
+    c->maps.clear();                     // (the last chunk of a file unmaps it)
+    std::lock_guard<std::mutex> lk(pool_m);
+    if (pool_free.size() < 512) pool_free.push_back(std::move(c));
+  }
+
+  struct Recycle {                       // chunks an assembly finished with go back to the pool
+    Loader* L;
+    std::vector<std::unique_ptr<Chunk>> v;
+    ~Recycle() {
+      for (auto& c : v) L->put_chunk(std::move(c));
+    }
+  };
+
+  // raw mode, one regular file: mapped once; framing + CRC in place, each chunk records where its
+  // payloads lie in the mapping -- the only copy of a record's bytes on the host is the assembly
+  // into the caller's pinned slot (read(2) into a block, a copy into the chunk and the assembly
+  // moved every byte three times)
+  template <class Push, class Fresh, class Fail>
+  int worker_raw_mapped(const std::string& path, std::unique_ptr<Chunk>& c, long long& rec, Push& push,
+                        Fresh& fresh, Fail& fail) {
+    const int fd = ::open(path.c_str(), O_RDONLY);
+    if (fd < 0) return -1;                              // (the caller reports it)
+    struct stat st;
+    if (fstat(fd, &st) != 0 || !S_ISREG(st.st_mode)) {
+      ::close(fd);
+      return 0;                                         // not a regular file: stream it instead
+    }
+    auto m = std::make_shared<Mapping>();
+    m->n = (size_t)st.st_size;
+    if (m->n > 0) {
+      void* a = mmap(nullptr, m->n, PROT_READ, MAP_PRIVATE | MAP_POPULATE, fd, 0);
+      if (a == MAP_FAILED) {
+        ::close(fd);
+        return 0;
+      }
+      madvise(a, m->n, MADV_SEQUENTIAL);
+      m->p = (const uint8_t*)a;
+    }
+    ::close(fd);
+    const uint8_t* p = m->p;
+    size_t at = 0;
+    while (at < m->n && !stop.load()) {
+      if (m->n - at < 12) {
+        fail("truncated TFRecord header in " + path);
+        return -2;
+      }
+      uint64_t len;
+      memcpy(&len, p + at, 8);
+      uint32_t hcrc;
+      memcpy(&hcrc, p + at + 8, 4);
+      if (verify && hcrc != masked(hfmio_crc32c(p + at, 8))) {
+        fail("TFRecord length CRC mismatch in " + path);
+        return -2;
+      }
+      if (len > (1ull << 31) || m->n - at - 12 < len + 4) {
+        fail("truncated TFRecord payload in " + path);
+        return -2;
+      }
+      const uint8_t* rp = p + at + 12;
+      if (verify) {
+        uint32_t dcrc;
+        memcpy(&dcrc, rp + len, 4);
+        if (dcrc != masked(hfmio_crc32c(rp, len))) {
+          fail("TFRecord data CRC mismatch in " + path);
+          return -2;
+        }
+      }
+      at += 12 + len + 4;
+      if (shard_n > 1 && (rec++ % shard_n) != shard_i) continue;
+      if (c->maps.empty() || c->maps.back() != m) c->maps.push_back(m);   // (a chunk may span files)
+      c->add_mapped(rp, (uint32_t)len);
+      if (++c->n == chunk) {
+        if (!push(std::move(c))) return -2;
+        c = fresh();
+      }
+    }
+    return 1;
+  }
+
+  // raw mode, one file: framing + CRC only, the Example bytes appended to the chunk
+  template <class Push, class Fresh, class Fail>
+  bool worker_raw_file(const std::string& path, std::unique_ptr<Chunk>& c, long long& rec, Push& push,
+                       Fresh& fresh, Fail& fail) {
+    const int mr = worker_raw_mapped(path, c, rec, push, fresh, fail);
+    if (mr == 1) return true;
+    if (mr == -2) return false;
+    BlockReader br(path);
+    if (!br.ok()) {
+      fail("cannot open " + path);
+      return false;
+    }
+    size_t pending = 0;
+    while (!stop.load()) {
+      const uint8_t* rp;
+      uint64_t rlen;
+      const int rc = next_tfrecord_view(br, rp, rlen, verify, pending);
+      if (rc == 0) break;
+      if (rc < 0) {
+        fail(g_err);
+        return false;
+      }
+      if (shard_n > 1 && (rec++ % shard_n) != shard_i) continue;
+      if (c->raw.size() + rlen > 0xFFFFFFFFull) {
+        fail("raw chunk exceeds 4 GB in " + path);
+        return false;
+      }
+      c->add_copied(rp, (uint32_t)rlen);
+      if (++c->n == chunk) {
+        if (!push(std::move(c))) return false;
+        c = fresh();
+      }
+    }
+    return true;
+  }
+
   void worker(int w, int W) {
     WorkerQueue& Q = *queues[w];
     auto push = [&](std::unique_ptr<Chunk> c) {
@@ -641,19 +855,16 @@ struct Loader {
       Q.done = true;
       Q.cv_get.notify_all();
     };
-    auto fresh = [&] {
-      auto c = std::make_unique<Chunk>();
-      c->label.resize(chunk);
-      if (narrow32) c->ids32.resize((size_t)chunk * F);
-      else c->ids.resize((size_t)chunk * F);
-      c->vals.resize((size_t)chunk * F);
-      return c;
-    };
+    auto fresh = [&] { return get_chunk(); };
     std::vector<int64_t> idrow((size_t)F);   // one record's ids before narrowing
     std::unique_ptr<Chunk> c = fresh();
     std::string line;
     long long rec = 0;   // record index in this worker's stream (record sharding uses W == 1)
     for (size_t fi = w; fi < paths.size() && !stop.load(); fi += W) {
+      if (raw) {
+        if (!worker_raw_file(paths[fi], c, rec, push, fresh, fail)) return;
+        continue;
+      }
       std::unique_ptr<ByteReader> lr;       // libsvm lines
       std::unique_ptr<BlockReader> br;      // TFRecords, parsed in place
       if (format == 0) br = std::make_unique<BlockReader>(paths[fi]);
@@ -776,20 +987,78 @@ struct Loader {
   // 1.0 in the batch's chunks (mask returned in *vmask, bit f = field f shipped; columns in field
   // order, ``vals`` then holds [rows, popcount(mask)]).  Requires F <= 64.  Lossless: the omitted
   // columns are exactly 1.0f in every row of the batch.
+  // Raw mode batch: up to B records' Example bytes back to back into `dst` (at most `cap` bytes)
+  // and their B + 1 start offsets into `offs` (offs[rows] = total bytes, also in *bytes).  Returns
+  // rows as next() does.  The copy pool assembles the pieces in parallel.
+  int next_raw(uint8_t* dst, size_t cap, uint32_t* offs, uint64_t* bytes) {
+    struct Piece {
+      const Chunk* c;
+      int src, dst, k;
+      size_t at;
+    };
+    std::vector<Piece> pieces;
+    Recycle done{this, {}};
+    int got = 0;
+    size_t total = 0;
+    while (got < B) {
+      if (!cur || cur_off >= cur->n) {
+        if (cur) done.v.push_back(std::move(cur));
+        cur = take();
+        cur_off = 0;
+        if (!cur) {
+          if (stop.load() && err.empty()) err = "loader stopped";
+          if (!err.empty()) return -1;
+          break;
+        }
+      }
+      const int k = std::min(B - got, cur->n - cur_off);
+      pieces.push_back({cur.get(), cur_off, got, k, total});
+      for (int i = 0; i < k; ++i) total += cur->rlen[cur_off + i];
+      got += k;
+      cur_off += k;
+    }
+    if (got < B && drop_remainder) return 0;
+    if (total > cap || total > 0xFFFFFFFFull) {
+      err = "raw batch of " + std::to_string(total) + " bytes exceeds the " + std::to_string(cap) +
+            "-byte staging buffer";
+      return -1;
+    }
+    auto copy = [&](int pi) {
+      const Piece& p = pieces[pi];
+      size_t at = p.at;
+      for (int i = 0; i < p.k; ++i) {
+        const uint32_t n = p.c->rlen[p.src + i];
+        memcpy(dst + at, p.c->rec(p.src + i), n);
+        offs[p.dst + i] = (uint32_t)at;
+        at += n;
+      }
+    };
+    if (pool && pieces.size() > 1) {
+      pool->run((int)pieces.size(), copy);
+    } else {
+      for (int i = 0; i < (int)pieces.size(); ++i) copy(i);
+    }
+    offs[got] = (uint32_t)total;
+    *bytes = total;
+    return got;
+  }
+
   int next(float* lab, int64_t* ids, float* vals, int32_t* ids32 = nullptr, uint64_t* vmask = nullptr) {
     struct Piece {
       const Chunk* c;
       int src, dst, k;
     };
     std::vector<Piece> pieces;
-    std::vector<std::unique_ptr<Chunk>> done_chunks;
+    Recycle done{this, {}};
     int got = 0;
     while (got < B) {
       if (!cur || cur_off >= cur->n) {
-        if (cur) done_chunks.push_back(std::move(cur));
+        if (cur) done.v.push_back(std::move(cur));
         cur = take();
         cur_off = 0;
         if (!cur) {
+          // (a shutdown is not the end of the data: never publish a batch it cut short)
+          if (stop.load() && err.empty()) err = "loader stopped";
           if (!err.empty()) return -1;
           break;
         }
@@ -898,6 +1167,48 @@ HFMIO_API void* hfmio_loader_create(const char** paths, int npaths, int format, 
   for (int w = 0; w < W; ++w) L->queues.emplace_back(new WorkerQueue());
   for (int w = 0; w < W; ++w) L->threads.emplace_back(&Loader::worker, L, w, W);
   return L;
+}
+
+// Raw-record loader (TFRecord only): workers frame + CRC-check, batches carry the serialized
+// Examples + offsets for the GPU decoder (csrc/kernels/decode.hip); ids are checked there.
+HFMIO_API void* hfmio_loader_create_raw(const char** paths, int npaths, int F, int batch, int drop_remainder,
+                                        int num_threads, int shard_n, int shard_i, int verify_crc,
+                                        int queue_depth) {
+  auto* L = new Loader();
+  L->raw = 1;
+  for (int i = 0; i < npaths; ++i) L->paths.emplace_back(paths[i]);
+  L->format = 0;
+  L->F = F;
+  L->B = batch;
+  L->drop_remainder = drop_remainder;
+  L->verify = verify_crc;
+  L->shard_n = shard_n < 1 ? 1 : shard_n;
+  L->shard_i = shard_i;
+  L->depth = queue_depth < 1 ? 4 : queue_depth;
+  int W = num_threads < 1 ? 1 : num_threads;
+  if (L->shard_n > 1) W = 1;
+  if (W > npaths) W = npaths < 1 ? 1 : npaths;
+  for (int w = 0; w < W; ++w) L->queues.emplace_back(new WorkerQueue());
+  for (int w = 0; w < W; ++w) L->threads.emplace_back(&Loader::worker, L, w, W);
+  return L;
+}
+
+HFMIO_API int hfmio_loader_next_raw(void* h, uint8_t* dst, size_t cap, uint32_t* offs, uint64_t* bytes) {
+  auto* L = (Loader*)h;
+  if (!L->raw) {
+    set_err("next_raw on a decoding loader");
+    return -1;
+  }
+  int r = L->next_raw(dst, cap, offs, bytes);
+  if (r < 0) set_err(L->err);
+  return r;
+}
+
+HFMIO_API int hfmio_loader_start_ring_raw(void* h, int n, uint8_t** rawb, size_t cap, uint32_t** offs) {
+  auto* L = (Loader*)h;
+  int r = L->start_ring_raw(n, rawb, cap, offs);
+  if (r < 0) set_err("raw assembly ring: a raw loader, >= 2 slots, once per loader");
+  return r;
 }
 
 HFMIO_API int hfmio_loader_next(void* h, float* labels, int64_t* ids, float* vals) {

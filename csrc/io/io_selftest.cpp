@@ -28,6 +28,9 @@ void hfmio_loader_set_copy_threads(void* h, int n);
 int hfmio_loader_start_ring(void* h, int n, float** labels, int32_t** ids, float** vals, int compact);
 int hfmio_loader_ring_take(void* h, int* slot, uint64_t* mask);
 void hfmio_loader_ring_give(void* h, int slot);
+void* hfmio_loader_create_raw(const char** paths, int npaths, int F, int batch, int drop_remainder,
+                              int num_threads, int shard_n, int shard_i, int verify_crc, int queue_depth);
+int hfmio_loader_start_ring_raw(void* h, int n, uint8_t** rawb, size_t cap, uint32_t** offs);
 int hfmio_write_examples(const char* path, const float* labels, const int64_t* ids,
                          const float* vals, long n, int F, int append);
 long hfmio_libsvm_to_tfrecord(const char* src, const char* dst, int F);
@@ -126,6 +129,55 @@ static Sum read_ring(const std::vector<std::string>& files, int threads, int cop
   return s;
 }
 
+// the raw-record ring (mapped files, framing + CRC by the workers, assembly by the copy pool):
+// every record's Example bytes once, in the decoding loader's order (host-decoded here), then
+// destroyed mid-stream with every slot held (TSan: hand-offs, chunk recycling, unmapping)
+static Sum read_ring_raw(const std::vector<std::string>& files, int threads, int copy_threads) {
+  std::vector<const char*> p;
+  for (auto& f : files) p.push_back(f.c_str());
+  const int n = 3, Bt = 64;
+  const size_t cap = (size_t)Bt * 2048;
+  Sum s;
+  for (int pass = 0; pass < 2; ++pass) {
+    void* h = hfmio_loader_create_raw(p.data(), (int)p.size(), F, Bt, 0, threads, 1, 0, 1, 8);
+    CHECK(h != nullptr);
+    hfmio_loader_set_copy_threads(h, copy_threads);
+    std::vector<std::vector<uint8_t>> raw(n, std::vector<uint8_t>(cap));
+    std::vector<std::vector<uint32_t>> offs(n, std::vector<uint32_t>(Bt + 1));
+    uint8_t* rp[n];
+    uint32_t* op[n];
+    for (int i = 0; i < n; ++i) rp[i] = raw[i].data(), op[i] = offs[i].data();
+    CHECK(hfmio_loader_start_ring_raw(h, n, rp, cap, op) == 0);
+    std::vector<float> lab(1), vals(F);
+    std::vector<int64_t> ids(F);
+    for (int taken = 0;; ++taken) {
+      int slot = -1;
+      uint64_t bytes = 0;
+      const int r = hfmio_loader_ring_take(h, &slot, &bytes);
+      CHECK(r >= 0);
+      if (r == 0 || (pass == 1 && taken == n - 1)) break;
+      CHECK(slot >= 0 && slot < n && offs[slot][r] == bytes && bytes <= cap);
+      if (pass == 0) {
+        for (int i = 0; i < r; ++i) {
+          const uint32_t o0 = offs[slot][i], o1 = offs[slot][i + 1];
+          CHECK(o0 < o1 && o1 <= bytes);
+          CHECK(hfmio_decode_example(raw[slot].data() + o0, o1 - o0, F, lab.data(), ids.data(), vals.data()) == 0);
+          s.lab += lab[0];
+          for (int f = 0; f < F; ++f) {
+            s.ids += (uint64_t)ids[f];
+            s.val += vals[f];
+          }
+          s.order = s.order * 1000003ull + (uint64_t)ids[0];
+          ++s.rows;
+        }
+      }
+      hfmio_loader_ring_give(h, slot);
+    }
+    hfmio_loader_destroy(h);
+  }
+  return s;
+}
+
 int main(int argc, char** argv) {
   const std::string dir = argc > 1 ? argv[1] : "/tmp";
   const long n_per = 1500;
@@ -161,6 +213,9 @@ int main(int argc, char** argv) {
   // the assembly ring reads the same stream, in the same order, through compact values
   const Sum rg = read_ring(files, 4, 3);
   CHECK(rg.rows == a.rows && rg.ids == a.ids && rg.order == a.order && rg.val == a.val && rg.lab == a.lab);
+  // the raw-record ring (GPU-decode wire) ships the same records in the same order
+  const Sum rr = read_ring_raw(files, 4, 3);
+  CHECK(rr.rows == a.rows && rr.ids == a.ids && rr.order == a.order && rr.val == a.val && rr.lab == a.lab);
   // 2) record-level sharding partitions the data
   const Sum s0 = read_all(files, 3, 2, 0), s1 = read_all(files, 3, 2, 1);
   CHECK(s0.rows + s1.rows == want.rows && s0.ids + s1.ids == want.ids);

@@ -52,6 +52,12 @@ def lib():
             L.hfmio_loader_ring_give.argtypes = [vp, ci]
             L.hfmio_loader_ring_give.restype = None
             L.hfmio_loader_destroy.argtypes = [vp]
+            L.hfmio_loader_create_raw.argtypes = [C.POINTER(C.c_char_p), ci, ci, ci, ci, ci, ci, ci, ci, ci]
+            L.hfmio_loader_create_raw.restype = vp
+            L.hfmio_loader_next_raw.argtypes = [vp, vp, C.c_size_t, vp, vp]
+            L.hfmio_loader_next_raw.restype = ci
+            L.hfmio_loader_start_ring_raw.argtypes = [vp, ci, vp, C.c_size_t, vp]
+            L.hfmio_loader_start_ring_raw.restype = ci
             L.hfmio_loader_set_copy_threads.argtypes = [vp, ci]
             L.hfmio_loader_set_copy_threads.restype = None
             L.hfmio_write_examples.argtypes = [C.c_char_p, vp, vp, vp, cl, ci, ci]
@@ -157,14 +163,24 @@ class NativeLoader:
                  fmt: int = FMT_TFRECORD, drop_remainder: bool = True, threads: int = 4,
                  record_shard: Tuple[int, int] = (1, 0), verify_crc: bool = True,
                  queue_depth: int = 4, id_limit: int = 0, copy_threads: Optional[int] = None,
-                 ids32: bool = False):
+                 ids32: bool = False, raw: bool = False):
         self.paths = [str(p) for p in paths]
         self.F, self.B = int(field_size), int(batch_size)
+        # raw (TFRecord only): the workers frame records and check CRCs, batches carry the
+        # serialized Examples for the GPU decoder (ops.kernels.decode_examples)
+        self.raw = bool(raw)
         arr = (C.c_char_p * max(1, len(self.paths)))(*[p.encode() for p in self.paths])
-        self._h = lib().hfmio_loader_create(arr, len(self.paths), fmt, self.F, self.B,
-                                            1 if drop_remainder else 0, threads, record_shard[0],
-                                            record_shard[1], 1 if verify_crc else 0, queue_depth,
-                                            int(id_limit), 1 if ids32 else 0)
+        if self.raw:
+            if fmt != FMT_TFRECORD:
+                raise ValueError("raw records are TFRecord Examples")
+            self._h = lib().hfmio_loader_create_raw(arr, len(self.paths), self.F, self.B,
+                                                    1 if drop_remainder else 0, threads, record_shard[0],
+                                                    record_shard[1], 1 if verify_crc else 0, queue_depth)
+        else:
+            self._h = lib().hfmio_loader_create(arr, len(self.paths), fmt, self.F, self.B,
+                                                1 if drop_remainder else 0, threads, record_shard[0],
+                                                record_shard[1], 1 if verify_crc else 0, queue_depth,
+                                                int(id_limit), 1 if ids32 else 0)
         # batches are assembled from the workers' chunks by a copy pool (the consumer alone
         # capped ingest near 49 M rows/s at B = 16384; on a 16-core share of an EPYC 9575F: 16
         # decode threads + 1 / 4 / 8 copy threads = 45 / 70 / 97 M rows/s with int64 chunks
@@ -215,6 +231,31 @@ class NativeLoader:
         self._ring_keep = bufs
         if lib().hfmio_loader_start_ring(self._h, n, arr([b[0] for b in bufs]), arr([b[1] for b in bufs]),
                                          arr([b[2] for b in bufs]), 1 if compact else 0) != 0:
+            raise IOError(_err())
+
+    def next_raw_into(self, raw, offs) -> Tuple[int, int]:
+        """Raw loader: the next batch's record bytes into ``raw`` (uint8, its size is the capacity)
+        and B + 1 int32 start offsets into ``offs``; returns (rows, bytes), rows 0 at end."""
+        if self._done:
+            return 0, 0
+        nb = C.c_uint64(0)
+        cap = raw.numel() if hasattr(raw, "numel") else raw.size
+        r = lib().hfmio_loader_next_raw(self._h, _addr(raw), cap, _addr(offs), C.addressof(nb))
+        if r < 0:
+            raise IOError(_err())
+        if r == 0:
+            self._done = True
+        return r, int(nb.value)
+
+    def start_ring_raw(self, bufs) -> None:
+        """Raw loader: assemble ahead into ``bufs`` = [(raw uint8 [cap], offs int32 [B + 1]), ...]
+        (equal capacities) on the C++ assembler thread; ``ring_take`` then returns (rows, slot,
+        bytes)."""
+        n = len(bufs)
+        cap = min(int(r.numel()) for r, _ in bufs)
+        self._ring_keep = bufs
+        if lib().hfmio_loader_start_ring_raw(self._h, n, (C.c_void_p * n)(*[_addr(r) for r, _ in bufs]), cap,
+                                             (C.c_void_p * n)(*[_addr(o) for _, o in bufs])) != 0:
             raise IOError(_err())
 
     def ring_take(self) -> Tuple[int, int, int]:

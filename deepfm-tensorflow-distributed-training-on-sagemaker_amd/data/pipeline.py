@@ -188,8 +188,9 @@ class _DeviceRing:
         self.G = max(1, nslots // 2)
         self.next = 0             # the next slot a fill thread writes (continues across epochs)
 
-    def fits(self, B: int, F: int, id_dtype, nslots: int) -> bool:
-        return (self.B, self.F, self.id_dtype, self.nslots) == (B, F, id_dtype, nslots)
+    def fits(self, B: int, F: int, id_dtype, nslots: int, compact: Optional[bool] = None) -> bool:
+        same = (self.B, self.F, self.id_dtype, self.nslots) == (B, F, id_dtype, nslots)
+        return same and (compact is None or bool(compact) == self.compact)
 
     def wire_bytes(self, mask: int) -> int:
         """Bytes one full batch copies host-to-device (compact: with popcount(mask) columns)."""
@@ -269,7 +270,7 @@ class _DeviceFeeder:
     -- and the consumer receives ``RingBatch`` views: no per-batch allocation, copy or Python work
     on the training thread."""
 
-    def __init__(self, loader, F: int, B: int, device, id_dtype, depth: int = 4, ring=None):
+    def __init__(self, loader, F: int, B: int, device, id_dtype, depth: int = 4, ring=None, id_limit: int = 0):
         self.loader, self.F, self.B, self.device, self.id_dtype = loader, F, B, device, id_dtype
         self.copy = torch.cuda.Stream(device)
         # ring mode: consecutive batches alternate over copy streams (each its own DMA queue; one
@@ -278,6 +279,31 @@ class _DeviceFeeder:
         self.dev_ring = ring
         pin = dict(pin_memory=True)
         self.compact = ring is not None and ring.compact
+        # GPU decode (a raw loader: ring mode only): pinned slots of record bytes + offsets, one
+        # device staging pair per copy stream (a stream's next copy is ordered after its decode)
+        self.raw = bool(getattr(loader, "raw", False))
+        self.id_limit = int(id_limit)
+        if self.raw:
+            if ring is None or ring.compact:
+                raise ValueError("raw records need a plain-layout device ring")
+            cap = B * int(knob("HIPFM_RAW_ROW_BYTES"))
+            self.praw = [(torch.empty(cap, dtype=torch.uint8, **pin), torch.empty(B + 1, dtype=torch.int32, **pin))
+                         for _ in range(depth)]
+            self.draw = [(torch.empty(cap, dtype=torch.uint8, device=device),
+                          torch.empty(B + 1, dtype=torch.int32, device=device)) for _ in self.copies]
+            self.derr = torch.tensor([0, 0x7FFFFFFF], dtype=torch.int32, device=device)
+            self.ring = [None] * depth
+            loader.start_ring_raw(self.praw)
+            self.asm = True
+            self.done = [None] * depth
+            self.h2d_s = self.h2d_bytes = 0
+            self.fill_take_s = self.fill_issue_s = 0.0
+            import queue
+            self._free, self._full = queue.Queue(), queue.Queue()
+            self._stop = False
+            self._th = None
+            self._batches = 0
+            return
         if ring is not None:
             self.pflat = [torch.empty(ring.lay["host"], dtype=torch.uint8, **pin) for _ in range(depth)]
             self.ring = []
@@ -352,6 +378,69 @@ class _DeviceFeeder:
         self.h2d_bytes += R.wire_bytes(mask or 0)
         return ev, s, (ev_copy or ev)
 
+    def _issue_raw(self, R, k: int, slot: int, nbytes: int):
+        """Raw mode ``_issue``: the batch's record bytes + offsets to the device on the next copy
+        stream, decoded there into ring slot k % nslots (csrc/kernels/decode.hip)."""
+        s = k % R.nslots
+        wait = R.acquire(s, lambda: self._stop)
+        if wait is _DeviceRing.STOPPED:
+            return None, s, None
+        if self._stop:
+            R.giveback(s, wait)
+            return None, s, None
+        i = (k + 1) % len(self.copies)
+        cs = self.copies[i]
+        draw, doffs = self.draw[i]
+        praw, poffs = self.praw[slot]
+        from ..ops import kernels as K
+        with CAPTURE_LOCK, torch.cuda.stream(cs):     # (never inside a graph capture)
+            if wait is not None:
+                cs.wait_event(wait)
+            draw[:nbytes].copy_(praw[:nbytes], non_blocking=True)
+            doffs.copy_(poffs, non_blocking=True)
+            ev_copy = torch.cuda.Event()
+            ev_copy.record(cs)
+            ids, vals, lab = R.views[s]
+            K.decode_examples(draw, doffs, self.B, self.F, self.id_limit, ids, vals, lab, self.derr)
+            ev = torch.cuda.Event()
+            ev.record(cs)
+        self.h2d_bytes += nbytes + 4 * (self.B + 1)
+        return ev, s, ev_copy
+
+    def _decode_partial(self, slot: int, r: int, nbytes: int, k: int):
+        """Raw mode, a final partial batch: decoded into fresh device tensors (the plain path's
+        per-batch tensors, marked for the compute stream by the consumer)."""
+        i = (k + 1) % len(self.copies)
+        cs = self.copies[i]
+        draw, doffs = self.draw[i]
+        praw, poffs = self.praw[slot]
+        from ..ops import kernels as K
+        with CAPTURE_LOCK, torch.cuda.stream(cs):
+            draw[:nbytes].copy_(praw[:nbytes], non_blocking=True)
+            doffs[:r + 1].copy_(poffs[:r + 1], non_blocking=True)
+            t = (torch.empty(r, self.F, dtype=self.id_dtype, device=self.device),
+                 torch.empty(r, self.F, dtype=torch.float32, device=self.device),
+                 torch.empty(r, dtype=torch.float32, device=self.device))
+            K.decode_examples(draw, doffs, r, self.F, self.id_limit, t[0], t[1], t[2], self.derr)
+            ev = torch.cuda.Event()
+            ev.record(cs)
+        self.h2d_bytes += nbytes + 4 * (r + 1)
+        return t, ev
+
+    def check_decode(self):
+        """Raw mode: raise on records the GPU decoder flagged (one host sync: end of the epoch)."""
+        if not self.raw:
+            return
+        e, first = (int(x) for x in self.derr.tolist())
+        if e:
+            what = []
+            if e & 1:
+                what.append("a record does not match the fixed Example schema (label, ids[F], values[F])")
+            if e & 2:
+                what.append("a feature id lies outside [0, feature_size) or int32")
+            raise IOError("GPU Example decode: " + "; ".join(what) +
+                          f" (first bad record: index {first} of its batch; its row was zeroed)")
+
     def _fill_asm(self, R, k: int):
         """Ring mode over the loader's assembler thread: take assembled pinned slots in order,
         issue their copies, hand each pinned slot back once its copy finished."""
@@ -381,12 +470,20 @@ class _DeviceFeeder:
             if r == self.B:
                 k += 1
                 R.next = k
-                ev, s, ev_copy = self._issue(R, k - 1, slot, mask if self.compact else None)
+                if self.raw:
+                    ev, s, ev_copy = self._issue_raw(R, k - 1, slot, mask)   # (mask: the byte count)
+                else:
+                    ev, s, ev_copy = self._issue(R, k - 1, slot, mask if self.compact else None)
                 self.fill_issue_s += time.perf_counter() - t1
                 if ev is None:
                     return
                 inflight.append((slot, ev_copy))
                 self._full.put((("ring", s), r, ev))
+                continue
+            if r > 0 and self.raw:               # final partial batch: fresh decoded tensors
+                t, ev = self._decode_partial(slot, r, mask, k)
+                inflight.append((slot, ev))
+                self._full.put((("dev", t), r, ev))
                 continue
             if r > 0 and self.compact:           # final partial batch: the plain path
                 from .native_io import expand_values
@@ -446,7 +543,7 @@ class _DeviceFeeder:
                 left = []
                 while not self._full.empty():
                     slot, _, _ = self._full.get_nowait()
-                    if isinstance(slot, tuple):
+                    if isinstance(slot, tuple) and slot[0] == "ring":
                         left.append(slot[1])
                 if left:
                     self.dev_ring.release(left, torch.cuda.current_stream(self.device))
@@ -462,11 +559,18 @@ class _DeviceFeeder:
                 slot, r, x = self._full.get()
                 if isinstance(x, BaseException):
                     raise x
+                if isinstance(slot, tuple) and slot[0] == "dev":   # decoded partial batch
+                    compute.wait_event(x)
+                    for t in slot[1]:
+                        t.record_stream(compute)
+                    yield slot[1]
+                    continue
                 if isinstance(slot, tuple):          # a ring slot, copied by the fill thread
                     compute.wait_event(x)
                     yield RingBatch(self.dev_ring.views[slot[1]], self.dev_ring, slot[1])
                     continue
                 if r == 0:
+                    self.check_decode()
                     return
                 lab, ids, vals = self.ring[slot]
                 t0 = time.perf_counter()
@@ -626,11 +730,21 @@ class InputPipeline:
             # streamed epoch whose consumer releases ring slots (Estimator.train): batches land in
             # the persistent device ring, two runs deep
             n = 2 * int(self.ring_steps)
-            if self._ring is None or not self._ring.fits(self.B, self.F, self.id_dtype, n):
-                self._ring = _DeviceRing(self.B, self.F, torch.device(self.device), self.id_dtype, n)
+            # GPU decode (HIPFM_GPU_DECODE): the loader ships raw Example bytes, the ring slots take
+            # the decoded plain layout
+            raw = (knob("HIPFM_GPU_DECODE") == "1" and self.fmt == FMT_TFRECORD and
+                   self.id_dtype == torch.int32)
+            compact = False if raw else None
+            if self._ring is None or not self._ring.fits(self.B, self.F, self.id_dtype, n, compact):
+                self._ring = _DeviceRing(self.B, self.F, torch.device(self.device), self.id_dtype, n,
+                                         compact=compact)
             ring = self._ring
+            if raw:
+                loader.close()
+                loader = NativeLoader(plan.files, self.F, self.B, self.fmt, self.drop_remainder,
+                                      self.threads, plan.record_shard, raw=True)
         src = (_DeviceFeeder(loader, self.F, self.B, torch.device(self.device), self.id_dtype, ring=ring,
-                             depth=8 if ring is not None else 4)
+                             depth=8 if ring is not None else 4, id_limit=self.id_limit)
                if on_gpu else None)
         k = 0
         try:

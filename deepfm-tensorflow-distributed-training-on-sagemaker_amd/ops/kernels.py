@@ -516,6 +516,15 @@ def struct_array_to_device(structs: Sequence[C.Structure], device) -> torch.Tens
     return host.to(device)
 
 
+# ------------------------------------------------------------------ Example decode (decode.hip)
+def decode_examples(raw, offs, rows: int, F: int, limit: int, ids, vals, labels, err):
+    """Serialized tf.train.Example records (``raw`` bytes, ``offs`` rows + 1 uint32 offsets) ->
+    ids int32 [rows, F], vals f32 [rows, F], labels f32 [rows] on the current stream; ``err``
+    int32 [2] = (error bits, smallest bad record index; initialise it to (0, INT32_MAX))."""
+    check(L().hfm_decode_examples(ptr(raw), ptr(offs), int(rows), int(F), int(limit), ptr(ids), ptr(vals),
+                                  ptr(labels), ptr(err), stream_handle()), "decode_examples")
+
+
 # ------------------------------------------------------------------ RCCL engine (comm.hip)
 def comm_unique_id() -> bytes:
     n = int(L().hfm_comm_id_bytes())

@@ -66,6 +66,9 @@ KNOBS: Dict[str, Knob] = {
                         "bf16 + fp32 w, 24 B; fused gather tower; the FM terms then read bf16-rounded v)"),
     "HIPFM_WIRE_COMPACT": Knob("1", "variant", "streamed input: a batch ships only the value columns of "
                                "fields not all 1.0 (expanded on the device; lossless) | 0: full [B, F] values"),
+    "HIPFM_GPU_DECODE": Knob("1", "variant", "streamed TFRecord epochs: the loader only frames + CRC-checks records "
+                             "and ships their Example bytes; the GPU decodes them into the ring slot "
+                             "(csrc/kernels/decode.hip) | 0: host decode + compact wire"),
     "HIPFM_ASM_RING": Knob("1", "variant", "streamed input: the loader's C++ assembler thread fills the "
                            "pinned buffers ahead of the copy-issuing thread (0: that thread assembles "
                            "each batch itself, next_into)"),
@@ -84,6 +87,8 @@ KNOBS: Dict[str, Knob] = {
                            "one GPU, 2 for the sharded routing)"),
     "HIPFM_FS_MAX_PB": Knob("4", "tuning", "tools/bench_sort.py: field sort partitions per field"),
     "HIPFM_H2D_STREAMS": Knob("2", "tuning", "streamed input: copy streams the device-ring batches alternate over"),
+    "HIPFM_RAW_ROW_BYTES": Knob("2048", "tuning", "GPU decode: staging bytes per row of a batch's raw records "
+                                "(a larger batch fails loudly; Criteo-shape Examples are ~330 B)"),
     "HIPFM_GRAPH_STEPS": Knob("32", "tuning", "most training steps per captured HIP graph (bench.py)"),
     # ---- harness
     "HIPFM_SAME_DEVICE": Knob("0", "harness", "multi-rank runs with every rank on device 0: gloo process "

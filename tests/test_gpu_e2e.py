@@ -129,8 +129,9 @@ def test_streamed_epochs_through_the_ring_train_like_the_cached_run(dataset, mon
     from hipfm.data.synthetic import make_synth
     sizes = ",".join(str(hi - lo) for lo, hi in make_synth("total:50000").field_ranges())
     out = []
-    for cache, compact in ((False, "1"), (False, "0"), (True, "1")):
+    for cache, compact, gdec in ((False, "1", "0"), (False, "0", "0"), (False, "1", "1"), (True, "1", "1")):
         monkeypatch.setenv("HIPFM_WIRE_COMPACT", compact)
+        monkeypatch.setenv("HIPFM_GPU_DECODE", gdec)
         cfg = RunConfig(feature_size=50000, field_size=39, embedding_size=8, batch_size=512,
                         deep_layers="64,32", dropout="0.9,0.9", device="cuda", log_steps=0,
                         watchdog_secs=0, graph_steps=8, num_threads=4, field_sizes=sizes)
@@ -146,12 +147,17 @@ def test_streamed_epochs_through_the_ring_train_like_the_cached_run(dataset, mon
             # own copy-in staging ring was never needed
             assert pipe.cached_batches == 0 and pipe._ring is not None
             assert getattr(est, "_ring", None) is None
-            assert pipe._ring.compact == (compact == "1")
-            # (the generator's values: 13 real-valued fields, 26 fields of 1.0)
             per_row = pipe.h2d_bytes / ((20000 // 512) * 512)
-            assert per_row == (39 * 4 + 4 + 13 * 4 if compact == "1" else 39 * 8 + 4), per_row
+            if gdec == "1":
+                # GPU decode: the raw Example bytes + an offset per row crossed the link, the ring
+                # slots hold the decoded plain layout
+                assert not pipe._ring.compact and per_row > 39 * 4, per_row
+            else:
+                assert pipe._ring.compact == (compact == "1")
+                # (the generator's values: 13 real-valued fields, 26 fields of 1.0)
+                assert per_row == (39 * 4 + 4 + 13 * 4 if compact == "1" else 39 * 8 + 4), per_row
         torch.cuda.synchronize()
         out.append((est.model.p.clone(), est.model.rec.clone(), est.global_step))
-    assert out[0][2] == out[1][2] == out[2][2] == 3 * (20000 // 512)
+    assert out[0][2] == out[1][2] == out[2][2] == out[3][2] == 3 * (20000 // 512)
     for a in out[1:]:
         assert torch.equal(out[0][0], a[0]) and torch.equal(out[0][1], a[1])

@@ -318,3 +318,56 @@ def test_loader_rejects_ids_outside_vocabulary(tmp_path, fmt):
     if fmt == "tfrecord":
         nio.write_examples(p, lab, ids, vals)
         assert len(list(nio.NativeLoader([p], F, 8, fmt=kind, id_limit=V))) == 5
+
+
+@pytest.mark.parametrize("threads,drop,ring", [(1, True, False), (3, False, False), (3, True, True)])
+def test_raw_loader_ships_the_records_of_the_decoding_loader(tmp_path, threads, drop, ring):
+    """Raw mode (hfm_io.cpp Loader::next_raw, the GPU-decode wire): each batch carries the records'
+    serialized Examples back to back + B + 1 offsets, in exactly the order the decoding loader
+    returns its rows; decoding the shipped bytes on the host gives the decoded batches bit for bit
+    (the GPU decoder, csrc/kernels/decode.hip, is checked against them in tests/test_gpu_decode.py)."""
+    F, B = 6, 128
+    files = []
+    for k in range(4):
+        lab, ids, vals = _rows(300 + 17 * k, F, 30 + k)
+        p = str(tmp_path / f"tr-{k}.tfrecords")
+        nio.write_examples(p, lab, ids, vals)
+        files.append(p)
+    ref = [(a.copy(), b.copy(), c.copy()) for a, b, c in
+           nio.NativeLoader(files, F, B, threads=threads, drop_remainder=drop)]
+    ld = nio.NativeLoader(files, F, B, threads=threads, drop_remainder=drop, raw=True)
+    bufs = [(torch.zeros(B * 1024, dtype=torch.uint8), torch.zeros(B + 1, dtype=torch.int32)) for _ in range(3)]
+    got = []
+    if ring:
+        ld.start_ring_raw(bufs)
+    while True:
+        if ring:
+            r, slot, nb = ld.ring_take()
+            raw, offs = bufs[slot]
+        else:
+            raw, offs = bufs[0]
+            r, nb = ld.next_raw_into(raw, offs)
+        if r == 0:
+            break
+        o = offs.numpy().astype(np.int64)
+        assert o[0] == 0 and o[r] == nb
+        rows = [nio.decode_example(raw.numpy()[o[i]:o[i + 1]].tobytes(), F) for i in range(r)]
+        got.append((np.array([x[0] for x in rows], np.float32), np.stack([x[1] for x in rows]),
+                    np.stack([x[2] for x in rows])))
+        if ring:
+            ld.ring_give(slot)
+    ld.close()
+    assert len(got) == len(ref)
+    for (l1, i1, v1), (l2, i2, v2) in zip(got, ref):
+        assert np.array_equal(l1, l2) and np.array_equal(i1, i2) and np.array_equal(v1, v2)
+
+
+def test_raw_loader_reports_a_batch_larger_than_its_buffer(tmp_path):
+    F = 6
+    lab, ids, vals = _rows(300, F, 3)
+    p = str(tmp_path / "tr-0.tfrecords")
+    nio.write_examples(p, lab, ids, vals)
+    ld = nio.NativeLoader([p], F, 128, threads=1, raw=True)
+    with pytest.raises(IOError, match="exceeds"):
+        ld.next_raw_into(torch.zeros(1000, dtype=torch.uint8), torch.zeros(129, dtype=torch.int32))
+    ld.close()
