@@ -356,8 +356,8 @@ def test_overlapped_exchange_matches_default(monkeypatch, N, run, sharded, updat
 
 @pytest.mark.parametrize("sharded", [True, False])
 def test_dense_allreduce_equals_rank_order_gather(monkeypatch, sharded):
-    """HIPFM_DENSE_XCHG: the fused exchange's dense gradient all-reduced (default from 4 ranks)
-    or all-gathered and summed in rank order by the owner launch.  The emulated all-reduce sums
+    """HIPFM_DENSE_XCHG: the fused exchange's dense gradient all-gathered and summed in rank order
+    by the owner launch (the default) or all-reduced (opt-in).  The emulated all-reduce sums
     in rank order too, so the two are bitwise equal here (RCCL's ring order differs only by
     reassociation); every rank ends identical."""
     from hipfm.ops import kernels as KN
@@ -375,11 +375,10 @@ def test_dense_allreduce_equals_rank_order_gather(monkeypatch, sharded):
         hub = _Hub(N)
         models = []
         for r in range(N):
-            m = NativeDeepFM(V, F, K, layers, keep, sparse_update=update, learning_rate=1e-3, batch_size=B,
+            m = NativeDeepFM(V, F, K, layers, keep, sparse_update="lazy", learning_rate=1e-3, batch_size=B,
                              device=DEV, init=False, comm=MeshComm(hub, r, sharded=sharded),
                              field_ranges=synth.field_ranges())
             m.load_tf_params(params)
-            assert update == "lazy" or m.tf1_xsplit          # (tf1_dense: the split form's owner sweep)
             x = m.shx if sharded else m.rpx
             x.trace = []
             models.append(m)
