@@ -458,44 +458,80 @@ __global__ void __launch_bounds__(RB_THREADS) __attribute__((amdgpu_waves_per_eu
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // K-tile staging: 32 A pieces + 32 B pieces of 1 KB, 8 + 8 per wave
-  auto stage = [&](char* buf, int k0) {
+  // K-tile staging: 32 A pieces + 32 B pieces of 1 KB, 8 + 8 per wave (pieces 0-7: A, 8-15: B);
+  // per-lane source offsets at k = 0 hoisted
+  int soff[16];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int piece = wave * 8 + i;
-      const int r = piece * 8 + (lane >> 3);
-      const int c = (lane & 7) ^ ((r >> 1) & 7);
-      __builtin_amdgcn_global_load_lds(
-          (const __attribute__((address_space(1))) void*)(A + (size_t)(m0 + r) * lda + k0 + c * 8),
-          (__attribute__((address_space(3))) void*)(buf + piece * 1024), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds(
-          (const __attribute__((address_space(1))) void*)(Bm + (size_t)(n0 + r) * ldb + k0 + c * 8),
-          (__attribute__((address_space(3))) void*)(buf + PP_PANEL + piece * 1024), 16, 0, 0);
-    }
+  for (int p = 0; p < 16; ++p) {
+    const int r = (wave * 8 + (p & 7)) * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ ((r >> 1) & 7);
+    soff[p] = p < 8 ? (m0 + r) * lda + c * 8 : (n0 + r) * ldb + c * 8;
+  }
+  auto piece = [&](char* buf, int k0, int p) {
+    __builtin_amdgcn_global_load_lds(
+        (const __attribute__((address_space(1))) void*)((p < 8 ? A : Bm) + soff[p] + k0),
+        (__attribute__((address_space(3))) void*)(buf + (p < 8 ? 0 : PP_PANEL) + (wave * 8 + (p & 7)) * 1024),
+        16, 0, 0);
   };
-  stage(smem, kb);
+  // fragment byte offsets (rows base + 16 i + fr: swizzle (fr >> 1) & 7), k-halves h = 0, 1
+  const int swz = (fr >> 1) & 7;
+  const int la0 = (wr * 128 + fr) * 128 + ((fq ^ swz) << 4), la1 = (wr * 128 + fr) * 128 + (((4 + fq) ^ swz) << 4);
+  const int lb0 = (wcn * 128 + fr) * 128 + ((fq ^ swz) << 4), lb1 = (wcn * 128 + fr) * 128 + (((4 + fq) ^ swz) << 4);
+#pragma unroll
+  for (int p = 0; p < 16; ++p) piece(smem, kb, p);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  bf16x8 fa[8], fb[8], ga[8], gb[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    fb[i] = *reinterpret_cast<const bf16x8*>(smem + PP_PANEL + lb0 + i * 2048);
+    fa[i] = *reinterpret_cast<const bf16x8*>(smem + la0 + i * 2048);
+  }
+  // Issue order pinned per K-tile (sched_barrier around every non-MFMA op: one wave per SIMD, so
+  // any stall of the in-order stream idles the matrix core):
+  //   half 0: 64 MFMAs; a staging DMA of the next K-tile after each of the first 16, a fragment
+  //           read of half 1 after each of the next 16
+  //   half 1: 48 MFMAs; vmcnt(0) lgkmcnt(0) + barrier; the last 16 MFMAs each followed by a
+  //           fragment read of the next K-tile's half 0 (from the buffer that just landed)
   for (int t = 0; t < nt; ++t) {
     const char* pa = smem + (t & 1) * PP_BUF;
-    const char* pb = pa + PP_PANEL;
-    if (t + 1 < nt) stage(smem + ((t + 1) & 1) * PP_BUF, kb + (t + 1) * PP_BK);
+    char* nb = smem + ((t + 1) & 1) * PP_BUF;
+    const bool more = t + 1 < nt;
+    const int kn = kb + (more ? t + 1 : t) * PP_BK;   // the last K-tile re-stages itself (idle buffer)
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      bf16x8 fa[8], fb[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        fa[i] = *reinterpret_cast<const bf16x8*>(pa + gl_slot(wr * 128 + i * 16 + fr, ks * 4 + fq));
-        fb[i] = *reinterpret_cast<const bf16x8*>(pb + gl_slot(wcn * 128 + i * 16 + fr, ks * 4 + fq));
+    for (int n = 0; n < 64; ++n) {
+      const int i = n >> 3, j = n & 7;
+      acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (n < 16) {
+        piece(nb, kn, n);
+        __builtin_amdgcn_sched_barrier(0);
+      } else if (n < 32) {
+        const int q = n - 16;
+        if (q < 8) gb[q] = *reinterpret_cast<const bf16x8*>(pa + PP_PANEL + lb1 + q * 2048);
+        else ga[q - 8] = *reinterpret_cast<const bf16x8*>(pa + la1 + (q - 8) * 2048);
+        __builtin_amdgcn_sched_barrier(0);
       }
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+#pragma unroll
+    for (int n = 0; n < 48; ++n) {
+      acc[n >> 3][n & 7] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ga[n >> 3], gb[n & 7], acc[n >> 3][n & 7], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int n = 48; n < 64; ++n) {
+      acc[n >> 3][n & 7] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ga[n >> 3], gb[n & 7], acc[n >> 3][n & 7], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (more) {
+        const int q = n - 48;
+        if (q < 8) fb[q] = *reinterpret_cast<const bf16x8*>(nb + PP_PANEL + lb0 + q * 2048);
+        else fa[q - 8] = *reinterpret_cast<const bf16x8*>(nb + la0 + (q - 8) * 2048);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
   }
 
   uint32_t salt = 0;
@@ -506,6 +542,176 @@ __global__ void __launch_bounds__(RB_THREADS) __attribute__((amdgpu_waves_per_eu
 #pragma unroll
     for (int j = 0; j < 8; ++j)
       epi_store<EPI>(ep, acc[i][j], m0 + wr * 128 + i * 16 + cr, n0 + wcn * 128 + j * 16 + fr, M, N, salt);
+}
+
+// ------------------------------------------------------------------ K-half ring GEMM (tile 12)
+// 256 x 256 workgroup tile, 8 waves as two staggered groups (G = wave >> 2 owns rows G*128..+128,
+// wc = wave & 3 columns wc*64..+64: acc[8][4] per wave), like tile 9/10 -- but the K loop runs over
+// 32-deep K-HALVES held in a ring of 4 LDS buffers (A [256][32] + B [256][32] bf16, 32 KB each:
+// 128 KB), so the LDS-DMA of K-half h + 3 is issued while h is consumed and stays in flight
+// across ~8 barriers, retired by a COUNTED vmcnt(8) (never 0 in the steady state).  Tile 9/10's
+// 64-deep K-tiles in two buffers left the DMA in flight for about one phase before its vmcnt(0).
+// Per K-half and wave: 2 phases of 16 MFMAs (rows 4s..4s+3 of the wave's 8 m-tiles x its 4
+// n-tiles); B fragments read in phase 0, A fragments of the phase's rows in each phase.
+// Slot schedule (G1 one slot behind G0: each SIMD alternates a G0 and a G1 wave between loading
+// and MFMAs): slot 4h + 2s = G0 load / G1 compute of phase (h, s), 4h + 2s + 1 the reverse.
+//   staging of K-half h + 3 into buffer (h - 1) % 4: G0 all 4 DMAs in its load slot of (h, 1)
+//   (slot 4h + 2), G1 two in each of its load slots of (h, 0) / (h, 1) (slots 4h + 1, 4h + 3):
+//   every read of K-half h - 1 was retired by its reader's lgkmcnt(0) before the barrier that
+//   ends slot 4h.
+//   retirement of K-half h + 1 before slot 4h + 4 (its first read): G0 at the end of its compute
+//   slot 4h + 3, G1 in its load slot 4h + 3 after issuing its DMAs -- 8 newer DMAs (K-halves
+//   h + 2, h + 3) may stay in flight; vmcnt(0) where fewer were issued (the last K-halves).
+// Image of a K-half operand: rows of 64 B, lane-linear DMA pieces of 16 rows; 16-B chunk c of row r
+// stored at slot c ^ ((r >> 2) & 3) (16 rows x one chunk = 16 distinct bank groups).
+constexpr int P8_KH = 32;                       // K-half depth
+constexpr int P8_OP = PP_BM * P8_KH * 2;        // 16 KB: one operand's K-half
+constexpr int P8_BUF = 2 * P8_OP;               // A + B: 32 KB, 4 in the ring
+
+template <int EPI>
+__global__ void __launch_bounds__(PP_THREADS, 1) gemm_p8_kernel(
+    const bf16* __restrict__ A, int lda, const bf16* __restrict__ Bm, int ldb, int M, int N,
+    int kchunk, EpiArgs ep) {
+  __shared__ __attribute__((aligned(16))) char smem[4 * P8_BUF];   // (the only __shared__ object)
+  // (wave-uniform in an SGPR: the group branches below are scalar)
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int grp = wave >> 2, wc = wave & 3;
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, rr = nwg & 7;
+  const int tid = (xcd < rr ? xcd * (q8 + 1) : rr * (q8 + 1) + (xcd - rr) * q8) + (bid >> 3);
+  const int tiles_n = N / PP_BM;
+  const int m0 = (tid / tiles_n) * PP_BM, n0 = (tid % tiles_n) * PP_BM;
+  const int kb = blockIdx.z * kchunk;
+  const int nkh = kchunk / P8_KH;
+  const int fr = lane & 15, fq = lane >> 4;
+  // this wave's 4 staging pieces per K-half: A pieces 2w, 2w + 1 and B pieces 2w, 2w + 1
+  int soff[4], doff[4];
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int piece = wave * 2 + (p & 1);
+    const int r = piece * 16 + (lane >> 2);
+    const int c = (lane & 3) ^ ((r >> 2) & 3);
+    soff[p] = p < 2 ? (m0 + r) * lda + c * 8 : (n0 + r) * ldb + c * 8;
+    doff[p] = (p < 2 ? 0 : P8_OP) + piece * 1024;
+  }
+  auto stage = [&](int h, int p) {
+    __builtin_amdgcn_global_load_lds(
+        (const __attribute__((address_space(1))) void*)((p < 2 ? A : Bm) + soff[p] + kb + h * P8_KH),
+        (__attribute__((address_space(3))) void*)(smem + (h & 3) * P8_BUF + doff[p]), 16, 0, 0);
+  };
+  // fragment byte offsets: row base + fr (bases multiples of 16: swizzle (fr >> 2) & 3), chunk fq
+  const int cs = (fq ^ ((fr >> 2) & 3)) << 4;
+  const int la = (grp * 128 + fr) * 64 + cs;
+  const int lb = P8_OP + (wc * 64 + fr) * 64 + cs;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // prologue: K-halves 0, 1, 2 in flight, 0 and 1 retired (the 4 DMAs of 2 may remain)
+#pragma unroll
+  for (int h = 0; h < 3; ++h)
+#pragma unroll
+    for (int p = 0; p < 4; ++p) stage(h, p);
+  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  if (grp == 1) {                         // the stagger: group 1 runs one slot behind
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  // fragments one phase ahead: fa[phase parity], fb[K-half parity]; phase (0, 0)'s now
+  bf16x8 fa[2][4], fb[2][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) fb[0][j] = *reinterpret_cast<const bf16x8*>(smem + lb + j * 1024);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) fa[0][i] = *reinterpret_cast<const bf16x8*>(smem + la + i * 1024);
+
+  // phase (h, s) with h parity HP (fragment sets static after unrolling by two K-halves)
+  auto phase = [&](int h, auto HPc, auto Sc) {
+    constexpr int HP = decltype(HPc)::value, S = decltype(Sc)::value;
+    const bool st3 = h + 3 < nkh;
+    // ---- load slot: staging of K-half h + 3, the retirement of h + 2 (group 1)
+    if (st3) {
+      if (grp == 0 && S == 1) {
+#pragma unroll
+        for (int p = 0; p < 4; ++p) stage(h + 3, p);
+      } else if (grp == 1) {
+        stage(h + 3, 2 * S);
+        stage(h + 3, 2 * S + 1);
+      }
+    }
+    if (grp == 1 && S == 1) {
+      if (st3) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    // ---- compute slot: this phase's fragments were read one slot ago
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+    // next phase: (h, 1) -> A rows 4-7 of K-half h; (h + 1, 0) -> B and A rows 0-3 of K-half h + 1
+    const bool nxt = S == 0 || h + 1 < nkh;
+    const char* nbuf = smem + ((S == 0 ? h : h + 1) & 3) * P8_BUF;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        acc[S * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[S][i], fb[HP][j], acc[S * 4 + i][j], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (nxt) {
+          if (S == 0 && j == 1) fa[1][i] = *reinterpret_cast<const bf16x8*>(nbuf + la + (4 + i) * 1024);
+          if (S == 1 && j == 1) fb[HP ^ 1][i] = *reinterpret_cast<const bf16x8*>(nbuf + lb + i * 1024);
+          if (S == 1 && j == 3) fa[0][i] = *reinterpret_cast<const bf16x8*>(nbuf + la + i * 1024);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    __builtin_amdgcn_s_setprio(0);
+    if (grp == 0 && S == 1) {              // retire K-half h + 2 (h + 3's DMAs may stay in flight)
+      if (st3) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  for (int h = 0; h < nkh; h += 2) {
+    phase(h, I0{}, I0{});
+    phase(h, I0{}, I1{});
+    phase(h + 1, I1{}, I0{});
+    phase(h + 1, I1{}, I1{});
+  }
+  if (grp == 0) __builtin_amdgcn_s_barrier();   // (every wave passes the same number of barriers)
+
+  uint32_t salt = 0;
+  if (EPI == EPI_FWD && ep.drop) salt = dropout_salt(ep.seed, (uint32_t)(*ep.step), ep.layer);
+  const int cr = fq * 4;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      epi_store<EPI>(ep, acc[i][j], m0 + grp * 128 + i * 16 + cr, n0 + wc * 64 + j * 16 + fr, M, N, salt);
+}
+
+template <int EPI>
+static int launch_gemm_p8(const bf16* A, int lda, const bf16* B, int ldb, int M, int N, int Kd,
+                          int splitk, const EpiArgs& ep, hipStream_t st) {
+  // (an even number of K-halves per split, at least 4: the loop runs K-half pairs, the prologue
+  // stages three)
+  if (M % PP_BM || N % PP_BM || splitk < 1 || Kd % (2 * P8_KH * splitk) || Kd / splitk < 4 * P8_KH || lda % 8 ||
+      ldb % 8 || ((uintptr_t)A & 15) || ((uintptr_t)B & 15))
+    return (int)hipErrorInvalidValue;
+  dim3 grid((M / PP_BM) * (N / PP_BM), 1, splitk);
+  hipLaunchKernelGGL((gemm_p8_kernel<EPI>), grid, dim3(PP_THREADS), 0, st, A, lda, B, ldb, M, N,
+                     Kd / splitk, ep);
+  HFM_LAUNCH_CHECK();
 }
 
 template <int EPI>
@@ -546,7 +752,8 @@ static int launch_gemm_lds(const bf16* A, int lda, const bf16* B, int ldb, int M
 
 // tile: 0 = 64x64 (2x2 waves), 1 = 128x32 (4x1), 2 = 32x128 (1x4), 3 = 32x32 (1x1), 4 = 32x64 (1x2),
 //       5 = 32x160 (1x5), 6 = 32x320 (1x10), 7 = 32x256 (1x8), 8 = 128x128 LDS-staged (wide layers),
-//       9 = 256x256 ping-pong (wide layers, 8 waves)
+//       9 = 256x256 ping-pong (wide layers, 8 waves), 10 = same, staging spread, 11 = 256x256
+//       register-blocked (4 waves), 12 = 256x256 K-half ring (8 waves, counted DMA waits)
 template <int EPI>
 static int gemm_tile(int tile, const bf16* A, int lda, const bf16* B, int ldb, int M, int N, int Kd,
                      int splitk, const EpiArgs& ep, hipStream_t st) {
@@ -563,6 +770,7 @@ static int gemm_tile(int tile, const bf16* A, int lda, const bf16* B, int ldb, i
     case 9: return launch_gemm_pp<EPI, 0>(A, lda, B, ldb, M, N, Kd, splitk, ep, st);
     case 10: return launch_gemm_pp<EPI, 1>(A, lda, B, ldb, M, N, Kd, splitk, ep, st);
     case 11: return launch_gemm_rb<EPI>(A, lda, B, ldb, M, N, Kd, splitk, ep, st);
+    case 12: return launch_gemm_p8<EPI>(A, lda, B, ldb, M, N, Kd, splitk, ep, st);
     default: return (int)hipErrorInvalidValue;
   }
 }

@@ -127,6 +127,12 @@ __global__ void __launch_bounds__(SH_THREADS) sh_scatter_kernel(
 // segments + sh_bucket produced.  Outputs: sid_incl[i] (1-based unique index of slot i's id),
 // send_ids[o][c] (-1 past the bucket's count), upos[u] = o*C + c, send_cnt[o], num_u.
 constexpr int RT_ITEMS = 16;
+
+// global-address-space access: the run kernels take their pointers from device descriptors, which
+// makes them flat -- and a flat load shares lgkmcnt with the LDS counters, so every LDS step of the
+// ranking waited on it (vmcnt(0) after each key load: the scatter measured 146 us vs 52)
+__device__ __forceinline__ int gld(const int* p) { return *(const __attribute__((address_space(1))) int*)p; }
+__device__ __forceinline__ void gst(int* p, int v) { *(__attribute__((address_space(1))) int*)p = v; }
 constexpr int RT_TILE = SH_THREADS * RT_ITEMS;
 
 // Per-tile head counts per owner.  Heads are counted per wave with ballots (lanes of one owner
@@ -141,16 +147,18 @@ __device__ __forceinline__ void sh_route_count_body(const int* __restrict__ sk, 
   const int i0 = bx * RT_TILE;
   const unsigned long long lt = (1ull << lane) - 1ull;
   int nh = 0;
-#pragma unroll 4
+  int ky[RT_ITEMS], kp[RT_ITEMS];
+#pragma unroll
+  for (int k = 0; k < RT_ITEMS; ++k) {     // all loads first (clamped: no branches around them)
+    const int ic = min(i0 + k * SH_THREADS + tid, n - 1);
+    ky[k] = gld(sk + ic);
+    kp[k] = gld(sk + max(ic - 1, 0));
+  }
+#pragma unroll
   for (int k = 0; k < RT_ITEMS; ++k) {
     const int i = i0 + k * SH_THREADS + tid;
-    bool head = false;
-    int o = 0;
-    if (i < n) {
-      const int key = sk[i];
-      head = (i == 0 || key != sk[i - 1]);
-      o = head ? key % N : 0;
-    }
+    const bool head = i < n && (i == 0 || ky[k] != kp[k]);
+    const int o = head ? ky[k] % N : 0;
     const unsigned long long hb = __ballot(head);
     unsigned long long peers = hb;
     for (int bit = 0; bit < nbits; ++bit) {
@@ -163,7 +171,7 @@ __device__ __forceinline__ void sh_route_count_body(const int* __restrict__ sk, 
   }
   if (lane == 0) atomicAdd(&h[N], nh);
   __syncthreads();
-  if (tid <= N) tcnt[bx * (N + 1) + tid] = h[tid];
+  if (tid <= N) gst(tcnt + bx * (N + 1) + tid, h[tid]);
 }
 
 __global__ void __launch_bounds__(SH_THREADS) sh_route_count_kernel(const int* __restrict__ sk, int n, int N,
@@ -175,7 +183,8 @@ __global__ void __launch_bounds__(SH_THREADS) sh_route_count_kernel(const int* _
 __device__ __forceinline__ void sh_route_scatter_body(
     const int* __restrict__ sk, int n, int N, int nbits, int C, const int* __restrict__ tcnt, int nt,
     int* __restrict__ sid_incl, int* __restrict__ send_ids, int* __restrict__ upos, int* __restrict__ send_cnt,
-    int* __restrict__ num_u, unsigned* __restrict__ err, int bx, int ostride) {
+    int* __restrict__ num_u, unsigned* __restrict__ err, int bx, int ostride,
+    const int* __restrict__ perm = nullptr, int* __restrict__ slot_row = nullptr, int F = 1, int ld = 0) {
   __shared__ int off[SH_MAXN + 1];
   __shared__ int tot[SH_MAXN + 1];
   __shared__ int wc[4][SH_MAXN + 1];  // per wave: heads per owner, [N]: all heads
@@ -184,37 +193,46 @@ __device__ __forceinline__ void sh_route_scatter_body(
   __syncthreads();
   for (int e = tid; e < nt * (N + 1); e += SH_THREADS) {
     const int b = e / (N + 1), o = e - b * (N + 1);
-    const int c = tcnt[e];
+    const int c = gld(tcnt + e);
     if (b < bx) atomicAdd(&off[o], c);
     atomicAdd(&tot[o], c);
   }
   __syncthreads();
   if (bx == 0) {
     if (tid < N) {
-      send_cnt[tid] = tot[tid];
+      gst(send_cnt + tid, tot[tid]);
       if (tot[tid] > C) atomicOr(err, 2u);
     }
-    if (tid == 0) *num_u = tot[N];
+    if (tid == 0) gst(num_u, tot[N]);
   }
   for (int e = bx * SH_THREADS + tid; e < N * C; e += nt * SH_THREADS) {
     const int o = e / C, c = e - o * C;
-    if (c >= tot[o]) send_ids[(size_t)o * ostride + c] = -1;  // unused capacity: padding entries
+    if (c >= tot[o]) gst(send_ids + (size_t)o * ostride + c, -1);  // unused capacity: padding entries
   }
   const int w0 = bx * RT_TILE + wv * 64 * RT_ITEMS;
   const unsigned long long lt = (1ull << lane) - 1ull;
-  int key[RT_ITEMS], own[RT_ITEMS], rnk[RT_ITEMS], hin[RT_ITEMS];
+  int key[RT_ITEMS], own[RT_ITEMS], rnk[RT_ITEMS], hin[RT_ITEMS], pq[RT_ITEMS], kp[RT_ITEMS];
+  // every load first, unconditional (clamped indices): branch-free, all in flight at once
+#pragma unroll
+  for (int k = 0; k < RT_ITEMS; ++k) {
+    const int ic = min(w0 + k * 64 + lane, n - 1);
+    key[k] = gld(sk + ic);
+    kp[k] = gld(sk + max(ic - 1, 0));
+    pq[k] = slot_row ? gld(perm + ic) : 0;
+  }
   unsigned hmask = 0;
   int run = 0;  // heads in this wave's earlier chunks (wave-uniform)
 #pragma unroll
   for (int k = 0; k < RT_ITEMS; ++k) {
     const int i = w0 + k * 64 + lane;
     const bool valid = i < n;
-    key[k] = valid ? sk[i] : 0;
-    const bool head = valid && (i == 0 || key[k] != sk[i - 1]);
+    const bool head = valid && (i == 0 || key[k] != kp[k]);
     const unsigned long long hb = __ballot(head);
     hin[k] = run + __popcll(hb & (lt | (1ull << lane)));  // heads up to and including slot i
     run += __popcll(hb);
-    const int o = head ? key[k] % N : 0;
+    // every slot's owner (not only the heads'): a slot's run head is the last head before it, so
+    // the last head of ITS owner -- its rank among this wave's heads of that owner is rk - 1
+    const int o = valid ? key[k] % N : 0;
     unsigned long long peers = hb;
     for (int bit = 0; bit < nbits; ++bit) {
       const bool bset = (o >> bit) & 1;
@@ -236,16 +254,24 @@ __device__ __forceinline__ void sh_route_scatter_body(
   for (int k = 0; k < RT_ITEMS; ++k) {
     const int i = w0 + k * 64 + lane;
     if (i >= n) continue;
-    sid_incl[i] = hw + hin[k];
-    if (!((hmask >> k) & 1u)) continue;
+    gst(sid_incl + i, hw + hin[k]);
+    const bool head = (hmask >> k) & 1u;
     const int o = own[k], u = hw + hin[k] - 1;
     int pos = off[o] + rnk[k];
     for (int w = 0; w < wv; ++w) pos += wc[w][o];
+    if (slot_row) {
+      // the slot -> received-row map (was sh_slot_rows_run: its dependent sid_incl -> upos reads);
+      // a run continuing from an earlier tile resolves to off[o] - 1, that tile's last head of o
+      const int rp = head ? pos : pos - 1;
+      const int q = pq[k];
+      gst(slot_row + (ld ? (size_t)(q % F) * ld + q / F : (size_t)q), rp < C ? o * C + rp : 0);
+    }
+    if (!head) continue;
     if (pos < C) {
-      send_ids[(size_t)o * ostride + pos] = key[k];
-      upos[u] = o * C + pos;
+      gst(send_ids + (size_t)o * ostride + pos, key[k]);
+      gst(upos + u, o * C + pos);
     } else {
-      upos[u] = -1;
+      gst(upos + u, -1);
       atomicOr(err, 2u);
     }
   }
@@ -291,22 +317,11 @@ __global__ void __launch_bounds__(SH_THREADS) sh_route_count_run_kernel(const Sh
 
 __global__ void __launch_bounds__(SH_THREADS) sh_route_scatter_run_kernel(const ShRouteBatch* __restrict__ rb, int n,
                                                                          int N, int nbits, int C, int nt,
-                                                                         unsigned* __restrict__ err, int ostride) {
+                                                                         unsigned* __restrict__ err, int ostride,
+                                                                         int F, int ld, int slot_rows) {
   const ShRouteBatch R = rb[blockIdx.y];
   sh_route_scatter_body(R.sk, n, N, nbits, C, R.tcnt, nt, R.sid_incl, R.send_ids, R.upos, R.send_cnt, R.num_u,
-                        err, blockIdx.x, ostride);
-}
-
-// slot -> row map; ld > 0: field-major [F][ld] (the tower gathers through idx_ld): the sorted
-// order scatters each field's writes over one 4*ld-byte span that L2 merges, where the row-major
-// map's stride-F writes each dirtied a line of their own (77 us for a 16-batch run vs ~10)
-__global__ void sh_slot_rows_run_kernel(const ShRouteBatch* __restrict__ rb, int n, int F, int ld) {
-  const ShRouteBatch R = rb[blockIdx.y];
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const int r = R.upos[R.sid_incl[i] - 1];
-  const int q = R.perm[i];
-  R.slot_row[ld ? (size_t)(q % F) * ld + q / F : (size_t)q] = r < 0 ? 0 : r;
+                        err, blockIdx.x, ostride, R.perm, slot_rows ? R.slot_row : nullptr, F, ld);
 }
 
 // Owner: rows[e] = the served row of each requested id (sh_row_words; zeros for padding entries)
@@ -473,7 +488,7 @@ HFM_API int hfm_sh_route(const int* sorted_keys, int n, int N, int C, int* tcnt,
   HFM_LAUNCH_CHECK();
 }
 
-// G batches' routing (descriptors rb [G], device): count, scatter, slot rows -- three launches;
+// G batches' routing (descriptors rb [G], device): count, then scatter + slot rows -- two launches;
 // ostride: owner block stride of every batch's send_ids (>= C); F, ld: slot map layout (ld = 0:
 // row-major [n], else field-major [F][ld], ld >= n / F)
 // slot_rows == 0: no slot -> row maps (the replicated exchange reads its gradient rows by unique
@@ -487,10 +502,9 @@ HFM_API int hfm_sh_route_run(const ShRouteBatch* rb, int G, int n, int N, int C,
   int nbits = 0;
   while ((1 << nbits) < N) ++nbits;
   hipLaunchKernelGGL(sh_route_count_run_kernel, dim3(nt, G), dim3(SH_THREADS), 0, st, rb, n, N, nbits);
+  // (the slot -> row maps come out of the scatter itself: 2 launches, was 3)
   hipLaunchKernelGGL(sh_route_scatter_run_kernel, dim3(nt, G), dim3(SH_THREADS), 0, st, rb, n, N, nbits, C, nt, err,
-                     ostride);
-  if (slot_rows)
-    hipLaunchKernelGGL(sh_slot_rows_run_kernel, dim3((n + 255) / 256, G), dim3(256), 0, st, rb, n, F, ld);
+                     ostride, F, ld, slot_rows);
   HFM_LAUNCH_CHECK();
 }
 
