@@ -767,9 +767,14 @@ class NativeDeepFM(GraphRunnerMixin, NativeStateMixin):
         output tile, 4 waves each; slabs, bias slabs, arrival counters."""
         M, dev = self.M, self.device
         f32 = dict(dtype=torch.float32, device=dev)
-        # 4 workgroup splits x 4 waves: same-box A/B 0.1214 (4) / 0.1228 (8) / 0.126 (16) ms/step
+        # 4 workgroup splits x 4 waves: same-box A/B 0.1214 (4) / 0.1228 (8) / 0.126 (16) ms/step;
+        # fewer at small batches, so every wave keeps >= 8 k-steps of 32 rows: at B = 1024 (the
+        # reference workload) 4 splits gave each wave 2 k-steps and 665 workgroups to dispatch ahead
+        # of the sparse tiles -- 0.0832-0.0837 (4) / 0.0764-0.0767 (2) / 0.0763-0.0764 (1) ms/step,
+        # while B = 16384 keeps 4: 0.1028-0.1037 (4) / 0.1038-0.1042 (2) / 0.131 (1)
+        # (profiles/r6_wgfin_splits_ab.log)
         ns = 4          # wgfin workgroups per output tile (8 / 16: equal or slower)
-        while ns > 1 and (M % (ns * 4 * 32) or M // (ns * 4) < 32):
+        while ns > 1 and (M % (ns * 4 * 32) or M // (ns * 4 * 32) < 8):
             ns //= 2
         self._wgfin_ns = ns
         self.wf_slabs, self.wf_bslabs, jobs = [], [], []
