@@ -172,7 +172,8 @@ class BlockReader {
 
 // One TFRecord, in place: rec / len point into the reader's block until the next call.
 // returns 1 = record, 0 = clean EOF, -1 = error
-static int next_tfrecord_view(BlockReader& r, const uint8_t*& rec, uint64_t& len, bool verify,
+// verify: 0 none, 1 length + data CRC, 2 length CRC only (the data CRC is checked on the GPU)
+static int next_tfrecord_view(BlockReader& r, const uint8_t*& rec, uint64_t& len, int verify,
                               size_t& pending) {
   r.consume(pending);
   pending = 0;
@@ -200,7 +201,7 @@ static int next_tfrecord_view(BlockReader& r, const uint8_t*& rec, uint64_t& len
     return -1;
   }
   rec = p + 12;
-  if (verify) {
+  if (verify == 1) {
     uint32_t dcrc;
     memcpy(&dcrc, rec + len, 4);
     if (dcrc != masked(hfmio_crc32c(rec, len))) {
@@ -782,7 +783,7 @@ struct Loader {
         return -2;
       }
       const uint8_t* rp = p + at + 12;
-      if (verify) {
+      if (verify == 1) {
         uint32_t dcrc;
         memcpy(&dcrc, rp + len, 4);
         if (dcrc != masked(hfmio_crc32c(rp, len))) {
@@ -793,7 +794,8 @@ struct Loader {
       at += 12 + len + 4;
       if (shard_n > 1 && (rec++ % shard_n) != shard_i) continue;
       if (c->maps.empty() || c->maps.back() != m) c->maps.push_back(m);   // (a chunk may span files)
-      c->add_mapped(rp, (uint32_t)len);
+      // verify 2: the record travels with its 4-byte masked data CRC (the decode kernel checks it)
+      c->add_mapped(rp, (uint32_t)len + (verify == 2 ? 4u : 0u));
       if (++c->n == chunk) {
         if (!push(std::move(c))) return -2;
         c = fresh();
@@ -825,11 +827,12 @@ struct Loader {
         return false;
       }
       if (shard_n > 1 && (rec++ % shard_n) != shard_i) continue;
-      if (c->raw.size() + rlen > 0xFFFFFFFFull) {
+      const uint64_t rl = rlen + (verify == 2 ? 4u : 0u);   // (+ the data CRC: contiguous in the view)
+      if (c->raw.size() + rl > 0xFFFFFFFFull) {
         fail("raw chunk exceeds 4 GB in " + path);
         return false;
       }
-      c->add_copied(rp, (uint32_t)rlen);
+      c->add_copied(rp, (uint32_t)rl);
       if (++c->n == chunk) {
         if (!push(std::move(c))) return false;
         c = fresh();
@@ -1157,7 +1160,7 @@ HFMIO_API void* hfmio_loader_create(const char** paths, int npaths, int format, 
   L->F = F;
   L->B = batch;
   L->drop_remainder = drop_remainder;
-  L->verify = verify_crc;
+  L->verify = verify_crc ? 1 : 0;        // (2 = device-side data CRC: raw loaders only)
   L->shard_n = shard_n < 1 ? 1 : shard_n;
   L->shard_i = shard_i;
   L->depth = queue_depth < 1 ? 4 : queue_depth;
@@ -1181,7 +1184,8 @@ HFMIO_API void* hfmio_loader_create_raw(const char** paths, int npaths, int F, i
   L->F = F;
   L->B = batch;
   L->drop_remainder = drop_remainder;
-  L->verify = verify_crc;
+  // 2: the length CRC here, the data CRC on the GPU (each record shipped with its 4 CRC bytes)
+  L->verify = verify_crc == 2 ? 2 : (verify_crc ? 1 : 0);
   L->shard_n = shard_n < 1 ? 1 : shard_n;
   L->shard_i = shard_i;
   L->depth = queue_depth < 1 ? 4 : queue_depth;

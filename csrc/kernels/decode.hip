@@ -1,8 +1,9 @@
 // GPU decode of serialized tf.train.Example records (TF's ParseExample on the
 // reference's input path, PS:79-133 / HVD:79-133), the streamed-epoch half of the input pipeline.
 //
-// The host loader (csrc/io/hfm_io.cpp, raw mode) only frames TFRecords and checks their CRCs
-// (~10 ns per record) and ships each batch as the records' bytes back to back + B + 1 offsets;
+// The host loader (csrc/io/hfm_io.cpp, raw mode) only frames TFRecords and checks their length
+// CRCs and ships each batch as the records' bytes back to back + B + 1 offsets (crc mode: each
+// record followed by its data CRC, verified here -- the host does no per-byte work at all);
 // this kernel writes the fixed-schema features straight into a device ring slot:
 //   label f32 [B], ids int32 [B, F] (checked against [0, V) and int32), values f32 [B, F].
 // Schema (any field / map-entry order, unknown fields skipped):
@@ -13,11 +14,100 @@
 // a time -- a ballot of the varint terminator bits gives every terminator lane its id index and
 // its varint's first byte, so each id is assembled by one lane.
 // Errors never fault: a record that does not match the schema gets zero ids / values and sets
-// err[0] bit 0, an id outside [0, V) or int32 is written as 0 and sets bit 1; err[1] holds the
-// smallest bad record index of the batch (the host reports it).
+// err[0] bit 0, an id outside [0, V) or int32 is written as 0 and sets bit 1, a data CRC mismatch
+// (crc mode) zeroes the row and sets bit 2; err[1] holds the smallest bad record index of the
+// batch (the host reports it).
 #include "common.h"
 
 namespace {
+
+// ---- TFRecord data CRC (crc mode): masked CRC32C of the payload, checked here instead of on the
+// host (the host's serial crc32 chain was ~57 ns of its ~66 ns per record).  Tables are built at
+// compile time.  Slice-by-8 over 8-byte steps; 8 lanes each take one of 8 equal segments (the
+// message is conceptually front-padded with zero bytes to 8 * seg: leading zeros leave a CRC
+// register of 0 unchanged) and the partial CRCs are combined in a shuffle tree, multiplying by
+// x^(8 seg), x^(16 seg), x^(32 seg) mod P; the initial register ~0 is folded in by inverting the
+// first 4 message bytes (a 32-bit reflected CRC depends on state ^ first word only).
+constexpr uint32_t CRC_POLY = 0x82F63B78u;    // CRC32C, reflected
+constexpr uint32_t crc_x1(uint32_t b) { return (b & 1u) ? (b >> 1) ^ CRC_POLY : b >> 1; }   // b * x
+__host__ __device__ constexpr uint32_t crc_mulmod(uint32_t a, uint32_t b) {                    // a * b mod P
+  uint32_t p = 0;
+  for (int k = 0; k < 32; ++k) {
+    if (a & (0x80000000u >> k)) p ^= b;
+    b = crc_x1(b);
+  }
+  return p;
+}
+struct CrcTabs {
+  uint32_t t[8][256];
+};
+constexpr CrcTabs make_crc_tabs() {
+  CrcTabs T{};
+  for (int i = 0; i < 256; ++i) {
+    uint32_t c = (uint32_t)i;
+    for (int k = 0; k < 8; ++k) c = crc_x1(c);
+    T.t[0][i] = c;
+  }
+  for (int k = 1; k < 8; ++k)
+    for (int i = 0; i < 256; ++i) T.t[k][i] = (T.t[k - 1][i] >> 8) ^ T.t[0][T.t[k - 1][i] & 0xFFu];
+  return T;
+}
+constexpr int CRC_SEGS = 128;                 // parallel path: seg = 8 (s + 1) bytes, n <= 8 * 1024
+struct CrcOps {
+  uint32_t op[CRC_SEGS][3];                   // x^(8 seg), x^(16 seg), x^(32 seg) mod P
+};
+constexpr CrcOps make_crc_ops() {
+  CrcOps O{};
+  uint32_t x = 0x80000000u;                   // x^0
+  for (int s = 0; s < CRC_SEGS; ++s) {
+    for (int k = 0; k < 64; ++k) x = crc_x1(x);
+    O.op[s][0] = x;
+    O.op[s][1] = crc_mulmod(x, x);
+    O.op[s][2] = crc_mulmod(O.op[s][1], O.op[s][1]);
+  }
+  return O;
+}
+__constant__ CrcTabs kCrcT = make_crc_tabs();
+__constant__ CrcOps kCrcOps = make_crc_ops();
+
+// masked CRC32C of the payload [0, n) of r (valid in lane 0)
+template <class R>
+__device__ uint32_t payload_crc(const R& r, uint32_t n, int lane) {
+  uint32_t v = 0;
+  if (n < 64 || n > 8u * 8u * CRC_SEGS) {     // short / very long: one lane, plain byte loop
+    if (lane == 0) {
+      v = 0xFFFFFFFFu;
+      for (uint32_t i = 0; i < n; ++i) v = kCrcT.t[0][(v ^ r.at(i)) & 0xFFu] ^ (v >> 8);
+      v = ~v;
+    }
+  } else {
+    const uint32_t seg = ((n + 63u) / 64u) * 8u, z = 8u * seg - n;
+    if (lane < 8) {
+      const int b1 = (int)((lane + 1) * seg) - (int)z;
+      int pos = max((int)(lane * seg) - (int)z, 0);
+      auto byte = [&](int i) { return r.at((uint32_t)i) ^ (i < 4 ? 0xFFu : 0u); };
+      while (pos < b1 && ((b1 - pos) & 7)) {   // (a lane wholly inside the zero padding: b1 <= 0)
+        v = kCrcT.t[0][(v ^ byte(pos)) & 0xFFu] ^ (v >> 8);
+        ++pos;
+      }
+      for (; pos < b1; pos += 8) {
+        const uint32_t lo = byte(pos) | (byte(pos + 1) << 8) | (byte(pos + 2) << 16) | (byte(pos + 3) << 24);
+        const uint32_t hi = byte(pos + 4) | (byte(pos + 5) << 8) | (byte(pos + 6) << 16) | (byte(pos + 7) << 24);
+        v ^= lo;
+        v = kCrcT.t[7][v & 0xFFu] ^ kCrcT.t[6][(v >> 8) & 0xFFu] ^ kCrcT.t[5][(v >> 16) & 0xFFu] ^ kCrcT.t[4][v >> 24] ^
+            kCrcT.t[3][hi & 0xFFu] ^ kCrcT.t[2][(hi >> 8) & 0xFFu] ^ kCrcT.t[1][(hi >> 16) & 0xFFu] ^ kCrcT.t[0][hi >> 24];
+      }
+    }
+    const uint32_t* op = kCrcOps.op[seg / 8u - 1u];
+#pragma unroll
+    for (int l = 0; l < 3; ++l) {             // (v_i, v_{i + 2^l}) -> v_i * x^(8 seg 2^l) ^ v_{i + 2^l}
+      const uint32_t o = (uint32_t)__shfl_down((int)v, 1 << l, 64);
+      if ((lane & ((2 << l) - 1)) == 0 && lane < 8) v = crc_mulmod(op[l], v) ^ o;
+    }
+    v = ~v;
+  }
+  return ((v >> 15) | (v << 17)) + 0xa282ead8u;
+}
 
 constexpr int DEC_WAVES = 4;          // records per 256-thread workgroup
 constexpr int DEC_STAGE = 1024;       // LDS bytes per wave (longer records read the rest from memory)
@@ -157,7 +247,8 @@ __device__ __forceinline__ bool name_is(const Rec& r, uint32_t pos, uint32_t len
 
 __global__ void __launch_bounds__(64 * DEC_WAVES) decode_examples_kernel(
     const uint8_t* __restrict__ raw, const uint32_t* __restrict__ offs, int rows, int F, int64_t limit,
-    int32_t* __restrict__ ids, float* __restrict__ vals, float* __restrict__ labels, int* __restrict__ err) {
+    int32_t* __restrict__ ids, float* __restrict__ vals, float* __restrict__ labels, int* __restrict__ err,
+    int crc) {
   __shared__ uint8_t stage[DEC_WAVES][DEC_STAGE];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int rec = blockIdx.x * DEC_WAVES + wv;
@@ -173,8 +264,21 @@ __global__ void __launch_bounds__(64 * DEC_WAVES) decode_examples_kernel(
   unsigned bad = 0;
   int have = 0;
   uint32_t pos = 0;
-  const uint32_t end = r.n;
+  uint32_t end = r.n;
   bool ok = true;
+  if (crc) {                            // the record's last 4 bytes: its masked data CRC
+    if (r.n < 4) {
+      ok = false;
+    } else {
+      end = r.n - 4;
+      const uint32_t want = r.at(end) | (r.at(end + 1) << 8) | (r.at(end + 2) << 16) | (r.at(end + 3) << 24);
+      const uint32_t got = (uint32_t)__shfl((int)payload_crc(r, end, lane), 0, 64);
+      if (got != want) {
+        bad |= 4u;
+        ok = false;
+      }
+    }
+  }
   while (ok && pos < end) {
     uint64_t key;
     if (!rd_varint(r, pos, end, key)) { ok = false; break; }
@@ -234,8 +338,8 @@ __global__ void __launch_bounds__(64 * DEC_WAVES) decode_examples_kernel(
       }
     }
   }
-  if (!ok || have != 7) bad |= 1u;
-  if (bad & 1u) {                       // schema mismatch: a defined (zero) row, never garbage ids
+  if (!(bad & 4u) && (!ok || have != 7)) bad |= 1u;
+  if (bad & 5u) {                       // schema / CRC mismatch: a defined (zero) row, never garbage ids
     for (int f = lane; f < F; f += 64) {
       idr[f] = 0;
       vr[f] = 0.f;
@@ -259,13 +363,15 @@ __global__ void __launch_bounds__(64 * DEC_WAVES) decode_examples_kernel(
 
 // raw: the batch's record bytes; offs: rows + 1 start offsets (offs[rows] = total bytes).
 // err: [2] ints, err[1] initialised to INT_MAX by the caller (the smallest bad record index).
+// crc: 1 = every record ends with its 4-byte masked data CRC (the raw loader's verify mode 2),
+// checked here (err bit 2 = value 4: mismatch; the row is zeroed)
 HFM_API int hfm_decode_examples(const void* raw, const void* offs, int rows, int F, long long limit, void* ids,
-                                void* vals, void* labels, void* err, hipStream_t st) {
+                                void* vals, void* labels, void* err, int crc, hipStream_t st) {
   if (rows <= 0) return 0;
   if (F <= 0 || !raw || !offs || !ids || !vals || !labels || !err) return (int)hipErrorInvalidValue;
   const int grid = (rows + DEC_WAVES - 1) / DEC_WAVES;
   hipLaunchKernelGGL(decode_examples_kernel, dim3(grid), dim3(64 * DEC_WAVES), 0, st, (const uint8_t*)raw,
                      (const uint32_t*)offs, rows, F, (int64_t)limit, (int32_t*)ids, (float*)vals, (float*)labels,
-                     (int*)err);
+                     (int*)err, crc);
   HFM_LAUNCH_CHECK();
 }

@@ -163,19 +163,24 @@ class NativeLoader:
                  fmt: int = FMT_TFRECORD, drop_remainder: bool = True, threads: int = 4,
                  record_shard: Tuple[int, int] = (1, 0), verify_crc: bool = True,
                  queue_depth: int = 4, id_limit: int = 0, copy_threads: Optional[int] = None,
-                 ids32: bool = False, raw: bool = False):
+                 ids32: bool = False, raw: bool = False, device_crc: bool = False):
         self.paths = [str(p) for p in paths]
         self.F, self.B = int(field_size), int(batch_size)
         # raw (TFRecord only): the workers frame records and check CRCs, batches carry the
         # serialized Examples for the GPU decoder (ops.kernels.decode_examples)
         self.raw = bool(raw)
+        # device_crc (raw, verify_crc): the workers check only each record's length CRC and ship
+        # the record with its 4-byte data CRC, which the decode kernel verifies (decode_examples
+        # crc=True) -- no per-byte work on the host
+        self.device_crc = self.raw and bool(device_crc) and bool(verify_crc)
         arr = (C.c_char_p * max(1, len(self.paths)))(*[p.encode() for p in self.paths])
         if self.raw:
             if fmt != FMT_TFRECORD:
                 raise ValueError("raw records are TFRecord Examples")
+            vmode = 2 if self.device_crc else (1 if verify_crc else 0)
             self._h = lib().hfmio_loader_create_raw(arr, len(self.paths), self.F, self.B,
                                                     1 if drop_remainder else 0, threads, record_shard[0],
-                                                    record_shard[1], 1 if verify_crc else 0, queue_depth)
+                                                    record_shard[1], vmode, queue_depth)
         else:
             self._h = lib().hfmio_loader_create(arr, len(self.paths), fmt, self.F, self.B,
                                                 1 if drop_remainder else 0, threads, record_shard[0],

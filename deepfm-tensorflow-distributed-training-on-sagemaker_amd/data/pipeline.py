@@ -282,6 +282,7 @@ class _DeviceFeeder:
         # GPU decode (a raw loader: ring mode only): pinned slots of record bytes + offsets, one
         # device staging pair per copy stream (a stream's next copy is ordered after its decode)
         self.raw = bool(getattr(loader, "raw", False))
+        self.dcrc = bool(getattr(loader, "device_crc", False))    # data CRCs checked by the decoder
         self.id_limit = int(id_limit)
         if self.raw:
             if ring is None or ring.compact:
@@ -401,7 +402,8 @@ class _DeviceFeeder:
             ev_copy = torch.cuda.Event()
             ev_copy.record(cs)
             ids, vals, lab = R.views[s]
-            K.decode_examples(draw, doffs, self.B, self.F, self.id_limit, ids, vals, lab, self.derr)
+            K.decode_examples(draw, doffs, self.B, self.F, self.id_limit, ids, vals, lab, self.derr,
+                              crc=self.dcrc)
             ev = torch.cuda.Event()
             ev.record(cs)
         self.h2d_bytes += nbytes + 4 * (self.B + 1)
@@ -421,7 +423,7 @@ class _DeviceFeeder:
             t = (torch.empty(r, self.F, dtype=self.id_dtype, device=self.device),
                  torch.empty(r, self.F, dtype=torch.float32, device=self.device),
                  torch.empty(r, dtype=torch.float32, device=self.device))
-            K.decode_examples(draw, doffs, r, self.F, self.id_limit, t[0], t[1], t[2], self.derr)
+            K.decode_examples(draw, doffs, r, self.F, self.id_limit, t[0], t[1], t[2], self.derr, crc=self.dcrc)
             ev = torch.cuda.Event()
             ev.record(cs)
         self.h2d_bytes += nbytes + 4 * (r + 1)
@@ -438,6 +440,8 @@ class _DeviceFeeder:
                 what.append("a record does not match the fixed Example schema (label, ids[F], values[F])")
             if e & 2:
                 what.append("a feature id lies outside [0, feature_size) or int32")
+            if e & 4:
+                what.append("TFRecord data CRC mismatch (corrupt record)")
             raise IOError("GPU Example decode: " + "; ".join(what) +
                           f" (first bad record: index {first} of its batch; its row was zeroed)")
 
@@ -732,8 +736,8 @@ class InputPipeline:
             n = 2 * int(self.ring_steps)
             # GPU decode (HIPFM_GPU_DECODE): the loader ships raw Example bytes, the ring slots take
             # the decoded plain layout
-            raw = (knob("HIPFM_GPU_DECODE") == "1" and self.fmt == FMT_TFRECORD and
-                   self.id_dtype == torch.int32)
+            gd = knob("HIPFM_GPU_DECODE")
+            raw = (gd in ("1", "2") and self.fmt == FMT_TFRECORD and self.id_dtype == torch.int32)
             compact = False if raw else None
             if self._ring is None or not self._ring.fits(self.B, self.F, self.id_dtype, n, compact):
                 self._ring = _DeviceRing(self.B, self.F, torch.device(self.device), self.id_dtype, n,
@@ -742,7 +746,7 @@ class InputPipeline:
             if raw:
                 loader.close()
                 loader = NativeLoader(plan.files, self.F, self.B, self.fmt, self.drop_remainder,
-                                      self.threads, plan.record_shard, raw=True)
+                                      self.threads, plan.record_shard, raw=True, device_crc=gd == "1")
         src = (_DeviceFeeder(loader, self.F, self.B, torch.device(self.device), self.id_dtype, ring=ring,
                              depth=8 if ring is not None else 4, id_limit=self.id_limit)
                if on_gpu else None)

@@ -518,12 +518,14 @@ def struct_array_to_device(structs: Sequence[C.Structure], device) -> torch.Tens
 
 
 # ------------------------------------------------------------------ Example decode (decode.hip)
-def decode_examples(raw, offs, rows: int, F: int, limit: int, ids, vals, labels, err):
+def decode_examples(raw, offs, rows: int, F: int, limit: int, ids, vals, labels, err, crc: bool = False):
     """Serialized tf.train.Example records (``raw`` bytes, ``offs`` rows + 1 uint32 offsets) ->
     ids int32 [rows, F], vals f32 [rows, F], labels f32 [rows] on the current stream; ``err``
-    int32 [2] = (error bits, smallest bad record index; initialise it to (0, INT32_MAX))."""
+    int32 [2] = (error bits, smallest bad record index; initialise it to (0, INT32_MAX)).
+    ``crc``: every record ends with its 4-byte masked CRC32C (a raw loader with
+    ``device_crc``), verified on the GPU (err bit value 4 on a mismatch, the row zeroed)."""
     check(L().hfm_decode_examples(ptr(raw), ptr(offs), int(rows), int(F), int(limit), ptr(ids), ptr(vals),
-                                  ptr(labels), ptr(err), stream_handle()), "decode_examples")
+                                  ptr(labels), ptr(err), 1 if crc else 0, stream_handle()), "decode_examples")
 
 
 # ------------------------------------------------------------------ RCCL engine (comm.hip)

@@ -66,9 +66,10 @@ KNOBS: Dict[str, Knob] = {
                         "bf16 + fp32 w, 24 B; fused gather tower; the FM terms then read bf16-rounded v)"),
     "HIPFM_WIRE_COMPACT": Knob("1", "variant", "streamed input: a batch ships only the value columns of "
                                "fields not all 1.0 (expanded on the device; lossless) | 0: full [B, F] values"),
-    "HIPFM_GPU_DECODE": Knob("1", "variant", "streamed TFRecord epochs: the loader only frames + CRC-checks records "
-                             "and ships their Example bytes; the GPU decodes them into the ring slot "
-                             "(csrc/kernels/decode.hip) | 0: host decode + compact wire"),
+    "HIPFM_GPU_DECODE": Knob("1", "variant", "streamed TFRecord epochs: the loader only frames records (length "
+                             "CRC) and ships their Example bytes with their data CRCs; the GPU verifies the "
+                             "CRCs and decodes into the ring slot (csrc/kernels/decode.hip) | 2: GPU decode, "
+                             "data CRCs on the host | 0: host decode + compact wire"),
     "HIPFM_ASM_RING": Knob("1", "variant", "streamed input: the loader's C++ assembler thread fills the "
                            "pinned buffers ahead of the copy-issuing thread (0: that thread assembles "
                            "each batch itself, next_into)"),

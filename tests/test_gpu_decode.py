@@ -31,7 +31,7 @@ def _rows(n, F, seed, big=False):
     return lab, ids, vals
 
 
-def _decode(raw: bytes, offs, F, limit=0):
+def _decode(raw: bytes, offs, F, limit=0, crc=False):
     rows = len(offs) - 1
     draw = torch.tensor(list(raw) or [0], dtype=torch.uint8, device=DEV)
     doffs = torch.tensor(offs, dtype=torch.int64).to(torch.int32).to(DEV)
@@ -39,13 +39,14 @@ def _decode(raw: bytes, offs, F, limit=0):
     vals = torch.full((rows, F), -7.0, device=DEV)
     lab = torch.full((rows,), -7.0, device=DEV)
     err = torch.tensor([0, 0x7FFFFFFF], dtype=torch.int32, device=DEV)
-    KN.decode_examples(draw, doffs, rows, F, limit, ids, vals, lab, err)
+    KN.decode_examples(draw, doffs, rows, F, limit, ids, vals, lab, err, crc=crc)
     torch.cuda.synchronize()
     return ids.cpu(), vals.cpu(), lab.cpu(), err.tolist()
 
 
-@pytest.mark.parametrize("F,big", [(39, True), (39, False), (100, True), (3, False)])
-def test_gpu_decode_matches_the_host_decoder(tmp_path, F, big):
+@pytest.mark.parametrize("F,big,dcrc", [(39, True, False), (39, False, False), (100, True, False), (3, False, False),
+                                         (39, True, True), (100, True, True), (3, False, True), (1, False, True)])
+def test_gpu_decode_matches_the_host_decoder(tmp_path, F, big, dcrc):
     B = 256
     files = []
     for k in range(3):
@@ -54,7 +55,9 @@ def test_gpu_decode_matches_the_host_decoder(tmp_path, F, big):
         nio.write_examples(p, lab, ids, vals)
         files.append(p)
     ref = [(a.copy(), b.copy(), c.copy()) for a, b, c in nio.NativeLoader(files, F, B, threads=2, ids32=True)]
-    ld = nio.NativeLoader(files, F, B, threads=2, raw=True)
+    # dcrc: records carry their data CRCs, verified by the decoder (short records at F = 1, 3 take
+    # its one-lane path, longer ones the 8-segment path)
+    ld = nio.NativeLoader(files, F, B, threads=2, raw=True, device_crc=dcrc)
     raw = torch.zeros(B * 2048, dtype=torch.uint8, pin_memory=True)
     offs = torch.zeros(B + 1, dtype=torch.int32, pin_memory=True)
     n = 0
@@ -62,7 +65,7 @@ def test_gpu_decode_matches_the_host_decoder(tmp_path, F, big):
         r, nb = ld.next_raw_into(raw, offs)
         if r == 0:
             break
-        ids, vals, lab, err = _decode(bytes(raw[:nb].numpy()), offs[:r + 1].tolist(), F)
+        ids, vals, lab, err = _decode(bytes(raw[:nb].numpy()), offs[:r + 1].tolist(), F, crc=dcrc)
         l2, i2, v2 = ref[n]
         assert err == [0, 0x7FFFFFFF]
         assert torch.equal(ids, torch.from_numpy(i2)) and torch.equal(vals, torch.from_numpy(v2))
@@ -103,3 +106,34 @@ def test_gpu_decode_flags_bad_records_without_faulting():
     for i in (1, 4):                                                       # zeroed rows
         assert ids[i].tolist() == [0] * F and vals[i].tolist() == [0.0] * F and lab[i].item() == 0.0
     assert ids[3].tolist() == [1, 2, 0, 4]                                 # the bad id written as 0
+
+
+@pytest.mark.parametrize("nbytes_pad", [0, 700, 9000])
+def test_gpu_decode_flags_a_corrupt_record_by_its_crc(nbytes_pad):
+    """crc mode: every record's masked CRC32C checked on the GPU (one-lane path for short records,
+    8 segments + combine up to 8 KB, one lane again beyond); a flipped payload byte or a wrong
+    stored CRC zeroes that row only and reports bit value 4 with the smallest bad index."""
+    F = 39
+    lab, ids, vals = _rows(12, F, 77)
+    recs = []
+    for i in range(12):
+        ex = tr.encode_example(float(lab[i]), [int(x) for x in ids[i]], [float(v) for v in vals[i]])
+        if nbytes_pad:      # an unknown top-level field (bytes) pads the record: skipped by the parser
+            ex = ex + tr._key(9, 2) + tr._varint(nbytes_pad) + bytes(range(256)) * (nbytes_pad // 256) + \
+                bytes(nbytes_pad % 256)
+        recs.append(bytearray(ex + struct.pack("<I", tr.masked_crc32c(ex))))
+    good = b"".join(bytes(r) for r in recs)
+    offs = [0]
+    for r in recs:
+        offs.append(offs[-1] + len(r))
+    i0, v0, l0, e0 = _decode(good, offs, F, crc=True)
+    assert e0 == [0, 0x7FFFFFFF]
+    assert torch.equal(i0, torch.from_numpy(ids.astype(np.int32))) and torch.equal(l0, torch.from_numpy(lab))
+    recs[5][len(recs[5]) // 2] ^= 0x10          # payload byte of record 5
+    recs[9][-1] ^= 0x01                          # stored CRC of record 9
+    i1, v1, l1, e1 = _decode(b"".join(bytes(r) for r in recs), offs, F, crc=True)
+    assert e1 == [4, 5]
+    for k in (5, 9):
+        assert not i1[k].any() and not v1[k].any() and l1[k] == 0
+    keep = [k for k in range(12) if k not in (5, 9)]
+    assert torch.equal(i1[keep], i0[keep]) and torch.equal(v1[keep], v0[keep])

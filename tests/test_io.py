@@ -362,6 +362,59 @@ def test_raw_loader_ships_the_records_of_the_decoding_loader(tmp_path, threads, 
         assert np.array_equal(l1, l2) and np.array_equal(i1, i2) and np.array_equal(v1, v2)
 
 
+@pytest.mark.parametrize("threads", [1, 3])
+def test_raw_loader_device_crc_ships_each_records_data_crc(tmp_path, threads):
+    """device_crc (verify mode 2): the workers check only the length CRCs and append each record's
+    stored masked data CRC to its bytes (the GPU decoder verifies it); a corrupted payload byte
+    reaches the batch unflagged by the host -- with the stored CRC that exposes it."""
+    F, B = 6, 64
+    files = []
+    for k in range(2):
+        lab, ids, vals = _rows(150 + 9 * k, F, 50 + k)
+        p = str(tmp_path / f"tr-{k}.tfrecords")
+        nio.write_examples(p, lab, ids, vals)
+        files.append(p)
+    plain = nio.NativeLoader(files, F, B, threads=threads, raw=True)
+    dev = nio.NativeLoader(files, F, B, threads=threads, raw=True, device_crc=True)
+    assert dev.device_crc and not plain.device_crc
+    bufs = [(torch.zeros(B * 1024, dtype=torch.uint8), torch.zeros(B + 1, dtype=torch.int32)) for _ in range(2)]
+    nb_all = 0
+    while True:
+        r1, n1 = plain.next_raw_into(*bufs[0])
+        r2, n2 = dev.next_raw_into(*bufs[1])
+        assert r1 == r2
+        if r1 == 0:
+            break
+        assert n2 == n1 + 4 * r1
+        o1, o2 = bufs[0][1].numpy().astype(np.int64), bufs[1][1].numpy().astype(np.int64)
+        for i in range(r1):
+            rec = bufs[0][0].numpy()[o1[i]:o1[i + 1]].tobytes()
+            got = bufs[1][0].numpy()[o2[i]:o2[i + 1]].tobytes()
+            assert got[:-4] == rec
+            assert int.from_bytes(got[-4:], "little") == nio.masked_crc32c(rec)
+        nb_all += r1
+    plain.close()
+    dev.close()
+    assert nb_all > 0
+    # one payload byte flipped in the first record: the host-CRC loader refuses the file, the
+    # device-CRC loader ships it (with the stored CRC, which no longer matches)
+    raw = bytearray(open(files[0], "rb").read())
+    raw[12 + 5] ^= 0x40
+    bad = str(tmp_path / "bad.tfrecords")
+    open(bad, "wb").write(bytes(raw))
+    ld = nio.NativeLoader([bad], F, B, threads=1, raw=True)
+    with pytest.raises(IOError, match="data CRC"):
+        ld.next_raw_into(*bufs[0])
+    ld.close()
+    ld = nio.NativeLoader([bad], F, B, threads=1, raw=True, device_crc=True)
+    r, nb = ld.next_raw_into(*bufs[1])
+    assert r == B
+    o = bufs[1][1].numpy().astype(np.int64)
+    first = bufs[1][0].numpy()[o[0]:o[1]].tobytes()
+    assert int.from_bytes(first[-4:], "little") != nio.masked_crc32c(first[:-4])
+    ld.close()
+
+
 def test_raw_loader_reports_a_batch_larger_than_its_buffer(tmp_path):
     F = 6
     lab, ids, vals = _rows(300, F, 3)
