@@ -416,6 +416,15 @@ __global__ void __launch_bounds__(PP_THREADS, 1) gemm_pp_kernel(
   }
   if (grp == 0) __builtin_amdgcn_s_barrier();   // (every wave passes the same number of barriers)
 
+#ifdef HFM_PP_NOEPI   // (diagnostic build: epilogue replaced by one store per lane -- timing only)
+  float sum = 0.f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) sum += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
+  if (sum == 1.2345e-30f) reinterpret_cast<float*>(ep.out)[threadIdx.x] = sum;
+  return;
+#endif
   uint32_t salt = 0;
   if (EPI == EPI_FWD && ep.drop) salt = dropout_salt(ep.seed, (uint32_t)(*ep.step), ep.layer);
   const int cr = fq * 4;
@@ -714,6 +723,160 @@ static int launch_gemm_p8(const bf16* A, int lda, const bf16* B, int ldb, int M,
   HFM_LAUNCH_CHECK();
 }
 
+// ------------------------------------------------------------------ register-blocked K-half ring (tile 13)
+// The shape of hipBLASLt's kernel on these GEMMs (profiles/r6_gemm_pmc_raw.md: 4 waves per 256 x 256
+// workgroup, one wave per SIMD, half the LDS reads per MFMA of the 8-wave tiles): each wave owns a
+// 128 x 128 block (acc[8][8], 256 accumulation registers), fed from tile 12's ring of four 32-deep
+// K-half buffers.  Per K-half and wave: 64 MFMAs on fragments read during the PREVIOUS K-half
+// (two register sets), the 8 staging DMAs of K-half h + 3 issued after the first 8 MFMAs, the 16
+// fragment reads of K-half h + 1 spread over the rest; one lgkmcnt(0) + counted vmcnt(8) (K-half
+// h + 2 retired, h + 3 in flight) + barrier per K-half.  Order pinned by sched_barrier.
+//   WAR: buffer (h + 3) & 3 = (h - 1) & 3 was last read during K-half h - 2, retired by the
+//   lgkmcnt(0) before the barrier that ends h - 2.  RAW: K-half h + 1 (read during h) was retired
+//   by every wave's vmcnt before the barrier that ends h - 1.
+template <int EPI>
+__global__ void __launch_bounds__(RB_THREADS) __attribute__((amdgpu_waves_per_eu(1, 1))) gemm_r8_kernel(
+    const bf16* __restrict__ A, int lda, const bf16* __restrict__ Bm, int ldb, int M, int N,
+    int kchunk, EpiArgs ep) {
+  __shared__ __attribute__((aligned(16))) char smem[4 * P8_BUF];   // (the only __shared__ object)
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int wr = wave >> 1, wcn = wave & 1;
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, rr = nwg & 7;
+  const int tid = (xcd < rr ? xcd * (q8 + 1) : rr * (q8 + 1) + (xcd - rr) * q8) + (bid >> 3);
+  const int tiles_n = N / PP_BM;
+  const int m0 = (tid / tiles_n) * PP_BM, n0 = (tid % tiles_n) * PP_BM;
+  const int kb = blockIdx.z * kchunk;
+  const int nkh = kchunk / P8_KH;
+  const int fr = lane & 15, fq = lane >> 4;
+  // this wave's 8 pieces per K-half: A pieces 4w..4w+3 (p 0-3), B pieces 4w..4w+3 (p 4-7)
+  int soff[8], doff[8];
+#pragma unroll
+  for (int p = 0; p < 8; ++p) {
+    const int piece = wave * 4 + (p & 3);
+    const int r = piece * 16 + (lane >> 2);
+    const int c = (lane & 3) ^ ((r >> 2) & 3);
+    soff[p] = p < 4 ? (m0 + r) * lda + c * 8 : (n0 + r) * ldb + c * 8;
+    doff[p] = (p < 4 ? 0 : P8_OP) + piece * 1024;
+  }
+  auto stage = [&](int h, int p) {
+    __builtin_amdgcn_global_load_lds(
+        (const __attribute__((address_space(1))) void*)((p < 4 ? A : Bm) + soff[p] + kb + h * P8_KH),
+        (__attribute__((address_space(3))) void*)(smem + (h & 3) * P8_BUF + doff[p]), 16, 0, 0);
+  };
+  const int cs = (fq ^ ((fr >> 2) & 3)) << 4;
+  const int la = (wr * 128 + fr) * 64 + cs;
+  const int lb = P8_OP + (wcn * 128 + fr) * 64 + cs;
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // prologue: K-halves 0, 1, 2 in flight; 0 retired and its fragments read
+#pragma unroll
+  for (int h = 0; h < 3; ++h)
+#pragma unroll
+    for (int p = 0; p < 8; ++p) stage(h, p);
+  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  bf16x8 fa[8], fb[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    fb[i] = *reinterpret_cast<const bf16x8*>(smem + lb + i * 1024);
+    fa[i] = *reinterpret_cast<const bf16x8*>(smem + la + i * 1024);
+  }
+  // (K-half 1 retired before the first K-half reads it)
+  asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+
+  // one register set, snake order: even K-halves run rows outer (fa[i] is free after row i and is
+  // reloaded at once; fb[j] after MFMA (7, j)), odd K-halves columns outer (the mirror) -- the
+  // next K-half's first MFMAs find their fragments read 7+ MFMAs earlier.  Staging past the last
+  // K-half re-stages the last one into the idle buffer (no branch; drained after the loop).
+  // fragment register freed by MFMA n of a K-half (snake order P), reloaded from the next K-half
+  auto reload = [&](int n, auto Pc, const char* nb) {
+    constexpr int P = decltype(Pc)::value;
+    const int o = n >> 3, q = n & 7;
+    const int i = P == 0 ? o : q, j = P == 0 ? q : o;
+    if (P == 0) {
+      if (q == 7) fa[i] = *reinterpret_cast<const bf16x8*>(nb + la + i * 1024);
+      if (o == 7) fb[j] = *reinterpret_cast<const bf16x8*>(nb + lb + j * 1024);
+    } else {
+      if (q == 7) fb[j] = *reinterpret_cast<const bf16x8*>(nb + lb + j * 1024);
+      if (o == 7) fa[i] = *reinterpret_cast<const bf16x8*>(nb + la + i * 1024);
+    }
+  };
+  auto khalf = [&](int h, auto Pc) {
+    constexpr int P = decltype(Pc)::value;     // 0: rows outer, 1: columns outer
+    const int hs = h + 3 < nkh ? h + 3 : nkh - 1;
+    const char* nb = smem + ((h + 1) & 3) * P8_BUF;
+#pragma unroll
+    for (int n = 0; n < 64; ++n) {
+      const int o = n >> 3, q = n & 7;          // outer / inner index
+      const int i = P == 0 ? o : q, j = P == 0 ? q : o;
+      // (inline asm pins the accumulator in the AGPR file: with the builtin the register allocator
+      // kept part of acc in VGPRs and copied it into AGPRs around every MFMA -- 500 v_accvgpr
+      // moves + nops per K-tile; independent accumulators, so no MFMA hazard for the asm to hide)
+      asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(fa[i]), "v"(fb[j]));
+      __builtin_amdgcn_sched_barrier(0);
+#ifndef HFM_R8_NODMA
+      if (n >= 4 && n < 12) stage(hs, n - 4);
+#endif
+#ifndef HFM_R8_NOLDS
+      // the fragment freed by the PREVIOUS MFMA (one MFMA between an MFMA and the overwrite of a
+      // register it reads); freed: rows outer -> fa[i] at the row's end, fb[j] in the last row
+      if (n > 0) reload(n - 1, Pc, nb);
+#endif
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#ifndef HFM_R8_NOLDS
+    reload(63, Pc, nb);
+#endif
+    __builtin_amdgcn_sched_barrier(0);
+#ifndef HFM_R8_NOBAR
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // K-half h + 2 retired (h + 3 in flight)
+    __builtin_amdgcn_s_barrier();
+#endif
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  for (int h = 0; h < nkh; h += 2) {
+    khalf(h, I0{});
+    khalf(h + 1, I1{});
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // (no DMA may land after the workgroup ends)
+  // the last MFMAs' results are read by the epilogue's compiler code: the asm MFMAs are not padded
+  // by hipcc (an 8-pass XDL result needs 12 wait states before another reader)
+  asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+
+  uint32_t salt = 0;
+  if (EPI == EPI_FWD && ep.drop) salt = dropout_salt(ep.seed, (uint32_t)(*ep.step), ep.layer);
+  const int cr = fq * 4;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      epi_store<EPI>(ep, acc[i][j], m0 + wr * 128 + i * 16 + cr, n0 + wcn * 128 + j * 16 + fr, M, N, salt);
+}
+
+template <int EPI>
+static int launch_gemm_r8(const bf16* A, int lda, const bf16* B, int ldb, int M, int N, int Kd,
+                          int splitk, const EpiArgs& ep, hipStream_t st) {
+  // (an even number of K-halves per split, at least 4)
+  if (M % PP_BM || N % PP_BM || splitk < 1 || Kd % (2 * P8_KH * splitk) || Kd / splitk < 4 * P8_KH || lda % 8 ||
+      ldb % 8 || ((uintptr_t)A & 15) || ((uintptr_t)B & 15))
+    return (int)hipErrorInvalidValue;
+  dim3 grid((M / PP_BM) * (N / PP_BM), 1, splitk);
+  hipLaunchKernelGGL((gemm_r8_kernel<EPI>), grid, dim3(RB_THREADS), 0, st, A, lda, B, ldb, M, N,
+                     Kd / splitk, ep);
+  HFM_LAUNCH_CHECK();
+}
+
 template <int EPI>
 static int launch_gemm_rb(const bf16* A, int lda, const bf16* B, int ldb, int M, int N, int Kd,
                           int splitk, const EpiArgs& ep, hipStream_t st) {
@@ -753,7 +916,8 @@ static int launch_gemm_lds(const bf16* A, int lda, const bf16* B, int ldb, int M
 // tile: 0 = 64x64 (2x2 waves), 1 = 128x32 (4x1), 2 = 32x128 (1x4), 3 = 32x32 (1x1), 4 = 32x64 (1x2),
 //       5 = 32x160 (1x5), 6 = 32x320 (1x10), 7 = 32x256 (1x8), 8 = 128x128 LDS-staged (wide layers),
 //       9 = 256x256 ping-pong (wide layers, 8 waves), 10 = same, staging spread, 11 = 256x256
-//       register-blocked (4 waves), 12 = 256x256 K-half ring (8 waves, counted DMA waits)
+//       register-blocked (4 waves), 12 = 256x256 K-half ring (8 waves, counted DMA waits),
+//       13 = 256x256 register-blocked on the K-half ring (4 waves)
 template <int EPI>
 static int gemm_tile(int tile, const bf16* A, int lda, const bf16* B, int ldb, int M, int N, int Kd,
                      int splitk, const EpiArgs& ep, hipStream_t st) {
@@ -771,6 +935,7 @@ static int gemm_tile(int tile, const bf16* A, int lda, const bf16* B, int ldb, i
     case 10: return launch_gemm_pp<EPI, 1>(A, lda, B, ldb, M, N, Kd, splitk, ep, st);
     case 11: return launch_gemm_rb<EPI>(A, lda, B, ldb, M, N, Kd, splitk, ep, st);
     case 12: return launch_gemm_p8<EPI>(A, lda, B, ldb, M, N, Kd, splitk, ep, st);
+    case 13: return launch_gemm_r8<EPI>(A, lda, B, ldb, M, N, Kd, splitk, ep, st);
     default: return (int)hipErrorInvalidValue;
   }
 }

@@ -21,7 +21,7 @@ OPT_IDS = {"Adam": 0, "Adagrad": 1, "Momentum": 2, "ftrl": 3, "GD": 4}
 # tile ids of hfm_gemm_nt: (rows per block, cols per block)
 TILES = {0: (64, 64), 1: (128, 32), 2: (32, 128), 3: (32, 32), 4: (32, 64), 5: (32, 160),
          6: (32, 320), 7: (32, 256), 8: (128, 128), 9: (256, 256), 10: (256, 256), 11: (256, 256),
-         12: (256, 256)}
+         12: (256, 256), 13: (256, 256)}
 TILE_LDS = 8          # 128 x 128 LDS-staged workgroup tile (mlp.hip gemm_lds_kernel): k-chunks of 64
 TILE_PP = 10          # 256 x 256 ping-pong tile, spread LDS-DMA staging (mlp.hip gemm_pp_kernel<., 1>)
 

@@ -37,7 +37,10 @@ def _ref(A, B):
                                               (11, 768, 256, 2048, 4), (11, 1024, 1024, 1024, 2),
                                               (12, 256, 256, 128, 1), (12, 512, 768, 320, 1), (12, 512, 512, 4096, 1),
                                               (12, 768, 256, 2048, 4), (12, 1024, 1024, 1024, 2),
-                                              (12, 2048, 1024, 8192, 1)])
+                                              (12, 2048, 1024, 8192, 1),
+                                              (13, 256, 256, 128, 1), (13, 512, 768, 320, 1), (13, 512, 512, 4096, 1),
+                                              (13, 768, 256, 2048, 4), (13, 1024, 1024, 1024, 2),
+                                              (13, 2048, 1024, 8192, 1)])
 def test_lds_gemm_f32_matches_reference(tile, M, N, K, split):
     A, B = _ops(M, N, K, seed=M + N + K)
     out = torch.full((split, M, N), float("nan"), device=DEV)
@@ -57,7 +60,7 @@ def test_lds_gemm_f32_matches_reference(tile, M, N, K, split):
     assert torch.equal(out, o2)
 
 
-@pytest.mark.parametrize("tile", [8, 9, 10, 11, 12])
+@pytest.mark.parametrize("tile", [8, 9, 10, 11, 12, 13])
 @pytest.mark.parametrize("epi", ["fwd", "fwd_eval", "dgrad", "relu_f32"])
 def test_lds_gemm_epilogues_match_register_tile(tile, epi):
     M, N, K = 512, 256, 640
