@@ -427,12 +427,115 @@ __global__ void __launch_bounds__(PP_THREADS, 1) gemm_pp_kernel(
 #endif
   uint32_t salt = 0;
   if (EPI == EPI_FWD && ep.drop) salt = dropout_salt(ep.seed, (uint32_t)(*ep.step), ep.layer);
-  const int cr = fq * 4;
+  __syncthreads();                      // (every wave past its last K-tile read: the images reuse it)
+  epi_tile_lds<EPI, 8, 4>(ep, acc, smem + wave * 16384, lane, m0 + grp * 128, n0 + wc * 64, M, N, salt);
+}
+
+// ------------------------------------------------------------------ LDS-staged wave epilogue
+// A wave's MI x NJ accumulator tiles (rows row0 + 16 i + 4 fq + k, cols col0 + 16 j + fr) leave
+// through a wave-private 16 KB LDS image, so every global access is a 16-byte row chunk: the output
+// rows (bf16 H / dZ, or the f32 C slab), and the dgrad mask's hprev rows.  The per-element
+// epilogue (epi_store) wrote 2- or 4-byte scattered stores and read hprev 2 bytes at a time: with
+// it the 256x256 tiles spent 19-41 % of a 16384x4096x4096 GEMM there (timing build without it:
+// profiles/r6_gemm_epilogue_ablation.log).  Same values, bit for bit: bias / relu / dropout in
+// registers as before; the dgrad mask is applied to the bf16-rounded value (rounding and a mask to
+// +0 commute).  out_t keeps its 8-byte column stores (masked values re-read from the image).
+// Image: rows of NJ * 16 elements, 16-byte chunk c of row r at chunk c ^ (r mod chunks-per-row).
+// Caller: every wave of the workgroup is past its last LDS read of the main loop.
+template <int EPI, int MI, int NJ>
+__device__ __forceinline__ void epi_tile_lds(const EpiArgs& ep, const f32x4 (&acc)[MI][NJ], char* img, int lane,
+                                             int row0, int col0, int M, int N, uint32_t salt) {
+  constexpr bool F32 = EPI == EPI_F32 || EPI == EPI_RELU_F32;
+  constexpr int ES = F32 ? 4 : 2;
+  constexpr int RB = NJ * 16 * ES;           // image row bytes
+  constexpr int CPR = RB / 16;               // 16-byte chunks per row
+  constexpr int ROWS = 16384 / RB;           // rows per pass
+  constexpr int MIP = ROWS / 16;             // m-tiles per pass
+  static_assert(MI % MIP == 0 && (CPR & (CPR - 1)) == 0, "image geometry");
+  const int fr = lane & 15, fq = lane >> 4;
+  const bool mask = EPI == EPI_DGRAD && ep.hprev != nullptr;
+  auto wsync = [] {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  };
+  auto eoff = [](int r, int cb) { return r * RB + ((((cb >> 4) ^ (r & (CPR - 1)))) << 4) + (cb & 15); };
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int p = 0; p < MI / MIP; ++p) {
+    // 1. registers -> image (and out_t straight from the registers when no mask applies)
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-      epi_store<EPI>(ep, acc[i][j], m0 + grp * 128 + i * 16 + cr, n0 + wc * 64 + j * 16 + fr, M, N, salt);
+    for (int ii = 0; ii < MIP; ++ii) {
+      const int i = p * MIP + ii;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int c = j * 16 + fr, col = col0 + c;
+        bf16x4 tv;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int ri = ii * 16 + fq * 4 + k, row = row0 + i * 16 + fq * 4 + k;
+          float v = acc[i][j][k];
+          if (EPI == EPI_FWD || EPI == EPI_FWD_EVAL) {
+            v = fmaxf(v + ep.bias[col], 0.f);
+            if (EPI == EPI_FWD && ep.drop)
+              v = dropout_keep((uint32_t)(row * N + col), salt, ep.keep_thr) ? v * ep.scale : 0.f;
+          } else if (EPI == EPI_DGRAD) {
+            v = v * ep.scale;
+          } else if (EPI == EPI_RELU_F32) {
+            v = fmaxf(v + ep.bias[col], 0.f);
+          }
+          if (F32) {
+            *reinterpret_cast<float*>(img + eoff(ri, c * 4)) = v;
+          } else {
+            const bf16 hv = f2bf(v);
+            *reinterpret_cast<bf16*>(img + eoff(ri, c * 2)) = hv;
+            tv[k] = hv;
+          }
+        }
+        if (!F32 && !mask && ep.out_t)
+          *reinterpret_cast<bf16x4*>(ep.out_t + (size_t)col * M + row0 + i * 16 + fq * 4) = tv;
+      }
+    }
+    wsync();
+    // 2. image rows -> global rows, 16 bytes per lane (dgrad: hprev rows masked in, written back)
+    const int rbase = row0 + p * ROWS;
+#pragma unroll 4
+    for (int e = lane; e < ROWS * CPR; e += 64) {
+      const int r = e / CPR, q = e % CPR;
+      char* ip = img + r * RB + ((q ^ (r & (CPR - 1))) << 4);
+      uint4 v = *reinterpret_cast<const uint4*>(ip);
+      const size_t g = (size_t)(rbase + r) * N + col0 + q * (16 / ES);
+      if (F32) {
+        *reinterpret_cast<uint4*>(reinterpret_cast<float*>(ep.out) + (size_t)blockIdx.z * M * N + g) = v;
+      } else {
+        if (mask) {
+          const uint4 h = *reinterpret_cast<const uint4*>(ep.hprev + g);
+          uint32_t* vw = reinterpret_cast<uint32_t*>(&v);
+          const uint32_t* hw = reinterpret_cast<const uint32_t*>(&h);
+#pragma unroll
+          for (int w = 0; w < 4; ++w) {
+            const bool lo = __uint_as_float(hw[w] << 16) > 0.f, hi = __uint_as_float(hw[w] & 0xFFFF0000u) > 0.f;
+            vw[w] &= (lo ? 0x0000FFFFu : 0u) | (hi ? 0xFFFF0000u : 0u);
+          }
+          if (ep.out_t) *reinterpret_cast<uint4*>(ip) = v;
+        }
+        *reinterpret_cast<uint4*>(reinterpret_cast<bf16*>(ep.out) + g) = v;
+      }
+    }
+    if (!F32 && mask && ep.out_t) {    // out_t of the masked values: the lane's own 4-row columns
+      wsync();
+#pragma unroll
+      for (int ii = 0; ii < MIP; ++ii)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const int c = j * 16 + fr;
+          bf16x4 tv;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) tv[k] = *reinterpret_cast<const bf16*>(img + eoff(ii * 16 + fq * 4 + k, c * 2));
+          *reinterpret_cast<bf16x4*>(ep.out_t + (size_t)(col0 + c) * M + rbase + ii * 16 + fq * 4) = tv;
+        }
+    }
+    wsync();                           // (the next pass overwrites the image)
+  }
 }
 
 // ------------------------------------------------------------------ register-blocked GEMM (tile 11)
@@ -701,12 +804,8 @@ __global__ void __launch_bounds__(PP_THREADS, 1) gemm_p8_kernel(
 
   uint32_t salt = 0;
   if (EPI == EPI_FWD && ep.drop) salt = dropout_salt(ep.seed, (uint32_t)(*ep.step), ep.layer);
-  const int cr = fq * 4;
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-      epi_store<EPI>(ep, acc[i][j], m0 + grp * 128 + i * 16 + cr, n0 + wc * 64 + j * 16 + fr, M, N, salt);
+  __syncthreads();                      // (every wave past its last K-tile read: the images reuse it)
+  epi_tile_lds<EPI, 8, 4>(ep, acc, smem + wave * 16384, lane, m0 + grp * 128, n0 + wc * 64, M, N, salt);
 }
 
 template <int EPI>
