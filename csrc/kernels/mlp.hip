@@ -1270,9 +1270,164 @@ __global__ void __launch_bounds__(256) head_wide_kernel(HeadArgs a) {
   }
 }
 
+// Wide head (L % 256 == 0, L > 256) in two launches with 16-byte accesses throughout; the
+// one-launch head_wide_kernel read H one bf16 per lane per row in a 256-workgroup grid and took
+// ~0.9 ms of a 6.5 ms step at L = 4096 (profiles/r6tw_kernels.md).
+// dot: one wave per 16 rows of a 64-row block, 4 rows' chunks in flight: y, p, loss, dlogit, and
+//      the block's dlogit / loss sums (partial columns L, L + 1, rows in order).
+// bwd: workgroup = 64 rows x 256 columns; thread = 8 rows x 8 columns (rows 8 rg.., chunk cc):
+//      dz / dh rows as 16-byte chunks, dz_t as 8-row 16-byte column chunks, and the block's
+//      column sums of dlogit * h (rows in order per thread, the 8 row groups in order).
+__global__ void __launch_bounds__(256) head_wide_dot_kernel(HeadArgs a) {
+  __shared__ float hw_dl[64], hw_loss[64];
+  const int L = a.L;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int bb = blockIdx.x * 64;
+  const int nch = L / 8;                      // 16-byte chunks per row
+  for (int s0 = 0; s0 < 16; s0 += 4) {
+    float yd[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int ch = lane; ch < nch; ch += 64) {
+      const f32x4 w0 = *reinterpret_cast<const f32x4*>(a.w_out + ch * 8);
+      const f32x4 w1 = *reinterpret_cast<const f32x4*>(a.w_out + ch * 8 + 4);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int b = bb + wv * 16 + s0 + u;
+        if (b < a.M) {
+          const bf16x8 h = *reinterpret_cast<const bf16x8*>(a.h + (size_t)b * L + ch * 8);
+          float d = 0.f;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) d += bf2f(h[k]) * w0[k];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) d += bf2f(h[4 + k]) * w1[k];
+          yd[u] += d;
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) yd[u] += __shfl_xor(yd[u], o, 64);
+      const int s = s0 + u, b = bb + wv * 16 + s;
+      float dl = 0.f, lossb = 0.f;
+      if (b < a.M) {
+        const float y = a.y_fm[b] + yd[u] + a.b_out[0];
+        const float p = 1.f / (1.f + __expf(-y));
+        if (lane == 0) {
+          a.prob[b] = p;
+          if (a.logit) a.logit[b] = y;
+        }
+        if (a.labels && b < a.nvalid) {
+          const float lab = a.labels[b];
+          if (a.square_loss) {
+            lossb = (p - lab) * (p - lab);
+            dl = 2.f * (p - lab) * p * (1.f - p) * a.gscale;
+          } else {
+            lossb = fmaxf(y, 0.f) - y * lab + log1pf(__expf(-fabsf(y)));
+            dl = (p - lab) * a.gscale;
+          }
+        }
+        if (a.train && lane == 0) a.dlogit[b] = dl;
+      }
+      if (lane == 0) {
+        hw_dl[wv * 16 + s] = dl;
+        hw_loss[wv * 16 + s] = lossb;
+      }
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float d = 0.f, l = 0.f;
+    for (int s = 0; s < 64; ++s) {
+      d += hw_dl[s];
+      l += hw_loss[s];
+    }
+    float* part = a.partial + (size_t)blockIdx.x * (L + 2);
+    part[L] = d;
+    part[L + 1] = l;
+  }
+}
+
+__global__ void __launch_bounds__(256) head_wide_bwd_kernel(HeadArgs a) {
+  __shared__ float red[8][257];
+  const int L = a.L, tid = threadIdx.x;
+  const int cc = tid & 31, rg = tid >> 5;
+  const int bb = blockIdx.x * 64, c0 = blockIdx.y * 256 + cc * 8;
+  float* part = a.partial + (size_t)blockIdx.x * (L + 2) + blockIdx.y * 256;
+  if (!a.train) {                       // (predict / eval: no gradients, zero partial columns)
+    part[tid] = 0.f;
+    return;
+  }
+  float w[8];
+  {
+    const f32x4 w0 = *reinterpret_cast<const f32x4*>(a.w_out + c0);
+    const f32x4 w1 = *reinterpret_cast<const f32x4*>(a.w_out + c0 + 4);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      w[k] = w0[k];
+      w[4 + k] = w1[k];
+    }
+  }
+  float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  bf16 zt[8][8];                        // [column][row] for the dz_t chunks
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    const int b = bb + rg * 8 + r;
+    const bool in = b < a.M;
+    const float dl = in ? a.dlogit[b] : 0.f;
+    bf16x8 h;
+    if (in) h = *reinterpret_cast<const bf16x8*>(a.h + (size_t)b * L + c0);
+    bf16x8 z;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float hv = in ? bf2f(h[k]) : 0.f;
+      cs[k] += dl * hv;
+      const float v = hv > 0.f ? dl * w[k] * a.scale_l : 0.f;
+      z[k] = f2bf(v);
+      zt[k][r] = z[k];
+    }
+    if (in) {
+      if (a.dh) {
+        float* dh = a.dh + (size_t)b * L + c0;
+        *reinterpret_cast<f32x4*>(dh) = f32x4{dl * w[0], dl * w[1], dl * w[2], dl * w[3]};
+        *reinterpret_cast<f32x4*>(dh + 4) = f32x4{dl * w[4], dl * w[5], dl * w[6], dl * w[7]};
+      } else {
+        *reinterpret_cast<bf16x8*>(a.dz + (size_t)b * L + c0) = z;
+      }
+    }
+  }
+  if (!a.dh) {
+    const int r0 = bb + rg * 8;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      bf16x8 col;
+#pragma unroll
+      for (int r = 0; r < 8; ++r) col[r] = zt[k][r];
+      if ((a.M & 7) == 0 && r0 + 8 <= a.M) {
+        *reinterpret_cast<bf16x8*>(a.dz_t + (size_t)(c0 + k) * a.M + r0) = col;
+      } else {
+#pragma unroll
+        for (int r = 0; r < 8; ++r)
+          if (r0 + r < a.M) a.dz_t[(size_t)(c0 + k) * a.M + r0 + r] = col[r];
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) red[rg][cc * 8 + k] = cs[k];
+  __syncthreads();
+  float t = 0.f;
+#pragma unroll
+  for (int g = 0; g < 8; ++g) t += red[g][tid];
+  part[tid] = t;
+}
+
 HFM_API int hfm_head(const HeadArgs* a, hipStream_t st) {
   const int grid = (a->M + 63) / 64;
   if (a->L > 256) {
+    if (a->L % 256 == 0) {
+      hipLaunchKernelGGL(head_wide_dot_kernel, dim3(grid), dim3(256), 0, st, *a);
+      hipLaunchKernelGGL(head_wide_bwd_kernel, dim3(grid, a->L / 256), dim3(256), 0, st, *a);
+      HFM_LAUNCH_CHECK();
+    }
     if (a->L % 64) return (int)hipErrorInvalidValue;
     hipLaunchKernelGGL(head_wide_kernel, dim3(grid), dim3(256), 0, st, *a);
     HFM_LAUNCH_CHECK();

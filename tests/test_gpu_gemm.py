@@ -131,3 +131,58 @@ def test_wide_tower_step_matches_register_tiles(monkeypatch, bn):
     (p8, v8), (p0, v0) = outs
     assert (p8 - p0).abs().max().item() <= 1e-4 * p0.abs().max().item()
     assert (v8 - v0).abs().max().item() <= 1e-4 * v0.abs().max().item()
+
+
+@pytest.mark.parametrize("L,M,nvalid,train,dh", [(4096, 1024, 1000, True, False), (512, 200, 200, True, False),
+                                                 (768, 256, 256, True, True), (1024, 128, 128, False, False),
+                                                 (320, 192, 190, True, False)])
+def test_wide_head_matches_fp32_reference(L, M, nvalid, train, dh):
+    """hfm_head for a last layer > 256 units (head_wide_dot / head_wide_bwd at L % 256 == 0, the
+    one-launch head_wide_kernel otherwise) against a plain fp32 PyTorch head: probabilities, loss,
+    dlogit, dZ = [h > 0] dlogit w / keep (bf16) and its transpose, or the batch-norm dh, and the
+    per-64-row partial sums (deep_out weight gradient, dlogit and loss sums)."""
+    from hipfm.ops._lib import HeadArgs
+    g = torch.Generator(device=DEV).manual_seed(L + M)
+    h = torch.relu(torch.randn(M, L, generator=g, device=DEV) - 0.3).bfloat16()
+    w = torch.randn(L, generator=g, device=DEV) * 0.05
+    b = torch.tensor([0.1], device=DEV)
+    yfm = torch.randn(M, generator=g, device=DEV) * 0.3
+    lab = (torch.rand(M, generator=g, device=DEV) < 0.4).float()
+    nb = (M + 63) // 64
+    prob, logit, dlog = (torch.full((M,), -9.0, device=DEV) for _ in range(3))
+    dz = torch.zeros(M, L, device=DEV).bfloat16()
+    dzt = torch.zeros(L, M, device=DEV).bfloat16()
+    dhb = torch.zeros(M, L, device=DEV) if dh else None
+    part = torch.full((nb, L + 2), -9.0, device=DEV)
+    a = HeadArgs()
+    a.h, a.w_out, a.b_out, a.y_fm, a.labels = h.data_ptr(), w.data_ptr(), b.data_ptr(), yfm.data_ptr(), lab.data_ptr()
+    a.M, a.L, a.nvalid, a.square_loss, a.train = M, L, nvalid, 0, int(train)
+    a.gscale, a.scale_l = 1.0 / nvalid, 2.0
+    a.prob, a.logit, a.dlogit, a.dz, a.dz_t, a.partial = (prob.data_ptr(), logit.data_ptr(), dlog.data_ptr(),
+                                                          dz.data_ptr(), dzt.data_ptr(), part.data_ptr())
+    a.dh = dhb.data_ptr() if dh else 0
+    KN.head(a)
+    torch.cuda.synchronize()
+    hf = h.float()
+    y = yfm + hf @ w + b
+    p = torch.sigmoid(y)
+    valid = torch.arange(M, device=DEV) < nvalid
+    dl = torch.where(valid, (p - lab) / nvalid, torch.zeros_like(p))
+    loss = torch.where(valid, torch.relu(y) - y * lab + torch.log1p(torch.exp(-y.abs())), torch.zeros_like(p))
+    assert torch.allclose(prob, p, atol=1e-5) and torch.allclose(logit, y, atol=1e-4)
+    pad = nb * 64 - M
+    blk = lambda t: torch.nn.functional.pad(t, (0, pad)).view(nb, 64)   # noqa: E731
+    assert torch.allclose(part[:, L + 1], blk(loss).sum(1), rtol=1e-4, atol=1e-5)
+    if not train:
+        assert (part[:, :L] == 0).all()
+        return
+    assert torch.allclose(dlog, dl, atol=1e-7)
+    assert torch.allclose(part[:, L], blk(dl).sum(1), rtol=1e-4, atol=1e-7)
+    ref_part = torch.nn.functional.pad(dl[:, None] * hf, (0, 0, 0, pad)).view(nb, 64, L).sum(1)
+    assert torch.allclose(part[:, :L], ref_part, rtol=1e-3, atol=1e-6)
+    if dh:
+        assert torch.allclose(dhb, dlog[:, None] * w[None, :], rtol=1e-6, atol=1e-9)
+    else:
+        # dZ from the kernel's own dlogit: bf16 rounding of the same fp32 product
+        ref = torch.where(hf > 0, dlog[:, None] * w[None, :] * 2.0, torch.zeros_like(hf)).bfloat16()
+        assert torch.equal(dz, ref) and torch.equal(dzt, ref.t().contiguous())
