@@ -237,7 +237,10 @@ __device__ __forceinline__ void dense_opt_apply(float* __restrict__ p, float gi,
     if (rel >= 0 && rel < sz) {
       const int r = (int)(rel / segs[s].cols), cc = (int)(rel % segs[s].cols);
       segs[s].w16[rel] = f2bf(pi);
-      segs[s].wt16[(long)cc * segs[s].rows + r] = f2bf(pi);
+      // (wt16 null: a large segment whose transposed shadow a tiled pass writes afterwards --
+      // optim.hip shadow_transpose; one scattered 2-byte store per element cost 0.5 ms per
+      // 4096x4096 step)
+      if (segs[s].wt16) segs[s].wt16[(long)cc * segs[s].rows + r] = f2bf(pi);
     }
   }
 }
@@ -270,7 +273,7 @@ __device__ __forceinline__ void fin_opt_apply(const FinOpt& o, float lr_t, const
     if (rel >= 0 && rel < (long)o.segs[s].rows * o.segs[s].cols) {
       const int r = (int)(rel / o.segs[s].cols), cc = (int)(rel % o.segs[s].cols);
       o.segs[s].w16[rel] = f2bf(pi);
-      o.segs[s].wt16[(long)cc * o.segs[s].rows + r] = f2bf(pi);
+      if (o.segs[s].wt16) o.segs[s].wt16[(long)cc * o.segs[s].rows + r] = f2bf(pi);
     }
   }
 }

@@ -217,6 +217,58 @@ __global__ void shadow_refresh_kernel(const float* __restrict__ p, long n,
 
 __global__ void step_inc_kernel(int64_t* step) { *step += 1; }
 
+// Transposed bf16 shadows of large weight segments, wt16[c][r] = w16[r][c], through 64 x 64 LDS
+// tiles (16-byte row reads, 16-byte column-chunk writes): the pass that replaces the dense
+// optimizer's per-element scattered wt16 stores for those segments.  Block = one tile of one
+// segment (tiles numbered segment by segment); edges handled element-wise.
+__global__ void __launch_bounds__(256) shadow_transpose_kernel(const ShadowSeg* __restrict__ segs, int nseg) {
+  __shared__ bf16 t[64][64 + 8];
+  int b = blockIdx.x, s = 0;
+  for (; s < nseg; ++s) {
+    const int nt = ((segs[s].rows + 63) / 64) * ((segs[s].cols + 63) / 64);
+    if (b < nt) break;
+    b -= nt;
+  }
+  if (s >= nseg) return;
+  const ShadowSeg g = segs[s];
+  const int tcols = (g.cols + 63) / 64;
+  const int r0 = (b / tcols) * 64, c0 = (b % tcols) * 64;
+  const int tid = threadIdx.x;
+  const bool full = r0 + 64 <= g.rows && c0 + 64 <= g.cols && (g.cols % 8) == 0 && (g.rows % 8) == 0;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {          // 64 rows x 8 chunks of 8 columns
+    const int e = tid + 256 * k, r = e >> 3, q = e & 7;
+    if (full) {
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(g.w16 + (size_t)(r0 + r) * g.cols + c0 + q * 8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) t[r][q * 8 + j] = v[j];
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int rr = r0 + r, cc = c0 + q * 8 + j;
+        t[r][q * 8 + j] = (rr < g.rows && cc < g.cols) ? g.w16[(size_t)rr * g.cols + cc] : f2bf(0.f);
+      }
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {          // 64 columns x 8 chunks of 8 rows
+    const int e = tid + 256 * k, c = e >> 3, q = e & 7;
+    bf16x8 v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = t[q * 8 + j][c];
+    if (full) {
+      *reinterpret_cast<bf16x8*>(g.wt16 + (size_t)(c0 + c) * g.rows + r0 + q * 8) = v;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int rr = r0 + q * 8 + j, cc = c0 + c;
+        if (rr < g.rows && cc < g.cols) g.wt16[(size_t)cc * g.rows + rr] = v[j];
+      }
+    }
+  }
+}
+
 // ------------------------------------------------------------------ dispatch
 #define HFM_OPT_DISPATCH(OPT, CALL)   \
   switch (OPT) {                      \
@@ -364,6 +416,13 @@ HFM_API int hfm_shadow_refresh(const float* p, long n, const void* segs, int nse
   const int grid = (int)(gg < 4096 ? gg : 4096);
   hipLaunchKernelGGL(shadow_refresh_kernel, dim3(grid), dim3(256), 0, st, p, n,
                      (const ShadowSeg*)segs, nseg);
+  HFM_LAUNCH_CHECK();
+}
+
+// segs: device table of nseg segments, ntiles = sum over them of ceil(rows / 64) * ceil(cols / 64)
+HFM_API int hfm_shadow_transpose(const void* segs, int nseg, int ntiles, hipStream_t st) {
+  if (nseg <= 0 || ntiles <= 0) return 0;
+  hipLaunchKernelGGL(shadow_transpose_kernel, dim3(ntiles), dim3(256), 0, st, (const ShadowSeg*)segs, nseg);
   HFM_LAUNCH_CHECK();
 }
 

@@ -52,6 +52,8 @@ _SHARD_PIPELINE = flag("HIPFM_SHARD_PIPELINE")
 _TOWER_GATHER = flag("HIPFM_TOWER_GATHER")   # FM gather fused into the tower
 # weight gradients + split-K combine + bias/head reductions + dense optimizer in one launch
 _WGFIN = flag("HIPFM_WGFIN")
+# weight segments from this size up get their transposed bf16 shadow from a tiled pass
+_SHADOW_T_MIN = 1 << 18
 # single GPU, lazy rows: wgfin inside the sparse backward's launch (sparse_fused.hip sfwg_kernel)
 _SFWG = flag("HIPFM_SFWG")
 # one GPU, multi-step graphs: the run's batches sorted up front (fsort_run.h) instead of each
@@ -264,6 +266,12 @@ class NativeDeepFM(GraphRunnerMixin, NativeStateMixin):
         self.d0 = F * K
         self.K0p = pad32(self.d0)
         self.Np = [pad32(L) for L in self.layers]
+        # a per-layer (unfused) tower with a wide first layer pads its input to 128 columns: the
+        # layer-0 weight-gradient and dX0 GEMMs then tile on the LDS-staged 128 x 128 tile (at
+        # K0p = 320 they ran on the 64 x 64 register tile: 0.75 of a 5.4 ms 4096x3 step,
+        # profiles/r6tw_tower4096_kernels.md); the padding columns stay exactly zero
+        if self._per_layer_tower(fused) and self.Np[0] >= 1024:
+            self.K0p = (self.d0 + 127) // 128 * 128
         self.Kp = [self.K0p] + self.Np[:-1]
         segs: List[DenseSeg] = []
         off = 0
@@ -357,6 +365,18 @@ class NativeDeepFM(GraphRunnerMixin, NativeStateMixin):
             shadow.append(ShadowSeg(s.off, self.Np[i], self.Kp[i], w16.data_ptr(), wt16.data_ptr()))
         self._shadow_dev = KN.struct_array_to_device(shadow, dev)
         self._nshadow = len(shadow)
+        # single-GPU dense optimizer (dense_opt / finalize_opt): large segments leave their
+        # transposed shadow to one tiled pass after the update (the per-element transposed stores
+        # cost 0.5 ms per step at 4096 x 4096 layers)
+        big = [sg for sg in shadow if sg.rows * sg.cols >= _SHADOW_T_MIN]
+        self._shadow_t = None
+        self._shadow_opt = self._shadow_dev
+        if big:
+            nt = [ShadowSeg(sg.off, sg.rows, sg.cols, sg.w16, 0 if sg.rows * sg.cols >= _SHADOW_T_MIN else sg.wt16)
+                  for sg in shadow]
+            self._shadow_opt = KN.struct_array_to_device(nt, dev)
+            self._shadow_t = (KN.struct_array_to_device(big, dev), len(big),
+                              sum(((sg.rows + 63) // 64) * ((sg.cols + 63) // 64) for sg in big))
         self.W8, self.sW, self.W8amax = [], [], []
         if self.fp8:
             jobs, row0 = [], 0
@@ -520,6 +540,14 @@ class NativeDeepFM(GraphRunnerMixin, NativeStateMixin):
     def _tower_lds_bytes(self) -> int:
         return self._tower_lds_layout()[4]
 
+    def _per_layer_tower(self, fused) -> bool:
+        """The fused-tower decision of the constructor, made before the dense layout exists
+        (it depends on the layer widths only: the gather's E tile is checked separately)."""
+        lds = 2 * (sum(32 * (n + 8) for n in self.Np) + 2 * 32 * (max(self.Np) + 8))
+        can_fuse = not self.batch_norm and len(self.layers) <= TW_MAXL and lds <= 150 * 1024
+        want = (knob("HIPFM_FUSED_TOWER") != "0") if fused is None else bool(fused)
+        return not (can_fuse and want)
+
     def _tower_grow_layout(self):
         """(byte offset, total LDS bytes) of the tower's sorted-gradient-row scratch, appended to
         the layout above: x [32][F] f32, S [32][K] f32, inverse perm [32][F] i32, and the 4 wave
@@ -588,6 +616,8 @@ class NativeDeepFM(GraphRunnerMixin, NativeStateMixin):
                 self.wg_cfg.append((None, s))
                 continue
             t = _pick_tile(Mg, Ng, row_major_stream=False, Kd=Kd)
+            if t not in (KN.TILE_LDS, KN.TILE_PP) and _LDS_GEMM and _lds_tile_ok(Mg, Ng, Kd, splitk=4):
+                t = KN.TILE_LDS     # (few output tiles, but the batch reduction splits 4+ ways)
             s = _pick_splitk(Mg, Ng, Kd, t)
             self.wg_cfg.append((t, s))
         self.slabs = [torch.zeros(s, self.Np[i], self.Kp[i], **f32) for i, (t, s) in enumerate(self.wg_cfg)]
@@ -733,7 +763,10 @@ class NativeDeepFM(GraphRunnerMixin, NativeStateMixin):
         for j in jobs:                       # finalize_kernel block mapping
             # slab-lanes per output: each thread sums <= 8 slabs, all its loads in flight at once
             # (the 512 head-partial rows of the 1-block jobs were 64 dependent-load rounds)
-            j.lanes = 64 if j.nslab >= 256 else (8 if j.nslab >= 64 else 4)
+            # (<= 4 slabs -- the per-layer wide wgrad's split-K -- one thread per element, its
+            # slabs summed in order: the same sums as 4 lanes, at 256 elements per workgroup
+            # instead of 64; 16.7M-element layers had 262K workgroups)
+            j.lanes = 64 if j.nslab >= 256 else (8 if j.nslab >= 64 else (4 if j.nslab > 4 else 1))
             j.chunk0 = nb
             nb += (j.n + 256 // j.lanes - 1) // (256 // j.lanes)
         self._slab_blocks = nb
@@ -1176,7 +1209,9 @@ class NativeDeepFM(GraphRunnerMixin, NativeStateMixin):
             KN.finalize_opt(self.opt_id, self._slab_jobs, self._nslab_jobs, self._slab_blocks,
                             self._row_jobs, self._nrow_jobs, self._row_total, self.p, self.g,
                             self.sd[0], self.sd[1], self.P, self.h_dense, self.step,
-                            self._shadow_dev, self._nshadow, self._done_ctr)
+                            self._shadow_opt, self._nshadow, self._done_ctr)
+            if self._shadow_t is not None:
+                KN.shadow_transpose(*self._shadow_t)
             return
         KN.finalize(self._slab_jobs, self._nslab_jobs, self._slab_blocks, self._row_jobs,
                     self._nrow_jobs, self._row_total)
@@ -1520,7 +1555,9 @@ class NativeDeepFM(GraphRunnerMixin, NativeStateMixin):
     def _dense_opt(self):
         """Dense optimizer over the flat buffer (+ bf16 / fp8 weight shadows); advances the step."""
         KN.dense_opt(self.opt_id, self.p, self.g, self.sd[0], self.sd[1], self.P, self.h_dense,
-                     self.step, self._shadow_dev, self._nshadow, done_ctr=self._done_ctr)
+                     self.step, self._shadow_opt, self._nshadow, done_ctr=self._done_ctr)
+        if self._shadow_t is not None:
+            KN.shadow_transpose(*self._shadow_t)
         if self.fp8:
             KN.w8_quant(self._w8_jobs, len(self.layers), self._w8_rows)
 

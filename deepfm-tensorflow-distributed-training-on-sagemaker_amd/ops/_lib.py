@@ -238,6 +238,7 @@ _SIGS = {
                     C.POINTER(EpiArgs), c_void_p],
     "hfm_epi_args_bytes": [],
     "hfm_head": [C.POINTER(HeadArgs), c_void_p],
+    "hfm_shadow_transpose": [c_void_p, c_int, c_int, c_void_p],
     "hfm_head_args_bytes": [],
     "hfm_slab_reduce": [c_void_p, c_int, c_int, c_void_p],
     "hfm_slab_job_bytes": [],

@@ -426,6 +426,11 @@ def finalize_opt(opt, slab_jobs_dev, nsj, nslab_blocks, row_jobs_dev, nrj, total
                                ptr(segs_dev), nseg, ptr(done_ctr), stream_handle()), "finalize_opt")
 
 
+def shadow_transpose(segs_dev, nseg: int, ntiles: int):
+    """wt16 = w16^T for the segments in ``segs_dev`` (64 x 64 LDS tiles; optim.hip)."""
+    check(L().hfm_shadow_transpose(ptr(segs_dev), int(nseg), int(ntiles), stream_handle()), "shadow_transpose")
+
+
 def shadow_refresh(p, n, segs_dev, nseg):
     check(L().hfm_shadow_refresh(ptr(p), n, ptr(segs_dev), nseg, stream_handle()), "shadow_refresh")
 

@@ -127,6 +127,10 @@ def test_wide_tower_step_matches_register_tiles(monkeypatch, bn):
             m.train_step(ids, vals, lab)
         torch.cuda.synchronize()
         m.check_errors()
+        # the 512 x 512 weight segments take the tiled transposed-shadow pass (optim.hip)
+        assert m._shadow_t is not None
+        for w16, wt16 in zip(m.W16, m.WT16):
+            assert torch.equal(wt16, w16.t())
         outs.append((m.p.clone(), m.tv[:synth.feature_size].clone()))
     (p8, v8), (p0, v0) = outs
     assert (p8 - p0).abs().max().item() <= 1e-4 * p0.abs().max().item()
@@ -186,3 +190,36 @@ def test_wide_head_matches_fp32_reference(L, M, nvalid, train, dh):
         # dZ from the kernel's own dlogit: bf16 rounding of the same fp32 product
         ref = torch.where(hf > 0, dlog[:, None] * w[None, :] * 2.0, torch.zeros_like(hf)).bfloat16()
         assert torch.equal(dz, ref) and torch.equal(dzt, ref.t().contiguous())
+
+
+def test_wide_first_layer_padded_input_matches_golden():
+    """A per-layer tower with a wide first layer pads its input to 128 columns (K0p 320 -> 384
+    at F = 39, K = 8: the layer-0 weight-gradient / dX0 GEMMs take the LDS tile); the trained
+    dense parameters, exported in TF shapes, still match the fp32 golden model and the padding
+    columns of W0 stay exactly zero."""
+    from hipfm.data.synthetic import make_synth
+    from hipfm.models.deepfm import NativeDeepFM
+    from hipfm.models.reference import GoldenDeepFM, init_params
+    synth = make_synth("total:4000", seed=21)
+    F, K, layers, keep = synth.F, 8, [1024, 64], [1.0, 1.0]
+    V = synth.feature_size
+    params = init_params(V, F, K, layers, False, seed=3)
+    kw = dict(adam_epsilon=1e-2)
+    nat = NativeDeepFM(V, F, K, layers, keep, batch_size=512, device=DEV, init=False, learning_rate=1e-3,
+                       fused=False, **kw)
+    assert not nat.fused and nat.K0p == 384 and nat.d0 == F * K
+    nat.load_tf_params(params)
+    gold = GoldenDeepFM(V, F, K, layers, keep, params=params, learning_rate=1e-3, **kw)
+    for s in range(2):
+        ids, vals, labels = synth.batch(512, step=s)
+        gold.train_step(ids, vals, labels)
+        nat.train_step(ids.to(DEV, torch.int32), vals.to(DEV), labels.to(DEV))
+    torch.cuda.synchronize()
+    nat.check_errors()
+    seg = nat.dense_segs["Deep-part/mlp0/weights"]
+    w0 = nat.p[seg.off:seg.off + nat.Np[0] * nat.K0p].view(nat.Np[0], nat.K0p)
+    assert not w0[:, nat.d0:].any()
+    dense = nat.dense_tf_params()
+    for k, v in dense.items():
+        g = gold.params[k]
+        assert (v - g).abs().max().item() <= 2e-3 * max(1.0, g.abs().max().item()), k
