@@ -29,10 +29,15 @@
 // slots per tile (K = 8, same-box: 256 -> 0.1116, 512 -> 0.1120, 1024 -> 0.1158 ms/step; 1024 drops
 // the merged launch to 3 workgroups per CU)
 __host__ __device__ constexpr int sf_tile_slots(int K) { return K <= 16 ? 512 : (K == 32 ? 256 : 128); }
+// K = 32 with few slots (the reference workload, B = 1024: 40K slots) -- every sparse launch
+// takes 128-slot tiles: twice the tiles, half the run heads per tile, so a tile's serial
+// record round trips halve (0.0766 -> 0.0695 ms/step there; at B = 16384 the 256-slot tiles stay
+// faster, 0.2585 vs 0.2734: profiles/r6_sf_tile32_ab.log).  Tile buffers are sized for 128.
+constexpr int SF_SMALL_N32 = 131072;
 
-template <int K>
+template <int K, int TPS = sf_tile_slots(K)>
 struct SfCfg {
-  static constexpr int TP = sf_tile_slots(K);  // slots per tile
+  static constexpr int TP = TPS;  // slots per tile
   static constexpr int LPS = K / 4;                                    // lanes per slot (f32x4 each)
   static constexpr int PPP = 256 / LPS;                                // slots per pass
   static constexpr int PASSES = TP / PPP;
@@ -261,26 +266,27 @@ __device__ __forceinline__ void sf_lookback(const SfArgs& A, int tile, unsigned 
   if (lane == 0) atomicOr(A.sync + 2, 4u);  // no origin before tile 0: impossible
 }
 
-template <int K>
+template <int K, int TPS = sf_tile_slots(K)>
 struct SfSmem {
-  float g[SfCfg<K>::TP][SfCfg<K>::CP];
-  int skl[SfCfg<K>::TP];
-  float lead[SfCfg<K>::NCH][SfCfg<K>::CP];
-  int fh[SfCfg<K>::NCH];  // offset of the first head in the chunk (CH: none)
-  unsigned hb[SfCfg<K>::NCH];  // head bits of the chunk's CH slots (bit q: slot j*CH + q heads a run)
-  int hl[SfCfg<K>::TP];   // head positions, ascending
+  using T = SfCfg<K, TPS>;
+  float g[T::TP][T::CP];
+  int skl[T::TP];
+  float lead[T::NCH][T::CP];
+  int fh[T::NCH];  // offset of the first head in the chunk (CH: none)
+  unsigned hb[T::NCH];  // head bits of the chunk's CH slots (bit q: slot j*CH + q heads a run)
+  int hl[T::TP];   // head positions, ascending
   int wcount[4];
   int open_key_s, open_pos_s;
-  float own_lead[SfCfg<K>::C];
+  float own_lead[T::C];
 };
 
 HFM_STAMP_BUF(hfm_st_sf)
 #define SF_ST(k) HFM_STAMP(hfm_st_sf, blockIdx.x, k)
 
 // tile `tile` of the sparse backward (the sf_tile_kernel workgroup, or one of sfwg_kernel's)
-template <int K, int MODE, int OPT>
-__device__ __forceinline__ void sf_tile_body(const SfArgs& A, const int tile, SfSmem<K>& sm) {
-  using T = SfCfg<K>;
+template <int K, int MODE, int OPT, int TPS = sf_tile_slots(K)>
+__device__ __forceinline__ void sf_tile_body(const SfArgs& A, const int tile, SfSmem<K, TPS>& sm) {
+  using T = SfCfg<K, TPS>;
   constexpr int CH = T::CH;
   auto& g = sm.g;
   auto& skl = sm.skl;
@@ -471,10 +477,10 @@ __device__ __forceinline__ void sf_tile_body(const SfArgs& A, const int tile, Sf
   SF_ST(6);
 }
 
-template <int K, int MODE, int OPT>
+template <int K, int MODE, int OPT, int TPS>
 __global__ void __launch_bounds__(256) sf_tile_kernel(SfArgs A) {
-  __shared__ SfSmem<K> sm;
-  sf_tile_body<K, MODE, OPT>(A, blockIdx.x, sm);
+  __shared__ SfSmem<K, TPS> sm;
+  sf_tile_body<K, MODE, OPT, TPS>(A, blockIdx.x, sm);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -498,9 +504,9 @@ constexpr int SFWG_MAXNS = 4;
 // same-box bf16 0.1109-0.1114 (1) / 0.1120-0.1128 (2) / 0.1169-0.1171 (4) ms/step
 constexpr int SFWG_TQ = 1;
 
-template <int K>
+template <int K, int TPS = sf_tile_slots(K)>
 union SfwgSmem {
-  SfSmem<K> sf;
+  SfSmem<K, TPS> sf;
   WgfSmem wg;
 };
 
@@ -509,11 +515,11 @@ union SfwgSmem {
 // every row outside the batch its l2-only update (tf1_sweep.h) -- disjoint rows, same step t
 // (a waves-per-SIMD floor of 5 -- 5 tile workgroups per CU at K <= 8, 8 VGPRs spilled in the
 // wgfin half -- did not hold up in a 3 x 3 A/B: profiles/r4zz_sfwg_occupancy_confirm.log)
-template <int K, int OPT, bool SWEEP>
+template <int K, int OPT, bool SWEEP, int TPS>
 __global__ void __launch_bounds__(256) sfwg_kernel(SfArgs A, WgFinArgs W, unsigned* done, SweepArgs S) {
-  __shared__ SfwgSmem<K> sm;
+  __shared__ SfwgSmem<K, TPS> sm;
   const int nw = W.tile_wgs + 1;
-  const int ntile = (A.n + SfCfg<K>::TP - 1) / SfCfg<K>::TP;
+  const int ntile = (A.n + TPS - 1) / TPS;
   // (the wgfin workgroups first: with the sparse tiles first and wgfin in the tail the launch
   // measured 0.1202-0.1213 vs 0.1032-0.1043 ms/step)
   const int bid = (int)blockIdx.x;
@@ -522,7 +528,7 @@ __global__ void __launch_bounds__(256) sfwg_kernel(SfArgs A, WgFinArgs W, unsign
     wgfin_body<OPT, SFWG_PF, SFWG_MAXNS, SFWG_TQ>(W, bid, sm.wg);
     SF_ST(9);
   } else if (!SWEEP || bid < nw + ntile) {
-    sf_tile_body<K, 0, OPT>(A, bid - nw, sm.sf);
+    sf_tile_body<K, 0, OPT, TPS>(A, bid - nw, sm.sf);
   } else if (SWEEP) {
     const int sb = bid - nw - ntile;
     // (2 rows per thread per pass: 98 VGPRs, 0.1596-0.1598 vs 0.1565-0.1619 ms -- no gain)
@@ -542,28 +548,28 @@ __global__ void __launch_bounds__(256) sfwg_kernel(SfArgs A, WgFinArgs W, unsign
   SF_ST(7);
 }
 
-template <int K, int OPT>
+template <int K, int OPT, int TPS>
 static void sfwg_launch(const SfArgs& A, const WgFinArgs& W, unsigned* done, const SweepArgs& S,
                         hipStream_t st) {
-  const dim3 g(W.tile_wgs + 1 + (A.n + SfCfg<K>::TP - 1) / SfCfg<K>::TP + S.nblk), blk(256);
+  const dim3 g(W.tile_wgs + 1 + (A.n + TPS - 1) / TPS + S.nblk), blk(256);
   if constexpr (K <= 32) {
     if (S.nblk) {
-      hipLaunchKernelGGL((sfwg_kernel<K, OPT, true>), g, blk, 0, st, A, W, done, S);
+      hipLaunchKernelGGL((sfwg_kernel<K, OPT, true, TPS>), g, blk, 0, st, A, W, done, S);
       return;
     }
   }
-  hipLaunchKernelGGL((sfwg_kernel<K, OPT, false>), g, blk, 0, st, A, W, done, S);
+  hipLaunchKernelGGL((sfwg_kernel<K, OPT, false, TPS>), g, blk, 0, st, A, W, done, S);
 }
 
-template <int K>
+template <int K, int TPS = sf_tile_slots(K)>
 static int sfwg_dispatch(int opt, const SfArgs& A, const WgFinArgs& W, unsigned* done,
                          const SweepArgs& S, hipStream_t st) {
   switch (opt) {
-    case OPT_ADAM: sfwg_launch<K, OPT_ADAM>(A, W, done, S, st); break;
-    case OPT_ADAGRAD: sfwg_launch<K, OPT_ADAGRAD>(A, W, done, S, st); break;
-    case OPT_MOMENTUM: sfwg_launch<K, OPT_MOMENTUM>(A, W, done, S, st); break;
-    case OPT_FTRL: sfwg_launch<K, OPT_FTRL>(A, W, done, S, st); break;
-    case OPT_GD: sfwg_launch<K, OPT_GD>(A, W, done, S, st); break;
+    case OPT_ADAM: sfwg_launch<K, OPT_ADAM, TPS>(A, W, done, S, st); break;
+    case OPT_ADAGRAD: sfwg_launch<K, OPT_ADAGRAD, TPS>(A, W, done, S, st); break;
+    case OPT_MOMENTUM: sfwg_launch<K, OPT_MOMENTUM, TPS>(A, W, done, S, st); break;
+    case OPT_FTRL: sfwg_launch<K, OPT_FTRL, TPS>(A, W, done, S, st); break;
+    case OPT_GD: sfwg_launch<K, OPT_GD, TPS>(A, W, done, S, st); break;
     default: return (int)hipErrorInvalidValue;
   }
   return 0;
@@ -575,12 +581,12 @@ static int sfwg_dispatch(int opt, const SfArgs& A, const WgFinArgs& W, unsigned*
 // rows (shard_table.h sh_serve_elem, stamped step + 2; this step's owner update patches what it
 // changes).  The highest block indices are dispatched last: they fill the CUs the tiles' look-back
 // tail leaves idle, instead of competing with the tower's workgroups in its launch.
-template <int K>
+template <int K, int TPS>
 __global__ void __launch_bounds__(256) sfwg_x_kernel(SfArgs A, WgFinArgs W, ShServeArgs S, int tiles) {
-  __shared__ SfwgSmem<K> sm;
+  __shared__ SfwgSmem<K, TPS> sm;
   const int nw = W.tile_wgs + 1;
   if ((int)blockIdx.x < nw) wgfin_body<-1, SFWG_PF, SFWG_MAXNS, SFWG_TQ>(W, blockIdx.x, sm.wg);
-  else if ((int)blockIdx.x < nw + tiles) sf_tile_body<K, 2, 0>(A, (int)blockIdx.x - nw, sm.sf);
+  else if ((int)blockIdx.x < nw + tiles) sf_tile_body<K, 2, 0, TPS>(A, (int)blockIdx.x - nw, sm.sf);
   else if (S.rows) sh_serve_elem<K>(S, ((int)blockIdx.x - nw - tiles) * 256 + (int)threadIdx.x);
   else sh_tag_elem(S, ((int)blockIdx.x - nw - tiles) * 256 + (int)threadIdx.x);   // (replicated run step)
 }
@@ -598,16 +604,18 @@ HFM_API int hfm_sparse_wgfin_x(int K, const SfArgs* A, const WgFinArgs* W, const
     return (int)hipErrorInvalidValue;
   const long sth = S ? (long)sv.total * (sv.rows ? K / 4 : 1) : 0;
   const int swg = (int)((sth + 255) / 256);
-#define X_(KK)                                                                                    \
-  hipLaunchKernelGGL(sfwg_x_kernel<KK>,                                                           \
-                     dim3(W->tile_wgs + 1 + (A->n + SfCfg<KK>::TP - 1) / SfCfg<KK>::TP + swg), dim3(256), \
-                     0, st, *A, *W, sv, (A->n + SfCfg<KK>::TP - 1) / SfCfg<KK>::TP)
+#define X_(KK, TT)                                                                                \
+  hipLaunchKernelGGL((sfwg_x_kernel<KK, TT>), dim3(W->tile_wgs + 1 + (A->n + TT - 1) / TT + swg),   \
+                     dim3(256), 0, st, *A, *W, sv, (A->n + TT - 1) / TT)
   switch (K) {
-    case 4: X_(4); break;
-    case 8: X_(8); break;
-    case 16: X_(16); break;
-    case 32: X_(32); break;
-    case 64: X_(64); break;
+    case 4: X_(4, sf_tile_slots(4)); break;
+    case 8: X_(8, sf_tile_slots(8)); break;
+    case 16: X_(16, sf_tile_slots(16)); break;
+    case 32:
+      if (A->n <= SF_SMALL_N32) X_(32, 128);
+      else X_(32, sf_tile_slots(32));
+      break;
+    case 64: X_(64, sf_tile_slots(64)); break;
     default: return (int)hipErrorInvalidValue;
   }
 #undef X_
@@ -636,7 +644,10 @@ HFM_API int hfm_sparse_wgfin(int K, int opt, const SfArgs* A, const WgFinArgs* W
     case 4: rc = sfwg_dispatch<4>(opt, *A, *W, done, S, st); break;
     case 8: rc = sfwg_dispatch<8>(opt, *A, *W, done, S, st); break;
     case 16: rc = sfwg_dispatch<16>(opt, *A, *W, done, S, st); break;
-    case 32: rc = sfwg_dispatch<32>(opt, *A, *W, done, S, st); break;
+    case 32:
+      rc = A->n <= SF_SMALL_N32 ? sfwg_dispatch<32, 128>(opt, *A, *W, done, S, st)
+                                : sfwg_dispatch<32>(opt, *A, *W, done, S, st);
+      break;
     case 64: rc = sfwg_dispatch<64>(opt, *A, *W, done, S, st); break;
     default: return (int)hipErrorInvalidValue;
   }
@@ -645,15 +656,22 @@ HFM_API int hfm_sparse_wgfin(int K, int opt, const SfArgs* A, const WgFinArgs* W
 }
 
 HFM_API int hfm_sparse_fused_tiles(int K, int n) {
-  const int tp = sf_tile_slots(K);
+  const int tp = K == 32 ? 128 : sf_tile_slots(K);     // (an upper bound for either K = 32 tile)
   return (n + tp - 1) / tp;
 }
 
 template <int K, int MODE, int OPT>
 static void sf_launch(const SfArgs& A, hipStream_t st) {
-  using T = SfCfg<K>;
-  const int tiles = (A.n + T::TP - 1) / T::TP;
-  hipLaunchKernelGGL((sf_tile_kernel<K, MODE, OPT>), dim3(tiles), dim3(256), 0, st, A);
+  // (K = 32 with few slots: the small tiles of every sparse launch, so all update forms sum each
+  // run in the same tile grouping -- bitwise equal to each other)
+  if constexpr (K == 32) {
+    if (A.n <= SF_SMALL_N32) {
+      hipLaunchKernelGGL((sf_tile_kernel<K, MODE, OPT, 128>), dim3((A.n + 127) / 128), dim3(256), 0, st, A);
+      return;
+    }
+  }
+  constexpr int TP = sf_tile_slots(K);
+  hipLaunchKernelGGL((sf_tile_kernel<K, MODE, OPT, TP>), dim3((A.n + TP - 1) / TP), dim3(256), 0, st, A);
 }
 
 template <int K>
