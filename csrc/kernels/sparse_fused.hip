@@ -28,7 +28,10 @@
 
 // slots per tile (K = 8, same-box: 256 -> 0.1116, 512 -> 0.1120, 1024 -> 0.1158 ms/step; 1024 drops
 // the merged launch to 3 workgroups per CU)
-__host__ __device__ constexpr int sf_tile_slots(int K) { return K <= 16 ? 512 : (K == 32 ? 256 : 128); }
+#ifndef HFM_SF_TP8
+#define HFM_SF_TP8 512     // (diagnostic variants: HIPFM_BUILD_VARIANT=<tag>:HFM_SF_TP8=<slots>)
+#endif
+__host__ __device__ constexpr int sf_tile_slots(int K) { return K <= 16 ? HFM_SF_TP8 : (K == 32 ? 256 : 128); }
 // K = 32 with few slots (the reference workload, B = 1024: 40K slots) -- every sparse launch
 // takes 128-slot tiles: twice the tiles, half the run heads per tile, so a tile's serial
 // record round trips halve (0.0766 -> 0.0695 ms/step there; at B = 16384 the 256-slot tiles stay
