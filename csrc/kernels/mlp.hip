@@ -1273,25 +1273,26 @@ __global__ void __launch_bounds__(256) head_wide_kernel(HeadArgs a) {
 // Wide head (L % 256 == 0, L > 256) in two launches with 16-byte accesses throughout; the
 // one-launch head_wide_kernel read H one bf16 per lane per row in a 256-workgroup grid and took
 // ~0.9 ms of a 6.5 ms step at L = 4096 (profiles/r6tw_kernels.md).
-// dot: one wave per 16 rows of a 64-row block, 4 rows' chunks in flight: y, p, loss, dlogit, and
+// dot: 16 waves per 64-row block, 4 rows each with all their chunks in flight: y, p, loss, dlogit, and
 //      the block's dlogit / loss sums (partial columns L, L + 1, rows in order).
 // bwd: workgroup = 64 rows x 256 columns; thread = 8 rows x 8 columns (rows 8 rg.., chunk cc):
 //      dz / dh rows as 16-byte chunks, dz_t as 8-row 16-byte column chunks, and the block's
 //      column sums of dlogit * h (rows in order per thread, the 8 row groups in order).
-__global__ void __launch_bounds__(256) head_wide_dot_kernel(HeadArgs a) {
+__global__ void __launch_bounds__(1024) head_wide_dot_kernel(HeadArgs a) {
   __shared__ float hw_dl[64], hw_loss[64];
   const int L = a.L;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int bb = blockIdx.x * 64;
   const int nch = L / 8;                      // 16-byte chunks per row
-  for (int s0 = 0; s0 < 16; s0 += 4) {
+  {                                     // 16 waves x 4 rows: every row's chunks in flight at once
+    const int s0 = 0;
     float yd[4] = {0.f, 0.f, 0.f, 0.f};
     for (int ch = lane; ch < nch; ch += 64) {
       const f32x4 w0 = *reinterpret_cast<const f32x4*>(a.w_out + ch * 8);
       const f32x4 w1 = *reinterpret_cast<const f32x4*>(a.w_out + ch * 8 + 4);
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const int b = bb + wv * 16 + s0 + u;
+        const int b = bb + wv * 4 + s0 + u;
         if (b < a.M) {
           const bf16x8 h = *reinterpret_cast<const bf16x8*>(a.h + (size_t)b * L + ch * 8);
           float d = 0.f;
@@ -1307,7 +1308,7 @@ __global__ void __launch_bounds__(256) head_wide_dot_kernel(HeadArgs a) {
     for (int u = 0; u < 4; ++u) {
 #pragma unroll
       for (int o = 32; o >= 1; o >>= 1) yd[u] += __shfl_xor(yd[u], o, 64);
-      const int s = s0 + u, b = bb + wv * 16 + s;
+      const int s = s0 + u, b = bb + wv * 4 + s;
       float dl = 0.f, lossb = 0.f;
       if (b < a.M) {
         const float y = a.y_fm[b] + yd[u] + a.b_out[0];
@@ -1329,8 +1330,8 @@ __global__ void __launch_bounds__(256) head_wide_dot_kernel(HeadArgs a) {
         if (a.train && lane == 0) a.dlogit[b] = dl;
       }
       if (lane == 0) {
-        hw_dl[wv * 16 + s] = dl;
-        hw_loss[wv * 16 + s] = lossb;
+        hw_dl[wv * 4 + s] = dl;
+        hw_loss[wv * 4 + s] = lossb;
       }
     }
   }
@@ -1424,7 +1425,7 @@ HFM_API int hfm_head(const HeadArgs* a, hipStream_t st) {
   const int grid = (a->M + 63) / 64;
   if (a->L > 256) {
     if (a->L % 256 == 0) {
-      hipLaunchKernelGGL(head_wide_dot_kernel, dim3(grid), dim3(256), 0, st, *a);
+      hipLaunchKernelGGL(head_wide_dot_kernel, dim3(grid), dim3(1024), 0, st, *a);
       hipLaunchKernelGGL(head_wide_bwd_kernel, dim3(grid, a->L / 256), dim3(256), 0, st, *a);
       HFM_LAUNCH_CHECK();
     }
