@@ -13,7 +13,7 @@ import glob
 import os
 import sys
 
-OURS = ("tower_kernel", "tower_light", "wgfin_kernel", "sfwg_kernel", "sfwg_x", "fs2_",  "dense_sweep", "fm_fwd", "wgrad_group", "finalize_kernel", "sf_tile", "sf_carry",
+OURS = ("decode_examples", "head_wide", "shadow_transpose", "tower_kernel", "tower_light", "wgfin_kernel", "sfwg_kernel", "sfwg_x", "fs2_",  "dense_sweep", "fm_fwd", "wgrad_group", "finalize_kernel", "sf_tile", "sf_carry",
         "fs_sort", "fs_transpose", "dense_opt", "w8_quant", "sh_", "seg_", "onesweep", "lsd_",
         "gemm_nt", "gemm_lds", "gemm_pp", "Cijk", "head_kernel", "rcclGenericKernel")
 SIMDS = 1024
