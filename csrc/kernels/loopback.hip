@@ -228,6 +228,54 @@ HFM_API int hfm_lb_create(void** out, int nranks, int rank, const char* path, in
   return 0;
 }
 
+// Host-only exercise of the engine's barrier (no GPU: tests/test_loopback_barrier.py runs it in
+// several CPU processes): `iters` barriers over the shared page at `path` (rank 0 creates it);
+// before barrier i every rank adds 1 to a check word in the page's spare half and after it reads
+// the word back, which must be >= (i + 1) * nranks (no rank passes a barrier before all arrive).
+// Rank `stall_rank` sleeps `stall_ms` before barrier `stall_at` (timeout / poison path).
+// Returns the engine's error word (0 ok, 1 this rank timed out, 2 a peer poisoned the page),
+// 3 on a check-word violation, -1 on setup failure.
+HFM_API int hfm_lb_barrier_selftest(const char* path, int nranks, int rank, int create, int timeout_ms, int iters,
+                                    int stall_rank, int stall_at, int stall_ms) {
+  if (nranks < 1 || nranks > LB_MAX_RANKS || rank < 0 || rank >= nranks) return -1;
+  const int fd = open(path, create ? (O_RDWR | O_CREAT | O_EXCL) : O_RDWR, 0600);
+  if (fd < 0) return -1;
+  if (create && ftruncate(fd, 4096) != 0) {
+    close(fd);
+    return -1;
+  }
+  void* m = mmap(nullptr, 4096, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+  close(fd);
+  if (m == MAP_FAILED) return -1;
+  LbEngine e;
+  e.rank = rank;
+  e.nranks = nranks;
+  e.timeout_ms = timeout_ms > 0 ? timeout_ms : 60000;
+  e.shm = (LbShared*)m;
+  auto* chk = reinterpret_cast<std::atomic<uint32_t>*>((char*)m + 2048);
+  if (create) {
+    e.shm->count.store(0);
+    e.shm->gen.store(0);
+    e.shm->poison.store(0);
+    e.shm->nranks = (uint32_t)nranks;
+    chk->store(0);
+  }
+  int rc = 0;
+  for (int i = 0; i < iters && rc == 0; ++i) {
+    if (rank == stall_rank && i == stall_at) {
+      timespec ts{stall_ms / 1000, (long)(stall_ms % 1000) * 1000000L};
+      nanosleep(&ts, nullptr);
+    }
+    chk->fetch_add(1, std::memory_order_acq_rel);
+    e.groups = (unsigned long long)i;
+    lb_barrier(&e);
+    rc = e.err.load();
+    if (rc == 0 && chk->load(std::memory_order_acquire) < (uint32_t)((i + 1) * nranks)) rc = 3;
+  }
+  munmap(m, 4096);
+  return rc;
+}
+
 HFM_API int hfm_lb_ipc_handle_bytes() { return (int)sizeof(hipIpcMemHandle_t); }
 
 // (Re)allocate this rank's staging (2 halves of `half` bytes) and export its IPC handle.  Every

@@ -266,6 +266,7 @@ _SIGS = {
     "hfm_decode_examples": [c_void_p, c_void_p, c_int, c_int, C.c_longlong, c_void_p, c_void_p, c_void_p,
                             c_void_p, c_int, c_void_p],
     "hfm_lb_shared_bytes": [],
+    "hfm_lb_barrier_selftest": [C.c_char_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int],
     "hfm_lb_create": [C.POINTER(c_void_p), c_int, c_int, C.c_char_p, c_int, c_int],
     "hfm_lb_ipc_handle_bytes": [],
     "hfm_lb_alloc_stage": [c_void_p, c_size_t, c_void_p],
