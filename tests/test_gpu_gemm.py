@@ -108,7 +108,7 @@ def test_lds_gemm_rejects_bad_shapes():
 def test_wide_tower_step_matches_register_tiles(monkeypatch, bn):
     """A per-layer (wide) tower trained with the LDS / ping-pong tiles equals the same model on the
     register-fed tiles to fp32 reassociation (split-K counts differ), batch norm included."""
-    import hipfm.models.deepfm as D
+    import hipfm.models.layers as D      # (the per-layer path's tile choices live there)
     from hipfm.data.synthetic import make_synth
     from hipfm.models.deepfm import NativeDeepFM
     from hipfm.models.reference import init_params
