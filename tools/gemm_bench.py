@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--k0", type=int, default=320)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--nodrop", action="store_true", help="forward epilogue without its dropout mask")
     args = ap.parse_args()
     import torch
     import hipfm  # noqa: F401
@@ -56,7 +57,7 @@ def main():
             ep = EpiArgs()
             ep.bias, ep.step, ep.out = bias.data_ptr(), step.data_ptr(), out.data_ptr()
             ep.out_t = out_t.data_ptr() if out_t is not None else 0
-            ep.scale, ep.keep_thr, ep.drop = 2.0, 0x7FFFFFFF, 1 if epi == KN.EPI_FWD else 0
+            ep.scale, ep.keep_thr, ep.drop = 2.0, 0x7FFFFFFF, 1 if (epi == KN.EPI_FWD and not args.nodrop) else 0
             if epi == KN.EPI_DGRAD:
                 ep.hprev = hprev.data_ptr()
             variants[f"tile{tile}" + {8: "_lds", 9: "_pp", 10: "_pp3", 11: "_rb", 12: "_p8", 13: "_r8"}.get(tile, "_old")] = (
