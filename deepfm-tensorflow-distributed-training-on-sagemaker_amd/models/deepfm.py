@@ -562,9 +562,16 @@ class NativeDeepFM(GraphRunnerMixin, NativeStateMixin, LayerPathMixin):
             t = LP._pick_tile(Mg, Ng, row_major_stream=False, Kd=Kd)
             if t not in (KN.TILE_LDS, KN.TILE_PP) and LP._LDS_GEMM and LP._lds_tile_ok(Mg, Ng, Kd, splitk=4):
                 t = KN.TILE_LDS     # (few output tiles, but the batch reduction splits 4+ ways)
-            s = LP._pick_splitk(Mg, Ng, Kd, t)
+            bm, bn = KN.TILES[t]
+            if t == KN.TILE_PP and LP._WG_DIRECT and (Mg // bm) * (Ng // bn) >= 256:
+                s = 0           # one 256x256 tile per CU already: unsplit, straight into g
+            else:
+                s = LP._pick_splitk(Mg, Ng, Kd, t)
             self.wg_cfg.append((t, s))
-        self.slabs = [torch.zeros(s, self.Np[i], self.Kp[i], **f32) for i, (t, s) in enumerate(self.wg_cfg)]
+        self.wg_direct = [s == 0 for (t, s) in self.wg_cfg]
+        self.wg_cfg = [(t, max(s, 1)) for (t, s) in self.wg_cfg]
+        self.slabs = [torch.zeros(0 if d else s, self.Np[i], self.Kp[i], **f32)
+                      for i, ((t, s), d) in enumerate(zip(self.wg_cfg, self.wg_direct))]
         # sparse path
         n = M * F
         gr = KN.grad_row_floats(K)

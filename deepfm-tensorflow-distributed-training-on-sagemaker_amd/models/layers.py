@@ -16,6 +16,7 @@ from ..utils.knobs import flag
 from ..utils.rng import keep_threshold
 
 _LDS_GEMM = flag("HIPFM_LDS_GEMM")           # wide per-layer GEMMs on the LDS-staged MFMA tiles
+_WG_DIRECT = flag("HIPFM_WG_DIRECT")         # unsplit wide wgrad stores straight into g
 
 
 def _lds_tile_ok(M: int, N: int, Kd: Optional[int], splitk: int = 1) -> bool:
@@ -185,7 +186,10 @@ class LayerPathMixin:
             Xt = self.Et if i == 0 else self.Ht[i - 1]
             t, s = self.wg_cfg[i]
             ep = EpiArgs()
-            ep.out = self.slabs[i].data_ptr()
+            if self.wg_direct[i]:       # unsplit: the GEMM writes the final gradient itself
+                ep.out = self.g.data_ptr() + 4 * self.dense_segs[f"Deep-part/mlp{i}/weights"].off
+            else:
+                ep.out = self.slabs[i].data_ptr()
             KN.gemm_nt(KN.EPI_F32, t, self.dZt[i], M, Xt, M, self.Np[i], self.Kp[i], M, s, ep)
             ep = EpiArgs()
             if i > 0 and self.batch_norm:
@@ -225,6 +229,8 @@ class LayerPathMixin:
         jobs = []
         maxn = 1
         for i in range(len(self.layers)):
+            if self.wg_direct[i]:
+                continue
             s = self.dense_segs[f"Deep-part/mlp{i}/weights"]
             n = self.Np[i] * self.Kp[i]
             nsl = self.wg_cfg[i][1]

@@ -81,6 +81,9 @@ KNOBS: Dict[str, Knob] = {
     "HIPFM_LDS_GEMM": Knob("1", "variant", "per-layer tower GEMMs with >= 256 128x128 output tiles on the "
                            "LDS-staged workgroup tile (mlp.hip gemm_lds_kernel); 0: the register-fed "
                            "32-row tiles (bitwise the same sums: tests/test_gpu_gemm.py)"),
+    "HIPFM_WG_DIRECT": Knob("1", "variant", "per-layer weight-gradient GEMMs on the 256x256 ping-pong "
+                            "tile with >= 256 output tiles run unsplit and store straight into the flat "
+                            "gradient (no slab, no finalize job); 0: split-K slabs summed by finalize"),
     "HIPFM_TABLE_LAYOUT": Knob("record", "variant", "record: one 128-B record per row (v, w, slots); "
                                "split: separate tables"),
     # ---- tuning

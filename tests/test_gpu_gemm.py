@@ -137,6 +137,33 @@ def test_wide_tower_step_matches_register_tiles(monkeypatch, bn):
     assert (v8 - v0).abs().max().item() <= 1e-4 * v0.abs().max().item()
 
 
+def test_wide_wgrad_direct_matches_split_slabs(monkeypatch):
+    """A 4096 x 4096 layer's weight gradient (256 ping-pong tiles) computed unsplit straight into
+    the flat gradient equals the split-K slabs summed by finalize, to fp32 reassociation."""
+    import hipfm.models.layers as D
+    from hipfm.data.synthetic import make_synth
+    from hipfm.models.deepfm import NativeDeepFM
+    from hipfm.models.reference import init_params
+    synth = make_synth("total:20000", seed=7)
+    F, K, layers, keep, B = synth.F, 8, [4096, 4096], [1.0, 1.0], 2048
+    params = init_params(synth.feature_size, F, K, layers, False, seed=3)
+    ids, vals, lab = synth.batch(B, step=0, device=DEV, id_dtype=torch.int32)
+    grads = []
+    for direct in (True, False):
+        monkeypatch.setattr(D, "_WG_DIRECT", direct)
+        m = NativeDeepFM(synth.feature_size, F, K, layers, keep, batch_size=B, device=DEV, init=False,
+                         batch_norm=False, learning_rate=1e-3, fused=False)
+        m.load_tf_params(params)
+        assert m.wg_direct == [False, direct]
+        m.train_step(ids, vals, lab)
+        torch.cuda.synchronize()
+        m.check_errors()
+        grads.append((m.g.clone(), m.p.clone()))
+    (gd, pd), (gs, ps) = grads
+    assert (gd - gs).abs().max().item() <= 1e-5 * gs.abs().max().item()
+    assert (pd - ps).abs().max().item() <= 1e-5 * ps.abs().max().item()
+
+
 @pytest.mark.parametrize("L,M,nvalid,train,dh", [(4096, 1024, 1000, True, False), (512, 200, 200, True, False),
                                                  (768, 256, 256, True, True), (1024, 128, 128, False, False),
                                                  (320, 192, 190, True, False)])
