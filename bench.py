@@ -421,7 +421,9 @@ def main():
                 "model": f"DeepFM {_SHAPE_NAMES.get(args.preset, args.preset)} (F={F}, V={synth.feature_size}, "
                          f"K={args.embedding_size}, deep {args.deep_layers}, keep {args.dropout}"
                          f"{', batch norm' if args.batch_norm else ''})",
-                "tower": "fused one-launch tower" if model.fused else "per-layer GEMMs (mlp.hip)",
+                "tower": "fused one-launch tower" if model.fused else (
+                    "per-layer: hipBLASLt GEMMs + mlp.hip epilogue passes" if getattr(model, "cbuf", None) is not None and model.cbuf.numel()
+                    else "per-layer GEMMs (mlp.hip)"),
                 "global_batch": world * B,
                 "per_gpu_batch": B,
                 "seq_len": None,

@@ -1055,6 +1055,75 @@ HFM_API int hfm_gemm_nt(int epi, int tile, const void* A, int lda, const void* B
 
 HFM_API int hfm_epi_args_bytes() { return (int)sizeof(EpiArgs); }
 
+// ------------------------------------------------------------------ stand-alone epilogue pass
+// The forward / dgrad epilogue over an fp32 product C [M, N] that a library GEMM (hipBLASLt via
+// torch.mm, bf16 operands, fp32 out) wrote: the same per-element values as epi_store /
+// epi_tile_lds (bias, relu, counter-hash dropout; dgrad scale, bf16 rounding, hprev>0 mask), the
+// row-major bf16 output in 16-byte stores, the transposed copy through a padded LDS tile.  One
+// 256-thread workgroup per 64 x 64 tile; M, N multiples of 64 (checked by the host entry).
+template <int EPI>
+__global__ void __launch_bounds__(256) epi_pass_kernel(const float* __restrict__ C, int M, int N, EpiArgs ep) {
+  __shared__ bf16 t[64][64 + 8];
+  const int tid = threadIdx.x;
+  const int row0 = blockIdx.y * 64, col0 = blockIdx.x * 64;
+  uint32_t salt = 0;
+  if (EPI == EPI_FWD && ep.drop) salt = dropout_salt(ep.seed, (uint32_t)(*ep.step), ep.layer);
+  const bool mask = EPI == EPI_DGRAD && ep.hprev != nullptr;
+  bf16* out = reinterpret_cast<bf16*>(ep.out);
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const int r = (tid >> 3) + 32 * p, c = (tid & 7) * 8;
+    const int row = row0 + r, col = col0 + c;
+    const size_t g = (size_t)row * N + col;
+    const float4 a0 = *reinterpret_cast<const float4*>(C + g);
+    const float4 a1 = *reinterpret_cast<const float4*>(C + g + 4);
+    const float a[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+    bf16x8 h;
+    if (mask) h = *reinterpret_cast<const bf16x8*>(ep.hprev + g);
+    bf16x8 o;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      float v = a[k];
+      if (EPI == EPI_FWD || EPI == EPI_FWD_EVAL) {
+        v = fmaxf(v + ep.bias[col + k], 0.f);
+        if (EPI == EPI_FWD && ep.drop)
+          v = dropout_keep((uint32_t)(row * N + col + k), salt, ep.keep_thr) ? v * ep.scale : 0.f;
+      } else {
+        v = v * ep.scale;
+        if (mask && !((float)h[k] > 0.f)) v = 0.f;
+      }
+      o[k] = f2bf(v);
+    }
+    *reinterpret_cast<bf16x8*>(out + g) = o;
+    *reinterpret_cast<bf16x8*>(&t[r][c]) = o;
+  }
+  if (!ep.out_t) return;
+  __syncthreads();
+  // transposed: thread -> column cc of the tile, 16 consecutive rows (32 contiguous bytes of out_t)
+  const int cc = tid >> 2, rr = (tid & 3) * 16;
+  bf16x8 o0, o1;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    o0[k] = t[rr + k][cc];
+    o1[k] = t[rr + 8 + k][cc];
+  }
+  bf16* dt = ep.out_t + (size_t)(col0 + cc) * M + row0 + rr;
+  *reinterpret_cast<bf16x8*>(dt) = o0;
+  *reinterpret_cast<bf16x8*>(dt + 8) = o1;
+}
+
+HFM_API int hfm_epi_pass(int epi, const float* C, int M, int N, const EpiArgs* ep, hipStream_t st) {
+  if (M <= 0 || N <= 0 || (M & 63) || (N & 63) || !ep->out) return (int)hipErrorInvalidValue;
+  const dim3 grid(N / 64, M / 64);
+  switch (epi) {
+    case EPI_FWD: epi_pass_kernel<EPI_FWD><<<grid, 256, 0, st>>>(C, M, N, *ep); break;
+    case EPI_FWD_EVAL: epi_pass_kernel<EPI_FWD_EVAL><<<grid, 256, 0, st>>>(C, M, N, *ep); break;
+    case EPI_DGRAD: epi_pass_kernel<EPI_DGRAD><<<grid, 256, 0, st>>>(C, M, N, *ep); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+  return (int)hipGetLastError();
+}
+
 // ------------------------------------------------------------------ K7 head
 // Per sample: y_d = h_L . w_out + b_out;  y = y_fm + y_d;  p = sigmoid(y);
 //   loss_b = BCE(y, label) (or (p-label)^2);  dlogit = dL/dy * gscale  (gscale = 1/global batch)

@@ -564,7 +564,10 @@ class NativeDeepFM(GraphRunnerMixin, NativeStateMixin, LayerPathMixin):
                 t = KN.TILE_LDS     # (few output tiles, but the batch reduction splits 4+ ways)
             bm, bn = KN.TILES[t]
             if t == KN.TILE_PP and LP._WG_DIRECT and (Mg // bm) * (Ng // bn) >= 256:
-                s = 0           # one 256x256 tile per CU already: unsplit, straight into g
+                # one 256x256 tile per CU already: unsplit, straight into g (the library GEMM by
+                # default; the 4096 x 384 layer-0 one stays on the split LDS tile + finalize: 90 +
+                # 14 us vs hipBLASLt's 107, profiles/r6tw_blas_kernels.md)
+                s = 0
             else:
                 s = LP._pick_splitk(Mg, Ng, Kd, t)
             self.wg_cfg.append((t, s))
@@ -572,6 +575,11 @@ class NativeDeepFM(GraphRunnerMixin, NativeStateMixin, LayerPathMixin):
         self.wg_cfg = [(t, max(s, 1)) for (t, s) in self.wg_cfg]
         self.slabs = [torch.zeros(0 if d else s, self.Np[i], self.Kp[i], **f32)
                       for i, ((t, s), d) in enumerate(zip(self.wg_cfg, self.wg_direct))]
+        # fp32 product scratch of the library-GEMM forward / dgrad (layers._epi_blas_ok)
+        cn = [] if (self.fused or self.batch_norm) else (
+            [self.Np[i] for i in range(len(self.layers)) if LP._epi_blas_ok(M, self.Np[i], self.Kp[i])]
+            + [self.Np[i - 1] for i in range(1, len(self.layers)) if LP._epi_blas_ok(M, self.Np[i - 1], self.Np[i])])
+        self.cbuf = torch.empty(M * max(cn) if cn else 0, **f32)
         # sparse path
         n = M * F
         gr = KN.grad_row_floats(K)

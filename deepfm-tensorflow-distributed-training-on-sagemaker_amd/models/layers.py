@@ -17,6 +17,8 @@ from ..utils.rng import keep_threshold
 
 _LDS_GEMM = flag("HIPFM_LDS_GEMM")           # wide per-layer GEMMs on the LDS-staged MFMA tiles
 _WG_DIRECT = flag("HIPFM_WG_DIRECT")         # unsplit wide wgrad stores straight into g
+_WG_BLAS = flag("HIPFM_WG_BLAS")             # ... as a plain library GEMM (no epilogue to fuse)
+_EPI_BLAS = flag("HIPFM_EPI_BLAS")           # wide fwd / dgrad: library GEMM + epilogue pass
 
 
 def _lds_tile_ok(M: int, N: int, Kd: Optional[int], splitk: int = 1) -> bool:
@@ -62,6 +64,12 @@ def _pick_tile(M: int, N: int, row_major_stream: bool = True, Kd: Optional[int] 
     return 3
 
 
+def _epi_blas_ok(M: int, N: int, Kd: int) -> bool:
+    """Wide forward / dgrad GEMMs (the 256 x 256 ping-pong tile's shapes, reduction >= 1024) as a
+    library GEMM into an fp32 scratch + the stand-alone epilogue pass (mlp.hip epi_pass_kernel)."""
+    return bool(_EPI_BLAS and Kd >= 1024 and _pick_tile(M, N, Kd=Kd) == KN.TILE_PP)
+
+
 def _pick_splitk(M: int, N: int, Kd: int, tile: int, target_blocks: int = 512,
                  max_split: int = 32) -> int:
     """Split the batch reduction of a weight-gradient GEMM: enough workgroups to fill the
@@ -103,6 +111,11 @@ class LayerPathMixin:
                 KN.gemm_nt(KN.EPI_RELU_F32, _pick_tile(M, N, Kd=self.Kp[i]), X, self.Kp[i], self.W16[i],
                            self.Kp[i], M, N, self.Kp[i], 1, ep)
                 self._bn_forward(i, B, train)
+            elif _epi_blas_ok(M, N, self.Kp[i]):
+                cf = self.cbuf[:M * N].view(M, N)
+                torch.mm(X.view(M, self.Kp[i]), self.W16[i].view(N, self.Kp[i]).t(), out_dtype=torch.float32,
+                         out=cf)
+                KN.epi_pass(KN.EPI_FWD if train else KN.EPI_FWD_EVAL, cf, M, N, ep)
             else:
                 KN.gemm_nt(KN.EPI_FWD if train else KN.EPI_FWD_EVAL, _pick_tile(M, N, Kd=self.Kp[i]), X,
                            self.Kp[i], self.W16[i], self.Kp[i], M, N, self.Kp[i], 1, ep)
@@ -186,11 +199,17 @@ class LayerPathMixin:
             Xt = self.Et if i == 0 else self.Ht[i - 1]
             t, s = self.wg_cfg[i]
             ep = EpiArgs()
-            if self.wg_direct[i]:       # unsplit: the GEMM writes the final gradient itself
-                ep.out = self.g.data_ptr() + 4 * self.dense_segs[f"Deep-part/mlp{i}/weights"].off
+            if self.wg_direct[i] and _WG_BLAS:
+                # a plain GEMM with nothing to fuse: bf16 operands, fp32 result written in place
+                go = self.dense_segs[f"Deep-part/mlp{i}/weights"].off
+                gw = self.g[go:go + self.Np[i] * self.Kp[i]].view(self.Np[i], self.Kp[i])
+                torch.mm(self.dZt[i], Xt.t(), out_dtype=torch.float32, out=gw)
             else:
-                ep.out = self.slabs[i].data_ptr()
-            KN.gemm_nt(KN.EPI_F32, t, self.dZt[i], M, Xt, M, self.Np[i], self.Kp[i], M, s, ep)
+                if self.wg_direct[i]:   # unsplit: the GEMM writes the final gradient itself
+                    ep.out = self.g.data_ptr() + 4 * self.dense_segs[f"Deep-part/mlp{i}/weights"].off
+                else:
+                    ep.out = self.slabs[i].data_ptr()
+                KN.gemm_nt(KN.EPI_F32, t, self.dZt[i], M, Xt, M, self.Np[i], self.Kp[i], M, s, ep)
             ep = EpiArgs()
             if i > 0 and self.batch_norm:
                 ep.out = self.dH[i - 1].data_ptr()    # f32 dL/dH_{i-1}; BN backward masks it
@@ -204,8 +223,14 @@ class LayerPathMixin:
                 ep.out = self.dZ[i - 1].data_ptr()
                 ep.out_t = self.dZt[i - 1].data_ptr()
                 N = self.Np[i - 1]
-                KN.gemm_nt(KN.EPI_DGRAD, _pick_tile(M, N, Kd=self.Np[i]), self.dZ[i], self.Np[i], self.WT16[i],
-                           self.Np[i], M, N, self.Np[i], 1, ep)
+                if _epi_blas_ok(M, N, self.Np[i]):
+                    cf = self.cbuf[:M * N].view(M, N)
+                    torch.mm(self.dZ[i].view(M, self.Np[i]), self.WT16[i].view(N, self.Np[i]).t(),
+                             out_dtype=torch.float32, out=cf)
+                    KN.epi_pass(KN.EPI_DGRAD, cf, M, N, ep)
+                else:
+                    KN.gemm_nt(KN.EPI_DGRAD, _pick_tile(M, N, Kd=self.Np[i]), self.dZ[i], self.Np[i],
+                               self.WT16[i], self.Np[i], M, N, self.Np[i], 1, ep)
             else:
                 ep.out = self.dX0.data_ptr()          # hprev = 0: unmasked bf16 store
                 ep.scale = 1.0

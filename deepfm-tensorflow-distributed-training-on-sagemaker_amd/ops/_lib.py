@@ -236,6 +236,7 @@ _SIGS = {
     "hfm_opt_hyper_bytes": [],
     "hfm_gemm_nt": [c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int,
                     C.POINTER(EpiArgs), c_void_p],
+    "hfm_epi_pass": [c_int, c_void_p, c_int, c_int, C.POINTER(EpiArgs), c_void_p],
     "hfm_epi_args_bytes": [],
     "hfm_head": [C.POINTER(HeadArgs), c_void_p],
     "hfm_shadow_transpose": [c_void_p, c_int, c_int, c_void_p],

@@ -444,6 +444,14 @@ def gemm_nt(epi, tile, A, lda, B, ldb, M, N, Kd, splitk, ep: EpiArgs):
                           stream_handle()), f"gemm_nt(epi={epi},tile={tile},M={M},N={N},K={Kd})")
 
 
+def epi_pass(epi, Cf32, M, N, ep: EpiArgs):
+    """The forward / dgrad epilogue (EPI_FWD, EPI_FWD_EVAL, EPI_DGRAD) over an fp32 product
+    ``Cf32`` [M, N] from a library GEMM: mlp.hip epi_pass_kernel, the same values as the fused
+    epilogues of gemm_nt."""
+    check(L().hfm_epi_pass(epi, ptr(Cf32), M, N, C.byref(ep), stream_handle()),
+          f"epi_pass(epi={epi},M={M},N={N})")
+
+
 def head(a: HeadArgs):
     check(L().hfm_head(C.byref(a), stream_handle()), "head")
 

@@ -84,6 +84,15 @@ KNOBS: Dict[str, Knob] = {
     "HIPFM_WG_DIRECT": Knob("1", "variant", "per-layer weight-gradient GEMMs on the 256x256 ping-pong "
                             "tile with >= 256 output tiles run unsplit and store straight into the flat "
                             "gradient (no slab, no finalize job); 0: split-K slabs summed by finalize"),
+    "HIPFM_WG_BLAS": Knob("1", "variant", "the unsplit wide weight gradients (HIPFM_WG_DIRECT) as a plain "
+                          "library GEMM (torch.mm bf16 -> fp32 out, hipBLASLt) into the flat gradient -- no "
+                          "epilogue to fuse there (4096x3 tower 4.28 -> 3.98 ms/step, same losses: "
+                          "profiles/r6_wgrad_blas_ab.log); 0: the 256x256 ping-pong tile"),
+    "HIPFM_EPI_BLAS": Knob("1", "variant", "wide per-layer forward / dgrad GEMMs (256x256 ping-pong shapes, "
+                           "reduction >= 1024) as a library GEMM (torch.mm, fp32 out) + the stand-alone "
+                           "epilogue pass (mlp.hip epi_pass_kernel): 4096x3 tower 3.89-3.91 -> 3.49-3.50 "
+                           "ms/step, bitwise the same losses (profiles/r6_epi_blas_ab.log); 0: the "
+                           "fused-epilogue ping-pong tile (0.63-0.66x hipBLASLt)"),
     "HIPFM_TABLE_LAYOUT": Knob("record", "variant", "record: one 128-B record per row (v, w, slots); "
                                "split: separate tables"),
     # ---- tuning

@@ -95,6 +95,71 @@ def test_lds_gemm_epilogues_match_register_tile(tile, epi):
         assert torch.equal(ot8.t(), o8)                  # the transposed copy
 
 
+@pytest.mark.parametrize("epi", ["fwd", "fwd_eval", "dgrad", "dgrad_nomask"])
+def test_epi_pass_matches_fused_epilogue(epi):
+    """mlp.hip epi_pass_kernel over the fp32 product equals the fused epilogue of the same GEMM
+    (register tile: the F32 output is exactly its accumulator), bit for bit, out and out_t."""
+    M, N, K = 512, 256, 640
+    A, B = _ops(M, N, K, seed=11)
+    bias = torch.randn(N, device=DEV)
+    step = torch.tensor([5], dtype=torch.int64, device=DEV)
+    hprev = torch.randn(M, N, device=DEV).bfloat16()
+    kind = {"fwd": KN.EPI_FWD, "fwd_eval": KN.EPI_FWD_EVAL, "dgrad": KN.EPI_DGRAD,
+            "dgrad_nomask": KN.EPI_DGRAD}[epi]
+    cf = torch.zeros(M, N, device=DEV)
+    e0 = EpiArgs()
+    e0.out = cf.data_ptr()
+    KN.gemm_nt(KN.EPI_F32, 0, A, K, B, K, M, N, K, 1, e0)
+    outs = []
+    for fused in (True, False):
+        o = torch.zeros(M, N, device=DEV, dtype=torch.bfloat16)
+        ot = torch.zeros(N, M, device=DEV, dtype=torch.bfloat16)
+        ep = EpiArgs()
+        ep.bias, ep.step, ep.out, ep.out_t = bias.data_ptr(), step.data_ptr(), o.data_ptr(), ot.data_ptr()
+        ep.seed, ep.layer, ep.keep_thr, ep.drop, ep.scale = 99, 2, keep_threshold(0.5), 1, 2.0
+        if epi == "dgrad":
+            ep.hprev = hprev.data_ptr()
+        if fused:
+            KN.gemm_nt(kind, 0, A, K, B, K, M, N, K, 1, ep)
+        else:
+            KN.epi_pass(kind, cf, M, N, ep)
+        torch.cuda.synchronize()
+        outs.append((o, ot))
+    (o1, t1), (o2, t2) = outs
+    assert torch.equal(o1, o2) and torch.equal(t1, t2)
+    assert torch.equal(t2.t(), o2)
+    if epi == "dgrad":
+        assert (o2[hprev <= 0] == 0).all() and (o2 != 0).any()
+
+
+def test_wide_tower_library_gemm_matches_fused_tiles(monkeypatch):
+    """The 4096-wide tower with its forward / dgrad GEMMs as library GEMM + epilogue pass trains
+    like the fused-epilogue ping-pong tiles (fp32 accumulation order may differ)."""
+    import hipfm.models.layers as D
+    from hipfm.data.synthetic import make_synth
+    from hipfm.models.deepfm import NativeDeepFM
+    from hipfm.models.reference import init_params
+    synth = make_synth("total:20000", seed=9)
+    F, K, layers, keep, B = synth.F, 8, [4096, 4096, 4096], [0.5, 0.5, 0.5], 2048
+    params = init_params(synth.feature_size, F, K, layers, False, seed=4)
+    data = [synth.batch(B, step=s, device=DEV, id_dtype=torch.int32) for s in range(2)]
+    outs = []
+    for lib in (True, False):
+        monkeypatch.setattr(D, "_EPI_BLAS", lib)
+        m = NativeDeepFM(synth.feature_size, F, K, layers, keep, batch_size=B, device=DEV, init=False,
+                         batch_norm=False, learning_rate=1e-3, fused=False)
+        m.load_tf_params(params)
+        assert (m.cbuf.numel() > 0) == lib
+        for ids, vals, lab in data:
+            m.train_step(ids, vals, lab)
+        torch.cuda.synchronize()
+        m.check_errors()
+        outs.append((m.p.clone(), m.tv[:synth.feature_size].clone(), m.H[2].clone()))
+    (p1, v1, h1), (p0, v0, h0) = outs
+    assert (p1 - p0).abs().max().item() <= 1e-4 * p0.abs().max().item()
+    assert (v1 - v0).abs().max().item() <= 1e-4 * v0.abs().max().item()
+
+
 def test_lds_gemm_rejects_bad_shapes():
     A, B = _ops(256, 256, 96)
     ep = EpiArgs()
@@ -137,9 +202,11 @@ def test_wide_tower_step_matches_register_tiles(monkeypatch, bn):
     assert (v8 - v0).abs().max().item() <= 1e-4 * v0.abs().max().item()
 
 
-def test_wide_wgrad_direct_matches_split_slabs(monkeypatch):
+@pytest.mark.parametrize("blas", [False, True])
+def test_wide_wgrad_direct_matches_split_slabs(monkeypatch, blas):
     """A 4096 x 4096 layer's weight gradient (256 ping-pong tiles) computed unsplit straight into
-    the flat gradient equals the split-K slabs summed by finalize, to fp32 reassociation."""
+    the flat gradient -- by the ping-pong tile or (blas) the library GEMM -- equals the split-K
+    slabs summed by finalize, to fp32 reassociation."""
     import hipfm.models.layers as D
     from hipfm.data.synthetic import make_synth
     from hipfm.models.deepfm import NativeDeepFM
@@ -149,6 +216,7 @@ def test_wide_wgrad_direct_matches_split_slabs(monkeypatch):
     params = init_params(synth.feature_size, F, K, layers, False, seed=3)
     ids, vals, lab = synth.batch(B, step=0, device=DEV, id_dtype=torch.int32)
     grads = []
+    monkeypatch.setattr(D, "_WG_BLAS", blas)
     for direct in (True, False):
         monkeypatch.setattr(D, "_WG_DIRECT", direct)
         m = NativeDeepFM(synth.feature_size, F, K, layers, keep, batch_size=B, device=DEV, init=False,
