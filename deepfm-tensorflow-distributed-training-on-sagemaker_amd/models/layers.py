@@ -214,8 +214,12 @@ class LayerPathMixin:
             if i > 0 and self.batch_norm:
                 ep.out = self.dH[i - 1].data_ptr()    # f32 dL/dH_{i-1}; BN backward masks it
                 N = self.Np[i - 1]
-                KN.gemm_nt(KN.EPI_F32, _pick_tile(M, N, Kd=self.Np[i]), self.dZ[i], self.Np[i], self.WT16[i],
-                           self.Np[i], M, N, self.Np[i], 1, ep)
+                if _epi_blas_ok(M, N, self.Np[i]):    # a plain GEMM: nothing to fuse
+                    torch.mm(self.dZ[i].view(M, self.Np[i]), self.WT16[i].view(N, self.Np[i]).t(),
+                             out_dtype=torch.float32, out=self.dH[i - 1].view(M, N))
+                else:
+                    KN.gemm_nt(KN.EPI_F32, _pick_tile(M, N, Kd=self.Np[i]), self.dZ[i], self.Np[i],
+                               self.WT16[i], self.Np[i], M, N, self.Np[i], 1, ep)
             elif i > 0:
                 keep = self.keep[i - 1]
                 ep.hprev = self.H[i - 1].data_ptr()

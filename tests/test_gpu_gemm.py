@@ -132,24 +132,26 @@ def test_epi_pass_matches_fused_epilogue(epi):
         assert (o2[hprev <= 0] == 0).all() and (o2 != 0).any()
 
 
-def test_wide_tower_library_gemm_matches_fused_tiles(monkeypatch):
-    """The 4096-wide tower with its forward / dgrad GEMMs as library GEMM + epilogue pass trains
-    like the fused-epilogue ping-pong tiles (fp32 accumulation order may differ)."""
+@pytest.mark.parametrize("bn", [False, True])
+def test_wide_tower_library_gemm_matches_fused_tiles(monkeypatch, bn):
+    """The 4096-wide tower with its forward / dgrad GEMMs as library GEMM + epilogue pass (batch
+    norm: the plain fp32 dgrad GEMM) trains like the hand-written ping-pong tiles (fp32
+    accumulation order may differ)."""
     import hipfm.models.layers as D
     from hipfm.data.synthetic import make_synth
     from hipfm.models.deepfm import NativeDeepFM
     from hipfm.models.reference import init_params
     synth = make_synth("total:20000", seed=9)
     F, K, layers, keep, B = synth.F, 8, [4096, 4096, 4096], [0.5, 0.5, 0.5], 2048
-    params = init_params(synth.feature_size, F, K, layers, False, seed=4)
+    params = init_params(synth.feature_size, F, K, layers, bn, seed=4)
     data = [synth.batch(B, step=s, device=DEV, id_dtype=torch.int32) for s in range(2)]
     outs = []
     for lib in (True, False):
         monkeypatch.setattr(D, "_EPI_BLAS", lib)
         m = NativeDeepFM(synth.feature_size, F, K, layers, keep, batch_size=B, device=DEV, init=False,
-                         batch_norm=False, learning_rate=1e-3, fused=False)
+                         batch_norm=bn, learning_rate=1e-3, fused=False)
         m.load_tf_params(params)
-        assert (m.cbuf.numel() > 0) == lib
+        assert (m.cbuf.numel() > 0) == (lib and not bn)
         for ids, vals, lab in data:
             m.train_step(ids, vals, lab)
         torch.cuda.synchronize()
