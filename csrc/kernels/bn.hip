@@ -157,6 +157,11 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(BnArgs a) {
   const size_t o = (size_t)row * N + cb;
   const f32x4 xr0 = *reinterpret_cast<const f32x4*>(a.r + o);
   const f32x4 xr1 = *reinterpret_cast<const f32x4*>(a.r + o + 4);
+  f32x4 d0 = {0.f, 0.f, 0.f, 0.f}, d1 = d0;      // dL/dh in 16-byte loads, issued with r's
+  if (BWD) {
+    d0 = *reinterpret_cast<const f32x4*>(a.dh + o);
+    d1 = *reinterpret_cast<const f32x4*>(a.dh + o + 4);
+  }
   bf16x8 ov;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -165,7 +170,7 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(BnArgs a) {
     float v;
     if (BWD) {
       if (row < a.nvalid && x > 0.f) {
-        const float dy = a.dh[o + j] * drop_factor(a, salt, row, col);
+        const float dy = (j < 4 ? d0[j] : d1[j - 4]) * drop_factor(a, salt, row, col);
         const float xhat = (x - sv[col]) * sv[N + col];
         v = sv[2 * N + col] * (dy - sv[4 * N + col] - xhat * sv[5 * N + col]);
       } else {
