@@ -44,45 +44,72 @@ __device__ __forceinline__ float drop_factor(const BnArgs& a, uint32_t salt, int
   return dropout_keep((uint32_t)(row * a.N + col), salt, a.keep_thr) ? a.inv_keep : 0.f;
 }
 
-// grid (M/64, N/32), 256 threads: 32 columns x 8 row-groups of 8 rows.
-template <int BWD>
+// grid (M/64, N/(32 CPT)), 256 threads: 32 column groups of CPT adjacent columns x 8 row-groups
+// of 8 rows.  CPT = 4 (N % 128 == 0): 16-byte loads of r / dh; every column's sums take the same
+// order for either CPT (8 rows in sequence per row-group, then the fixed 8-way tree), so both
+// variants write bitwise the same partials.
+template <int BWD, int CPT>
 __global__ void __launch_bounds__(256) bn_partial_kernel(BnArgs a) {
-  __shared__ float red[2][8][32];
+  typedef float vecT __attribute__((ext_vector_type(CPT)));
+  __shared__ float red[2][8][32 * CPT];
   const int c = threadIdx.x & 31, rg = threadIdx.x >> 5;
-  const int col = blockIdx.y * 32 + c;
+  const int col = blockIdx.y * 32 * CPT + c * CPT;
   const int r0 = blockIdx.x * 64 + rg * 8;
   const float* sv = a.save;
-  float mean = 0.f, rstd = 0.f;
+  float mean[CPT], rstd[CPT];
   uint32_t salt = 0;
+#pragma unroll
+  for (int q = 0; q < CPT; ++q) mean[q] = rstd[q] = 0.f;
   if (BWD) {
-    mean = sv[col];
-    rstd = sv[a.N + col];
+#pragma unroll
+    for (int q = 0; q < CPT; ++q) {
+      mean[q] = sv[col + q];
+      rstd[q] = sv[a.N + col + q];
+    }
     if (a.drop) salt = dropout_salt(a.seed, (uint32_t)(*a.step), a.layer);
   }
-  float s0 = 0.f, s1 = 0.f;
+  float s0[CPT], s1[CPT];
+#pragma unroll
+  for (int q = 0; q < CPT; ++q) s0[q] = s1[q] = 0.f;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const int row = r0 + j;
     if (row < a.nvalid) {
       const size_t o = (size_t)row * a.N + col;
-      const float x = a.r[o];
-      if (BWD) {
-        const float dy = a.dh[o] * drop_factor(a, salt, row, col);
-        s0 += dy;
-        s1 += dy * (x - mean) * rstd;
+      vecT x, d;
+      if (CPT == 1) {
+        x[0] = a.r[o];
+        if (BWD) d[0] = a.dh[o];
       } else {
-        s0 += x;
-        s1 += x * x;
+        x = *reinterpret_cast<const vecT*>(a.r + o);
+        if (BWD) d = *reinterpret_cast<const vecT*>(a.dh + o);
+      }
+#pragma unroll
+      for (int q = 0; q < CPT; ++q) {
+        if (BWD) {
+          const float dy = d[q] * drop_factor(a, salt, row, col + q);
+          s0[q] += dy;
+          s1[q] += dy * (x[q] - mean[q]) * rstd[q];
+        } else {
+          s0[q] += x[q];
+          s1[q] += x[q] * x[q];
+        }
       }
     }
   }
-  red[0][rg][c] = s0;
-  red[1][rg][c] = s1;
+#pragma unroll
+  for (int q = 0; q < CPT; ++q) {
+    red[0][rg][c * CPT + q] = s0[q];
+    red[1][rg][c * CPT + q] = s1[q];
+  }
   __syncthreads();
-  if (rg < 2) {
-    const float* v = red[rg][0] + c;
-    const float t = ((v[0] + v[32]) + (v[64] + v[96])) + ((v[128] + v[160]) + (v[192] + v[224]));
-    a.part[(size_t)blockIdx.x * 2 * a.N + rg * a.N + col] = t;
+  // 2 x 32 CPT output columns: thread -> (sum kind, column)
+  for (int e = threadIdx.x; e < 2 * 32 * CPT; e += 256) {
+    const int k = e / (32 * CPT), cc = e % (32 * CPT);
+    const float* v = &red[k][0][cc];
+    constexpr int S = 32 * CPT;
+    const float t = ((v[0] + v[S]) + (v[2 * S] + v[3 * S])) + ((v[4 * S] + v[5 * S]) + (v[6 * S] + v[7 * S]));
+    a.part[(size_t)blockIdx.x * 2 * a.N + k * a.N + blockIdx.y * 32 * CPT + cc] = t;
   }
 }
 
@@ -202,11 +229,17 @@ HFM_API int hfm_bn(int phase, const BnArgs* ap, hipStream_t st) {
   const dim3 tiles(a.M / 64, a.N / 32);
   const int nrow = a.M / 64;
   switch (phase) {
-    case 0: hipLaunchKernelGGL(bn_partial_kernel<0>, tiles, dim3(256), 0, st, a); break;
+    case 0:
+      if (a.N % 128 == 0) hipLaunchKernelGGL((bn_partial_kernel<0, 4>), dim3(a.M / 64, a.N / 128), dim3(256), 0, st, a);
+      else hipLaunchKernelGGL((bn_partial_kernel<0, 1>), tiles, dim3(256), 0, st, a);
+      break;
     case 1: hipLaunchKernelGGL(bn_finalize_kernel<0>, dim3(a.N / 32), dim3(256), 0, st, a, nrow); break;
     case 2: hipLaunchKernelGGL(bn_finalize_kernel<1>, dim3(a.N / 32), dim3(256), 0, st, a, nrow); break;
     case 3: hipLaunchKernelGGL(bn_apply_kernel<0>, tiles, dim3(256), 0, st, a); break;
-    case 4: hipLaunchKernelGGL(bn_partial_kernel<1>, tiles, dim3(256), 0, st, a); break;
+    case 4:
+      if (a.N % 128 == 0) hipLaunchKernelGGL((bn_partial_kernel<1, 4>), dim3(a.M / 64, a.N / 128), dim3(256), 0, st, a);
+      else hipLaunchKernelGGL((bn_partial_kernel<1, 1>), tiles, dim3(256), 0, st, a);
+      break;
     case 5: hipLaunchKernelGGL(bn_finalize_kernel<2>, dim3(a.N / 32), dim3(256), 0, st, a, nrow); break;
     case 6: hipLaunchKernelGGL(bn_apply_kernel<1>, tiles, dim3(256), 0, st, a); break;
     default: return (int)hipErrorInvalidValue;
