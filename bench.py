@@ -66,12 +66,22 @@ _SHAPE_NAMES = {"criteo_1tb": "Criteo-1TB-shape", "criteo_kaggle": "Criteo-Kaggl
 
 
 def _free_port() -> int:
+    """A rendezvous port below the kernel's ephemeral range (hipfm/utils/net.py says why), checked
+    by a bind; inlined so the supervisor process imports nothing of the package."""
+    import random
     import socket
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+    rnd = random.SystemRandom()
+    for _ in range(64):
+        p = rnd.randrange(20000, 32000)
+        with socket.socket() as s:
+            try:
+                s.bind(("127.0.0.1", p))
+            except OSError:
+                continue
+            return p
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
 
 
 def supervise(argv) -> int:

@@ -23,8 +23,9 @@ from hipfm.parallel.dist import Comm  # noqa: E402
 @pytest.fixture(scope="module")
 def group():
     if not dist.is_initialized():
+        from hipfm.utils.net import free_port
         s = socket.socket()
-        s.bind(("127.0.0.1", 0))
+        s.bind(("127.0.0.1", free_port()))
         port = s.getsockname()[1]
         s.close()
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1",

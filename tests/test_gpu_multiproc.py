@@ -30,8 +30,9 @@ DEV = torch.device("cuda", 0)
 
 def _free_port() -> int:
     import socket
+    from hipfm.utils.net import free_port
     s = socket.socket()
-    s.bind(("127.0.0.1", 0))
+    s.bind(("127.0.0.1", free_port()))
     p = s.getsockname()[1]
     s.close()
     return p

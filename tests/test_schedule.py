@@ -14,8 +14,9 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _port():
+    from hipfm.utils.net import free_port
     s = socket.socket()
-    s.bind(("127.0.0.1", 0))
+    s.bind(("127.0.0.1", free_port()))
     p = s.getsockname()[1]
     s.close()
     return p
