@@ -219,6 +219,82 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(BnArgs a) {
   *reinterpret_cast<bf16x8*>(a.out_t + (size_t)(blockIdx.y * 32 + tc) * a.M + blockIdx.x * 64 + tr) = w;
 }
 
+// The same per-element values as bn_apply_kernel over 64 x 64 tiles (N % 64 == 0): two 8-column
+// row pieces per thread, every load (r, dh, the per-column statistics) in 16-byte vectors, the
+// transposed copy through a padded LDS tile with 32 contiguous bytes of out_t per thread.
+template <int BWD>
+__global__ void __launch_bounds__(256) bn_apply64_kernel(BnArgs a) {
+  __shared__ bf16 tile[64][64 + 8];
+  const int t = threadIdx.x;
+  const int row0 = blockIdx.x * 64, col0 = blockIdx.y * 64;
+  const int N = a.N;
+  const float* sv = a.save;
+  uint32_t salt = 0;
+  if (a.drop) salt = dropout_salt(a.seed, (uint32_t)(*a.step), a.layer);
+  const int c = (t & 7) * 8, cb = col0 + c;
+  // per-column statistics of the thread's 8 columns (the same for both row pieces)
+  f32x4 s2[2], s3[2], s0[2], s1[2], s4[2], s5[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    s2[h] = *reinterpret_cast<const f32x4*>(sv + 2 * N + cb + 4 * h);
+    if (BWD) {
+      s0[h] = *reinterpret_cast<const f32x4*>(sv + cb + 4 * h);
+      s1[h] = *reinterpret_cast<const f32x4*>(sv + N + cb + 4 * h);
+      s4[h] = *reinterpret_cast<const f32x4*>(sv + 4 * N + cb + 4 * h);
+      s5[h] = *reinterpret_cast<const f32x4*>(sv + 5 * N + cb + 4 * h);
+    } else {
+      s3[h] = *reinterpret_cast<const f32x4*>(sv + 3 * N + cb + 4 * h);
+    }
+  }
+  f32x4 xr[2][2], dr[2][2];
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const size_t o = (size_t)(row0 + (t >> 3) + 32 * p) * N + cb;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      xr[p][h] = *reinterpret_cast<const f32x4*>(a.r + o + 4 * h);
+      if (BWD) dr[p][h] = *reinterpret_cast<const f32x4*>(a.dh + o + 4 * h);
+    }
+  }
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const int lr = (t >> 3) + 32 * p, row = row0 + lr;
+    bf16x8 ov;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int col = cb + j, h = j >> 2, q = j & 3;
+      const float x = xr[p][h][q];
+      float v;
+      if (BWD) {
+        if (row < a.nvalid && x > 0.f) {
+          const float dy = dr[p][h][q] * drop_factor(a, salt, row, col);
+          const float xhat = (x - s0[h][q]) * s1[h][q];
+          v = s2[h][q] * (dy - s4[h][q] - xhat * s5[h][q]);
+        } else {
+          v = 0.f;
+        }
+      } else {
+        v = (x * s2[h][q] + s3[h][q]) * drop_factor(a, salt, row, col);
+      }
+      ov[j] = f2bf(v);
+    }
+    *reinterpret_cast<bf16x8*>(a.out + (size_t)row * N + cb) = ov;
+    *reinterpret_cast<bf16x8*>(&tile[lr][c]) = ov;
+  }
+  if (!a.out_t) return;
+  __syncthreads();
+  const int cc = t >> 2, rr = (t & 3) * 16;
+  bf16x8 w0, w1;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    w0[k] = tile[rr + k][cc];
+    w1[k] = tile[rr + 8 + k][cc];
+  }
+  bf16* dt = a.out_t + (size_t)(col0 + cc) * a.M + row0 + rr;
+  *reinterpret_cast<bf16x8*>(dt) = w0;
+  *reinterpret_cast<bf16x8*>(dt + 8) = w1;
+}
+
 static bool bn_shape_ok(const BnArgs& a) { return a.M % 64 == 0 && a.N % 32 == 0 && a.M > 0 && a.N > 0; }
 
 // phase: 0 fwd partial, 1 fwd finalize (train), 2 eval finalize, 3 fwd apply,
@@ -235,13 +311,19 @@ HFM_API int hfm_bn(int phase, const BnArgs* ap, hipStream_t st) {
       break;
     case 1: hipLaunchKernelGGL(bn_finalize_kernel<0>, dim3(a.N / 32), dim3(256), 0, st, a, nrow); break;
     case 2: hipLaunchKernelGGL(bn_finalize_kernel<1>, dim3(a.N / 32), dim3(256), 0, st, a, nrow); break;
-    case 3: hipLaunchKernelGGL(bn_apply_kernel<0>, tiles, dim3(256), 0, st, a); break;
+    case 3:
+      if (a.N % 64 == 0) hipLaunchKernelGGL(bn_apply64_kernel<0>, dim3(a.M / 64, a.N / 64), dim3(256), 0, st, a);
+      else hipLaunchKernelGGL(bn_apply_kernel<0>, tiles, dim3(256), 0, st, a);
+      break;
     case 4:
       if (a.N % 128 == 0) hipLaunchKernelGGL((bn_partial_kernel<1, 4>), dim3(a.M / 64, a.N / 128), dim3(256), 0, st, a);
       else hipLaunchKernelGGL((bn_partial_kernel<1, 1>), tiles, dim3(256), 0, st, a);
       break;
     case 5: hipLaunchKernelGGL(bn_finalize_kernel<2>, dim3(a.N / 32), dim3(256), 0, st, a, nrow); break;
-    case 6: hipLaunchKernelGGL(bn_apply_kernel<1>, tiles, dim3(256), 0, st, a); break;
+    case 6:
+      if (a.N % 64 == 0) hipLaunchKernelGGL(bn_apply64_kernel<1>, dim3(a.M / 64, a.N / 64), dim3(256), 0, st, a);
+      else hipLaunchKernelGGL(bn_apply_kernel<1>, tiles, dim3(256), 0, st, a);
+      break;
     default: return (int)hipErrorInvalidValue;
   }
   HFM_LAUNCH_CHECK();
