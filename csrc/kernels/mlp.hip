@@ -1070,6 +1070,12 @@ __global__ void __launch_bounds__(256) epi_pass_kernel(const float* __restrict__
   if (EPI == EPI_FWD && ep.drop) salt = dropout_salt(ep.seed, (uint32_t)(*ep.step), ep.layer);
   const bool mask = EPI == EPI_DGRAD && ep.hprev != nullptr;
   bf16* out = reinterpret_cast<bf16*>(ep.out);
+  // the thread's 8 bias values (the same columns in both row pieces) in two 16-byte loads
+  f32x4 bv[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+  if (EPI == EPI_FWD || EPI == EPI_FWD_EVAL) {
+    bv[0] = *reinterpret_cast<const f32x4*>(ep.bias + col0 + (tid & 7) * 8);
+    bv[1] = *reinterpret_cast<const f32x4*>(ep.bias + col0 + (tid & 7) * 8 + 4);
+  }
 #pragma unroll
   for (int p = 0; p < 2; ++p) {
     const int r = (tid >> 3) + 32 * p, c = (tid & 7) * 8;
@@ -1085,7 +1091,7 @@ __global__ void __launch_bounds__(256) epi_pass_kernel(const float* __restrict__
     for (int k = 0; k < 8; ++k) {
       float v = a[k];
       if (EPI == EPI_FWD || EPI == EPI_FWD_EVAL) {
-        v = fmaxf(v + ep.bias[col + k], 0.f);
+        v = fmaxf(v + bv[k >> 2][k & 3], 0.f);
         if (EPI == EPI_FWD && ep.drop)
           v = dropout_keep((uint32_t)(row * N + col + k), salt, ep.keep_thr) ? v * ep.scale : 0.f;
       } else {
