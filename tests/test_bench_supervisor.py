@@ -24,7 +24,9 @@ def _port():
     return p
 
 
-def _run(fake, hang_s="4", first_s="6"):
+def _run(fake, hang_s="4", first_s="20"):
+    # first_s: a healthy fake child marks progress within a second, but a loaded host (right after
+    # a parallel hipcc build) has delayed that start past 6 s -- the rung then fell back early
     env = dict(os.environ, HIPFM_BENCH_FAKE=fake, HIPFM_BENCH_HANG_S=hang_s, HIPFM_BENCH_FIRST_S=first_s)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(REPO, "bench.py"),
