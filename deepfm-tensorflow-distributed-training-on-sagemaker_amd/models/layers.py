@@ -19,6 +19,7 @@ _LDS_GEMM = flag("HIPFM_LDS_GEMM")           # wide per-layer GEMMs on the LDS-s
 _WG_DIRECT = flag("HIPFM_WG_DIRECT")         # unsplit wide wgrad stores straight into g
 _WG_BLAS = flag("HIPFM_WG_BLAS")             # ... as a plain library GEMM (no epilogue to fuse)
 _EPI_BLAS = flag("HIPFM_EPI_BLAS")           # wide fwd / dgrad: library GEMM + epilogue pass
+_DX0_BLAS = flag("HIPFM_DX0_BLAS")           # the wide tower's dX0 as a library GEMM (bf16 out)
 
 
 def _lds_tile_ok(M: int, N: int, Kd: Optional[int], splitk: int = 1) -> bool:
@@ -235,6 +236,10 @@ class LayerPathMixin:
                 else:
                     KN.gemm_nt(KN.EPI_DGRAD, _pick_tile(M, N, Kd=self.Np[i]), self.dZ[i], self.Np[i],
                                self.WT16[i], self.Np[i], M, N, self.Np[i], 1, ep)
+            elif _DX0_BLAS and self.Np[0] >= 1024 and not self.batch_norm:
+                # unmasked, unscaled bf16 product: a plain library GEMM with a bf16 result
+                torch.mm(self.dZ[0].view(M, self.Np[0]), self.WT16[0].view(self.K0p, self.Np[0]).t(),
+                         out=self.dX0.view(M, self.K0p))
             else:
                 ep.out = self.dX0.data_ptr()          # hprev = 0: unmasked bf16 store
                 ep.scale = 1.0

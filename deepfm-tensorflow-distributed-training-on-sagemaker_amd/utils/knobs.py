@@ -93,6 +93,9 @@ KNOBS: Dict[str, Knob] = {
                            "epilogue pass (mlp.hip epi_pass_kernel): 4096x3 tower 3.89-3.91 -> 3.49-3.50 "
                            "ms/step, bitwise the same losses (profiles/r6_epi_blas_ab.log); 0: the "
                            "fused-epilogue ping-pong tile (0.63-0.66x hipBLASLt)"),
+    "HIPFM_DX0_BLAS": Knob("1", "variant", "per-layer wide tower (first layer >= 1024 units): dX0 (unmasked "
+                           "bf16 product) as a library GEMM with a bf16 result, 58 vs 81 us at 16384x384x4096, "
+                           "same losses (profiles/r6_dx0_blas_ab.log); 0: the LDS tile"),
     "HIPFM_TABLE_LAYOUT": Knob("record", "variant", "record: one 128-B record per row (v, w, slots); "
                                "split: separate tables"),
     # ---- tuning

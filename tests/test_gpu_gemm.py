@@ -148,6 +148,7 @@ def test_wide_tower_library_gemm_matches_fused_tiles(monkeypatch, bn):
     outs = []
     for lib in (True, False):
         monkeypatch.setattr(D, "_EPI_BLAS", lib)
+        monkeypatch.setattr(D, "_DX0_BLAS", lib)
         m = NativeDeepFM(synth.feature_size, F, K, layers, keep, batch_size=B, device=DEV, init=False,
                          batch_norm=bn, learning_rate=1e-3, fused=False)
         m.load_tf_params(params)
