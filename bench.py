@@ -92,6 +92,7 @@ def supervise(argv) -> int:
     rank kills its child and the job moves to the next rung on a fresh rendezvous port, so one
     misbehaving execution mode costs a retry instead of the whole measurement.  Ranks coordinate
     through torchrun's agent store (keys ``hipfm_bench/*``).  Returns the exit code."""
+    import shutil
     import signal
     import subprocess
     import tempfile
@@ -110,8 +111,11 @@ def supervise(argv) -> int:
         if rank == 0:
             store.set(f"hipfm_bench/port{k}", str(_free_port()))
         port = store.get(f"hipfm_bench/port{k}").decode()
-        prog = os.path.join(tempfile.gettempdir(), f"hipfm_bench_progress_{os.getpid()}_{k}")
-        result = os.path.join(tempfile.gettempdir(), f"hipfm_bench_result_{os.getpid()}_{k}.json")
+        # a fresh directory per rung: a progress file left by an earlier process with the same
+        # (recycled) pid would read as an old mark and declare the new child hung at once
+        rdir = tempfile.mkdtemp(prefix=f"hipfm_bench_{os.getpid()}_{k}_")
+        prog = os.path.join(rdir, "progress")
+        result = os.path.join(rdir, "result.json")
         env = dict(os.environ, HIPFM_BENCH_CHILD="1", HIPFM_BENCH_RUNG=name, MASTER_PORT=port,
                    TORCHELASTIC_USE_AGENT_STORE="False", HIPFM_BENCH_PROGRESS=prog,
                    HIPFM_BENCH_RESULT=result, **extra)
@@ -153,8 +157,10 @@ def supervise(argv) -> int:
             if store.check(oks):
                 if rank == 0 and os.path.exists(result):
                     print(open(result).read().strip(), flush=True)
+                shutil.rmtree(rdir, ignore_errors=True)
                 return 0
             failed = True
+        shutil.rmtree(rdir, ignore_errors=True)
         store.set(f"hipfm_bench/fail{k}", "1")
         print(f"[bench rank {rank}] rung {name} failed (rc={child.returncode}); "
               f"{'retrying with ' + ladder[k + 1][0] if k + 1 < len(ladder) else 'no rung left'}",

@@ -25,8 +25,9 @@ def _port():
 
 
 def _run(fake, hang_s="4", first_s="20"):
-    # first_s: a healthy fake child marks progress within a second, but a loaded host (right after
-    # a parallel hipcc build) has delayed that start past 6 s -- the rung then fell back early
+    # first_s: a healthy fake child marks progress within a second; the margin is for a loaded host
+    # (the supervisor's per-rung temp dirs fixed the real early fallback: a stale progress file of
+    # a recycled pid read as an old mark)
     env = dict(os.environ, HIPFM_BENCH_FAKE=fake, HIPFM_BENCH_HANG_S=hang_s, HIPFM_BENCH_FIRST_S=first_s)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(REPO, "bench.py"),
